@@ -1,0 +1,134 @@
+#!/usr/bin/env python
+"""ray_amd headline benchmark.
+
+Default workload (BASELINE.json config 2): Ray Train TorchTrainer GPT-2-small DDP,
+bf16, synthetic tokens, random init — one rank per MI355X over RCCL. Each rank
+runs exactly the per-worker step of ``ray_amd.train.examples.gpt2.train_func``
+(forward, backward with bucketed RCCL all-reduce overlapped, clip, fused AdamW).
+
+    python bench.py                       # N=1
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+
+``--workload ppo`` runs the RLlib PPO synthetic-Atari learner throughput bench
+(BASELINE.json config 3). Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="gpt2", choices=["gpt2", "ppo"])
+    ap.add_argument("--micro-batch", type=int, default=16)
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--model", default="small")
+    return ap.parse_args()
+
+
+def bench_gpt2(args):
+    import torch
+    import torch.distributed as dist
+
+    from ray_amd.models.gpt2 import GPT2Config
+    from ray_amd.train.gpt2_step import GPT2Trainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = getattr(GPT2Config, args.model)()
+    tr = GPT2Trainer(cfg, args.micro_batch, args.seq_len, dev, bucket_mb=args.bucket_mb,
+                     total_steps=args.warmup + args.steps, grad_accum=args.grad_accum,
+                     seed=1234)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    # synthetic token stream: pre-generate a pool so data generation is not timed work
+    pool = [tr.synthetic_batch(gen) for _ in range(4 * args.grad_accum)]
+
+    def batches(i):
+        return [pool[(i * args.grad_accum + j) % len(pool)] for j in range(args.grad_accum)]
+
+    for i in range(args.warmup):
+        tr.step(batches(i))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.step(batches(args.warmup + i))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = float(tr.last_loss)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    tokens = tr.tokens_per_step() * args.steps
+    value = tokens / dt
+    n_params = tr.model.num_params()
+    flops = tr.model.flops_per_token(args.seq_len) * tokens
+    if rank == 0:
+        out = {
+            "metric": "ray_train_gpt2_small_ddp_tokens_per_sec" if args.model == "small"
+            else f"ray_train_gpt2_{args.model}_ddp_tokens_per_sec",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": f"gpt2-{args.model}",
+                "params": n_params,
+                "global_batch": args.micro_batch * args.grad_accum * world,
+                "micro_batch_per_gpu": args.micro_batch,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "bucket_mb": args.bucket_mb,
+            },
+            "model_tflops_per_gpu": round(flops / dt / world / 1e12, 1),
+            "final_loss": round(loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.workload == "gpt2":
+        bench_gpt2(args)
+    else:
+        from ray_amd.rllib.bench import bench_ppo
+
+        bench_ppo(args)
+
+
+if __name__ == "__main__":
+    main()

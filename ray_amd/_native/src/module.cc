@@ -1,0 +1,227 @@
+// pybind11 bindings: ray_amd._native._core
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <unistd.h>
+
+#include <random>
+
+#include "io_loop.h"
+#include "scheduler.h"
+#include "shm_store.h"
+
+namespace py = pybind11;
+using namespace ray_amd;
+
+static py::object info_to_py(const ObjInfo& o) {
+  py::dict d;
+  d["id"] = py::bytes(o.id);
+  d["state"] = o.state;
+  d["device"] = o.device;
+  d["offset"] = o.offset;
+  d["data_size"] = o.data_size;
+  d["meta_size"] = o.meta_size;
+  d["ref_count"] = o.ref_count;
+  d["lru_tick"] = o.lru_tick;
+  d["pinned"] = o.pinned;
+  d["creator_pid"] = o.creator_pid;
+  return d;
+}
+
+static std::string as_str(const py::bytes& b) { return std::string(b); }
+
+static thread_local std::mt19937_64* tl_rng = nullptr;
+
+PYBIND11_MODULE(_core, m) {
+  m.doc() = "ray_amd native runtime core: shm object store, frame I/O loop, scheduler";
+
+  m.def("random_id", [](int n) {
+    if (!tl_rng) {
+      std::random_device rd;
+      tl_rng = new std::mt19937_64(((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)getpid());
+    }
+    std::string s(n, '\0');
+    for (int i = 0; i < n; i += 8) {
+      uint64_t v = (*tl_rng)();
+      for (int j = 0; j < 8 && i + j < n; ++j) s[i + j] = (char)((v >> (8 * j)) & 0xff);
+    }
+    return py::bytes(s);
+  });
+
+  py::class_<ShmStore>(m, "ShmStore")
+      .def(py::init<const std::string&, uint64_t, bool, uint64_t>(), py::arg("path"),
+           py::arg("size") = 0, py::arg("create") = false, py::arg("table_cap") = 1 << 16)
+      .def("create",
+           [](ShmStore& s, py::bytes id, uint64_t n, uint64_t meta, int device, bool pinned) {
+             std::string k = as_str(id);
+             py::gil_scoped_release r;
+             return s.create(k, n, meta, device, pinned);
+           },
+           py::arg("id"), py::arg("data_size"), py::arg("meta_size") = 0, py::arg("device") = -1,
+           py::arg("pinned") = false)
+      .def("seal", [](ShmStore& s, py::bytes id) { return s.seal(as_str(id)); })
+      .def("get",
+           [](ShmStore& s, py::bytes id, bool pin) -> py::object {
+             ObjInfo o;
+             bool ok;
+             std::string k = as_str(id);
+             {
+               py::gil_scoped_release r;
+               ok = s.get(k, &o, pin);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(o.offset, o.data_size, o.meta_size, o.device);
+           },
+           py::arg("id"), py::arg("pin") = true)
+      .def("info",
+           [](ShmStore& s, py::bytes id) -> py::object {
+             ObjInfo o;
+             if (!s.get(as_str(id), &o, false)) return py::none();
+             return info_to_py(o);
+           })
+      .def("release", [](ShmStore& s, py::bytes id) { return s.release(as_str(id)); })
+      .def("remove", [](ShmStore& s, py::bytes id) { return s.remove(as_str(id)); })
+      .def("contains", [](ShmStore& s, py::bytes id) { return s.contains(as_str(id)); })
+      .def("state", [](ShmStore& s, py::bytes id) { return s.state(as_str(id)); })
+      .def("set_pinned", [](ShmStore& s, py::bytes id, bool p) { return s.set_pinned(as_str(id), p); })
+      .def("evict",
+           [](ShmStore& s, uint64_t bytes, int device) {
+             std::vector<py::bytes> out;
+             for (auto& x : s.evict(bytes, device)) out.emplace_back(x);
+             return out;
+           },
+           py::arg("bytes"), py::arg("device") = -1)
+      .def("spill_candidates",
+           [](ShmStore& s, uint64_t bytes, int device) {
+             std::vector<py::bytes> out;
+             for (auto& x : s.spill_candidates(bytes, device)) out.emplace_back(x);
+             return out;
+           },
+           py::arg("bytes"), py::arg("device") = -1)
+      .def("list",
+           [](ShmStore& s) {
+             py::list l;
+             for (auto& o : s.list()) l.append(info_to_py(o));
+             return l;
+           })
+      .def("buffer",
+           [](ShmStore& s, uint64_t off, uint64_t n) {
+             if (off + n > s.size()) throw std::out_of_range("buffer out of range");
+             return py::memoryview::from_memory((void*)(s.base() + off), (ssize_t)n, false);
+           })
+      .def("address", [](ShmStore& s) { return (uintptr_t)s.base(); })
+      .def("write",
+           [](ShmStore& s, uint64_t off, py::buffer b) {
+             py::buffer_info bi = b.request();
+             uint64_t n = (uint64_t)bi.size * bi.itemsize;
+             if (off + n > s.size()) throw std::out_of_range("write out of range");
+             py::gil_scoped_release r;
+             memcpy(s.base() + off, bi.ptr, n);
+           })
+      .def("init_device_heap", &ShmStore::init_device_heap)
+      .def("device_heap_ready", &ShmStore::device_heap_ready)
+      .def("used", &ShmStore::used, py::arg("device") = -1)
+      .def("capacity", &ShmStore::capacity, py::arg("device") = -1)
+      .def("num_objects", &ShmStore::num_objects)
+      .def("evictions", &ShmStore::evictions)
+      .def("release_all_pins_of", &ShmStore::release_all_pins_of)
+      .def_property_readonly("size", &ShmStore::size);
+
+  py::class_<IOLoop>(m, "IOLoop")
+      .def(py::init<>())
+      .def("listen_unix", &IOLoop::listen_unix)
+      .def("listen_tcp",
+           [](IOLoop& io, const std::string& host, int port) {
+             int bound = 0;
+             int id = io.listen_tcp(host, port, &bound);
+             return py::make_tuple(id, bound);
+           })
+      .def("connect_unix", &IOLoop::connect_unix, py::arg("path"), py::arg("timeout_ms") = 10000,
+           py::call_guard<py::gil_scoped_release>())
+      .def("connect_tcp", &IOLoop::connect_tcp, py::arg("host"), py::arg("port"),
+           py::arg("timeout_ms") = 10000, py::call_guard<py::gil_scoped_release>())
+      .def("send",
+           [](IOLoop& io, int conn, py::bytes data) {
+             char* p;
+             ssize_t n;
+             PyBytes_AsStringAndSize(data.ptr(), &p, &n);
+             py::gil_scoped_release r;
+             return io.send(conn, p, (size_t)n);
+           })
+      .def("send2",
+           [](IOLoop& io, int conn, py::bytes a, py::buffer b) {
+             char* p;
+             ssize_t n;
+             PyBytes_AsStringAndSize(a.ptr(), &p, &n);
+             py::buffer_info bi = b.request();
+             py::gil_scoped_release r;
+             return io.send2(conn, p, (size_t)n, (const char*)bi.ptr, (size_t)(bi.size * bi.itemsize));
+           })
+      .def("close", &IOLoop::close_conn)
+      .def("poll",
+           [](IOLoop& io, int timeout_ms, size_t max_events) {
+             std::vector<Event> ev;
+             {
+               py::gil_scoped_release r;
+               ev = io.poll(timeout_ms, max_events);
+             }
+             py::list out;
+             for (auto& e : ev) {
+               if (e.type == kMessage)
+                 out.append(py::make_tuple(e.type, e.conn, py::bytes(e.data)));
+               else
+                 out.append(py::make_tuple(e.type, e.conn, e.aux));
+             }
+             return out;
+           },
+           py::arg("timeout_ms") = -1, py::arg("max_events") = 1024)
+      .def("wakeup", &IOLoop::wakeup)
+      .def("pending", &IOLoop::pending)
+      .def("stop", &IOLoop::stop, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<Allocation>(m, "Allocation")
+      .def(py::init<>())
+      .def_readonly("node", &Allocation::node)
+      .def_property_readonly("instances", [](const Allocation& a) {
+        py::dict d;
+        for (auto& kv : a.instances) {
+          py::list l;
+          for (auto& p : kv.second) l.append(py::make_tuple(p.first, (double)p.second / Scheduler::kUnit));
+          d[py::str(kv.first)] = l;
+        }
+        return d;
+      });
+
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<>())
+      .def_readwrite("spread_threshold", &Scheduler::spread_threshold)
+      .def("add_node", &Scheduler::add_node, py::arg("node_id"), py::arg("total"),
+           py::arg("labels") = LabelMap())
+      .def("remove_node", &Scheduler::remove_node)
+      .def("set_draining", &Scheduler::set_draining)
+      .def("nodes", &Scheduler::nodes)
+      .def("total", &Scheduler::total)
+      .def("available", &Scheduler::available)
+      .def("cluster_total", &Scheduler::cluster_total)
+      .def("cluster_available", &Scheduler::cluster_available)
+      .def("labels", &Scheduler::labels)
+      .def("pick_node", &Scheduler::pick_node, py::arg("req"), py::arg("strategy") = 0,
+           py::arg("target") = "", py::arg("local") = "", py::arg("hard_labels") = LabelMap(),
+           py::arg("soft_labels") = LabelMap())
+      .def("feasible_anywhere", &Scheduler::feasible_anywhere, py::arg("req"),
+           py::arg("hard_labels") = LabelMap())
+      .def("allocate",
+           [](Scheduler& s, const std::string& node, const ResMap& req) -> py::object {
+             Allocation a;
+             if (!s.allocate(node, req, &a)) return py::none();
+             return py::cast(a);
+           })
+      .def("release", &Scheduler::release)
+      .def("place_bundles",
+           [](Scheduler& s, const std::vector<ResMap>& b, int strategy) {
+             bool inf = false;
+             auto nodes = s.place_bundles(b, strategy, &inf);
+             return py::make_tuple(nodes, inf);
+           })
+      .def("commit_bundles", &Scheduler::commit_bundles)
+      .def("remove_bundles", &Scheduler::remove_bundles);
+}

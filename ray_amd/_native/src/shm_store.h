@@ -1,0 +1,142 @@
+// Shared-memory object store ("plasma" equivalent) for ray_amd.
+//
+// Reference behaviour: src/ray/object_manager/plasma/{store.cc,object_lifecycle_manager.cc,
+// dlmalloc.cc,eviction_policy.cc}: create -> seal -> get/release, ref-counted pins,
+// LRU eviction of unpinned sealed objects.
+//
+// Design difference: the reference runs the store inside the raylet and every
+// create/get is an IPC round trip over a Unix socket. Here the allocator, the
+// object table and the LRU clock live INSIDE the shared segment, guarded by a
+// robust process-shared mutex, so any process on the node creates, seals and
+// reads objects with a lock + a hash probe and zero IPC. Offsets (not pointers)
+// are stored, since every process maps the segment at a different address.
+//
+// Block metadata is kept out-of-line (a record pool in the segment), so the
+// very same allocator also manages the per-GPU HBM arenas (ops/csrc/gpu_arena.hip)
+// whose bytes the host never touches: a GPU object is an entry whose `device`
+// is >= 0 and whose `offset` is inside that GPU's arena.
+#pragma once
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace ray_amd {
+
+constexpr int kIdSize = 20;
+constexpr int kMaxDevices = 16;
+constexpr int kNumBins = 64;
+constexpr uint64_t kAlign = 64;
+
+enum ObjState : uint32_t { kEmpty = 0, kCreated = 1, kSealed = 2, kTombstone = 3 };
+
+struct ObjEntry {
+  uint8_t id[kIdSize];
+  uint32_t state;
+  int32_t device;  // -1 = host heap, else GPU index (HBM arena)
+  uint32_t block;  // block record index
+  uint32_t pinned;  // primary copy pinned by its owner (spillable, not evictable)
+  uint64_t offset;  // data offset: from segment start (host) or arena start (device)
+  uint64_t data_size;
+  uint64_t meta_size;
+  int64_t ref_count;  // reader pins
+  uint64_t lru_tick;
+  uint32_t delete_pending;
+  int32_t creator_pid;
+};
+
+struct Block {
+  uint64_t off, size;
+  uint32_t prev, next;    // address-order neighbours (index+1, 0 = none)
+  uint32_t fprev, fnext;  // free-list links (index+1)
+  uint32_t free_;
+  uint32_t in_use;  // record slot in use
+};
+
+struct HeapHdr {
+  uint64_t base, size, used;
+  uint32_t bins[kNumBins];  // free-list heads (index+1)
+  uint32_t first;           // first block (index+1)
+  uint32_t valid;
+  uint64_t n_objects;
+};
+
+struct SegHeader {
+  uint64_t magic, version, total_size;
+  uint64_t table_cap, table_off;
+  uint64_t blocks_cap, blocks_off;
+  uint64_t heap_off;
+  uint32_t block_free_head;  // free record stack (index+1)
+  uint32_t pad0;
+  uint64_t num_objects, lru_clock;
+  uint64_t stats_evictions, stats_creates;
+  pthread_mutex_t mu;
+  HeapHdr heaps[1 + kMaxDevices];  // [0] host, [1+d] device d
+};
+
+struct ObjInfo {
+  std::string id;
+  int state = 0;
+  int device = -1;
+  uint64_t offset = 0, data_size = 0, meta_size = 0;
+  int64_t ref_count = 0;
+  uint64_t lru_tick = 0;
+  bool pinned = false;
+  int creator_pid = 0;
+};
+
+class ShmStore {
+ public:
+  ShmStore(const std::string& path, uint64_t size, bool create, uint64_t table_cap);
+  ~ShmStore();
+
+  uint8_t* base() const { return base_; }
+  uint64_t size() const { return size_; }
+
+  // Returns data offset, or UINT64_MAX when the heap is full. Throws on duplicate id.
+  uint64_t create(const std::string& id, uint64_t data_size, uint64_t meta_size, int device,
+                  bool pinned);
+  bool seal(const std::string& id);
+  bool get(const std::string& id, ObjInfo* out, bool pin);
+  bool release(const std::string& id);
+  bool remove(const std::string& id);
+  bool contains(const std::string& id);
+  int state(const std::string& id);
+  bool set_pinned(const std::string& id, bool pinned);
+  std::vector<std::string> evict(uint64_t bytes, int device);
+  std::vector<std::string> spill_candidates(uint64_t bytes, int device);
+  std::vector<ObjInfo> list();
+  void init_device_heap(int device, uint64_t arena_size);
+  bool device_heap_ready(int device);
+  uint64_t used(int device);
+  uint64_t capacity(int device);
+  uint64_t num_objects();
+  uint64_t evictions();
+  void release_all_pins_of(int pid);
+
+ private:
+  ObjEntry* table() const;
+  Block* blocks() const;
+  ObjEntry* find(const uint8_t* id);
+  ObjEntry* insert_slot(const uint8_t* id);
+  HeapHdr* heap(int device);
+  uint32_t rec_alloc();
+  void rec_free(uint32_t r);
+  void bin_push(HeapHdr* h, uint32_t r);
+  void bin_remove(HeapHdr* h, uint32_t r);
+  uint32_t heap_alloc(int device, uint64_t n);
+  void heap_free(int device, uint32_t r);
+  void free_entry(ObjEntry* e);
+  void lock();
+  void unlock();
+  friend struct Guard;
+
+  std::string path_;
+  uint8_t* base_ = nullptr;
+  uint64_t size_ = 0;
+  SegHeader* hdr_ = nullptr;
+};
+
+}  // namespace ray_amd

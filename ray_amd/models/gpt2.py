@@ -1,0 +1,151 @@
+"""GPT-2 (small/medium/large/xl) for MI355X, random init.
+
+The headline Ray Train workload (BASELINE.json config 2: TorchTrainer GPT-2-small
+DDP bf16). Architecture per Radford et al. 2019 / HF GPT2LMHeadModel (pre-LN,
+learned positions, tanh-GELU, tied input/output embedding).
+
+MI355X-first choices:
+* bf16 weights/activations end to end (fp32 master lives in the flat optimizer).
+* Every GEMM is a plain hipBLASLt GEMM with NO bias; the bias, activation and
+  residual are fused into a single HBM pass by our HIP epilogue kernels
+  (``bias_gelu``, ``bias_residual``), LayerNorm and the vocab cross-entropy are
+  hand-written kernels (ray_amd/ops/csrc).
+* Vocab padded 50257 → 50304 (multiple of 64/128) so the LM-head GEMM tiles
+  cleanly on MFMA; padded columns are masked inside the fused cross-entropy.
+* Attention: fused causal flash attention (torch SDPA flash backend on ROCm)
+  — [B, H, T, 64] head layout straight from the QKV GEMM view.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ray_amd.ops import functional as rf
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    padded_vocab: int = 50304
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    layer_norm_eps: float = 1e-5
+    init_std: float = 0.02
+
+    @staticmethod
+    def small():
+        return GPT2Config()
+
+    @staticmethod
+    def medium():
+        return GPT2Config(n_embd=1024, n_layer=24, n_head=16)
+
+    @staticmethod
+    def large():
+        return GPT2Config(n_embd=1280, n_layer=36, n_head=20)
+
+    @staticmethod
+    def xl():
+        return GPT2Config(n_embd=1600, n_layer=48, n_head=25)
+
+    @staticmethod
+    def tiny():
+        return GPT2Config(vocab_size=512, padded_vocab=512, n_positions=128, n_embd=64,
+                          n_layer=2, n_head=4)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, d, eps):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.bias = nn.Parameter(torch.zeros(d))
+        self.eps = eps
+
+    def forward(self, x):
+        return rf.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        C = cfg.n_embd
+        self.n_head = cfg.n_head
+        self.ln_1 = LayerNorm(C, cfg.layer_norm_eps)
+        self.c_attn_w = nn.Parameter(torch.empty(3 * C, C))
+        self.c_attn_b = nn.Parameter(torch.zeros(3 * C))
+        self.c_proj_w = nn.Parameter(torch.empty(C, C))
+        self.c_proj_b = nn.Parameter(torch.zeros(C))
+        self.ln_2 = LayerNorm(C, cfg.layer_norm_eps)
+        self.c_fc_w = nn.Parameter(torch.empty(4 * C, C))
+        self.c_fc_b = nn.Parameter(torch.zeros(4 * C))
+        self.mlp_proj_w = nn.Parameter(torch.empty(C, 4 * C))
+        self.mlp_proj_b = nn.Parameter(torch.zeros(C))
+
+    def forward(self, x):
+        B, T, C = x.shape
+        H = self.n_head
+        h = self.ln_1(x)
+        qkv = F.linear(h, self.c_attn_w, self.c_attn_b)  # hipBLASLt GEMM + bias epilogue
+        q, k, v = qkv.view(B, T, 3, H, C // H).permute(2, 0, 3, 1, 4).unbind(0)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        y = y.transpose(1, 2).reshape(B, T, C)
+        x = rf.bias_residual(F.linear(y, self.c_proj_w), self.c_proj_b, x)
+        h = self.ln_2(x)
+        a = rf.bias_gelu(F.linear(h, self.c_fc_w), self.c_fc_b)
+        x = rf.bias_residual(F.linear(a, self.mlp_proj_w), self.mlp_proj_b, x)
+        return x
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.cfg = cfg
+        self.wte = nn.Parameter(torch.empty(cfg.padded_vocab, cfg.n_embd))
+        self.wpe = nn.Parameter(torch.empty(cfg.n_positions, cfg.n_embd))
+        self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_eps)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        std = self.cfg.init_std
+        proj_std = std / math.sqrt(2 * self.cfg.n_layer)
+        with torch.no_grad():
+            nn.init.normal_(self.wte, 0, std)
+            self.wte[self.cfg.vocab_size:].zero_()
+            nn.init.normal_(self.wpe, 0, 0.01)
+            for b in self.h:
+                nn.init.normal_(b.c_attn_w, 0, std)
+                nn.init.normal_(b.c_fc_w, 0, std)
+                nn.init.normal_(b.c_proj_w, 0, proj_std)
+                nn.init.normal_(b.mlp_proj_w, 0, proj_std)
+
+    def num_params(self, non_embedding=True):
+        n = sum(p.numel() for p in self.parameters())
+        if non_embedding:
+            n -= self.wpe.numel()
+        return n
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        pos = torch.arange(T, device=idx.device)
+        x = F.embedding(idx, self.wte) + F.embedding(pos, self.wpe)[None]
+        for blk in self.h:
+            x = blk(x)
+        x = self.ln_f(x)
+        logits = F.linear(x, self.wte)  # tied LM head, [B, T, padded_vocab]
+        if targets is None:
+            return logits[..., : self.cfg.vocab_size]
+        return rf.cross_entropy(logits, targets, self.cfg.vocab_size)
+
+    def flops_per_token(self, T: int) -> float:
+        """6N + 12·L·H·hd·T (PaLM appendix B convention), training FLOPs per token."""
+        cfg = self.cfg
+        N = self.num_params()
+        return 6 * N + 12 * cfg.n_layer * cfg.n_embd * T

@@ -1,0 +1,97 @@
+// Shared device helpers for the ray_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: lane = threadIdx.x & 63, reductions use __shfl_xor over 64 lanes.
+//  * bf16 tensors are moved as 8-byte (4 x bf16) or 16-byte (8 x bf16) vectors
+//    (Guideline 13: hipcc does not vectorise scalar bf16 loads).
+//  * bf16 <-> f32 conversion goes through clang's __bf16, which lowers to
+//    v_cvt_pk_bf16_f32 (RNE) on gfx950.
+//  * Every entry point is `extern "C"`, takes raw device pointers and a
+//    hipStream_t, and returns hipError_t: the Python side (ray_amd/ops) loads the
+//    library with ctypes and passes torch's current stream, so launches are
+//    hipGraph-capturable (no malloc/sync inside a launch function).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RA_EXPORT extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;  // raw storage type on the ABI boundary
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+// 4 x bf16 packed in 8 bytes <-> 4 floats
+struct bf16v4 { uint2 u; };
+__device__ __forceinline__ void unpack4(uint2 u, float (&f)[4]) {
+  f[0] = __uint_as_float(u.x << 16);
+  f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16);
+  f[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint2 pack4(const float (&f)[4]) {
+  bf16x2 a = {(__bf16)f[0], (__bf16)f[1]};
+  bf16x2 b = {(__bf16)f[2], (__bf16)f[3]};
+  return make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+}
+__device__ __forceinline__ void unpack8(uint4 u, float (&f)[8]) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  bf16x2 a = {(__bf16)f[0], (__bf16)f[1]}, b = {(__bf16)f[2], (__bf16)f[3]};
+  bf16x2 c = {(__bf16)f[4], (__bf16)f[5]}, d = {(__bf16)f[6], (__bf16)f[7]};
+  return make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                    __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blocks of NW waves; `red` must hold NW floats. Result broadcast.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// Grid size for memory-bound grid-stride kernels (Guideline 11): fill 256 CUs x 8.
+__host__ __forceinline__ int ra_grid(long long work_items, int block) {
+  long long g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}

@@ -1,0 +1,183 @@
+// Flat-buffer optimizer kernels (one launch for the whole model).
+//
+// The trainer keeps every parameter as a view into ONE bf16 buffer (compute
+// copy) backed by ONE fp32 master buffer, and every gradient as a view into
+// ONE bf16 grad buffer (which is also what RCCL all-reduces, bucket by bucket,
+// with no packing copy). So the optimizer step is a single streaming pass:
+//   read g(bf16) p(f32) m(f32) v(f32) -> write p(f32) m v p16(bf16) = 28 B/param.
+// Decayed parameters occupy [0, n_decay), the rest is not decayed.
+// Global-norm clipping stays on device: ra_sumsq_bf16 -> ra_clip_scale writes
+// the scale factor that ra_adamw_flat reads through a pointer (no host sync).
+#include "common.h"
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const bf16_t* __restrict__ g, long n4,
+                                                    float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float v[4];
+    unpack4(reinterpret_cast<const uint2*>(g)[i], v);
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void clip_scale_kernel(const float* __restrict__ part, int P, float max_norm,
+                                  float pre_scale, float* __restrict__ scale_out,
+                                  float* __restrict__ norm_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) s += part[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(s) * pre_scale;
+    if (norm_out) *norm_out = norm;
+    float sc = pre_scale;
+    if (max_norm > 0.f && norm > max_norm) sc *= max_norm / (norm + 1e-6f);
+    *scale_out = sc;
+  }
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p32,
+                                                    bf16_t* __restrict__ p16,
+                                                    const bf16_t* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    long n4, long nd4, float lr, float b1,
+                                                    float b2, float eps, float wd, float rbc1,
+                                                    float rbc2, const float* __restrict__ gscale) {
+  const float sc = gscale ? *gscale : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float gv[4];
+    unpack4(reinterpret_cast<const uint2*>(g)[i], gv);
+    float4 p = reinterpret_cast<float4*>(p32)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    const float decay = (i < nd4) ? (1.f - lr * wd) : 1.f;
+    float pa[4] = {p.x, p.y, p.z, p.w};
+    float ma[4] = {mm.x, mm.y, mm.z, mm.w};
+    float va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gr = gv[j] * sc;
+      ma[j] = b1 * ma[j] + (1.f - b1) * gr;
+      va[j] = b2 * va[j] + (1.f - b2) * gr * gr;
+      const float upd = (ma[j] * rbc1) / (sqrtf(va[j] * rbc2) + eps);
+      pa[j] = pa[j] * decay - lr * upd;
+    }
+    reinterpret_cast<float4*>(p32)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+    reinterpret_cast<uint2*>(p16)[i] = pack4(pa);
+  }
+}
+
+// Plain SGD/momentum on the same flat layout (used by RL learners).
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p32, bf16_t* __restrict__ p16,
+                                                  const bf16_t* __restrict__ g,
+                                                  float* __restrict__ buf, long n4, float lr,
+                                                  float mom, float wd,
+                                                  const float* __restrict__ gscale) {
+  const float sc = gscale ? *gscale : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float gv[4];
+    unpack4(reinterpret_cast<const uint2*>(g)[i], gv);
+    float4 p = reinterpret_cast<float4*>(p32)[i];
+    float4 b = reinterpret_cast<float4*>(buf)[i];
+    float pa[4] = {p.x, p.y, p.z, p.w}, ba[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gr = gv[j] * sc + wd * pa[j];
+      ba[j] = mom * ba[j] + gr;
+      pa[j] -= lr * ba[j];
+    }
+    reinterpret_cast<float4*>(p32)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    reinterpret_cast<float4*>(buf)[i] = make_float4(ba[0], ba[1], ba[2], ba[3]);
+    if (p16) reinterpret_cast<uint2*>(p16)[i] = pack4(pa);
+  }
+}
+
+// fp32-grad variant of AdamW (for fp32 learners, e.g. RLlib policies).
+__global__ __launch_bounds__(256) void adamw_f32_kernel(float* __restrict__ p,
+                                                        const float* __restrict__ g,
+                                                        float* __restrict__ m,
+                                                        float* __restrict__ v, long n, long nd,
+                                                        float lr, float b1, float b2, float eps,
+                                                        float wd, float rbc1, float rbc2,
+                                                        const float* __restrict__ gscale) {
+  const float sc = gscale ? *gscale : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float gr = g[i] * sc;
+    const float mm = b1 * m[i] + (1.f - b1) * gr;
+    const float vv = b2 * v[i] + (1.f - b2) * gr * gr;
+    m[i] = mm;
+    v[i] = vv;
+    const float decay = (i < nd) ? (1.f - lr * wd) : 1.f;
+    p[i] = p[i] * decay - lr * (mm * rbc1) / (sqrtf(vv * rbc2) + eps);
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict__ g, long n,
+                                                        float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    s += g[i] * g[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+static const int kNormParts = 1024;
+
+RA_EXPORT int ra_norm_parts() { return kNormParts; }
+
+// work: kNormParts floats. scale_out/norm_out: device floats.
+RA_EXPORT int ra_grad_clip(const void* g, long n, int is_bf16, float max_norm, float pre_scale,
+                           float* work, float* scale_out, float* norm_out, hipStream_t st) {
+  if (is_bf16) {
+    if (n % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sumsq_kernel, dim3(kNormParts), dim3(256), 0, st, (const bf16_t*)g, n / 4,
+                       work);
+  } else {
+    hipLaunchKernelGGL(sumsq_f32_kernel, dim3(kNormParts), dim3(256), 0, st, (const float*)g, n,
+                       work);
+  }
+  hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(256), 0, st, work, kNormParts, max_norm,
+                     pre_scale, scale_out, norm_out);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_adamw_flat(float* p32, void* p16, const void* g, float* m, float* v, long n,
+                            long n_decay, float lr, float b1, float b2, float eps, float wd,
+                            int step, const float* gscale, hipStream_t st) {
+  if (n % 4 || n_decay % 4) return hipErrorInvalidValue;
+  const float rbc1 = 1.f / (1.f - powf(b1, (float)step));
+  const float rbc2 = 1.f / (1.f - powf(b2, (float)step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(ra_grid(n / 4, 256)), dim3(256), 0, st, p32,
+                     (bf16_t*)p16, (const bf16_t*)g, m, v, n / 4, n_decay / 4, lr, b1, b2, eps,
+                     wd, rbc1, rbc2, gscale);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_adamw_f32(float* p, const float* g, float* m, float* v, long n, long n_decay,
+                           float lr, float b1, float b2, float eps, float wd, int step,
+                           const float* gscale, hipStream_t st) {
+  const float rbc1 = 1.f / (1.f - powf(b1, (float)step));
+  const float rbc2 = 1.f / (1.f - powf(b2, (float)step));
+  hipLaunchKernelGGL(adamw_f32_kernel, dim3(ra_grid(n, 256)), dim3(256), 0, st, p, g, m, v, n,
+                     n_decay, lr, b1, b2, eps, wd, rbc1, rbc2, gscale);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_sgd_flat(float* p32, void* p16, const void* g, float* buf, long n, float lr,
+                          float mom, float wd, const float* gscale, hipStream_t st) {
+  if (n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_kernel, dim3(ra_grid(n / 4, 256)), dim3(256), 0, st, p32, (bf16_t*)p16,
+                     (const bf16_t*)g, buf, n / 4, lr, mom, wd, gscale);
+  return hipGetLastError();
+}

@@ -1,0 +1,336 @@
+"""Autograd-aware entry points for the CDNA4 kernels.
+
+Every op dispatches on device: CUDA(HIP) tensors go to the hand-written kernels
+in ``libray_amd_hip.so`` (failing loudly if it is missing), CPU tensors go to the
+fp32 references in ``ray_amd.ops.reference``.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import reference as ref
+from ._lib import check, ptr, stream_ptr
+
+
+def _hip(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# --------------------------------------------------------------------- LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        D = x.shape[-1]
+        x2 = x.contiguous().view(-1, D)
+        N = x2.shape[0]
+        y = torch.empty_like(x2)
+        mean = torch.empty(N, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(N, device=x.device, dtype=torch.float32)
+        check(_lib.lib().ra_layernorm_fwd(ptr(x2), ptr(w), ptr(b), ptr(y), ptr(mean), ptr(rstd),
+                                          N, D, eps, stream_ptr()), "layernorm_fwd")
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        N, D = x2.shape
+        dy2 = dy.contiguous().view(N, D)
+        L = _lib.lib()
+        P = L.ra_layernorm_bwd_parts(N)
+        work = torch.empty(2 * P * D, device=dy.device, dtype=torch.float32)
+        dx = torch.empty_like(x2)
+        dw = torch.empty_like(w)
+        db = torch.empty_like(w)
+        check(L.ra_layernorm_bwd(ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dx),
+                                 ptr(dw), ptr(db), ptr(work), N, D,
+                                 1 if w.dtype == torch.bfloat16 else 0, stream_ptr()),
+              "layernorm_bwd")
+        return dx.view(ctx.shape), dw, db, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 4 == 0:
+        return _LayerNorm.apply(x, weight, bias, eps)
+    return ref.layer_norm(x, weight, bias, eps)
+
+
+# --------------------------------------------------------------------- bias + GELU
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, bias):
+        F_ = h.shape[-1]
+        h2 = h.contiguous().view(-1, F_)
+        y = torch.empty_like(h2)
+        check(_lib.lib().ra_bias_gelu_fwd(ptr(h2), ptr(bias), ptr(y), h2.shape[0], F_,
+                                          stream_ptr()), "bias_gelu_fwd")
+        ctx.save_for_backward(h2, bias)
+        ctx.shape = h.shape
+        return y.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h2, bias = ctx.saved_tensors
+        N, F_ = h2.shape
+        L = _lib.lib()
+        work = torch.empty(L.ra_colsum_parts(N) * F_, device=dy.device, dtype=torch.float32)
+        dh = torch.empty_like(h2)
+        db = torch.empty_like(bias)
+        check(L.ra_bias_gelu_bwd(ptr(dy.contiguous()), ptr(h2), ptr(bias), ptr(dh), ptr(db),
+                                 ptr(work), N, F_, stream_ptr()), "bias_gelu_bwd")
+        return dh.view(ctx.shape), db
+
+
+def bias_gelu(h, bias):
+    if _hip(h) and h.dtype == torch.bfloat16 and h.shape[-1] % 8 == 0:
+        return _BiasGelu.apply(h, bias)
+    return ref.bias_gelu(h, bias)
+
+
+# --------------------------------------------------------------------- bias + residual
+def _colsum_bf16(x2):
+    N, F_ = x2.shape
+    L = _lib.lib()
+    work = torch.empty(L.ra_colsum_parts(N) * F_, device=x2.device, dtype=torch.float32)
+    out = torch.empty(F_, device=x2.device, dtype=x2.dtype)
+    check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_, stream_ptr()), "colsum")
+    return out
+
+
+class _BiasResidual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, bias, res):
+        F_ = h.shape[-1]
+        h2 = h.contiguous().view(-1, F_)
+        r2 = res.contiguous().view(-1, F_)
+        y = torch.empty_like(h2)
+        check(_lib.lib().ra_bias_residual(ptr(h2), ptr(bias), ptr(r2), ptr(y), h2.shape[0], F_,
+                                          stream_ptr()), "bias_residual")
+        ctx.has_bias = bias is not None
+        return y.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        db = _colsum_bf16(dy.contiguous().view(-1, dy.shape[-1])) if ctx.has_bias else None
+        return dy, db, dy
+
+
+def bias_residual(h, bias, res):
+    if _hip(h) and h.dtype == torch.bfloat16 and h.shape[-1] % 8 == 0:
+        return _BiasResidual.apply(h, bias, res)
+    return ref.bias_residual(h, bias, res)
+
+
+# --------------------------------------------------------------------- cross entropy
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, V, ignore_index):
+        Vp = logits.shape[-1]
+        l2 = logits.contiguous().view(-1, Vp)
+        t = targets.contiguous().view(-1).long()
+        N = l2.shape[0]
+        loss = torch.empty(N, device=logits.device, dtype=torch.float32)
+        lse = torch.empty(N, device=logits.device, dtype=torch.float32)
+        check(_lib.lib().ra_xent_fwd(ptr(l2), ptr(t), ptr(loss), ptr(lse), N, V, Vp,
+                                     ignore_index, stream_ptr()), "xent_fwd")
+        count = (t != ignore_index).sum().clamp_min(1)
+        ctx.save_for_backward(l2, t, lse, count)
+        ctx.V, ctx.ignore_index, ctx.shape = V, ignore_index, logits.shape
+        return loss.sum() / count
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, t, lse, count = ctx.saved_tensors
+        N, Vp = l2.shape
+        # fold 1/count into the device-side grad scalar: no host sync
+        gs = (g.float() / count.float()).reshape(1).contiguous()
+        dl = torch.empty_like(l2)
+        check(_lib.lib().ra_xent_bwd(ptr(l2), ptr(t), ptr(lse), ptr(gs), 1.0, ptr(dl), N, ctx.V,
+                                     Vp, ctx.ignore_index, stream_ptr()), "xent_bwd")
+        return dl.view(ctx.shape), None, None, None
+
+
+def cross_entropy(logits, targets, vocab_size=None, ignore_index=-100):
+    """Mean token cross-entropy. ``logits`` may be vocab-padded; columns >= vocab_size are
+    excluded from the softmax."""
+    V = vocab_size or logits.shape[-1]
+    if _hip(logits) and logits.dtype == torch.bfloat16 and logits.shape[-1] % 8 == 0:
+        return _CrossEntropy.apply(logits, targets, V, ignore_index)
+    return ref.cross_entropy(logits, targets, V, ignore_index)
+
+
+# --------------------------------------------------------------------- RL kernels
+def gae(rewards, values, dones, bootstrap, gamma=0.99, lam=0.95):
+    """Time-major [T,B] GAE → (advantages, value_targets), fp32."""
+    if not _hip(rewards):
+        return ref.gae(rewards, values, dones, bootstrap, gamma, lam)
+    T, B = rewards.shape
+    r, v, d, bs = (x.float().contiguous() for x in (rewards, values, dones, bootstrap))
+    adv = torch.empty_like(r)
+    vt = torch.empty_like(r)
+    check(_lib.lib().ra_gae(ptr(r), ptr(v), ptr(d), ptr(bs), ptr(adv), ptr(vt), T, B, gamma, lam,
+                            stream_ptr()), "gae")
+    return adv, vt
+
+
+def vtrace(log_rhos, discounts, rewards, values, bootstrap, clip_rho=1.0, clip_c=1.0,
+           clip_pg_rho=1.0, lam=1.0):
+    """Time-major [T,B] V-trace → (vs, pg_advantages), fp32."""
+    if not _hip(values):
+        return ref.vtrace(log_rhos, discounts, rewards, values, bootstrap, clip_rho, clip_c,
+                          clip_pg_rho, lam)
+    T, B = values.shape
+    lr, dc, r, v, bs = (x.float().contiguous() for x in
+                        (log_rhos, discounts, rewards, values, bootstrap))
+    vs = torch.empty_like(v)
+    pg = torch.empty_like(v)
+    check(_lib.lib().ra_vtrace(ptr(lr), ptr(dc), ptr(r), ptr(v), ptr(bs), ptr(vs), ptr(pg), T, B,
+                               clip_rho, clip_c, clip_pg_rho, lam, stream_ptr()), "vtrace")
+    return vs, pg
+
+
+class _PPOLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, vpred, old_logits, actions, old_logp, adv, vtarg, hp):
+        N, A = logits.shape
+        lg = logits.float().contiguous()
+        dl = torch.empty_like(lg)
+        has_v = vpred is not None
+        vp = vpred.float().contiguous() if has_v else None
+        dv = torch.empty_like(vp) if has_v else None
+        stats = torch.empty(6, device=logits.device, dtype=torch.float32)
+        ol = old_logits.float().contiguous() if old_logits is not None else None
+        check(_lib.lib().ra_ppo_loss(
+            ptr(lg), ptr(ol), ptr(actions.long().contiguous()), ptr(old_logp.float().contiguous()),
+            ptr(adv.float().contiguous()), ptr(vp), ptr(vtarg.float().contiguous()) if has_v else None,
+            ptr(dl), ptr(dv), ptr(stats), N, A, hp[0], hp[1], hp[2], hp[3], hp[4], stream_ptr()),
+            "ppo_loss")
+        ctx.save_for_backward(dl, dv if has_v else dl)
+        ctx.has_v = has_v
+        ctx.dtypes = (logits.dtype, vpred.dtype if has_v else None)
+        ctx.mark_non_differentiable(stats)
+        return stats[0].clone(), stats
+
+    @staticmethod
+    def backward(ctx, g, _gs):
+        dl, dv = ctx.saved_tensors
+        dlog = (dl * g).to(ctx.dtypes[0])
+        dvp = (dv * g).to(ctx.dtypes[1]) if ctx.has_v else None
+        return dlog, dvp, None, None, None, None, None, None
+
+
+def ppo_loss(logits, old_logits, actions, old_logp, adv, vpred, vtarg, clip=0.2, vf_clip=10.0,
+             vf_coeff=1.0, ent_coeff=0.0, kl_coeff=0.0):
+    """Fused PPO loss: returns (total_loss, stats[6] = total, policy, vf, entropy, kl, clipfrac).
+    The kernel computes the loss AND its gradient wrt logits/values in one pass."""
+    if not _hip(logits) or logits.shape[-1] > 64:
+        return ref.ppo_loss(logits, old_logits, actions, old_logp, adv, vpred, vtarg, clip,
+                            vf_clip, vf_coeff, ent_coeff, kl_coeff)
+    hp = (float(clip), float(vf_clip), float(vf_coeff), float(ent_coeff), float(kl_coeff))
+    return _PPOLoss.apply(logits, vpred, old_logits, actions, old_logp, adv, vtarg, hp)
+
+
+class RunningMeanStd:
+    """Running observation normalisation (RLlib MeanStdFilter) with device-side Welford merge."""
+
+    def __init__(self, shape, device="cpu", clip=10.0, eps=1e-8):
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        D = 1
+        for s in self.shape:
+            D *= s
+        self.D = D
+        self.mean = torch.zeros(D, device=device, dtype=torch.float32)
+        self.m2 = torch.zeros(D, device=device, dtype=torch.float32)
+        self.count = 0
+        self.clip = clip
+        self.eps = eps
+
+    @property
+    def var(self):
+        return self.m2 / max(self.count - 1, 1)
+
+    def update(self, x):
+        x2 = x.reshape(-1, self.D).float().contiguous()
+        N = x2.shape[0]
+        if N == 0:
+            return
+        if x2.is_cuda:
+            L = _lib.lib()
+            work = torch.empty(2 * L.ra_obsnorm_parts(N) * self.D, device=x2.device)
+            check(L.ra_obsnorm_update(ptr(x2), N, self.D, float(self.count), ptr(self.mean),
+                                      ptr(self.m2), ptr(work), stream_ptr()), "obsnorm_update")
+        else:
+            bm = x2.mean(0)
+            bm2 = ((x2 - bm) ** 2).sum(0)
+            n = self.count + N
+            d = bm - self.mean
+            self.mean = self.mean + d * N / n
+            self.m2 = self.m2 + bm2 + d * d * self.count * N / n
+        self.count += N
+
+    def normalize(self, x):
+        x2 = x.reshape(-1, self.D).float().contiguous()
+        if x2.is_cuda:
+            y = torch.empty_like(x2)
+            check(_lib.lib().ra_obsnorm_apply(ptr(x2), ptr(y), ptr(self.mean), ptr(self.m2),
+                                              x2.shape[0], self.D, float(self.count), self.clip,
+                                              self.eps, stream_ptr()), "obsnorm_apply")
+        else:
+            sd = torch.sqrt(torch.clamp(self.var, min=0))
+            y = torch.clamp((x2 - self.mean) / (sd + self.eps), -self.clip, self.clip)
+        return y.view(x.shape)
+
+    def __call__(self, x, update=True):
+        if update:
+            self.update(x)
+        return self.normalize(x)
+
+    def state_dict(self):
+        return {"mean": self.mean.cpu(), "m2": self.m2.cpu(), "count": self.count}
+
+    def load_state_dict(self, s):
+        self.mean = s["mean"].to(self.mean.device)
+        self.m2 = s["m2"].to(self.m2.device)
+        self.count = s["count"]
+
+
+# --------------------------------------------------------------------- Data preprocessing
+def image_normalize(x_u8_nhwc, mean, std, out_dtype=torch.float32):
+    """uint8 NHWC → normalised NCHW (fp32 or bf16)."""
+    if not _hip(x_u8_nhwc):
+        return ref.image_normalize(x_u8_nhwc, mean, std, out_dtype)
+    N, H, W, C = x_u8_nhwc.shape
+    dev = x_u8_nhwc.device
+    m = torch.as_tensor(mean, dtype=torch.float32).to(dev)
+    istd = (1.0 / torch.as_tensor(std, dtype=torch.float32)).to(dev)
+    y = torch.empty((N, C, H, W), dtype=out_dtype, device=dev)
+    check(_lib.lib().ra_image_normalize(ptr(x_u8_nhwc.contiguous()), ptr(y), N, H, W, C, ptr(m),
+                                        ptr(istd), 1 if out_dtype == torch.bfloat16 else 0,
+                                        stream_ptr()), "image_normalize")
+    return y
+
+
+def resize_bilinear(x_nchw, size):
+    OH, OW = size
+    if not _hip(x_nchw) or x_nchw.dtype not in (torch.float32, torch.bfloat16):
+        return torch.nn.functional.interpolate(x_nchw.float(), size=size, mode="bilinear",
+                                               align_corners=False).to(x_nchw.dtype)
+    N, C, H, W = x_nchw.shape
+    y = torch.empty((N, C, OH, OW), dtype=x_nchw.dtype, device=x_nchw.device)
+    check(_lib.lib().ra_resize_bilinear(ptr(x_nchw.contiguous()), ptr(y), N * C, H, W, OH, OW,
+                                        1 if x_nchw.dtype == torch.bfloat16 else 0, stream_ptr()),
+          "resize_bilinear")
+    return y
+
+
+def cast_scale_u8(x_u8, scale=1.0 / 255.0):
+    """uint8 → bf16 * scale (Atari frame scaling)."""
+    if not _hip(x_u8) or x_u8.numel() % 8:
+        return (x_u8.float() * scale).to(torch.bfloat16)
+    y = torch.empty(x_u8.shape, dtype=torch.bfloat16, device=x_u8.device)
+    check(_lib.lib().ra_cast_scale_u8(ptr(x_u8.contiguous()), ptr(y), x_u8.numel(), scale,
+                                      stream_ptr()), "cast_scale_u8")
+    return y

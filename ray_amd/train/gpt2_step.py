@@ -1,0 +1,63 @@
+"""One GPT-2 DDP training step on MI355X — the per-worker body of the headline
+Ray Train benchmark (TorchTrainer GPT-2-small DDP bf16).
+
+Used by ``bench.py`` (one rank per GPU under torch.distributed.run) and by
+``ray_amd.train.examples.gpt2.train_func`` (one rank per GPU as Train worker
+actors). Everything inside ``step()`` is real work: forward, backward, bucketed
+RCCL all-reduce overlapped with backward, global-norm clip, fused AdamW.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ray_amd.models.gpt2 import GPT2, GPT2Config
+from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams, cosine_lr
+
+
+class GPT2Trainer:
+    def __init__(self, cfg: GPT2Config, micro_batch: int, seq_len: int, device,
+                 lr: float = 6e-4, bucket_mb: float = 32.0, total_steps: int = 1000,
+                 warmup_steps: int = 10, seed: int = 1234, grad_accum: int = 1):
+        torch.manual_seed(seed)
+        self.cfg = cfg
+        self.B, self.T = micro_batch, seq_len
+        self.device = device
+        self.grad_accum = grad_accum
+        model = GPT2(cfg).to(device=device, dtype=torch.bfloat16)
+        self.model = model
+        self.flat = FlatParams(model)
+        self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb)
+        self.opt = FlatAdamW(self.flat, lr=lr, weight_decay=0.1, max_grad_norm=1.0,
+                             grad_scale=self.ddp.grad_scale / grad_accum)
+        self.base_lr = lr
+        self.total_steps = total_steps
+        self.warmup = warmup_steps
+        self.step_idx = 0
+        self.last_loss = None
+
+    def synthetic_batch(self, gen: torch.Generator | None = None):
+        x = torch.randint(0, self.cfg.vocab_size, (self.B, self.T + 1), device=self.device,
+                          generator=gen)
+        return x[:, :-1].contiguous(), x[:, 1:].contiguous()
+
+    def step(self, batches):
+        """batches: list of (idx, targets), len == grad_accum."""
+        self.flat.zero_grad()
+        loss_sum = None
+        for i, (x, y) in enumerate(batches):
+            self.ddp.sync = i == len(batches) - 1
+            loss = self.model(x, y)
+            loss.backward()
+            loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        self.ddp.finish()
+        lr = cosine_lr(self.step_idx, self.base_lr, self.warmup, self.total_steps)
+        self.opt.step(lr)
+        self.step_idx += 1
+        self.last_loss = loss_sum / len(batches)
+        return self.last_loss
+
+    def tokens_per_step(self) -> int:
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        return self.B * self.T * self.grad_accum * world

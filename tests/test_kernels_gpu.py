@@ -1,0 +1,206 @@
+"""Numerics of every HIP kernel vs a plain fp32 PyTorch reference (GPU only)."""
+
+import pytest
+import torch
+
+from ray_amd.ops import _lib
+from ray_amd.ops import functional as rf
+from ray_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_lib(cuda_device):
+    assert _lib.available(), "libray_amd_hip.so must load on a GPU box"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N,D", [(1000, 768), (64, 1024), (33, 1600), (8, 256)])
+def test_layernorm_fwd_bwd(cuda_device, N, D):
+    torch.manual_seed(0)
+    x = torch.randn(N, D, device=cuda_device).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    y = rf.layer_norm(x, w, b)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,F", [(512, 3072), (37, 64)])
+def test_bias_gelu(cuda_device, N, F):
+    torch.manual_seed(1)
+    h = torch.randn(N, F, device=cuda_device).bfloat16().requires_grad_()
+    b = (0.5 * torch.randn(F, device=cuda_device)).bfloat16().requires_grad_()
+    y = rf.bias_gelu(h, b)
+    hr, br = h.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = ref.gelu_tanh(hr + br)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert _rel(h.grad, hr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_bias_residual(cuda_device):
+    torch.manual_seed(2)
+    h = torch.randn(300, 768, device=cuda_device).bfloat16().requires_grad_()
+    b = torch.randn(768, device=cuda_device).bfloat16().requires_grad_()
+    r = torch.randn(300, 768, device=cuda_device).bfloat16().requires_grad_()
+    y = rf.bias_residual(h, b, r)
+    yr = h.detach().float() + b.detach().float() + r.detach().float()
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    assert _rel(b.grad, g.sum(0)) < 2e-2
+    assert _rel(h.grad, g) < 1e-2
+
+
+@pytest.mark.parametrize("N,V,Vp", [(256, 50257, 50304), (100, 1000, 1000)])
+def test_cross_entropy(cuda_device, N, V, Vp):
+    torch.manual_seed(3)
+    logits = (3 * torch.randn(N, Vp, device=cuda_device)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=cuda_device)
+    t[::17] = -100
+    loss = rf.cross_entropy(logits, t, V)
+    lr_ = logits.detach().float().requires_grad_()
+    lref = torch.nn.functional.cross_entropy(lr_[:, :V], t, ignore_index=-100)
+    assert abs(loss.item() - lref.item()) < 2e-3 * max(1.0, abs(lref.item()))
+    loss.backward()
+    lref.backward()
+    assert _rel(logits.grad, lr_.grad) < 2e-2
+    if Vp > V:
+        assert logits.grad[:, V:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("T,B", [(128, 8), (512, 16), (33, 2048), (1000, 3)])
+def test_gae(cuda_device, T, B):
+    torch.manual_seed(4)
+    r = torch.randn(T, B, device=cuda_device)
+    v = torch.randn(T, B, device=cuda_device)
+    d = (torch.rand(T, B, device=cuda_device) < 0.05).float()
+    bs = torch.randn(B, device=cuda_device)
+    adv, vt = rf.gae(r, v, d, bs, 0.99, 0.95)
+    adv_r, vt_r = ref.gae(r.double(), v.double(), d.double(), bs.double(), 0.99, 0.95)
+    assert torch.allclose(adv.double(), adv_r.double(), atol=1e-3, rtol=1e-3)
+    assert torch.allclose(vt.double(), vt_r.double(), atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("T,B", [(80, 32), (20, 4096), (300, 5)])
+def test_vtrace(cuda_device, T, B):
+    torch.manual_seed(5)
+    lr_ = 0.5 * torch.randn(T, B, device=cuda_device)
+    disc = 0.99 * (torch.rand(T, B, device=cuda_device) > 0.05).float()
+    r = torch.randn(T, B, device=cuda_device)
+    v = torch.randn(T, B, device=cuda_device)
+    bs = torch.randn(B, device=cuda_device)
+    vs, pg = rf.vtrace(lr_, disc, r, v, bs)
+    vs_r, pg_r = ref.vtrace(lr_.double(), disc.double(), r.double(), v.double(), bs.double())
+    assert torch.allclose(vs.double(), vs_r, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(pg.double(), pg_r, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("A", [2, 6, 18])
+def test_ppo_loss(cuda_device, A):
+    torch.manual_seed(6)
+    N = 1000
+    logits = torch.randn(N, A, device=cuda_device, requires_grad=True)
+    old = (logits.detach() + 0.3 * torch.randn(N, A, device=cuda_device))
+    acts = torch.randint(0, A, (N,), device=cuda_device)
+    old_lp = torch.log_softmax(old, -1).gather(-1, acts[:, None])[:, 0]
+    adv = torch.randn(N, device=cuda_device)
+    vp = torch.randn(N, device=cuda_device, requires_grad=True)
+    vt = torch.randn(N, device=cuda_device) * 3
+    kw = dict(clip=0.2, vf_clip=4.0, vf_coeff=0.5, ent_coeff=0.01, kl_coeff=0.2)
+    loss, stats = rf.ppo_loss(logits, old, acts, old_lp, adv, vp, vt, **kw)
+    lr_ = logits.detach().clone().requires_grad_()
+    vr = vp.detach().clone().requires_grad_()
+    lref, sref = ref.ppo_loss(lr_, old, acts, old_lp, adv, vr, vt, **kw)
+    assert abs(loss.item() - lref.item()) < 1e-4 * max(1, abs(lref.item()))
+    assert torch.allclose(stats, sref, atol=1e-4, rtol=1e-3)
+    loss.backward()
+    lref.backward()
+    assert torch.allclose(logits.grad, lr_.grad, atol=1e-6, rtol=1e-3)
+    assert torch.allclose(vp.grad, vr.grad, atol=1e-6, rtol=1e-3)
+
+
+def test_obsnorm(cuda_device):
+    torch.manual_seed(7)
+    rms = rf.RunningMeanStd(17, device=cuda_device)
+    cpu = rf.RunningMeanStd(17, device="cpu")
+    for n in (5, 300, 1000):
+        x = torch.randn(n, 17) * 3 + 2
+        rms.update(x.to(cuda_device))
+        cpu.update(x)
+    assert torch.allclose(rms.mean.cpu(), cpu.mean, atol=1e-4)
+    assert torch.allclose(rms.var.cpu(), cpu.var, atol=1e-3, rtol=1e-3)
+    x = torch.randn(64, 17) * 3 + 2
+    assert torch.allclose(rms.normalize(x.to(cuda_device)).cpu(), cpu.normalize(x), atol=1e-3)
+
+
+def test_image_normalize(cuda_device):
+    x = torch.randint(0, 256, (4, 37, 130, 3), dtype=torch.uint8, device=cuda_device)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    y = rf.image_normalize(x, mean, std)
+    yr = ref.image_normalize(x.cpu(), mean, std)
+    assert torch.allclose(y.cpu(), yr, atol=1e-5)
+    yb = rf.image_normalize(x, mean, std, torch.bfloat16)
+    assert _rel(yb, yr.to(cuda_device)) < 1e-2
+    z = rf.resize_bilinear(y, (20, 64))
+    zr = torch.nn.functional.interpolate(y, size=(20, 64), mode="bilinear", align_corners=False)
+    assert torch.allclose(z, zr, atol=1e-4)
+    c = rf.cast_scale_u8(x)
+    assert _rel(c, x.float() / 255) < 1e-2
+
+
+def test_flat_adamw_matches_torch(cuda_device):
+    from ray_amd.parallel.flat import FlatAdamW, FlatParams
+
+    torch.manual_seed(8)
+    m1 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.LayerNorm(128),
+                             torch.nn.Linear(128, 8)).to(cuda_device)
+    m2 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.LayerNorm(128),
+                             torch.nn.Linear(128, 8)).to(cuda_device)
+    m2.load_state_dict(m1.state_dict())
+    flat = FlatParams(m1, dtype=torch.float32)
+    opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=None)
+    decay = [p for p in m2.parameters() if p.dim() >= 2]
+    nod = [p for p in m2.parameters() if p.dim() < 2]
+    topt = torch.optim.AdamW([{"params": decay, "weight_decay": 0.1},
+                              {"params": nod, "weight_decay": 0.0}], lr=1e-2, betas=(0.9, 0.95),
+                             eps=1e-8)
+    for _ in range(5):
+        x = torch.randn(32, 64, device=cuda_device)
+        flat.zero_grad()
+        m1(x).square().mean().backward()
+        opt.step()
+        topt.zero_grad()
+        m2(x).square().mean().backward()
+        topt.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+
+
+def test_gpt2_tiny_trains(cuda_device):
+    from ray_amd.models.gpt2 import GPT2Config
+    from ray_amd.train.gpt2_step import GPT2Trainer
+
+    cfg = GPT2Config.tiny()
+    tr = GPT2Trainer(cfg, 8, 64, cuda_device, lr=3e-3, warmup_steps=2, total_steps=60)
+    x, y = tr.synthetic_batch()
+    first = None
+    for _ in range(40):
+        loss = float(tr.step([(x, y)]))
+        first = first or loss
+    assert loss < first * 0.7, (first, loss)
