@@ -31,6 +31,21 @@ static std::string as_str(const py::bytes& b) { return std::string(b); }
 
 static thread_local std::mt19937_64* tl_rng = nullptr;
 
+// A pinned view of a sealed object: exposes the buffer protocol and drops the
+// reader pin when the last Python view of it dies (numpy arrays deserialized
+// zero-copy from the store keep it alive through their base chain).
+struct PinnedBuf {
+  ShmStore* s = nullptr;
+  std::string id;
+  uint8_t* p = nullptr;
+  uint64_t n = 0;
+  bool readonly = true;
+  bool pinned = false;
+  ~PinnedBuf() {
+    if (pinned && s) s->release(id);
+  }
+};
+
 PYBIND11_MODULE(_core, m) {
   m.doc() = "ray_amd native runtime core: shm object store, frame I/O loop, scheduler";
 
@@ -72,6 +87,26 @@ PYBIND11_MODULE(_core, m) {
              return py::make_tuple(o.offset, o.data_size, o.meta_size, o.device);
            },
            py::arg("id"), py::arg("pin") = true)
+      .def("get_buffer",
+           [](ShmStore& s, py::bytes id, bool readonly) -> py::object {
+             ObjInfo o;
+             bool ok;
+             std::string k = as_str(id);
+             {
+               py::gil_scoped_release r;
+               ok = s.get(k, &o, true);
+             }
+             if (!ok) return py::none();
+             auto* b = new PinnedBuf();
+             b->s = &s;
+             b->id = k;
+             b->p = s.base() + o.offset;
+             b->n = o.data_size + o.meta_size;
+             b->readonly = readonly;
+             b->pinned = true;
+             return py::cast(b, py::return_value_policy::take_ownership);
+           },
+           py::arg("id"), py::arg("readonly") = true, py::keep_alive<0, 1>())
       .def("info",
            [](ShmStore& s, py::bytes id) -> py::object {
              ObjInfo o;
@@ -125,6 +160,17 @@ PYBIND11_MODULE(_core, m) {
       .def("evictions", &ShmStore::evictions)
       .def("release_all_pins_of", &ShmStore::release_all_pins_of)
       .def_property_readonly("size", &ShmStore::size);
+
+  py::class_<PinnedBuf>(m, "PinnedBuf", py::buffer_protocol())
+      .def_buffer([](PinnedBuf& b) {
+        return py::buffer_info(b.p, 1, py::format_descriptor<uint8_t>::format(), 1,
+                               {(ssize_t)b.n}, {(ssize_t)1}, b.readonly);
+      })
+      .def_property_readonly("size", [](PinnedBuf& b) { return b.n; })
+      .def("release", [](PinnedBuf& b) {
+        if (b.pinned && b.s) b.s->release(b.id);
+        b.pinned = false;
+      });
 
   py::class_<IOLoop>(m, "IOLoop")
       .def(py::init<>())

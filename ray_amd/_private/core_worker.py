@@ -1,0 +1,1792 @@
+"""CoreWorker: the per-process runtime (reference: src/ray/core_worker/core_worker.cc,
+reference_count.cc, task_manager.cc, transport/normal_task_submitter.cc,
+transport/actor_task_submitter.cc, task_receiver.cc).
+
+Threads:
+  * native IOLoop thread (C++): socket I/O, frame parsing, GIL-free.
+  * dispatcher thread: pulls frames, runs protocol handlers (never blocks).
+  * main thread: user code; in worker processes also the task executor loop.
+  * actor pools: thread pool (max_concurrency>1 / concurrency groups) or an
+    asyncio loop thread (async actors).
+
+Ownership: the process that creates an ObjectRef (by .remote() or put) owns it.
+Owners keep value (inline bytes for small objects, or the shm store entry),
+readiness, borrower set and containment pins. Borrowers register with the owner
+(async when ordering is implied by the channel, synchronously otherwise — see
+``_register_borrow``) and deregister when their local count reaches zero.
+"""
+
+from __future__ import annotations
+
+import collections
+import ctypes
+import hashlib
+import os
+import queue
+import sys
+import threading
+import time
+import traceback
+
+import cloudpickle
+
+from ray_amd._native import _core
+from ray_amd.exceptions import (GetTimeoutError, ObjectLostError, OwnerDiedError,
+                                RayActorError, RayTaskError, TaskCancelledError,
+                                WorkerCrashedError, ActorDiedError)
+
+from . import protocol as P
+from . import serialization as ser
+from .ids import object_id_for_put, object_id_for_return
+
+INLINE_MAX = 100 * 1024  # reference: max_direct_call_object_size
+ARGS_INLINE_MAX = 100 * 1024
+LEASE_IDLE_S = 0.02
+MAX_PENDING_LEASES_PER_KEY = 64
+
+_dumps = P.dumps
+_loads = P.loads
+
+
+class _Owned:
+    __slots__ = ("ready", "inline", "in_store", "callbacks", "borrowers", "contained",
+                 "release_when_ready", "task_id", "size", "node")
+
+    def __init__(self, task_id=None):
+        self.ready = False
+        self.inline = None
+        self.in_store = False
+        self.callbacks = None
+        self.borrowers = None
+        self.contained = None
+        self.release_when_ready = False
+        self.task_id = task_id
+        self.size = 0
+        self.node = None
+
+
+class _Remote:
+    """Borrower-side view of an object owned elsewhere."""
+
+    __slots__ = ("state", "inline", "error", "callbacks")
+
+    def __init__(self):
+        self.state = 0  # 0 unknown, 1 requested, 2 ready, 3 failed
+        self.inline = None
+        self.error = None
+        self.callbacks = []
+
+
+class _Lease:
+    __slots__ = ("addr", "lease_id", "inflight", "idle_since", "key", "gpu_ids", "worker_id")
+
+    def __init__(self, addr, lease_id, key, gpu_ids, worker_id):
+        self.addr = addr
+        self.lease_id = lease_id
+        self.inflight = {}
+        self.idle_since = time.monotonic()
+        self.key = key
+        self.gpu_ids = gpu_ids
+        self.worker_id = worker_id
+
+
+class _ActorConn:
+    __slots__ = ("actor_id", "state", "addr", "queue", "inflight", "seq", "subscribed",
+                 "death", "max_task_retries", "num_restarts")
+
+    def __init__(self, actor_id):
+        self.actor_id = actor_id
+        self.state = P.PENDING_CREATION
+        self.addr = None
+        self.queue = collections.deque()
+        self.inflight = {}
+        self.seq = 0
+        self.subscribed = False
+        self.death = None
+        self.max_task_retries = 0
+        self.num_restarts = 0
+
+
+class _Stream:
+    __slots__ = ("items", "done", "error_ref", "cv_waiters", "total")
+
+    def __init__(self):
+        self.items = {}
+        self.done = False
+        self.error_ref = None
+        self.total = None
+
+
+class _Waiter:
+    __slots__ = ("need", "done", "ev")
+
+    def __init__(self, need):
+        self.need = need
+        self.done = set()
+        self.ev = threading.Event()
+
+    def hit(self, oid):
+        self.done.add(oid)
+        if len(self.done) >= self.need:
+            self.ev.set()
+
+
+def _raise_in_thread(tid: int, exc_type) -> None:
+    ctypes.pythonapi.PyThreadState_SetAsyncExc(ctypes.c_ulong(tid), ctypes.py_object(exc_type))
+
+
+class CoreWorker:
+    def __init__(self, *, mode: str, session_dir: str, raylet_addr: str, worker_id: bytes,
+                 job_id: int | None = None, namespace: str | None = None,
+                 gpu_ids=None, node_id=None, startup_token=None, runtime_env=None):
+        self.mode = mode  # "driver" | "worker"
+        self.session_dir = session_dir
+        self.worker_id = worker_id
+        self.addr = os.path.join(session_dir, "sockets", worker_id.hex()[:24] + ".sock")
+        self.io = _core.IOLoop()
+        self.io.listen_unix(self.addr)
+        self.lock = threading.RLock()
+        self.raylet_addr = raylet_addr
+        self.conns: dict[str, int] = {}
+        self.conn_addr: dict[int, str] = {}
+        self._rid = 1
+        self._rpc_cb: dict[int, object] = {}
+        # ownership
+        self.refs: dict[bytes, list] = {}  # oid -> [count, owner, registered]
+        self.owned: dict[bytes, _Owned] = {}
+        self.remote: dict[bytes, _Remote] = {}
+        self.streams: dict[bytes, _Stream] = {}
+        # submission
+        self.sched_queues: dict = collections.defaultdict(collections.deque)
+        self.leases: dict = collections.defaultdict(list)
+        self.pending_leases: dict = collections.defaultdict(int)
+        self.task_specs: dict[bytes, dict] = {}  # tid -> spec (pending/running)
+        self.task_lease: dict[bytes, _Lease] = {}
+        self.actors: dict[bytes, _ActorConn] = {}
+        self.actor_handle_counts: collections.Counter = collections.Counter()
+        self.actor_escaped: set = set()
+        self.exported: set = set()
+        self.fn_cache: dict = {}
+        self.put_index = 0
+        self.task_counter = 0
+        # execution (worker side)
+        self.exec_queue: queue.Queue = queue.Queue()
+        self.current_task = threading.local()
+        self.running: dict[bytes, int] = {}  # tid -> thread ident
+        self.cancelled: set = set()
+        self.actor_instance = None
+        self.actor_id = None
+        self.actor_spec = None
+        self.actor_pools: dict = {}
+        self.async_loop = None
+        self.exiting = False
+        self.blocked_depth = 0
+        self.task_events: list = []
+        self.gpu_ids = gpu_ids or []
+        self.node_id = node_id
+        self.namespace = namespace
+        self.job_id = job_id
+        self.local_mode = False
+        self.runtime_env = runtime_env or {}
+        self.store = None
+        # connect to raylet
+        self.raylet_conn = self._connect(raylet_addr)
+        self._stopped = False
+        self.dispatcher = threading.Thread(target=self._dispatch_loop, name="ray_amd-dispatch",
+                                           daemon=True)
+        self.dispatcher.start()
+        reg = self.call_raylet("register", mode, worker_id, os.getpid(), self.addr, job_id,
+                               namespace, startup_token)
+        from .object_store import ObjectStore
+
+        self.node_id = reg["node_id"]
+        self.job_id = reg["job_id"]
+        self.namespace = reg.get("namespace") or namespace
+        self.node_ip = reg.get("node_ip", "127.0.0.1")
+        self.store = ObjectStore(reg["store_path"], reg["spill_dir"], create=False)
+        self.cluster_info = reg
+        self.task_id_base = os.urandom(12)
+
+    # ------------------------------------------------------------------ connections
+    def _connect(self, addr: str) -> int:
+        c = self.io.connect_unix(addr, 30000)
+        if c < 0:
+            raise ConnectionError(f"cannot connect to {addr}")
+        self.conns[addr] = c
+        self.conn_addr[c] = addr
+        self.io.send(c, _dumps((P.HELLO, self.addr, self.worker_id)))
+        return c
+
+    def _conn(self, addr: str) -> int:
+        c = self.conns.get(addr)
+        if c is not None:
+            return c
+        with self.lock:
+            c = self.conns.get(addr)
+            if c is not None:
+                return c
+            return self._connect(addr)
+
+    def send(self, addr: str, msg) -> bool:
+        try:
+            c = self._conn(addr)
+        except ConnectionError:
+            return False
+        ok = self.io.send(c, _dumps(msg))
+        return ok
+
+    def _next_rid(self) -> int:
+        with self.lock:
+            self._rid += 1
+            return self._rid
+
+    def call_async(self, addr: str, method: str, args: tuple, cb) -> None:
+        """cb(ok, value) runs on the dispatcher thread."""
+        rid = self._next_rid()
+        self._rpc_cb[rid] = (cb, addr)
+        if not self.send(addr, (P.REQ, rid, method, args)):
+            self._rpc_cb.pop(rid, None)
+            cb(False, ConnectionError(f"peer {addr} unreachable"))
+
+    def call(self, addr: str, method: str, *args, timeout: float | None = None):
+        if threading.current_thread() is self.dispatcher:
+            raise RuntimeError("blocking RPC from the dispatcher thread")
+        box = []
+        ev = threading.Event()
+
+        def cb(ok, value):
+            box.append((ok, value))
+            ev.set()
+
+        self.call_async(addr, method, args, cb)
+        if not ev.wait(timeout):
+            raise GetTimeoutError(f"RPC {method} to {addr} timed out")
+        ok, value = box[0]
+        if not ok:
+            if isinstance(value, BaseException):
+                raise value
+            raise RuntimeError(value)
+        return value
+
+    def call_raylet(self, method: str, *args, timeout: float | None = None):
+        return self.call(self.raylet_addr, method, *args, timeout=timeout)
+
+    def notify_raylet(self, method: str, *args):
+        self.send(self.raylet_addr, (P.REQ, 0, method, args))
+
+    # ------------------------------------------------------------------ dispatcher
+    def _dispatch_loop(self):
+        io = self.io
+        handlers = {
+            P.REQ: self._on_req,
+            P.RESP: self._on_resp,
+            P.PUSH: self._on_push,
+            P.HELLO: self._on_hello,
+            P.TASK: self._on_task,
+            P.TASK_REPLY: self._on_task_reply,
+            P.STREAM_ITEM: self._on_stream_item,
+        }
+        while not self._stopped:
+            try:
+                events = io.poll(10, 4096)
+            except Exception:
+                break
+            for typ, conn, payload in events:
+                try:
+                    if typ == 0:
+                        msg = _loads(payload)
+                        h = handlers.get(msg[0])
+                        if h is not None:
+                            h(conn, msg)
+                    elif typ == 2:
+                        self._on_conn_closed(conn)
+                except Exception:
+                    if not self._stopped:
+                        traceback.print_exc()
+            try:
+                self._reap_idle_leases()
+                if self.task_events and self.mode == "worker":
+                    self._flush_task_events()
+            except Exception:
+                if not self._stopped:
+                    traceback.print_exc()
+
+    def _on_hello(self, conn, msg):
+        addr = msg[1]
+        self.conn_addr[conn] = addr
+        with self.lock:
+            if addr not in self.conns:
+                self.conns[addr] = conn
+
+    def _on_resp(self, conn, msg):
+        _, rid, ok, value = msg
+        ent = self._rpc_cb.pop(rid, None)
+        if ent is not None:
+            ent[0](ok, value)
+
+    def _reply(self, conn, rid, ok, value):
+        if rid:
+            addr = self.conn_addr.get(conn)
+            if addr is not None and addr in self.conns:
+                self.send(addr, (P.RESP, rid, ok, value))
+            else:
+                self.io.send(conn, _dumps((P.RESP, rid, ok, value)))
+
+    def _on_req(self, conn, msg):
+        _, rid, method, args = msg
+        h = getattr(self, "_rpc_" + method, None)
+        if h is None:
+            self._reply(conn, rid, False, f"unknown method {method}")
+            return
+        try:
+            h(conn, rid, *args)
+        except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            self._reply(conn, rid, False, repr(e))
+
+    def _on_conn_closed(self, conn):
+        addr = self.conn_addr.pop(conn, None)
+        if addr is None:
+            return
+        with self.lock:
+            if self.conns.get(addr) == conn:
+                del self.conns[addr]
+        if addr == self.raylet_addr:
+            if not self._stopped and self.mode == "worker":
+                os._exit(1)
+            return
+        # fail outstanding RPCs to that peer
+        for rid, (cb, a) in list(self._rpc_cb.items()):
+            if a == addr:
+                self._rpc_cb.pop(rid, None)
+                cb(False, ConnectionError(f"peer {addr} died"))
+        # borrowers that died
+        with self.lock:
+            for o in self.owned.values():
+                if o.borrowers and addr in o.borrowers:
+                    o.borrowers.discard(addr)
+        dead = [oid for oid, o in list(self.owned.items())]
+        for oid in dead:
+            self._maybe_free(oid)
+        # leased worker died -> fail/retry its tasks
+        self._on_worker_lost(addr)
+        # actor died -> handled through raylet PUSH, but fail in-flight fast
+        for ac in list(self.actors.values()):
+            if ac.addr == addr and ac.state == P.ALIVE:
+                self._on_actor_conn_lost(ac)
+
+    def _on_push(self, conn, msg):
+        _, topic, data = msg
+        if topic == "actor":
+            self._on_actor_update(*data)
+        elif topic == "exit":
+            self.exiting = True
+            os._exit(0)
+
+    # ------------------------------------------------------------------ references
+    def add_local_ref(self, oid: bytes, owner: str, deserialized: bool = False):
+        register = False
+        with self.lock:
+            e = self.refs.get(oid)
+            if e is None:
+                e = self.refs[oid] = [1, owner, False]
+                if owner != self.addr and owner:
+                    e[2] = True
+                    register = True
+            else:
+                e[0] += 1
+        if register:
+            self._register_borrow(oid, owner)
+
+    def _register_borrow(self, oid, owner):
+        ctx = ser.current_deser_context()
+        anchor = ctx.anchor if ctx is not None else None
+        if anchor is None or anchor == owner or threading.current_thread() is self.dispatcher:
+            self.send(owner, (P.REQ, 0, "add_borrower", (oid, self.addr)))
+        else:
+            try:
+                self.call(owner, "add_borrower", oid, self.addr, timeout=30)
+            except Exception:
+                pass
+
+    def remove_local_ref(self, oid: bytes):
+        notify = None
+        with self.lock:
+            e = self.refs.get(oid)
+            if e is None:
+                return
+            e[0] -= 1
+            if e[0] > 0:
+                return
+            del self.refs[oid]
+            owned = e[1] == self.addr
+            if not owned:
+                self.remote.pop(oid, None)
+                if e[2]:
+                    notify = e[1]
+        if owned:
+            self._maybe_free(oid)
+        elif notify and not self._stopped:
+            self.send(notify, (P.REQ, 0, "remove_borrower", (oid, self.addr)))
+
+    def _maybe_free(self, oid: bytes):
+        contained = None
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is None or oid in self.refs or o.borrowers:
+                return
+            if not o.ready:
+                o.release_when_ready = True
+                return
+            del self.owned[oid]
+            contained = o.contained
+            in_store = o.in_store
+        if in_store and self.store is not None:
+            try:
+                self.store.delete(oid)
+            except Exception:
+                pass
+        del contained
+
+    def _rpc_add_borrower(self, conn, rid, oid, addr):
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is not None:
+                if o.borrowers is None:
+                    o.borrowers = set()
+                o.borrowers.add(addr)
+        self._reply(conn, rid, True, o is not None)
+
+    def _rpc_remove_borrower(self, conn, rid, oid, addr):
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is not None and o.borrowers:
+                o.borrowers.discard(addr)
+        self._maybe_free(oid)
+        self._reply(conn, rid, True, None)
+
+    # ------------------------------------------------------------------ object values
+    def _mark_ready(self, oid, inline=None, in_store=False, contained=None, size=0):
+        cbs = None
+        free = False
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is None:
+                # released while pending
+                if in_store and self.store is not None:
+                    self.store.delete(oid)
+                return
+            if o.ready:
+                return
+            o.inline = inline
+            o.in_store = in_store
+            o.contained = contained
+            o.size = size
+            o.ready = True
+            cbs = o.callbacks
+            o.callbacks = None
+            free = o.release_when_ready
+        if cbs:
+            for cb in cbs:
+                try:
+                    cb(oid)
+                except Exception:
+                    traceback.print_exc()
+        if free:
+            self._maybe_free(oid)
+
+    def put_object(self, value, owner_pinned=True) -> "object":
+        from ray_amd.object_ref import ObjectRef
+
+        with self.lock:
+            self.put_index += 1
+            idx = self.put_index
+        oid = object_id_for_put(self._current_task_id(), idx)
+        sobj = ser.serialize(value, oid)
+        return self._store_owned(oid, sobj, ObjectRef)
+
+    def put_serialized_object(self, oid, sobj):
+        from ray_amd.object_ref import ObjectRef
+
+        return self._store_owned(oid, sobj, ObjectRef)
+
+    def _store_owned(self, oid, sobj, ObjectRef):
+        o = _Owned()
+        with self.lock:
+            self.owned[oid] = o
+        ref = ObjectRef(oid, self.addr, _cw_obj=self)
+        contained = sobj.refs or None
+        if sobj.total <= INLINE_MAX and not sobj.gpu:
+            self._mark_ready(oid, inline=sobj.to_bytes(), contained=contained, size=sobj.total)
+        else:
+            self.store.put_serialized(oid, sobj, pinned=True)
+            self._mark_ready(oid, in_store=True, contained=contained, size=sobj.total)
+        return ref
+
+    def _current_task_id(self) -> bytes:
+        t = getattr(self.current_task, "tid", None)
+        if t is not None:
+            return t
+        return self.task_id_base + (0).to_bytes(4, "little")
+
+    def _on_ready(self, oid: bytes, cb) -> bool:
+        """Register cb(oid) for readiness. Returns True if already ready (cb not called)."""
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is not None:
+                if o.ready:
+                    return True
+                if o.callbacks is None:
+                    o.callbacks = []
+                o.callbacks.append(cb)
+                return False
+            e = self.refs.get(oid)
+            owner = e[1] if e else None
+            r = self.remote.get(oid)
+            if r is None:
+                r = self.remote[oid] = _Remote()
+            if r.state in (2, 3):
+                return True
+        if owner is None or owner == self.addr:
+            # not owned by us and no owner known: treat as lost
+            with self.lock:
+                r.state = 3
+                r.error = ObjectLostError(oid.hex())
+            return True
+        if self.store is not None and self.store.contains(oid):
+            with self.lock:
+                r.state = 2
+            return True
+        with self.lock:
+            r.callbacks.append(cb)
+            need_req = r.state == 0
+            if need_req:
+                r.state = 1
+        if need_req:
+            def on_reply(ok, value, oid=oid):
+                cbs = []
+                with self.lock:
+                    rr = self.remote.get(oid)
+                    if rr is None:
+                        rr = _Remote()
+                    if ok and value[0] == "inline":
+                        rr.state, rr.inline = 2, value[1]
+                    elif ok and value[0] == "store":
+                        rr.state = 2
+                    else:
+                        rr.state = 3
+                        rr.error = (OwnerDiedError(oid.hex()) if not ok else
+                                    ObjectLostError(oid.hex()))
+                    cbs, rr.callbacks = rr.callbacks, []
+                for c in cbs:
+                    c(oid)
+
+            self.call_async(owner, "get_object", (oid,), on_reply)
+        return False
+
+    def _rpc_get_object(self, conn, rid, oid):
+        def respond(_oid=oid):
+            with self.lock:
+                o = self.owned.get(oid)
+                if o is None:
+                    val = ("lost", None)
+                elif o.inline is not None:
+                    val = ("inline", o.inline)
+                else:
+                    val = ("store", self.node_id)
+            self._reply(conn, rid, True, val)
+
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is None:
+                self._reply(conn, rid, True, ("lost", None))
+                return
+            if not o.ready:
+                if o.callbacks is None:
+                    o.callbacks = []
+                o.callbacks.append(lambda _o: respond())
+                return
+        respond()
+
+    def _value_of(self, oid: bytes, anchor: str | None):
+        """Deserialize a READY object. Raises the stored error for error objects."""
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is not None:
+                inline, in_store = o.inline, o.in_store
+                owner = self.addr
+            else:
+                r = self.remote.get(oid)
+                inline = r.inline if r else None
+                in_store = inline is None
+                e = self.refs.get(oid)
+                owner = e[1] if e else None
+                if r is not None and r.state == 3:
+                    raise r.error
+        if inline is not None:
+            buf = inline
+        else:
+            buf = self.store.get_buffer(oid)
+            if buf is None:
+                raise ObjectLostError(oid.hex())
+        kind, value = ser.deserialize(buf, ser.DeserializeContext(anchor=owner))
+        if kind == ser.KIND_ERROR:
+            if isinstance(value, RayTaskError):
+                raise value.as_instanceof_cause()
+            raise value
+        return value
+
+    def wait_refs(self, oids, num_returns, timeout):
+        """Returns the list of ready oids (at least num_returns unless timeout)."""
+        w = _Waiter(num_returns)
+        pending = []
+        for oid in oids:
+            if self._on_ready(oid, w.hit):
+                w.done.add(oid)
+            else:
+                pending.append(oid)
+        if len(w.done) >= num_returns:
+            return w.done
+        deadline = None if timeout is None else time.monotonic() + timeout
+        blocked = self._maybe_notify_blocked()
+        try:
+            while len(w.done) < num_returns:
+                rem = None if deadline is None else max(0.0, deadline - time.monotonic())
+                if rem == 0.0:
+                    break
+                w.ev.wait(rem if rem is not None else 1.0)
+                w.ev.clear()
+                if len(w.done) >= num_returns:
+                    break
+                if self.exiting:
+                    break
+        finally:
+            if blocked:
+                self._notify_unblocked()
+        return set(w.done)
+
+    def get_objects(self, refs, timeout=None):
+        oids = [r._id for r in refs]
+        uniq = list(dict.fromkeys(oids))
+        ready = self.wait_refs(uniq, len(uniq), timeout)
+        if len(ready) < len(uniq):
+            raise GetTimeoutError(f"Get timed out: {len(uniq) - len(ready)} objects not ready "
+                                  f"after {timeout}s")
+        out = []
+        for r in refs:
+            out.append(self._value_of(r._id, None))
+        return out
+
+    def as_concurrent_future(self, ref):
+        import concurrent.futures
+
+        fut = concurrent.futures.Future()
+
+        def done(oid, ref=ref):
+            try:
+                fut.set_result(self._value_of(oid, None))
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        def cb(oid):
+            threading.Thread(target=done, args=(oid,), daemon=True).start()
+
+        if self._on_ready(ref._id, cb):
+            done(ref._id)
+        return fut
+
+    def _maybe_notify_blocked(self) -> bool:
+        if self.mode != "worker" or getattr(self.current_task, "tid", None) is None:
+            return False
+        lid = getattr(self.current_task, "lease_id", None)
+        if lid is None:
+            return False
+        with self.lock:
+            self.blocked_depth += 1
+            first = self.blocked_depth == 1
+        if first:
+            self.notify_raylet("notify_blocked", self.worker_id)
+        return True
+
+    def _notify_unblocked(self):
+        with self.lock:
+            self.blocked_depth -= 1
+            last = self.blocked_depth == 0
+        if last:
+            self.notify_raylet("notify_unblocked", self.worker_id)
+
+    # ------------------------------------------------------------------ functions
+    def export(self, obj) -> bytes:
+        """Export a function/class to the cluster KV; returns its key."""
+        key = getattr(obj, "__ray_amd_key__", None)
+        if key is not None and key in self.exported:
+            return key
+        data = cloudpickle.dumps(obj)
+        key = hashlib.blake2b(data, digest_size=16).digest()
+        if key not in self.exported:
+            self.notify_raylet("kv_put", "fn", key, data, True)
+            self.exported.add(key)
+            self.fn_cache[key] = obj
+        return key
+
+    def _load_function(self, key):
+        fn = self.fn_cache.get(key)
+        if fn is None:
+            data = self.call_raylet("kv_get", "fn", key)
+            if data is None:
+                raise RuntimeError(f"function {key.hex()} not found in cluster KV")
+            fn = cloudpickle.loads(data)
+            self.fn_cache[key] = fn
+        return fn
+
+    # ------------------------------------------------------------------ args
+    def _encode_args(self, args, kwargs):
+        """Top-level ObjectRef args are resolved by the executor; everything else is
+        serialized in one blob (large blobs go to the store)."""
+        from ray_amd.object_ref import ObjectRef
+
+        ref_args = []
+        holders = []
+        if any(isinstance(a, ObjectRef) for a in args) or \
+                any(isinstance(v, ObjectRef) for v in kwargs.values()):
+            a2 = []
+            for a in args:
+                if isinstance(a, ObjectRef):
+                    a2.append(_ArgRef(len(ref_args)))
+                    ref_args.append(self._ref_desc(a))
+                    holders.append(a)
+                else:
+                    a2.append(a)
+            k2 = {}
+            for k, v in kwargs.items():
+                if isinstance(v, ObjectRef):
+                    k2[k] = _ArgRef(len(ref_args))
+                    ref_args.append(self._ref_desc(v))
+                    holders.append(v)
+                else:
+                    k2[k] = v
+            args, kwargs = a2, k2
+        if not args and not kwargs:
+            return (None, ref_args), holders
+        sobj = ser.serialize((args, kwargs))
+        holders.extend(sobj.refs)
+        if sobj.total > ARGS_INLINE_MAX or sobj.gpu:
+            ref = self.put_serialized_object(
+                object_id_for_put(self._current_task_id(), self._bump_put()), sobj)
+            holders.append(ref)
+            return (("s", ref._id, self.addr), ref_args), holders
+        return (sobj.to_bytes(), ref_args), holders
+
+    def _bump_put(self):
+        with self.lock:
+            self.put_index += 1
+            return self.put_index
+
+    def _ref_desc(self, ref):
+        oid = ref._id
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is not None and o.ready and o.inline is not None:
+                return (oid, ref._owner, o.inline)
+        return (oid, ref._owner, None)
+
+    def _decode_args(self, encoded, owner_addr):
+        blob, ref_args = encoded
+        vals = []
+        if ref_args:
+            from ray_amd.object_ref import ObjectRef
+
+            need = []
+            for oid, owner, inline in ref_args:
+                if inline is not None:
+                    vals.append(("v", inline, owner))
+                else:
+                    ref = ObjectRef(oid, owner, _cw_obj=self)
+                    need.append(ref)
+                    vals.append(("r", ref, owner))
+            if need:
+                self.wait_refs([r._id for r in need], len(need), None)
+            res = []
+            for kind, x, owner in vals:
+                if kind == "v":
+                    k, v = ser.deserialize(x, ser.DeserializeContext(anchor=owner_addr))
+                    if k == ser.KIND_ERROR:
+                        raise v.as_instanceof_cause() if isinstance(v, RayTaskError) else v
+                    res.append(v)
+                else:
+                    res.append(self._value_of(x._id, owner_addr))
+            vals = res
+        if blob is None:
+            args, kwargs = [], {}
+        else:
+            if isinstance(blob, tuple):
+                _, oid, owner = blob
+                buf = self.store.get_buffer(oid)
+                if buf is None:
+                    raise ObjectLostError(oid.hex())
+            else:
+                buf = blob
+            _, (args, kwargs) = ser.deserialize(buf, ser.DeserializeContext(anchor=owner_addr))
+        if ref_args:
+            args = [vals[a.i] if isinstance(a, _ArgRef) else a for a in args]
+            kwargs = {k: (vals[v.i] if isinstance(v, _ArgRef) else v) for k, v in kwargs.items()}
+        return args, kwargs
+
+    # ------------------------------------------------------------------ normal tasks
+    def new_task_id(self) -> bytes:
+        with self.lock:
+            self.task_counter += 1
+            c = self.task_counter
+        return self.task_id_base + c.to_bytes(4, "little")
+
+    def submit_task(self, fn_key, args, kwargs, opts: dict, name: str):
+        """Submit a normal task; returns list of ObjectRefs (or a generator)."""
+        from ray_amd.object_ref import ObjectRef, ObjectRefGenerator
+
+        tid = self.new_task_id()
+        nret = opts.get("num_returns", 1)
+        dynamic = nret == "dynamic"
+        if dynamic:
+            nret = 1
+        streaming = nret == "streaming"
+        encoded, holders = self._encode_args(args, kwargs)
+        spec = {
+            "tid": tid, "type": P.NORMAL_TASK, "fn": fn_key, "args": encoded,
+            "nret": -1 if streaming else nret, "owner": self.addr, "name": name,
+            "resources": opts["resources"], "strategy": opts.get("strategy"),
+            "retries": opts.get("max_retries", 3), "retry_exc": opts.get("retry_exceptions", False),
+            "runtime_env": opts.get("runtime_env"), "attempt": 0, "job": self.job_id,
+            "dynamic": dynamic,
+        }
+        refs = []
+        with self.lock:
+            if streaming:
+                self.streams[tid] = _Stream()
+            else:
+                for i in range(nret):
+                    oid = object_id_for_return(tid, i + 1)
+                    self.owned[oid] = _Owned(tid)
+            self.task_specs[tid] = spec
+        if not streaming:
+            refs = [ObjectRef(object_id_for_return(tid, i + 1), self.addr, _cw_obj=self)
+                    for i in range(nret)]
+        spec["_holders"] = holders
+        if self.local_mode:
+            self._run_local(spec)
+        else:
+            self._resolve_and_schedule(spec)
+        if streaming:
+            return ObjectRefGenerator(tid, self, self.addr)
+        return refs
+
+    def _resolve_and_schedule(self, spec):
+        """Owner-side dependency resolution: wait for owned pending args."""
+        pending = []
+        for oid, owner, inline in spec["args"][1]:
+            if owner == self.addr and inline is None:
+                with self.lock:
+                    o = self.owned.get(oid)
+                    if o is not None and not o.ready:
+                        pending.append(oid)
+        if not pending:
+            self._inline_ready_args(spec)
+            self._schedule(spec)
+            return
+        remaining = [len(pending)]
+        lock = threading.Lock()
+
+        def dep_ready(_oid):
+            with lock:
+                remaining[0] -= 1
+                done = remaining[0] == 0
+            if done:
+                self._inline_ready_args(spec)
+                self._schedule(spec)
+
+        for oid in pending:
+            if self._on_ready(oid, dep_ready):
+                dep_ready(oid)
+
+    def _inline_ready_args(self, spec):
+        blob, ref_args = spec["args"]
+        if not ref_args:
+            return
+        new = []
+        for oid, owner, inline in ref_args:
+            if inline is None and owner == self.addr:
+                with self.lock:
+                    o = self.owned.get(oid)
+                    if o is not None and o.ready and o.inline is not None:
+                        inline = o.inline
+            new.append((oid, owner, inline))
+        spec["args"] = (blob, new)
+
+    @staticmethod
+    def _sched_key(spec):
+        res = spec["resources"]
+        st = spec.get("strategy")
+        renv = spec.get("runtime_env")
+        return (tuple(sorted(res.items())), repr(st), repr(renv) if renv else None)
+
+    def _schedule(self, spec):
+        key = self._sched_key(spec)
+        with self.lock:
+            if spec["tid"] in self.cancelled:
+                cancelled = True
+            else:
+                cancelled = False
+                self.sched_queues[key].append(spec)
+        if cancelled:
+            self._fail_task(spec, TaskCancelledError(spec["tid"].hex()))
+            return
+        self._pump(key)
+
+    def _pump(self, key):
+        to_send = []
+        request = 0
+        with self.lock:
+            q = self.sched_queues.get(key)
+            if not q:
+                return
+            for lease in self.leases.get(key, ()):
+                while q and not lease.inflight:
+                    spec = q.popleft()
+                    lease.inflight[spec["tid"]] = spec
+                    self.task_lease[spec["tid"]] = lease
+                    to_send.append((lease, spec))
+            if q:
+                want = min(len(q), MAX_PENDING_LEASES_PER_KEY) - self.pending_leases[key]
+                if want > 0:
+                    request = want
+                    self.pending_leases[key] += want
+        for lease, spec in to_send:
+            self._push_task(lease.addr, spec, lease.lease_id)
+        for _ in range(request):
+            self._request_lease(key)
+
+    def _push_task(self, addr, spec, lease_id):
+        wire = {k: v for k, v in spec.items() if not k.startswith("_")}
+        wire["lease_id"] = lease_id
+        if not self.send(addr, (P.TASK, wire)):
+            self._on_worker_lost(addr)
+
+    def _request_lease(self, key):
+        res, strat_repr, _ = key
+        with self.lock:
+            q = self.sched_queues.get(key)
+            sample = q[0] if q else None
+        if sample is None:
+            with self.lock:
+                self.pending_leases[key] -= 1
+            return
+        req = {
+            "resources": sample["resources"], "strategy": sample.get("strategy"),
+            "runtime_env": sample.get("runtime_env"), "owner": self.addr, "job": self.job_id,
+            "name": sample.get("name"),
+        }
+
+        def on_lease(ok, value, key=key):
+            with self.lock:
+                self.pending_leases[key] -= 1
+            if not ok:
+                err = value if isinstance(value, BaseException) else RuntimeError(str(value))
+                with self.lock:
+                    q = self.sched_queues.pop(key, collections.deque())
+                for spec in q:
+                    self._fail_task(spec, err)
+                return
+            lease = _Lease(value["addr"], value["lease_id"], key, value.get("gpu_ids"),
+                           value.get("worker_id"))
+            with self.lock:
+                self.leases[key].append(lease)
+            self._pump(key)
+            # nothing left to run on it: give it back
+            self._maybe_return_lease(lease, force=False)
+
+        self.call_async(self.raylet_addr, "request_lease", (req,), on_lease)
+
+    def _maybe_return_lease(self, lease, force):
+        with self.lock:
+            if lease.inflight:
+                return
+            q = self.sched_queues.get(lease.key)
+            if q and not force:
+                return
+            if not force and time.monotonic() - lease.idle_since < LEASE_IDLE_S:
+                return
+            try:
+                self.leases[lease.key].remove(lease)
+            except ValueError:
+                return
+        self.notify_raylet("return_lease", lease.lease_id, False)
+
+    def _reap_idle_leases(self):
+        now = time.monotonic()
+        for key, ls in list(self.leases.items()):
+            for lease in list(ls):
+                if not lease.inflight and now - lease.idle_since >= LEASE_IDLE_S:
+                    self._maybe_return_lease(lease, force=False)
+
+    def _on_task_reply(self, conn, msg):
+        _, tid, returns, extra = msg
+        with self.lock:
+            spec = self.task_specs.get(tid)
+        if spec is None:
+            # unknown (cancelled / duplicate): drop store results
+            for oid, kind, payload, contained in returns:
+                if kind == P.RET_STORE:
+                    self.store.delete(oid)
+            return
+        if spec["type"] == P.ACTOR_TASK:
+            self._on_actor_task_reply(spec, returns, extra)
+            return
+        lease = None
+        with self.lock:
+            lease = self.task_lease.pop(tid, None)
+            if lease is not None:
+                lease.inflight.pop(tid, None)
+                lease.idle_since = time.monotonic()
+        # application-level retry
+        if extra.get("app_error") and self._should_retry_exc(spec, extra.get("exc_type")):
+            for oid, kind, payload, contained in returns:
+                if kind == P.RET_STORE:
+                    self.store.delete(oid)
+            spec["retries"] -= 1 if spec["retries"] > 0 else 0
+            spec["attempt"] += 1
+            self._schedule(spec)
+        else:
+            self._complete(spec, returns, extra)
+        if lease is not None:
+            self._pump(lease.key)
+
+    def _should_retry_exc(self, spec, exc_type_name):
+        re = spec.get("retry_exc")
+        if not re or spec["retries"] == 0:
+            return False
+        if re is True:
+            return True
+        names = {getattr(c, "__name__", str(c)) for c in re}
+        return exc_type_name in names
+
+    def _complete(self, spec, returns, extra):
+        from ray_amd.object_ref import ObjectRef
+
+        tid = spec["tid"]
+        with self.lock:
+            self.task_specs.pop(tid, None)
+        if spec["nret"] == -1:
+            st = self.streams.get(tid)
+            if st is not None:
+                with self.lock:
+                    st.done = True
+                    st.total = extra.get("num_items")
+                    if returns:
+                        oid, kind, payload, contained = returns[0]
+                        self.owned[oid] = _Owned(tid)
+                        st.error_ref = ObjectRef(oid, self.addr, _cw_obj=self)
+                    else:
+                        st.error_ref = None
+                if returns:
+                    self._mark_ready(returns[0][0], inline=returns[0][2])
+                self._wake_stream(tid)
+            return
+        for oid, kind, payload, contained in returns:
+            pins = None
+            if contained:
+                pins = [ObjectRef(c_oid, c_owner, _cw_obj=self) for c_oid, c_owner in contained]
+            if kind == P.RET_INLINE:
+                self._mark_ready(oid, inline=payload, contained=pins, size=len(payload))
+            else:
+                self._mark_ready(oid, in_store=True, contained=pins, size=payload)
+        spec.pop("_holders", None)
+
+    def _fail_task(self, spec, exc):
+        sobj = ser.serialize_error(exc)
+        data = sobj.to_bytes()
+        tid = spec["tid"]
+        with self.lock:
+            self.task_specs.pop(tid, None)
+        if spec["nret"] == -1:
+            st = self.streams.get(tid)
+            if st is not None:
+                from ray_amd.object_ref import ObjectRef
+
+                oid = object_id_for_return(tid, 0x7FFFFFFF)
+                with self.lock:
+                    self.owned[oid] = _Owned(tid)
+                    st.error_ref = ObjectRef(oid, self.addr, _cw_obj=self)
+                    st.done = True
+                self._mark_ready(oid, inline=data)
+                self._wake_stream(tid)
+            return
+        n = spec["nret"] if spec["type"] != P.ACTOR_CREATION_TASK else 0
+        for i in range(n):
+            self._mark_ready(object_id_for_return(tid, i + 1), inline=data)
+        spec.pop("_holders", None)
+
+    def _on_worker_lost(self, addr):
+        lost = []
+        with self.lock:
+            for key, ls in list(self.leases.items()):
+                for lease in list(ls):
+                    if lease.addr == addr:
+                        ls.remove(lease)
+                        lost.extend(lease.inflight.values())
+                        for t in lease.inflight:
+                            self.task_lease.pop(t, None)
+                        lease.inflight.clear()
+        for spec in lost:
+            if spec["retries"] != 0:
+                if spec["retries"] > 0:
+                    spec["retries"] -= 1
+                spec["attempt"] += 1
+                self._schedule(spec)
+            else:
+                self._fail_task(spec, WorkerCrashedError())
+
+    # ------------------------------------------------------------------ streaming
+    def _on_stream_item(self, conn, msg):
+        _, tid, index, ret = msg
+        from ray_amd.object_ref import ObjectRef
+
+        oid, kind, payload, contained = ret
+        st = self.streams.get(tid)
+        if st is None:
+            if kind == P.RET_STORE:
+                self.store.delete(oid)
+            return
+        with self.lock:
+            self.owned[oid] = _Owned(tid)
+        ref = ObjectRef(oid, self.addr, _cw_obj=self)
+        pins = [ObjectRef(a, b, _cw_obj=self) for a, b in contained] if contained else None
+        if kind == P.RET_INLINE:
+            self._mark_ready(oid, inline=payload, contained=pins)
+        else:
+            self._mark_ready(oid, in_store=True, contained=pins, size=payload)
+        with self.lock:
+            st.items[index] = ref
+        self._wake_stream(tid)
+
+    def _wake_stream(self, tid):
+        with self.lock:
+            self._stream_cv().notify_all()
+
+    def _stream_cv(self):
+        cv = getattr(self, "_scv", None)
+        if cv is None:
+            self._scv = cv = threading.Condition(self.lock)
+        return cv
+
+    def next_stream_item(self, tid, index, timeout):
+        cv = self._stream_cv()
+        with self.lock:
+            st = self.streams.get(tid)
+            if st is None:
+                return None
+            while True:
+                if index in st.items:
+                    return st.items.pop(index)
+                if st.done:
+                    if st.total is not None and index < st.total:
+                        pass  # item message still in flight
+                    else:
+                        if st.error_ref is not None:
+                            r, st.error_ref = st.error_ref, None
+                            return r
+                        return None
+                cv.wait(0.5)
+
+    def stream_completed_ref(self, tid):
+        with self.lock:
+            st = self.streams.get(tid)
+            return st is not None and st.done
+
+    def drop_stream(self, tid):
+        with self.lock:
+            self.streams.pop(tid, None)
+
+    # ------------------------------------------------------------------ cancellation
+    def cancel(self, ref, force=False, recursive=True):
+        tid = ref._id[:16]
+        with self.lock:
+            spec = self.task_specs.get(tid)
+            if spec is None:
+                return
+            self.cancelled.add(tid)
+            # still queued locally?
+            for key, q in self.sched_queues.items():
+                if spec in q:
+                    q.remove(spec)
+                    queued = True
+                    break
+            else:
+                queued = False
+            lease = self.task_lease.get(tid)
+        if queued:
+            self._fail_task(spec, TaskCancelledError(tid.hex()))
+            return
+        if spec["type"] == P.ACTOR_TASK:
+            ac = self.actors.get(spec["actor_id"])
+            if ac is not None and ac.addr:
+                self.send(ac.addr, (P.REQ, 0, "cancel_task", (tid, force)))
+            return
+        if lease is not None:
+            self.send(lease.addr, (P.REQ, 0, "cancel_task", (tid, force)))
+
+    def _rpc_cancel_task(self, conn, rid, tid, force):
+        with self.lock:
+            self.cancelled.add(tid)
+            th = self.running.get(tid)
+        if th is not None:
+            if force:
+                os._exit(1)
+            _raise_in_thread(th, KeyboardInterrupt)
+        self._reply(conn, rid, True, None)
+
+    # ------------------------------------------------------------------ actors (caller)
+    def create_actor(self, actor_id: bytes, cls_key, args, kwargs, opts: dict, cls_name: str,
+                     method_meta: dict):
+        encoded, holders = self._encode_args(args, kwargs)
+        spec = {
+            "tid": self.new_task_id(), "type": P.ACTOR_CREATION_TASK, "fn": cls_key,
+            "args": encoded, "nret": 0, "owner": self.addr, "name": cls_name,
+            "resources": opts["resources"], "strategy": opts.get("strategy"),
+            "actor_id": actor_id, "max_concurrency": opts.get("max_concurrency"),
+            "concurrency_groups": opts.get("concurrency_groups"),
+            "is_async": method_meta.get("__is_async__", False),
+            "runtime_env": opts.get("runtime_env"), "job": self.job_id,
+            "method_meta": method_meta,
+        }
+        self._inline_ready_args(spec)
+        info = {
+            "actor_id": actor_id, "name": opts.get("name"),
+            "namespace": opts.get("namespace") or self.namespace,
+            "lifetime": opts.get("lifetime"), "max_restarts": opts.get("max_restarts", 0),
+            "owner": self.addr, "class_name": cls_name, "get_if_exists": opts.get("get_if_exists"),
+            "max_task_retries": opts.get("max_task_retries", 0),
+        }
+        # args that are pending owned refs must be ready before the raylet runs __init__
+        pend = [oid for oid, owner, inline in encoded[1] if owner == self.addr and inline is None]
+        if pend:
+            self.wait_refs(pend, len(pend), None)
+            self._inline_ready_args(spec)
+        existing = self.call_raylet("create_actor", info, {k: v for k, v in spec.items()
+                                                            if not k.startswith("_")})
+        with self.lock:
+            ac = self.actors.get(actor_id)
+            if ac is None:
+                ac = self.actors[actor_id] = _ActorConn(actor_id)
+            ac.max_task_retries = opts.get("max_task_retries", 0)
+        self._holders_keepalive(actor_id, holders)
+        self._subscribe_actor(actor_id)
+        return existing
+
+    def _holders_keepalive(self, actor_id, holders):
+        if holders:
+            if not hasattr(self, "_actor_arg_pins"):
+                self._actor_arg_pins = {}
+            self._actor_arg_pins[actor_id] = holders
+
+    def _subscribe_actor(self, actor_id):
+        with self.lock:
+            ac = self.actors.get(actor_id)
+            if ac is None:
+                ac = self.actors[actor_id] = _ActorConn(actor_id)
+            if ac.subscribed:
+                return
+            ac.subscribed = True
+        self.call_async(self.raylet_addr, "subscribe_actor", (actor_id,),
+                        lambda ok, v: self._on_actor_update(*v) if ok and v else None)
+
+    def _on_actor_update(self, actor_id, state, addr, death, num_restarts=0):
+        to_send = []
+        to_fail = []
+        with self.lock:
+            ac = self.actors.get(actor_id)
+            if ac is None:
+                return
+            if state == P.ALIVE:
+                if ac.state == P.ALIVE and ac.addr == addr:
+                    return
+                ac.state, ac.addr = P.ALIVE, addr
+                ac.num_restarts = num_restarts
+                # resend in-flight (retryable) + queued, in sequence order
+                pending = sorted(list(ac.inflight.values()) + list(ac.queue),
+                                 key=lambda s: s["seq"])
+                ac.inflight.clear()
+                ac.queue.clear()
+                for s in pending:
+                    ac.inflight[s["tid"]] = s
+                    to_send.append(s)
+            elif state == P.DEAD:
+                ac.state = P.DEAD
+                ac.death = death
+                to_fail = list(ac.inflight.values()) + list(ac.queue)
+                ac.inflight.clear()
+                ac.queue.clear()
+            else:
+                if ac.state == P.ALIVE and state == P.RESTARTING:
+                    self._requeue_inflight(ac)
+                ac.state = state
+        for s in to_send:
+            self._send_actor_task(addr, s)
+        for s in to_fail:
+            self._fail_task(s, self._actor_error(actor_id, death))
+
+    def _actor_error(self, actor_id, death):
+        if isinstance(death, RayActorError):
+            return death
+        if isinstance(death, BaseException):
+            e = ActorDiedError(actor_id.hex(), "The actor died because of an error raised in "
+                               f"its creation task, {death}")
+            e.cause = death
+            return e
+        return ActorDiedError(actor_id.hex(), death or "The actor died unexpectedly.")
+
+    def _requeue_inflight(self, ac):
+        # called with lock held; in-flight tasks either retry or fail
+        fail = []
+        for tid, s in list(ac.inflight.items()):
+            if s.get("retries", 0) != 0:
+                if s["retries"] > 0:
+                    s["retries"] -= 1
+                ac.queue.append(s)
+            else:
+                fail.append(s)
+        ac.inflight.clear()
+        for s in fail:
+            threading.Thread(target=self._fail_task,
+                             args=(s, RayActorError(ac.actor_id.hex(),
+                                                    "The actor died while running this task.")),
+                             daemon=True).start()
+
+    def _on_actor_conn_lost(self, ac):
+        with self.lock:
+            if ac.state != P.ALIVE:
+                return
+            ac.state = P.RESTARTING
+            self._requeue_inflight(ac)
+
+    def submit_actor_task(self, actor_id, method, args, kwargs, opts):
+        from ray_amd.object_ref import ObjectRef, ObjectRefGenerator
+
+        tid = self.new_task_id()
+        nret = opts.get("num_returns", 1)
+        streaming = nret in ("streaming", "dynamic")
+        encoded, holders = self._encode_args(args, kwargs)
+        with self.lock:
+            ac = self.actors.get(actor_id)
+            if ac is None:
+                ac = self.actors[actor_id] = _ActorConn(actor_id)
+            ac.seq += 1
+            seq = ac.seq
+        spec = {
+            "tid": tid, "type": P.ACTOR_TASK, "actor_id": actor_id, "method": method,
+            "args": encoded, "nret": -1 if streaming else nret, "owner": self.addr,
+            "seq": seq, "name": opts.get("name") or method, "job": self.job_id,
+            "retries": opts.get("max_task_retries", ac.max_task_retries),
+            "concurrency_group": opts.get("concurrency_group"), "_holders": holders,
+        }
+        with self.lock:
+            if streaming:
+                self.streams[tid] = _Stream()
+            else:
+                for i in range(nret):
+                    self.owned[object_id_for_return(tid, i + 1)] = _Owned(tid)
+            self.task_specs[tid] = spec
+        refs = [] if streaming else [ObjectRef(object_id_for_return(tid, i + 1), self.addr,
+                                               _cw_obj=self) for i in range(nret)]
+        self._subscribe_actor(actor_id)
+        # wait for owned pending args (ordering preserved: we block the caller)
+        pend = [oid for oid, owner, inline in encoded[1] if owner == self.addr and inline is None]
+        if pend:
+            def go():
+                self.wait_refs(pend, len(pend), None)
+                self._inline_ready_args(spec)
+                self._enqueue_actor_task(ac, spec)
+
+            if threading.current_thread() is self.dispatcher:
+                threading.Thread(target=go, daemon=True).start()
+            else:
+                go()
+        else:
+            self._enqueue_actor_task(ac, spec)
+        if streaming:
+            return ObjectRefGenerator(tid, self, self.addr)
+        return refs
+
+    def _enqueue_actor_task(self, ac, spec):
+        send_to = None
+        fail = None
+        with self.lock:
+            if ac.state == P.ALIVE:
+                ac.inflight[spec["tid"]] = spec
+                send_to = ac.addr
+            elif ac.state == P.DEAD:
+                fail = ac.death
+            else:
+                ac.queue.append(spec)
+        if send_to:
+            self._send_actor_task(send_to, spec)
+        elif fail is not None or (ac.state == P.DEAD):
+            self._fail_task(spec, self._actor_error(ac.actor_id, fail))
+
+    def _send_actor_task(self, addr, spec):
+        wire = {k: v for k, v in spec.items() if not k.startswith("_")}
+        if not self.send(addr, (P.TASK, wire)):
+            with self.lock:
+                ac = self.actors.get(spec["actor_id"])
+            if ac is not None:
+                self._on_actor_conn_lost(ac)
+
+    def _on_actor_task_reply(self, spec, returns, extra):
+        with self.lock:
+            ac = self.actors.get(spec["actor_id"])
+            if ac is not None:
+                ac.inflight.pop(spec["tid"], None)
+        self._complete(spec, returns, extra)
+
+    def kill_actor(self, actor_id, no_restart=True):
+        self.call_raylet("kill_actor", actor_id, no_restart)
+
+    def actor_handle_created(self, actor_id):
+        with self.lock:
+            self.actor_handle_counts[actor_id] += 1
+
+    def actor_handle_deleted(self, actor_id, owner_addr):
+        kill = False
+        with self.lock:
+            self.actor_handle_counts[actor_id] -= 1
+            if self.actor_handle_counts[actor_id] <= 0:
+                del self.actor_handle_counts[actor_id]
+                kill = (owner_addr == self.addr and actor_id not in self.actor_escaped)
+        if kill and not self._stopped:
+            self.notify_raylet("actor_out_of_scope", actor_id)
+
+    # ------------------------------------------------------------------ execution
+    def _on_task(self, conn, msg):
+        spec = msg[1]
+        spec["_conn"] = conn
+        if spec["type"] == P.ACTOR_TASK and self.actor_pools:
+            self._dispatch_actor_task(spec)
+        else:
+            self.exec_queue.put(spec)
+
+    def _dispatch_actor_task(self, spec):
+        if self.async_loop is not None:
+            import asyncio
+
+            asyncio.run_coroutine_threadsafe(self._run_async_actor_task(spec), self.async_loop)
+            return
+        grp = spec.get("concurrency_group")
+        if grp is None:
+            grp = self.actor_method_groups.get(spec["method"], "_default")
+        pool = self.actor_pools.get(grp) or self.actor_pools["_default"]
+        pool.submit(self._execute, spec)
+
+    def run_task_loop(self):
+        """Main-thread executor loop for worker processes."""
+        while not self.exiting:
+            try:
+                spec = self.exec_queue.get(timeout=1.0)
+            except queue.Empty:
+                continue
+            if spec is None:
+                break
+            if spec["type"] == P.ACTOR_TASK and self.actor_pools:
+                self._dispatch_actor_task(spec)
+                continue
+            self._execute(spec)
+
+    def _execute(self, spec):
+        tid = spec["tid"]
+        reply_to = spec["owner"] if spec["type"] != P.ACTOR_CREATION_TASK else None
+        conn = spec.pop("_conn", None)
+        if tid in self.cancelled:
+            self._send_reply(conn, reply_to, tid, self._error_returns(
+                spec, TaskCancelledError(tid.hex())), {})
+            return
+        self.current_task.tid = tid
+        self.current_task.spec = spec
+        self.current_task.lease_id = spec.get("lease_id")
+        with self.lock:
+            self.running[tid] = threading.get_ident()
+        t0 = time.time()
+        extra = {}
+        name = spec.get("name") or "task"
+        try:
+            if spec["type"] == P.ACTOR_CREATION_TASK:
+                returns = self._execute_actor_creation(spec)
+            else:
+                if spec["type"] == P.NORMAL_TASK:
+                    fn = self._load_function(spec["fn"])
+                elif spec["method"] == "__ray_terminate__":
+                    raise _ActorExit()
+                elif spec["method"] == "__ray_ready__":
+                    fn = _ready
+                else:
+                    fn = getattr(self.actor_instance, spec["method"])
+                args, kwargs = self._decode_args(spec["args"], spec["owner"])
+                self._apply_runtime_env(spec)
+                if spec["nret"] == -1:
+                    returns = self._run_generator(spec, fn, args, kwargs, conn, reply_to)
+                    extra["num_items"] = self._last_gen_count
+                else:
+                    result = fn(*args, **kwargs)
+                    if spec.get("dynamic"):
+                        result = _DynamicRefs([self.put_object(v) for v in result])
+                    returns = self._package_returns(spec, result)
+        except _ActorExit:
+            returns = self._package_returns(spec, None) if spec["nret"] != -1 else []
+            self._send_reply(conn, reply_to, tid, returns, extra)
+            self._exit_actor()
+            return
+        except KeyboardInterrupt:
+            returns = self._error_returns(spec, TaskCancelledError(tid.hex()))
+        except BaseException as e:  # noqa: BLE001
+            err = RayTaskError.from_exception(e, name, pid=os.getpid(),
+                                              actor_repr=repr(self.actor_instance)
+                                              if self.actor_instance is not None else None)
+            if spec["type"] == P.ACTOR_CREATION_TASK:
+                returns = [("__init_error__", ser.serialize_error(err).to_bytes())]
+            else:
+                returns = self._error_returns(spec, err)
+                extra["app_error"] = True
+                extra["exc_type"] = type(e).__name__
+        finally:
+            with self.lock:
+                self.running.pop(tid, None)
+            self.current_task.tid = None
+            self.current_task.spec = None
+        self.task_events.append((tid, name, t0, time.time(), os.getpid(),
+                                 spec.get("actor_id"), "FAILED" if extra.get("app_error")
+                                 else "FINISHED"))
+        self._send_reply(conn, reply_to, tid, returns, extra)
+
+    def _apply_runtime_env(self, spec):
+        renv = spec.get("runtime_env")
+        if renv and renv.get("env_vars"):
+            os.environ.update({k: str(v) for k, v in renv["env_vars"].items()})
+
+    def _send_reply(self, conn, reply_to, tid, returns, extra):
+        msg = (P.TASK_REPLY, tid, returns, extra)
+        if reply_to is not None and self.send(reply_to, msg):
+            return
+        if conn is not None:
+            self.io.send(conn, _dumps(msg))
+
+    def _error_returns(self, spec, exc):
+        data = ser.serialize_error(exc).to_bytes()
+        n = spec["nret"] if spec["nret"] > 0 else 0
+        if spec["nret"] == -1:
+            return [(object_id_for_return(spec["tid"], 0x7FFFFFFF), P.RET_INLINE, data, None)]
+        return [(object_id_for_return(spec["tid"], i + 1), P.RET_INLINE, data, None)
+                for i in range(n)]
+
+    def _package_one(self, oid, value, owner):
+        sobj = ser.serialize(value, oid)
+        contained = None
+        if sobj.refs:
+            contained = []
+            for r in sobj.refs:
+                contained.append((r._id, r._owner))
+                self._pin_for(r, owner)
+        if sobj.total <= INLINE_MAX and not sobj.gpu:
+            return (oid, P.RET_INLINE, sobj.to_bytes(), contained)
+        self.store.put_serialized(oid, sobj, pinned=True)
+        return (oid, P.RET_STORE, sobj.total, contained)
+
+    def _pin_for(self, ref, owner_addr):
+        """Register `owner_addr` as a borrower of `ref` before handing it over."""
+        if ref._owner == self.addr:
+            with self.lock:
+                o = self.owned.get(ref._id)
+                if o is not None:
+                    if o.borrowers is None:
+                        o.borrowers = set()
+                    o.borrowers.add(owner_addr)
+        elif ref._owner != owner_addr:
+            try:
+                self.call(ref._owner, "add_borrower", ref._id, owner_addr, timeout=30)
+            except Exception:
+                pass
+
+    def _package_returns(self, spec, result):
+        n = spec["nret"]
+        tid = spec["tid"]
+        owner = spec["owner"]
+        if n == 0:
+            return []
+        if n == 1:
+            return [self._package_one(object_id_for_return(tid, 1), result, owner)]
+        if not isinstance(result, (tuple, list)) or len(result) != n:
+            raise ValueError(f"Task returned {result!r} but num_returns={n}")
+        return [self._package_one(object_id_for_return(tid, i + 1), v, owner)
+                for i, v in enumerate(result)]
+
+    def _run_generator(self, spec, fn, args, kwargs, conn, reply_to):
+        tid = spec["tid"]
+        owner = spec["owner"]
+        gen = fn(*args, **kwargs)
+        i = 0
+        if hasattr(gen, "__anext__"):
+            import asyncio
+
+            loop = asyncio.new_event_loop()
+            try:
+                while True:
+                    try:
+                        v = loop.run_until_complete(gen.__anext__())
+                    except StopAsyncIteration:
+                        break
+                    ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
+                    self.send(owner, (P.STREAM_ITEM, tid, i, ret))
+                    i += 1
+            finally:
+                loop.close()
+        else:
+            for v in gen:
+                ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
+                self.send(owner, (P.STREAM_ITEM, tid, i, ret))
+                i += 1
+        self._last_gen_count = i
+        return []
+
+    # ---- actor side
+    def _execute_actor_creation(self, spec):
+        cls = self._load_function(spec["fn"])
+        args, kwargs = self._decode_args(spec["args"], spec["owner"])
+        self._apply_runtime_env(spec)
+        self.actor_id = spec["actor_id"]
+        self.actor_spec = spec
+        self.current_task.actor_id = self.actor_id
+        meta = spec.get("method_meta") or {}
+        is_async = spec.get("is_async")
+        groups = spec.get("concurrency_groups") or {}
+        self.actor_method_groups = meta.get("__groups__", {})
+        instance = cls.__new__(cls)
+        self.actor_instance = instance
+        if is_async:
+            import asyncio
+
+            loop = asyncio.new_event_loop()
+            self.async_loop = loop
+            self._async_sem = asyncio.Semaphore(spec.get("max_concurrency") or 1000)
+            t = threading.Thread(target=loop.run_forever, name="ray_amd-asyncio", daemon=True)
+            t.start()
+            fut = asyncio.run_coroutine_threadsafe(self._async_init(instance, args, kwargs), loop)
+            fut.result()
+        else:
+            instance.__init__(*args, **kwargs)
+        mc = spec.get("max_concurrency") or 1
+        if not is_async and (mc > 1 or groups):
+            from concurrent.futures import ThreadPoolExecutor
+
+            self.actor_pools["_default"] = ThreadPoolExecutor(mc, "ray_amd-actor")
+            for g, n in groups.items():
+                self.actor_pools[g] = ThreadPoolExecutor(n, f"ray_amd-cg-{g}")
+        elif is_async:
+            self.actor_pools["_default"] = None
+        return []
+
+    async def _async_init(self, instance, args, kwargs):
+        instance.__init__(*args, **kwargs)
+
+    async def _run_async_actor_task(self, spec):
+        import asyncio
+        import inspect
+
+        tid = spec["tid"]
+        conn = spec.pop("_conn", None)
+        owner = spec["owner"]
+        async with self._async_sem:
+            self.current_task.tid = tid
+            try:
+                fn = getattr(self.actor_instance, spec["method"])
+                loop = asyncio.get_running_loop()
+                args, kwargs = await loop.run_in_executor(None, self._decode_args, spec["args"],
+                                                          owner)
+                if spec["nret"] == -1:
+                    returns = await loop.run_in_executor(None, self._run_generator_async_bridge,
+                                                         spec, fn, args, kwargs)
+                    extra = {"num_items": self._last_gen_count}
+                else:
+                    r = fn(*args, **kwargs)
+                    if inspect.isawaitable(r):
+                        r = await r
+                    returns = await loop.run_in_executor(None, self._package_returns, spec, r)
+                    extra = {}
+            except _ActorExit:
+                self._send_reply(conn, owner, tid, self._package_returns(spec, None), {})
+                self._exit_actor()
+                return
+            except BaseException as e:  # noqa: BLE001
+                err = RayTaskError.from_exception(e, spec.get("name", "task"), pid=os.getpid())
+                returns = self._error_returns(spec, err)
+                extra = {"app_error": True, "exc_type": type(e).__name__}
+        self._send_reply(conn, owner, tid, returns, extra)
+
+    def _run_generator_async_bridge(self, spec, fn, args, kwargs):
+        return self._run_generator(spec, fn, args, kwargs, None, spec["owner"])
+
+    def _exit_actor(self):
+        self.exiting = True
+        self.notify_raylet("actor_exit", self.actor_id)
+        time.sleep(0.05)
+        os._exit(0)
+
+    def _flush_task_events(self):
+        ev, self.task_events = self.task_events, []
+        self.notify_raylet("task_events", ev)
+
+    # ------------------------------------------------------------------ local mode
+    def _run_local(self, spec):
+        fn = self.fn_cache[spec["fn"]]
+        args, kwargs = self._decode_args(spec["args"], self.addr)
+        try:
+            r = fn(*args, **kwargs)
+            returns = self._package_returns(spec, r)
+        except BaseException as e:  # noqa: BLE001
+            returns = self._error_returns(spec, RayTaskError.from_exception(
+                e, spec.get("name", "task"), pid=os.getpid()))
+        self._complete(spec, returns, {})
+
+    # ------------------------------------------------------------------ shutdown
+    def shutdown(self):
+        if self._stopped:
+            return
+        self._stopped = True
+        try:
+            self._flush_task_events()
+        except Exception:
+            pass
+        try:
+            self.io.stop()
+        except Exception:
+            pass
+        try:
+            os.unlink(self.addr)
+        except OSError:
+            pass
+
+
+class _ArgRef:
+    __slots__ = ("i",)
+
+    def __init__(self, i):
+        self.i = i
+
+    def __reduce__(self):
+        return (_ArgRef, (self.i,))
+
+
+class _ActorExit(BaseException):
+    pass
+
+
+class _DynamicRefs(list):
+    """Value of a num_returns="dynamic" task: iterable of ObjectRefs."""
+
+
+def _ready():
+    return True

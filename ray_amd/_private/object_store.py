@@ -1,0 +1,152 @@
+"""Node-local object store client (reference: plasma client + external_storage.py spilling).
+
+Wraps the native ``_core.ShmStore``: every process on the node maps the same
+/dev/shm segment, so put/get are in-process operations (no store IPC).
+When the heap is full: evict unpinned secondary copies (LRU), then spill pinned
+primary copies to ``<session>/spill/<oid>`` (write + rename, THEN drop from the
+store, so a concurrent reader that misses the store always finds the file).
+Spilled objects are read back through mmap — still zero-copy.
+"""
+
+from __future__ import annotations
+
+import mmap
+import os
+import threading
+
+from ray_amd._native import _core
+from ray_amd.exceptions import ObjectStoreFullError
+
+from . import serialization as ser
+
+NO_SPACE = (1 << 64) - 1
+
+
+class _MmapBuf:
+    """Keeps a spill-file mapping alive while views of it exist."""
+
+    __slots__ = ("mm", "mv")
+
+    def __init__(self, path):
+        with open(path, "rb") as f:
+            self.mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+        self.mv = memoryview(self.mm)
+
+
+class ObjectStore:
+    def __init__(self, path: str, spill_dir: str, create: bool = False, size: int = 0,
+                 table_cap: int = 1 << 18):
+        self.path = path
+        self.spill_dir = spill_dir
+        self.store = _core.ShmStore(path, size, create, table_cap)
+        os.makedirs(spill_dir, exist_ok=True)
+        self._lock = threading.Lock()
+        self.spilled_bytes = 0
+        self.restored_bytes = 0
+
+    # ------------------------------------------------------------------ write
+    def _alloc(self, oid: bytes, size: int, pinned: bool, device: int = -1) -> int:
+        off = self.store.create(oid, size, 0, device, pinned)
+        if off != NO_SPACE:
+            return off
+        # 1) evict unpinned LRU copies
+        self.store.evict(size * 2, device)
+        off = self.store.create(oid, size, 0, device, pinned)
+        if off != NO_SPACE:
+            return off
+        if device >= 0:
+            raise ObjectStoreFullError(f"HBM object store on GPU {device} is full "
+                                       f"({self.store.used(device)} / "
+                                       f"{self.store.capacity(device)} bytes)")
+        # 2) spill pinned primary copies
+        for _ in range(8):
+            cands = self.store.spill_candidates(max(size * 2, 64 << 20), device)
+            if not cands:
+                break
+            for c in cands:
+                self.spill(c)
+            off = self.store.create(oid, size, 0, device, pinned)
+            if off != NO_SPACE:
+                return off
+        raise ObjectStoreFullError(
+            f"object of {size} bytes does not fit in the object store "
+            f"({self.store.used(-1)} / {self.store.capacity(-1)} bytes in use, nothing spillable)")
+
+    def put_serialized(self, oid: bytes, sobj: "ser.SerializedObject", pinned: bool = True):
+        off = self._alloc(oid, sobj.total, pinned)
+        mv = self.store.buffer(off, sobj.total)
+        try:
+            sobj.write_to(mv)
+        finally:
+            mv.release()
+        self.store.seal(oid)
+
+    def put_bytes(self, oid: bytes, data, pinned: bool = True):
+        n = len(data)
+        off = self._alloc(oid, n, pinned)
+        self.store.write(off, data)
+        self.store.seal(oid)
+
+    # ------------------------------------------------------------------ read
+    def get_buffer(self, oid: bytes):
+        """Pinned read-only memoryview of a sealed object, or None."""
+        b = self.store.get_buffer(oid, True)
+        if b is not None:
+            return memoryview(b)
+        p = self._spill_path(oid)
+        if os.path.exists(p):
+            try:
+                m = _MmapBuf(p)
+            except (FileNotFoundError, ValueError):
+                return None
+            self.restored_bytes += len(m.mv)
+            return m.mv
+        return None
+
+    def contains(self, oid: bytes) -> bool:
+        return self.store.contains(oid) or os.path.exists(self._spill_path(oid))
+
+    def delete(self, oid: bytes):
+        self.store.remove(oid)
+        p = self._spill_path(oid)
+        if self.spilled_bytes or os.path.exists(p):
+            try:
+                os.unlink(p)
+            except FileNotFoundError:
+                pass
+
+    # ------------------------------------------------------------------ spill
+    def _spill_path(self, oid: bytes) -> str:
+        return os.path.join(self.spill_dir, oid.hex())
+
+    def spill(self, oid: bytes) -> bool:
+        b = self.store.get_buffer(oid, True)
+        if b is None:
+            return False
+        try:
+            mv = memoryview(b)
+            p = self._spill_path(oid)
+            tmp = p + f".tmp{os.getpid()}"
+            with open(tmp, "wb") as f:
+                f.write(mv)
+            os.replace(tmp, p)
+            self.spilled_bytes += len(mv)
+            mv.release()
+        finally:
+            b.release()
+        self.store.remove(oid)
+        return True
+
+    def stats(self):
+        return {
+            "used": self.store.used(-1),
+            "capacity": self.store.capacity(-1),
+            "num_objects": self.store.num_objects(),
+            "evictions": self.store.evictions(),
+            "spilled_bytes": self.spilled_bytes,
+            "restored_bytes": self.restored_bytes,
+        }
+
+
+def deserialize_buffer(mv, ctx=None):
+    return ser.deserialize(mv, ctx)

@@ -1,0 +1,1088 @@
+"""Raylet + GCS process for a ray_amd node (reference: src/ray/raylet/node_manager.cc,
+worker_pool.cc, local_task_manager.cc; src/ray/gcs/gcs_server/{gcs_actor_manager,
+gcs_placement_group_manager,gcs_kv_manager,gcs_job_manager}.cc).
+
+One single-threaded event loop over the native IOLoop. Scheduling decisions
+(resource fit, GPU instance assignment, hybrid/spread/affinity policies,
+placement-group bundle placement) are delegated to the native
+``_core.Scheduler``; this module owns the worker pool, leases, the actor
+lifecycle (create → ALIVE → RESTARTING → DEAD), named actors, placement groups,
+the internal KV, jobs and task events.
+"""
+
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+import traceback
+
+from ray_amd._native import _core
+
+from . import protocol as P
+from . import serialization as ser
+
+_dumps = P.dumps
+
+
+class WorkerRec:
+    __slots__ = ("wid", "pid", "addr", "conn", "key", "state", "lease", "proc", "token",
+                 "actor_id", "job", "gpu_ids", "mode", "idle_since", "namespace", "started")
+
+    def __init__(self):
+        self.wid = None
+        self.pid = None
+        self.addr = None
+        self.conn = None
+        self.key = None
+        self.state = "starting"
+        self.lease = None
+        self.proc = None
+        self.token = None
+        self.actor_id = None
+        self.job = None
+        self.gpu_ids = ()
+        self.mode = "worker"
+        self.idle_since = time.monotonic()
+        self.namespace = None
+        self.started = time.monotonic()
+
+
+class Lease:
+    __slots__ = ("lid", "worker", "alloc", "resources", "owner", "strategy", "cpu_released",
+                 "pg", "actor_id")
+
+    def __init__(self, lid, worker, alloc, resources, owner, strategy):
+        self.lid = lid
+        self.worker = worker
+        self.alloc = alloc
+        self.resources = resources
+        self.owner = owner
+        self.strategy = strategy
+        self.cpu_released = False
+        self.pg = None
+        self.actor_id = None
+
+
+class LeaseReq:
+    __slots__ = ("rid", "conn", "req", "alloc", "node", "waiting_token", "cb", "t0", "warned",
+                 "resources")
+
+    def __init__(self, rid, conn, req, cb=None):
+        self.rid = rid
+        self.conn = conn
+        self.req = req
+        self.alloc = None
+        self.node = None
+        self.waiting_token = None
+        self.cb = cb
+        self.t0 = time.monotonic()
+        self.warned = False
+        self.resources = None
+
+
+class ActorRec:
+    def __init__(self, info, spec):
+        self.info = info
+        self.spec = spec
+        self.aid = info["actor_id"]
+        self.state = P.PENDING_CREATION
+        self.worker = None
+        self.lease = None
+        self.death = None
+        self.restarts = 0
+        self.max_restarts = info.get("max_restarts") or 0
+        self.no_restart = False
+        self.subscribers = set()
+        self.pid = None
+        self.start_time = time.time()
+        self.end_time = None
+
+
+class PGRec:
+    def __init__(self, pg_id, bundles, strategy, name, lifetime, owner, namespace):
+        self.pg_id = pg_id
+        self.bundles = bundles
+        self.strategy = strategy
+        self.name = name
+        self.lifetime = lifetime
+        self.owner = owner
+        self.namespace = namespace
+        self.state = "PENDING"
+        self.nodes = []
+        self.waiters = []
+        self.created_at = time.time()
+
+
+_PG_STRATEGY = {"PACK": 0, "SPREAD": 1, "STRICT_PACK": 2, "STRICT_SPREAD": 3}
+
+
+def detect_gpus() -> int:
+    """Count AMD GPUs without initialising HIP (reads KFD topology)."""
+    env = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") \
+        or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if env is not None and env.strip() != "":
+        return len([x for x in env.split(",") if x.strip() != ""])
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in os.listdir(base):
+            try:
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = f.read()
+                for line in props.splitlines():
+                    if line.startswith("simd_count") and int(line.split()[1]) > 0:
+                        n += 1
+                        break
+            except OSError:
+                continue
+    except OSError:
+        return 0
+    return n
+
+
+class Raylet:
+    def __init__(self, args):
+        self.session_dir = args.session_dir
+        os.makedirs(os.path.join(self.session_dir, "sockets"), exist_ok=True)
+        os.makedirs(os.path.join(self.session_dir, "logs"), exist_ok=True)
+        self.addr = os.path.join(self.session_dir, "sockets", "raylet.sock")
+        self.node_id = _core.random_id(16)
+        self.node_ip = "127.0.0.1"
+        self.store_path = args.store_path
+        self.spill_dir = os.path.join(self.session_dir, "spill")
+        os.makedirs(self.spill_dir, exist_ok=True)
+        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True, 1 << 18)
+        self.io = _core.IOLoop()
+        self.io.listen_unix(self.addr)
+        self.sched = _core.Scheduler()
+        res = json.loads(args.resources or "{}")
+        ncpu = args.num_cpus if args.num_cpus is not None else (os.cpu_count() or 1)
+        ngpu = args.num_gpus if args.num_gpus is not None else detect_gpus()
+        total = {"CPU": float(ncpu), "memory": float(args.memory or 8 << 30),
+                 "object_store_memory": float(args.object_store_memory),
+                 f"node:{self.node_ip}": 1.0}
+        if ngpu:
+            total["GPU"] = float(ngpu)
+        if args.head:
+            total["node:__internal_head__"] = 1.0
+        total.update({k: float(v) for k, v in res.items()})
+        self.labels = json.loads(args.labels or "{}")
+        self.labels.setdefault("ray.io/node_id", self.node_id.hex())
+        self.sched.add_node(self.node_id.hex(), total, self.labels)
+        self.total = total
+        self.num_cpus = ncpu
+        self.conn_addr = {}
+        self.addr_conn = {}
+        self.conn_worker = {}
+        self.workers = {}  # wid -> WorkerRec
+        self.starting = {}  # token -> WorkerRec
+        self.idle = collections.defaultdict(list)
+        self.leases = {}
+        self.pending = collections.deque()
+        self.kv = {}
+        self.actors = {}
+        self.named = {}
+        self.pgs = {}
+        self.pg_names = {}
+        self.jobs = {}
+        self.job_counter = 0
+        self.task_events = collections.deque(maxlen=100000)
+        self.next_token = 1
+        self.next_lease = 1
+        self.dirty = True
+        self.stop = False
+        self.max_starting = max(4, ncpu)
+        self.python = sys.executable
+        self.internal_cb = {}
+        self.next_internal = -1
+        self.start_time = time.time()
+        self.gpu_arenas = {}
+
+    # ------------------------------------------------------------------ io helpers
+    def send(self, conn, msg):
+        self.io.send(conn, _dumps(msg))
+
+    def reply(self, conn, rid, ok, value):
+        if rid and conn is not None:
+            self.send(conn, (P.RESP, rid, ok, value))
+
+    def run(self):
+        handlers = {P.REQ: self.on_req, P.HELLO: self.on_hello, P.TASK_REPLY: self.on_task_reply,
+                    P.RESP: self.on_resp}
+        last_tick = 0.0
+        while not self.stop:
+            ev = self.io.poll(20, 4096)
+            for typ, conn, payload in ev:
+                try:
+                    if typ == 0:
+                        msg = P.loads(payload)
+                        h = handlers.get(msg[0])
+                        if h:
+                            h(conn, msg)
+                    elif typ == 2:
+                        self.on_closed(conn)
+                except Exception:
+                    traceback.print_exc()
+            now = time.monotonic()
+            if self.dirty or now - last_tick > 0.1:
+                self.dirty = False
+                try:
+                    self.try_schedule()
+                    if now - last_tick > 0.1:
+                        last_tick = now
+                        self.tick()
+                except Exception:
+                    traceback.print_exc()
+        self.shutdown()
+
+    def on_hello(self, conn, msg):
+        self.conn_addr[conn] = msg[1]
+        self.addr_conn[msg[1]] = conn
+
+    def on_resp(self, conn, msg):
+        pass
+
+    def on_req(self, conn, msg):
+        _, rid, method, args = msg
+        h = getattr(self, "rpc_" + method, None)
+        if h is None:
+            self.reply(conn, rid, False, f"unknown raylet method {method}")
+            return
+        try:
+            h(conn, rid, *args)
+        except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            self.reply(conn, rid, False, e if _picklable(e) else RuntimeError(repr(e)))
+
+    # ------------------------------------------------------------------ registration
+    def rpc_register(self, conn, rid, mode, wid, pid, addr, job_id, namespace, token):
+        w = None
+        if mode == "worker":
+            w = self.starting.pop(token, None)
+        if w is None:
+            w = WorkerRec()
+        w.wid, w.pid, w.addr, w.conn, w.mode = wid, pid, addr, conn, mode
+        self.conn_worker[conn] = w
+        self.workers[wid] = w
+        if mode == "driver":
+            self.job_counter += 1
+            job_id = self.job_counter
+            w.state = "driver"
+            w.job = job_id
+            w.namespace = namespace or f"anon-{job_id}"
+            self.jobs[job_id] = {"job_id": job_id, "driver_pid": pid, "driver_addr": addr,
+                                 "start_time": time.time(), "end_time": None,
+                                 "status": "RUNNING", "namespace": w.namespace,
+                                 "sys_path": None}
+        else:
+            w.state = "idle"
+            w.idle_since = time.monotonic()
+            if w.key is not None:
+                self.idle[w.key].append(w)
+            self.dirty = True
+        info = {"node_id": self.node_id, "job_id": w.job if mode == "driver" else job_id,
+                "namespace": w.namespace if mode == "driver" else namespace,
+                "store_path": self.store_path, "spill_dir": self.spill_dir,
+                "node_ip": self.node_ip, "session_dir": self.session_dir,
+                "resources": self.total}
+        self.reply(conn, rid, True, info)
+
+    def rpc_set_job_info(self, conn, rid, job_id, sys_path, runtime_env):
+        j = self.jobs.get(job_id)
+        if j is not None:
+            j["sys_path"] = sys_path
+            j["runtime_env"] = runtime_env
+        self.reply(conn, rid, True, None)
+
+    # ------------------------------------------------------------------ worker pool
+    def _pool_key(self, job, renv, gpu_ids):
+        return (job, json.dumps(renv, sort_keys=True, default=str) if renv else None,
+                tuple(gpu_ids) if gpu_ids else ())
+
+    def _start_worker(self, key, renv, job):
+        w = WorkerRec()
+        w.token = self.next_token
+        self.next_token += 1
+        w.key = key
+        w.job = job
+        w.gpu_ids = key[2]
+        env = dict(os.environ)
+        env["RAY_AMD_NODE_ID"] = self.node_id.hex()
+        j = self.jobs.get(job) or {}
+        if j.get("sys_path"):
+            env["RAY_AMD_JOB_SYS_PATH"] = json.dumps(j["sys_path"])
+        pp = env.get("PYTHONPATH", "")
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + (os.pathsep + pp if pp else "")
+        if w.gpu_ids:
+            vis = os.environ.get("HIP_VISIBLE_DEVICES")
+            ids = [str(i) for i in w.gpu_ids]
+            if vis:
+                base = [x for x in vis.split(",") if x.strip() != ""]
+                ids = [base[i] for i in w.gpu_ids if i < len(base)]
+            env["HIP_VISIBLE_DEVICES"] = ",".join(ids)
+            env["RAY_AMD_GPU_IDS"] = ",".join(str(i) for i in w.gpu_ids)
+        allr = {}
+        for src in (j.get("runtime_env") or {}, renv or {}):
+            allr.update(src)
+        for k, v in (allr.get("env_vars") or {}).items():
+            env[k] = str(v)
+        cwd = None
+        if allr.get("working_dir"):
+            cwd = allr["working_dir"]
+            env["PYTHONPATH"] = cwd + os.pathsep + env["PYTHONPATH"]
+        if allr.get("py_modules"):
+            env["PYTHONPATH"] = os.pathsep.join(map(str, allr["py_modules"])) + os.pathsep + \
+                env["PYTHONPATH"]
+        cmd = [self.python, "-u", "-m", "ray_amd._private.worker_main", "--session-dir",
+               self.session_dir, "--raylet", self.addr, "--token", str(w.token), "--job",
+               str(job), "--node-id", self.node_id.hex()]
+        w.proc = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
+        w.pid = w.proc.pid
+        self.starting[w.token] = w
+        return w
+
+    def _take_idle(self, key):
+        lst = self.idle.get(key)
+        while lst:
+            w = lst.pop()
+            if w.state == "idle" and w.conn is not None:
+                return w
+        return None
+
+    def _n_starting_for(self, key):
+        return sum(1 for w in self.starting.values() if w.key == key)
+
+    # ------------------------------------------------------------------ leases
+    def rpc_request_lease(self, conn, rid, req):
+        self.pending.append(LeaseReq(rid, conn, req))
+        self.dirty = True
+
+    def _resolve_resources(self, req):
+        res = {k: float(v) for k, v in (req.get("resources") or {}).items() if v}
+        st = req.get("strategy")
+        if isinstance(st, dict) and st.get("type") == "pg":
+            pg = st["pg_id"]
+            idx = st.get("bundle_index", -1)
+            out = {}
+            for k, v in res.items():
+                out[f"{k}_group_{pg}"] = v
+                if idx is not None and idx >= 0:
+                    out[f"{k}_group_{idx}_{pg}"] = v
+            if idx is not None and idx >= 0:
+                out[f"bundle_group_{idx}_{pg}"] = 0.001
+            else:
+                out[f"bundle_group_{pg}"] = 0.001
+            return out
+        return res
+
+    def try_schedule(self):
+        if not self.pending:
+            return
+        keep = collections.deque()
+        starting_budget = self.max_starting - len(self.starting)
+        while self.pending:
+            lr = self.pending.popleft()
+            if lr.conn is not None and lr.conn not in self.conn_worker and lr.cb is None:
+                # requester gone
+                if lr.alloc is not None:
+                    self.sched.release(lr.alloc, lr.resources)
+                continue
+            if lr.alloc is None:
+                res = self._resolve_resources(lr.req)
+                lr.resources = res
+                st = lr.req.get("strategy")
+                strategy, target, soft = 0, "", False
+                hard_l, soft_l = {}, {}
+                if st == "SPREAD":
+                    strategy = 1
+                elif isinstance(st, dict):
+                    if st.get("type") == "node_affinity":
+                        strategy = 3 if st.get("soft") else 2
+                        target = st["node_id"]
+                    elif st.get("type") == "node_label":
+                        hard_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
+                                  for k, v in (st.get("hard") or {}).items()}
+                        soft_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
+                                  for k, v in (st.get("soft") or {}).items()}
+                node = self.sched.pick_node(res, strategy, target, self.node_id.hex(), hard_l,
+                                            soft_l)
+                if node == "!":
+                    if isinstance(st, dict) and st.get("type") == "pg" and \
+                            st["pg_id"] not in self.pgs:
+                        self._fail_lease(lr, "placement group was removed")
+                        continue
+                    if not lr.warned:
+                        lr.warned = True
+                        print(f"[ray_amd] warning: task/actor {lr.req.get('name')} requires "
+                              f"{res} which no node can satisfy; it stays pending.",
+                              file=sys.stderr, flush=True)
+                    keep.append(lr)
+                    continue
+                if node == "":
+                    keep.append(lr)
+                    continue
+                alloc = self.sched.allocate(node, res)
+                if alloc is None:
+                    keep.append(lr)
+                    continue
+                lr.alloc = alloc
+                lr.node = node
+            gpu_ids = self._gpu_ids(lr.alloc)
+            key = self._pool_key(lr.req.get("job"), lr.req.get("runtime_env"), gpu_ids)
+            w = self._take_idle(key)
+            if w is None:
+                if lr.waiting_token is None or lr.waiting_token not in self.starting:
+                    if starting_budget > 0 or self._n_starting_for(key) == 0:
+                        nw = self._start_worker(key, lr.req.get("runtime_env"),
+                                                lr.req.get("job"))
+                        lr.waiting_token = nw.token
+                        starting_budget -= 1
+                keep.append(lr)
+                continue
+            self._grant(lr, w, gpu_ids)
+        self.pending = keep
+
+    def _gpu_ids(self, alloc):
+        inst = alloc.instances
+        if not inst:
+            return []
+        best = None
+        for name, lst in inst.items():
+            if best is None or len(name) > len(best):
+                best = name
+        return sorted(i for i, _ in inst[best])
+
+    def _grant(self, lr, w, gpu_ids):
+        lid = self.next_lease
+        self.next_lease += 1
+        lease = Lease(lid, w, lr.alloc, lr.resources, lr.req.get("owner"), lr.req.get("strategy"))
+        st = lr.req.get("strategy")
+        if isinstance(st, dict) and st.get("type") == "pg":
+            lease.pg = st["pg_id"]
+        self.leases[lid] = lease
+        w.state = "leased"
+        w.lease = lease
+        grant = {"addr": w.addr, "lease_id": lid, "gpu_ids": gpu_ids, "worker_id": w.wid,
+                 "pid": w.pid}
+        if lr.cb is not None:
+            lr.cb(grant)
+        else:
+            self.reply(lr.conn, lr.rid, True, grant)
+
+    def _fail_lease(self, lr, msg):
+        from ray_amd.exceptions import TaskUnschedulableError
+
+        err = TaskUnschedulableError(msg)
+        if lr.cb is not None:
+            lr.cb(None, err)
+        else:
+            self.reply(lr.conn, lr.rid, False, err)
+
+    def rpc_return_lease(self, conn, rid, lid, worker_dead):
+        self._return_lease(lid, kill=worker_dead)
+        self.reply(conn, rid, True, None)
+
+    def _return_lease(self, lid, kill=False):
+        lease = self.leases.pop(lid, None)
+        if lease is None:
+            return
+        res = dict(lease.resources)
+        if lease.cpu_released:
+            res.pop("CPU", None)
+        self.sched.release(lease.alloc, res)
+        w = lease.worker
+        w.lease = None
+        if kill or w.actor_id is not None:
+            self._kill_worker(w)
+        elif w.conn is not None:
+            w.state = "idle"
+            w.idle_since = time.monotonic()
+            self.idle[w.key].append(w)
+        self.dirty = True
+
+    def rpc_notify_blocked(self, conn, rid, wid):
+        w = self.workers.get(wid)
+        if w is None or w.lease is None or w.lease.cpu_released:
+            return
+        cpu = w.lease.resources.get("CPU")
+        if cpu:
+            # give the CPU back while the task waits in ray.get (avoids nested-task deadlock)
+            self.sched.release(self._node_alloc(), {"CPU": cpu})
+            w.lease.cpu_released = True
+            self.dirty = True
+
+    def rpc_notify_unblocked(self, conn, rid, wid):
+        w = self.workers.get(wid)
+        if w is None or w.lease is None or not w.lease.cpu_released:
+            return
+        cpu = w.lease.resources.get("CPU")
+        if cpu and self.sched.allocate(self.node_id.hex(), {"CPU": cpu}) is not None:
+            w.lease.cpu_released = False
+
+    def _node_alloc(self):
+        a = self.sched.allocate(self.node_id.hex(), {})
+        return a
+
+    # ------------------------------------------------------------------ worker death
+    def on_closed(self, conn):
+        addr = self.conn_addr.pop(conn, None)
+        if addr:
+            self.addr_conn.pop(addr, None)
+        w = self.conn_worker.pop(conn, None)
+        if w is None:
+            return
+        w.conn = None
+        self.workers.pop(w.wid, None)
+        if w.mode == "driver":
+            self._on_driver_exit(w)
+            return
+        prev_state = w.state
+        w.state = "dead"
+        if w.lease is not None:
+            lease = w.lease
+            self.leases.pop(lease.lid, None)
+            res = dict(lease.resources)
+            if lease.cpu_released:
+                res.pop("CPU", None)
+            self.sched.release(lease.alloc, res)
+            w.lease = None
+        if w.proc is not None:
+            try:
+                w.proc.wait(timeout=0.5)
+            except Exception:
+                pass
+        if w.actor_id is not None:
+            self._on_actor_worker_died(w.actor_id, prev_state)
+        self.dirty = True
+
+    def _kill_worker(self, w, graceful=False):
+        w.state = "dead"
+        if w.conn is not None:
+            try:
+                self.send(w.conn, (P.PUSH, "exit", None))
+            except Exception:
+                pass
+        if w.proc is not None:
+            try:
+                if not graceful:
+                    w.proc.kill()
+            except Exception:
+                pass
+        elif w.pid:
+            try:
+                os.kill(w.pid, signal.SIGKILL)
+            except OSError:
+                pass
+
+    def _on_driver_exit(self, w):
+        j = self.jobs.get(w.job)
+        if j:
+            j["status"] = "SUCCEEDED"
+            j["end_time"] = time.time()
+        # leases held by the driver: kill those workers (they may run its tasks)
+        for lid, lease in list(self.leases.items()):
+            if lease.owner == w.addr:
+                self._return_lease(lid, kill=True)
+        for aid, a in list(self.actors.items()):
+            if a.info.get("owner") == w.addr and a.info.get("lifetime") != "detached":
+                self._kill_actor(a, no_restart=True, reason="owner (driver) exited")
+        for pg in list(self.pgs.values()):
+            if pg.owner == w.addr and pg.lifetime != "detached":
+                self._remove_pg(pg)
+        # idle workers of this job are useless now
+        for key, lst in list(self.idle.items()):
+            if key[0] == w.job:
+                for iw in lst:
+                    self._kill_worker(iw)
+                lst.clear()
+
+    # ------------------------------------------------------------------ periodic
+    def tick(self):
+        now = time.monotonic()
+        # reap idle workers beyond the soft limit
+        n_idle = sum(len(v) for v in self.idle.values())
+        if n_idle > self.num_cpus:
+            for key, lst in self.idle.items():
+                for w in list(lst):
+                    if n_idle <= self.num_cpus:
+                        break
+                    if now - w.idle_since > 2.0:
+                        lst.remove(w)
+                        self._kill_worker(w, graceful=True)
+                        n_idle -= 1
+        # workers that failed to start
+        for tok, w in list(self.starting.items()):
+            if w.proc is not None and w.proc.poll() is not None:
+                self.starting.pop(tok, None)
+                print(f"[ray_amd] worker process {w.pid} exited during startup "
+                      f"(code {w.proc.returncode})", file=sys.stderr, flush=True)
+                self.dirty = True
+
+    # ------------------------------------------------------------------ kv
+    def rpc_kv_put(self, conn, rid, ns, key, value, overwrite=True):
+        k = (ns, key)
+        existed = k in self.kv
+        if overwrite or not existed:
+            self.kv[k] = value
+        self.reply(conn, rid, True, not existed)
+
+    def rpc_kv_get(self, conn, rid, ns, key):
+        self.reply(conn, rid, True, self.kv.get((ns, key)))
+
+    def rpc_kv_del(self, conn, rid, ns, key, prefix=False):
+        if prefix:
+            ks = [k for k in self.kv if k[0] == ns and _startswith(k[1], key)]
+            for k in ks:
+                del self.kv[k]
+            self.reply(conn, rid, True, len(ks))
+        else:
+            self.reply(conn, rid, True, 1 if self.kv.pop((ns, key), None) is not None else 0)
+
+    def rpc_kv_keys(self, conn, rid, ns, prefix):
+        self.reply(conn, rid, True, [k[1] for k in self.kv if k[0] == ns and
+                                     _startswith(k[1], prefix)])
+
+    def rpc_kv_exists(self, conn, rid, ns, key):
+        self.reply(conn, rid, True, (ns, key) in self.kv)
+
+    # ------------------------------------------------------------------ actors
+    def rpc_create_actor(self, conn, rid, info, spec):
+        name = info.get("name")
+        ns = info.get("namespace")
+        if name:
+            existing = self.named.get((ns, name))
+            if existing is not None and self.actors[existing].state != P.DEAD:
+                if info.get("get_if_exists"):
+                    a = self.actors[existing]
+                    self.reply(conn, rid, True, {"existing": existing,
+                                                 "method_meta": a.spec.get("method_meta"),
+                                                 "class_name": a.info.get("class_name"),
+                                                 "owner": a.info.get("owner")})
+                    return
+                self.reply(conn, rid, False, ValueError(
+                    f"The name {name} (namespace={ns}) is already taken. Please use a "
+                    f"different name or get the existing actor using ray.get_actor('{name}')"))
+                return
+        a = ActorRec(info, spec)
+        self.actors[a.aid] = a
+        if name:
+            self.named[(ns, name)] = a.aid
+        self._schedule_actor(a)
+        self.reply(conn, rid, True, None)
+
+    def _schedule_actor(self, a):
+        req = {"resources": a.spec.get("resources") or {}, "strategy": a.spec.get("strategy"),
+               "runtime_env": a.spec.get("runtime_env"), "owner": self.addr,
+               "job": a.spec.get("job"), "name": a.info.get("class_name")}
+
+        def granted(grant, err=None, a=a):
+            if grant is None:
+                self._actor_dead(a, str(err))
+                return
+            if a.state == P.DEAD:
+                self._return_lease(grant["lease_id"], kill=False)
+                return
+            lease = self.leases[grant["lease_id"]]
+            lease.actor_id = a.aid
+            w = lease.worker
+            w.actor_id = a.aid
+            w.state = "actor"
+            a.worker = w
+            a.lease = lease
+            a.pid = w.pid
+            spec = dict(a.spec)
+            spec["lease_id"] = grant["lease_id"]
+            self.send(w.conn, (P.TASK, spec))
+
+        self.pending.append(LeaseReq(0, None, req, cb=granted))
+        self.dirty = True
+
+    def on_task_reply(self, conn, msg):
+        _, tid, returns, extra = msg
+        w = self.conn_worker.get(conn)
+        if w is None or w.actor_id is None:
+            return
+        a = self.actors.get(w.actor_id)
+        if a is None:
+            return
+        if returns and returns[0][0] == "__init_error__":
+            a.no_restart = True
+            self._actor_dead(a, ("err", returns[0][1]))
+            self._kill_worker(w)
+            return
+        a.state = P.ALIVE
+        self._publish(a)
+
+    def _publish(self, a):
+        death = a.death
+        if isinstance(death, tuple) and death and death[0] == "err":
+            try:
+                _, exc = ser.deserialize(death[1])
+                death = exc
+            except Exception:
+                death = "actor creation failed"
+        msg = (P.PUSH, "actor", (a.aid, a.state, a.worker.addr if a.worker and
+                                 a.state == P.ALIVE else None, death, a.restarts))
+        for c in list(a.subscribers):
+            if c in self.conn_worker:
+                self.send(c, msg)
+            else:
+                a.subscribers.discard(c)
+
+    def rpc_subscribe_actor(self, conn, rid, aid):
+        a = self.actors.get(aid)
+        if a is None:
+            self.reply(conn, rid, True, (aid, P.DEAD, None, "actor not found", 0))
+            return
+        a.subscribers.add(conn)
+        death = a.death
+        if isinstance(death, tuple):
+            try:
+                _, death = ser.deserialize(death[1])
+            except Exception:
+                death = "actor creation failed"
+        self.reply(conn, rid, True, (aid, a.state, a.worker.addr if a.worker and
+                                     a.state == P.ALIVE else None, death, a.restarts))
+
+    def _on_actor_worker_died(self, aid, prev_state):
+        a = self.actors.get(aid)
+        if a is None or a.state == P.DEAD:
+            return
+        a.worker = None
+        a.lease = None
+        can_restart = not a.no_restart and (a.max_restarts == -1 or a.restarts < a.max_restarts)
+        if can_restart:
+            a.restarts += 1
+            a.state = P.RESTARTING
+            self._publish(a)
+            self._schedule_actor(a)
+        else:
+            self._actor_dead(a, "The actor died unexpectedly (worker process exited)."
+                             if not a.no_restart else "The actor was killed (ray.kill).")
+
+    def _actor_dead(self, a, death):
+        a.state = P.DEAD
+        a.death = death
+        a.end_time = time.time()
+        self._publish(a)
+
+    def _kill_actor(self, a, no_restart=True, reason="ray.kill"):
+        a.no_restart = a.no_restart or no_restart
+        if a.worker is not None:
+            w = a.worker
+            if a.lease is not None:
+                self.leases.pop(a.lease.lid, None)
+                res = dict(a.lease.resources)
+                self.sched.release(a.lease.alloc, res)
+                w.lease = None
+                a.lease = None
+            self._kill_worker(w)
+            if no_restart:
+                self._actor_dead(a, f"The actor was killed ({reason}).")
+                a.worker = None
+        elif no_restart:
+            self._actor_dead(a, f"The actor was killed ({reason}).")
+        self.dirty = True
+
+    def rpc_kill_actor(self, conn, rid, aid, no_restart):
+        a = self.actors.get(aid)
+        if a is not None:
+            self._kill_actor(a, no_restart)
+        self.reply(conn, rid, True, a is not None)
+
+    def rpc_actor_out_of_scope(self, conn, rid, aid):
+        a = self.actors.get(aid)
+        if a is not None and a.info.get("lifetime") != "detached" and not a.info.get("name"):
+            self._kill_actor(a, True, "all handles out of scope")
+
+    def rpc_actor_exit(self, conn, rid, aid):
+        a = self.actors.get(aid)
+        if a is not None:
+            a.no_restart = True
+            self._actor_dead(a, "The actor exited via exit_actor().")
+
+    def rpc_get_named_actor(self, conn, rid, name, namespace):
+        aid = self.named.get((namespace, name))
+        if aid is None or self.actors[aid].state == P.DEAD:
+            self.reply(conn, rid, True, None)
+            return
+        a = self.actors[aid]
+        self.reply(conn, rid, True, {"actor_id": aid, "method_meta": a.spec.get("method_meta"),
+                                     "class_name": a.info.get("class_name"),
+                                     "owner": a.info.get("owner")})
+
+    def rpc_list_named_actors(self, conn, rid, all_namespaces, namespace):
+        out = []
+        for (ns, name), aid in self.named.items():
+            if self.actors[aid].state == P.DEAD:
+                continue
+            if all_namespaces:
+                out.append({"name": name, "namespace": ns})
+            elif ns == namespace:
+                out.append(name)
+        self.reply(conn, rid, True, out)
+
+    def rpc_list_actors(self, conn, rid):
+        out = []
+        for aid, a in self.actors.items():
+            out.append({"actor_id": aid.hex(), "class_name": a.info.get("class_name"),
+                        "state": a.state, "name": a.info.get("name") or "",
+                        "namespace": a.info.get("namespace"), "pid": a.pid,
+                        "num_restarts": a.restarts, "job_id": a.spec.get("job"),
+                        "node_id": self.node_id.hex(),
+                        "death_cause": a.death if isinstance(a.death, str) else
+                        ("creation task error" if a.death else None),
+                        "lifetime": a.info.get("lifetime") or "non_detached",
+                        "required_resources": a.spec.get("resources"),
+                        "start_time": a.start_time, "end_time": a.end_time})
+        self.reply(conn, rid, True, out)
+
+    # ------------------------------------------------------------------ placement groups
+    def rpc_create_pg(self, conn, rid, pg_id, bundles, strategy, name, lifetime, owner,
+                      namespace):
+        if name and (namespace, name) in self.pg_names:
+            self.reply(conn, rid, False, ValueError(f"placement group name {name} exists"))
+            return
+        pg = PGRec(pg_id, bundles, strategy, name, lifetime, owner, namespace)
+        self.pgs[pg_id] = pg
+        if name:
+            self.pg_names[(namespace, name)] = pg_id
+        self._try_place(pg)
+        self.reply(conn, rid, True, None)
+
+    def _try_place(self, pg):
+        if pg.state != "PENDING":
+            return
+        nodes, infeasible = self.sched.place_bundles(
+            [{k: float(v) for k, v in b.items()} for b in pg.bundles],
+            _PG_STRATEGY.get(pg.strategy, 0))
+        if not nodes:
+            if infeasible:
+                pg.state = "PENDING"  # stays pending (reference behaviour), flagged infeasible
+                pg.infeasible = True
+            return
+        if self.sched.commit_bundles(pg.pg_id, [{k: float(v) for k, v in b.items()}
+                                                for b in pg.bundles], nodes):
+            pg.nodes = nodes
+            pg.state = "CREATED"
+            for conn, rid in pg.waiters:
+                self.reply(conn, rid, True, True)
+            pg.waiters.clear()
+            self.dirty = True
+
+    def rpc_wait_pg(self, conn, rid, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is None:
+            self.reply(conn, rid, False, ValueError("placement group does not exist"))
+            return
+        if pg.state == "CREATED":
+            self.reply(conn, rid, True, True)
+        elif pg.state == "REMOVED":
+            self.reply(conn, rid, False, ValueError("placement group was removed"))
+        else:
+            pg.waiters.append((conn, rid))
+
+    def rpc_remove_pg(self, conn, rid, pg_id):
+        pg = self.pgs.get(pg_id)
+        if pg is not None:
+            self._remove_pg(pg)
+        self.reply(conn, rid, True, None)
+
+    def _remove_pg(self, pg):
+        if pg.state == "REMOVED":
+            return
+        # kill workers leased inside the pg
+        for lid, lease in list(self.leases.items()):
+            if lease.pg == pg.pg_id:
+                if lease.actor_id is not None and lease.actor_id in self.actors:
+                    self._kill_actor(self.actors[lease.actor_id], True, "placement group removed")
+                else:
+                    self._return_lease(lid, kill=True)
+        if pg.state == "CREATED":
+            self.sched.remove_bundles(pg.pg_id, [{k: float(v) for k, v in b.items()}
+                                                 for b in pg.bundles], pg.nodes)
+        pg.state = "REMOVED"
+        pg.removed_at = time.time()
+        for conn, rid in pg.waiters:
+            self.reply(conn, rid, False, ValueError("placement group was removed"))
+        pg.waiters.clear()
+        if pg.name:
+            self.pg_names.pop((pg.namespace, pg.name), None)
+        self.dirty = True
+
+    def rpc_pg_table(self, conn, rid, pg_id):
+        def rec(pg):
+            return {"placement_group_id": pg.pg_id, "name": pg.name or "",
+                    "bundles": {i: b for i, b in enumerate(pg.bundles)},
+                    "bundles_to_node_id": {i: n for i, n in enumerate(pg.nodes)},
+                    "strategy": pg.strategy, "state": pg.state,
+                    "stats": {"scheduling_state": "FINISHED" if pg.state == "CREATED"
+                              else "PENDING"}}
+        if pg_id is not None:
+            pg = self.pgs.get(pg_id)
+            self.reply(conn, rid, True, rec(pg) if pg else None)
+        else:
+            self.reply(conn, rid, True, {k: rec(v) for k, v in self.pgs.items()})
+
+    def rpc_get_named_pg(self, conn, rid, name, namespace):
+        pid = self.pg_names.get((namespace, name))
+        if pid is None:
+            self.reply(conn, rid, True, None)
+            return
+        pg = self.pgs[pid]
+        self.reply(conn, rid, True, {"pg_id": pid, "bundles": pg.bundles,
+                                     "strategy": pg.strategy})
+
+    # ------------------------------------------------------------------ cluster info
+    def rpc_cluster_resources(self, conn, rid):
+        tot = self.sched.cluster_total()
+        self.reply(conn, rid, True, {k: v for k, v in tot.items() if "_group_" not in k})
+
+    def rpc_available_resources(self, conn, rid):
+        av = self.sched.cluster_available()
+        self.reply(conn, rid, True, {k: v for k, v in av.items()
+                                     if "_group_" not in k and v > 0})
+
+    def rpc_nodes(self, conn, rid):
+        self.reply(conn, rid, True, [{
+            "NodeID": self.node_id.hex(), "Alive": True, "NodeManagerAddress": self.node_ip,
+            "NodeManagerHostname": os.uname().nodename, "Resources": self.sched.total(
+                self.node_id.hex()), "alive": True, "RayletSocketName": self.addr,
+            "ObjectStoreSocketName": self.store_path, "Labels": self.labels,
+            "node_id": self.node_id.hex()}])
+
+    def rpc_list_workers(self, conn, rid):
+        out = []
+        for w in self.workers.values():
+            out.append({"worker_id": w.wid.hex(), "pid": w.pid, "worker_type": w.mode,
+                        "state": w.state, "job_id": w.job, "actor_id": w.actor_id.hex()
+                        if w.actor_id else None, "gpu_ids": list(w.gpu_ids)})
+        self.reply(conn, rid, True, out)
+
+    def rpc_list_jobs(self, conn, rid):
+        self.reply(conn, rid, True, list(self.jobs.values()))
+
+    def rpc_task_events(self, conn, rid, events):
+        self.task_events.extend(events)
+
+    def rpc_get_task_events(self, conn, rid):
+        self.reply(conn, rid, True, list(self.task_events))
+
+    def rpc_store_stats(self, conn, rid):
+        self.reply(conn, rid, True, {"used": self.store.used(-1),
+                                     "capacity": self.store.capacity(-1),
+                                     "num_objects": self.store.num_objects()})
+
+    def rpc_list_objects(self, conn, rid):
+        out = []
+        for o in self.store.list():
+            out.append({"object_id": o["id"].hex(), "object_size": o["data_size"],
+                        "pinned": o["pinned"], "ref_count": o["ref_count"],
+                        "device": o["device"], "node_id": self.node_id.hex()})
+        self.reply(conn, rid, True, out)
+
+    def rpc_ping(self, conn, rid):
+        self.reply(conn, rid, True, "pong")
+
+    # ------------------------------------------------------------------ GPU arenas
+    def rpc_gpu_arena(self, conn, rid, device, size):
+        """HBM object store arena for `device` (allocated by a holder process so the raylet
+        itself never initialises HIP)."""
+        a = self.gpu_arenas.get(device)
+        if a is None:
+            a = self._start_arena_holder(device, size)
+        self.reply(conn, rid, True, a)
+
+    def _start_arena_holder(self, device, size):
+        import tempfile
+
+        out = os.path.join(self.session_dir, f"arena_{device}.json")
+        env = dict(os.environ)
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
+        proc = subprocess.Popen([self.python, "-m", "ray_amd._private.gpu_object_store",
+                                 "--device", str(device), "--size", str(size), "--out", out,
+                                 "--store", self.store_path], env=env, close_fds=True)
+        t0 = time.time()
+        while not os.path.exists(out):
+            if proc.poll() is not None or time.time() - t0 > 120:
+                raise RuntimeError(f"GPU arena holder for device {device} failed")
+            time.sleep(0.05)
+        with open(out) as f:
+            info = json.load(f)
+        info["pid"] = proc.pid
+        self.gpu_arenas[device] = info
+        self._arena_procs = getattr(self, "_arena_procs", []) + [proc]
+        tempfile  # noqa: B018
+        return info
+
+    # ------------------------------------------------------------------ shutdown
+    def rpc_shutdown(self, conn, rid):
+        self.reply(conn, rid, True, None)
+        self.stop = True
+
+    def shutdown(self):
+        for w in list(self.workers.values()) + list(self.starting.values()):
+            if w.mode != "driver":
+                self._kill_worker(w)
+        for lst in self.idle.values():
+            for w in lst:
+                self._kill_worker(w)
+        for p in getattr(self, "_arena_procs", []):
+            try:
+                p.kill()
+            except Exception:
+                pass
+        try:
+            os.unlink(self.store_path)
+        except OSError:
+            pass
+        self.io.stop()
+
+
+def _startswith(k, prefix):
+    if isinstance(k, bytes) and isinstance(prefix, str):
+        prefix = prefix.encode()
+    if isinstance(k, str) and isinstance(prefix, bytes):
+        prefix = prefix.decode()
+    return k.startswith(prefix)
+
+
+def _picklable(e):
+    try:
+        P.dumps(e)
+        return True
+    except Exception:
+        return False
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--session-dir", required=True)
+    ap.add_argument("--store-path", required=True)
+    ap.add_argument("--object-store-memory", type=int, default=2 << 30)
+    ap.add_argument("--num-cpus", type=int, default=None)
+    ap.add_argument("--num-gpus", type=int, default=None)
+    ap.add_argument("--memory", type=int, default=None)
+    ap.add_argument("--resources", default="{}")
+    ap.add_argument("--labels", default="{}")
+    ap.add_argument("--head", action="store_true")
+    args = ap.parse_args()
+    signal.signal(signal.SIGTERM, lambda *_: setattr(r, "stop", True))
+    r = Raylet(args)
+    ready = os.path.join(args.session_dir, "raylet.ready")
+    with open(ready + ".tmp", "w") as f:
+        json.dump({"addr": r.addr, "node_id": r.node_id.hex(), "pid": os.getpid()}, f)
+    os.replace(ready + ".tmp", ready)
+    r.run()
+
+
+if __name__ == "__main__":
+    main()

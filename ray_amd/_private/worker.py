@@ -1,0 +1,356 @@
+"""Global worker state and the core public API (reference: python/ray/_private/worker.py).
+
+``init`` starts (or attaches to) a node: it launches the raylet process, which
+creates the shared-memory object store and the worker pool, then connects this
+process as the job's driver.
+"""
+
+from __future__ import annotations
+
+import atexit
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+from ray_amd.exceptions import GetTimeoutError, RaySystemError
+
+SCRIPT_MODE = 0
+WORKER_MODE = 1
+LOCAL_MODE = 2
+
+ROOT_TMP = os.environ.get("RAY_AMD_TMPDIR", os.path.join(tempfile.gettempdir(), "ray_amd"))
+CURRENT_CLUSTER_FILE = os.path.join(ROOT_TMP, "ray_current_cluster")
+
+
+class Worker:
+    def __init__(self):
+        self.core = None
+        self.mode = None
+        self.raylet_proc = None
+        self.session_dir = None
+        self.node_started_here = False
+        self.lock = threading.RLock()
+        self.namespace = None
+        self.runtime_env = None
+        self._local_mode = False
+
+    @property
+    def connected(self):
+        return self.core is not None
+
+    def connect_worker(self, cw):
+        self.core = cw
+        self.mode = WORKER_MODE
+        self.session_dir = cw.session_dir
+
+
+global_worker = Worker()
+_global_node_lock = threading.Lock()
+
+
+def is_initialized() -> bool:
+    return global_worker.connected
+
+
+def _default_object_store_memory():
+    try:
+        st = os.statvfs("/dev/shm")
+        shm_free = st.f_bavail * st.f_frsize
+    except OSError:
+        shm_free = 4 << 30
+    total = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    return int(max(256 << 20, min(0.3 * total, 0.8 * shm_free, 200 << 30)))
+
+
+def _start_raylet(session_dir, num_cpus, num_gpus, resources, object_store_memory, labels,
+                  head=True):
+    os.makedirs(session_dir, exist_ok=True)
+    store_path = "/dev/shm/ray_amd_" + os.path.basename(session_dir)
+    cmd = [sys.executable, "-m", "ray_amd._private.raylet", "--session-dir", session_dir,
+           "--store-path", store_path, "--object-store-memory", str(object_store_memory),
+           "--resources", json.dumps(resources or {}), "--labels", json.dumps(labels or {})]
+    if num_cpus is not None:
+        cmd += ["--num-cpus", str(int(num_cpus))]
+    if num_gpus is not None:
+        cmd += ["--num-gpus", str(int(num_gpus))]
+    if head:
+        cmd.append("--head")
+    env = dict(os.environ)
+    pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
+                                    else "")
+    proc = subprocess.Popen(cmd, env=env, close_fds=True, start_new_session=True)
+    ready = os.path.join(session_dir, "raylet.ready")
+    t0 = time.time()
+    while not os.path.exists(ready):
+        if proc.poll() is not None:
+            raise RaySystemError(RuntimeError(f"raylet exited with code {proc.returncode}"))
+        if time.time() - t0 > 120:
+            proc.kill()
+            raise RaySystemError(RuntimeError("timed out waiting for the raylet"))
+        time.sleep(0.01)
+    with open(ready) as f:
+        info = json.load(f)
+    return proc, info["addr"]
+
+
+def new_session_dir():
+    os.makedirs(ROOT_TMP, exist_ok=True)
+    ts = time.strftime("%Y-%m-%d_%H-%M-%S")
+    return os.path.join(ROOT_TMP, f"session_{ts}_{os.getpid()}_{os.urandom(3).hex()}")
+
+
+def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=None,
+         labels=None, object_store_memory=None, local_mode=False, ignore_reinit_error=False,
+         include_dashboard=None, dashboard_host=None, dashboard_port=None, job_config=None,
+         configure_logging=True, logging_level=None, logging_format=None, log_to_driver=True,
+         namespace=None, runtime_env=None, _temp_dir=None, _system_config=None,
+         storage=None, **kwargs):
+    """Start or connect to a ray_amd node (parity: ray.init)."""
+    from .core_worker import CoreWorker
+    from .ids import random_bytes
+
+    with _global_node_lock:
+        if global_worker.connected:
+            if ignore_reinit_error:
+                return RayContext(global_worker)
+            raise RuntimeError("Maybe you called ray_amd.init twice by accident? Use "
+                               "ignore_reinit_error=True to ignore this.")
+        if address is None:
+            address = os.environ.get("RAY_ADDRESS") or os.environ.get("RAY_AMD_ADDRESS")
+        if address in (None, "local", ""):
+            session = new_session_dir() if _temp_dir is None else os.path.join(
+                _temp_dir, os.path.basename(new_session_dir()))
+            osm = int(object_store_memory or _default_object_store_memory())
+            proc, raylet_addr = _start_raylet(session, num_cpus, num_gpus, resources, osm,
+                                              labels)
+            global_worker.raylet_proc = proc
+            global_worker.node_started_here = True
+        else:
+            if address == "auto":
+                if not os.path.exists(CURRENT_CLUSTER_FILE):
+                    raise ConnectionError("Could not find any running ray_amd instance. "
+                                          "Start one with `python -m ray_amd.scripts start "
+                                          "--head`.")
+                with open(CURRENT_CLUSTER_FILE) as f:
+                    session = f.read().strip()
+            else:
+                session = address
+            raylet_addr = os.path.join(session, "sockets", "raylet.sock")
+            global_worker.node_started_here = False
+        cw = CoreWorker(mode="driver", session_dir=session, raylet_addr=raylet_addr,
+                        worker_id=random_bytes(16), namespace=namespace)
+        cw.local_mode = bool(local_mode)
+        global_worker.core = cw
+        global_worker.mode = LOCAL_MODE if local_mode else SCRIPT_MODE
+        global_worker.session_dir = session
+        global_worker.namespace = cw.namespace
+        global_worker.runtime_env = runtime_env
+        sp = [os.path.abspath(p) if p else os.getcwd() for p in sys.path]
+        main = sys.modules.get("__main__")
+        if main is not None and getattr(main, "__file__", None):
+            sp.insert(0, os.path.dirname(os.path.abspath(main.__file__)))
+        sp.insert(0, os.getcwd())
+        cw.call_raylet("set_job_info", cw.job_id, sp, runtime_env)
+        atexit.register(shutdown)
+        return RayContext(global_worker)
+
+
+class RayContext(dict):
+    def __init__(self, w):
+        super().__init__(address=w.session_dir, session_dir=w.session_dir,
+                         node_id=w.core.node_id.hex() if w.core else None,
+                         namespace=w.namespace)
+        self.address_info = dict(self)
+        self.dashboard_url = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        shutdown()
+
+    def disconnect(self):
+        shutdown()
+
+
+def shutdown(_exiting_interpreter=False):
+    w = global_worker
+    with _global_node_lock:
+        cw = w.core
+        if cw is None:
+            return
+        try:
+            if w.node_started_here:
+                try:
+                    cw.call_raylet("shutdown", timeout=5)
+                except Exception:
+                    pass
+        finally:
+            cw.shutdown()
+            w.core = None
+            if w.raylet_proc is not None:
+                try:
+                    w.raylet_proc.wait(timeout=10)
+                except Exception:
+                    w.raylet_proc.kill()
+                w.raylet_proc = None
+        _reset_module_state()
+
+
+def _reset_module_state():
+    try:
+        from ray_amd import actor as _actor
+
+        _actor._reset()
+    except Exception:
+        pass
+
+
+def _check_connected():
+    if not global_worker.connected:
+        # auto-init (reference: auto_init_hook)
+        init()
+    return global_worker.core
+
+
+def put(value, *, _owner=None):
+    from ray_amd.object_ref import ObjectRef
+
+    cw = _check_connected()
+    if isinstance(value, ObjectRef):
+        raise TypeError("Calling 'put' on an ObjectRef is not allowed.")
+    return cw.put_object(value)
+
+
+def get(object_refs, *, timeout=None):
+    from ray_amd.object_ref import ObjectRef, ObjectRefGenerator
+
+    cw = _check_connected()
+    if isinstance(object_refs, ObjectRefGenerator):
+        object_refs = list(object_refs)
+    single = isinstance(object_refs, ObjectRef)
+    if single:
+        refs = [object_refs]
+    elif isinstance(object_refs, (list, tuple)):
+        refs = list(object_refs)
+        for r in refs:
+            if not isinstance(r, ObjectRef):
+                raise TypeError(f"ray_amd.get() expects ObjectRef or list of ObjectRefs, got "
+                                f"{type(r)}")
+    else:
+        raise ValueError(f"Invalid type of object refs, {type(object_refs)}, is given. "
+                         "'object_refs' must either be an ObjectRef or a list of ObjectRefs.")
+    if timeout is not None and timeout < 0:
+        raise ValueError("timeout must be >= 0")
+    vals = cw.get_objects(refs, timeout)
+    return vals[0] if single else vals
+
+
+def wait(object_refs, *, num_returns=1, timeout=None, fetch_local=True):
+    from ray_amd.object_ref import ObjectRef
+
+    cw = _check_connected()
+    if isinstance(object_refs, ObjectRef):
+        raise TypeError("wait() expected a list of ray_amd.ObjectRef, got a single ObjectRef")
+    refs = list(object_refs)
+    if len(set(r._id for r in refs)) != len(refs):
+        raise ValueError("Wait requires a list of unique object refs.")
+    if num_returns <= 0 or num_returns > len(refs):
+        raise ValueError("Invalid number of objects to return %d." % num_returns)
+    ready = cw.wait_refs([r._id for r in refs], num_returns, timeout)
+    r_list, nr = [], []
+    for r in refs:
+        if r._id in ready and len(r_list) < num_returns:
+            r_list.append(r)
+        else:
+            nr.append(r)
+    return r_list, nr
+
+
+def kill(actor, *, no_restart=True):
+    from ray_amd.actor import ActorHandle
+
+    if not isinstance(actor, ActorHandle):
+        raise ValueError(f"ray_amd.kill() only supported for actors. Got: {type(actor)}.")
+    cw = _check_connected()
+    cw.kill_actor(actor._actor_id, no_restart)
+
+
+def cancel(object_ref, *, force=False, recursive=True):
+    from ray_amd.object_ref import ObjectRef
+
+    cw = _check_connected()
+    if not isinstance(object_ref, ObjectRef):
+        raise TypeError("ray_amd.cancel() only supported for ObjectRefs")
+    cw.cancel(object_ref, force, recursive)
+
+
+def get_actor(name: str, namespace: str | None = None):
+    from ray_amd.actor import ActorHandle
+
+    cw = _check_connected()
+    ns = namespace or cw.namespace
+    info = cw.call_raylet("get_named_actor", name, ns)
+    if info is None:
+        raise ValueError(f"Failed to look up actor with name '{name}'. This could because 1. "
+                         "You are trying to look up a named actor you didn't create. 2. The "
+                         "named actor died. 3. You did not use a namespace matching the "
+                         "namespace of the actor.")
+    return ActorHandle._from_info(info["actor_id"], info["class_name"], info["method_meta"],
+                                  info["owner"])
+
+
+def cluster_resources():
+    return _check_connected().call_raylet("cluster_resources")
+
+
+def available_resources():
+    return _check_connected().call_raylet("available_resources")
+
+
+def nodes():
+    return _check_connected().call_raylet("nodes")
+
+
+def get_gpu_ids():
+    cw = _check_connected()
+    return list(cw.gpu_ids)
+
+
+def timeline(filename=None):
+    """Chrome-trace of task execution (reference: ray.timeline)."""
+    cw = _check_connected()
+    cw._flush_task_events()
+    time.sleep(0.05)
+    events = cw.call_raylet("get_task_events")
+    trace = []
+    for tid, name, t0, t1, pid, actor_id, status in events:
+        trace.append({"cat": "task", "name": name, "ph": "X", "pid": pid, "tid": pid,
+                      "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6,
+                      "args": {"task_id": tid.hex(), "status": status,
+                               "actor_id": actor_id.hex() if actor_id else None}})
+    if filename:
+        with open(filename, "w") as f:
+            json.dump(trace, f)
+        return None
+    return trace
+
+
+def method(*args, **kwargs):
+    """@ray.method decorator: per-method options (num_returns, concurrency_group...)."""
+
+    def deco(m):
+        m.__ray_amd_method_options__ = kwargs
+        return m
+
+    if len(args) == 1 and callable(args[0]) and not kwargs:
+        return deco(args[0])
+    return deco
+
+
+GetTimeoutError  # noqa: B018

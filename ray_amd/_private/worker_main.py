@@ -1,0 +1,41 @@
+"""Worker process entry point (reference: python/ray/_private/workers/default_worker.py)."""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--session-dir", required=True)
+    ap.add_argument("--raylet", required=True)
+    ap.add_argument("--token", type=int, required=True)
+    ap.add_argument("--job", default=None)
+    ap.add_argument("--node-id", default=None)
+    args = ap.parse_args()
+    extra = os.environ.get("RAY_AMD_JOB_SYS_PATH")
+    if extra:
+        for p in reversed(json.loads(extra)):
+            if p and p not in sys.path:
+                sys.path.insert(1, p)
+    from ray_amd._private import worker as W
+    from ray_amd._private.core_worker import CoreWorker
+    from ray_amd._private.ids import random_bytes
+
+    job = int(args.job) if args.job not in (None, "None") else None
+    gpu_ids = [int(x) for x in os.environ.get("RAY_AMD_GPU_IDS", "").split(",") if x != ""]
+    cw = CoreWorker(mode="worker", session_dir=args.session_dir, raylet_addr=args.raylet,
+                    worker_id=random_bytes(16), job_id=job, gpu_ids=gpu_ids,
+                    startup_token=args.token)
+    W.global_worker.connect_worker(cw)
+    try:
+        cw.run_task_loop()
+    finally:
+        os._exit(0)
+
+
+if __name__ == "__main__":
+    main()

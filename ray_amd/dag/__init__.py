@@ -1,0 +1,195 @@
+"""Lazy task/actor DAGs (reference: python/ray/dag/{dag_node,function_node,class_node,
+input_node,output_node}.py).
+
+``f.bind(x)`` builds a node; ``node.execute(*inputs)`` submits the graph with
+each node's upstream results passed as ObjectRefs (so data never returns to the
+driver between stages)."""
+
+from __future__ import annotations
+
+import uuid
+
+
+class DAGNode:
+    def __init__(self, args, kwargs, options):
+        self._bound_args = tuple(args)
+        self._bound_kwargs = dict(kwargs)
+        self._bound_options = dict(options or {})
+        self._stable_uuid = uuid.uuid4().hex
+
+    def get_args(self):
+        return self._bound_args
+
+    def get_kwargs(self):
+        return self._bound_kwargs
+
+    def get_options(self):
+        return self._bound_options
+
+    def _children(self):
+        out = []
+        for a in list(self._bound_args) + list(self._bound_kwargs.values()):
+            if isinstance(a, DAGNode):
+                out.append(a)
+            elif isinstance(a, (list, tuple)):
+                out.extend(x for x in a if isinstance(x, DAGNode))
+            elif isinstance(a, dict):
+                out.extend(x for x in a.values() if isinstance(x, DAGNode))
+        return out
+
+    def _resolve(self, v, cache, inputs):
+        if isinstance(v, DAGNode):
+            return v._exec(cache, inputs)
+        if isinstance(v, list):
+            return [self._resolve(x, cache, inputs) for x in v]
+        if isinstance(v, tuple):
+            return tuple(self._resolve(x, cache, inputs) for x in v)
+        if isinstance(v, dict):
+            return {k: self._resolve(x, cache, inputs) for k, x in v.items()}
+        return v
+
+    def _exec(self, cache, inputs):
+        key = self._stable_uuid
+        if key not in cache:
+            args = [self._resolve(a, cache, inputs) for a in self._bound_args]
+            kwargs = {k: self._resolve(v, cache, inputs) for k, v in self._bound_kwargs.items()}
+            cache[key] = self._execute_impl(args, kwargs, cache, inputs)
+        return cache[key]
+
+    def execute(self, *args, **kwargs):
+        return self._exec({}, (args, kwargs))
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        raise NotImplementedError
+
+    def experimental_compile(self, **kw):
+        return CompiledDAG(self)
+
+
+class InputNode(DAGNode):
+    def __init__(self, *a, **k):
+        super().__init__((), {}, {})
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+    def __getitem__(self, key):
+        return InputAttributeNode(self, key)
+
+    def __getattr__(self, key):
+        if key.startswith("_"):
+            raise AttributeError(key)
+        return InputAttributeNode(self, key, attr=True)
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        a, k = inputs
+        if len(a) == 1 and not k:
+            return a[0]
+        if not a and k:
+            return k
+        return a
+
+
+class InputAttributeNode(DAGNode):
+    def __init__(self, parent, key, attr=False):
+        super().__init__((), {}, {})
+        self._parent = parent
+        self._key = key
+        self._attr = attr
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        a, k = inputs
+        if isinstance(self._key, int):
+            return a[self._key]
+        if self._key in k:
+            return k[self._key]
+        v = self._parent._exec(cache, inputs)
+        return getattr(v, self._key) if self._attr else v[self._key]
+
+
+class FunctionNode(DAGNode):
+    def __init__(self, fn, args, kwargs, options):
+        super().__init__(args, kwargs, options)
+        self._fn = fn
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        return self._fn._remote(args, kwargs, self._bound_options)
+
+
+class ClassNode(DAGNode):
+    def __init__(self, cls, args, kwargs, options):
+        super().__init__(args, kwargs, options)
+        self._cls = cls
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        return self._cls._remote(args, kwargs, self._bound_options)
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return _UnboundClassMethod(self, name)
+
+
+class _UnboundClassMethod:
+    def __init__(self, cls_node, name):
+        self._cls_node = cls_node
+        self._name = name
+
+    def bind(self, *args, **kwargs):
+        return ClassMethodNode(self._cls_node, self._name, args, kwargs, {})
+
+    def options(self, **opts):
+        parent = self
+
+        class _O:
+            def bind(self, *a, **k):
+                return ClassMethodNode(parent._cls_node, parent._name, a, k, opts)
+
+        return _O()
+
+
+class ClassMethodNode(DAGNode):
+    def __init__(self, actor_or_node, method, args, kwargs, options):
+        super().__init__(args, kwargs, options)
+        self._actor = actor_or_node
+        self._method = method
+
+    def _children(self):
+        c = super()._children()
+        if isinstance(self._actor, DAGNode):
+            c.append(self._actor)
+        return c
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        handle = self._actor._exec(cache, inputs) if isinstance(self._actor, DAGNode) \
+            else self._actor
+        return getattr(handle, self._method).options(**self._bound_options).remote(*args,
+                                                                                  **kwargs)
+
+
+class MultiOutputNode(DAGNode):
+    def __init__(self, outputs):
+        super().__init__((list(outputs),), {}, {})
+
+    def _execute_impl(self, args, kwargs, cache, inputs):
+        return list(args[0])
+
+
+class CompiledDAG:
+    """Reference `experimental_compile`: here a cached re-executable graph handle."""
+
+    def __init__(self, root):
+        self.root = root
+
+    def execute(self, *args, **kwargs):
+        return self.root.execute(*args, **kwargs)
+
+    def teardown(self):
+        pass
+
+
+__all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode",
+           "MultiOutputNode", "InputAttributeNode"]

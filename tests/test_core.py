@@ -1,0 +1,503 @@
+"""Core API tests (modelled on python/ray/tests/test_basic*.py, test_actor*.py,
+test_placement_group*.py, test_reference_counting.py, test_cancel.py,
+test_streaming_generator.py)."""
+
+import asyncio
+import os
+import time
+
+import numpy as np
+import pytest
+
+import ray_amd as ray
+from ray_amd.exceptions import (GetTimeoutError, RayActorError, RayTaskError,
+                                TaskCancelledError)
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4, num_gpus=2, resources={"custom": 2}, object_store_memory=512 << 20)
+    yield
+    ray.shutdown()
+
+
+@ray.remote
+def add(a, b):
+    return a + b
+
+
+@ray.remote
+def echo(x):
+    return x
+
+
+def test_simple_tasks(cluster):
+    assert ray.get(add.remote(1, 2)) == 3
+    refs = [add.remote(i, i) for i in range(50)]
+    assert ray.get(refs) == [2 * i for i in range(50)]
+
+
+def test_args_by_ref_and_chaining(cluster):
+    x = add.remote(1, 1)
+    y = add.remote(x, 10)
+    z = add.remote(y, b=x)
+    assert ray.get(z) == 14
+    r = ray.put(5)
+    assert ray.get(add.remote(r, r)) == 10
+
+
+def test_nested_refs_are_not_resolved(cluster):
+    r = ray.put(7)
+
+    @ray.remote
+    def f(lst):
+        assert isinstance(lst[0], ray.ObjectRef)
+        return ray.get(lst[0]) + 1
+
+    assert ray.get(f.remote([r])) == 8
+
+
+def test_multiple_returns(cluster):
+    @ray.remote(num_returns=3)
+    def three():
+        return 1, 2, 3
+
+    a, b, c = three.remote()
+    assert ray.get([a, b, c]) == [1, 2, 3]
+
+    @ray.remote(num_returns=0)
+    def none():
+        return None
+
+    assert none.remote() is None
+
+
+def test_large_objects_zero_copy(cluster):
+    a = np.arange(5_000_000, dtype=np.float64)
+    r = ray.put(a)
+    b = ray.get(r)
+    assert np.array_equal(a, b)
+    assert not b.flags.writeable  # view of the shared segment
+
+    @ray.remote
+    def s(x):
+        return float(x.sum())
+
+    assert ray.get(s.remote(r)) == float(a.sum())
+    assert ray.get(s.remote(a)) == float(a.sum())  # large arg auto-promoted to the store
+
+    @ray.remote
+    def make(n):
+        return np.ones(n, dtype=np.int32)
+
+    out = ray.get(make.remote(3_000_000))
+    assert out.sum() == 3_000_000
+
+
+def test_task_error(cluster):
+    @ray.remote
+    def boom():
+        raise ValueError("bad")
+
+    with pytest.raises(ValueError):
+        ray.get(boom.remote())
+    with pytest.raises(RayTaskError):
+        ray.get(boom.remote())
+
+
+def test_retry_exceptions(cluster, tmp_path):
+    p = str(tmp_path / "cnt")
+
+    @ray.remote(max_retries=3, retry_exceptions=True)
+    def flaky(path):
+        n = int(open(path).read()) if os.path.exists(path) else 0
+        open(path, "w").write(str(n + 1))
+        if n < 2:
+            raise RuntimeError("flaky")
+        return n
+
+    assert ray.get(flaky.remote(p)) == 2
+
+
+def test_worker_crash_retry(cluster, tmp_path):
+    p = str(tmp_path / "crash")
+
+    @ray.remote(max_retries=2)
+    def die_once(path):
+        if not os.path.exists(path):
+            open(path, "w").write("1")
+            os._exit(1)
+        return "ok"
+
+    assert ray.get(die_once.remote(p)) == "ok"
+
+    @ray.remote(max_retries=0)
+    def die():
+        os._exit(1)
+
+    with pytest.raises(ray.exceptions.WorkerCrashedError):
+        ray.get(die.remote())
+
+
+def test_get_timeout_and_wait(cluster):
+    @ray.remote
+    def slow(t):
+        time.sleep(t)
+        return t
+
+    r = slow.remote(2.0)
+    with pytest.raises(GetTimeoutError):
+        ray.get(r, timeout=0.2)
+    fast = [slow.remote(0.01) for _ in range(3)]
+    ready, not_ready = ray.wait(fast + [r], num_returns=3, timeout=5)
+    assert len(ready) == 3 and not_ready == [r]
+    ready, not_ready = ray.wait([r], timeout=0.01)
+    assert ready == []
+    assert ray.get(r) == 2.0
+
+
+def test_nested_tasks_no_deadlock(cluster):
+    @ray.remote
+    def fib(n):
+        if n < 2:
+            return n
+        return sum(ray.get([fib.remote(n - 1), fib.remote(n - 2)]))
+
+    assert ray.get(fib.remote(7)) == 13
+
+
+def test_resources(cluster):
+    @ray.remote(num_gpus=1)
+    def gpu_ids():
+        return ray.get_gpu_ids()
+
+    ids = ray.get([gpu_ids.remote() for _ in range(2)])
+    assert all(len(i) == 1 for i in ids)
+
+    @ray.remote(resources={"custom": 1})
+    def c():
+        return 1
+
+    assert ray.get(c.remote()) == 1
+    res = ray.cluster_resources()
+    assert res["CPU"] == 4 and res["GPU"] == 2 and res["custom"] == 2
+
+    @ray.remote(num_gpus=0.5)
+    def half():
+        return ray.get_gpu_ids()
+
+    assert all(len(x) == 1 for x in ray.get([half.remote() for _ in range(4)]))
+
+
+def test_infeasible_times_out(cluster):
+    @ray.remote(num_gpus=100)
+    def never():
+        return 1
+
+    with pytest.raises(GetTimeoutError):
+        ray.get(never.remote(), timeout=0.5)
+
+
+def test_actor_basic(cluster):
+    @ray.remote
+    class Counter:
+        def __init__(self, start=0):
+            self.n = start
+
+        def inc(self, k=1):
+            self.n += k
+            return self.n
+
+        def get(self):
+            return self.n
+
+    c = Counter.remote(10)
+    refs = [c.inc.remote() for _ in range(20)]
+    assert ray.get(refs) == list(range(11, 31))
+    assert ray.get(c.get.remote()) == 30
+
+    @ray.remote
+    def use(h):
+        return ray.get(h.inc.remote(100))
+
+    assert ray.get(use.remote(c)) == 130
+
+
+def test_actor_error_and_init_error(cluster):
+    @ray.remote
+    class A:
+        def f(self):
+            raise KeyError("x")
+
+    a = A.remote()
+    with pytest.raises(KeyError):
+        ray.get(a.f.remote())
+
+    @ray.remote
+    class Bad:
+        def __init__(self):
+            raise RuntimeError("init fails")
+
+        def f(self):
+            return 1
+
+    b = Bad.remote()
+    with pytest.raises(RayActorError):
+        ray.get(b.f.remote(), timeout=30)
+
+
+def test_named_and_detached_actor(cluster):
+    @ray.remote
+    class Store:
+        def __init__(self):
+            self.d = {}
+
+        def put(self, k, v):
+            self.d[k] = v
+
+        def get(self, k):
+            return self.d.get(k)
+
+    s = Store.options(name="kv", lifetime="detached").remote()
+    ray.get(s.put.remote("a", 1))
+    s2 = ray.get_actor("kv")
+    assert ray.get(s2.get.remote("a")) == 1
+    with pytest.raises(ValueError):
+        Store.options(name="kv").remote()
+    s3 = Store.options(name="kv", get_if_exists=True).remote()
+    assert ray.get(s3.get.remote("a")) == 1
+    ray.kill(s)
+    time.sleep(0.2)
+    with pytest.raises(ValueError):
+        ray.get_actor("kv")
+
+
+def test_actor_kill_and_restart(cluster):
+    @ray.remote(max_restarts=1)
+    class R:
+        def pid(self):
+            return os.getpid()
+
+        def die(self):
+            os._exit(1)
+
+    r = R.remote()
+    p1 = ray.get(r.pid.remote())
+    r.die.remote()
+    deadline = time.time() + 30
+    while True:
+        try:
+            p2 = ray.get(r.pid.remote(), timeout=10)
+            break
+        except RayActorError:
+            assert time.time() < deadline
+            time.sleep(0.1)
+    assert p2 != p1
+    ray.kill(r)
+    with pytest.raises(RayActorError):
+        ray.get(r.pid.remote(), timeout=30)
+
+
+def test_threaded_and_async_actors(cluster):
+    @ray.remote(max_concurrency=4)
+    class T:
+        def sleep(self, t):
+            time.sleep(t)
+            return t
+
+    t = T.remote()
+    ray.get(t.sleep.remote(0))
+    t0 = time.time()
+    ray.get([t.sleep.remote(0.5) for _ in range(4)])
+    assert time.time() - t0 < 1.5
+
+    @ray.remote
+    class AA:
+        async def work(self, t):
+            await asyncio.sleep(t)
+            return t
+
+    a = AA.remote()
+    ray.get(a.work.remote(0))
+    t0 = time.time()
+    assert ray.get([a.work.remote(0.5) for _ in range(10)]) == [0.5] * 10
+    assert time.time() - t0 < 2.0
+
+
+def test_exit_actor(cluster):
+    @ray.remote
+    class E:
+        def bye(self):
+            ray.actor.exit_actor()
+
+        def hi(self):
+            return "hi"
+
+    e = E.remote()
+    assert ray.get(e.hi.remote()) == "hi"
+    e.bye.remote()
+    with pytest.raises(RayActorError):
+        ray.get(e.hi.remote(), timeout=30)
+
+
+def test_placement_group(cluster):
+    from ray_amd.util.placement_group import (placement_group, placement_group_table,
+                                              remove_placement_group)
+    from ray_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+    pg = placement_group([{"CPU": 1, "GPU": 1}, {"CPU": 1, "GPU": 1}], strategy="PACK")
+    assert ray.get(pg.ready(), timeout=10)
+    assert placement_group_table(pg)["state"] == "CREATED"
+    assert ray.available_resources().get("GPU", 0) == 0
+
+    @ray.remote(num_gpus=1, num_cpus=1)
+    def where():
+        return ray.get_gpu_ids()
+
+    ids = ray.get([where.options(scheduling_strategy=PlacementGroupSchedulingStrategy(
+        pg, placement_group_bundle_index=i)).remote() for i in range(2)])
+    assert sorted(i[0] for i in ids) == [0, 1]
+    remove_placement_group(pg)
+    time.sleep(0.2)
+    assert ray.available_resources()["GPU"] == 2
+    big = placement_group([{"CPU": 100}])
+    assert not big.wait(timeout_seconds=0.5)
+    remove_placement_group(big)
+
+
+def test_cancel(cluster):
+    @ray.remote
+    def forever():
+        while True:
+            time.sleep(0.01)
+
+    r = forever.remote()
+    time.sleep(0.5)
+    ray.cancel(r)
+    with pytest.raises((TaskCancelledError, RayTaskError)):
+        ray.get(r, timeout=10)
+
+
+def test_streaming_generator(cluster):
+    @ray.remote
+    def gen(n):
+        for i in range(n):
+            yield i * i
+
+    out = [ray.get(r) for r in gen.remote(5)]
+    assert out == [0, 1, 4, 9, 16]
+
+    @ray.remote
+    class G:
+        def stream(self, n):
+            for i in range(n):
+                yield i
+
+    g = G.remote()
+    assert [ray.get(r) for r in g.stream.remote(4)] == [0, 1, 2, 3]
+
+
+def test_dynamic_returns(cluster):
+    @ray.remote(num_returns="dynamic")
+    def dyn(n):
+        for i in range(n):
+            yield i
+
+    refs = ray.get(dyn.remote(3))
+    assert [ray.get(r) for r in refs] == [0, 1, 2]
+
+
+def test_object_freed_when_out_of_scope(cluster):
+    from ray_amd._private import worker as W
+
+    store = W.global_worker.core.store.store
+    before = store.num_objects()
+    r = ray.put(np.zeros(1_000_000))
+    assert store.num_objects() == before + 1
+    del r
+    time.sleep(0.05)
+    assert store.num_objects() == before
+
+
+def test_borrowed_ref_outlives_owner_scope(cluster):
+    @ray.remote
+    class Holder:
+        def hold(self, lst):
+            self.r = lst[0]
+            return True
+
+        def read(self):
+            return ray.get(self.r).sum()
+
+    h = Holder.remote()
+    r = ray.put(np.ones(200_000))
+    ray.get(h.hold.remote([r]))
+    del r
+    time.sleep(0.2)
+    assert ray.get(h.read.remote()) == 200_000
+
+
+def test_runtime_context(cluster):
+    ctx = ray.get_runtime_context()
+    assert ctx.get_job_id()
+
+    @ray.remote
+    class A:
+        def ids(self):
+            c = ray.get_runtime_context()
+            return c.get_actor_id(), c.get_task_id()
+
+    a = A.remote()
+    aid, tid = ray.get(a.ids.remote())
+    assert aid == a._actor_id.hex() and tid
+
+
+def test_runtime_env_env_vars(cluster):
+    @ray.remote(runtime_env={"env_vars": {"FOO_RA": "bar"}})
+    def env():
+        return os.environ.get("FOO_RA")
+
+    assert ray.get(env.remote()) == "bar"
+
+
+def test_dag(cluster):
+    from ray_amd.dag import InputNode
+
+    with InputNode() as inp:
+        a = add.bind(inp, 1)
+        b = add.bind(a, a)
+    assert ray.get(b.execute(3)) == 8
+
+
+def test_actor_handle_in_object(cluster):
+    @ray.remote
+    class Acc:
+        def __init__(self):
+            self.v = 0
+
+        def add(self, x):
+            self.v += x
+            return self.v
+
+    acc = Acc.remote()
+    ref = ray.put({"h": acc})
+
+    @ray.remote
+    def use(d):
+        return ray.get(d["h"].add.remote(5))
+
+    assert ray.get(use.remote(ref)) == 5
+
+
+def test_timeline(cluster):
+    ray.get([echo.remote(i) for i in range(5)])
+    time.sleep(0.1)
+    tr = ray.timeline()
+    assert isinstance(tr, list)
+
+
+def test_await_ref(cluster):
+    async def main():
+        return await add.remote(2, 3)
+
+    assert asyncio.run(main()) == 5
