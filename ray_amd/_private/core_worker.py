@@ -146,6 +146,7 @@ class CoreWorker:
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.lock = threading.RLock()
+        self._ready_cv = threading.Condition(self.lock)
         self.raylet_addr = raylet_addr
         self.conns: dict[str, int] = {}
         self.conn_addr: dict[int, str] = {}
@@ -483,6 +484,7 @@ class CoreWorker:
             o.contained = contained
             o.size = size
             o.ready = True
+            self._ready_cv.notify_all()
             cbs = o.callbacks
             o.callbacks = None
             free = o.release_when_ready
@@ -638,32 +640,86 @@ class CoreWorker:
 
     def wait_refs(self, oids, num_returns, timeout):
         """Returns the list of ready oids (at least num_returns unless timeout)."""
-        w = _Waiter(num_returns)
-        pending = []
-        for oid in oids:
-            if self._on_ready(oid, w.hit):
-                w.done.add(oid)
+        # Owned objects are polled under the readiness condition variable (notified by
+        # _mark_ready); only borrowed objects need per-object owner callbacks.
+        done = set()
+        owned_pending = []
+        remote_pending = []
+        with self.lock:
+            for oid in oids:
+                o = self.owned.get(oid)
+                if o is not None:
+                    if o.ready:
+                        done.add(oid)
+                    else:
+                        owned_pending.append(oid)
+                else:
+                    remote_pending.append(oid)
+        if len(done) >= num_returns:
+            return done
+        cv = self._ready_cv
+
+        def remote_hit(oid):
+            with self.lock:
+                done.add(oid)
+                cv.notify_all()
+
+        registered = []
+        for oid in remote_pending:
+            if self._on_ready(oid, remote_hit):
+                done.add(oid)
             else:
-                pending.append(oid)
-        if len(w.done) >= num_returns:
-            return w.done
+                registered.append(oid)
+        if len(done) >= num_returns or (timeout is not None and timeout <= 0):
+            self._drop_waiter(registered, remote_hit)
+            return self._collect_ready(done, owned_pending, num_returns)
         deadline = None if timeout is None else time.monotonic() + timeout
         blocked = self._maybe_notify_blocked()
         try:
-            while len(w.done) < num_returns:
-                rem = None if deadline is None else max(0.0, deadline - time.monotonic())
-                if rem == 0.0:
-                    break
-                w.ev.wait(rem if rem is not None else 1.0)
-                w.ev.clear()
-                if len(w.done) >= num_returns:
-                    break
-                if self.exiting:
-                    break
+            with self.lock:
+                while True:
+                    still = []
+                    for oid in owned_pending:
+                        o = self.owned.get(oid)
+                        if o is None or o.ready:
+                            done.add(oid)
+                        else:
+                            still.append(oid)
+                    owned_pending = still
+                    if len(done) >= num_returns or self.exiting:
+                        break
+                    rem = None if deadline is None else deadline - time.monotonic()
+                    if rem is not None and rem <= 0:
+                        break
+                    cv.wait(rem if rem is not None else 1.0)
         finally:
             if blocked:
                 self._notify_unblocked()
-        return set(w.done)
+            self._drop_waiter(registered, remote_hit)
+        return set(done)
+
+    def _collect_ready(self, done, owned_pending, num_returns):
+        with self.lock:
+            for oid in owned_pending:
+                o = self.owned.get(oid)
+                if o is None or o.ready:
+                    done.add(oid)
+        return set(done)
+
+    def _drop_waiter(self, oids, cb):
+        """Unregister a finished waiter so callbacks do not pile up on pending objects."""
+        with self.lock:
+            for oid in oids:
+                o = self.owned.get(oid)
+                lst = o.callbacks if o is not None else None
+                if lst is None:
+                    r = self.remote.get(oid)
+                    lst = r.callbacks if r is not None else None
+                if lst:
+                    try:
+                        lst.remove(cb)
+                    except ValueError:
+                        pass
 
     def get_objects(self, refs, timeout=None):
         oids = [r._id for r in refs]

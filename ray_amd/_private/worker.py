@@ -22,7 +22,7 @@ SCRIPT_MODE = 0
 WORKER_MODE = 1
 LOCAL_MODE = 2
 
-ROOT_TMP = os.environ.get("RAY_AMD_TMPDIR", os.path.join(tempfile.gettempdir(), "ray_amd"))
+ROOT_TMP = os.environ.get("RAY_AMD_TMPDIR", os.path.join(tempfile.gettempdir(), "ray_amd_sessions"))
 CURRENT_CLUSTER_FILE = os.path.join(ROOT_TMP, "ray_current_cluster")
 
 

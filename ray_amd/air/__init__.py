@@ -1,0 +1,4 @@
+"""ray_amd.air — shared configs (reference: python/ray/air)."""
+from ray_amd.air.config import (CheckpointConfig, DatasetConfig, FailureConfig,  # noqa: F401
+                                RunConfig, ScalingConfig)
+from ray_amd.train.result import Result  # noqa: F401

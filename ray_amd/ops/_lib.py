@@ -30,7 +30,9 @@ _SIGS = {
     "ra_layernorm_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
     "ra_layernorm_bwd_parts": [c_int],
     "ra_layernorm_bwd": [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
-    "ra_colsum": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "ra_colsum": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "ra_layernorm_bwd_work": [c_int, c_int],
+    "ra_colsum_work": [c_int, c_int],
     "ra_colsum_parts": [c_int],
     "ra_bias_gelu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ra_bias_gelu_bwd": [c_void_p] * 6 + [c_int, c_int, c_void_p],
@@ -98,7 +100,7 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = c_int
+            f.restype = c_long if name.endswith("_work") else c_int
         _lib = L
     return _lib
 

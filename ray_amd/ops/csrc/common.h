@@ -88,6 +88,58 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
+// ---------------------------------------------------------------------------
+// Column reduction of a [P, D] fp32 partial slab -> out[D] (bf16 or fp32).
+// Stage 1: grid (ceil(D/64), S) blocks of 64 columns x 4 row-lanes; each block sums
+// a strided subset of the P rows and writes scratch[S][D]. Stage 2: one thread per
+// column sums S values. Replaces a one-thread-per-column loop that launched only
+// ceil(D/256) workgroups (measured 0.12 ms per LayerNorm bwd on MI355X).
+constexpr int kColsumSplits = 32;
+namespace {  // internal linkage: every TU gets its own copy of these kernels
+
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ part,
+                                                     float* __restrict__ scratch, int P, int D) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (c < D) {
+    for (int p = blockIdx.y * 4 + ty; p < P; p += gridDim.y * 4) s += part[(size_t)p * D + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < D)
+    scratch[(size_t)blockIdx.y * D + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ scratch, void* out,
+                                                     int S, int D) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += scratch[(size_t)i * D + c];
+  if (OUT_BF16) reinterpret_cast<uint16_t*>(out)[c] = __builtin_bit_cast(uint16_t, (__bf16)s);
+  else reinterpret_cast<float*>(out)[c] = s;
+}
+
+// scratch must hold kColsumSplits * D floats.
+static inline void colsum_launch(const float* part, float* scratch, void* out, int P, int D,
+                                 bool out_bf16, hipStream_t st) {
+  int S = (P + 15) / 16;
+  if (S > kColsumSplits) S = kColsumSplits;
+  if (S < 1) S = 1;
+  hipLaunchKernelGGL(colsum_stage1, dim3((D + 63) / 64, S), dim3(256), 0, st, part, scratch, P, D);
+  if (out_bf16)
+    hipLaunchKernelGGL(colsum_stage2<true>, dim3((D + 255) / 256), dim3(256), 0, st, scratch, out,
+                       S, D);
+  else
+    hipLaunchKernelGGL(colsum_stage2<false>, dim3((D + 255) / 256), dim3(256), 0, st, scratch,
+                       out, S, D);
+}
+
+}  // namespace
+
 // Grid size for memory-bound grid-stride kernels (Guideline 11): fill 256 CUs x 8.
 __host__ __forceinline__ int ra_grid(long long work_items, int block) {
   long long g = (work_items + block - 1) / block;

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16_t* __rest
 
 // grid: (ceil(F8/256), P). Thread owns 8 columns, walks the rows of chunk blockIdx.y.
 template <bool GELU>
-__global__ __launch_bounds__(256) void bwd_colpart_kernel(const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(64) void bwd_colpart_kernel(const bf16_t* __restrict__ dy,
                                                           const bf16_t* __restrict__ h,
                                                           const bf16_t* __restrict__ bias,
                                                           bf16_t* __restrict__ dh,
@@ -80,15 +80,6 @@ __global__ __launch_bounds__(256) void bwd_colpart_kernel(const bf16_t* __restri
   *reinterpret_cast<float4*>(pr + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
-__global__ __launch_bounds__(256) void colsum8_kernel(const float* __restrict__ part,
-                                                      bf16_t* __restrict__ out, int P, int F) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= F) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * F + c];
-  out[c] = f2bf(s);
-}
-
 __global__ __launch_bounds__(256) void bias_residual_kernel(const bf16_t* __restrict__ h,
                                                             const bf16_t* __restrict__ bias,
                                                             const bf16_t* __restrict__ res,
@@ -115,6 +106,11 @@ static inline int parts_for(int N) {
 
 RA_EXPORT int ra_colsum_parts(int N) { return parts_for(N); }
 
+// fp32 workspace (floats) for ra_bias_gelu_bwd / ra_colsum_bf16.
+RA_EXPORT long ra_colsum_work(int N, int F) {
+  return (long)parts_for(N) * F + (long)kColsumSplits * F;
+}
+
 RA_EXPORT int ra_bias_gelu_fwd(const void* h, const void* bias, void* y, long N, int F,
                                hipStream_t st) {
   if (F % 8) return hipErrorInvalidValue;
@@ -124,17 +120,16 @@ RA_EXPORT int ra_bias_gelu_fwd(const void* h, const void* bias, void* y, long N,
   return hipGetLastError();
 }
 
-// work: parts_for(N) * F floats
+// work: ra_colsum_work(N, F) floats
 RA_EXPORT int ra_bias_gelu_bwd(const void* dy, const void* h, const void* bias, void* dh,
                                void* dbias, float* work, int N, int F, hipStream_t st) {
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  hipLaunchKernelGGL(bwd_colpart_kernel<true>, dim3((F8 + 255) / 256, P), dim3(256), 0, st,
+  hipLaunchKernelGGL(bwd_colpart_kernel<true>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                      (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh, work,
                      N, F8, rpp);
-  hipLaunchKernelGGL(colsum8_kernel, dim3((F + 255) / 256), dim3(256), 0, st, work,
-                     (bf16_t*)dbias, P, F);
+  colsum_launch(work, work + (size_t)P * F, dbias, P, F, true, st);
   return hipGetLastError();
 }
 
@@ -143,10 +138,9 @@ RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 255) / 256, P), dim3(256), 0, st,
+  hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                      (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
-  hipLaunchKernelGGL(colsum8_kernel, dim3((F + 255) / 256), dim3(256), 0, st, work,
-                     (bf16_t*)out, P, F);
+  colsum_launch(work, work + (size_t)P * F, out, P, F, true, st);
   return hipGetLastError();
 }
 

@@ -147,18 +147,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[c] = sum_p part[p][c]  (fp32 accumulate, bf16 or fp32 output)
-template <bool OUT_BF16>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, void* out,
-                                                     int P, int D) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + c];
-  if (OUT_BF16) reinterpret_cast<bf16_t*>(out)[c] = f2bf(s);
-  else reinterpret_cast<float*>(out)[c] = s;
-}
-
 #define LN_DISPATCH(MACRO)                       \
   switch ((D + 255) / 256) {                     \
     case 1: MACRO(1); break;                     \
@@ -186,10 +174,15 @@ RA_EXPORT int ra_layernorm_fwd(const void* x, const void* g, const void* b, void
   return hipGetLastError();
 }
 
-// Partial-row count for the backward; workspace must hold 2 * ra_layernorm_bwd_parts(N) * D floats.
+// Partial-row count for the backward (1024 blocks x 4 waves fill 256 CUs 4-deep).
 RA_EXPORT int ra_layernorm_bwd_parts(int N) {
   int p = (N + 3) / 4;
-  return p < 512 ? p : 512;
+  return p < 1024 ? p : 1024;
+}
+
+// fp32 workspace (in floats) required by ra_layernorm_bwd.
+RA_EXPORT long ra_layernorm_bwd_work(int N, int D) {
+  return 2L * ra_layernorm_bwd_parts(N) * D + 2L * kColsumSplits * D;
 }
 
 RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
@@ -199,27 +192,21 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
   const int P = ra_layernorm_bwd_parts(N);
   float* dgp = work;
   float* dbp = work + (size_t)P * D;
+  float* scr = work + 2 * (size_t)P * D;
   const size_t lds = 2 * (size_t)D * sizeof(float);
 #define L(V)                                                                                  \
   hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(P), dim3(256), lds, st, (const bf16_t*)dy,        \
                      (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (bf16_t*)dx, dgp, dbp, N, D)
   LN_DISPATCH(L)
 #undef L
-  dim3 cg((D + 255) / 256);
-  if (out_bf16) {
-    hipLaunchKernelGGL(colsum_kernel<true>, cg, dim3(256), 0, st, dgp, dg, P, D);
-    hipLaunchKernelGGL(colsum_kernel<true>, cg, dim3(256), 0, st, dbp, db, P, D);
-  } else {
-    hipLaunchKernelGGL(colsum_kernel<false>, cg, dim3(256), 0, st, dgp, dg, P, D);
-    hipLaunchKernelGGL(colsum_kernel<false>, cg, dim3(256), 0, st, dbp, db, P, D);
-  }
+  colsum_launch(dgp, scr, dg, P, D, out_bf16 != 0, st);
+  colsum_launch(dbp, scr + (size_t)kColsumSplits * D, db, P, D, out_bf16 != 0, st);
   return hipGetLastError();
 }
 
-RA_EXPORT int ra_colsum(const float* part, void* out, int P, int D, int out_bf16,
+// out[c] = sum_p part[p][c]; scratch: kColsumSplits * D floats.
+RA_EXPORT int ra_colsum(const float* part, float* scratch, void* out, int P, int D, int out_bf16,
                         hipStream_t st) {
-  dim3 cg((D + 255) / 256);
-  if (out_bf16) hipLaunchKernelGGL(colsum_kernel<true>, cg, dim3(256), 0, st, part, out, P, D);
-  else hipLaunchKernelGGL(colsum_kernel<false>, cg, dim3(256), 0, st, part, out, P, D);
+  colsum_launch(part, scratch, out, P, D, out_bf16 != 0, st);
   return hipGetLastError();
 }

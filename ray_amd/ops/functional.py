@@ -40,8 +40,7 @@ class _LayerNorm(torch.autograd.Function):
         N, D = x2.shape
         dy2 = dy.contiguous().view(N, D)
         L = _lib.lib()
-        P = L.ra_layernorm_bwd_parts(N)
-        work = torch.empty(2 * P * D, device=dy.device, dtype=torch.float32)
+        work = torch.empty(L.ra_layernorm_bwd_work(N, D), device=dy.device, dtype=torch.float32)
         dx = torch.empty_like(x2)
         dw = torch.empty_like(w)
         db = torch.empty_like(w)
@@ -76,7 +75,7 @@ class _BiasGelu(torch.autograd.Function):
         h2, bias = ctx.saved_tensors
         N, F_ = h2.shape
         L = _lib.lib()
-        work = torch.empty(L.ra_colsum_parts(N) * F_, device=dy.device, dtype=torch.float32)
+        work = torch.empty(L.ra_colsum_work(N, F_), device=dy.device, dtype=torch.float32)
         dh = torch.empty_like(h2)
         db = torch.empty_like(bias)
         check(L.ra_bias_gelu_bwd(ptr(dy.contiguous()), ptr(h2), ptr(bias), ptr(dh), ptr(db),
@@ -94,7 +93,7 @@ def bias_gelu(h, bias):
 def _colsum_bf16(x2):
     N, F_ = x2.shape
     L = _lib.lib()
-    work = torch.empty(L.ra_colsum_parts(N) * F_, device=x2.device, dtype=torch.float32)
+    work = torch.empty(L.ra_colsum_work(N, F_), device=x2.device, dtype=torch.float32)
     out = torch.empty(F_, device=x2.device, dtype=x2.dtype)
     check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_, stream_ptr()), "colsum")
     return out

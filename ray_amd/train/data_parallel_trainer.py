@@ -1,0 +1,227 @@
+"""DataParallelTrainer + BackendExecutor (reference: python/ray/train/
+data_parallel_trainer.py, _internal/backend_executor.py, base_trainer.py).
+
+``fit()``: reserve one placement-group bundle per worker, start the worker actors,
+run the backend's ``on_start`` (process-group rendezvous), launch the training
+loop in every worker and drain reports in lock-step. Rank-0 metrics become the
+result; checkpoints are persisted to ``<storage_path>/<name>/checkpoint_XXXXXX``
+and pruned to ``CheckpointConfig.num_to_keep`` by score. On a worker failure the
+whole group restarts from the latest checkpoint, up to ``FailureConfig.max_failures``
+times.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import time
+import uuid
+
+import ray_amd as ray
+from ray_amd.air.config import CheckpointConfig, RunConfig, ScalingConfig
+from ray_amd.train._checkpoint import Checkpoint
+from ray_amd.train._internal.session import TrainContext
+from ray_amd.train._internal.worker_group import WorkerGroup
+from ray_amd.train.backend import BackendConfig
+from ray_amd.train.result import Result
+
+
+class TrainingFailedError(RuntimeError):
+    pass
+
+
+class _CheckpointManager:
+    def __init__(self, cfg: CheckpointConfig):
+        self.cfg = cfg
+        self.items: list[tuple[Checkpoint, dict]] = []
+
+    def register(self, ckpt: Checkpoint, metrics: dict):
+        self.items.append((ckpt, metrics))
+        k = self.cfg.num_to_keep
+        if k is not None and len(self.items) > k:
+            attr = self.cfg.checkpoint_score_attribute
+            latest = self.items[-1]
+            if attr:
+                rev = self.cfg.checkpoint_score_order == "max"
+                ranked = sorted(self.items, key=lambda x: x[1].get(attr, float("-inf") if rev
+                                                                     else float("inf")),
+                                reverse=rev)
+                keep = ranked[:k]
+            else:
+                keep = self.items[-k:]
+            if latest not in keep:
+                keep = keep[:-1] + [latest] if k > 0 else keep
+            for c, m in self.items:
+                if (c, m) not in keep:
+                    shutil.rmtree(c.path, ignore_errors=True)
+            self.items = [x for x in self.items if x in keep]
+
+    @property
+    def latest(self):
+        return self.items[-1][0] if self.items else None
+
+    @property
+    def best(self):
+        attr = self.cfg.checkpoint_score_attribute
+        if not self.items:
+            return None
+        if not attr:
+            return self.items[-1][0]
+        rev = self.cfg.checkpoint_score_order == "max"
+        return sorted(self.items, key=lambda x: x[1].get(attr, 0), reverse=rev)[0][0]
+
+
+class DataParallelTrainer:
+    _default_backend_config = BackendConfig
+
+    def __init__(self, train_loop_per_worker, *, train_loop_config: dict | None = None,
+                 backend_config: BackendConfig | None = None,
+                 scaling_config: ScalingConfig | None = None,
+                 run_config: RunConfig | None = None, datasets: dict | None = None,
+                 dataset_config=None, resume_from_checkpoint: Checkpoint | None = None,
+                 metadata: dict | None = None):
+        self.train_loop_per_worker = train_loop_per_worker
+        self.train_loop_config = train_loop_config
+        self.backend_config = backend_config or self._default_backend_config()
+        self.scaling_config = scaling_config or ScalingConfig()
+        self.run_config = run_config or RunConfig()
+        self.datasets = datasets or {}
+        self.dataset_config = dataset_config
+        self.resume_from_checkpoint = resume_from_checkpoint
+        self.metadata = metadata or {}
+
+    # ---------------------------------------------------------------------------
+    def _shards(self, n):
+        shards = [dict() for _ in range(n)]
+        for name, ds in self.datasets.items():
+            split = name == "train" or (self.dataset_config is not None and
+                                        getattr(self.dataset_config, "datasets_to_split", None)
+                                        and name in self.dataset_config.datasets_to_split)
+            if split and hasattr(ds, "streaming_split"):
+                parts = ds.streaming_split(n, equal=True)
+                for i in range(n):
+                    shards[i][name] = parts[i]
+            else:
+                for i in range(n):
+                    shards[i][name] = ds.iterator() if hasattr(ds, "iterator") else ds
+        return shards
+
+    def fit(self) -> Result:
+        if not ray.is_initialized():
+            ray.init()
+        rc = self.run_config
+        name = rc.name or f"{type(self).__name__}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
+        trial_dir = os.path.join(rc.storage_path, name)
+        os.makedirs(trial_dir, exist_ok=True)
+        mgr = _CheckpointManager(rc.checkpoint_config)
+        history = []
+        failures = 0
+        ckpt = self.resume_from_checkpoint
+        ckpt_index = 0
+        error = None
+        while True:
+            try:
+                metrics, ckpt_index = self._run_once(trial_dir, name, ckpt, ckpt_index, mgr,
+                                                     history)
+                error = None
+                break
+            except TrainingFailedError as e:
+                failures += 1
+                error = e
+                maxf = rc.failure_config.max_failures
+                if maxf != -1 and failures > maxf:
+                    break
+                ckpt = mgr.latest or ckpt
+        if error is not None:
+            res = Result(metrics=history[-1] if history else {}, checkpoint=mgr.latest,
+                         error=error, path=trial_dir, metrics_history=history,
+                         best_checkpoints=[(c, m) for c, m in mgr.items])
+            raise error
+        with open(os.path.join(trial_dir, "result.json"), "w") as f:
+            for m in history:
+                f.write(json.dumps({k: v for k, v in m.items()
+                                    if isinstance(v, (int, float, str, bool))}) + "\n")
+        return Result(metrics=history[-1] if history else {}, checkpoint=mgr.latest, error=None,
+                      path=trial_dir, metrics_history=history,
+                      best_checkpoints=[(c, m) for c, m in mgr.items])
+
+    def _run_once(self, trial_dir, name, ckpt, ckpt_index, mgr, history):
+        sc = self.scaling_config
+        wg = WorkerGroup(sc.num_workers, sc._resources_per_worker_not_none,
+                         sc.placement_strategy)
+        backend = self.backend_config.backend_cls()
+        try:
+            try:
+                backend.on_start(wg, self.backend_config)
+            except Exception as e:
+                raise TrainingFailedError(f"backend setup failed: {e!r}") from e
+            shards = self._shards(sc.num_workers)
+            node_ranks = {}
+            local_counts = {}
+            futs = []
+            trial_id = uuid.uuid4().hex[:8]
+            for rank, (w, info) in enumerate(zip(wg.workers, wg.infos)):
+                nid = info["node_id"]
+                node_ranks.setdefault(nid, len(node_ranks))
+                lr = local_counts.get(nid, 0)
+                local_counts[nid] = lr + 1
+                ctx = TrainContext(world_rank=rank, local_rank=lr, world_size=sc.num_workers,
+                                   node_rank=node_ranks[nid], experiment_name=name,
+                                   trial_name=name, trial_id=trial_id, trial_dir=trial_dir,
+                                   storage_path=self.run_config.storage_path,
+                                   metadata=self.metadata)
+                futs.append((w, ctx))
+            for w, ctx in futs:
+                ctx.local_world_size = local_counts[wg.infos[ctx.world_rank]["node_id"]]
+            ray.get([w.start_training.remote(self.train_loop_per_worker, self.train_loop_config,
+                                             ctx, ckpt, shards[ctx.world_rank], ckpt_index)
+                     for w, ctx in futs])
+            done = [False] * len(futs)
+            while not all(done):
+                try:
+                    outs = ray.get([w.get_next.remote() for (w, _), d in zip(futs, done)
+                                    if not d])
+                except ray.exceptions.RayActorError as e:
+                    raise TrainingFailedError(f"a training worker died: {e}") from e
+                idx = [i for i, d in enumerate(done) if not d]
+                rank0 = None
+                for i, (kind, a, b) in zip(idx, outs):
+                    if kind == "error":
+                        exc, tb = a
+                        raise TrainingFailedError(f"training function raised on rank {i}:\n{tb}"
+                                                  ) from exc
+                    if kind == "done":
+                        done[i] = True
+                    elif i == 0:
+                        rank0 = (a, b)
+                if rank0 is not None:
+                    metrics, cpath = rank0
+                    history.append(metrics)
+                    if cpath:
+                        c = Checkpoint(cpath)
+                        mgr.register(c, metrics)
+                        ckpt_index = int(os.path.basename(cpath).split("_")[-1]) + 1
+                    stop = self.run_config.stop
+                    if stop and _should_stop(stop, metrics):
+                        break
+            return (history[-1] if history else {}), ckpt_index
+        finally:
+            try:
+                backend.on_shutdown(wg, self.backend_config)
+            except Exception:
+                pass
+            wg.shutdown()
+
+    @classmethod
+    def restore(cls, path, **kwargs):
+        return cls(**kwargs)
+
+
+def _should_stop(stop, metrics):
+    if callable(stop):
+        return stop(metrics)
+    for k, v in stop.items():
+        if k in metrics and metrics[k] >= v:
+            return True
+    return False

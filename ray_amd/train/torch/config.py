@@ -1,0 +1,91 @@
+"""Torch backend: one process group per Train worker group on RCCL over xGMI
+(reference: python/ray/train/torch/config.py).
+
+MI355X specifics:
+* backend "nccl" is RCCL on ROCm; CPU-only groups use gloo.
+* all ranks on a node see the union of the group's GPUs (HIP_VISIBLE_DEVICES),
+  each rank binds ``cuda:<its index in that list>`` — RCCL then uses xGMI
+  peer-to-peer between the ranks' processes (like the reference's
+  share_cuda_visible_devices).
+* rendezvous over TCP on 127.0.0.1 for single-node groups.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from datetime import timedelta
+
+from ray_amd.train.backend import Backend, BackendConfig
+
+
+@dataclass
+class TorchConfig(BackendConfig):
+    backend: str | None = None
+    init_method: str = "env"
+    timeout_s: int = 1800
+
+    @property
+    def backend_cls(self):
+        return _TorchBackend
+
+
+def _setup_env(global_gpu_ids, my_gpu_ids):
+    if global_gpu_ids:
+        os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in global_gpu_ids)
+        os.environ.pop("CUDA_VISIBLE_DEVICES", None)
+        idx = global_gpu_ids.index(my_gpu_ids[0]) if my_gpu_ids else 0
+        os.environ["RAY_AMD_LOCAL_DEVICE"] = str(idx)
+    return True
+
+
+def _init_pg(backend, master_addr, master_port, rank, world, local_rank, timeout_s):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = master_addr
+    os.environ["MASTER_PORT"] = str(master_port)
+    os.environ["RANK"] = str(rank)
+    os.environ["WORLD_SIZE"] = str(world)
+    os.environ["LOCAL_RANK"] = str(local_rank)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    kw = {}
+    if backend == "nccl":
+        dev = int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))
+        torch.cuda.set_device(dev)
+        kw["device_id"] = torch.device("cuda", dev)
+    dist.init_process_group(backend, init_method=f"tcp://{master_addr}:{master_port}",
+                            rank=rank, world_size=world, timeout=timedelta(seconds=timeout_s),
+                            **kw)
+    return True
+
+
+class _TorchBackend(Backend):
+    share_cuda_visible_devices = True
+
+    def on_start(self, worker_group, backend_config: TorchConfig):
+        import ray_amd as ray
+
+        infos = worker_group.infos
+        use_gpu = any(i["gpu_ids"] for i in infos)
+        backend = backend_config.backend or ("nccl" if use_gpu else "gloo")
+        if use_gpu:
+            by_node = {}
+            for i in infos:
+                by_node.setdefault(i["node_id"], []).extend(i["physical_gpu_ids"])
+            futs = [w.execute.remote(_setup_env, sorted(set(by_node[i["node_id"]]), key=int),
+                                     i["physical_gpu_ids"])
+                    for w, i in zip(worker_group.workers, infos)]
+            ray.get(futs)
+        port = ray.get(worker_group.workers[0].free_port.remote())
+        local = {}
+        futs = []
+        for rank, (w, i) in enumerate(zip(worker_group.workers, infos)):
+            lr = local.get(i["node_id"], 0)
+            local[i["node_id"]] = lr + 1
+            futs.append(w.execute.remote(_init_pg, backend, "127.0.0.1", port, rank,
+                                         len(infos), lr, backend_config.timeout_s))
+        ray.get(futs)
+
+    def on_shutdown(self, worker_group, backend_config):
+        pass

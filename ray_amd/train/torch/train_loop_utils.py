@@ -1,0 +1,183 @@
+"""Torch helpers for training loops (reference: python/ray/train/torch/train_loop_utils.py).
+
+``prepare_model`` on MI355X: bf16 models on GPU go through the flat-buffer DDP of
+``ray_amd.parallel.flat`` (zero-copy bf16 grad buckets all-reduced on RCCL while
+backward runs, fused AdamW); any other model is wrapped in torch DDP (gloo on CPU).
+"""
+
+from __future__ import annotations
+
+import os
+import random
+
+import torch
+import torch.distributed as dist
+
+
+def get_device() -> torch.device:
+    if torch.cuda.is_available():
+        idx = int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))
+        if idx >= torch.cuda.device_count():
+            idx = 0
+        return torch.device("cuda", idx)
+    return torch.device("cpu")
+
+
+def get_devices():
+    return [get_device()]
+
+
+class FlatPreparedModel(torch.nn.Module):
+    """Wrapper returned by prepare_model(parallel_strategy='flat'): the module plus its
+    flat parameter/gradient buffers, bucketed all-reduce and fused optimizer."""
+
+    def __init__(self, module, flat, ddp):
+        super().__init__()
+        self.module = module
+        self.flat = flat
+        self.ddp = ddp
+
+    def forward(self, *a, **k):
+        return self.module(*a, **k)
+
+    def make_optimizer(self, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0):
+        from ray_amd.parallel.flat import FlatAdamW
+
+        return _FlatOptimizer(self, FlatAdamW(self.flat, lr=lr, betas=betas,
+                                              weight_decay=weight_decay,
+                                              max_grad_norm=max_grad_norm,
+                                              grad_scale=self.ddp.grad_scale))
+
+
+class _FlatOptimizer:
+    def __init__(self, model: FlatPreparedModel, opt):
+        self.model = model
+        self.opt = opt
+
+    def zero_grad(self, set_to_none=False):
+        self.model.flat.zero_grad()
+
+    def step(self, lr=None):
+        self.model.ddp.finish()
+        self.opt.step(lr)
+
+    @property
+    def param_groups(self):
+        return [{"lr": self.opt.lr}]
+
+
+def prepare_model(model: torch.nn.Module, move_to_device: bool = True,
+                  parallel_strategy: str | None = "auto", parallel_strategy_kwargs=None):
+    dev = get_device()
+    if move_to_device:
+        model = model.to(dev)
+    kw = parallel_strategy_kwargs or {}
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    params = list(model.parameters())
+    is_bf16 = params and all(p.dtype == torch.bfloat16 for p in params)
+    if parallel_strategy == "flat" or (parallel_strategy == "auto" and dev.type == "cuda" and
+                                       is_bf16):
+        from ray_amd.parallel.flat import FlatDDP, FlatParams
+
+        flat = FlatParams(model, dtype=params[0].dtype)
+        ddp = FlatDDP(flat, bucket_mb=kw.get("bucket_mb", 32.0))
+        return FlatPreparedModel(model, flat, ddp)
+    if world > 1 and parallel_strategy in ("auto", "ddp"):
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        if dev.type == "cuda":
+            return DDP(model, device_ids=[dev], output_device=dev,
+                       bucket_cap_mb=kw.get("bucket_cap_mb", 32), **{k: v for k, v in kw.items()
+                                                                    if k != "bucket_cap_mb"})
+        return DDP(model, **kw)
+    if parallel_strategy == "fsdp" and world > 1:
+        from torch.distributed.fsdp import FullyShardedDataParallel as FSDP
+
+        return FSDP(model, device_id=dev if dev.type == "cuda" else None, **kw)
+    return model
+
+
+class _DeviceLoader:
+    def __init__(self, loader, device, auto_transfer=True):
+        self.loader = loader
+        self.device = device
+        self.auto = auto_transfer
+        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+
+    def _move(self, b):
+        if isinstance(b, torch.Tensor):
+            return b.to(self.device, non_blocking=True)
+        if isinstance(b, (list, tuple)):
+            return type(b)(self._move(x) for x in b)
+        if isinstance(b, dict):
+            return {k: self._move(v) for k, v in b.items()}
+        return b
+
+    def __iter__(self):
+        it = iter(self.loader)
+        if self.stream is None or not self.auto:
+            for b in it:
+                yield self._move(b) if self.auto else b
+            return
+        # double-buffered H2D on a side stream (pinned host memory -> HBM overlaps compute)
+        nxt = None
+        try:
+            first = next(it)
+        except StopIteration:
+            return
+        with torch.cuda.stream(self.stream):
+            nxt = self._move(first)
+        for b in it:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            cur = nxt
+            with torch.cuda.stream(self.stream):
+                nxt = self._move(b)
+            yield cur
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        yield nxt
+
+    def __len__(self):
+        return len(self.loader)
+
+
+def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_device: bool = True,
+                        auto_transfer: bool = True):
+    from torch.utils.data import DataLoader, DistributedSampler
+
+    if add_dist_sampler and dist.is_initialized() and dist.get_world_size() > 1 and \
+            not isinstance(getattr(data_loader, "sampler", None), DistributedSampler):
+        shuffle = isinstance(getattr(data_loader, "sampler", None),
+                             torch.utils.data.RandomSampler)
+        sampler = DistributedSampler(data_loader.dataset, shuffle=shuffle)
+        data_loader = DataLoader(data_loader.dataset, batch_size=data_loader.batch_size,
+                                 sampler=sampler, num_workers=data_loader.num_workers,
+                                 collate_fn=data_loader.collate_fn,
+                                 pin_memory=get_device().type == "cuda",
+                                 drop_last=data_loader.drop_last)
+    if move_to_device:
+        return _DeviceLoader(data_loader, get_device(), auto_transfer)
+    return data_loader
+
+
+def prepare_optimizer(optimizer):
+    return optimizer
+
+
+def backward(tensor):
+    tensor.backward()
+
+
+def enable_reproducibility(seed: int = 0):
+    torch.manual_seed(seed)
+    random.seed(seed)
+    try:
+        import numpy as np
+
+        np.random.seed(seed)
+    except ImportError:
+        pass
+    torch.use_deterministic_algorithms(True, warn_only=True)
+
+
+def accelerate(amp: bool = False):
+    pass
