@@ -1580,6 +1580,9 @@ class CoreWorker:
                     raise _ActorExit()
                 elif spec["method"] == "__ray_ready__":
                     fn = _ready
+                elif spec["method"] == "__ray_call__":
+                    inst = self.actor_instance
+                    fn = lambda f, *a, **k: f(inst, *a, **k)  # noqa: E731
                 else:
                     fn = getattr(self.actor_instance, spec["method"])
                 args, kwargs = self._decode_args(spec["args"], spec["owner"])

@@ -84,10 +84,11 @@ class ActorHandle:
         return ActorID(self._actor_id)
 
     def __getattr__(self, name):
-        if name.startswith("_") and name not in ("__ray_terminate__", "__call__"):
+        special = ("__ray_terminate__", "__call__", "__ray_call__", "__ray_ready__")
+        if name.startswith("_") and name not in special:
             raise AttributeError(name)
         meta = self._meta
-        if name not in meta and name != "__ray_terminate__" and meta:
+        if name not in meta and name not in special and meta:
             raise AttributeError(f"'{self._class_name}' actor has no method '{name}'")
         return ActorMethod(self, name, dict(meta.get(name, {})))
 

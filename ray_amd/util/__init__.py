@@ -1,0 +1,35 @@
+"""ray_amd.util (reference: python/ray/util/__init__.py)."""
+
+from ray_amd._private.serialization import (deregister_serializer,  # noqa: F401
+                                            register_serializer)
+from ray_amd.util.actor_pool import ActorPool  # noqa: F401
+from ray_amd.util.placement_group import (get_current_placement_group,  # noqa: F401
+                                          get_placement_group, placement_group,
+                                          placement_group_table, remove_placement_group)
+
+
+def get_node_ip_address():
+    return "127.0.0.1"
+
+
+def list_named_actors(all_namespaces: bool = False):
+    from ray_amd._private import worker as W
+
+    cw = W._check_connected()
+    return cw.call_raylet("list_named_actors", all_namespaces, cw.namespace)
+
+
+def inspect_serializability(obj, name=None, depth=3, print_file=None):
+    import cloudpickle
+
+    try:
+        cloudpickle.dumps(obj)
+        return True, set()
+    except Exception as e:  # noqa: BLE001
+        return False, {repr(e)}
+
+
+__all__ = ["ActorPool", "placement_group", "placement_group_table", "get_placement_group",
+           "remove_placement_group", "get_current_placement_group", "register_serializer",
+           "deregister_serializer", "get_node_ip_address", "list_named_actors",
+           "inspect_serializability"]

@@ -1,0 +1,143 @@
+"""ray_amd.util tests (modelled on test_actor_pool.py, test_queue.py, test_multiprocessing.py,
+util/collective/tests/single_node_cpu_tests)."""
+
+import time
+
+import pytest
+import torch
+
+import ray_amd as ray
+from ray_amd.util import ActorPool
+from ray_amd.util.multiprocessing import Pool
+from ray_amd.util.queue import Empty, Full, Queue
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=6)
+    yield
+    ray.shutdown()
+
+
+@ray.remote
+class Doubler:
+    def double(self, v):
+        return 2 * v
+
+
+def test_actor_pool(cluster):
+    pool = ActorPool([Doubler.remote(), Doubler.remote()])
+    assert list(pool.map(lambda a, v: a.double.remote(v), [1, 2, 3, 4])) == [2, 4, 6, 8]
+    assert sorted(pool.map_unordered(lambda a, v: a.double.remote(v), range(5))) == \
+        [0, 2, 4, 6, 8]
+    pool.submit(lambda a, v: a.double.remote(v), 10)
+    assert pool.get_next() == 20
+    assert not pool.has_next()
+
+
+def test_queue(cluster):
+    q = Queue(maxsize=2)
+    q.put(1)
+    q.put(2)
+    with pytest.raises(Full):
+        q.put(3, timeout=0.1)
+    assert q.size() == 2
+    assert q.get() == 1
+    assert q.get() == 2
+    with pytest.raises(Empty):
+        q.get(timeout=0.1)
+    q.put_nowait_batch([5, 6])
+    assert q.get_nowait_batch(2) == [5, 6]
+
+    @ray.remote
+    def consumer(q):
+        return q.get(timeout=10)
+
+    r = consumer.remote(q)
+    time.sleep(0.2)
+    q.put("x")
+    assert ray.get(r) == "x"
+
+
+def _sq(x):
+    return x * x
+
+
+def test_multiprocessing_pool(cluster):
+    with Pool(processes=3) as p:
+        assert p.map(_sq, range(10)) == [x * x for x in range(10)]
+        assert p.apply(_sq, (7,)) == 49
+        assert sorted(p.imap_unordered(_sq, range(5))) == [0, 1, 4, 9, 16]
+        assert list(p.imap(_sq, range(4))) == [0, 1, 4, 9]
+        assert p.starmap(pow, [(2, 3), (3, 2)]) == [8, 9]
+        r = p.map_async(_sq, [1, 2])
+        assert r.get(timeout=10) == [1, 4]
+
+
+@ray.remote
+class CollWorker:
+    def setup(self, world, rank):
+        from ray_amd.util import collective as col
+
+        col.init_collective_group(world, rank, backend="gloo", group_name="g")
+        return True
+
+    def run(self, rank):
+        from ray_amd.util import collective as col
+
+        t = torch.ones(4) * (rank + 1)
+        col.allreduce(t, group_name="g")
+        out = [torch.zeros(2) for _ in range(2)]
+        col.allgather(out, torch.full((2,), float(rank)), group_name="g")
+        b = torch.full((3,), float(rank))
+        col.broadcast(b, src_rank=1, group_name="g")
+        rs = torch.zeros(2)
+        col.reducescatter(rs, [torch.ones(2) * (rank + 1), torch.ones(2) * 10], group_name="g")
+        ts = [torch.ones(1) * (rank + 1) * 3]
+        col.allreduce_coalesced(ts, group_name="g")
+        a2a_out = [torch.zeros(1), torch.zeros(1)]
+        col.alltoall(a2a_out, [torch.tensor([rank * 10.0]), torch.tensor([rank * 10.0 + 1])],
+                     group_name="g")
+        col.barrier(group_name="g")
+        return (t.tolist(), [o.tolist() for o in out], b.tolist(), rs.tolist(), ts[0].item(),
+                [x.item() for x in a2a_out], col.get_rank("g"),
+                col.get_collective_group_size("g"))
+
+
+def test_collective_gloo(cluster):
+    ws = [CollWorker.remote() for _ in range(2)]
+    ray.get([w.setup.remote(2, i) for i, w in enumerate(ws)])
+    r0, r1 = ray.get([w.run.remote(i) for i, w in enumerate(ws)])
+    assert r0[0] == [3.0] * 4 and r1[0] == [3.0] * 4
+    assert r0[1] == [[0.0, 0.0], [1.0, 1.0]]
+    assert r0[2] == [1.0] * 3
+    assert r0[3] == [3.0, 3.0] and r1[3] == [20.0, 20.0]
+    assert r0[4] == 9.0
+    assert r0[5] == [0.0, 10.0] and r1[5] == [1.0, 11.0]
+    assert (r0[6], r1[6], r0[7]) == (0, 1, 2)
+
+
+def test_create_collective_group_from_driver(cluster):
+    from ray_amd.util import collective as col
+
+    @ray.remote
+    class W:
+        def go(self):
+            t = torch.ones(2)
+            col.allreduce(t, group_name="drv")
+            return t.tolist()
+
+    ws = [W.remote() for _ in range(2)]
+    col.create_collective_group(ws, 2, [0, 1], backend="gloo", group_name="drv")
+    assert ray.get([w.go.remote() for w in ws]) == [[2.0, 2.0]] * 2
+
+
+def test_internal_kv(cluster):
+    from ray_amd.experimental import internal_kv as kv
+
+    assert not kv._internal_kv_put(b"k", b"v")
+    assert kv._internal_kv_get(b"k") == b"v"
+    assert kv._internal_kv_exists(b"k")
+    assert kv._internal_kv_list(b"k") == [b"k"]
+    kv._internal_kv_del(b"k")
+    assert kv._internal_kv_get(b"k") is None
