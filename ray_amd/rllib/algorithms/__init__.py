@@ -1,0 +1,5 @@
+from ray_amd.rllib.algorithms.algorithm import Algorithm  # noqa: F401
+from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig  # noqa: F401
+from ray_amd.rllib.algorithms.dqn import DQN, DQNConfig  # noqa: F401
+from ray_amd.rllib.algorithms.impala import APPO, IMPALA, APPOConfig, IMPALAConfig  # noqa: F401
+from ray_amd.rllib.algorithms.ppo import PPO, PPOConfig  # noqa: F401

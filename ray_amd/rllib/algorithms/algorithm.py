@@ -1,0 +1,221 @@
+"""Algorithm base (reference: rllib/algorithms/algorithm.py).
+
+Owns the EnvRunner actors (CPU sampling), the LearnerGroup (GPU learning) and
+the train()/save()/restore()/evaluate() lifecycle; subclasses implement
+``training_step``."""
+
+from __future__ import annotations
+
+import os
+import pickle
+import time
+
+import numpy as np
+
+import ray_amd as ray
+from ray_amd.rllib.env.env_runner import SingleAgentEnvRunner
+from ray_amd.rllib.env.envs import make_env
+
+
+class Algorithm:
+    kind = "ppo"
+
+    def __init__(self, config):
+        if not ray.is_initialized():
+            ray.init()
+        self.config = config
+        self.cfg = config.to_dict()
+        self.cfg["module_kind"] = getattr(self, "module_kind", "actor_critic")
+        probe = make_env(config.env, config.env_config)
+        self.observation_space = probe.observation_space
+        self.action_space = probe.action_space
+        probe.close()
+        self.iteration = 0
+        self.total_env_steps = 0
+        self.weights_version = 0
+        self._episode_returns = []
+        self._episode_lengths = []
+        self._t_start = time.time()
+        nr = int(config.num_env_runners)
+        runner_cls = ray.remote(SingleAgentEnvRunner)
+        opts = {"num_cpus": config.num_cpus_per_env_runner}
+        if config.num_gpus_per_env_runner:
+            opts["num_gpus"] = config.num_gpus_per_env_runner
+        if nr > 0:
+            self.env_runners = [runner_cls.options(**opts).remote(self.cfg, i + 1)
+                                for i in range(nr)]
+            ray.get([r.ping.remote() for r in self.env_runners])
+            self.local_runner = None
+        else:
+            self.env_runners = []
+            self.local_runner = SingleAgentEnvRunner(self.cfg, 0)
+        self.setup()
+
+    def setup(self):
+        pass
+
+    # ---------------------------------------------------------------- weights
+    def _sync_weights(self, weights):
+        self.weights_version += 1
+        if self.env_runners:
+            ref = ray.put(weights)
+            ray.get([r.set_weights.remote(ref, self.weights_version) for r in self.env_runners])
+        else:
+            self.local_runner.set_weights(weights, self.weights_version)
+
+    def _collect_metrics(self):
+        if self.env_runners:
+            ms = ray.get([r.get_metrics.remote() for r in self.env_runners])
+        else:
+            ms = [self.local_runner.get_metrics()]
+        for m in ms:
+            self._episode_returns.extend(m["episode_returns"])
+            self._episode_lengths.extend(m["episode_lengths"])
+        k = self.config.metrics_num_episodes_for_smoothing
+        self._episode_returns = self._episode_returns[-k:]
+        self._episode_lengths = self._episode_lengths[-k:]
+
+    # ---------------------------------------------------------------- train loop
+    def train(self) -> dict:
+        t0 = time.time()
+        steps0 = self.total_env_steps
+        res = self.training_step()
+        mt = self.config.min_time_s_per_iteration
+        while mt and time.time() - t0 < mt:
+            r2 = self.training_step()
+            res.update(r2)
+        self.iteration += 1
+        self._collect_metrics()
+        dt = time.time() - t0
+        rets = self._episode_returns
+        out = {
+            "training_iteration": self.iteration,
+            "env_runners": {
+                "episode_return_mean": float(np.mean(rets)) if rets else float("nan"),
+                "episode_return_max": float(np.max(rets)) if rets else float("nan"),
+                "episode_return_min": float(np.min(rets)) if rets else float("nan"),
+                "episode_len_mean": float(np.mean(self._episode_lengths))
+                if self._episode_lengths else float("nan"),
+                "num_episodes": len(rets),
+            },
+            "num_env_steps_sampled_lifetime": self.total_env_steps,
+            "num_env_steps_sampled_this_iter": self.total_env_steps - steps0,
+            "env_steps_per_sec": (self.total_env_steps - steps0) / max(dt, 1e-9),
+            "time_this_iter_s": dt,
+            "time_total_s": time.time() - self._t_start,
+            "learners": res,
+        }
+        out["episode_reward_mean"] = out["env_runners"]["episode_return_mean"]
+        if self.config.evaluation_interval and self.iteration % self.config.evaluation_interval \
+                == 0:
+            out["evaluation"] = self.evaluate()
+        return out
+
+    def training_step(self) -> dict:
+        raise NotImplementedError
+
+    def _sample(self, total: int):
+        """Synchronous parallel sampling of >= total env steps (reference:
+        rllib/execution/rollout_ops.py:synchronous_parallel_sample)."""
+        cfg = self.config
+        per = cfg.rollout_fragment_length
+        batches = []
+        got = 0
+        while got < total:
+            if self.env_runners:
+                bs = ray.get([r.sample.remote(per) for r in self.env_runners])
+            else:
+                bs = [self.local_runner.sample(per)]
+            for b in bs:
+                got += b["env_steps"]
+            batches.extend(bs)
+        self.total_env_steps += got
+        return batches
+
+    def evaluate(self) -> dict:
+        runner = SingleAgentEnvRunner(self.cfg, 999)
+        runner.set_weights(self.get_weights(), None)
+        n = self.config.evaluation_duration
+        rets = []
+        while len(rets) < n:
+            runner.sample(self.config.rollout_fragment_length, explore=False)
+            rets.extend(runner.get_metrics()["episode_returns"])
+        return {"env_runners": {"episode_return_mean": float(np.mean(rets[:n]))}}
+
+    # ---------------------------------------------------------------- inference
+    def compute_single_action(self, obs, explore=False):
+        import torch
+
+        from ray_amd.rllib.core.rl_module import RLModule
+
+        if not hasattr(self, "_infer_module"):
+            self._infer_module = RLModule(self.observation_space, self.action_space,
+                                          self.config.model)
+        self._infer_module.load_state_dict(self.get_weights())
+        with torch.no_grad():
+            x = torch.as_tensor(np.asarray(obs)[None])
+            di = self._infer_module.forward_inference(x)["action_dist_inputs"]
+            a, _ = self._infer_module.sample_actions(di, explore)
+        a = a[0].numpy()
+        return int(a) if a.ndim == 0 else a
+
+    compute_action = compute_single_action
+
+    # ---------------------------------------------------------------- checkpoints
+    def get_weights(self):
+        return self.learner_group.get_weights()
+
+    def get_state(self):
+        return {"learner": self.learner_group.get_state(), "iteration": self.iteration,
+                "total_env_steps": self.total_env_steps, "config": self.cfg}
+
+    def set_state(self, s):
+        self.learner_group.set_state(s["learner"])
+        self.iteration = s["iteration"]
+        self.total_env_steps = s["total_env_steps"]
+        self._sync_weights(self.get_weights())
+
+    def save(self, checkpoint_dir: str | None = None):
+        import tempfile
+
+        d = checkpoint_dir or tempfile.mkdtemp(prefix="rllib_ckpt_")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "algorithm_state.pkl"), "wb") as f:
+            pickle.dump(self.get_state(), f)
+        from ray_amd.train._checkpoint import Checkpoint
+
+        return Checkpoint(d)
+
+    save_to_path = save
+
+    def restore(self, checkpoint):
+        path = checkpoint.path if hasattr(checkpoint, "path") else checkpoint
+        with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
+            self.set_state(pickle.load(f))
+
+    restore_from_path = restore
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint, config=None):
+        path = checkpoint.path if hasattr(checkpoint, "path") else checkpoint
+        with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
+            state = pickle.load(f)
+        if config is None:
+            from ray_amd.rllib.algorithms.registry import get_config_class
+
+            config = get_config_class(cls)().update_from_dict(state["config"])
+        algo = cls(config)
+        algo.set_state(state)
+        return algo
+
+    def stop(self):
+        for r in self.env_runners:
+            try:
+                ray.kill(r)
+            except Exception:
+                pass
+        self.env_runners = []
+        self.learner_group.shutdown()
+
+    def __del__(self):
+        pass

@@ -1,0 +1,144 @@
+"""AlgorithmConfig builder (reference: rllib/algorithms/algorithm_config.py)."""
+
+from __future__ import annotations
+
+import copy
+
+
+class AlgorithmConfig:
+    algo_class = None
+
+    def __init__(self, algo_class=None):
+        self.algo_class = algo_class or type(self).algo_class
+        self.env = None
+        self.env_config = {}
+        self.num_env_runners = 2
+        self.num_envs_per_env_runner = 1
+        self.rollout_fragment_length = 200
+        self.num_cpus_per_env_runner = 1
+        self.num_gpus_per_env_runner = 0
+        self.gamma = 0.99
+        self.lr = 5e-5
+        self.train_batch_size = 4000
+        self.model = {}
+        self.grad_clip = None
+        self.num_learners = 0
+        self.num_gpus_per_learner = 1
+        self.seed = None
+        self.evaluation_interval = None
+        self.evaluation_duration = 10
+        self.evaluation_num_env_runners = 0
+        self.evaluation_config = {}
+        self.min_time_s_per_iteration = None
+        self.framework_str = "torch"
+        self.learner_bf16 = True
+        self.bootstrap_truncated = False
+        self.metrics_num_episodes_for_smoothing = 100
+
+    # ---------------------------------------------------------------- builders
+    def environment(self, env=None, *, env_config=None, **kw):
+        if env is not None:
+            self.env = env
+        if env_config is not None:
+            self.env_config = dict(env_config)
+        return self
+
+    def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None,
+                    rollout_fragment_length=None, num_cpus_per_env_runner=None,
+                    num_gpus_per_env_runner=None, **kw):
+        for k, v in dict(num_env_runners=num_env_runners,
+                         num_envs_per_env_runner=num_envs_per_env_runner,
+                         rollout_fragment_length=rollout_fragment_length,
+                         num_cpus_per_env_runner=num_cpus_per_env_runner,
+                         num_gpus_per_env_runner=num_gpus_per_env_runner).items():
+            if v is not None:
+                setattr(self, k, v)
+        return self
+
+    def rollouts(self, *, num_rollout_workers=None, num_envs_per_worker=None, **kw):
+        return self.env_runners(num_env_runners=num_rollout_workers,
+                                num_envs_per_env_runner=num_envs_per_worker, **kw)
+
+    def training(self, **kw):
+        aliases = {"sgd_minibatch_size": "minibatch_size", "num_sgd_iter": "num_epochs",
+                   "lambda": "lambda_"}
+        for k, v in kw.items():
+            if v is None:
+                continue
+            setattr(self, aliases.get(k, k), v)
+        return self
+
+    def resources(self, *, num_gpus=None, **kw):
+        if num_gpus is not None:
+            self.num_gpus_per_learner = num_gpus if num_gpus <= 1 else 1
+            if num_gpus > 1:
+                self.num_learners = int(num_gpus)
+        return self
+
+    def learners(self, *, num_learners=None, num_gpus_per_learner=None, **kw):
+        if num_learners is not None:
+            self.num_learners = num_learners
+        if num_gpus_per_learner is not None:
+            self.num_gpus_per_learner = num_gpus_per_learner
+        return self
+
+    def framework(self, framework="torch", **kw):
+        if framework not in ("torch",):
+            raise ValueError("ray_amd RLlib supports framework='torch' only (MI355X/ROCm)")
+        self.framework_str = framework
+        return self
+
+    def debugging(self, *, seed=None, **kw):
+        if seed is not None:
+            self.seed = seed
+        return self
+
+    def evaluation(self, *, evaluation_interval=None, evaluation_duration=None,
+                   evaluation_num_env_runners=None, evaluation_config=None, **kw):
+        if evaluation_interval is not None:
+            self.evaluation_interval = evaluation_interval
+        if evaluation_duration is not None:
+            self.evaluation_duration = evaluation_duration
+        if evaluation_num_env_runners is not None:
+            self.evaluation_num_env_runners = evaluation_num_env_runners
+        if evaluation_config is not None:
+            self.evaluation_config = evaluation_config
+        return self
+
+    def reporting(self, *, min_time_s_per_iteration=None, metrics_num_episodes_for_smoothing=None,
+                  **kw):
+        if min_time_s_per_iteration is not None:
+            self.min_time_s_per_iteration = min_time_s_per_iteration
+        if metrics_num_episodes_for_smoothing is not None:
+            self.metrics_num_episodes_for_smoothing = metrics_num_episodes_for_smoothing
+        return self
+
+    def api_stack(self, **kw):
+        return self
+
+    def update_from_dict(self, d: dict):
+        for k, v in d.items():
+            setattr(self, "lambda_" if k == "lambda" else k, v)
+        return self
+
+    def copy(self, copy_frozen=None):
+        return copy.deepcopy(self)
+
+    def to_dict(self) -> dict:
+        return {k: v for k, v in self.__dict__.items() if k != "algo_class"}
+
+    def get(self, k, default=None):
+        return getattr(self, k, default)
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+    def build(self, env=None, logger_creator=None):
+        if env is not None:
+            self.env = env
+        if self.algo_class is None:
+            raise ValueError("no algorithm class bound to this config")
+        return self.algo_class(self.copy())
+
+    def build_algo(self, *a, **k):
+        return self.build(*a, **k)

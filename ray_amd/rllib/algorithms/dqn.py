@@ -1,0 +1,144 @@
+"""DQN (double, dueling, prioritized replay, n-step=1) (reference: rllib/algorithms/dqn/)."""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import ray_amd as ray
+from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.rl_module import QModule
+from ray_amd.rllib.utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
+
+
+class DQNConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or DQN)
+        self.lr = 5e-4
+        self.train_batch_size = 32
+        self.rollout_fragment_length = 4
+        self.num_env_runners = 0
+        self.replay_buffer_config = {"type": "PrioritizedEpisodeReplayBuffer", "capacity": 50000,
+                                     "alpha": 0.6, "beta": 0.4}
+        self.num_steps_sampled_before_learning_starts = 1000
+        self.target_network_update_freq = 500
+        self.double_q = True
+        self.dueling = True
+        self.epsilon = [(0, 1.0), (10000, 0.05)]
+        self.training_intensity = None
+        self.grad_clip = 40.0
+        self.model = {"fcnet_hiddens": [256], "fcnet_activation": "relu"}
+
+
+class _QLearner:
+    def __init__(self, cfg, obs_space, act_space):
+        self.cfg = cfg
+        dev = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
+            "num_gpus_per_learner", 1) else torch.device("cpu")
+        self.device = dev
+        mc = dict(cfg.get("model") or {})
+        mc["dueling"] = cfg.get("dueling", True)
+        self.q = QModule(obs_space, act_space, mc).to(dev)
+        self.target = QModule(obs_space, act_space, mc).to(dev)
+        self.target.load_state_dict(self.q.state_dict())
+        self.opt = torch.optim.Adam(self.q.parameters(), lr=cfg.get("lr", 5e-4))
+
+    def update(self, b):
+        dev = self.device
+        obs = torch.as_tensor(b["obs"]).to(dev)
+        nobs = torch.as_tensor(b["next_obs"]).to(dev)
+        a = torch.as_tensor(b["actions"]).long().to(dev)
+        r = torch.as_tensor(b["rewards"]).float().to(dev)
+        d = torch.as_tensor(b["terminateds"]).float().to(dev)
+        w = torch.as_tensor(b.get("weights", np.ones(len(r), np.float32))).to(dev)
+        q = self.q(obs).gather(-1, a[:, None])[:, 0]
+        with torch.no_grad():
+            if self.cfg.get("double_q", True):
+                na = self.q(nobs).argmax(-1)
+                nq = self.target(nobs).gather(-1, na[:, None])[:, 0]
+            else:
+                nq = self.target(nobs).max(-1).values
+            tgt = r + self.cfg.get("gamma", 0.99) * (1 - d) * nq
+        td = q - tgt
+        loss = (w * torch.nn.functional.huber_loss(q, tgt, reduction="none")).mean()
+        self.opt.zero_grad()
+        loss.backward()
+        if self.cfg.get("grad_clip"):
+            torch.nn.utils.clip_grad_norm_(self.q.parameters(), self.cfg["grad_clip"])
+        self.opt.step()
+        return float(loss), td.detach().abs().cpu().numpy()
+
+    def sync_target(self):
+        self.target.load_state_dict(self.q.state_dict())
+
+    def get_weights(self):
+        return {k: v.detach().cpu() for k, v in self.q.state_dict().items()}
+
+    def get_state(self):
+        return {"q": self.get_weights(), "opt": self.opt.state_dict()}
+
+    def set_state(self, s):
+        self.q.load_state_dict(s["q"])
+        self.target.load_state_dict(s["q"])
+        self.opt.load_state_dict(s["opt"])
+
+    def shutdown(self):
+        pass
+
+
+class DQN(Algorithm):
+    module_kind = "q"
+
+    @classmethod
+    def get_default_config(cls):
+        return DQNConfig()
+
+    def setup(self):
+        rb = self.config.replay_buffer_config
+        cap = rb.get("capacity", 50000)
+        self.prioritized = "Prioritized" in rb.get("type", "")
+        self.buffer = PrioritizedReplayBuffer(cap, rb.get("alpha", 0.6), self.config.seed) \
+            if self.prioritized else ReplayBuffer(cap, self.config.seed)
+        self.learner_group = _QLearner(self.cfg, self.observation_space, self.action_space)
+        self._last_target = 0
+        self._sync_weights(self.learner_group.get_weights())
+
+    def _epsilon(self):
+        sched = self.config.epsilon
+        t = self.total_env_steps
+        (t0, e0), (t1, e1) = sched[0], sched[-1]
+        if t >= t1:
+            return e1
+        return e0 + (e1 - e0) * (t - t0) / max(1, t1 - t0)
+
+    def training_step(self):
+        cfg = self.config
+        eps = self._epsilon()
+        if self.env_runners:
+            bs = ray.get([r.sample.remote(cfg.rollout_fragment_length, True, eps)
+                          for r in self.env_runners])
+        else:
+            bs = [self.local_runner.sample(cfg.rollout_fragment_length, True, eps)]
+        for b in bs:
+            T, B = b["rewards"].shape
+            flat = {k: b[k].reshape((T * B,) + b[k].shape[2:])
+                    for k in ("obs", "next_obs", "actions", "rewards", "terminateds")}
+            self.buffer.add(flat)
+            self.total_env_steps += T * B
+        stats = {"epsilon": eps}
+        if self.total_env_steps < cfg.num_steps_sampled_before_learning_starts:
+            return stats
+        n_updates = max(1, sum(b["env_steps"] for b in bs) // max(1, cfg.rollout_fragment_length))
+        for _ in range(n_updates):
+            kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} if self.prioritized else {}
+            mb = self.buffer.sample(cfg.train_batch_size, **kw)
+            loss, td = self.learner_group.update(mb)
+            if self.prioritized:
+                self.buffer.update_priorities(mb["batch_indexes"], td)
+            stats["loss"] = loss
+        if self.total_env_steps - self._last_target >= cfg.target_network_update_freq:
+            self.learner_group.sync_target()
+            self._last_target = self.total_env_steps
+        self._sync_weights(self.learner_group.get_weights())
+        return stats

@@ -1,0 +1,52 @@
+"""PPO (reference: rllib/algorithms/ppo/ppo.py, ppo_torch_learner.py)."""
+
+from __future__ import annotations
+
+from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.learner import LearnerGroup
+
+
+class PPOConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or PPO)
+        self.lr = 5e-5
+        self.rollout_fragment_length = "auto"
+        self.train_batch_size = 4000
+        self.minibatch_size = 128
+        self.num_epochs = 30
+        self.lambda_ = 1.0
+        self.use_gae = True
+        self.use_critic = True
+        self.use_kl_loss = True
+        self.kl_coeff = 0.2
+        self.kl_target = 0.01
+        self.vf_loss_coeff = 1.0
+        self.entropy_coeff = 0.0
+        self.clip_param = 0.3
+        self.vf_clip_param = 10.0
+        self.grad_clip = None
+
+
+class PPO(Algorithm):
+    kind = "ppo"
+
+    def __init__(self, config):
+        if config.rollout_fragment_length == "auto":
+            nr = max(1, config.num_env_runners) * config.num_envs_per_env_runner
+            config.rollout_fragment_length = max(1, config.train_batch_size // nr)
+        super().__init__(config)
+
+    @classmethod
+    def get_default_config(cls):
+        return PPOConfig()
+
+    def setup(self):
+        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space)
+        self._sync_weights(self.learner_group.get_weights())
+
+    def training_step(self) -> dict:
+        batches = self._sample(self.config.train_batch_size)
+        stats = self.learner_group.update("ppo", batches)
+        self._sync_weights(self.learner_group.get_weights())
+        return stats

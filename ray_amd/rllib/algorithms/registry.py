@@ -1,0 +1,24 @@
+"""Algorithm registry (reference: rllib/algorithms/registry.py)."""
+
+
+def _algos():
+    from ray_amd.rllib.algorithms.dqn import DQN, DQNConfig
+    from ray_amd.rllib.algorithms.impala import APPO, IMPALA, APPOConfig, IMPALAConfig
+    from ray_amd.rllib.algorithms.ppo import PPO, PPOConfig
+
+    return {"PPO": (PPO, PPOConfig), "IMPALA": (IMPALA, IMPALAConfig),
+            "APPO": (APPO, APPOConfig), "DQN": (DQN, DQNConfig)}
+
+
+def get_algorithm_class(name: str):
+    return _algos()[name][0]
+
+
+def get_config_class(cls):
+    for a, c in _algos().values():
+        if a is cls:
+            return c
+    raise KeyError(cls)
+
+
+ALGORITHMS = property(_algos)

@@ -1,0 +1,352 @@
+"""Learners and LearnerGroup (reference: rllib/core/learner/learner.py, learner_group.py,
+rllib/algorithms/ppo/torch/ppo_torch_learner.py, rllib/algorithms/impala/torch/
+impala_torch_learner.py, rllib/algorithms/appo/torch/appo_torch_learner.py).
+
+MI355X learner hot loop (one GPU per learner):
+  rollouts [T, B] → HBM (uint8 frames, pinned async H2D) → value forward (bf16
+  autocast, MFMA convs/GEMMs) → GAE or V-trace (HIP reverse-scan kernels) →
+  advantage standardisation → minibatch epochs: forward → fused PPO loss+grad
+  kernel (one pass computes loss, stats and d/dlogits, d/dV) → backward →
+  flat-buffer gradient all-reduce over RCCL (multi-learner) → fused AdamW kernel.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ray_amd.ops import functional as rf
+from ray_amd.rllib.core.rl_module import RLModule, gaussian_entropy, gaussian_logp
+
+
+def _to_t(x, device, dtype=None, non_blocking=True):
+    t = torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x
+    if device.type == "cuda" and not t.is_pinned() and t.device.type == "cpu":
+        t = t.pin_memory()
+    t = t.to(device, non_blocking=non_blocking)
+    return t if dtype is None else t.to(dtype)
+
+
+def concat_batches(batches):
+    """Concatenate runner fragments along the env (B) axis."""
+    out = {}
+    for k in batches[0]:
+        v = batches[0][k]
+        if isinstance(v, np.ndarray):
+            axis = 0 if k == "bootstrap_obs" else 1
+            out[k] = np.concatenate([b[k] for b in batches], axis=axis)
+        elif isinstance(v, (int, float)):
+            out[k] = sum(b[k] for b in batches)
+    return out
+
+
+class Learner:
+    def __init__(self, config: dict, observation_space, action_space, device=None, rank=0,
+                 world=1):
+        self.config = config
+        if device is None:
+            device = torch.device("cuda", int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))) \
+                if torch.cuda.is_available() and config.get("num_gpus_per_learner", 1) else \
+                torch.device("cpu")
+        self.device = device
+        self.rank, self.world = rank, world
+        torch.manual_seed(config.get("seed") or 0)
+        self.module = RLModule(observation_space, action_space, config.get("model")).to(device)
+        from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams
+
+        self.flat = FlatParams(self.module, dtype=torch.float32)
+        self.ddp = FlatDDP(self.flat, bucket_mb=32.0)
+        self.opt = FlatAdamW(self.flat, lr=config.get("lr", 5e-5), betas=(0.9, 0.999), eps=1e-7,
+                             weight_decay=0.0, max_grad_norm=config.get("grad_clip"),
+                             grad_scale=self.ddp.grad_scale)
+        self.kl_coeff = config.get("kl_coeff", 0.2)
+        self.amp = device.type == "cuda" and config.get("learner_bf16", True)
+        self.updates = 0
+
+    # ---------------------------------------------------------------- weights
+    def get_weights(self):
+        return {k: v.detach().float().cpu() for k, v in self.module.state_dict().items()}
+
+    def set_weights(self, w):
+        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+        self.flat.sync_master_from_params()
+
+    def get_state(self):
+        return {"weights": self.get_weights(), "opt": {k: v.cpu() if torch.is_tensor(v) else v
+                                                       for k, v in self.opt.state_dict().items()},
+                "kl_coeff": self.kl_coeff}
+
+    def set_state(self, s):
+        self.set_weights(s["weights"])
+        self.opt.load_state_dict({k: v.to(self.device) if torch.is_tensor(v) else v
+                                  for k, v in s["opt"].items()})
+        self.kl_coeff = s.get("kl_coeff", self.kl_coeff)
+
+    # ---------------------------------------------------------------- helpers
+    def _fwd(self, obs):
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
+            return self.module.forward_train(obs)
+
+    def _values(self, obs_flat, chunk=8192):
+        out = []
+        with torch.no_grad():
+            for i in range(0, obs_flat.shape[0], chunk):
+                with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
+                    out.append(self.module.value(obs_flat[i:i + chunk]).float())
+        return torch.cat(out)
+
+    def _step(self, loss):
+        self.flat.zero_grad()
+        loss.backward()
+        self.ddp.finish()
+        self.opt.step()
+
+    # ---------------------------------------------------------------- PPO
+    def update_ppo(self, batch: dict) -> dict:
+        c = self.config
+        dev = self.device
+        obs = _to_t(batch["obs"], dev)
+        T, B = obs.shape[:2]
+        rewards = _to_t(batch["rewards"], dev)
+        dones = _to_t(batch["terminateds"], dev)
+        acts = _to_t(batch["actions"], dev)
+        old_logp = _to_t(batch["action_logp"], dev)
+        old_di = _to_t(batch["action_dist_inputs"], dev)
+        boot_obs = _to_t(batch["bootstrap_obs"], dev)
+        obs_flat = obs.reshape((T * B,) + tuple(obs.shape[2:]))
+        vals = self._values(obs_flat).view(T, B)
+        boot_v = self._values(boot_obs)
+        adv, vtarg = rf.gae(rewards, vals, dones, boot_v, c.get("gamma", 0.99),
+                            c.get("lambda_", 0.95))
+        adv = adv.reshape(-1)
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        vtarg = vtarg.reshape(-1)
+        acts = acts.reshape((T * B,) + tuple(acts.shape[2:]))
+        old_logp = old_logp.reshape(-1)
+        old_di = old_di.reshape(T * B, -1)
+        N = T * B
+        mb = min(int(c.get("minibatch_size", 128)), N)
+        stats_acc = torch.zeros(6, device=dev)
+        n_mb = 0
+        for _ in range(int(c.get("num_epochs", 1))):
+            perm = torch.randperm(N, device=dev)
+            for s in range(0, N - mb + 1, mb):
+                idx = perm[s:s + mb]
+                out = self._fwd(obs_flat[idx])
+                loss, st = self._ppo_loss(out, old_di[idx], acts[idx], old_logp[idx], adv[idx],
+                                          vtarg[idx])
+                self._step(loss)
+                stats_acc += st.detach()
+                n_mb += 1
+        stats = (stats_acc / max(1, n_mb)).tolist()
+        kl = stats[4]
+        if c.get("use_kl_loss", True) and c.get("kl_target"):
+            if kl > 2.0 * c["kl_target"]:
+                self.kl_coeff *= 1.5
+            elif kl < 0.5 * c["kl_target"]:
+                self.kl_coeff *= 0.5
+        self.updates += 1
+        return {"total_loss": stats[0], "policy_loss": stats[1], "vf_loss": stats[2],
+                "entropy": stats[3], "mean_kl_loss": kl, "clip_frac": stats[5],
+                "curr_kl_coeff": self.kl_coeff, "num_minibatches": n_mb,
+                "vf_explained_var": _explained_var(vtarg, vals.reshape(-1))}
+
+    def _ppo_loss(self, out, old_di, acts, old_logp, adv, vtarg):
+        c = self.config
+        kl_c = self.kl_coeff if c.get("use_kl_loss", True) else 0.0
+        logits = out["action_dist_inputs"].float()
+        v = out["vf_preds"].float()
+        if self.module.discrete:
+            return rf.ppo_loss(logits, old_di, acts, old_logp, adv, v, vtarg,
+                               clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),
+                               vf_coeff=c.get("vf_loss_coeff", 1.0),
+                               ent_coeff=c.get("entropy_coeff", 0.0), kl_coeff=kl_c)
+        # DiagGaussian (continuous) path
+        mean, log_std = logits.chunk(2, -1)
+        logp = gaussian_logp(acts, mean, log_std)
+        ratio = torch.exp(logp - old_logp)
+        clip = c.get("clip_param", 0.3)
+        surr = torch.minimum(adv * ratio, adv * ratio.clamp(1 - clip, 1 + clip))
+        om, ols = old_di.float().chunk(2, -1)
+        ols = ols.clamp(-20, 2)
+        ls = log_std.clamp(-20, 2)
+        kl = (ls - ols + (ols.exp() ** 2 + (om - mean) ** 2) / (2 * ls.exp() ** 2) - 0.5).sum(-1)
+        ent = gaussian_entropy(log_std)
+        vf = ((v - vtarg) ** 2).clamp(0, c.get("vf_clip_param", 10.0))
+        total = (-surr + c.get("vf_loss_coeff", 1.0) * vf - c.get("entropy_coeff", 0.0) * ent
+                 + kl_c * kl).mean()
+        cf = ((ratio < 1 - clip) | (ratio > 1 + clip)).float().mean()
+        st = torch.stack([total.detach(), -surr.mean().detach(), vf.mean().detach(),
+                          ent.mean().detach(), kl.mean().detach(), cf])
+        return total, st
+
+    # ---------------------------------------------------------------- IMPALA / APPO
+    def update_vtrace(self, batch: dict) -> dict:
+        c = self.config
+        dev = self.device
+        obs = _to_t(batch["obs"], dev)
+        T, B = obs.shape[:2]
+        rewards = _to_t(batch["rewards"], dev)
+        dones = _to_t(batch["terminateds"], dev)
+        acts = _to_t(batch["actions"], dev)
+        beh_logp = _to_t(batch["action_logp"], dev)
+        boot_obs = _to_t(batch["bootstrap_obs"], dev)
+        obs_flat = obs.reshape((T * B,) + tuple(obs.shape[2:]))
+        out = self._fwd(obs_flat)
+        logits = out["action_dist_inputs"].float()
+        v = out["vf_preds"].float().view(T, B)
+        with torch.no_grad():
+            boot_v = self._values(boot_obs)
+        lp_all = torch.log_softmax(logits, -1)
+        tgt_logp = lp_all.gather(-1, acts.reshape(-1, 1)).view(T, B)
+        disc = c.get("gamma", 0.99) * (1.0 - dones)
+        with torch.no_grad():
+            vs, pg_adv = rf.vtrace(tgt_logp.detach() - beh_logp, disc, rewards, v.detach(), boot_v,
+                                   c.get("vtrace_clip_rho_threshold", 1.0), 1.0,
+                                   c.get("vtrace_clip_pg_rho_threshold", 1.0))
+        if c.get("appo", False):
+            ratio = torch.exp(tgt_logp - beh_logp)
+            clip = c.get("clip_param", 0.4)
+            pg = -torch.minimum(pg_adv * ratio, pg_adv * ratio.clamp(1 - clip, 1 + clip)).mean()
+        else:
+            pg = -(tgt_logp * pg_adv).mean()
+        vf = 0.5 * ((vs - v) ** 2).mean()
+        ent = -(lp_all.exp() * lp_all).sum(-1).mean()
+        loss = pg + c.get("vf_loss_coeff", 0.5) * vf - c.get("entropy_coeff", 0.01) * ent
+        self._step(loss)
+        self.updates += 1
+        return {"total_loss": float(loss), "pi_loss": float(pg), "vf_loss": float(vf),
+                "entropy": float(ent)}
+
+
+def _explained_var(y, pred):
+    vy = torch.var(y)
+    return float(1 - torch.var(y - pred) / (vy + 1e-8))
+
+
+class LearnerActor:
+    """One learner process per GPU; a LearnerGroup of these all-reduces gradients on RCCL."""
+
+    def __init__(self, config, observation_space, action_space, rank, world):
+        self.config = config
+        self.args = (observation_space, action_space, rank, world)
+        self.learner = None
+
+    def setup(self):
+        obs_space, act_space, rank, world = self.args
+        self.learner = Learner(self.config, obs_space, act_space, rank=rank, world=world)
+        return True
+
+    def update(self, kind, batches):
+        b = concat_batches(batches) if isinstance(batches, list) else batches
+        return self.learner.update_ppo(b) if kind == "ppo" else self.learner.update_vtrace(b)
+
+    def get_weights(self):
+        return self.learner.get_weights()
+
+    def set_weights(self, w):
+        self.learner.set_weights(w)
+
+    def get_state(self):
+        return self.learner.get_state()
+
+    def set_state(self, s):
+        self.learner.set_state(s)
+
+
+class LearnerGroup:
+    def __init__(self, config: dict, observation_space, action_space):
+        self.config = config
+        n = int(config.get("num_learners", 0))
+        self.remote = n > 0
+        if not self.remote:
+            self.local = Learner(config, observation_space, action_space)
+            self.actors = []
+            return
+        import ray_amd as ray
+        from ray_amd.train._internal.worker_group import WorkerGroup
+        from ray_amd.train.torch.config import TorchConfig, _TorchBackend
+
+        ngpu = config.get("num_gpus_per_learner", 1)
+        res = {"CPU": 1}
+        if ngpu:
+            res["GPU"] = ngpu
+
+        class _LW(LearnerActor):
+            pass
+
+        self.wg = WorkerGroup(n, res)
+        _TorchBackend().on_start(self.wg, TorchConfig())
+        self.actors = self.wg.workers
+        ray.get([a.execute.remote(_make_learner, config, observation_space, action_space, i, n)
+                 for i, a in enumerate(self.actors)])
+        self.local = None
+
+    def update(self, kind, batches):
+        if not self.remote:
+            b = concat_batches(batches) if isinstance(batches, list) else batches
+            return self.local.update_ppo(b) if kind == "ppo" else self.local.update_vtrace(b)
+        import ray_amd as ray
+
+        n = len(self.actors)
+        shards = [batches[i::n] for i in range(n)] if len(batches) >= n else \
+            [_split_b(concat_batches(batches), n, i) for i in range(n)]
+        res = ray.get([a.execute.remote(_learner_update, kind, s)
+                       for a, s in zip(self.actors, shards)])
+        return res[0]
+
+    def get_weights(self):
+        if not self.remote:
+            return self.local.get_weights()
+        import ray_amd as ray
+
+        return ray.get(self.actors[0].execute.remote(_learner_call, "get_weights"))
+
+    def get_state(self):
+        if not self.remote:
+            return self.local.get_state()
+        import ray_amd as ray
+
+        return ray.get(self.actors[0].execute.remote(_learner_call, "get_state"))
+
+    def set_state(self, s):
+        if not self.remote:
+            return self.local.set_state(s)
+        import ray_amd as ray
+
+        ray.get([a.execute.remote(_learner_call, "set_state", s) for a in self.actors])
+
+    def shutdown(self):
+        if self.remote:
+            self.wg.shutdown()
+
+
+_LEARNER = None
+
+
+def _make_learner(config, obs_space, act_space, rank, world):
+    global _LEARNER
+    _LEARNER = Learner(config, obs_space, act_space, rank=rank, world=world)
+    return True
+
+
+def _learner_update(kind, batches):
+    b = concat_batches(batches) if isinstance(batches, list) else batches
+    return _LEARNER.update_ppo(b) if kind == "ppo" else _LEARNER.update_vtrace(b)
+
+
+def _learner_call(name, *a):
+    return getattr(_LEARNER, name)(*a)
+
+
+def _split_b(batch, n, i):
+    out = {}
+    for k, v in batch.items():
+        if isinstance(v, np.ndarray):
+            axis = 0 if k == "bootstrap_obs" else 1
+            out[k] = np.array_split(v, n, axis=axis)[i]
+        else:
+            out[k] = v
+    return out

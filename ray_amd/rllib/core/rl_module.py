@@ -1,0 +1,191 @@
+"""RLModule + model catalog (reference: rllib/core/rl_module/rl_module.py,
+rllib/core/models/catalog.py, rllib/algorithms/ppo/ppo_catalog.py,
+rllib/models/torch/torch_action_dist.py).
+
+Encoders: MLP for vector observations, Nature-CNN (Mnih et al. 2015) for image
+observations ([H, W, C] uint8 frames; the /255 scaling is fused into the uint8
+→ bf16 HIP cast kernel on GPU). Heads: policy logits (Categorical) or
+mean/log-std (DiagGaussian) and a value head.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ray_amd.rllib.env import spaces
+
+
+def _act(name):
+    return {"relu": nn.ReLU, "tanh": nn.Tanh, "swish": nn.SiLU, "silu": nn.SiLU,
+            "elu": nn.ELU}.get(name or "tanh", nn.Tanh)
+
+
+class MLP(nn.Module):
+    def __init__(self, in_dim, hiddens, activation="tanh"):
+        super().__init__()
+        layers = []
+        d = in_dim
+        for h in hiddens:
+            layers += [nn.Linear(d, h), _act(activation)()]
+            d = h
+        self.net = nn.Sequential(*layers)
+        self.out_dim = d
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class NatureCNN(nn.Module):
+    """Conv(32,8,4) → Conv(64,4,2) → Conv(64,3,1) → FC(512), RLlib's default Atari stack."""
+
+    def __init__(self, obs_shape, out_dim=512):
+        super().__init__()
+        H, W, C = obs_shape
+        self.convs = nn.Sequential(
+            nn.Conv2d(C, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+            nn.Conv2d(64, 64, 3, 1), nn.ReLU())
+        with torch.no_grad():
+            n = self.convs(torch.zeros(1, C, H, W)).numel()
+        self.fc = nn.Sequential(nn.Linear(n, out_dim), nn.ReLU())
+        self.out_dim = out_dim
+
+    def forward(self, x):
+        # x: [B, H, W, C] uint8 or float
+        if x.dtype == torch.uint8:
+            if x.is_cuda:
+                from ray_amd.ops.functional import cast_scale_u8
+
+                x = cast_scale_u8(x).to(self.fc[0].weight.dtype)
+            else:
+                x = x.float().mul_(1.0 / 255.0)
+        x = x.permute(0, 3, 1, 2)
+        return self.fc(self.convs(x).flatten(1))
+
+
+class RLModule(nn.Module):
+    """Actor-critic module used by PPO / IMPALA / APPO."""
+
+    framework = "torch"
+
+    def __init__(self, observation_space, action_space, model_config: dict | None = None):
+        super().__init__()
+        cfg = dict(model_config or {})
+        self.observation_space = observation_space
+        self.action_space = action_space
+        self.model_config = cfg
+        obs_shape = tuple(observation_space.shape)
+        self.is_image = len(obs_shape) == 3
+        hiddens = cfg.get("fcnet_hiddens", [256, 256])
+        act = cfg.get("fcnet_activation", "tanh")
+        self.discrete = isinstance(action_space, spaces.Discrete)
+        if self.discrete:
+            self.n_out = action_space.n
+        else:
+            self.act_dim = int(np.prod(action_space.shape))
+            self.n_out = 2 * self.act_dim
+        self.vf_share = cfg.get("vf_share_layers", self.is_image)
+        if self.is_image:
+            self.encoder = NatureCNN(obs_shape)
+            self.vf_encoder = None if self.vf_share else NatureCNN(obs_shape)
+        else:
+            d = int(np.prod(obs_shape))
+            self.encoder = MLP(d, hiddens, act)
+            self.vf_encoder = None if self.vf_share else MLP(d, hiddens, act)
+        self.pi = nn.Linear(self.encoder.out_dim, self.n_out)
+        self.vf = nn.Linear(self.encoder.out_dim, 1)
+        nn.init.orthogonal_(self.pi.weight, 0.01)
+        nn.init.zeros_(self.pi.bias)
+        nn.init.orthogonal_(self.vf.weight, 1.0)
+        nn.init.zeros_(self.vf.bias)
+
+    def _flat(self, obs):
+        if self.is_image:
+            return obs
+        return obs.reshape(obs.shape[0], -1).float()
+
+    def forward_train(self, obs):
+        x = self._flat(obs)
+        h = self.encoder(x)
+        logits = self.pi(h)
+        hv = h if self.vf_encoder is None else self.vf_encoder(x)
+        v = self.vf(hv).squeeze(-1)
+        return {"action_dist_inputs": logits, "vf_preds": v}
+
+    def forward_inference(self, obs):
+        return {"action_dist_inputs": self.pi(self.encoder(self._flat(obs)))}
+
+    def forward_exploration(self, obs):
+        return self.forward_train(obs)
+
+    def value(self, obs):
+        x = self._flat(obs)
+        hv = self.encoder(x) if self.vf_encoder is None else self.vf_encoder(x)
+        return self.vf(hv).squeeze(-1)
+
+    # ---------------------------------------------------------------- distributions
+    def sample_actions(self, dist_inputs, explore=True):
+        """Returns (actions, logp)."""
+        if self.discrete:
+            logits = dist_inputs.float()
+            if explore:
+                a = torch.distributions.Categorical(logits=logits).sample()
+            else:
+                a = logits.argmax(-1)
+            logp = torch.log_softmax(logits, -1).gather(-1, a[:, None])[:, 0]
+            return a, logp
+        mean, log_std = dist_inputs.float().chunk(2, -1)
+        std = log_std.clamp(-20, 2).exp()
+        a = mean + std * torch.randn_like(mean) if explore else mean
+        logp = gaussian_logp(a, mean, log_std)
+        return a, logp
+
+    def get_state(self):
+        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+
+    def set_state(self, state):
+        self.load_state_dict(state)
+
+
+def gaussian_logp(a, mean, log_std):
+    log_std = log_std.clamp(-20, 2)
+    return (-0.5 * ((a - mean) / log_std.exp()) ** 2 - log_std -
+            0.5 * math.log(2 * math.pi)).sum(-1)
+
+
+def gaussian_entropy(log_std):
+    return (log_std.clamp(-20, 2) + 0.5 * math.log(2 * math.pi * math.e)).sum(-1)
+
+
+class QModule(nn.Module):
+    """Q-network (optionally dueling) for DQN (reference: rllib/algorithms/dqn)."""
+
+    def __init__(self, observation_space, action_space, model_config=None):
+        super().__init__()
+        cfg = dict(model_config or {})
+        obs_shape = tuple(observation_space.shape)
+        self.is_image = len(obs_shape) == 3
+        self.dueling = cfg.get("dueling", True)
+        if self.is_image:
+            self.encoder = NatureCNN(obs_shape)
+        else:
+            self.encoder = MLP(int(np.prod(obs_shape)), cfg.get("fcnet_hiddens", [256, 256]),
+                               cfg.get("fcnet_activation", "relu"))
+        n = action_space.n
+        self.adv = nn.Linear(self.encoder.out_dim, n)
+        self.val = nn.Linear(self.encoder.out_dim, 1) if self.dueling else None
+
+    def forward(self, obs):
+        x = obs if self.is_image else obs.reshape(obs.shape[0], -1).float()
+        h = self.encoder(x)
+        a = self.adv(h)
+        if self.val is None:
+            return a
+        return self.val(h) + a - a.mean(-1, keepdim=True)
+
+
+F  # noqa: B018

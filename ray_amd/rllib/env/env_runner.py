@@ -1,0 +1,163 @@
+"""Single-agent EnvRunner (reference: rllib/env/single_agent_env_runner.py,
+rllib/evaluation/rollout_worker.py).
+
+Each runner steps ``num_envs_per_env_runner`` envs in lock-step (vectorised)
+and returns time-major [T, B] fragments as numpy arrays; the fragment travels
+to the learner through the shared-memory object store (zero-copy), where GAE /
+V-trace run as HIP kernels. Episodes auto-reset; ``terminateds`` marks episode
+ends (truncation is folded into termination: no bootstrap across a time-limit
+cut)."""
+
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from ray_amd.rllib.env.envs import make_env
+
+
+class SingleAgentEnvRunner:
+    def __init__(self, config: dict, worker_index: int = 0):
+        torch.set_num_threads(int(config.get("num_cpus_per_env_runner", 1) or 1))
+        self.config = config
+        self.worker_index = worker_index
+        n = int(config.get("num_envs_per_env_runner", 1))
+        seed = config.get("seed")
+        self.envs = []
+        for i in range(n):
+            ec = dict(config.get("env_config") or {})
+            ec.setdefault("seed", (seed or 0) * 1000 + worker_index * 100 + i)
+            self.envs.append(make_env(config["env"], ec))
+        self.observation_space = self.envs[0].observation_space
+        self.action_space = self.envs[0].action_space
+        from ray_amd.rllib.core.rl_module import RLModule
+
+        self.module_kind = config.get("module_kind", "actor_critic")
+        if self.module_kind == "q":
+            from ray_amd.rllib.core.rl_module import QModule
+
+            mc = dict(config.get("model") or {})
+            mc["dueling"] = config.get("dueling", True)
+            self.module = QModule(self.observation_space, self.action_space, mc)
+        else:
+            self.module = RLModule(self.observation_space, self.action_space, config.get("model"))
+        self.module.eval()
+        self.device = torch.device("cpu")
+        if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
+            self.device = torch.device("cuda", 0)
+            self.module.to(self.device)
+        self.obs = []
+        for i, e in enumerate(self.envs):
+            o, _ = e.reset(seed=None if seed is None else seed * 1000 + worker_index * 100 + i)
+            self.obs.append(o)
+        self.ep_ret = np.zeros(n)
+        self.ep_len = np.zeros(n, dtype=np.int64)
+        self.done_returns = []
+        self.done_lengths = []
+        self.weights_version = -1
+        self.total_steps = 0
+        self.epsilon = 1.0
+
+    # ---------------------------------------------------------------- weights
+    def set_weights(self, weights, version: int = 0):
+        if version is not None and version == self.weights_version:
+            return
+        sd = {k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(v))
+              for k, v in weights.items()}
+        self.module.load_state_dict(sd)
+        self.weights_version = version
+
+    def get_weights(self):
+        return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
+
+    def ping(self):
+        return self.worker_index
+
+    # ---------------------------------------------------------------- sampling
+    def sample(self, num_timesteps: int | None = None, explore: bool = True,
+               epsilon: float | None = None):
+        T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
+        B = len(self.envs)
+        osh = self.observation_space.shape
+        obs_buf = np.empty((T, B) + tuple(osh), dtype=self.observation_space.dtype)
+        discrete = hasattr(self.action_space, "n")
+        act_buf = np.empty((T, B) if discrete else (T, B) + tuple(self.action_space.shape),
+                           dtype=np.int64 if discrete else np.float32)
+        rew = np.zeros((T, B), np.float32)
+        term = np.zeros((T, B), np.float32)
+        trunc = np.zeros((T, B), np.float32)
+        logp = np.zeros((T, B), np.float32)
+        dist_in = None
+        next_obs_buf = None
+        if self.module_kind == "q":
+            next_obs_buf = np.empty_like(obs_buf)
+        t0 = time.perf_counter()
+        for t in range(T):
+            ob = np.stack(self.obs)
+            obs_buf[t] = ob
+            with torch.no_grad():
+                x = torch.from_numpy(ob).to(self.device)
+                if self.module_kind == "q":
+                    q = self.module(x)
+                    a = q.argmax(-1).cpu().numpy()
+                    eps = self.epsilon if epsilon is None else epsilon
+                    if explore:
+                        rnd = np.random.random(B) < eps
+                        a = np.where(rnd, np.random.randint(0, self.action_space.n, B), a)
+                    lp = np.zeros(B, np.float32)
+                else:
+                    out = self.module.forward_inference(x)
+                    di = out["action_dist_inputs"]
+                    at, lpt = self.module.sample_actions(di, explore)
+                    a = at.cpu().numpy()
+                    lp = lpt.cpu().numpy()
+                    if dist_in is None:
+                        dist_in = np.zeros((T, B, di.shape[-1]), np.float32)
+                    dist_in[t] = di.float().cpu().numpy()
+            act_buf[t] = a
+            logp[t] = lp
+            for i, env in enumerate(self.envs):
+                ai = a[i]
+                if not discrete:
+                    ai = np.clip(ai, self.action_space.low, self.action_space.high)
+                o, r, te, tr, _ = env.step(ai if not discrete else int(ai))
+                rew[t, i] = r
+                self.ep_ret[i] += r
+                self.ep_len[i] += 1
+                if next_obs_buf is not None:
+                    next_obs_buf[t, i] = o
+                if te or tr:
+                    term[t, i] = 1.0 if (te or not self.config.get("bootstrap_truncated")) \
+                        else 0.0
+                    trunc[t, i] = float(tr)
+                    self.done_returns.append(float(self.ep_ret[i]))
+                    self.done_lengths.append(int(self.ep_len[i]))
+                    self.ep_ret[i] = 0.0
+                    self.ep_len[i] = 0
+                    o, _ = env.reset()
+                self.obs[i] = o
+        self.total_steps += T * B
+        batch = {"obs": obs_buf, "actions": act_buf, "rewards": rew, "terminateds": term,
+                 "truncateds": trunc, "action_logp": logp,
+                 "bootstrap_obs": np.stack(self.obs), "env_steps": T * B,
+                 "sample_time_s": time.perf_counter() - t0,
+                 "weights_version": self.weights_version}
+        if dist_in is not None:
+            batch["action_dist_inputs"] = dist_in
+        if next_obs_buf is not None:
+            batch["next_obs"] = next_obs_buf
+        return batch
+
+    def get_metrics(self):
+        r, ln = self.done_returns, self.done_lengths
+        self.done_returns, self.done_lengths = [], []
+        return {"episode_returns": r, "episode_lengths": ln, "num_env_steps": self.total_steps}
+
+    def set_epsilon(self, eps):
+        self.epsilon = eps
+
+    def stop(self):
+        for e in self.envs:
+            e.close()
