@@ -1,0 +1,30 @@
+"""ray_amd.data — streaming distributed datasets (reference: python/ray/data)."""
+
+from ray_amd.data.dataset import (ActorPoolStrategy, AggregateFn, Count, Dataset,  # noqa: F401
+                                  GroupedData, Max, MaterializedDataset, Mean, Min, Std, Sum,
+                                  TaskPoolStrategy)
+from ray_amd.data.iterator import DataIterator  # noqa: F401
+from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface,  # noqa: F401
+                                   from_items, from_numpy, from_numpy_refs, from_pandas,
+                                   from_pandas_refs, from_torch, range, range_tensor,
+                                   read_binary_files, read_csv, read_datasource, read_images,
+                                   read_json, read_numpy, read_parquet, read_text)
+from ray_amd.data import preprocessors  # noqa: F401
+
+
+class DataContext:
+    _current = None
+
+    def __init__(self):
+        self.target_max_block_size = 128 << 20
+        self.execution_options = None
+        self.use_push_based_shuffle = False
+
+    @classmethod
+    def get_current(cls):
+        if cls._current is None:
+            cls._current = DataContext()
+        return cls._current
+
+
+DatasetContext = DataContext

@@ -1,0 +1,176 @@
+"""Blocks (reference: python/ray/data/block.py, _internal/{arrow,pandas,table}_block.py).
+
+Canonical block = ``dict[str, np.ndarray]`` (columnar, equal length). Columnar
+numpy is what the shared-memory object store moves zero-copy (pickle-5
+out-of-band buffers) and what tensor columns need (images, token ids), so it is
+also the cheapest form to hand to a HIP preprocessing kernel or a pinned H2D copy.
+Arrow / pandas views are produced on demand (``to_batch``)."""
+
+from __future__ import annotations
+
+import numpy as np
+
+Block = dict
+
+
+def num_rows(b: Block) -> int:
+    for v in b.values():
+        return len(v)
+    return 0
+
+
+def _col(values):
+    if isinstance(values, np.ndarray):
+        return values
+    try:
+        arr = np.asarray(values)
+        if arr.dtype == object and len(values) and isinstance(values[0], np.ndarray):
+            try:
+                return np.stack(values)
+            except ValueError:
+                return arr
+        return arr
+    except (ValueError, TypeError):
+        out = np.empty(len(values), dtype=object)
+        for i, v in enumerate(values):
+            out[i] = v
+        return out
+
+
+def from_rows(rows: list) -> Block:
+    if not rows:
+        return {}
+    if not isinstance(rows[0], dict):
+        rows = [{"item": r} for r in rows]
+    keys = list(rows[0].keys())
+    return {k: _col([r[k] for r in rows]) for k in keys}
+
+
+def to_rows(b: Block):
+    keys = list(b.keys())
+    n = num_rows(b)
+    cols = [b[k] for k in keys]
+    for i in range(n):
+        yield {k: _py(c[i]) for k, c in zip(keys, cols)}
+
+
+def _py(v):
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def slice_block(b: Block, start: int, end: int) -> Block:
+    return {k: v[start:end] for k, v in b.items()}
+
+
+def take_idx(b: Block, idx) -> Block:
+    return {k: v[idx] for k, v in b.items()}
+
+
+def concat(blocks: list) -> Block:
+    blocks = [b for b in blocks if b and num_rows(b) > 0]
+    if not blocks:
+        return {}
+    if len(blocks) == 1:
+        return blocks[0]
+    keys = list(blocks[0].keys())
+    out = {}
+    for k in keys:
+        parts = [b[k] for b in blocks]
+        try:
+            out[k] = np.concatenate(parts)
+        except ValueError:
+            o = np.empty(sum(len(p) for p in parts), dtype=object)
+            i = 0
+            for p in parts:
+                for v in p:
+                    o[i] = v
+                    i += 1
+            out[k] = o
+    return out
+
+
+def size_bytes(b: Block) -> int:
+    n = 0
+    for v in b.values():
+        n += v.nbytes if v.dtype != object else 64 * len(v)
+    return n
+
+
+def from_batch(batch) -> Block:
+    """Normalise a UDF output (dict of arrays/lists, pandas, arrow) to a block."""
+    if batch is None:
+        return {}
+    if isinstance(batch, dict):
+        return {k: _col(v) for k, v in batch.items()}
+    try:
+        import pandas as pd
+
+        if isinstance(batch, pd.DataFrame):
+            out = {}
+            for c in batch.columns:
+                col = batch[c]
+                v = col.to_numpy()
+                if v.dtype == object and len(v) and isinstance(v[0], np.ndarray):
+                    try:
+                        v = np.stack(v)
+                    except ValueError:
+                        pass
+                out[str(c)] = v
+            return out
+    except ImportError:
+        pass
+    try:
+        import pyarrow as pa
+
+        if isinstance(batch, pa.Table):
+            return {c: _arrow_col_to_numpy(batch.column(c)) for c in batch.column_names}
+    except ImportError:
+        pass
+    if isinstance(batch, list):
+        return from_rows(batch)
+    raise TypeError(f"cannot convert {type(batch)} to a block")
+
+
+def _arrow_col_to_numpy(col):
+    try:
+        return col.to_numpy()
+    except Exception:
+        v = col.to_pylist()
+        return _col(v)
+
+
+def to_batch(b: Block, batch_format: str = "numpy"):
+    if batch_format in ("numpy", "default", None):
+        return b
+    if batch_format == "pandas":
+        import pandas as pd
+
+        return pd.DataFrame({k: (list(v) if v.ndim > 1 else v) for k, v in b.items()})
+    if batch_format == "pyarrow":
+        import pyarrow as pa
+
+        cols = {}
+        for k, v in b.items():
+            cols[k] = pa.array(list(v)) if v.ndim > 1 or v.dtype == object else pa.array(v)
+        return pa.table(cols)
+    raise ValueError(f"unknown batch_format {batch_format}")
+
+
+def schema_of(b: Block) -> dict:
+    return {k: (v.dtype, v.shape[1:]) for k, v in b.items()}
+
+
+class Schema:
+    def __init__(self, s: dict):
+        self._s = s
+        self.names = list(s.keys())
+        self.types = [str(t) + (str(list(sh)) if sh else "") for t, sh in s.values()]
+
+    def __repr__(self):
+        inner = ", ".join(f"{n}: {t}" for n, t in zip(self.names, self.types))
+        return f"Column names & types: {{{inner}}}"
+
+    def __eq__(self, o):
+        return isinstance(o, Schema) and o.names == self.names and o.types == self.types

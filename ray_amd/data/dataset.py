@@ -1,0 +1,800 @@
+"""Dataset (reference: python/ray/data/dataset.py, grouped_data.py, iterator.py).
+
+Lazy: transformations append stages to a Plan; consumption (iter_*, take, count,
+write_*, materialize) runs the streaming executor. All-to-all operations
+(repartition, random_shuffle, sort, groupby, union, zip, split) are map/reduce
+task graphs over the materialised upstream blocks.
+"""
+
+from __future__ import annotations
+
+import builtins
+import itertools
+import math
+import os
+import time
+
+import numpy as np
+
+import ray_amd as ray
+
+from . import _executor as X
+from . import block as B
+
+
+class ActorPoolStrategy:
+    def __init__(self, size: int | None = None, min_size: int | None = None,
+                 max_size: int | None = None, max_tasks_in_flight_per_actor: int = 2):
+        if size is not None:
+            min_size = max_size = size
+        self.min_size = min_size or 1
+        self.max_size = max_size or self.min_size
+        self.max_tasks_in_flight_per_actor = max_tasks_in_flight_per_actor
+
+
+class TaskPoolStrategy:
+    def __init__(self, size: int | None = None):
+        self.size = size
+
+
+# --------------------------------------------------------------------------- UDF adapters
+def _batcher(fn, batch_size, batch_format, fn_args, fn_kwargs, zero_copy=False):
+    def run(blk):
+        n = B.num_rows(blk)
+        if n == 0:
+            return blk
+        bs = n if batch_size in (None, "default") else int(batch_size)
+        outs = []
+        for s in range(0, n, bs):
+            part = B.slice_block(blk, s, s + bs)
+            if not zero_copy:
+                part = {k: (np.array(v) if not v.flags.writeable else v) for k, v in part.items()}
+            r = fn(B.to_batch(part, batch_format), *fn_args, **fn_kwargs)
+            if hasattr(r, "__next__") and not isinstance(r, dict):
+                for x in r:
+                    outs.append(B.from_batch(x))
+            else:
+                outs.append(B.from_batch(r))
+        return B.concat(outs)
+
+    return run
+
+
+def _row_map(fn):
+    def run(blk):
+        return B.from_rows([fn(r) for r in B.to_rows(blk)])
+
+    return run
+
+
+def _row_flat_map(fn):
+    def run(blk):
+        rows = []
+        for r in B.to_rows(blk):
+            rows.extend(fn(r))
+        return B.from_rows(rows)
+
+    return run
+
+
+def _row_filter(fn):
+    def run(blk):
+        n = B.num_rows(blk)
+        if n == 0:
+            return blk
+        keep = np.fromiter((bool(fn(r)) for r in B.to_rows(blk)), dtype=bool, count=n)
+        return B.take_idx(blk, np.nonzero(keep)[0])
+
+    return run
+
+
+def _make_callable_class(cls, batch_size, batch_format, ctor_args, ctor_kwargs, fn_args,
+                         fn_kwargs, zero_copy):
+    def make():
+        inst = cls(*ctor_args, **ctor_kwargs)
+        return _batcher(inst, batch_size, batch_format, fn_args, fn_kwargs, zero_copy)
+
+    return make
+
+
+# --------------------------------------------------------------------------- remote helpers
+@ray.remote
+def _agg_block(blk, cols, ops):
+    out = {}
+    for c in cols:
+        v = blk.get(c)
+        if v is None or len(v) == 0:
+            out[c] = None
+            continue
+        v = v.astype(np.float64) if v.dtype != object else np.asarray(v, dtype=np.float64)
+        out[c] = {"n": len(v), "sum": float(v.sum()), "sumsq": float((v * v).sum()),
+                  "min": float(v.min()), "max": float(v.max())}
+    return out
+
+
+@ray.remote
+def _partition_block(blk, n, mode, key, boundaries, seed, descending):
+    rows = B.num_rows(blk)
+    if n == 1:
+        return blk
+    if rows == 0:
+        return tuple([blk] * n)
+    if mode == "random":
+        rng = np.random.default_rng(seed)
+        assign = rng.integers(0, n, size=rows)
+    elif mode == "hash":
+        col = blk[key]
+        assign = np.array([hash(x.item() if isinstance(x, np.generic) else
+                                (tuple(x) if isinstance(x, np.ndarray) else x)) % n
+                           for x in col], dtype=np.int64)
+    elif mode == "range":
+        assign = np.searchsorted(np.asarray(boundaries), blk[key], side="right")
+        if descending:
+            assign = (n - 1) - assign
+    else:  # contiguous split
+        assign = np.minimum((np.arange(rows) * n) // rows, n - 1)
+    return tuple(B.take_idx(blk, np.nonzero(assign == j)[0]) for j in range(n))
+
+
+def _partition(ref, n, mode, key, boundaries, seed, descending):
+    """Map side of a shuffle: one task, n output objects (never routed via the driver)."""
+    out = _partition_block.options(num_returns=n).remote(ref, n, mode, key, boundaries, seed,
+                                                         descending)
+    return [out] if n == 1 else out
+
+
+@ray.remote(num_returns=2)
+def _reduce_parts(mode, key, descending, seed, *parts):
+    blk = B.concat(list(parts))
+    if mode == "random" and B.num_rows(blk):
+        idx = np.random.default_rng(seed).permutation(B.num_rows(blk))
+        blk = B.take_idx(blk, idx)
+    elif mode == "range" and B.num_rows(blk):
+        order = np.argsort(blk[key], kind="stable")
+        if descending:
+            order = order[::-1]
+        blk = B.take_idx(blk, order)
+    return blk, X._meta(blk)
+
+
+@ray.remote
+def _sample_keys(blk, key, k):
+    v = blk.get(key)
+    if v is None or len(v) == 0:
+        return np.array([])
+    idx = np.random.default_rng(0).choice(len(v), size=min(k, len(v)), replace=False)
+    return np.asarray(v)[idx]
+
+
+@ray.remote(num_returns=2)
+def _slice_remote(blk, start, end):
+    b = B.slice_block(blk, start, end)
+    return b, X._meta(b)
+
+
+@ray.remote(num_returns=2)
+def _concat_remote(*blks):
+    b = B.concat(list(blks))
+    return b, X._meta(b)
+
+
+@ray.remote(num_returns=2)
+def _zip_remote(a, b):
+    out = dict(a)
+    for k, v in b.items():
+        kk = k if k not in out else f"{k}_1"
+        out[kk] = v
+    return out, X._meta(out)
+
+
+@ray.remote(num_returns=2)
+def _groupby_reduce(key, aggs, map_fn, batch_format, *parts):
+    blk = B.concat(list(parts))
+    if B.num_rows(blk) == 0:
+        return {}, X._meta({})
+    keys = blk[key]
+    uniq, inv = np.unique(keys, return_inverse=True)
+    if map_fn is not None:
+        outs = []
+        for gi in range(len(uniq)):
+            g = B.take_idx(blk, np.nonzero(inv == gi)[0])
+            outs.append(B.from_batch(map_fn(B.to_batch(g, batch_format))))
+        out = B.concat(outs)
+        return out, X._meta(out)
+    out = {key: uniq}
+    for name, col, op in aggs:
+        vals = []
+        for gi in range(len(uniq)):
+            m = inv == gi
+            if op == "count":
+                vals.append(int(m.sum()))
+                continue
+            v = blk[col][m].astype(np.float64)
+            vals.append({"sum": v.sum(), "mean": v.mean(), "min": v.min(), "max": v.max(),
+                         "std": v.std(ddof=1) if len(v) > 1 else 0.0}[op])
+        out[name] = np.asarray(vals)
+    return out, X._meta(out)
+
+
+@ray.remote
+def _write_block(blk, path, fmt, idx, kw):
+    os.makedirs(path, exist_ok=True)
+    base = os.path.join(path, f"part_{idx:06d}")
+    if fmt == "parquet":
+        import pyarrow.parquet as pq
+
+        pq.write_table(B.to_batch(blk, "pyarrow"), base + ".parquet", **kw)
+    elif fmt == "csv":
+        B.to_batch(blk, "pandas").to_csv(base + ".csv", index=False, **kw)
+    elif fmt == "json":
+        B.to_batch(blk, "pandas").to_json(base + ".json", orient="records", lines=True, **kw)
+    elif fmt == "numpy":
+        np.save(base + ".npy", blk[kw["column"]])
+    return B.num_rows(blk)
+
+
+# --------------------------------------------------------------------------- Dataset
+class Dataset:
+    def __init__(self, plan: X.Plan):
+        self._plan = plan
+        self._name = None
+
+    # ------------------------------------------------------------- transformations
+    def _with(self, stage: X.Stage) -> "Dataset":
+        return Dataset(self._plan.with_stage(stage))
+
+    def map_batches(self, fn, *, batch_size="default", compute=None, batch_format="default",
+                    zero_copy_batch=False, fn_args=None, fn_kwargs=None,
+                    fn_constructor_args=None, fn_constructor_kwargs=None, num_cpus=None,
+                    num_gpus=None, concurrency=None, **ray_remote_args) -> "Dataset":
+        if batch_size == "default":
+            batch_size = 1024
+        res = {"num_cpus": num_cpus if num_cpus is not None else 1}
+        if num_gpus:
+            res["num_gpus"] = num_gpus
+        if ray_remote_args.get("resources"):
+            res["resources"] = ray_remote_args["resources"]
+        is_class = isinstance(fn, type)
+        if is_class or isinstance(compute, ActorPoolStrategy) or (concurrency is not None and
+                                                                  is_class):
+            pool = (1, 1)
+            if isinstance(compute, ActorPoolStrategy):
+                pool = (compute.min_size, compute.max_size)
+            elif isinstance(concurrency, int):
+                pool = (concurrency, concurrency)
+            elif isinstance(concurrency, tuple):
+                pool = concurrency
+            if not is_class:
+                f = fn
+                fn = type("_FnWrapper", (), {"__call__": lambda self, b, *a, **k: f(b, *a, **k)})
+            make = _make_callable_class(fn, batch_size, batch_format,
+                                        fn_constructor_args or (), fn_constructor_kwargs or {},
+                                        fn_args or (), fn_kwargs or {}, zero_copy_batch)
+            return self._with(X.Stage("actor", make_fn=make, resources=res, pool=pool,
+                                      name=getattr(fn, "__name__", "MapBatches")))
+        return self._with(X.Stage("task", [_batcher(fn, batch_size, batch_format, fn_args or (),
+                                                    fn_kwargs or {}, zero_copy_batch)],
+                                  resources=res, name="MapBatches"))
+
+    def map(self, fn, *, compute=None, num_cpus=None, num_gpus=None, concurrency=None,
+            **kw) -> "Dataset":
+        if isinstance(fn, type):
+            cls = fn
+
+            class _RowCls:
+                def __init__(self, *a, **k):
+                    self.inner = cls(*a, **k)
+
+                def __call__(self, batch):
+                    return B.from_rows([self.inner(r) for r in B.to_rows(batch)])
+
+            return self.map_batches(_RowCls, batch_size=None, compute=compute, num_cpus=num_cpus,
+                                    num_gpus=num_gpus, concurrency=concurrency,
+                                    zero_copy_batch=True,
+                                    fn_constructor_args=kw.get("fn_constructor_args"),
+                                    fn_constructor_kwargs=kw.get("fn_constructor_kwargs"))
+        res = {"num_cpus": num_cpus if num_cpus is not None else 1}
+        if num_gpus:
+            res["num_gpus"] = num_gpus
+        return self._with(X.Stage("task", [_row_map(fn)], resources=res, name="Map"))
+
+    def flat_map(self, fn, **kw) -> "Dataset":
+        return self._with(X.Stage("task", [_row_flat_map(fn)], resources={"num_cpus": 1},
+                                  name="FlatMap"))
+
+    def filter(self, fn=None, *, expr=None, **kw) -> "Dataset":
+        return self._with(X.Stage("task", [_row_filter(fn)], resources={"num_cpus": 1},
+                                  name="Filter"))
+
+    def add_column(self, col, fn, **kw) -> "Dataset":
+        def f(batch):
+            batch = dict(batch)
+            batch[col] = np.asarray(fn(batch))
+            return batch
+
+        return self.map_batches(f, batch_format="numpy")
+
+    def drop_columns(self, cols, **kw) -> "Dataset":
+        cols = [cols] if isinstance(cols, str) else list(cols)
+        return self.map_batches(lambda b: {k: v for k, v in b.items() if k not in cols},
+                                batch_size=None, zero_copy_batch=True)
+
+    def select_columns(self, cols, **kw) -> "Dataset":
+        cols = [cols] if isinstance(cols, str) else list(cols)
+        return self.map_batches(lambda b: {k: b[k] for k in cols}, batch_size=None,
+                                zero_copy_batch=True)
+
+    def rename_columns(self, names: dict, **kw) -> "Dataset":
+        return self.map_batches(lambda b: {names.get(k, k): v for k, v in b.items()},
+                                batch_size=None, zero_copy_batch=True)
+
+    def random_sample(self, fraction: float, *, seed=None) -> "Dataset":
+        def f(b):
+            n = B.num_rows(b)
+            rng = np.random.default_rng(seed)
+            return B.take_idx(b, np.nonzero(rng.random(n) < fraction)[0])
+
+        return self._with(X.Stage("task", [f], resources={"num_cpus": 1}, name="RandomSample"))
+
+    def limit(self, limit: int) -> "Dataset":
+        parent = self
+
+        def lazy():
+            refs, metas, got = [], [], 0
+            for r, m in X.execute(parent._plan):
+                if got >= limit:
+                    break
+                n = m["num_rows"]
+                if got + n > limit:
+                    r, m2 = _slice_remote.remote(r, 0, limit - got)
+                    m = ray.get(m2)
+                    n = m["num_rows"]
+                refs.append(r)
+                metas.append(m)
+                got += n
+            return refs, metas
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    # ------------------------------------------------------------- all-to-all
+    def _blocks(self):
+        return X.materialize(self._plan)
+
+    def _shuffle(self, n_out, mode, key=None, boundaries=None, seed=None, descending=False):
+        parent = self
+
+        def lazy():
+            refs, metas = parent._blocks()
+            if not refs:
+                return [], []
+            plist = [_partition(r, n_out, mode, key, boundaries,
+                                None if seed is None else seed + i, descending)
+                     for i, r in enumerate(refs)]
+            outs, oms = [], []
+            for j in range(n_out):
+                b, m = _reduce_parts.remote(mode, key, descending,
+                                            None if seed is None else seed * 7919 + j,
+                                            *[pl[j] for pl in plist])
+                outs.append(b)
+                oms.append(m)
+            return outs, ray.get(oms)
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def random_shuffle(self, *, seed=None, num_blocks=None, **kw) -> "Dataset":
+        n = num_blocks or max(1, len(self._blocks()[0]))
+        return self._shuffle(n, "random", seed=seed if seed is not None else
+                             int(time.time_ns() % (1 << 31)))
+
+    def repartition(self, num_blocks: int, *, shuffle: bool = False, **kw) -> "Dataset":
+        if shuffle:
+            return self._shuffle(num_blocks, "random", seed=0)
+        parent = self
+
+        def lazy():
+            refs, metas = parent._blocks()
+            total = sum(m["num_rows"] for m in metas)
+            bounds = [total * i // num_blocks for i in range(num_blocks + 1)]
+            starts = np.cumsum([0] + [m["num_rows"] for m in metas])
+            outs, oms = [], []
+            for j in range(num_blocks):
+                lo, hi = bounds[j], bounds[j + 1]
+                pieces = []
+                for i, r in enumerate(refs):
+                    s, e = starts[i], starts[i + 1]
+                    a, b = max(lo, s), min(hi, e)
+                    if a < b:
+                        pieces.append(_slice_remote.remote(r, int(a - s), int(b - s))[0])
+                bl, m = _concat_remote.remote(*pieces)
+                outs.append(bl)
+                oms.append(m)
+            return outs, ray.get(oms)
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def sort(self, key, descending: bool = False, **kw) -> "Dataset":
+        if isinstance(key, (list, tuple)):
+            key = key[0]
+        parent = self
+
+        def lazy():
+            refs, metas = parent._blocks()
+            n = max(1, len(refs))
+            samples = np.concatenate([s for s in ray.get([_sample_keys.remote(r, key, 64)
+                                                          for r in refs]) if len(s)] or
+                                     [np.array([])])
+            bounds = np.quantile(np.sort(samples), np.linspace(0, 1, n + 1)[1:-1]) \
+                if len(samples) else []
+            ds = parent._shuffle(n, "range", key=key, boundaries=list(bounds),
+                                 descending=descending)
+            r2, m2 = ds._blocks()
+            if descending:
+                pass
+            return r2, m2
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def groupby(self, key) -> "GroupedData":
+        return GroupedData(self, key)
+
+    def union(self, *others) -> "Dataset":
+        dss = [self] + list(others)
+
+        def lazy():
+            refs, metas = [], []
+            for d in dss:
+                r, m = d._blocks()
+                refs.extend(r)
+                metas.extend(m)
+            return refs, metas
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def zip(self, other) -> "Dataset":
+        a, b = self, other
+
+        def lazy():
+            ra, ma = a.repartition(1)._blocks()
+            rb, mb = b.repartition(1)._blocks()
+            if ma[0]["num_rows"] != mb[0]["num_rows"]:
+                raise ValueError("Cannot zip datasets of different number of rows")
+            z, m = _zip_remote.remote(ra[0], rb[0])
+            return [z], [ray.get(m)]
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def unique(self, column: str) -> list:
+        vals = set()
+        for b in self.iter_batches(batch_size=None):
+            vals.update(np.unique(b[column]).tolist())
+        return sorted(vals)
+
+    # ------------------------------------------------------------- splitting
+    def split(self, n: int, *, equal: bool = False, locality_hints=None) -> list:
+        refs, metas = self._blocks()
+        if equal:
+            total = sum(m["num_rows"] for m in metas)
+            per = total // n
+            return [self._range_subset(refs, metas, i * per, (i + 1) * per) for i in range(n)]
+        groups = [[] for _ in range(n)]
+        for i, (r, m) in enumerate(zip(refs, metas)):
+            groups[i % n].append((r, m))
+        return [Dataset(X.Plan(("refs", [r for r, _ in g]), source_meta=[m for _, m in g]))
+                for g in groups]
+
+    def _range_subset(self, refs, metas, lo, hi):
+        starts = np.cumsum([0] + [m["num_rows"] for m in metas])
+        out_r, out_m = [], []
+        for i, r in enumerate(refs):
+            s, e = starts[i], starts[i + 1]
+            a, b = max(lo, s), min(hi, e)
+            if a < b:
+                if a == s and b == e:
+                    out_r.append(r)
+                    out_m.append(metas[i])
+                else:
+                    br, bm = _slice_remote.remote(r, int(a - s), int(b - s))
+                    out_r.append(br)
+                    out_m.append(ray.get(bm))
+        return Dataset(X.Plan(("refs", out_r), source_meta=out_m))
+
+    def split_at_indices(self, indices) -> list:
+        refs, metas = self._blocks()
+        total = sum(m["num_rows"] for m in metas)
+        pts = [0] + list(indices) + [total]
+        return [self._range_subset(refs, metas, pts[i], pts[i + 1]) for i in range(len(pts) - 1)]
+
+    def split_proportionately(self, proportions) -> list:
+        total = self.count()
+        idx, acc = [], 0
+        for p in proportions:
+            acc += int(total * p)
+            idx.append(acc)
+        return self.split_at_indices(idx)
+
+    def train_test_split(self, test_size, *, shuffle=False, seed=None, **kw):
+        ds = self.random_shuffle(seed=seed) if shuffle else self
+        total = ds.count()
+        n_test = int(test_size if isinstance(test_size, int) else math.ceil(total * test_size))
+        a, b = ds.split_at_indices([total - n_test])
+        return a, b
+
+    def streaming_split(self, n: int, *, equal: bool = False, locality_hints=None) -> list:
+        from .iterator import SplitCoordinator, StreamSplitIterator
+
+        coord = ray.remote(SplitCoordinator).options(num_cpus=0, max_concurrency=n + 2).remote(
+            self._plan, n, equal)
+        return [StreamSplitIterator(coord, i) for i in range(n)]
+
+    # ------------------------------------------------------------- consumption
+    def iter_internal_ref_bundles(self):
+        return X.execute(self._plan)
+
+    def iterator(self):
+        from .iterator import DataIterator
+
+        return DataIterator(self)
+
+    def iter_batches(self, *, batch_size=256, batch_format="default", drop_last=False,
+                     local_shuffle_buffer_size=None, local_shuffle_seed=None,
+                     prefetch_batches=1, **kw):
+        from .iterator import batch_blocks
+
+        refs = (r for r, _ in X.execute(self._plan))
+        yield from batch_blocks(refs, batch_size, batch_format, drop_last,
+                                local_shuffle_buffer_size, local_shuffle_seed)
+
+    def iter_rows(self, **kw):
+        for r, _ in X.execute(self._plan):
+            yield from B.to_rows(ray.get(r))
+
+    def __iter__(self):
+        return self.iter_rows()
+
+    def iter_torch_batches(self, *, batch_size=256, dtypes=None, device="auto",
+                           collate_fn=None, drop_last=False, local_shuffle_buffer_size=None,
+                           local_shuffle_seed=None, prefetch_batches=1, pin_memory=True, **kw):
+        from .iterator import torch_batches
+
+        yield from torch_batches(self.iter_batches(
+            batch_size=batch_size, drop_last=drop_last,
+            local_shuffle_buffer_size=local_shuffle_buffer_size,
+            local_shuffle_seed=local_shuffle_seed), dtypes, device, collate_fn, pin_memory)
+
+    def to_torch(self, **kw):
+        return self.iter_torch_batches(**kw)
+
+    def take(self, limit: int = 20) -> list:
+        out = []
+        for r, _ in X.execute(self.limit(limit)._plan):
+            for row in B.to_rows(ray.get(r)):
+                out.append(row)
+                if len(out) >= limit:
+                    return out
+        return out
+
+    def take_all(self, limit=None) -> list:
+        out = []
+        for r, _ in X.execute(self._plan):
+            out.extend(B.to_rows(ray.get(r)))
+            if limit is not None and len(out) > limit:
+                raise ValueError(f"The dataset has more than the given limit of {limit} rows")
+        return out
+
+    def take_batch(self, batch_size: int = 20, *, batch_format="default"):
+        for b in self.limit(batch_size).iter_batches(batch_size=batch_size,
+                                                     batch_format=batch_format):
+            return b
+        return {}
+
+    def show(self, limit: int = 20):
+        for r in self.take(limit):
+            print(r)
+
+    def count(self) -> int:
+        return builtins.sum(m["num_rows"] for _, m in X.execute(self._plan))
+
+    def schema(self):
+        for r, m in X.execute(self.limit(1)._plan):
+            if m and m.get("schema"):
+                return B.Schema(m["schema"])
+        return None
+
+    def columns(self):
+        s = self.schema()
+        return s.names if s else []
+
+    def num_blocks(self) -> int:
+        return len(self._blocks()[0])
+
+    def size_bytes(self) -> int:
+        return builtins.sum(m["size_bytes"] for m in self._blocks()[1])
+
+    def input_files(self):
+        return list(getattr(self, "_input_files", []))
+
+    def materialize(self) -> "Dataset":
+        refs, metas = self._blocks()
+        return MaterializedDataset(X.Plan(("refs", refs), source_meta=metas))
+
+    def stats(self) -> str:
+        refs, metas = self._blocks()
+        rows = builtins.sum(m["num_rows"] for m in metas)
+        return (f"Dataset: {len(refs)} blocks, {rows} rows, "
+                f"{builtins.sum(m['size_bytes'] for m in metas)} bytes; stages: "
+                + " -> ".join(s.name for s in self._plan.stages))
+
+    def _aggregate(self, cols):
+        cols = [cols] if isinstance(cols, str) else list(cols)
+        parts = ray.get([_agg_block.remote(r, cols, None) for r, _ in X.execute(self._plan)])
+        out = {}
+        for c in cols:
+            ps = [p[c] for p in parts if p[c] is not None]
+            n = builtins.sum(p["n"] for p in ps)
+            s = builtins.sum(p["sum"] for p in ps)
+            ss = builtins.sum(p["sumsq"] for p in ps)
+            out[c] = {"n": n, "sum": s, "mean": s / n if n else None,
+                      "min": builtins.min(p["min"] for p in ps) if ps else None,
+                      "max": builtins.max(p["max"] for p in ps) if ps else None,
+                      "std": math.sqrt(max(0.0, (ss - s * s / n) / (n - 1))) if n > 1 else 0.0}
+        return out
+
+    def _single(self, on, what):
+        cols = [on] if isinstance(on, str) or on is None else list(on)
+        if on is None:
+            cols = self.columns()
+        a = self._aggregate(cols)
+        vals = [a[c][what] for c in cols]
+        return vals[0] if len(vals) == 1 else vals
+
+    def sum(self, on=None, **kw):
+        return self._single(on, "sum")
+
+    def min(self, on=None, **kw):
+        return self._single(on, "min")
+
+    def max(self, on=None, **kw):
+        return self._single(on, "max")
+
+    def mean(self, on=None, **kw):
+        return self._single(on, "mean")
+
+    def std(self, on=None, ddof=1, **kw):
+        return self._single(on, "std")
+
+    def aggregate(self, *aggs):
+        out = {}
+        for a in aggs:
+            out.update(a._run(self))
+        return out
+
+    def to_pandas(self, limit=None):
+        import pandas as pd
+
+        blocks = [ray.get(r) for r, _ in X.execute(self._plan)]
+        return B.to_batch(B.concat(blocks), "pandas") if blocks else pd.DataFrame()
+
+    def to_numpy_refs(self, *, column=None):
+        return [r for r, _ in X.execute(self._plan)]
+
+    def to_arrow_refs(self):
+        return [ray.put(B.to_batch(ray.get(r), "pyarrow")) for r, _ in X.execute(self._plan)]
+
+    def get_internal_block_refs(self):
+        return self._blocks()[0]
+
+    # ------------------------------------------------------------- writes
+    def _write(self, path, fmt, **kw):
+        refs = [_write_block.remote(r, path, fmt, i, kw)
+                for i, (r, _) in enumerate(X.execute(self._plan))]
+        ray.get(refs)
+
+    def write_parquet(self, path, **kw):
+        self._write(path, "parquet", **kw)
+
+    def write_csv(self, path, **kw):
+        self._write(path, "csv", **kw)
+
+    def write_json(self, path, **kw):
+        self._write(path, "json", **kw)
+
+    def write_numpy(self, path, *, column, **kw):
+        self._write(path, "numpy", column=column)
+
+    def __repr__(self):
+        return f"Dataset(stages={[s.name for s in self._plan.stages]})"
+
+    def __len__(self):
+        raise TypeError("Use ds.count() to compute the length of a distributed Dataset.")
+
+
+class MaterializedDataset(Dataset):
+    pass
+
+
+class GroupedData:
+    def __init__(self, ds: Dataset, key):
+        self._ds = ds
+        self._key = key if isinstance(key, str) else key[0]
+
+    def _run(self, aggs=None, map_fn=None, batch_format="numpy"):
+        key = self._key
+        ds = self._ds
+        parent = ds
+
+        def lazy():
+            refs, metas = parent._blocks()
+            n = max(1, len(refs))
+            plist = [_partition(r, n, "hash", key, None, None, False) for r in refs]
+            outs, oms = [], []
+            for j in range(n):
+                b, m = _groupby_reduce.remote(key, aggs, map_fn, batch_format,
+                                              *[pl[j] for pl in plist])
+                outs.append(b)
+                oms.append(m)
+            return outs, ray.get(oms)
+
+        return Dataset(X.Plan(("lazy", lazy))).sort(key)
+
+    def count(self):
+        return self._run([("count()", None, "count")])
+
+    def sum(self, on):
+        return self._run([(f"sum({on})", on, "sum")])
+
+    def mean(self, on):
+        return self._run([(f"mean({on})", on, "mean")])
+
+    def min(self, on):
+        return self._run([(f"min({on})", on, "min")])
+
+    def max(self, on):
+        return self._run([(f"max({on})", on, "max")])
+
+    def std(self, on, ddof=1):
+        return self._run([(f"std({on})", on, "std")])
+
+    def aggregate(self, *aggs):
+        return self._run([(a.name, a.on, a.op) for a in aggs])
+
+    def map_groups(self, fn, *, batch_format="default", **kw):
+        return self._run(None, fn, "numpy" if batch_format == "default" else batch_format)
+
+
+class AggregateFn:
+    def __init__(self, op, on=None, alias_name=None):
+        self.op = op
+        self.on = on
+        self.name = alias_name or (f"{op}({on})" if on else f"{op}()")
+
+    def _run(self, ds):
+        if self.op == "count":
+            return {self.name: ds.count()}
+        return {self.name: ds._aggregate([self.on])[self.on][self.op]}
+
+
+def Count():  # noqa: N802
+    return AggregateFn("count")
+
+
+def Sum(on, alias_name=None):  # noqa: N802
+    return AggregateFn("sum", on, alias_name)
+
+
+def Mean(on, alias_name=None):  # noqa: N802
+    return AggregateFn("mean", on, alias_name)
+
+
+def Min(on, alias_name=None):  # noqa: N802
+    return AggregateFn("min", on, alias_name)
+
+
+def Max(on, alias_name=None):  # noqa: N802
+    return AggregateFn("max", on, alias_name)
+
+
+def Std(on, alias_name=None):  # noqa: N802
+    return AggregateFn("std", on, alias_name)
+
+
+itertools  # noqa: B018

@@ -1,0 +1,257 @@
+"""Dataset iteration + Train ingest (reference: python/ray/data/iterator.py,
+_internal/iterator/stream_split_iterator.py, _internal/block_batching/*).
+
+``iter_torch_batches(device="cuda")`` on MI355X: each numpy batch (a zero-copy
+view of the shared-memory block) is copied ONCE into a reusable pinned host
+buffer and moved to HBM with a non-blocking H2D on a side stream, one batch
+ahead of the consumer; the consumer's stream waits on an event, so the DMA
+overlaps the training step."""
+
+from __future__ import annotations
+
+import collections
+
+import numpy as np
+
+import ray_amd as ray
+
+from . import block as B
+
+
+def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer, seed):
+    rng = np.random.default_rng(seed)
+    buf = []
+    buffered = 0
+    bs = None if batch_size in (None, "default") else int(batch_size)
+    fmt = "numpy" if batch_format in ("default", None) else batch_format
+
+    def emit(blk):
+        return B.to_batch(blk, fmt)
+
+    pending = collections.deque()
+    for ref in block_refs:
+        blk = ray.get(ref)
+        if B.num_rows(blk) == 0:
+            continue
+        if bs is None:
+            yield emit(blk)
+            continue
+        buf.append(blk)
+        buffered += B.num_rows(blk)
+        min_buf = bs if not shuffle_buffer else max(bs, shuffle_buffer)
+        while buffered >= min_buf:
+            cat = B.concat(buf)
+            if shuffle_buffer:
+                cat = B.take_idx(cat, rng.permutation(B.num_rows(cat)))
+            out = B.slice_block(cat, 0, bs)
+            rest = B.slice_block(cat, bs, B.num_rows(cat))
+            buf = [rest] if B.num_rows(rest) else []
+            buffered = B.num_rows(rest)
+            yield emit(out)
+    pending  # noqa: B018
+    if buf and bs is not None:
+        cat = B.concat(buf)
+        if shuffle_buffer:
+            cat = B.take_idx(cat, rng.permutation(B.num_rows(cat)))
+        n = B.num_rows(cat)
+        for s in range(0, n, bs):
+            part = B.slice_block(cat, s, min(n, s + bs))
+            if drop_last and B.num_rows(part) < bs:
+                break
+            yield emit(part)
+
+
+def _resolve_device(device):
+    import torch
+
+    if device == "auto":
+        from ray_amd.train._internal import session as S
+
+        if S._get_session(required=False) is not None and torch.cuda.is_available():
+            from ray_amd.train.torch import get_device
+
+            return get_device()
+        return torch.device("cpu")
+    return torch.device(device) if device is not None else torch.device("cpu")
+
+
+def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
+    import torch
+
+    dev = _resolve_device(device)
+    if collate_fn is not None:
+        for b in batches:
+            yield collate_fn(b)
+        return
+
+    def to_tensors(b):
+        out = {}
+        for k, v in b.items():
+            if v.dtype == object:
+                out[k] = list(v)
+                continue
+            t = torch.from_numpy(np.array(v, copy=not v.flags.writeable))
+            if dtypes is not None:
+                dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
+                if dt is not None:
+                    t = t.to(dt)
+            out[k] = t
+        return out
+
+    if dev.type != "cuda":
+        for b in batches:
+            yield to_tensors(b)
+        return
+    stream = torch.cuda.Stream(dev)
+    # two pinned staging sets (ping-pong): set s is refilled only after the H2D that
+    # read it two batches ago has retired (its event), so host copies never race DMA
+    pinned = [{}, {}]
+    fence = [None, None]
+    slot = [0]
+
+    def stage(b):
+        s = slot[0]
+        slot[0] ^= 1
+        if fence[s] is not None:
+            fence[s].synchronize()
+        out = {}
+        with torch.cuda.stream(stream):
+            for k, v in b.items():
+                if v.dtype == object:
+                    out[k] = list(v)
+                    continue
+                src = torch.from_numpy(v) if v.flags.writeable else torch.from_numpy(np.array(v))
+                key = (k, tuple(src.shape), src.dtype)
+                buf = pinned[s].get(key)
+                if buf is None:
+                    buf = torch.empty(src.shape, dtype=src.dtype, pin_memory=pin_memory)
+                    pinned[s][key] = buf
+                buf.copy_(src)
+                t = buf.to(dev, non_blocking=True)
+                if dtypes is not None:
+                    dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
+                    if dt is not None:
+                        t = t.to(dt)
+                out[k] = t
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        fence[s] = ev
+        return out, ev
+
+    nxt = None
+    for b in batches:
+        cur = stage(b)
+        if nxt is not None:
+            out, ev = nxt
+            torch.cuda.current_stream(dev).wait_event(ev)
+            yield out
+        nxt = cur
+    if nxt is not None:
+        out, ev = nxt
+        torch.cuda.current_stream(dev).wait_event(ev)
+        yield out
+
+
+class DataIterator:
+    def __init__(self, ds):
+        self._ds = ds
+
+    def iter_batches(self, **kw):
+        return self._ds.iter_batches(**kw)
+
+    def iter_torch_batches(self, **kw):
+        return self._ds.iter_torch_batches(**kw)
+
+    def iter_rows(self, **kw):
+        return self._ds.iter_rows(**kw)
+
+    def materialize(self):
+        return self._ds.materialize()
+
+    def stats(self):
+        return self._ds.stats()
+
+
+class SplitCoordinator:
+    """Actor that runs ONE streaming execution and deals its blocks to n consumers
+    (reference: stream_split_iterator.SplitCoordinator)."""
+
+    def __init__(self, plan, n, equal):
+        self.plan = plan
+        self.n = n
+        self.equal = equal
+        self.epoch = -1
+        self._start()
+
+    def _start(self):
+        from . import _executor as X
+
+        self.epoch += 1
+        self.gen = X.execute(self.plan)
+        self.queues = [collections.deque() for _ in range(self.n)]
+        self.rows = [0] * self.n
+        self.done = False
+        self.finished = [False] * self.n
+
+    def next_block(self, i, epoch):
+        import threading
+
+        if not hasattr(self, "_lock"):
+            self._lock = threading.Lock()
+        with self._lock:
+            return self._next_block(i, epoch)
+
+    def _next_block(self, i, epoch):
+        if epoch > self.epoch and all(self.finished):
+            self._start()
+        while not self.queues[i]:
+            if self.done:
+                self.finished[i] = True
+                return None
+            try:
+                ref, meta = next(self.gen)
+            except StopIteration:
+                self.done = True
+                continue
+            # equal: give the block to the consumer with the fewest rows
+            j = int(np.argmin(self.rows)) if self.equal else (sum(len(q) for q in
+                                                                  self.queues) % self.n)
+            self.queues[j].append(ref)
+            self.rows[j] += meta["num_rows"] if meta else 0
+        return [self.queues[i].popleft()]
+
+
+class StreamSplitIterator(DataIterator):
+    def __init__(self, coord, index):
+        self._coord = coord
+        self._index = index
+        self._epoch = 0
+
+    def _blocks(self):
+        ep = self._epoch
+        self._epoch += 1
+        while True:
+            r = ray.get(self._coord.next_block.remote(self._index, ep))
+            if r is None:
+                return
+            yield r[0]
+
+    def iter_batches(self, *, batch_size=256, batch_format="default", drop_last=False,
+                     local_shuffle_buffer_size=None, local_shuffle_seed=None, **kw):
+        return batch_blocks(self._blocks(), batch_size, batch_format, drop_last,
+                            local_shuffle_buffer_size, local_shuffle_seed)
+
+    def iter_rows(self, **kw):
+        for ref in self._blocks():
+            yield from B.to_rows(ray.get(ref))
+
+    def iter_torch_batches(self, *, batch_size=256, dtypes=None, device="auto", collate_fn=None,
+                           drop_last=False, local_shuffle_buffer_size=None,
+                           local_shuffle_seed=None, **kw):
+        return torch_batches(self.iter_batches(batch_size=batch_size, drop_last=drop_last,
+                                               local_shuffle_buffer_size=local_shuffle_buffer_size,
+                                               local_shuffle_seed=local_shuffle_seed),
+                             dtypes, device, collate_fn)
+
+    def __reduce__(self):
+        return (StreamSplitIterator, (self._coord, self._index))

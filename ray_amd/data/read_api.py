@@ -1,0 +1,210 @@
+"""Dataset sources (reference: python/ray/data/read_api.py, datasource/*)."""
+
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+
+import ray_amd as ray
+
+from . import _executor as X
+from . import block as B
+from .dataset import Dataset, MaterializedDataset
+
+
+def _parallelism(p, n_items=None):
+    if p in (None, -1, "auto"):
+        p = X.default_parallelism() * 2
+    if n_items is not None:
+        p = max(1, min(p, n_items))
+    return int(p)
+
+
+def range(n: int, *, parallelism: int = -1, override_num_blocks=None) -> Dataset:  # noqa: A001
+    k = _parallelism(override_num_blocks or parallelism, n)
+    bounds = [n * i // k for i in builtins_range(k + 1)]
+
+    def mk(lo, hi):
+        return lambda: {"id": np.arange(lo, hi, dtype=np.int64)}
+
+    return Dataset(X.Plan(("read", [mk(bounds[i], bounds[i + 1]) for i in builtins_range(k)])))
+
+
+def range_tensor(n: int, *, shape=(1,), parallelism: int = -1, override_num_blocks=None):
+    k = _parallelism(override_num_blocks or parallelism, n)
+    bounds = [n * i // k for i in builtins_range(k + 1)]
+
+    def mk(lo, hi):
+        def f():
+            ids = np.arange(lo, hi, dtype=np.int64)
+            return {"data": np.broadcast_to(ids.reshape((-1,) + (1,) * len(shape)),
+                                            (hi - lo,) + tuple(shape)).copy()}
+        return f
+
+    return Dataset(X.Plan(("read", [mk(bounds[i], bounds[i + 1]) for i in builtins_range(k)])))
+
+
+def from_items(items: list, *, parallelism: int = -1, override_num_blocks=None) -> Dataset:
+    k = _parallelism(override_num_blocks or parallelism, max(1, len(items)))
+    bounds = [len(items) * i // k for i in builtins_range(k + 1)]
+    refs, metas = [], []
+    for i in builtins_range(k):
+        blk = B.from_rows(items[bounds[i]:bounds[i + 1]])
+        refs.append(ray.put(blk))
+        metas.append(X._meta(blk))
+    return MaterializedDataset(X.Plan(("refs", refs), source_meta=metas))
+
+
+def _from_blocks(blocks):
+    refs = [ray.put(b) for b in blocks]
+    return MaterializedDataset(X.Plan(("refs", refs), source_meta=[X._meta(b) for b in blocks]))
+
+
+def from_numpy(ndarrays) -> Dataset:
+    if isinstance(ndarrays, np.ndarray):
+        ndarrays = [ndarrays]
+    return _from_blocks([{"data": a} for a in ndarrays])
+
+
+def from_numpy_refs(refs) -> Dataset:
+    return _from_blocks([{"data": ray.get(r)} for r in refs])
+
+
+def from_pandas(dfs) -> Dataset:
+    if not isinstance(dfs, list):
+        dfs = [dfs]
+    return _from_blocks([B.from_batch(d) for d in dfs])
+
+
+def from_pandas_refs(refs):
+    return from_pandas([ray.get(r) for r in refs])
+
+
+def from_arrow(tables) -> Dataset:
+    if not isinstance(tables, list):
+        tables = [tables]
+    return _from_blocks([B.from_batch(t) for t in tables])
+
+
+def from_arrow_refs(refs):
+    return from_arrow([ray.get(r) for r in refs])
+
+
+def from_torch(dataset) -> Dataset:
+    return from_items([{"item": dataset[i]} for i in builtins_range(len(dataset))])
+
+
+def from_huggingface(dataset) -> Dataset:
+    return from_items([dict(r) for r in dataset])
+
+
+def _expand(paths, exts=None):
+    if isinstance(paths, str):
+        paths = [paths]
+    out = []
+    for p in paths:
+        if os.path.isdir(p):
+            for root, _, files in os.walk(p):
+                for f in sorted(files):
+                    if exts is None or any(f.endswith(e) for e in exts):
+                        out.append(os.path.join(root, f))
+        elif any(c in p for c in "*?["):
+            out.extend(sorted(glob.glob(p)))
+        else:
+            out.append(p)
+    if not out:
+        raise FileNotFoundError(f"no files found for {paths}")
+    return out
+
+
+def _file_ds(paths, exts, reader, include_paths=False):
+    files = _expand(paths, exts)
+
+    def mk(f):
+        def r():
+            blk = B.from_batch(reader(f))
+            if include_paths:
+                blk["path"] = np.array([f] * B.num_rows(blk), dtype=object)
+            return blk
+        return r
+
+    ds = Dataset(X.Plan(("read", [mk(f) for f in files])))
+    ds._input_files = files
+    return ds
+
+
+def read_parquet(paths, *, columns=None, include_paths=False, **kw) -> Dataset:
+    def rd(f):
+        import pyarrow.parquet as pq
+
+        return pq.read_table(f, columns=columns)
+
+    return _file_ds(paths, [".parquet"], rd, include_paths)
+
+
+def read_csv(paths, *, include_paths=False, **kw) -> Dataset:
+    def rd(f):
+        import pyarrow.csv as pc
+
+        return pc.read_csv(f)
+
+    return _file_ds(paths, [".csv"], rd, include_paths)
+
+
+def read_json(paths, *, include_paths=False, lines=True, **kw) -> Dataset:
+    def rd(f):
+        import pandas as pd
+
+        try:
+            return pd.read_json(f, lines=True)
+        except ValueError:
+            return pd.read_json(f)
+
+    return _file_ds(paths, [".json", ".jsonl"], rd, include_paths)
+
+
+def read_numpy(paths, *, include_paths=False, **kw) -> Dataset:
+    return _file_ds(paths, [".npy"], lambda f: {"data": np.load(f)}, include_paths)
+
+
+def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, include_paths=False, **kw):
+    def rd(f):
+        with open(f, encoding=encoding) as fh:
+            lines = [ln.rstrip("\n") for ln in fh]
+        if drop_empty_lines:
+            lines = [ln for ln in lines if ln.strip()]
+        return {"text": np.array(lines, dtype=object)}
+
+    return _file_ds(paths, None, rd, include_paths)
+
+
+def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
+    def rd(f):
+        with open(f, "rb") as fh:
+            b = np.empty(1, dtype=object)
+            b[0] = fh.read()
+        return {"bytes": b}
+
+    return _file_ds(paths, None, rd, include_paths)
+
+
+def read_images(paths, *, size=None, mode=None, include_paths=False, **kw) -> Dataset:
+    """Reads .npy image arrays (PIL is not installed in this image): HWC uint8."""
+
+    def rd(f):
+        img = np.load(f)
+        return {"image": img[None]}
+
+    return _file_ds(paths, [".npy"], rd, include_paths)
+
+
+def read_datasource(datasource, *, parallelism=-1, **kw) -> Dataset:
+    tasks = datasource.get_read_tasks(_parallelism(parallelism))
+    return Dataset(X.Plan(("read", list(tasks))))
+
+
+import builtins  # noqa: E402
+
+builtins_range = builtins.range
