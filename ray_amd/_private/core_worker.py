@@ -445,6 +445,9 @@ class CoreWorker:
         if in_store and self.store is not None:
             try:
                 self.store.delete(oid)
+                from . import gpu_object_store
+
+                gpu_object_store.free_sub_objects(self.store.store, oid)
             except Exception:
                 pass
         del contained
@@ -824,11 +827,11 @@ class CoreWorker:
             args, kwargs = a2, k2
         if not args and not kwargs:
             return (None, ref_args), holders
-        sobj = ser.serialize((args, kwargs))
+        put_oid = object_id_for_put(self._current_task_id(), self._bump_put())
+        sobj = ser.serialize((args, kwargs), put_oid)
         holders.extend(sobj.refs)
         if sobj.total > ARGS_INLINE_MAX or sobj.gpu:
-            ref = self.put_serialized_object(
-                object_id_for_put(self._current_task_id(), self._bump_put()), sobj)
+            ref = self.put_serialized_object(put_oid, sobj)
             holders.append(ref)
             return (("s", ref._id, self.addr), ref_args), holders
         return (sobj.to_bytes(), ref_args), holders

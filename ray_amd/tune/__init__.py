@@ -1,0 +1,16 @@
+"""ray_amd.tune — hyperparameter tuning (reference: python/ray/tune)."""
+
+from ray_amd.air.config import CheckpointConfig, FailureConfig, RunConfig  # noqa: F401
+from ray_amd.train._checkpoint import Checkpoint  # noqa: F401
+from ray_amd.train._internal.session import get_checkpoint, get_context, report  # noqa: F401
+from ray_amd.tune import schedulers  # noqa: F401
+from ray_amd.tune.search.sample import (choice, grid_search, lograndint, loguniform,  # noqa
+                                        qlograndint, qloguniform, qrandint, qrandn, quniform,
+                                        randint, randn, sample_from, uniform)
+from ray_amd.tune.trainable import Trainable, with_parameters, with_resources  # noqa: F401
+from ray_amd.tune.tuner import (CombinedStopper, ExperimentAnalysis,  # noqa: F401
+                                FunctionStopper, MaximumIterationStopper, ResultGrid, Stopper,
+                                TimeoutStopper, TrialPlateauStopper, TuneConfig, Tuner, run)
+from ray_amd.train.result import Result  # noqa: F401
+
+TuneError = RuntimeError

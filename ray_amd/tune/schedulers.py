@@ -1,0 +1,203 @@
+"""Trial schedulers (reference: python/ray/tune/schedulers/{trial_scheduler,async_hyperband,
+hyperband,median_stopping_rule,pbt,resource_changing_scheduler}.py)."""
+
+from __future__ import annotations
+
+import copy
+import math
+import random
+
+import numpy as np
+
+
+class TrialScheduler:
+    CONTINUE = "CONTINUE"
+    PAUSE = "PAUSE"
+    STOP = "STOP"
+    NOOP = "NOOP"
+
+    def __init__(self, metric=None, mode=None):
+        self.metric = metric
+        self.mode = mode
+
+    def set_search_properties(self, metric, mode):
+        self.metric = self.metric or metric
+        self.mode = self.mode or mode
+
+    def _score(self, result):
+        v = result.get(self.metric)
+        if v is None:
+            return None
+        return v if self.mode == "max" else -v
+
+    def on_trial_add(self, runner, trial):
+        pass
+
+    def on_trial_result(self, runner, trial, result):
+        return self.CONTINUE
+
+    def on_trial_complete(self, runner, trial, result):
+        pass
+
+    def on_trial_error(self, runner, trial):
+        pass
+
+
+class FIFOScheduler(TrialScheduler):
+    pass
+
+
+class AsyncHyperBandScheduler(TrialScheduler):
+    """ASHA (Li et al. 2018): successive halving at rungs r·η^k, asynchronous promotion."""
+
+    def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=100,
+                 grace_period=1, reduction_factor=4, brackets=1, stop_last_trials=True):
+        super().__init__(metric, mode)
+        self.time_attr = time_attr
+        self.max_t = max_t
+        self.rf = reduction_factor
+        rungs = []
+        t = grace_period
+        while t < max_t:
+            rungs.append(t)
+            t *= reduction_factor
+        self.rungs = {r: [] for r in rungs}
+
+    def on_trial_result(self, runner, trial, result):
+        t = result.get(self.time_attr, 0)
+        if t >= self.max_t:
+            return self.STOP
+        s = self._score(result)
+        if s is None:
+            return self.CONTINUE
+        for r in sorted(self.rungs, reverse=True):
+            if t >= r and r not in trial._asha_rungs:
+                trial._asha_rungs.add(r)
+                rec = self.rungs[r]
+                rec.append(s)
+                k = int(len(rec) / self.rf)
+                if k >= 1:
+                    cutoff = sorted(rec, reverse=True)[k - 1]
+                    if s < cutoff:
+                        return self.STOP
+                elif len(rec) > 1 and s < max(rec) and len(rec) >= self.rf:
+                    return self.STOP
+                break
+        return self.CONTINUE
+
+
+ASHAScheduler = AsyncHyperBandScheduler
+
+
+class HyperBandScheduler(AsyncHyperBandScheduler):
+    """Synchronous HyperBand approximated by its asynchronous variant with several
+    brackets (grace periods η^s)."""
+
+    def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=81,
+                 reduction_factor=3, stop_last_trials=True):
+        super().__init__(time_attr, metric, mode, max_t, 1, reduction_factor)
+
+
+class MedianStoppingRule(TrialScheduler):
+    def __init__(self, time_attr="time_total_s", metric=None, mode=None, grace_period=60.0,
+                 min_samples_required=3, min_time_slice=0, hard_stop=True):
+        super().__init__(metric, mode)
+        self.time_attr = time_attr
+        self.grace = grace_period
+        self.min_samples = min_samples_required
+        self.hist = {}
+
+    def on_trial_result(self, runner, trial, result):
+        s = self._score(result)
+        if s is None:
+            return self.CONTINUE
+        self.hist.setdefault(trial.trial_id, []).append(s)
+        if result.get(self.time_attr, 0) < self.grace:
+            return self.CONTINUE
+        others = [np.mean(v) for k, v in self.hist.items() if k != trial.trial_id]
+        if len(others) < self.min_samples:
+            return self.CONTINUE
+        if max(self.hist[trial.trial_id]) < np.median(others):
+            return self.STOP
+        return self.CONTINUE
+
+
+class PopulationBasedTraining(TrialScheduler):
+    """PBT (Jaderberg et al. 2017): every perturbation_interval, bottom-quantile trials
+    clone the checkpoint of a top-quantile trial and perturb its hyperparameters."""
+
+    def __init__(self, time_attr="training_iteration", metric=None, mode=None,
+                 perturbation_interval=5, hyperparam_mutations=None, quantile_fraction=0.25,
+                 resample_probability=0.25, perturbation_factors=(1.2, 0.8),
+                 custom_explore_fn=None, seed=None):
+        super().__init__(metric, mode)
+        self.time_attr = time_attr
+        self.interval = perturbation_interval
+        self.mutations = hyperparam_mutations or {}
+        self.q = quantile_fraction
+        self.p_resample = resample_probability
+        self.factors = perturbation_factors
+        self.explore_fn = custom_explore_fn
+        self.rng = random.Random(seed)
+        self.last = {}
+        self.scores = {}
+        self.num_perturbations = 0
+
+    def _explore(self, config):
+        new = copy.deepcopy(config)
+        from ray_amd.tune.search.sample import Domain
+
+        for k, spec in self.mutations.items():
+            if isinstance(spec, dict):
+                continue
+            if self.rng.random() < self.p_resample or k not in new:
+                new[k] = spec.sample(self.rng) if isinstance(spec, Domain) else \
+                    (self.rng.choice(spec) if isinstance(spec, list) else spec())
+            elif isinstance(spec, list):
+                i = spec.index(new[k]) if new[k] in spec else 0
+                i = max(0, min(len(spec) - 1, i + self.rng.choice([-1, 1])))
+                new[k] = spec[i]
+            else:
+                new[k] = new[k] * self.rng.choice(self.factors)
+                if isinstance(config[k], int):
+                    new[k] = int(new[k])
+        if self.explore_fn:
+            new = self.explore_fn(new)
+        return new
+
+    def on_trial_result(self, runner, trial, result):
+        t = result.get(self.time_attr, 0)
+        s = self._score(result)
+        if s is None:
+            return self.CONTINUE
+        self.scores[trial.trial_id] = (s, trial)
+        if t - self.last.get(trial.trial_id, 0) < self.interval:
+            return self.CONTINUE
+        self.last[trial.trial_id] = t
+        ranked = sorted(self.scores.values(), key=lambda x: x[0])
+        n = len(ranked)
+        k = max(1, int(math.ceil(n * self.q))) if n > 1 else 0
+        bottom = [tr for _, tr in ranked[:k]]
+        top = [tr for _, tr in ranked[-k:]] if k else []
+        if trial in bottom and top and trial not in top:
+            donor = self.rng.choice(top)
+            if donor.last_checkpoint is not None:
+                trial.pending_exploit = (donor.last_checkpoint, self._explore(donor.config))
+                self.num_perturbations += 1
+        return self.CONTINUE
+
+
+class PB2(PopulationBasedTraining):
+    """PB2 requires GP libraries that are not installed; behaves as PBT."""
+
+
+class ResourceChangingScheduler(TrialScheduler):
+    def __init__(self, base_scheduler=None, resources_allocation_function=None):
+        super().__init__()
+        self.base = base_scheduler or FIFOScheduler()
+
+    def set_search_properties(self, metric, mode):
+        self.base.set_search_properties(metric, mode)
+
+    def on_trial_result(self, runner, trial, result):
+        return self.base.on_trial_result(runner, trial, result)

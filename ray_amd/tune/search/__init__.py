@@ -1,0 +1,5 @@
+from ray_amd.tune.search.sample import (choice, grid_search, lograndint, loguniform,  # noqa
+                                        qlograndint, qloguniform, qrandint, qrandn, quniform,
+                                        randint, randn, sample_from, uniform)
+from ray_amd.tune.tuner import (BasicVariantGenerator, ConcurrencyLimiter, Repeater,  # noqa
+                                Searcher)

@@ -1,0 +1,251 @@
+"""Trainables (reference: python/ray/tune/trainable/{trainable,function_trainable}.py).
+
+Each trial runs inside a ``_TrialActor``. Function trainables run in a thread and
+hand each ``tune.report`` / ``train.report`` to the controller through a
+one-slot queue (the thread blocks until the controller asks for the next
+result, so a STOP decision takes effect at the next report). Class trainables
+are stepped directly."""
+
+from __future__ import annotations
+
+import os
+import queue
+import shutil
+import tempfile
+import threading
+import time
+import traceback
+
+from ray_amd.train._checkpoint import Checkpoint
+
+
+class Trainable:
+    """Class API: override setup/step/save_checkpoint/load_checkpoint."""
+
+    def __init__(self, config=None, trial_dir=None):
+        self.config = config or {}
+        self._iteration = 0
+        self._time_total = 0.0
+        self.logdir = trial_dir or tempfile.mkdtemp(prefix="trainable_")
+        self.setup(dict(self.config))
+
+    @property
+    def iteration(self):
+        return self._iteration
+
+    @property
+    def training_iteration(self):
+        return self._iteration
+
+    def setup(self, config):
+        pass
+
+    def step(self):
+        raise NotImplementedError
+
+    def save_checkpoint(self, checkpoint_dir):
+        return None
+
+    def load_checkpoint(self, checkpoint):
+        pass
+
+    def reset_config(self, new_config):
+        return False
+
+    def cleanup(self):
+        pass
+
+    def train(self):
+        t0 = time.time()
+        r = self.step() or {}
+        self._iteration += 1
+        self._time_total += time.time() - t0
+        r = dict(r)
+        r.setdefault("training_iteration", self._iteration)
+        r.setdefault("time_total_s", self._time_total)
+        return r
+
+    def save(self, checkpoint_dir=None):
+        d = checkpoint_dir or os.path.join(self.logdir, f"checkpoint_{self._iteration:06d}")
+        os.makedirs(d, exist_ok=True)
+        extra = self.save_checkpoint(d)
+        if isinstance(extra, dict):
+            import pickle
+
+            with open(os.path.join(d, "_state.pkl"), "wb") as f:
+                pickle.dump(extra, f)
+        with open(os.path.join(d, "_iter"), "w") as f:
+            f.write(f"{self._iteration} {self._time_total}")
+        return d
+
+    def restore(self, checkpoint_dir):
+        p = os.path.join(checkpoint_dir, "_state.pkl")
+        if os.path.exists(p):
+            import pickle
+
+            with open(p, "rb") as f:
+                self.load_checkpoint(pickle.load(f))
+        else:
+            self.load_checkpoint(checkpoint_dir)
+        it = os.path.join(checkpoint_dir, "_iter")
+        if os.path.exists(it):
+            a, b = open(it).read().split()
+            self._iteration, self._time_total = int(a), float(b)
+
+    def stop(self):
+        self.cleanup()
+
+
+# ------------------------------------------------------------------ function trainables
+class _FnSession:
+    def __init__(self, trial_dir, checkpoint, trial_id, trial_name, config):
+        self.q = queue.Queue(maxsize=1)
+        self.cont = threading.Semaphore(0)
+        self.trial_dir = trial_dir
+        self.checkpoint = checkpoint
+        self.trial_id = trial_id
+        self.trial_name = trial_name
+        self.config = config
+        self.iteration = 0
+        self.t0 = time.time()
+        self.ckpt_i = 0
+        self.stop = False
+
+
+_fn_session: _FnSession | None = None
+
+
+def function_report(metrics, checkpoint=None):
+    s = _fn_session
+    if s is None:
+        raise RuntimeError("report() called outside of a Tune / Train session")
+    if s.stop:
+        raise SystemExit(0)
+    s.iteration += 1
+    m = dict(metrics)
+    m.setdefault("training_iteration", s.iteration)
+    m.setdefault("time_total_s", time.time() - s.t0)
+    cpath = None
+    if checkpoint is not None:
+        cpath = os.path.join(s.trial_dir, f"checkpoint_{s.ckpt_i:06d}")
+        s.ckpt_i += 1
+        if os.path.abspath(checkpoint.path) != os.path.abspath(cpath):
+            shutil.copytree(checkpoint.path, cpath, dirs_exist_ok=True)
+    s.q.put(("result", m, cpath))
+    s.cont.acquire()
+    if s.stop:
+        raise SystemExit(0)
+
+
+def function_get_checkpoint():
+    s = _fn_session
+    return s.checkpoint if s is not None else None
+
+
+def function_get_context():
+    from ray_amd.train._internal.session import TrainContext
+
+    s = _fn_session
+    if s is None:
+        return TrainContext()
+    return TrainContext(trial_dir=s.trial_dir, trial_id=s.trial_id, trial_name=s.trial_name,
+                        experiment_name=os.path.basename(os.path.dirname(s.trial_dir)))
+
+
+class _TrialActor:
+    def __init__(self, trainable, config, trial_dir, trial_id, trial_name, checkpoint_path):
+        os.makedirs(trial_dir, exist_ok=True)
+        self.trainable = trainable
+        self.config = config
+        self.trial_dir = trial_dir
+        self.ckpt = Checkpoint(checkpoint_path) if checkpoint_path else None
+        self.is_class = isinstance(trainable, type) and issubclass(trainable, Trainable)
+        self.thread = None
+        self.inst = None
+        self.trial_id = trial_id
+        self.trial_name = trial_name
+
+    def start(self):
+        global _fn_session
+        if self.is_class:
+            self.inst = self.trainable(self.config, self.trial_dir)
+            if self.ckpt is not None:
+                self.inst.restore(self.ckpt.path)
+            return True
+        s = _FnSession(self.trial_dir, self.ckpt, self.trial_id, self.trial_name, self.config)
+        _fn_session = s
+        self.s = s
+
+        def run():
+            try:
+                out = self.trainable(self.config)
+                if isinstance(out, dict):
+                    function_report(out)
+                s.q.put(("done", None, None))
+            except SystemExit:
+                s.q.put(("done", None, None))
+            except BaseException as e:  # noqa: BLE001
+                s.q.put(("error", traceback.format_exc(), repr(e)))
+
+        self.thread = threading.Thread(target=run, daemon=True)
+        self.thread.start()
+        return True
+
+    def next_result(self):
+        if self.is_class:
+            try:
+                return ("result", self.inst.train(), None)
+            except BaseException as e:  # noqa: BLE001
+                return ("error", traceback.format_exc(), repr(e))
+        kind, a, b = self.s.q.get()
+        if kind == "result":
+            self.s.cont.release()
+        return kind, a, b
+
+    def save(self):
+        if self.is_class:
+            return self.inst.save()
+        return None
+
+    def stop(self):
+        if self.is_class and self.inst is not None:
+            self.inst.stop()
+        elif self.thread is not None:
+            self.s.stop = True
+            self.s.cont.release()
+        return True
+
+    def reset(self, config, checkpoint_path):
+        if self.is_class and self.inst.reset_config(config):
+            self.inst.config = config
+            if checkpoint_path:
+                self.inst.restore(checkpoint_path)
+            return True
+        return False
+
+
+def with_parameters(trainable, **kwargs):
+    """Bind large objects once (stored in the object store) to a trainable."""
+    import ray_amd as ray
+
+    refs = {k: ray.put(v) for k, v in kwargs.items()}
+    if isinstance(trainable, type):
+        class _Bound(trainable):
+            def setup(self, config):
+                vals = {k: ray.get(r) for k, r in refs.items()}
+                super().setup(config, **vals)
+
+        _Bound.__name__ = trainable.__name__
+        return _Bound
+
+    def fn(config):
+        vals = {k: ray.get(r) for k, r in refs.items()}
+        return trainable(config, **vals)
+
+    fn.__name__ = getattr(trainable, "__name__", "trainable")
+    return fn
+
+
+def with_resources(trainable, resources):
+    trainable._ray_amd_resources = resources
+    return trainable

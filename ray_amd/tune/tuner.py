@@ -1,0 +1,580 @@
+"""Tuner / TuneConfig / ResultGrid and the trial controller (reference:
+python/ray/tune/{tuner,tune_config,result_grid}.py, execution/tune_controller.py,
+stopper/*, search/{basic_variant,concurrency_limiter,searcher}.py)."""
+
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import time
+import uuid
+from dataclasses import dataclass, field
+
+import ray_amd as ray
+from ray_amd.air.config import RunConfig
+from ray_amd.train._checkpoint import Checkpoint
+from ray_amd.train.result import Result
+from ray_amd.tune.schedulers import FIFOScheduler, TrialScheduler
+from ray_amd.tune.search.sample import generate_variants
+from ray_amd.tune.trainable import _TrialActor
+
+
+# ------------------------------------------------------------------ searchers
+class Searcher:
+    def __init__(self, metric=None, mode=None):
+        self.metric = metric
+        self.mode = mode
+
+    def set_search_properties(self, metric, mode, config):
+        self.metric = self.metric or metric
+        self.mode = self.mode or mode
+        return True
+
+    def suggest(self, trial_id):
+        raise NotImplementedError
+
+    def on_trial_result(self, trial_id, result):
+        pass
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        pass
+
+
+class BasicVariantGenerator(Searcher):
+    def __init__(self, points_to_evaluate=None, max_concurrent=0, random_state=None):
+        super().__init__()
+        self.points = list(points_to_evaluate or [])
+        self.seed = random_state
+        self._it = None
+
+    def _setup(self, space, num_samples):
+        self._it = iter(list(self.points) + list(generate_variants(space, num_samples,
+                                                                   self.seed)))
+
+    def suggest(self, trial_id):
+        try:
+            return next(self._it)
+        except StopIteration:
+            return None
+
+
+class ConcurrencyLimiter(Searcher):
+    def __init__(self, searcher, max_concurrent):
+        super().__init__()
+        self.searcher = searcher
+        self.max_concurrent = max_concurrent
+        self.live = set()
+
+    def set_search_properties(self, metric, mode, config):
+        return self.searcher.set_search_properties(metric, mode, config)
+
+    def suggest(self, trial_id):
+        if len(self.live) >= self.max_concurrent:
+            return "PAUSE"
+        c = self.searcher.suggest(trial_id)
+        if c is not None and c != "PAUSE":
+            self.live.add(trial_id)
+        return c
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        self.live.discard(trial_id)
+        self.searcher.on_trial_complete(trial_id, result, error)
+
+
+class Repeater(Searcher):
+    def __init__(self, searcher, repeat=1, set_index=True):
+        super().__init__()
+        self.searcher = searcher
+        self.repeat = repeat
+        self._cur = None
+        self._n = 0
+
+    def suggest(self, trial_id):
+        if self._cur is None or self._n >= self.repeat:
+            self._cur = self.searcher.suggest(trial_id)
+            self._n = 0
+        self._n += 1
+        return self._cur
+
+
+# ------------------------------------------------------------------ stoppers
+class Stopper:
+    def __call__(self, trial_id, result):
+        return False
+
+    def stop_all(self):
+        return False
+
+
+class MaximumIterationStopper(Stopper):
+    def __init__(self, max_iter):
+        self.max_iter = max_iter
+
+    def __call__(self, trial_id, result):
+        return result.get("training_iteration", 0) >= self.max_iter
+
+
+class FunctionStopper(Stopper):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self, trial_id, result):
+        return self.fn(trial_id, result)
+
+
+class TrialPlateauStopper(Stopper):
+    def __init__(self, metric, std=0.01, num_results=4, grace_period=4, metric_threshold=None,
+                 mode=None):
+        self.metric, self.std, self.n, self.grace = metric, std, num_results, grace_period
+        self.hist = {}
+
+    def __call__(self, trial_id, result):
+        import numpy as np
+
+        h = self.hist.setdefault(trial_id, [])
+        h.append(result.get(self.metric, 0))
+        if len(h) < max(self.grace, self.n):
+            return False
+        return float(np.std(h[-self.n:])) <= self.std
+
+
+class TimeoutStopper(Stopper):
+    def __init__(self, timeout):
+        self.deadline = time.time() + (timeout.total_seconds() if hasattr(timeout,
+                                                                         "total_seconds")
+                                       else timeout)
+
+    def stop_all(self):
+        return time.time() > self.deadline
+
+
+class CombinedStopper(Stopper):
+    def __init__(self, *stoppers):
+        self.stoppers = stoppers
+
+    def __call__(self, trial_id, result):
+        return any(s(trial_id, result) for s in self.stoppers)
+
+    def stop_all(self):
+        return any(s.stop_all() for s in self.stoppers)
+
+
+# ------------------------------------------------------------------ config / results
+@dataclass
+class TuneConfig:
+    metric: str | None = None
+    mode: str | None = None
+    search_alg: object = None
+    scheduler: object = None
+    num_samples: int = 1
+    max_concurrent_trials: int | None = None
+    time_budget_s: float | None = None
+    reuse_actors: bool = False
+    trial_name_creator: object = None
+    trial_dirname_creator: object = None
+
+
+class Trial:
+    def __init__(self, config, trial_id, exp_dir, resources):
+        self.config = config
+        self.trial_id = trial_id
+        self.status = "PENDING"
+        self.results = []
+        self.last_result = {}
+        self.last_checkpoint = None
+        self.error = None
+        self.actor = None
+        self.pending_ref = None
+        self.resources = resources
+        self.local_path = os.path.join(exp_dir, f"trial_{trial_id}")
+        self.pending_exploit = None
+        self._asha_rungs = set()
+        self.restore_from = None
+
+    def __repr__(self):
+        return f"Trial({self.trial_id}, {self.status})"
+
+
+class ResultGrid:
+    def __init__(self, results: list, experiment_path: str, metric=None, mode=None):
+        self._results = results
+        self.experiment_path = experiment_path
+        self._metric = metric
+        self._mode = mode
+
+    def __len__(self):
+        return len(self._results)
+
+    def __getitem__(self, i):
+        return self._results[i]
+
+    def __iter__(self):
+        return iter(self._results)
+
+    @property
+    def errors(self):
+        return [r.error for r in self._results if r.error is not None]
+
+    @property
+    def num_errors(self):
+        return len(self.errors)
+
+    @property
+    def num_terminated(self):
+        return sum(1 for r in self._results if r.error is None)
+
+    def get_best_result(self, metric=None, mode=None, scope="last", filter_nan_and_inf=True):
+        metric = metric or self._metric
+        mode = mode or self._mode
+        if metric is None or mode is None:
+            raise ValueError("get_best_result needs metric and mode")
+        import math
+
+        best, bv = None, None
+        for r in self._results:
+            hist = r.metrics_history or [r.metrics or {}]
+            vals = [m.get(metric) for m in hist if m.get(metric) is not None]
+            if not vals:
+                continue
+            if scope == "last":
+                v = vals[-1]
+            elif scope == "avg":
+                v = sum(vals) / len(vals)
+            else:
+                v = max(vals) if mode == "max" else min(vals)
+            if filter_nan_and_inf and (math.isnan(v) or math.isinf(v)):
+                continue
+            if bv is None or (v > bv if mode == "max" else v < bv):
+                best, bv = r, v
+        if best is None:
+            raise RuntimeError(f"no trial reported {metric}")
+        return best
+
+    def get_dataframe(self, filter_metric=None, filter_mode=None):
+        import pandas as pd
+
+        rows = []
+        for r in self._results:
+            row = dict(r.metrics or {})
+            for k, v in (r._config or {}).items():
+                row[f"config/{k}"] = v
+            row["logdir"] = r.path
+            rows.append(row)
+        return pd.DataFrame(rows)
+
+
+# ------------------------------------------------------------------ controller
+class _Controller:
+    def __init__(self, trainable, space, tc: TuneConfig, rc: RunConfig, exp_dir, resources):
+        self.trainable = trainable
+        self.space = space
+        self.tc = tc
+        self.rc = rc
+        self.exp_dir = exp_dir
+        self.resources = resources
+        self.scheduler: TrialScheduler = tc.scheduler or FIFOScheduler()
+        self.scheduler.set_search_properties(tc.metric, tc.mode)
+        self.searcher = tc.search_alg or BasicVariantGenerator()
+        self.searcher.set_search_properties(tc.metric, tc.mode, space)
+        base = self.searcher.searcher if isinstance(self.searcher, ConcurrencyLimiter) else \
+            self.searcher
+        if isinstance(base, BasicVariantGenerator):
+            base._setup(space, tc.num_samples)
+        self.trials: list[Trial] = []
+        self.stopper = self._make_stopper(rc.stop)
+        self.exhausted = False
+        self.actor_cls = ray.remote(_TrialActor)
+        self.start = time.time()
+
+    @staticmethod
+    def _make_stopper(stop):
+        if stop is None:
+            return None
+        if isinstance(stop, Stopper):
+            return stop
+        if callable(stop):
+            return FunctionStopper(stop)
+
+        class _Dict(Stopper):
+            def __call__(self, tid, result):
+                return any(k in result and result[k] >= v for k, v in stop.items())
+
+        return _Dict()
+
+    def _max_concurrent(self):
+        cpus = ray.cluster_resources().get("CPU", 1)
+        need = max(self.resources.get("CPU", 1), 1e-3)
+        gpus = ray.cluster_resources().get("GPU", 0)
+        n = int(cpus // need)
+        if self.resources.get("GPU"):
+            n = min(n, int(gpus // self.resources["GPU"]))
+        if self.tc.max_concurrent_trials:
+            n = min(n, self.tc.max_concurrent_trials)
+        return max(1, n)
+
+    def _new_trial(self):
+        if self.exhausted:
+            return None
+        tid = uuid.uuid4().hex[:8]
+        cfg = self.searcher.suggest(tid)
+        if cfg == "PAUSE":
+            return None
+        if cfg is None:
+            self.exhausted = True
+            return None
+        t = Trial(cfg, tid, self.exp_dir, self.resources)
+        self.trials.append(t)
+        self.scheduler.on_trial_add(self, t)
+        return t
+
+    def _launch(self, t: Trial, checkpoint=None):
+        opts = {"num_cpus": self.resources.get("CPU", 1)}
+        if self.resources.get("GPU"):
+            opts["num_gpus"] = self.resources["GPU"]
+        t.actor = self.actor_cls.options(**opts).remote(self.trainable, t.config, t.local_path,
+                                                        t.trial_id, f"trial_{t.trial_id}",
+                                                        checkpoint)
+        t.actor.start.remote()  # actor calls are ordered: next_result runs after start
+        t.status = "RUNNING"
+        t.pending_ref = t.actor.next_result.remote()
+
+    def _stop_trial(self, t, status="TERMINATED", error=None):
+        t.status = status
+        t.error = error
+        if t.actor is not None:
+            try:
+                ray.get(t.actor.stop.remote(), timeout=5)
+            except Exception:
+                pass
+            ray.kill(t.actor)
+        t.actor = None
+        t.pending_ref = None
+        if status == "ERROR":
+            self.scheduler.on_trial_error(self, t)
+        else:
+            self.scheduler.on_trial_complete(self, t, t.last_result)
+        self.searcher.on_trial_complete(t.trial_id, t.last_result, error is not None)
+
+    def _log(self, t, result):
+        os.makedirs(t.local_path, exist_ok=True)
+        with open(os.path.join(t.local_path, "result.json"), "a") as f:
+            f.write(json.dumps({k: v for k, v in result.items()
+                                if isinstance(v, (int, float, str, bool, type(None)))}) + "\n")
+        with open(os.path.join(t.local_path, "params.json"), "w") as f:
+            json.dump(t.config, f, default=str)
+
+    def _save_state(self):
+        st = {"trials": [(t.trial_id, t.config, t.status, t.last_checkpoint, t.results)
+                         for t in self.trials], "exhausted": self.exhausted}
+        with open(os.path.join(self.exp_dir, "experiment_state.pkl"), "wb") as f:
+            pickle.dump(st, f)
+
+    def run(self):
+        maxc = self._max_concurrent()
+        budget = self.tc.time_budget_s
+        while True:
+            running = [t for t in self.trials if t.status == "RUNNING"]
+            pending = [t for t in self.trials if t.status == "PENDING"]
+            while len(running) < maxc:
+                t = pending.pop(0) if pending else self._new_trial()
+                if t is None:
+                    break
+                self._launch(t, t.restore_from)
+                running.append(t)
+            if not running:
+                break
+            refs = {t.pending_ref: t for t in running}
+            ready, _ = ray.wait(list(refs), num_returns=1, timeout=1.0)
+            if budget and time.time() - self.start > budget:
+                for t in running:
+                    self._stop_trial(t)
+                break
+            if self.stopper is not None and self.stopper.stop_all():
+                for t in running:
+                    self._stop_trial(t)
+                break
+            for r in ready:
+                t = refs[r]
+                try:
+                    kind, a, b = ray.get(r)
+                except Exception as e:  # noqa: BLE001
+                    self._stop_trial(t, "ERROR", e)
+                    continue
+                if kind == "done":
+                    self._stop_trial(t)
+                    continue
+                if kind == "error":
+                    self._stop_trial(t, "ERROR", RuntimeError(a))
+                    continue
+                result = dict(a)
+                result["trial_id"] = t.trial_id
+                result["config"] = t.config
+                if b:
+                    t.last_checkpoint = b
+                t.results.append(result)
+                t.last_result = result
+                self._log(t, result)
+                self.searcher.on_trial_result(t.trial_id, result)
+                decision = self.scheduler.on_trial_result(self, t, result)
+                if self.stopper is not None and self.stopper(t.trial_id, result):
+                    decision = TrialScheduler.STOP
+                if decision == TrialScheduler.STOP:
+                    self._stop_trial(t)
+                    continue
+                if t.pending_exploit is not None:
+                    ckpt, cfg = t.pending_exploit
+                    t.pending_exploit = None
+                    self._stop_trial(t, "PENDING")
+                    t.status = "PENDING"
+                    t.config = cfg
+                    t.restore_from = ckpt
+                    t._asha_rungs = set()
+                    continue
+                t.pending_ref = t.actor.next_result.remote()
+            self._save_state()
+        self._save_state()
+        return self.trials
+
+
+def _trainer_to_trainable(trainer):
+    """Run a Train trainer as a Tune trial: param_space["train_loop_config"] is merged."""
+    import copy
+
+    def fn(config):
+        from ray_amd.tune.trainable import function_report
+
+        tr = copy.copy(trainer)
+        tlc = dict(tr.train_loop_config or {})
+        tlc.update(config.get("train_loop_config", {}))
+        tr.train_loop_config = tlc
+        if "scaling_config" in config:
+            tr.scaling_config = config["scaling_config"]
+        res = tr.fit()
+        for m in res.metrics_history[:-1]:
+            function_report(m)
+        function_report(res.metrics or {}, res.checkpoint)
+
+    return fn
+
+
+class Tuner:
+    def __init__(self, trainable=None, *, param_space=None, tune_config=None, run_config=None,
+                 _restore_path=None):
+        self.trainable = trainable
+        self.param_space = param_space or {}
+        self.tune_config = tune_config or TuneConfig()
+        self.run_config = run_config or RunConfig()
+        self._restore_path = _restore_path
+
+    def fit(self) -> ResultGrid:
+        if not ray.is_initialized():
+            ray.init()
+        rc = self.run_config
+        name = rc.name or f"tune_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
+        exp_dir = self._restore_path or os.path.join(rc.storage_path, name)
+        os.makedirs(exp_dir, exist_ok=True)
+        trainable = self.trainable
+        resources = {"CPU": 1}
+        from ray_amd.train.data_parallel_trainer import DataParallelTrainer
+
+        if isinstance(trainable, DataParallelTrainer):
+            resources = {"CPU": 0}
+            trainable = _trainer_to_trainable(trainable)
+        elif getattr(trainable, "_ray_amd_resources", None):
+            resources = dict(trainable._ray_amd_resources)
+            resources = {("CPU" if k == "cpu" else "GPU" if k == "gpu" else k): v
+                         for k, v in resources.items()}
+        ctl = _Controller(trainable, self.param_space, self.tune_config, rc, exp_dir, resources)
+        if self._restore_path:
+            self._restore_into(ctl)
+        trials = ctl.run()
+        results = []
+        for t in trials:
+            results.append(Result(metrics=t.last_result, checkpoint=Checkpoint(t.last_checkpoint)
+                                  if t.last_checkpoint else None, error=t.error,
+                                  path=t.local_path, metrics_history=t.results,
+                                  _config=t.config))
+        return ResultGrid(results, exp_dir, self.tune_config.metric, self.tune_config.mode)
+
+    def _restore_into(self, ctl):
+        p = os.path.join(self._restore_path, "experiment_state.pkl")
+        if not os.path.exists(p):
+            return
+        with open(p, "rb") as f:
+            st = pickle.load(f)
+        for tid, cfg, status, ckpt, results in st["trials"]:
+            t = Trial(cfg, tid, ctl.exp_dir, ctl.resources)
+            t.results = results
+            t.last_result = results[-1] if results else {}
+            t.last_checkpoint = ckpt
+            if status in ("TERMINATED",):
+                t.status = status
+            else:
+                t.status = "PENDING"
+                t.restore_from = ckpt
+            ctl.trials.append(t)
+        ctl.exhausted = st["exhausted"]
+
+    @classmethod
+    def restore(cls, path, trainable=None, **kw):
+        return cls(trainable, _restore_path=path, **kw)
+
+    @classmethod
+    def can_restore(cls, path):
+        return os.path.exists(os.path.join(path, "experiment_state.pkl"))
+
+    def get_results(self):
+        return self.fit()
+
+
+def run(run_or_experiment, *, config=None, num_samples=1, metric=None, mode=None,
+        scheduler=None, search_alg=None, stop=None, resources_per_trial=None, name=None,
+        storage_path=None, max_concurrent_trials=None, time_budget_s=None, **kw):
+    """Legacy tune.run API."""
+    t = run_or_experiment
+    if resources_per_trial:
+        t = _with_res(t, resources_per_trial)
+    tuner = Tuner(t, param_space=config or {},
+                  tune_config=TuneConfig(metric=metric, mode=mode, num_samples=num_samples,
+                                         scheduler=scheduler, search_alg=search_alg,
+                                         max_concurrent_trials=max_concurrent_trials,
+                                         time_budget_s=time_budget_s),
+                  run_config=RunConfig(name=name, storage_path=storage_path, stop=stop))
+    return ExperimentAnalysis(tuner.fit(), metric, mode)
+
+
+def _with_res(t, res):
+    from ray_amd.tune.trainable import with_resources
+
+    return with_resources(t, res)
+
+
+class ExperimentAnalysis:
+    def __init__(self, grid: ResultGrid, metric, mode):
+        self.grid = grid
+        self.default_metric = metric
+        self.default_mode = mode
+        self.trials = list(grid)
+
+    def get_best_config(self, metric=None, mode=None):
+        return self.grid.get_best_result(metric or self.default_metric,
+                                         mode or self.default_mode).config
+
+    @property
+    def best_config(self):
+        return self.get_best_config()
+
+    @property
+    def best_result(self):
+        return self.grid.get_best_result(self.default_metric, self.default_mode).metrics
+
+    def dataframe(self):
+        return self.grid.get_dataframe()
+
+    @property
+    def results_df(self):
+        return self.grid.get_dataframe()
+
+
+field  # noqa: B018

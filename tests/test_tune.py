@@ -1,0 +1,123 @@
+"""Tune tests (modelled on python/ray/tune/tests/test_tuner.py, test_trial_scheduler.py,
+test_sample.py)."""
+
+import os
+
+import pytest
+
+import ray_amd as ray
+from ray_amd import train, tune
+from ray_amd.tune.schedulers import AsyncHyperBandScheduler, PopulationBasedTraining
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4)
+    yield
+    ray.shutdown()
+
+
+def objective(config):
+    for i in range(10):
+        train.report({"score": config["a"] * (i + 1) + config.get("b", 0)})
+
+
+def test_grid_and_random(cluster, tmp_path):
+    tuner = tune.Tuner(objective,
+                       param_space={"a": tune.grid_search([1, 2, 3]),
+                                    "b": tune.uniform(0, 1)},
+                       tune_config=tune.TuneConfig(metric="score", mode="max", num_samples=2),
+                       run_config=tune.RunConfig(storage_path=str(tmp_path), name="g"))
+    rg = tuner.fit()
+    assert len(rg) == 6 and rg.num_errors == 0
+    best = rg.get_best_result()
+    assert best.config["a"] == 3 and best.metrics["training_iteration"] == 10
+    df = rg.get_dataframe()
+    assert len(df) == 6 and "config/a" in df.columns
+
+
+def test_asha_stops_bad_trials(cluster, tmp_path):
+    def f(config):
+        for i in range(20):
+            train.report({"acc": config["q"] * i})
+
+    # best trials first: ASHA can only cut a trial that is below the top 1/rf of the
+    # trials already recorded at a rung
+    rg = tune.Tuner(f, param_space={"q": tune.grid_search([5.0, 4.0, 3.0, 2.0, 1.0, 0.5, 0.2,
+                                                           0.1])},
+                    tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=
+                                                AsyncHyperBandScheduler(max_t=20,
+                                                                        grace_period=2,
+                                                                        reduction_factor=2),
+                                                max_concurrent_trials=8),
+                    run_config=tune.RunConfig(storage_path=str(tmp_path))).fit()
+    iters = sorted(r.metrics["training_iteration"] for r in rg)
+    assert iters[0] < 20 and iters[-1] >= 19
+
+
+class MyTrainable(tune.Trainable):
+    def setup(self, config):
+        self.x = 0
+        self.lr = config["lr"]
+
+    def step(self):
+        self.x += self.lr
+        return {"x": self.x}
+
+    def save_checkpoint(self, d):
+        return {"x": self.x}
+
+    def load_checkpoint(self, state):
+        self.x = state["x"]
+
+
+def test_class_trainable_and_stop(cluster, tmp_path):
+    rg = tune.Tuner(MyTrainable, param_space={"lr": tune.choice([1.0, 2.0])},
+                    tune_config=tune.TuneConfig(num_samples=2),
+                    run_config=tune.RunConfig(stop={"training_iteration": 5},
+                                              storage_path=str(tmp_path))).fit()
+    assert all(r.metrics["training_iteration"] == 5 for r in rg)
+
+
+def test_pbt_exploits(cluster, tmp_path):
+    def f(config):
+        step = 0
+        val = 0.0
+        ck = train.get_checkpoint()
+        if ck:
+            with open(os.path.join(ck.path, "s")) as fh:
+                step, val = map(float, fh.read().split())
+        while step < 12:
+            step += 1
+            val += config["lr"]
+            d = os.path.join(config["tmp"], f"{os.getpid()}_{step}_{config['lr']}")
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, "s"), "w") as fh:
+                fh.write(f"{step} {val}")
+            train.report({"val": val}, checkpoint=tune.Checkpoint(d))
+
+    pbt = PopulationBasedTraining(metric="val", mode="max", perturbation_interval=3,
+                                  hyperparam_mutations={"lr": [0.01, 0.1, 1.0, 2.0]}, seed=0)
+    rg = tune.Tuner(f, param_space={"lr": tune.grid_search([0.01, 0.1, 1.0, 2.0]),
+                                    "tmp": str(tmp_path)},
+                    tune_config=tune.TuneConfig(scheduler=pbt, max_concurrent_trials=4),
+                    run_config=tune.RunConfig(storage_path=str(tmp_path / "r"))).fit()
+    assert pbt.num_perturbations > 0
+    assert rg.get_best_result("val", "max").metrics["val"] > 1.0
+
+
+def test_tune_run_legacy(cluster, tmp_path):
+    a = tune.run(objective, config={"a": tune.grid_search([1, 2])}, metric="score", mode="max",
+                 storage_path=str(tmp_path))
+    assert a.best_config["a"] == 2
+
+
+def test_sample_domains():
+    from ray_amd.tune.search.sample import generate_variants
+
+    vs = list(generate_variants({"x": tune.randint(0, 5), "y": tune.loguniform(1e-4, 1e-1),
+                                 "z": tune.grid_search(["a", "b"]),
+                                 "w": tune.sample_from(lambda spec: spec.config["x"] * 2)},
+                                num_samples=3, seed=0))
+    assert len(vs) == 6
+    assert all(0 <= v["x"] < 5 and 1e-4 <= v["y"] <= 1e-1 and v["w"] == 2 * v["x"] for v in vs)
