@@ -1,0 +1,287 @@
+"""Serve public API (reference: python/ray/serve/api.py, deployment.py)."""
+
+from __future__ import annotations
+
+import hashlib
+import inspect
+import time
+
+import cloudpickle
+
+import ray_amd as ray
+from ray_amd.serve._controller import CONTROLLER_NAME, SERVE_NAMESPACE, ServeController
+from ray_amd.serve.handle import DeploymentHandle
+
+_controller = None
+_proxy = None
+_http_port = 8000
+
+try:  # starlette's State recurses in __getattr__ when unpickled: reduce it explicitly
+    import copyreg
+
+    from starlette.datastructures import State as _State
+
+    copyreg.pickle(_State, lambda s: (_State, (dict(s._state),)))
+except ImportError:  # pragma: no cover
+    pass
+
+
+def _get_controller(create=False):
+    global _controller
+    if _controller is not None:
+        return _controller
+    try:
+        _controller = ray.get_actor(CONTROLLER_NAME, namespace=SERVE_NAMESPACE)
+    except ValueError:
+        if not create:
+            raise RuntimeError("Serve is not running; call serve.run() or serve.start() first")
+        _controller = ray.remote(ServeController).options(
+            name=CONTROLLER_NAME, namespace=SERVE_NAMESPACE, lifetime="detached", num_cpus=0,
+            max_concurrency=1000, get_if_exists=True).remote()
+    return _controller
+
+
+def start(http_options: dict | None = None, detached: bool = True, **kw):
+    global _proxy, _http_port
+    if not ray.is_initialized():
+        ray.init()
+    c = _get_controller(create=True)
+    opts = http_options or {}
+    port = opts.get("port", 8000)
+    existing = ray.get(c.get_proxy.remote())
+    if existing is None and opts.get("location", "HeadOnly") != "NoServer":
+        from ray_amd.serve._proxy import HTTPProxy
+
+        _proxy = ray.remote(HTTPProxy).options(num_cpus=0, max_concurrency=1000,
+                                               name="SERVE_PROXY", namespace=SERVE_NAMESPACE,
+                                               lifetime="detached").remote(
+            opts.get("host", "127.0.0.1"), port)
+        err = ray.get(_proxy.ping.remote())
+        if err != "ok":
+            raise RuntimeError(f"HTTP proxy failed to start: {err}")
+        ray.get(c.set_proxy.remote(_proxy))
+        _http_port = port
+    return c
+
+
+class Deployment:
+    def __init__(self, func_or_class, name, num_replicas=1, ray_actor_options=None,
+                 user_config=None, max_ongoing_requests=100, autoscaling_config=None,
+                 route_prefix=None, graceful_shutdown_timeout_s=5.0, health_check_period_s=10.0,
+                 version=None, **kw):
+        self.func_or_class = func_or_class
+        self.name = name
+        if num_replicas == "auto":
+            autoscaling_config = autoscaling_config or {"min_replicas": 1, "max_replicas": 100}
+            num_replicas = 1
+        self.num_replicas = num_replicas
+        self.ray_actor_options = ray_actor_options or {}
+        self.user_config = user_config
+        self.max_ongoing_requests = max_ongoing_requests
+        self.autoscaling_config = dict(autoscaling_config) if autoscaling_config else None
+        self.route_prefix = route_prefix
+        self.graceful_shutdown_timeout_s = graceful_shutdown_timeout_s
+        self.version = version
+
+    def options(self, **kw):
+        d = dict(num_replicas=self.num_replicas, ray_actor_options=self.ray_actor_options,
+                 user_config=self.user_config, max_ongoing_requests=self.max_ongoing_requests,
+                 autoscaling_config=self.autoscaling_config, route_prefix=self.route_prefix,
+                 graceful_shutdown_timeout_s=self.graceful_shutdown_timeout_s,
+                 version=self.version, name=self.name)
+        if "max_concurrent_queries" in kw:
+            kw["max_ongoing_requests"] = kw.pop("max_concurrent_queries")
+        d.update(kw)
+        name = d.pop("name")
+        return Deployment(self.func_or_class, name, **d)
+
+    def bind(self, *args, **kwargs):
+        return Application(self, args, kwargs)
+
+    def __call__(self, *a, **k):
+        raise RuntimeError("Deployments cannot be constructed directly; use .bind().")
+
+
+class Application:
+    def __init__(self, deployment: Deployment, args, kwargs):
+        self.deployment = deployment
+        self.args = args
+        self.kwargs = kwargs
+
+
+def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_options=None,
+               user_config=None, max_ongoing_requests=100, max_concurrent_queries=None,
+               autoscaling_config=None, route_prefix=None, graceful_shutdown_timeout_s=5.0,
+               health_check_period_s=10.0, version=None, **kw):
+    if max_concurrent_queries is not None:
+        max_ongoing_requests = max_concurrent_queries
+
+    def deco(fc):
+        return Deployment(fc, name or fc.__name__, num_replicas, ray_actor_options, user_config,
+                          max_ongoing_requests, autoscaling_config, route_prefix,
+                          graceful_shutdown_timeout_s, health_check_period_s, version)
+
+    if _func_or_class is not None and callable(_func_or_class):
+        return deco(_func_or_class)
+    return deco
+
+
+def ingress(app):
+    """Class decorator: serve an ASGI (FastAPI/starlette) app from this deployment."""
+
+    def deco(cls):
+        orig_init = cls.__init__
+
+        def __serve_bind_asgi__(self, asgi_app):
+            try:
+                from fastapi.routing import APIRoute
+            except ImportError:
+                return
+            for route in list(asgi_app.router.routes):
+                ep = getattr(route, "endpoint", None)
+                if isinstance(route, APIRoute) and ep is not None and \
+                        ep.__qualname__.split(".")[-2:] == [cls.__name__, ep.__name__]:
+                    # (cloudpickle rebuilds dynamic classes with a bare __qualname__)
+                    bound = getattr(self, ep.__name__)
+                    asgi_app.router.routes.remove(route)
+                    asgi_app.add_api_route(route.path, bound, methods=list(route.methods),
+                                           response_model=route.response_model,
+                                           status_code=route.status_code)
+
+        cls.__serve_bind_asgi__ = __serve_bind_asgi__
+        cls._serve_asgi_app = app
+        cls.__init__ = orig_init
+        return cls
+
+    return deco
+
+
+def _build(app: Application, app_name, specs: dict):
+    dep = app.deployment
+    if dep.name in specs:
+        return DeploymentHandle(dep.name, app_name)
+
+    def conv(v):
+        if isinstance(v, Application):
+            return _build(v, app_name, specs)
+        if isinstance(v, (list, tuple)):
+            return type(v)(conv(x) for x in v)
+        if isinstance(v, dict):
+            return {k: conv(x) for k, x in v.items()}
+        return v
+
+    args = tuple(conv(a) for a in app.args)
+    kwargs = {k: conv(v) for k, v in app.kwargs.items()}
+    fc = dep.func_or_class
+    blob = cloudpickle.dumps(fc)
+    asgi = getattr(fc, "_serve_asgi_app", None) if inspect.isclass(fc) else None
+    specs[dep.name] = {
+        "name": dep.name, "callable": blob, "is_function": not inspect.isclass(fc),
+        "init_args": args, "init_kwargs": kwargs, "num_replicas": dep.num_replicas,
+        "autoscaling_config": dep.autoscaling_config, "ray_actor_options": dep.ray_actor_options,
+        "user_config": dep.user_config, "max_ongoing_requests": dep.max_ongoing_requests,
+        "asgi_app": cloudpickle.dumps(asgi) if asgi is not None else None,
+        "graceful_shutdown_timeout_s": dep.graceful_shutdown_timeout_s,
+        "code_version": dep.version or hashlib.blake2b(blob, digest_size=8).hexdigest(),
+    }
+    return DeploymentHandle(dep.name, app_name)
+
+
+def run(target: Application, *, name: str = "default", route_prefix: str | None = "/",
+        blocking: bool = False, _blocking=None, **kw) -> DeploymentHandle:
+    if isinstance(target, Deployment):
+        target = target.bind()
+    c = start(kw.get("http_options"))
+    specs: dict = {}
+    handle = _build(target, name, specs)
+    rp = target.deployment.route_prefix or route_prefix
+    ray.get(c.deploy_application.remote(name, rp, target.deployment.name, list(specs.values())))
+    st = ray.get(c.status.remote()).get(name, {})
+    if st.get("status") == "DEPLOY_FAILED":
+        errs = {d: s["status"] for d, s in st.get("deployments", {}).items()}
+        raise RuntimeError(f"application {name} failed to deploy: {errs}")
+    if blocking:
+        while True:
+            time.sleep(1)
+    return handle
+
+
+def delete(name: str, _blocking: bool = True):
+    ray.get(_get_controller().delete_application.remote(name))
+
+
+def shutdown():
+    global _controller, _proxy
+    try:
+        c = _get_controller()
+    except Exception:
+        return
+    try:
+        ray.get(c.shutdown.remote())
+    except Exception:
+        pass
+    try:
+        ray.kill(c)
+    except Exception:
+        pass
+    _controller = None
+    _proxy = None
+    from ray_amd.serve import handle as H
+
+    H._routers.clear()
+
+
+def status():
+    return ray.get(_get_controller().status.remote())
+
+
+def get_app_handle(name: str) -> DeploymentHandle:
+    ing = ray.get(_get_controller().get_ingress.remote(name))
+    if ing is None:
+        raise RuntimeError(f"application {name} does not exist")
+    return DeploymentHandle(ing, name)
+
+
+def get_deployment_handle(deployment_name: str, app_name: str = "default"):
+    return DeploymentHandle(deployment_name, app_name)
+
+
+def get_replica_context():
+    from ray_amd.serve import context
+
+    return context.get_replica_context()
+
+
+def multiplexed(_fn=None, *, max_num_models_per_replica: int = 3):
+    """Cache up to N loaded models per replica keyed by the request's multiplexed model id."""
+    import collections
+    import functools
+
+    def deco(fn):
+        cache = collections.OrderedDict()
+
+        @functools.wraps(fn)
+        async def wrapper(*args):
+            model_id = args[-1]
+            if model_id in cache:
+                cache.move_to_end(model_id)
+                return cache[model_id]
+            r = fn(*args)
+            if inspect.isawaitable(r):
+                r = await r
+            cache[model_id] = r
+            while len(cache) > max_num_models_per_replica:
+                cache.popitem(last=False)
+            return r
+
+        return wrapper
+
+    if _fn is not None and callable(_fn):
+        return deco(_fn)
+    return deco
+
+
+def get_multiplexed_model_id() -> str:
+    from ray_amd.serve import context
+
+    return context.current_model_id()

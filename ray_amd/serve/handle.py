@@ -1,0 +1,176 @@
+"""DeploymentHandle / DeploymentResponse and the replica router (reference:
+python/ray/serve/handle.py, _private/router.py, _private/replica_scheduler/pow_2_scheduler.py).
+
+Routing: power-of-two-choices on the number of requests this handle has in
+flight to each replica (no extra RPC on the hot path); the replica set is
+refreshed from the controller when its version changes or a replica fails."""
+
+from __future__ import annotations
+
+import asyncio
+import random
+import threading
+import time
+
+import ray_amd as ray
+
+
+class _Router:
+    def __init__(self, app_name, deployment_name):
+        self.app = app_name
+        self.dep = deployment_name
+        self.version = -1
+        self.replicas = []  # [(rid, handle)]
+        self.inflight = {}
+        self.max_ongoing = 100
+        self.lock = threading.Lock()
+        self.last_refresh = 0.0
+
+    def _controller(self):
+        from ray_amd.serve.api import _get_controller
+
+        return _get_controller()
+
+    def refresh(self, force=False):
+        now = time.time()
+        if not force and self.replicas and now - self.last_refresh < 1.0:
+            return
+        info = ray.get(self._controller().get_replicas.remote(self.app, self.dep))
+        self.last_refresh = now
+        if info is None:
+            raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
+        version, reps, mo = info
+        with self.lock:
+            if version != self.version:
+                self.version = version
+                self.replicas = reps
+                self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
+            self.max_ongoing = mo
+
+    def choose(self):
+        deadline = time.time() + 30
+        while True:
+            self.refresh()
+            with self.lock:
+                reps = list(self.replicas)
+            if reps:
+                break
+            if time.time() > deadline:
+                raise RuntimeError(f"no replicas available for {self.dep}")
+            time.sleep(0.05)
+            self.refresh(force=True)
+        if len(reps) == 1:
+            rid, h = reps[0]
+        else:
+            a, b = random.sample(reps, 2)
+            rid, h = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
+        with self.lock:
+            self.inflight[rid] = self.inflight.get(rid, 0) + 1
+        return rid, h
+
+    def done(self, rid):
+        with self.lock:
+            if rid in self.inflight:
+                self.inflight[rid] = max(0, self.inflight[rid] - 1)
+
+
+_routers: dict = {}
+_rlock = threading.Lock()
+
+
+def _router(app, dep):
+    with _rlock:
+        r = _routers.get((app, dep))
+        if r is None:
+            r = _routers[(app, dep)] = _Router(app, dep)
+        return r
+
+
+class DeploymentResponse:
+    def __init__(self, ref, router, rid):
+        self._ref = ref
+        self._router = router
+        self._rid = rid
+        self._done = False
+
+    def _finish(self):
+        if not self._done:
+            self._done = True
+            self._router.done(self._rid)
+
+    def result(self, timeout_s: float | None = None):
+        try:
+            return ray.get(self._ref, timeout=timeout_s)
+        finally:
+            self._finish()
+
+    def __await__(self):
+        async def _w():
+            try:
+                return await self._ref
+            finally:
+                self._finish()
+
+        return _w().__await__()
+
+    def _to_object_ref(self):
+        return self._ref
+
+    async def _to_object_ref_async(self):
+        return self._ref
+
+    def cancel(self):
+        ray.cancel(self._ref)
+
+    def __reduce__(self):
+        # passing a response to another deployment passes the underlying object
+        return (_resolve, (self._ref,))
+
+
+def _resolve(ref):
+    return ref
+
+
+class DeploymentHandle:
+    def __init__(self, deployment_name: str, app_name: str = "default", *, method_name=None,
+                 multiplexed_model_id: str = "", stream: bool = False):
+        self.deployment_name = deployment_name
+        self.app_name = app_name
+        self._method = method_name
+        self._mux = multiplexed_model_id
+        self._stream = stream
+
+    def options(self, *, method_name=None, multiplexed_model_id=None, stream=None,
+                use_new_handle_api=None, **kw):
+        return DeploymentHandle(self.deployment_name, self.app_name,
+                                method_name=method_name or self._method,
+                                multiplexed_model_id=multiplexed_model_id if
+                                multiplexed_model_id is not None else self._mux,
+                                stream=self._stream if stream is None else stream)
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return self.options(method_name=name)
+
+    def remote(self, *args, **kwargs):
+        r = _router(self.app_name, self.deployment_name)
+        rid, h = r.choose()
+        args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
+        kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v)
+                  for k, v in kwargs.items()}
+        ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
+        return DeploymentResponse(ref, r, rid)
+
+    def __reduce__(self):
+        return (DeploymentHandle, (self.deployment_name, self.app_name),
+                {"_method": self._method, "_mux": self._mux, "_stream": self._stream})
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+
+    def __repr__(self):
+        return f"DeploymentHandle(deployment='{self.deployment_name}', app='{self.app_name}')"
+
+
+asyncio  # noqa: B018
