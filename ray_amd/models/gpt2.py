@@ -93,9 +93,8 @@ class Block(nn.Module):
         H = self.n_head
         h = self.ln_1(x)
         qkv = F.linear(h, self.c_attn_w, self.c_attn_b)  # hipBLASLt GEMM + bias epilogue
-        q, k, v = qkv.view(B, T, 3, H, C // H).permute(2, 0, 3, 1, 4).unbind(0)
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        y = y.transpose(1, 2).reshape(B, T, C)
+        # HIP MFMA flash attention straight off the packed QKV layout (no permutes/copies)
+        y = rf.causal_attention_qkv(qkv.view(B, T, 3, H, C // H)).reshape(B, T, C)
         x = rf.bias_residual(F.linear(y, self.c_proj_w), self.c_proj_b, x)
         h = self.ln_2(x)
         a = rf.bias_gelu(F.linear(h, self.c_fc_w), self.c_fc_b)

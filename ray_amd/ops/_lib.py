@@ -59,6 +59,9 @@ _SIGS = {
                            c_int, c_void_p],
     "ra_resize_bilinear": [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p],
     "ra_cast_scale_u8": [c_void_p, c_void_p, c_long, c_float, c_void_p],
+    "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                    c_void_p],
+    "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],
     "ra_arena_open": [c_int, c_void_p, ctypes.POINTER(c_void_p)],

@@ -123,6 +123,46 @@ def bias_residual(h, bias, res):
     return ref.bias_residual(h, bias, res)
 
 
+# --------------------------------------------------------------------- flash attention
+class _FlashAttnQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, scale):
+        B, T, _, H, D = qkv.shape
+        qkv = qkv.contiguous()
+        out = torch.empty((B, T, H, D), device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty((B, H, T), device=qkv.device, dtype=torch.float32)
+        check(_lib.lib().ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), B, T, H, D, scale,
+                                     stream_ptr()), "attn_fwd")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, T, _, H, D = qkv.shape
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty((B, H, T), device=qkv.device, dtype=torch.float32)
+        check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
+                                     ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()), "attn_bwd")
+        return dqkv, None
+
+
+def causal_attention_qkv(qkv, scale=None):
+    """Causal self-attention from a packed [B, T, 3, H, D] QKV tensor → [B, T, H, D].
+
+    HIP MFMA flash attention for D == 64, T % 128 == 0 (bf16); otherwise PyTorch SDPA."""
+    B, T, _, H, D = qkv.shape
+    if scale is None:
+        scale = D ** -0.5
+    if _hip(qkv) and qkv.dtype == torch.bfloat16 and D == 64 and T % 128 == 0:
+        return _FlashAttnQKV.apply(qkv, float(scale))
+    q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
+    y = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale)
+    return y.transpose(1, 2)
+
+
 # --------------------------------------------------------------------- cross entropy
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod

@@ -164,6 +164,27 @@ def test_image_normalize(cuda_device):
     assert _rel(c, x.float() / 255) < 1e-2
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2)])
+def test_flash_attention_fwd_bwd(cuda_device, B, T, H):
+    torch.manual_seed(9)
+    D = 64
+    qkv = torch.randn(B, T, 3, H, D, device=cuda_device).bfloat16().requires_grad_()
+    y = rf.causal_attention_qkv(qkv)
+    ref_in = qkv.detach().float().requires_grad_()
+    q, k, v = ref_in.permute(2, 0, 3, 1, 4).unbind(0)
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    mask = torch.ones(T, T, device=cuda_device, dtype=torch.bool).triu(1)
+    p = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+    yr = (p @ v).transpose(1, 2)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert _rel(qkv.grad, ref_in.grad) < 2e-2
+    for i in range(3):
+        assert _rel(qkv.grad[:, :, i], ref_in.grad[:, :, i]) < 2e-2, i
+
+
 def test_flat_adamw_matches_torch(cuda_device):
     from ray_amd.parallel.flat import FlatAdamW, FlatParams
 
