@@ -4,18 +4,32 @@
 // O as [B, T, H, 64] (= the proj GEMM's input) and dQKV packed like QKV, so the
 // model needs no permute / contiguous / cat copies around attention.
 //
-// Orientation (see cdna_hip_programming.md §3 "An accumulator tile as the next
-// MFMA's operand"): the forward computes S^T = K·Q^T so each lane owns ONE query
-// (column) and 16 keys (registers) — row-max / row-sum / rescale are lane-local
-// plus one xor-32 exchange — and P^T's accumulator registers feed O^T = V^T·P^T
-// directly as the B operand (no LDS round trip for P). V is staged transposed in
-// LDS so its A fragments are two 8-byte reads.
+// Orientation (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's
+// operand"): the forward computes S^T = K·Q^T so each lane owns ONE query (column)
+// and 16 keys (registers) — row-max / row-sum / rescale are lane-local plus one
+// permlane32 swap — and P^T's accumulator registers feed O^T = V^T·P^T directly as
+// the B operand (no LDS round trip for P).
+//
+// LDS images: every K/V/Q/dO tile is staged ONCE, row-major ([row][64] bf16, 128-B
+// rows, no padding) with 16-byte writes, under an XOR swizzle of the 16-B chunk
+// index (`swz`). The same image serves row reads (ds_read_b128, MFMA operand with k
+// along the row) and column reads (ds_read_b64_tr_b16 hardware transpose, operand
+// with k down the column) — both conflict-free:
+//   * b128 row reads: a 16-lane group reads 16 rows at one chunk; rows alternate
+//     between the two 64-B bank halves (row&1) and swz(row) takes all 8 values over
+//     each group's 8 same-parity rows.
+//   * tr reads: a 32-lane half reads rows R..R+3 (R%4==0) × 32 columns; swz(R) and
+//     swz(R+2) differ in bit 2, so rows R and R+2 use complementary chunk sets.
+// Tiles are double buffered: one barrier per tile; the next tile's global loads are
+// in flight during the current tile's MFMAs.
 //
 // Backward = two kernels (no float atomics; dQ would otherwise cost ~400 MB of
-// atomic adds per step at GPT-2 shape, far above the 1.3 TB/s atomic rate):
+// atomic adds per step at GPT-2 shape, far above the chip's atomic rate):
 //   attn_bwd_dkdv : one workgroup per 128 keys, each wave owns 32 keys; loops over
 //                   the causal q tiles: S = Q·K^T, dP = dO·V^T (keys on lanes), then
-//                   dV += P^T·dO and dK += dS^T·Q with P / dS as A operands.
+//                   dV += P^T·dO and dK += dS^T·Q with P / dS as A operands. The
+//                   accumulators of S and dP start at -LSE/c and -delta (row constants
+//                   as the initial accumulator), so P = exp2(c·S'), dS = P·dP'.
 //   attn_bwd_dq   : one workgroup per 128 queries (forward orientation):
 //                   dQ^T += K^T·dS^T.
 // Softmax statistics are kept in the log2 domain (exp2 with scale·log2e folded).
@@ -23,10 +37,11 @@
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define HD 64
-#define TSTR 72  // LDS row stride (elements) for 64-wide tiles: 144 B, conflict-free b128 rows
+#define TILE_ELEMS (64 * 64)
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -36,10 +51,13 @@ __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
-// two 4-element (8-byte) LDS reads → one 8-element fragment
-__device__ __forceinline__ bf16x8_t ld4x2(const bf16_t* p0, const bf16_t* p1) {
-  bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(p0);
-  bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(p1);
+__device__ __forceinline__ bf16x4_t tr4(const bf16_t* p) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+  s16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)const_cast<bf16_t*>(p));
+  return __builtin_bit_cast(bf16x4_t, v);
+}
+
+__device__ __forceinline__ bf16x8_t cat44(bf16x4_t a, bf16x4_t b) {
   return bf16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
@@ -51,38 +69,89 @@ __device__ __forceinline__ bf16x8_t acc_frag(const f32x16& x, int s) {
   return r;
 }
 
+// value of x in the other 32-lane half (lane ^ 32)
+__device__ __forceinline__ float half_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // row index (within a 32x32 C tile) of accumulator register i for lane half hh
 __device__ __forceinline__ int crow(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
 
-// ----------------------------------------------------------------------------
-// Stage a [64 rows][64] bf16 tile from global (row stride `gstride` elements) into
-// LDS, natural layout (dst[row*TSTR + c]) and/or transposed (dstT[c*TSTR + row]).
-// 256 threads, 2 x 16-byte chunks each.
+// ---------------------------------------------------------------- swizzled LDS image
+__device__ __forceinline__ int swz(int row) {
+  const int u = (row >> 1) & 7;
+  return ((u & 1) << 2) | (u & 2) | (u >> 2);  // bit0 <-> bit2 of (row>>1)&7
+}
+// element offset of 16-B chunk `ch` (0..7) of row `row`
+__device__ __forceinline__ int img_off(int row, int ch) { return row * 64 + ((ch ^ swz(row)) << 3); }
+
+// Lane-constant offsets. Row read of a 32-row operand block starting at row 32x:
+// lane (r, hh) reads row 32x + r, chunk 2kk + hh → offset 2048x + rowoff[kk].
+// Transposed read (k rows kb + 4hh + 8e + q, columns 32dt + 16(g&1) + 4p) for a
+// k-block starting at kb (multiple of 16): offset 64*kb + troff[e][dt].
+struct LaneOffs {
+  int row[4];
+  int tr[2][2];
+  __device__ __forceinline__ LaneOffs(int lane) {
+    const int r = lane & 31, hh = lane >> 5, g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) row[kk] = img_off(r, 2 * kk + hh);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = 32 * dt + 16 * (g & 1) + 4 * p;
+        tr[e][dt] = img_off(4 * hh + 8 * e + q, col >> 3) + (col & 7);
+      }
+  }
+};
+
+// operand fragment with k down the image's rows: k = kb + {4hh+0..3, 8+4hh+0..3}
+// (the acc_frag k order), column 32dt + (lane&31)
+__device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* img, const LaneOffs& lo, int kb, int dt) {
+  return cat44(tr4(img + 64 * kb + lo.tr[0][dt]), tr4(img + 64 * kb + lo.tr[1][dt]));
+}
+
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2): map
+// physical block id → logical id so that consecutive logical blocks (the q- or key-blocks
+// of one (b, h), which all stream the same K/V or Q/dO) share an XCD and its L2.
+__device__ __forceinline__ int xcd_block(int bid, int n) {
+  return (n & 7) ? bid : (bid & 7) * (n >> 3) + (bid >> 3);
+}
+
+// ---------------------------------------------------------------- tile staging
+// [64 rows][64] bf16 tile, global row stride `gstride` elements; 256 threads x 2 chunks
 struct TileRegs {
   uint4 v[2];
 };
+struct KV {
+  TileRegs k, v;
+};
+struct QD {
+  TileRegs q, d;
+  float rc;  // -lse/c (threads 0..63) or -delta (64..127) of the tile's rows
+};
 
-__device__ __forceinline__ void tile_load(TileRegs& r, const bf16_t* g, long gstride, int rows_valid) {
+__device__ __forceinline__ void tile_load(TileRegs& r, const bf16_t* g, long gstride) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = threadIdx.x + 256 * u;
-    const int row = c >> 3, col = (c & 7) * 8;
-    if (row < rows_valid) r.v[u] = *reinterpret_cast<const uint4*>(g + row * gstride + col);
-    else r.v[u] = make_uint4(0, 0, 0, 0);
+    r.v[u] = *reinterpret_cast<const uint4*>(g + (c >> 3) * gstride + (c & 7) * 8);
   }
 }
 
-__device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* dst, bf16_t* dstT) {
+__device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* img) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = threadIdx.x + 256 * u;
-    const int row = c >> 3, col = (c & 7) * 8;
-    if (dst) *reinterpret_cast<uint4*>(dst + row * TSTR + col) = r.v[u];
-    if (dstT) {
-      const bf16_t* e = reinterpret_cast<const bf16_t*>(&r.v[u]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dstT[(col + j) * TSTR + row] = e[j];
-    }
+    *reinterpret_cast<uint4*>(img + img_off(c >> 3, c & 7)) = r.v[u];
   }
 }
 
@@ -91,17 +160,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                                                        bf16_t* __restrict__ out,
                                                        float* __restrict__ lse, int T, int H,
                                                        float sc_log2) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 64 * TSTR];
-  bf16_t* Ks = lds;
-  bf16_t* Vt = lds + 64 * TSTR;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS];  // [buf][K,V]
   const int nqb = T / 128;
-  const int qb = nqb - 1 - (int)(blockIdx.x % nqb);  // heaviest causal blocks first
-  const int bh = blockIdx.x / nqb;
+  const int L = xcd_block(blockIdx.x, gridDim.x);
+  const int qb = nqb - 1 - L % nqb;  // heaviest causal blocks first
+  const int bh = L / nqb;
   const int b = bh / H, h = bh % H;
   const int C = H * HD;
   const long tok = 3L * C;
   const bf16_t* base = qkv + (long)b * T * tok + h * HD;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const LaneOffs lo(lane);
   const int q0 = qb * 128;
   const int qrow = q0 + 32 * w + r;
   bf16x8_t qf[4];
@@ -110,72 +179,85 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   f32x16 o[2] = {};
   float m_run = -INFINITY, l_run = 0.f;
   const int ntiles = (q0 + 128) / 64;
-  TileRegs kr, vr;
-  tile_load(kr, base + C, tok, 64);
-  tile_load(vr, base + 2 * C, tok, 64);
   const int wave_qmax = q0 + 32 * w + 31;
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    tile_store(kr, Ks, nullptr);
-    tile_store(vr, nullptr, Vt);
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      const long off = (long)(t + 1) * 64 * tok;
-      tile_load(kr, base + C + off, tok, 64);
-      tile_load(vr, base + 2 * C + off, tok, 64);
-    }
+  KV A, B;
+  auto load_kv = [&](KV& x, int t) {
+    const long off = (long)t * 64 * tok;
+    tile_load(x.k, base + C + off, tok);
+    tile_load(x.v, base + 2 * C + off, tok);
+  };
+  auto store_kv = [&](const KV& x, int t) {
+    bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
+    tile_store(x.k, d);
+    tile_store(x.v, d + TILE_ELEMS);
+  };
+  auto compute = [&](int t) {
+    const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
+    const bf16_t* Vs = Ks + TILE_ELEMS;
     const int kv0 = t * 64;
-    if (kv0 > wave_qmax) continue;  // fully masked for this wave (still joined the barriers)
-    f32x16 st[2];
+    if (kv0 <= wave_qmax) {
+      f32x16 st[2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      st[kt] = f32x16{};
+      for (int kt = 0; kt < 2; ++kt) {
+        st[kt] = f32x16{};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        st[kt] = mfma32(ld8(Ks + (32 * kt + r) * TSTR + 16 * kk + 8 * hh), qf[kk], st[kt]);
-    }
-    const bool diag = kv0 + 63 > q0 + 32 * w;
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float s = st[kt][i] * sc_log2;
-        if (diag && kv0 + 32 * kt + crow(i, hh) > qrow) s = -INFINITY;
-        st[kt][i] = s;
-        mt = fmaxf(mt, s);
+        for (int kk = 0; kk < 4; ++kk)
+          st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st[kt]);
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
-    float ls = 0.f;
+      if (kv0 + 63 > q0 + 32 * w) {  // diagonal tile: mask keys > query
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(st[kt][i] - m_new);
-        st[kt][i] = p;
-        ls += p;
+          for (int i = 0; i < 16; ++i)
+            if (kv0 + 32 * kt + crow(i, hh) > qrow) st[kt][i] = -INFINITY;
       }
-    ls += __shfl_xor(ls, 32, 64);
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
+      float mt = st[0][0];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, st[kt][i]);
+      mt = half_max(mt) * sc_log2;
+      const float m_new = fmaxf(m_run, mt);
+      const float alpha = fast_exp2(m_run - m_new);
+      float ls = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t pf = acc_frag(st[kt], s);
-        const int key = 32 * kt + 16 * s + 4 * hh;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16_t* vrow = Vt + (32 * dt + r) * TSTR + key;
-          o[dt] = mfma32(ld4x2(vrow, vrow + 8), pf, o[dt]);
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(fmaf(st[kt][i], sc_log2, -m_new));
+          st[kt][i] = p;
+          ls += p;
         }
-      }
+      l_run = l_run * alpha + half_sum(ls);
+      m_run = m_new;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8_t pf = acc_frag(st[kt], s);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(tr_frag(Vs, lo, 32 * kt + 16 * s, dt), pf, o[dt]);
+        }
+    }
+  };
+  // 2-deep register prefetch: tile t+2's loads are in flight during tiles t and t+1
+  auto step = [&](int t, KV& held, KV& next) {
+    if (t + 2 < ntiles) load_kv(next, t + 2);
+    compute(t);
+    if (t + 1 < ntiles) store_kv(held, t + 1);
+    __syncthreads();
+  };
+  load_kv(A, 0);
+  store_kv(A, 0);
+  load_kv(A, 1);  // ntiles >= 2
+  __syncthreads();
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, A, B);
+    if (t + 1 < ntiles) step(t + 1, B, A);
   }
   const float inv = 1.f / l_run;
   bf16_t* orow = out + ((long)b * T + qrow) * C + h * HD;
@@ -191,12 +273,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
 }
 
 // ============================================================================ backward
-// delta[bh][t] = sum_d dO[b,t,h,d] * O[b,t,h,d]   (one wave per (b, t), 4 heads' rows per block)
+// delta[bh][t] = sum_d dO[b,t,h,d] * O[b,t,h,d]   (one thread per (token, head) row)
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ o,
                                                            const bf16_t* __restrict__ dout,
                                                            float* __restrict__ delta, int BT,
                                                            int T, int H) {
-  // each thread handles one (token, head) row of 64 elements with 8 x 16B loads
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)BT * H) return;
   const long tokn = idx / H;
@@ -217,25 +298,24 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 // dK, dV: workgroup = 128 keys of one (b, h); wave owns 32 keys.
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     int T, int H, float sc_log2, float scale) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * 64 * TSTR];
-  __shared__ float s_lse[64], s_del[64];
-  bf16_t* Qs = lds;                 // [q][d]
-  bf16_t* Qt = lds + 64 * TSTR;     // [d][q]
-  bf16_t* Ds = lds + 128 * TSTR;    // dO [q][d]
-  bf16_t* Dt = lds + 192 * TSTR;    // dO^T [d][q]
+  // [buf][Q, dO] images, then per buf 64 x (-lse/c) and 64 x (-delta)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS + 2 * 2 * 64 * 2];
+  float* rowc = reinterpret_cast<float*>(lds + 4 * TILE_ELEMS);  // [buf][2][64]
   const int nkb = T / 128;
-  const int kb = (int)(blockIdx.x % nkb);
-  const int bh = blockIdx.x / nkb;
+  const int L = xcd_block(blockIdx.x, gridDim.x);
+  const int kb = L % nkb;  // kb 0 = most q tiles: heaviest first
+  const int bh = L / nkb;
   const int b = bh / H, h = bh % H;
   const int C = H * HD;
   const long tok = 3L * C;
   const bf16_t* base = qkv + (long)b * T * tok + h * HD;
   const bf16_t* dobase = dout + (long)b * T * C + h * HD;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const LaneOffs lo(lane);
   const int kv0 = kb * 128;
   const int key = kv0 + 32 * w + r;  // this lane's key (C-tile column)
   bf16x8_t kf[4], vf[4];
@@ -248,57 +328,85 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(
   const int t0 = kv0 / 64;
   const int ntiles = T / 64;
   const int wave_kmin = kv0 + 32 * w;
-  TileRegs qr, dr;
-  tile_load(qr, base + (long)t0 * 64 * tok, tok, 64);
-  tile_load(dr, dobase + (long)t0 * 64 * C, C, 64);
-  for (int t = t0; t < ntiles; ++t) {
+  const float inv_c = -1.f / sc_log2;
+  const float* lse_bh = lse + (long)bh * T;
+  const float* del_bh = delta + (long)bh * T;
+  QD A, B;
+  auto load_qd = [&](QD& x, int t) {
+    tile_load(x.q, base + (long)t * 64 * tok, tok);
+    tile_load(x.d, dobase + (long)t * 64 * C, C);
+    if (threadIdx.x < 128) {
+      const int i = t * 64 + (threadIdx.x & 63);
+      x.rc = threadIdx.x < 64 ? lse_bh[i] * inv_c : -del_bh[i];
+    }
+  };
+  auto store_qd = [&](const QD& x, int t) {
+    const int buf = (t - t0) & 1;
+    bf16_t* d = lds + buf * 2 * TILE_ELEMS;
+    tile_store(x.q, d);
+    tile_store(x.d, d + TILE_ELEMS);
+    if (threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = x.rc;
+  };
+  auto compute = [&](int t) {
+    const int cur = (t - t0) & 1;
     const int q0 = t * 64;
-    __syncthreads();
-    tile_store(qr, Qs, Qt);
-    tile_store(dr, Ds, Dt);
-    if (threadIdx.x < 64) {
-      s_lse[threadIdx.x] = lse[(long)bh * T + q0 + threadIdx.x];
-      s_del[threadIdx.x] = delta[(long)bh * T + q0 + threadIdx.x];
-    }
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      tile_load(qr, base + (long)(t + 1) * 64 * tok, tok, 64);
-      tile_load(dr, dobase + (long)(t + 1) * 64 * C, C, 64);
-    }
-    if (q0 + 63 < wave_kmin) continue;
-    const bool diag = q0 < wave_kmin + 31;
+    if (q0 + 63 >= wave_kmin) {
+      const bf16_t* Qs = lds + cur * 2 * TILE_ELEMS;
+      const bf16_t* Ds = Qs + TILE_ELEMS;
+      const float* nl = rowc + cur * 128;
+      const float* nd = nl + 64;
+      const bool diag = q0 < wave_kmin + 31;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      // S = Q K^T (rows q, cols = this wave's keys), dP = dO V^T
-      f32x16 s = {}, dp = {};
+      for (int qt = 0; qt < 2; ++qt) {
+        // S' = Q K^T - LSE/c ; dP' = dO V^T - delta   (rows q, cols = this wave's keys)
+        f32x16 s, dp;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        s = mfma32(ld8(Qs + (32 * qt + r) * TSTR + 16 * kk + 8 * hh), kf[kk], s);
-        dp = mfma32(ld8(Ds + (32 * qt + r) * TSTR + 16 * kk + 8 * hh), vf[kk], dp);
-      }
+        for (int g = 0; g < 4; ++g) {
+          const float4 a = *reinterpret_cast<const float4*>(nl + 32 * qt + 8 * g + 4 * hh);
+          const float4 d = *reinterpret_cast<const float4*>(nd + 32 * qt + 8 * g + 4 * hh);
+          s[4 * g] = a.x; s[4 * g + 1] = a.y; s[4 * g + 2] = a.z; s[4 * g + 3] = a.w;
+          dp[4 * g] = d.x; dp[4 * g + 1] = d.y; dp[4 * g + 2] = d.z; dp[4 * g + 3] = d.w;
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ql = 32 * qt + crow(i, hh);
-        float p = exp2f(s[i] * sc_log2 - s_lse[ql]);
-        if (diag && key > q0 + ql) p = 0.f;
-        s[i] = p;                        // P
-        dp[i] = p * (dp[i] - s_del[ql]);  // dS (wrt scaled scores)
-      }
-      // dV += P^T dO ; dK += dS^T Q   (P / dS registers as A operands, k = q)
+        for (int kk = 0; kk < 4; ++kk) {
+          s = mfma32(ld8(Qs + 2048 * qt + lo.row[kk]), kf[kk], s);
+          dp = mfma32(ld8(Ds + 2048 * qt + lo.row[kk]), vf[kk], dp);
+        }
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t pa = acc_frag(s, ks);
-        const bf16x8_t da = acc_frag(dp, ks);
-        const int qk = 32 * qt + 16 * ks + 4 * hh;
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(s[i] * sc_log2);
+          if (diag && key > q0 + 32 * qt + crow(i, hh)) p = 0.f;
+          s[i] = p;              // P
+          dp[i] = p * dp[i];     // dS (wrt scaled scores)
+        }
+        // dV += P^T dO ; dK += dS^T Q   (P / dS registers as A operands, k = q)
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16_t* drow = Dt + (32 * dt + r) * TSTR + qk;
-          const bf16_t* qrow = Qt + (32 * dt + r) * TSTR + qk;
-          dv[dt] = mfma32(pa, ld4x2(drow, drow + 8), dv[dt]);
-          dk[dt] = mfma32(da, ld4x2(qrow, qrow + 8), dk[dt]);
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8_t pa = acc_frag(s, ks);
+          const bf16x8_t da = acc_frag(dp, ks);
+          const int kbq = 32 * qt + 16 * ks;
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            dv[dt] = mfma32(pa, tr_frag(Ds, lo, kbq, dt), dv[dt]);
+            dk[dt] = mfma32(da, tr_frag(Qs, lo, kbq, dt), dk[dt]);
+          }
         }
       }
     }
+  };
+  auto step = [&](int t, QD& held, QD& next) {
+    if (t + 2 < ntiles) load_qd(next, t + 2);
+    compute(t);
+    if (t + 1 < ntiles) store_qd(held, t + 1);
+    __syncthreads();
+  };
+  load_qd(A, t0);
+  store_qd(A, t0);
+  load_qd(A, t0 + 1);  // t0 + 2 <= ntiles
+  __syncthreads();
+  for (int t = t0; t < ntiles; t += 2) {
+    step(t, A, B);
+    if (t + 1 < ntiles) step(t + 1, B, A);
   }
   // dV / dK tiles: rows = keys (registers), cols = d (lane)
 #pragma unroll
@@ -317,18 +425,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     int T, int H, float sc_log2, float scale) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[3 * 64 * TSTR];
-  bf16_t* Ks = lds;                // [key][d]
-  bf16_t* Kt = lds + 64 * TSTR;    // [d][key]
-  bf16_t* Vs = lds + 128 * TSTR;   // [key][d]
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS];  // [buf][K, V]
   const int nqb = T / 128;
-  const int qb = nqb - 1 - (int)(blockIdx.x % nqb);
-  const int bh = blockIdx.x / nqb;
+  const int L = xcd_block(blockIdx.x, gridDim.x);
+  const int qb = nqb - 1 - L % nqb;
+  const int bh = L / nqb;
   const int b = bh / H, h = bh % H;
   const int C = H * HD;
   const long tok = 3L * C;
   const bf16_t* base = qkv + (long)b * T * tok + h * HD;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const LaneOffs lo(lane);
   const int q0 = qb * 128;
   const int qrow = q0 + 32 * w + r;
   bf16x8_t qf[4], df[4];
@@ -337,52 +444,70 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     qf[kk] = ld8(base + (long)qrow * tok + 16 * kk + 8 * hh);
     df[kk] = ld8(dout + ((long)b * T + qrow) * C + h * HD + 16 * kk + 8 * hh);
   }
-  const float lq = lse[(long)bh * T + qrow];
-  const float dq_del = delta[(long)bh * T + qrow];
+  const float nlq = -lse[(long)bh * T + qrow] / sc_log2;
+  const float ndel = -delta[(long)bh * T + qrow];
   f32x16 dq[2] = {};
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
-  TileRegs kr, vr;
-  tile_load(kr, base + C, tok, 64);
-  tile_load(vr, base + 2 * C, tok, 64);
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    tile_store(kr, Ks, Kt);
-    tile_store(vr, Vs, nullptr);
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      const long off = (long)(t + 1) * 64 * tok;
-      tile_load(kr, base + C + off, tok, 64);
-      tile_load(vr, base + 2 * C + off, tok, 64);
-    }
+  KV A, B;
+  auto load_kv = [&](KV& x, int t) {
+    const long off = (long)t * 64 * tok;
+    tile_load(x.k, base + C + off, tok);
+    tile_load(x.v, base + 2 * C + off, tok);
+  };
+  auto store_kv = [&](const KV& x, int t) {
+    bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
+    tile_store(x.k, d);
+    tile_store(x.v, d + TILE_ELEMS);
+  };
+  auto compute = [&](int t) {
     const int kv0 = t * 64;
-    if (kv0 > wave_qmax) continue;
-    const bool diag = kv0 + 63 > q0 + 32 * w;
+    if (kv0 <= wave_qmax) {
+      const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
+      const bf16_t* Vs = Ks + TILE_ELEMS;
+      const bool diag = kv0 + 63 > q0 + 32 * w;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f32x16 st = {}, dpt = {};
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 st, dpt;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        st = mfma32(ld8(Ks + (32 * kt + r) * TSTR + 16 * kk + 8 * hh), qf[kk], st);
-        dpt = mfma32(ld8(Vs + (32 * kt + r) * TSTR + 16 * kk + 8 * hh), df[kk], dpt);
-      }
+        for (int i = 0; i < 16; ++i) {
+          st[i] = nlq;
+          dpt[i] = ndel;
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = exp2f(st[i] * sc_log2 - lq);
-        if (diag && kv0 + 32 * kt + crow(i, hh) > qrow) p = 0.f;
-        dpt[i] = p * (dpt[i] - dq_del);  // dS^T
-      }
+        for (int kk = 0; kk < 4; ++kk) {
+          st = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st);
+          dpt = mfma32(ld8(Vs + 2048 * kt + lo.row[kk]), df[kk], dpt);
+        }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t bfrag = acc_frag(dpt, s);
-        const int kk2 = 32 * kt + 16 * s + 4 * hh;
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(st[i] * sc_log2);
+          if (diag && kv0 + 32 * kt + crow(i, hh) > qrow) p = 0.f;
+          dpt[i] = p * dpt[i];  // dS^T
+        }
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16_t* krow = Kt + (32 * dt + r) * TSTR + kk2;
-          dq[dt] = mfma32(ld4x2(krow, krow + 8), bfrag, dq[dt]);
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8_t bfrag = acc_frag(dpt, s);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dq[dt] = mfma32(tr_frag(Ks, lo, 32 * kt + 16 * s, dt), bfrag, dq[dt]);
         }
       }
     }
+  };
+  auto step = [&](int t, KV& held, KV& next) {
+    if (t + 2 < ntiles) load_kv(next, t + 2);
+    compute(t);
+    if (t + 1 < ntiles) store_kv(held, t + 1);
+    __syncthreads();
+  };
+  load_kv(A, 0);
+  store_kv(A, 0);
+  load_kv(A, 1);  // ntiles >= 2
+  __syncthreads();
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, A, B);
+    if (t + 1 < ntiles) step(t + 1, B, A);
   }
   bf16_t* g = dqkv + ((long)b * T + qrow) * tok + h * HD;
 #pragma unroll
