@@ -183,6 +183,7 @@ class CoreWorker:
         self.exiting = False
         self.blocked_depth = 0
         self.task_events: list = []
+        self._events_flushed = 0.0
         self.gpu_ids = gpu_ids or []
         self.node_id = node_id
         self.namespace = namespace
@@ -306,7 +307,8 @@ class CoreWorker:
                         traceback.print_exc()
             try:
                 self._reap_idle_leases()
-                if self.task_events and self.mode == "worker":
+                if self.task_events and (self.mode == "worker" or len(self.task_events) > 4096
+                                         or time.monotonic() - self._events_flushed > 0.5):
                     self._flush_task_events()
             except Exception:
                 if not self._stopped:
@@ -930,6 +932,8 @@ class CoreWorker:
             refs = [ObjectRef(object_id_for_return(tid, i + 1), self.addr, _cw_obj=self)
                     for i in range(nret)]
         spec["_holders"] = holders
+        self.task_events.append((tid, name, time.time(), None, None, None, "PENDING_NODE_ASSIGNMENT",
+                                 P.NORMAL_TASK, self.job_id, 0, None))
         if self.local_mode:
             self._run_local(spec)
         else:
@@ -1455,6 +1459,8 @@ class CoreWorker:
             self.task_specs[tid] = spec
         refs = [] if streaming else [ObjectRef(object_id_for_return(tid, i + 1), self.addr,
                                                _cw_obj=self) for i in range(nret)]
+        self.task_events.append((tid, spec["name"], time.time(), None, None, actor_id,
+                                 "SUBMITTED_TO_WORKER", P.ACTOR_TASK, self.job_id, 0, None))
         self._subscribe_actor(actor_id)
         # wait for owned pending args (ordering preserved: we block the caller)
         pend = [oid for oid, owner, inline in encoded[1] if owner == self.addr and inline is None]
@@ -1573,6 +1579,8 @@ class CoreWorker:
         t0 = time.time()
         extra = {}
         name = spec.get("name") or "task"
+        self.task_events.append((tid, name, t0, None, os.getpid(), spec.get("actor_id"), "RUNNING",
+                                 spec["type"], spec.get("job"), spec.get("attempt", 0), None))
         try:
             if spec["type"] == P.ACTOR_CREATION_TASK:
                 returns = self._execute_actor_creation(spec)
@@ -1622,7 +1630,8 @@ class CoreWorker:
             self.current_task.spec = None
         self.task_events.append((tid, name, t0, time.time(), os.getpid(),
                                  spec.get("actor_id"), "FAILED" if extra.get("app_error")
-                                 else "FINISHED"))
+                                 else "FINISHED", spec["type"], spec.get("job"),
+                                 spec.get("attempt", 0), extra.get("exc_type")))
         self._send_reply(conn, reply_to, tid, returns, extra)
 
     def _apply_runtime_env(self, spec):
@@ -1798,6 +1807,7 @@ class CoreWorker:
         os._exit(0)
 
     def _flush_task_events(self):
+        self._events_flushed = time.monotonic()
         ev, self.task_events = self.task_events, []
         self.notify_raylet("task_events", ev)
 

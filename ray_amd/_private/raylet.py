@@ -192,7 +192,9 @@ class Raylet:
         self.pg_names = {}
         self.jobs = {}
         self.job_counter = 0
-        self.task_events = collections.deque(maxlen=100000)
+        self.task_events = collections.deque(maxlen=100000)  # terminal events (timeline)
+        self.task_table: "collections.OrderedDict[bytes, dict]" = collections.OrderedDict()
+        self.app_metrics: dict = {}  # pid -> metric snapshots (ray_amd.util.metrics)
         self.next_token = 1
         self.next_lease = 1
         self.dirty = True
@@ -969,8 +971,90 @@ class Raylet:
     def rpc_list_jobs(self, conn, rid):
         self.reply(conn, rid, True, list(self.jobs.values()))
 
+    _TASK_RANK = {"PENDING_ARGS_AVAIL": 0, "PENDING_NODE_ASSIGNMENT": 1, "SUBMITTED_TO_WORKER": 2,
+                  "RUNNING": 3, "FINISHED": 4, "FAILED": 4}
+    _TASK_TYPES = {P.NORMAL_TASK: "NORMAL_TASK", P.ACTOR_TASK: "ACTOR_TASK",
+                   P.ACTOR_CREATION_TASK: "ACTOR_CREATION_TASK"}
+
     def rpc_task_events(self, conn, rid, events):
-        self.task_events.extend(events)
+        """Task lifecycle events from owners (submission) and executors (running / done).
+        Merged per (task, attempt) into the state table behind `ray_amd.util.state`
+        (reference: core_worker/task_event_buffer.cc → gcs_task_manager.cc)."""
+        table = self.task_table
+        rank = self._TASK_RANK
+        for ev in events:
+            tid, name, t0, t1, pid, aid, status = ev[:7]
+            ttype, job, attempt, err = ev[7:11] if len(ev) >= 11 else (None, None, 0, None)
+            if t1 is not None:
+                self.task_events.append(ev)
+            key = (tid, attempt)
+            rec = table.get(key)
+            if rec is None:
+                rec = table[key] = {
+                    "task_id": tid.hex(), "attempt_number": attempt, "name": name,
+                    "func_or_class_name": name, "state": status,
+                    "job_id": job.hex() if isinstance(job, bytes) else job,
+                    "actor_id": aid.hex() if aid else None,
+                    "type": self._TASK_TYPES.get(ttype, "NORMAL_TASK"),
+                    "node_id": self.node_id.hex(), "worker_pid": None, "error_type": None,
+                    "creation_time_ms": int(t0 * 1000), "start_time_ms": None,
+                    "end_time_ms": None, "language": "PYTHON"}
+                if len(table) > 200000:
+                    table.popitem(last=False)
+            if rank.get(status, 0) >= rank.get(rec["state"], 0):
+                rec["state"] = status
+            if pid is not None:
+                rec["worker_pid"] = pid
+            if status == "RUNNING" or (t1 is not None and rec["start_time_ms"] is None):
+                rec["start_time_ms"] = int(t0 * 1000)
+            if t1 is not None:
+                rec["end_time_ms"] = int(t1 * 1000)
+                rec["error_type"] = err
+            if aid and not rec["actor_id"]:
+                rec["actor_id"] = aid.hex()
+
+    def rpc_metrics(self, conn, rid, pid, snapshot):
+        self.app_metrics[pid] = snapshot
+
+    def rpc_get_metrics(self, conn, rid):
+        """Application metric snapshots of every process + node/system series
+        (reference: metrics agent + ray_* system metrics in metric_defs.cc)."""
+        node = (("NodeId", self.node_id.hex()),)
+        states = collections.Counter(r["state"] for r in self.task_table.values())
+        actors = collections.Counter(a.state for a in self.actors.values())
+        workers = collections.Counter(w.state for w in self.workers.values())
+        tot = self.sched.cluster_total()
+        av = self.sched.cluster_available()
+        sysm = [
+            {"kind": "gauge", "name": "ray_tasks", "description": "Tasks by state",
+             "series": {node + (("State", k),): float(v) for k, v in states.items()}},
+            {"kind": "gauge", "name": "ray_actors", "description": "Actors by state",
+             "series": {node + (("State", k),): float(v) for k, v in actors.items()}},
+            {"kind": "gauge", "name": "ray_workers", "description": "Worker processes by state",
+             "series": {node + (("State", k),): float(v) for k, v in workers.items()}},
+            {"kind": "gauge", "name": "ray_object_store_memory",
+             "description": "Object store bytes in use",
+             "series": {node: float(self.store.used(-1))}},
+            {"kind": "gauge", "name": "ray_object_store_capacity",
+             "description": "Object store capacity bytes",
+             "series": {node: float(self.store.capacity(-1))}},
+            {"kind": "gauge", "name": "ray_object_store_num_objects",
+             "description": "Objects in the store", "series": {node: float(self.store.num_objects())}},
+            {"kind": "gauge", "name": "ray_resources_total", "description": "Node resources",
+             "series": {node + (("Name", k),): float(v) for k, v in tot.items()
+                        if "_group_" not in k}},
+            {"kind": "gauge", "name": "ray_resources_available",
+             "description": "Available node resources",
+             "series": {node + (("Name", k),): float(v) for k, v in av.items()
+                        if "_group_" not in k}},
+        ]
+        out = list(sysm)
+        for snap in self.app_metrics.values():
+            out.extend(snap)
+        self.reply(conn, rid, True, out)
+
+    def rpc_list_tasks(self, conn, rid):
+        self.reply(conn, rid, True, list(self.task_table.values()))
 
     def rpc_get_task_events(self, conn, rid):
         self.reply(conn, rid, True, list(self.task_events))

@@ -329,7 +329,8 @@ def timeline(filename=None):
     time.sleep(0.05)
     events = cw.call_raylet("get_task_events")
     trace = []
-    for tid, name, t0, t1, pid, actor_id, status in events:
+    for ev in events:
+        tid, name, t0, t1, pid, actor_id, status = ev[:7]
         trace.append({"cat": "task", "name": name, "ph": "X", "pid": pid, "tid": pid,
                       "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6,
                       "args": {"task_id": tid.hex(), "status": status,
