@@ -182,7 +182,7 @@ class CoreWorker:
         self.async_loop = None
         self.exiting = False
         self.blocked_depth = 0
-        self.task_events: list = []
+        self.task_events = collections.deque()  # append/popleft are atomic across threads
         self._events_flushed = 0.0
         self.gpu_ids = gpu_ids or []
         self.node_id = node_id
@@ -1808,8 +1808,10 @@ class CoreWorker:
 
     def _flush_task_events(self):
         self._events_flushed = time.monotonic()
-        ev, self.task_events = self.task_events, []
-        self.notify_raylet("task_events", ev)
+        q = self.task_events
+        ev = [q.popleft() for _ in range(len(q))]
+        if ev:
+            self.notify_raylet("task_events", ev)
 
     # ------------------------------------------------------------------ local mode
     def _run_local(self, spec):
@@ -1836,6 +1838,11 @@ class CoreWorker:
             self.io.stop()
         except Exception:
             pass
+        # the dispatcher may still be inside io.poll(): let it leave the native loop before the
+        # interpreter can finalize (and free the IOLoop) under it
+        d = getattr(self, "dispatcher", None)
+        if d is not None and d is not threading.current_thread():
+            d.join(timeout=2.0)
         try:
             os.unlink(self.addr)
         except OSError:

@@ -52,7 +52,7 @@ def test_gae_reference_matches_rllib_formula():
         acc = delta[t] + gamma * lam * acc
         adv[t] = acc
     a, vt = ref.gae(torch.tensor(r)[:, None], torch.tensor(v)[:, None], torch.zeros(T, 1),
-                    torch.tensor([last]), gamma, lam)
+                    torch.tensor([last], dtype=torch.float64), gamma, lam)
     assert np.allclose(a[:, 0].numpy(), adv)
     assert np.allclose(vt[:, 0].numpy(), adv + v)
 

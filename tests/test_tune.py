@@ -2,6 +2,7 @@
 test_sample.py)."""
 
 import os
+import time
 
 import pytest
 
@@ -90,6 +91,7 @@ def test_pbt_exploits(cluster, tmp_path):
         while step < 12:
             step += 1
             val += config["lr"]
+            time.sleep(0.05)  # keep the population concurrent (PBT compares live trials)
             d = os.path.join(config["tmp"], f"{os.getpid()}_{step}_{config['lr']}")
             os.makedirs(d, exist_ok=True)
             with open(os.path.join(d, "s"), "w") as fh:
