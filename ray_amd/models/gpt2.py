@@ -12,8 +12,12 @@ MI355X-first choices:
   hand-written kernels (ray_amd/ops/csrc).
 * Vocab padded 50257 → 50304 (multiple of 64/128) so the LM-head GEMM tiles
   cleanly on MFMA; padded columns are masked inside the fused cross-entropy.
-* Attention: fused causal flash attention (torch SDPA flash backend on ROCm)
-  — [B, H, T, 64] head layout straight from the QKV GEMM view.
+* Attention: our HIP MFMA causal flash attention (ops/csrc/attn.hip) reading the
+  packed QKV GEMM output directly.
+* Backward: split-K fp32 weight-gradient GEMMs and every parameter gradient
+  (weights, biases, LayerNorm) accumulated in place into the flat DDP gradient
+  buffer (no AccumulateGrad adds); the residual stream's two gradients are summed
+  inside the LayerNorm backward kernel (``LayerNorm.fork``).
 """
 
 from __future__ import annotations
@@ -71,6 +75,10 @@ class LayerNorm(nn.Module):
     def forward(self, x):
         return rf.layer_norm(x, self.weight, self.bias, self.eps)
 
+    def fork(self, x):
+        """(x for the residual add, LN(x)) — the residual grads are summed in the LN bwd."""
+        return rf.layer_norm_fork(x, self.weight, self.bias, self.eps)
+
 
 class Block(nn.Module):
     def __init__(self, cfg: GPT2Config):
@@ -91,14 +99,14 @@ class Block(nn.Module):
     def forward(self, x):
         B, T, C = x.shape
         H = self.n_head
-        h = self.ln_1(x)
-        qkv = F.linear(h, self.c_attn_w, self.c_attn_b)  # hipBLASLt GEMM + bias epilogue
+        x, h = self.ln_1.fork(x)
+        qkv = rf.linear(h, self.c_attn_w, self.c_attn_b)  # hipBLASLt GEMM + bias epilogue
         # HIP MFMA flash attention straight off the packed QKV layout (no permutes/copies)
         y = rf.causal_attention_qkv(qkv.view(B, T, 3, H, C // H)).reshape(B, T, C)
-        x = rf.bias_residual(F.linear(y, self.c_proj_w), self.c_proj_b, x)
-        h = self.ln_2(x)
-        a = rf.bias_gelu(F.linear(h, self.c_fc_w), self.c_fc_b)
-        x = rf.bias_residual(F.linear(a, self.mlp_proj_w), self.mlp_proj_b, x)
+        x = rf.bias_residual(rf.linear(y, self.c_proj_w), self.c_proj_b, x)
+        x, h = self.ln_2.fork(x)
+        a = rf.bias_gelu(rf.linear(h, self.c_fc_w), self.c_fc_b)
+        x = rf.bias_residual(rf.linear(a, self.mlp_proj_w), self.mlp_proj_b, x)
         return x
 
 

@@ -29,14 +29,15 @@ c_size_t = ctypes.c_size_t
 _SIGS = {
     "ra_layernorm_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
     "ra_layernorm_bwd_parts": [c_int],
-    "ra_layernorm_bwd": [c_void_p] * 9 + [c_int, c_int, c_int, c_void_p],
+    "ra_layernorm_bwd": [c_void_p] * 10 + [c_int, c_int, c_int, c_void_p],
     "ra_colsum": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "ra_layernorm_bwd_work": [c_int, c_int],
     "ra_colsum_work": [c_int, c_int],
     "ra_colsum_parts": [c_int],
     "ra_bias_gelu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
-    "ra_bias_gelu_bwd": [c_void_p] * 6 + [c_int, c_int, c_void_p],
-    "ra_colsum_bf16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "ra_bias_gelu_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_void_p],
+    "ra_colsum_bf16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+    "ra_splitk_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p],
     "ra_bias_residual": [c_void_p] * 4 + [c_long, c_int, c_void_p],
     "ra_xent_fwd": [c_void_p] * 4 + [c_int, c_int, c_int, c_long, c_void_p],
     "ra_xent_bwd": [c_void_p] * 4 + [c_float, c_void_p, c_int, c_int, c_int, c_long, c_void_p],

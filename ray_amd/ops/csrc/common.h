@@ -112,30 +112,40 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ p
     scratch[(size_t)blockIdx.y * D + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
-template <bool OUT_BF16>
+// ACC: out += sum (parameter gradients accumulated in place into the flat grad buffer,
+// so autograd never launches a separate AccumulateGrad add)
+template <bool OUT_BF16, bool ACC>
 __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ scratch, void* out,
                                                      int S, int D) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= D) return;
   float s = 0.f;
   for (int i = 0; i < S; ++i) s += scratch[(size_t)i * D + c];
-  if (OUT_BF16) reinterpret_cast<uint16_t*>(out)[c] = __builtin_bit_cast(uint16_t, (__bf16)s);
-  else reinterpret_cast<float*>(out)[c] = s;
+  if (OUT_BF16) {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out) + c;
+    if (ACC) s += (float)__builtin_bit_cast(__bf16, *o);
+    *o = __builtin_bit_cast(uint16_t, (__bf16)s);
+  } else {
+    float* o = reinterpret_cast<float*>(out) + c;
+    *o = ACC ? *o + s : s;
+  }
 }
 
-// scratch must hold kColsumSplits * D floats.
+// flags: bit0 = bf16 output, bit1 = accumulate into out. scratch: kColsumSplits * D floats.
+enum { kColsumBF16 = 1, kColsumAcc = 2 };
 static inline void colsum_launch(const float* part, float* scratch, void* out, int P, int D,
-                                 bool out_bf16, hipStream_t st) {
+                                 int flags, hipStream_t st) {
   int S = (P + 15) / 16;
   if (S > kColsumSplits) S = kColsumSplits;
   if (S < 1) S = 1;
   hipLaunchKernelGGL(colsum_stage1, dim3((D + 63) / 64, S), dim3(256), 0, st, part, scratch, P, D);
-  if (out_bf16)
-    hipLaunchKernelGGL(colsum_stage2<true>, dim3((D + 255) / 256), dim3(256), 0, st, scratch, out,
-                       S, D);
-  else
-    hipLaunchKernelGGL(colsum_stage2<false>, dim3((D + 255) / 256), dim3(256), 0, st, scratch,
-                       out, S, D);
+  const dim3 g((D + 255) / 256), b(256);
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((colsum_stage2<false, false>), g, b, 0, st, scratch, out, S, D); break;
+    case 1: hipLaunchKernelGGL((colsum_stage2<true, false>), g, b, 0, st, scratch, out, S, D); break;
+    case 2: hipLaunchKernelGGL((colsum_stage2<false, true>), g, b, 0, st, scratch, out, S, D); break;
+    default: hipLaunchKernelGGL((colsum_stage2<true, true>), g, b, 0, st, scratch, out, S, D);
+  }
 }
 
 }  // namespace

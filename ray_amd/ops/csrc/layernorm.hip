@@ -72,8 +72,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 template <int VPL>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
-    const float* __restrict__ mean, const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-    float* __restrict__ dg_part, float* __restrict__ db_part, int N, int D) {
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ dg_part,
+    float* __restrict__ db_part, int N, int D) {
+  // dres (optional): gradient arriving at x through the residual branch, added into dx here
+  // so the two gradients of the residual stream are summed in this pass (no separate add)
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][D]
   float* sdg = lds;
   float* sdb = lds + D;
@@ -125,6 +128,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (wd[i][j] - c1 - xh[i][j] * c2) * rs;
+        if (dres) {
+          float r[4];
+          unpack4(*reinterpret_cast<const uint2*>(dres + (size_t)row * D + col), r);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] += r[j];
+        }
         *reinterpret_cast<uint2*>(dx + (size_t)row * D + col) = pack4(o);
       }
     }
@@ -186,8 +195,10 @@ RA_EXPORT long ra_layernorm_bwd_work(int N, int D) {
 }
 
 RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
-                               const float* rstd, void* dx, void* dg, void* db, float* work,
-                               int N, int D, int out_bf16, hipStream_t st) {
+                               const float* rstd, const void* dres, void* dx, void* dg, void* db,
+                               float* work,
+                               int N, int D, int flags, hipStream_t st) {
+  // flags: bit0 bf16 dg/db, bit1 accumulate dg/db into the (flat) gradient buffers
   if (D % 4 != 0) return hipErrorInvalidValue;
   const int P = ra_layernorm_bwd_parts(N);
   float* dgp = work;
@@ -196,17 +207,18 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
   const size_t lds = 2 * (size_t)D * sizeof(float);
 #define L(V)                                                                                  \
   hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(P), dim3(256), lds, st, (const bf16_t*)dy,        \
-                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (bf16_t*)dx, dgp, dbp, N, D)
+                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,      \
+                     (bf16_t*)dx, dgp, dbp, N, D)
   LN_DISPATCH(L)
 #undef L
-  colsum_launch(dgp, scr, dg, P, D, out_bf16 != 0, st);
-  colsum_launch(dbp, scr + (size_t)kColsumSplits * D, db, P, D, out_bf16 != 0, st);
+  colsum_launch(dgp, scr, dg, P, D, flags, st);
+  colsum_launch(dbp, scr + (size_t)kColsumSplits * D, db, P, D, flags, st);
   return hipGetLastError();
 }
 
 // out[c] = sum_p part[p][c]; scratch: kColsumSplits * D floats.
-RA_EXPORT int ra_colsum(const float* part, float* scratch, void* out, int P, int D, int out_bf16,
+RA_EXPORT int ra_colsum(const float* part, float* scratch, void* out, int P, int D, int flags,
                         hipStream_t st) {
-  colsum_launch(part, scratch, out, P, D, out_bf16 != 0, st);
+  colsum_launch(part, scratch, out, P, D, flags, st);
   return hipGetLastError();
 }

@@ -18,36 +18,92 @@ def _hip(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+# --------------------------------------------------------------------- flat-grad sinks
+# Parameters managed by ray_amd.parallel.flat keep .grad as a view into one flat bf16
+# buffer and are tagged ``_ra_direct_grad``. Our backward kernels then ACCUMULATE their
+# parameter gradients straight into that view (fp32 math, one HBM pass) and return None,
+# so autograd never allocates a gradient tensor nor launches an AccumulateGrad add; the
+# DDP bucket hook (``_ra_grad_ready``) is signalled exactly once per backward instead.
+def _grad_sink(p):
+    if p is not None and getattr(p, "_ra_direct_grad", False) and p.grad is not None:
+        return p.grad
+    return None
+
+
+def _grad_done(p):
+    cb = getattr(p, "_ra_grad_ready", None)
+    if cb is not None:
+        cb()
+
+
 # --------------------------------------------------------------------- LayerNorm
+def _ln_forward(x, w, b, eps):
+    D = x.shape[-1]
+    x2 = x.contiguous().view(-1, D)
+    N = x2.shape[0]
+    y = torch.empty_like(x2)
+    mean = torch.empty(N, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(N, device=x.device, dtype=torch.float32)
+    check(_lib.lib().ra_layernorm_fwd(ptr(x2), ptr(w), ptr(b), ptr(y), ptr(mean), ptr(rstd),
+                                      N, D, eps, stream_ptr()), "layernorm_fwd")
+    return x2, y, mean, rstd
+
+
+def _ln_backward(dy, x2, w, b, mean, rstd, dres=None):
+    """dx (+ dres) and the weight/bias grads (into flat sinks when available)."""
+    N, D = x2.shape
+    dy2 = dy.contiguous().view(N, D)
+    L = _lib.lib()
+    work = torch.empty(L.ra_layernorm_bwd_work(N, D), device=dy.device, dtype=torch.float32)
+    dx = torch.empty_like(x2)
+    sw, sb = _grad_sink(w), _grad_sink(b)
+    direct = sw is not None and sb is not None
+    dw = sw if direct else torch.empty_like(w)
+    db = sb if direct else torch.empty_like(w)
+    flags = (1 if w.dtype == torch.bfloat16 else 0) | (2 if direct else 0)
+    dr = None if dres is None else dres.contiguous().view(N, D)
+    check(L.ra_layernorm_bwd(ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dr), ptr(dx),
+                             ptr(dw), ptr(db), ptr(work), N, D, flags, stream_ptr()),
+          "layernorm_bwd")
+    if direct:
+        _grad_done(w)
+        _grad_done(b)
+        return dx, None, None
+    return dx, dw, db
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, eps):
-        D = x.shape[-1]
-        x2 = x.contiguous().view(-1, D)
-        N = x2.shape[0]
-        y = torch.empty_like(x2)
-        mean = torch.empty(N, device=x.device, dtype=torch.float32)
-        rstd = torch.empty(N, device=x.device, dtype=torch.float32)
-        check(_lib.lib().ra_layernorm_fwd(ptr(x2), ptr(w), ptr(b), ptr(y), ptr(mean), ptr(rstd),
-                                          N, D, eps, stream_ptr()), "layernorm_fwd")
+        x2, y, mean, rstd = _ln_forward(x, w, b, eps)
         ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.b = b
         ctx.shape = x.shape
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
-        N, D = x2.shape
-        dy2 = dy.contiguous().view(N, D)
-        L = _lib.lib()
-        work = torch.empty(L.ra_layernorm_bwd_work(N, D), device=dy.device, dtype=torch.float32)
-        dx = torch.empty_like(x2)
-        dw = torch.empty_like(w)
-        db = torch.empty_like(w)
-        check(L.ra_layernorm_bwd(ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dx),
-                                 ptr(dw), ptr(db), ptr(work), N, D,
-                                 1 if w.dtype == torch.bfloat16 else 0, stream_ptr()),
-              "layernorm_bwd")
+        dx, dw, db = _ln_backward(dy, x2, w, ctx.b, mean, rstd)
+        return dx.view(ctx.shape), dw, db, None
+
+
+class _LayerNormFork(torch.autograd.Function):
+    """(x, LN(x)) for a pre-LN residual block: the residual stream's two gradients (through
+    the skip connection and through LN) are summed inside the LN backward kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x2, y, mean, rstd = _ln_forward(x, w, b, eps)
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.b = b
+        ctx.shape = x.shape
+        return x.view_as(x), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dskip, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _ln_backward(dy, x2, w, ctx.b, mean, rstd, dres=dskip)
         return dx.view(ctx.shape), dw, db, None
 
 
@@ -55,6 +111,13 @@ def layer_norm(x, weight, bias, eps=1e-5):
     if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 4 == 0:
         return _LayerNorm.apply(x, weight, bias, eps)
     return ref.layer_norm(x, weight, bias, eps)
+
+
+def layer_norm_fork(x, weight, bias, eps=1e-5):
+    """Returns (x_skip, layer_norm(x)); use x_skip for the residual add."""
+    if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 4 == 0:
+        return _LayerNormFork.apply(x, weight, bias, eps)
+    return x, ref.layer_norm(x, weight, bias, eps)
 
 
 # --------------------------------------------------------------------- bias + GELU
@@ -66,20 +129,27 @@ class _BiasGelu(torch.autograd.Function):
         y = torch.empty_like(h2)
         check(_lib.lib().ra_bias_gelu_fwd(ptr(h2), ptr(bias), ptr(y), h2.shape[0], F_,
                                           stream_ptr()), "bias_gelu_fwd")
-        ctx.save_for_backward(h2, bias)
+        ctx.save_for_backward(h2)
+        ctx.bias = bias
         ctx.shape = h.shape
         return y.view(h.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        h2, bias = ctx.saved_tensors
+        (h2,) = ctx.saved_tensors
+        bias = ctx.bias
         N, F_ = h2.shape
         L = _lib.lib()
         work = torch.empty(L.ra_colsum_work(N, F_), device=dy.device, dtype=torch.float32)
         dh = torch.empty_like(h2)
-        db = torch.empty_like(bias)
+        sink = _grad_sink(bias)
+        db = sink if sink is not None else torch.empty_like(bias)
         check(L.ra_bias_gelu_bwd(ptr(dy.contiguous()), ptr(h2), ptr(bias), ptr(dh), ptr(db),
-                                 ptr(work), N, F_, stream_ptr()), "bias_gelu_bwd")
+                                 ptr(work), N, F_, 1 if sink is not None else 0, stream_ptr()),
+              "bias_gelu_bwd")
+        if sink is not None:
+            _grad_done(bias)
+            return dh.view(ctx.shape), None
         return dh.view(ctx.shape), db
 
 
@@ -90,13 +160,27 @@ def bias_gelu(h, bias):
 
 
 # --------------------------------------------------------------------- bias + residual
-def _colsum_bf16(x2):
+def _colsum_bf16(x2, out=None):
+    """Column sum of [N, F] bf16 -> [F] bf16; with `out` given, accumulate into it."""
     N, F_ = x2.shape
     L = _lib.lib()
     work = torch.empty(L.ra_colsum_work(N, F_), device=x2.device, dtype=torch.float32)
-    out = torch.empty(F_, device=x2.device, dtype=x2.dtype)
-    check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_, stream_ptr()), "colsum")
+    acc = out is not None
+    if out is None:
+        out = torch.empty(F_, device=x2.device, dtype=x2.dtype)
+    check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_, 1 if acc else 0, stream_ptr()),
+          "colsum")
     return out
+
+
+def _bias_grad(dy2, bias):
+    """bias gradient: accumulated into the flat sink (returns None) or a new tensor."""
+    sink = _grad_sink(bias)
+    if sink is not None:
+        _colsum_bf16(dy2, out=sink)
+        _grad_done(bias)
+        return None
+    return _colsum_bf16(dy2)
 
 
 class _BiasResidual(torch.autograd.Function):
@@ -108,12 +192,14 @@ class _BiasResidual(torch.autograd.Function):
         y = torch.empty_like(h2)
         check(_lib.lib().ra_bias_residual(ptr(h2), ptr(bias), ptr(r2), ptr(y), h2.shape[0], F_,
                                           stream_ptr()), "bias_residual")
-        ctx.has_bias = bias is not None
+        ctx.bias = bias
         return y.view(h.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        db = _colsum_bf16(dy.contiguous().view(-1, dy.shape[-1])) if ctx.has_bias else None
+        db = None
+        if ctx.bias is not None and ctx.needs_input_grad[1]:
+            db = _bias_grad(dy.contiguous().view(-1, dy.shape[-1]), ctx.bias)
         return dy, db, dy
 
 
@@ -121,6 +207,65 @@ def bias_residual(h, bias, res):
     if _hip(h) and h.dtype == torch.bfloat16 and h.shape[-1] % 8 == 0:
         return _BiasResidual.apply(h, bias, res)
     return ref.bias_residual(h, bias, res)
+
+
+# --------------------------------------------------------------------- linear (split-K wgrad)
+def _splitk(M: int, N: int, K: int) -> int:
+    """Token slices for the wgrad GEMM: enough (N/128)*(K/128) tiles x S to fill 256 CUs
+    twice, each slice >= 1024 tokens (measured best S: qkv/proj 8, fc/mlp_proj 4)."""
+    tiles = max(1, (N // 128) * (K // 128))
+    S = 1
+    while S < 8 and S * tiles < 512 and M % (2 * S) == 0 and M // (2 * S) >= 1024:
+        S *= 2
+    return S
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.b = b
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        K, N = x.shape[-1], w.shape[0]
+        x2 = x.reshape(-1, K)
+        dy2 = dy.reshape(-1, N)
+        M = x2.shape[0]
+        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            sink = _grad_sink(w)
+            S = _splitk(M, N, K)
+            if S > 1 or sink is not None:
+                # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into
+                # the flat gradient) by one HIP pass
+                part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K),
+                                 out_dtype=torch.float32)
+                target = sink if sink is not None else torch.empty_like(w)
+                check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(target),
+                                                 1 if sink is not None else 0, stream_ptr()),
+                      "splitk_accum")
+                if sink is None:
+                    dw = target
+                else:
+                    _grad_done(w)
+            else:
+                dw = dy2.t() @ x2
+        if ctx.b is not None and ctx.needs_input_grad[2]:
+            db = _bias_grad(dy2, ctx.b)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    """y = x @ w^T + b with the MI355X backward (split-K fp32 wgrad, in-place flat-grad
+    accumulation). Same numerics contract as F.linear."""
+    if _hip(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and \
+            (w.shape[0] * w.shape[1]) % 4 == 0:
+        return _Linear.apply(x, w, b)
+    return torch.nn.functional.linear(x, w, b)
 
 
 # --------------------------------------------------------------------- flash attention

@@ -24,6 +24,7 @@ parallel_strategy="flat")`` uses by default on GPU.
 
 from __future__ import annotations
 
+import functools
 import math
 from typing import Iterable
 
@@ -79,6 +80,8 @@ class FlatParams:
                 self.p16[off:off + k].copy_(self.p32[off:off + k])
                 p.data = self.p16[off:off + k].view(p.shape)
                 p.grad = self.g[off:off + k].view(p.shape)
+                # ray_amd.ops backward kernels may accumulate straight into p.grad
+                p._ra_direct_grad = True
 
     def params(self) -> list[torch.nn.Parameter]:
         return [p for _, p in self.order]
@@ -94,7 +97,8 @@ class FlatParams:
 class FlatDDP:
     """Bucketed, backward-overlapped gradient all-reduce over the flat grad buffer."""
 
-    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0):
+    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0,
+                 always_hook: bool = False):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -118,13 +122,18 @@ class FlatDDP:
             sizes.append(sum(1 for x in self.param_bucket if x == b))
         self.bucket_sizes = sizes
         self._ready = [0] * len(self.buckets)
+        self._seen = [False] * len(flat.order)
         self._works = []
         self._hooks = []
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 or (always_hook and dist.is_initialized())
         self.sync = True  # False inside gradient-accumulation micro-steps (no_sync)
         if self.enabled:
             for i, (_, p) in enumerate(flat.order):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+                hook = self._make_hook(i)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                # direct-accumulating ops (ray_amd.ops.functional) bypass AccumulateGrad and
+                # signal readiness through this callback instead
+                p._ra_grad_ready = functools.partial(hook, p)
         # bucket broadcast of initial weights so every rank starts identical
         if self.enabled:
             dist.broadcast(flat.p32, src=0, group=group)
@@ -135,8 +144,11 @@ class FlatDDP:
         b = self.param_bucket[i]
 
         def hook(_p):
-            if not self.sync:
+            # a param can be signalled twice per backward (a direct-accumulating op, then the
+            # AccumulateGrad post-hook which PyTorch also runs for a None grad): count once
+            if not self.sync or self._seen[i]:
                 return
+            self._seen[i] = True
             self._ready[b] += 1
             if self._ready[b] == self.bucket_sizes[b]:
                 s, e = self.buckets[b]
@@ -158,6 +170,7 @@ class FlatDDP:
                 dist.all_reduce(self.flat.g[s:e], group=self.group)
         self._works.clear()
         self._ready = [0] * len(self.buckets)
+        self._seen = [False] * len(self.flat.order)
 
     @property
     def grad_scale(self) -> float:
