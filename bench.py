@@ -31,12 +31,50 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gpt2", choices=["gpt2", "ppo"])
-    ap.add_argument("--micro-batch", type=int, default=16)
+    ap.add_argument("--micro-batch", type=int, default=64,
+                    help="per-GPU sequences; 64 x 1024 tokens x 8 GPUs = 524k tokens, the GPT-3 "
+                         "Small global batch")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--model", default="small")
+    ap.add_argument("--tunableop", default="auto", choices=["off", "tune", "auto"],
+                    help="PyTorch TunableOp GEMM selection: 'tune' benchmarks every hipBLASLt/"
+                         "rocBLAS solution per GEMM shape during warmup and writes "
+                         "profiles/tunableop/<config>.csv; 'auto' uses that file if present")
     return ap.parse_args()
+
+
+def _setup_tunableop(args, rank):
+    """Per-shape GEMM kernel selection (TunableOp) from a committed results file.
+
+    TunableOp's validators pin the ROCm/hipBLASLt versions and the gfx arch, so a file
+    tuned on this image's MI355X applies to every rank (each gets its own copy: the
+    library keys result files by device)."""
+    import shutil
+
+    import torch
+
+    if args.tunableop == "off":
+        return None
+    tdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "tunableop")
+    name = f"gpt2_{args.model}_mb{args.micro_batch}_t{args.seq_len}.csv"
+    src = os.path.join(tdir, name)
+    if args.tunableop == "auto" and not os.path.exists(src):
+        return None
+    os.makedirs("/tmp/ray_amd_tunableop", exist_ok=True)
+    dst = f"/tmp/ray_amd_tunableop/{os.getpid()}_{rank}_{name}"
+    if os.path.exists(src):
+        shutil.copyfile(src, dst)
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(args.tunableop == "tune")
+    torch.cuda.tunable.set_filename(dst, insert_device_ordinal=False)
+    if os.path.exists(dst):
+        torch.cuda.tunable.read_file(dst)
+    if args.tunableop == "tune":
+        torch.cuda.tunable.set_max_tuning_duration(30)
+        torch.cuda.tunable.set_max_tuning_iterations(20)
+    return (dst, src) if args.tunableop == "tune" else None
 
 
 def bench_gpt2(args):
@@ -53,6 +91,7 @@ def bench_gpt2(args):
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    tuned = _setup_tunableop(args, rank)
     cfg = getattr(GPT2Config, args.model)()
     tr = GPT2Trainer(cfg, args.micro_batch, args.seq_len, dev, bucket_mb=args.bucket_mb,
                      total_steps=args.warmup + args.steps, grad_accum=args.grad_accum,
@@ -68,6 +107,17 @@ def bench_gpt2(args):
     for i in range(args.warmup):
         tr.step(batches(i))
     torch.cuda.synchronize()
+    if tuned is not None and rank == 0:
+        import shutil
+
+        os.makedirs(os.path.dirname(tuned[1]), exist_ok=True)
+        with open(tuned[1], "w") as f:  # TunableOp results-file format
+            for k, v in torch.cuda.tunable.get_validators():
+                f.write(f"Validator,{k},{v}\n")
+            for op, params, kernel, t in torch.cuda.tunable.get_results():
+                f.write(f"{op},{params},{kernel},{t}\n")
+        torch.cuda.tunable.tuning_enable(False)
+        shutil  # noqa: B018
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -111,6 +161,7 @@ def bench_gpt2(args):
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{world}",
                 "bucket_mb": args.bucket_mb,
+                "gemm_selection": "tunableop" if torch.cuda.tunable.is_enabled() else "heuristic",
             },
             "model_tflops_per_gpu": round(flops / dt / world / 1e12, 1),
             "final_loss": round(loss, 4),

@@ -96,18 +96,24 @@ class Block(nn.Module):
         self.mlp_proj_w = nn.Parameter(torch.empty(C, 4 * C))
         self.mlp_proj_b = nn.Parameter(torch.zeros(C))
 
-    def forward(self, x):
-        B, T, C = x.shape
-        H = self.n_head
-        x, h = self.ln_1.fork(x)
+    def attn(self, h):
+        """Attention sub-block on the normalised input; returns the projection output
+        WITHOUT its bias (added by the fused residual+LayerNorm seam)."""
+        B, T, C = h.shape
         qkv = rf.linear(h, self.c_attn_w, self.c_attn_b)  # hipBLASLt GEMM + bias epilogue
         # HIP MFMA flash attention straight off the packed QKV layout (no permutes/copies)
-        y = rf.causal_attention_qkv(qkv.view(B, T, 3, H, C // H)).reshape(B, T, C)
-        x = rf.bias_residual(rf.linear(y, self.c_proj_w), self.c_proj_b, x)
-        x, h = self.ln_2.fork(x)
+        y = rf.causal_attention_qkv(qkv.view(B, T, 3, self.n_head, C // self.n_head))
+        return rf.linear(y.reshape(B, T, C), self.c_proj_w)
+
+    def mlp(self, h):
         a = rf.bias_gelu(rf.linear(h, self.c_fc_w), self.c_fc_b)
-        x = rf.bias_residual(rf.linear(a, self.mlp_proj_w), self.mlp_proj_b, x)
-        return x
+        return rf.linear(a, self.mlp_proj_w)
+
+    def forward(self, x):
+        x, h = self.ln_1.fork(x)
+        x = rf.bias_residual(self.attn(h), self.c_proj_b, x)
+        x, h = self.ln_2.fork(x)
+        return rf.bias_residual(self.mlp(h), self.mlp_proj_b, x)
 
 
 class GPT2(nn.Module):
@@ -143,10 +149,17 @@ class GPT2(nn.Module):
         B, T = idx.shape
         pos = torch.arange(T, device=idx.device)
         x = F.embedding(idx, self.wte) + F.embedding(pos, self.wpe)[None]
-        for blk in self.h:
-            x = blk(x)
-        x = self.ln_f(x)
-        logits = F.linear(x, self.wte)  # tied LM head, [B, T, padded_vocab]
+        # Pre-LN seams fused: every "x += sub_block(h) + bias; h = LN(x)" is ONE kernel
+        # forward and ONE kernel backward (residual grads, LN grads and the projection-bias
+        # grad together) — see ops.functional.residual_layer_norm.
+        x, h = self.h[0].ln_1.fork(x)
+        for i, blk in enumerate(self.h):
+            x, h = rf.residual_layer_norm(blk.attn(h), blk.c_proj_b, x, blk.ln_2.weight,
+                                          blk.ln_2.bias, blk.ln_2.eps)
+            nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
+            x, h = rf.residual_layer_norm(blk.mlp(h), blk.mlp_proj_b, x, nxt.weight, nxt.bias,
+                                          nxt.eps)
+        logits = F.linear(h, self.wte)  # tied LM head on ln_f(x), [B, T, padded_vocab]
         if targets is None:
             return logits[..., : self.cfg.vocab_size]
         return rf.cross_entropy(logits, targets, self.cfg.vocab_size)

@@ -29,7 +29,8 @@ c_size_t = ctypes.c_size_t
 _SIGS = {
     "ra_layernorm_fwd": [c_void_p] * 6 + [c_int, c_int, c_float, c_void_p],
     "ra_layernorm_bwd_parts": [c_int],
-    "ra_layernorm_bwd": [c_void_p] * 10 + [c_int, c_int, c_int, c_void_p],
+    "ra_layernorm_bwd": [c_void_p] * 11 + [c_int, c_int, c_int, c_void_p],
+    "ra_residual_layernorm_fwd": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
     "ra_colsum": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "ra_layernorm_bwd_work": [c_int, c_int],
     "ra_colsum_work": [c_int, c_int],

@@ -11,8 +11,13 @@
 // workload: release/train_tests + train/examples GPT-2 DDP).
 #include "common.h"
 
-template <int VPL>
+// RES: the row is x = h + bias + skip (pre-LN residual add of the previous sub-block,
+// fused: x is computed once, written once (the next residual input) and normalised)
+template <int VPL, bool RES>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ rbias,
+                                                     const bf16_t* __restrict__ skip,
+                                                     bf16_t* __restrict__ xout,
                                                      const bf16_t* __restrict__ g,
                                                      const bf16_t* __restrict__ b,
                                                      bf16_t* __restrict__ y,
@@ -30,6 +35,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
     const int col = (i * 64 + lane) * 4;
     if (col < D) {
       unpack4(*reinterpret_cast<const uint2*>(xr + col), v[i]);
+      if (RES) {
+        float sk[4], bb[4] = {0.f, 0.f, 0.f, 0.f};
+        unpack4(*reinterpret_cast<const uint2*>(skip + (size_t)row * D + col), sk);
+        if (rbias) unpack4(*reinterpret_cast<const uint2*>(rbias + col), bb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] += bb[j] + sk[j];
+        const uint2 packed = pack4(v[i]);
+        *reinterpret_cast<uint2*>(xout + (size_t)row * D + col) = packed;
+        unpack4(packed, v[i]);  // normalise exactly the bf16 values the next layer sees
+      }
     } else {
       v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
     }
@@ -69,72 +84,86 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int VPL>
+// Backward. dres (optional): gradient reaching x through the skip connection, added into
+// dx here (the residual stream's two gradients summed in this pass). NP = 3 also emits
+// the column sums of dx itself: the bias gradient of the residual add that produced x.
+// Each wave handles two rows per iteration (twice the loads in flight per wave).
+template <int VPL, int NP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
     const float* __restrict__ mean, const float* __restrict__ rstd,
-    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ dg_part,
-    float* __restrict__ db_part, int N, int D) {
-  // dres (optional): gradient arriving at x through the residual branch, added into dx here
-  // so the two gradients of the residual stream are summed in this pass (no separate add)
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][D]
-  float* sdg = lds;
-  float* sdb = lds + D;
-  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) lds[i] = 0.f;
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N,
+    int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [NP][D]
+  for (int i = threadIdx.x; i < NP * D; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  float gg[VPL][4], adg[VPL][4], adb[VPL][4];
+  float gg[VPL][4], acc[NP][VPL][4];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int col = (i * 64 + lane) * 4;
     if (col < D) unpack4(*reinterpret_cast<const uint2*>(g + col), gg[i]);
     else gg[i][0] = gg[i][1] = gg[i][2] = gg[i][3] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) adg[i][j] = adb[i][j] = 0.f;
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[k][i][j] = 0.f;
   }
   const float invD = 1.f / (float)D;
-  for (int row = blockIdx.x * 4 + w; row < N; row += gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[VPL][4], wd[VPL][4];
-    float s1 = 0.f, s2 = 0.f;
+  const int stride = gridDim.x * 4;
+  for (int r0 = blockIdx.x * 4 + w; r0 < N; r0 += 2 * stride) {
+    const int rows[2] = {r0, r0 + stride};
+    float xv[2][VPL][4], dv[2][VPL][4], rv[2][VPL][4];
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      float xv[4], dv[4];
-      if (col < D) {
-        unpack4(*reinterpret_cast<const uint2*>(x + (size_t)row * D + col), xv);
-        unpack4(*reinterpret_cast<const uint2*>(dy + (size_t)row * D + col), dv);
-      } else {
+    for (int u = 0; u < 2; ++u) {
+      const bool ok = rows[u] < N;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = dv[j] = 0.f;
-      }
+      for (int i = 0; i < VPL; ++i) {
+        const int col = (i * 64 + lane) * 4;
+        if (ok && col < D) {
+          const size_t o = (size_t)rows[u] * D + col;
+          unpack4(*reinterpret_cast<const uint2*>(x + o), xv[u][i]);
+          unpack4(*reinterpret_cast<const uint2*>(dy + o), dv[u][i]);
+          if (dres) unpack4(*reinterpret_cast<const uint2*>(dres + o), rv[u][i]);
+          else rv[u][i][0] = rv[u][i][1] = rv[u][i][2] = rv[u][i][3] = 0.f;
+        } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        xh[i][j] = (xv[j] - mu) * rs;
-        wd[i][j] = dv[j] * gg[i][j];
-        s1 += wd[i][j];
-        s2 += wd[i][j] * xh[i][j];
-        adg[i][j] += dv[j] * xh[i][j];
-        adb[i][j] += dv[j];
+          for (int j = 0; j < 4; ++j) xv[u][i][j] = dv[u][i][j] = rv[u][i][j] = 0.f;
+        }
       }
     }
-    const float c1 = wave_sum(s1) * invD;
-    const float c2 = wave_sum(s2) * invD;
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int col = (i * 64 + lane) * 4;
-      if (col < D) {
-        float o[4];
+    for (int u = 0; u < 2; ++u) {
+      if (rows[u] >= N) break;
+      const float mu = mean[rows[u]], rs = rstd[rows[u]];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (wd[i][j] - c1 - xh[i][j] * c2) * rs;
-        if (dres) {
-          float r[4];
-          unpack4(*reinterpret_cast<const uint2*>(dres + (size_t)row * D + col), r);
+      for (int i = 0; i < VPL; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] += r[j];
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (xv[u][i][j] - mu) * rs;
+          const float wd = dv[u][i][j] * gg[i][j];
+          xv[u][i][j] = xh;
+          s1 += wd;
+          s2 += wd * xh;
+          acc[0][i][j] += dv[u][i][j] * xh;
+          acc[1][i][j] += dv[u][i][j];
         }
-        *reinterpret_cast<uint2*>(dx + (size_t)row * D + col) = pack4(o);
+      const float c1 = wave_sum(s1) * invD;
+      const float c2 = wave_sum(s2) * invD;
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        const int col = (i * 64 + lane) * 4;
+        if (col < D) {
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            o[j] = (dv[u][i][j] * gg[i][j] - c1 - xv[u][i][j] * c2) * rs + rv[u][i][j];
+            if (NP == 3) acc[NP - 1][i][j] += o[j];
+          }
+          *reinterpret_cast<uint2*>(dx + (size_t)rows[u] * D + col) = pack4(o);
+        }
       }
     }
   }
@@ -143,16 +172,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const int col = (i * 64 + lane) * 4;
     if (col < D) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        atomicAdd(&sdg[col + j], adg[i][j]);
-        atomicAdd(&sdb[col + j], adb[i][j]);
-      }
+      for (int k = 0; k < NP; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(&lds[k * D + col + j], acc[k][i][j]);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < D; i += blockDim.x) {
-    dg_part[(size_t)blockIdx.x * D + i] = sdg[i];
-    db_part[(size_t)blockIdx.x * D + i] = sdb[i];
+  const size_t P = gridDim.x;
+  for (int i = threadIdx.x; i < NP * D; i += blockDim.x) {
+    const int k = i / D, c = i - k * D;
+    part[((size_t)k * P + blockIdx.x) * D + c] = lds[i];
   }
 }
 
@@ -176,43 +205,67 @@ RA_EXPORT int ra_layernorm_fwd(const void* x, const void* g, const void* b, void
   if (D % 4 != 0) return hipErrorInvalidValue;
   dim3 grid((N + 3) / 4);
 #define L(V)                                                                                  \
-  hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, dim3(256), 0, st, (const bf16_t*)x,              \
+  hipLaunchKernelGGL((ln_fwd_kernel<V, false>), grid, dim3(256), 0, st, (const bf16_t*)x,     \
+                     nullptr, nullptr, nullptr, (const bf16_t*)g, (const bf16_t*)b,           \
+                     (bf16_t*)y, mean, rstd, N, D, eps)
+  LN_DISPATCH(L)
+#undef L
+  return hipGetLastError();
+}
+
+// xout = h + rbias + skip (rbias may be null); y = LayerNorm(xout)
+RA_EXPORT int ra_residual_layernorm_fwd(const void* h, const void* rbias, const void* skip,
+                                        void* xout, const void* g, const void* b, void* y,
+                                        float* mean, float* rstd, int N, int D, float eps,
+                                        hipStream_t st) {
+  if (D % 4 != 0) return hipErrorInvalidValue;
+  dim3 grid((N + 3) / 4);
+#define L(V)                                                                                  \
+  hipLaunchKernelGGL((ln_fwd_kernel<V, true>), grid, dim3(256), 0, st, (const bf16_t*)h,      \
+                     (const bf16_t*)rbias, (const bf16_t*)skip, (bf16_t*)xout,                \
                      (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, mean, rstd, N, D, eps)
   LN_DISPATCH(L)
 #undef L
   return hipGetLastError();
 }
 
-// Partial-row count for the backward (1024 blocks x 4 waves fill 256 CUs 4-deep).
+// Partial-row count for the backward (512 blocks x 4 waves x 2 rows in flight).
 RA_EXPORT int ra_layernorm_bwd_parts(int N) {
-  int p = (N + 3) / 4;
-  return p < 1024 ? p : 1024;
+  int p = (N + 7) / 8;
+  return p < 512 ? p : 512;
 }
 
-// fp32 workspace (in floats) required by ra_layernorm_bwd.
+// fp32 workspace (in floats) required by ra_layernorm_bwd (3 partial slabs + scratch).
 RA_EXPORT long ra_layernorm_bwd_work(int N, int D) {
-  return 2L * ra_layernorm_bwd_parts(N) * D + 2L * kColsumSplits * D;
+  return 3L * ra_layernorm_bwd_parts(N) * D + 3L * kColsumSplits * D;
 }
 
+// dbias (optional): column sums of dx (bias grad of the residual add that produced x).
+// flags: bit0 bf16 dg/db/dbias, bit1 accumulate them into (flat) gradient buffers.
 RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, const float* mean,
                                const float* rstd, const void* dres, void* dx, void* dg, void* db,
-                               float* work,
-                               int N, int D, int flags, hipStream_t st) {
-  // flags: bit0 bf16 dg/db, bit1 accumulate dg/db into the (flat) gradient buffers
+                               void* dbias, float* work, int N, int D, int flags,
+                               hipStream_t st) {
   if (D % 4 != 0) return hipErrorInvalidValue;
   const int P = ra_layernorm_bwd_parts(N);
-  float* dgp = work;
-  float* dbp = work + (size_t)P * D;
-  float* scr = work + 2 * (size_t)P * D;
-  const size_t lds = 2 * (size_t)D * sizeof(float);
+  const int NP = dbias ? 3 : 2;
+  float* scr = work + (size_t)NP * P * D;
+  const size_t lds = (size_t)NP * D * sizeof(float);
 #define L(V)                                                                                  \
-  hipLaunchKernelGGL(ln_bwd_kernel<V>, dim3(P), dim3(256), lds, st, (const bf16_t*)dy,        \
-                     (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,      \
-                     (bf16_t*)dx, dgp, dbp, N, D)
+  if (NP == 3)                                                                                \
+    hipLaunchKernelGGL((ln_bwd_kernel<V, 3>), dim3(P), dim3(256), lds, st, (const bf16_t*)dy, \
+                       (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,   \
+                       (bf16_t*)dx, work, N, D);                                              \
+  else                                                                                        \
+    hipLaunchKernelGGL((ln_bwd_kernel<V, 2>), dim3(P), dim3(256), lds, st, (const bf16_t*)dy, \
+                       (const bf16_t*)x, (const bf16_t*)g, mean, rstd, (const bf16_t*)dres,   \
+                       (bf16_t*)dx, work, N, D);
   LN_DISPATCH(L)
 #undef L
-  colsum_launch(dgp, scr, dg, P, D, flags, st);
-  colsum_launch(dbp, scr + (size_t)kColsumSplits * D, db, P, D, flags, st);
+  void* outs[3] = {dg, db, dbias};
+  for (int k = 0; k < NP; ++k)
+    colsum_launch(work + (size_t)k * P * D, scr + (size_t)k * kColsumSplits * D, outs[k], P, D,
+                  flags, st);
   return hipGetLastError();
 }
 

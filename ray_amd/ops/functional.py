@@ -49,27 +49,31 @@ def _ln_forward(x, w, b, eps):
     return x2, y, mean, rstd
 
 
-def _ln_backward(dy, x2, w, b, mean, rstd, dres=None):
-    """dx (+ dres) and the weight/bias grads (into flat sinks when available)."""
+def _ln_backward(dy, x2, w, b, mean, rstd, dres=None, rbias=None):
+    """dx (+ dres) and the weight/bias grads (into flat sinks when available). With
+    ``rbias`` (the bias of the residual add that produced x) also its gradient colsum(dx).
+    Returns (dx, dw, db, drbias) with None for gradients accumulated in place."""
     N, D = x2.shape
     dy2 = dy.contiguous().view(N, D)
     L = _lib.lib()
     work = torch.empty(L.ra_layernorm_bwd_work(N, D), device=dy.device, dtype=torch.float32)
     dx = torch.empty_like(x2)
-    sw, sb = _grad_sink(w), _grad_sink(b)
-    direct = sw is not None and sb is not None
-    dw = sw if direct else torch.empty_like(w)
-    db = sb if direct else torch.empty_like(w)
+    params = [w, b] + ([rbias] if rbias is not None else [])
+    sinks = [_grad_sink(p) for p in params]
+    direct = all(s_ is not None for s_ in sinks)
+    outs = sinks if direct else [torch.empty_like(p) for p in params]
+    if rbias is None:
+        outs.append(None)
     flags = (1 if w.dtype == torch.bfloat16 else 0) | (2 if direct else 0)
     dr = None if dres is None else dres.contiguous().view(N, D)
     check(L.ra_layernorm_bwd(ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dr), ptr(dx),
-                             ptr(dw), ptr(db), ptr(work), N, D, flags, stream_ptr()),
-          "layernorm_bwd")
+                             ptr(outs[0]), ptr(outs[1]), ptr(outs[2]), ptr(work), N, D, flags,
+                             stream_ptr()), "layernorm_bwd")
     if direct:
-        _grad_done(w)
-        _grad_done(b)
-        return dx, None, None
-    return dx, dw, db
+        for p in params:
+            _grad_done(p)
+        return dx, None, None, None
+    return dx, outs[0], outs[1], outs[2]
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -84,7 +88,7 @@ class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _ln_backward(dy, x2, w, ctx.b, mean, rstd)
+        dx, dw, db, _ = _ln_backward(dy, x2, w, ctx.b, mean, rstd)
         return dx.view(ctx.shape), dw, db, None
 
 
@@ -103,8 +107,49 @@ class _LayerNormFork(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dskip, dy):
         x2, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _ln_backward(dy, x2, w, ctx.b, mean, rstd, dres=dskip)
+        dx, dw, db, _ = _ln_backward(dy, x2, w, ctx.b, mean, rstd, dres=dskip)
         return dx.view(ctx.shape), dw, db, None
+
+
+class _ResidualLayerNorm(torch.autograd.Function):
+    """x = h + rbias + skip ; (x, LN(x)) in one kernel. Backward: one kernel computes
+    dx = dskip_out + LN_bwd(dy) and the column sums for dgamma, dbeta AND d(rbias)."""
+
+    @staticmethod
+    def forward(ctx, h, rbias, skip, w, b, eps):
+        D = h.shape[-1]
+        h2 = h.contiguous().view(-1, D)
+        s2 = skip.contiguous().view(-1, D)
+        N = h2.shape[0]
+        xo = torch.empty_like(h2)
+        y = torch.empty_like(h2)
+        mean = torch.empty(N, device=h.device, dtype=torch.float32)
+        rstd = torch.empty(N, device=h.device, dtype=torch.float32)
+        check(_lib.lib().ra_residual_layernorm_fwd(ptr(h2), ptr(rbias), ptr(s2), ptr(xo), ptr(w),
+                                                   ptr(b), ptr(y), ptr(mean), ptr(rstd), N, D,
+                                                   eps, stream_ptr()), "residual_layernorm_fwd")
+        ctx.save_for_backward(xo, w, mean, rstd)
+        ctx.b, ctx.rbias = b, rbias
+        ctx.shape = h.shape
+        return xo.view(h.shape), y.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dxo, dy):
+        xo, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(xo)
+        dx, dw, db, drb = _ln_backward(dy, xo, w, ctx.b, mean, rstd, dres=dxo,
+                                       rbias=ctx.rbias)
+        dx = dx.view(ctx.shape)
+        return dx, drb, dx, dw, db, None
+
+
+def residual_layer_norm(h, rbias, skip, weight, bias, eps=1e-5):
+    """Pre-LN transformer seam: x = h + rbias + skip; returns (x, LayerNorm(x))."""
+    if _hip(h) and h.dtype == torch.bfloat16 and h.shape[-1] % 8 == 0 and rbias is not None:
+        return _ResidualLayerNorm.apply(h, rbias, skip, weight, bias, eps)
+    x = ref.bias_residual(h, rbias, skip) if rbias is not None else h + skip
+    return x, ref.layer_norm(x, weight, bias, eps)
 
 
 def layer_norm(x, weight, bias, eps=1e-5):

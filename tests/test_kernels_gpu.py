@@ -294,3 +294,23 @@ def test_flat_direct_grads_match_autograd(cuda_device):
     ddp.finish()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         assert _rel(pb.grad, pa.grad) < 3e-2, n
+
+
+def test_residual_layer_norm(cuda_device):
+    torch.manual_seed(13)
+    N, D = 2048, 768
+    h = torch.randn(N, D, device=cuda_device).bfloat16().requires_grad_()
+    skip = torch.randn(N, D, device=cuda_device).bfloat16().requires_grad_()
+    rb = (0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    x, y = rf.residual_layer_norm(h, rb, skip, w, b)
+    hr, sr, rbr, wr, br = (t.detach().float().requires_grad_() for t in (h, skip, rb, w, b))
+    xr = hr + rbr + sr
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    assert _rel(x, xr) < 1e-2 and _rel(y, yr) < 1e-2
+    gx, gy = torch.randn_like(xr), torch.randn_like(yr)
+    torch.autograd.backward([x, y], [gx.bfloat16(), gy.bfloat16()])
+    torch.autograd.backward([xr, yr], [gx, gy])
+    for a, r in ((h, hr), (skip, sr), (rb, rbr), (w, wr), (b, br)):
+        assert _rel(a.grad, r.grad) < 2e-2
