@@ -785,7 +785,9 @@ class CoreWorker:
         data = cloudpickle.dumps(obj)
         key = hashlib.blake2b(data, digest_size=16).digest()
         if key not in self.exported:
-            self.notify_raylet("kv_put", "fn", key, data, True)
+            # Synchronous: a cached lease pushes the task straight to a worker, whose
+            # kv_get must not overtake this put on the raylet.
+            self.call_raylet("kv_put", "fn", key, data, True)
             self.exported.add(key)
             self.fn_cache[key] = obj
         return key
