@@ -92,6 +92,17 @@ def bench_gpt2(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     tuned = _setup_tunableop(args, rank)
+    if tuned is not None:
+        # GEMM tuning can run minutes without output: keep a heartbeat on stderr
+        import threading
+
+        def _beat(t0=time.time()):
+            while True:
+                time.sleep(30)
+                print(f"[bench] tunableop tuning... {time.time() - t0:.0f}s", file=sys.stderr,
+                      flush=True)
+
+        threading.Thread(target=_beat, daemon=True).start()
     cfg = getattr(GPT2Config, args.model)()
     tr = GPT2Trainer(cfg, args.micro_batch, args.seq_len, dev, bucket_mb=args.bucket_mb,
                      total_steps=args.warmup + args.steps, grad_accum=args.grad_accum,

@@ -68,13 +68,14 @@ class _Owned:
 class _Remote:
     """Borrower-side view of an object owned elsewhere."""
 
-    __slots__ = ("state", "inline", "error", "callbacks")
+    __slots__ = ("state", "inline", "error", "callbacks", "node")
 
     def __init__(self):
         self.state = 0  # 0 unknown, 1 requested, 2 ready, 3 failed
         self.inline = None
         self.error = None
         self.callbacks = []
+        self.node = None  # node holding the primary copy (hex), None = ours
 
 
 class _Lease:
@@ -198,7 +199,7 @@ class CoreWorker:
                                            daemon=True)
         self.dispatcher.start()
         reg = self.call_raylet("register", mode, worker_id, os.getpid(), self.addr, job_id,
-                               namespace, startup_token)
+                               namespace, startup_token, os.environ.get("RAY_AMD_NODE_ID"))
         from .object_store import ObjectStore
 
         self.node_id = reg["node_id"]
@@ -207,6 +208,8 @@ class CoreWorker:
         self.node_ip = reg.get("node_ip", "127.0.0.1")
         self.store = ObjectStore(reg["store_path"], reg["spill_dir"], create=False)
         self.cluster_info = reg
+        self.node_hex = self.node_id.hex()
+        self._node_addrs: dict[str, str] = {}
         self.task_id_base = os.urandom(12)
 
     # ------------------------------------------------------------------ connections
@@ -444,7 +447,16 @@ class CoreWorker:
             del self.owned[oid]
             contained = o.contained
             in_store = o.in_store
-        if in_store and self.store is not None:
+            node = o.node
+        if in_store:
+            self._delete_stored(oid, node)
+        del contained
+
+    def _delete_stored(self, oid, node):
+        """Free a primary copy: in our node's store, or via its node's agent."""
+        if node is None or node == self.node_hex:
+            if self.store is None:
+                return
             try:
                 self.store.delete(oid)
                 from . import gpu_object_store
@@ -452,7 +464,49 @@ class CoreWorker:
                 gpu_object_store.free_sub_objects(self.store.store, oid)
             except Exception:
                 pass
-        del contained
+            return
+        if self._stopped:
+            return
+        addr = self._node_addrs.get(node)
+        if addr is not None:
+            self.send(addr, (P.REQ, 0, "free_objects", ([oid],)))
+            return
+
+        def got(ok, a, oid=oid, node=node):
+            if ok and a:
+                self._node_addrs[node] = a
+                self.send(a, (P.REQ, 0, "free_objects", ([oid],)))
+
+        self.call_async(self.raylet_addr, "node_addr", (node,), got)
+
+    def _node_addr(self, node):
+        a = self._node_addrs.get(node)
+        if a is None:
+            a = self.call_raylet("node_addr", node, timeout=30)
+            if a is not None:
+                self._node_addrs[node] = a
+        return a
+
+    def _fetch_remote(self, oid, node):
+        """Pull a copy of an object whose primary lives on another node into our node's
+        store as an unpinned (evictable) secondary copy (reference: ObjectManager::Pull).
+        Returns a buffer over the local copy, or None if the node no longer has it."""
+        addr = self._node_addr(node)
+        if addr is None:
+            return None
+        try:
+            data = self.call(addr, "fetch_object", oid, timeout=300)
+        except Exception:
+            return None
+        if data is None:
+            return None
+        if not self.store.contains(oid):
+            try:
+                self.store.put_bytes(oid, data, pinned=False)
+            except Exception:
+                return memoryview(data)  # store full: serve this read from the heap copy
+        buf = self.store.get_buffer(oid)
+        return buf if buf is not None else memoryview(data)
 
     def _rpc_add_borrower(self, conn, rid, oid, addr):
         with self.lock:
@@ -472,15 +526,17 @@ class CoreWorker:
         self._reply(conn, rid, True, None)
 
     # ------------------------------------------------------------------ object values
-    def _mark_ready(self, oid, inline=None, in_store=False, contained=None, size=0):
+    def _mark_ready(self, oid, inline=None, in_store=False, contained=None, size=0, node=None):
         cbs = None
         free = False
+        if node == self.node_hex:
+            node = None
         with self.lock:
             o = self.owned.get(oid)
             if o is None:
                 # released while pending
-                if in_store and self.store is not None:
-                    self.store.delete(oid)
+                if in_store:
+                    self._delete_stored(oid, node)
                 return
             if o.ready:
                 return
@@ -488,6 +544,7 @@ class CoreWorker:
             o.in_store = in_store
             o.contained = contained
             o.size = size
+            o.node = node
             o.ready = True
             self._ready_cv.notify_all()
             cbs = o.callbacks
@@ -580,6 +637,8 @@ class CoreWorker:
                         rr.state, rr.inline = 2, value[1]
                     elif ok and value[0] == "store":
                         rr.state = 2
+                        if value[1] is not None and value[1] != self.node_hex:
+                            rr.node = value[1]
                     else:
                         rr.state = 3
                         rr.error = (OwnerDiedError(oid.hex()) if not ok else
@@ -600,7 +659,7 @@ class CoreWorker:
                 elif o.inline is not None:
                     val = ("inline", o.inline)
                 else:
-                    val = ("store", self.node_id)
+                    val = ("store", o.node or self.node_hex)
             self._reply(conn, rid, True, val)
 
         with self.lock:
@@ -622,10 +681,12 @@ class CoreWorker:
             if o is not None:
                 inline, in_store = o.inline, o.in_store
                 owner = self.addr
+                node = o.node
             else:
                 r = self.remote.get(oid)
                 inline = r.inline if r else None
                 in_store = inline is None
+                node = r.node if r else None
                 e = self.refs.get(oid)
                 owner = e[1] if e else None
                 if r is not None and r.state == 3:
@@ -634,6 +695,8 @@ class CoreWorker:
             buf = inline
         else:
             buf = self.store.get_buffer(oid)
+            if buf is None and node is not None and node != self.node_hex:
+                buf = self._fetch_remote(oid, node)
             if buf is None:
                 raise ObjectLostError(oid.hex())
         kind, value = ser.deserialize(buf, ser.DeserializeContext(anchor=owner))
@@ -1100,7 +1163,7 @@ class CoreWorker:
             # unknown (cancelled / duplicate): drop store results
             for oid, kind, payload, contained in returns:
                 if kind == P.RET_STORE:
-                    self.store.delete(oid)
+                    self._delete_stored(oid, extra.get("node"))
             return
         if spec["type"] == P.ACTOR_TASK:
             self._on_actor_task_reply(spec, returns, extra)
@@ -1115,7 +1178,7 @@ class CoreWorker:
         if extra.get("app_error") and self._should_retry_exc(spec, extra.get("exc_type")):
             for oid, kind, payload, contained in returns:
                 if kind == P.RET_STORE:
-                    self.store.delete(oid)
+                    self._delete_stored(oid, extra.get("node"))
             spec["retries"] -= 1 if spec["retries"] > 0 else 0
             spec["attempt"] += 1
             self._schedule(spec)
@@ -1155,6 +1218,7 @@ class CoreWorker:
                     self._mark_ready(returns[0][0], inline=returns[0][2])
                 self._wake_stream(tid)
             return
+        node = extra.get("node")
         for oid, kind, payload, contained in returns:
             pins = None
             if contained:
@@ -1162,7 +1226,7 @@ class CoreWorker:
             if kind == P.RET_INLINE:
                 self._mark_ready(oid, inline=payload, contained=pins, size=len(payload))
             else:
-                self._mark_ready(oid, in_store=True, contained=pins, size=payload)
+                self._mark_ready(oid, in_store=True, contained=pins, size=payload, node=node)
         spec.pop("_holders", None)
 
     def _fail_task(self, spec, exc):
@@ -1211,14 +1275,15 @@ class CoreWorker:
 
     # ------------------------------------------------------------------ streaming
     def _on_stream_item(self, conn, msg):
-        _, tid, index, ret = msg
+        tid, index, ret = msg[1], msg[2], msg[3]
+        node = msg[4] if len(msg) > 4 else None
         from ray_amd.object_ref import ObjectRef
 
         oid, kind, payload, contained = ret
         st = self.streams.get(tid)
         if st is None:
             if kind == P.RET_STORE:
-                self.store.delete(oid)
+                self._delete_stored(oid, node)
             return
         with self.lock:
             self.owned[oid] = _Owned(tid)
@@ -1227,7 +1292,7 @@ class CoreWorker:
         if kind == P.RET_INLINE:
             self._mark_ready(oid, inline=payload, contained=pins)
         else:
-            self._mark_ready(oid, in_store=True, contained=pins, size=payload)
+            self._mark_ready(oid, in_store=True, contained=pins, size=payload, node=node)
         with self.lock:
             st.items[index] = ref
         self._wake_stream(tid)
@@ -1642,6 +1707,8 @@ class CoreWorker:
             os.environ.update({k: str(v) for k, v in renv["env_vars"].items()})
 
     def _send_reply(self, conn, reply_to, tid, returns, extra):
+        if any(r[1] == P.RET_STORE for r in returns):
+            extra["node"] = self.node_hex
         msg = (P.TASK_REPLY, tid, returns, extra)
         if reply_to is not None and self.send(reply_to, msg):
             return
@@ -1713,14 +1780,14 @@ class CoreWorker:
                     except StopAsyncIteration:
                         break
                     ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
-                    self.send(owner, (P.STREAM_ITEM, tid, i, ret))
+                    self.send(owner, (P.STREAM_ITEM, tid, i, ret, self.node_hex))
                     i += 1
             finally:
                 loop.close()
         else:
             for v in gen:
                 ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
-                self.send(owner, (P.STREAM_ITEM, tid, i, ret))
+                self.send(owner, (P.STREAM_ITEM, tid, i, ret, self.node_hex))
                 i += 1
         self._last_gen_count = i
         return []

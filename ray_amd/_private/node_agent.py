@@ -1,0 +1,158 @@
+"""Worker-node raylet agent (reference: src/ray/raylet/node_manager.cc running on a
+non-head node, src/ray/object_manager/object_manager.cc for Pull/Push).
+
+The head raylet (``raylet.py``) is the cluster's scheduler and GCS: it owns every
+lease, the actor table and placement groups, and it places work on any registered
+node through the native multi-node ``Scheduler``. A worker node runs this agent,
+which
+
+  * hosts the node's shared-memory object store (its own ``/dev/shm`` arena and
+    spill directory), so workers on the node put/get without IPC;
+  * forks worker processes on request from the head (``spawn_worker``) — the workers
+    then register with the head directly and are leased like head-node workers;
+  * serves object copies to other nodes (``fetch_object``: the reader writes a
+    secondary, evictable copy into its own node's store) and frees primaries on the
+    owner's request (``free_objects``);
+  * dies with its head connection and takes its workers with it, which is how the
+    head observes a node failure.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+import traceback
+
+from ray_amd._native import _core
+
+from . import protocol as P
+from .raylet import free_object, node_resources, read_object_bytes
+
+_dumps = P.dumps
+
+
+class NodeAgent:
+    def __init__(self, args):
+        self.session_dir = args.session_dir
+        sock_dir = os.path.join(self.session_dir, "sockets")
+        os.makedirs(sock_dir, exist_ok=True)
+        self.node_id = _core.random_id(16)
+        self.node_hex = self.node_id.hex()
+        self.node_ip = "127.0.0.1"
+        self.addr = os.path.join(sock_dir, f"raylet_{self.node_hex[:16]}.sock")
+        self.store_path = args.store_path
+        self.spill_dir = os.path.join(self.session_dir, f"spill_{self.node_hex[:16]}")
+        os.makedirs(self.spill_dir, exist_ok=True)
+        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True, 1 << 18)
+        self.io = _core.IOLoop()
+        self.io.listen_unix(self.addr)
+        self.total, self.num_cpus = node_resources(args, self.node_ip, head=False)
+        self.labels = json.loads(args.labels or "{}")
+        self.procs: dict[int, subprocess.Popen] = {}
+        self.stop = False
+        self.head_conn = self.io.connect_unix(args.head_address, 30000)
+        if self.head_conn < 0:
+            raise ConnectionError(f"cannot reach head raylet at {args.head_address}")
+        self.io.send(self.head_conn, _dumps((P.HELLO, self.addr, self.node_id)))
+        self.io.send(self.head_conn, _dumps((P.REQ, 1, "register_node", (
+            self.node_hex, self.total, self.labels, self.addr, self.store_path,
+            self.spill_dir, os.getpid(), self.num_cpus))))
+        self.registered = False
+
+    def reply(self, conn, rid, ok, value):
+        if rid:
+            self.io.send(conn, _dumps((P.RESP, rid, ok, value)))
+
+    def run(self):
+        last = 0.0
+        while not self.stop:
+            for typ, conn, payload in self.io.poll(50, 1024):
+                try:
+                    if typ == 0:
+                        msg = P.loads(payload)
+                        if msg[0] == P.REQ:
+                            _, rid, method, args = msg
+                            h = getattr(self, "rpc_" + method, None)
+                            if h is None:
+                                self.reply(conn, rid, False, f"unknown agent method {method}")
+                            else:
+                                h(conn, rid, *args)
+                        elif msg[0] == P.RESP and msg[1] == 1:
+                            self.registered = bool(msg[2])
+                    elif typ == 2 and conn == self.head_conn:
+                        self.stop = True
+                except Exception:
+                    traceback.print_exc()
+            now = time.monotonic()
+            if now - last > 0.5:
+                last = now
+                for pid, p in list(self.procs.items()):
+                    if p.poll() is not None:
+                        self.procs.pop(pid, None)
+        self.shutdown()
+
+    # ------------------------------------------------------------------ head requests
+    def rpc_spawn_worker(self, conn, rid, token, cmd, env, cwd):
+        env = dict(env)
+        env["RAY_AMD_NODE_ID"] = self.node_hex
+        try:
+            p = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
+            self.procs[p.pid] = p
+            self.reply(conn, rid, True, p.pid)
+        except Exception as e:  # noqa: BLE001
+            print(f"[ray_amd] node {self.node_hex[:12]}: worker spawn failed: {e}",
+                  file=sys.stderr, flush=True)
+            self.reply(conn, rid, False, str(e))
+
+    def rpc_kill_worker(self, conn, rid, pid, graceful):
+        p = self.procs.get(pid)
+        try:
+            if p is not None:
+                if not graceful:
+                    p.kill()
+            else:
+                os.kill(pid, signal.SIGKILL)
+        except OSError:
+            pass
+        self.reply(conn, rid, True, None)
+
+    def rpc_fetch_object(self, conn, rid, oid):
+        self.reply(conn, rid, True, read_object_bytes(self.store, self.spill_dir, oid))
+
+    def rpc_free_objects(self, conn, rid, oids):
+        for oid in oids:
+            free_object(self.store, self.spill_dir, oid)
+        self.reply(conn, rid, True, None)
+
+    def rpc_store_stats(self, conn, rid):
+        self.reply(conn, rid, True, {"used": self.store.used(-1),
+                                     "capacity": self.store.capacity(-1),
+                                     "num_objects": self.store.num_objects()})
+
+    def rpc_ping(self, conn, rid):
+        self.reply(conn, rid, True, self.node_hex)
+
+    def rpc_shutdown(self, conn, rid):
+        self.reply(conn, rid, True, None)
+        self.stop = True
+
+    def shutdown(self):
+        for p in list(self.procs.values()):
+            try:
+                p.kill()
+            except OSError:
+                pass
+        for p in list(self.procs.values()):
+            try:
+                p.wait(timeout=2)
+            except Exception:
+                pass
+        try:
+            os.unlink(self.store_path)
+        except OSError:
+            pass
+        self.io.stop()

@@ -32,7 +32,8 @@ _dumps = P.dumps
 
 class WorkerRec:
     __slots__ = ("wid", "pid", "addr", "conn", "key", "state", "lease", "proc", "token",
-                 "actor_id", "job", "gpu_ids", "mode", "idle_since", "namespace", "started")
+                 "actor_id", "job", "gpu_ids", "mode", "idle_since", "namespace", "started",
+                 "node")
 
     def __init__(self):
         self.wid = None
@@ -51,6 +52,7 @@ class WorkerRec:
         self.idle_since = time.monotonic()
         self.namespace = None
         self.started = time.monotonic()
+        self.node = None
 
 
 class Lease:
@@ -122,6 +124,22 @@ class PGRec:
 _PG_STRATEGY = {"PACK": 0, "SPREAD": 1, "STRICT_PACK": 2, "STRICT_SPREAD": 3}
 
 
+def node_resources(args, node_ip, head):
+    """Resource vector a node advertises (reference: resource_spec.py auto-detection)."""
+    res = json.loads(args.resources or "{}")
+    ncpu = args.num_cpus if args.num_cpus is not None else (os.cpu_count() or 1)
+    ngpu = args.num_gpus if args.num_gpus is not None else detect_gpus()
+    total = {"CPU": float(ncpu), "memory": float(args.memory or 8 << 30),
+             "object_store_memory": float(args.object_store_memory),
+             f"node:{node_ip}": 1.0}
+    if ngpu:
+        total["GPU"] = float(ngpu)
+    if head:
+        total["node:__internal_head__"] = 1.0
+    total.update({k: float(v) for k, v in res.items()})
+    return total, ncpu
+
+
 def detect_gpus() -> int:
     """Count AMD GPUs without initialising HIP (reads KFD topology)."""
     env = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") \
@@ -161,22 +179,22 @@ class Raylet:
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.sched = _core.Scheduler()
-        res = json.loads(args.resources or "{}")
-        ncpu = args.num_cpus if args.num_cpus is not None else (os.cpu_count() or 1)
-        ngpu = args.num_gpus if args.num_gpus is not None else detect_gpus()
-        total = {"CPU": float(ncpu), "memory": float(args.memory or 8 << 30),
-                 "object_store_memory": float(args.object_store_memory),
-                 f"node:{self.node_ip}": 1.0}
-        if ngpu:
-            total["GPU"] = float(ngpu)
-        if args.head:
-            total["node:__internal_head__"] = 1.0
-        total.update({k: float(v) for k, v in res.items()})
+        total, ncpu = node_resources(args, self.node_ip, head=True)
         self.labels = json.loads(args.labels or "{}")
         self.labels.setdefault("ray.io/node_id", self.node_id.hex())
         self.sched.add_node(self.node_id.hex(), total, self.labels)
         self.total = total
         self.num_cpus = ncpu
+        # cluster membership (reference: gcs_node_manager.cc). The head raylet schedules
+        # the whole cluster; worker-node agents (node_agent.py) spawn workers and serve
+        # their node's object store.
+        self.node_hex = self.node_id.hex()
+        self.node_recs = {self.node_hex: {
+            "node_id": self.node_hex, "addr": self.addr, "conn": None,
+            "store_path": self.store_path, "spill_dir": self.spill_dir, "labels": self.labels,
+            "resources": total, "alive": True, "pid": os.getpid(), "is_head": True,
+            "start_time": time.time(), "num_cpus": ncpu}}
+        self.node_conn = {}
         self.conn_addr = {}
         self.addr_conn = {}
         self.conn_worker = {}
@@ -263,12 +281,15 @@ class Raylet:
             self.reply(conn, rid, False, e if _picklable(e) else RuntimeError(repr(e)))
 
     # ------------------------------------------------------------------ registration
-    def rpc_register(self, conn, rid, mode, wid, pid, addr, job_id, namespace, token):
+    def rpc_register(self, conn, rid, mode, wid, pid, addr, job_id, namespace, token,
+                     node_hex=None):
         w = None
         if mode == "worker":
             w = self.starting.pop(token, None)
         if w is None:
             w = WorkerRec()
+            rec = self.node_recs.get(node_hex or "")
+            w.node = node_hex if rec is not None and rec["alive"] else self.node_hex
         w.wid, w.pid, w.addr, w.conn, w.mode = wid, pid, addr, conn, mode
         self.conn_worker[conn] = w
         self.workers[wid] = w
@@ -288,11 +309,13 @@ class Raylet:
             if w.key is not None:
                 self.idle[w.key].append(w)
             self.dirty = True
-        info = {"node_id": self.node_id, "job_id": w.job if mode == "driver" else job_id,
+        nrec = self.node_recs[w.node]
+        info = {"node_id": bytes.fromhex(w.node),
+                "job_id": w.job if mode == "driver" else job_id,
                 "namespace": w.namespace if mode == "driver" else namespace,
-                "store_path": self.store_path, "spill_dir": self.spill_dir,
+                "store_path": nrec["store_path"], "spill_dir": nrec["spill_dir"],
                 "node_ip": self.node_ip, "session_dir": self.session_dir,
-                "resources": self.total}
+                "resources": nrec["resources"], "head_node_id": self.node_hex}
         self.reply(conn, rid, True, info)
 
     def rpc_set_job_info(self, conn, rid, job_id, sys_path, runtime_env):
@@ -303,9 +326,9 @@ class Raylet:
         self.reply(conn, rid, True, None)
 
     # ------------------------------------------------------------------ worker pool
-    def _pool_key(self, job, renv, gpu_ids):
+    def _pool_key(self, job, renv, gpu_ids, node):
         return (job, json.dumps(renv, sort_keys=True, default=str) if renv else None,
-                tuple(gpu_ids) if gpu_ids else ())
+                tuple(gpu_ids) if gpu_ids else (), node)
 
     def _start_worker(self, key, renv, job):
         w = WorkerRec()
@@ -314,8 +337,9 @@ class Raylet:
         w.key = key
         w.job = job
         w.gpu_ids = key[2]
+        w.node = node = key[3]
         env = dict(os.environ)
-        env["RAY_AMD_NODE_ID"] = self.node_id.hex()
+        env["RAY_AMD_NODE_ID"] = node
         j = self.jobs.get(job) or {}
         if j.get("sys_path"):
             env["RAY_AMD_JOB_SYS_PATH"] = json.dumps(j["sys_path"])
@@ -344,9 +368,14 @@ class Raylet:
                 env["PYTHONPATH"]
         cmd = [self.python, "-u", "-m", "ray_amd._private.worker_main", "--session-dir",
                self.session_dir, "--raylet", self.addr, "--token", str(w.token), "--job",
-               str(job), "--node-id", self.node_id.hex()]
-        w.proc = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
-        w.pid = w.proc.pid
+               str(job), "--node-id", node]
+        if node == self.node_hex:
+            w.proc = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
+            w.pid = w.proc.pid
+        else:
+            # the node agent forks it (its pid arrives with the worker's registration)
+            self.send(self.node_recs[node]["conn"],
+                      (P.REQ, 0, "spawn_worker", (w.token, cmd, env, cwd)))
         self.starting[w.token] = w
         return w
 
@@ -413,8 +442,9 @@ class Raylet:
                                   for k, v in (st.get("hard") or {}).items()}
                         soft_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
                                   for k, v in (st.get("soft") or {}).items()}
-                node = self.sched.pick_node(res, strategy, target, self.node_id.hex(), hard_l,
-                                            soft_l)
+                rw = self.conn_worker.get(lr.conn)
+                local = rw.node if rw is not None and rw.node else self.node_hex
+                node = self.sched.pick_node(res, strategy, target, local, hard_l, soft_l)
                 if node == "!":
                     if isinstance(st, dict) and st.get("type") == "pg" and \
                             st["pg_id"] not in self.pgs:
@@ -436,8 +466,13 @@ class Raylet:
                     continue
                 lr.alloc = alloc
                 lr.node = node
+            if not self.node_recs.get(lr.node, {}).get("alive"):
+                lr.alloc = None  # node died after allocation: pick again
+                keep.append(lr)
+                continue
             gpu_ids = self._gpu_ids(lr.alloc)
-            key = self._pool_key(lr.req.get("job"), lr.req.get("runtime_env"), gpu_ids)
+            key = self._pool_key(lr.req.get("job"), lr.req.get("runtime_env"), gpu_ids,
+                                 lr.node)
             w = self._take_idle(key)
             if w is None:
                 if lr.waiting_token is None or lr.waiting_token not in self.starting:
@@ -472,7 +507,7 @@ class Raylet:
         w.state = "leased"
         w.lease = lease
         grant = {"addr": w.addr, "lease_id": lid, "gpu_ids": gpu_ids, "worker_id": w.wid,
-                 "pid": w.pid}
+                 "pid": w.pid, "node_id": w.node}
         if lr.cb is not None:
             lr.cb(grant)
         else:
@@ -516,7 +551,7 @@ class Raylet:
         cpu = w.lease.resources.get("CPU")
         if cpu:
             # give the CPU back while the task waits in ray.get (avoids nested-task deadlock)
-            self.sched.release(self._node_alloc(), {"CPU": cpu})
+            self.sched.release(self._node_alloc(w.node), {"CPU": cpu})
             w.lease.cpu_released = True
             self.dirty = True
 
@@ -525,11 +560,11 @@ class Raylet:
         if w is None or w.lease is None or not w.lease.cpu_released:
             return
         cpu = w.lease.resources.get("CPU")
-        if cpu and self.sched.allocate(self.node_id.hex(), {"CPU": cpu}) is not None:
+        if cpu and self.sched.allocate(w.node, {"CPU": cpu}) is not None:
             w.lease.cpu_released = False
 
-    def _node_alloc(self):
-        a = self.sched.allocate(self.node_id.hex(), {})
+    def _node_alloc(self, node):
+        a = self.sched.allocate(node, {})
         return a
 
     # ------------------------------------------------------------------ worker death
@@ -537,6 +572,10 @@ class Raylet:
         addr = self.conn_addr.pop(conn, None)
         if addr:
             self.addr_conn.pop(addr, None)
+        nh = self.node_conn.pop(conn, None)
+        if nh is not None:
+            self._on_node_dead(nh)
+            return
         w = self.conn_worker.pop(conn, None)
         if w is None:
             return
@@ -577,6 +616,10 @@ class Raylet:
                     w.proc.kill()
             except Exception:
                 pass
+        elif w.node != self.node_hex and w.node in self.node_recs:
+            rec = self.node_recs[w.node]
+            if rec["alive"] and w.pid:
+                self.send(rec["conn"], (P.REQ, 0, "kill_worker", (w.pid, graceful)))
         elif w.pid:
             try:
                 os.kill(w.pid, signal.SIGKILL)
@@ -608,6 +651,9 @@ class Raylet:
     # ------------------------------------------------------------------ periodic
     def tick(self):
         now = time.monotonic()
+        for pg in self.pgs.values():
+            if pg.state == "PENDING":
+                self._try_place(pg)
         # reap idle workers beyond the soft limit
         n_idle = sum(len(v) for v in self.idle.values())
         if n_idle > self.num_cpus:
@@ -953,12 +999,80 @@ class Raylet:
                                      if "_group_" not in k and v > 0})
 
     def rpc_nodes(self, conn, rid):
-        self.reply(conn, rid, True, [{
-            "NodeID": self.node_id.hex(), "Alive": True, "NodeManagerAddress": self.node_ip,
-            "NodeManagerHostname": os.uname().nodename, "Resources": self.sched.total(
-                self.node_id.hex()), "alive": True, "RayletSocketName": self.addr,
-            "ObjectStoreSocketName": self.store_path, "Labels": self.labels,
-            "node_id": self.node_id.hex()}])
+        out = []
+        for nh, rec in self.node_recs.items():
+            res = self.sched.total(nh) if rec["alive"] else dict(rec["resources"])
+            out.append({
+                "NodeID": nh, "Alive": rec["alive"], "NodeManagerAddress": self.node_ip,
+                "NodeManagerHostname": os.uname().nodename,
+                "Resources": {k: v for k, v in res.items() if "_group_" not in k},
+                "alive": rec["alive"], "RayletSocketName": rec["addr"],
+                "ObjectStoreSocketName": rec["store_path"], "Labels": rec["labels"],
+                "node_id": nh, "is_head_node": rec.get("is_head", False)})
+        self.reply(conn, rid, True, out)
+
+    def rpc_fetch_object(self, conn, rid, oid):
+        """Serve a copy of an object held in this node's store (object_manager Pull)."""
+        self.reply(conn, rid, True, read_object_bytes(self.store, self.spill_dir, oid))
+
+    def rpc_free_objects(self, conn, rid, oids):
+        for oid in oids:
+            free_object(self.store, self.spill_dir, oid)
+        self.reply(conn, rid, True, None)
+
+    def rpc_node_addr(self, conn, rid, node_hex):
+        rec = self.node_recs.get(node_hex)
+        self.reply(conn, rid, True, rec["addr"] if rec is not None and rec["alive"] else None)
+
+    # ------------------------------------------------------------------ cluster membership
+    def rpc_register_node(self, conn, rid, node_hex, total, labels, addr, store_path,
+                          spill_dir, pid, ncpu):
+        """A worker-node agent joins (reference: GcsNodeManager::HandleRegisterNode)."""
+        labels = dict(labels)
+        labels.setdefault("ray.io/node_id", node_hex)
+        self.sched.add_node(node_hex, total, labels)
+        self.node_recs[node_hex] = {
+            "node_id": node_hex, "addr": addr, "conn": conn, "store_path": store_path,
+            "spill_dir": spill_dir, "labels": labels, "resources": dict(total),
+            "alive": True, "pid": pid, "is_head": False, "start_time": time.time(),
+            "num_cpus": ncpu}
+        self.node_conn[conn] = node_hex
+        self.num_cpus += ncpu
+        self.max_starting = max(self.max_starting, 4, self.num_cpus)
+        for pg in list(self.pgs.values()):
+            self._try_place(pg)
+        self.dirty = True
+        self.reply(conn, rid, True, {"head_node_id": self.node_hex})
+
+    def _on_node_dead(self, nh):
+        """Node agent connection lost: remove the node (reference: OnNodeFailure)."""
+        rec = self.node_recs.get(nh)
+        if rec is None or not rec["alive"]:
+            return
+        rec["alive"] = False
+        rec["end_time"] = time.time()
+        self.num_cpus -= rec.get("num_cpus", 0)
+        print(f"[ray_amd] node {nh[:12]} died", file=sys.stderr, flush=True)
+        for tok, w in list(self.starting.items()):
+            if w.node == nh:
+                self.starting.pop(tok, None)
+        for w in list(self.workers.values()):
+            if w.node == nh and w.conn is not None:
+                # its socket will close too; do not wait for that to free the actor/lease
+                self.on_closed(w.conn)
+        for lst in self.idle.values():
+            lst[:] = [w for w in lst if w.node != nh]
+        for pg in self.pgs.values():
+            if pg.state == "CREATED" and nh in pg.nodes:
+                # bundles on the dead node are gone: reschedule the whole group
+                self.sched.remove_bundles(pg.pg_id, [{k: float(v) for k, v in b.items()}
+                                                     for b in pg.bundles], pg.nodes)
+                pg.state = "PENDING"
+                pg.nodes = []
+        self.sched.remove_node(nh)
+        for pg in list(self.pgs.values()):
+            self._try_place(pg)
+        self.dirty = True
 
     def rpc_list_workers(self, conn, rid):
         out = []
@@ -1131,6 +1245,32 @@ class Raylet:
         self.io.stop()
 
 
+def read_object_bytes(store, spill_dir, oid):
+    """Bytes of a sealed object in a node's shm store (or its spill file), else None."""
+    b = store.get_buffer(oid, True)
+    if b is not None:
+        mv = memoryview(b)
+        try:
+            return bytes(mv)
+        finally:
+            mv.release()
+            b.release()
+    p = os.path.join(spill_dir, oid.hex())
+    try:
+        with open(p, "rb") as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def free_object(store, spill_dir, oid):
+    store.remove(oid)
+    try:
+        os.unlink(os.path.join(spill_dir, oid.hex()))
+    except OSError:
+        pass
+
+
 def _startswith(k, prefix):
     if isinstance(k, bytes) and isinstance(prefix, str):
         prefix = prefix.encode()
@@ -1158,10 +1298,18 @@ def main():
     ap.add_argument("--resources", default="{}")
     ap.add_argument("--labels", default="{}")
     ap.add_argument("--head", action="store_true")
+    ap.add_argument("--head-address", default=None,
+                    help="join an existing cluster as a worker node (head raylet socket)")
+    ap.add_argument("--ready-file", default="raylet.ready")
     args = ap.parse_args()
+    if args.head_address:
+        from .node_agent import NodeAgent
+
+        r = NodeAgent(args)
+    else:
+        r = Raylet(args)
     signal.signal(signal.SIGTERM, lambda *_: setattr(r, "stop", True))
-    r = Raylet(args)
-    ready = os.path.join(args.session_dir, "raylet.ready")
+    ready = os.path.join(args.session_dir, args.ready_file)
     with open(ready + ".tmp", "w") as f:
         json.dump({"addr": r.addr, "node_id": r.node_id.hex(), "pid": os.getpid()}, f)
     os.replace(ready + ".tmp", ready)

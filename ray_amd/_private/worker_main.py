@@ -16,6 +16,13 @@ def main():
     ap.add_argument("--job", default=None)
     ap.add_argument("--node-id", default=None)
     args = ap.parse_args()
+    try:  # die with the raylet / node agent that forked us (PR_SET_PDEATHSIG)
+        import ctypes
+        import signal
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGKILL))
+    except Exception:
+        pass
     extra = os.environ.get("RAY_AMD_JOB_SYS_PATH")
     if extra:
         for p in reversed(json.loads(extra)):

@@ -37,13 +37,58 @@ def _connect(address=None):
 
 
 # ---------------------------------------------------------------------------- start / stop
+def _start_worker_node(a):
+    """`start --address=<head session>`: join a running cluster as a worker node."""
+    import subprocess
+
+    session = _session() if a.address in (None, "auto") else a.address
+    if not session or not os.path.isdir(session):
+        print("No head node to join: pass --address=<session dir> or start one with "
+              "`start --head`.", file=sys.stderr)
+        return 1
+    from ray_amd._private import worker as W
+
+    osm = int(a.object_store_memory or W._default_object_store_memory() // 4)
+    tag = os.urandom(4).hex()
+    ready = f"node_{tag}.ready"
+    cmd = [sys.executable, "-m", "ray_amd._private.raylet", "--session-dir", session,
+           "--store-path", f"/dev/shm/ray_amd_{os.path.basename(session)}_{tag}",
+           "--object-store-memory", str(osm), "--resources", a.resources or "{}",
+           "--labels", a.labels or "{}", "--head-address",
+           os.path.join(session, "sockets", "raylet.sock"), "--ready-file", ready]
+    if a.num_cpus is not None:
+        cmd += ["--num-cpus", str(a.num_cpus)]
+    if a.num_gpus is not None:
+        cmd += ["--num-gpus", str(a.num_gpus)]
+    env = dict(os.environ)
+    pkg = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = pkg + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    out = open(os.path.join(session, f"node_{tag}.out"), "ab")
+    proc = subprocess.Popen(cmd, env=env, close_fds=True, start_new_session=True, stdout=out,
+                            stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
+    t0 = time.time()
+    while not os.path.exists(os.path.join(session, ready)):
+        if proc.poll() is not None or time.time() - t0 > 60:
+            print("worker node failed to start", file=sys.stderr)
+            return 1
+        time.sleep(0.05)
+    pf = os.path.join(session, "cluster_pids.json")
+    pids = {}
+    if os.path.exists(pf):
+        with open(pf) as f:
+            pids = json.load(f)
+    pids.setdefault("nodes", []).append(proc.pid)
+    with open(pf, "w") as f:
+        json.dump(pids, f)
+    print(f"ray_amd worker node started (pid {proc.pid}) and joined {session}")
+    return 0
+
+
 def cmd_start(a):
     from ray_amd._private import worker as W
 
     if not a.head:
-        print("Only single-node (--head) clusters are supported by `start`; worker nodes join "
-              "via ray_amd.cluster_utils.", file=sys.stderr)
-        return 1
+        return _start_worker_node(a)
     if _session() is not None:
         print(f"A ray_amd cluster is already running at {_session()}; run `stop` first.",
               file=sys.stderr)
@@ -114,6 +159,9 @@ def cmd_stop(a):
                 time.sleep(0.05)
             if _pid_alive(pid):
                 os.kill(pid, signal.SIGKILL)
+    for pid in pids.get("nodes", []):  # worker-node agents exit with the head; make sure
+        if _pid_alive(pid):
+            os.kill(pid, signal.SIGKILL)
     try:
         os.unlink(CURRENT_CLUSTER_FILE)
     except FileNotFoundError:
@@ -127,7 +175,7 @@ def cmd_status(a):
     ray = _connect(a.address)
     tot = ray.cluster_resources()
     av = ray.available_resources()
-    nodes = ray.nodes()
+    nodes = [n for n in ray.nodes() if n["Alive"]]
     print("======== ray_amd cluster status ========")
     print(f"Nodes: {len(nodes)} alive")
     for n in nodes:
@@ -335,6 +383,7 @@ def build_parser():
 
     s = sub.add_parser("start", help="start a head node")
     s.add_argument("--head", action="store_true")
+    s.add_argument("--address", help="join this cluster (session dir or 'auto') as a worker node")
     s.add_argument("--num-cpus", type=int)
     s.add_argument("--num-gpus", type=int)
     s.add_argument("--resources")

@@ -113,6 +113,11 @@ def test_cli_start_status_stop():
         assert r.returncode == 0 and json.loads(r.stdout), r.stderr
         r = run("summary", "tasks")
         assert r.returncode == 0 and "cluster" in json.loads(r.stdout)
+        r = run("start", "--address", "auto", "--num-cpus", "3")  # join a worker node
+        assert r.returncode == 0, r.stderr
+        r = run("status")
+        assert r.returncode == 0 and "Nodes: 2 alive" in r.stdout and "0/5 CPU" in r.stdout, \
+            r.stdout + r.stderr
     finally:
         r = run("stop")
     assert r.returncode == 0 and "Stopped" in r.stdout
