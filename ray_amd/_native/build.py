@@ -55,8 +55,11 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
 
     def cc(so):
         s, o = so
+        # VGPR-form MFMA: accumulators live in arch VGPRs, so the softmax / epilogue VALU
+        # work on them needs no v_accvgpr_read/write round trips (gfx950 unified RF)
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-              "-munsafe-fp-atomics", "-Wno-unused-result", "-c", s, "-o", o])
+              "-munsafe-fp-atomics", "-Wno-unused-result", "-mllvm", "-amdgpu-mfma-vgpr-form",
+              "-c", s, "-o", o])
 
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -128,8 +128,11 @@ __device__ __forceinline__ int xcd_block(int bid, int n) {
 
 // ---------------------------------------------------------------- tile staging
 // [64 rows][64] bf16 tile, global row stride `gstride` elements; 256 threads x 2 chunks
+// native vector type: HIP's uint4 is a struct, whose copies lower to memcpy through a
+// stack slot (scratch) that SROA cannot promote
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct TileRegs {
-  uint4 v[2];
+  u32x4 v0, v1;
 };
 struct KV {
   TileRegs k, v;
@@ -140,19 +143,15 @@ struct QD {
 };
 
 __device__ __forceinline__ void tile_load(TileRegs& r, const bf16_t* g, long gstride) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = threadIdx.x + 256 * u;
-    r.v[u] = *reinterpret_cast<const uint4*>(g + (c >> 3) * gstride + (c & 7) * 8);
-  }
+  const int c = threadIdx.x;
+  r.v0 = *reinterpret_cast<const u32x4*>(g + (c >> 3) * gstride + (c & 7) * 8);
+  r.v1 = *reinterpret_cast<const u32x4*>(g + ((c + 256) >> 3) * gstride + (c & 7) * 8);
 }
 
 __device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* img) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = threadIdx.x + 256 * u;
-    *reinterpret_cast<uint4*>(img + img_off(c >> 3, c & 7)) = r.v[u];
-  }
+  const int c = threadIdx.x;
+  *reinterpret_cast<u32x4*>(img + img_off(c >> 3, c & 7)) = r.v0;
+  *reinterpret_cast<u32x4*>(img + img_off((c + 256) >> 3, c & 7)) = r.v1;
 }
 
 // ============================================================================ forward
@@ -181,17 +180,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
   KV A, B;
-  auto load_kv = [&](KV& x, int t) {
+  auto load_kv = [&](KV& x, int t) __attribute__((always_inline)) {
     const long off = (long)t * 64 * tok;
     tile_load(x.k, base + C + off, tok);
     tile_load(x.v, base + 2 * C + off, tok);
   };
-  auto store_kv = [&](const KV& x, int t) {
+  auto store_kv = [&](const KV& x, int t) __attribute__((always_inline)) {
     bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
     tile_store(x.k, d);
     tile_store(x.v, d + TILE_ELEMS);
   };
-  auto compute = [&](int t) {
+  auto compute = [&](int t) __attribute__((always_inline)) {
     const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
     const bf16_t* Vs = Ks + TILE_ELEMS;
     const int kv0 = t * 64;
@@ -245,7 +244,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     }
   };
   // 2-deep register prefetch: tile t+2's loads are in flight during tiles t and t+1
-  auto step = [&](int t, KV& held, KV& next) {
+  auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
     if (t + 2 < ntiles) load_kv(next, t + 2);
     compute(t);
     if (t + 1 < ntiles) store_kv(held, t + 1);
@@ -332,7 +331,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* lse_bh = lse + (long)bh * T;
   const float* del_bh = delta + (long)bh * T;
   QD A, B;
-  auto load_qd = [&](QD& x, int t) {
+  auto load_qd = [&](QD& x, int t) __attribute__((always_inline)) {
     tile_load(x.q, base + (long)t * 64 * tok, tok);
     tile_load(x.d, dobase + (long)t * 64 * C, C);
     if (threadIdx.x < 128) {
@@ -340,14 +339,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       x.rc = threadIdx.x < 64 ? lse_bh[i] * inv_c : -del_bh[i];
     }
   };
-  auto store_qd = [&](const QD& x, int t) {
+  auto store_qd = [&](const QD& x, int t) __attribute__((always_inline)) {
     const int buf = (t - t0) & 1;
     bf16_t* d = lds + buf * 2 * TILE_ELEMS;
     tile_store(x.q, d);
     tile_store(x.d, d + TILE_ELEMS);
     if (threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = x.rc;
   };
-  auto compute = [&](int t) {
+  auto compute = [&](int t) __attribute__((always_inline)) {
     const int cur = (t - t0) & 1;
     const int q0 = t * 64;
     if (q0 + 63 >= wave_kmin) {
@@ -394,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
   };
-  auto step = [&](int t, QD& held, QD& next) {
+  auto step = [&](int t, QD& held, QD& next) __attribute__((always_inline)) {
     if (t + 2 < ntiles) load_qd(next, t + 2);
     compute(t);
     if (t + 1 < ntiles) store_qd(held, t + 1);
@@ -450,17 +449,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
   KV A, B;
-  auto load_kv = [&](KV& x, int t) {
+  auto load_kv = [&](KV& x, int t) __attribute__((always_inline)) {
     const long off = (long)t * 64 * tok;
     tile_load(x.k, base + C + off, tok);
     tile_load(x.v, base + 2 * C + off, tok);
   };
-  auto store_kv = [&](const KV& x, int t) {
+  auto store_kv = [&](const KV& x, int t) __attribute__((always_inline)) {
     bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
     tile_store(x.k, d);
     tile_store(x.v, d + TILE_ELEMS);
   };
-  auto compute = [&](int t) {
+  auto compute = [&](int t) __attribute__((always_inline)) {
     const int kv0 = t * 64;
     if (kv0 <= wave_qmax) {
       const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
@@ -495,7 +494,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
       }
     }
   };
-  auto step = [&](int t, KV& held, KV& next) {
+  auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
     if (t + 2 < ntiles) load_kv(next, t + 2);
     compute(t);
     if (t + 1 < ntiles) store_kv(held, t + 1);
