@@ -34,7 +34,7 @@ _SIGS = {
     "ra_colsum": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "ra_layernorm_bwd_work": [c_int, c_int],
     "ra_colsum_work": [c_int, c_int],
-    "ra_colsum_parts": [c_int],
+    "ra_colsum_parts": [c_int, c_int],
     "ra_bias_gelu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ra_bias_gelu_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_void_p],
     "ra_colsum_bf16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
