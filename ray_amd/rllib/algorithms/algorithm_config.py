@@ -34,6 +34,8 @@ class AlgorithmConfig:
         self.learner_bf16 = True
         self.bootstrap_truncated = False
         self.metrics_num_episodes_for_smoothing = 100
+        self.input_ = None
+        self.output = None
 
     # ---------------------------------------------------------------- builders
     def environment(self, env=None, *, env_config=None, **kw):
@@ -111,6 +113,14 @@ class AlgorithmConfig:
             self.min_time_s_per_iteration = min_time_s_per_iteration
         if metrics_num_episodes_for_smoothing is not None:
             self.metrics_num_episodes_for_smoothing = metrics_num_episodes_for_smoothing
+        return self
+
+    def offline_data(self, *, input_=None, output=None, **kw):
+        """Offline experience source / sink (reference: AlgorithmConfig.offline_data)."""
+        if input_ is not None:
+            self.input_ = input_
+        if output is not None:
+            self.output = output
         return self
 
     def api_stack(self, **kw):

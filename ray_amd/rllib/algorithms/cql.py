@@ -1,0 +1,100 @@
+"""Conservative Q-Learning (reference: rllib/algorithms/cql/cql.py,
+torch/cql_torch_learner.py; Kumar et al. 2020, CQL(H) with SAC as the base learner).
+
+Critic loss = SAC's Bellman error + min_q_weight * (logsumexp_a Q(s, a) - Q(s, a_data)),
+where the log-sum-exp is estimated by importance sampling over ``num_actions``
+uniform-random actions and current-policy actions at s and s' (their log-densities
+subtracted). For the first ``bc_iters`` updates the actor is trained by behaviour
+cloning (alpha * logpi - logpi(a_data|s)) instead of the SAC objective."""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ray_amd.rllib.algorithms.sac import SAC, SACConfig, SACLearner
+from ray_amd.rllib.offline import OfflineData
+
+
+class CQLConfig(SACConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or CQL)
+        self.bc_iters = 200
+        self.temperature = 1.0
+        self.num_actions = 10
+        self.min_q_weight = 5.0
+        self.updates_per_iteration = 100
+        self.eval_steps_per_iteration = 200
+
+
+class CQLLearner(SACLearner):
+    def __init__(self, cfg, obs_space, act_space):
+        super().__init__(cfg, obs_space, act_space)
+        self.n_updates = 0
+        self.low = torch.as_tensor(np.asarray(act_space.low, np.float32)).to(self.device)
+        self.high = torch.as_tensor(np.asarray(act_space.high, np.float32)).to(self.device)
+
+    def _q_rep(self, obs, act, N):
+        o = obs.repeat_interleave(N, 0)
+        q1, q2 = self.q(o, act)
+        return q1.view(-1, N), q2.view(-1, N)
+
+    def extra_critic_loss(self, b, q1, q2):
+        N = int(self.cfg.get("num_actions", 10))
+        T = float(self.cfg.get("temperature", 1.0))
+        obs, nobs = b["obs"], b["next_obs"]
+        B = obs.shape[0]
+        ad = self.low.numel()
+        rnd = torch.rand(B * N, ad, device=obs.device) * (self.high - self.low) + self.low
+        rnd_logp = -torch.log(self.high - self.low).sum()
+        with torch.no_grad():
+            a_cur, lp_cur = self.pi(obs.repeat_interleave(N, 0))
+            a_nxt, lp_nxt = self.pi(nobs.repeat_interleave(N, 0))
+        terms = []
+        for (a, lp) in ((rnd, rnd_logp.expand(B * N)), (a_cur, lp_cur), (a_nxt, lp_nxt)):
+            r1, r2 = self._q_rep(obs, a, N)
+            lp = lp.view(B, N)
+            terms.append((r1 - lp, r2 - lp))
+        c1 = torch.cat([t[0] for t in terms], 1)
+        c2 = torch.cat([t[1] for t in terms], 1)
+        lse1 = torch.logsumexp(c1 / T, 1) * T - math.log(3 * N)
+        lse2 = torch.logsumexp(c2 / T, 1) * T - math.log(3 * N)
+        w = float(self.cfg.get("min_q_weight", 5.0))
+        return w * ((lse1 - q1).mean() + (lse2 - q2).mean())
+
+    def actor_loss(self, b, a, logp, qmin, alpha):
+        self.n_updates += 1
+        if self.n_updates <= int(self.cfg.get("bc_iters", 200)):
+            return (alpha * logp - self.pi.logp_of(b["obs"], b["actions"])).mean()
+        return (alpha * logp - qmin).mean()
+
+
+class CQL(SAC):
+    learner_class = CQLLearner
+
+    @classmethod
+    def get_default_config(cls):
+        return CQLConfig()
+
+    def setup(self):
+        if not self.config.input_:
+            raise ValueError("CQL is offline: set config.offline_data(input_=<dir>)")
+        self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
+        self.learner_group = CQLLearner(self.cfg, self.observation_space, self.action_space)
+        self.prioritized = False
+        self._sync_weights(self.learner_group.get_weights())
+
+    def training_step(self):
+        cfg = self.config
+        stats = {}
+        for _ in range(int(cfg.updates_per_iteration)):
+            b = self.offline.sample(cfg.train_batch_size)
+            b["terminateds"] = b["terminateds"].astype(np.float32)
+            stats, _ = self.learner_group.update(b)
+        self._sync_weights(self.learner_group.get_weights())
+        if cfg.eval_steps_per_iteration:
+            self.local_runner.sample(cfg.eval_steps_per_iteration, explore=False) \
+                if self.local_runner else None
+        return stats

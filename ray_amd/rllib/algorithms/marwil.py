@@ -1,0 +1,144 @@
+"""MARWIL and BC (reference: rllib/algorithms/marwil/marwil.py,
+torch/marwil_torch_learner.py, rllib/algorithms/bc/bc.py; Wang et al. 2018).
+
+Offline: minibatches come from ``OfflineData`` (recorded EnvRunner fragments with
+discounted returns). Loss = -E[exp(beta * A / c) * log pi(a|s)] + vf_coeff * 0.5 *
+(V(s) - R)^2 with A = R - V(s) and c the running RMS of A (moving-average update
+rate ``moving_average_sqd_adv_norm_update_rate``). BC is MARWIL with beta = 0: the
+value head is not trained and the loss is plain negative log-likelihood.
+An env-runner rollout with the current weights every iteration reports
+``episode_return_mean`` (the reference does the same through evaluation)."""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.rl_module import RLModule
+from ray_amd.rllib.offline import OfflineData
+
+
+class MARWILConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or MARWIL)
+        self.lr = 1e-4
+        self.beta = 1.0
+        self.vf_coeff = 1.0
+        self.moving_average_sqd_adv_norm_start = 100.0
+        self.moving_average_sqd_adv_norm_update_rate = 1e-8
+        self.train_batch_size = 2000
+        self.num_env_runners = 0
+        self.updates_per_iteration = 10
+        self.eval_steps_per_iteration = 500
+        self.grad_clip = None
+        self.model = {"fcnet_hiddens": [256, 256], "fcnet_activation": "tanh"}
+
+
+class BCConfig(MARWILConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or BC)
+        self.beta = 0.0
+        self.vf_coeff = 0.0
+
+
+class MARWILLearner:
+    def __init__(self, cfg, obs_space, act_space):
+        self.cfg = cfg
+        self.device = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
+            "num_gpus_per_learner", 1) else torch.device("cpu")
+        self.module = RLModule(obs_space, act_space, cfg.get("model")).to(self.device)
+        self.opt = torch.optim.Adam(self.module.parameters(), lr=cfg.get("lr", 1e-4))
+        self.ma_sqd = float(cfg.get("moving_average_sqd_adv_norm_start", 100.0))
+
+    def _logp(self, di, actions):
+        m = self.module
+        if m.discrete:
+            return torch.log_softmax(di.float(), -1).gather(-1, actions.long()[:, None])[:, 0]
+        from ray_amd.rllib.core.rl_module import gaussian_logp
+
+        mean, log_std = di.float().chunk(2, -1)
+        return gaussian_logp(actions.float(), mean, log_std)
+
+    def update(self, b):
+        dev = self.device
+        obs = torch.as_tensor(b["obs"]).to(dev)
+        act = torch.as_tensor(b["actions"]).to(dev)
+        ret = torch.as_tensor(b["returns"]).float().to(dev)
+        out = self.module.forward_train(obs)
+        logp = self._logp(out["action_dist_inputs"], act)
+        beta = float(self.cfg.get("beta", 1.0))
+        stats = {}
+        if beta != 0.0:
+            v = out["vf_preds"].float()
+            adv = ret - v
+            with torch.no_grad():
+                rate = float(self.cfg.get("moving_average_sqd_adv_norm_update_rate", 1e-8))
+                self.ma_sqd += rate * (float((adv.detach() ** 2).mean()) - self.ma_sqd)
+                w = torch.exp(beta * adv.detach() / (1e-8 + self.ma_sqd ** 0.5)).clamp(max=20.0)
+            pi_loss = -(w * logp).mean()
+            vf_loss = 0.5 * (adv ** 2).mean()
+            loss = pi_loss + float(self.cfg.get("vf_coeff", 1.0)) * vf_loss
+            stats["vf_loss"] = float(vf_loss.detach())
+        else:
+            pi_loss = -logp.mean()
+            loss = pi_loss
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.cfg.get("grad_clip"):
+            torch.nn.utils.clip_grad_norm_(self.module.parameters(), self.cfg["grad_clip"])
+        self.opt.step()
+        stats.update(policy_loss=float(pi_loss.detach()), total_loss=float(loss.detach()))
+        return stats
+
+    def get_weights(self):
+        return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
+
+    def get_state(self):
+        return {"module": self.get_weights(), "opt": self.opt.state_dict(), "ma": self.ma_sqd}
+
+    def set_state(self, s):
+        self.module.load_state_dict(s["module"])
+        self.opt.load_state_dict(s["opt"])
+        self.ma_sqd = s["ma"]
+
+    def shutdown(self):
+        pass
+
+
+class MARWIL(Algorithm):
+    @classmethod
+    def get_default_config(cls):
+        return MARWILConfig()
+
+    def setup(self):
+        if not self.config.input_:
+            raise ValueError(f"{type(self).__name__} is offline: set "
+                             "config.offline_data(input_=<recorded experience dir>)")
+        self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
+        self.learner_group = MARWILLearner(self.cfg, self.observation_space, self.action_space)
+        self._sync_weights(self.learner_group.get_weights())
+
+    def training_step(self):
+        cfg = self.config
+        stats = {}
+        for _ in range(int(cfg.updates_per_iteration)):
+            stats = self.learner_group.update(self.offline.sample(cfg.train_batch_size))
+        self._sync_weights(self.learner_group.get_weights())
+        if cfg.eval_steps_per_iteration:  # online metrics with the current policy
+            runner = self.env_runners[0] if self.env_runners else self.local_runner
+            n = max(1, cfg.eval_steps_per_iteration // max(1, cfg.num_envs_per_env_runner))
+            if self.env_runners:
+                import ray_amd as ray
+
+                ray.get(runner.sample.remote(n, False))
+            else:
+                runner.sample(n, explore=False)
+        return stats
+
+
+class BC(MARWIL):
+    @classmethod
+    def get_default_config(cls):
+        return BCConfig()

@@ -5,9 +5,13 @@ def _algos():
     from ray_amd.rllib.algorithms.dqn import DQN, DQNConfig
     from ray_amd.rllib.algorithms.impala import APPO, IMPALA, APPOConfig, IMPALAConfig
     from ray_amd.rllib.algorithms.ppo import PPO, PPOConfig
+    from ray_amd.rllib.algorithms.cql import CQL, CQLConfig
+    from ray_amd.rllib.algorithms.marwil import BC, MARWIL, BCConfig, MARWILConfig
+    from ray_amd.rllib.algorithms.sac import SAC, SACConfig
 
     return {"PPO": (PPO, PPOConfig), "IMPALA": (IMPALA, IMPALAConfig),
-            "APPO": (APPO, APPOConfig), "DQN": (DQN, DQNConfig)}
+            "APPO": (APPO, APPOConfig), "DQN": (DQN, DQNConfig), "SAC": (SAC, SACConfig),
+            "CQL": (CQL, CQLConfig), "MARWIL": (MARWIL, MARWILConfig), "BC": (BC, BCConfig)}
 
 
 def get_algorithm_class(name: str):

@@ -1,0 +1,217 @@
+"""Soft Actor-Critic (reference: rllib/algorithms/sac/sac.py, sac_learner.py,
+torch/sac_torch_learner.py; Haarnoja et al. 2018 with automatic entropy tuning).
+
+Off-policy loop shared with DQN's structure: env-runner actors sample with the
+squashed-Gaussian actor, transitions go to a (prioritised) replay buffer, and the
+learner GPU runs critic / actor / temperature updates with Polyak-averaged target
+critics. ``CQL`` (offline) subclasses the learner (``cql.py``)."""
+
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+
+import ray_amd as ray
+from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy, TwinQ
+from ray_amd.rllib.utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
+
+
+class SACConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or SAC)
+        self.lr = None
+        self.actor_lr = 3e-4
+        self.critic_lr = 3e-4
+        self.alpha_lr = 3e-4
+        self.train_batch_size = 256
+        self.rollout_fragment_length = 1
+        self.num_env_runners = 0
+        self.tau = 5e-3
+        self.initial_alpha = 1.0
+        self.target_entropy = "auto"
+        self.n_step = 1
+        self.twin_q = True
+        self.replay_buffer_config = {"type": "ReplayBuffer", "capacity": 100000}
+        self.num_steps_sampled_before_learning_starts = 1500
+        self.training_intensity = None
+        self.target_network_update_freq = 0
+        self.grad_clip = None
+        self.bootstrap_truncated = True  # time-limit truncation is not termination
+        self.model = {"fcnet_hiddens": [256, 256], "fcnet_activation": "relu"}
+        self.policy_model_config = None
+        self.q_model_config = None
+
+
+def _to(b, dev):
+    return {k: torch.as_tensor(np.asarray(v)).to(dev) for k, v in b.items()
+            if k in ("obs", "next_obs", "actions", "rewards", "terminateds", "weights")}
+
+
+class SACLearner:
+    def __init__(self, cfg, obs_space, act_space):
+        self.cfg = cfg
+        self.device = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
+            "num_gpus_per_learner", 1) else torch.device("cpu")
+        dev = self.device
+        pm = cfg.get("policy_model_config") or cfg.get("model")
+        qm = cfg.get("q_model_config") or cfg.get("model")
+        self.pi = SquashedGaussianPolicy(obs_space, act_space, pm).to(dev)
+        self.q = TwinQ(obs_space, act_space, qm).to(dev)
+        self.q_t = copy.deepcopy(self.q)
+        for p in self.q_t.parameters():
+            p.requires_grad_(False)
+        act_dim = int(np.prod(act_space.shape))
+        te = cfg.get("target_entropy", "auto")
+        self.target_entropy = -float(act_dim) if te in (None, "auto") else float(te)
+        self.log_alpha = torch.tensor(float(np.log(cfg.get("initial_alpha", 1.0))),
+                                      device=dev, requires_grad=True)
+        fused = dev.type == "cuda"
+        self.opt_pi = torch.optim.Adam(self.pi.parameters(), lr=cfg.get("actor_lr", 3e-4),
+                                       fused=fused)
+        self.opt_q = torch.optim.Adam(self.q.parameters(), lr=cfg.get("critic_lr", 3e-4),
+                                      fused=fused)
+        self.opt_a = torch.optim.Adam([self.log_alpha], lr=cfg.get("alpha_lr", 3e-4))
+        self.gamma = cfg.get("gamma", 0.99)
+        self.tau = cfg.get("tau", 5e-3)
+
+    # ---------------------------------------------------------------- losses
+    def critic_target(self, b):
+        with torch.no_grad():
+            na, nlogp = self.pi(b["next_obs"])
+            q1, q2 = self.q_t(b["next_obs"], na)
+            alpha = self.log_alpha.exp()
+            v = torch.min(q1, q2) - alpha * nlogp
+            return b["rewards"].float() + self.gamma * (1 - b["terminateds"].float()) * v
+
+    def extra_critic_loss(self, b, q1, q2):
+        return None  # CQL adds its conservative regulariser here
+
+    def update(self, batch):
+        b = _to(batch, self.device)
+        w = b.get("weights")
+        tgt = self.critic_target(b)
+        q1, q2 = self.q(b["obs"], b["actions"])
+        td = (q1 - tgt).detach()
+        l1 = (q1 - tgt) ** 2
+        l2 = (q2 - tgt) ** 2
+        if w is not None:
+            l1, l2 = l1 * w, l2 * w
+        critic_loss = 0.5 * (l1.mean() + l2.mean())
+        extra = self.extra_critic_loss(b, q1, q2)
+        if extra is not None:
+            critic_loss = critic_loss + extra
+        self.opt_q.zero_grad(set_to_none=True)
+        critic_loss.backward()
+        if self.cfg.get("grad_clip"):
+            torch.nn.utils.clip_grad_norm_(self.q.parameters(), self.cfg["grad_clip"])
+        self.opt_q.step()
+        # actor: maximise min-Q - alpha * logp (critics frozen for this step)
+        for p in self.q.parameters():
+            p.requires_grad_(False)
+        a, logp = self.pi(b["obs"])
+        qa1, qa2 = self.q(b["obs"], a)
+        alpha = self.log_alpha.exp().detach()
+        actor_loss = self.actor_loss(b, a, logp, torch.min(qa1, qa2), alpha)
+        self.opt_pi.zero_grad(set_to_none=True)
+        actor_loss.backward()
+        self.opt_pi.step()
+        for p in self.q.parameters():
+            p.requires_grad_(True)
+        alpha_loss = -(self.log_alpha * (logp.detach() + self.target_entropy)).mean()
+        self.opt_a.zero_grad(set_to_none=True)
+        alpha_loss.backward()
+        self.opt_a.step()
+        with torch.no_grad():  # Polyak target update
+            for pt, p in zip(self.q_t.parameters(), self.q.parameters()):
+                pt.lerp_(p, self.tau)
+        stats = {"critic_loss": float(critic_loss.detach()),
+                 "actor_loss": float(actor_loss.detach()), "alpha_loss": float(alpha_loss.detach()), "alpha_value": float(alpha),
+                 "mean_q": float(q1.detach().mean()), "entropy": float(-logp.detach().mean())}
+        return stats, td.abs().cpu().numpy()
+
+    def actor_loss(self, b, a, logp, qmin, alpha):
+        return (alpha * logp - qmin).mean()
+
+    # ---------------------------------------------------------------- state
+    def get_weights(self):
+        return {k: v.detach().cpu() for k, v in self.pi.state_dict().items()}
+
+    def get_state(self):
+        return {"pi": self.get_weights(),
+                "q": {k: v.detach().cpu() for k, v in self.q.state_dict().items()},
+                "q_t": {k: v.detach().cpu() for k, v in self.q_t.state_dict().items()},
+                "log_alpha": float(self.log_alpha.detach()),
+                "opt": [o.state_dict() for o in (self.opt_pi, self.opt_q, self.opt_a)]}
+
+    def set_state(self, s):
+        self.pi.load_state_dict(s["pi"])
+        self.q.load_state_dict(s["q"])
+        self.q_t.load_state_dict(s["q_t"])
+        with torch.no_grad():
+            self.log_alpha.fill_(s["log_alpha"])
+        for o, st in zip((self.opt_pi, self.opt_q, self.opt_a), s["opt"]):
+            o.load_state_dict(st)
+
+    def shutdown(self):
+        pass
+
+
+class SAC(Algorithm):
+    module_kind = "sac"
+    learner_class = SACLearner
+
+    @classmethod
+    def get_default_config(cls):
+        return SACConfig()
+
+    def setup(self):
+        rb = self.config.replay_buffer_config
+        cap = rb.get("capacity", 100000)
+        self.prioritized = "Prioritized" in rb.get("type", "")
+        self.buffer = PrioritizedReplayBuffer(cap, rb.get("alpha", 0.6), self.config.seed) \
+            if self.prioritized else ReplayBuffer(cap, self.config.seed)
+        self.learner_group = self.learner_class(self.cfg, self.observation_space,
+                                                self.action_space)
+        self._sync_weights(self.learner_group.get_weights())
+
+    def training_step(self):
+        cfg = self.config
+        frag = max(1, cfg.rollout_fragment_length)
+        if self.env_runners:
+            bs = ray.get([r.sample.remote(frag) for r in self.env_runners])
+        else:
+            bs = [self.local_runner.sample(frag)]
+        new = 0
+        for b in bs:
+            T, B = b["rewards"].shape
+            self.buffer.add({k: b[k].reshape((T * B,) + b[k].shape[2:])
+                             for k in ("obs", "next_obs", "actions", "rewards", "terminateds")})
+            new += T * B
+        self.total_env_steps += new
+        stats = {}
+        if self.total_env_steps < cfg.num_steps_sampled_before_learning_starts:
+            return stats
+        # reference default: one gradient step per sampled env step (training_intensity 1)
+        ti = cfg.training_intensity or cfg.train_batch_size
+        n_updates = max(1, int(round(new * ti / cfg.train_batch_size)))
+        for _ in range(n_updates):
+            kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} if self.prioritized else {}
+            mb = self.buffer.sample(cfg.train_batch_size, **kw)
+            stats, td = self.learner_group.update(mb)
+            if self.prioritized:
+                self.buffer.update_priorities(mb["batch_indexes"], td)
+        self._sync_weights(self.learner_group.get_weights())
+        return stats
+
+    def compute_single_action(self, obs, explore=False):
+        lg = self.learner_group
+        with torch.no_grad():
+            x = torch.as_tensor(np.asarray(obs, np.float32)[None]).to(lg.device)
+            a, _ = lg.pi(x, explore, with_logp=False)
+        return a[0].cpu().numpy()
+
+    compute_action = compute_single_action

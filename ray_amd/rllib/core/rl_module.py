@@ -188,4 +188,66 @@ class QModule(nn.Module):
         return self.val(h) + a - a.mean(-1, keepdim=True)
 
 
+class SquashedGaussianPolicy(nn.Module):
+    """SAC actor: tanh-squashed diagonal Gaussian rescaled to the Box bounds
+    (reference: rllib/algorithms/sac/torch/default_sac_torch_rl_module.py and
+    rllib/models/torch/torch_distributions.py:TorchSquashedGaussian)."""
+
+    def __init__(self, observation_space, action_space, model_config=None):
+        super().__init__()
+        cfg = dict(model_config or {})
+        d = int(np.prod(observation_space.shape))
+        self.act_dim = int(np.prod(action_space.shape))
+        self.encoder = MLP(d, cfg.get("fcnet_hiddens", [256, 256]),
+                           cfg.get("fcnet_activation", "relu"))
+        self.head = nn.Linear(self.encoder.out_dim, 2 * self.act_dim)
+        low = torch.tensor(np.array(action_space.low, np.float32)).reshape(-1)
+        high = torch.tensor(np.array(action_space.high, np.float32)).reshape(-1)
+        self.register_buffer("a_scale", (high - low) / 2)
+        self.register_buffer("a_bias", (high + low) / 2)
+
+    def forward(self, obs, explore=True, with_logp=True):
+        """Returns (env-scaled actions, log pi(a|s)). Reparameterised: gradients flow."""
+        h = self.encoder(obs.reshape(obs.shape[0], -1).float())
+        mean, log_std = self.head(h).chunk(2, -1)
+        log_std = log_std.clamp(-20, 2)
+        u = mean + log_std.exp() * torch.randn_like(mean) if explore else mean
+        a = torch.tanh(u)
+        logp = None
+        if with_logp:
+            # change of variables for tanh + affine rescale (numerically stable form)
+            logp = gaussian_logp(u, mean, log_std) - (
+                2 * (math.log(2) - u - F.softplus(-2 * u))).sum(-1) - \
+                torch.log(self.a_scale).sum()
+        return a * self.a_scale + self.a_bias, logp
+
+    def logp_of(self, obs, actions):
+        """log pi(a|s) of given env-scaled actions (behaviour cloning in CQL/BC)."""
+        h = self.encoder(obs.reshape(obs.shape[0], -1).float())
+        mean, log_std = self.head(h).chunk(2, -1)
+        log_std = log_std.clamp(-20, 2)
+        a = ((actions.float() - self.a_bias) / self.a_scale).clamp(-0.999999, 0.999999)
+        u = torch.atanh(a)
+        return gaussian_logp(u, mean, log_std) - (
+            2 * (math.log(2) - u - F.softplus(-2 * u))).sum(-1) - torch.log(self.a_scale).sum()
+
+
+class TwinQ(nn.Module):
+    """Q(s, a) critic pair for SAC / CQL (clipped double-Q)."""
+
+    def __init__(self, observation_space, action_space, model_config=None):
+        super().__init__()
+        cfg = dict(model_config or {})
+        d = int(np.prod(observation_space.shape)) + int(np.prod(action_space.shape))
+        hid = cfg.get("fcnet_hiddens", [256, 256])
+        act = cfg.get("fcnet_activation", "relu")
+        self.q1 = nn.Sequential(MLP(d, hid, act), nn.Linear(hid[-1], 1))
+        self.q2 = nn.Sequential(MLP(d, hid, act), nn.Linear(hid[-1], 1))
+
+    def forward(self, obs, act):
+        x = torch.cat([obs.reshape(obs.shape[0], -1).float(),
+                       act.reshape(act.shape[0], -1).float()], -1)
+        return self.q1(x).squeeze(-1), self.q2(x).squeeze(-1)
+
+
 F  # noqa: B018

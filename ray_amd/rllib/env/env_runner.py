@@ -41,6 +41,12 @@ class SingleAgentEnvRunner:
             mc = dict(config.get("model") or {})
             mc["dueling"] = config.get("dueling", True)
             self.module = QModule(self.observation_space, self.action_space, mc)
+        elif self.module_kind == "sac":
+            from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy
+
+            self.module = SquashedGaussianPolicy(self.observation_space, self.action_space,
+                                                 config.get("policy_model_config") or
+                                                 config.get("model"))
         else:
             self.module = RLModule(self.observation_space, self.action_space, config.get("model"))
         self.module.eval()
@@ -91,7 +97,7 @@ class SingleAgentEnvRunner:
         logp = np.zeros((T, B), np.float32)
         dist_in = None
         next_obs_buf = None
-        if self.module_kind == "q":
+        if self.module_kind in ("q", "sac"):
             next_obs_buf = np.empty_like(obs_buf)
         t0 = time.perf_counter()
         for t in range(T):
@@ -107,6 +113,10 @@ class SingleAgentEnvRunner:
                         rnd = np.random.random(B) < eps
                         a = np.where(rnd, np.random.randint(0, self.action_space.n, B), a)
                     lp = np.zeros(B, np.float32)
+                elif self.module_kind == "sac":
+                    at, lpt = self.module(x, explore)
+                    a = at.float().cpu().numpy()
+                    lp = lpt.float().cpu().numpy()
                 else:
                     out = self.module.forward_inference(x)
                     di = out["action_dist_inputs"]
@@ -148,6 +158,15 @@ class SingleAgentEnvRunner:
             batch["action_dist_inputs"] = dist_in
         if next_obs_buf is not None:
             batch["next_obs"] = next_obs_buf
+        if self.config.get("output"):
+            if getattr(self, "_writer", None) is None:
+                from ray_amd.rllib.offline import JsonWriter
+
+                self._writer = JsonWriter(self.config["output"], self.worker_index)
+            if next_obs_buf is None:  # next_obs from the rolled-forward observations
+                nxt = np.concatenate([obs_buf[1:], np.stack(self.obs)[None]], 0)
+                batch = dict(batch, next_obs=nxt)
+            self._writer.write(batch)
         return batch
 
     def get_metrics(self):
