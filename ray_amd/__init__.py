@@ -66,3 +66,16 @@ __all__ = [
     "shutdown", "timeline", "wait", "get_runtime_context", "ObjectRef", "ObjectRefGenerator",
     "ActorHandle", "LOCAL_MODE", "SCRIPT_MODE", "WORKER_MODE", "exceptions", "Language",
 ]
+
+_LAZY_SUBPACKAGES = ("data", "train", "tune", "serve", "rllib", "util", "workflow", "dag",
+                     "air", "cluster_utils", "job_submission", "dashboard", "experimental")
+
+
+def __getattr__(name):
+    # `import ray_amd; ray_amd.data.range(...)` without importing heavy subpackages up
+    # front (reference: python/ray/__init__.py module __getattr__)
+    if name in _LAZY_SUBPACKAGES:
+        import importlib
+
+        return importlib.import_module(f"ray_amd.{name}")
+    raise AttributeError(f"module 'ray_amd' has no attribute {name!r}")
