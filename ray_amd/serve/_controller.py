@@ -225,11 +225,12 @@ class ServeController:
     async def shutdown(self):
         for name in list(self.apps):
             await self.delete_application(name)
-        if self.proxy is not None:
-            try:
-                ray.kill(self.proxy)
-            except Exception:
-                pass
+        for p in (self.proxy, getattr(self, "grpc_proxy", None)):
+            if p is not None:
+                try:
+                    ray.kill(p)
+                except Exception:
+                    pass
         return True
 
     def set_proxy(self, proxy):
@@ -238,3 +239,10 @@ class ServeController:
 
     def get_proxy(self):
         return self.proxy
+
+    def set_grpc_proxy(self, proxy):
+        self.grpc_proxy = proxy
+        return True
+
+    def get_grpc_proxy(self):
+        return getattr(self, "grpc_proxy", None)

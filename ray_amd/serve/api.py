@@ -61,7 +61,31 @@ def start(http_options: dict | None = None, detached: bool = True, **kw):
             raise RuntimeError(f"HTTP proxy failed to start: {err}")
         ray.get(c.set_proxy.remote(_proxy))
         _http_port = port
+    g = kw.get("grpc_options")
+    if g is not None:
+        g = g if isinstance(g, dict) else vars(g)
+        if g.get("grpc_servicer_functions") and ray.get(c.get_grpc_proxy.remote()) is None:
+            from ray_amd.serve._grpc_proxy import gRPCProxy
+
+            gp = ray.remote(gRPCProxy).options(
+                num_cpus=0, max_concurrency=1000, name="SERVE_GRPC_PROXY",
+                namespace=SERVE_NAMESPACE, lifetime="detached").remote(
+                g.get("host", "127.0.0.1"), int(g.get("port", 9000)),
+                list(g["grpc_servicer_functions"]))
+            err = ray.get(gp.ping.remote())
+            if err != "ok":
+                raise RuntimeError(f"gRPC proxy failed to start: {err}")
+            ray.get(c.set_grpc_proxy.remote(gp))
     return c
+
+
+class gRPCOptions:
+    """gRPC ingress options (reference: python/ray/serve/config.py:gRPCOptions)."""
+
+    def __init__(self, port: int = 9000, grpc_servicer_functions=(), host="127.0.0.1"):
+        self.port = port
+        self.grpc_servicer_functions = list(grpc_servicer_functions)
+        self.host = host
 
 
 class Deployment:
@@ -191,7 +215,7 @@ def run(target: Application, *, name: str = "default", route_prefix: str | None 
         blocking: bool = False, _blocking=None, **kw) -> DeploymentHandle:
     if isinstance(target, Deployment):
         target = target.bind()
-    c = start(kw.get("http_options"))
+    c = start(kw.get("http_options"), grpc_options=kw.get("grpc_options"))
     specs: dict = {}
     handle = _build(target, name, specs)
     rp = target.deployment.route_prefix or route_prefix
