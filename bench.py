@@ -10,8 +10,10 @@ runs exactly the per-worker step of ``ray_amd.train.examples.gpt2.train_func``
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
-``--workload ppo`` runs the RLlib PPO synthetic-Atari learner throughput bench
-(BASELINE.json config 3). Prints ONE JSON line on rank 0.
+``--workload ppo`` runs the RLlib PPO synthetic-Atari throughput bench (BASELINE.json
+config 3), ``impala`` the IMPALA V-trace one (config 5, 1 learner), ``data`` the Ray Data
+→ GPU ingest pipeline (config 4, 1 GPU) and ``microbench`` the task/actor call-rate
+microbenchmark (config 1). Prints ONE JSON line on rank 0.
 """
 
 from __future__ import annotations
@@ -30,7 +32,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="gpt2", choices=["gpt2", "ppo"])
+    ap.add_argument("--workload", default="gpt2",
+                    choices=["gpt2", "ppo", "impala", "data", "microbench"])
     ap.add_argument("--micro-batch", type=int, default=64,
                     help="per-GPU sequences; 64 x 1024 tokens x 8 GPUs = 524k tokens, the GPT-3 "
                          "Small global batch")
@@ -186,10 +189,27 @@ def main():
     args = parse()
     if args.workload == "gpt2":
         bench_gpt2(args)
-    else:
+    elif args.workload == "ppo":
         from ray_amd.rllib.bench import bench_ppo
 
         bench_ppo(args)
+    elif args.workload == "impala":
+        from ray_amd.rllib.bench import bench_impala
+
+        bench_impala(args)
+    elif args.workload == "data":
+        from ray_amd.data.bench import bench_data
+
+        bench_data(args)
+    else:  # BASELINE.json config 1: task/actor call rates (CPU plumbing)
+        from ray_amd._private import ray_perf
+
+        from ray_amd._private.raylet import detect_cpus
+
+        res = ray_perf.main(quick=False, num_cpus=min(16, detect_cpus()))
+        print(json.dumps({"metric": "ray_microbenchmark_calls_per_sec", "results": {
+            r[0]: round(r[1], 1) for r in res}, "unit": "calls/s", "n_gpus": 0,
+            "higher_is_better": True, "data": "synthetic"}), flush=True)
 
 
 if __name__ == "__main__":

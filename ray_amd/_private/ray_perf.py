@@ -69,10 +69,10 @@ def small_value():
     return b"ok"
 
 
-def main(quick=False):
+def main(quick=False, num_cpus=None):
     results = []
     d = 1.0 if quick else 2.0
-    ray.init()
+    ray.init(num_cpus=num_cpus)
     value = ray.put(0)
     results.append(timeit("single client get calls (Plasma Store)", lambda: ray.get(value),
                           duration=d))

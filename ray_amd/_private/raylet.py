@@ -124,10 +124,38 @@ class PGRec:
 _PG_STRATEGY = {"PACK": 0, "SPREAD": 1, "STRICT_PACK": 2, "STRICT_SPREAD": 3}
 
 
+def detect_cpus() -> int:
+    """Usable CPUs: affinity mask, capped by a cgroup CPU quota (reference:
+    ray._private.utils.get_num_cpus, which also honours container quotas)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota|max> <period>"
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
+
+
 def node_resources(args, node_ip, head):
     """Resource vector a node advertises (reference: resource_spec.py auto-detection)."""
     res = json.loads(args.resources or "{}")
-    ncpu = args.num_cpus if args.num_cpus is not None else (os.cpu_count() or 1)
+    ncpu = args.num_cpus if args.num_cpus is not None else detect_cpus()
     ngpu = args.num_gpus if args.num_gpus is not None else detect_gpus()
     total = {"CPU": float(ncpu), "memory": float(args.memory or 8 << 30),
              "object_store_memory": float(args.object_store_memory),

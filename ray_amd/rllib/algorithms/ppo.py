@@ -2,6 +2,8 @@
 
 from __future__ import annotations
 
+import time
+
 from ray_amd.rllib.algorithms.algorithm import Algorithm
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.learner import LearnerGroup
@@ -46,7 +48,12 @@ class PPO(Algorithm):
         self._sync_weights(self.learner_group.get_weights())
 
     def training_step(self) -> dict:
+        t0 = time.perf_counter()
         batches = self._sample(self.config.train_batch_size)
+        t1 = time.perf_counter()
         stats = self.learner_group.update("ppo", batches)
+        t2 = time.perf_counter()
         self._sync_weights(self.learner_group.get_weights())
+        stats = dict(stats, sample_time_s=t1 - t0, learn_time_s=t2 - t1,
+                     sync_time_s=time.perf_counter() - t2)
         return stats

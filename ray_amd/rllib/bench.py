@@ -21,9 +21,11 @@ def bench_ppo(args):
 
     n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", "8"))
     ray.init(num_cpus=max(n_runners + 2, os.cpu_count() or 1), ignore_reinit_error=True)
+    # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
+    runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
     cfg = (PPOConfig().environment("SyntheticAtari-v0")
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
-                        rollout_fragment_length=100)
+                        rollout_fragment_length=100, num_gpus_per_env_runner=runner_gpus)
            .training(train_batch_size=5000, minibatch_size=500, num_epochs=10, lr=1e-4,
                      lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
                      entropy_coeff=0.01, model={"vf_share_layers": True})
@@ -49,8 +51,50 @@ def bench_ppo(args):
         "data": "synthetic",
         "config": {"model": "nature-cnn-ppo", "env": "SyntheticAtari-v0 84x84x4",
                    "env_runners": n_runners, "envs_per_runner": 5, "train_batch_size": 5000,
-                   "minibatch_size": 500, "num_epochs": 10, "parallelism": "1 learner"},
-        "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss")},
+                   "minibatch_size": 500, "num_epochs": 10, "parallelism": "1 learner",
+                   "env_runner_gpus": runner_gpus},
+        "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
+                                                     "sample_time_s", "learn_time_s",
+                                                     "sync_time_s")},
+    }), flush=True)
+    algo.stop()
+    ray.shutdown()
+
+
+def bench_impala(args):
+    """RLlib IMPALA synthetic-Atari throughput (BASELINE.json config 5, 1-learner slice):
+    asynchronous env-runner sampling + V-trace HIP kernel learner on one MI355X."""
+    import ray_amd as ray
+    from ray_amd.rllib.algorithms import IMPALAConfig
+
+    n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", "8"))
+    ray.init(num_cpus=max(n_runners + 2, os.cpu_count() or 1), ignore_reinit_error=True)
+    cfg = (IMPALAConfig().environment("SyntheticAtari-v0")
+           .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
+                        rollout_fragment_length=50)
+           .training(train_batch_size=500, lr=6e-4, vf_loss_coeff=0.5, entropy_coeff=0.01,
+                     grad_clip=40.0)
+           .learners(num_learners=0, num_gpus_per_learner=1)
+           .debugging(seed=0))
+    cfg.min_time_s_per_iteration = 2.0
+    algo = cfg.build()
+    for _ in range(args.warmup):
+        algo.train()
+    t0 = time.perf_counter()
+    steps = 0
+    for _ in range(args.steps):
+        r = algo.train()
+        steps += r["num_env_steps_sampled_this_iter"]
+    dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "rllib_impala_synthetic_atari_env_steps_per_sec",
+        "value": round(steps / dt, 1), "unit": "env_steps/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic",
+        "config": {"model": "nature-cnn-impala", "env": "SyntheticAtari-v0 84x84x4",
+                   "env_runners": n_runners, "envs_per_runner": 5, "rollout_fragment_length": 50,
+                   "train_batch_size": 500, "parallelism": "1 learner"},
     }), flush=True)
     algo.stop()
     ray.shutdown()

@@ -56,7 +56,10 @@ class Learner:
         self.module = RLModule(observation_space, action_space, config.get("model")).to(device)
         from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams
 
-        self.flat = FlatParams(self.module, dtype=torch.float32)
+        # bf16 compute weights + fp32 master in the flat optimizer on GPU: no per-forward
+        # autocast weight casts (they were ~30 copy kernels per SGD step)
+        bf16 = device.type == "cuda" and config.get("learner_bf16", True)
+        self.flat = FlatParams(self.module, dtype=torch.bfloat16 if bf16 else torch.float32)
         self.ddp = FlatDDP(self.flat, bucket_mb=32.0)
         self.opt = FlatAdamW(self.flat, lr=config.get("lr", 5e-5), betas=(0.9, 0.999), eps=1e-7,
                              weight_decay=0.0, max_grad_norm=config.get("grad_clip"),
@@ -130,7 +133,22 @@ class Learner:
         mb = min(int(c.get("minibatch_size", 128)), N)
         stats_acc = torch.zeros(6, device=dev)
         n_mb = 0
-        for _ in range(int(c.get("num_epochs", 1))):
+        g = self._ppo_graph(obs_flat, old_di, acts, old_logp, adv, vtarg, mb)
+        if g is not None:
+            # replay one captured SGD step (gather, fwd, fused loss, bwd) per minibatch;
+            # the optimizer's two kernels stay eager (Adam's step count is a kernel arg)
+            idx_buf, stats_buf = self._graph_io
+            stats_buf.zero_()
+            for _ in range(int(c.get("num_epochs", 1))):
+                perm = torch.randperm(N, device=dev)
+                for s in range(0, N - mb + 1, mb):
+                    idx_buf.copy_(perm[s:s + mb])
+                    g.replay()
+                    self.ddp.finish()
+                    self.opt.step()
+                    n_mb += 1
+            stats_acc = stats_buf
+        for _ in range(int(c.get("num_epochs", 1)) if g is None else 0):
             perm = torch.randperm(N, device=dev)
             for s in range(0, N - mb + 1, mb):
                 idx = perm[s:s + mb]
@@ -152,6 +170,65 @@ class Learner:
                 "entropy": stats[3], "mean_kl_loss": kl, "clip_frac": stats[5],
                 "curr_kl_coeff": self.kl_coeff, "num_minibatches": n_mb,
                 "vf_explained_var": _explained_var(vtarg, vals.reshape(-1))}
+
+    def _ppo_graph(self, obs, old_di, acts, old_logp, adv, vtarg, mb):
+        """HIP graph of one PPO SGD step over static full-batch buffers (the minibatch
+        is gathered inside the graph from a static index buffer). Re-captured when the
+        batch shape or the adaptive KL coefficient (a kernel scalar) changes. Single
+        learner only: multi-learner steps all-reduce inside backward."""
+        if (self.device.type != "cuda" or self.world > 1
+                or not self.config.get("learner_cuda_graph", True)
+                or getattr(self, "_graph_failed", False)):
+            return None
+        src = (obs, old_di, acts, old_logp, adv, vtarg)
+        key = (mb, self.kl_coeff) + tuple((tuple(t.shape), t.dtype) for t in src)
+        if getattr(self, "_graph_key", None) == key:
+            for d, s in zip(self._graph_bufs, src):
+                d.copy_(s)
+            return self._graph
+        self._graph = None
+        try:
+            self._graph = self._capture_ppo_graph(src, mb)
+            self._graph_key = key
+        except Exception as e:  # noqa: BLE001
+            import warnings
+
+            warnings.warn(f"PPO learner graph capture failed ({e!r}); running eagerly")
+            self._graph_failed = True
+            torch.cuda.synchronize()
+            self.flat.zero_grad()
+        return self._graph
+
+    def _capture_ppo_graph(self, src, mb):
+        dev = self.device
+        self._graph_bufs = bufs = [torch.empty_like(t) for t in src]
+        for d, s in zip(bufs, src):
+            d.copy_(s)
+        idx = torch.zeros(mb, dtype=torch.long, device=dev)
+        stats = torch.zeros(6, device=dev)
+        self._graph_io = (idx, stats)
+        obs, old_di, acts, old_logp, adv, vtarg = bufs
+
+        def body():
+            self.flat.zero_grad()
+            out = self._fwd(obs.index_select(0, idx))
+            loss, st = self._ppo_loss(out, old_di.index_select(0, idx), acts.index_select(0, idx),
+                                      old_logp.index_select(0, idx), adv.index_select(0, idx),
+                                      vtarg.index_select(0, idx))
+            loss.backward()
+            stats.add_(st.detach())
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):  # warm kernels and solver choices; no optimizer step
+                body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            body()
+        self.flat.zero_grad()
+        return graph
 
     def _ppo_loss(self, out, old_di, acts, old_logp, adv, vtarg):
         c = self.config
