@@ -129,6 +129,21 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
                                "ignore_reinit_error=True to ignore this.")
         if address is None:
             address = os.environ.get("RAY_ADDRESS") or os.environ.get("RAY_AMD_ADDRESS")
+        if address and address.startswith("ray://"):
+            # Ray Client mode: every API call is forwarded to a client server
+            from ray_amd.util.client import DEFAULT_PORT, ClientCoreWorker
+
+            hp = address[len("ray://"):]
+            host, _, port = hp.partition(":")
+            cw = ClientCoreWorker(host or "127.0.0.1", int(port or DEFAULT_PORT), namespace,
+                                  runtime_env)
+            global_worker.core = cw
+            global_worker.mode = SCRIPT_MODE
+            global_worker.session_dir = address
+            global_worker.namespace = cw.namespace
+            global_worker.node_started_here = False
+            atexit.register(shutdown)
+            return RayContext(global_worker)
         if address in (None, "local", ""):
             session = new_session_dir() if _temp_dir is None else os.path.join(
                 _temp_dir, os.path.basename(new_session_dir()))

@@ -100,6 +100,19 @@ def cmd_start(a):
     proc, _addr = W._start_raylet(session, a.num_cpus, a.num_gpus, resources, osm, labels,
                                   detach_output=True)
     pids = {"raylet": proc.pid}
+    if getattr(a, "ray_client_server_port", None):
+        import subprocess
+
+        env = dict(os.environ)
+        pkg = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
+                                   else "")
+        out = open(os.path.join(session, "client_server.out"), "ab")
+        cs = subprocess.Popen([sys.executable, "-m", "ray_amd.util.client.server", "--address",
+                               session, "--port", str(a.ray_client_server_port)], env=env,
+                              stdout=out, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                              start_new_session=True, close_fds=True)
+        pids["client_server"] = cs.pid
     url = None
     if a.include_dashboard:
         from ray_amd.dashboard import start_dashboard
@@ -150,7 +163,7 @@ def cmd_stop(a):
     except FileNotFoundError:
         pass
     # dashboard first (it is a driver of the cluster), then the raylet, which reaps workers
-    for name in ("dashboard", "raylet"):
+    for name in ("client_server", "dashboard", "raylet"):
         pid = pids.get(name)
         if pid and _pid_alive(pid):
             os.kill(pid, signal.SIGKILL if a.force else signal.SIGTERM)
@@ -394,6 +407,8 @@ def build_parser():
     s.add_argument("--dashboard-host", default="127.0.0.1")
     s.add_argument("--dashboard-port", type=int, default=8265)
     s.add_argument("--block", action="store_true")
+    s.add_argument("--ray-client-server-port", type=int, default=None,
+                   help="also serve Ray Client connections (ray://127.0.0.1:<port>)")
     s.set_defaults(fn=cmd_start)
 
     s = sub.add_parser("stop", help="stop the running cluster")

@@ -1,0 +1,172 @@
+"""Ray Client server (reference: python/ray/util/client/server/server.py).
+
+A driver of the cluster that serves client connections: one thread and one session
+(table of server-side ObjectRefs / ActorHandles held for that client) per
+connection. Closing the connection releases everything the session holds.
+
+    python -m ray_amd.util.client.server --address auto --port 10001
+"""
+
+from __future__ import annotations
+
+import argparse
+import pickle
+import threading
+import traceback
+from multiprocessing.connection import Listener
+
+import cloudpickle
+
+import ray_amd as ray
+from ray_amd.util.client import common
+
+
+class _Session:
+    def __init__(self, cw):
+        self.cw = cw
+        self.refs = {}
+        self.actors = {}
+
+    def dumps(self, obj):
+        def on_ref(r):
+            self.refs[r._id] = r
+            return ("ref", r._id)
+
+        def on_actor(h):
+            self.actors[h._actor_id] = h
+            return ("actor", h._actor_id, h._class_name, h._meta)
+
+        return common.dumps(obj, on_ref, on_actor)
+
+    def loads(self, data):
+        def load(pid):
+            if pid[0] == "ref":
+                return self.refs[pid[1]]
+            return self.actors[pid[1]]
+
+        return common.loads(data, load)
+
+    def keep(self, refs):
+        for r in refs:
+            self.refs[r._id] = r
+        return [r._id for r in refs]
+
+    # ---------------------------------------------------------------- ops
+    def op_init(self, namespace, runtime_env):
+        cw = self.cw
+        return {"namespace": cw.namespace, "job_id": cw.job_id, "node_id": cw.node_id,
+                "server_version": ray.__version__}
+
+    def op_export(self, blob):
+        return self.cw.export(cloudpickle.loads(blob))
+
+    def op_put(self, blob):
+        return self.keep([ray.put(self.loads(blob))])[0]
+
+    def op_get(self, oids, timeout):
+        return self.dumps(ray.get([self.refs[o] for o in oids], timeout=timeout))
+
+    def op_wait(self, oids, num_returns, timeout):
+        ready, _ = ray.wait([self.refs[o] for o in oids], num_returns=num_returns,
+                            timeout=timeout)
+        return [r._id for r in ready]
+
+    def op_task(self, key, blob, opts, name):
+        args, kwargs = self.loads(blob)
+        return self.keep(self.cw.submit_task(key, args, kwargs, opts, name))
+
+    def op_actor(self, aid, key, blob, opts, cls_name, meta):
+        from ray_amd.actor import ActorHandle
+
+        args, kwargs = self.loads(blob)
+        cw = self.cw
+        res = cw.create_actor(aid, key, args, kwargs, opts, cls_name, meta)
+        if res and res.get("existing"):
+            h = ActorHandle(res["existing"], res["class_name"], res["method_meta"], res["owner"])
+            cw._subscribe_actor(res["existing"])
+            self.actors[res["existing"]] = h
+        else:
+            if opts.get("name") or opts.get("lifetime") == "detached":
+                cw.actor_escaped.add(aid)
+            self.actors[aid] = ActorHandle(aid, cls_name, meta, cw.addr)
+        return res
+
+    def op_actor_task(self, aid, method, blob, opts):
+        args, kwargs = self.loads(blob)
+        if aid not in self.actors:
+            raise ValueError(f"unknown actor {aid.hex()} in this client session")
+        return self.keep(self.cw.submit_actor_task(aid, method, args, kwargs, opts))
+
+    def op_kill(self, aid, no_restart):
+        self.cw.kill_actor(aid, no_restart)
+
+    def op_cancel(self, oid, force, recursive):
+        self.cw.cancel(self.refs[oid], force, recursive)
+
+    def op_raylet(self, method, args):
+        from ray_amd.actor import ActorHandle
+
+        out = self.cw.call_raylet(method, *args)
+        if method == "get_named_actor" and out:
+            self.actors[out["actor_id"]] = ActorHandle._from_info(
+                out["actor_id"], out["class_name"], out["method_meta"], out["owner"])
+        return out
+
+    def op_release(self, oid):
+        self.refs.pop(oid, None)
+
+    def op_release_actor(self, aid):
+        self.actors.pop(aid, None)
+
+
+def _serve_conn(conn, cw):
+    s = _Session(cw)
+    try:
+        while True:
+            try:
+                op, args = pickle.loads(conn.recv_bytes())
+            except (EOFError, OSError):
+                break
+            if op == "disconnect":
+                conn.send_bytes(pickle.dumps((True, None)))
+                break
+            try:
+                out = (True, getattr(s, "op_" + op)(*args))
+            except Exception as e:  # noqa: BLE001
+                try:
+                    pickle.dumps(e)
+                except Exception:
+                    e = RuntimeError(f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
+                out = (False, e)
+            conn.send_bytes(pickle.dumps(out, protocol=5))
+    finally:
+        s.refs.clear()
+        s.actors.clear()
+        conn.close()
+
+
+def serve(address, host="127.0.0.1", port=10001, ready_event=None):
+    ray.init(address=address, namespace=None, ignore_reinit_error=True)
+    from ray_amd._private import worker as W
+
+    cw = W.global_worker.core
+    lst = Listener((host, port), authkey=common.AUTHKEY)
+    if ready_event is not None:
+        ready_event.set()
+    print(f"ray_amd client server listening on ray://{host}:{lst.address[1]}", flush=True)
+    while True:
+        conn = lst.accept()
+        threading.Thread(target=_serve_conn, args=(conn, cw), daemon=True).start()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--address", default="auto")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=10001)
+    a = ap.parse_args()
+    serve(a.address, a.host, a.port)
+
+
+if __name__ == "__main__":
+    main()
