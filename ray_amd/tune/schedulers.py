@@ -188,16 +188,127 @@ class PopulationBasedTraining(TrialScheduler):
 
 
 class PB2(PopulationBasedTraining):
-    """PB2 requires GP libraries that are not installed; behaves as PBT."""
+    """Population Based Bandits (Parker-Holder et al. 2020; reference:
+    python/ray/tune/schedulers/pb2.py). Exploit like PBT, but explore by GP-UCB instead
+    of random perturbation: a Gaussian process (RBF kernel, numpy — no GPy needed) is
+    fitted to (time, normalised hyperparameters) -> reward change over the last
+    perturbation interval, and the new configuration maximises mu + kappa * sigma over
+    random candidates inside ``hyperparam_bounds``."""
+
+    def __init__(self, time_attr="training_iteration", metric=None, mode=None,
+                 perturbation_interval=5, hyperparam_bounds=None, quantile_fraction=0.25,
+                 log_config=False, require_attrs=True, synch=False, seed=None,
+                 kappa=2.0, n_candidates=512):
+        super().__init__(time_attr, metric, mode, perturbation_interval, {},
+                         quantile_fraction, 0.0, (1.2, 0.8), None, seed)
+        self.bounds = {k: (float(v[0]), float(v[1])) for k, v in (hyperparam_bounds or {}).items()}
+        self.kappa = kappa
+        self.n_cand = n_candidates
+        self.np_rng = np.random.default_rng(seed)
+        self.data = []  # (t, x_norm..., dy)
+        self.prev = {}  # trial_id -> (t, score)
+
+    def _norm(self, cfg):
+        return [(float(cfg.get(k, lo)) - lo) / max(hi - lo, 1e-12)
+                for k, (lo, hi) in self.bounds.items()]
+
+    def on_trial_result(self, runner, trial, result):
+        t = result.get(self.time_attr, 0)
+        sc = self._score(result)
+        if sc is not None and t - self.last.get(trial.trial_id, 0) >= self.interval:
+            pt = self.prev.get(trial.trial_id)
+            if pt is not None:
+                self.data.append([t] + self._norm(trial.config) + [sc - pt[1]])
+                self.data = self.data[-256:]
+            self.prev[trial.trial_id] = (t, sc)
+        return super().on_trial_result(runner, trial, result)
+
+    @staticmethod
+    def _gp(X, y, Xs, ls=0.3, noise=1e-2):
+        def k(a, b):
+            d = ((a[:, None, :] - b[None, :, :]) ** 2).sum(-1)
+            return np.exp(-0.5 * d / ls ** 2)
+
+        K = k(X, X) + noise * np.eye(len(X))
+        L = np.linalg.cholesky(K)
+        alpha = np.linalg.solve(L.T, np.linalg.solve(L, y))
+        Ks = k(Xs, X)
+        mu = Ks @ alpha
+        v = np.linalg.solve(L, Ks.T)
+        var = np.clip(1.0 - (v ** 2).sum(0), 1e-12, None)
+        return mu, np.sqrt(var)
+
+    def _explore(self, config):
+        new = copy.deepcopy(config)
+        if not self.bounds:
+            return new
+        d = len(self.bounds)
+        cand = self.np_rng.random((self.n_cand, d))
+        if len(self.data) >= 3:
+            D = np.asarray(self.data, np.float64)
+            tmax = max(D[:, 0].max(), 1.0)
+            X = np.concatenate([D[:, :1] / tmax, D[:, 1:1 + d]], 1)
+            y = D[:, -1]
+            y = (y - y.mean()) / (y.std() + 1e-8)
+            Xs = np.concatenate([np.ones((self.n_cand, 1)), cand], 1)
+            mu, sd = self._gp(X, y, Xs)
+            best = cand[int(np.argmax(mu + self.kappa * sd))]
+        else:
+            best = cand[0]  # not enough data yet: uniform sample
+        for (k, (lo, hi)), u in zip(self.bounds.items(), best):
+            val = lo + float(u) * (hi - lo)
+            new[k] = int(round(val)) if isinstance(config.get(k), int) else val
+        return new
+
+
+def evenly_distribute_cpus_gpus(runner, trial, result, scheduler):
+    """Reference DistributeResources: split the cluster's CPUs/GPUs evenly over the live
+    trials (never below the trial's base request)."""
+    import ray_amd as ray
+
+    live = [t for t in runner.trials if t.status in ("RUNNING", "PENDING")] or [trial]
+    tot = ray.cluster_resources()
+    base = scheduler.base_resources.setdefault(trial.trial_id, dict(trial.resources))
+    out = dict(base)
+    out["CPU"] = max(base.get("CPU", 1), float(int(tot.get("CPU", 1) // len(live))))
+    if base.get("GPU"):
+        out["GPU"] = max(base["GPU"], float(int(tot.get("GPU", 0) // len(live))))
+    return out
+
+
+DistributeResources = evenly_distribute_cpus_gpus
 
 
 class ResourceChangingScheduler(TrialScheduler):
+    """Re-allocates trial resources while they run (reference:
+    python/ray/tune/schedulers/resource_changing_scheduler.py): after each result the
+    allocation function proposes resources; a change checkpoints-and-restarts the trial
+    with the new request (same config)."""
+
     def __init__(self, base_scheduler=None, resources_allocation_function=None):
         super().__init__()
         self.base = base_scheduler or FIFOScheduler()
+        self.alloc = resources_allocation_function or evenly_distribute_cpus_gpus
+        self.base_resources = {}
+        self.num_reallocations = 0
 
     def set_search_properties(self, metric, mode):
         self.base.set_search_properties(metric, mode)
 
+    def on_trial_add(self, runner, trial):
+        self.base_resources[trial.trial_id] = dict(trial.resources)
+        if hasattr(self.base, "on_trial_add"):
+            self.base.on_trial_add(runner, trial)
+
     def on_trial_result(self, runner, trial, result):
-        return self.base.on_trial_result(runner, trial, result)
+        decision = self.base.on_trial_result(runner, trial, result)
+        if decision != self.CONTINUE or trial.pending_exploit is not None:
+            return decision
+        new = self.alloc(runner, trial, result, self)
+        if new and {k: float(v) for k, v in new.items()} != \
+                {k: float(v) for k, v in trial.resources.items()} and \
+                trial.last_checkpoint is not None:
+            trial.pending_exploit = (trial.last_checkpoint, trial.config)
+            trial.pending_resources = dict(new)
+            self.num_reallocations += 1
+        return decision

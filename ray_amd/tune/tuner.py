@@ -329,9 +329,13 @@ class _Controller:
         return t
 
     def _launch(self, t: Trial, checkpoint=None):
-        opts = {"num_cpus": self.resources.get("CPU", 1)}
-        if self.resources.get("GPU"):
-            opts["num_gpus"] = self.resources["GPU"]
+        res = t.resources or self.resources
+        opts = {"num_cpus": res.get("CPU", 1)}
+        if res.get("GPU"):
+            opts["num_gpus"] = res["GPU"]
+        extra = {k: v for k, v in res.items() if k not in ("CPU", "GPU")}
+        if extra:
+            opts["resources"] = extra
         t.actor = self.actor_cls.options(**opts).remote(self.trainable, t.config, t.local_path,
                                                         t.trial_id, f"trial_{t.trial_id}",
                                                         checkpoint)
@@ -429,6 +433,9 @@ class _Controller:
                     t.status = "PENDING"
                     t.config = cfg
                     t.restore_from = ckpt
+                    if getattr(t, "pending_resources", None):
+                        t.resources = t.pending_resources
+                        t.pending_resources = None
                     t._asha_rungs = set()
                     continue
                 t.pending_ref = t.actor.next_result.remote()

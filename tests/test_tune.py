@@ -123,3 +123,53 @@ def test_sample_domains():
                                 num_samples=3, seed=0))
     assert len(vs) == 6
     assert all(0 <= v["x"] < 5 and 1e-4 <= v["y"] <= 1e-1 and v["w"] == 2 * v["x"] for v in vs)
+
+
+def _ckpt_trainable(config):
+    step, val = 0, 0.0
+    ck = train.get_checkpoint()
+    if ck:
+        with open(os.path.join(ck.path, "s")) as fh:
+            step, val = map(float, fh.read().split())
+    while step < 12:
+        step += 1
+        val += config["lr"]
+        time.sleep(0.05)
+        d = os.path.join(config["tmp"], f"{os.getpid()}_{step}_{config['lr']}_{time.time()}")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "s"), "w") as fh:
+            fh.write(f"{step} {val}")
+        cpus = ray.get_runtime_context().get_assigned_resources().get("CPU", 0)
+        train.report({"val": val, "cpus": cpus}, checkpoint=tune.Checkpoint(d))
+
+
+def test_pb2_gp_explore(cluster, tmp_path):
+    from ray_amd.tune.schedulers import PB2
+
+    pb2 = PB2(metric="val", mode="max", perturbation_interval=3,
+              hyperparam_bounds={"lr": [0.01, 2.0]}, seed=0)
+    rg = tune.Tuner(_ckpt_trainable,
+                    param_space={"lr": tune.grid_search([0.01, 0.05, 1.0, 2.0]),
+                                 "tmp": str(tmp_path)},
+                    tune_config=tune.TuneConfig(scheduler=pb2, max_concurrent_trials=4),
+                    run_config=tune.RunConfig(storage_path=str(tmp_path / "r"))).fit()
+    assert pb2.num_perturbations > 0 and len(pb2.data) > 0
+    assert rg.get_best_result("val", "max").metrics["val"] > 1.0
+    # explored configs stay inside the bounds
+    for r in rg:
+        assert 0.01 <= r.config["lr"] <= 2.0
+
+
+def test_resource_changing_scheduler(cluster, tmp_path):
+    from ray_amd.tune.schedulers import ResourceChangingScheduler
+
+    sched = ResourceChangingScheduler()
+    rg = tune.Tuner(_ckpt_trainable,
+                    param_space={"lr": tune.grid_search([0.1, 0.2]), "tmp": str(tmp_path)},
+                    tune_config=tune.TuneConfig(scheduler=sched, metric="val", mode="max",
+                                                max_concurrent_trials=2),
+                    run_config=tune.RunConfig(storage_path=str(tmp_path / "r"))).fit()
+    # 4 CPUs over 2 trials: both grow from 1 to 2 CPUs (checkpoint + restart) and finish
+    assert sched.num_reallocations >= 2
+    assert all(abs(r.metrics["val"] - 12 * r.config["lr"]) < 1e-6 for r in rg)
+    assert all(r.metrics["cpus"] == 2 for r in rg)
