@@ -3,7 +3,7 @@
 from ray_amd.air.config import CheckpointConfig, FailureConfig, RunConfig  # noqa: F401
 from ray_amd.train._checkpoint import Checkpoint  # noqa: F401
 from ray_amd.train._internal.session import get_checkpoint, get_context, report  # noqa: F401
-from ray_amd.tune import schedulers  # noqa: F401
+from ray_amd.tune import schedulers, search  # noqa: F401
 from ray_amd.tune.search.sample import (choice, grid_search, lograndint, loguniform,  # noqa
                                         qlograndint, qloguniform, qrandint, qrandn, quniform,
                                         randint, randn, sample_from, uniform)

@@ -279,8 +279,14 @@ class _Controller:
         self.searcher.set_search_properties(tc.metric, tc.mode, space)
         base = self.searcher.searcher if isinstance(self.searcher, ConcurrencyLimiter) else \
             self.searcher
+        # reference SearchGenerator (tune/search/search_generator.py): a non-variant searcher
+        # is asked for at most num_samples configs
+        self._suggest_limit = None
         if isinstance(base, BasicVariantGenerator):
             base._setup(space, tc.num_samples)
+        elif tc.num_samples and tc.num_samples > 0:
+            self._suggest_limit = tc.num_samples
+        self._n_suggested = 0
         self.trials: list[Trial] = []
         self.stopper = self._make_stopper(rc.stop)
         self.exhausted = False
@@ -316,6 +322,9 @@ class _Controller:
     def _new_trial(self):
         if self.exhausted:
             return None
+        if self._suggest_limit is not None and self._n_suggested >= self._suggest_limit:
+            self.exhausted = True
+            return None
         tid = uuid.uuid4().hex[:8]
         cfg = self.searcher.suggest(tid)
         if cfg == "PAUSE":
@@ -323,6 +332,7 @@ class _Controller:
         if cfg is None:
             self.exhausted = True
             return None
+        self._n_suggested += 1
         t = Trial(cfg, tid, self.exp_dir, self.resources)
         self.trials.append(t)
         self.scheduler.on_trial_add(self, t)

