@@ -19,6 +19,7 @@ from ray_amd.rllib.env.envs import make_env
 
 class Algorithm:
     kind = "ppo"
+    supports_multi_agent = False
 
     def __init__(self, config):
         if not ray.is_initialized():
@@ -29,15 +30,29 @@ class Algorithm:
         probe = make_env(config.env, config.env_config)
         self.observation_space = probe.observation_space
         self.action_space = probe.action_space
+        self.is_multi_agent = bool(getattr(config, "is_multi_agent", False))
+        if self.is_multi_agent and not self.supports_multi_agent:
+            raise NotImplementedError(f"{type(self).__name__} does not support multi-agent "
+                                      "configs yet (PPO does)")
+        if self.is_multi_agent:
+            self.module_specs = self._module_specs(config, probe)
+            self.cfg["_module_specs"] = self.module_specs
         probe.close()
         self.iteration = 0
         self.total_env_steps = 0
         self.weights_version = 0
         self._episode_returns = []
         self._episode_lengths = []
+        self._module_returns = {}
         self._t_start = time.time()
         nr = int(config.num_env_runners)
-        runner_cls = ray.remote(SingleAgentEnvRunner)
+        local_cls = SingleAgentEnvRunner
+        if self.is_multi_agent:
+            from ray_amd.rllib.env.multi_agent_env_runner import MultiAgentEnvRunner
+
+            local_cls = MultiAgentEnvRunner
+        self._runner_cls = local_cls
+        runner_cls = ray.remote(local_cls)
         opts = {"num_cpus": config.num_cpus_per_env_runner}
         if config.num_gpus_per_env_runner:
             opts["num_gpus"] = config.num_gpus_per_env_runner
@@ -48,8 +63,37 @@ class Algorithm:
             self.local_runner = None
         else:
             self.env_runners = []
-            self.local_runner = SingleAgentEnvRunner(self.cfg, 0)
+            self.local_runner = local_cls(self.cfg, 0)
         self.setup()
+
+    @staticmethod
+    def _module_specs(config, probe):
+        """{module_id: (observation_space, action_space)}; spaces not given in ``policies``
+        come from the first agent ``policy_mapping_fn`` routes to that module."""
+        from ray_amd.rllib.env.multi_agent_env_runner import DEFAULT_MODULE_ID, _default_mapping
+
+        pols = config.policies
+        ids = list(pols) if not isinstance(pols, dict) else list(pols.keys())
+        ids = ids or [DEFAULT_MODULE_ID]
+        fn = config.policy_mapping_fn or _default_mapping
+        agents = sorted(probe.get_agent_ids(), key=str) if hasattr(probe, "get_agent_ids") \
+            else []
+        specs = {}
+        for mid in ids:
+            spec = pols.get(mid) if isinstance(pols, dict) else None
+            os_ = getattr(spec, "observation_space", None) or \
+                (spec[0] if isinstance(spec, (tuple, list)) and len(spec) >= 2 else None)
+            as_ = getattr(spec, "action_space", None) or \
+                (spec[1] if isinstance(spec, (tuple, list)) and len(spec) >= 2 else None)
+            if os_ is None or as_ is None:
+                aid = next((a for a in agents if fn(a, None) == mid), agents[0] if agents
+                           else None)
+                os_ = os_ or (probe.get_observation_space(aid) if aid is not None
+                              else probe.observation_space)
+                as_ = as_ or (probe.get_action_space(aid) if aid is not None
+                              else probe.action_space)
+            specs[mid] = (os_, as_)
+        return specs
 
     def setup(self):
         pass
@@ -71,9 +115,12 @@ class Algorithm:
         for m in ms:
             self._episode_returns.extend(m["episode_returns"])
             self._episode_lengths.extend(m["episode_lengths"])
+            for mid, rs in m.get("module_episode_returns", {}).items():
+                self._module_returns.setdefault(mid, []).extend(rs)
         k = self.config.metrics_num_episodes_for_smoothing
         self._episode_returns = self._episode_returns[-k:]
         self._episode_lengths = self._episode_lengths[-k:]
+        self._module_returns = {mid: r[-k:] for mid, r in self._module_returns.items()}
 
     # ---------------------------------------------------------------- train loop
     def train(self) -> dict:
@@ -98,6 +145,9 @@ class Algorithm:
                 if self._episode_lengths else float("nan"),
                 "num_episodes": len(rets),
             },
+            **({"module_episode_returns_mean": {
+                mid: float(np.mean(r)) for mid, r in self._module_returns.items() if r}}
+               if self.is_multi_agent else {}),
             "num_env_steps_sampled_lifetime": self.total_env_steps,
             "num_env_steps_sampled_this_iter": self.total_env_steps - steps0,
             "env_steps_per_sec": (self.total_env_steps - steps0) / max(dt, 1e-9),
@@ -133,7 +183,7 @@ class Algorithm:
         return batches
 
     def evaluate(self) -> dict:
-        runner = SingleAgentEnvRunner(self.cfg, 999)
+        runner = self._runner_cls(self.cfg, 999)
         runner.set_weights(self.get_weights(), None)
         n = self.config.evaluation_duration
         rets = []
@@ -143,15 +193,26 @@ class Algorithm:
         return {"env_runners": {"episode_return_mean": float(np.mean(rets[:n]))}}
 
     # ---------------------------------------------------------------- inference
-    def compute_single_action(self, obs, explore=False):
+    def compute_single_action(self, obs, explore=False, policy_id=None):
         import torch
 
         from ray_amd.rllib.core.rl_module import RLModule
 
-        if not hasattr(self, "_infer_module"):
-            self._infer_module = RLModule(self.observation_space, self.action_space,
-                                          self.config.model)
-        self._infer_module.load_state_dict(self.get_weights())
+        if self.is_multi_agent:
+            from ray_amd.rllib.env.multi_agent_env_runner import DEFAULT_MODULE_ID
+
+            mid = policy_id or DEFAULT_MODULE_ID
+            os_, as_ = self.module_specs[mid]
+            mods = self.__dict__.setdefault("_infer_modules", {})
+            if mid not in mods:
+                mods[mid] = RLModule(os_, as_, self.config.model)
+            self._infer_module = mods[mid]
+            self._infer_module.load_state_dict(self.get_weights()[mid])
+        else:
+            if not hasattr(self, "_infer_module"):
+                self._infer_module = RLModule(self.observation_space, self.action_space,
+                                              self.config.model)
+            self._infer_module.load_state_dict(self.get_weights())
         with torch.no_grad():
             x = torch.as_tensor(np.asarray(obs)[None])
             di = self._infer_module.forward_inference(x)["action_dist_inputs"]
@@ -180,8 +241,10 @@ class Algorithm:
 
         d = checkpoint_dir or tempfile.mkdtemp(prefix="rllib_ckpt_")
         os.makedirs(d, exist_ok=True)
+        import cloudpickle  # policy_mapping_fn is usually a lambda
+
         with open(os.path.join(d, "algorithm_state.pkl"), "wb") as f:
-            pickle.dump(self.get_state(), f)
+            cloudpickle.dump(self.get_state(), f)
         from ray_amd.train._checkpoint import Checkpoint
 
         return Checkpoint(d)

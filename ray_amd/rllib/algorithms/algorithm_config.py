@@ -36,6 +36,9 @@ class AlgorithmConfig:
         self.metrics_num_episodes_for_smoothing = 100
         self.input_ = None
         self.output = None
+        self.policies = None
+        self.policy_mapping_fn = None
+        self.policies_to_train = None
 
     # ---------------------------------------------------------------- builders
     def environment(self, env=None, *, env_config=None, **kw):
@@ -122,6 +125,22 @@ class AlgorithmConfig:
         if output is not None:
             self.output = output
         return self
+
+    def multi_agent(self, *, policies=None, policy_mapping_fn=None, policies_to_train=None,
+                    **kw):
+        """reference: AlgorithmConfig.multi_agent -- ``policies`` is a set/list of module ids
+        or a dict id -> (observation_space, action_space) / PolicySpec / None."""
+        if policies is not None:
+            self.policies = policies
+        if policy_mapping_fn is not None:
+            self.policy_mapping_fn = policy_mapping_fn
+        if policies_to_train is not None:
+            self.policies_to_train = list(policies_to_train)
+        return self
+
+    @property
+    def is_multi_agent(self):
+        return self.policies is not None
 
     def api_stack(self, **kw):
         return self

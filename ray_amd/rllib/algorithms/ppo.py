@@ -32,6 +32,7 @@ class PPOConfig(AlgorithmConfig):
 
 class PPO(Algorithm):
     kind = "ppo"
+    supports_multi_agent = True
 
     def __init__(self, config):
         if config.rollout_fragment_length == "auto":
@@ -44,7 +45,14 @@ class PPO(Algorithm):
         return PPOConfig()
 
     def setup(self):
-        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space)
+        if self.is_multi_agent:
+            from ray_amd.rllib.core.learner import MultiAgentLearnerGroup
+
+            self.learner_group = MultiAgentLearnerGroup(self.cfg, self.module_specs,
+                                                        self.config.policies_to_train)
+        else:
+            self.learner_group = LearnerGroup(self.cfg, self.observation_space,
+                                              self.action_space)
         self._sync_weights(self.learner_group.get_weights())
 
     def training_step(self) -> dict:

@@ -124,16 +124,26 @@ class Learner:
         adv, vtarg = rf.gae(rewards, vals, dones, boot_v, c.get("gamma", 0.99),
                             c.get("lambda_", 0.95))
         adv = adv.reshape(-1)
-        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
         vtarg = vtarg.reshape(-1)
         acts = acts.reshape((T * B,) + tuple(acts.shape[2:]))
         old_logp = old_logp.reshape(-1)
         old_di = old_di.reshape(T * B, -1)
-        N = T * B
+        vals = vals.reshape(-1)
+        masked = "loss_mask" in batch
+        if masked:
+            # multi-agent padding rows (terminated, so GAE never crossed them) are dropped
+            keep = _to_t(batch["loss_mask"], dev).reshape(-1).nonzero().squeeze(1)
+            obs_flat, acts, old_logp, old_di, adv, vtarg, vals = (
+                t.index_select(0, keep)
+                for t in (obs_flat, acts, old_logp, old_di, adv, vtarg, vals))
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        N = adv.shape[0]
         mb = min(int(c.get("minibatch_size", 128)), N)
         stats_acc = torch.zeros(6, device=dev)
         n_mb = 0
-        g = self._ppo_graph(obs_flat, old_di, acts, old_logp, adv, vtarg, mb)
+        # masked (multi-agent) batches change N every update: no graph re-capture per call
+        g = None if masked else self._ppo_graph(obs_flat, old_di, acts, old_logp, adv, vtarg,
+                                                mb)
         if g is not None:
             # replay one captured SGD step (gather, fwd, fused loss, bwd) per minibatch;
             # the optimizer's two kernels stay eager (Adam's step count is a kernel arg)
@@ -169,7 +179,7 @@ class Learner:
         return {"total_loss": stats[0], "policy_loss": stats[1], "vf_loss": stats[2],
                 "entropy": stats[3], "mean_kl_loss": kl, "clip_frac": stats[5],
                 "curr_kl_coeff": self.kl_coeff, "num_minibatches": n_mb,
-                "vf_explained_var": _explained_var(vtarg, vals.reshape(-1))}
+                "vf_explained_var": _explained_var(vtarg, vals)}
 
     def _ppo_graph(self, obs, old_di, acts, old_logp, adv, vtarg, mb):
         """HIP graph of one PPO SGD step over static full-batch buffers (the minibatch
@@ -427,3 +437,38 @@ def _split_b(batch, n, i):
         else:
             out[k] = v
     return out
+
+
+class MultiAgentLearnerGroup:
+    """One LearnerGroup per trainable module (reference: rllib/core/learner/learner_group.py
+    over a MultiRLModule).  Modules are independent networks with independent optimizers,
+    so each gets its own flat-param learner; runner outputs are split by module id."""
+
+    def __init__(self, config: dict, specs: dict, policies_to_train=None):
+        self.specs = specs
+        self.trainable = set(policies_to_train) if policies_to_train else set(specs)
+        self.groups = {mid: LearnerGroup(config, os_, as_) for mid, (os_, as_) in specs.items()}
+
+    def update(self, kind, batches):
+        stats = {}
+        for mid, g in self.groups.items():
+            if mid not in self.trainable:
+                continue
+            mb = [b["modules"][mid] for b in batches if mid in b["modules"]]
+            if mb:
+                stats[mid] = g.update(kind, mb)
+        return stats
+
+    def get_weights(self):
+        return {mid: g.get_weights() for mid, g in self.groups.items()}
+
+    def get_state(self):
+        return {mid: g.get_state() for mid, g in self.groups.items()}
+
+    def set_state(self, s):
+        for mid, st in s.items():
+            self.groups[mid].set_state(st)
+
+    def shutdown(self):
+        for g in self.groups.values():
+            g.shutdown()

@@ -1,0 +1,139 @@
+"""Multi-agent RLlib tests (modelled on rllib/env/tests/test_multi_agent_env.py and
+rllib/examples/multi_agent/multi_agent_cartpole.py)."""
+
+import numpy as np
+import pytest
+
+import ray_amd as ray
+from ray_amd.rllib.algorithms.ppo import PPOConfig
+from ray_amd.rllib.env import MultiAgentCartPole, make_multi_agent
+from ray_amd.rllib.env.multi_agent_env_runner import MultiAgentEnvRunner
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4)
+    yield
+    ray.shutdown()
+
+
+def test_make_multi_agent_env_semantics():
+    env = MultiAgentCartPole({"num_agents": 3})
+    obs, _ = env.reset(seed=1)
+    assert set(obs) == {0, 1, 2} and env.get_agent_ids() == {0, 1, 2}
+    done_all = False
+    steps = 0
+    while not done_all:
+        o, r, te, tr, _ = env.step({a: 0 for a in env.agents})
+        assert set(r) <= {0, 1, 2}
+        done_all = te["__all__"]
+        steps += 1
+    assert 5 < steps < 500 and env.agents == []
+
+
+def _runner_cfg(num_agents=3, mapping=None, policies=("p0", "p1")):
+    env = MultiAgentCartPole({"num_agents": num_agents})
+    specs = {p: (env.observation_space, env.action_space) for p in policies}
+    return {"env": "MultiAgentCartPole", "env_config": {"num_agents": num_agents},
+            "num_envs_per_env_runner": 2, "seed": 0, "_module_specs": specs,
+            "policy_mapping_fn": mapping or (lambda aid, ep, **kw: f"p{aid % 2}"),
+            "model": {"fcnet_hiddens": [16]}}
+
+
+def test_runner_columns_padding_and_mask():
+    r = MultiAgentEnvRunner(_runner_cfg(), 0)
+    out = r.sample(120)
+    assert out["env_steps"] == 240
+    b0, b1 = out["modules"]["p0"], out["modules"]["p1"]
+    # agents 0,2 -> p0 and agent 1 -> p1, in each of the 2 envs
+    assert b0["obs"].shape[:2] == (120, 4) and b1["obs"].shape[:2] == (120, 2)
+    for b in (b0, b1):
+        m = b["loss_mask"]
+        # every padding row is a terminal row (so GAE cannot cross it) with zero reward
+        assert np.all(b["terminateds"][m == 0] == 1) and np.all(b["rewards"][m == 0] == 0)
+        # CartPole: reward 1 on every acted step
+        assert np.all(b["rewards"][m == 1] == 1)
+    total_agent_steps = b0["loss_mask"].sum() + b1["loss_mask"].sum()
+    assert total_agent_steps == out["agent_steps"] > 240
+    # episodes ended, returns are summed over agents
+    met = r.get_metrics()
+    assert met["episode_returns"] and set(met["module_episode_returns"]) == {"p0", "p1"}
+
+
+def test_runner_rejects_unknown_module():
+    with pytest.raises(ValueError):
+        MultiAgentEnvRunner(_runner_cfg(mapping=lambda aid, ep, **kw: "nope"), 0).sample(2)
+
+
+def test_multi_agent_ppo_two_policies_learn(cluster, tmp_path):
+    cfg = (PPOConfig().environment("MultiAgentCartPole", env_config={"num_agents": 2})
+           .env_runners(num_env_runners=2, num_envs_per_env_runner=2)
+           .multi_agent(policies={"p0", "p1"},
+                        policy_mapping_fn=lambda aid, ep, **kw: f"p{aid}")
+           .training(train_batch_size=2000, minibatch_size=256, num_epochs=8, lr=3e-4,
+                     lambda_=0.95, vf_loss_coeff=0.5, clip_param=0.2,
+                     model={"fcnet_hiddens": [64, 64]})
+           .debugging(seed=0))
+    algo = cfg.build()
+    first, best = None, {}
+    for _ in range(10):
+        res = algo.train()
+        mr = res["module_episode_returns_mean"]
+        if first is None and len(mr) == 2:
+            first = dict(mr)
+        for k, v in mr.items():
+            best[k] = max(best.get(k, 0), v)
+        if best and min(best.values()) > 80:
+            break
+    assert {"p0", "p1"} <= set(res["learners"])
+    assert all(best[k] > max(40, 1.5 * first[k]) for k in ("p0", "p1")), (first, best)
+    w = algo.get_weights()
+    assert set(w) == {"p0", "p1"}
+    a = algo.compute_single_action(np.zeros(4, np.float32), policy_id="p1")
+    assert a in (0, 1)
+    ck = algo.save(str(tmp_path / "ck"))
+    algo.stop()
+    algo2 = cfg.build()
+    algo2.restore(ck)
+    w2 = algo2.get_weights()
+    for mid in ("p0", "p1"):
+        for k in w[mid]:
+            assert np.allclose(np.asarray(w[mid][k], np.float32),
+                               np.asarray(w2[mid][k], np.float32))
+    algo2.stop()
+
+
+def test_policies_to_train_freezes_others(cluster):
+    cfg = (PPOConfig().environment("MultiAgentCartPole", env_config={"num_agents": 2})
+           .env_runners(num_env_runners=0)
+           .multi_agent(policies={"p0", "p1"}, policy_mapping_fn=lambda aid, ep, **kw: f"p{aid}",
+                        policies_to_train=["p0"])
+           .training(train_batch_size=400, minibatch_size=128, num_epochs=2,
+                     model={"fcnet_hiddens": [16]}))
+    algo = cfg.build()
+    w0 = {m: {k: np.array(v, np.float32, copy=True) for k, v in w.items()}
+          for m, w in algo.get_weights().items()}
+    res = algo.train()
+    w1 = algo.get_weights()
+    assert "p0" in res["learners"] and "p1" not in res["learners"]
+    k = next(iter(w0["p1"]))
+    assert np.allclose(np.asarray(w0["p1"][k]), np.asarray(w1["p1"][k]))
+    assert not all(np.allclose(np.asarray(w0["p0"][k2]), np.asarray(w1["p0"][k2]))
+                   for k2 in w0["p0"])
+    algo.stop()
+
+
+def test_non_ppo_multi_agent_rejected(cluster):
+    from ray_amd.rllib.algorithms.dqn import DQNConfig
+    cfg = (DQNConfig().environment("MultiAgentCartPole")
+           .multi_agent(policies={"p0"}, policy_mapping_fn=lambda aid, ep, **kw: "p0"))
+    with pytest.raises(NotImplementedError):
+        cfg.build()
+
+
+def test_make_multi_agent_from_creator():
+    from ray_amd.rllib.env import CartPoleEnv
+    cls = make_multi_agent(lambda cfg: CartPoleEnv(cfg))
+    env = cls({"num_agents": 2})
+    obs, _ = env.reset()
+    assert set(obs) == {0, 1}
