@@ -269,5 +269,6 @@ PYBIND11_MODULE(_core, m) {
              return py::make_tuple(nodes, inf);
            })
       .def("commit_bundles", &Scheduler::commit_bundles)
-      .def("remove_bundles", &Scheduler::remove_bundles);
+      .def("remove_bundles", &Scheduler::remove_bundles)
+      .def("pg_gpu_instances", &Scheduler::pg_gpu_instances);
 }

@@ -466,4 +466,17 @@ void Scheduler::remove_bundles(const std::string& pg, const std::vector<ResMap>&
   if (gi != pg_gpu_.end()) pg_gpu_.erase(gi);
 }
 
+std::vector<std::vector<int>> Scheduler::pg_gpu_instances(const std::string& pg) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::vector<int>> out;
+  auto it = pg_gpu_.find(pg);
+  if (it == pg_gpu_.end()) return out;
+  for (auto& b : it->second) {
+    std::vector<int> ids;
+    for (auto& p : b) ids.push_back(p.first);
+    out.push_back(ids);
+  }
+  return out;
+}
+
 }  // namespace ray_amd

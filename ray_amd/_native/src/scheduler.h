@@ -72,6 +72,8 @@ class Scheduler {
                       const std::vector<std::string>& nodes);
   void remove_bundles(const std::string& pg_id, const std::vector<ResMap>& bundles,
                       const std::vector<std::string>& nodes);
+  // GPU instance indices reserved by each bundle of a committed placement group.
+  std::vector<std::vector<int>> pg_gpu_instances(const std::string& pg_id);
   double spread_threshold = 0.5;
 
  private:

@@ -92,9 +92,12 @@ def strategy_of(opts: dict):
     if isinstance(st, PlacementGroupSchedulingStrategy):
         p = st.placement_group
         if isinstance(p, PlacementGroup):
-            return {"type": "pg", "pg_id": p.id.hex(), "bundle_index":
-                    st.placement_group_bundle_index if st.placement_group_bundle_index is not None
-                    else -1, "capture": bool(st.placement_group_capture_child_tasks)}
+            out = {"type": "pg", "pg_id": p.id.hex(), "bundle_index":
+                   st.placement_group_bundle_index if st.placement_group_bundle_index is not None
+                   else -1, "capture": bool(st.placement_group_capture_child_tasks)}
+            if getattr(st, "_share_gpus", False):
+                out["share_gpus"] = True
+            return out
         return None
     if isinstance(st, NodeAffinitySchedulingStrategy):
         return {"type": "node_affinity", "node_id": st.node_id, "soft": st.soft}

@@ -354,9 +354,28 @@ class Raylet:
         self.reply(conn, rid, True, None)
 
     # ------------------------------------------------------------------ worker pool
-    def _pool_key(self, job, renv, gpu_ids, node):
+    def _pool_key(self, job, renv, gpu_ids, node, visible=()):
+        # `visible`: GPUs the worker process sees (HIP_VISIBLE_DEVICES) when it differs from
+        # its own assignment — a Train worker group shares the union of its placement
+        # group's GPUs on the node so RCCL ranks see their xGMI peers, exactly like
+        # torchrun. Decided HERE, before the process exists, so HIP initialises with it.
         return (job, json.dumps(renv, sort_keys=True, default=str) if renv else None,
-                tuple(gpu_ids) if gpu_ids else (), node)
+                tuple(gpu_ids) if gpu_ids else (), node, tuple(visible))
+
+    def _shared_visible(self, lr, gpu_ids):
+        st = lr.req.get("strategy")
+        if not gpu_ids or not isinstance(st, dict) or st.get("type") != "pg" or \
+                not st.get("share_gpus"):
+            return ()
+        pg = self.pgs.get(st["pg_id"])
+        if pg is None or not pg.nodes:
+            return ()
+        inst = self.sched.pg_gpu_instances(st["pg_id"])
+        ids = set(gpu_ids)
+        for b, node in enumerate(pg.nodes):
+            if node == lr.node and b < len(inst):
+                ids.update(inst[b])
+        return tuple(sorted(ids))
 
     def _start_worker(self, key, renv, job):
         w = WorkerRec()
@@ -376,12 +395,17 @@ class Raylet:
         env["PYTHONPATH"] = pkg_root + (os.pathsep + pp if pp else "")
         if w.gpu_ids:
             vis = os.environ.get("HIP_VISIBLE_DEVICES")
-            ids = [str(i) for i in w.gpu_ids]
+            shown = key[4] if len(key) > 4 and key[4] else w.gpu_ids
+            ids = [str(i) for i in shown]
             if vis:
                 base = [x for x in vis.split(",") if x.strip() != ""]
-                ids = [base[i] for i in w.gpu_ids if i < len(base)]
+                ids = [base[i] for i in shown if i < len(base)]
             env["HIP_VISIBLE_DEVICES"] = ",".join(ids)
+            env.pop("CUDA_VISIBLE_DEVICES", None)
+            env.pop("ROCR_VISIBLE_DEVICES", None)
             env["RAY_AMD_GPU_IDS"] = ",".join(str(i) for i in w.gpu_ids)
+            # device ordinal of this worker's (first) GPU inside its visible set
+            env["RAY_AMD_LOCAL_DEVICE"] = str(list(shown).index(w.gpu_ids[0]))
         allr = {}
         for src in (j.get("runtime_env") or {}, renv or {}):
             allr.update(src)
@@ -500,7 +524,7 @@ class Raylet:
                 continue
             gpu_ids = self._gpu_ids(lr.alloc)
             key = self._pool_key(lr.req.get("job"), lr.req.get("runtime_env"), gpu_ids,
-                                 lr.node)
+                                 lr.node, self._shared_visible(lr, gpu_ids))
             w = self._take_idle(key)
             if w is None:
                 if lr.waiting_token is None or lr.waiting_token not in self.starting:

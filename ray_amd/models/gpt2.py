@@ -12,6 +12,9 @@ MI355X-first choices:
   hand-written kernels (ray_amd/ops/csrc).
 * Vocab padded 50257 → 50304 (multiple of 64/128) so the LM-head GEMM tiles
   cleanly on MFMA; padded columns are masked inside the fused cross-entropy.
+* LM head + cross-entropy fused and chunked over tokens (``lm_head_cross_entropy``):
+  the 64x1024x50304 logits tensor (6.6 GB) never exists; each chunk's logits are
+  turned into dlogits in place by one register-resident HIP pass.
 * Attention: our HIP MFMA causal flash attention (ops/csrc/attn.hip) reading the
   packed QKV GEMM output directly.
 * Backward: split-K fp32 weight-gradient GEMMs and every parameter gradient
@@ -124,6 +127,7 @@ class GPT2(nn.Module):
         self.wpe = nn.Parameter(torch.empty(cfg.n_positions, cfg.n_embd))
         self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_eps)
+        self.lm_head_chunk = 8192  # tokens per fused LM-head/CE chunk
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -147,8 +151,7 @@ class GPT2(nn.Module):
 
     def forward(self, idx, targets=None):
         B, T = idx.shape
-        pos = torch.arange(T, device=idx.device)
-        x = F.embedding(idx, self.wte) + F.embedding(pos, self.wpe)[None]
+        x = rf.embedding(idx, self.wte, self.wpe)
         # Pre-LN seams fused: every "x += sub_block(h) + bias; h = LN(x)" is ONE kernel
         # forward and ONE kernel backward (residual grads, LN grads and the projection-bias
         # grad together) — see ops.functional.residual_layer_norm.
@@ -159,10 +162,13 @@ class GPT2(nn.Module):
             nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
             x, h = rf.residual_layer_norm(blk.mlp(h), blk.mlp_proj_b, x, nxt.weight, nxt.bias,
                                           nxt.eps)
-        logits = F.linear(h, self.wte)  # tied LM head on ln_f(x), [B, T, padded_vocab]
         if targets is None:
+            logits = F.linear(h, self.wte)  # tied LM head on ln_f(x), [B, T, padded_vocab]
             return logits[..., : self.cfg.vocab_size]
-        return rf.cross_entropy(logits, targets, self.cfg.vocab_size)
+        # tied LM head + CE fused and chunked over tokens (never the full logits); the
+        # embedding backward, which runs last, signals wte's DDP readiness
+        return rf.lm_head_cross_entropy(h, self.wte, targets, self.cfg.vocab_size,
+                                        chunk=self.lm_head_chunk, signal_w=False)
 
     def flops_per_token(self, T: int) -> float:
         """6N + 12·L·H·hd·T (PaLM appendix B convention), training FLOPs per token."""

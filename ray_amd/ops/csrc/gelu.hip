@@ -145,10 +145,16 @@ RA_EXPORT int ra_bias_gelu_fwd(const void* h, const void* bias, void* y, long N,
   return hipGetLastError();
 }
 
+// Sink flags shared by the bias-gradient entry points below:
+//   bit0: accumulate into `out` (direct write into a flat gradient buffer view)
+//   bit1: `out` is fp32 (the default fp32 gradient buffer) instead of bf16
+static inline int sink_flags(int flags) {
+  return ((flags & 1) ? kColsumAcc : 0) | ((flags & 2) ? 0 : kColsumBF16);
+}
+
 // work: ra_colsum_work(N, F) floats
-// accumulate != 0: dbias += (direct write into a flat gradient buffer)
 RA_EXPORT int ra_bias_gelu_bwd(const void* dy, const void* h, const void* bias, void* dh,
-                               void* dbias, float* work, int N, int F, int accumulate,
+                               void* dbias, float* work, int N, int F, int flags,
                                hipStream_t st) {
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
@@ -156,20 +162,18 @@ RA_EXPORT int ra_bias_gelu_bwd(const void* dy, const void* h, const void* bias, 
   hipLaunchKernelGGL(bwd_colpart_kernel<true>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                      (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh, work,
                      N, F8, rpp);
-  colsum_launch(work, work + (size_t)P * F, dbias, P, F,
-                kColsumBF16 | (accumulate ? kColsumAcc : 0), st);
+  colsum_launch(work, work + (size_t)P * F, dbias, P, F, sink_flags(flags), st);
   return hipGetLastError();
 }
 
-RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F, int accumulate,
+RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F, int flags,
                              hipStream_t st) {
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
   hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                      (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
-  colsum_launch(work, work + (size_t)P * F, out, P, F,
-                kColsumBF16 | (accumulate ? kColsumAcc : 0), st);
+  colsum_launch(work, work + (size_t)P * F, out, P, F, sink_flags(flags), st);
   return hipGetLastError();
 }
 

@@ -9,11 +9,13 @@
 //   grad[i] = bf16( grad[i] + sum_s part[s][i] )          (grad = flat gradient buffer view)
 //
 // one HBM pass that also replaces autograd's separate AccumulateGrad add, and sums the
-// split partials in fp32 (relative error 1.5e-6 vs 1.7e-3 for a bf16-output GEMM).
+// split partials in fp32 (relative error 1.5e-6 vs 1.7e-3 for a bf16-output GEMM). With
+// the default fp32 flat gradient buffer the sum is never rounded to bf16 at all.
 #include "common.h"
 
+template <bool OUT_F32>
 __global__ __launch_bounds__(256) void splitk_accum_kernel(const float* __restrict__ part, int S,
-                                                           long n4, bf16_t* __restrict__ grad,
+                                                           long n4, void* __restrict__ grad,
                                                            int accumulate) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -25,26 +27,110 @@ __global__ __launch_bounds__(256) void splitk_accum_kernel(const float* __restri
       a.z += b.z;
       a.w += b.w;
     }
-    uint2* g = reinterpret_cast<uint2*>(grad) + i;
-    float v[4] = {a.x, a.y, a.z, a.w};
-    if (accumulate) {
-      float o[4];
-      unpack4(*g, o);
-      v[0] += o[0];
-      v[1] += o[1];
-      v[2] += o[2];
-      v[3] += o[3];
+    if (OUT_F32) {
+      // fp32 flat gradient (default): the split partials land in full precision
+      float4* g = reinterpret_cast<float4*>(grad) + i;
+      if (accumulate) {
+        const float4 o = *g;
+        a.x += o.x;
+        a.y += o.y;
+        a.z += o.z;
+        a.w += o.w;
+      }
+      *g = a;
+    } else {
+      uint2* g = reinterpret_cast<uint2*>(grad) + i;
+      float v[4] = {a.x, a.y, a.z, a.w};
+      if (accumulate) {
+        float o[4];
+        unpack4(*g, o);
+        v[0] += o[0];
+        v[1] += o[1];
+        v[2] += o[2];
+        v[3] += o[3];
+      }
+      *g = pack4(v);
     }
-    *g = pack4(v);
   }
 }
 
-// part: [S, n] fp32; grad: n bf16 (n % 4 == 0, 8-byte aligned)
-RA_EXPORT int ra_splitk_accum(const float* part, int S, long n, void* grad, int accumulate,
+// part: [S, n] fp32; grad: n bf16 or fp32 (n % 4 == 0, 16-byte aligned).
+// flags: bit0 accumulate into grad, bit1 grad is fp32.
+RA_EXPORT int ra_splitk_accum(const float* part, int S, long n, void* grad, int flags,
                               hipStream_t st) {
   if (n % 4 || S < 1) return hipErrorInvalidValue;
   const long n4 = n / 4;
-  hipLaunchKernelGGL(splitk_accum_kernel, dim3(ra_grid(n4, 256)), dim3(256), 0, st, part, S, n4,
-                     (bf16_t*)grad, accumulate);
+  if (flags & 2)
+    hipLaunchKernelGGL(splitk_accum_kernel<true>, dim3(ra_grid(n4, 256)), dim3(256), 0, st, part,
+                       S, n4, grad, flags & 1);
+  else
+    hipLaunchKernelGGL(splitk_accum_kernel<false>, dim3(ra_grid(n4, 256)), dim3(256), 0, st, part,
+                       S, n4, grad, flags & 1);
+  return hipGetLastError();
+}
+
+// sink[i] += (*g) * src[i]   (src fp32; sink fp32 or bf16 by `sink_f32`; g device scalar or
+// null = 1). Used by fused ops that precompute a parameter gradient before the upstream
+// gradient is known (the LM-head cross-entropy computes it inside forward).
+template <bool SINK_F32>
+__global__ __launch_bounds__(256) void scaled_accum_kernel(const float* __restrict__ src,
+                                                           void* __restrict__ sink, long n4,
+                                                           const float* __restrict__ g) {
+  const float sc = g ? *g : 1.f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(src)[i];
+    if (SINK_F32) {
+      float4* o = reinterpret_cast<float4*>(sink) + i;
+      float4 v = *o;
+      v.x += sc * a.x;
+      v.y += sc * a.y;
+      v.z += sc * a.z;
+      v.w += sc * a.w;
+      *o = v;
+    } else {
+      uint2* o = reinterpret_cast<uint2*>(sink) + i;
+      float v[4];
+      unpack4(*o, v);
+      v[0] += sc * a.x;
+      v[1] += sc * a.y;
+      v[2] += sc * a.z;
+      v[3] += sc * a.w;
+      *o = pack4(v);
+    }
+  }
+}
+
+RA_EXPORT int ra_scaled_accum(const float* src, void* sink, long n, int sink_f32, const float* g,
+                              hipStream_t st) {
+  if (n % 4) return hipErrorInvalidValue;
+  const long n4 = n / 4;
+  if (sink_f32)
+    hipLaunchKernelGGL(scaled_accum_kernel<true>, dim3(ra_grid(n4, 256)), dim3(256), 0, st, src,
+                       sink, n4, g);
+  else
+    hipLaunchKernelGGL(scaled_accum_kernel<false>, dim3(ra_grid(n4, 256)), dim3(256), 0, st, src,
+                       sink, n4, g);
+  return hipGetLastError();
+}
+
+// x[i] *= (*g), bf16 in place (n % 8 == 0)
+__global__ __launch_bounds__(256) void scale_bf16_kernel(bf16_t* __restrict__ x, long n8,
+                                                         const float* __restrict__ g) {
+  const float sc = *g;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= sc;
+    reinterpret_cast<uint4*>(x)[i] = pack8(v);
+  }
+}
+
+RA_EXPORT int ra_scale_bf16(void* x, long n, const float* g, hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scale_bf16_kernel, dim3(ra_grid(n / 8, 256)), dim3(256), 0, st, (bf16_t*)x,
+                     n / 8, g);
   return hipGetLastError();
 }

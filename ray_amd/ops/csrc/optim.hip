@@ -2,9 +2,11 @@
 //
 // The trainer keeps every parameter as a view into ONE bf16 buffer (compute
 // copy) backed by ONE fp32 master buffer, and every gradient as a view into
-// ONE bf16 grad buffer (which is also what RCCL all-reduces, bucket by bucket,
-// with no packing copy). So the optimizer step is a single streaming pass:
-//   read g(bf16) p(f32) m(f32) v(f32) -> write p(f32) m v p16(bf16) = 28 B/param.
+// ONE grad buffer — fp32 by default (the reference's DDP precision), bf16 when
+// gradient compression is requested — which is also what RCCL all-reduces,
+// bucket by bucket, with no packing copy. So the optimizer step is a single
+// streaming pass (fp32 grads, zeroed in the same pass):
+//   read g p m v -> write p m v p16 g(=0) = 38 B/param.
 // Decayed parameters occupy [0, n_decay), the rest is not decayed.
 // Global-norm clipping stays on device: ra_sumsq_bf16 -> ra_clip_scale writes
 // the scale factor that ra_adamw_flat reads through a pointer (no host sync).
@@ -40,9 +42,13 @@ __global__ void clip_scale_kernel(const float* __restrict__ part, int P, float m
   }
 }
 
+// G = bf16_t (compressed gradient buffer) or float (default fp32 gradient buffer).
+// ZERO: also clear the gradient after reading it — the optimizer is the last reader of
+// the flat grad every step, so this replaces the separate zero_grad memset pass.
+template <typename G, bool ZERO>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p32,
                                                     bf16_t* __restrict__ p16,
-                                                    const bf16_t* __restrict__ g,
+                                                    G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     long n4, long nd4, float lr, float b1,
                                                     float b2, float eps, float wd, float rbc1,
@@ -51,7 +57,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p32,
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float gv[4];
-    unpack4(reinterpret_cast<const uint2*>(g)[i], gv);
+    if constexpr (sizeof(G) == 2) {
+      unpack4(reinterpret_cast<const uint2*>(g)[i], gv);
+      if (ZERO) reinterpret_cast<uint2*>(g)[i] = make_uint2(0u, 0u);
+    } else {
+      const float4 g4 = reinterpret_cast<const float4*>(g)[i];
+      gv[0] = g4.x; gv[1] = g4.y; gv[2] = g4.z; gv[3] = g4.w;
+      if (ZERO) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float4 p = reinterpret_cast<float4*>(p32)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
@@ -70,7 +83,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p32,
     reinterpret_cast<float4*>(p32)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
     reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
     reinterpret_cast<float4*>(v)[i] = make_float4(va[0], va[1], va[2], va[3]);
-    reinterpret_cast<uint2*>(p16)[i] = pack4(pa);
+    if (p16) reinterpret_cast<uint2*>(p16)[i] = pack4(pa);
   }
 }
 
@@ -125,8 +138,13 @@ __global__ __launch_bounds__(256) void sumsq_f32_kernel(const float* __restrict_
                                                         float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x)
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
     s += g[i] * g[i];
   s = block_sum<4>(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
@@ -152,15 +170,24 @@ RA_EXPORT int ra_grad_clip(const void* g, long n, int is_bf16, float max_norm, f
   return hipGetLastError();
 }
 
-RA_EXPORT int ra_adamw_flat(float* p32, void* p16, const void* g, float* m, float* v, long n,
+// flags: bit0 g is fp32 (else bf16), bit1 zero g after use. p16 may be null.
+RA_EXPORT int ra_adamw_flat(float* p32, void* p16, void* g, float* m, float* v, long n,
                             long n_decay, float lr, float b1, float b2, float eps, float wd,
-                            int step, const float* gscale, hipStream_t st) {
+                            int step, const float* gscale, int flags, hipStream_t st) {
   if (n % 4 || n_decay % 4) return hipErrorInvalidValue;
   const float rbc1 = 1.f / (1.f - powf(b1, (float)step));
   const float rbc2 = 1.f / (1.f - powf(b2, (float)step));
-  hipLaunchKernelGGL(adamw_kernel, dim3(ra_grid(n / 4, 256)), dim3(256), 0, st, p32,
-                     (bf16_t*)p16, (const bf16_t*)g, m, v, n / 4, n_decay / 4, lr, b1, b2, eps,
-                     wd, rbc1, rbc2, gscale);
+  const dim3 grid(ra_grid(n / 4, 256)), blk(256);
+#define A(G, Z)                                                                              \
+  hipLaunchKernelGGL((adamw_kernel<G, Z>), grid, blk, 0, st, p32, (bf16_t*)p16, (G*)g, m, v, \
+                     n / 4, n_decay / 4, lr, b1, b2, eps, wd, rbc1, rbc2, gscale)
+  switch (flags & 3) {
+    case 0: A(bf16_t, false); break;
+    case 1: A(float, false); break;
+    case 2: A(bf16_t, true); break;
+    default: A(float, true);
+  }
+#undef A
   return hipGetLastError();
 }
 

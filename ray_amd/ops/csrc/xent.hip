@@ -94,6 +94,104 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused LM-head cross-entropy chunk (forward AND backward in one pass, in place).
+//
+// The LM head runs token-chunk by token-chunk (ops.functional.lm_head_cross_entropy):
+//   logits_c = h_c @ W^T (hipBLASLt) -> THIS KERNEL -> dh_c = dlogits_c @ W,
+//   dW += dlogits_c^T @ h_c (hipBLASLt, fp32 accumulate)
+// so the [tokens, vocab] logits tensor (6.6 GB at 64x1024 tokens x 50304) never exists
+// whole. Each 512-thread block owns one row and keeps it in REGISTERS (NV 16-byte
+// vectors per lane: 8 waves x 64 lanes x NV x 8 = up to 65536 columns), so the row is
+// read from HBM/MALL once and overwritten once with
+//   dlogits = (softmax(row) - onehot(target)) * inv_count     (0 on padding columns)
+// and loss[row] = lse - row[target]. inv_count is a device scalar (no host sync).
+template <int NV>
+__global__ __launch_bounds__(512) void xent_fused_kernel(bf16_t* __restrict__ logits,
+                                                         const long* __restrict__ targets,
+                                                         const float* __restrict__ inv_count,
+                                                         float* __restrict__ loss, int V, int Vp,
+                                                         long ignore_index) {
+  __shared__ float red[8];
+  __shared__ float tlogit;
+  const int row = blockIdx.x;
+  bf16_t* lr = logits + (size_t)row * Vp;
+  const long t = targets[row];
+  const bool ign = (t == ignore_index || t < 0 || t >= V);
+  if (threadIdx.x == 0) tlogit = ign ? 0.f : bf2f(lr[t]);  // read before any overwrite
+  const int Vp8 = Vp >> 3;
+  uint4 raw[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c8 = k * 512 + threadIdx.x;
+    if (c8 < Vp8) raw[k] = reinterpret_cast<const uint4*>(lr)[c8];
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c8 = k * 512 + threadIdx.x;
+    if (c8 < Vp8) {
+      float v[8];
+      unpack8(raw[k], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c8 * 8 + j < V) m = fmaxf(m, v[j]);
+    }
+  }
+  m = block_max<8>(m, red);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c8 = k * 512 + threadIdx.x;
+    if (c8 < Vp8) {
+      float v[8];
+      unpack8(raw[k], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c8 * 8 + j < V) s += __expf(v[j] - m);
+    }
+  }
+  s = block_sum<8>(s, red);
+  const float lse = m + __logf(s);
+  const float scale = ign ? 0.f : *inv_count;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c8 = k * 512 + threadIdx.x;
+    if (c8 < Vp8) {
+      float v[8], o[8];
+      unpack8(raw[k], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c8 * 8 + j;
+        float p = (c < V) ? __expf(v[j] - lse) : 0.f;
+        if (c == t) p -= 1.f;
+        o[j] = p * scale;
+      }
+      reinterpret_cast<uint4*>(lr)[c8] = pack8(o);
+    }
+  }
+  if (threadIdx.x == 0) loss[row] = ign ? 0.f : lse - tlogit;
+}
+
+// logits: [N, Vp] bf16, overwritten with dlogits. loss: [N] fp32 (per-row, unscaled).
+RA_EXPORT int ra_xent_fused(void* logits, const long* targets, const float* inv_count,
+                            float* loss, int N, int V, int Vp, long ignore_index,
+                            hipStream_t st) {
+  if (Vp % 8 || V > Vp || N <= 0) return hipErrorInvalidValue;
+  const int per = (Vp / 8 + 511) / 512;
+#define X(NV)                                                                                 \
+  hipLaunchKernelGGL((xent_fused_kernel<NV>), dim3(N), dim3(512), 0, st, (bf16_t*)logits,     \
+                     targets, inv_count, loss, V, Vp, ignore_index)
+  if (per <= 2) X(2);
+  else if (per <= 4) X(4);
+  else if (per <= 8) X(8);
+  else if (per <= 13) X(13);
+  else if (per <= 16) X(16);
+  else return hipErrorInvalidValue;
+#undef X
+  return hipGetLastError();
+}
+
 RA_EXPORT int ra_xent_fwd(const void* logits, const long* targets, float* loss, float* lse,
                           int N, int V, int Vp, long ignore_index, hipStream_t st) {
   if (Vp % 8 || V > Vp) return hipErrorInvalidValue;

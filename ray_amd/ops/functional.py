@@ -19,15 +19,20 @@ def _hip(t: torch.Tensor) -> bool:
 
 
 # --------------------------------------------------------------------- flat-grad sinks
-# Parameters managed by ray_amd.parallel.flat keep .grad as a view into one flat bf16
-# buffer and are tagged ``_ra_direct_grad``. Our backward kernels then ACCUMULATE their
-# parameter gradients straight into that view (fp32 math, one HBM pass) and return None,
-# so autograd never allocates a gradient tensor nor launches an AccumulateGrad add; the
+# Parameters managed by ray_amd.parallel.flat carry ``_ra_grad``: a view into ONE flat
+# gradient buffer (fp32 by default, bf16 when gradient compression is on), and are
+# tagged ``_ra_direct_grad``. Our backward kernels then ACCUMULATE their parameter
+# gradients straight into that view (fp32 math, one HBM pass) and return None, so
+# autograd never allocates a gradient tensor nor launches an AccumulateGrad add; the
 # DDP bucket hook (``_ra_grad_ready``) is signalled exactly once per backward instead.
 def _grad_sink(p):
-    if p is not None and getattr(p, "_ra_direct_grad", False) and p.grad is not None:
-        return p.grad
+    if p is not None and getattr(p, "_ra_direct_grad", False):
+        return getattr(p, "_ra_grad", None)
     return None
+
+
+def _sink_f32(t) -> int:
+    return 1 if t is not None and t.dtype == torch.float32 else 0
 
 
 def _grad_done(p):
@@ -64,7 +69,7 @@ def _ln_backward(dy, x2, w, b, mean, rstd, dres=None, rbias=None):
     outs = sinks if direct else [torch.empty_like(p) for p in params]
     if rbias is None:
         outs.append(None)
-    flags = (1 if w.dtype == torch.bfloat16 else 0) | (2 if direct else 0)
+    flags = (1 if outs[0].dtype == torch.bfloat16 else 0) | (2 if direct else 0)
     dr = None if dres is None else dres.contiguous().view(N, D)
     check(L.ra_layernorm_bwd(ptr(dy2), ptr(x2), ptr(w), ptr(mean), ptr(rstd), ptr(dr), ptr(dx),
                              ptr(outs[0]), ptr(outs[1]), ptr(outs[2]), ptr(work), N, D, flags,
@@ -189,9 +194,9 @@ class _BiasGelu(torch.autograd.Function):
         dh = torch.empty_like(h2)
         sink = _grad_sink(bias)
         db = sink if sink is not None else torch.empty_like(bias)
+        flags = (1 if sink is not None else 0) | (2 * _sink_f32(db))
         check(L.ra_bias_gelu_bwd(ptr(dy.contiguous()), ptr(h2), ptr(bias), ptr(dh), ptr(db),
-                                 ptr(work), N, F_, 1 if sink is not None else 0, stream_ptr()),
-              "bias_gelu_bwd")
+                                 ptr(work), N, F_, flags, stream_ptr()), "bias_gelu_bwd")
         if sink is not None:
             _grad_done(bias)
             return dh.view(ctx.shape), None
@@ -206,15 +211,16 @@ def bias_gelu(h, bias):
 
 # --------------------------------------------------------------------- bias + residual
 def _colsum_bf16(x2, out=None):
-    """Column sum of [N, F] bf16 -> [F] bf16; with `out` given, accumulate into it."""
+    """Column sum of [N, F] bf16 -> [F] bf16; with `out` given (bf16 or fp32), accumulate
+    into it."""
     N, F_ = x2.shape
     L = _lib.lib()
     work = torch.empty(L.ra_colsum_work(N, F_), device=x2.device, dtype=torch.float32)
     acc = out is not None
     if out is None:
         out = torch.empty(F_, device=x2.device, dtype=x2.dtype)
-    check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_, 1 if acc else 0, stream_ptr()),
-          "colsum")
+    check(L.ra_colsum_bf16(ptr(x2), ptr(out), ptr(work), N, F_,
+                           (1 if acc else 0) | 2 * _sink_f32(out), stream_ptr()), "colsum")
     return out
 
 
@@ -291,7 +297,8 @@ class _Linear(torch.autograd.Function):
                                  out_dtype=torch.float32)
                 target = sink if sink is not None else torch.empty_like(w)
                 check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(target),
-                                                 1 if sink is not None else 0, stream_ptr()),
+                                                 (1 if sink is not None else 0) |
+                                                 2 * _sink_f32(target), stream_ptr()),
                       "splitk_accum")
                 if sink is None:
                     dw = target
@@ -380,6 +387,126 @@ class _CrossEntropy(torch.autograd.Function):
         check(_lib.lib().ra_xent_bwd(ptr(l2), ptr(t), ptr(lse), ptr(gs), 1.0, ptr(dl), N, ctx.V,
                                      Vp, ctx.ignore_index, stream_ptr()), "xent_bwd")
         return dl.view(ctx.shape), None, None, None
+
+
+class _LMHeadCrossEntropy(torch.autograd.Function):
+    """Tied LM head + mean token cross-entropy, chunked over tokens so the full
+    [tokens, vocab] logits never exist. Forward computes the loss AND the gradients
+    (the standard fused-linear-cross-entropy trick): per chunk one hipBLASLt GEMM for the
+    logits, ``ra_xent_fused`` turning them into dlogits in place, and two GEMMs for dh
+    and dW (fp32 accumulate). Backward only scales by the upstream gradient and
+    accumulates dW into the flat fp32 (or bf16) gradient sink.
+
+    ``signal_w=False`` for a tied weight whose other use (the embedding) runs later in
+    backward and signals DDP readiness itself."""
+
+    @staticmethod
+    def forward(ctx, h, w, targets, V, ignore_index, chunk, signal_w):
+        C = h.shape[-1]
+        h2 = h.contiguous().view(-1, C)
+        t = targets.contiguous().view(-1).long()
+        N, Vp = h2.shape[0], w.shape[0]
+        dev = h.device
+        count = (t != ignore_index).sum().clamp_min(1).float()
+        inv = (1.0 / count).reshape(1)
+        loss_rows = torch.empty(N, device=dev, dtype=torch.float32)
+        need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        dh = torch.empty_like(h2) if need_grad else None
+        dw = torch.zeros(w.shape, device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] \
+            else None
+        ch = max(1, min(chunk, N))
+        buf = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
+        L = _lib.lib()
+        wt = w.t()
+        for s0 in range(0, N, ch):
+            e = min(N, s0 + ch)
+            lg = buf[: e - s0]
+            torch.mm(h2[s0:e], wt, out=lg)
+            check(L.ra_xent_fused(ptr(lg), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]), e - s0,
+                                  V, Vp, ignore_index, stream_ptr()), "xent_fused")
+            if dh is not None:
+                torch.mm(lg, w, out=dh[s0:e])
+            if dw is not None:
+                torch.addmm(dw, lg.t(), h2[s0:e], out_dtype=torch.float32, out=dw)
+        ctx.save_for_backward(dh, dw)
+        ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
+        return loss_rows.sum() * inv[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        dh, dw = ctx.saved_tensors
+        L = _lib.lib()
+        gs = g.float().reshape(1).contiguous()
+        dhv = None
+        if dh is not None and ctx.needs_input_grad[0]:
+            check(L.ra_scale_bf16(ptr(dh), dh.numel(), ptr(gs), stream_ptr()), "scale_bf16")
+            dhv = dh.view(ctx.shape)
+        dwv = None
+        if dw is not None:
+            sink = _grad_sink(ctx.w)
+            if sink is not None:
+                check(L.ra_scaled_accum(ptr(dw), ptr(sink), dw.numel(), _sink_f32(sink), ptr(gs),
+                                        stream_ptr()), "scaled_accum")
+                if ctx.signal_w:
+                    _grad_done(ctx.w)
+            else:
+                dwv = (dw * gs).to(ctx.w.dtype)
+        return dhv, dwv, None, None, None, None, None
+
+
+def lm_head_cross_entropy(h, w, targets, vocab_size=None, ignore_index=-100, chunk=8192,
+                          signal_w=True):
+    """mean CE(h @ w^T, targets) with w [padded_vocab, C]; columns >= vocab_size are
+    excluded from the softmax. HIP path never materialises the full logits."""
+    V = vocab_size or w.shape[0]
+    if _hip(h) and h.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and \
+            (w.shape[0] // 8 + 511) // 512 <= 16:
+        return _LMHeadCrossEntropy.apply(h, w, targets, V, ignore_index, int(chunk),
+                                         bool(signal_w))
+    logits = torch.nn.functional.linear(h, w)
+    return ref.cross_entropy(logits, targets, V, ignore_index)
+
+
+class _Embedding(torch.autograd.Function):
+    """x = wte[idx] + wpe[:T]; backward scatters straight into the flat gradient sinks
+    (fp32 index_add for the token table, a column-batch sum for positions)."""
+
+    @staticmethod
+    def forward(ctx, idx, wte, wpe):
+        T = idx.shape[1]
+        x = torch.nn.functional.embedding(idx, wte) + wpe[:T].unsqueeze(0)
+        ctx.save_for_backward(idx)
+        ctx.wte, ctx.wpe = wte, wpe
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (idx,) = ctx.saved_tensors
+        wte, wpe = ctx.wte, ctx.wpe
+        B, T, C = dx.shape
+        d2 = dx.reshape(-1, C)
+        outs = []
+        for p, fill in ((wte, lambda acc: acc.index_add_(0, idx.reshape(-1),
+                                                         d2.to(acc.dtype))),
+                        (wpe, lambda acc: acc[:T].add_(dx.float().sum(0).to(acc.dtype)))):
+            sink = _grad_sink(p)
+            if sink is not None:
+                fill(sink)
+                _grad_done(p)
+                outs.append(None)
+            else:
+                acc = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+                fill(acc)
+                outs.append(acc.to(p.dtype))
+        return None, outs[0], outs[1]
+
+
+def embedding(idx, wte, wpe):
+    """Token + learned position embedding for [B, T] indices."""
+    if getattr(wte, "_ra_direct_grad", False) or getattr(wpe, "_ra_direct_grad", False):
+        return _Embedding.apply(idx, wte, wpe)
+    T = idx.shape[1]
+    return torch.nn.functional.embedding(idx, wte) + wpe[:T].unsqueeze(0)
 
 
 def cross_entropy(logits, targets, vocab_size=None, ignore_index=-100):

@@ -3,10 +3,16 @@
 Design (vs torch DDP, which copies grads into bucket buffers and all-reduces fp32):
 
 * All parameters become views into ONE bf16 compute buffer ``p16`` backed by ONE
-  fp32 master buffer ``p32``; all gradients are views into ONE bf16 buffer
-  ``g16``. Layout is [decay group | no-decay group], each group in *reverse
+  fp32 master buffer ``p32``; all gradients are views into ONE buffer ``g`` —
+  fp32 by default (the precision torch DDP under AMP reduces in), or bf16 as an
+  explicit gradient-compression opt-in (``grad_dtype=torch.bfloat16``, half the
+  RCCL bytes). Layout is [decay group | no-decay group], each group in *reverse
   registration order* (≈ the order backward produces gradients).
-* ``g16`` is cut into buckets (default 32 MiB, sized for ring all-reduce over
+* Our HIP backward kernels accumulate parameter gradients straight into their
+  ``_ra_grad`` views (fp32 math; with the fp32 buffer nothing is ever rounded to
+  bf16). Parameters reached through plain PyTorch ops fall back to autograd's
+  ``.grad`` and a post-accumulate hook adds it into the flat buffer.
+* ``g`` is cut into buckets (default 32 MiB, sized for ring all-reduce over
   7 point-to-point xGMI links: large enough to run each link near its
   ~150 GB/s, small enough that the first bucket starts while backward still
   has most of its work ahead). A ``post_accumulate_grad`` hook counts ready
@@ -43,7 +49,7 @@ def _round(n: int, a: int = ALIGN) -> int:
 
 class FlatParams:
     def __init__(self, module: torch.nn.Module, dtype=torch.bfloat16,
-                 no_decay: callable | None = None):
+                 no_decay: callable | None = None, grad_dtype=torch.float32):
         self.module = module
         seen = {}
         for name, p in module.named_parameters():
@@ -70,17 +76,28 @@ class FlatParams:
         self.device = dev
         self.p32 = torch.zeros(o, dtype=torch.float32, device=dev)
         self.p16 = torch.zeros(o, dtype=dtype, device=dev) if dtype != torch.float32 else self.p32
-        self.g = torch.zeros(o, dtype=dtype, device=dev)
+        self.grad_dtype = grad_dtype
+        self.g = torch.zeros(o, dtype=grad_dtype, device=dev)
         self.offsets = offs
         self.names = [n for n, _ in self.order]
+        # .grad can alias the flat buffer only when dtypes match; otherwise autograd
+        # gradients are folded in by a post-accumulate hook (registered before any DDP
+        # readiness hook, so the bucket never launches before the add)
+        self.alias_grad = grad_dtype == dtype
+        self._fold_hooks = []
         with torch.no_grad():
             for (n, p), off in zip(self.order, offs):
                 k = p.numel()
                 self.p32[off:off + k].copy_(p.detach().reshape(-1).float())
                 self.p16[off:off + k].copy_(self.p32[off:off + k])
                 p.data = self.p16[off:off + k].view(p.shape)
-                p.grad = self.g[off:off + k].view(p.shape)
-                # ray_amd.ops backward kernels may accumulate straight into p.grad
+                p._ra_grad = self.g[off:off + k].view(p.shape)
+                if self.alias_grad:
+                    p.grad = p._ra_grad
+                else:
+                    p.grad = None
+                    self._fold_hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
+                # ray_amd.ops backward kernels accumulate straight into p._ra_grad
                 p._ra_direct_grad = True
 
     def params(self) -> list[torch.nn.Parameter]:
@@ -88,10 +105,21 @@ class FlatParams:
 
     def zero_grad(self):
         self.g.zero_()
+        if not self.alias_grad:
+            for _, p in self.order:
+                p.grad = None
 
     def sync_master_from_params(self):
         with torch.no_grad():
             self.p32.copy_(self.p16.float())
+
+
+def _fold_grad(p):
+    """post-accumulate hook: fold an autograd-produced .grad into the flat buffer."""
+    if p.grad is not None:
+        with torch.no_grad():
+            p._ra_grad.add_(p.grad.to(p._ra_grad.dtype))
+        p.grad = None
 
 
 class FlatDDP:
@@ -181,7 +209,8 @@ class FlatAdamW:
     """Fused AdamW over a FlatParams buffer (fp32 master, bf16 compute/grad)."""
 
     def __init__(self, flat: FlatParams, lr=6e-4, betas=(0.9, 0.95), eps=1e-8,
-                 weight_decay=0.1, max_grad_norm: float | None = 1.0, grad_scale: float = 1.0):
+                 weight_decay=0.1, max_grad_norm: float | None = 1.0, grad_scale: float = 1.0,
+                 zero_grad: bool = False):
         self.flat = flat
         self.lr = lr
         self.b1, self.b2 = betas
@@ -197,6 +226,8 @@ class FlatAdamW:
         self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self._work = None
         self.use_hip = flat.p32.is_cuda
+        # clear the gradient inside the AdamW pass (the caller then skips zero_grad)
+        self.zero_grad = zero_grad
 
     def step(self, lr: float | None = None):
         self.step_count += 1
@@ -215,14 +246,11 @@ class FlatAdamW:
                                      ptr(self._work), gptr, ptr(self.last_norm), s), "grad_clip")
             else:
                 gptr = None
-            if f.g.dtype == torch.bfloat16:
-                check(L.ra_adamw_flat(ptr(f.p32), ptr(f.p16), ptr(f.g), ptr(self.m), ptr(self.v),
-                                      f.numel, f.n_decay, lr, self.b1, self.b2, self.eps, self.wd,
-                                      self.step_count, gptr, s), "adamw")
-            else:
-                check(L.ra_adamw_f32(ptr(f.p32), ptr(f.g), ptr(self.m), ptr(self.v), f.numel,
-                                     f.n_decay, lr, self.b1, self.b2, self.eps, self.wd,
-                                     self.step_count, gptr, s), "adamw_f32")
+            g32 = f.g.dtype == torch.float32
+            check(L.ra_adamw_flat(ptr(f.p32), ptr(f.p16) if f.p16 is not f.p32 else None,
+                                  ptr(f.g), ptr(self.m), ptr(self.v), f.numel, f.n_decay, lr,
+                                  self.b1, self.b2, self.eps, self.wd, self.step_count, gptr,
+                                  (1 if g32 else 0) | (2 if self.zero_grad else 0), s), "adamw")
             return
         # CPU reference path (same math)
         g = f.g.float() * self.grad_scale
@@ -240,6 +268,8 @@ class FlatAdamW:
         f.p32.mul_(decay).sub_(lr * upd)
         if f.p16 is not f.p32:
             f.p16.copy_(f.p32)
+        if self.zero_grad:
+            f.g.zero_()
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}

@@ -59,7 +59,10 @@ class Learner:
         # bf16 compute weights + fp32 master in the flat optimizer on GPU: no per-forward
         # autocast weight casts (they were ~30 copy kernels per SGD step)
         bf16 = device.type == "cuda" and config.get("learner_bf16", True)
-        self.flat = FlatParams(self.module, dtype=torch.bfloat16 if bf16 else torch.float32)
+        pdt = torch.bfloat16 if bf16 else torch.float32
+        # grads alias .grad (same dtype as the compute weights): the whole SGD step,
+        # including MIOpen's conv weight grads, stays capturable in one HIP graph
+        self.flat = FlatParams(self.module, dtype=pdt, grad_dtype=pdt)
         self.ddp = FlatDDP(self.flat, bucket_mb=32.0)
         self.opt = FlatAdamW(self.flat, lr=config.get("lr", 5e-5), betas=(0.9, 0.999), eps=1e-7,
                              weight_decay=0.0, max_grad_norm=config.get("grad_clip"),

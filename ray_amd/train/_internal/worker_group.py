@@ -22,8 +22,10 @@ class RayTrainWorker:
     def node_info(self):
         ctx = ray.get_runtime_context()
         gpu_ids = ray.get_gpu_ids()
-        vis = os.environ.get("HIP_VISIBLE_DEVICES", "")
-        phys = [x for x in vis.split(",") if x.strip() != ""] if gpu_ids else []
+        vis = [x for x in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if x.strip()]
+        loc = int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))
+        # physical id of this rank's own GPU (the process may see the group's union)
+        phys = [vis[loc]] if gpu_ids and loc < len(vis) else []
         return {"node_id": ctx.get_node_id(), "pid": os.getpid(),
                 "gpu_ids": gpu_ids, "physical_gpu_ids": phys,
                 "hostname": socket.gethostname(), "ip": "127.0.0.1"}
@@ -100,10 +102,12 @@ class WorkerGroup:
         other = {k: v for k, v in resources_per_worker.items() if k not in ("CPU", "GPU")}
         self.workers = []
         for i in range(num_workers):
+            st = PlacementGroupSchedulingStrategy(self.pg, i)
+            # GPU ranks on one node see each other's devices (set at process spawn)
+            st._share_gpus = bool(num_gpus)
             self.workers.append(remote_cls.options(
                 num_cpus=num_cpus, num_gpus=num_gpus, resources=other or None,
-                scheduling_strategy=PlacementGroupSchedulingStrategy(self.pg, i),
-                max_concurrency=4).remote())
+                scheduling_strategy=st, max_concurrency=4).remote())
         self.infos = ray.get([w.node_info.remote() for w in self.workers])
 
     def execute(self, fn, *args, **kwargs):

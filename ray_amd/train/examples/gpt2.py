@@ -1,0 +1,190 @@
+"""GPT-2 DDP training as a Ray Train workload — the headline benchmark body.
+
+``train_func`` is the ``train_loop_per_worker`` that ``bench.py`` hands to
+``TorchTrainer(scaling_config=ScalingConfig(num_workers=N, use_gpu=True))``. Each
+worker actor owns one MI355X (the raylet binds the device before the process
+starts), the TorchConfig backend has already initialised an RCCL process group
+over all N workers, and the loop runs ``GPT2Trainer.step`` (forward, backward with
+bucketed RCCL all-reduce overlapped, clip, fused AdamW) on synthetic tokens.
+
+Timing protocol (same as the bare-loop baseline ``bench.py --no-ray``): ``warmup``
+untimed steps, then exactly ``steps`` timed steps bracketed by barrier +
+device synchronize on both sides; the MAX elapsed time over ranks is the step
+time. Rank 0 reports through ``train.report``.
+
+Reference parity: release/air_tests/air_benchmarks/workloads/torch_benchmark.py:81
+(train_func run under TorchTrainer, :233, compared against a vanilla torch run).
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+
+DEFAULTS = dict(model="small", micro_batch=64, seq_len=1024, steps=20, warmup=5,
+                grad_accum=1, bucket_mb=32.0, grad_dtype="fp32", tunableop="auto",
+                lm_head_chunk=8192, device=None)
+
+
+def tunableop_file(model: str, micro_batch: int, seq_len: int) -> str:
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))))
+    return os.path.join(root, "profiles", "tunableop",
+                        f"gpt2_{model}_mb{micro_batch}_t{seq_len}.csv")
+
+
+def setup_tunableop(mode: str, src: str, rank: int):
+    """Per-shape GEMM kernel selection (PyTorch TunableOp) from a committed results file.
+
+    'tune' benchmarks every hipBLASLt/rocBLAS solution per GEMM shape during warmup (the
+    caller writes the file afterwards with ``save_tunableop``); 'auto' uses the file if
+    present; 'off' keeps hipBLASLt's heuristic. Returns the selection label."""
+    import shutil
+
+    import torch
+
+    if mode == "off" or (mode == "auto" and not os.path.exists(src)):
+        return "heuristic"
+    os.makedirs("/tmp/ray_amd_tunableop", exist_ok=True)
+    dst = f"/tmp/ray_amd_tunableop/{os.getpid()}_{rank}_{os.path.basename(src)}"
+    if os.path.exists(src):
+        shutil.copyfile(src, dst)
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(mode == "tune")
+    torch.cuda.tunable.set_filename(dst, insert_device_ordinal=False)
+    if os.path.exists(dst):
+        torch.cuda.tunable.read_file(dst)
+    if mode == "tune":
+        torch.cuda.tunable.set_max_tuning_duration(30)
+        torch.cuda.tunable.set_max_tuning_iterations(20)
+
+        def _beat(t0=time.time()):  # tuning can run minutes without output
+            while torch.cuda.tunable.tuning_is_enabled():
+                time.sleep(30)
+                print(f"[gpt2] tunableop tuning... {time.time() - t0:.0f}s", file=sys.stderr,
+                      flush=True)
+
+        threading.Thread(target=_beat, daemon=True).start()
+        return "tunableop-tuning"
+    return "tunableop"
+
+
+def save_tunableop(dst: str):
+    import torch
+
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    with open(dst, "w") as f:  # TunableOp results-file format
+        for k, v in torch.cuda.tunable.get_validators():
+            f.write(f"Validator,{k},{v}\n")
+        for op, params, kernel, t in torch.cuda.tunable.get_results():
+            f.write(f"{op},{params},{kernel},{t}\n")
+    torch.cuda.tunable.tuning_enable(False)
+
+
+def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
+    """Build the model on ``device`` and run warmup + timed steps (shared by the Ray Train
+    worker and the bare torchrun baseline). torch.distributed must already be set up
+    when world > 1."""
+    import torch
+    import torch.distributed as dist
+
+    from ray_amd.models.gpt2 import GPT2Config
+    from ray_amd.train.gpt2_step import GPT2Trainer
+
+    c = dict(DEFAULTS, **(cfg or {}))
+    on_gpu = device.type == "cuda"
+    gemm = "heuristic"
+    tfile = tunableop_file(c["model"], c["micro_batch"], c["seq_len"])
+    if on_gpu:
+        gemm = setup_tunableop(c["tunableop"], tfile, rank)
+    mcfg = getattr(GPT2Config, c["model"])()
+    gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
+    tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],
+                     total_steps=c["warmup"] + c["steps"], grad_accum=c["grad_accum"],
+                     seed=1234, grad_dtype=gdt, lm_head_chunk=c["lm_head_chunk"])
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1000 + rank)
+    # synthetic token pool generated up front: data generation is not timed work
+    pool = [tr.synthetic_batch(gen) for _ in range(4 * c["grad_accum"])]
+
+    def batches(i):
+        ga = c["grad_accum"]
+        return [pool[(i * ga + j) % len(pool)] for j in range(ga)]
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(device)
+
+    for i in range(c["warmup"]):
+        tr.step(batches(i))
+    sync()
+    if gemm == "tunableop-tuning":
+        if rank == 0:
+            save_tunableop(tfile)
+        else:
+            torch.cuda.tunable.tuning_enable(False)
+        gemm = "tunableop"
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(c["steps"]):
+        tr.step(batches(c["warmup"] + i))
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    loss = float(tr.last_loss)
+    per_rank = [dt]
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank = [float(x) for x in allt]
+        dt = max(per_rank)
+        # ranks must hold identical weights after the run (same all-reduced grads)
+        chk = tr.flat.p32[: min(4096, tr.flat.numel)].double().sum().reshape(1)
+        allc = [torch.zeros_like(chk) for _ in range(world)]
+        dist.all_gather(allc, chk)
+        in_sync = all(float(x) == float(allc[0]) for x in allc)
+    else:
+        in_sync = True
+    tokens = tr.tokens_per_step() * c["steps"]
+    flops = tr.model.flops_per_token(c["seq_len"]) * tokens
+    return {
+        "tokens_per_sec": tokens / dt,
+        "ms_per_step": dt / c["steps"] * 1000,
+        "per_rank_ms_per_step": [round(x / c["steps"] * 1000, 3) for x in per_rank],
+        "world_size": world,
+        "rccl_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+        "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+        "model_tflops_per_gpu": flops / dt / world / 1e12,
+        "params": tr.model.num_params(),
+        "loss": loss,
+        "ranks_in_sync": in_sync,
+        "gemm_selection": gemm,
+        "grad_dtype": c["grad_dtype"],
+        "global_batch": c["micro_batch"] * c["grad_accum"] * world,
+    }
+
+
+def train_func(config: dict):
+    """train_loop_per_worker for TorchTrainer."""
+    import torch.distributed as dist
+
+    from ray_amd import train
+    from ray_amd.train.torch import get_device
+
+    ctx = train.get_context()
+    dev = get_device()
+    if (config or {}).get("device") == "cpu":
+        import torch
+
+        dev = torch.device("cpu")
+    world = dist.get_world_size() if dist.is_initialized() else ctx.get_world_size()
+    out = run_steps(config, dev, ctx.get_world_rank(), world)
+    out["device"] = str(dev)
+    train.report(out)

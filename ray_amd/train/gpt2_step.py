@@ -1,9 +1,9 @@
 """One GPT-2 DDP training step on MI355X — the per-worker body of the headline
 Ray Train benchmark (TorchTrainer GPT-2-small DDP bf16).
 
-Used by ``bench.py`` (one rank per GPU under torch.distributed.run) and by
-``ray_amd.train.examples.gpt2.train_func`` (one rank per GPU as Train worker
-actors). Everything inside ``step()`` is real work: forward, backward, bucketed
+Used by ``ray_amd.train.examples.gpt2.train_func`` (one rank per GPU as
+TorchTrainer worker actors — what ``bench.py`` runs) and by ``bench.py --no-ray``
+(the same step in a bare torch.distributed.run loop, for comparison). Everything inside ``step()`` is real work: forward, backward, bucketed
 RCCL all-reduce overlapped with backward, global-norm clip, fused AdamW.
 """
 
@@ -17,20 +17,29 @@ from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams, cosine_lr
 
 
 class GPT2Trainer:
+    """grad_dtype: fp32 (default — the precision torch DDP reduces in) or bf16 (explicit
+    gradient compression: half the all-reduce bytes, bf16-rounded accumulation)."""
+
     def __init__(self, cfg: GPT2Config, micro_batch: int, seq_len: int, device,
                  lr: float = 6e-4, bucket_mb: float = 32.0, total_steps: int = 1000,
-                 warmup_steps: int = 10, seed: int = 1234, grad_accum: int = 1):
+                 warmup_steps: int = 10, seed: int = 1234, grad_accum: int = 1,
+                 grad_dtype: torch.dtype = torch.float32, param_dtype: torch.dtype | None = None,
+                 lm_head_chunk: int = 8192):
         torch.manual_seed(seed)
         self.cfg = cfg
         self.B, self.T = micro_batch, seq_len
-        self.device = device
+        self.device = torch.device(device)
         self.grad_accum = grad_accum
-        model = GPT2(cfg).to(device=device, dtype=torch.bfloat16)
+        if param_dtype is None:  # bf16 compute on the GPU; fp32 for CPU (gloo) runs
+            param_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        model = GPT2(cfg).to(device=self.device, dtype=param_dtype)
+        model.lm_head_chunk = lm_head_chunk
         self.model = model
-        self.flat = FlatParams(model)
+        self.flat = FlatParams(model, dtype=param_dtype, grad_dtype=grad_dtype)
         self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb)
+        # AdamW clears the flat gradient in its own pass (no zero_grad memset per step)
         self.opt = FlatAdamW(self.flat, lr=lr, weight_decay=0.1, max_grad_norm=1.0,
-                             grad_scale=self.ddp.grad_scale / grad_accum)
+                             grad_scale=self.ddp.grad_scale / grad_accum, zero_grad=True)
         self.base_lr = lr
         self.total_steps = total_steps
         self.warmup = warmup_steps
@@ -44,7 +53,7 @@ class GPT2Trainer:
 
     def step(self, batches):
         """batches: list of (idx, targets), len == grad_accum."""
-        self.flat.zero_grad()
+        # the flat gradient was zeroed by the previous AdamW pass (or at creation)
         loss_sum = None
         for i, (x, y) in enumerate(batches):
             self.ddp.sync = i == len(batches) - 1

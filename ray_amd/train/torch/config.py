@@ -5,8 +5,11 @@ MI355X specifics:
 * backend "nccl" is RCCL on ROCm; CPU-only groups use gloo.
 * all ranks on a node see the union of the group's GPUs (HIP_VISIBLE_DEVICES),
   each rank binds ``cuda:<its index in that list>`` — RCCL then uses xGMI
-  peer-to-peer between the ranks' processes (like the reference's
-  share_cuda_visible_devices).
+  peer-to-peer between the ranks' processes (the reference's
+  share_cuda_visible_devices, config.py:150). Unlike the reference, the
+  visibility is fixed by the raylet when it SPAWNS the worker process (the
+  placement-group strategy carries ``share_gpus``), never rewritten inside a
+  running actor.
 * rendezvous over TCP on 127.0.0.1 for single-node groups.
 """
 
@@ -30,13 +33,15 @@ class TorchConfig(BackendConfig):
         return _TorchBackend
 
 
-def _setup_env(global_gpu_ids, my_gpu_ids):
-    if global_gpu_ids:
-        os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in global_gpu_ids)
-        os.environ.pop("CUDA_VISIBLE_DEVICES", None)
-        idx = global_gpu_ids.index(my_gpu_ids[0]) if my_gpu_ids else 0
-        os.environ["RAY_AMD_LOCAL_DEVICE"] = str(idx)
-    return True
+def _check_binding():
+    """Report this worker's device binding. The raylet spawned the process with
+    HIP_VISIBLE_DEVICES = the union of the group's GPUs on this node and
+    RAY_AMD_LOCAL_DEVICE = its own ordinal in that list (raylet._shared_visible), so
+    nothing here rewrites the environment of a process that may already have
+    initialised HIP."""
+    return {"visible": os.environ.get("HIP_VISIBLE_DEVICES", ""),
+            "local_device": int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0")),
+            "gpu_ids": os.environ.get("RAY_AMD_GPU_IDS", "")}
 
 
 def _init_pg(backend, master_addr, master_port, rank, world, local_rank, timeout_s):
@@ -70,13 +75,13 @@ class _TorchBackend(Backend):
         use_gpu = any(i["gpu_ids"] for i in infos)
         backend = backend_config.backend or ("nccl" if use_gpu else "gloo")
         if use_gpu:
-            by_node = {}
-            for i in infos:
-                by_node.setdefault(i["node_id"], []).extend(i["physical_gpu_ids"])
-            futs = [w.execute.remote(_setup_env, sorted(set(by_node[i["node_id"]]), key=int),
-                                     i["physical_gpu_ids"])
-                    for w, i in zip(worker_group.workers, infos)]
-            ray.get(futs)
+            binds = ray.get([w.execute.remote(_check_binding) for w in worker_group.workers])
+            seen = {}
+            for b, i in zip(binds, infos):
+                key = (i["node_id"], b["visible"], b["local_device"])
+                if key in seen:
+                    raise RuntimeError(f"two Train ranks bound to the same GPU: {b}")
+                seen[key] = True
         port = ray.get(worker_group.workers[0].free_port.remote())
         local = {}
         futs = []

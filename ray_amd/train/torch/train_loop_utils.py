@@ -79,7 +79,8 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True,
                                        is_bf16):
         from ray_amd.parallel.flat import FlatDDP, FlatParams
 
-        flat = FlatParams(model, dtype=params[0].dtype)
+        gd = kw.get("grad_dtype", torch.float32)  # fp32 reduce by default (torch DDP parity)
+        flat = FlatParams(model, dtype=params[0].dtype, grad_dtype=gd)
         ddp = FlatDDP(flat, bucket_mb=kw.get("bucket_mb", 32.0))
         return FlatPreparedModel(model, flat, ddp)
     if world > 1 and parallel_strategy in ("auto", "ddp"):

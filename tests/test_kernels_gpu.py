@@ -293,7 +293,7 @@ def test_flat_direct_grads_match_autograd(cuda_device):
     assert ddp._ready == ddp.bucket_sizes  # each param signalled once
     ddp.finish()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
-        assert _rel(pb.grad, pa.grad) < 3e-2, n
+        assert _rel(pb._ra_grad, pa.grad) < 3e-2, n
 
 
 def test_residual_layer_norm(cuda_device):

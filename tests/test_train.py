@@ -124,3 +124,37 @@ def test_gpt2_tiny_flat_ddp_cpu_gloo(cluster, tmp_path):
     r = TorchTrainer(loop, scaling_config=ScalingConfig(num_workers=2),
                      run_config=RunConfig(storage_path=str(tmp_path))).fit()
     assert r.metrics["synced"] and r.metrics["buckets"] > 1
+
+
+def _bench_json(out: str) -> dict:
+    import json
+
+    lines = [ln for ln in out.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("no_ray", [False, True])
+def test_bench_launcher_gloo_two_ranks(no_ray):
+    """bench.py under torch.distributed.run with 2 ranks (the driver's N>1 launch), GPT-2
+    tiny on gloo: the TorchTrainer path (rank 0 drives Ray, 2 Train workers) and the bare
+    loop report the same world size, stay in sync and reach the same loss."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29600 + (7 if no_ray else 3)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--device", "cpu", "--model", "tiny", "--micro-batch", "2", "--seq-len", "64",
+           "--steps", "3", "--warmup", "1"] + (["--no-ray"] if no_ray else [])
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _bench_json(r.stdout)
+    assert j["n_gpus"] == 2 and j["rccl_world_size"] == 2 and j["dist_backend"] == "gloo"
+    assert j["ranks_in_sync"] is True
+    assert len(j["per_rank_ms_per_step"]) == 2
+    assert j["config"]["launcher"] == ("torch.distributed.run (no Ray)" if no_ray
+                                       else "ray_amd TorchTrainer")
+    assert abs(j["final_loss"] - 6.24) < 0.05  # same seed, same synthetic data either way
