@@ -502,8 +502,13 @@ class _Embedding(torch.autograd.Function):
 
 
 def embedding(idx, wte, wpe):
-    """Token + learned position embedding for [B, T] indices."""
-    if getattr(wte, "_ra_direct_grad", False) or getattr(wpe, "_ra_direct_grad", False):
+    """Token + learned position embedding for [B, T] indices.
+
+    The direct-sink path is taken under the same condition as the HIP LM head
+    (bf16 on the GPU): a tied ``wte`` must receive ALL its gradient contributions
+    through sinks, or the DDP readiness signal would fire before autograd's part."""
+    if _hip(idx) and wte.dtype == torch.bfloat16 and \
+            (getattr(wte, "_ra_direct_grad", False) or getattr(wpe, "_ra_direct_grad", False)):
         return _Embedding.apply(idx, wte, wpe)
     T = idx.shape[1]
     return torch.nn.functional.embedding(idx, wte) + wpe[:T].unsqueeze(0)
