@@ -1,104 +1,146 @@
-"""ActorPool (reference: python/ray/util/actor_pool.py)."""
+"""ActorPool: schedule a stream of calls over a fixed set of actors.
+
+API contract (reference: python/ray/util/actor_pool.py — ``map``, ``map_unordered``,
+``submit``, ``has_next``, ``get_next``, ``get_next_unordered``, ``has_free``,
+``pop_idle``, ``push``).
+
+Design: every submission is a ``_Job`` that moves through
+``queued -> running -> ready -> consumed``. Queued jobs wait in a backlog until an
+actor is free; a running job's actor is released the moment its result is known to be
+ready (``ready``), so the backlog keeps draining while the caller has not consumed the
+value yet. One deque keeps the unconsumed jobs in submission order, so ordered and
+unordered retrieval can be mixed freely: ``get_next`` returns the oldest unconsumed
+result, ``get_next_unordered`` whichever is ready first.
+"""
 
 from __future__ import annotations
 
+import collections
+from typing import Any, Callable, Iterable
+
 import ray_amd as ray
+
+_QUEUED, _RUNNING, _READY, _CONSUMED = range(4)
+
+
+class _Job:
+    __slots__ = ("fn", "value", "ref", "actor", "state")
+
+    def __init__(self, fn: Callable, value: Any):
+        self.fn, self.value = fn, value
+        self.ref = self.actor = None
+        self.state = _QUEUED
 
 
 class ActorPool:
     def __init__(self, actors: list):
-        self._idle_actors = list(actors)
-        self._future_to_actor = {}
-        self._index_to_future = {}
-        self._next_task_index = 0
-        self._next_return_index = 0
-        self._pending_submits = []
+        self._free: collections.deque = collections.deque(actors)
+        self._backlog: collections.deque[_Job] = collections.deque()
+        self._running: dict = {}  # ObjectRef -> _Job
+        self._order: collections.deque[_Job] = collections.deque()  # unconsumed jobs
 
-    def map(self, fn, values):
-        while self.has_next():
-            try:
-                self.get_next_unordered(timeout=0)
-            except TimeoutError:
-                break
-        for v in values:
-            self.submit(fn, v)
+    # -------------------------------------------------------------- scheduling
+    def _dispatch(self):
+        while self._free and self._backlog:
+            job = self._backlog.popleft()
+            job.actor = self._free.popleft()
+            job.ref = job.fn(job.actor, job.value)
+            job.state = _RUNNING
+            self._running[job.ref] = job
 
-        def gen():
-            while self.has_next():
-                yield self.get_next()
+    def _mark_ready(self, job: _Job):
+        del self._running[job.ref]
+        job.state = _READY
+        self._free.append(job.actor)
+        job.actor = None
+        self._dispatch()
 
-        return gen()
+    def _consume(self, job: _Job):
+        job.state = _CONSUMED
+        while self._order and self._order[0].state == _CONSUMED:
+            self._order.popleft()
+        return ray.get(job.ref)
 
-    def map_unordered(self, fn, values):
-        for v in values:
-            self.submit(fn, v)
+    def _wait(self, refs, timeout, ignore_if_timedout):
+        ready, _ = ray.wait(refs, num_returns=1, timeout=timeout)
+        if ready:
+            return ready[0]
+        if ignore_if_timedout:
+            return None
+        raise TimeoutError("Timed out waiting for result")
 
-        def gen():
-            while self.has_next():
-                yield self.get_next_unordered()
+    def submit(self, fn: Callable, value) -> None:
+        """Schedule ``fn(actor, value)`` (which must return an ObjectRef) on a free actor,
+        or queue it until one frees up."""
+        job = _Job(fn, value)
+        self._backlog.append(job)
+        self._order.append(job)
+        self._dispatch()
 
-        return gen()
-
-    def submit(self, fn, value):
-        if self._idle_actors:
-            actor = self._idle_actors.pop()
-            future = fn(actor, value)
-            key = future
-            self._future_to_actor[key] = (self._next_task_index, actor)
-            self._index_to_future[self._next_task_index] = future
-            self._next_task_index += 1
-        else:
-            self._pending_submits.append((fn, value))
-
-    def has_next(self):
-        return bool(self._future_to_actor)
+    # -------------------------------------------------------------- retrieval
+    def has_next(self) -> bool:
+        return bool(self._order)
 
     def get_next(self, timeout=None, ignore_if_timedout=False):
-        if not self.has_next():
+        """Result of the oldest unconsumed submission (blocking)."""
+        if not self._order:
             raise StopIteration("No more results to get")
-        if self._next_return_index >= self._next_task_index:
-            raise ValueError("It is not allowed to call get_next() after get_next_unordered().")
-        future = self._index_to_future[self._next_return_index]
-        if timeout is not None:
-            res, _ = ray.wait([future], timeout=timeout)
-            if not res:
-                if not ignore_if_timedout:
-                    raise TimeoutError("Timed out waiting for result")
+        job = self._order[0]
+        while job.state == _QUEUED:  # free an actor for it: wait for any running job
+            ref = self._wait(list(self._running), timeout, ignore_if_timedout)
+            if ref is None:
                 return None
-        del self._index_to_future[self._next_return_index]
-        self._next_return_index += 1
-        i, a = self._future_to_actor.pop(future)
-        self._return_actor(a)
-        return ray.get(future)
+            self._mark_ready(self._running[ref])
+        if job.state == _RUNNING:
+            if self._wait([job.ref], timeout, ignore_if_timedout) is None:
+                return None
+            self._mark_ready(job)
+        return self._consume(job)
 
     def get_next_unordered(self, timeout=None, ignore_if_timedout=False):
-        if not self.has_next():
+        """Result of whichever unconsumed submission is ready first."""
+        if not self._order:
             raise StopIteration("No more results to get")
-        res, _ = ray.wait(list(self._future_to_actor), num_returns=1, timeout=timeout)
-        if not res:
-            if ignore_if_timedout:
-                return None
-            raise TimeoutError("Timed out waiting for result")
-        future = res[0]
-        i, a = self._future_to_actor.pop(future)
-        self._return_actor(a)
-        del self._index_to_future[i]
-        self._next_return_index = max(self._next_return_index, i + 1)
-        return ray.get(future)
+        for job in self._order:  # already known ready (released early by get_next)
+            if job.state == _READY:
+                return self._consume(job)
+        if not self._running:
+            raise RuntimeError("ActorPool has queued work but no actors")
+        ref = self._wait(list(self._running), timeout, ignore_if_timedout)
+        if ref is None:
+            return None
+        job = self._running[ref]
+        self._mark_ready(job)
+        return self._consume(job)
 
-    def _return_actor(self, actor):
-        self._idle_actors.append(actor)
-        if self._pending_submits:
-            self.submit(*self._pending_submits.pop(0))
+    def map(self, fn: Callable, values: Iterable):
+        """Apply ``fn(actor, v)`` to every value (submitted now); results in input order."""
+        for v in values:
+            self.submit(fn, v)
+        return self._drain(self.get_next)
 
-    def has_free(self):
-        return bool(self._idle_actors) and not self._pending_submits
+    def map_unordered(self, fn: Callable, values: Iterable):
+        """Like ``map`` but yields results as they complete."""
+        for v in values:
+            self.submit(fn, v)
+        return self._drain(self.get_next_unordered)
+
+    def _drain(self, get):
+        while self.has_next():
+            yield get()
+
+    # -------------------------------------------------------------- membership
+    def has_free(self) -> bool:
+        return bool(self._free) and not self._backlog
 
     def pop_idle(self):
-        return self._idle_actors.pop() if self.has_free() else None
+        """Remove and return an idle actor (None if none is idle)."""
+        return self._free.popleft() if self.has_free() else None
 
-    def push(self, actor):
-        busy = [a for _, a in self._future_to_actor.values()]
-        if actor in self._idle_actors or actor in busy:
+    def push(self, actor) -> None:
+        """Add an actor to the pool (it immediately takes queued work)."""
+        busy = [j.actor for j in self._running.values()]
+        if actor in self._free or actor in busy:
             raise ValueError("Actor already belongs to current ActorPool")
-        self._return_actor(actor)
+        self._free.append(actor)
+        self._dispatch()

@@ -1,0 +1,103 @@
+"""Round-2 GPT-2 component microbenchmarks on one MI355X (GPT-2 small, 64 x 1024 tokens).
+
+    python scripts/r2_perf_bench.py [--part wgrad,lmhead,xent]
+
+wgrad : weight-gradient GEMM variants into an fp32 flat-gradient sink
+lmhead: fused chunked LM-head cross-entropy (fwd+bwd) per chunk size
+xent  : the in-place fused softmax-xent kernel alone (HBM GB/s)
+"""
+
+import argparse
+import json
+
+import torch
+
+from ray_amd.ops import _lib
+from ray_amd.ops import functional as rf
+from ray_amd.ops._lib import ptr, stream_ptr
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def bench_wgrad(M=65536, C=768):
+    dev, bf = "cuda", torch.bfloat16
+    L = _lib.lib()
+    out = {}
+    for name, (N, K) in {"qkv": (3 * C, C), "proj": (C, C), "fc": (4 * C, C),
+                         "mlp_proj": (C, 4 * C)}.items():
+        x = torch.randn(M, K, device=dev, dtype=bf)
+        dy = torch.randn(M, N, device=dev, dtype=bf)
+        sink = torch.zeros(N, K, device=dev, dtype=torch.float32)
+        fl = 2 * M * N * K
+        r = {}
+        for S in (1, 2, 4, 8, 16):
+            dys = dy.view(S, M // S, N).transpose(1, 2)
+            xs = x.view(S, M // S, K)
+
+            def f(S=S, dys=dys, xs=xs):
+                part = torch.bmm(dys, xs, out_dtype=torch.float32)
+                L.ra_splitk_accum(ptr(part), S, N * K, ptr(sink), 3, stream_ptr())
+
+            r[f"splitk{S}"] = timeit(f)
+        r["addmm_f32"] = timeit(lambda: torch.addmm(sink, dy.t(), x, out_dtype=torch.float32,
+                                                    out=sink))
+        r["addmm_f32_T"] = timeit(lambda: torch.addmm(sink.t(), x.t(), dy,
+                                                      out_dtype=torch.float32, out=sink.t()))
+        out[name] = {k: f"{v:.4f} ms {fl / v / 1e9:.0f} TF" for k, v in r.items()}
+    return out
+
+
+def bench_lmhead(N=65536, C=768, V=50257, Vp=50304):
+    dev = "cuda"
+    h = (torch.randn(N, C, device=dev) * 0.5).bfloat16().requires_grad_()
+    w = (torch.randn(Vp, C, device=dev) * 0.05).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=dev)
+    fl = 3 * 2 * N * Vp * C
+    out = {}
+    for ch in (2048, 4096, 8192, 16384):
+        def f(ch=ch):
+            h.grad = None
+            w.grad = None
+            rf.lm_head_cross_entropy(h, w, t, V, chunk=ch).backward()
+
+        ms = timeit(f, iters=5, warmup=2)
+        out[f"chunk{ch}"] = f"{ms:.3f} ms {fl / ms / 1e9:.0f} TF(gemm-equiv)"
+    return out
+
+
+def bench_xent(N=8192, V=50257, Vp=50304):
+    dev = "cuda"
+    L = _lib.lib()
+    lg = torch.randn(N, Vp, device=dev).bfloat16()
+    t = torch.randint(0, V, (N,), device=dev)
+    inv = torch.ones(1, device=dev)
+    loss = torch.empty(N, device=dev)
+    ms = timeit(lambda: L.ra_xent_fused(ptr(lg), ptr(t), ptr(inv), ptr(loss), N, V, Vp, -100,
+                                        stream_ptr()))
+    gb = 2 * N * Vp * 2 / 1e9
+    return {"xent_fused_8192": f"{ms:.4f} ms {gb / ms:.2f} TB/s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--part", default="wgrad,lmhead,xent")
+    a = ap.parse_args()
+    res = {}
+    for p in a.part.split(","):
+        res[p] = {"wgrad": bench_wgrad, "lmhead": bench_lmhead, "xent": bench_xent}[p]()
+        print(json.dumps({p: res[p]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,63 @@ def test_actor_pool(cluster):
     assert not pool.has_next()
 
 
+def test_actor_pool_backlog_mixed_order_and_membership(cluster):
+    @ray.remote
+    class Sleeper:
+        def run(self, v):
+            time.sleep(0.05 * (v % 3))
+            return v
+
+    a, b = Sleeper.remote(), Sleeper.remote()
+    pool = ActorPool([a])
+    for v in range(6):  # more work than actors: backlog drains as actors free up
+        pool.submit(lambda ac, v: ac.run.remote(v), v)
+    assert not pool.has_free()
+    got = [pool.get_next_unordered(), pool.get_next()]  # mixing is allowed
+    pool.push(b)
+    with pytest.raises(ValueError):
+        pool.push(b)
+    while pool.has_next():
+        got.append(pool.get_next())
+    assert sorted(got) == list(range(6))
+    assert pool.has_free()
+    idle = pool.pop_idle()
+    assert idle is not None
+    with pytest.raises(StopIteration):
+        pool.get_next()
+    pool.submit(lambda ac, v: ac.run.remote(v), 7)
+    assert pool.get_next(timeout=10) == 7
+
+
+def test_queue_nowait_and_async(cluster):
+    import asyncio
+
+    q = Queue(maxsize=3)
+    with pytest.raises(Empty):
+        q.get_nowait()
+    q.put_nowait_batch([1, 2, 3])
+    assert q.full() and len(q) == 3
+    with pytest.raises(Full):
+        q.put_nowait(4)
+    with pytest.raises(Full):
+        q.put_nowait_batch([4, 5, 6, 7])
+    with pytest.raises(Empty):
+        q.get_nowait_batch(4)
+    with pytest.raises(ValueError):
+        q.get(timeout=-1)
+
+    async def go():
+        await q.put_async(9, block=False) if False else None
+        x = await q.get_async()
+        await q.put_async(10)
+        return x
+
+    assert asyncio.run(go()) == 1
+    assert q.get_nowait_batch(3) == [2, 3, 10]
+    assert q.empty()
+    q.shutdown()
+
+
 def test_queue(cluster):
     q = Queue(maxsize=2)
     q.put(1)
