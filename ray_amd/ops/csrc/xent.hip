@@ -106,6 +106,13 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16_t* __restrict_
 // read from HBM/MALL once and overwritten once with
 //   dlogits = (softmax(row) - onehot(target)) * inv_count     (0 on padding columns)
 // and loss[row] = lse - row[target]. inv_count is a device scalar (no host sync).
+//
+// VALU diet (the kernel is VALU- as much as HBM-bound at 50304 columns): the max pass
+// is unpack+max; the sum pass computes e = exp2(v*log2e - m*log2e) ONCE and keeps it,
+// re-packed to bf16, in the same registers; the output pass is one multiply per element.
+// Column bounds are checked per 8-wide vector, not per element, and the target column
+// is patched by its owning lane from the fp32 target logit (p_t - 1 must not lose the
+// cancellation to a bf16-rounded e).
 template <int NV>
 __global__ __launch_bounds__(512) void xent_fused_kernel(bf16_t* __restrict__ logits,
                                                          const long* __restrict__ targets,
@@ -120,12 +127,22 @@ __global__ __launch_bounds__(512) void xent_fused_kernel(bf16_t* __restrict__ lo
   const bool ign = (t == ignore_index || t < 0 || t >= V);
   if (threadIdx.x == 0) tlogit = ign ? 0.f : bf2f(lr[t]);  // read before any overwrite
   const int Vp8 = Vp >> 3;
+  const int Vfull = V >> 3;  // vectors [0, Vfull) hold only real columns
   uint4 raw[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c8 = k * 512 + threadIdx.x;
     if (c8 < Vp8) raw[k] = reinterpret_cast<const uint4*>(lr)[c8];
   }
+  // vector-level masks: partial vector (the one holding column V-1 when V % 8) and
+  // all-padding vectors get per-element / zero treatment
+  auto masked = [&](int c8, float (&v)[8]) __attribute__((always_inline)) {
+    if (c8 >= Vfull) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c8 * 8 + j >= V) v[j] = -INFINITY;
+    }
+  };
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -133,12 +150,14 @@ __global__ __launch_bounds__(512) void xent_fused_kernel(bf16_t* __restrict__ lo
     if (c8 < Vp8) {
       float v[8];
       unpack8(raw[k], v);
+      masked(c8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c8 * 8 + j < V) m = fmaxf(m, v[j]);
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, v[j]);
     }
   }
   m = block_max<8>(m, red);
+  const float L2E = 1.4426950408889634f;
+  const float mb = m * L2E;
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -146,26 +165,33 @@ __global__ __launch_bounds__(512) void xent_fused_kernel(bf16_t* __restrict__ lo
     if (c8 < Vp8) {
       float v[8];
       unpack8(raw[k], v);
+      masked(c8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c8 * 8 + j < V) s += __expf(v[j] - m);
+      for (int j = 0; j < 8; ++j) {
+        v[j] = __builtin_amdgcn_exp2f(fmaf(v[j], L2E, -mb));  // exp(-inf) = 0 on padding
+        s += v[j];
+      }
+      raw[k] = pack8(v);
     }
   }
   s = block_sum<8>(s, red);
   const float lse = m + __logf(s);
   const float scale = ign ? 0.f : *inv_count;
+  const float c = scale / s;
+  const int tv = ign ? -1 : (int)(t >> 3);
+  const float pt_grad = (__expf(tlogit - lse) - 1.f) * scale;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c8 = k * 512 + threadIdx.x;
     if (c8 < Vp8) {
-      float v[8], o[8];
-      unpack8(raw[k], v);
+      float o[8];
+      unpack8(raw[k], o);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c8 * 8 + j;
-        float p = (c < V) ? __expf(v[j] - lse) : 0.f;
-        if (c == t) p -= 1.f;
-        o[j] = p * scale;
+      for (int j = 0; j < 8; ++j) o[j] *= c;
+      if (c8 == tv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == (int)(t & 7)) o[j] = pt_grad;
       }
       reinterpret_cast<uint4*>(lr)[c8] = pack8(o);
     }

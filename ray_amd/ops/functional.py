@@ -262,11 +262,13 @@ def bias_residual(h, bias, res):
 
 # --------------------------------------------------------------------- linear (split-K wgrad)
 def _splitk(M: int, N: int, K: int) -> int:
-    """Token slices for the wgrad GEMM: enough (N/128)*(K/128) tiles x S to fill 256 CUs
-    twice, each slice >= 1024 tokens (measured best S: qkv/proj 8, fc/mlp_proj 4)."""
-    tiles = max(1, (N // 128) * (K // 128))
+    """Token slices for the wgrad GEMM. Measured on MI355X at M = 65536 (GPT-2 small,
+    profiles/r2_perf_bench.log): S = 16 is the fastest for every projection (qkv 0.28 ms
+    vs 0.39 at S = 4, proj 0.09 vs 0.14 at S = 8, fc/mlp_proj within 3 %) — hipBLASLt's
+    batched kernels fill the 256 CUs only with many (N/256)*(K/256)*S tiles. Slices
+    stay >= 2048 tokens so each batch GEMM keeps a long K loop."""
     S = 1
-    while S < 8 and S * tiles < 512 and M % (2 * S) == 0 and M // (2 * S) >= 1024:
+    while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 2048:
         S *= 2
     return S
 

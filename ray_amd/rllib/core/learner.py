@@ -80,15 +80,38 @@ class Learner:
         self.flat.sync_master_from_params()
 
     def get_state(self):
-        return {"weights": self.get_weights(), "opt": {k: v.cpu() if torch.is_tensor(v) else v
-                                                       for k, v in self.opt.state_dict().items()},
+        """Lossless learner state: the fp32 MASTER weights (not the bf16 compute copy),
+        their flat layout, and the optimizer moments."""
+        return {"weights": self.get_weights(),
+                "master": {"p32": self.flat.p32.detach().cpu(), "names": list(self.flat.names),
+                           "offsets": list(self.flat.offsets)},
+                "opt": {k: v.cpu() if torch.is_tensor(v) else v
+                        for k, v in self.opt.state_dict().items()},
                 "kl_coeff": self.kl_coeff}
 
     def set_state(self, s):
-        self.set_weights(s["weights"])
+        m = s.get("master")
+        if m is not None and m["names"] == list(self.flat.names) and \
+                m["offsets"] == list(self.flat.offsets):
+            with torch.no_grad():
+                self.flat.p32.copy_(m["p32"].to(self.device))
+                if self.flat.p16 is not self.flat.p32:
+                    self.flat.p16.copy_(self.flat.p32)
+        else:  # older checkpoint / different layout: rebuild the master from the weights
+            self.set_weights(s["weights"])
         self.opt.load_state_dict({k: v.to(self.device) if torch.is_tensor(v) else v
                                   for k, v in s["opt"].items()})
         self.kl_coeff = s.get("kl_coeff", self.kl_coeff)
+
+    # ---------------------------------------------------------------- multi-learner agreement
+    def _allreduce(self, t, op="sum"):
+        """all-reduce across the learner group (no-op for a single learner)."""
+        if self.world <= 1:
+            return t
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MIN if op == "min" else dist.ReduceOp.SUM)
+        return t
 
     # ---------------------------------------------------------------- helpers
     def _fwd(self, obs):
@@ -139,9 +162,25 @@ class Learner:
             obs_flat, acts, old_logp, old_di, adv, vtarg, vals = (
                 t.index_select(0, keep)
                 for t in (obs_flat, acts, old_logp, old_di, adv, vtarg, vals))
-        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        # advantage standardisation over the WHOLE learner group's batch; population std so
+        # a 1-row shard is not NaN
         N = adv.shape[0]
-        mb = min(int(c.get("minibatch_size", 128)), N)
+        mom = self._allreduce(torch.stack([adv.sum(), (adv * adv).sum(),
+                                           torch.tensor(float(N), device=dev)]).double())
+        cnt = max(float(mom[2]), 1.0)
+        mean = mom[0] / cnt
+        std = torch.sqrt(torch.clamp(mom[1] / cnt - mean * mean, min=0.0))
+        adv = ((adv - mean.float()) / (std.float() + 1e-8))
+        # every rank must run the SAME number of SGD steps (each step all-reduces inside
+        # backward): agree on the smallest shard and subsample to it
+        if self.world > 1:
+            n_common = int(self._allreduce(torch.tensor([N], device=dev), op="min")[0])
+        else:
+            n_common = N
+        if n_common == 0:
+            self.updates += 1
+            return {"num_minibatches": 0, "curr_kl_coeff": self.kl_coeff}
+        mb = min(int(c.get("minibatch_size", 128)), n_common)
         stats_acc = torch.zeros(6, device=dev)
         n_mb = 0
         # masked (multi-agent) batches change N every update: no graph re-capture per call
@@ -153,8 +192,8 @@ class Learner:
             idx_buf, stats_buf = self._graph_io
             stats_buf.zero_()
             for _ in range(int(c.get("num_epochs", 1))):
-                perm = torch.randperm(N, device=dev)
-                for s in range(0, N - mb + 1, mb):
+                perm = torch.randperm(N, device=dev)[:n_common]
+                for s in range(0, n_common - mb + 1, mb):
                     idx_buf.copy_(perm[s:s + mb])
                     g.replay()
                     self.ddp.finish()
@@ -162,8 +201,8 @@ class Learner:
                     n_mb += 1
             stats_acc = stats_buf
         for _ in range(int(c.get("num_epochs", 1)) if g is None else 0):
-            perm = torch.randperm(N, device=dev)
-            for s in range(0, N - mb + 1, mb):
+            perm = torch.randperm(N, device=dev)[:n_common]
+            for s in range(0, n_common - mb + 1, mb):
                 idx = perm[s:s + mb]
                 out = self._fwd(obs_flat[idx])
                 loss, st = self._ppo_loss(out, old_di[idx], acts[idx], old_logp[idx], adv[idx],
@@ -381,8 +420,11 @@ class LearnerGroup:
         import ray_amd as ray
 
         n = len(self.actors)
-        shards = [batches[i::n] for i in range(n)] if len(batches) >= n else \
-            [_split_b(concat_batches(batches), n, i) for i in range(n)]
+        # split the env (column) axis of the whole batch evenly: shards differ by at most
+        # one column whatever the runner / learner counts (the learners additionally agree
+        # on a common minibatch count, see Learner.update_ppo)
+        whole = concat_batches(batches) if isinstance(batches, list) else batches
+        shards = [_split_b(whole, n, i) for i in range(n)]
         res = ray.get([a.execute.remote(_learner_update, kind, s)
                        for a, s in zip(self.actors, shards)])
         return res[0]

@@ -57,8 +57,10 @@ def setup_tunableop(mode: str, src: str, rank: int):
     if os.path.exists(dst):
         torch.cuda.tunable.read_file(dst)
     if mode == "tune":
-        torch.cuda.tunable.set_max_tuning_duration(30)
-        torch.cuda.tunable.set_max_tuning_iterations(20)
+        # per candidate solution: at most 20 ms / 10 timed runs (hundreds of hipBLASLt
+        # solutions per GEMM shape)
+        torch.cuda.tunable.set_max_tuning_duration(20)
+        torch.cuda.tunable.set_max_tuning_iterations(10)
 
         def _beat(t0=time.time()):  # tuning can run minutes without output
             while torch.cuda.tunable.tuning_is_enabled():
