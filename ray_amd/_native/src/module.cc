@@ -159,6 +159,7 @@ PYBIND11_MODULE(_core, m) {
       .def("num_objects", &ShmStore::num_objects)
       .def("evictions", &ShmStore::evictions)
       .def("release_all_pins_of", &ShmStore::release_all_pins_of)
+      .def("abort", [](ShmStore& s, py::bytes id) { return s.abort(as_str(id)); })
       .def_property_readonly("size", &ShmStore::size);
 
   py::class_<PinnedBuf>(m, "PinnedBuf", py::buffer_protocol())

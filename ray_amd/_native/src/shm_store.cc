@@ -164,11 +164,12 @@ uint32_t ShmStore::heap_alloc(int device, uint64_t n) {
   for (int k = bin_of(n); k < kNumBins; ++k) {
     for (uint32_t r = h->bins[k]; r; r = bl[r - 1].fnext) {
       if (bl[r - 1].size < n) continue;
+      // take the split record BEFORE unlinking the free block: if the record pool is
+      // exhausted the block is handed out whole instead of being orphaned
+      uint32_t r2 = 0;
+      if (bl[r - 1].size - n >= kAlign && hdr_->block_free_head) r2 = rec_alloc();
       bin_remove(h, r);
-      Block& b = bl[r - 1];
-      if (b.size - n >= kAlign) {  // split, remainder stays free
-        uint32_t r2 = rec_alloc();
-        bl = blocks();
+      if (r2) {  // split, remainder stays free
         Block& b1 = bl[r - 1];
         Block& b2 = bl[r2 - 1];
         b2.off = b1.off + n;
@@ -226,13 +227,33 @@ ObjEntry* ShmStore::find(const uint8_t* id) {
 ObjEntry* ShmStore::insert_slot(const uint8_t* id) {
   ObjEntry* t = table();
   const uint64_t mask = hdr_->table_cap - 1;
-  if (hdr_->num_objects * 10 >= hdr_->table_cap * 7)
-    throw std::runtime_error("object table full");
   for (uint64_t i = hash_id(id) & mask, n = 0; n <= mask; i = (i + 1) & mask, ++n) {
     ObjEntry* e = &t[i];
     if (e->state == kEmpty || e->state == kTombstone) return e;
   }
   throw std::runtime_error("object table full");
+}
+
+// Linear probing with backward-shift deletion: after emptying slot i, every later entry
+// of the probe run whose home slot is NOT cyclically in (i, j] moves back into the hole.
+// The table never accumulates tombstones, so a miss stops at the first empty slot
+// whatever the insert/delete history (a tombstone scheme decays to full-table scans).
+void ShmStore::erase_slot(ObjEntry* e) {
+  ObjEntry* t = table();
+  const uint64_t mask = hdr_->table_cap - 1;
+  uint64_t i = (uint64_t)(e - t);
+  memset(&t[i], 0, sizeof(ObjEntry));  // kEmpty
+  uint64_t j = i;
+  for (;;) {
+    j = (j + 1) & mask;
+    if (t[j].state == kEmpty) break;
+    const uint64_t k = hash_id(t[j].id) & mask;
+    const bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
+    if (stays) continue;
+    memcpy(&t[i], &t[j], sizeof(ObjEntry));
+    memset(&t[j], 0, sizeof(ObjEntry));
+    i = j;
+  }
 }
 
 static inline void check_id(const std::string& id) {
@@ -245,6 +266,8 @@ uint64_t ShmStore::create(const std::string& id, uint64_t data_size, uint64_t me
   Guard g(this);
   const uint8_t* k = (const uint8_t*)id.data();
   if (find(k)) throw std::runtime_error("object already exists");
+  // capacity check BEFORE the heap allocation (a full table must not leak the block)
+  if (hdr_->num_objects * 10 >= hdr_->table_cap * 7) throw std::runtime_error("object table full");
   uint32_t r = heap_alloc(device, data_size + meta_size);
   if (!r) return UINT64_MAX;
   ObjEntry* e = insert_slot(k);
@@ -278,12 +301,29 @@ bool ShmStore::seal(const std::string& id) {
   return true;
 }
 
+// NOTE: moves other entries of the probe run (erase_slot): callers must not hold other
+// ObjEntry pointers across a free_entry call — collect ids, then re-find.
 void ShmStore::free_entry(ObjEntry* e) {
   heap_free(e->device, e->block);
   heap(e->device)->n_objects--;
-  memset(e, 0, sizeof(ObjEntry));
-  e->state = kTombstone;
+  erase_slot(e);
   hdr_->num_objects--;
+}
+
+static void pin_add(ObjEntry* e, int pid, int d) {
+  for (int i = 0; i < kPinPids; ++i)
+    if (e->pin_pid[i] == pid && e->pin_cnt[i] > 0) {
+      e->pin_cnt[i] += d;
+      if (e->pin_cnt[i] <= 0) e->pin_pid[i] = e->pin_cnt[i] = 0;
+      return;
+    }
+  if (d > 0)
+    for (int i = 0; i < kPinPids; ++i)
+      if (e->pin_cnt[i] == 0) {
+        e->pin_pid[i] = pid;
+        e->pin_cnt[i] = d;
+        return;
+      }
 }
 
 static void fill(const ObjEntry* e, ObjInfo* o) {
@@ -304,7 +344,10 @@ bool ShmStore::get(const std::string& id, ObjInfo* out, bool pin) {
   Guard g(this);
   ObjEntry* e = find((const uint8_t*)id.data());
   if (!e || e->state != kSealed || e->delete_pending) return false;
-  if (pin) e->ref_count++;
+  if (pin) {
+    e->ref_count++;
+    pin_add(e, (int)getpid(), 1);
+  }
   e->lru_tick = ++hdr_->lru_clock;
   if (out) fill(e, out);
   return true;
@@ -315,7 +358,10 @@ bool ShmStore::release(const std::string& id) {
   Guard g(this);
   ObjEntry* e = find((const uint8_t*)id.data());
   if (!e) return false;
-  if (e->ref_count > 0) e->ref_count--;
+  if (e->ref_count > 0) {
+    e->ref_count--;
+    pin_add(e, (int)getpid(), -1);
+  }
   if (e->ref_count == 0 && e->delete_pending) free_entry(e);
   return true;
 }
@@ -358,21 +404,28 @@ bool ShmStore::set_pinned(const std::string& id, bool pinned) {
 
 std::vector<std::string> ShmStore::evict(uint64_t bytes, int device) {
   Guard g(this);
-  std::vector<ObjEntry*> cands;
+  struct Cand {
+    std::string id;
+    uint64_t tick, size;
+  };
+  std::vector<Cand> cands;
   ObjEntry* t = table();
   for (uint64_t i = 0; i < hdr_->table_cap; ++i) {
     ObjEntry* e = &t[i];
     if (e->state == kSealed && e->device == device && e->ref_count == 0 && !e->pinned)
-      cands.push_back(e);
+      cands.push_back({std::string((const char*)e->id, kIdSize), e->lru_tick,
+                       e->data_size + e->meta_size});
   }
   std::sort(cands.begin(), cands.end(),
-            [](const ObjEntry* a, const ObjEntry* b) { return a->lru_tick < b->lru_tick; });
+            [](const Cand& a, const Cand& b) { return a.tick < b.tick; });
   std::vector<std::string> out;
   uint64_t freed = 0;
-  for (ObjEntry* e : cands) {
+  for (const Cand& c : cands) {
     if (freed >= bytes) break;
-    freed += e->data_size + e->meta_size;
-    out.emplace_back((const char*)e->id, kIdSize);
+    ObjEntry* e = find((const uint8_t*)c.id.data());  // entries move on every free
+    if (!e) continue;
+    freed += c.size;
+    out.push_back(c.id);
     free_entry(e);
     hdr_->stats_evictions++;
   }
@@ -452,14 +505,45 @@ uint64_t ShmStore::evictions() {
   return hdr_->stats_evictions;
 }
 
-void ShmStore::release_all_pins_of(int pid) {
-  // Objects a dead process created but never sealed are aborted.
+uint64_t ShmStore::release_all_pins_of(int pid) {
   Guard g(this);
   ObjEntry* t = table();
+  std::vector<std::string> drop;
+  uint64_t changed = 0;
   for (uint64_t i = 0; i < hdr_->table_cap; ++i) {
     ObjEntry* e = &t[i];
-    if (e->state == kCreated && e->creator_pid == pid) free_entry(e);
+    if (e->state != kCreated && e->state != kSealed) continue;
+    bool touched = false;
+    for (int k = 0; k < kPinPids; ++k)
+      if (e->pin_pid[k] == pid && e->pin_cnt[k] > 0) {
+        e->ref_count -= e->pin_cnt[k];
+        if (e->ref_count < 0) e->ref_count = 0;
+        e->pin_pid[k] = e->pin_cnt[k] = 0;
+        touched = true;
+      }
+    // objects it created but never sealed are aborted; freed pins may complete a remove
+    if ((e->state == kCreated && e->creator_pid == pid) ||
+        (e->ref_count == 0 && e->delete_pending))
+      drop.emplace_back((const char*)e->id, kIdSize);
+    changed += touched;
   }
+  for (const std::string& id : drop) {
+    ObjEntry* e = find((const uint8_t*)id.data());
+    if (e) {
+      free_entry(e);
+      ++changed;
+    }
+  }
+  return changed;
+}
+
+bool ShmStore::abort(const std::string& id) {
+  check_id(id);
+  Guard g(this);
+  ObjEntry* e = find((const uint8_t*)id.data());
+  if (!e || e->state != kCreated) return false;
+  free_entry(e);
+  return true;
 }
 
 }  // namespace ray_amd

@@ -30,7 +30,11 @@ constexpr int kMaxDevices = 16;
 constexpr int kNumBins = 64;
 constexpr uint64_t kAlign = 64;
 
+// kTombstone is never written any more (deletion shifts the probe chain back); it is
+// kept so that probes stay well defined on a segment created by an older build.
 enum ObjState : uint32_t { kEmpty = 0, kCreated = 1, kSealed = 2, kTombstone = 3 };
+
+constexpr int kPinPids = 4;  // reader pins tracked per process (crash cleanup)
 
 struct ObjEntry {
   uint8_t id[kIdSize];
@@ -41,10 +45,15 @@ struct ObjEntry {
   uint64_t offset;  // data offset: from segment start (host) or arena start (device)
   uint64_t data_size;
   uint64_t meta_size;
-  int64_t ref_count;  // reader pins
+  int64_t ref_count;  // all pins (creator + readers)
   uint64_t lru_tick;
   uint32_t delete_pending;
   int32_t creator_pid;
+  // Reader pins by process: the first kPinPids pinning processes are tracked so the
+  // raylet can drop the pins of a process that died holding zero-copy views
+  // (release_all_pins_of). Pins beyond that are counted in ref_count only.
+  int32_t pin_pid[kPinPids];
+  int32_t pin_cnt[kPinPids];
 };
 
 struct Block {
@@ -114,7 +123,11 @@ class ShmStore {
   uint64_t capacity(int device);
   uint64_t num_objects();
   uint64_t evictions();
-  void release_all_pins_of(int pid);
+  // Drops every pin `pid` holds and aborts the objects it created but never sealed;
+  // returns how many entries changed. Called by the raylet when a worker dies.
+  uint64_t release_all_pins_of(int pid);
+  // Abort an unsealed object (creator error path). False if absent or already sealed.
+  bool abort(const std::string& id);
 
  private:
   ObjEntry* table() const;
@@ -127,6 +140,7 @@ class ShmStore {
   void bin_push(HeapHdr* h, uint32_t r);
   void bin_remove(HeapHdr* h, uint32_t r);
   uint32_t heap_alloc(int device, uint64_t n);
+  void erase_slot(ObjEntry* e);  // backward-shift deletion (no tombstones)
   void heap_free(int device, uint32_t r);
   void free_entry(ObjEntry* e);
   void lock();

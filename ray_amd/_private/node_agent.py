@@ -27,6 +27,7 @@ import sys
 import time
 import traceback
 
+from ray_amd._private.object_store import table_capacity
 from ray_amd._native import _core
 
 from . import protocol as P
@@ -47,7 +48,8 @@ class NodeAgent:
         self.store_path = args.store_path
         self.spill_dir = os.path.join(self.session_dir, f"spill_{self.node_hex[:16]}")
         os.makedirs(self.spill_dir, exist_ok=True)
-        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True, 1 << 18)
+        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
+                                    table_capacity(args.object_store_memory))
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.total, self.num_cpus = node_resources(args, self.node_ip, head=False)
@@ -127,6 +129,11 @@ class NodeAgent:
         for oid in oids:
             free_object(self.store, self.spill_dir, oid)
         self.reply(conn, rid, True, None)
+
+    def rpc_release_pins_of(self, conn, rid, pid):
+        """A worker of this node died: drop its object-store pins, abort its unsealed
+        creates (reference: plasma client disconnect -> release all of its objects)."""
+        self.reply(conn, rid, True, self.store.release_all_pins_of(int(pid)))
 
     def rpc_store_stats(self, conn, rid):
         self.reply(conn, rid, True, {"used": self.store.used(-1),

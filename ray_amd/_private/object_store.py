@@ -22,6 +22,12 @@ from . import serialization as ser
 NO_SPACE = (1 << 64) - 1
 
 
+def table_capacity(store_bytes: int) -> int:
+    """Object-table slots for a store of ``store_bytes``: one per 16 KiB (small objects
+    live inline in their owner's memory store, not here), between 4096 and 2^18."""
+    return max(4096, min(1 << 18, int(store_bytes) >> 14))
+
+
 class _MmapBuf:
     """Keeps a spill-file mapping alive while views of it exist."""
 
@@ -74,17 +80,25 @@ class ObjectStore:
 
     def put_serialized(self, oid: bytes, sobj: "ser.SerializedObject", pinned: bool = True):
         off = self._alloc(oid, sobj.total, pinned)
-        mv = self.store.buffer(off, sobj.total)
         try:
-            sobj.write_to(mv)
-        finally:
-            mv.release()
+            mv = self.store.buffer(off, sobj.total)
+            try:
+                sobj.write_to(mv)
+            finally:
+                mv.release()
+        except BaseException:
+            self.store.abort(oid)  # never leave a half-written kCreated entry behind
+            raise
         self.store.seal(oid)
 
     def put_bytes(self, oid: bytes, data, pinned: bool = True):
         n = len(data)
         off = self._alloc(oid, n, pinned)
-        self.store.write(off, data)
+        try:
+            self.store.write(off, data)
+        except BaseException:
+            self.store.abort(oid)
+            raise
         self.store.seal(oid)
 
     # ------------------------------------------------------------------ read

@@ -26,6 +26,7 @@ from ray_amd._native import _core
 
 from . import protocol as P
 from . import serialization as ser
+from .object_store import table_capacity
 
 _dumps = P.dumps
 
@@ -203,7 +204,8 @@ class Raylet:
         self.store_path = args.store_path
         self.spill_dir = os.path.join(self.session_dir, "spill")
         os.makedirs(self.spill_dir, exist_ok=True)
-        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True, 1 << 18)
+        self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
+                                    table_capacity(args.object_store_memory))
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.sched = _core.Scheduler()
@@ -651,9 +653,25 @@ class Raylet:
                 w.proc.wait(timeout=0.5)
             except Exception:
                 pass
+        self._release_store_pins(w)
         if w.actor_id is not None:
             self._on_actor_worker_died(w.actor_id, prev_state)
         self.dirty = True
+
+    def _release_store_pins(self, w):
+        """Zero-copy views / unsealed creates of a dead worker must not pin store memory
+        forever (its process can no longer release them)."""
+        if not w.pid:
+            return
+        try:
+            if w.node == self.node_hex:
+                self.store.release_all_pins_of(int(w.pid))
+            else:
+                rec = self.node_recs.get(w.node)
+                if rec and rec["alive"] and rec.get("conn") is not None:
+                    self.send(rec["conn"], (P.REQ, 0, "release_pins_of", (int(w.pid),)))
+        except Exception:
+            traceback.print_exc()
 
     def _kill_worker(self, w, graceful=False):
         w.state = "dead"

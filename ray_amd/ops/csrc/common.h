@@ -131,6 +131,32 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ s
   }
 }
 
+// fp32 destination: every stage-1 block adds its column sums straight into `out` with
+// float atomics (S*D adds, far below the atomic rate), so the tiny latency-bound second
+// launch disappears. Summation order across blocks is not fixed (last-bit nondeterminism).
+__global__ __launch_bounds__(256) void colsum_atomic(const float* __restrict__ part,
+                                                     float* __restrict__ out, int P, int D) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (c < D) {
+    for (int p = blockIdx.y * 4 + ty; p < P; p += gridDim.y * 4) s += part[(size_t)p * D + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < D) atomicAdd(out + c, red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
+}
+
+}  // namespace
+
+// Runtime tuning knobs (A/B without rebuilding; set through ra_set_knob, defined in
+// layernorm.hip): 0 = LayerNorm-bwd partial rows cap, 1 = column-partial waves target,
+// 2 = fp32 colsum via atomics (1) or two-stage (0).
+extern int ra_knobs[8];
+
+namespace {
+
 // flags: bit0 = bf16 output, bit1 = accumulate into out. scratch: kColsumSplits * D floats.
 enum { kColsumBF16 = 1, kColsumAcc = 2 };
 static inline void colsum_launch(const float* part, float* scratch, void* out, int P, int D,
@@ -138,6 +164,12 @@ static inline void colsum_launch(const float* part, float* scratch, void* out, i
   int S = (P + 15) / 16;
   if (S > kColsumSplits) S = kColsumSplits;
   if (S < 1) S = 1;
+  if (!(flags & kColsumBF16) && ra_knobs[2]) {
+    if (!(flags & kColsumAcc)) hipMemsetAsync(out, 0, (size_t)D * sizeof(float), st);
+    hipLaunchKernelGGL(colsum_atomic, dim3((D + 63) / 64, S), dim3(256), 0, st, part,
+                       (float*)out, P, D);
+    return;
+  }
   hipLaunchKernelGGL(colsum_stage1, dim3((D + 63) / 64, S), dim3(256), 0, st, part, scratch, P, D);
   const dim3 g((D + 255) / 256), b(256);
   switch (flags & 3) {

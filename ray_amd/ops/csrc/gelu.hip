@@ -118,11 +118,13 @@ __global__ __launch_bounds__(256) void bias_residual_kernel(const bf16_t* __rest
   }
 }
 
-// Row partitions of a column reduction: enough (64-thread) blocks to put ~8 waves on
-// every CU whatever F is (F = 768 gives only 2 column blocks), >= 32 rows per partial.
+// Row partitions of a column reduction: enough (64-thread) blocks to put ~ra_knobs[1]
+// waves on the chip (8192 = 32 per CU) whatever F is (F = 768 gives only 2 column
+// blocks), >= 32 rows per partial.
 static inline int parts_for(int N, int F) {
   const int bx = (F / 8 + 63) / 64;
-  int p = (2048 + bx - 1) / bx;
+  const int waves = ra_knobs[1] > 0 ? ra_knobs[1] : 8192;
+  int p = (waves + bx - 1) / bx;
   if (p < 256) p = 256;
   const int pmax = (N + 31) / 32;
   return p < pmax ? p : (pmax > 0 ? pmax : 1);

@@ -229,10 +229,21 @@ RA_EXPORT int ra_residual_layernorm_fwd(const void* h, const void* rbias, const 
   return hipGetLastError();
 }
 
-// Partial-row count for the backward (512 blocks x 4 waves x 2 rows in flight).
+int ra_knobs[8] = {512, 8192, 1, 0, 0, 0, 0, 0};
+
+RA_EXPORT int ra_set_knob(int k, int v) {
+  if (k < 0 || k >= 8) return hipErrorInvalidValue;
+  ra_knobs[k] = v;
+  return hipSuccess;
+}
+
+// Partial-row count for the backward: up to ra_knobs[0] blocks, each wave >= 2 rows.
+// Measured at 65536 x 768 (profiles/r2_perf_bench.log, "norm"): 512 blocks beat 1024 /
+// 2048 / 4096 — more blocks only add partial-slab traffic and LDS-atomic tails.
 RA_EXPORT int ra_layernorm_bwd_parts(int N) {
   int p = (N + 7) / 8;
-  return p < 512 ? p : 512;
+  const int cap = ra_knobs[0] > 0 ? ra_knobs[0] : 2048;
+  return p < cap ? p : cap;
 }
 
 // fp32 workspace (in floats) required by ra_layernorm_bwd (3 partial slabs + scratch).

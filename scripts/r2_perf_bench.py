@@ -89,13 +89,64 @@ def bench_xent(N=8192, V=50257, Vp=50304):
     return {"xent_fused_8192": f"{ms:.4f} ms {gb / ms:.2f} TB/s"}
 
 
+def bench_norm(N=65536, D=768, F=3072):
+    """LayerNorm backward (residual seam, 3 column sums into fp32 sinks) and bias-GELU
+    backward at the GPT-2 shape, under the occupancy / colsum knobs."""
+    dev = "cuda"
+    L = _lib.lib()
+    x = torch.randn(N, D, device=dev).bfloat16()
+    dy = torch.randn(N, D, device=dev).bfloat16()
+    dres = torch.randn(N, D, device=dev).bfloat16()
+    w = torch.ones(D, device=dev).bfloat16()
+    b = torch.zeros(D, device=dev).bfloat16()
+    rb = torch.zeros(D, device=dev).bfloat16()
+    mean = x.float().mean(-1)
+    rstd = torch.rsqrt(x.float().var(-1, unbiased=False) + 1e-5)
+    sinks = [torch.zeros(D, device=dev) for _ in range(3)]
+    for p_, s_ in zip((w, b, rb), sinks):
+        p_._ra_direct_grad = True
+        p_._ra_grad = s_
+    h = torch.randn(N, F, device=dev).bfloat16()
+    dyf = torch.randn(N, F, device=dev).bfloat16()
+    fb = torch.zeros(F, device=dev).bfloat16()
+    fb._ra_direct_grad = True
+    fb._ra_grad = torch.zeros(F, device=dev)
+    out = {}
+    for cap, waves, atom in ((512, 2048, 0), (2048, 2048, 0), (2048, 8192, 0), (2048, 8192, 1),
+                             (1024, 8192, 1), (4096, 16384, 1)):
+        L.ra_set_knob(0, cap)
+        L.ra_set_knob(1, waves)
+        L.ra_set_knob(2, atom)
+        t_ln = timeit(lambda: rf._ln_backward(dy, x, w, b, mean, rstd, dres=dres, rbias=rb))
+        ctx = type("C", (), {})()
+
+        def gelu_bwd():
+            dh = torch.empty_like(h)
+            work = torch.empty(L.ra_colsum_work(N, F), device=dev)
+            L.ra_bias_gelu_bwd(ptr(dyf), ptr(h), ptr(fb), ptr(dh), ptr(fb._ra_grad), ptr(work),
+                               N, F, 3, stream_ptr())
+
+        t_g = timeit(gelu_bwd)
+        t_c = timeit(lambda: rf._colsum_bf16(dyf, out=fb._ra_grad))
+        ln_gb = 4 * N * D * 2 / 1e9
+        g_gb = 3 * N * F * 2 / 1e9
+        out[f"cap{cap}_waves{waves}_atomic{atom}"] = (
+            f"ln_bwd {t_ln:.4f} ms {ln_gb / t_ln:.2f} TB/s | gelu_bwd {t_g:.4f} ms "
+            f"{g_gb / t_g:.2f} TB/s | colsum {t_c:.4f} ms {N * F * 2 / 1e9 / t_c:.2f} TB/s")
+    L.ra_set_knob(0, 2048)
+    L.ra_set_knob(1, 8192)
+    L.ra_set_knob(2, 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--part", default="wgrad,lmhead,xent")
+    ap.add_argument("--part", default="norm,wgrad,lmhead,xent")
     a = ap.parse_args()
     res = {}
     for p in a.part.split(","):
-        res[p] = {"wgrad": bench_wgrad, "lmhead": bench_lmhead, "xent": bench_xent}[p]()
+        res[p] = {"wgrad": bench_wgrad, "lmhead": bench_lmhead, "xent": bench_xent,
+                  "norm": bench_norm}[p]()
         print(json.dumps({p: res[p]}), flush=True)
 
 

@@ -1,0 +1,135 @@
+"""Shared-memory object store: allocator/table invariants, LRU eviction, spilling, crash
+cleanup (modelled on python/ray/tests/test_object_spilling.py, test_plasma_unlimited.py
+and src/ray/object_manager/plasma/test/)."""
+
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+import ray_amd as ray
+from ray_amd._native import _core
+from ray_amd._private.object_store import NO_SPACE, ObjectStore
+
+
+def _oid(i: int) -> bytes:
+    return i.to_bytes(20, "little")
+
+
+@pytest.fixture
+def store(tmp_path):
+    return _core.ShmStore(str(tmp_path / "seg"), 64 << 20, True, 1024)
+
+
+def test_table_churn_keeps_probes_short(store):
+    """Millions of create/remove cycles on a small table used to decay into tombstone
+    scans; with backward-shift deletion a miss still stops at the first empty slot."""
+    live = []
+    for i in range(200_000):
+        k = _oid(i)
+        assert store.create(k, 64, 0, -1, False) != NO_SPACE
+        store.seal(k)
+        live.append(k)
+        if len(live) > 300:  # keep ~30 % load on the 1024-slot table
+            assert store.remove(live.pop(0))
+    assert store.num_objects() == len(live)
+    for k in live:
+        assert store.contains(k)
+    t0 = time.perf_counter()
+    for i in range(10_000):
+        assert not store.contains(_oid(10**9 + i))
+    assert time.perf_counter() - t0 < 2.0  # would be ~10k full-table scans with tombstones
+    for k in live:
+        assert store.remove(k)
+    assert store.num_objects() == 0 and store.used(-1) == 0
+
+
+def test_abort_and_table_full_do_not_leak(store):
+    k = _oid(1)
+    store.create(k, 1 << 20, 0, -1, False)
+    assert store.used(-1) >= 1 << 20
+    assert store.abort(k) and not store.contains(k)
+    assert store.used(-1) == 0
+    # fill the table to its 70 % load limit with tiny objects; the failing create must not
+    # leave its heap block behind
+    n = 0
+    with pytest.raises(RuntimeError):
+        while True:
+            store.create(_oid(100 + n), 64, 0, -1, False)
+            store.seal(_oid(100 + n))
+            n += 1
+    used = store.used(-1)
+    assert used == n * 64
+
+
+def test_pins_of_dead_process_are_released(tmp_path):
+    """A reader that dies holding a zero-copy pin, or between create and seal, must not
+    keep store memory forever: the raylet calls release_all_pins_of(pid)."""
+    path = str(tmp_path / "seg2")
+    st = _core.ShmStore(path, 32 << 20, True, 1024)
+    k = _oid(7)
+    st.create(k, 4096, 0, -1, False)
+    st.seal(k)
+    code = (
+        "from ray_amd._native import _core\n"
+        f"s = _core.ShmStore({path!r}, 0, False, 0)\n"
+        f"b = s.get_buffer({k!r}, True)\n"             # pin, then die holding it
+        f"s.create({_oid(8)!r}, 4096, 0, -1, False)\n"  # unsealed create, then die
+        "import os; os._exit(0)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-c", code], cwd=root)
+    assert p.wait(timeout=60) == 0
+    assert st.state(_oid(8)) == 1  # kCreated, orphaned by the dead creator
+    st.remove(k)  # pinned by the dead reader: only marked delete-pending
+    assert st.used(-1) > 0
+    assert st.release_all_pins_of(p.pid) == 3  # 1 pin dropped + 2 entries freed
+    assert st.used(-1) == 0 and st.num_objects() == 0
+
+
+def test_store_evicts_lru_unpinned_and_spills_primary(tmp_path):
+    spill = str(tmp_path / "spill")
+    os_ = ObjectStore(str(tmp_path / "seg3"), spill, create=True, size=24 << 20,
+                      table_cap=1024)
+    blob = np.random.default_rng(0).integers(0, 255, 4 << 20, dtype=np.uint8).tobytes()
+    # secondary (unpinned) copies are evicted first, LRU order
+    for i in range(3):
+        os_.put_bytes(_oid(i), blob, pinned=False)
+    os_.get_buffer(_oid(0)).release()  # touch 0: 1 is now least recent
+    for i in range(10, 13):
+        os_.put_bytes(_oid(i), blob, pinned=True)  # primaries
+    assert os_.stats()["evictions"] >= 1
+    assert not os_.store.contains(_oid(1))
+    # keep putting primaries: pinned ones are spilled to disk, still readable zero-copy
+    for i in range(20, 28):
+        os_.put_bytes(_oid(i), blob, pinned=True)
+    assert os_.stats()["spilled_bytes"] > 0
+    spilled = [i for i in range(10, 28) if not os_.store.contains(_oid(i)) and
+               os.path.exists(os.path.join(spill, _oid(i).hex()))]
+    assert spilled
+    mv = os_.get_buffer(_oid(spilled[0]))
+    assert bytes(mv[:64]) == blob[:64] and len(mv) == len(blob)
+    os_.delete(_oid(spilled[0]))
+    assert not os.path.exists(os.path.join(spill, _oid(spilled[0]).hex()))
+
+
+def test_spilled_objects_roundtrip_through_runtime(tmp_path):
+    """Object spilling end to end: a driver that puts 3x the store size keeps every
+    ObjectRef readable (reference: test_object_spilling.py::test_spilling_not_done)."""
+    ray.init(num_cpus=2, object_store_memory=48 << 20)
+    try:
+        arrs = [np.full(6 << 20, i, dtype=np.uint8) for i in range(24)]  # 144 MB total
+        refs = [ray.put(a) for a in arrs]
+        for i, r in enumerate(refs):
+            v = ray.get(r)
+            assert v.shape == (6 << 20,) and int(v[0]) == i and int(v[-1]) == i
+
+        @ray.remote
+        def total(x):
+            return int(x[:16].sum())
+
+        assert ray.get([total.remote(r) for r in refs[:4]]) == [16 * i for i in range(4)]
+    finally:
+        ray.shutdown()
