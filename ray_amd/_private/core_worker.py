@@ -31,6 +31,9 @@ import traceback
 import cloudpickle
 
 from ray_amd._native import _core
+from ray_amd.exceptions import (ObjectReconstructionFailedError,
+                                ObjectReconstructionFailedLineageEvictedError,
+                                ObjectReconstructionFailedMaxAttemptsExceededError)
 from ray_amd.exceptions import (GetTimeoutError, ObjectLostError, OwnerDiedError,
                                 RayActorError, RayTaskError, TaskCancelledError,
                                 WorkerCrashedError, ActorDiedError)
@@ -50,7 +53,7 @@ _loads = P.loads
 
 class _Owned:
     __slots__ = ("ready", "inline", "in_store", "callbacks", "borrowers", "contained",
-                 "release_when_ready", "task_id", "size", "node")
+                 "release_when_ready", "task_id", "size", "node", "recon")
 
     def __init__(self, task_id=None):
         self.ready = False
@@ -63,6 +66,19 @@ class _Owned:
         self.task_id = task_id
         self.size = 0
         self.node = None
+        self.recon = 0  # times this object was reconstructed from lineage
+
+
+# Lineage (creating-task specs of stored task returns) kept per owner; the oldest specs
+# are dropped beyond this many (their objects then fail with LineageEvicted if lost).
+LINEAGE_MAX = 20000
+
+
+class _CopyLost(Exception):
+    """Internal: the stored copy of a ready object could not be read."""
+
+    def __init__(self, node):
+        self.node = node
 
 
 class _Remote:
@@ -163,6 +179,10 @@ class CoreWorker:
         self.leases: dict = collections.defaultdict(list)
         self.pending_leases: dict = collections.defaultdict(int)
         self.task_specs: dict[bytes, dict] = {}  # tid -> spec (pending/running)
+        # tid -> spec of FINISHED normal tasks whose stored returns are still owned: the
+        # lineage re-executed when a primary copy is lost (object_recovery_manager.cc)
+        self.lineage: "collections.OrderedDict[bytes, dict]" = collections.OrderedDict()
+        self.lineage_evicted: set = set()
         self.task_lease: dict[bytes, _Lease] = {}
         self.actors: dict[bytes, _ActorConn] = {}
         self.actor_handle_counts: collections.Counter = collections.Counter()
@@ -448,6 +468,11 @@ class CoreWorker:
             contained = o.contained
             in_store = o.in_store
             node = o.node
+            spec = self.lineage.get(o.task_id) if o.task_id is not None else None
+            if spec is not None and not any(
+                    object_id_for_return(o.task_id, i + 1) in self.owned
+                    for i in range(max(spec["nret"], 0))):
+                del self.lineage[o.task_id]  # releases the args it pinned
         if in_store:
             self._delete_stored(oid, node)
         del contained
@@ -675,7 +700,117 @@ class CoreWorker:
         respond()
 
     def _value_of(self, oid: bytes, anchor: str | None):
-        """Deserialize a READY object. Raises the stored error for error objects."""
+        """Deserialize a READY object. Raises the stored error for error objects. A lost
+        stored copy is recovered by re-executing its creating task (lineage)."""
+        for _ in range(8):
+            try:
+                return self._value_of_once(oid, anchor)
+            except _CopyLost as lost:
+                self._recover(oid, lost.node)
+        raise ObjectReconstructionFailedError(oid.hex(), "object kept getting lost")
+
+    def _recover(self, oid, failed_node):
+        """Block until a lost object is available again (owner: re-execute lineage;
+        borrower: ask the owner to). Raises the reconstruction error if it cannot."""
+        with self.lock:
+            owned = oid in self.owned
+            e = self.refs.get(oid)
+            owner = e[1] if e else None
+        if owned:
+            err = self._reconstruct(oid, failed_node)
+            if err is not None:
+                raise err
+            self.wait_refs([oid], 1, None)
+            return
+        if owner is None or owner == self.addr:
+            raise ObjectLostError(oid.hex())
+        try:
+            ok, err = self.call(owner, "recover_object", oid, failed_node, timeout=None)
+        except Exception:
+            raise OwnerDiedError(oid.hex()) from None
+        if not ok:
+            raise err
+        with self.lock:
+            self.remote.pop(oid, None)  # stale location: ask the owner again
+        self.wait_refs([oid], 1, None)
+
+    def _reconstruct(self, oid, failed_node=None):
+        """Owner side: resubmit the task that created `oid`. Returns None when the object
+        is (or will become) available, else the error to raise."""
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is None:
+                return ObjectLostError(oid.hex())
+            if not o.ready:
+                return None  # a reconstruction is already running
+            if o.inline is not None or (o.node or None) != (failed_node or None):
+                return None  # already recovered (another caller saw the loss first)
+            tid = o.task_id
+            if tid is None:  # ray.put objects have no lineage (reference semantics)
+                return ObjectLostError(oid.hex())
+            spec = self.lineage.get(tid)
+            if spec is None:
+                if tid in self.lineage_evicted:
+                    return ObjectReconstructionFailedLineageEvictedError(
+                        oid.hex(), "the lineage of the creating task was evicted")
+                return ObjectReconstructionFailedError(oid.hex(), "no lineage for the task")
+            if spec["retries"] == 0:
+                return ObjectReconstructionFailedMaxAttemptsExceededError(
+                    oid.hex(), "the creating task's max_retries is exhausted")
+            if spec["retries"] > 0:
+                spec["retries"] -= 1
+            spec["attempt"] += 1
+            del self.lineage[tid]
+            self.task_specs[tid] = spec
+            for i in range(spec["nret"]):
+                r = self.owned.get(object_id_for_return(tid, i + 1))
+                if r is not None:
+                    r.ready = False
+                    r.inline = None
+                    r.in_store = False
+                    r.node = None
+                    r.recon += 1
+            args = [a for a, owner, inline in spec["args"][1]
+                    if owner == self.addr and inline is None]
+        # lost arguments are re-created first; dependency resolution waits for them
+        for a in args:
+            with self.lock:
+                ao = self.owned.get(a)
+                check = ao is not None and ao.ready and ao.in_store
+                anode = ao.node if ao is not None else None
+            if check and not self._copy_available(a, anode):
+                err = self._reconstruct(a, anode)
+                if err is not None:
+                    self._fail_task(spec, err)
+                    return None
+        self.task_events.append((tid, spec.get("name"), time.time(), None, None, None,
+                                 "PENDING_ARGS_AVAIL", P.NORMAL_TASK, self.job_id,
+                                 spec["attempt"], None))
+        self._resolve_and_schedule(spec)
+        return None
+
+    def _copy_available(self, oid, node) -> bool:
+        """Non-blocking check (runs on the dispatcher too): only a local copy can be
+        verified; an argument on another node is assumed present — if it is not, the
+        re-executed task's worker reports it through recover_object, recursively."""
+        if node is None or node == self.node_hex:
+            return self.store is not None and self.store.contains(oid)
+        return True
+
+    def _rpc_recover_object(self, conn, rid, oid, failed_node):
+        """A borrower could not fetch `oid`: reconstruct it, reply once it is ready."""
+        err = self._reconstruct(oid, failed_node)
+        if err is not None:
+            self._reply(conn, rid, True, (False, err))
+            return
+
+        def done(_oid):
+            self._reply(conn, rid, True, (True, None))
+
+        if self._on_ready(oid, done):
+            done(oid)
+
+    def _value_of_once(self, oid: bytes, anchor: str | None):
         with self.lock:
             o = self.owned.get(oid)
             if o is not None:
@@ -698,7 +833,7 @@ class CoreWorker:
             if buf is None and node is not None and node != self.node_hex:
                 buf = self._fetch_remote(oid, node)
             if buf is None:
-                raise ObjectLostError(oid.hex())
+                raise _CopyLost(node)
         kind, value = ser.deserialize(buf, ser.DeserializeContext(anchor=owner))
         if kind == ser.KIND_ERROR:
             if isinstance(value, RayTaskError):
@@ -1219,6 +1354,7 @@ class CoreWorker:
                 self._wake_stream(tid)
             return
         node = extra.get("node")
+        stored = False
         for oid, kind, payload, contained in returns:
             pins = None
             if contained:
@@ -1226,7 +1362,21 @@ class CoreWorker:
             if kind == P.RET_INLINE:
                 self._mark_ready(oid, inline=payload, contained=pins, size=len(payload))
             else:
+                stored = True
                 self._mark_ready(oid, in_store=True, contained=pins, size=payload, node=node)
+        if stored and spec["type"] == P.NORMAL_TASK and not spec.get("dynamic"):
+            # keep the spec (and the arg refs it holds) as lineage while its stored
+            # returns are referenced; inline returns can never be lost
+            with self.lock:
+                if any(object_id_for_return(tid, i + 1) in self.owned
+                       for i in range(spec["nret"])):
+                    self.lineage[tid] = spec
+                    self.lineage.move_to_end(tid)
+                    while len(self.lineage) > LINEAGE_MAX:
+                        old_tid, old = self.lineage.popitem(last=False)
+                        old.pop("_holders", None)
+                        self.lineage_evicted.add(old_tid)
+            return
         spec.pop("_holders", None)
 
     def _fail_task(self, spec, exc):

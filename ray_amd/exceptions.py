@@ -140,6 +140,32 @@ class ReferenceCountingAssertionError(ObjectLostError):
     pass
 
 
+class ObjectReconstructionFailedError(ObjectLostError):
+    """The object was lost and re-executing the task that created it failed
+    (reference: python/ray/exceptions.py:581)."""
+
+    def __init__(self, object_ref_hex="", reason="", *a):
+        self.reason = reason
+        super().__init__(object_ref_hex)
+        if reason:
+            self.args = (f"Object {object_ref_hex} is lost and could not be reconstructed: "
+                         f"{reason}",)
+
+    def __str__(self):
+        return self.args[0] if self.args else super().__str__()
+
+    def __reduce__(self):
+        return (type(self), (self.object_ref_hex, self.reason))
+
+
+class ObjectReconstructionFailedMaxAttemptsExceededError(ObjectReconstructionFailedError):
+    """Lineage re-execution would exceed the creating task's max_retries."""
+
+
+class ObjectReconstructionFailedLineageEvictedError(ObjectReconstructionFailedError):
+    """The creating task's spec (lineage) was evicted, so it cannot be re-executed."""
+
+
 class ObjectStoreFullError(RayError):
     pass
 

@@ -1,0 +1,116 @@
+"""Lineage reconstruction of lost objects (modelled on python/ray/tests/
+test_reconstruction.py and test_object_spilling.py: test_basic_reconstruction,
+test_basic_reconstruction_put, reconstruction with max_retries=0, recursive
+reconstruction of lost arguments, loss of a node holding primary copies)."""
+
+import numpy as np
+import pytest
+
+import ray_amd as ray
+from ray_amd._private import worker as W
+from ray_amd.cluster_utils import Cluster
+from ray_amd.exceptions import (ObjectLostError,
+                                ObjectReconstructionFailedMaxAttemptsExceededError)
+
+
+@pytest.fixture
+def local():
+    ray.init(num_cpus=2)
+    yield
+    ray.shutdown()
+
+
+def _lose(ref):
+    """Drop the primary copy of `ref` from the node's object store (what a store crash /
+    lost spill file / dead node does to the owner)."""
+    W.global_worker.core.store.delete(ref._id)
+    assert not W.global_worker.core.store.contains(ref._id)
+
+
+@ray.remote
+def big(n, fill):
+    return np.full(n, fill, dtype=np.float32)
+
+
+@ray.remote
+def add_one(x):
+    return x + 1
+
+
+def test_basic_reconstruction(local):
+    r = big.remote(1_000_000, 3.0)
+    assert float(ray.get(r)[0]) == 3.0
+    _lose(r)
+    v = ray.get(r)  # creating task re-executed transparently
+    assert v.shape == (1_000_000,) and float(v[-1]) == 3.0
+
+
+def test_put_objects_are_not_reconstructable(local):
+    r = ray.put(np.zeros(1_000_000, np.float32))
+    _lose(r)
+    with pytest.raises(ObjectLostError):
+        ray.get(r)
+
+
+def test_max_retries_zero_cannot_reconstruct(local):
+    r = big.options(max_retries=0).remote(1_000_000, 1.0)
+    ray.get(r)
+    _lose(r)
+    with pytest.raises(ObjectReconstructionFailedMaxAttemptsExceededError):
+        ray.get(r)
+
+
+def test_reconstruction_budget_is_max_retries(local):
+    r = big.options(max_retries=2).remote(500_000, 2.0)
+    for _ in range(2):
+        ray.get(r)
+        _lose(r)
+    assert float(ray.get(r)[0]) == 2.0  # 2 reconstructions allowed
+    _lose(r)
+    with pytest.raises(ObjectReconstructionFailedMaxAttemptsExceededError):
+        ray.get(r)
+
+
+def test_recursive_reconstruction_of_lost_arguments(local):
+    a = big.remote(800_000, 5.0)
+    b = add_one.remote(a)
+    assert float(ray.get(b)[0]) == 6.0
+    _lose(a)
+    _lose(b)
+    assert float(ray.get(b)[0]) == 6.0  # b re-runs, which first re-creates a
+    assert float(ray.get(a)[0]) == 5.0
+
+
+def test_borrower_triggers_owner_reconstruction(local):
+    r = big.remote(900_000, 7.0)
+    ray.get(r)
+
+    @ray.remote
+    def total(refs):
+        return float(ray.get(refs[0]).sum())
+
+    _lose(r)
+    # the task borrows r (nested ref), misses the copy and asks the owner to recover it
+    assert ray.get(total.remote([r])) == 7.0 * 900_000
+
+
+def test_node_death_loses_primary_copy_then_reconstructs():
+    c = Cluster(initialize_head=True, head_node_args={"num_cpus": 1})
+    n1 = c.add_node(num_cpus=1, resources={"a": 1})
+    c.add_node(num_cpus=1, resources={"a": 1})
+    ray.init(address=c.address)
+    try:
+        r = big.options(resources={"a": 0.5}).remote(1_000_000, 9.0)
+        ray.wait([r])
+        node = W.global_worker.core.owned[r._id].node
+        victim = [n for n in c.worker_nodes if n.node_id == node]
+        if victim:  # primary on a worker node: kill it
+            c.remove_node(victim[0])
+        else:
+            _lose(r)
+        v = ray.get(r, timeout=60)
+        assert float(v[0]) == 9.0
+        del n1
+    finally:
+        ray.shutdown()
+        c.shutdown()
