@@ -8,6 +8,7 @@
 #include "io_loop.h"
 #include "scheduler.h"
 #include "shm_store.h"
+#include "memory_monitor.h"
 
 namespace py = pybind11;
 using namespace ray_amd;
@@ -272,4 +273,24 @@ PYBIND11_MODULE(_core, m) {
       .def("commit_bundles", &Scheduler::commit_bundles)
       .def("remove_bundles", &Scheduler::remove_bundles)
       .def("pg_gpu_instances", &Scheduler::pg_gpu_instances);
+
+  py::class_<MemoryMonitor>(m, "MemoryMonitor")
+      .def(py::init<double, int64_t, std::string, std::string>(), py::arg("threshold") = 0.95,
+           py::arg("min_free_bytes") = -1, py::arg("cgroup_root") = "/sys/fs/cgroup",
+           py::arg("proc_root") = "/proc")
+      .def("snapshot",
+           [](const MemoryMonitor& mm) {
+             MemorySnapshot s = mm.snapshot();
+             return py::make_tuple(s.used, s.total, s.source);
+           })
+      .def("over_threshold",
+           [](const MemoryMonitor& mm, uint64_t used, uint64_t total) {
+             MemorySnapshot s;
+             s.used = used;
+             s.total = total;
+             return mm.over_threshold(s);
+           })
+      .def("process_private_bytes", &MemoryMonitor::process_private_bytes,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("threshold", &MemoryMonitor::threshold);
 }

@@ -34,6 +34,7 @@ from ray_amd._native import _core
 from ray_amd.exceptions import (ObjectReconstructionFailedError,
                                 ObjectReconstructionFailedLineageEvictedError,
                                 ObjectReconstructionFailedMaxAttemptsExceededError)
+from ray_amd.exceptions import OutOfMemoryError
 from ray_amd.exceptions import (GetTimeoutError, ObjectLostError, OwnerDiedError,
                                 RayActorError, RayTaskError, TaskCancelledError,
                                 WorkerCrashedError, ActorDiedError)
@@ -109,7 +110,7 @@ class _Lease:
 
 class _ActorConn:
     __slots__ = ("actor_id", "state", "addr", "queue", "inflight", "seq", "subscribed",
-                 "death", "max_task_retries", "num_restarts")
+                 "death", "max_task_retries", "num_restarts", "lost")
 
     def __init__(self, actor_id):
         self.actor_id = actor_id
@@ -122,6 +123,9 @@ class _ActorConn:
         self.death = None
         self.max_task_retries = 0
         self.num_restarts = 0
+        # non-retriable in-flight tasks of a lost connection, failed once the actor's
+        # death cause arrives (e.g. the memory monitor killed it) or after a grace period
+        self.lost = []
 
 
 class _Stream:
@@ -1245,7 +1249,7 @@ class CoreWorker:
         req = {
             "resources": sample["resources"], "strategy": sample.get("strategy"),
             "runtime_env": sample.get("runtime_env"), "owner": self.addr, "job": self.job_id,
-            "name": sample.get("name"),
+            "name": sample.get("name"), "retriable": sample.get("retries", 0) != 0,
         }
 
         def on_lease(ok, value, key=key):
@@ -1414,14 +1418,24 @@ class CoreWorker:
                         for t in lease.inflight:
                             self.task_lease.pop(t, None)
                         lease.inflight.clear()
-        for spec in lost:
-            if spec["retries"] != 0:
-                if spec["retries"] > 0:
-                    spec["retries"] -= 1
-                spec["attempt"] += 1
-                self._schedule(spec)
-            else:
-                self._fail_task(spec, WorkerCrashedError())
+        if not lost:
+            return
+
+        def with_cause(ok, cause, lost=lost):
+            # the raylet tells us whether IT killed the worker (memory monitor)
+            oom = ok and isinstance(cause, str) and cause.startswith("oom:")
+            for spec in lost:
+                if spec["retries"] != 0:
+                    if spec["retries"] > 0:
+                        spec["retries"] -= 1
+                    spec["attempt"] += 1
+                    self._schedule(spec)
+                elif oom:
+                    self._fail_task(spec, OutOfMemoryError(cause[4:]))
+                else:
+                    self._fail_task(spec, WorkerCrashedError())
+
+        self.call_async(self.raylet_addr, "death_cause", (addr,), with_cause)
 
     # ------------------------------------------------------------------ streaming
     def _on_stream_item(self, conn, msg):
@@ -1589,6 +1603,10 @@ class CoreWorker:
                 if ac.state == P.ALIVE and ac.addr == addr:
                     return
                 ac.state, ac.addr = P.ALIVE, addr
+                if ac.lost:  # restarted: tasks that died with the old process fail
+                    lost, ac.lost = ac.lost, []
+                    threading.Thread(target=self._fail_lost, args=(actor_id, lost, None),
+                                     daemon=True).start()
                 ac.num_restarts = num_restarts
                 # resend in-flight (retryable) + queued, in sequence order
                 pending = sorted(list(ac.inflight.values()) + list(ac.queue),
@@ -1601,9 +1619,10 @@ class CoreWorker:
             elif state == P.DEAD:
                 ac.state = P.DEAD
                 ac.death = death
-                to_fail = list(ac.inflight.values()) + list(ac.queue)
+                to_fail = list(ac.inflight.values()) + list(ac.queue) + ac.lost
                 ac.inflight.clear()
                 ac.queue.clear()
+                ac.lost = []
             else:
                 if ac.state == P.ALIVE and state == P.RESTARTING:
                     self._requeue_inflight(ac)
@@ -1634,11 +1653,24 @@ class CoreWorker:
             else:
                 fail.append(s)
         ac.inflight.clear()
-        for s in fail:
-            threading.Thread(target=self._fail_task,
-                             args=(s, RayActorError(ac.actor_id.hex(),
-                                                    "The actor died while running this task.")),
-                             daemon=True).start()
+        if fail:
+            ac.lost.extend(fail)
+
+            def fallback(ac=ac, fail=fail):
+                with self.lock:
+                    left = [x for x in fail if x in ac.lost]
+                    ac.lost = [x for x in ac.lost if x not in left]
+                self._fail_lost(ac.actor_id, left, None)
+
+            t = threading.Timer(5.0, fallback)
+            t.daemon = True
+            t.start()
+
+    def _fail_lost(self, actor_id, specs, death):
+        err = self._actor_error(actor_id, death) if death else \
+            RayActorError(actor_id.hex(), "The actor died while running this task.")
+        for sp in specs:
+            self._fail_task(sp, err)
 
     def _on_actor_conn_lost(self, ac):
         with self.lock:

@@ -34,7 +34,7 @@ _dumps = P.dumps
 class WorkerRec:
     __slots__ = ("wid", "pid", "addr", "conn", "key", "state", "lease", "proc", "token",
                  "actor_id", "job", "gpu_ids", "mode", "idle_since", "namespace", "started",
-                 "node")
+                 "node", "death_cause")
 
     def __init__(self):
         self.wid = None
@@ -58,9 +58,9 @@ class WorkerRec:
 
 class Lease:
     __slots__ = ("lid", "worker", "alloc", "resources", "owner", "strategy", "cpu_released",
-                 "pg", "actor_id")
+                 "pg", "actor_id", "retriable", "granted_at")
 
-    def __init__(self, lid, worker, alloc, resources, owner, strategy):
+    def __init__(self, lid, worker, alloc, resources, owner, strategy, retriable=True):
         self.lid = lid
         self.worker = worker
         self.alloc = alloc
@@ -70,6 +70,31 @@ class Lease:
         self.cpu_released = False
         self.pg = None
         self.actor_id = None
+        self.retriable = retriable
+        self.granted_at = time.monotonic()
+
+
+def select_worker_to_kill(leases, policy: str = "group_by_owner"):
+    """Memory-pressure victim (reference: src/ray/raylet/worker_killing_policy_*.cc).
+
+    group_by_owner: group running leases by owner; prefer retriable groups, then the
+    largest group, then the newest; inside the group kill the NEWEST lease (the work
+    least far along). retriable_fifo: retriable first, then the OLDEST lease.
+    Returns (lease, should_retry) or (None, False)."""
+    if not leases:
+        return None, False
+    if policy == "retriable_fifo":
+        best = sorted(leases, key=lambda l: (0 if l.retriable else 1, l.granted_at))[0]
+        return best, best.retriable
+    groups = {}
+    for l in leases:
+        key = (l.owner, True) if l.retriable else ("__non_retriable__", False)
+        groups.setdefault(key, []).append(l)
+    ordered = sorted(groups.items(), key=lambda kv: (0 if kv[0][1] else 1, -len(kv[1]),
+                                                     -max(x.granted_at for x in kv[1])))
+    (_, retriable), members = ordered[0]
+    victim = max(members, key=lambda x: x.granted_at)
+    return victim, retriable and len(members) > 1
 
 
 class LeaseReq:
@@ -253,6 +278,20 @@ class Raylet:
         self.next_internal = -1
         self.start_time = time.time()
         self.gpu_arenas = {}
+        # memory monitor + worker killing policy (reference: memory_monitor.cc,
+        # worker_killing_policy.cc; config names follow RAY_memory_usage_threshold etc.)
+        env = os.environ
+        self.mem_refresh = float(env.get("RAY_memory_monitor_refresh_ms", "250")) / 1000.0
+        self.mem_monitor = _core.MemoryMonitor(
+            float(env.get("RAY_memory_usage_threshold", "0.95")),
+            int(env.get("RAY_min_memory_free_bytes", "-1")),
+            env.get("RAY_AMD_CGROUP_ROOT", "/sys/fs/cgroup"), "/proc") \
+            if self.mem_refresh > 0 else None
+        self.kill_policy = env.get("RAY_worker_killing_policy", "group_by_owner")
+        self._mem_last = 0.0
+        self._oom_victim = None  # (worker rec, deadline) of the last kill, until it exits
+        self.death_causes: "collections.OrderedDict[str, str]" = collections.OrderedDict()
+        self.oom_kills = 0
 
     # ------------------------------------------------------------------ io helpers
     def send(self, conn, msg):
@@ -553,7 +592,8 @@ class Raylet:
     def _grant(self, lr, w, gpu_ids):
         lid = self.next_lease
         self.next_lease += 1
-        lease = Lease(lid, w, lr.alloc, lr.resources, lr.req.get("owner"), lr.req.get("strategy"))
+        lease = Lease(lid, w, lr.alloc, lr.resources, lr.req.get("owner"), lr.req.get("strategy"),
+                      lr.req.get("retriable", True))
         st = lr.req.get("strategy")
         if isinstance(st, dict) and st.get("type") == "pg":
             lease.pg = st["pg_id"]
@@ -655,6 +695,10 @@ class Raylet:
                 pass
         self._release_store_pins(w)
         if w.actor_id is not None:
+            cause = getattr(w, "death_cause", None)
+            a = self.actors.get(w.actor_id)
+            if a is not None and cause and cause.startswith("oom:"):
+                a._oom_cause = "The actor died because its node ran out of memory. " + cause[4:]
             self._on_actor_worker_died(w.actor_id, prev_state)
         self.dirty = True
 
@@ -719,8 +763,50 @@ class Raylet:
                 lst.clear()
 
     # ------------------------------------------------------------------ periodic
+    def _memory_check(self, now):
+        if self.mem_monitor is None or now - self._mem_last < self.mem_refresh:
+            return
+        self._mem_last = now
+        if self._oom_victim is not None:
+            w, deadline = self._oom_victim
+            if w.state != "dead" and now < deadline:
+                return  # give the last victim time to exit before killing again
+            self._oom_victim = None
+        used, total, src = self.mem_monitor.snapshot()
+        if not self.mem_monitor.over_threshold(used, total):
+            return
+        cands = [l for l in self.leases.values()
+                 if l.worker is not None and l.worker.node == self.node_hex and
+                 l.worker.mode == "worker" and l.worker.state != "dead" and l.worker.pid]
+        lease, retry = select_worker_to_kill(cands, self.kill_policy)
+        if lease is None:
+            return
+        w = lease.worker
+        rss = self.mem_monitor.process_private_bytes(int(w.pid))
+        msg = (f"Task was killed due to the node running low on memory. Memory on the node "
+               f"({src}) was {used / 2**30:.2f}GB / {total / 2**30:.2f}GB "
+               f"({used / max(total, 1):.3f}), which exceeds the memory usage threshold of "
+               f"{self.mem_monitor.threshold}. ray_amd killed this worker (pid={w.pid}, "
+               f"private memory {max(rss, 0) / 2**30:.2f}GB) because it was the most recent "
+               f"{'retriable ' if lease.retriable else ''}lease of the policy "
+               f"'{self.kill_policy}' choice. Set RAY_memory_usage_threshold / "
+               f"RAY_memory_monitor_refresh_ms=0 to tune or disable.")
+        print(f"[ray_amd] memory monitor: {msg}", file=sys.stderr, flush=True)
+        self.death_causes[w.addr] = "oom:" + msg
+        while len(self.death_causes) > 1000:
+            self.death_causes.popitem(last=False)
+        w.death_cause = "oom:" + msg
+        self.oom_kills += 1
+        self._oom_victim = (w, now + 5.0)
+        self._kill_worker(w)
+
+    def rpc_death_cause(self, conn, rid, addr):
+        """Why a worker died, if the raylet killed it (e.g. "oom:<message>")."""
+        self.reply(conn, rid, True, self.death_causes.get(addr))
+
     def tick(self):
         now = time.monotonic()
+        self._memory_check(now)
         for pg in self.pgs.values():
             if pg.state == "PENDING":
                 self._try_place(pg)
@@ -798,7 +884,8 @@ class Raylet:
     def _schedule_actor(self, a):
         req = {"resources": a.spec.get("resources") or {}, "strategy": a.spec.get("strategy"),
                "runtime_env": a.spec.get("runtime_env"), "owner": self.addr,
-               "job": a.spec.get("job"), "name": a.info.get("class_name")}
+               "job": a.spec.get("job"), "name": a.info.get("class_name"),
+               "retriable": a.max_restarts != 0}
 
         def granted(grant, err=None, a=a):
             if grant is None:
@@ -882,7 +969,9 @@ class Raylet:
             self._publish(a)
             self._schedule_actor(a)
         else:
-            self._actor_dead(a, "The actor died unexpectedly (worker process exited)."
+            cause = getattr(a, "_oom_cause", None)
+            self._actor_dead(a, cause if cause else
+                             "The actor died unexpectedly (worker process exited)."
                              if not a.no_restart else "The actor was killed (ray.kill).")
 
     def _actor_dead(self, a, death):
