@@ -187,10 +187,10 @@ class ActorClass:
         from ray_amd._private.ids import random_bytes
 
         cw = W._check_connected()
-        key = self._keys.get(id(cw))
+        key = self._keys.get(cw.worker_id)
         if key is None:
             key = cw.export(self._cls)
-            self._keys[id(cw)] = key
+            self._keys[cw.worker_id] = key
         max_conc = opts.get("max_concurrency")
         if max_conc is None:
             max_conc = 1000 if self._meta.get("__is_async__") else 1

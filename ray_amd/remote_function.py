@@ -48,10 +48,10 @@ class RemoteFunction:
         return FunctionNode(self, args, kwargs, self._default_options)
 
     def _key(self, cw):
-        k = self._keys.get(id(cw))
+        k = self._keys.get(cw.worker_id)
         if k is None:
             k = cw.export(self._function)
-            self._keys[id(cw)] = k
+            self._keys[cw.worker_id] = k
         return k
 
     def _remote(self, args, kwargs, opts):
