@@ -108,22 +108,45 @@ class DataParallelTrainer:
         return shards
 
     def fit(self) -> Result:
+        from ray_amd.tune.callback import CallbackList
+        from ray_amd.tune.logger import default_callbacks
+
         if not ray.is_initialized():
             ray.init()
         rc = self.run_config
         name = rc.name or f"{type(self).__name__}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
         trial_dir = os.path.join(rc.storage_path, name)
         os.makedirs(trial_dir, exist_ok=True)
+        self._save_trainer(trial_dir)
         mgr = _CheckpointManager(rc.checkpoint_config)
         history = []
         failures = 0
         ckpt = self.resume_from_checkpoint
-        ckpt_index = 0
+        ckpt_index = getattr(self, "_restored_ckpt_index", 0)
         error = None
+        # RunConfig.callbacks (+ default JSON/CSV loggers) see the run as one trial, the
+        # same events a Tuner fires (reference: Trainer.fit runs as a Tune trial)
+        trial = _TrainerTrial(name, self.train_loop_config, trial_dir)
+        cbs = CallbackList(default_callbacks(rc.callbacks))
+        cbs.fire("setup", stop=rc.stop, num_samples=1, total_num_samples=1)
+        cbs.fire("on_trial_restore" if ckpt is not None else "on_trial_start", trials=[trial],
+                 trial=trial)
+
+        def on_report(metrics, cpath):
+            cbs.step([trial])
+            trial.last_result = metrics
+            cbs.fire("on_trial_result", trials=[trial], trial=trial, result=metrics)
+            if cpath:
+                cbs.fire("on_trial_save", trials=[trial], trial=trial)
+                cbs.fire("on_checkpoint", trials=[trial], trial=trial,
+                         checkpoint=Checkpoint(cpath))
+                self._save_state(trial_dir, cpath, metrics)
+            cbs.end_step([trial])
+
         while True:
             try:
                 metrics, ckpt_index = self._run_once(trial_dir, name, ckpt, ckpt_index, mgr,
-                                                     history)
+                                                     history, on_report)
                 error = None
                 break
             except TrainingFailedError as e:
@@ -132,21 +155,92 @@ class DataParallelTrainer:
                 maxf = rc.failure_config.max_failures
                 if maxf != -1 and failures > maxf:
                     break
+                cbs.fire("on_trial_recover", trials=[trial], trial=trial)
                 ckpt = mgr.latest or ckpt
         if error is not None:
-            res = Result(metrics=history[-1] if history else {}, checkpoint=mgr.latest,
-                         error=error, path=trial_dir, metrics_history=history,
-                         best_checkpoints=[(c, m) for c, m in mgr.items])
+            trial.status = "ERROR"
+            cbs.fire("on_trial_error", trials=[trial], trial=trial)
+            cbs.fire("on_experiment_end", trials=[trial])
             raise error
-        with open(os.path.join(trial_dir, "result.json"), "w") as f:
-            for m in history:
-                f.write(json.dumps({k: v for k, v in m.items()
-                                    if isinstance(v, (int, float, str, bool))}) + "\n")
+        trial.status = "TERMINATED"
+        cbs.fire("on_trial_complete", trials=[trial], trial=trial)
+        cbs.fire("on_experiment_end", trials=[trial])
         return Result(metrics=history[-1] if history else {}, checkpoint=mgr.latest, error=None,
                       path=trial_dir, metrics_history=history,
                       best_checkpoints=[(c, m) for c, m in mgr.items])
 
-    def _run_once(self, trial_dir, name, ckpt, ckpt_index, mgr, history):
+    # ------------------------------------------------------------------ restore
+    _TRAINER_FILE = "trainer.pkl"
+    _STATE_FILE = "trainer_state.json"
+
+    def _save_trainer(self, trial_dir):
+        """Persist the trainer definition (minus datasets, which are re-supplied on
+        restore) so ``restore(path)`` can rebuild it (reference: base_trainer.py:250)."""
+        import cloudpickle
+
+        d = dict(self.__dict__)
+        d["_dataset_names"] = list((self.datasets or {}).keys())
+        d["datasets"] = {}
+        d.pop("resume_from_checkpoint", None)
+        try:
+            blob = cloudpickle.dumps((type(self), d))
+        except Exception:  # noqa: BLE001 - unpicklable user state: restore needs overrides
+            return
+        tmp = os.path.join(trial_dir, self._TRAINER_FILE + ".tmp")
+        with open(tmp, "wb") as f:
+            f.write(blob)
+        os.replace(tmp, os.path.join(trial_dir, self._TRAINER_FILE))
+
+    def _save_state(self, trial_dir, cpath, metrics):
+        st = {"latest_checkpoint": os.path.basename(cpath),
+              "metrics": {k: v for k, v in metrics.items()
+                          if isinstance(v, (int, float, str, bool))}}
+        tmp = os.path.join(trial_dir, self._STATE_FILE + ".tmp")
+        with open(tmp, "w") as f:
+            json.dump(st, f)
+        os.replace(tmp, os.path.join(trial_dir, self._STATE_FILE))
+
+    @classmethod
+    def can_restore(cls, path) -> bool:
+        return os.path.exists(os.path.join(path, cls._TRAINER_FILE))
+
+    @classmethod
+    def restore(cls, path, datasets: dict | None = None, train_loop_per_worker=None,
+                train_loop_config: dict | None = None, **overrides):
+        """Rebuild an interrupted trainer from its run directory and resume from the latest
+        persisted checkpoint. Datasets must be passed again (they are not pickled)."""
+        import cloudpickle
+
+        path = os.path.abspath(os.path.expanduser(path))
+        with open(os.path.join(path, cls._TRAINER_FILE), "rb") as f:
+            tcls, d = cloudpickle.loads(f.read())
+        obj = tcls.__new__(tcls)
+        obj.__dict__.update(d)
+        missing = [n for n in d.get("_dataset_names", []) if n not in (datasets or {})]
+        if missing:
+            raise ValueError(f"restore() needs the datasets the run was started with: "
+                             f"{missing}")
+        obj.datasets = datasets or {}
+        if train_loop_per_worker is not None:
+            obj.train_loop_per_worker = train_loop_per_worker
+        if train_loop_config is not None:
+            obj.train_loop_config = train_loop_config
+        for k, v in overrides.items():
+            setattr(obj, k, v)
+        import copy
+
+        rc = copy.copy(obj.run_config)
+        rc.name = os.path.basename(path)
+        rc.storage_path = os.path.dirname(path)
+        obj.run_config = rc
+        ckpts = sorted(x for x in os.listdir(path) if x.startswith("checkpoint_") and
+                       os.path.isdir(os.path.join(path, x)) and os.listdir(os.path.join(path, x)))
+        obj.resume_from_checkpoint = Checkpoint(os.path.join(path, ckpts[-1])) if ckpts \
+            else None
+        obj._restored_ckpt_index = (int(ckpts[-1].split("_")[-1]) + 1) if ckpts else 0
+        return obj
+
+    def _run_once(self, trial_dir, name, ckpt, ckpt_index, mgr, history, on_report=None):
         sc = self.scaling_config
         wg = WorkerGroup(sc.num_workers, sc._resources_per_worker_not_none,
                          sc.placement_strategy)
@@ -202,6 +296,8 @@ class DataParallelTrainer:
                         c = Checkpoint(cpath)
                         mgr.register(c, metrics)
                         ckpt_index = int(os.path.basename(cpath).split("_")[-1]) + 1
+                    if on_report is not None:
+                        on_report(metrics, cpath)
                     stop = self.run_config.stop
                     if stop and _should_stop(stop, metrics):
                         break
@@ -213,9 +309,21 @@ class DataParallelTrainer:
                 pass
             wg.shutdown()
 
-    @classmethod
-    def restore(cls, path, **kwargs):
-        return cls(**kwargs)
+
+
+class _TrainerTrial:
+    """The single pseudo-trial a Trainer run presents to Tune callbacks."""
+
+    def __init__(self, name, config, path):
+        self.trial_id = name
+        self.config = config or {}
+        self.local_path = path
+        self.path = path
+        self.status = "RUNNING"
+        self.last_result = {}
+
+    def __repr__(self):
+        return f"TrainerTrial({self.trial_id}, {self.status})"
 
 
 def _should_stop(stop, metrics):

@@ -292,6 +292,13 @@ class _Controller:
         self.exhausted = False
         self.actor_cls = ray.remote(_TrialActor)
         self.start = time.time()
+        from ray_amd.tune.callback import CallbackList
+        from ray_amd.tune.logger import default_callbacks
+
+        # RunConfig.callbacks + the default JSON / CSV loggers (result.json, progress.csv)
+        self.cb = CallbackList(default_callbacks(rc.callbacks))
+        self.cb.fire("setup", stop=rc.stop, num_samples=tc.num_samples,
+                     total_num_samples=tc.num_samples)
 
     @staticmethod
     def _make_stopper(stop):
@@ -352,6 +359,8 @@ class _Controller:
         t.actor.start.remote()  # actor calls are ordered: next_result runs after start
         t.status = "RUNNING"
         t.pending_ref = t.actor.next_result.remote()
+        self.cb.fire("on_trial_restore" if checkpoint else "on_trial_start",
+                     trials=self.trials, trial=t)
 
     def _stop_trial(self, t, status="TERMINATED", error=None):
         t.status = status
@@ -366,17 +375,21 @@ class _Controller:
         t.pending_ref = None
         if status == "ERROR":
             self.scheduler.on_trial_error(self, t)
+            self.cb.fire("on_trial_error", trials=self.trials, trial=t)
         else:
             self.scheduler.on_trial_complete(self, t, t.last_result)
+            if status == "TERMINATED":
+                self.cb.fire("on_trial_complete", trials=self.trials, trial=t)
         self.searcher.on_trial_complete(t.trial_id, t.last_result, error is not None)
 
-    def _log(self, t, result):
-        os.makedirs(t.local_path, exist_ok=True)
-        with open(os.path.join(t.local_path, "result.json"), "a") as f:
-            f.write(json.dumps({k: v for k, v in result.items()
-                                if isinstance(v, (int, float, str, bool, type(None)))}) + "\n")
-        with open(os.path.join(t.local_path, "params.json"), "w") as f:
-            json.dump(t.config, f, default=str)
+    def _log(self, t, result, checkpoint=None):
+        """Result / checkpoint events to the callbacks (the JSON and CSV loggers write
+        result.json, params.json and progress.csv)."""
+        self.cb.fire("on_trial_result", trials=self.trials, trial=t, result=result)
+        if checkpoint:
+            ck = Checkpoint(checkpoint)
+            self.cb.fire("on_trial_save", trials=self.trials, trial=t)
+            self.cb.fire("on_checkpoint", trials=self.trials, trial=t, checkpoint=ck)
 
     def _save_state(self):
         st = {"trials": [(t.trial_id, t.config, t.status, t.last_checkpoint, t.results)
@@ -398,6 +411,7 @@ class _Controller:
                 running.append(t)
             if not running:
                 break
+            self.cb.step(self.trials)
             refs = {t.pending_ref: t for t in running}
             ready, _ = ray.wait(list(refs), num_returns=1, timeout=1.0)
             if budget and time.time() - self.start > budget:
@@ -428,7 +442,7 @@ class _Controller:
                     t.last_checkpoint = b
                 t.results.append(result)
                 t.last_result = result
-                self._log(t, result)
+                self._log(t, result, b)
                 self.searcher.on_trial_result(t.trial_id, result)
                 decision = self.scheduler.on_trial_result(self, t, result)
                 if self.stopper is not None and self.stopper(t.trial_id, result):
@@ -449,8 +463,10 @@ class _Controller:
                     t._asha_rungs = set()
                     continue
                 t.pending_ref = t.actor.next_result.remote()
+            self.cb.end_step(self.trials)
             self._save_state()
         self._save_state()
+        self.cb.fire("on_experiment_end", trials=self.trials)
         return self.trials
 
 
