@@ -188,6 +188,11 @@ def node_resources(args, node_ip, head):
              f"node:{node_ip}": 1.0}
     if ngpu:
         total["GPU"] = float(ngpu)
+        from ray_amd.util.accelerators import detect_accelerator_type
+
+        acc = os.environ.get("RAY_AMD_ACCELERATOR_TYPE") or detect_accelerator_type()
+        if acc:  # reference: accelerator_type:<type> node resource (amd_gpu.py)
+            total[f"accelerator_type:{acc}"] = 1.0
     if head:
         total["node:__internal_head__"] = 1.0
     total.update({k: float(v) for k, v in res.items()})
@@ -237,6 +242,9 @@ class Raylet:
         total, ncpu = node_resources(args, self.node_ip, head=True)
         self.labels = json.loads(args.labels or "{}")
         self.labels.setdefault("ray.io/node_id", self.node_id.hex())
+        for k in total:
+            if k.startswith("accelerator_type:"):  # label twin of the resource
+                self.labels.setdefault("ray.io/accelerator-type", k.split(":", 1)[1])
         self.sched.add_node(self.node_id.hex(), total, self.labels)
         self.total = total
         self.num_cpus = ncpu
@@ -1364,9 +1372,11 @@ class Raylet:
         env = dict(os.environ)
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
+        sock = os.path.join(self.session_dir, "sockets", f"arena_{device}.sock")
         proc = subprocess.Popen([self.python, "-m", "ray_amd._private.gpu_object_store",
                                  "--device", str(device), "--size", str(size), "--out", out,
-                                 "--store", self.store_path], env=env, close_fds=True)
+                                 "--store", self.store_path, "--sock", sock], env=env,
+                                close_fds=True)
         t0 = time.time()
         while not os.path.exists(out):
             if proc.poll() is not None or time.time() - t0 > 120:

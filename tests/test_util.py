@@ -198,3 +198,4 @@ def test_internal_kv(cluster):
     assert kv._internal_kv_list(b"k") == [b"k"]
     kv._internal_kv_del(b"k")
     assert kv._internal_kv_get(b"k") is None
+
