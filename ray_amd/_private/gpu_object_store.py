@@ -97,8 +97,37 @@ def _arena_info(phys: int) -> dict:
     return _cw().call_raylet("gpu_arena", phys, _DEFAULT_ARENA)
 
 
+_session = [None]
+
+
+def _check_session():
+    """Arena mappings and holder connections belong to ONE ray_amd session: a new
+    session (new raylet, new holders, new arenas) must not reuse stale IPC mappings.
+    Called with _lock held."""
+    cw = _cw()
+    key = getattr(cw, "worker_id", None)
+    if _session[0] == key:
+        return
+    from ray_amd.ops import _lib
+
+    for base, _, _ in _arenas.values():
+        try:
+            _lib.lib().ra_arena_close(base)
+        except Exception:  # noqa: BLE001
+            pass
+    _arenas.clear()
+    for c in _holder_conns.values():
+        try:
+            c.close()
+        except Exception:  # noqa: BLE001
+            pass
+    _holder_conns.clear()
+    _session[0] = key
+
+
 def _arena(phys: int):
     with _lock:
+        _check_session()
         a = _arenas.get(phys)
         if a is not None:
             return a
@@ -463,6 +492,7 @@ def _holder_call(phys: int, req, timeout=120.0):
     if not addr:
         raise RuntimeError(f"arena holder of GPU {phys} has no RPC socket")
     with _lock:
+        _check_session()
         c = _holder_conns.get(phys)
         if c is None:
             c = _holder_conns[phys] = Client(addr, family="AF_UNIX")
