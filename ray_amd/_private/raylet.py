@@ -1178,6 +1178,41 @@ class Raylet:
                 "node_id": nh, "is_head_node": rec.get("is_head", False)})
         self.reply(conn, rid, True, out)
 
+    def rpc_resource_load(self, conn, rid):
+        """Autoscaler input (reference: GcsResourceManager load report / autoscaler
+        LoadMetrics): resource shapes waiting for a node, pending placement-group
+        bundles, and per-node usage with an idle-since timestamp."""
+        demand = []
+        for lr in self.pending:
+            if lr.alloc is None:
+                r = {k: float(v) for k, v in (lr.req.get("resources") or {}).items() if v}
+                st = lr.req.get("strategy")
+                if not (isinstance(st, dict) and st.get("type") == "pg"):
+                    demand.append(r)
+        pg_demand = [[{k: float(v) for k, v in b.items()} for b in pg.bundles]
+                     for pg in self.pgs.values() if pg.state == "PENDING"]
+        now = time.time()
+        busy = collections.Counter(l.worker.node for l in self.leases.values()
+                                   if l.worker is not None)
+        nodes = []
+        for nh, rec in self.node_recs.items():
+            if not rec["alive"]:
+                continue
+            tot = {k: v for k, v in self.sched.total(nh).items() if "_group_" not in k}
+            av = {k: v for k, v in self.sched.available(nh).items() if "_group_" not in k}
+            idle = busy.get(nh, 0) == 0 and all(av.get(k, 0) >= v - 1e-9 for k, v in tot.items())
+            if idle:
+                rec.setdefault("idle_since", now)
+            else:
+                rec.pop("idle_since", None)
+            nodes.append({"node_id": nh, "total": tot, "available": av,
+                          "is_head": rec.get("is_head", False), "labels": rec["labels"],
+                          "idle_s": now - rec["idle_since"] if idle else 0.0,
+                          "num_leases": busy.get(nh, 0)})
+        req = self.kv.get(("__autoscaler", b"resource_request"))
+        self.reply(conn, rid, True, {"demand": demand, "pg_demand": pg_demand, "nodes": nodes,
+                                     "requested": req})
+
     def rpc_fetch_object(self, conn, rid, oid):
         """Serve a copy of an object held in this node's store (object_manager Pull)."""
         self.reply(conn, rid, True, read_object_bytes(self.store, self.spill_dir, oid))

@@ -193,3 +193,66 @@ class Cluster:
         if self.head_node is not None:
             self.head_node.kill(True)
             self.head_node = None
+
+
+class AutoscalingCluster:
+    """A local cluster whose worker nodes are launched and removed by the autoscaler
+    (reference: python/ray/cluster_utils.py AutoscalingCluster over the
+    fake_multi_node provider).
+
+        cluster = AutoscalingCluster(head_resources={"CPU": 0},
+                                     worker_node_types={"cpu2": {"resources": {"CPU": 2},
+                                                                 "max_workers": 2}},
+                                     idle_timeout_minutes=0.05)
+        cluster.start()
+        ray.init(address=cluster.address)
+    """
+
+    def __init__(self, head_resources: dict, worker_node_types: dict,
+                 idle_timeout_minutes: float = 1.0, max_workers: int = 20,
+                 upscaling_speed: float = 1.0, update_interval_s: float = 0.5, **_):
+        from ray_amd.autoscaler.autoscaler import AutoscalerConfig, NodeTypeConfig
+
+        self.head_resources = dict(head_resources)
+        types = {}
+        for name, spec in worker_node_types.items():
+            types[name] = NodeTypeConfig(resources=dict(spec["resources"]),
+                                         min_workers=spec.get("min_workers", 0),
+                                         max_workers=spec.get("max_workers", 10),
+                                         node_config=dict(spec.get("node_config", {})))
+        self.config = AutoscalerConfig(node_types=types, max_workers=max_workers,
+                                       idle_timeout_s=idle_timeout_minutes * 60.0,
+                                       upscaling_speed=upscaling_speed,
+                                       update_interval_s=update_interval_s)
+        self.cluster = None
+        self.monitor = None
+        self.autoscaler = None
+
+    @property
+    def address(self):
+        return self.cluster.address if self.cluster else None
+
+    def start(self, **_):
+        from ray_amd.autoscaler.autoscaler import Monitor, StandardAutoscaler
+        from ray_amd.autoscaler.node_provider import FakeMultiNodeProvider
+
+        res = dict(self.head_resources)
+        self.cluster = Cluster(initialize_head=True, head_node_args={
+            "num_cpus": int(res.pop("CPU", 0)), "num_gpus": int(res.pop("GPU", 0)),
+            "resources": res})
+        provider = FakeMultiNodeProvider(self.cluster)
+
+        def load():
+            if not ray_amd.is_initialized():
+                return {"demand": [], "pg_demand": [], "nodes": [], "requested": None}
+            return _W.global_worker.core.call_raylet("resource_load", timeout=30)
+
+        self.autoscaler = StandardAutoscaler(self.config, provider, load_fn=load)
+        self.monitor = Monitor(self.autoscaler).start()
+        return self
+
+    def shutdown(self):
+        if self.monitor is not None:
+            self.monitor.stop()
+        if self.cluster is not None:
+            self.cluster.shutdown()
