@@ -35,6 +35,8 @@
 // Softmax statistics are kept in the log2 domain (exp2 with scale·log2e folded).
 #include "common.h"
 
+#include <type_traits>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -190,11 +192,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     tile_store(x.k, d);
     tile_store(x.v, d + TILE_ELEMS);
   };
-  auto compute = [&](int t) __attribute__((always_inline)) {
+  auto body = [&](int t, auto diag_c) __attribute__((always_inline)) {
+    constexpr bool diag = decltype(diag_c)::value;
     const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
     const bf16_t* Vs = Ks + TILE_ELEMS;
     const int kv0 = t * 64;
-    if (kv0 <= wave_qmax) {
+    {
       f32x16 st[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
         for (int kk = 0; kk < 4; ++kk)
           st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st[kt]);
       }
-      if (kv0 + 63 > q0 + 32 * w) {  // diagonal tile: mask keys > query
+      if (diag) {  // diagonal tile: mask keys > query
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -241,6 +244,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(tr_frag(Vs, lo, 32 * kt + 16 * s, dt), pf, o[dt]);
         }
+    }
+  };
+  auto compute = [&](int t) __attribute__((always_inline)) {
+    const int kv0 = t * 64;
+    if (kv0 <= wave_qmax) {
+      if (kv0 + 63 > q0 + 32 * w) body(t, std::true_type{});
+      else body(t, std::false_type{});
     }
   };
   // 2-deep register prefetch: tile t+2's loads are in flight during tiles t and t+1
@@ -346,15 +356,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     tile_store(x.d, d + TILE_ELEMS);
     if (threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = x.rc;
   };
-  auto compute = [&](int t) __attribute__((always_inline)) {
+  // DIAG is a template-like constant: the causal mask costs 3 VALU per score element
+  // (compare, select, index add), so only the diagonal tiles instantiate it — the
+  // compiler does not split a runtime-predicated mask out of the unrolled loop itself.
+  auto body = [&](int t, auto diag_c) __attribute__((always_inline)) {
+    constexpr bool diag = decltype(diag_c)::value;
     const int cur = (t - t0) & 1;
     const int q0 = t * 64;
-    if (q0 + 63 >= wave_kmin) {
+    {
       const bf16_t* Qs = lds + cur * 2 * TILE_ELEMS;
       const bf16_t* Ds = Qs + TILE_ELEMS;
       const float* nl = rowc + cur * 128;
       const float* nd = nl + 64;
-      const bool diag = q0 < wave_kmin + 31;
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         // S' = Q K^T - LSE/c ; dP' = dO V^T - delta   (rows q, cols = this wave's keys)
@@ -391,6 +404,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
       }
+    }
+  };
+  auto compute = [&](int t) __attribute__((always_inline)) {
+    const int q0 = t * 64;
+    if (q0 + 63 >= wave_kmin) {
+      if (q0 < wave_kmin + 31) body(t, std::true_type{});
+      else body(t, std::false_type{});
     }
   };
   auto step = [&](int t, QD& held, QD& next) __attribute__((always_inline)) {
@@ -459,12 +479,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     tile_store(x.k, d);
     tile_store(x.v, d + TILE_ELEMS);
   };
-  auto compute = [&](int t) __attribute__((always_inline)) {
+  auto body = [&](int t, auto diag_c) __attribute__((always_inline)) {
+    constexpr bool diag = decltype(diag_c)::value;
     const int kv0 = t * 64;
-    if (kv0 <= wave_qmax) {
+    {
       const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
       const bf16_t* Vs = Ks + TILE_ELEMS;
-      const bool diag = kv0 + 63 > q0 + 32 * w;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f32x16 st, dpt;
@@ -492,6 +512,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
             dq[dt] = mfma32(tr_frag(Ks, lo, 32 * kt + 16 * s, dt), bfrag, dq[dt]);
         }
       }
+    }
+  };
+  auto compute = [&](int t) __attribute__((always_inline)) {
+    const int kv0 = t * 64;
+    if (kv0 <= wave_qmax) {
+      if (kv0 + 63 > q0 + 32 * w) body(t, std::true_type{});
+      else body(t, std::false_type{});
     }
   };
   auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {

@@ -165,7 +165,7 @@ static inline void colsum_launch(const float* part, float* scratch, void* out, i
   if (S > kColsumSplits) S = kColsumSplits;
   if (S < 1) S = 1;
   if (!(flags & kColsumBF16) && ra_knobs[2]) {
-    if (!(flags & kColsumAcc)) hipMemsetAsync(out, 0, (size_t)D * sizeof(float), st);
+    if (!(flags & kColsumAcc)) (void)hipMemsetAsync(out, 0, (size_t)D * sizeof(float), st);
     hipLaunchKernelGGL(colsum_atomic, dim3((D + 63) / 64, S), dim3(256), 0, st, part,
                        (float*)out, P, D);
     return;
