@@ -30,6 +30,20 @@ class Algorithm:
         probe = make_env(config.env, config.env_config)
         self.observation_space = probe.observation_space
         self.action_space = probe.action_space
+        # the modules see the env-to-module connector pipeline's output space; a
+        # learner-side MeanStdFilter keeps its statistics on the learner (HIP kernel)
+        from ray_amd.rllib.callbacks import MetricsLogger, make_callbacks
+        from ray_amd.rllib.connectors.connector_v2 import build_pipeline
+
+        pipe = build_pipeline(config.env_to_module_connector, self.observation_space,
+                              self.action_space)
+        learner_filter = config.observation_filter == "MeanStdFilter" or any(
+            getattr(c, "learner_side", False) for c in pipe.connectors)
+        self.cfg["_learner_obs_filter"] = learner_filter
+        self.observation_space = pipe.observation_space
+        self.callbacks = make_callbacks(config.callbacks_class)
+        self.metrics = MetricsLogger()
+        self._custom_metrics = {}
         self.is_multi_agent = bool(getattr(config, "is_multi_agent", False))
         if self.is_multi_agent and not self.supports_multi_agent:
             raise NotImplementedError(f"{type(self).__name__} does not support multi-agent "
@@ -65,6 +79,7 @@ class Algorithm:
             self.env_runners = []
             self.local_runner = local_cls(self.cfg, 0)
         self.setup()
+        self.callbacks.on_algorithm_init(algorithm=self, metrics_logger=self.metrics)
 
     @staticmethod
     def _module_specs(config, probe):
@@ -112,11 +127,15 @@ class Algorithm:
             ms = ray.get([r.get_metrics.remote() for r in self.env_runners])
         else:
             ms = [self.local_runner.get_metrics()]
+        cm = {}
         for m in ms:
             self._episode_returns.extend(m["episode_returns"])
             self._episode_lengths.extend(m["episode_lengths"])
+            for k, v in (m.get("custom_metrics") or {}).items():
+                cm.setdefault(k, []).append(v)
             for mid, rs in m.get("module_episode_returns", {}).items():
                 self._module_returns.setdefault(mid, []).extend(rs)
+        self._custom_metrics = {k: float(np.mean(v)) for k, v in cm.items()}
         k = self.config.metrics_num_episodes_for_smoothing
         self._episode_returns = self._episode_returns[-k:]
         self._episode_lengths = self._episode_lengths[-k:]
@@ -156,9 +175,19 @@ class Algorithm:
             "learners": res,
         }
         out["episode_reward_mean"] = out["env_runners"]["episode_return_mean"]
+        if self._custom_metrics:
+            out["env_runners"]["custom_metrics"] = dict(self._custom_metrics)
+            out["custom_metrics"] = dict(self._custom_metrics)
         if self.config.evaluation_interval and self.iteration % self.config.evaluation_interval \
                 == 0:
+            self.callbacks.on_evaluate_start(algorithm=self, metrics_logger=self.metrics)
             out["evaluation"] = self.evaluate()
+            self.callbacks.on_evaluate_end(algorithm=self, evaluation_metrics=out["evaluation"],
+                                           metrics_logger=self.metrics)
+        self.callbacks.on_train_result(algorithm=self, result=out, metrics_logger=self.metrics)
+        extra = self.metrics.reduce_all()
+        if extra:
+            out.setdefault("custom_metrics", {}).update(extra)
         return out
 
     def training_step(self) -> dict:
@@ -212,7 +241,15 @@ class Algorithm:
             if not hasattr(self, "_infer_module"):
                 self._infer_module = RLModule(self.observation_space, self.action_space,
                                               self.config.model)
-            self._infer_module.load_state_dict(self.get_weights())
+            w = dict(self.get_weights())
+            cs = w.pop("__connector_state__", None)
+            self._infer_module.load_state_dict(w)
+            if cs is not None:  # same normalization the EnvRunners apply
+                from ray_amd.ops.functional import RunningMeanStd
+
+                f = RunningMeanStd(tuple(cs["mean"].shape))
+                f.load_state_dict(cs)
+                obs = f.normalize(torch.as_tensor(np.asarray(obs, np.float32))).numpy()
         with torch.no_grad():
             x = torch.as_tensor(np.asarray(obs)[None])
             di = self._infer_module.forward_inference(x)["action_dist_inputs"]
@@ -255,6 +292,7 @@ class Algorithm:
         path = checkpoint.path if hasattr(checkpoint, "path") else checkpoint
         with open(os.path.join(path, "algorithm_state.pkl"), "rb") as f:
             self.set_state(pickle.load(f))
+        self.callbacks.on_checkpoint_loaded(algorithm=self)
 
     restore_from_path = restore
 

@@ -39,6 +39,12 @@ class AlgorithmConfig:
         self.policies = None
         self.policy_mapping_fn = None
         self.policies_to_train = None
+        # ConnectorV2 pipelines (callables returning connector(s)) and observation filter
+        self.env_to_module_connector = None
+        self.module_to_env_connector = None
+        self.learner_connector = None
+        self.observation_filter = "NoFilter"
+        self.callbacks_class = None
 
     # ---------------------------------------------------------------- builders
     def environment(self, env=None, *, env_config=None, **kw):
@@ -50,12 +56,16 @@ class AlgorithmConfig:
 
     def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None,
                     rollout_fragment_length=None, num_cpus_per_env_runner=None,
-                    num_gpus_per_env_runner=None, **kw):
+                    num_gpus_per_env_runner=None, env_to_module_connector=None,
+                    module_to_env_connector=None, observation_filter=None, **kw):
         for k, v in dict(num_env_runners=num_env_runners,
                          num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length,
                          num_cpus_per_env_runner=num_cpus_per_env_runner,
-                         num_gpus_per_env_runner=num_gpus_per_env_runner).items():
+                         num_gpus_per_env_runner=num_gpus_per_env_runner,
+                         env_to_module_connector=env_to_module_connector,
+                         module_to_env_connector=module_to_env_connector,
+                         observation_filter=observation_filter).items():
             if v is not None:
                 setattr(self, k, v)
         return self
@@ -85,6 +95,12 @@ class AlgorithmConfig:
             self.num_learners = num_learners
         if num_gpus_per_learner is not None:
             self.num_gpus_per_learner = num_gpus_per_learner
+        return self
+
+    def callbacks(self, callbacks_class=None, **kw):
+        """RLlibCallback subclass / instance / list of them (reference:
+        AlgorithmConfig.callbacks)."""
+        self.callbacks_class = callbacks_class
         return self
 
     def framework(self, framework="torch", **kw):

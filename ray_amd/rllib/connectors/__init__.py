@@ -1,0 +1,10 @@
+"""ConnectorV2 pipelines (reference: rllib/connectors/connector_v2.py,
+connector_pipeline_v2.py, env_to_module/, module_to_env/, learner/)."""
+
+from ray_amd.rllib.connectors.connector_v2 import ConnectorPipelineV2, ConnectorV2
+from ray_amd.rllib.connectors.env_to_module import (FlattenObservations, MeanStdFilter,
+                                                    PrevActionsPrevRewards)
+from ray_amd.rllib.connectors.module_to_env import ClipActions, NormalizeAndClipActions
+
+__all__ = ["ConnectorV2", "ConnectorPipelineV2", "MeanStdFilter", "FlattenObservations",
+           "PrevActionsPrevRewards", "ClipActions", "NormalizeAndClipActions"]

@@ -70,12 +70,51 @@ class Learner:
         self.kl_coeff = config.get("kl_coeff", 0.2)
         self.amp = device.type == "cuda" and config.get("learner_bf16", True)
         self.updates = 0
+        # MeanStdFilter statistics live HERE: updated over every training batch by the HIP
+        # Welford kernel (obsnorm_update) and broadcast to the EnvRunners with the weights
+        self.obs_filter = None
+        if config.get("_learner_obs_filter"):
+            from ray_amd.ops.functional import RunningMeanStd
+
+            self.obs_filter = RunningMeanStd(observation_space.shape, device)
+
+    def _filter_obs(self, obs_flat, boot_obs):
+        """Normalize raw observations (updating the running stats with this batch)."""
+        if self.obs_filter is None:
+            return obs_flat, boot_obs
+        f = self.obs_filter
+        if self.world > 1:  # every learner must see the same statistics: merge first
+            import torch.distributed as dist
+
+            n = torch.tensor([obs_flat.shape[0]], device=obs_flat.device, dtype=torch.float64)
+            x = obs_flat.reshape(obs_flat.shape[0], -1).float()
+            s1 = x.sum(0).double()
+            s2 = (x.double() ** 2).sum(0)
+            for t in (n, s1, s2):
+                dist.all_reduce(t)
+            tot = f.count + int(n.item())
+            bm = (s1 / n).float()
+            bv = (s2 / n - (s1 / n) ** 2).clamp_min(0).float()
+            d = bm - f.mean
+            f.mean = f.mean + d * (float(n) / tot)
+            f.m2 = f.m2 + bv * float(n) + d * d * f.count * float(n) / tot
+            f.count = tot
+        else:
+            f.update(obs_flat)
+        return f.normalize(obs_flat), f.normalize(boot_obs)
 
     # ---------------------------------------------------------------- weights
     def get_weights(self):
-        return {k: v.detach().float().cpu() for k, v in self.module.state_dict().items()}
+        w = {k: v.detach().float().cpu() for k, v in self.module.state_dict().items()}
+        if self.obs_filter is not None:
+            w["__connector_state__"] = self.obs_filter.state_dict()
+        return w
 
     def set_weights(self, w):
+        w = dict(w)
+        cs = w.pop("__connector_state__", None)
+        if cs is not None and self.obs_filter is not None:
+            self.obs_filter.load_state_dict(cs)
         self.module.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
         self.flat.sync_master_from_params()
 
@@ -87,9 +126,13 @@ class Learner:
                            "offsets": list(self.flat.offsets)},
                 "opt": {k: v.cpu() if torch.is_tensor(v) else v
                         for k, v in self.opt.state_dict().items()},
-                "kl_coeff": self.kl_coeff}
+                "kl_coeff": self.kl_coeff,
+                "obs_filter": self.obs_filter.state_dict() if self.obs_filter is not None
+                else None}
 
     def set_state(self, s):
+        if s.get("obs_filter") is not None and self.obs_filter is not None:
+            self.obs_filter.load_state_dict(s["obs_filter"])
         m = s.get("master")
         if m is not None and m["names"] == list(self.flat.names) and \
                 m["offsets"] == list(self.flat.offsets):
@@ -145,6 +188,7 @@ class Learner:
         old_di = _to_t(batch["action_dist_inputs"], dev)
         boot_obs = _to_t(batch["bootstrap_obs"], dev)
         obs_flat = obs.reshape((T * B,) + tuple(obs.shape[2:]))
+        obs_flat, boot_obs = self._filter_obs(obs_flat, boot_obs)
         vals = self._values(obs_flat).view(T, B)
         boot_v = self._values(boot_obs)
         adv, vtarg = rf.gae(rewards, vals, dones, boot_v, c.get("gamma", 0.99),
@@ -323,6 +367,7 @@ class Learner:
         beh_logp = _to_t(batch["action_logp"], dev)
         boot_obs = _to_t(batch["bootstrap_obs"], dev)
         obs_flat = obs.reshape((T * B,) + tuple(obs.shape[2:]))
+        obs_flat, boot_obs = self._filter_obs(obs_flat, boot_obs)
         out = self._fwd(obs_flat)
         logits = out["action_dist_inputs"].float()
         v = out["vf_preds"].float().view(T, B)

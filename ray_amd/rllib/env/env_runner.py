@@ -32,6 +32,37 @@ class SingleAgentEnvRunner:
             self.envs.append(make_env(config["env"], ec))
         self.observation_space = self.envs[0].observation_space
         self.action_space = self.envs[0].action_space
+        # ConnectorV2 pipelines: env -> module (per batched step) and module -> env
+        from ray_amd.rllib.callbacks import EpisodeState, MetricsLogger, make_callbacks
+        from ray_amd.rllib.connectors.connector_v2 import build_pipeline
+
+        self.env_to_module = build_pipeline(config.get("env_to_module_connector"),
+                                            self.observation_space, self.action_space)
+        if config.get("observation_filter") == "MeanStdFilter" and \
+                not any(getattr(c, "learner_side", False) for c in self.env_to_module.connectors):
+            from ray_amd.rllib.connectors.env_to_module import MeanStdFilter
+
+            self.env_to_module.append(MeanStdFilter(self.observation_space, self.action_space))
+        # learner-side connectors (MeanStdFilter: stats owned by the learner) run last and
+        # are NOT applied to the recorded observations
+        self._pre = [c for c in self.env_to_module.connectors
+                     if not getattr(c, "learner_side", False)]
+        self._post = [c for c in self.env_to_module.connectors
+                      if getattr(c, "learner_side", False)]
+        self.module_to_env = build_pipeline(config.get("module_to_env_connector"),
+                                            self.observation_space, self.action_space)
+        self.module_obs_space = self.env_to_module.observation_space
+        self.callbacks = make_callbacks(config.get("callbacks_class"))
+        self.metrics = MetricsLogger()
+        for e in self.envs:
+            self.callbacks.on_environment_created(env_runner=self, env=e,
+                                                  env_context=config.get("env_config"),
+                                                  metrics_logger=self.metrics)
+        act_dummy = 0 if hasattr(self.action_space, "n") else \
+            np.zeros(self.action_space.shape, np.float32)
+        self._act_dummy = act_dummy
+        self.episodes = [EpisodeState(i, worker_index, act_dummy) for i in range(n)]
+        self._next_eid = n
         from ray_amd.rllib.core.rl_module import RLModule
 
         self.module_kind = config.get("module_kind", "actor_critic")
@@ -40,15 +71,15 @@ class SingleAgentEnvRunner:
 
             mc = dict(config.get("model") or {})
             mc["dueling"] = config.get("dueling", True)
-            self.module = QModule(self.observation_space, self.action_space, mc)
+            self.module = QModule(self.module_obs_space, self.action_space, mc)
         elif self.module_kind == "sac":
             from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy
 
-            self.module = SquashedGaussianPolicy(self.observation_space, self.action_space,
+            self.module = SquashedGaussianPolicy(self.module_obs_space, self.action_space,
                                                  config.get("policy_model_config") or
                                                  config.get("model"))
         else:
-            self.module = RLModule(self.observation_space, self.action_space, config.get("model"))
+            self.module = RLModule(self.module_obs_space, self.action_space, config.get("model"))
         self.module.eval()
         self.device = torch.device("cpu")
         if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
@@ -58,6 +89,9 @@ class SingleAgentEnvRunner:
         for i, e in enumerate(self.envs):
             o, _ = e.reset(seed=None if seed is None else seed * 1000 + worker_index * 100 + i)
             self.obs.append(o)
+            self.episodes[i].id_ = i
+            self.callbacks.on_episode_start(episode=self.episodes[i], env_runner=self,
+                                            env_index=i, metrics_logger=self.metrics)
         self.ep_ret = np.zeros(n)
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.done_returns = []
@@ -70,6 +104,11 @@ class SingleAgentEnvRunner:
     def set_weights(self, weights, version: int = 0):
         if version is not None and version == self.weights_version:
             return
+        weights = dict(weights)
+        cstate = weights.pop("__connector_state__", None)
+        if cstate is not None:  # learner-owned filter statistics
+            for c in self._post:
+                c.set_state(cstate)
         sd = {k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(v))
               for k, v in weights.items()}
         self.module.load_state_dict(sd)
@@ -87,7 +126,8 @@ class SingleAgentEnvRunner:
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
         B = len(self.envs)
         osh = self.observation_space.shape
-        obs_buf = np.empty((T, B) + tuple(osh), dtype=self.observation_space.dtype)
+        obs_buf = np.empty((T, B) + tuple(osh), dtype=self.observation_space.dtype) \
+            if not self._pre else None  # connector output shape known after step 0
         discrete = hasattr(self.action_space, "n")
         act_buf = np.empty((T, B) if discrete else (T, B) + tuple(self.action_space.shape),
                            dtype=np.int64 if discrete else np.float32)
@@ -101,10 +141,14 @@ class SingleAgentEnvRunner:
             next_obs_buf = np.empty_like(obs_buf)
         t0 = time.perf_counter()
         for t in range(T):
-            ob = np.stack(self.obs)
-            obs_buf[t] = ob
+            rec, ob = self._module_obs(np.stack(self.obs), explore)
+            if obs_buf is None:
+                obs_buf = np.empty((T,) + rec.shape, dtype=rec.dtype)
+                if next_obs_buf is not None:
+                    next_obs_buf = np.empty_like(obs_buf)
+            obs_buf[t] = rec
             with torch.no_grad():
-                x = torch.from_numpy(ob).to(self.device)
+                x = torch.from_numpy(np.ascontiguousarray(ob)).to(self.device)
                 if self.module_kind == "q":
                     q = self.module(x)
                     a = q.argmax(-1).cpu().numpy()
@@ -128,16 +172,30 @@ class SingleAgentEnvRunner:
                     dist_in[t] = di.float().cpu().numpy()
             act_buf[t] = a
             logp[t] = lp
+            a_env = a
+            if len(self.module_to_env):
+                a_env = self.module_to_env(rl_module=self.module,
+                                           batch={"actions": a, "actions_for_env": a},
+                                           episodes=self.episodes,
+                                           explore=explore)["actions_for_env"]
             for i, env in enumerate(self.envs):
-                ai = a[i]
+                ai = a_env[i]
                 if not discrete:
                     ai = np.clip(ai, self.action_space.low, self.action_space.high)
                 o, r, te, tr, _ = env.step(ai if not discrete else int(ai))
                 rew[t, i] = r
                 self.ep_ret[i] += r
                 self.ep_len[i] += 1
+                ep = self.episodes[i]
+                ep.t += 1
+                ep.total_reward += float(r)
+                ep.prev_action = a[i]
+                ep.prev_reward = float(r)
+                self.callbacks.on_episode_step(episode=ep, env_runner=self, env_index=i,
+                                               metrics_logger=self.metrics)
                 if next_obs_buf is not None:
-                    next_obs_buf[t, i] = o
+                    next_obs_buf[t, i] = self._module_obs(o[None], explore, update=False)[0][0] \
+                        if self._pre else o
                 if te or tr:
                     term[t, i] = 1.0 if (te or not self.config.get("bootstrap_truncated")) \
                         else 0.0
@@ -146,12 +204,23 @@ class SingleAgentEnvRunner:
                     self.done_lengths.append(int(self.ep_len[i]))
                     self.ep_ret[i] = 0.0
                     self.ep_len[i] = 0
+                    self.callbacks.on_episode_end(episode=ep, env_runner=self, env_index=i,
+                                                  metrics_logger=self.metrics)
+                    for k, v in ep.custom_metrics.items():
+                        self.metrics.log_value(k, v)
                     o, _ = env.reset()
+                    ep.reset(self._act_dummy, self._next_eid)
+                    self._next_eid += 1
+                    self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i,
+                                                    metrics_logger=self.metrics)
                 self.obs[i] = o
         self.total_steps += T * B
+        boot = np.stack(self.obs)
+        if self._pre:
+            boot = self._module_obs(boot, explore, update=False)[0]
         batch = {"obs": obs_buf, "actions": act_buf, "rewards": rew, "terminateds": term,
                  "truncateds": trunc, "action_logp": logp,
-                 "bootstrap_obs": np.stack(self.obs), "env_steps": T * B,
+                 "bootstrap_obs": boot, "env_steps": T * B,
                  "sample_time_s": time.perf_counter() - t0,
                  "weights_version": self.weights_version}
         if dist_in is not None:
@@ -167,12 +236,30 @@ class SingleAgentEnvRunner:
                 nxt = np.concatenate([obs_buf[1:], np.stack(self.obs)[None]], 0)
                 batch = dict(batch, next_obs=nxt)
             self._writer.write(batch)
+        self.callbacks.on_sample_end(env_runner=self, samples=batch, metrics_logger=self.metrics)
         return batch
+
+    def _module_obs(self, ob, explore, update=True):
+        """(observation to record, module input) for a batched env step: the env-to-module
+        connectors run in order; learner-side ones (MeanStdFilter) only shape the module
+        input, the recorded observation stays un-normalized for the learner."""
+        if not self.env_to_module.connectors:
+            return ob, ob
+        b = {"obs": ob}
+        for c in self._pre:
+            b = c(rl_module=self.module, batch=b, episodes=self.episodes, explore=explore)
+        rec = b["obs"]
+        if self._post:
+            b = {"obs": rec}
+            for c in self._post:
+                b = c(rl_module=self.module, batch=b, episodes=self.episodes, explore=explore)
+        return rec, b["obs"]
 
     def get_metrics(self):
         r, ln = self.done_returns, self.done_lengths
         self.done_returns, self.done_lengths = [], []
-        return {"episode_returns": r, "episode_lengths": ln, "num_env_steps": self.total_steps}
+        return {"episode_returns": r, "episode_lengths": ln, "num_env_steps": self.total_steps,
+                "custom_metrics": self.metrics.reduce_all()}
 
     def set_epsilon(self, eps):
         self.epsilon = eps
