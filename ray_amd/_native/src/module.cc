@@ -5,6 +5,7 @@
 
 #include <random>
 
+#include "channel.h"
 #include "io_loop.h"
 #include "scheduler.h"
 #include "shm_store.h"
@@ -293,4 +294,38 @@ PYBIND11_MODULE(_core, m) {
       .def("process_private_bytes", &MemoryMonitor::process_private_bytes,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("threshold", &MemoryMonitor::threshold);
+
+  py::register_exception<ChannelClosed>(m, "ChannelClosedError");
+  py::class_<ShmChannel>(m, "ShmChannel")
+      .def(py::init<std::string, uint64_t, int, bool>(), py::arg("path"),
+           py::arg("capacity") = 0, py::arg("num_readers") = 1, py::arg("create") = false)
+      .def("write",
+           [](ShmChannel& c, py::buffer b, double timeout) {
+             py::buffer_info bi = b.request();
+             const uint64_t n = (uint64_t)bi.size * (uint64_t)bi.itemsize;
+             // fast path with the GIL held: releasing it costs a GIL hand-off to any
+             // other Python thread of the process (tens of microseconds)
+             if (n <= (64u << 10) && c.try_write((const char*)bi.ptr, n)) return true;
+             py::gil_scoped_release r;
+             return c.write((const char*)bi.ptr, n, timeout);
+           },
+           py::arg("data"), py::arg("timeout") = -1.0)
+      .def("read",
+           [](ShmChannel& c, int reader, double timeout) -> py::object {
+             std::string out;
+             bool ok = c.try_read(reader, &out);
+             if (!ok && timeout != 0.0) {
+               py::gil_scoped_release r;
+               ok = c.read(reader, &out, timeout);
+             }
+             if (!ok) return py::none();
+             return py::bytes(out);
+           },
+           py::arg("reader") = 0, py::arg("timeout") = -1.0)
+      .def("close", &ShmChannel::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("closed", &ShmChannel::closed)
+      .def_property_readonly("version", &ShmChannel::version)
+      .def_property_readonly("capacity", &ShmChannel::capacity)
+      .def_property_readonly("num_readers", &ShmChannel::num_readers)
+      .def_static("set_spin_us", &ShmChannel::set_spin_us);
 }

@@ -2024,7 +2024,16 @@ class CoreWorker:
         async with self._async_sem:
             self.current_task.tid = tid
             try:
-                fn = getattr(self.actor_instance, spec["method"])
+                m = spec["method"]
+                if m == "__ray_terminate__":
+                    raise _ActorExit()
+                if m == "__ray_ready__":
+                    fn = _ready
+                elif m == "__ray_call__":
+                    inst = self.actor_instance
+                    fn = lambda f, *a, **k: f(inst, *a, **k)  # noqa: E731
+                else:
+                    fn = getattr(self.actor_instance, m)
                 loop = asyncio.get_running_loop()
                 args, kwargs = await loop.run_in_executor(None, self._decode_args, spec["args"],
                                                           owner)

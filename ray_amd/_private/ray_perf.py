@@ -63,6 +63,34 @@ class Client:
             res.extend([s.small_value.remote() for _ in range(n)])
         ray.get(res)
 
+    def small_value_batch_arg(self, n):
+        x = ray.put(0)
+        res = []
+        for s in self.servers:
+            res.extend([s.small_value_arg.remote(x) for _ in range(n)])
+        ray.get(res)
+
+
+@ray.remote(num_cpus=0)
+class PutClient:
+    def put_small(self, n):
+        for _ in range(n):
+            ray.put(0)
+
+    def put_large(self, mb):
+        arr = np.zeros(mb * 1024 * 1024 // 8, dtype=np.int64)
+        for _ in range(10):
+            ray.put(arr)
+
+    def tasks(self, n):
+        ray.get([small_value.remote() for _ in range(n)])
+
+
+@ray.remote(num_cpus=0)
+class DagStage:
+    def f(self, x):
+        return x
+
 
 @ray.remote
 def small_value():
@@ -86,9 +114,28 @@ def main(quick=False, num_cpus=None):
         ray.get([small_value.remote() for _ in range(1000)])
 
     results.append(timeit("single client tasks and get batch", batch, duration=d))
+    n_clients = max(2, min(8, multiprocessing.cpu_count() // 2))
+    clients = [PutClient.remote() for _ in range(n_clients)]
+    ray.get([c.put_small.remote(1) for c in clients])
+    results.append(timeit("multi client put calls (Plasma Store)",
+                          lambda: ray.get([c.put_small.remote(1000) for c in clients]),
+                          1000 * n_clients, duration=d))
+    results.append(timeit("multi client put gigabytes",
+                          lambda: ray.get([c.put_large.remote(80) for c in clients]),
+                          n_clients * 10 * 80 / 1024, duration=d))
+
+    def get_containing_object_ref():
+        obj_containing_ref = ray.put([ray.put(0) for _ in range(10000)])
+        ray.get(obj_containing_ref)
+
+    results.append(timeit("single client get object containing 10k refs",
+                          get_containing_object_ref, duration=d))
     results.append(timeit("single client tasks sync", lambda: ray.get(small_value.remote()),
                           duration=d))
     results.append(timeit("single client tasks async", batch, 1000, duration=d))
+    results.append(timeit("multi client tasks async",
+                          lambda: ray.get([c.tasks.remote(1000) for c in clients]),
+                          1000 * n_clients, duration=d))
 
     def wait_multiple_refs():
         not_ready = [small_value.remote() for _ in range(1000)]
@@ -114,6 +161,32 @@ def main(quick=False, num_cpus=None):
     results.append(timeit("1:n actor calls async",
                           lambda: ray.get(client.small_value_batch.remote(n)), n * n_cpu,
                           duration=d))
+    m = max(2, n_cpu // 2)
+    servers = [Actor.remote() for _ in range(m)]
+    nn_clients = [Client.remote(s) for s in servers]
+    results.append(timeit("n:n actor calls async",
+                          lambda: ray.get([c.small_value_batch.remote(1000)
+                                           for c in nn_clients]), 1000 * m, duration=d))
+    results.append(timeit("n:n actor calls with arg async",
+                          lambda: ray.get([c.small_value_batch_arg.remote(1000)
+                                           for c in nn_clients]), 1000 * m, duration=d))
+    from ray_amd.dag import InputNode
+
+    s1, s2 = DagStage.remote(), DagStage.remote()
+    with InputNode() as inp:
+        dag1 = s1.f.bind(inp)
+    cd = dag1.experimental_compile()
+    results.append(timeit("compiled DAG 1:1 actor calls sync",
+                          lambda: ray.get(cd.execute(b"ok")), duration=d))
+    cd.teardown()
+    with InputNode() as inp:
+        dag2 = s2.f.bind(s1.f.bind(inp))
+    cd = dag2.experimental_compile()
+    results.append(timeit("compiled DAG 2-actor chain sync",
+                          lambda: ray.get(cd.execute(b"ok")), duration=d))
+    cd.teardown()
+    results.append(timeit("2-actor .remote() chain sync",
+                          lambda: ray.get(s2.f.remote(s1.f.remote(b"ok"))), duration=d))
     aa = AsyncActor.remote()
     results.append(timeit("1:1 async-actor calls sync", lambda: ray.get(aa.small_value.remote()),
                           duration=d))

@@ -268,6 +268,9 @@ def get(object_refs, *, timeout=None):
     cw = _check_connected()
     if isinstance(object_refs, ObjectRefGenerator):
         object_refs = list(object_refs)
+    cd = _compiled_dag_get(object_refs, timeout)
+    if cd is not None:
+        return cd[0]
     single = isinstance(object_refs, ObjectRef)
     if single:
         refs = [object_refs]
@@ -284,6 +287,21 @@ def get(object_refs, *, timeout=None):
         raise ValueError("timeout must be >= 0")
     vals = cw.get_objects(refs, timeout)
     return vals[0] if single else vals
+
+
+def _compiled_dag_get(refs, timeout):
+    """ray.get on CompiledDAGRef(s): resolved through the DAG's output channels."""
+    import sys
+
+    m = sys.modules.get("ray_amd.dag.compiled_dag_node")
+    if m is None:
+        return None
+    R = m.CompiledDAGRef
+    if isinstance(refs, R):
+        return (refs.get(timeout),)
+    if isinstance(refs, (list, tuple)) and refs and all(isinstance(r, R) for r in refs):
+        return ([r.get(timeout) for r in refs],)
+    return None
 
 
 def wait(object_refs, *, num_returns=1, timeout=None, fetch_local=True):

@@ -62,8 +62,25 @@ class DAGNode:
     def _execute_impl(self, args, kwargs, cache, inputs):
         raise NotImplementedError
 
-    def experimental_compile(self, **kw):
-        return CompiledDAG(self)
+    def experimental_compile(self, *, enable_asyncio: bool = False,
+                             _submit_timeout=None, _buffer_size_bytes=None,
+                             _max_inflight_executions=None, _get_timeout=None, **kw):
+        """Compile into channel-connected persistent actor loops (reference:
+        dag_node.py:experimental_compile). See ``compiled_dag_node``."""
+        from .compiled_dag_node import CompiledDAG
+
+        return CompiledDAG(self, buffer_size_bytes=_buffer_size_bytes,
+                           max_inflight_executions=_max_inflight_executions,
+                           submit_timeout=_submit_timeout, get_timeout=_get_timeout,
+                           enable_asyncio=enable_asyncio)
+
+    def with_tensor_transport(self, transport: str = "auto", **kw):
+        """Move torch tensors in this node's output through the HBM object store
+        (device-to-device, zero-copy readers) instead of host memory."""
+        self._tensor_transport = transport
+        return self
+
+    with_type_hint = with_tensor_transport
 
 
 class InputNode(DAGNode):
@@ -178,18 +195,14 @@ class MultiOutputNode(DAGNode):
         return list(args[0])
 
 
-class CompiledDAG:
-    """Reference `experimental_compile`: here a cached re-executable graph handle."""
+def __getattr__(name):
+    if name in ("CompiledDAG", "CompiledDAGRef", "CompiledDAGFuture"):
+        from . import compiled_dag_node
 
-    def __init__(self, root):
-        self.root = root
-
-    def execute(self, *args, **kwargs):
-        return self.root.execute(*args, **kwargs)
-
-    def teardown(self):
-        pass
+        return getattr(compiled_dag_node, name)
+    raise AttributeError(name)
 
 
 __all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode",
-           "MultiOutputNode", "InputAttributeNode"]
+           "MultiOutputNode", "InputAttributeNode", "CompiledDAG",
+           "CompiledDAGRef", "CompiledDAGFuture"]

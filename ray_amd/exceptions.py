@@ -210,5 +210,13 @@ class RayChannelError(RayError):
     pass
 
 
+class RayChannelTimeoutError(RayChannelError, TimeoutError):
+    pass
+
+
+class RayCgraphCapacityExceeded(RayChannelError):
+    pass
+
+
 class CollectiveError(RayError):
     pass
