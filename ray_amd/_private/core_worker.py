@@ -211,7 +211,7 @@ class CoreWorker:
         self._events_flushed = 0.0
         self.gpu_ids = gpu_ids or []
         self.node_id = node_id
-        self.namespace = namespace
+        self._ns = namespace
         self.job_id = job_id
         self.local_mode = False
         self.runtime_env = runtime_env or {}
@@ -228,13 +228,23 @@ class CoreWorker:
 
         self.node_id = reg["node_id"]
         self.job_id = reg["job_id"]
-        self.namespace = reg.get("namespace") or namespace
+        self._ns = reg.get("namespace") or namespace
         self.node_ip = reg.get("node_ip", "127.0.0.1")
         self.store = ObjectStore(reg["store_path"], reg["spill_dir"], create=False)
         self.cluster_info = reg
         self.node_hex = self.node_id.hex()
         self._node_addrs: dict[str, str] = {}
         self.task_id_base = os.urandom(12)
+
+    @property
+    def namespace(self):
+        """The namespace of the task running on this thread (its driver's), else this
+        process's own."""
+        return getattr(self.current_task, "ns", None) or self._ns
+
+    @namespace.setter
+    def namespace(self, v):
+        self._ns = v
 
     # ------------------------------------------------------------------ connections
     def _connect(self, addr: str) -> int:
@@ -1121,7 +1131,7 @@ class CoreWorker:
             "resources": opts["resources"], "strategy": opts.get("strategy"),
             "retries": opts.get("max_retries", 3), "retry_exc": opts.get("retry_exceptions", False),
             "runtime_env": opts.get("runtime_env"), "attempt": 0, "job": self.job_id,
-            "dynamic": dynamic,
+            "dynamic": dynamic, "ns": self.namespace,
         }
         refs = []
         with self.lock:
@@ -1549,7 +1559,7 @@ class CoreWorker:
             "concurrency_groups": opts.get("concurrency_groups"),
             "is_async": method_meta.get("__is_async__", False),
             "runtime_env": opts.get("runtime_env"), "job": self.job_id,
-            "method_meta": method_meta,
+            "method_meta": method_meta, "ns": self.namespace,
         }
         self._inline_ready_args(spec)
         info = {
@@ -1822,6 +1832,9 @@ class CoreWorker:
             return
         self.current_task.tid = tid
         self.current_task.spec = spec
+        self.current_task.ns = spec.get("ns")
+        if spec["type"] == P.ACTOR_CREATION_TASK and spec.get("ns"):
+            self._ns = spec["ns"]  # an actor lives in its creator's namespace
         self.current_task.lease_id = spec.get("lease_id")
         with self.lock:
             self.running[tid] = threading.get_ident()

@@ -13,6 +13,11 @@ import weakref
 from ray_amd._private import options as _opt
 
 
+def _cw_key(cw):
+    """Cache key of a connection: the worker id (client connections: the object)."""
+    return getattr(cw, "worker_id", None) or id(cw)
+
+
 def _method_meta(cls):
     meta = {}
     is_async = False
@@ -187,10 +192,10 @@ class ActorClass:
         from ray_amd._private.ids import random_bytes
 
         cw = W._check_connected()
-        key = self._keys.get(cw.worker_id)
+        key = self._keys.get(_cw_key(cw))
         if key is None:
             key = cw.export(self._cls)
-            self._keys[cw.worker_id] = key
+            self._keys[_cw_key(cw)] = key
         max_conc = opts.get("max_concurrency")
         if max_conc is None:
             max_conc = 1000 if self._meta.get("__is_async__") else 1

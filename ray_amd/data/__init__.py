@@ -10,6 +10,7 @@ from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface
                                    read_binary_files, read_csv, read_datasource, read_images,
                                    read_json, read_numpy, read_parquet, read_text)
 from ray_amd.data import preprocessors  # noqa: F401
+from ray_amd.data._executor import ExecutionOptions, ExecutionResources  # noqa: F401
 
 
 class DataContext:
@@ -17,7 +18,7 @@ class DataContext:
 
     def __init__(self):
         self.target_max_block_size = 128 << 20
-        self.execution_options = None
+        self.execution_options = ExecutionOptions()
         self.use_push_based_shuffle = False
 
     @classmethod

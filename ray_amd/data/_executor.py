@@ -1,21 +1,38 @@
-"""Streaming executor (reference: python/ray/data/_internal/execution/streaming_executor.py,
-operators/{map_operator,actor_pool_map_operator,task_pool_map_operator}.py,
-logical/rules/operator_fusion.py).
+"""Streaming executor with resource budgets and backpressure.
 
-A plan is a source (read tasks or existing block refs) followed by stages. Runs of
-task-based transforms are FUSED into the read task (one remote task per input
-block: read → map → filter → map_batches ...). Actor-pool stages (stateful UDFs,
-e.g. a model or a HIP preprocessing kernel on a GPU) run on a pool of long-lived
-actors. Backpressure: each stage keeps at most ``max_in_flight`` tasks; outputs
-are yielded in input order, so consumers (iter_batches, Train ingest) start as
-soon as the first block is ready while upstream keeps producing.
+Reference behaviour: python/ray/data/_internal/execution/streaming_executor.py
+(scheduling loop on its own thread), streaming_executor_state.py
+(``select_operator_to_run``), resource_manager.py (``ReservationOpResourceAllocator``:
+a reserved share of the global limits per operator plus a shared pool),
+backpressure_policy/ (concurrency cap, resource budget), operators/
+{task_pool_map_operator,actor_pool_map_operator}.py (autoscaling actor pools) and
+logical/rules/operator_fusion.py.
+
+Structure:
+  * a ``Plan`` (source + stages) becomes a chain of physical operators; runs of task
+    stages are FUSED into one remote task per block (read -> map -> filter -> ...);
+  * one scheduling thread per execution: harvest finished tasks (``ray.wait`` over every
+    operator's in-flight metadata refs), hand outputs downstream, then launch work
+    downstream-first, each launch gated by the backpressure policies;
+  * the ``ResourceManager`` accounts per operator: CPU/GPU of running tasks and live
+    actors, and object-store bytes of outputs that are produced but not yet consumed
+    (queued for the next operator or for the consumer) plus the estimated output of
+    in-flight tasks. Each operator gets ``reservation_ratio / n_ops`` of the limits
+    reserved and competes for the rest; when the consumer is slow the last operator's
+    queued bytes hit its budget and the pressure propagates upstream;
+  * actor-pool operators autoscale between ``min_size`` and ``max_size``: a new actor
+    starts when every live actor is saturated and inputs are waiting (and the budget
+    allows its resources); idle actors above ``min_size`` are released once their
+    input is exhausted.
+Outputs are yielded in input order.
 """
 
 from __future__ import annotations
 
 import collections
-import itertools
 import os
+import threading
+import time
 
 import ray_amd as ray
 
@@ -67,7 +84,7 @@ class _MapWorker:
 
 class Stage:
     def __init__(self, kind, fns=None, make_fn=None, resources=None, pool=(1, 1),
-                 max_tasks_in_flight_per_actor=2, name="Map"):
+                 max_tasks_in_flight_per_actor=2, name="Map", concurrency=None):
         self.kind = kind  # "task" | "actor"
         self.fns = list(fns or [])
         self.make_fn = make_fn
@@ -75,10 +92,11 @@ class Stage:
         self.pool = pool
         self.max_tasks_in_flight_per_actor = max_tasks_in_flight_per_actor
         self.name = name
+        self.concurrency = concurrency  # task stages: cap on concurrent tasks
 
     def fusable_with(self, other):
         return self.kind == "task" and other.kind == "task" and \
-            self.resources == other.resources
+            self.resources == other.resources and self.concurrency == other.concurrency
 
 
 class Plan:
@@ -88,16 +106,44 @@ class Plan:
         self.stages = list(stages or [])
         self.source_meta = source_meta
         self._cache = None  # materialized (refs, metas)
+        self.last_stats = None
 
     def with_stage(self, st: Stage) -> "Plan":
         stages = list(self.stages)
         if stages and stages[-1].fusable_with(st):
             last = stages[-1]
             stages[-1] = Stage("task", last.fns + st.fns, resources=last.resources,
-                               name=f"{last.name}->{st.name}")
+                               name=f"{last.name}->{st.name}", concurrency=last.concurrency)
         else:
             stages.append(st)
         return Plan(self.source, stages, self.source_meta)
+
+
+# ============================================================================ resources
+class ExecutionResources:
+    """cpu / gpu slots and object-store bytes (None = unlimited)."""
+
+    __slots__ = ("cpu", "gpu", "object_store_memory")
+
+    def __init__(self, cpu=None, gpu=None, object_store_memory=None):
+        self.cpu = cpu
+        self.gpu = gpu
+        self.object_store_memory = object_store_memory
+
+    def __repr__(self):
+        return (f"ExecutionResources(cpu={self.cpu}, gpu={self.gpu}, "
+                f"object_store_memory={self.object_store_memory})")
+
+
+class ExecutionOptions:
+    def __init__(self, resource_limits: ExecutionResources | None = None,
+                 preserve_order: bool = True, reservation_ratio: float = 0.5,
+                 max_tasks_in_flight: int | None = None, verbose_progress: bool = False):
+        self.resource_limits = resource_limits or ExecutionResources()
+        self.preserve_order = preserve_order
+        self.reservation_ratio = reservation_ratio
+        self.max_tasks_in_flight = max_tasks_in_flight
+        self.verbose_progress = verbose_progress
 
 
 def _task_opts(res):
@@ -118,156 +164,482 @@ def default_parallelism():
         return os.cpu_count() or 2
 
 
-def execute(plan: Plan, max_in_flight: int | None = None):
+def _cluster_limits(opts: ExecutionOptions) -> ExecutionResources:
+    lim = opts.resource_limits
+    try:
+        cr = ray.cluster_resources()
+    except Exception:  # noqa: BLE001
+        cr = {}
+    cpu = lim.cpu if lim.cpu is not None else float(cr.get("CPU", os.cpu_count() or 2))
+    gpu = lim.gpu if lim.gpu is not None else float(cr.get("GPU", 0.0))
+    mem = lim.object_store_memory
+    if mem is None:
+        store = cr.get("object_store_memory")
+        mem = int(0.5 * store) if store else 2 << 30
+    return ExecutionResources(cpu, gpu, mem)
+
+
+# ============================================================================ operators
+class _Op:
+    """Common runtime state of a physical operator."""
+
+    def __init__(self, name, res, cap):
+        self.name = name
+        self.res = res
+        self.cpu = float(res.get("num_cpus", 1) or 0)
+        self.gpu = float(res.get("num_gpus", 0) or 0)
+        self.cap = cap  # concurrency cap (backpressure policy 1)
+        self.inq = collections.deque()  # (ref, meta, seq, nbytes) waiting to be processed
+        self.inflight = {}  # meta ref -> (seq, block ref, extra)
+        self.reorder = {}  # seq -> (block ref, meta dict)
+        self.next_seq = 0
+        self.outq = collections.deque()  # (ref, meta, seq) ready for downstream
+        self.upstream_done = False
+        self.out_bytes = 0  # bytes in reorder + outq
+        self.inq_bytes = 0  # bytes of queued inputs (charged to the upstream operator)
+        self.downstream = None
+        self.out_count = 0
+        self.out_total_bytes = 0
+        self.stats = {"tasks": 0, "rows": 0, "bytes": 0, "wall_s": 0.0, "backpressured_s": 0.0}
+        self._bp_since = None
+
+    # --- usage ---------------------------------------------------------------
+    def avg_out_bytes(self):
+        return self.out_total_bytes / self.out_count if self.out_count else 0
+
+    def mem_usage(self):
+        """Produced-but-unconsumed bytes: own queued outputs, outputs waiting in the next
+        operator's input queue, and the estimated output of running tasks."""
+        ds = self.downstream.inq_bytes if self.downstream is not None else 0
+        return self.out_bytes + ds + len(self.inflight) * self.avg_out_bytes()
+
+    def push_input(self, item):
+        self.inq.append(item)
+        self.inq_bytes += item[3]
+
+    def pop_input(self):
+        item = self.inq.popleft()
+        self.inq_bytes -= item[3]
+        return item
+
+    def cpu_usage(self):
+        return self.cpu * len(self.inflight)
+
+    def gpu_usage(self):
+        return self.gpu * len(self.inflight)
+
+    def pending_inputs(self):
+        return len(self.inq)
+
+    def done(self):
+        return self.upstream_done and not self.inq and not self.inflight and \
+            not self.reorder and not self.outq
+
+    # --- completions -----------------------------------------------------------
+    def on_complete(self, m):
+        seq, b, extra = self.inflight.pop(m)
+        meta = ray.get(m)
+        nb = int(meta.get("size_bytes", 0)) if meta else 0
+        self.out_count += 1
+        self.out_total_bytes += nb
+        self.out_bytes += nb
+        self.stats["tasks"] += 1
+        self.stats["rows"] += meta.get("num_rows", 0) if meta else 0
+        self.stats["bytes"] += nb
+        self.reorder[seq] = (b, meta)
+        while self.next_seq in self.reorder:
+            b2, m2 = self.reorder.pop(self.next_seq)
+            self.outq.append((b2, m2, self.next_seq))
+            self.next_seq += 1
+        return extra
+
+    def take_output(self):
+        b, m, seq = self.outq.popleft()
+        self.out_bytes -= int(m.get("size_bytes", 0)) if m else 0
+        return b, m, seq
+
+    def can_launch_more(self):
+        return bool(self.inq) and len(self.inflight) < self.cap
+
+    def launch(self):
+        raise NotImplementedError
+
+    def shutdown(self):
+        pass
+
+
+class _TaskOp(_Op):
+    """Fused read/map tasks (a task pool)."""
+
+    def __init__(self, name, fns, res, cap, read=False):
+        super().__init__(name, res, cap)
+        self.fns = fns
+        self.read = read
+        self.opts = _task_opts(res)
+
+    def launch(self):
+        item, _meta_in, seq, _nb = self.pop_input()
+        if self.read:
+            b, m = _read_and_map.options(**self.opts).remote(item, self.fns)
+        else:
+            b, m = _map_block.options(**self.opts).remote(item, self.fns)
+        self.inflight[m] = (seq, b, None)
+        return m
+
+
+class _ActorPoolOp(_Op):
+    """Stateful UDF on an autoscaling actor pool."""
+
+    def __init__(self, st: Stage):
+        lo, hi = st.pool
+        self.min_size = max(1, int(lo or 1))
+        self.max_size = max(self.min_size, int(hi or self.min_size))
+        self.per = max(1, int(st.max_tasks_in_flight_per_actor))
+        super().__init__(st.name, st.resources or {"num_cpus": 1}, self.max_size * self.per)
+        self.fns = st.fns
+        self.make_fn = st.make_fn
+        self.cls = ray.remote(_MapWorker)
+        self.opts = _task_opts(self.res)
+        self.actors = {}  # idx -> handle (ready)
+        self.starting = {}  # ready ref -> (idx, handle)
+        self.load = {}
+        self._next_idx = 0
+        self.stats.update({"actors_started": 0, "actors_released": 0, "max_actors": 0})
+        for _ in range(self.min_size):
+            self._start_actor()
+
+    def _start_actor(self):
+        h = self.cls.options(**self.opts).remote(self.make_fn)
+        i = self._next_idx
+        self._next_idx += 1
+        self.starting[h.ready.remote()] = (i, h)
+        self.stats["actors_started"] += 1
+
+    def n_actors(self):
+        return len(self.actors) + len(self.starting)
+
+    # actors hold their resources whether busy or not
+    def cpu_usage(self):
+        return self.cpu * self.n_actors()
+
+    def gpu_usage(self):
+        return self.gpu * self.n_actors()
+
+    def on_actor_ready(self, r):
+        i, h = self.starting.pop(r)
+        ray.get(r)
+        self.actors[i] = h
+        self.load[i] = 0
+        self.stats["max_actors"] = max(self.stats["max_actors"], len(self.actors))
+
+    def can_launch_more(self):
+        return bool(self.inq) and any(n < self.per for n in self.load.values())
+
+    def launch(self):
+        i = min((j for j, n in self.load.items() if n < self.per), key=lambda j: self.load[j])
+        ref, _m, seq, _nb = self.pop_input()
+        b, m = self.actors[i].process.options(num_returns=2).remote(ref, [], self.fns)
+        self.load[i] += 1
+        self.inflight[m] = (seq, b, i)
+        return m
+
+    def on_complete(self, m):
+        i = super().on_complete(m)
+        if i in self.load:
+            self.load[i] -= 1
+        return i
+
+    def want_scale_up(self):
+        return (self.inq and not self.starting and self.n_actors() < self.max_size and
+                all(n >= self.per for n in self.load.values()))
+
+    def scale_down_idle(self):
+        if not (self.upstream_done and not self.inq):
+            return
+        keep = 0 if not self.inflight else self.min_size
+        for i in [j for j, n in self.load.items() if n == 0]:
+            if len(self.actors) <= keep:
+                break
+            h = self.actors.pop(i)
+            self.load.pop(i)
+            self.stats["actors_released"] += 1
+            try:
+                ray.kill(h)
+            except Exception:  # noqa: BLE001
+                pass
+
+    def shutdown(self):
+        for h in list(self.actors.values()) + [h for _, h in self.starting.values()]:
+            try:
+                ray.kill(h)
+            except Exception:  # noqa: BLE001
+                pass
+        self.actors.clear()
+        self.starting.clear()
+        self.load.clear()
+
+
+class ResourceManager:
+    """Global limits, per-operator reservations and the shared remainder (reference:
+    resource_manager.py ReservationOpResourceAllocator)."""
+
+    def __init__(self, ops, limits: ExecutionResources, reservation_ratio: float):
+        self.ops = ops
+        self.limits = limits
+        n = max(1, len(ops))
+        self.reserved_mem = limits.object_store_memory * reservation_ratio / n
+        self.shared_mem = limits.object_store_memory * (1 - reservation_ratio)
+
+    def total_cpu(self):
+        return sum(o.cpu_usage() for o in self.ops)
+
+    def total_gpu(self):
+        return sum(o.gpu_usage() for o in self.ops)
+
+    def mem_budget_left(self, op):
+        """Bytes `op` may still add: its reservation plus what is left of the shared pool
+        after every operator's overflow beyond its own reservation."""
+        over = sum(max(0.0, o.mem_usage() - self.reserved_mem) for o in self.ops)
+        shared_left = max(0.0, self.shared_mem - over)
+        mine = max(0.0, self.reserved_mem - op.mem_usage())
+        return mine + shared_left
+
+    def can_launch(self, op, actor=False):
+        # backpressure policy 2: CPU/GPU slots (a task of an actor op uses the actor's)
+        if not actor:
+            if op.cpu and self.total_cpu() + op.cpu > self.limits.cpu + 1e-9:
+                return False
+            if op.gpu and self.total_gpu() + op.gpu > self.limits.gpu + 1e-9:
+                return False
+        # backpressure policy 3: object store budget (estimated output of one more task)
+        est = op.avg_out_bytes()
+        return est <= self.mem_budget_left(op) or not op.inflight
+
+    def can_add_actor(self, op):
+        if op.cpu and self.total_cpu() + op.cpu > self.limits.cpu + 1e-9:
+            return False
+        if op.gpu and self.total_gpu() + op.gpu > self.limits.gpu + 1e-9:
+            return False
+        return True
+
+
+# ============================================================================ execution
+class StreamingExecutor:
+    """Runs one plan on a scheduling thread; iterate to receive (block_ref, meta)."""
+
+    def __init__(self, plan: Plan, options: ExecutionOptions | None = None):
+        self.plan = plan
+        self.options = options or _default_options()
+        self._cv = threading.Condition()
+        self._out = collections.deque()
+        self._out_bytes = 0  # bytes of blocks handed to the consumer but not yet read
+        self._finished = False
+        self._error = None
+        self._stop = False
+        self._thread = None
+        self.ops = []
+        self.stats = {}
+
+    # --- plan -> operators --------------------------------------------------------
+    def _build(self):
+        plan = self.plan
+        cap_default = self.options.max_tasks_in_flight or max(4, 2 * default_parallelism())
+        kind, src = plan.source
+        if kind == "lazy":
+            refs, metas = src()
+            kind, src, src_meta = "refs", refs, metas
+        else:
+            src_meta = plan.source_meta
+        stages = list(plan.stages)
+        first_fns, first_res, first_cap = [], {"num_cpus": 1}, cap_default
+        if stages and stages[0].kind == "task":
+            first_fns = stages[0].fns
+            first_res = stages[0].resources or first_res
+            first_cap = stages[0].concurrency or cap_default
+            first_name = stages[0].name
+            stages = stages[1:]
+        else:
+            first_name = "Read" if kind == "read" else "Input"
+        ops = []
+        if kind == "refs" and not first_fns:
+            self._source = [(r, (src_meta[i] if src_meta else None), i)
+                            for i, r in enumerate(src)]
+        else:
+            name = ("Read->" + first_name) if kind == "read" and first_fns else first_name
+            ops.append(_TaskOp(name, first_fns, first_res, first_cap, read=(kind == "read")))
+            self._source = [(item, None, i) for i, item in enumerate(src)]
+        for st in stages:
+            if st.kind == "task":
+                ops.append(_TaskOp(st.name, st.fns, st.resources or {"num_cpus": 1},
+                                   st.concurrency or cap_default))
+            else:
+                ops.append(_ActorPoolOp(st))
+        for a, b in zip(ops, ops[1:]):
+            a.downstream = b
+        self.ops = ops
+        self.rm = ResourceManager(ops, _cluster_limits(self.options),
+                                  self.options.reservation_ratio)
+        if ops:
+            for item, meta, seq in self._source:
+                ops[0].inq.append((item, meta, seq, 0))
+            ops[0].upstream_done = True
+
+    # --- thread ---------------------------------------------------------------------
+    def start(self):
+        self._build()
+        if not self.ops:  # plain refs, nothing to run
+            for r, m, _ in self._source:
+                self._out.append((r, m))
+            self._finished = True
+            return self
+        self._t0 = time.perf_counter()
+        self._thread = threading.Thread(target=self._run, daemon=True, name="data-exec")
+        self._thread.start()
+        return self
+
+    def _run(self):
+        try:
+            self._loop()
+        except BaseException as e:  # noqa: BLE001
+            self._error = e
+        finally:
+            for op in self.ops:
+                op.shutdown()
+            self._collect_stats()
+            with self._cv:
+                self._finished = True
+                self._cv.notify_all()
+
+    def _loop(self):
+        ops = self.ops
+        last = ops[-1]
+        while not self._stop:
+            progressed = False
+            # 1. hand outputs downstream / to the consumer
+            for k, op in enumerate(ops):
+                while op.outq:
+                    b, m, seq = op.take_output()
+                    if k + 1 < len(ops):
+                        ops[k + 1].push_input((b, m, seq, int(m.get("size_bytes", 0))
+                                               if m else 0))
+                    else:
+                        with self._cv:
+                            self._out.append((b, m))
+                            self._out_bytes += int(m.get("size_bytes", 0)) if m else 0
+                            self._cv.notify_all()
+                    progressed = True
+                if k + 1 < len(ops) and op.done():
+                    ops[k + 1].upstream_done = True
+            # 2. launch, downstream first (drains memory before producing more)
+            for op in reversed(ops):
+                if isinstance(op, _ActorPoolOp):
+                    if op.want_scale_up() and self.rm.can_add_actor(op):
+                        op._start_actor()
+                    op.scale_down_idle()
+                launched = 0
+                while op.can_launch_more() and self.rm.can_launch(
+                        op, actor=isinstance(op, _ActorPoolOp)) and \
+                        self._consumer_ok(op, last):
+                    op.launch()
+                    launched += 1
+                if launched:
+                    progressed = True
+                    op._bp_since = None
+                elif op.inq and op._bp_since is None:
+                    op._bp_since = time.perf_counter()
+            if all(op.done() for op in ops):
+                return
+            # 3. wait for a completion (task or actor start)
+            waits = {}
+            for op in ops:
+                for m in op.inflight:
+                    waits[m] = op
+                if isinstance(op, _ActorPoolOp):
+                    for r in op.starting:
+                        waits[r] = op
+            if not waits:
+                if not progressed:
+                    with self._cv:  # blocked on the consumer: wait until it reads
+                        self._cv.wait(0.05)
+                continue
+            ready, _ = ray.wait(list(waits), num_returns=1, timeout=0.05 if not progressed
+                                else 0)
+            ready2, _ = ray.wait(list(waits), num_returns=len(waits), timeout=0) \
+                if ready else ([], None)
+            for r in set(ready) | set(ready2):
+                op = waits[r]
+                if isinstance(op, _ActorPoolOp) and r in op.starting:
+                    op.on_actor_ready(r)
+                else:
+                    op.on_complete(r)
+            for op in ops:
+                if op._bp_since is not None and not op.inq:
+                    op.stats["backpressured_s"] += time.perf_counter() - op._bp_since
+                    op._bp_since = None
+
+    def _consumer_ok(self, op, last):
+        """The consumer not keeping up: stop the last operator once its unread output
+        exceeds its memory reservation (and the shared pool)."""
+        if op is not last or not last.inflight and not self._out:
+            return True
+        pending = self._out_bytes + last.mem_usage()
+        return pending <= self.rm.reserved_mem + self.rm.shared_mem
+
+    def _collect_stats(self):
+        wall = time.perf_counter() - getattr(self, "_t0", time.perf_counter())
+        self.stats = {op.name: dict(op.stats) for op in self.ops}
+        self.stats["_wall_s"] = wall
+        self.plan.last_stats = self.stats
+
+    # --- consumer side --------------------------------------------------------------
+    def __iter__(self):
+        try:
+            while True:
+                with self._cv:
+                    while not self._out and not self._finished:
+                        self._cv.wait(1.0)
+                    if self._out:
+                        item = self._out.popleft()
+                        m = item[1]
+                        self._out_bytes -= int(m.get("size_bytes", 0)) if m else 0
+                        self._cv.notify_all()
+                    elif self._error is not None:
+                        raise self._error
+                    else:
+                        return
+                yield item
+        finally:
+            self.shutdown()
+
+    def shutdown(self):
+        self._stop = True
+        if self._thread is not None and self._thread is not threading.current_thread():
+            self._thread.join(timeout=30)
+
+
+def _default_options():
+    from . import DataContext
+
+    o = DataContext.get_current().execution_options
+    return o if isinstance(o, ExecutionOptions) else ExecutionOptions()
+
+
+def execute(plan: Plan, max_in_flight: int | None = None,
+            options: ExecutionOptions | None = None):
     """Yields (block_ref, meta) in order."""
     if plan._cache is not None:
         for r, m in zip(*plan._cache):
             yield r, m
         return
-    cap = max_in_flight or max(4, 2 * default_parallelism())
-    kind, src = plan.source
-    if kind == "lazy":
-        refs, metas = src()
-        kind, src = "refs", refs
-        src_meta = metas
-    else:
-        src_meta = plan.source_meta
-    stages = list(plan.stages)
-    # stage 0 fuses the read (or the first task stage) when it is a task stage
-    first_fns = []
-    first_res = {"num_cpus": 1}
-    if stages and stages[0].kind == "task":
-        first_fns = stages[0].fns
-        first_res = stages[0].resources or first_res
-        stages = stages[1:]
-    if kind == "refs" and not first_fns:
-        upstream = ((r, (src_meta[i] if src_meta else None), i) for i, r in enumerate(src))
-    else:
-        upstream = _run_first(kind, src, first_fns, first_res, cap)
-    for st in stages:
-        if st.kind == "task":
-            upstream = _run_task_stage(upstream, st, cap)
-        else:
-            upstream = _run_actor_stage(upstream, st)
-    for ref, meta, _ in upstream:
+    opts = options or _default_options()
+    if max_in_flight is not None:
+        opts = ExecutionOptions(opts.resource_limits, opts.preserve_order,
+                                opts.reservation_ratio, max_in_flight, opts.verbose_progress)
+    ex = StreamingExecutor(plan, opts).start()
+    for ref, meta in ex:
         if meta is not None and not isinstance(meta, dict):
             meta = ray.get(meta)
         yield ref, meta
-
-
-def _run_first(kind, src, fns, res, cap):
-    opts = _task_opts(res)
-    items = iter(enumerate(src))
-    inflight = collections.OrderedDict()
-    done = {}
-    next_out = 0
-    exhausted = False
-    while True:
-        while not exhausted and len(inflight) + len(done) < cap:
-            try:
-                i, item = next(items)
-            except StopIteration:
-                exhausted = True
-                break
-            if kind == "read":
-                b, m = _read_and_map.options(**opts).remote(item, fns)
-            else:
-                b, m = _map_block.options(**opts).remote(item, fns)
-            inflight[m] = (i, b)
-        if next_out in done:
-            b, m = done.pop(next_out)
-            yield b, m, next_out
-            next_out += 1
-            continue
-        if not inflight:
-            if exhausted and not done:
-                return
-            continue
-        ready, _ = ray.wait(list(inflight), num_returns=1)
-        for m in ready:
-            i, b = inflight.pop(m)
-            done[i] = (b, m)
-
-
-def _run_task_stage(upstream, st, cap):
-    opts = _task_opts(st.resources or {"num_cpus": 1})
-    inflight = collections.OrderedDict()
-    done = {}
-    next_out = 0
-    up = iter(upstream)
-    exhausted = False
-    while True:
-        while not exhausted and len(inflight) + len(done) < cap:
-            try:
-                ref, _m, seq = next(up)
-            except StopIteration:
-                exhausted = True
-                break
-            b, m = _map_block.options(**opts).remote(ref, st.fns)
-            inflight[m] = (seq, b)
-        if next_out in done:
-            b, m = done.pop(next_out)
-            yield b, m, next_out
-            next_out += 1
-            continue
-        if not inflight:
-            if exhausted and not done:
-                return
-            continue
-        ready, _ = ray.wait(list(inflight), num_returns=1)
-        for m in ready:
-            seq, b = inflight.pop(m)
-            done[seq] = (b, m)
-
-
-def _run_actor_stage(upstream, st):
-    opts = _task_opts(st.resources or {"num_cpus": 1})
-    lo, hi = st.pool
-    cls = ray.remote(_MapWorker)
-    actors = [cls.options(**opts).remote(st.make_fn) for _ in range(max(1, hi))]
-    ray.get([a.ready.remote() for a in actors])
-    load = {i: 0 for i in range(len(actors))}
-    per = st.max_tasks_in_flight_per_actor
-    inflight = {}
-    done = {}
-    next_out = 0
-    up = iter(upstream)
-    exhausted = False
-    try:
-        while True:
-            while not exhausted:
-                free = [i for i, n in load.items() if n < per]
-                if not free:
-                    break
-                try:
-                    ref, _m, seq = next(up)
-                except StopIteration:
-                    exhausted = True
-                    break
-                i = min(free, key=lambda j: load[j])
-                b, m = actors[i].process.options(num_returns=2).remote(ref, [], st.fns)
-                load[i] += 1
-                inflight[m] = (seq, b, i)
-            if next_out in done:
-                b, m = done.pop(next_out)
-                yield b, m, next_out
-                next_out += 1
-                continue
-            if not inflight:
-                if exhausted and not done:
-                    return
-                continue
-            ready, _ = ray.wait(list(inflight), num_returns=1)
-            for m in ready:
-                seq, b, i = inflight.pop(m)
-                load[i] -= 1
-                done[seq] = (b, m)
-    finally:
-        for a in actors:
-            try:
-                ray.kill(a)
-            except Exception:
-                pass
 
 
 def materialize(plan: Plan):
@@ -280,4 +652,18 @@ def materialize(plan: Plan):
     return plan._cache
 
 
-itertools  # noqa: B018
+def format_stats(stats: dict | None) -> str:
+    if not stats:
+        return ""
+    lines = []
+    for name, s in stats.items():
+        if name.startswith("_"):
+            continue
+        extra = ""
+        if "max_actors" in s:
+            extra = (f", actors started {s['actors_started']} (peak {s['max_actors']}), "
+                     f"released {s['actors_released']}")
+        lines.append(f"Operator {name}: {s['tasks']} tasks, {s['rows']} rows, "
+                     f"{s['bytes']} bytes, backpressured {s['backpressured_s']:.3f}s{extra}")
+    lines.append(f"Total wall time: {stats.get('_wall_s', 0):.3f}s")
+    return "\n".join(lines)

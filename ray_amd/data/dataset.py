@@ -274,7 +274,9 @@ class Dataset:
                                       name=getattr(fn, "__name__", "MapBatches")))
         return self._with(X.Stage("task", [_batcher(fn, batch_size, batch_format, fn_args or (),
                                                     fn_kwargs or {}, zero_copy_batch)],
-                                  resources=res, name="MapBatches"))
+                                  resources=res, name="MapBatches",
+                                  concurrency=concurrency if isinstance(concurrency, int)
+                                  else None))
 
     def map(self, fn, *, compute=None, num_cpus=None, num_gpus=None, concurrency=None,
             **kw) -> "Dataset":
@@ -620,9 +622,11 @@ class Dataset:
     def stats(self) -> str:
         refs, metas = self._blocks()
         rows = builtins.sum(m["num_rows"] for m in metas)
-        return (f"Dataset: {len(refs)} blocks, {rows} rows, "
+        head = (f"Dataset: {len(refs)} blocks, {rows} rows, "
                 f"{builtins.sum(m['size_bytes'] for m in metas)} bytes; stages: "
                 + " -> ".join(s.name for s in self._plan.stages))
+        detail = X.format_stats(self._plan.last_stats)
+        return head + ("\n" + detail if detail else "")
 
     def _aggregate(self, cols):
         cols = [cols] if isinstance(cols, str) else list(cols)

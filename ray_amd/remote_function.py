@@ -8,6 +8,11 @@ import inspect
 from ray_amd._private import options as _opt
 
 
+def _cw_key(cw):
+    """Cache key of a connection: the worker id (client connections: the object)."""
+    return getattr(cw, "worker_id", None) or id(cw)
+
+
 class RemoteFunction:
     def __init__(self, function, options: dict):
         _opt.validate(options, actor=False)
@@ -48,10 +53,10 @@ class RemoteFunction:
         return FunctionNode(self, args, kwargs, self._default_options)
 
     def _key(self, cw):
-        k = self._keys.get(cw.worker_id)
+        k = self._keys.get(_cw_key(cw))
         if k is None:
             k = cw.export(self._function)
-            self._keys[cw.worker_id] = k
+            self._keys[_cw_key(cw)] = k
         return k
 
     def _remote(self, args, kwargs, opts):
