@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--lm-head-chunk", type=int, default=8192,
                     help="tokens per fused LM-head + cross-entropy chunk")
     ap.add_argument("--model", default="small")
+    ap.add_argument("--data-path", default="hbm", choices=["hbm", "h2d"],
+                    help="data workload: GPU-preprocessed device blocks through the HBM "
+                         "store (hbm) or host blocks + pinned H2D + consumer-side kernel")
     ap.add_argument("--tunableop", default="auto", choices=["off", "tune", "auto"],
                     help="PyTorch TunableOp GEMM selection: 'tune' benchmarks every hipBLASLt/"
                          "rocBLAS solution per GEMM shape during warmup and writes "

@@ -4,7 +4,12 @@ Canonical block = ``dict[str, np.ndarray]`` (columnar, equal length). Columnar
 numpy is what the shared-memory object store moves zero-copy (pickle-5
 out-of-band buffers) and what tensor columns need (images, token ids), so it is
 also the cheapest form to hand to a HIP preprocessing kernel or a pinned H2D copy.
-Arrow / pandas views are produced on demand (``to_batch``)."""
+Arrow / pandas views are produced on demand (``to_batch``).
+
+A column may also be a ``torch.Tensor`` on a GPU (a *device block*, e.g. the output of
+a HIP preprocessing UDF): returned from a task it lands in the node's HBM object store
+and readers on the same node map it zero-copy (hipIpc), so GPU-preprocessed batches
+reach the trainer without a host round trip."""
 
 from __future__ import annotations
 
@@ -19,8 +24,12 @@ def num_rows(b: Block) -> int:
     return 0
 
 
+def _is_tensor(v):
+    return type(v).__name__ in ("Tensor", "Parameter") and type(v).__module__.startswith("torch")
+
+
 def _col(values):
-    if isinstance(values, np.ndarray):
+    if isinstance(values, np.ndarray) or _is_tensor(values):
         return values
     try:
         arr = np.asarray(values)
@@ -78,6 +87,13 @@ def concat(blocks: list) -> Block:
     out = {}
     for k in keys:
         parts = [b[k] for b in blocks]
+        if any(_is_tensor(p) for p in parts):
+            import torch
+
+            dev = next(p.device for p in parts if _is_tensor(p))
+            out[k] = torch.cat([p if _is_tensor(p) else torch.from_numpy(np.asarray(p)).to(dev)
+                                for p in parts])
+            continue
         try:
             out[k] = np.concatenate(parts)
         except ValueError:
@@ -94,7 +110,10 @@ def concat(blocks: list) -> Block:
 def size_bytes(b: Block) -> int:
     n = 0
     for v in b.values():
-        n += v.nbytes if v.dtype != object else 64 * len(v)
+        if _is_tensor(v):
+            n += v.numel() * v.element_size()
+        else:
+            n += v.nbytes if v.dtype != object else 64 * len(v)
     return n
 
 

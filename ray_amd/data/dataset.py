@@ -48,7 +48,8 @@ def _batcher(fn, batch_size, batch_format, fn_args, fn_kwargs, zero_copy=False):
         for s in range(0, n, bs):
             part = B.slice_block(blk, s, s + bs)
             if not zero_copy:
-                part = {k: (np.array(v) if not v.flags.writeable else v) for k, v in part.items()}
+                part = {k: (np.array(v) if isinstance(v, np.ndarray) and not v.flags.writeable
+                            else v) for k, v in part.items()}
             r = fn(B.to_batch(part, batch_format), *fn_args, **fn_kwargs)
             if hasattr(r, "__next__") and not isinstance(r, dict):
                 for x in r:

@@ -75,6 +75,18 @@ def _resolve_device(device):
     return torch.device(device) if device is not None else torch.device("cpu")
 
 
+def _same_device(a, b):
+    import torch
+
+    if a.type != b.type:
+        return False
+    if a.type != "cuda":
+        return True
+    ia = a.index if a.index is not None else torch.cuda.current_device()
+    ib = b.index if b.index is not None else torch.cuda.current_device()
+    return ia == ib
+
+
 def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
     import torch
 
@@ -87,6 +99,14 @@ def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
     def to_tensors(b):
         out = {}
         for k, v in b.items():
+            if B._is_tensor(v):  # device block column: already a tensor
+                t = v.to(dev)
+                if dtypes is not None:
+                    dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
+                    if dt is not None:
+                        t = t.to(dt)
+                out[k] = t
+                continue
             if v.dtype == object:
                 out[k] = list(v)
                 continue
@@ -117,6 +137,12 @@ def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
         out = {}
         with torch.cuda.stream(stream):
             for k, v in b.items():
+                if B._is_tensor(v):
+                    # HBM-resident block: no copy on the same GPU, a D2D/H2D otherwise
+                    t = v if _same_device(v.device, dev) else v.to(dev, non_blocking=True)
+                    dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
+                    out[k] = t if dt is None else t.to(dt)
+                    continue
                 if v.dtype == object:
                     out[k] = list(v)
                     continue
@@ -138,18 +164,22 @@ def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
         fence[s] = ev
         return out, ev
 
+    def hand_over(out, ev):
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_event(ev)
+        for t in out.values():
+            if isinstance(t, torch.Tensor):
+                t.record_stream(cur)  # allocated on the copy stream, consumed on `cur`
+        return out
+
     nxt = None
     for b in batches:
         cur = stage(b)
         if nxt is not None:
-            out, ev = nxt
-            torch.cuda.current_stream(dev).wait_event(ev)
-            yield out
+            yield hand_over(*nxt)
         nxt = cur
     if nxt is not None:
-        out, ev = nxt
-        torch.cuda.current_stream(dev).wait_event(ev)
-        yield out
+        yield hand_over(*nxt)
 
 
 class DataIterator:

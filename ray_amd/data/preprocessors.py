@@ -256,9 +256,10 @@ class Chain(Preprocessor):
 
 
 class _GPUNormalizeUDF:
-    def __init__(self, column, mean, std, out_dtype, resize):
+    def __init__(self, column, mean, std, out_dtype, resize, keep_on_device=False):
         import torch
 
+        self.keep_on_device = keep_on_device
         self.column, self.mean, self.std = column, mean, std
         self.dtype = torch.bfloat16 if out_dtype == "bf16" else torch.float32
         self.resize = resize
@@ -275,6 +276,9 @@ class _GPUNormalizeUDF:
         if self.resize is not None:
             y = rf.resize_bilinear(y, self.resize)
         out = dict(batch)
+        if self.keep_on_device:  # device block: travels through the HBM object store
+            out[self.column] = y
+            return out
         arr = y.float().cpu().numpy() if self.dtype == torch.float32 else \
             y.view(torch.int16).cpu().numpy()
         out[self.column] = arr
@@ -288,9 +292,10 @@ class GPUImageNormalize(Preprocessor):
     _is_fittable = False
 
     def __init__(self, column="image", mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
-                 out_dtype="fp32", resize=None, concurrency=1, num_gpus=1, batch_size=256):
+                 out_dtype="fp32", resize=None, concurrency=1, num_gpus=1, batch_size=256,
+                 keep_on_device=False):
         super().__init__()
-        self.args = (column, mean, std, out_dtype, resize)
+        self.args = (column, mean, std, out_dtype, resize, keep_on_device)
         self.concurrency = concurrency
         self.num_gpus = num_gpus
         self.batch_size = batch_size

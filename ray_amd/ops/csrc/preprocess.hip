@@ -4,27 +4,83 @@
 //   ra_resize_bilinear: bf16/f32 NCHW bilinear resize (align_corners=False)
 //   ra_cast_scale     : uint8 -> bf16 with scale (Atari frames: x/255)
 //
-// The NHWC -> NCHW transpose goes through an LDS tile so both the uint8 reads
-// (contiguous W*C bytes per image row) and the planar writes are coalesced.
+// image_normalize treats each image as a flat run of H*W pixels (NHWC -> NCHW never
+// needs a row structure): 16 pixels per thread, 16-byte loads and stores.
 #include "common.h"
 
-#define TW 64
-// grid: (ceil(W/TW), H, N); block 256 threads.
+// y[c] = x * scale[c] + bias[c]  with scale = 1/(255 std), bias = -mean/std (one FMA)
+struct NormParams {
+  float scale[4];
+  float bias[4];
+};
+
+// Vector path (H*W % 16 == 0): one thread = 16 consecutive pixels of one image.
+// Loads 16*C bytes as C x 16-byte loads (adjacent lanes read adjacent 16*C-byte chunks,
+// fully coalesced), converts bytes with v_cvt_f32_ubyteN + one FMA, and writes each of
+// the C output planes as 32 contiguous bytes (bf16: 2 x 16-byte stores; fp32: 4).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int C, bool BF16_OUT, bool NT>
+__global__ __launch_bounds__(256) void image_normalize_vec_kernel(const uint8_t* __restrict__ x,
+                                                                  void* __restrict__ y,
+                                                                  long groups, long hw16,
+                                                                  NormParams p) {
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= groups) return;
+  const long n = g / hw16;
+  const long hw = (g - n * hw16) * 16;
+  const long HW = hw16 * 16;
+  uint32_t w[4 * C];
+  const u32x4_t* src = reinterpret_cast<const u32x4_t*>(x) + g * C;
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    const u32x4_t v = NT ? __builtin_nontemporal_load(src + k) : src[k];
+    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    float f[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int b = j * C + c;  // compile-time byte index
+      f[j] = (float)((w[b >> 2] >> ((b & 3) * 8)) & 0xffu) * p.scale[c] + p.bias[c];
+    }
+    const long o = (n * C + c) * HW + hw;
+    u32x4_t v[BF16_OUT ? 2 : 4];
+    if (BF16_OUT) {
+      float a[8], b2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] = f[j]; b2[j] = f[8 + j]; }
+      const uint4 p0 = pack8(a), p1 = pack8(b2);
+      v[0] = u32x4_t{p0.x, p0.y, p0.z, p0.w};
+      v[1] = u32x4_t{p1.x, p1.y, p1.z, p1.w};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        v[q] = u32x4_t{__float_as_uint(f[4 * q]), __float_as_uint(f[4 * q + 1]),
+                       __float_as_uint(f[4 * q + 2]), __float_as_uint(f[4 * q + 3])};
+    }
+    u32x4_t* dst = reinterpret_cast<u32x4_t*>(reinterpret_cast<char*>(y) +
+                                              o * (BF16_OUT ? 2 : 4));
+#pragma unroll
+    for (int q = 0; q < (BF16_OUT ? 2 : 4); ++q) {
+      if (NT) __builtin_nontemporal_store(v[q], dst + q);
+      else dst[q] = v[q];
+    }
+  }
+}
+
+// Generic path: one thread per pixel.
 template <bool BF16_OUT>
-__global__ __launch_bounds__(256) void image_normalize_kernel(const uint8_t* __restrict__ x,
-                                                              void* __restrict__ y, int H, int W,
-                                                              int C, const float* __restrict__ mean,
-                                                              const float* __restrict__ istd) {
-  __shared__ float tile[TW * 4 + 4];  // up to C=4 channels
-  const int n = blockIdx.z, h = blockIdx.y, w0 = blockIdx.x * TW;
-  const int wn = min(TW, W - w0);
-  const uint8_t* src = x + (((size_t)n * H + h) * W + w0) * C;
-  for (int i = threadIdx.x; i < wn * C; i += blockDim.x) tile[i] = (float)src[i];
-  __syncthreads();
-  for (int i = threadIdx.x; i < wn * C; i += blockDim.x) {
-    const int c = i / wn, w = i % wn;
-    const float v = (tile[w * C + c] * (1.f / 255.f) - mean[c]) * istd[c];
-    const size_t o = (((size_t)n * C + c) * H + h) * W + w0 + w;
+__global__ __launch_bounds__(256) void image_normalize_px_kernel(const uint8_t* __restrict__ x,
+                                                                 void* __restrict__ y, long npx,
+                                                                 long HW, int C, NormParams p) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npx) return;
+  const long n = i / HW, hw = i - n * HW;
+  for (int c = 0; c < C; ++c) {
+    const float v = (float)x[i * C + c] * p.scale[c] + p.bias[c];
+    const long o = (n * C + c) * HW + hw;
     if (BF16_OUT) reinterpret_cast<bf16_t*>(y)[o] = f2bf(v);
     else reinterpret_cast<float*>(y)[o] = v;
   }
@@ -71,17 +127,47 @@ __global__ __launch_bounds__(256) void cast_scale_kernel(const uint8_t* __restri
   }
 }
 
+// mean / std are HOST pointers (C floats): folded into kernel arguments, no H2D copy.
 RA_EXPORT int ra_image_normalize(const void* x, void* y, int N, int H, int W, int C,
-                                 const float* mean, const float* istd, int bf16_out,
+                                 const float* mean, const float* std_, int bf16_out,
                                  hipStream_t st) {
-  if (C > 4) return hipErrorInvalidValue;
-  dim3 g((W + TW - 1) / TW, H, N);
-  if (bf16_out)
-    hipLaunchKernelGGL(image_normalize_kernel<true>, g, dim3(256), 0, st, (const uint8_t*)x, y, H,
-                       W, C, mean, istd);
-  else
-    hipLaunchKernelGGL(image_normalize_kernel<false>, g, dim3(256), 0, st, (const uint8_t*)x, y,
-                       H, W, C, mean, istd);
+  if (C < 1 || C > 4) return hipErrorInvalidValue;
+  NormParams p;
+  for (int c = 0; c < 4; ++c) {
+    const float sd = c < C ? std_[c] : 1.f, m = c < C ? mean[c] : 0.f;
+    p.scale[c] = 1.f / (255.f * sd);
+    p.bias[c] = -m / sd;
+  }
+  const long HW = (long)H * W;
+  const bool vec = (HW % 16) == 0 && (((uintptr_t)x) % 16) == 0 && (((uintptr_t)y) % 16) == 0;
+  if (vec) {
+    const long groups = (long)N * HW / 16;
+    const dim3 g((unsigned)((groups + 255) / 256));
+    // ra_knobs[5]: 1 = plain (cached) loads/stores instead of nontemporal streaming
+#define RA_IMN2(CC, NTV)                                                                        \
+  if (bf16_out)                                                                                 \
+    hipLaunchKernelGGL((image_normalize_vec_kernel<CC, true, NTV>), g, dim3(256), 0, st,        \
+                       (const uint8_t*)x, y, groups, HW / 16, p);                              \
+  else                                                                                          \
+    hipLaunchKernelGGL((image_normalize_vec_kernel<CC, false, NTV>), g, dim3(256), 0, st,       \
+                       (const uint8_t*)x, y, groups, HW / 16, p);
+#define RA_IMN(CC)                                                                              \
+  if (C == CC) {                                                                                \
+    if (ra_knobs[5] == 1) { RA_IMN2(CC, false) } else { RA_IMN2(CC, true) }                     \
+  }
+    RA_IMN(1) RA_IMN(2) RA_IMN(3) RA_IMN(4)
+#undef RA_IMN
+#undef RA_IMN2
+  } else {
+    const long npx = (long)N * HW;
+    const dim3 g((unsigned)((npx + 255) / 256));
+    if (bf16_out)
+      hipLaunchKernelGGL(image_normalize_px_kernel<true>, g, dim3(256), 0, st, (const uint8_t*)x,
+                         y, npx, HW, C, p);
+    else
+      hipLaunchKernelGGL(image_normalize_px_kernel<false>, g, dim3(256), 0, st, (const uint8_t*)x,
+                         y, npx, HW, C, p);
+  }
   return hipGetLastError();
 }
 

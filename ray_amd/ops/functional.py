@@ -665,14 +665,21 @@ def image_normalize(x_u8_nhwc, mean, std, out_dtype=torch.float32):
     """uint8 NHWC → normalised NCHW (fp32 or bf16)."""
     if not _hip(x_u8_nhwc):
         return ref.image_normalize(x_u8_nhwc, mean, std, out_dtype)
+    import ctypes
+
     N, H, W, C = x_u8_nhwc.shape
-    dev = x_u8_nhwc.device
-    m = torch.as_tensor(mean, dtype=torch.float32).to(dev)
-    istd = (1.0 / torch.as_tensor(std, dtype=torch.float32)).to(dev)
-    y = torch.empty((N, C, H, W), dtype=out_dtype, device=dev)
-    check(_lib.lib().ra_image_normalize(ptr(x_u8_nhwc.contiguous()), ptr(y), N, H, W, C, ptr(m),
-                                        ptr(istd), 1 if out_dtype == torch.bfloat16 else 0,
-                                        stream_ptr()), "image_normalize")
+    if C > 4:
+        return ref.image_normalize(x_u8_nhwc, mean, std, out_dtype)
+    mean = [float(v) for v in (mean if hasattr(mean, "__len__") else [mean] * C)]
+    std = [float(v) for v in (std if hasattr(std, "__len__") else [std] * C)]
+    m = (ctypes.c_float * 4)(*(mean + [0.0] * (4 - len(mean))))
+    s = (ctypes.c_float * 4)(*(std + [1.0] * (4 - len(std))))
+    x = x_u8_nhwc.contiguous()
+    y = torch.empty((N, C, H, W), dtype=out_dtype, device=x.device)
+    check(_lib.lib().ra_image_normalize(ptr(x), ptr(y), N, H, W, C, ctypes.addressof(m),
+                                        ctypes.addressof(s),
+                                        1 if out_dtype == torch.bfloat16 else 0, stream_ptr()),
+          "image_normalize")
     return y
 
 

@@ -122,8 +122,16 @@ class Algorithm:
         else:
             self.local_runner.set_weights(weights, self.weights_version)
 
+    def _take_metrics(self, batch):
+        """Metrics that came back attached to a sample (async sampling paths)."""
+        m = batch.pop("_metrics", None) if isinstance(batch, dict) else None
+        if m is not None:
+            self.__dict__.setdefault("_async_ms", []).append(m)
+
     def _collect_metrics(self):
-        if self.env_runners:
+        if getattr(self, "_metrics_from_samples", False) and self.env_runners:
+            ms, self._async_ms = self.__dict__.get("_async_ms", []), []
+        elif self.env_runners:
             ms = ray.get([r.get_metrics.remote() for r in self.env_runners])
         else:
             ms = [self.local_runner.get_metrics()]

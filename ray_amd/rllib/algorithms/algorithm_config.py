@@ -44,6 +44,9 @@ class AlgorithmConfig:
         self.module_to_env_connector = None
         self.learner_connector = None
         self.observation_filter = "NoFilter"
+        # sample the next train batch while the learner updates on this one (one
+        # iteration of policy lag; the PPO ratio uses the recorded behaviour logp)
+        self.sample_async = False
         self.callbacks_class = None
 
     # ---------------------------------------------------------------- builders
@@ -57,7 +60,8 @@ class AlgorithmConfig:
     def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None,
                     rollout_fragment_length=None, num_cpus_per_env_runner=None,
                     num_gpus_per_env_runner=None, env_to_module_connector=None,
-                    module_to_env_connector=None, observation_filter=None, **kw):
+                    module_to_env_connector=None, observation_filter=None,
+                    sample_async=None, **kw):
         for k, v in dict(num_env_runners=num_env_runners,
                          num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length,
@@ -65,7 +69,8 @@ class AlgorithmConfig:
                          num_gpus_per_env_runner=num_gpus_per_env_runner,
                          env_to_module_connector=env_to_module_connector,
                          module_to_env_connector=module_to_env_connector,
-                         observation_filter=observation_filter).items():
+                         observation_filter=observation_filter,
+                         sample_async=sample_async).items():
             if v is not None:
                 setattr(self, k, v)
         return self

@@ -49,9 +49,11 @@ class IMPALA(Algorithm):
             stats = self.learner_group.update("vtrace", [b])
             self._sync_weights(self.learner_group.get_weights())
             return stats
+        self._metrics_from_samples = True
         for r in self.env_runners:
             if r not in self._inflight.values():
-                self._inflight[r.sample.remote(cfg.rollout_fragment_length)] = r
+                self._inflight[r.sample.remote(cfg.rollout_fragment_length,
+                                               with_metrics=True)] = r
         need = max(1, cfg.train_batch_size // (cfg.rollout_fragment_length *
                                                 cfg.num_envs_per_env_runner))
         batches = []
@@ -61,9 +63,11 @@ class IMPALA(Algorithm):
             ref = ready[0]
             runner = self._inflight.pop(ref)
             b = ray.get(ref)
+            self._take_metrics(b)
             self.total_env_steps += b["env_steps"]
             batches.append(b)
-            self._inflight[runner.sample.remote(cfg.rollout_fragment_length)] = runner
+            self._inflight[runner.sample.remote(cfg.rollout_fragment_length,
+                                                with_metrics=True)] = runner
         stats = self.learner_group.update("vtrace", batches)
         self._updates += 1
         if self._updates % cfg.broadcast_interval == 0:

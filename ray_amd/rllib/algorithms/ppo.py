@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import time
 
+import ray_amd as ray
 from ray_amd.rllib.algorithms.algorithm import Algorithm
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.learner import LearnerGroup
@@ -56,6 +57,8 @@ class PPO(Algorithm):
         self._sync_weights(self.learner_group.get_weights())
 
     def training_step(self) -> dict:
+        if self.config.sample_async and self.env_runners:
+            return self._training_step_async()
         t0 = time.perf_counter()
         batches = self._sample(self.config.train_batch_size)
         t1 = time.perf_counter()
@@ -65,3 +68,36 @@ class PPO(Algorithm):
         stats = dict(stats, sample_time_s=t1 - t0, learn_time_s=t2 - t1,
                      sync_time_s=time.perf_counter() - t2)
         return stats
+
+    def _launch_round(self):
+        per = self.config.rollout_fragment_length
+        return [r.sample.remote(per, with_metrics=True) for r in self.env_runners]
+
+    def _training_step_async(self) -> dict:
+        """Overlapped sampling (``sample_async``): the runners already sample batch k+1
+        while the learner updates on batch k; fresh weights are queued behind that
+        sample, so each batch is collected by the policy of one iteration earlier."""
+        self._metrics_from_samples = True
+        total = self.config.train_batch_size
+        t0 = time.perf_counter()
+        pending = self.__dict__.pop("_pending_round", None) or self._launch_round()
+        batches, got = [], 0
+        while True:
+            for b in ray.get(pending):
+                self._take_metrics(b)
+                got += b["env_steps"]
+                batches.append(b)
+            if got >= total:
+                break
+            pending = self._launch_round()
+        self.total_env_steps += got
+        self._pending_round = self._launch_round()  # overlaps the update below
+        t1 = time.perf_counter()
+        stats = self.learner_group.update("ppo", batches)
+        t2 = time.perf_counter()
+        self.weights_version += 1
+        ref = ray.put(self.learner_group.get_weights())
+        for r in self.env_runners:  # applied right after the in-flight sample
+            r.set_weights.remote(ref, self.weights_version)
+        return dict(stats, sample_wait_s=t1 - t0, learn_time_s=t2 - t1,
+                    sync_time_s=time.perf_counter() - t2)

@@ -23,9 +23,13 @@ def bench_ppo(args):
     ray.init(num_cpus=max(n_runners + 2, os.cpu_count() or 1), ignore_reinit_error=True)
     # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
     runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
+    sample_async = os.environ.get("RAY_AMD_PPO_ASYNC", "0") == "1"
+    # rollout_fragment_length "auto": 5000 / (runners x 5 envs) per env, so one sampling
+    # round is exactly train_batch_size env steps (atari-ppo.yaml uses 10 x 5 x 100)
     cfg = (PPOConfig().environment("SyntheticAtari-v0")
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
-                        rollout_fragment_length=100, num_gpus_per_env_runner=runner_gpus)
+                        rollout_fragment_length="auto", num_gpus_per_env_runner=runner_gpus,
+                        sample_async=sample_async)
            .training(train_batch_size=5000, minibatch_size=500, num_epochs=10, lr=1e-4,
                      lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
                      entropy_coeff=0.01, model={"vf_share_layers": True})
@@ -37,9 +41,11 @@ def bench_ppo(args):
     t0 = time.perf_counter()
     steps = 0
     learn_stats = {}
+    per_iter = []
     for _ in range(args.steps):
         r = algo.train()
         steps += r["num_env_steps_sampled_this_iter"]
+        per_iter.append(r["num_env_steps_sampled_this_iter"])
         learn_stats = r["learners"]
     dt = time.perf_counter() - t0
     value = steps / dt
@@ -51,11 +57,13 @@ def bench_ppo(args):
         "data": "synthetic",
         "config": {"model": "nature-cnn-ppo", "env": "SyntheticAtari-v0 84x84x4",
                    "env_runners": n_runners, "envs_per_runner": 5, "train_batch_size": 5000,
+                   "env_steps_per_iter_measured": sorted(set(per_iter)),
+                   "rollout_fragment_length": algo.config.rollout_fragment_length,
                    "minibatch_size": 500, "num_epochs": 10, "parallelism": "1 learner",
-                   "env_runner_gpus": runner_gpus},
+                   "env_runner_gpus": runner_gpus, "sample_async": sample_async},
         "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
-                                                     "sample_time_s", "learn_time_s",
-                                                     "sync_time_s")},
+                                                     "sample_time_s", "sample_wait_s",
+                                                     "learn_time_s", "sync_time_s")},
     }), flush=True)
     algo.stop()
     ray.shutdown()

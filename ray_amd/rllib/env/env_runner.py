@@ -122,7 +122,7 @@ class SingleAgentEnvRunner:
 
     # ---------------------------------------------------------------- sampling
     def sample(self, num_timesteps: int | None = None, explore: bool = True,
-               epsilon: float | None = None):
+               epsilon: float | None = None, with_metrics: bool = False):
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
         B = len(self.envs)
         osh = self.observation_space.shape
@@ -237,6 +237,8 @@ class SingleAgentEnvRunner:
                 batch = dict(batch, next_obs=nxt)
             self._writer.write(batch)
         self.callbacks.on_sample_end(env_runner=self, samples=batch, metrics_logger=self.metrics)
+        if with_metrics:  # async samplers: no separate get_metrics call behind a sample
+            batch["_metrics"] = self.get_metrics()
         return batch
 
     def _module_obs(self, ob, explore, update=True):

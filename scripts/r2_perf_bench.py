@@ -139,6 +139,23 @@ def bench_norm(N=65536, D=768, F=3072):
     return out
 
 
+def bench_imgnorm(N=256, H=224, W=224, C=3):
+    """uint8 NHWC -> bf16/fp32 NCHW normalisation: HBM bytes moved per second."""
+    x = torch.randint(0, 256, (N, H, W, C), dtype=torch.uint8, device="cuda")
+    out = {}
+    L = _lib.lib()
+    for mode, knob in (("nontemporal", 0), ("cached", 1)):
+        L.ra_set_knob(5, knob)
+        for name, dt, ob in (("bf16", torch.bfloat16, 2), ("fp32", torch.float32, 4)):
+            ms = timeit(lambda dt=dt: rf.image_normalize(x, (0.485, 0.456, 0.406),
+                                                         (0.229, 0.224, 0.225), dt), iters=50)
+            nbytes = N * H * W * C * (1 + ob)
+            out[f"{name}_{mode}"] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
+                                     "images_per_s": round(N / ms * 1e3, 1)}
+    L.ra_set_knob(5, 0)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--part", default="norm,wgrad,lmhead,xent")
@@ -146,7 +163,7 @@ def main():
     res = {}
     for p in a.part.split(","):
         res[p] = {"wgrad": bench_wgrad, "lmhead": bench_lmhead, "xent": bench_xent,
-                  "norm": bench_norm}[p]()
+                  "norm": bench_norm, "imgnorm": bench_imgnorm}[p]()
         print(json.dumps({p: res[p]}), flush=True)
 
 

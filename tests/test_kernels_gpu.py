@@ -164,6 +164,19 @@ def test_image_normalize(cuda_device):
     assert _rel(c, x.float() / 255) < 1e-2
 
 
+@pytest.mark.parametrize("C", [1, 3, 4])
+def test_image_normalize_vector_path(cuda_device, C):
+    """H*W % 16 == 0: the 16-pixels-per-thread kernel (16-byte loads/stores)."""
+    x = torch.randint(0, 256, (5, 224, 224, C), dtype=torch.uint8, device=cuda_device)
+    mean, std = [0.485, 0.456, 0.406, 0.5][:C], [0.229, 0.224, 0.225, 0.25][:C]
+    yr = ref.image_normalize(x.cpu(), mean, std)
+    y = rf.image_normalize(x, mean, std)
+    assert y.shape == (5, C, 224, 224)
+    assert torch.allclose(y.cpu(), yr, atol=1e-5)
+    yb = rf.image_normalize(x, mean, std, torch.bfloat16)
+    assert torch.allclose(yb.float().cpu(), yr, atol=2e-2, rtol=8e-3)
+
+
 @pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2)])
 def test_flash_attention_fwd_bwd(cuda_device, B, T, H):
     torch.manual_seed(9)

@@ -194,3 +194,21 @@ def test_learner_state_roundtrip_is_lossless():
     b = Learner(cfg, env.observation_space, env.action_space, device=torch.device("cpu"))
     b.set_state(st)
     assert torch.equal(a.flat.p32, b.flat.p32)
+
+
+def test_ppo_sample_async_overlaps_and_counts_exactly(cluster):
+    from ray_amd.rllib.algorithms import PPOConfig
+
+    cfg = (PPOConfig().environment("CartPole-v1")
+           .env_runners(num_env_runners=2, num_envs_per_env_runner=2, sample_async=True)
+           .learners(num_gpus_per_learner=0)
+           .training(train_batch_size=200, minibatch_size=100, num_epochs=1,
+                     model={"fcnet_hiddens": [16]}))
+    algo = cfg.build()
+    assert algo.config.rollout_fragment_length == 50  # auto: 200 / (2 runners x 2 envs)
+    for _ in range(3):
+        r = algo.train()
+        assert r["num_env_steps_sampled_this_iter"] == 200
+        assert "sample_wait_s" in r["learners"]
+    assert r["env_runners"]["num_episodes"] > 0
+    algo.stop()
