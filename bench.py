@@ -99,6 +99,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
             "bucket_mb": args.bucket_mb,
             "grad_dtype": r["grad_dtype"],
             "gemm_selection": r["gemm_selection"],
+            "wgrad_gemm": r.get("wgrad_gemm"),
             "launcher": mode,
         },
         "rccl_world_size": r["rccl_world_size"],

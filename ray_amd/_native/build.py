@@ -66,7 +66,10 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
             list(ex.map(cc, todo))
     if force or _newer(HIP_LIB, objs):
         tmp = HIP_LIB + ".tmp"
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+        # hipBLASLt (fp32-output GEMM selection, ops/csrc/gemm_lt.hip): SONAME
+        # libhipblaslt.so.1, resolved to the copy torch already loaded when imported after it
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
+             ["-L/opt/rocm/lib", "-lhipblaslt"])
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

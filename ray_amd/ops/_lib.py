@@ -61,6 +61,22 @@ _SIGS = {
     "ra_obsnorm_update": [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_void_p,
                           c_void_p],
     "ra_obsnorm_apply": [c_void_p] * 4 + [c_long, c_int, c_double, c_float, c_float, c_void_p],
+    "ra_lt_num_cands": [c_int, c_int] + [c_long] * 6,
+    "ra_lt_set_choice": [c_int, c_int] + [c_long] * 6 + [c_int],
+    "ra_lt_gemm": [c_int, c_int, c_long, c_long, c_long, c_void_p, c_long, c_void_p, c_long,
+                   c_void_p, c_long, c_float, c_float, c_void_p],
+    "ra_lt_tune": [c_int, c_int, c_long, c_long, c_long, c_void_p, c_long, c_void_p, c_long,
+                   c_void_p, c_long, c_int, c_void_p, c_int, c_long, c_long, c_long, c_void_p],
+    "ra_lt_gemm_batched": [c_int, c_int, c_long, c_long, c_long, c_void_p, c_long, c_long,
+                           c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_int, c_float,
+                           c_float, c_void_p],
+    "ra_lt_ep_num_cands": [c_int, c_int] + [c_long] * 6 + [c_int, c_long],
+    "ra_lt_ep_set_choice": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_int],
+    "ra_lt_gemm_ep": [c_int, c_int, c_long, c_long, c_long, c_void_p, c_long, c_void_p, c_long,
+                      c_void_p, c_long, c_int, c_void_p, c_void_p, c_long, c_int, c_void_p],
+    "ra_lt_num_cands_batched": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long],
+    "ra_lt_set_choice_batched": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long,
+                                                                  c_int],
     "ra_image_normalize": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                            c_int, c_void_p],
     "ra_resize_bilinear": [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p],

@@ -112,7 +112,36 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
   const float invD = 1.f / (float)D;
   const int stride = gridDim.x * 4;
-  for (int r0 = blockIdx.x * 4 + w; r0 < N; r0 += 2 * stride) {
+  const int step = 2 * stride;
+  // software pipeline: the next row pair's raw (packed bf16) loads are issued before the
+  // current pair is reduced, so each wave keeps two pairs of rows in flight
+  uint2 rx[2][VPL], rd[2][VPL], rr[2][VPL];
+  float rmu[2], rrs[2];  // the row statistics travel with the prefetched rows
+  auto load_pair = [&](int r0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = r0 + u * stride;
+      if (row < N) {
+        rmu[u] = mean[row];
+        rrs[u] = rstd[row];
+      }
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        const int col = (i * 64 + lane) * 4;
+        if (row < N && col < D) {
+          const size_t o = (size_t)row * D + col;
+          rx[u][i] = *reinterpret_cast<const uint2*>(x + o);
+          rd[u][i] = *reinterpret_cast<const uint2*>(dy + o);
+          if (dres) rr[u][i] = *reinterpret_cast<const uint2*>(dres + o);
+        }
+      }
+    }
+  };
+  constexpr bool PF = VPL <= 8;  // wider rows: the doubled register set would spill
+  int r0 = blockIdx.x * 4 + w;
+  if (PF && r0 < N) load_pair(r0);
+  for (; r0 < N; r0 += step) {
+    if (!PF) load_pair(r0);
     const int rows[2] = {r0, r0 + stride};
     float xv[2][VPL][4], dv[2][VPL][4], rv[2][VPL][4];
 #pragma unroll
@@ -122,10 +151,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       for (int i = 0; i < VPL; ++i) {
         const int col = (i * 64 + lane) * 4;
         if (ok && col < D) {
-          const size_t o = (size_t)rows[u] * D + col;
-          unpack4(*reinterpret_cast<const uint2*>(x + o), xv[u][i]);
-          unpack4(*reinterpret_cast<const uint2*>(dy + o), dv[u][i]);
-          if (dres) unpack4(*reinterpret_cast<const uint2*>(dres + o), rv[u][i]);
+          unpack4(rx[u][i], xv[u][i]);
+          unpack4(rd[u][i], dv[u][i]);
+          if (dres) unpack4(rr[u][i], rv[u][i]);
           else rv[u][i][0] = rv[u][i][1] = rv[u][i][2] = rv[u][i][3] = 0.f;
         } else {
 #pragma unroll
@@ -133,10 +161,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         }
       }
     }
+    const float cmu[2] = {rmu[0], rmu[1]}, crs[2] = {rrs[0], rrs[1]};
+    if (PF && r0 + step < N) load_pair(r0 + step);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (rows[u] >= N) break;
-      const float mu = mean[rows[u]], rs = rstd[rows[u]];
+      const float mu = cmu[u], rs = crs[u];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int i = 0; i < VPL; ++i)

@@ -7,6 +7,8 @@ fp32 references in ``ray_amd.ops.reference``.
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -261,6 +263,14 @@ def bias_residual(h, bias, res):
 
 
 # --------------------------------------------------------------------- linear (split-K wgrad)
+# Weight-gradient GEMMs (fp32 out): "lt-splitk" (default) = split-K fp32 partials from a
+# tuned strided-batched hipBLASLt GEMM (ops/lt.py) summed by ra_splitk_accum; "splitk" =
+# the same with torch.bmm's heuristic kernel; "lt" = one tuned GEMM accumulating straight
+# into the fp32 sink (beta = 1; measured slower at GPT-2 shapes: K = 65536 wants split-K)
+_WGRAD = os.environ.get("RAY_AMD_WGRAD", "lt-splitk")
+_WGRAD_LT = _WGRAD == "lt"
+
+
 def _splitk(M: int, N: int, K: int) -> int:
     """Token slices for the wgrad GEMM. Measured on MI355X at M = 65536 (GPT-2 small,
     profiles/r2_perf_bench.log): S = 16 is the fastest for every projection (qkv 0.28 ms
@@ -292,11 +302,23 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             S = _splitk(M, N, K)
-            if S > 1 or sink is not None:
+            if sink is not None and _sink_f32(sink) and _WGRAD_LT:
+                # hipBLASLt accumulates straight into the fp32 flat gradient (beta = 1),
+                # per-shape tuned solution (ops/lt.py)
+                from . import lt
+
+                lt.wgrad_accum(dy2, x2, sink.view(N, K))
+                _grad_done(w)
+            elif S > 1 or sink is not None:
                 # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into
                 # the flat gradient) by one HIP pass
-                part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K),
-                                 out_dtype=torch.float32)
+                if _WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous():
+                    from . import lt
+
+                    part = lt.wgrad_partials(dy2, x2, S)
+                else:
+                    part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2),
+                                     x2.view(S, M // S, K), out_dtype=torch.float32)
                 target = sink if sink is not None else torch.empty_like(w)
                 check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(target),
                                                  (1 if sink is not None else 0) |
@@ -414,8 +436,8 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         loss_rows = torch.empty(N, device=dev, dtype=torch.float32)
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         dh = torch.empty_like(h2) if need_grad else None
-        dw = torch.zeros(w.shape, device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] \
-            else None
+        dw = (torch.empty if _WGRAD_LT else torch.zeros)(
+            w.shape, device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] else None
         ch = max(1, min(chunk, N))
         buf = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
         L = _lib.lib()
@@ -429,7 +451,12 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
             if dh is not None:
                 torch.mm(lg, w, out=dh[s0:e])
             if dw is not None:
-                torch.addmm(dw, lg.t(), h2[s0:e], out_dtype=torch.float32, out=dw)
+                if _WGRAD_LT:
+                    from . import lt
+
+                    lt.wgrad_accum(lg, h2[s0:e], dw, beta=0.0 if s0 == 0 else 1.0)
+                else:
+                    torch.addmm(dw, lg.t(), h2[s0:e], out_dtype=torch.float32, out=dw)
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]

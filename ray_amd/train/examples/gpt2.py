@@ -101,6 +101,10 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
     tfile = tunableop_file(c["model"], c["micro_batch"], c["seq_len"])
     if on_gpu:
         gemm = setup_tunableop(c["tunableop"], tfile, rank)
+        if c["tunableop"] == "tune":
+            from ray_amd.ops import lt
+
+            lt.set_tuning(True)  # fp32-output wgrad GEMMs: ops/lt.py selector
     mcfg = getattr(GPT2Config, c["model"])()
     gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
     tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],
@@ -128,6 +132,13 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         else:
             torch.cuda.tunable.tuning_enable(False)
         gemm = "tunableop"
+    if on_gpu:
+        from ray_amd.ops import lt
+
+        if lt._tuning:  # tunableop=tune or RAY_AMD_LT_TUNE=1: keep the fp32-out choices
+            if rank == 0:
+                print(f"[gpt2] hipBLASLt fp32-out choices -> {lt.save()}", file=sys.stderr)
+            lt.set_tuning(False)
     if world > 1:
         dist.barrier()
     sync()
@@ -168,9 +179,19 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         "loss": loss,
         "ranks_in_sync": in_sync,
         "gemm_selection": gemm,
+        "wgrad_gemm": _wgrad_mode(on_gpu),
         "grad_dtype": c["grad_dtype"],
         "global_batch": c["micro_batch"] * c["grad_accum"] * world,
     }
+
+
+def _wgrad_mode(on_gpu: bool) -> str:
+    if not on_gpu:
+        return "torch"
+    from ray_amd.ops import functional as rf
+
+    return {"lt": "hipblaslt-lt-beta1", "lt-splitk": "splitk-partials-hipblaslt-tuned"}.get(
+        rf._WGRAD, "splitk-partials-torch-bmm")
 
 
 def train_func(config: dict):

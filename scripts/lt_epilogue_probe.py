@@ -1,0 +1,109 @@
+"""Probe hipBLASLt GELU epilogues for the GPT-2 MLP on one MI355X: support, numerics
+(tanh vs erf GELU) and time vs the current GEMM + HIP elementwise kernels.
+
+    python scripts/lt_epilogue_probe.py
+"""
+
+import json
+
+import torch
+
+from ray_amd.ops import _lib
+from ray_amd.ops import functional as rf
+from ray_amd.ops._lib import ptr, stream_ptr
+
+GELU_AUX_BIAS, DGELU_BGRAD = 164, 208
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def main(M=65536, C=768, F=3072):
+    L = _lib.lib()
+    dev, bf = "cuda", torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = (torch.randn(M, C, device=dev, generator=g)).to(bf)
+    wfc = (torch.randn(F, C, device=dev, generator=g) * 0.03).to(bf)
+    bfc = (torch.randn(F, device=dev, generator=g) * 0.1).to(bf)
+    wpr = (torch.randn(C, F, device=dev, generator=g) * 0.03).to(bf)
+    dout = (torch.randn(M, C, device=dev, generator=g)).to(bf)
+    out = {}
+    # ---- forward: a = gelu(x Wfc^T + b), aux = x Wfc^T + b
+    a = torch.empty(M, F, device=dev, dtype=bf)
+    aux = torch.empty(M, F, device=dev, dtype=bf)
+    shape = (1, 0, F, M, C, C, C, F)
+    n = L.ra_lt_ep_num_cands(*shape, GELU_AUX_BIAS, F)
+    out["fwd_cands"] = n
+    if n > 0:
+        pre = (x.float() @ wfc.float().t() + bfc.float())
+        L.ra_lt_gemm_ep(1, 0, F, M, C, ptr(wfc), C, ptr(x), C, ptr(a), F, GELU_AUX_BIAS,
+                        ptr(bfc), ptr(aux), F, -1, stream_ptr())
+        torch.cuda.synchronize()
+        out["fwd_aux_rel"] = rel(aux, pre)
+        out["fwd_rel_vs_tanh"] = rel(a, torch.nn.functional.gelu(pre, approximate="tanh"))
+        out["fwd_rel_vs_erf"] = rel(a, torch.nn.functional.gelu(pre))
+        best = None
+        for i in range(n):
+            t = timeit(lambda i=i: L.ra_lt_gemm_ep(1, 0, F, M, C, ptr(wfc), C, ptr(x), C, ptr(a),
+                                                   F, GELU_AUX_BIAS, ptr(bfc), ptr(aux), F, i,
+                                                   stream_ptr()), iters=5, warmup=1)
+            if best is None or t < best[1]:
+                best = (i, t)
+        out["fwd_best"] = best
+    h = torch.empty(M, F, device=dev, dtype=bf)
+    out["fwd_current_ms"] = timeit(lambda: rf.bias_gelu(torch.mm(x, wfc.t(), out=h), bfc))
+    out["fwd_gemm_only_ms"] = timeit(lambda: torch.mm(x, wfc.t(), out=h))
+    # ---- backward: dh = (dout Wpr) * gelu'(aux), db = colsum(dh)
+    dh = torch.empty(M, F, device=dev, dtype=bf)
+    db = torch.empty(F, device=dev, dtype=torch.float32)
+    shape = (0, 0, F, M, C, F, C, F)
+    n = L.ra_lt_ep_num_cands(*shape, DGELU_BGRAD, F)
+    out["bwd_cands"] = n
+    if n > 0 and "fwd_best" in out:
+        L.ra_lt_gemm_ep(0, 0, F, M, C, ptr(wpr), F, ptr(dout), C, ptr(dh), F, DGELU_BGRAD,
+                        ptr(db), ptr(aux), F, -1, stream_ptr())
+        torch.cuda.synchronize()
+        pre = aux.float().requires_grad_(True)
+        ga = dout.float() @ wpr.float()
+        y = torch.nn.functional.gelu(pre, approximate="tanh")
+        (ref_dh,) = torch.autograd.grad(y, pre, ga)
+        out["bwd_rel_dh"] = rel(dh, ref_dh)
+        out["bwd_rel_db"] = rel(db, ref_dh.sum(0))
+        best = None
+        for i in range(n):
+            t = timeit(lambda i=i: L.ra_lt_gemm_ep(0, 0, F, M, C, ptr(wpr), F, ptr(dout), C,
+                                                   ptr(dh), F, DGELU_BGRAD, ptr(db), ptr(aux),
+                                                   F, i, stream_ptr()), iters=5, warmup=1)
+            if best is None or t < best[1]:
+                best = (i, t)
+        out["bwd_best"] = best
+    ga16 = torch.empty(M, F, device=dev, dtype=bf)
+    work = torch.empty(L.ra_colsum_work(M, F), device=dev, dtype=torch.float32)
+    dbias = torch.empty(F, device=dev, dtype=torch.float32)
+
+    def cur():
+        torch.mm(dout, wpr, out=ga16)
+        L.ra_bias_gelu_bwd(ptr(ga16), ptr(h), ptr(bfc), ptr(dh), ptr(dbias), ptr(work), M, F, 2,
+                           stream_ptr())
+
+    out["bwd_current_ms"] = timeit(cur)
+    out["bwd_gemm_only_ms"] = timeit(lambda: torch.mm(dout, wpr, out=ga16))
+    print(json.dumps(out, indent=1), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -327,3 +327,40 @@ def test_residual_layer_norm(cuda_device):
     torch.autograd.backward([xr, yr], [gx, gy])
     for a, r in ((h, hr), (skip, sr), (rb, rbr), (w, wr), (b, br)):
         assert _rel(a.grad, r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 768, 768), (8192, 2304, 768), (4096, 3072, 768),
+                                   (4096, 768, 3072), (2048, 50304, 768)])
+def test_lt_wgrad_accum_matches_fp32(cuda_device, M, N, K):
+    """hipBLASLt fp32-output selector: out = dy^T x + out, beta 0 and 1, tuned and default."""
+    from ray_amd.ops import lt
+
+    g = torch.Generator(device=cuda_device).manual_seed(0)
+    dy = torch.randn(M, N, device=cuda_device, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=cuda_device, generator=g).to(torch.bfloat16)
+    ref_ = dy.float().t() @ x.float()
+    out = torch.full((N, K), 7.0, device=cuda_device)
+    lt.wgrad_accum(dy, x, out, beta=0.0)
+    assert _rel(out, ref_) < 1e-5
+    lt.wgrad_accum(dy, x, out, beta=1.0)
+    assert _rel(out, 2 * ref_) < 1e-5
+    lt.set_tuning(True)
+    try:
+        lt._applied.clear()
+        out2 = torch.zeros((N, K), device=cuda_device)
+        lt.wgrad_accum(dy, x, out2)
+        assert _rel(out2, ref_) < 1e-5
+    finally:
+        lt.set_tuning(False)
+
+
+def test_lt_wgrad_partials_match_fp32(cuda_device):
+    from ray_amd.ops import lt
+
+    g = torch.Generator(device=cuda_device).manual_seed(1)
+    dy = torch.randn(16384, 768, device=cuda_device, generator=g).to(torch.bfloat16)
+    x = torch.randn(16384, 2304, device=cuda_device, generator=g).to(torch.bfloat16)
+    part = lt.wgrad_partials(dy, x, 8)
+    assert part.shape == (8, 768, 2304)
+    ref_ = dy.float().view(8, 2048, 768).transpose(1, 2) @ x.float().view(8, 2048, 2304)
+    assert _rel(part, ref_) < 1e-5
