@@ -957,9 +957,13 @@ class CoreWorker:
 
         def done(oid, ref=ref):
             try:
-                fut.set_result(self._value_of(oid, None))
+                v = self._value_of(oid, None)
             except BaseException as e:  # noqa: BLE001
-                fut.set_exception(e)
+                if not fut.done():
+                    fut.set_exception(e)
+                return
+            if not fut.done():
+                fut.set_result(v)
 
         def cb(oid):
             threading.Thread(target=done, args=(oid,), daemon=True).start()
@@ -2050,7 +2054,19 @@ class CoreWorker:
                 loop = asyncio.get_running_loop()
                 args, kwargs = await loop.run_in_executor(None, self._decode_args, spec["args"],
                                                           owner)
-                if spec["nret"] == -1:
+                if spec["nret"] == -1 and inspect.isasyncgenfunction(
+                        getattr(fn, "__func__", fn)):
+                    # async generators run on the actor's own event loop (they may share
+                    # loop-bound state with the actor's other coroutines)
+                    gen = fn(*args, **kwargs)
+                    i = 0
+                    async for v in gen:
+                        ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
+                        self.send(owner, (P.STREAM_ITEM, tid, i, ret, self.node_hex))
+                        i += 1
+                    returns = []
+                    extra = {"num_items": i}
+                elif spec["nret"] == -1:
                     returns = await loop.run_in_executor(None, self._run_generator_async_bridge,
                                                          spec, fn, args, kwargs)
                     extra = {"num_items": self._last_gen_count}

@@ -84,6 +84,7 @@ _SIGS = {
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],
     "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "ra_attn_bwd_fused": [c_void_p] * 7 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],
     "ra_arena_open": [c_int, c_void_p, ctypes.POINTER(c_void_p)],

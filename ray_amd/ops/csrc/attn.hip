@@ -23,8 +23,12 @@
 // Tiles are double buffered: one barrier per tile; the next tile's global loads are
 // in flight during the current tile's MFMAs.
 //
-// Backward = two kernels (no float atomics; dQ would otherwise cost ~400 MB of
-// atomic adds per step at GPT-2 shape, far above the chip's atomic rate):
+// Backward, split form (ra_attn_bwd, default: no float atomics) = two kernels below; fused
+// form (ra_attn_bwd_fused) = attn_bwd_dkdv_kernel<true>: dQ from the same pass through
+// LDS-staged dS and fp32 atomics. Measured at B64 T1024 H12 (rocprofv3): split 384 + 337 us,
+// fused 730 us (436 without the dQ product, 606 with plain stores instead of atomics): the
+// 16 KB of fp32 dQ per workgroup x q-tile (0.9 GB per call) costs more than recomputing S
+// and dP at head_dim 64, so the fused form stays opt-in (RAY_AMD_ATTN_BWD=fused):
 //   attn_bwd_dkdv : one workgroup per 128 keys, each wave owns 32 keys; loops over
 //                   the causal q tiles: S = Q·K^T, dP = dO·V^T (keys on lanes), then
 //                   dV += P^T·dO and dK += dS^T·Q with P / dS as A operands. The
@@ -307,13 +311,24 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 // dK, dV: workgroup = 128 keys of one (b, h); wave owns 32 keys.
+// FUSED: the same pass also produces dQ. Each tile's dS (bf16) is staged once in LDS as a
+// [128 keys][64 q] image beside a [128 keys][64 d] image of the workgroup's K, and after a
+// barrier wave w computes the 32 x 32 block (q half w>>1, d half w&1) of dQ_tile = dS K
+// over all 128 keys (8 MFMAs) and adds it to an fp32 dQ workspace with no-return float
+// atomics (two 128-B row segments per instruction: the full-rate shape). This replaces the
+// separate dq kernel, which recomputed S and dP (2 of its 3 MFMA products) from scratch.
+template <bool FUSED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-    int T, int H, float sc_log2, float scale) {
-  // [buf][Q, dO] images, then per buf 64 x (-lse/c) and 64 x (-delta)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS + 2 * 2 * 64 * 2];
+    float* __restrict__ dq_ws, int T, int H, float sc_log2, float scale, int dbg) {
+  // [buf][Q, dO] images, then per buf 64 x (-lse/c) and 64 x (-delta); FUSED: + K image
+  // [128][64] and dS^T image [128][64]
+  __shared__ __attribute__((aligned(16)))
+  bf16_t lds[2 * 2 * TILE_ELEMS + 2 * 2 * 64 * 2 + (FUSED ? 4 * TILE_ELEMS : 0)];
   float* rowc = reinterpret_cast<float*>(lds + 4 * TILE_ELEMS);  // [buf][2][64]
+  bf16_t* Kimg = lds + 4 * TILE_ELEMS + 512;
+  bf16_t* dsT = Kimg + 2 * TILE_ELEMS;
   const int nkb = T / 128;
   const int L = xcd_block(blockIdx.x, gridDim.x);
   const int kb = L % nkb;  // kb 0 = most q tiles: heaviest first
@@ -327,11 +342,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const LaneOffs lo(lane);
   const int kv0 = kb * 128;
   const int key = kv0 + 32 * w + r;  // this lane's key (C-tile column)
-  bf16x8_t kf[4], vf[4];
+  // FUSED: this wave's K operand is read from the K image (frees 16 VGPRs: the fused
+  // pass is at the 256-register cap and spill reloads would drain the dQ atomics)
+  bf16x8_t kf[FUSED ? 1 : 4], vf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
-    kf[kk] = ld8(base + C + (long)key * tok + 16 * kk + 8 * hh);
+    if (!FUSED) kf[kk] = ld8(base + C + (long)key * tok + 16 * kk + 8 * hh);
     vf[kk] = ld8(base + 2 * C + (long)key * tok + 16 * kk + 8 * hh);
+  }
+  if (FUSED) {  // K rows kv0..kv0+127 -> swizzled image (visible after the first barrier)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = threadIdx.x + 256 * j, row = c >> 3, ch = c & 7;
+      *reinterpret_cast<u32x4*>(Kimg + img_off(row, ch)) =
+          *reinterpret_cast<const u32x4*>(base + C + (long)(kv0 + row) * tok + ch * 8);
+    }
   }
   f32x16 dv[2] = {}, dk[2] = {};
   const int t0 = kv0 / 64;
@@ -381,7 +406,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-          s = mfma32(ld8(Qs + 2048 * qt + lo.row[kk]), kf[kk], s);
+          s = mfma32(ld8(Qs + 2048 * qt + lo.row[kk]),
+                     FUSED ? ld8(Kimg + 2048 * w + lo.row[kk]) : kf[FUSED ? 0 : kk], s);
           dp = mfma32(ld8(Ds + 2048 * qt + lo.row[kk]), vf[kk], dp);
         }
 #pragma unroll
@@ -390,6 +416,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           if (diag && key > q0 + 32 * qt + crow(i, hh)) p = 0.f;
           s[i] = p;              // P
           dp[i] = p * dp[i];     // dS (wrt scaled scores)
+        }
+        if (FUSED) {  // dS^T rows = this lane's key, 4 consecutive q per 8-byte write
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float v4[4] = {dp[4 * g], dp[4 * g + 1], dp[4 * g + 2], dp[4 * g + 3]};
+            *reinterpret_cast<uint2*>(dsT + img_off(32 * w + r, 4 * qt + g) + 4 * hh) =
+                pack4(v4);
+          }
         }
         // dV += P^T dO ; dK += dS^T Q   (P / dS registers as A operands, k = q)
 #pragma unroll
@@ -411,11 +445,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (q0 + 63 >= wave_kmin) {
       if (q0 < wave_kmin + 31) body(t, std::true_type{});
       else body(t, std::false_type{});
+    } else if (FUSED) {  // every key of this wave is after every query of the tile: dS = 0
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        *reinterpret_cast<uint2*>(dsT + img_off(32 * w + r, c) + 4 * hh) = make_uint2(0, 0);
     }
+  };
+  const int qh = w >> 1, dh = w & 1;  // FUSED: this wave's dQ block
+  float* dq_bh = FUSED ? dq_ws + (long)bh * T * HD : nullptr;
+  auto dq_tile = [&](int t) __attribute__((always_inline)) {
+    f32x16 acc = {};
+#pragma unroll 2  // bounded fragment prefetch: keeps the pass under the register cap
+    for (int ks = 0; ks < 8; ++ks)
+      acc = mfma32(tr_frag(dsT, lo, 16 * ks, qh), tr_frag(Kimg, lo, 16 * ks, dh), acc);
+    float* g = dq_bh + (long)(t * 64 + 32 * qh) * HD + 32 * dh + r;
+    if (dbg & 1) {  // diagnostic (ra_knobs[6]): plain stores instead of atomics
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[crow(i, hh) * HD] = acc[i];
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) unsafeAtomicAdd(g + crow(i, hh) * HD, acc[i]);
   };
   auto step = [&](int t, QD& held, QD& next) __attribute__((always_inline)) {
     if (t + 2 < ntiles) load_qd(next, t + 2);
     compute(t);
+    if (FUSED) {
+      __syncthreads();  // dS^T image complete
+      if (!(dbg & 2)) dq_tile(t);
+    }
     if (t + 1 < ntiles) store_qd(held, t + 1);
     __syncthreads();
   };
@@ -546,6 +604,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     }
 }
 
+// dqkv[b, t, 0, h, :] = bf16(scale * dq_ws[b, h, t, :]); one thread per 8 head dims,
+// threads ordered by the OUTPUT (contiguous 16-B stores, 32-B contiguous reads)
+__global__ __launch_bounds__(256) void attn_dq_convert_kernel(const float* __restrict__ ws,
+                                                              bf16_t* __restrict__ dqkv, long n8,
+                                                              int T, int H, float scale) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const int c8 = (int)(i & 7);
+  const long row = i >> 3;  // (b*T + t)*H + h
+  const int h = (int)(row % H);
+  const long bt = row / H;
+  const long b = bt / T, t = bt - b * T;
+  const float* src = ws + ((b * H + h) * T + t) * HD + 8 * c8;
+  const float4 x0 = *reinterpret_cast<const float4*>(src);
+  const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+  float v[8] = {x0.x * scale, x0.y * scale, x0.z * scale, x0.w * scale,
+                x1.x * scale, x1.y * scale, x1.z * scale, x1.w * scale};
+  *reinterpret_cast<uint4*>(dqkv + bt * 3L * H * HD + (long)h * HD + 8 * c8) = pack8(v);
+}
+
 static inline bool attn_shape_ok(int T, int D) { return D == HD && T % 128 == 0 && T >= 128; }
 
 RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, int D,
@@ -566,11 +644,31 @@ RA_EXPORT int ra_attn_bwd(const void* qkv, const void* out, const void* dout, co
   const long rows = (long)B * T * H;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
-                     sc_log2, scale);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
+                     (float*)nullptr, T, H, sc_log2, scale, 0);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
                      sc_log2, scale);
+  return hipGetLastError();
+}
+
+// Fused backward: dK, dV and dQ in one pass over the key blocks (see attn_bwd_dkdv_kernel).
+// dq_ws: B*H*T*64 floats of workspace (zeroed here).
+RA_EXPORT int ra_attn_bwd_fused(const void* qkv, const void* out, const void* dout,
+                                const float* lse, float* delta, float* dq_ws, void* dqkv, int B,
+                                int T, int H, int D, float scale, hipStream_t st) {
+  if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
+  const float sc_log2 = scale * 1.4426950408889634f;
+  const long rows = (long)B * T * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                     (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
+  (void)hipMemsetAsync(dq_ws, 0, (size_t)rows * HD * sizeof(float), st);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, dq_ws,
+                     T, H, sc_log2, scale, ra_knobs[6]);
+  const long n8 = rows * 8;
+  hipLaunchKernelGGL(attn_dq_convert_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
+                     st, (const float*)dq_ws, (bf16_t*)dqkv, n8, T, H, scale);
   return hipGetLastError();
 }

@@ -268,6 +268,12 @@ def bias_residual(h, bias, res):
 # the same with torch.bmm's heuristic kernel; "lt" = one tuned GEMM accumulating straight
 # into the fp32 sink (beta = 1; measured slower at GPT-2 shapes: K = 65536 wants split-K)
 _WGRAD = os.environ.get("RAY_AMD_WGRAD", "lt-splitk")
+# attention backward: "split" (dkdv + dq kernels, no atomics, bitwise reproducible dQ) or
+# "fused" (dK, dV, dQ in one pass with fp32 dQ atomics). Measured at GPT-2 small, B 64
+# (profiles/r2/attn_bwd_fused_vs_split.md): split 384 + 337 us, fused 730 us — the fused
+# pass moves 0.9 GB of fp32 dQ partial sums (16 KB per workgroup x q-tile) against the
+# split dq kernel's 100 MB, which outweighs the S / dP recompute it saves at head_dim 64
+_ATTN_BWD = os.environ.get("RAY_AMD_ATTN_BWD", "split")
 _WGRAD_LT = _WGRAD == "lt"
 
 
@@ -365,8 +371,15 @@ class _FlashAttnQKV(torch.autograd.Function):
         dout = dout.contiguous()
         dqkv = torch.empty_like(qkv)
         delta = torch.empty((B, H, T), device=qkv.device, dtype=torch.float32)
-        check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
-                                     ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()), "attn_bwd")
+        if _ATTN_BWD == "fused":  # one pass: dK, dV + dQ through fp32 atomics
+            dq_ws = torch.empty((B * H * T * D,), device=qkv.device, dtype=torch.float32)
+            check(_lib.lib().ra_attn_bwd_fused(ptr(qkv), ptr(out), ptr(dout), ptr(lse),
+                                               ptr(delta), ptr(dq_ws), ptr(dqkv), B, T, H, D,
+                                               ctx.scale, stream_ptr()), "attn_bwd_fused")
+        else:
+            check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
+                                         ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()),
+                  "attn_bwd")
         return dqkv, None
 
 

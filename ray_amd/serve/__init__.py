@@ -5,4 +5,5 @@ from ray_amd.serve.api import (Application, Deployment, delete, deployment,  # n
                                get_replica_context, gRPCOptions, ingress, multiplexed, run, shutdown, start,
                                status)
 from ray_amd.serve.batching import batch  # noqa: F401
-from ray_amd.serve.handle import DeploymentHandle, DeploymentResponse  # noqa: F401
+from ray_amd.serve.handle import (DeploymentHandle, DeploymentResponse,  # noqa: F401
+                                  DeploymentResponseGenerator)

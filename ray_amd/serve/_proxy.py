@@ -1,8 +1,13 @@
-"""HTTP proxy actor (reference: python/ray/serve/_private/proxy.py, proxy_router.py).
+"""HTTP proxy actor (reference: python/ray/serve/_private/proxy.py, proxy_router.py;
+``send_request_to_replica`` streaming path, proxy.py:518).
 
-Runs uvicorn + a raw ASGI app in a background thread inside an actor; each
-request is matched by longest route prefix and forwarded to the ingress
-deployment's replica (``handle_http``) chosen by the handle router."""
+Runs uvicorn + a raw ASGI app on its own event loop inside an actor; each request is
+matched by longest route prefix and forwarded to the ingress deployment's replica
+chosen by the handle router. Forwarding is fully asynchronous: the route table and
+replica set are refreshed with awaited controller calls, and the response comes back
+as a streaming generator (``handle_http_streaming``) whose messages are written to the
+client as they arrive (chunked transfer for streamed bodies) — no blocking ``ray.get``
+and no thread per request."""
 
 from __future__ import annotations
 
@@ -17,19 +22,12 @@ class HTTPProxy:
         self.port = port
         self.routes = {}
         self.routes_ts = 0.0
+        self.inflight = 0
         self.ready = threading.Event()
         self.error = None
         t = threading.Thread(target=self._serve, daemon=True)
         t.start()
         self.ready.wait(30)
-
-    def _refresh(self):
-        if time.time() - self.routes_ts > 0.5:
-            import ray_amd as ray
-            from ray_amd.serve.api import _get_controller
-
-            self.routes = ray.get(_get_controller().get_routes.remote())
-            self.routes_ts = time.time()
 
     def _match(self, path):
         best = None
@@ -39,6 +37,13 @@ class HTTPProxy:
                 if best is None or len(p) > len(best[0]):
                     best = (p, target)
         return best
+
+    async def _arefresh(self):
+        if time.time() - self.routes_ts > 0.5:
+            from ray_amd.serve.api import _get_controller
+
+            self.routes = await _get_controller().get_routes.remote()
+            self.routes_ts = time.time()
 
     async def _app(self, scope, receive, send):
         if scope["type"] == "lifespan":
@@ -57,40 +62,60 @@ class HTTPProxy:
             body += m.get("body", b"")
             if not m.get("more_body"):
                 break
-        loop = asyncio.get_running_loop()
+        started = False
         try:
-            await loop.run_in_executor(None, self._refresh)
+            await self._arefresh()
             hit = self._match(scope["path"])
+            if hit is None:  # a route deployed since the last refresh: look again once
+                self.routes_ts = 0.0
+                await self._arefresh()
+                hit = self._match(scope["path"])
             if hit is None:
-                status, headers, out = 404, [("content-type", "text/plain")], \
-                    f"Path '{scope['path']}' not found".encode()
-            else:
-                prefix, (app_name, ingress) = hit
-                fwd = {k: v for k, v in scope.items() if k in ("method", "path", "query_string",
-                                                               "headers", "type",
-                                                               "http_version", "scheme")}
-                fwd["headers"] = [(k.decode(), v.decode()) for k, v in scope.get("headers", [])]
-                if prefix != "/":
-                    fwd["root_path"] = ""
-                    fwd["path"] = scope["path"][len(prefix):] or "/"
-                status, headers, out = await loop.run_in_executor(
-                    None, self._forward, app_name, ingress, fwd, body)
+                await self._reply(send, 404, [("content-type", "text/plain")],
+                                  f"Path '{scope['path']}' not found".encode())
+                return
+            prefix, (app_name, ingress) = hit
+            fwd = {k: v for k, v in scope.items() if k in ("method", "path", "query_string",
+                                                           "headers", "type", "http_version",
+                                                           "scheme")}
+            fwd["headers"] = [(k.decode(), v.decode()) for k, v in scope.get("headers", [])]
+            if prefix != "/":
+                fwd["root_path"] = ""
+                fwd["path"] = scope["path"][len(prefix):] or "/"
+            from ray_amd.serve.handle import _router
+
+            r = _router(app_name, ingress)
+            rid, h = await r.achoose()
+            self.inflight += 1
+            try:
+                gen = h.handle_http_streaming.remote(fwd, body)
+                async for ref in gen:
+                    msg = await ref
+                    if msg[0] == "start":
+                        await send({"type": "http.response.start", "status": msg[1],
+                                    "headers": [(k.encode(), v.encode()) for k, v in msg[2]]})
+                        started = True
+                    else:
+                        await send({"type": "http.response.body", "body": msg[1],
+                                    "more_body": True})
+                if not started:
+                    raise RuntimeError("replica produced no response")
+                await send({"type": "http.response.body", "body": b"", "more_body": False})
+            finally:
+                self.inflight -= 1
+                r.done(rid)
         except Exception as e:  # noqa: BLE001
-            status, headers, out = 500, [("content-type", "text/plain")], repr(e).encode()
+            if not started:
+                await self._reply(send, 500, [("content-type", "text/plain")], repr(e).encode())
+
+    @staticmethod
+    async def _reply(send, status, headers, out):
         await send({"type": "http.response.start", "status": status,
                     "headers": [(k.encode(), v.encode()) for k, v in headers]})
         await send({"type": "http.response.body", "body": out})
 
-    def _forward(self, app_name, ingress, scope, body):
-        import ray_amd as ray
-        from ray_amd.serve.handle import _router
-
-        r = _router(app_name, ingress)
-        rid, h = r.choose()
-        try:
-            return ray.get(h.handle_http.remote(scope, body))
-        finally:
-            r.done(rid)
+    def num_inflight(self):
+        return self.inflight
 
     def _serve(self):
         try:

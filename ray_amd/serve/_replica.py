@@ -69,6 +69,88 @@ async def _call_asgi(app, scope, body):
     return sent["status"], sent["headers"], sent["body"]
 
 
+def _chunk_bytes(c):
+    if isinstance(c, bytes):
+        return c
+    if isinstance(c, str):
+        return c.encode()
+    import json
+
+    return json.dumps(c).encode()
+
+
+def _streaming_body(result):
+    """(status, headers, async iterator of bytes) for streamed results, else None."""
+    try:
+        from starlette.responses import StreamingResponse
+
+        if isinstance(result, StreamingResponse):
+            async def it():
+                async for c in result.body_iterator:
+                    yield _chunk_bytes(c)
+
+            return (result.status_code, [(k, v) for k, v in result.headers.items()], it())
+    except ImportError:
+        pass
+    if inspect.isasyncgen(result):
+        async def ait():
+            async for c in result:
+                yield _chunk_bytes(c)
+
+        return 200, [("content-type", "text/plain; charset=utf-8")], ait()
+    if inspect.isgenerator(result):
+        async def git():
+            for c in result:
+                yield _chunk_bytes(c)
+
+        return 200, [("content-type", "text/plain; charset=utf-8")], git()
+    return None
+
+
+async def _stream_asgi(app, scope, body):
+    """Run an ASGI app, yielding response messages as it sends them."""
+    q: asyncio.Queue = asyncio.Queue()
+    chunks = [body]
+
+    async def receive():
+        if chunks:
+            return {"type": "http.request", "body": chunks.pop(), "more_body": False}
+        await asyncio.sleep(3600)
+        return {"type": "http.disconnect"}
+
+    async def send(msg):
+        await q.put(msg)
+
+    s = dict(scope)
+    s.setdefault("type", "http")
+    s.setdefault("asgi", {"version": "3.0"})
+    s.setdefault("http_version", "1.1")
+    s.setdefault("scheme", "http")
+    s.setdefault("server", ("127.0.0.1", 8000))
+    s.setdefault("client", ("127.0.0.1", 0))
+    s.setdefault("root_path", "")
+    s["headers"] = [(k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str)
+                     else v) for k, v in s.get("headers", [])]
+    task = asyncio.ensure_future(app(s, receive, send))
+    done_sentinel = object()
+    task.add_done_callback(lambda t: q.put_nowait(done_sentinel))
+    while True:
+        msg = await q.get()
+        if msg is done_sentinel:
+            break
+        if msg["type"] == "http.response.start":
+            yield ("start", msg["status"],
+                   [(k.decode(), v.decode()) for k, v in msg.get("headers", [])])
+        elif msg["type"] == "http.response.body":
+            b = msg.get("body", b"")
+            if b:
+                yield ("body", b)
+            if not msg.get("more_body"):
+                break
+    if task.done() and task.exception() is not None:
+        raise task.exception()
+
+
 def _to_http_response(result):
     import json
 
@@ -177,6 +259,60 @@ class Replica:
             if inspect.isawaitable(r):
                 r = await r
             return _to_http_response(r)
+        finally:
+            self.ongoing -= 1
+
+    async def handle_request_streaming(self, method_name, args, kwargs, multiplexed_model_id=""):
+        """Streaming variant (handle.options(stream=True)): yields each item the user's
+        generator / async generator produces as its own stream element."""
+        from ray_amd.serve import context
+
+        self.ongoing += 1
+        self.total += 1
+        token = context._set_request_context(multiplexed_model_id)
+        try:
+            fn = self.obj if self.is_function else getattr(self.obj, method_name or "__call__")
+            r = fn(*args, **kwargs)
+            if inspect.isawaitable(r):
+                r = await r
+            if inspect.isasyncgen(r):
+                async for x in r:
+                    yield x
+            elif inspect.isgenerator(r):
+                for x in r:
+                    yield x
+            else:
+                yield r
+        finally:
+            context._reset_request_context(token)
+            self.ongoing -= 1
+
+    async def handle_http_streaming(self, scope, body):
+        """HTTP with streamed responses: yields ("start", status, headers) then
+        ("body", chunk) messages as the application produces them (ASGI apps: every
+        ``http.response.body`` send; StreamingResponse / generator results: every chunk)."""
+        self.ongoing += 1
+        self.total += 1
+        try:
+            if self.asgi is not None:
+                async for m in _stream_asgi(self.asgi, scope, body):
+                    yield m
+                return
+            req = _Request(scope, body)
+            fn = self.obj if self.is_function else getattr(self.obj, "__call__")
+            r = fn(req)
+            if inspect.isawaitable(r):
+                r = await r
+            it = _streaming_body(r)
+            if it is not None:
+                status, headers, chunks = it
+                yield ("start", status, headers)
+                async for c in chunks:
+                    yield ("body", c)
+                return
+            status, headers, out = _to_http_response(r)
+            yield ("start", status, headers)
+            yield ("body", out)
         finally:
             self.ongoing -= 1
 

@@ -47,6 +47,33 @@ class _Router:
                 self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
             self.max_ongoing = mo
 
+    async def arefresh(self, force=False):
+        now = time.time()
+        if not force and self.replicas and now - self.last_refresh < 1.0:
+            return
+        info = await self._controller().get_replicas.remote(self.app, self.dep)
+        self.last_refresh = now
+        if info is None:
+            raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
+        version, reps, mo = info
+        with self.lock:
+            if version != self.version:
+                self.version = version
+                self.replicas = reps
+                self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
+            self.max_ongoing = mo
+
+    async def achoose(self):
+        """choose() for event loops: the replica-set refresh is awaited, never blocks."""
+        deadline = time.time() + 30
+        await self.arefresh()
+        while not self.replicas:
+            if time.time() > deadline:
+                raise RuntimeError(f"no replicas available for {self.dep}")
+            await asyncio.sleep(0.05)
+            await self.arefresh(force=True)
+        return self._pick()
+
     def choose(self):
         deadline = time.time() + 30
         while True:
@@ -59,6 +86,11 @@ class _Router:
                 raise RuntimeError(f"no replicas available for {self.dep}")
             time.sleep(0.05)
             self.refresh(force=True)
+        return self._pick()
+
+    def _pick(self):
+        with self.lock:
+            reps = list(self.replicas)
         if len(reps) == 1:
             rid, h = reps[0]
         else:
@@ -131,6 +163,53 @@ def _resolve(ref):
     return ref
 
 
+class DeploymentResponseGenerator:
+    """Streaming response (``handle.options(stream=True)``): iterate (sync or async) to
+    receive each item the deployment's generator yields, as it is produced."""
+
+    def __init__(self, gen, router, rid):
+        self._gen = gen
+        self._router = router
+        self._rid = rid
+        self._done = False
+
+    def _finish(self):
+        if not self._done:
+            self._done = True
+            self._router.done(self._rid)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        try:
+            ref = next(self._gen)
+        except StopIteration:
+            self._finish()
+            raise
+        return ray.get(ref)
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        try:
+            ref = await self._gen.__anext__()
+        except StopAsyncIteration:
+            self._finish()
+            raise
+        return await ref
+
+    def cancel(self):
+        self._finish()
+
+    def __del__(self):
+        try:
+            self._finish()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 class DeploymentHandle:
     def __init__(self, deployment_name: str, app_name: str = "default", *, method_name=None,
                  multiplexed_model_id: str = "", stream: bool = False):
@@ -159,6 +238,10 @@ class DeploymentHandle:
         args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
         kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v)
                   for k, v in kwargs.items()}
+        if self._stream:
+            gen = h.handle_request_streaming.remote(self._method or "__call__", args, kwargs,
+                                                    self._mux)
+            return DeploymentResponseGenerator(gen, r, rid)
         ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
         return DeploymentResponse(ref, r, rid)
 

@@ -177,8 +177,10 @@ def test_image_normalize_vector_path(cuda_device, C):
     assert torch.allclose(yb.float().cpu(), yr, atol=2e-2, rtol=8e-3)
 
 
-@pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2)])
-def test_flash_attention_fwd_bwd(cuda_device, B, T, H):
+@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2), (2, 128, 1)])
+def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch):
+    monkeypatch.setattr(rf, "_ATTN_BWD", mode)
     torch.manual_seed(9)
     D = 64
     qkv = torch.randn(B, T, 3, H, D, device=cuda_device).bfloat16().requires_grad_()

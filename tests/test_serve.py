@@ -144,3 +144,93 @@ def test_fastapi_ingress(cluster):
     assert r.status_code == 200 and r.json() == {"answer": 42}, r.text
     serve.delete("api")
     assert "api" not in serve.status()
+
+
+def test_handle_streaming(cluster):
+    @serve.deployment
+    class Streamer:
+        def __call__(self, n):
+            for i in range(n):
+                yield i * i
+
+        async def agen(self, n):
+            for i in range(n):
+                await asyncio.sleep(0.01)
+                yield f"tok{i}"
+
+    h = serve.run(Streamer.bind(), name="stream", route_prefix=None)
+    assert list(h.options(stream=True).remote(5)) == [0, 1, 4, 9, 16]
+
+    async def consume():
+        return [x async for x in h.options(stream=True, method_name="agen").remote(3)]
+
+    assert asyncio.run(consume()) == ["tok0", "tok1", "tok2"]
+    serve.delete("stream")
+
+
+def test_http_streaming_responses(cluster):
+    from fastapi import FastAPI
+    from fastapi.responses import StreamingResponse
+
+    app = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(app)
+    class Chat:
+        @app.get("/gen")
+        def gen(self, n: int = 4):
+            def chunks():
+                for i in range(n):
+                    time.sleep(0.2)
+                    yield f"chunk{i}\n"
+
+            return StreamingResponse(chunks(), media_type="text/plain")
+
+    serve.run(Chat.bind(), name="chat", route_prefix="/chat")
+    t0 = time.time()
+    with requests.get("http://127.0.0.1:18123/chat/gen?n=4", stream=True, timeout=30) as r:
+        assert r.status_code == 200
+        arrivals = []
+        for line in r.iter_lines():
+            if line:
+                arrivals.append((line.decode(), time.time() - t0))
+    assert [a for a, _ in arrivals] == [f"chunk{i}" for i in range(4)]
+    # streamed: the first chunk arrives well before the last one was produced
+    assert arrivals[0][1] < arrivals[-1][1] - 0.3
+
+    @serve.deployment
+    def plain(request):
+        def g():
+            yield "a"
+            yield "b"
+
+        return g()
+
+    serve.run(plain.bind(), name="plain", route_prefix="/plain")
+    r = requests.get("http://127.0.0.1:18123/plain", timeout=10)
+    assert r.text == "ab"
+    serve.delete("chat")
+    serve.delete("plain")
+
+
+def test_proxy_concurrency_not_thread_bound(cluster):
+    """64 concurrent slow requests complete in about one request's latency: the proxy
+    forwards asynchronously instead of parking a thread per request."""
+    import concurrent.futures as cf
+
+    @serve.deployment(max_ongoing_requests=100)
+    class Slow:
+        async def __call__(self, request):
+            await asyncio.sleep(0.5)
+            return "ok"
+
+    serve.run(Slow.bind(), name="slow", route_prefix="/slow")
+    requests.get("http://127.0.0.1:18123/slow", timeout=10)
+    t0 = time.time()
+    with cf.ThreadPoolExecutor(64) as ex:
+        rs = list(ex.map(lambda _: requests.get("http://127.0.0.1:18123/slow", timeout=30).text,
+                         range(64)))
+    dt = time.time() - t0
+    assert rs == ["ok"] * 64
+    assert dt < 3.0, dt
+    serve.delete("slow")
