@@ -2,6 +2,8 @@
 
 from ray_amd._private.serialization import (deregister_serializer,  # noqa: F401
                                             register_serializer)
+from ray_amd.util import iter  # noqa: F401,A004
+from ray_amd.util.actor_group import ActorGroup  # noqa: F401
 from ray_amd.util.actor_pool import ActorPool  # noqa: F401
 from ray_amd.util.placement_group import (get_current_placement_group,  # noqa: F401
                                           get_placement_group, placement_group,
@@ -29,7 +31,7 @@ def inspect_serializability(obj, name=None, depth=3, print_file=None):
         return False, {repr(e)}
 
 
-__all__ = ["ActorPool", "placement_group", "placement_group_table", "get_placement_group",
+__all__ = ["ActorPool", "ActorGroup", "iter", "placement_group", "placement_group_table", "get_placement_group",
            "remove_placement_group", "get_current_placement_group", "register_serializer",
            "deregister_serializer", "get_node_ip_address", "list_named_actors",
            "inspect_serializability"]

@@ -199,3 +199,58 @@ def test_internal_kv(cluster):
     kv._internal_kv_del(b"k")
     assert kv._internal_kv_get(b"k") is None
 
+
+
+class _Member:
+    def __init__(self, base):
+        self.base = base
+
+    def add(self, x):
+        return self.base + x
+
+    def get_actor_metadata(self):
+        return {"base": self.base}
+
+
+def test_actor_group(cluster):
+    from ray_amd.util.actor_group import ActorGroup
+
+    g = ActorGroup(_Member, num_actors=3, num_cpus_per_actor=0, init_args=(10,))
+    assert len(g) == 3 and g.actor_metadata == [{"base": 10}] * 3
+    assert ray.get(g.add.remote(5)) == [15, 15, 15]
+    g.add_actors(1)
+    assert len(g) == 4
+    g.remove_actors([0])
+    assert len(g) == 3
+    assert ray.get(g[0].actor.add.remote(1)) == 11
+    g.shutdown(patience_s=5)
+    assert len(g) == 0
+    with pytest.raises(RuntimeError):
+        g.add.remote(1)
+
+
+def test_parallel_iterator(cluster):
+    from ray_amd.util import iter as rit
+
+    it = rit.from_range(20, num_shards=4)
+    assert it.num_shards() == 4
+    assert sorted(it.gather_sync()) == list(range(20))
+    sq = it.for_each(lambda x: x * x).filter(lambda x: x % 2 == 0)
+    assert sorted(sq.gather_async()) == sorted(x * x for x in range(20) if x % 2 == 0)
+    assert sorted(sum(it.batch(3).gather_sync(), [])) == list(range(20))
+    rows = list(rit.from_items([1, 2, 3, 4], num_shards=2).batch_across_shards())
+    assert rows == [[1, 2], [3, 4]]
+    rep = it.repartition(2)
+    assert rep.num_shards() == 2 and sorted(rep.gather_sync()) == list(range(20))
+    u = rit.from_items([1, 2], num_shards=1).union(rit.from_items([3], num_shards=1))
+    assert sorted(u.gather_sync()) == [1, 2, 3]
+    s0 = it.get_shard(0)
+    assert list(s0) == list(range(5))
+    loc = it.gather_sync().for_each(lambda x: x + 1).batch(5).take(2)
+    assert len(loc) == 2 and all(len(b) == 5 for b in loc)
+    a, b = rit.from_range(6, num_shards=1).gather_sync().duplicate(2)
+    assert list(a) == list(range(6)) and list(b) == list(range(6))
+    shuf = list(rit.from_range(50, num_shards=2).local_shuffle(10, seed=0).gather_sync())
+    assert sorted(shuf) == list(range(50)) and shuf != sorted(shuf)
+    rep_it = rit.from_items([1, 2], num_shards=1, repeat=True).gather_sync().take(5)
+    assert rep_it == [1, 2, 1, 2, 1]
