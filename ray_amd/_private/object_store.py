@@ -83,7 +83,7 @@ class ObjectStore:
         try:
             mv = self.store.buffer(off, sobj.total)
             try:
-                sobj.write_to(mv)
+                sobj.write_to(mv, lambda o, b: self.store.write(off + o, b))
             finally:
                 mv.release()
         except BaseException:

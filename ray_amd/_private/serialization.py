@@ -169,7 +169,9 @@ class SerializedObject:
         self._layout = layout
         self.total = off
 
-    def write_to(self, mv) -> None:
+    def write_to(self, mv, big_copy=None) -> None:
+        """Lay the object out in `mv`. big_copy(offset, buffer), if given, moves the
+        out-of-band buffers of 16 MiB and more (the store's multi-threaded copy)."""
         _HDR.pack_into(mv, 0, _MAGIC, self.kind, len(self.buffers), 0, len(self.inband))
         p = _HDR.size
         for off, n in self._layout:
@@ -178,7 +180,10 @@ class SerializedObject:
         mv[p:p + len(self.inband)] = self.inband
         for (off, n), b in zip(self._layout, self.buffers):
             if n:
-                mv[off:off + n] = b.cast("B") if b.format != "B" or b.ndim != 1 else b
+                if big_copy is not None and n >= (16 << 20) and b.c_contiguous:
+                    big_copy(off, b)
+                else:
+                    mv[off:off + n] = b.cast("B") if b.format != "B" or b.ndim != 1 else b
 
     def to_bytes(self) -> bytes:
         if not self.buffers:

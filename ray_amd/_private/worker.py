@@ -311,17 +311,16 @@ def wait(object_refs, *, num_returns=1, timeout=None, fetch_local=True):
     if isinstance(object_refs, ObjectRef):
         raise TypeError("wait() expected a list of ray_amd.ObjectRef, got a single ObjectRef")
     refs = list(object_refs)
-    if len(set(r._id for r in refs)) != len(refs):
+    ids = [r._id for r in refs]
+    if len(set(ids)) != len(ids):
         raise ValueError("Wait requires a list of unique object refs.")
     if num_returns <= 0 or num_returns > len(refs):
         raise ValueError("Invalid number of objects to return %d." % num_returns)
-    ready = cw.wait_refs([r._id for r in refs], num_returns, timeout)
-    r_list, nr = [], []
-    for r in refs:
-        if r._id in ready and len(r_list) < num_returns:
-            r_list.append(r)
-        else:
-            nr.append(r)
+    ready = cw.wait_refs(ids, num_returns, timeout)
+    if len(ready) > num_returns:  # keep the first ready ones in input order
+        ready = set([i for i in ids if i in ready][:num_returns])
+    r_list = [r for r in refs if r._id in ready]
+    nr = [r for r in refs if r._id not in ready]
     return r_list, nr
 
 
