@@ -6,3 +6,4 @@ from ray_amd.rllib.algorithms.ppo import PPO, PPOConfig  # noqa: F401
 from ray_amd.rllib.algorithms.sac import SAC, SACConfig  # noqa: F401
 from ray_amd.rllib.algorithms.cql import CQL, CQLConfig  # noqa: F401
 from ray_amd.rllib.algorithms.marwil import BC, MARWIL, BCConfig, MARWILConfig  # noqa: F401
+from ray_amd.rllib.algorithms.dreamerv3 import DreamerV3, DreamerV3Config  # noqa: F401

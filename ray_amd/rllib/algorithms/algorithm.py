@@ -60,7 +60,7 @@ class Algorithm:
         self._module_returns = {}
         self._t_start = time.time()
         nr = int(config.num_env_runners)
-        local_cls = SingleAgentEnvRunner
+        local_cls = getattr(self, "env_runner_cls", None) or SingleAgentEnvRunner
         if self.is_multi_agent:
             from ray_amd.rllib.env.multi_agent_env_runner import MultiAgentEnvRunner
 

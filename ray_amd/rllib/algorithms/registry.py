@@ -8,10 +8,12 @@ def _algos():
     from ray_amd.rllib.algorithms.cql import CQL, CQLConfig
     from ray_amd.rllib.algorithms.marwil import BC, MARWIL, BCConfig, MARWILConfig
     from ray_amd.rllib.algorithms.sac import SAC, SACConfig
+    from ray_amd.rllib.algorithms.dreamerv3 import DreamerV3, DreamerV3Config
 
     return {"PPO": (PPO, PPOConfig), "IMPALA": (IMPALA, IMPALAConfig),
             "APPO": (APPO, APPOConfig), "DQN": (DQN, DQNConfig), "SAC": (SAC, SACConfig),
-            "CQL": (CQL, CQLConfig), "MARWIL": (MARWIL, MARWILConfig), "BC": (BC, BCConfig)}
+            "CQL": (CQL, CQLConfig), "MARWIL": (MARWIL, MARWILConfig), "BC": (BC, BCConfig),
+            "DreamerV3": (DreamerV3, DreamerV3Config)}
 
 
 def get_algorithm_class(name: str):
