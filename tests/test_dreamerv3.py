@@ -60,3 +60,17 @@ def test_world_model_fits_a_batch_and_checkpoints(cluster):
     assert algo2.replayed_steps == algo.replayed_steps
     algo.stop()
     algo2.stop()
+
+
+@pytest.mark.gpu
+def test_dreamerv3_on_gpu_learner(cluster):
+    import torch
+
+    algo = (_cfg("CartPole-v1").learners(num_gpus_per_learner=1)).build()
+    assert algo.device.type == "cuda"
+    algo.train()
+    st = algo._update(algo.replay.sample(4, 16))
+    assert np.isfinite(st["WORLD_MODEL_L_total"]) and np.isfinite(st["ACTOR_L_total"])
+    assert next(algo.world.parameters()).is_cuda
+    torch.cuda.synchronize()
+    algo.stop()
