@@ -275,6 +275,8 @@ _WGRAD = os.environ.get("RAY_AMD_WGRAD", "lt-splitk")
 # split dq kernel's 100 MB, which outweighs the S / dP recompute it saves at head_dim 64
 _ATTN_BWD = os.environ.get("RAY_AMD_ATTN_BWD", "split")
 _WGRAD_LT = _WGRAD == "lt"
+# RAY_AMD_WGRAD_STREAM=1: weight-gradient GEMMs (into flat grads) run on a side stream
+_WGRAD_STREAM = os.environ.get("RAY_AMD_WGRAD_STREAM", "1") == "1"
 
 
 def _splitk(M: int, N: int, K: int) -> int:
@@ -287,6 +289,61 @@ def _splitk(M: int, N: int, K: int) -> int:
     while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 2048:
         S *= 2
     return S
+
+
+def _wgrad_partials(dy2, x2, S, M, N, K):
+    if _WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous():
+        from . import lt
+
+        return lt.wgrad_partials(dy2, x2, S)
+    return torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K),
+                     out_dtype=torch.float32)
+
+
+def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K):
+    """sink += dy2^T x2 (fp32 or bf16 flat-gradient view), then signal DDP readiness."""
+    if _sink_f32(sink) and _WGRAD_LT:
+        # hipBLASLt accumulates straight into the fp32 flat gradient (beta = 1)
+        from . import lt
+
+        lt.wgrad_accum(dy2, x2, sink.view(N, K))
+    else:
+        # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into the
+        # flat gradient) by one HIP pass
+        part = _wgrad_partials(dy2, x2, S, M, N, K)
+        check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(sink),
+                                         1 | 2 * _sink_f32(sink), stream_ptr()), "splitk_accum")
+    _grad_done(w)
+
+
+_side: dict = {}
+
+
+def _side_stream(device):
+    st = _side.get(device)
+    if st is None:
+        st = _side[device] = torch.cuda.Stream(device)
+    return st
+
+
+def join_side_streams():
+    """Make the current stream wait for weight-gradient work queued on side streams (call
+    before consuming the flat gradients: optimizer step, collective)."""
+    for dev, st in _side.items():
+        torch.cuda.current_stream(dev).wait_stream(st)
+
+
+def sync_streams_for_collective():
+    """Before a collective on the current stream: also wait for the other stream of the
+    main/side pair (grads of one bucket can come from both)."""
+    if not _side:
+        return
+    for dev, st in _side.items():
+        cur = torch.cuda.current_stream(dev)
+        if cur == st:
+            cur.wait_stream(torch.cuda.default_stream(dev))
+        else:
+            cur.wait_stream(st)
 
 
 class _Linear(torch.autograd.Function):
@@ -308,32 +365,22 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             S = _splitk(M, N, K)
-            if sink is not None and _sink_f32(sink) and _WGRAD_LT:
-                # hipBLASLt accumulates straight into the fp32 flat gradient (beta = 1),
-                # per-shape tuned solution (ops/lt.py)
-                from . import lt
-
-                lt.wgrad_accum(dy2, x2, sink.view(N, K))
-                _grad_done(w)
-            elif S > 1 or sink is not None:
-                # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into
-                # the flat gradient) by one HIP pass
-                if _WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous():
-                    from . import lt
-
-                    part = lt.wgrad_partials(dy2, x2, S)
-                else:
-                    part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2),
-                                     x2.view(S, M // S, K), out_dtype=torch.float32)
-                target = sink if sink is not None else torch.empty_like(w)
-                check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(target),
-                                                 (1 if sink is not None else 0) |
-                                                 2 * _sink_f32(target), stream_ptr()),
-                      "splitk_accum")
-                if sink is None:
-                    dw = target
-                else:
-                    _grad_done(w)
+            if sink is not None and _WGRAD_STREAM and dy2.is_cuda:
+                # weight gradient on the side stream: it overlaps the memory-bound kernels
+                # of the dX chain that continues on the main stream
+                side = _side_stream(dy2.device)
+                side.wait_stream(torch.cuda.current_stream(dy2.device))
+                with torch.cuda.stream(side):
+                    _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K)
+                    dy2.record_stream(side)
+                    x2.record_stream(side)
+            elif sink is not None:
+                _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K)
+            elif S > 1:
+                part = _wgrad_partials(dy2, x2, S, M, N, K)
+                dw = torch.empty_like(w)
+                check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(dw), 2 * _sink_f32(dw),
+                                                 stream_ptr()), "splitk_accum")
             else:
                 dw = dy2.t() @ x2
         if ctx.b is not None and ctx.needs_input_grad[2]:
@@ -426,6 +473,15 @@ class _CrossEntropy(torch.autograd.Function):
         return dl.view(ctx.shape), None, None, None
 
 
+def _lm_head_dw(lg, h2s, dw, first):
+    if _WGRAD_LT:
+        from . import lt
+
+        lt.wgrad_accum(lg, h2s, dw, beta=0.0 if first else 1.0)
+    else:
+        torch.addmm(dw, lg.t(), h2s, out_dtype=torch.float32, out=dw)
+
+
 class _LMHeadCrossEntropy(torch.autograd.Function):
     """Tied LM head + mean token cross-entropy, chunked over tokens so the full
     [tokens, vocab] logits never exist. Forward computes the loss AND the gradients
@@ -452,24 +508,38 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         dw = (torch.empty if _WGRAD_LT else torch.zeros)(
             w.shape, device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] else None
         ch = max(1, min(chunk, N))
-        buf = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
         L = _lib.lib()
         wt = w.t()
-        for s0 in range(0, N, ch):
+        # side stream: each chunk's dW GEMM (compute-bound) overlaps the next chunk's
+        # memory-bound softmax-xent; two logits buffers alternate between the streams
+        side = _side_stream(dev) if (_WGRAD_STREAM and dw is not None and h.is_cuda) else None
+        nbuf = 2 if side is not None and N > ch else 1
+        bufs = [torch.empty((ch, Vp), device=dev, dtype=h.dtype) for _ in range(nbuf)]
+        freed = [None] * nbuf  # side-stream event after the dW that last read each buffer
+        main = torch.cuda.current_stream(dev) if side is not None else None
+        for i, s0 in enumerate(range(0, N, ch)):
             e = min(N, s0 + ch)
-            lg = buf[: e - s0]
+            k = i % nbuf
+            if freed[k] is not None:
+                main.wait_event(freed[k])
+            lg = bufs[k][: e - s0]
             torch.mm(h2[s0:e], wt, out=lg)
             check(L.ra_xent_fused(ptr(lg), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]), e - s0,
                                   V, Vp, ignore_index, stream_ptr()), "xent_fused")
             if dh is not None:
                 torch.mm(lg, w, out=dh[s0:e])
             if dw is not None:
-                if _WGRAD_LT:
-                    from . import lt
-
-                    lt.wgrad_accum(lg, h2[s0:e], dw, beta=0.0 if s0 == 0 else 1.0)
+                if side is not None:
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        _lm_head_dw(lg, h2[s0:e], dw, s0 == 0)
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                    freed[k] = ev
                 else:
-                    torch.addmm(dw, lg.t(), h2[s0:e], out_dtype=torch.float32, out=dw)
+                    _lm_head_dw(lg, h2[s0:e], dw, s0 == 0)
+        if side is not None:
+            main.wait_stream(side)
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]

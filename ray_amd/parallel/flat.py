@@ -180,6 +180,10 @@ class FlatDDP:
             self._ready[b] += 1
             if self._ready[b] == self.bucket_sizes[b]:
                 s, e = self.buckets[b]
+                if self.flat.g.is_cuda:
+                    from ray_amd.ops import functional as rf
+
+                    rf.sync_streams_for_collective()
                 self._works.append(dist.all_reduce(self.flat.g[s:e], group=self.group,
                                                    async_op=True))
 
@@ -189,6 +193,10 @@ class FlatDDP:
         """Wait (on-stream, no host block) for every bucket; reset counters."""
         if not self.enabled:
             return
+        if self.flat.g.is_cuda:
+            from ray_amd.ops import functional as rf
+
+            rf.join_side_streams()
         for w in self._works:
             w.wait()
         # buckets never triggered (unused params) are reduced now
@@ -230,6 +238,10 @@ class FlatAdamW:
         self.zero_grad = zero_grad
 
     def step(self, lr: float | None = None):
+        if self.use_hip:
+            from ray_amd.ops import functional as rf
+
+            rf.join_side_streams()  # weight gradients queued on the side stream
         self.step_count += 1
         lr = self.lr if lr is None else lr
         f = self.flat
