@@ -230,7 +230,7 @@ class Raylet:
         os.makedirs(os.path.join(self.session_dir, "logs"), exist_ok=True)
         self.addr = os.path.join(self.session_dir, "sockets", "raylet.sock")
         self.node_id = _core.random_id(16)
-        self.node_ip = "127.0.0.1"
+        self.node_ip = os.environ.get("RAY_AMD_NODE_IP", "127.0.0.1")
         self.store_path = args.store_path
         self.spill_dir = os.path.join(self.session_dir, "spill")
         os.makedirs(self.spill_dir, exist_ok=True)

@@ -84,6 +84,9 @@ _SIGS = {
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],
     "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "ra_attn_bwd_pre": [c_void_p] * 3 + [c_int] * 3 + [c_void_p],
+    "ra_attn_bwd_kv": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
+    "ra_attn_bwd_q": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
     "ra_attn_bwd_fused": [c_void_p] * 7 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],

@@ -672,3 +672,37 @@ RA_EXPORT int ra_attn_bwd_fused(const void* qkv, const void* out, const void* do
                      st, (const float*)dq_ws, (bf16_t*)dqkv, n8, T, H, scale);
   return hipGetLastError();
 }
+
+// Split backward as two launches for two streams: ra_attn_bwd_kv (delta pre-pass + dK/dV)
+// and ra_attn_bwd_q (dQ, after delta). The caller orders q after kv's pre-pass with an
+// event; the two main kernels then run concurrently (each one's causal tail is filled by
+// the other's blocks).
+RA_EXPORT int ra_attn_bwd_pre(const void* out, const void* dout, float* delta, int B, int T,
+                              int H, hipStream_t st) {
+  const long rows = (long)B * T * H;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                     (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_attn_bwd_kv(const void* qkv, const void* dout, const float* lse,
+                             const float* delta, void* dqkv, int B, int T, int H, int D,
+                             float scale, hipStream_t st) {
+  if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
+  const float sc_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
+                     (float*)nullptr, T, H, sc_log2, scale, 0);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_attn_bwd_q(const void* qkv, const void* dout, const float* lse,
+                            const float* delta, void* dqkv, int B, int T, int H, int D,
+                            float scale, hipStream_t st) {
+  if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
+  const float sc_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
+                     sc_log2, scale);
+  return hipGetLastError();
+}

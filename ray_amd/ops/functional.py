@@ -326,6 +326,16 @@ def _side_stream(device):
     return st
 
 
+_side2: dict = {}
+
+
+def _side_stream2(device):
+    st = _side2.get(device)
+    if st is None:
+        st = _side2[device] = torch.cuda.Stream(device)
+    return st
+
+
 def join_side_streams():
     """Make the current stream wait for weight-gradient work queued on side streams (call
     before consuming the flat gradients: optimizer step, collective)."""
@@ -423,6 +433,22 @@ class _FlashAttnQKV(torch.autograd.Function):
             check(_lib.lib().ra_attn_bwd_fused(ptr(qkv), ptr(out), ptr(dout), ptr(lse),
                                                ptr(delta), ptr(dq_ws), ptr(dqkv), B, T, H, D,
                                                ctx.scale, stream_ptr()), "attn_bwd_fused")
+        elif _ATTN_BWD == "split2":  # dK/dV and dQ kernels concurrently on two streams
+            L = _lib.lib()
+            dev = qkv.device
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream2(dev)
+            check(L.ra_attn_bwd_pre(ptr(out), ptr(dout), ptr(delta), B, T, H, stream_ptr()),
+                  "attn_bwd_pre")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                check(L.ra_attn_bwd_q(ptr(qkv), ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), B,
+                                      T, H, D, ctx.scale, stream_ptr()), "attn_bwd_q")
+                for t_ in (qkv, dout, lse, delta, dqkv):
+                    t_.record_stream(side)
+            check(L.ra_attn_bwd_kv(ptr(qkv), ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), B, T,
+                                   H, D, ctx.scale, stream_ptr()), "attn_bwd_kv")
+            main.wait_stream(side)
         else:
             check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
                                          ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()),

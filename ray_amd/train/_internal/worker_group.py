@@ -28,7 +28,8 @@ class RayTrainWorker:
         phys = [vis[loc]] if gpu_ids and loc < len(vis) else []
         return {"node_id": ctx.get_node_id(), "pid": os.getpid(),
                 "gpu_ids": gpu_ids, "physical_gpu_ids": phys,
-                "hostname": socket.gethostname(), "ip": "127.0.0.1"}
+                "hostname": socket.gethostname(),
+                "ip": __import__("ray_amd.util", fromlist=["x"]).get_node_ip_address()}
 
     def execute(self, fn, *args, **kwargs):
         return fn(*args, **kwargs)

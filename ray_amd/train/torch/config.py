@@ -88,7 +88,8 @@ class _TorchBackend(Backend):
         for rank, (w, i) in enumerate(zip(worker_group.workers, infos)):
             lr = local.get(i["node_id"], 0)
             local[i["node_id"]] = lr + 1
-            futs.append(w.execute.remote(_init_pg, backend, "127.0.0.1", port, rank,
+            futs.append(w.execute.remote(_init_pg, backend, infos[0].get("ip", "127.0.0.1"),
+                                         port, rank,
                                          len(infos), lr, backend_config.timeout_s))
         ray.get(futs)
 

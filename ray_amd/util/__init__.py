@@ -11,7 +11,15 @@ from ray_amd.util.placement_group import (get_current_placement_group,  # noqa: 
 
 
 def get_node_ip_address():
-    return "127.0.0.1"
+    """This node's address as registered with the cluster (RAY_AMD_NODE_IP on the node,
+    else 127.0.0.1 for a single-machine cluster)."""
+    import os
+
+    from ray_amd._private import worker as W
+
+    cw = W.global_worker.core
+    ip = getattr(cw, "node_ip", None) if cw is not None else None
+    return ip or os.environ.get("RAY_AMD_NODE_IP", "127.0.0.1")
 
 
 def list_named_actors(all_namespaces: bool = False):

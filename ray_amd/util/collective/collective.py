@@ -73,7 +73,9 @@ def init_collective_group(world_size: int, rank: int, backend=Backend.NCCL,
     kv = _kv()
     key = f"collective:{group_name}:addr"
     if rank == 0:
-        addr = f"127.0.0.1:{_free_port()}"
+        from ray_amd.util import get_node_ip_address
+
+        addr = f"{get_node_ip_address()}:{_free_port()}"
         kv._internal_kv_put(key, addr.encode(), overwrite=True, namespace="collective")
     else:
         t0 = time.time()
@@ -168,6 +170,15 @@ def allreduce_coalesced(tensors, group_name: str = "default", op=ReduceOp.SUM,
     """All-reduce many tensors with a few large flat buckets (one kernel per bucket)."""
     g = _g(group_name)
     if not tensors:
+        return tensors
+    if g.backend == Backend.NCCL and all(t.is_cuda and t.is_contiguous() for t in tensors):
+        # RCCL: one grouped launch over the tensors in place (ncclGroupStart/End under the
+        # coalescing manager) - no flatten / unflatten copies through a staging buffer
+        from torch.distributed.distributed_c10d import _coalescing_manager
+
+        with _coalescing_manager(group=g.pg, device=tensors[0].device):
+            for t in tensors:
+                dist.all_reduce(t, op=_TORCH_OPS[op], group=g.pg)
         return tensors
     by_dtype = {}
     for t in tensors:
