@@ -30,7 +30,11 @@ def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer
 
     pending = collections.deque()
     for ref in block_refs:
-        blk = ray.get(ref)
+        if isinstance(ref, tuple):  # (block ref, start row, end row): an equal split's share
+            r0, a, b = ref
+            blk = B.slice_block(ray.get(r0), a, b)
+        else:
+            blk = ray.get(ref)
         if B.num_rows(blk) == 0:
             continue
         if bs is None:
@@ -220,6 +224,8 @@ class SplitCoordinator:
         self.gen = X.execute(self.plan)
         self.queues = [collections.deque() for _ in range(self.n)]
         self.rows = [0] * self.n
+        self.carry = collections.deque()
+        self.carry_rows = 0
         self.done = False
         self.finished = [False] * self.n
 
@@ -243,12 +249,38 @@ class SplitCoordinator:
             except StopIteration:
                 self.done = True
                 continue
-            # equal: give the block to the consumer with the fewest rows
-            j = int(np.argmin(self.rows)) if self.equal else (sum(len(q) for q in
-                                                                  self.queues) % self.n)
+            if self.equal:
+                self._deal_equal(ref, meta["num_rows"] if meta else 0)
+                continue
+            j = sum(len(q) for q in self.queues) % self.n
             self.queues[j].append(ref)
             self.rows[j] += meta["num_rows"] if meta else 0
         return [self.queues[i].popleft()]
+
+    def _deal_equal(self, ref, rows):
+        """equal=True: every consumer gets floor(rows / n) rows of each block (a row range
+        of the same block ref, sliced zero-copy by the consumer); the < n leftover rows of
+        each block join a carry pool that is dealt the same way once it holds n rows, and
+        is dropped at the end — so all consumers receive exactly the same number of rows."""
+        n = self.n
+        per = rows // n
+        if per:
+            for j in range(n):
+                self.queues[j].append((ref, j * per, (j + 1) * per))
+                self.rows[j] += per
+        if rows - per * n:
+            self.carry.append((ref, per * n, rows))
+            self.carry_rows += rows - per * n
+        while self.carry_rows >= n:
+            for j in range(n):  # one row from the carry pool to each consumer
+                r, a, b = self.carry[0]
+                self.queues[j].append((r, a, a + 1))
+                self.rows[j] += 1
+                if a + 1 == b:
+                    self.carry.popleft()
+                else:
+                    self.carry[0] = (r, a + 1, b)
+            self.carry_rows -= n
 
 
 class StreamSplitIterator(DataIterator):
@@ -273,7 +305,10 @@ class StreamSplitIterator(DataIterator):
 
     def iter_rows(self, **kw):
         for ref in self._blocks():
-            yield from B.to_rows(ray.get(ref))
+            if isinstance(ref, tuple):
+                yield from B.to_rows(B.slice_block(ray.get(ref[0]), ref[1], ref[2]))
+            else:
+                yield from B.to_rows(ray.get(ref))
 
     def iter_torch_batches(self, *, batch_size=256, dtypes=None, device="auto", collate_fn=None,
                            drop_last=False, local_shuffle_buffer_size=None,

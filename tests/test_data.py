@@ -131,3 +131,22 @@ def test_streaming_split_for_train(cluster):
 
     counts = ray.get([consume.remote(i) for i in its])
     assert sum(counts) == 100 and min(counts) >= 40
+
+
+def test_streaming_split_equal_exact_rows(cluster):
+    """equal=True: identical row counts per consumer, remainder dropped (reference:
+    OutputSplitter equal=True); every delivered row is distinct."""
+    ds = rd.range(103, override_num_blocks=7)
+    its = ds.streaming_split(3, equal=True)
+
+    @ray.remote
+    def consume(it):
+        out = []
+        for b in it.iter_batches(batch_size=10):
+            out.extend(int(x) for x in b["id"])
+        return out
+
+    parts = ray.get([consume.remote(i) for i in its])
+    assert [len(p) for p in parts] == [34, 34, 34]
+    allrows = sum(parts, [])
+    assert len(set(allrows)) == len(allrows)
