@@ -83,6 +83,10 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True,
         flat = FlatParams(model, dtype=params[0].dtype, grad_dtype=gd)
         ddp = FlatDDP(flat, bucket_mb=kw.get("bucket_mb", 32.0))
         return FlatPreparedModel(model, flat, ddp)
+    return _maybe_autocast(_wrap_parallel(model, dev, world, parallel_strategy, kw), dev)
+
+
+def _wrap_parallel(model, dev, world, parallel_strategy, kw):
     if world > 1 and parallel_strategy in ("auto", "ddp"):
         from torch.nn.parallel import DistributedDataParallel as DDP
 
@@ -96,6 +100,12 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True,
 
         return FSDP(model, device_id=dev if dev.type == "cuda" else None, **kw)
     return model
+
+
+def _maybe_autocast(model, dev):
+    if not _AMP["enabled"]:
+        return model
+    return _AutocastModule(model, dev.type, _AMP["dtype"])
 
 
 class _DeviceLoader:
@@ -160,12 +170,65 @@ def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_devi
     return data_loader
 
 
+# accelerate(amp=True) state: models prepared afterwards run their forward under autocast
+# (bf16 on MI355X: no loss scaling needed); fp16 autocast adds a GradScaler
+_AMP = {"enabled": False, "dtype": torch.bfloat16, "scaler": None}
+
+
+class _AutocastModule(torch.nn.Module):
+    """Runs the wrapped (possibly DDP) module's forward under torch.autocast."""
+
+    def __init__(self, module, device_type, dtype):
+        super().__init__()
+        self.module = module
+        self._dev = device_type
+        self._dtype = dtype
+
+    def forward(self, *a, **k):
+        with torch.autocast(self._dev, dtype=self._dtype):
+            return self.module(*a, **k)
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(super().__getattr__("module"), name)
+
+
+class _AmpOptimizer:
+    """Optimizer facade for fp16 AMP: step / zero_grad go through the GradScaler
+    (reference: train/torch/train_loop_utils.py _WrappedOptimizer)."""
+
+    def __init__(self, optimizer, scaler):
+        self.optimizer = optimizer
+        self.scaler = scaler
+
+    def step(self, closure=None):
+        self.scaler.step(self.optimizer, closure) if closure else self.scaler.step(self.optimizer)
+        self.scaler.update()
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    def __getattr__(self, name):
+        return getattr(self.optimizer, name)
+
+
 def prepare_optimizer(optimizer):
+    """With accelerate(amp=True) in fp16 mode: wrap for loss scaling; otherwise unchanged
+    (bf16 autocast needs no scaler)."""
+    if _AMP["enabled"] and _AMP["scaler"] is not None and \
+            not isinstance(optimizer, (_AmpOptimizer, _FlatOptimizer)):
+        return _AmpOptimizer(optimizer, _AMP["scaler"])
     return optimizer
 
 
 def backward(tensor):
-    tensor.backward()
+    """loss.backward(), scaled when fp16 AMP is active."""
+    if _AMP["enabled"] and _AMP["scaler"] is not None:
+        _AMP["scaler"].scale(tensor).backward()
+    else:
+        tensor.backward()
 
 
 def enable_reproducibility(seed: int = 0):
@@ -180,5 +243,14 @@ def enable_reproducibility(seed: int = 0):
     torch.use_deterministic_algorithms(True, warn_only=True)
 
 
-def accelerate(amp: bool = False):
-    pass
+def accelerate(amp: bool = False, amp_dtype: str = "bf16"):
+    """Enable automatic mixed precision for the models / optimizers prepared after this call
+    (reference: ray.train.torch.accelerate). bf16 (default on MI355X) autocasts matmuls to
+    bf16 with fp32 master weights; fp16 adds dynamic loss scaling via prepare_optimizer /
+    backward."""
+    _AMP["enabled"] = bool(amp)
+    _AMP["dtype"] = torch.float16 if amp_dtype == "fp16" else torch.bfloat16
+    _AMP["scaler"] = None
+    if amp and _AMP["dtype"] == torch.float16:
+        dev = get_device()
+        _AMP["scaler"] = torch.amp.GradScaler(dev.type)

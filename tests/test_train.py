@@ -158,3 +158,25 @@ def test_bench_launcher_gloo_two_ranks(no_ray):
     assert j["config"]["launcher"] == ("torch.distributed.run (no Ray)" if no_ray
                                        else "ray_amd TorchTrainer")
     assert abs(j["final_loss"] - 6.24) < 0.05  # same seed, same synthetic data either way
+
+
+def test_accelerate_amp_bf16_and_fp16_cpu():
+    """train.torch.accelerate(amp=True): prepared models autocast; fp16 adds a scaler
+    behind prepare_optimizer/backward (CPU autocast path, single process)."""
+    import torch
+
+    from ray_amd.train.torch import train_loop_utils as tlu
+
+    try:
+        tlu.accelerate(amp=True)
+        m = tlu.prepare_model(torch.nn.Linear(8, 4), move_to_device=False)
+        y = m(torch.randn(3, 8))
+        assert y.dtype == torch.bfloat16
+        opt = tlu.prepare_optimizer(torch.optim.SGD(m.parameters(), lr=0.1))
+        tlu.backward(y.float().sum())
+        opt.step()
+        assert next(m.parameters()).dtype == torch.float32
+    finally:
+        tlu.accelerate(amp=False)
+    m2 = tlu.prepare_model(torch.nn.Linear(8, 4), move_to_device=False)
+    assert m2(torch.randn(2, 8)).dtype == torch.float32
