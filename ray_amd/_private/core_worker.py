@@ -530,26 +530,73 @@ class CoreWorker:
                 self._node_addrs[node] = a
         return a
 
+    PULL_CHUNK = 16 << 20  # bytes per pull request
+    PULL_PARALLEL = 4  # chunk requests in flight
+
     def _fetch_remote(self, oid, node):
         """Pull a copy of an object whose primary lives on another node into our node's
-        store as an unpinned (evictable) secondary copy (reference: ObjectManager::Pull).
+        store as an unpinned (evictable) secondary copy (reference: ObjectManager::Pull with
+        chunked transfers). The first request returns the size; the remaining chunks are
+        requested PULL_PARALLEL at a time and written straight into the local store entry.
         Returns a buffer over the local copy, or None if the node no longer has it."""
         addr = self._node_addr(node)
         if addr is None:
             return None
+        C = self.PULL_CHUNK
         try:
-            data = self.call(addr, "fetch_object", oid, timeout=300)
+            first = self.call(addr, "fetch_object_chunk", oid, 0, C, timeout=120)
         except Exception:
             return None
-        if data is None:
+        if first is None:
             return None
-        if not self.store.contains(oid):
-            try:
-                self.store.put_bytes(oid, data, pinned=False)
-            except Exception:
-                return memoryview(data)  # store full: serve this read from the heap copy
-        buf = self.store.get_buffer(oid)
-        return buf if buf is not None else memoryview(data)
+        total, head = first
+        if self.store.contains(oid):
+            buf = self.store.get_buffer(oid)
+            if buf is not None:
+                return buf
+        try:
+            off0 = self.store._alloc(oid, total, False)
+        except Exception:
+            off0 = None
+        if off0 is None:  # store full: assemble on the heap and serve this read from it
+            data = bytearray(total)
+            data[:len(head)] = head
+            ok = self._pull_rest(addr, oid, total, len(head),
+                                 lambda o, b: data.__setitem__(slice(o, o + len(b)), b))
+            return memoryview(bytes(data)) if ok else None
+        try:
+            self.store.store.write(off0, head)
+            ok = self._pull_rest(addr, oid, total, len(head),
+                                 lambda o, b: self.store.store.write(off0 + o, b))
+        except BaseException:
+            self.store.store.abort(oid)
+            raise
+        if not ok:
+            self.store.store.abort(oid)
+            return None
+        self.store.store.seal(oid)
+        return self.store.get_buffer(oid)
+
+    def _pull_rest(self, addr, oid, total, start, sink) -> bool:
+        import concurrent.futures as cf
+
+        C = self.PULL_CHUNK
+        offs = list(range(start, total, C))
+        if not offs:
+            return True
+
+        def one(o):
+            r = self.call(addr, "fetch_object_chunk", oid, o, C, timeout=120)
+            if r is None:
+                raise KeyError(oid)
+            sink(o, r[1])
+
+        try:
+            with cf.ThreadPoolExecutor(self.PULL_PARALLEL) as ex:
+                list(ex.map(one, offs))
+        except Exception:
+            return False
+        return True
 
     def _rpc_add_borrower(self, conn, rid, oid, addr):
         with self.lock:

@@ -31,7 +31,7 @@ from ray_amd._private.object_store import table_capacity
 from ray_amd._native import _core
 
 from . import protocol as P
-from .raylet import free_object, node_resources, read_object_bytes
+from .raylet import free_object, node_resources, read_object_bytes, read_object_chunk
 
 _dumps = P.dumps
 
@@ -124,6 +124,9 @@ class NodeAgent:
 
     def rpc_fetch_object(self, conn, rid, oid):
         self.reply(conn, rid, True, read_object_bytes(self.store, self.spill_dir, oid))
+
+    def rpc_fetch_object_chunk(self, conn, rid, oid, off, n):
+        self.reply(conn, rid, True, read_object_chunk(self.store, self.spill_dir, oid, off, n))
 
     def rpc_free_objects(self, conn, rid, oids):
         for oid in oids:

@@ -1217,6 +1217,10 @@ class Raylet:
         """Serve a copy of an object held in this node's store (object_manager Pull)."""
         self.reply(conn, rid, True, read_object_bytes(self.store, self.spill_dir, oid))
 
+    def rpc_fetch_object_chunk(self, conn, rid, oid, off, n):
+        """One chunk of an object (object_manager chunked Pull)."""
+        self.reply(conn, rid, True, read_object_chunk(self.store, self.spill_dir, oid, off, n))
+
     def rpc_free_objects(self, conn, rid, oids):
         for oid in oids:
             free_object(self.store, self.spill_dir, oid)
@@ -1463,6 +1467,27 @@ def read_object_bytes(store, spill_dir, oid):
     try:
         with open(p, "rb") as f:
             return f.read()
+    except OSError:
+        return None
+
+
+def read_object_chunk(store, spill_dir, oid, off, n):
+    """(total size, bytes [off, off + n)) of a sealed object, or None (chunked pulls)."""
+    b = store.get_buffer(oid, True)
+    if b is not None:
+        mv = memoryview(b)
+        try:
+            total = len(mv)
+            return total, bytes(mv[off:min(total, off + n)])
+        finally:
+            mv.release()
+            b.release()
+    p = os.path.join(spill_dir, oid.hex())
+    try:
+        with open(p, "rb") as f:
+            total = os.fstat(f.fileno()).st_size
+            f.seek(off)
+            return total, f.read(max(0, min(n, total - off)))
     except OSError:
         return None
 

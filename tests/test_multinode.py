@@ -120,3 +120,20 @@ def test_strict_spread_pg_and_late_node(cluster3):
     assert placement_group_table(pg4)["state"] == "PENDING"
     c.add_node(num_cpus=1)
     assert ray.get(pg4.ready(), timeout=20)
+
+
+def test_large_object_pulled_in_chunks(cluster3):
+    """A 48 MB object made on another node arrives intact through chunked parallel pulls
+    (reference: object_manager chunked transfers, test_object_manager.py)."""
+    c, n1, n2 = cluster3
+    from ray_amd._private import worker as W
+
+    cw = W.global_worker.core
+    old = cw.PULL_CHUNK
+    cw.PULL_CHUNK = 4 << 20  # force 12 chunks
+    try:
+        ref = make.options(resources={"b": 1}).remote(6 << 20)  # 6M float64 = 48 MB
+        arr = ray.get(ref)
+        assert arr.shape == (6 << 20,) and float(arr.sum()) == float(6 << 20)
+    finally:
+        cw.PULL_CHUNK = old
