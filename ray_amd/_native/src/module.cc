@@ -77,6 +77,16 @@ static void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
 PYBIND11_MODULE(_core, m) {
   m.doc() = "ray_amd native runtime core: shm object store, frame I/O loop, scheduler";
 
+  // dst[:] = src (both contiguous buffers of equal byte size), split over threads with
+  // the GIL released: staging a rollout batch into pinned host memory for the H2D copy
+  m.def("copy_into", [](py::buffer dst, py::buffer src) {
+    py::buffer_info d = dst.request(true), s = src.request();
+    const uint64_t nd = (uint64_t)d.size * d.itemsize, ns = (uint64_t)s.size * s.itemsize;
+    if (nd != ns) throw std::invalid_argument("copy_into: size mismatch");
+    py::gil_scoped_release r;
+    parallel_copy((uint8_t*)d.ptr, (const uint8_t*)s.ptr, nd);
+  });
+
   m.def("random_id", [](int n) {
     if (!tl_rng) {
       std::random_device rd;

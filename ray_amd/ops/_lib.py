@@ -56,7 +56,13 @@ _SIGS = {
     "ra_sgd_flat": [c_void_p] * 4 + [c_long, c_float, c_float, c_float, c_void_p, c_void_p],
     "ra_gae": [c_void_p] * 6 + [c_int, c_int, c_float, c_float, c_void_p],
     "ra_vtrace": [c_void_p] * 7 + [c_int, c_int] + [c_float] * 4 + [c_void_p],
-    "ra_ppo_loss": [c_void_p] * 10 + [c_int, c_int] + [c_float] * 5 + [c_void_p],
+    "ra_ppo_loss": [c_void_p] * 10 + [c_int, c_int] + [c_float] * 5 + [c_int, c_void_p],
+    "ra_ppo_loss_packed": [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 4
+                          + [c_int, c_int] + [c_float] * 5 + [c_void_p, c_int, c_float, c_void_p],
+    "ra_scale_to_bf16": [c_void_p, c_long, c_void_p, c_void_p, c_void_p],
+    "ra_bias_relu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
+    "ra_relu_bwd_work": [c_int, c_int],
+    "ra_relu_bwd_bias": [c_void_p] * 5 + [c_int, c_int, c_int, c_void_p],
     "ra_obsnorm_parts": [c_int],
     "ra_obsnorm_update": [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_void_p,
                           c_void_p],
@@ -81,6 +87,7 @@ _SIGS = {
                            c_int, c_void_p],
     "ra_resize_bilinear": [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p],
     "ra_cast_scale_u8": [c_void_p, c_void_p, c_long, c_float, c_void_p],
+    "ra_gather_cast_u8": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_float, c_void_p],
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],
     "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],

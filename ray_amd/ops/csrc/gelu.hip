@@ -4,6 +4,8 @@
 //   ra_bias_gelu_bwd   dh = dy * gelu_tanh'(h + bias);  dbias = sum_rows(dh)
 //   ra_bias_residual   y  = res + h + bias
 //   ra_colsum_bf16     out = sum_rows(x)     (bias gradient of a projection)
+//   ra_bias_relu_fwd   y  = relu(h + bias)   (conv / linear epilogue, rows = NHWC pixels)
+//   ra_relu_bwd_bias   dh = dy * (y > 0);  dbias = sum_rows(dh)   (two launches)
 //
 // The GEMM itself stays on hipBLASLt (plain library GEMM); these kernels fuse
 // everything around it into one HBM pass. Each thread moves 8 bf16 (16 bytes);
@@ -25,17 +27,19 @@ __device__ __forceinline__ float gelu_tanh(float u, float* dgelu) {
 }
 
 // grid-stride over 16-B vectors; 32-bit index math (n8 < 2^31 is checked on the host)
-__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16_t* __restrict__ h,
-                                                            const bf16_t* __restrict__ bias,
-                                                            bf16_t* __restrict__ y, int n8,
-                                                            int F8) {
+template <bool RELU>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ h,
+                                                           const bf16_t* __restrict__ bias,
+                                                           bf16_t* __restrict__ y, int n8,
+                                                           int F8) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
     const int c8 = (int)((unsigned)i % (unsigned)F8);
     float hv[8], bv[8], o[8];
     unpack8(reinterpret_cast<const uint4*>(h)[i], hv);
     unpack8(reinterpret_cast<const uint4*>(bias)[c8], bv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = gelu_tanh(hv[j] + bv[j], nullptr);
+    for (int j = 0; j < 8; ++j)
+      o[j] = RELU ? fmaxf(hv[j] + bv[j], 0.f) : gelu_tanh(hv[j] + bv[j], nullptr);
     reinterpret_cast<uint4*>(y)[i] = pack8(o);
   }
 }
@@ -99,6 +103,100 @@ __global__ __launch_bounds__(64) void bwd_colpart_kernel(const bf16_t* __restric
   *reinterpret_cast<float4*>(pr + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
+// ReLU backward + bias-gradient partials for NARROW rows (F8 divides 256: conv channel
+// counts 32/64/..., F <= 2048). A 256-thread block covers 256/F8 rows per step, so every
+// lane is busy even at F = 32 (the wide-row kernel above would run 4 of 64 lanes).
+// part[blockIdx.x][F] = column sums of dh over this block's rows.
+__global__ __launch_bounds__(256) void relu_bwd_rows_kernel(const bf16_t* __restrict__ dy,
+                                                            const bf16_t* __restrict__ y,
+                                                            bf16_t* __restrict__ dh,
+                                                            float* __restrict__ part, int N,
+                                                            int F8, int rows_per_block) {
+  __shared__ float red[256 * 8];
+  const int t = threadIdx.x, c8 = t % F8, rs = t / F8, RPI = 256 / F8;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(N, r0 + rows_per_block);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const uint4* dy4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* y4 = reinterpret_cast<const uint4*>(y);
+  constexpr int RB = 4;
+  for (int rb = r0 + rs; rb < r1; rb += RB * RPI) {
+    uint4 dv[RB], yv[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int r = rb + k * RPI < r1 ? rb + k * RPI : rb;
+      const long ix = (long)r * F8 + c8;
+      dv[k] = dy4[ix];
+      yv[k] = y4[ix];
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int r = rb + k * RPI;
+      if (r >= r1) break;
+      float d[8], o[8];
+      unpack8(dv[k], d);
+      const uint32_t w[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // bf16 > 0 <=> sign bit clear and not +0 (ReLU outputs are never negative or NaN)
+        const uint32_t b = (j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xffffu);
+        o[j] = b != 0 && b < 0x8000u ? d[j] : 0.f;
+        acc[j] += o[j];
+      }
+      reinterpret_cast<uint4*>(dh)[(long)r * F8 + c8] = pack8(o);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t * 8 + j] = acc[j];
+  __syncthreads();
+  const int F = F8 * 8;
+  for (int c = t; c < F; c += 256) {
+    float s = 0.f;
+    for (int q = 0; q < RPI; ++q) s += red[(q * F8 + (c >> 3)) * 8 + (c & 7)];
+    part[(size_t)blockIdx.x * F + c] = s;
+  }
+}
+
+// out[c] (+)= sum_p part[p][c]: grid ceil(F/64) blocks of 64 columns x 16 row lanes
+// (a single block serves F <= 64, so the row walk must be short and wide).
+template <bool OUT_BF16, bool ACC>
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ part,
+                                                            void* out, int P, int F) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < F) {
+    int p = ty;
+    for (; p + 16 < P; p += 32) {
+      s0 += part[(size_t)p * F + c];
+      s1 += part[(size_t)(p + 16) * F + c];
+    }
+    if (p < P) s0 += part[(size_t)p * F + c];
+  }
+  red[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty != 0 || c >= F) return;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s += red[q][tx];
+  if (OUT_BF16) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + c;
+    *o = f2bf(ACC ? s + bf2f(*o) : s);
+  } else {
+    float* o = reinterpret_cast<float*>(out) + c;
+    *o = ACC ? *o + s : s;
+  }
+}
+
+static inline int relu_rows_per_block(int N, int F8) {
+  const int RPI = 256 / F8;
+  int rpb = (N + 511) / 512;                   // <= 512 partial rows
+  rpb = (rpb + RPI - 1) / RPI * RPI;           // whole block steps
+  return rpb < RPI ? RPI : rpb;
+}
+
 __global__ __launch_bounds__(256) void bias_residual_kernel(const bf16_t* __restrict__ h,
                                                             const bf16_t* __restrict__ bias,
                                                             const bf16_t* __restrict__ res,
@@ -142,7 +240,7 @@ RA_EXPORT int ra_bias_gelu_fwd(const void* h, const void* bias, void* y, long N,
   if (F % 8) return hipErrorInvalidValue;
   const long n8 = N * (long)F / 8;
   if (n8 >= (1L << 31) - 65536L * 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3(ra_grid(n8, 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(bias_act_fwd_kernel<false>, dim3(ra_grid(n8, 256)), dim3(256), 0, st,
                      (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)y, (int)n8, F / 8);
   return hipGetLastError();
 }
@@ -176,6 +274,44 @@ RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F
   hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                      (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
   colsum_launch(work, work + (size_t)P * F, out, P, F, sink_flags(flags), st);
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_bias_relu_fwd(const void* h, const void* bias, void* y, long N, int F,
+                               hipStream_t st) {
+  if (F % 8) return hipErrorInvalidValue;
+  const long n8 = N * (long)F / 8;
+  if (n8 >= (1L << 31) - 65536L * 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bias_act_fwd_kernel<true>, dim3(ra_grid(n8, 256)), dim3(256), 0, st,
+                     (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)y, (int)n8, F / 8);
+  return hipGetLastError();
+}
+
+// fp32 workspace (floats) for ra_relu_bwd_bias
+RA_EXPORT long ra_relu_bwd_work(int N, int F) {
+  const int F8 = F / 8;
+  if (F % 8 || 256 % F8) return -1;
+  const int rpb = relu_rows_per_block(N, F8);
+  return (long)((N + rpb - 1) / rpb) * F;
+}
+
+// dh = dy * (y > 0), dbias (+)= sum_rows(dh); flags as sink_flags (bit0 accumulate,
+// bit1 fp32 destination). Narrow rows only (F8 | 256); work: ra_relu_bwd_work floats.
+RA_EXPORT int ra_relu_bwd_bias(const void* dy, const void* y, void* dh, void* dbias,
+                               float* work, int N, int F, int flags, hipStream_t st) {
+  const int F8 = F / 8;
+  if (F % 8 || 256 % F8 || N <= 0) return hipErrorInvalidValue;
+  const int rpb = relu_rows_per_block(N, F8);
+  const int P = (N + rpb - 1) / rpb;
+  hipLaunchKernelGGL(relu_bwd_rows_kernel, dim3(P), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)y, (bf16_t*)dh, work, N, F8, rpb);
+  const dim3 g((F + 63) / 64), b(1024);
+  switch (((flags & 1) ? 2 : 0) | ((flags & 2) ? 0 : 1)) {
+    case 0: hipLaunchKernelGGL((colsum_final_kernel<false, false>), g, b, 0, st, work, dbias, P, F); break;
+    case 1: hipLaunchKernelGGL((colsum_final_kernel<true, false>), g, b, 0, st, work, dbias, P, F); break;
+    case 2: hipLaunchKernelGGL((colsum_final_kernel<false, true>), g, b, 0, st, work, dbias, P, F); break;
+    default: hipLaunchKernelGGL((colsum_final_kernel<true, true>), g, b, 0, st, work, dbias, P, F);
+  }
   return hipGetLastError();
 }
 

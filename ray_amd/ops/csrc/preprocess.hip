@@ -3,6 +3,7 @@
 //   ra_image_normalize: uint8 NHWC -> bf16/f32 NCHW, y = (x/255 - mean[c]) / std[c]
 //   ra_resize_bilinear: bf16/f32 NCHW bilinear resize (align_corners=False)
 //   ra_cast_scale     : uint8 -> bf16 with scale (Atari frames: x/255)
+//   ra_gather_cast_u8 : y[i] = x[idx[i]] * scale, uint8 rows -> bf16 (PPO minibatch frames)
 //
 // image_normalize treats each image as a flat run of H*W pixels (NHWC -> NCHW never
 // needs a row structure): 16 pixels per thread, 16-byte loads and stores.
@@ -127,6 +128,32 @@ __global__ __launch_bounds__(256) void cast_scale_kernel(const uint8_t* __restri
   }
 }
 
+// Minibatch gather + cast in one pass: y[i, :] = x[idx[i], :] * scale (uint8 rows of
+// `row` bytes, row % 16 == 0) — the PPO learner's minibatch frames straight from the
+// resident train batch, 16 pixels per thread (16-B load, 2 x 16-B stores).
+__global__ __launch_bounds__(256) void gather_cast_kernel(const uint8_t* __restrict__ x,
+                                                          const long* __restrict__ idx,
+                                                          bf16_t* __restrict__ y, int row16,
+                                                          long n16, float scale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16;
+       i += (long)gridDim.x * blockDim.x) {
+    const long r = i / row16, c = i - r * row16;
+    const uint4 u = reinterpret_cast<const uint4*>(x)[idx[r] * row16 + c];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    float f[8], h[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = (float)((w[0] >> (8 * j)) & 0xff) * scale;
+      f[4 + j] = (float)((w[1] >> (8 * j)) & 0xff) * scale;
+      h[j] = (float)((w[2] >> (8 * j)) & 0xff) * scale;
+      h[4 + j] = (float)((w[3] >> (8 * j)) & 0xff) * scale;
+    }
+    uint4* yo = reinterpret_cast<uint4*>(y) + 2 * i;
+    yo[0] = pack8(f);
+    yo[1] = pack8(h);
+  }
+}
+
 // mean / std are HOST pointers (C floats): folded into kernel arguments, no H2D copy.
 RA_EXPORT int ra_image_normalize(const void* x, void* y, int N, int H, int W, int C,
                                  const float* mean, const float* std_, int bf16_out,
@@ -180,6 +207,16 @@ RA_EXPORT int ra_resize_bilinear(const void* x, void* y, int NC, int H, int W, i
   else
     hipLaunchKernelGGL(resize_bilinear_kernel<false>, dim3(ra_grid(total, 256)), dim3(256), 0, st,
                        x, y, NC, H, W, OH, OW);
+  return hipGetLastError();
+}
+
+// idx values must lie in [0, rows of x): the caller passes a permutation of the batch.
+RA_EXPORT int ra_gather_cast_u8(const void* x, const long* idx, void* y, long nrows, long row,
+                                float scale, hipStream_t st) {
+  if (row % 16 || row / 16 > (1L << 30)) return hipErrorInvalidValue;
+  const long n16 = nrows * (row / 16);
+  hipLaunchKernelGGL(gather_cast_kernel, dim3(ra_grid(n16, 256)), dim3(256), 0, st,
+                     (const uint8_t*)x, idx, (bf16_t*)y, (int)(row / 16), n16, scale);
   return hipGetLastError();
 }
 

@@ -159,20 +159,33 @@ RA_EXPORT int ra_vtrace(const float* log_rhos, const float* discounts, const flo
 // ---------------------------------------------------------------------------
 // Fused PPO loss, categorical policy. One thread per sample, logits in registers.
 // stats[0..5] += {total, policy_loss, vf_loss, entropy, kl, clip_frac} (means)
+//
+// The policy outputs (logits, vpred) are the minibatch rows in order, fp32 or bf16
+// (the learner's bf16 heads are read directly: no cast kernels). The behaviour-side
+// fields (old_logits, action, old_logp, adv, vtarg) are read through row pointers +
+// row strides, optionally GATHERED by `idx` from the full train batch: the learner
+// packs them into one fp32 table [N_full, A+4], so a minibatch needs no gather
+// kernels at all.
 struct PPOArgs {
-  const float* logits;      // [N,A] current policy
-  const float* old_logits;  // [N,A] behaviour policy (action_dist_inputs); may be null
-  const long* actions;      // [N]
-  const float* old_logp;    // [N]
-  const float* adv;         // [N]
-  const float* vpred;       // [N] (may be null: no value loss)
-  const float* vtarg;       // [N]
-  float* dlogits;           // [N,A]
+  const void* logits;       // [N,A] current policy (bf16 when in_bf16)
+  const void* vpred;        // [N] (may be null: no value loss)
+  const float* old_logits;  // row r at old_logits + r*ld_old; may be null
+  const void* actions;      // long (act_f32 == 0) or float, row r at actions + r*ld_act
+  const float* old_logp;    // row r at + r*ld_aux (same stride for old_logp/adv/vtarg)
+  const float* adv;
+  const float* vtarg;
+  const long* idx;          // [N] rows of the behaviour table; null = identity
+  float* dlogits;           // [N,A] fp32 d(mean loss)/dlogits
   float* dvpred;            // [N]
-  float* stats;             // [6]
-  int N, A;
+  float* stats;             // [6] accumulated (the caller zeroes it when it wants)
+  const float* kl_dev;      // device-resident KL coefficient (overrides kl_coeff; may be null)
+  int N, A, in_bf16, act_f32, ld_old, ld_act, ld_aux;
   float clip, vf_clip, vf_coeff, ent_coeff, kl_coeff, inv_n;
 };
+
+__device__ __forceinline__ float ld_in(const void* p, long k, int bf) {
+  return bf ? bf2f(reinterpret_cast<const bf16_t*>(p)[k]) : reinterpret_cast<const float*>(p)[k];
+}
 
 template <int AMAX>
 __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
@@ -180,11 +193,12 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   float s_total = 0.f, s_pol = 0.f, s_vf = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
   if (i < p.N) {
+    const long r = p.idx ? p.idx[i] : (long)i;
     float z[AMAX], lp[AMAX];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < AMAX; ++j) {
-      z[j] = (j < p.A) ? p.logits[(long)i * p.A + j] : -INFINITY;
+      z[j] = (j < p.A) ? ld_in(p.logits, (long)i * p.A + j, p.in_bf16) : -INFINITY;
       mx = fmaxf(mx, z[j]);
     }
     float se = 0.f;
@@ -200,10 +214,11 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
     // KL(old || new)
     float kl = 0.f, olp[AMAX];
     if (p.old_logits) {
+      const float* orow = p.old_logits + r * p.ld_old;
       float omx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < AMAX; ++j) {
-        olp[j] = (j < p.A) ? p.old_logits[(long)i * p.A + j] : -INFINITY;
+        olp[j] = (j < p.A) ? orow[j] : -INFINITY;
         omx = fmaxf(omx, olp[j]);
       }
       float ose = 0.f;
@@ -216,12 +231,14 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
         if (j < p.A) kl += __expf(olp[j]) * (olp[j] - lp[j]);
       }
     }
-    const long act = p.actions[i];
+    const long act = p.act_f32 ? (long)reinterpret_cast<const float*>(p.actions)[r * p.ld_act]
+                               : reinterpret_cast<const long*>(p.actions)[r * p.ld_act];
     float logp = 0.f;
 #pragma unroll
     for (int j = 0; j < AMAX; ++j) if (j == act) logp = lp[j];
-    const float ratio = __expf(logp - p.old_logp[i]);
-    const float A_ = p.adv[i];
+    const long ra = r * p.ld_aux;
+    const float ratio = __expf(logp - p.old_logp[ra]);
+    const float A_ = p.adv[ra];
     const float rc = fminf(fmaxf(ratio, 1.f - p.clip), 1.f + p.clip);
     const float s1 = A_ * ratio, s2 = A_ * rc;
     const float surr = fminf(s1, s2);
@@ -232,13 +249,14 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
     const bool clipped = (ratio < 1.f - p.clip) || (ratio > 1.f + p.clip);
     float vf = 0.f, dv = 0.f;
     if (p.vpred) {
-      const float e = p.vpred[i] - p.vtarg[i];
+      const float e = ld_in(p.vpred, i, p.in_bf16) - p.vtarg[ra];
       const float e2 = e * e;
       vf = fminf(e2, p.vf_clip);
       dv = (e2 < p.vf_clip) ? 2.f * e : 0.f;
       p.dvpred[i] = p.vf_coeff * dv * p.inv_n;
     }
-    const float total = -surr + p.vf_coeff * vf - p.ent_coeff * ent + p.kl_coeff * kl;
+    const float kl_c = p.kl_dev ? p.kl_dev[0] : p.kl_coeff;
+    const float total = -surr + p.vf_coeff * vf - p.ent_coeff * ent + kl_c * kl;
     // gradient wrt logits
 #pragma unroll
     for (int j = 0; j < AMAX; ++j) {
@@ -246,7 +264,7 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
         const float pj = __expf(lp[j]);
         float g = -dsurr * ((j == act ? 1.f : 0.f) - pj);   // policy term
         g += p.ent_coeff * pj * (lp[j] + ent);               // -c * dH/dz, dH/dz = -p(logp+H)
-        if (p.old_logits) g += p.kl_coeff * (pj - __expf(olp[j]));
+        if (p.old_logits) g += kl_c * (pj - __expf(olp[j]));
         p.dlogits[(long)i * p.A + j] = g * p.inv_n;
       }
     }
@@ -260,21 +278,62 @@ __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
   }
 }
 
-RA_EXPORT int ra_ppo_loss(const float* logits, const float* old_logits, const long* actions,
-                          const float* old_logp, const float* adv, const float* vpred,
+static int ppo_launch(const PPOArgs& p, hipStream_t st) {
+  const dim3 g((p.N + 255) / 256);
+  if (p.A <= 4) hipLaunchKernelGGL(ppo_loss_kernel<4>, g, dim3(256), 0, st, p);
+  else if (p.A <= 8) hipLaunchKernelGGL(ppo_loss_kernel<8>, g, dim3(256), 0, st, p);
+  else if (p.A <= 18) hipLaunchKernelGGL(ppo_loss_kernel<18>, g, dim3(256), 0, st, p);
+  else if (p.A <= 32) hipLaunchKernelGGL(ppo_loss_kernel<32>, g, dim3(256), 0, st, p);
+  else if (p.A <= 64) hipLaunchKernelGGL(ppo_loss_kernel<64>, g, dim3(256), 0, st, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// Contiguous per-minibatch inputs (fp32 or bf16 logits/vpred); stats are zeroed here.
+RA_EXPORT int ra_ppo_loss(const void* logits, const float* old_logits, const long* actions,
+                          const float* old_logp, const float* adv, const void* vpred,
                           const float* vtarg, float* dlogits, float* dvpred, float* stats, int N,
                           int A, float clip, float vf_clip, float vf_coeff, float ent_coeff,
-                          float kl_coeff, hipStream_t st) {
-  PPOArgs p{logits, old_logits, actions, old_logp, adv, vpred, vtarg, dlogits, dvpred, stats,
-            N, A, clip, vf_clip, vf_coeff, ent_coeff, kl_coeff, 1.f / (float)N};
+                          float kl_coeff, int in_bf16, hipStream_t st) {
+  PPOArgs p{logits, vpred, old_logits, actions, old_logp, adv, vtarg, nullptr, dlogits, dvpred,
+            stats, nullptr, N, A, in_bf16, 0, A, 1, 1, clip, vf_clip, vf_coeff, ent_coeff,
+            kl_coeff, 1.f / (float)N};
   hipMemsetAsync(stats, 0, 6 * sizeof(float), st);
-  dim3 g((N + 255) / 256);
-  if (A <= 4) hipLaunchKernelGGL(ppo_loss_kernel<4>, g, dim3(256), 0, st, p);
-  else if (A <= 8) hipLaunchKernelGGL(ppo_loss_kernel<8>, g, dim3(256), 0, st, p);
-  else if (A <= 18) hipLaunchKernelGGL(ppo_loss_kernel<18>, g, dim3(256), 0, st, p);
-  else if (A <= 32) hipLaunchKernelGGL(ppo_loss_kernel<32>, g, dim3(256), 0, st, p);
-  else if (A <= 64) hipLaunchKernelGGL(ppo_loss_kernel<64>, g, dim3(256), 0, st, p);
-  else return hipErrorInvalidValue;
+  return ppo_launch(p, st);
+}
+
+// Behaviour fields packed in one fp32 table aux[N_full, ld] = [old_logits(A) | action |
+// old_logp | adv | vtarg] and gathered by idx[N] inside the kernel; stats ACCUMULATE
+// (the learner sums them over every minibatch of an update without extra kernels).
+// kl_dev (optional) is a device scalar read at run time, so a captured graph survives
+// the adaptive KL coefficient changing between updates.
+RA_EXPORT int ra_ppo_loss_packed(const void* logits, const void* vpred, const float* aux, int ld,
+                                 int has_old, const long* idx, float* dlogits, float* dvpred,
+                                 float* stats, int N, int A, float clip, float vf_clip,
+                                 float vf_coeff, float ent_coeff, float kl_coeff,
+                                 const float* kl_dev, int in_bf16, float inv_n, hipStream_t st) {
+  if (ld < A + 4) return hipErrorInvalidValue;
+  PPOArgs p{logits, vpred, has_old ? aux : nullptr, aux + A, aux + A + 1, aux + A + 2,
+            aux + A + 3, idx, dlogits, dvpred, stats, kl_dev, N, A, in_bf16, 1, ld, ld, ld, clip,
+            vf_clip, vf_coeff, ent_coeff, kl_coeff, inv_n};
+  return ppo_launch(p, st);
+}
+
+// out_bf16[k] = g[0] * src[k] for the concatenated fp32 loss gradients (one launch for
+// dlogits and dvpred; g is the upstream scalar gradient, read on device).
+__global__ __launch_bounds__(256) void scale_to_bf16_kernel(const float* __restrict__ src, long n,
+                                                             const float* __restrict__ g,
+                                                             bf16_t* __restrict__ out) {
+  const float s = g ? g[0] : 1.f;
+  for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < n;
+       k += (long)gridDim.x * blockDim.x)
+    out[k] = f2bf(src[k] * s);
+}
+
+RA_EXPORT int ra_scale_to_bf16(const float* src, long n, const float* g, void* out,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(scale_to_bf16_kernel, dim3(ra_grid(n, 256)), dim3(256), 0, st, src, n, g,
+                     (bf16_t*)out);
   return hipGetLastError();
 }
 

@@ -691,33 +691,54 @@ def vtrace(log_rhos, discounts, rewards, values, bootstrap, clip_rho=1.0, clip_c
     return vs, pg
 
 
+def _ppo_grads_bwd(ctx, g):
+    """(dlogits, dvpred) = g * the fp32 gradients the fused loss kernel wrote; bf16 heads
+    get both in ONE scale-and-cast launch over the concatenated buffer."""
+    (grad,) = ctx.saved_tensors
+    N, A = ctx.shape
+    ldt, vdt = ctx.dtypes
+    if grad.is_cuda and ldt == torch.bfloat16 and vdt in (None, torch.bfloat16):
+        out = torch.empty(grad.numel(), device=grad.device, dtype=torch.bfloat16)
+        check(_lib.lib().ra_scale_to_bf16(ptr(grad), grad.numel(), ptr(g.float().contiguous()),
+                                          ptr(out), stream_ptr()), "scale_to_bf16")
+    else:
+        out = grad * g
+    dlog = out[:N * A].view(N, A).to(ldt)
+    dvp = out[N * A:].to(vdt) if ctx.has_v else None
+    return dlog, dvp
+
+
+def _ppo_heads(logits, vpred):
+    """Kernel inputs for the policy heads: bf16 read directly, anything else as fp32."""
+    bf = logits.dtype == torch.bfloat16 and (vpred is None or vpred.dtype == torch.bfloat16)
+    cast = (lambda t: t.contiguous()) if bf else (lambda t: t.float().contiguous())
+    return cast(logits), (cast(vpred) if vpred is not None else None), int(bf)
+
+
 class _PPOLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, vpred, old_logits, actions, old_logp, adv, vtarg, hp):
         N, A = logits.shape
-        lg = logits.float().contiguous()
-        dl = torch.empty_like(lg)
         has_v = vpred is not None
-        vp = vpred.float().contiguous() if has_v else None
-        dv = torch.empty_like(vp) if has_v else None
+        lg, vp, bf = _ppo_heads(logits, vpred)
+        grad = torch.empty(N * A + N, device=logits.device, dtype=torch.float32)
         stats = torch.empty(6, device=logits.device, dtype=torch.float32)
         ol = old_logits.float().contiguous() if old_logits is not None else None
         check(_lib.lib().ra_ppo_loss(
             ptr(lg), ptr(ol), ptr(actions.long().contiguous()), ptr(old_logp.float().contiguous()),
             ptr(adv.float().contiguous()), ptr(vp), ptr(vtarg.float().contiguous()) if has_v else None,
-            ptr(dl), ptr(dv), ptr(stats), N, A, hp[0], hp[1], hp[2], hp[3], hp[4], stream_ptr()),
-            "ppo_loss")
-        ctx.save_for_backward(dl, dv if has_v else dl)
+            ptr(grad), ptr(grad[N * A:]) if has_v else None, ptr(stats), N, A, hp[0], hp[1], hp[2],
+            hp[3], hp[4], bf, stream_ptr()), "ppo_loss")
+        ctx.save_for_backward(grad)
         ctx.has_v = has_v
+        ctx.shape = (N, A)
         ctx.dtypes = (logits.dtype, vpred.dtype if has_v else None)
         ctx.mark_non_differentiable(stats)
         return stats[0].clone(), stats
 
     @staticmethod
     def backward(ctx, g, _gs):
-        dl, dv = ctx.saved_tensors
-        dlog = (dl * g).to(ctx.dtypes[0])
-        dvp = (dv * g).to(ctx.dtypes[1]) if ctx.has_v else None
+        dlog, dvp = _ppo_grads_bwd(ctx, g)
         return dlog, dvp, None, None, None, None, None, None
 
 
@@ -730,6 +751,124 @@ def ppo_loss(logits, old_logits, actions, old_logp, adv, vpred, vtarg, clip=0.2,
                             vf_clip, vf_coeff, ent_coeff, kl_coeff)
     hp = (float(clip), float(vf_clip), float(vf_coeff), float(ent_coeff), float(kl_coeff))
     return _PPOLoss.apply(logits, vpred, old_logits, actions, old_logp, adv, vtarg, hp)
+
+
+def ppo_pack(old_logits, actions, old_logp, adv, vtarg):
+    """The behaviour-side PPO fields of a whole train batch as ONE fp32 table
+    [N, A+4] = [old_logits | action | old_logp | adv | vtarg] for ``ppo_loss_packed``
+    (actions are exact in fp32 below 2^24)."""
+    return torch.cat([old_logits.float(), actions.float().unsqueeze(1), old_logp.float()[:, None],
+                      adv.float()[:, None], vtarg.float()[:, None]], 1).contiguous()
+
+
+class _PPOLossPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, vpred, aux, idx, stats, hp, has_old, inv_n, kl_dev):
+        N, A = logits.shape
+        lg, vp, bf = _ppo_heads(logits, vpred)
+        grad = torch.empty(N * A + N, device=logits.device, dtype=torch.float32)
+        check(_lib.lib().ra_ppo_loss_packed(
+            ptr(lg), ptr(vp), ptr(aux), aux.shape[1], int(has_old), ptr(idx), ptr(grad),
+            ptr(grad[N * A:]), ptr(stats), N, A, hp[0], hp[1], hp[2], hp[3], hp[4],
+            ptr(kl_dev), bf, float(inv_n), stream_ptr()), "ppo_loss_packed")
+        ctx.save_for_backward(grad)
+        ctx.has_v = True
+        ctx.shape = (N, A)
+        ctx.dtypes = (logits.dtype, vpred.dtype)
+        # backward handle only: the loss values are accumulated into `stats`
+        return logits.new_empty((), dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        dlog, dvp = _ppo_grads_bwd(ctx, g)
+        return dlog, dvp, None, None, None, None, None, None, None
+
+
+def ppo_loss_packed(logits, vpred, aux, idx, stats, clip=0.2, vf_clip=10.0, vf_coeff=1.0,
+                    ent_coeff=0.0, kl_coeff=0.0, has_old=True, inv_n=None, kl_dev=None):
+    """Fused PPO loss over a minibatch whose behaviour fields are rows ``idx`` of the packed
+    table ``aux`` (``ppo_pack``): no gather kernels. The six statistics (means over the
+    minibatch, or scaled by ``inv_n``) are ACCUMULATED into ``stats``; the returned scalar
+    is a backward handle whose value is undefined (gradients are exact). ``kl_dev``: an
+    optional 1-element fp32 device tensor holding the KL coefficient (read at run time, so
+    a captured HIP graph stays valid when it changes). GPU only."""
+    if not _hip(logits) or logits.shape[-1] > 64:
+        raise ValueError("ppo_loss_packed needs HIP tensors and at most 64 actions")
+    N = logits.shape[0]
+    hp = (float(clip), float(vf_clip), float(vf_coeff), float(ent_coeff), float(kl_coeff))
+    return _PPOLossPacked.apply(logits, vpred, aux, idx, stats, hp, has_old,
+                                1.0 / N if inv_n is None else inv_n, kl_dev)
+
+
+# --------------------------------------------------------------------- bias + ReLU
+def _nhwc_rows(t):
+    """[M, C] row view of a 2-D tensor or a channels-last NCHW tensor (None if neither)."""
+    if t.dim() == 2:
+        return t if t.is_contiguous() else None
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+    return None
+
+
+class _BiasReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, bias):
+        h2 = _nhwc_rows(h)
+        y = torch.empty_like(h)  # keeps channels-last strides
+        y2 = _nhwc_rows(y)
+        check(_lib.lib().ra_bias_relu_fwd(ptr(h2), ptr(bias), ptr(y2), h2.shape[0], h2.shape[1],
+                                          stream_ptr()), "bias_relu_fwd")
+        ctx.save_for_backward(y)
+        ctx.bias = bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        bias = ctx.bias
+        if _nhwc_rows(dy) is None:
+            dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 \
+                else dy.contiguous()
+        dy2, y2 = _nhwc_rows(dy), _nhwc_rows(y)
+        M, C = y2.shape
+        L = _lib.lib()
+        dh = torch.empty_like(y)
+        work = torch.empty(L.ra_relu_bwd_work(M, C), device=y.device, dtype=torch.float32)
+        sink = _grad_sink(bias)
+        db = sink if sink is not None else torch.empty_like(bias)
+        flags = (1 if sink is not None else 0) | (2 * _sink_f32(db))
+        check(L.ra_relu_bwd_bias(ptr(dy2), ptr(y2), ptr(_nhwc_rows(dh)), ptr(db), ptr(work), M, C,
+                                 flags, stream_ptr()), "relu_bwd_bias")
+        if sink is not None:
+            _grad_done(bias)
+            return dh, None
+        return dh, db
+
+
+def bias_relu(h, bias):
+    """relu(h + bias) over the channel axis (last dim of a 2-D tensor, dim 1 of a
+    channels-last NCHW conv output): one fused pass forward, and ONE pass backward that
+    also reduces the bias gradient (instead of add + relu + threshold_backward + sum)."""
+    C = h.shape[1] if h.dim() == 4 else h.shape[-1]
+    if (_hip(h) and h.dtype == torch.bfloat16 and bias is not None
+            and bias.dtype == torch.bfloat16 and C % 8 == 0 and 256 % (C // 8) == 0
+            and _nhwc_rows(h) is not None and h.numel() > 0):
+        return _BiasReLU.apply(h, bias)
+    if bias is not None:
+        h = h + (bias.view(1, -1, 1, 1) if h.dim() == 4 else bias).to(h.dtype)
+    return torch.relu(h)
+
+
+def gather_cast_u8(x_u8, idx, scale=1.0 / 255.0):
+    """bf16 rows ``x_u8[idx] * scale`` in one pass (no uint8 gather copy)."""
+    row = x_u8[0].numel() if x_u8.shape[0] else 0
+    if not _hip(x_u8) or row % 16 or not x_u8.is_contiguous():
+        return (x_u8.index_select(0, idx).float() * scale).to(torch.bfloat16)
+    y = torch.empty((idx.shape[0],) + tuple(x_u8.shape[1:]), dtype=torch.bfloat16,
+                    device=x_u8.device)
+    check(_lib.lib().ra_gather_cast_u8(ptr(x_u8), ptr(idx.long().contiguous()), ptr(y),
+                                       idx.shape[0], row, scale, stream_ptr()), "gather_cast_u8")
+    return y
 
 
 class RunningMeanStd:

@@ -88,10 +88,15 @@ class FlatParams:
         with torch.no_grad():
             for (n, p), off in zip(self.order, offs):
                 k = p.numel()
-                self.p32[off:off + k].copy_(p.detach().reshape(-1).float())
+                # a channels-last conv weight keeps its layout (OHWI in the flat buffers):
+                # NHWC convolutions then never re-layout the weight or its gradient
+                cl = (p.dim() == 4 and not p.is_contiguous()
+                      and p.is_contiguous(memory_format=torch.channels_last))
+                src = p.detach().permute(0, 2, 3, 1) if cl else p.detach()
+                self.p32[off:off + k].copy_(src.reshape(-1).float())
                 self.p16[off:off + k].copy_(self.p32[off:off + k])
-                p.data = self.p16[off:off + k].view(p.shape)
-                p._ra_grad = self.g[off:off + k].view(p.shape)
+                p.data = self._view(self.p16, off, p.shape, cl)
+                p._ra_grad = self._view(self.g, off, p.shape, cl)
                 if self.alias_grad:
                     p.grad = p._ra_grad
                 else:
@@ -99,6 +104,14 @@ class FlatParams:
                     self._fold_hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
                 # ray_amd.ops backward kernels accumulate straight into p._ra_grad
                 p._ra_direct_grad = True
+
+    @staticmethod
+    def _view(buf, off, shape, channels_last):
+        k = math.prod(shape)
+        if not channels_last:
+            return buf[off:off + k].view(shape)
+        o, i, h, w = shape
+        return buf[off:off + k].view(o, h, w, i).permute(0, 3, 1, 2)
 
     def params(self) -> list[torch.nn.Parameter]:
         return [p for _, p in self.order]

@@ -54,6 +54,10 @@ class Learner:
         self.rank, self.world = rank, world
         torch.manual_seed(config.get("seed") or 0)
         self.module = RLModule(observation_space, action_space, config.get("model")).to(device)
+        if device.type == "cuda":
+            # NHWC conv weights (FlatParams keeps the layout): no per-call weight relayout
+            self.module.to(memory_format=torch.channels_last)
+        self._pinned = {}
         from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams
 
         # bf16 compute weights + fp32 master in the flat optimizer on GPU: no per-forward
@@ -161,6 +165,29 @@ class Learner:
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
             return self.module.forward_train(obs)
 
+    def _h2d(self, x, key):
+        """Host batch field -> device. Large arrays are staged through a persistent pinned
+        buffer per field (multi-threaded host copy, then an async DMA), instead of
+        page-locking a fresh copy of every rollout batch."""
+        dev = self.device
+        if not (isinstance(x, np.ndarray) and dev.type == "cuda" and x.nbytes >= (1 << 20)):
+            return _to_t(x, dev)
+        x = np.ascontiguousarray(x)
+        ent = self._pinned.get(key)
+        if ent is None or ent[0].shape != x.shape or ent[0].numpy().dtype != x.dtype:
+            ent = [torch.empty(x.shape, dtype=torch.from_numpy(x[:0]).dtype, pin_memory=True),
+                   None]
+            self._pinned[key] = ent
+        if ent[1] is not None:
+            ent[1].synchronize()  # the previous DMA out of this buffer has finished
+        from ray_amd._native import _core
+
+        _core.copy_into(ent[0].numpy(), x)
+        t = ent[0].to(dev, non_blocking=True)
+        ent[1] = torch.cuda.Event()
+        ent[1].record()
+        return t
+
     def _values(self, obs_flat, chunk=8192):
         out = []
         with torch.no_grad():
@@ -179,7 +206,7 @@ class Learner:
     def update_ppo(self, batch: dict) -> dict:
         c = self.config
         dev = self.device
-        obs = _to_t(batch["obs"], dev)
+        obs = self._h2d(batch["obs"], "obs")
         T, B = obs.shape[:2]
         rewards = _to_t(batch["rewards"], dev)
         dones = _to_t(batch["terminateds"], dev)
@@ -276,15 +303,30 @@ class Learner:
                 or not self.config.get("learner_cuda_graph", True)
                 or getattr(self, "_graph_failed", False)):
             return None
-        src = (obs, old_di, acts, old_logp, adv, vtarg)
-        key = (mb, self.kl_coeff) + tuple((tuple(t.shape), t.dtype) for t in src)
+        packed = (self.module.discrete and obs.dtype == torch.uint8 and obs.dim() >= 2
+                  and obs[0].numel() % 16 == 0 and old_di.shape[-1] <= 64)
+        if packed:
+            src = (obs, rf.ppo_pack(old_di, acts, old_logp, adv, vtarg))
+        else:
+            src = (obs, old_di, acts, old_logp, adv, vtarg)
+        # the packed graph reads the KL coefficient from device memory: no re-capture when
+        # the adaptive coefficient moves
+        key = (mb, None if packed else self.kl_coeff, packed) + tuple(
+            (tuple(t.shape), t.dtype) for t in src)
+        if packed:
+            if getattr(self, "_kl_dev", None) is None:
+                self._kl_dev = torch.zeros(1, device=self.device)
+            c = self.config
+            self._kl_dev.fill_(self.kl_coeff if c.get("use_kl_loss", True) else 0.0)
         if getattr(self, "_graph_key", None) == key:
             for d, s in zip(self._graph_bufs, src):
                 d.copy_(s)
             return self._graph
         self._graph = None
         try:
-            self._graph = self._capture_ppo_graph(src, mb)
+            self._graph_packed = packed
+            self._graph = self._capture_ppo_graph(src, mb, packed)
+            self._n_captures = getattr(self, "_n_captures", 0) + 1
             self._graph_key = key
         except Exception as e:  # noqa: BLE001
             import warnings
@@ -295,7 +337,7 @@ class Learner:
             self.flat.zero_grad()
         return self._graph
 
-    def _capture_ppo_graph(self, src, mb):
+    def _capture_ppo_graph(self, src, mb, packed=False):
         dev = self.device
         self._graph_bufs = bufs = [torch.empty_like(t) for t in src]
         for d, s in zip(bufs, src):
@@ -303,16 +345,47 @@ class Learner:
         idx = torch.zeros(mb, dtype=torch.long, device=dev)
         stats = torch.zeros(6, device=dev)
         self._graph_io = (idx, stats)
-        obs, old_di, acts, old_logp, adv, vtarg = bufs
+        params = self.flat.params()
+        grads = [p._ra_grad for p in params]
+        one = torch.ones((), device=dev)
+        c = self.config
+        kl_c = self.kl_coeff if c.get("use_kl_loss", True) else 0.0
 
-        def body():
-            self.flat.zero_grad()
-            out = self._fwd(obs.index_select(0, idx))
-            loss, st = self._ppo_loss(out, old_di.index_select(0, idx), acts.index_select(0, idx),
-                                      old_logp.index_select(0, idx), adv.index_select(0, idx),
-                                      vtarg.index_select(0, idx))
-            loss.backward()
-            stats.add_(st.detach())
+        if packed:
+            obs, aux = bufs
+
+            def body():
+                # minibatch frames gathered + cast to bf16 in one kernel; behaviour fields
+                # read by the loss kernel straight from the packed table through `idx`
+                # (stats accumulate in-kernel); gradients come back from autograd.grad and
+                # land in the flat buffer in one multi-tensor copy instead of one
+                # AccumulateGrad add per parameter (the fused bias kernels write their
+                # bias gradients into the zeroed buffer directly)
+                self.flat.g.zero_()
+                with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=self.amp):
+                    out = self.module.forward_train(rf.gather_cast_u8(obs, idx))
+                loss = rf.ppo_loss_packed(
+                    out["action_dist_inputs"], out["vf_preds"], aux, idx, stats,
+                    clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),
+                    vf_coeff=c.get("vf_loss_coeff", 1.0), ent_coeff=c.get("entropy_coeff", 0.0),
+                    kl_coeff=kl_c, has_old=True, kl_dev=self._kl_dev)
+                gs = torch.autograd.grad(loss, params, grad_outputs=one, allow_unused=True)
+                dst = [g for g, x in zip(grads, gs) if x is not None]
+                src_ = [x for x in gs if x is not None]
+                if dst:
+                    torch._foreach_copy_(dst, src_)
+        else:
+            obs, old_di, acts, old_logp, adv, vtarg = bufs
+
+            def body():
+                self.flat.zero_grad()
+                out = self._fwd(obs.index_select(0, idx))
+                loss, st = self._ppo_loss(out, old_di.index_select(0, idx),
+                                          acts.index_select(0, idx),
+                                          old_logp.index_select(0, idx), adv.index_select(0, idx),
+                                          vtarg.index_select(0, idx))
+                loss.backward()
+                stats.add_(st.detach())
 
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -329,14 +402,15 @@ class Learner:
     def _ppo_loss(self, out, old_di, acts, old_logp, adv, vtarg):
         c = self.config
         kl_c = self.kl_coeff if c.get("use_kl_loss", True) else 0.0
-        logits = out["action_dist_inputs"].float()
-        v = out["vf_preds"].float()
-        if self.module.discrete:
+        logits = out["action_dist_inputs"]
+        v = out["vf_preds"]
+        if self.module.discrete:  # the fused kernel reads bf16 heads directly
             return rf.ppo_loss(logits, old_di, acts, old_logp, adv, v, vtarg,
                                clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),
                                vf_coeff=c.get("vf_loss_coeff", 1.0),
                                ent_coeff=c.get("entropy_coeff", 0.0), kl_coeff=kl_c)
         # DiagGaussian (continuous) path
+        logits, v = logits.float(), v.float()
         mean, log_std = logits.chunk(2, -1)
         logp = gaussian_logp(acts, mean, log_std)
         ratio = torch.exp(logp - old_logp)
@@ -359,7 +433,7 @@ class Learner:
     def update_vtrace(self, batch: dict) -> dict:
         c = self.config
         dev = self.device
-        obs = _to_t(batch["obs"], dev)
+        obs = self._h2d(batch["obs"], "obs")
         T, B = obs.shape[:2]
         rewards = _to_t(batch["rewards"], dev)
         dones = _to_t(batch["terminateds"], dev)

@@ -63,8 +63,23 @@ class NatureCNN(nn.Module):
                 x = cast_scale_u8(x).to(self.fc[0].weight.dtype)
             else:
                 x = x.float().mul_(1.0 / 255.0)
+        # NHWC frames are a channels-last NCHW view: MIOpen runs NHWC implicit-GEMM convs
+        # (with channels-last weights no per-call weight relayout), the conv bias + ReLU
+        # is one fused pass (and its backward one pass + the bias reduction), and the
+        # flatten below is NHWC order, a free view of the channels-last output
         x = x.permute(0, 3, 1, 2)
-        return self.fc(self.convs(x).flatten(1))
+        fused = x.is_cuda and x.dtype == torch.bfloat16
+        mods = list(self.convs)
+        for conv, act in zip(mods[0::2], mods[1::2]):
+            if fused:
+                from ray_amd.ops.functional import bias_relu
+
+                w = conv.weight.to(x.dtype)
+                x = bias_relu(F.conv2d(x, w, None, conv.stride, conv.padding),
+                              conv.bias.to(x.dtype))
+            else:
+                x = act(conv(x))
+        return self.fc(x.permute(0, 2, 3, 1).flatten(1))
 
 
 class RLModule(nn.Module):

@@ -48,9 +48,17 @@ def main():
         st = lr.update_ppo(batch)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    # phase: host -> HBM staging of the 141 MB frame batch alone
+    t1 = time.perf_counter()
+    for _ in range(a.iters):
+        lr._h2d(batch["obs"], "obs")
+    torch.cuda.synchronize()
+    h2d = (time.perf_counter() - t1) / a.iters
     print(json.dumps({"metric": "ppo_learner_frames_per_sec", "value": round(T * B / dt, 1),
                       "ms_per_update": round(dt * 1e3, 2), "sgd_steps": st["num_minibatches"],
-                      "ms_per_sgd_step": round(dt * 1e3 / st["num_minibatches"], 3)}), flush=True)
+                      "ms_per_sgd_step": round(dt * 1e3 / st["num_minibatches"], 3),
+                      "ms_obs_h2d": round(h2d * 1e3, 2),
+                      "graph_captures": getattr(lr, "_n_captures", None)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -135,6 +135,112 @@ def test_ppo_loss(cuda_device, A):
     assert torch.allclose(vp.grad, vr.grad, atol=1e-6, rtol=1e-3)
 
 
+def _ppo_case(dev, N, A, seed):
+    torch.manual_seed(seed)
+    logits = torch.randn(N, A, device=dev)
+    old = logits + 0.3 * torch.randn(N, A, device=dev)
+    acts = torch.randint(0, A, (N,), device=dev)
+    old_lp = torch.log_softmax(old, -1).gather(-1, acts[:, None])[:, 0]
+    adv = torch.randn(N, device=dev)
+    vp = torch.randn(N, device=dev)
+    vt = torch.randn(N, device=dev) * 3
+    return logits, old, acts, old_lp, adv, vp, vt
+
+
+def test_ppo_loss_bf16_heads(cuda_device):
+    """bf16 logits / values are read directly by the kernel; grads come back bf16."""
+    logits, old, acts, old_lp, adv, vp, vt = _ppo_case(cuda_device, 700, 6, 16)
+    kw = dict(clip=0.2, vf_clip=4.0, vf_coeff=0.5, ent_coeff=0.01, kl_coeff=0.2)
+    lb = logits.bfloat16().requires_grad_()
+    vb = vp.bfloat16().requires_grad_()
+    loss, stats = rf.ppo_loss(lb, old, acts, old_lp, adv, vb, vt, **kw)
+    lr_ = lb.detach().float().requires_grad_()
+    vr = vb.detach().float().requires_grad_()
+    lref, sref = ref.ppo_loss(lr_, old, acts, old_lp, adv, vr, vt, **kw)
+    assert torch.allclose(stats, sref, atol=1e-4, rtol=1e-3)
+    (2.0 * loss).backward()
+    (2.0 * lref).backward()
+    assert lb.grad.dtype == torch.bfloat16 and vb.grad.dtype == torch.bfloat16
+    assert _rel(lb.grad, lr_.grad) < 1e-2
+    assert _rel(vb.grad, vr.grad) < 1e-2
+
+
+def test_ppo_loss_packed_gathers_rows(cuda_device):
+    """Packed behaviour table + in-kernel gather == loss over the gathered minibatch;
+    stats accumulate across calls."""
+    Nf, A, mb = 2000, 6, 500
+    logits_f, old, acts, old_lp, adv, vp_f, vt = _ppo_case(cuda_device, Nf, A, 17)
+    aux = rf.ppo_pack(old, acts, old_lp, adv, vt)
+    idx = torch.randperm(Nf, device=cuda_device)[:mb]
+    kw = dict(clip=0.2, vf_clip=4.0, vf_coeff=0.5, ent_coeff=0.01, kl_coeff=0.2)
+    lg = logits_f[idx].bfloat16().requires_grad_()
+    vv = vp_f[idx].bfloat16().requires_grad_()
+    stats = torch.zeros(6, device=cuda_device)
+    h = rf.ppo_loss_packed(lg, vv, aux, idx, stats, **kw)
+    rf.ppo_loss_packed(lg.detach(), vv.detach(), aux, idx, stats, **kw)  # accumulates
+    lr_ = lg.detach().float().requires_grad_()
+    vr = vv.detach().float().requires_grad_()
+    lref, sref = ref.ppo_loss(lr_, old[idx], acts[idx], old_lp[idx], adv[idx], vr, vt[idx], **kw)
+    assert torch.allclose(stats, 2 * sref, atol=2e-4, rtol=1e-3)
+    torch.autograd.backward(h, torch.ones((), device=cuda_device))
+    lref.backward()
+    assert _rel(lg.grad, lr_.grad) < 1e-2
+    assert _rel(vv.grad, vr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(64, 32, 20, 20), (37, 64, 9, 9), (500, 64, 7, 7), (300, 512)])
+def test_bias_relu(cuda_device, shape):
+    torch.manual_seed(18)
+    h = torch.randn(*shape, device=cuda_device).bfloat16()
+    if h.dim() == 4:
+        h = h.contiguous(memory_format=torch.channels_last)
+    h.requires_grad_()
+    C = shape[1]
+    b = (0.3 * torch.randn(C, device=cuda_device)).bfloat16().requires_grad_()
+    y = rf.bias_relu(h, b)
+    assert y.shape == h.shape and y.stride() == h.stride()
+    hr, br = h.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = torch.relu(hr + (br.view(1, -1, 1, 1) if h.dim() == 4 else br))
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    if h.dim() == 4:
+        g = g.contiguous(memory_format=torch.channels_last)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    # the mask comes from the bf16 output: rows where h+b rounds to exactly 0 may differ
+    assert _rel(h.grad, hr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_bias_relu_flat_sink(cuda_device):
+    """With a flat-managed bias the gradient is written into the flat buffer directly."""
+    from ray_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(19)
+    conv = torch.nn.Conv2d(4, 32, 8, 4).to(cuda_device).to(memory_format=torch.channels_last)
+    flat = FlatParams(conv, dtype=torch.bfloat16, grad_dtype=torch.bfloat16)
+    assert conv.weight.is_contiguous(memory_format=torch.channels_last)
+    x = torch.randn(16, 84, 84, 4, device=cuda_device).bfloat16().permute(0, 3, 1, 2)
+    flat.zero_grad()
+    y = rf.bias_relu(torch.nn.functional.conv2d(x, conv.weight, None, 4), conv.bias)
+    y.float().sum().backward()
+    wr = conv.weight.detach().float().requires_grad_()
+    br = conv.bias.detach().float().requires_grad_()
+    yr = torch.relu(torch.nn.functional.conv2d(x.float(), wr, br, 4))
+    yr.sum().backward()
+    assert _rel(conv.bias._ra_grad, br.grad) < 2e-2
+    assert _rel(conv.weight._ra_grad, wr.grad) < 2e-2
+
+
+def test_gather_cast_u8(cuda_device):
+    x = torch.randint(0, 256, (300, 84, 84, 4), dtype=torch.uint8, device=cuda_device)
+    idx = torch.randperm(300, device=cuda_device)[:77]
+    y = rf.gather_cast_u8(x, idx)
+    assert y.dtype == torch.bfloat16 and y.shape == (77, 84, 84, 4)
+    yr = (x[idx].float() * (1.0 / 255.0)).bfloat16()
+    assert torch.allclose(y.float(), yr.float(), atol=4e-3, rtol=0)
+
+
 def test_obsnorm(cuda_device):
     torch.manual_seed(7)
     rms = rf.RunningMeanStd(17, device=cuda_device)
@@ -177,7 +283,7 @@ def test_image_normalize_vector_path(cuda_device, C):
     assert torch.allclose(yb.float().cpu(), yr, atol=2e-2, rtol=8e-3)
 
 
-@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("mode", ["fused", "split", "split2"])
 @pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2), (2, 128, 1)])
 def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch):
     monkeypatch.setattr(rf, "_ATTN_BWD", mode)
