@@ -88,6 +88,12 @@ _SIGS = {
     "ra_resize_bilinear": [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p],
     "ra_cast_scale_u8": [c_void_p, c_void_p, c_long, c_float, c_void_p],
     "ra_gather_cast_u8": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_float, c_void_p],
+    "ra_conv_supported": [c_int] * 6,
+    "ra_conv_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 8
+                   + [c_float, c_int, c_void_p],
+    "ra_conv_wgrad_work": [c_int] * 8,
+    "ra_conv_wgrad": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int]
+                     + [c_int] * 8 + [c_float, c_void_p],
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],
     "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],

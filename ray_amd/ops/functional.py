@@ -810,6 +810,28 @@ def _nhwc_rows(t):
     return None
 
 
+def _relu_bias_bwd(dy, y, bias):
+    """dh = dy * (y > 0) and the bias gradient (written into the flat sink, returning None,
+    or returned) for a ReLU output y in [M, C] row layout (2-D or channels-last)."""
+    if _nhwc_rows(dy) is None:
+        dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 \
+            else dy.contiguous()
+    dy2, y2 = _nhwc_rows(dy), _nhwc_rows(y)
+    M, C = y2.shape
+    L = _lib.lib()
+    dh = torch.empty_like(y)
+    work = torch.empty(L.ra_relu_bwd_work(M, C), device=y.device, dtype=torch.float32)
+    sink = _grad_sink(bias)
+    db = sink if sink is not None else torch.empty_like(bias)
+    flags = (1 if sink is not None else 0) | (2 * _sink_f32(db))
+    check(L.ra_relu_bwd_bias(ptr(dy2), ptr(y2), ptr(_nhwc_rows(dh)), ptr(db), ptr(work), M, C,
+                             flags, stream_ptr()), "relu_bwd_bias")
+    if sink is not None:
+        _grad_done(bias)
+        return dh, None
+    return dh, db
+
+
 class _BiasReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, bias):
@@ -825,24 +847,7 @@ class _BiasReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        bias = ctx.bias
-        if _nhwc_rows(dy) is None:
-            dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 \
-                else dy.contiguous()
-        dy2, y2 = _nhwc_rows(dy), _nhwc_rows(y)
-        M, C = y2.shape
-        L = _lib.lib()
-        dh = torch.empty_like(y)
-        work = torch.empty(L.ra_relu_bwd_work(M, C), device=y.device, dtype=torch.float32)
-        sink = _grad_sink(bias)
-        db = sink if sink is not None else torch.empty_like(bias)
-        flags = (1 if sink is not None else 0) | (2 * _sink_f32(db))
-        check(L.ra_relu_bwd_bias(ptr(dy2), ptr(y2), ptr(_nhwc_rows(dh)), ptr(db), ptr(work), M, C,
-                                 flags, stream_ptr()), "relu_bwd_bias")
-        if sink is not None:
-            _grad_done(bias)
-            return dh, None
-        return dh, db
+        return _relu_bias_bwd(dy, y, ctx.bias)
 
 
 def bias_relu(h, bias):
@@ -857,6 +862,95 @@ def bias_relu(h, bias):
     if bias is not None:
         h = h + (bias.view(1, -1, 1, 1) if h.dim() == 4 else bias).to(h.dtype)
     return torch.relu(h)
+
+
+# --------------------------------------------------------------------- conv + bias + ReLU
+def _is_ohwi(w):
+    return w.dim() == 4 and w.permute(0, 2, 3, 1).is_contiguous()
+
+
+class _ConvBiasReLU(torch.autograd.Function):
+    """relu(conv2d(x, w, stride) + b) on the conv.hip MFMA kernels. x is a bf16
+    channels-last NCHW activation, or the uint8 NHWC frame batch (rows ``idx``, scaled by
+    ``scale`` while loading). Backward: one fused ReLU-mask + bias-gradient pass, the
+    MFMA weight-gradient kernel (written straight into the flat gradient buffer), and the
+    input gradient on MIOpen (only when x is a differentiable activation)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, idx, scale):
+        u8 = x.dtype == torch.uint8
+        if u8:
+            xh = x
+            B = idx.shape[0] if idx is not None else x.shape[0]
+            H, W, C = x.shape[1:]
+        else:
+            xh = x.permute(0, 2, 3, 1)
+            B, C, H, W = x.shape
+        O, I, KH, KW = w.shape
+        OH, OW = (H - KH) // stride + 1, (W - KW) // stride + 1
+        y = torch.empty((B, OH, OW, O), device=x.device, dtype=torch.bfloat16).permute(0, 3, 1, 2)
+        check(_lib.lib().ra_conv_fwd(ptr(xh), ptr(idx), int(u8), ptr(w), ptr(b), ptr(y), B, H, W,
+                                     C, KH, KW, stride, O, float(scale), 1, stream_ptr()),
+              "conv_fwd")
+        ctx.save_for_backward(x, w, y, idx)
+        ctx.geom = (u8, B, H, W, C, KH, KW, stride, O, float(scale))
+        ctx.bias = b
+        ctx.weight = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y, idx = ctx.saved_tensors
+        u8, B, H, W, C, KH, KW, S, O, scale = ctx.geom
+        dh, db = _relu_bias_bwd(dy, y, ctx.bias)
+        L = _lib.lib()
+        work = torch.empty(L.ra_conv_wgrad_work(B, H, W, C, KH, KW, S, O), device=dy.device,
+                           dtype=torch.float32)
+        sink = _grad_sink(ctx.weight)
+        if sink is not None and not _is_ohwi(sink):
+            sink = None
+        dw = sink if sink is not None else torch.empty(
+            (O, KH, KW, C), device=dy.device, dtype=w.dtype).permute(0, 3, 1, 2)
+        flags = (1 if sink is not None else 0) | (2 * _sink_f32(dw))
+        xh = x if u8 else x.permute(0, 2, 3, 1)
+        check(L.ra_conv_wgrad(ptr(xh), ptr(idx), int(u8), ptr(_nhwc_rows(dh)), ptr(work), ptr(dw),
+                              flags, B, H, W, C, KH, KW, S, O, scale, stream_ptr()), "conv_wgrad")
+        if sink is not None:
+            _grad_done(ctx.weight)
+            dw = None
+        dx = None
+        if not u8 and ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dh, x, w, None, [S, S], [0, 0], [1, 1], False,
+                                                     [0, 0], 1, [True, False, False])[0]
+        return dx, dw, db, None, None, None
+
+
+def conv2d_bias_relu(x, w, b, stride, idx=None, scale=1.0 / 255.0):
+    """relu(conv2d(x, w, b, stride)) (no padding) for the Nature-CNN layer shapes on the
+    MFMA kernels; other shapes / devices fall back to MIOpen + ``bias_relu``.
+
+    x: bf16 channels-last NCHW activations, or uint8 NHWC frames (the first layer: rows
+    ``idx`` of the batch, multiplied by ``scale``). Returns channels-last NCHW bf16."""
+    u8 = x.dtype == torch.uint8
+    ok = (_hip(x) and w.dtype == torch.bfloat16 and b is not None and b.dtype == torch.bfloat16
+          and _is_ohwi(w) and (idx is None or u8))
+    if ok:
+        if u8:
+            ok = x.dim() == 4 and x.is_contiguous() and x.shape[3] == w.shape[1]
+        else:
+            ok = x.dtype == torch.bfloat16 and _nhwc_rows(x) is not None and x.shape[1] == w.shape[1]
+    if ok:  # the kernels index the input with 32-bit element offsets
+        O, I, KH, KW = w.shape
+        ok = x.numel() < 2 ** 31 and bool(_lib.lib().ra_conv_supported(KH, KW, I, stride, O,
+                                                                          int(u8)))
+    if ok and x.shape[0] > 0:
+        return _ConvBiasReLU.apply(x, w, b, stride,
+                                   idx.long().contiguous() if idx is not None else None, scale)
+    if idx is not None:
+        x = x.index_select(0, idx)
+    if u8:
+        x = (x.float() * scale).to(w.dtype).permute(0, 3, 1, 2)
+    return bias_relu(torch.nn.functional.conv2d(x, w, None, stride), b)
 
 
 def gather_cast_u8(x_u8, idx, scale=1.0 / 255.0):

@@ -355,7 +355,8 @@ class Learner:
             obs, aux = bufs
 
             def body():
-                # minibatch frames gathered + cast to bf16 in one kernel; behaviour fields
+                # minibatch frames read by the first conv kernel straight from the uint8
+                # batch (gather + /255 fused into its loads); behaviour fields
                 # read by the loss kernel straight from the packed table through `idx`
                 # (stats accumulate in-kernel); gradients come back from autograd.grad and
                 # land in the flat buffer in one multi-tensor copy instead of one
@@ -363,7 +364,7 @@ class Learner:
                 # bias gradients into the zeroed buffer directly)
                 self.flat.g.zero_()
                 with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=self.amp):
-                    out = self.module.forward_train(rf.gather_cast_u8(obs, idx))
+                    out = self.module.forward_train(obs, idx=idx)
                 loss = rf.ppo_loss_packed(
                     out["action_dist_inputs"], out["vf_preds"], aux, idx, stats,
                     clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),

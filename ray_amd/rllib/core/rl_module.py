@@ -54,8 +54,29 @@ class NatureCNN(nn.Module):
         self.fc = nn.Sequential(nn.Linear(n, out_dim), nn.ReLU())
         self.out_dim = out_dim
 
-    def forward(self, x):
-        # x: [B, H, W, C] uint8 or float
+    def forward(self, x, idx=None):
+        """x: [B, H, W, C] uint8 or float frames; idx: optional rows of x to encode (the
+        learner's minibatch — the first conv gathers them itself on GPU)."""
+        mods = list(self.convs)
+        convs, acts = mods[0::2], mods[1::2]
+        if x.is_cuda and convs[0].weight.dtype == torch.bfloat16:
+            # GPU: MFMA NHWC implicit-GEMM convs with fused bias + ReLU (ray_amd.ops conv.hip);
+            # the first layer reads the uint8 frames (and the minibatch rows) directly.
+            # NHWC frames are a channels-last NCHW view, and the flatten below is NHWC
+            # order: a free view of the channels-last output
+            from ray_amd.ops.functional import conv2d_bias_relu
+
+            if x.dtype != torch.uint8:
+                if idx is not None:
+                    x = x.index_select(0, idx)
+                    idx = None
+                x = x.to(torch.bfloat16).permute(0, 3, 1, 2)
+            for i, conv in enumerate(convs):
+                x = conv2d_bias_relu(x, conv.weight, conv.bias, conv.stride[0],
+                                     idx=idx if i == 0 else None)
+            return self.fc(x.permute(0, 2, 3, 1).flatten(1))
+        if idx is not None:
+            x = x.index_select(0, idx)
         if x.dtype == torch.uint8:
             if x.is_cuda:
                 from ray_amd.ops.functional import cast_scale_u8
@@ -63,22 +84,9 @@ class NatureCNN(nn.Module):
                 x = cast_scale_u8(x).to(self.fc[0].weight.dtype)
             else:
                 x = x.float().mul_(1.0 / 255.0)
-        # NHWC frames are a channels-last NCHW view: MIOpen runs NHWC implicit-GEMM convs
-        # (with channels-last weights no per-call weight relayout), the conv bias + ReLU
-        # is one fused pass (and its backward one pass + the bias reduction), and the
-        # flatten below is NHWC order, a free view of the channels-last output
         x = x.permute(0, 3, 1, 2)
-        fused = x.is_cuda and x.dtype == torch.bfloat16
-        mods = list(self.convs)
-        for conv, act in zip(mods[0::2], mods[1::2]):
-            if fused:
-                from ray_amd.ops.functional import bias_relu
-
-                w = conv.weight.to(x.dtype)
-                x = bias_relu(F.conv2d(x, w, None, conv.stride, conv.padding),
-                              conv.bias.to(x.dtype))
-            else:
-                x = act(conv(x))
+        for conv, act in zip(convs, acts):
+            x = act(conv(x))
         return self.fc(x.permute(0, 2, 3, 1).flatten(1))
 
 
@@ -123,11 +131,19 @@ class RLModule(nn.Module):
             return obs
         return obs.reshape(obs.shape[0], -1).float()
 
-    def forward_train(self, obs):
+    def _encode(self, enc, x, idx):
+        if idx is None:
+            return enc(x)
+        if self.is_image:  # the conv encoder gathers the rows itself
+            return enc(x, idx)
+        return enc(x.index_select(0, idx))
+
+    def forward_train(self, obs, idx=None):
+        """idx: optional rows of ``obs`` (a minibatch of a resident train batch)."""
         x = self._flat(obs)
-        h = self.encoder(x)
+        h = self._encode(self.encoder, x, idx)
         logits = self.pi(h)
-        hv = h if self.vf_encoder is None else self.vf_encoder(x)
+        hv = h if self.vf_encoder is None else self._encode(self.vf_encoder, x, idx)
         v = self.vf(hv).squeeze(-1)
         return {"action_dist_inputs": logits, "vf_preds": v}
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PPO learner kernels + learner bench + kernel trace (round 2, learner fusion pass)
+# conv kernels: numerics, per-layer microbench (knob sweeps), learner bench + trace
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
@@ -7,9 +7,8 @@ export TMPDIR=/tmp PYTHONPATH="$R"
 mkdir -p gpurun_out
 rm -rf gpurun_out/ppoprof4
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_kernels_gpu.py -k "ppo or bias_relu or gather_cast or conv or nature" > gpurun_out/ppo4_tests.log 2>&1 || exit $?
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
-  tests/test_rllib_gpu.py > gpurun_out/ppo4_rllib_gpu.log 2>&1 || exit $?
+  tests/test_kernels_gpu.py -k "conv or nature or bias_relu" > gpurun_out/conv_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/conv_bench.py --fwd-caps 256,512,1024,4096 --wg-rows 128,256,512 > gpurun_out/conv_bench.log 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/ppo_learner_bench.py > gpurun_out/ppo_learner4.log 2>&1 || exit $?
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ppoprof4" -o run -- python3 "$R/scripts/ppo_learner_bench.py" --iters 2 --warmup 1 > "$R/gpurun_out/ppoprof4.log" 2>&1 || exit $?
 echo done

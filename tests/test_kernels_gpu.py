@@ -232,6 +232,59 @@ def test_bias_relu_flat_sink(cuda_device):
     assert _rel(conv.weight._ra_grad, wr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("cfg", [(84, 4, 32, 8, 4, True), (84, 4, 32, 8, 4, False),
+                                 (20, 32, 64, 4, 2, False), (9, 64, 64, 3, 1, False)])
+def test_conv_bias_relu(cuda_device, cfg):
+    """MFMA NHWC conv (+bias+ReLU) fwd, weight grad (and MIOpen input grad) vs fp32 torch;
+    the uint8 first layer gathers its rows by index."""
+    HW, C, O, Kk, S, u8 = cfg
+    torch.manual_seed(20)
+    Nfull, B = 70, 45
+    w = (torch.randn(O, C, Kk, Kk, device=cuda_device) / (C * Kk * Kk) ** 0.5).bfloat16()
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_()
+    b = (0.1 * torch.randn(O, device=cuda_device)).bfloat16().requires_grad_()
+    idx = None
+    if u8:
+        frames = torch.randint(0, 256, (Nfull, HW, HW, C), dtype=torch.uint8, device=cuda_device)
+        idx = torch.randperm(Nfull, device=cuda_device)[:B]
+        x = frames
+        xr = (frames[idx].float() * (1.0 / 255.0)).permute(0, 3, 1, 2)
+    else:
+        x0 = torch.randn(B, HW, HW, C, device=cuda_device).bfloat16().requires_grad_()
+        x = x0.permute(0, 3, 1, 2)
+        xr0 = x0.detach().float().requires_grad_()
+        xr = xr0.permute(0, 3, 1, 2)
+    y = rf.conv2d_bias_relu(x, w, b, S, idx=idx)
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_()
+    yr = torch.relu(torch.nn.functional.conv2d(xr, wr, br, S))
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr).contiguous(memory_format=torch.channels_last)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+    if not u8:
+        assert _rel(x0.grad, xr0.grad) < 2e-2
+
+
+def test_nature_cnn_fused_matches_eager(cuda_device):
+    """The fused GPU encoder (u8 frames + idx) == the generic path on the same weights."""
+    from ray_amd.rllib.core.rl_module import NatureCNN
+
+    torch.manual_seed(21)
+    net = NatureCNN((84, 84, 4)).to(cuda_device).bfloat16()
+    net = net.to(memory_format=torch.channels_last)
+    frames = torch.randint(0, 256, (64, 84, 84, 4), dtype=torch.uint8, device=cuda_device)
+    idx = torch.randperm(64, device=cuda_device)[:40]
+    h = net(frames, idx)
+    ref_net = NatureCNN((84, 84, 4)).to(cuda_device)
+    ref_net.load_state_dict({k: v.float() for k, v in net.state_dict().items()})
+    hr = ref_net(frames[idx].float() * (1.0 / 255.0))
+    assert _rel(h, hr) < 2e-2
+
+
 def test_gather_cast_u8(cuda_device):
     x = torch.randint(0, 256, (300, 84, 84, 4), dtype=torch.uint8, device=cuda_device)
     idx = torch.randperm(300, device=cuda_device)[:77]
