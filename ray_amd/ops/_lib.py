@@ -92,7 +92,7 @@ _SIGS = {
     "ra_conv_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 8
                    + [c_float, c_int, c_void_p],
     "ra_conv_wgrad_work": [c_int] * 8,
-    "ra_conv_wgrad": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int]
+    "ra_conv_wgrad": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p, c_int]
                      + [c_int] * 8 + [c_float, c_void_p],
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],

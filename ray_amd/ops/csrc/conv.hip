@@ -14,7 +14,7 @@
 // gathered/converted bf16 copy of the frames is ever written.
 //
 // Forward orientation (mfma_f32_32x32x16_bf16, C^T = W . im2col^T): A = weights
-// (rows = output channels) from an LDS copy of the whole filter bank, B = im2col^T
+// (rows = output channels) from an LDS copy of a 32-filter slice, B = im2col^T
 // (columns = 32 output pixels per wave) loaded straight from global memory: lane
 // (r, h) needs pixel r's 8 contiguous k values 8h..8h+7 of a 16-wide k step — one
 // 16-byte load (8 bytes for uint8). Accumulator register i holds channel
@@ -70,68 +70,64 @@ struct ConvArgs {
 };
 
 // ------------------------------------------------------------------ forward
+// grid (ceil(M/128), NOUT/32): workgroup = 4 waves x 32 pixels, one 32-channel slice of
+// the filter bank in LDS (<= 37 KB static: no > 64 KB dynamic-LDS opt-in, which graph
+// replays do not honour).
 template <int KH, int KW, int C, int S, int NOUT, bool U8>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
-  constexpr int K = KH * KW * C, KWC = KW * C, LDW = K + 8, NT = NOUT / 32, KS = KWC / 16;
+  constexpr int K = KH * KW * C, KWC = KW * C, LDW = K + 8, KS = KWC / 16;
   static_assert(KWC % 16 == 0 && NOUT % 32 == 0, "conv tile shape");
-  extern __shared__ __attribute__((aligned(16))) bf16_t Ws[];  // [NOUT][LDW]
-  for (int i = threadIdx.x; i < NOUT * (K / 8); i += 256) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ws[32 * LDW];
+  const int nb = blockIdx.y * 32;
+  for (int i = threadIdx.x; i < 32 * (K / 8); i += 256) {
     const int n = i / (K / 8), k8 = i - n * (K / 8);
-    *reinterpret_cast<uint4*>(Ws + n * LDW + k8 * 8) = reinterpret_cast<const uint4*>(a.w)[i];
+    *reinterpret_cast<uint4*>(Ws + n * LDW + k8 * 8) =
+        reinterpret_cast<const uint4*>(a.w + (long)(nb + n) * K)[k8];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int ohw = a.OH * a.OW, M = a.B * ohw, tiles = (M + 31) / 32;
-  // grid-stride over 32-pixel tiles: the filter bank is staged once per workgroup
-  for (int tile = blockIdx.x * 4 + wv; tile < tiles; tile += gridDim.x * 4) {
-    const int m0 = tile * 32;
-    const int m = min(m0 + r, M - 1);  // tail lanes compute a duplicate and skip the store
-    const int b = m / ohw, rem = m - b * ohw, oh = rem / a.OW, ow = rem - oh * a.OW;
-    const long img = (U8 && a.idx) ? a.idx[b] : (long)b;
-    const long base = img * (long)a.H * a.W * C + ((long)oh * S * a.W + (long)ow * S) * C + 8 * h;
-    f32x16 acc[NT];
+  const int ohw = a.OH * a.OW, M = a.B * ohw;
+  const int m0 = (blockIdx.x * 4 + wv) * 32;
+  if (m0 >= M) return;  // no barrier follows
+  const int m = min(m0 + r, M - 1);  // tail lanes compute a duplicate and skip the store
+  const int b = m / ohw, rem = m - b * ohw, oh = rem / a.OW, ow = rem - oh * a.OW;
+  const long img = (U8 && a.idx) ? a.idx[b] : (long)b;
+  const long base = img * (long)a.H * a.W * C + ((long)oh * S * a.W + (long)ow * S) * C + 8 * h;
+  f32x16 acc;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  for (int kh = 0; kh < KH; ++kh) {
+    const long rb = base + (long)kh * a.W * C;
+    bf16x8_t bf[KS];
 #pragma unroll
-    for (int kh = 0; kh < KH; ++kh) {
-      const long rb = base + (long)kh * a.W * C;
-      bf16x8_t bf[KS];
-#pragma unroll
-      for (int kc = 0; kc < KS; ++kc) {
-        if constexpr (U8)
-          bf[kc] = u8x8_to_bf16(*reinterpret_cast<const uint2*>(
-                                    reinterpret_cast<const uint8_t*>(a.x) + rb + kc * 16),
-                                a.scale);
-        else
-          bf[kc] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16_t*>(a.x) + rb +
-                                                      kc * 16);
-      }
-#pragma unroll
-      for (int kc = 0; kc < KS; ++kc) {
-        const int k0 = kh * KWC + kc * 16 + 8 * h;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[t] = mfma32(*reinterpret_cast<const bf16x8_t*>(Ws + (t * 32 + r) * LDW + k0),
-                          bf[kc], acc[t]);
-      }
+    for (int kc = 0; kc < KS; ++kc) {
+      if constexpr (U8)
+        bf[kc] = u8x8_to_bf16(*reinterpret_cast<const uint2*>(
+                                  reinterpret_cast<const uint8_t*>(a.x) + rb + kc * 16),
+                              a.scale);
+      else
+        bf[kc] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16_t*>(a.x) + rb +
+                                                    kc * 16);
     }
-    if (m0 + r >= M) continue;
-    bf16_t* y = reinterpret_cast<bf16_t*>(a.out) + (long)(m0 + r) * NOUT;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int kc = 0; kc < KS; ++kc) {
+      const int k0 = kh * KWC + kc * 16 + 8 * h;
+      acc = mfma32(*reinterpret_cast<const bf16x8_t*>(Ws + r * LDW + k0), bf[kc], acc);
+    }
+  }
+  if (m0 + r >= M) return;
+  bf16_t* y = reinterpret_cast<bf16_t*>(a.out) + (long)(m0 + r) * NOUT + nb;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = t * 32 + 8 * q + 4 * h;
-        float v[4];
+  for (int q = 0; q < 4; ++q) {
+    const int n = 8 * q + 4 * h;
+    float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = acc[t][4 * q + j] + (a.bias ? bf2f(a.bias[n + j]) : 0.f);
-          if (a.relu) v[j] = fmaxf(v[j], 0.f);
-        }
-        *reinterpret_cast<uint2*>(y + n) = pack4(v);
-      }
+    for (int j = 0; j < 4; ++j) {
+      v[j] = acc[4 * q + j] + (a.bias ? bf2f(a.bias[nb + n + j]) : 0.f);
+      if (a.relu) v[j] = fmaxf(v[j], 0.f);
+    }
+    *reinterpret_cast<uint2*>(y + n) = pack4(v);
   }
 }
 
@@ -306,21 +302,9 @@ static int config_id(int KH, int KW, int C, int S, int NOUT, int u8) {
 
 template <int KH, int KW, int C, int S, int NOUT, bool U8>
 static int launch_fwd(const ConvArgs& a, hipStream_t st) {
-  constexpr int K = KH * KW * C;
-  const size_t lds = (size_t)NOUT * (K + 8) * sizeof(bf16_t);
-  auto kern = conv_fwd_kernel<KH, KW, C, S, NOUT, U8>;
-  static bool attr = false;
-  if (!attr) {  // > 64 KiB of dynamic LDS must be opted into once per kernel
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
   const int M = a.B * a.OH * a.OW;
-  int wgs = (M + 127) / 128;
-  const int cap = ra_knobs[4] > 0 ? ra_knobs[4] : 512;  // filter-bank stagings per launch
-  if (wgs > cap) wgs = cap;
-  hipLaunchKernelGGL(kern, dim3(wgs), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<KH, KW, C, S, NOUT, U8>), dim3((M + 127) / 128, NOUT / 32),
+                     dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -376,9 +360,10 @@ RA_EXPORT long ra_conv_wgrad_work(int B, int H, int W, int C, int KH, int KW, in
 
 // dW [NOUT][K] (OHWI) (+)= sum over output pixels of dY^T . im2col(x).
 // flags: bit0 accumulate into dw, bit1 dw is fp32 (else bf16).
+// work_cap: floats available at `work` (checked: the partial slab size depends on knob 7).
 RA_EXPORT int ra_conv_wgrad(const void* x, const long* idx, int u8, const void* dy, float* work,
-                            void* dw, int flags, int B, int H, int W, int C, int KH, int KW, int S,
-                            int NOUT, float scale, hipStream_t st) {
+                            long work_cap, void* dw, int flags, int B, int H, int W, int C, int KH,
+                            int KW, int S, int NOUT, float scale, hipStream_t st) {
   const int id = config_id(KH, KW, C, S, NOUT, u8);
   if (id == kUnsupported || H < KH || W < KW) return hipErrorNotSupported;
   ConvArgs a{};
@@ -388,6 +373,7 @@ RA_EXPORT int ra_conv_wgrad(const void* x, const long* idx, int u8, const void* 
   const int M = B * a.OH * a.OW, K = KH * KW * C;
   a.rows_per_wg = wgrad_rows(M, K, NOUT);
   const int P = (M + a.rows_per_wg - 1) / a.rows_per_wg;
+  if ((long)P * NOUT * K > work_cap) return hipErrorInvalidValue;
   int e;
   switch (id) {
     case 0: e = launch_wgrad<8, 8, 4, 4, 32, true>(a, P, st); break;

@@ -347,7 +347,9 @@ class Learner:
         self._graph_io = (idx, stats)
         params = self.flat.params()
         grads = [p._ra_grad for p in params]
-        one = torch.ones((), device=dev)
+        # the upstream gradient of the loss handle: the graph reads it by address, so it
+        # must outlive this call (a freed scalar is reused by later allocations)
+        self._graph_one = one = torch.ones((), device=dev)
         c = self.config
         kl_c = self.kl_coeff if c.get("use_kl_loss", True) else 0.0
 
@@ -375,6 +377,8 @@ class Learner:
                 src_ = [x for x in gs if x is not None]
                 if dst:
                     torch._foreach_copy_(dst, src_)
+                if rf._CONV_WGRAD_STREAM:
+                    rf.join_side_streams()  # conv weight gradients ran on the side stream
         else:
             obs, old_di, acts, old_logp, adv, vtarg = bufs
 

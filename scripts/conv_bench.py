@@ -61,8 +61,6 @@ def main():
         y = torch.empty(B, OH, OH, O, device=dev, dtype=torch.bfloat16)
         dy = torch.randn(B, OH, OH, O, device=dev).bfloat16()
         dw = torch.empty(O, K, K, C, device=dev, dtype=torch.bfloat16)
-        work = torch.empty(L.ra_conv_wgrad_work(B, HW, HW, C, K, K, S, O) + (1 << 22),
-                           device=dev)
         xh = xin if u8 else xin.permute(0, 2, 3, 1)
         rec = {"layer": name, "B": B}
         for cap in [int(v) for v in a.fwd_caps.split(",")]:
@@ -73,8 +71,10 @@ def main():
         L.ra_set_knob(4, 0)
         for rows in [int(v) for v in a.wg_rows.split(",")]:
             L.ra_set_knob(7, rows)
+            # partial-slab size depends on the rows knob: size it AFTER setting the knob
+            work = torch.empty(L.ra_conv_wgrad_work(B, HW, HW, C, K, K, S, O), device=dev)
             rec[f"wgrad_us_rows{rows}"] = round(timeit(lambda: check(L.ra_conv_wgrad(
-                ptr(xh), ptr(idx), int(u8), ptr(dy), ptr(work), ptr(dw), 0, B, HW, HW, C, K, K,
+                ptr(xh), ptr(idx), int(u8), ptr(dy), ptr(work), work.numel(), ptr(dw), 0, B, HW, HW, C, K, K,
                 S, O, 1 / 255.0, stream_ptr()), "wgrad")), 2)
         L.ra_set_knob(7, 0)
         dyc = dy.permute(0, 3, 1, 2)

@@ -269,6 +269,51 @@ def test_conv_bias_relu(cuda_device, cfg):
         assert _rel(x0.grad, xr0.grad) < 2e-2
 
 
+@pytest.mark.parametrize("u8", [True, False])
+def test_conv_bias_relu_graph_replay(cuda_device, u8):
+    """Captured in a HIP graph, the conv fwd + weight-grad kernels recompute on replay
+    (new input values, same buffers) exactly like eager calls."""
+    torch.manual_seed(22)
+    if u8:
+        HW, C, O, Kk, S = 84, 4, 32, 8, 4
+        src = torch.randint(0, 256, (50, HW, HW, C), dtype=torch.uint8, device=cuda_device)
+        idx = torch.randperm(50, device=cuda_device)[:32]
+    else:
+        HW, C, O, Kk, S = 9, 64, 64, 3, 1
+        src = torch.randn(32, HW, HW, C, device=cuda_device).bfloat16()
+        idx = None
+    w = (torch.randn(O, C, Kk, Kk, device=cuda_device) * 0.05).bfloat16()
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_()
+    b = (0.1 * torch.randn(O, device=cuda_device)).bfloat16().requires_grad_()
+    gy = torch.randn(32, (HW - Kk) // S + 1, (HW - Kk) // S + 1, O,
+                     device=cuda_device).bfloat16().permute(0, 3, 1, 2)
+
+    def step():
+        x = src if u8 else src.permute(0, 3, 1, 2)
+        y = rf.conv2d_bias_relu(x, w, b, S, idx=idx)
+        gw, gb = torch.autograd.grad(y, (w, b), gy)
+        return y, gw, gb
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    for _ in range(2):  # new values in the same buffers, then replay
+        if u8:
+            src.copy_(torch.randint(0, 256, src.shape, dtype=torch.uint8, device=cuda_device))
+        else:
+            src.copy_(torch.randn(src.shape, device=cuda_device).bfloat16())
+        g.replay()
+        ref_out = step()
+        torch.cuda.synchronize()
+        for a_, b_ in zip(out, ref_out):
+            assert torch.equal(a_, b_)
+
+
 def test_nature_cnn_fused_matches_eager(cuda_device):
     """The fused GPU encoder (u8 frames + idx) == the generic path on the same weights."""
     from ray_amd.rllib.core.rl_module import NatureCNN

@@ -40,8 +40,9 @@ def test_ppo_learner_gpu_update(cuda_device):
 
 def test_ppo_learner_graph_matches_eager(cuda_device):
     """The HIP-graph SGD step (captured gather/fwd/loss/bwd, replayed per minibatch)
-    must train like the eager loop: same seed, same batch, same permutations."""
-    cfg = _cfg()
+    must train like the eager loop: same seed, same batch, same permutations. Compared on
+    the weight UPDATES (the weights themselves barely move in one update)."""
+    cfg = _cfg(lr=1e-3)
     runner = SingleAgentEnvRunner(cfg, 1)
     env = make_env("SyntheticAtari-v0")
     Lg = Learner(cfg, env.observation_space, env.action_space, device=cuda_device)
@@ -49,6 +50,7 @@ def test_ppo_learner_graph_matches_eager(cuda_device):
                  device=cuda_device)
     runner.set_weights(Lg.get_weights(), 1)
     batch = runner.sample(32)
+    w0 = {k: v.clone() for k, v in Lg.get_weights().items()}
     torch.manual_seed(7)
     sg = Lg.update_ppo(batch)
     torch.manual_seed(7)
@@ -57,10 +59,45 @@ def test_ppo_learner_graph_matches_eager(cuda_device):
     assert sg["num_minibatches"] == se["num_minibatches"] == 4
     assert abs(sg["total_loss"] - se["total_loss"]) < 1e-2 * max(1.0, abs(se["total_loss"]))
     wg, we = Lg.get_weights(), Le.get_weights()
-    for k in wg:
-        assert torch.allclose(wg[k], we[k], atol=2e-2, rtol=2e-2), k
-    batch2 = runner.sample(32)  # second update replays the captured graph with new data
-    assert np.isfinite(Lg.update_ppo(batch2)["total_loss"])
+    dg = torch.cat([(wg[k] - w0[k]).flatten() for k in w0])
+    de = torch.cat([(we[k] - w0[k]).flatten() for k in w0])
+    assert torch.isfinite(dg).all() and de.norm() > 0
+    # Adam's first steps are sign-like, so elements with near-zero gradients may flip
+    # between the two paths (MIOpen's input-gradient reduction order): a broken graph
+    # (stale or unexecuted nodes) differs by O(100%)
+    assert ((dg - de).norm() / de.norm()).item() < 0.25
+    # the master weights and optimizer moments stay finite over replays with new data
+    for _ in range(2):
+        assert np.isfinite(Lg.update_ppo(runner.sample(32))["total_loss"])
+    assert torch.isfinite(Lg.flat.p32).all() and torch.isfinite(Lg.opt.v).all()
+
+
+def test_ppo_learner_graph_learns(cuda_device):
+    """Graph-mode PPO on frames where action 0 is always advantageous raises p(a=0)."""
+    cfg = _cfg(lr=3e-4, minibatch_size=100, num_epochs=4)
+    env = make_env("SyntheticAtari-v0")
+    L = Learner(cfg, env.observation_space, env.action_space, device=cuda_device)
+    T, B = 10, 40
+    rng = np.random.default_rng(0)
+    obs = rng.integers(0, 256, (T, B, 84, 84, 4), dtype=np.uint8)
+    acts = rng.integers(0, env.action_space.n, (T, B))
+    batch = {"obs": obs, "rewards": np.where(acts == 0, 1.0, -1.0).astype(np.float32),
+             "terminateds": np.ones((T, B), np.float32), "actions": acts,
+             "action_logp": np.full((T, B), -np.log(env.action_space.n), np.float32),
+             "action_dist_inputs": np.zeros((T, B, env.action_space.n), np.float32),
+             "bootstrap_obs": rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)}
+    x = torch.from_numpy(obs[0]).to(cuda_device)
+
+    def p0():
+        with torch.no_grad():
+            lg = L.module.forward_train(x)["action_dist_inputs"].float()
+        return torch.softmax(lg, -1)[:, 0].mean().item()
+
+    before = p0()
+    for _ in range(3):
+        L.update_ppo(batch)
+    assert getattr(L, "_graph", None) is not None
+    assert p0() > before + 0.05
 
 
 def test_vtrace_learner_gpu(cuda_device):
