@@ -162,12 +162,15 @@ class RLModule(nn.Module):
     def sample_actions(self, dist_inputs, explore=True):
         """Returns (actions, logp)."""
         if self.discrete:
-            logits = dist_inputs.float()
+            lp_all = torch.log_softmax(dist_inputs.float(), -1)
             if explore:
-                a = torch.distributions.Categorical(logits=logits).sample()
+                # Gumbel-max draw: argmax(logp + G), G = -log(-log U) ~ Gumbel(0, 1) —
+                # exact categorical sampling in three ops (no Distribution object per step)
+                u = torch.rand_like(lp_all).clamp_(1e-20, 1.0)
+                a = (lp_all - torch.log(-torch.log(u))).argmax(-1)
             else:
-                a = logits.argmax(-1)
-            logp = torch.log_softmax(logits, -1).gather(-1, a[:, None])[:, 0]
+                a = lp_all.argmax(-1)
+            logp = lp_all.gather(-1, a[:, None])[:, 0]
             return a, logp
         mean, log_std = dist_inputs.float().chunk(2, -1)
         std = log_std.clamp(-20, 2).exp()

@@ -85,6 +85,10 @@ class SingleAgentEnvRunner:
         if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
             self.device = torch.device("cuda", 0)
             self.module.to(self.device)
+            if self.module_kind == "pg" and getattr(self.module, "is_image", False):
+                # bf16 channels-last weights: the conv encoder runs on the MFMA kernels and
+                # reads the uint8 frames directly (weights arrive fp32, cast on load)
+                self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
         self.obs = []
         for i, e in enumerate(self.envs):
             o, _ = e.reset(seed=None if seed is None else seed * 1000 + worker_index * 100 + i)
@@ -163,13 +167,19 @@ class SingleAgentEnvRunner:
                     lp = lpt.float().cpu().numpy()
                 else:
                     out = self.module.forward_inference(x)
-                    di = out["action_dist_inputs"]
+                    di = out["action_dist_inputs"].float()
                     at, lpt = self.module.sample_actions(di, explore)
-                    a = at.cpu().numpy()
-                    lp = lpt.cpu().numpy()
                     if dist_in is None:
                         dist_in = np.zeros((T, B, di.shape[-1]), np.float32)
-                    dist_in[t] = di.float().cpu().numpy()
+                    if discrete and di.is_cuda:  # one device->host copy per step
+                        h = torch.cat([at.float()[:, None], lpt[:, None], di], 1).cpu().numpy()
+                        a = h[:, 0].astype(np.int64)
+                        lp = h[:, 1]
+                        dist_in[t] = h[:, 2:]
+                    else:
+                        a = at.cpu().numpy()
+                        lp = lpt.cpu().numpy()
+                        dist_in[t] = di.cpu().numpy()
             act_buf[t] = a
             logp[t] = lp
             a_env = a

@@ -212,3 +212,22 @@ def test_ppo_sample_async_overlaps_and_counts_exactly(cluster):
         assert "sample_wait_s" in r["learners"]
     assert r["env_runners"]["num_episodes"] > 0
     algo.stop()
+
+
+def test_sample_actions_matches_categorical():
+    """Gumbel-max sampling draws from softmax(logits); logp is the log-prob of the draw."""
+    import torch
+
+    from ray_amd.rllib.core.rl_module import RLModule
+    from ray_amd.rllib.env import spaces
+
+    m = RLModule(spaces.Box(-1, 1, (4,)), spaces.Discrete(4), {})
+    torch.manual_seed(0)
+    logits = torch.tensor([[2.0, 0.5, -1.0, 0.0]]).repeat(40000, 1)
+    a, logp = m.sample_actions(logits, explore=True)
+    freq = torch.bincount(a, minlength=4).float() / a.numel()
+    p = torch.softmax(logits[0], -1)
+    assert torch.allclose(freq, p, atol=0.01)
+    assert torch.allclose(logp, torch.log(p)[a], atol=1e-6)
+    a2, _ = m.sample_actions(logits[:3], explore=False)
+    assert a2.tolist() == [0, 0, 0]
