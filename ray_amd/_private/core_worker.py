@@ -921,9 +921,8 @@ class CoreWorker:
             if len(done) >= num_returns:
                 return done
             rest = ids - done
-            owned_pending = [oid for oid in rest if oid in owned]
-            remote_pending = [oid for oid in rest if oid not in owned] \
-                if len(owned_pending) != len(rest) else []
+            owned_pending = rest & owned.keys()
+            remote_pending = rest - owned_pending if len(owned_pending) != len(rest) else ()
         cv = self._ready_cv
 
         def remote_hit(oid):
@@ -946,13 +945,14 @@ class CoreWorker:
         # ready log), not at every pending ref: wait() on 1k refs was quadratic.
         try:
             with self.lock:
-                pend = set()
-                for oid in owned_pending:
-                    o = self.owned.get(oid)
-                    if o is None or o.ready:
-                        done.add(oid)
-                    else:
-                        pend.add(oid)
+                # re-check what became ready (or was freed: counts as ready) since the
+                # first look, with set algebra instead of a per-ref loop
+                done |= owned_pending & self._ready_owned
+                pend = owned_pending - done
+                gone = pend - self.owned.keys()
+                if gone:
+                    done |= gone
+                    pend -= gone
                 seen = self._ready_seq
                 log = self._ready_log
                 while len(done) < num_returns and not self.exiting:
@@ -978,11 +978,9 @@ class CoreWorker:
 
     def _collect_ready(self, done, owned_pending, num_returns):
         with self.lock:
-            for oid in owned_pending:
-                o = self.owned.get(oid)
-                if o is None or o.ready:
-                    done.add(oid)
-        return set(done)
+            done = set(done) | (owned_pending & self._ready_owned)
+            done |= owned_pending - self.owned.keys()  # freed meanwhile: ready
+        return done
 
     def _drop_waiter(self, oids, cb):
         """Unregister a finished waiter so callbacks do not pile up on pending objects."""

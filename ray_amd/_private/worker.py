@@ -304,6 +304,9 @@ def _compiled_dag_get(refs, timeout):
     return None
 
 
+_ref_id = __import__("operator").attrgetter("_id")
+
+
 def wait(object_refs, *, num_returns=1, timeout=None, fetch_local=True):
     from ray_amd.object_ref import ObjectRef
 
@@ -311,16 +314,28 @@ def wait(object_refs, *, num_returns=1, timeout=None, fetch_local=True):
     if isinstance(object_refs, ObjectRef):
         raise TypeError("wait() expected a list of ray_amd.ObjectRef, got a single ObjectRef")
     refs = list(object_refs)
-    ids = [r._id for r in refs]
-    if len(set(ids)) != len(ids):
+    ids = list(map(_ref_id, refs))
+    idset = set(ids)
+    if len(idset) != len(ids):
         raise ValueError("Wait requires a list of unique object refs.")
     if num_returns <= 0 or num_returns > len(refs):
         raise ValueError("Invalid number of objects to return %d." % num_returns)
-    ready = cw.wait_refs(ids, num_returns, timeout)
+    ready = cw.wait_refs(idset, num_returns, timeout)
+    if len(ready) * 8 < len(ids):
+        # few ready refs (the common one-at-a-time loop): locate them with C-level index
+        # scans and cut the not-ready list out of the input by slicing
+        pos = sorted(ids.index(i) for i in ready)[:num_returns]
+        r_list = [refs[i] for i in pos]
+        nr, prev = [], 0
+        for i in pos:
+            nr += refs[prev:i]
+            prev = i + 1
+        nr += refs[prev:]
+        return r_list, nr
     if len(ready) > num_returns:  # keep the first ready ones in input order
         ready = set([i for i in ids if i in ready][:num_returns])
-    r_list = [r for r in refs if r._id in ready]
-    nr = [r for r in refs if r._id not in ready]
+    r_list = [r for r, i in zip(refs, ids) if i in ready]
+    nr = [r for r, i in zip(refs, ids) if i not in ready]
     return r_list, nr
 
 

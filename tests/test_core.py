@@ -501,3 +501,29 @@ def test_await_ref(cluster):
         return await add.remote(2, 3)
 
     assert asyncio.run(main()) == 5
+
+
+def test_wait_order_and_partition(cluster):
+    """wait() returns the first ready refs in INPUT order and keeps the rest in order,
+    both on the few-ready slicing path and the many-ready path."""
+    import time as _t
+
+    @ray.remote
+    def delayed(i, d):
+        _t.sleep(d)
+        return i
+
+    ready_now = [ray.put(i) for i in range(3)]
+    slow = [delayed.remote(i, 30) for i in range(5)]
+    mixed = [slow[0], ready_now[2], slow[1], slow[2], ready_now[0], slow[3], ready_now[1],
+             slow[4]]
+    r, nr = ray.wait(mixed, num_returns=2, timeout=5)
+    assert r == [ready_now[2], ready_now[0]]
+    assert nr == [slow[0], slow[1], slow[2], slow[3], ready_now[1], slow[4]]
+    many = [ray.put(i) for i in range(40)] + slow
+    r, nr = ray.wait(many, num_returns=30, timeout=5)
+    assert r == many[:30] and nr == many[30:]
+    r, nr = ray.wait(many, num_returns=45, timeout=0.2)  # timeout: only the 40 ready
+    assert r == many[:40] and nr == slow
+    for s in slow:
+        ray.cancel(s, force=True)
