@@ -87,6 +87,41 @@ PYBIND11_MODULE(_core, m) {
     parallel_copy((uint8_t*)d.ptr, (const uint8_t*)s.ptr, nd);
   });
 
+  // Strided row copy: for r < rows, dst[dst_off + r*dst_stride : +row_bytes] =
+  // src[r*src_stride : +row_bytes] (byte offsets into two buffers), rows split over
+  // threads with the GIL released. Assembles [T, B_total, ...] rollout batches straight
+  // from per-runner [T, B_i, ...] fragments into pinned staging memory.
+  m.def("copy_rows", [](py::buffer dst, uint64_t dst_off, uint64_t dst_stride, py::buffer src,
+                        uint64_t src_stride, uint64_t rows, uint64_t row_bytes) {
+    py::buffer_info d = dst.request(true), s = src.request();
+    const uint64_t nd = (uint64_t)d.size * d.itemsize, ns = (uint64_t)s.size * s.itemsize;
+    if (rows && (dst_off + (rows - 1) * dst_stride + row_bytes > nd ||
+                 (rows - 1) * src_stride + row_bytes > ns))
+      throw std::out_of_range("copy_rows: out of range");
+    uint8_t* dp = (uint8_t*)d.ptr + dst_off;
+    const uint8_t* sp = (const uint8_t*)s.ptr;
+    py::gil_scoped_release r;
+    const uint64_t total = rows * row_bytes;
+    unsigned hw = std::thread::hardware_concurrency();
+    unsigned nt = (unsigned)std::min<uint64_t>(total / (4ull << 20), std::min(8u, hw ? hw : 1u));
+    if (nt > rows) nt = (unsigned)rows;
+    auto work = [&](uint64_t r0, uint64_t r1) {
+      for (uint64_t i = r0; i < r1; ++i) memcpy(dp + i * dst_stride, sp + i * src_stride, row_bytes);
+    };
+    if (nt <= 1) {
+      work(0, rows);
+      return;
+    }
+    std::vector<std::thread> ts;
+    const uint64_t per = (rows + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; ++t) {
+      const uint64_t r0 = per * t, r1 = std::min(rows, r0 + per);
+      if (r0 < r1) ts.emplace_back(work, r0, r1);
+    }
+    work(0, std::min(rows, per));
+    for (auto& t : ts) t.join();
+  });
+
   m.def("random_id", [](int n) {
     if (!tl_rng) {
       std::random_device rd;

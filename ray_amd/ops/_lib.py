@@ -60,6 +60,10 @@ _SIGS = {
     "ra_ppo_loss_packed": [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 4
                           + [c_int, c_int] + [c_float] * 5 + [c_void_p, c_int, c_float, c_void_p],
     "ra_scale_to_bf16": [c_void_p, c_long, c_void_p, c_void_p, c_void_p],
+    "ra_ppo_heads_fwd": [c_void_p, c_int] + [c_void_p] * 5 + [c_int, c_int] + [c_void_p] * 3
+                        + [c_int, c_int] + [c_float] * 5 + [c_void_p, c_float, c_void_p],
+    "ra_ppo_heads_work": [c_int, c_int],
+    "ra_ppo_heads_bwd": [c_void_p, c_int] + [c_void_p] * 10 + [c_int, c_int, c_int, c_void_p],
     "ra_bias_relu_fwd": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p],
     "ra_relu_bwd_work": [c_int, c_int],
     "ra_relu_bwd_bias": [c_void_p] * 5 + [c_int, c_int, c_int, c_void_p],

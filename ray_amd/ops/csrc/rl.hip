@@ -187,94 +187,292 @@ __device__ __forceinline__ float ld_in(const void* p, long k, int bf) {
   return bf ? bf2f(reinterpret_cast<const bf16_t*>(p)[k]) : reinterpret_cast<const float*>(p)[k];
 }
 
+// Per-sample PPO loss and its gradient: z = logits (registers), v = value prediction,
+// r = row of the behaviour table. Writes dz = d(total)/dz and *dv (NOT yet scaled by
+// 1/N) and the six statistics of the sample.
+template <int AMAX>
+__device__ __forceinline__ void ppo_row(const PPOArgs& p, long r, const float (&z)[AMAX], float v,
+                                        bool has_v, float (&dz)[AMAX], float* dv, float (&s6)[6]) {
+  float lp[AMAX];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) mx = fmaxf(mx, j < p.A ? z[j] : -INFINITY);
+  float se = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) se += (j < p.A) ? __expf(z[j] - mx) : 0.f;
+  const float lse = mx + __logf(se);
+  float ent = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) {
+    lp[j] = (j < p.A) ? z[j] - lse : 0.f;
+    if (j < p.A) ent -= __expf(lp[j]) * lp[j];
+  }
+  // KL(old || new)
+  float kl = 0.f, olp[AMAX];
+  if (p.old_logits) {
+    const float* orow = p.old_logits + r * p.ld_old;
+    float omx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+      olp[j] = (j < p.A) ? orow[j] : -INFINITY;
+      omx = fmaxf(omx, olp[j]);
+    }
+    float ose = 0.f;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) ose += (j < p.A) ? __expf(olp[j] - omx) : 0.f;
+    const float olse = omx + __logf(ose);
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+      olp[j] = (j < p.A) ? olp[j] - olse : 0.f;
+      if (j < p.A) kl += __expf(olp[j]) * (olp[j] - lp[j]);
+    }
+  }
+  const long act = p.act_f32 ? (long)reinterpret_cast<const float*>(p.actions)[r * p.ld_act]
+                             : reinterpret_cast<const long*>(p.actions)[r * p.ld_act];
+  float logp = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) if (j == act) logp = lp[j];
+  const long ra = r * p.ld_aux;
+  const float ratio = __expf(logp - p.old_logp[ra]);
+  const float A_ = p.adv[ra];
+  const float rc = fminf(fmaxf(ratio, 1.f - p.clip), 1.f + p.clip);
+  const float s1 = A_ * ratio, s2 = A_ * rc;
+  const float surr = fminf(s1, s2);
+  // d surr / d logp
+  float dsurr;
+  if (s1 <= s2) dsurr = A_ * ratio;
+  else dsurr = (ratio > 1.f - p.clip && ratio < 1.f + p.clip) ? A_ * ratio : 0.f;
+  const bool clipped = (ratio < 1.f - p.clip) || (ratio > 1.f + p.clip);
+  float vf = 0.f;
+  *dv = 0.f;
+  if (has_v) {
+    const float e = v - p.vtarg[ra];
+    const float e2 = e * e;
+    vf = fminf(e2, p.vf_clip);
+    *dv = p.vf_coeff * ((e2 < p.vf_clip) ? 2.f * e : 0.f);
+  }
+  const float kl_c = p.kl_dev ? p.kl_dev[0] : p.kl_coeff;
+  const float total = -surr + p.vf_coeff * vf - p.ent_coeff * ent + kl_c * kl;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) {
+    dz[j] = 0.f;
+    if (j < p.A) {
+      const float pj = __expf(lp[j]);
+      float g = -dsurr * ((j == act ? 1.f : 0.f) - pj);   // policy term
+      g += p.ent_coeff * pj * (lp[j] + ent);               // -c * dH/dz, dH/dz = -p(logp+H)
+      if (p.old_logits) g += kl_c * (pj - __expf(olp[j]));
+      dz[j] = g;
+    }
+  }
+  s6[0] = total; s6[1] = -surr; s6[2] = vf; s6[3] = ent; s6[4] = kl; s6[5] = clipped ? 1.f : 0.f;
+}
+
 template <int AMAX>
 __global__ __launch_bounds__(256) void ppo_loss_kernel(PPOArgs p) {
   __shared__ float red[4];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  float s_total = 0.f, s_pol = 0.f, s_vf = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
+  float s6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (i < p.N) {
     const long r = p.idx ? p.idx[i] : (long)i;
-    float z[AMAX], lp[AMAX];
-    float mx = -INFINITY;
+    float z[AMAX], dz[AMAX], dv;
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j) {
-      z[j] = (j < p.A) ? ld_in(p.logits, (long)i * p.A + j, p.in_bf16) : -INFINITY;
-      mx = fmaxf(mx, z[j]);
-    }
-    float se = 0.f;
+    for (int j = 0; j < AMAX; ++j)
+      z[j] = (j < p.A) ? ld_in(p.logits, (long)i * p.A + j, p.in_bf16) : 0.f;
+    const float v = p.vpred ? ld_in(p.vpred, i, p.in_bf16) : 0.f;
+    ppo_row<AMAX>(p, r, z, v, p.vpred != nullptr, dz, &dv, s6);
+    if (p.vpred) p.dvpred[i] = dv * p.inv_n;
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j) se += (j < p.A) ? __expf(z[j] - mx) : 0.f;
-    const float lse = mx + __logf(se);
-    float ent = 0.f;
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j) {
-      lp[j] = (j < p.A) ? z[j] - lse : 0.f;
-      if (j < p.A) ent -= __expf(lp[j]) * lp[j];
-    }
-    // KL(old || new)
-    float kl = 0.f, olp[AMAX];
-    if (p.old_logits) {
-      const float* orow = p.old_logits + r * p.ld_old;
-      float omx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < AMAX; ++j) {
-        olp[j] = (j < p.A) ? orow[j] : -INFINITY;
-        omx = fmaxf(omx, olp[j]);
-      }
-      float ose = 0.f;
-#pragma unroll
-      for (int j = 0; j < AMAX; ++j) ose += (j < p.A) ? __expf(olp[j] - omx) : 0.f;
-      const float olse = omx + __logf(ose);
-#pragma unroll
-      for (int j = 0; j < AMAX; ++j) {
-        olp[j] = (j < p.A) ? olp[j] - olse : 0.f;
-        if (j < p.A) kl += __expf(olp[j]) * (olp[j] - lp[j]);
-      }
-    }
-    const long act = p.act_f32 ? (long)reinterpret_cast<const float*>(p.actions)[r * p.ld_act]
-                               : reinterpret_cast<const long*>(p.actions)[r * p.ld_act];
-    float logp = 0.f;
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j) if (j == act) logp = lp[j];
-    const long ra = r * p.ld_aux;
-    const float ratio = __expf(logp - p.old_logp[ra]);
-    const float A_ = p.adv[ra];
-    const float rc = fminf(fmaxf(ratio, 1.f - p.clip), 1.f + p.clip);
-    const float s1 = A_ * ratio, s2 = A_ * rc;
-    const float surr = fminf(s1, s2);
-    // d surr / d logp
-    float dsurr;
-    if (s1 <= s2) dsurr = A_ * ratio;
-    else dsurr = (ratio > 1.f - p.clip && ratio < 1.f + p.clip) ? A_ * ratio : 0.f;
-    const bool clipped = (ratio < 1.f - p.clip) || (ratio > 1.f + p.clip);
-    float vf = 0.f, dv = 0.f;
-    if (p.vpred) {
-      const float e = ld_in(p.vpred, i, p.in_bf16) - p.vtarg[ra];
-      const float e2 = e * e;
-      vf = fminf(e2, p.vf_clip);
-      dv = (e2 < p.vf_clip) ? 2.f * e : 0.f;
-      p.dvpred[i] = p.vf_coeff * dv * p.inv_n;
-    }
-    const float kl_c = p.kl_dev ? p.kl_dev[0] : p.kl_coeff;
-    const float total = -surr + p.vf_coeff * vf - p.ent_coeff * ent + kl_c * kl;
-    // gradient wrt logits
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j) {
-      if (j < p.A) {
-        const float pj = __expf(lp[j]);
-        float g = -dsurr * ((j == act ? 1.f : 0.f) - pj);   // policy term
-        g += p.ent_coeff * pj * (lp[j] + ent);               // -c * dH/dz, dH/dz = -p(logp+H)
-        if (p.old_logits) g += kl_c * (pj - __expf(olp[j]));
-        p.dlogits[(long)i * p.A + j] = g * p.inv_n;
-      }
-    }
-    s_total = total; s_pol = -surr; s_vf = vf; s_ent = ent; s_kl = kl; s_clip = clipped ? 1.f : 0.f;
+    for (int j = 0; j < AMAX; ++j)
+      if (j < p.A) p.dlogits[(long)i * p.A + j] = dz[j] * p.inv_n;
   }
-  float vals[6] = {s_total, s_pol, s_vf, s_ent, s_kl, s_clip};
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
-    const float t = block_sum<4>(vals[k], red);
+    const float t = block_sum<4>(s6[k], red);
     if (threadIdx.x == 0) atomicAdd(&p.stats[k], t * p.inv_n);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused policy/value heads + PPO loss (shared encoder): per minibatch row, one wave
+//   forward : logits = h Wpi^T + bpi, v = h wvf + bvf (wave dot products over F),
+//             the PPO row math, d7[row] = [dlogits | dv] / N       (ra_ppo_heads_fwd)
+//   backward: dh = g * (d7[:, :A] Wpi + d7[:, A] wvf), per-wave partials of
+//             dW = d7^T h and db = sum d7, then one reduction writing the four
+//             parameter gradients (flat-buffer sinks)                (ra_ppo_heads_bwd)
+// replacing two head GEMMs, two bias adds, the loss, two casts, four backward GEMMs,
+// the dX add and two bias reductions of the unfused graph.
+struct HeadsArgs {
+  const bf16_t* h;      // [N, F]
+  const bf16_t* wpi;    // [A, F]
+  const bf16_t* bpi;    // [A]
+  const bf16_t* wvf;    // [F]
+  const bf16_t* bvf;    // [1]
+  float* d7;            // [N, A+1]
+  const float* g;       // upstream scalar gradient (bwd; may be null = 1)
+  bf16_t* dh;           // [N, F]
+  float* part;          // [P4][(A+1)*(F+1)] per-wave partials
+  int F;
+};
+
+template <int AMAX>
+__global__ __launch_bounds__(256) void ppo_heads_fwd_kernel(PPOArgs p, HeadsArgs q) {
+  __shared__ float red[4][6];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int A = p.A, F = q.F;
+  float sacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = blockIdx.x * 4 + wv; i < p.N; i += gridDim.x * 4) {
+    float z[AMAX], v = 0.f;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) z[j] = 0.f;
+    for (int c = lane * 8; c < F; c += 512) {
+      float hv[8], wv8[8];
+      unpack8(*reinterpret_cast<const uint4*>(q.h + (long)i * F + c), hv);
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j) {
+        if (j >= A) break;
+        unpack8(*reinterpret_cast<const uint4*>(q.wpi + (long)j * F + c), wv8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[j] += hv[e] * wv8[e];
+      }
+      unpack8(*reinterpret_cast<const uint4*>(q.wvf + c), wv8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v += hv[e] * wv8[e];
+    }
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) z[j] = j < A ? wave_sum(z[j]) + bf2f(q.bpi[j]) : 0.f;
+    v = wave_sum(v) + bf2f(q.bvf[0]);
+    // heads outputs are bf16 in the unfused model: round the same way
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) z[j] = bf2f(f2bf(z[j]));
+    v = bf2f(f2bf(v));
+    const long r = p.idx ? p.idx[i] : (long)i;
+    float dz[AMAX], dv, s6[6];
+    ppo_row<AMAX>(p, r, z, v, true, dz, &dv, s6);
+    if (lane == 0) {
+      float* o = q.d7 + (long)i * (A + 1);
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) o[j] = dz[j] * p.inv_n;
+      o[A] = dv * p.inv_n;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) sacc[k] += s6[k];
+    }
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[wv][k] = sacc[k];
+  __syncthreads();
+  if (threadIdx.x < 6)
+    atomicAdd(&p.stats[threadIdx.x], (red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                      red[2][threadIdx.x] + red[3][threadIdx.x]) * p.inv_n);
+}
+
+// grid P blocks x 4 waves; wave w of block b takes rows b*4+w, +4P, ...; each lane owns
+// 8-column slices c = 8*lane + 512k of F and keeps (A+1) x 8 dW partials per slice.
+template <int AMAX, int NSL>
+__global__ __launch_bounds__(256) void ppo_heads_bwd_kernel(int N, int A, HeadsArgs q) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, F = q.F;
+  const int wave = blockIdx.x * 4 + wv, nwaves = gridDim.x * 4;
+  const float gs = q.g ? q.g[0] : 1.f;
+  float acc[NSL][AMAX + 1][8];
+  float dbacc[AMAX + 1];
+#pragma unroll
+  for (int s = 0; s < NSL; ++s)
+#pragma unroll
+    for (int j = 0; j <= AMAX; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[s][j][e] = 0.f;
+#pragma unroll
+  for (int j = 0; j <= AMAX; ++j) dbacc[j] = 0.f;
+  for (int i = wave; i < N; i += nwaves) {
+    float d[AMAX + 1];
+#pragma unroll
+    for (int j = 0; j <= AMAX; ++j) d[j] = 0.f;
+    for (int j = 0; j <= A; ++j) d[j < A ? j : AMAX] = gs * q.d7[(long)i * (A + 1) + j];
+#pragma unroll
+    for (int j = 0; j <= AMAX; ++j) dbacc[j] += d[j];
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const int c = lane * 8 + 512 * s;
+      if (c >= F) break;
+      float hv[8], o[8], w8[8];
+      unpack8(*reinterpret_cast<const uint4*>(q.h + (long)i * F + c), hv);
+      unpack8(*reinterpret_cast<const uint4*>(q.wvf + c), w8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = d[AMAX] * w8[e];
+        acc[s][AMAX][e] += d[AMAX] * hv[e];
+      }
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j) {
+        if (j >= A) break;
+        unpack8(*reinterpret_cast<const uint4*>(q.wpi + (long)j * F + c), w8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] += d[j] * w8[e];
+          acc[s][j][e] += d[j] * hv[e];
+        }
+      }
+      *reinterpret_cast<uint4*>(q.dh + (long)i * F + c) = pack8(o);
+    }
+  }
+  // per-wave partial row: [W rows 0..A-1 = pi, row A = vf][F] then [b 0..A]
+  const int L = (A + 1) * (F + 1);
+  float* pr = q.part + (size_t)wave * L;
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) {
+    const int c = lane * 8 + 512 * s;
+    if (c >= F) break;
+#pragma unroll
+    for (int j = 0; j <= AMAX; ++j) {
+      if (j < AMAX && j >= A) continue;
+      const int row = j < AMAX ? j : A;
+      float* dst = pr + (size_t)row * F + c;
+      *reinterpret_cast<float4*>(dst) = make_float4(acc[s][j][0], acc[s][j][1], acc[s][j][2], acc[s][j][3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[s][j][4], acc[s][j][5], acc[s][j][6], acc[s][j][7]);
+    }
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j <= AMAX; ++j) {
+      if (j < AMAX && j >= A) continue;
+      pr[(size_t)(A + 1) * F + (j < AMAX ? j : A)] = dbacc[j];
+    }
+}
+
+// out[col] (+)= sum over the P4 wave partials; columns map to the four gradients.
+struct HeadsGrads {
+  void* wpi; void* bpi; void* wvf; void* bvf;
+};
+
+template <bool F32, bool ACC>
+__global__ __launch_bounds__(1024) void ppo_heads_reduce(const float* __restrict__ part, int P4,
+                                                         int A, int F, HeadsGrads o) {
+  __shared__ float red[16][65];
+  const int L = (A + 1) * (F + 1);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (j < L)
+    for (int p = ty; p < P4; p += 16) s += part[(size_t)p * L + j];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty != 0 || j >= L) return;
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += red[i][tx];
+  void* dst;
+  long k;
+  if (j < A * F) { dst = o.wpi; k = j; }
+  else if (j < (A + 1) * F) { dst = o.wvf; k = j - A * F; }
+  else if (j < (A + 1) * F + A) { dst = o.bpi; k = j - (A + 1) * F; }
+  else { dst = o.bvf; k = 0; }
+  if (F32) {
+    float* d = reinterpret_cast<float*>(dst) + k;
+    *d = ACC ? *d + s : s;
+  } else {
+    bf16_t* d = reinterpret_cast<bf16_t*>(dst) + k;
+    *d = f2bf(ACC ? s + bf2f(*d) : s);
   }
 }
 
@@ -317,6 +515,56 @@ RA_EXPORT int ra_ppo_loss_packed(const void* logits, const void* vpred, const fl
             aux + A + 3, idx, dlogits, dvpred, stats, kl_dev, N, A, in_bf16, 1, ld, ld, ld, clip,
             vf_clip, vf_coeff, ent_coeff, kl_coeff, inv_n};
   return ppo_launch(p, st);
+}
+
+static constexpr int kHeadsWaves = 64 * 4;  // bwd partial rows (64 blocks x 4 waves)
+
+RA_EXPORT int ra_ppo_heads_fwd(const void* h, int F, const void* wpi, const void* bpi,
+                               const void* wvf, const void* bvf, const float* aux, int ld,
+                               int has_old, const long* idx, float* d7, float* stats, int N,
+                               int A, float clip, float vf_clip, float vf_coeff, float ent_coeff,
+                               float kl_coeff, const float* kl_dev, float inv_n, hipStream_t st) {
+  if (ld < A + 4 || F % 8 || F > 1024 || A > 18 || N <= 0) return hipErrorInvalidValue;
+  PPOArgs p{nullptr, nullptr, has_old ? aux : nullptr, aux + A, aux + A + 1, aux + A + 2,
+            aux + A + 3, idx, nullptr, nullptr, stats, kl_dev, N, A, 0, 1, ld, ld, ld, clip,
+            vf_clip, vf_coeff, ent_coeff, kl_coeff, inv_n};
+  HeadsArgs q{(const bf16_t*)h, (const bf16_t*)wpi, (const bf16_t*)bpi, (const bf16_t*)wvf,
+              (const bf16_t*)bvf, d7, nullptr, nullptr, nullptr, F};
+  int blocks = (N + 3) / 4;
+  if (blocks > 128) blocks = 128;
+  if (A <= 8) hipLaunchKernelGGL(ppo_heads_fwd_kernel<8>, dim3(blocks), dim3(256), 0, st, p, q);
+  else hipLaunchKernelGGL(ppo_heads_fwd_kernel<18>, dim3(blocks), dim3(256), 0, st, p, q);
+  return hipGetLastError();
+}
+
+RA_EXPORT long ra_ppo_heads_work(int A, int F) { return (long)kHeadsWaves * (A + 1) * (F + 1); }
+
+// flags: bit0 accumulate into the gradients, bit1 gradients are fp32 (else bf16)
+RA_EXPORT int ra_ppo_heads_bwd(const void* h, int F, const void* wpi, const void* wvf,
+                               const float* d7, const float* g, void* dh, float* work,
+                               void* dwpi, void* dbpi, void* dwvf, void* dbvf, int flags, int N,
+                               int A, hipStream_t st) {
+  if (F % 8 || F > 1024 || A > 18 || N <= 0) return hipErrorInvalidValue;
+  HeadsArgs q{(const bf16_t*)h, (const bf16_t*)wpi, nullptr, (const bf16_t*)wvf, nullptr,
+              const_cast<float*>(d7), g, (bf16_t*)dh, work, F};
+  const dim3 gb(kHeadsWaves / 4), b(256);
+  if (A <= 8) {
+    if (F <= 512) hipLaunchKernelGGL((ppo_heads_bwd_kernel<8, 1>), gb, b, 0, st, N, A, q);
+    else hipLaunchKernelGGL((ppo_heads_bwd_kernel<8, 2>), gb, b, 0, st, N, A, q);
+  } else {
+    if (F <= 512) hipLaunchKernelGGL((ppo_heads_bwd_kernel<18, 1>), gb, b, 0, st, N, A, q);
+    else hipLaunchKernelGGL((ppo_heads_bwd_kernel<18, 2>), gb, b, 0, st, N, A, q);
+  }
+  HeadsGrads o{dwpi, dbpi, dwvf, dbvf};
+  const int L = (A + 1) * (F + 1);
+  const dim3 rg((L + 63) / 64), rb(1024);
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((ppo_heads_reduce<false, false>), rg, rb, 0, st, work, kHeadsWaves, A, F, o); break;
+    case 1: hipLaunchKernelGGL((ppo_heads_reduce<false, true>), rg, rb, 0, st, work, kHeadsWaves, A, F, o); break;
+    case 2: hipLaunchKernelGGL((ppo_heads_reduce<true, false>), rg, rb, 0, st, work, kHeadsWaves, A, F, o); break;
+    default: hipLaunchKernelGGL((ppo_heads_reduce<true, true>), rg, rb, 0, st, work, kHeadsWaves, A, F, o);
+  }
+  return hipGetLastError();
 }
 
 // out_bf16[k] = g[0] * src[k] for the concatenated fp32 loss gradients (one launch for

@@ -802,6 +802,68 @@ def ppo_loss_packed(logits, vpred, aux, idx, stats, clip=0.2, vf_clip=10.0, vf_c
                                 1.0 / N if inv_n is None else inv_n, kl_dev)
 
 
+class _PPOHeadsLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, wpi, bpi, wvf, bvf, aux, idx, stats, hp, kl_dev, inv_n, has_old):
+        N, F = h.shape
+        A = wpi.shape[0]
+        d7 = torch.empty(N, A + 1, device=h.device, dtype=torch.float32)
+        check(_lib.lib().ra_ppo_heads_fwd(
+            ptr(h), F, ptr(wpi), ptr(bpi), ptr(wvf), ptr(bvf), ptr(aux), aux.shape[1],
+            int(has_old), ptr(idx), ptr(d7), ptr(stats), N, A, hp[0], hp[1], hp[2], hp[3], hp[4],
+            ptr(kl_dev), float(inv_n), stream_ptr()), "ppo_heads_fwd")
+        ctx.save_for_backward(h, wpi, wvf, d7)
+        ctx.params = (wpi, bpi, wvf, bvf)
+        return h.new_empty((), dtype=torch.float32)  # backward handle (stats hold the loss)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, wpi, wvf, d7 = ctx.saved_tensors
+        N, F = h.shape
+        A = wpi.shape[0]
+        L = _lib.lib()
+        dh = torch.empty_like(h)
+        work = torch.empty(L.ra_ppo_heads_work(A, F), device=h.device, dtype=torch.float32)
+        sinks = [_grad_sink(p) for p in ctx.params]
+        use_sink = all(t is not None for t in sinks) and len({t.dtype for t in sinks}) == 1
+        if use_sink:
+            outs = sinks
+            flags = 1 | (2 * _sink_f32(sinks[0]))
+        else:
+            outs = [torch.empty_like(p) for p in ctx.params]
+            flags = 2 * _sink_f32(outs[0])
+        check(L.ra_ppo_heads_bwd(ptr(h), F, ptr(wpi), ptr(wvf), ptr(d7),
+                                 ptr(g.float().contiguous()), ptr(dh), ptr(work), ptr(outs[0]),
+                                 ptr(outs[1]), ptr(outs[2]), ptr(outs[3]), flags, N, A,
+                                 stream_ptr()), "ppo_heads_bwd")
+        if use_sink:
+            for p in ctx.params:
+                _grad_done(p)
+            outs = [None] * 4
+        return (dh, *outs, None, None, None, None, None, None, None)
+
+
+def ppo_heads_supported(h, wpi, bpi, wvf, bvf) -> bool:
+    ok = (_hip(h) and h.dim() == 2 and h.dtype == torch.bfloat16 and h.is_contiguous()
+          and h.shape[1] % 8 == 0 and h.shape[1] <= 1024 and wpi.shape[0] <= 18)
+    return ok and all(t.dtype == torch.bfloat16 and t.is_contiguous()
+                      for t in (wpi, bpi, wvf, bvf)) and wvf.numel() == h.shape[1]
+
+
+def ppo_heads_loss(h, wpi, bpi, wvf, bvf, aux, idx, stats, clip=0.2, vf_clip=10.0, vf_coeff=1.0,
+                   ent_coeff=0.0, kl_coeff=0.0, has_old=True, inv_n=None, kl_dev=None):
+    """Policy + value heads fused with the PPO loss over a shared encoder output h [N, F]:
+    logits = h Wpi^T + bpi, v = h wvf + bvf, the PPO loss of each row (behaviour fields
+    gathered from the packed table ``aux`` by ``idx``, statistics ACCUMULATED into
+    ``stats``), and a backward producing dh and the four head gradients (written into the
+    flat-buffer sinks). Returns a backward handle (value undefined). GPU only."""
+    if not ppo_heads_supported(h, wpi, bpi, wvf, bvf):
+        raise ValueError("ppo_heads_loss: unsupported shapes/dtypes")
+    hp = (float(clip), float(vf_clip), float(vf_coeff), float(ent_coeff), float(kl_coeff))
+    return _PPOHeadsLoss.apply(h, wpi, bpi, wvf, bvf, aux, idx, stats, hp, kl_dev,
+                               1.0 / h.shape[0] if inv_n is None else inv_n, has_old)
+
+
 # --------------------------------------------------------------------- bias + ReLU
 def _nhwc_rows(t):
     """[M, C] row view of a 2-D tensor or a channels-last NCHW tensor (None if neither)."""

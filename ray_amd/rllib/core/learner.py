@@ -22,6 +22,8 @@ from ray_amd.rllib.core.rl_module import RLModule, gaussian_entropy, gaussian_lo
 
 
 def _to_t(x, device, dtype=None, non_blocking=True):
+    if isinstance(x, Fragments):
+        x = x.materialize()
     t = torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x
     if device.type == "cuda" and not t.is_pinned() and t.device.type == "cpu":
         t = t.pin_memory()
@@ -29,14 +31,38 @@ def _to_t(x, device, dtype=None, non_blocking=True):
     return t if dtype is None else t.to(dtype)
 
 
-def concat_batches(batches):
-    """Concatenate runner fragments along the env (B) axis."""
+class Fragments:
+    """Runner fragments [T, B_i, ...] of one batch field, concatenated along the env axis
+    only when materialised: a GPU learner stages them straight into pinned memory
+    (``Learner._h2d``), skipping a full host copy of the frame batch."""
+
+    def __init__(self, parts):
+        self.parts = [np.ascontiguousarray(p) for p in parts]
+        p0 = self.parts[0]
+        self.shape = (p0.shape[0], sum(p.shape[1] for p in self.parts)) + tuple(p0.shape[2:])
+        self.dtype = p0.dtype
+        self.nbytes = sum(p.nbytes for p in self.parts)
+
+    def materialize(self):
+        return np.concatenate(self.parts, axis=1)
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.materialize()
+        return a if dtype is None else a.astype(dtype)
+
+
+def concat_batches(batches, lazy=()):
+    """Concatenate runner fragments along the env (B) axis (keys in ``lazy`` become
+    ``Fragments``)."""
     out = {}
     for k in batches[0]:
         v = batches[0][k]
         if isinstance(v, np.ndarray):
             axis = 0 if k == "bootstrap_obs" else 1
-            out[k] = np.concatenate([b[k] for b in batches], axis=axis)
+            if k in lazy and axis == 1 and len(batches) > 1:
+                out[k] = Fragments([b[k] for b in batches])
+            else:
+                out[k] = np.concatenate([b[k] for b in batches], axis=axis)
         elif isinstance(v, (int, float)):
             out[k] = sum(b[k] for b in batches)
     return out
@@ -170,19 +196,32 @@ class Learner:
         buffer per field (multi-threaded host copy, then an async DMA), instead of
         page-locking a fresh copy of every rollout batch."""
         dev = self.device
-        if not (isinstance(x, np.ndarray) and dev.type == "cuda" and x.nbytes >= (1 << 20)):
+        if not (isinstance(x, (np.ndarray, Fragments)) and dev.type == "cuda"
+                and x.nbytes >= (1 << 20)):
             return _to_t(x, dev)
-        x = np.ascontiguousarray(x)
+        if isinstance(x, np.ndarray):
+            x = np.ascontiguousarray(x)
+        shape, dtype = tuple(x.shape), np.dtype(x.dtype)
         ent = self._pinned.get(key)
-        if ent is None or ent[0].shape != x.shape or ent[0].numpy().dtype != x.dtype:
-            ent = [torch.empty(x.shape, dtype=torch.from_numpy(x[:0]).dtype, pin_memory=True),
-                   None]
+        if ent is None or tuple(ent[0].shape) != shape or ent[0].numpy().dtype != dtype:
+            ent = [torch.empty(shape, dtype=torch.from_numpy(np.empty(0, dtype)).dtype,
+                               pin_memory=True), None]
             self._pinned[key] = ent
         if ent[1] is not None:
             ent[1].synchronize()  # the previous DMA out of this buffer has finished
         from ray_amd._native import _core
 
-        _core.copy_into(ent[0].numpy(), x)
+        dst = ent[0].numpy()
+        if isinstance(x, Fragments):  # [T, B_i, ...] runner blocks -> [T, B, ...] rows
+            row = int(np.prod(shape[2:], dtype=np.int64)) * dtype.itemsize
+            b0 = 0
+            for p in x.parts:
+                bi = p.shape[1]
+                _core.copy_rows(dst.reshape(-1), b0 * row, shape[1] * row, p.reshape(-1),
+                                bi * row, shape[0], bi * row)
+                b0 += bi
+        else:
+            _core.copy_into(dst, x)
         t = ent[0].to(dev, non_blocking=True)
         ent[1] = torch.cuda.Event()
         ent[1].record()
@@ -355,6 +394,13 @@ class Learner:
 
         if packed:
             obs, aux = bufs
+            m = self.module
+            # the fused heads kernel needs a shared encoder and bf16 heads on the GPU
+            fused_heads = (m.vf_encoder is None and self.amp
+                           and os.environ.get("RAY_AMD_PPO_FUSED_HEADS", "1") == "1"
+                           and m.pi.weight.dtype == torch.bfloat16
+                           and m.encoder.out_dim % 8 == 0 and m.encoder.out_dim <= 1024
+                           and m.pi.weight.shape[0] <= 18)
 
             def body():
                 # minibatch frames read by the first conv kernel straight from the uint8
@@ -365,13 +411,22 @@ class Learner:
                 # AccumulateGrad add per parameter (the fused bias kernels write their
                 # bias gradients into the zeroed buffer directly)
                 self.flat.g.zero_()
+                hp = dict(clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),
+                          vf_coeff=c.get("vf_loss_coeff", 1.0),
+                          ent_coeff=c.get("entropy_coeff", 0.0), kl_coeff=kl_c, has_old=True,
+                          kl_dev=self._kl_dev)
+                m = self.module
                 with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=self.amp):
-                    out = self.module.forward_train(obs, idx=idx)
-                loss = rf.ppo_loss_packed(
-                    out["action_dist_inputs"], out["vf_preds"], aux, idx, stats,
-                    clip=c.get("clip_param", 0.3), vf_clip=c.get("vf_clip_param", 10.0),
-                    vf_coeff=c.get("vf_loss_coeff", 1.0), ent_coeff=c.get("entropy_coeff", 0.0),
-                    kl_coeff=kl_c, has_old=True, kl_dev=self._kl_dev)
+                    if fused_heads:  # heads + loss in one kernel over the encoder output
+                        h = m._encode(m.encoder, m._flat(obs), idx)
+                    else:
+                        out = m.forward_train(obs, idx=idx)
+                if fused_heads:
+                    loss = rf.ppo_heads_loss(h, m.pi.weight, m.pi.bias, m.vf.weight, m.vf.bias,
+                                             aux, idx, stats, **hp)
+                else:
+                    loss = rf.ppo_loss_packed(out["action_dist_inputs"], out["vf_preds"], aux,
+                                              idx, stats, **hp)
                 gs = torch.autograd.grad(loss, params, grad_outputs=one, allow_unused=True)
                 dst = [g for g, x in zip(grads, gs) if x is not None]
                 src_ = [x for x in gs if x is not None]
@@ -539,7 +594,8 @@ class LearnerGroup:
 
     def update(self, kind, batches):
         if not self.remote:
-            b = concat_batches(batches) if isinstance(batches, list) else batches
+            lazy = ("obs",) if self.local.device.type == "cuda" else ()
+            b = concat_batches(batches, lazy) if isinstance(batches, list) else batches
             return self.local.update_ppo(b) if kind == "ppo" else self.local.update_vtrace(b)
         import ray_amd as ray
 

@@ -188,6 +188,34 @@ def test_ppo_loss_packed_gathers_rows(cuda_device):
     assert _rel(vv.grad, vr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("A,F", [(6, 512), (4, 256), (18, 1024)])
+def test_ppo_heads_loss_matches_unfused(cuda_device, A, F):
+    """Fused heads + PPO loss == bf16 linear heads followed by the packed loss kernel."""
+    torch.manual_seed(23)
+    Nf, mb = 900, 300
+    h = torch.relu(torch.randn(mb, F, device=cuda_device)).bfloat16().requires_grad_()
+    wpi = (0.05 * torch.randn(A, F, device=cuda_device)).bfloat16().requires_grad_()
+    bpi = (0.1 * torch.randn(A, device=cuda_device)).bfloat16().requires_grad_()
+    wvf = (0.05 * torch.randn(1, F, device=cuda_device)).bfloat16().requires_grad_()
+    bvf = (0.1 * torch.randn(1, device=cuda_device)).bfloat16().requires_grad_()
+    _, old, acts, old_lp, adv, _, vt = _ppo_case(cuda_device, Nf, A, 24)
+    aux = rf.ppo_pack(old, acts, old_lp, adv, vt)
+    idx = torch.randperm(Nf, device=cuda_device)[:mb]
+    kw = dict(clip=0.2, vf_clip=4.0, vf_coeff=0.5, ent_coeff=0.01, kl_coeff=0.2)
+    st = torch.zeros(6, device=cuda_device)
+    hdl = rf.ppo_heads_loss(h, wpi, bpi, wvf, bvf, aux, idx, st, **kw)
+    torch.autograd.backward(hdl, torch.full((), 2.0, device=cuda_device))
+    refs = [t.detach().clone().requires_grad_() for t in (h, wpi, bpi, wvf, bvf)]
+    lg = torch.nn.functional.linear(refs[0], refs[1], refs[2])
+    v = torch.nn.functional.linear(refs[0], refs[3], refs[4]).squeeze(-1)
+    st_r = torch.zeros(6, device=cuda_device)
+    hr = rf.ppo_loss_packed(lg, v, aux, idx, st_r, **kw)
+    torch.autograd.backward(hr, torch.full((), 2.0, device=cuda_device))
+    assert torch.allclose(st, st_r, atol=2e-3, rtol=2e-2)
+    for a_, b_ in zip((h, wpi, bpi, wvf, bvf), refs):
+        assert _rel(a_.grad, b_.grad) < 2e-2
+
+
 @pytest.mark.parametrize("shape", [(64, 32, 20, 20), (37, 64, 9, 9), (500, 64, 7, 7), (300, 512)])
 def test_bias_relu(cuda_device, shape):
     torch.manual_seed(18)
