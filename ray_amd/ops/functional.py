@@ -288,9 +288,12 @@ def _splitk(M: int, N: int, K: int) -> int:
     batched kernels fill the 256 CUs only with many (N/256)*(K/256)*S tiles. Slices
     stay >= 2048 tokens so each batch GEMM keeps a long K loop."""
     S = 1
-    while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 2048:
+    while S < _WGRAD_MAX_SPLITS and M % (2 * S) == 0 and M // (2 * S) >= 2048:
         S *= 2
     return S
+
+
+_WGRAD_MAX_SPLITS = int(os.environ.get("RAY_AMD_WGRAD_SPLITS", "16"))
 
 
 def _wgrad_partials(dy2, x2, S, M, N, K):
@@ -912,6 +915,43 @@ class _BiasReLU(torch.autograd.Function):
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
         return _relu_bias_bwd(dy, y, ctx.bias)
+
+
+class _LinearReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = torch.empty((x.shape[0], w.shape[0]), device=x.device, dtype=x.dtype)
+        torch.mm(x, w.t(), out=y)
+        check(_lib.lib().ra_bias_relu_fwd(ptr(y), ptr(b), ptr(y), y.shape[0], y.shape[1],
+                                          stream_ptr()), "bias_relu_fwd")
+        ctx.save_for_backward(x, w, y)
+        ctx.bias = b
+        ctx.weight = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dh, db = _relu_bias_bwd(dy, y, ctx.bias)
+        dx = torch.mm(dh, w) if ctx.needs_input_grad[0] else None
+        sink = _grad_sink(ctx.weight)
+        if sink is not None and sink.is_contiguous():
+            sink.addmm_(dh.t(), x)  # weight gradient accumulated straight into the flat buffer
+            _grad_done(ctx.weight)
+            return dx, None, db
+        return dx, torch.mm(dh.t(), x), db
+
+
+def linear_relu(x, w, b):
+    """relu(x @ w.T + b) for 2-D bf16 x: hipBLASLt GEMM + one fused bias/ReLU pass; the
+    backward fuses the ReLU mask with the bias-gradient reduction and accumulates the
+    weight gradient into the flat-buffer sink (no separate AccumulateGrad)."""
+    F_ = w.shape[0]
+    if (_hip(x) and x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and b is not None and b.dtype == torch.bfloat16 and F_ % 8 == 0
+            and 256 % (F_ // 8) == 0 and x.shape[0] > 0):
+        return _LinearReLU.apply(x.contiguous(), w, b)
+    return torch.relu(torch.nn.functional.linear(x, w, b))
 
 
 def bias_relu(h, bias):

@@ -71,10 +71,13 @@ class NatureCNN(nn.Module):
                     x = x.index_select(0, idx)
                     idx = None
                 x = x.to(torch.bfloat16).permute(0, 3, 1, 2)
+            from ray_amd.ops.functional import linear_relu
+
             for i, conv in enumerate(convs):
                 x = conv2d_bias_relu(x, conv.weight, conv.bias, conv.stride[0],
                                      idx=idx if i == 0 else None)
-            return self.fc(x.permute(0, 2, 3, 1).flatten(1))
+            fc = self.fc[0]
+            return linear_relu(x.permute(0, 2, 3, 1).flatten(1), fc.weight, fc.bias)
         if idx is not None:
             x = x.index_select(0, idx)
         if x.dtype == torch.uint8:

@@ -240,6 +240,22 @@ def test_bias_relu(cuda_device, shape):
     assert _rel(b.grad, br.grad) < 2e-2
 
 
+def test_linear_relu(cuda_device):
+    torch.manual_seed(25)
+    x = torch.randn(300, 3136, device=cuda_device).bfloat16().requires_grad_()
+    w = (0.02 * torch.randn(512, 3136, device=cuda_device)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(512, device=cuda_device)).bfloat16().requires_grad_()
+    y = rf.linear_relu(x, w, b)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.relu(torch.nn.functional.linear(xr, wr, br))
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    for a_, b_ in ((x, xr), (w, wr), (b, br)):
+        assert _rel(a_.grad, b_.grad) < 2e-2
+
+
 def test_bias_relu_flat_sink(cuda_device):
     """With a flat-managed bias the gradient is written into the flat buffer directly."""
     from ray_amd.parallel.flat import FlatParams
