@@ -96,6 +96,8 @@ _SIGS = {
     "ra_conv_fwd": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 8
                    + [c_float, c_int, c_void_p],
     "ra_conv_wgrad_work": [c_int] * 8,
+    "ra_conv_dgrad_supported": [c_int] * 5,
+    "ra_conv_dgrad": [c_void_p] * 3 + [c_int] * 8 + [c_void_p],
     "ra_conv_wgrad": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p, c_int]
                      + [c_int] * 8 + [c_float, c_void_p],
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,

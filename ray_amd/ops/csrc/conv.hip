@@ -288,6 +288,84 @@ __global__ __launch_bounds__(1024) void conv_wgrad_reduce(const float* __restric
   }
 }
 
+// ------------------------------------------------------------------ input gradient
+// dX[b, ih, iw, ci] = sum over taps (kh, kw) with ih = S*oh + kh, iw = S*ow + kw of
+// dY[b, oh, ow, :] . W[:, kh, kw, ci]. Input pixels are split into S*S parity classes
+// (ph, pw) = (ih % S, iw % S): inside a class the taps are kh = ph + S*j, kw = pw + S*jw
+// and oh = ih/S - j, so each class is a stride-1 implicit GEMM over TAPS*NOUT
+// reduction values with the SAME filter taps for every pixel (MFMA operand shared by the
+// wave). Orientation as the forward: A = W^T slice [32 ci][tap, co] transposed into LDS
+// once per workgroup, B = gathered dY rows (16-B loads, zero outside the output), C =
+// 32 input channels x 32 pixels.
+struct DgradArgs {
+  const bf16_t* dy;   // [B, OH, OW, NOUT]
+  const bf16_t* w;    // [NOUT, KH, KW, CI]
+  bf16_t* dx;         // [B, H, W, CI]
+  int B, H, W, OH, OW;
+  int wg_start[10];   // prefix sums of workgroups per parity class (S*S <= 9)
+};
+
+template <int KH, int KW, int CI, int S, int NOUT>
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(DgradArgs a) {
+  constexpr int TH = KH / S, TW = KW / S, TAPS = TH * TW, KP = TAPS * NOUT, LDW = KP + 8;
+  static_assert(KH % S == 0 && KW % S == 0 && NOUT % 16 == 0 && CI % 32 == 0, "dgrad shape");
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[32 * LDW];
+  int cls = 0;
+  while (cls + 1 < S * S && (int)blockIdx.x >= a.wg_start[cls + 1]) ++cls;
+  const int ph = cls / S, pw = cls % S;
+  const int H2 = (a.H - ph + S - 1) / S, W2 = (a.W - pw + S - 1) / S;
+  const int cib = blockIdx.y * 32;
+  // W[co][kh][kw][ci] -> Wt[ci - cib][t * NOUT + co], t = j * TW + jw (this class's taps)
+  for (int i = threadIdx.x; i < TAPS * NOUT * 4; i += 256) {
+    const int c8 = i & 3, rest = i >> 2, co = rest % NOUT, t = rest / NOUT;
+    const int kh = ph + S * (t / TW), kw = pw + S * (t % TW);
+    const uint4 u = *reinterpret_cast<const uint4*>(
+        a.w + (((long)co * KH + kh) * KW + kw) * CI + cib + c8 * 8);
+    const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      Wt[(c8 * 8 + e) * LDW + t * NOUT + co] =
+          (bf16_t)((e & 1) ? (wd[e >> 1] >> 16) : (wd[e >> 1] & 0xffffu));
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int npx = a.B * H2 * W2;
+  const int m0 = ((blockIdx.x - a.wg_start[cls]) * 4 + wv) * 32;
+  if (m0 >= npx) return;
+  const int m = min(m0 + r, npx - 1);
+  const int b = m / (H2 * W2), rem = m - b * (H2 * W2), ih2 = rem / W2, iw2 = rem - ih2 * W2;
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t) {
+    const int oh = ih2 - t / TW, ow = iw2 - t % TW;
+    const bool ok = oh >= 0 && oh < a.OH && ow >= 0 && ow < a.OW;
+    const bf16_t* src = a.dy + (((long)b * a.OH + (ok ? oh : 0)) * a.OW + (ok ? ow : 0)) * NOUT +
+                        8 * h;
+    bf16x8_t bv[NOUT / 16];
+#pragma unroll
+    for (int kc = 0; kc < NOUT / 16; ++kc) {
+      const uint4 u = ok ? *reinterpret_cast<const uint4*>(src + kc * 16) : make_uint4(0, 0, 0, 0);
+      bv[kc] = __builtin_bit_cast(bf16x8_t, u);
+    }
+#pragma unroll
+    for (int kc = 0; kc < NOUT / 16; ++kc)
+      acc = mfma32(*reinterpret_cast<const bf16x8_t*>(Wt + r * LDW + t * NOUT + kc * 16 + 8 * h),
+                   bv[kc], acc);
+  }
+  if (m0 + r >= npx) return;
+  const int ih = S * ih2 + ph, iw = S * iw2 + pw;
+  bf16_t* o = a.dx + (((long)b * a.H + ih) * a.W + iw) * CI + cib;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = acc[4 * q + j];
+    *reinterpret_cast<uint2*>(o + 8 * q + 4 * h) = pack4(v);
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 // Supported layer shapes (KH, KW, C, S, NOUT, U8): the Nature-CNN stack; anything else
 // returns hipErrorNotSupported and the caller uses MIOpen.
@@ -327,6 +405,39 @@ static int wgrad_rows(int M, int K, int NOUT) {
 }
 
 }  // namespace
+
+// Input-gradient kernels exist for the activation layers (conv2, conv3 shapes).
+static int dgrad_id(int KH, int KW, int C, int S, int NOUT) {
+  if (KH == 4 && KW == 4 && C == 32 && S == 2 && NOUT == 64) return 0;
+  if (KH == 3 && KW == 3 && C == 64 && S == 1 && NOUT == 64) return 1;
+  return kUnsupported;
+}
+
+RA_EXPORT int ra_conv_dgrad_supported(int KH, int KW, int C, int S, int NOUT) {
+  return dgrad_id(KH, KW, C, S, NOUT) != kUnsupported;
+}
+
+// dx [B, H, W, C] bf16 (every element written) from dy [B, OH, OW, NOUT] and w OHWI.
+RA_EXPORT int ra_conv_dgrad(const void* dy, const void* w, void* dx, int B, int H, int W, int C,
+                            int KH, int KW, int S, int NOUT, hipStream_t st) {
+  const int id = dgrad_id(KH, KW, C, S, NOUT);
+  if (id == kUnsupported || H < KH || W < KW || S * S > 9) return hipErrorNotSupported;
+  DgradArgs a{};
+  a.dy = (const bf16_t*)dy; a.w = (const bf16_t*)w; a.dx = (bf16_t*)dx;
+  a.B = B; a.H = H; a.W = W; a.OH = (H - KH) / S + 1; a.OW = (W - KW) / S + 1;
+  int total = 0;
+  for (int c = 0; c < S * S; ++c) {
+    const int ph = c / S, pw = c % S;
+    const int np = B * ((H - ph + S - 1) / S) * ((W - pw + S - 1) / S);
+    a.wg_start[c] = total;
+    total += (np + 127) / 128;
+  }
+  for (int c = S * S; c < 10; ++c) a.wg_start[c] = total;
+  const dim3 g(total, C / 32), b(256);
+  if (id == 0) hipLaunchKernelGGL((conv_dgrad_kernel<4, 4, 32, 2, 64>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((conv_dgrad_kernel<3, 3, 64, 1, 64>), g, b, 0, st, a);
+  return hipGetLastError();
+}
 
 RA_EXPORT int ra_conv_supported(int KH, int KW, int C, int S, int NOUT, int u8) {
   return config_id(KH, KW, C, S, NOUT, u8) != kUnsupported;

@@ -277,6 +277,8 @@ _ATTN_BWD = os.environ.get("RAY_AMD_ATTN_BWD", "split")
 _WGRAD_LT = _WGRAD == "lt"
 # RAY_AMD_WGRAD_STREAM=1: weight-gradient GEMMs (into flat grads) run on a side stream
 _WGRAD_STREAM = os.environ.get("RAY_AMD_WGRAD_STREAM", "1") == "1"
+# RAY_AMD_CONV_DGRAD=0: conv input gradients on MIOpen instead of conv.hip
+_CONV_DGRAD = os.environ.get("RAY_AMD_CONV_DGRAD", "1") == "1"
 # RAY_AMD_CONV_WGRAD_STREAM=1: the same for the conv weight-gradient kernels
 _CONV_WGRAD_STREAM = os.environ.get("RAY_AMD_CONV_WGRAD_STREAM", "0") == "1"
 
@@ -1041,8 +1043,15 @@ class _ConvBiasReLU(torch.autograd.Function):
             dw = None
         dx = None
         if not u8 and ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dh, x, w, None, [S, S], [0, 0], [1, 1], False,
-                                                     [0, 0], 1, [True, False, False])[0]
+            if _CONV_DGRAD and L.ra_conv_dgrad_supported(KH, KW, C, S, O):
+                dxh = torch.empty((B, H, W, C), device=dy.device, dtype=torch.bfloat16)
+                check(L.ra_conv_dgrad(ptr(_nhwc_rows(dh)), ptr(w), ptr(dxh), B, H, W, C, KH, KW,
+                                      S, O, stream_ptr()), "conv_dgrad")
+                dx = dxh.permute(0, 3, 1, 2)
+            else:
+                dx = torch.ops.aten.convolution_backward(dh, x, w, None, [S, S], [0, 0], [1, 1],
+                                                         False, [0, 0], 1,
+                                                         [True, False, False])[0]
         return dx, dw, db, None, None, None
 
 

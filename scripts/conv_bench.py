@@ -82,6 +82,10 @@ def main():
         rec["miopen_wgrad_us"] = round(timeit(lambda: torch.ops.aten.convolution_backward(
             dyc, xb, w, None, [S, S], [0, 0], [1, 1], False, [0, 0], 1,
             [False, True, False])), 2)
+        if not u8 and L.ra_conv_dgrad_supported(K, K, C, S, O):
+            dx = torch.empty(B, HW, HW, C, device=dev, dtype=torch.bfloat16)
+            rec["dgrad_us"] = round(timeit(lambda: check(L.ra_conv_dgrad(
+                ptr(dy), ptr(w), ptr(dx), B, HW, HW, C, K, K, S, O, stream_ptr()), "dgrad")), 2)
         if not u8:
             rec["miopen_dgrad_us"] = round(timeit(lambda: torch.ops.aten.convolution_backward(
                 dyc, xb, w, None, [S, S], [0, 0], [1, 1], False, [0, 0], 1,
