@@ -164,50 +164,57 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   }
   // im2col pieces: PE contiguous k values (16 uint8 = one 16-B load, or 8 bf16); every
   // piece of a thread has the same k (so one k offset), rows rowb + i*rstep of a chunk
-  constexpr int PE = U8 ? 16 : 8, XPR = KB / PE, XQ = 64 * XPR / 256;
+  constexpr int PE = U8 ? 16 : 8, XPR = KB / PE, XQ = 64 * XPR / 256;  // XQ pieces/thread
   static_assert(KWC % PE == 0 && 256 % XPR == 0 && XQ >= 1, "im2col pieces");
   const int xk = tid % XPR, xrow = tid / XPR;
   const int kx = kbase + xk * PE, kxh = kx / KWC;
   const int koff = kxh * a.W * C + (kx - kxh * KWC);
-  uint4 dreg[DP], xreg[XQ * (PE / 8)];
-  auto load = [&](int c) {
+  // Raw global data of one chunk in registers (uint8 pieces stay packed until the LDS
+  // store, so the loads of a chunk can stay in flight for two chunk steps)
+  struct Regs {
+    uint4 d[DP], x[XQ];
+  };
+  auto load = [&](int c, Regs& R) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < DP; ++i) {
       const int pc = tid + 256 * i, row = pc / (NOUT / 8), c8 = pc - row * (NOUT / 8);
       const int m = mbeg + c * 64 + row;
-      dreg[i] = m < mend ? *reinterpret_cast<const uint4*>(a.dy + (long)m * NOUT + c8 * 8)
-                         : make_uint4(0, 0, 0, 0);
+      R.d[i] = m < mend ? *reinterpret_cast<const uint4*>(a.dy + (long)m * NOUT + c8 * 8)
+                        : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int local = c * 64 + xrow + i * (256 / XPR);
       if (mbeg + local >= mend) {
-#pragma unroll
-        for (int e = 0; e < PE / 8; ++e) xreg[i * (PE / 8) + e] = make_uint4(0, 0, 0, 0);
+        R.x[i] = make_uint4(0, 0, 0, 0);
         continue;
       }
       const long off = (long)sbase[local] + koff;
-      if constexpr (U8) {
-        const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.x) + off);
-        xreg[2 * i] = __builtin_bit_cast(uint4, u8x8_to_bf16(make_uint2(u.x, u.y), a.scale));
-        xreg[2 * i + 1] = __builtin_bit_cast(uint4, u8x8_to_bf16(make_uint2(u.z, u.w), a.scale));
-      } else {
-        xreg[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.x) + off);
-      }
+      if constexpr (U8)
+        R.x[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(a.x) + off);
+      else
+        R.x[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.x) + off);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const Regs& R) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < DP; ++i) {
       const int pc = tid + 256 * i, row = pc / (NOUT / 8), c8 = pc - row * (NOUT / 8);
-      *reinterpret_cast<uint4*>(&dys[buf][row * DS + c8 * 8]) = dreg[i];
+      *reinterpret_cast<uint4*>(&dys[buf][row * DS + c8 * 8]) = R.d[i];
     }
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int row = xrow + i * (256 / XPR);
-#pragma unroll
-      for (int e = 0; e < PE / 8; ++e)
-        *reinterpret_cast<uint4*>(&xs[buf][row * XS + xk * PE + 8 * e]) = xreg[i * (PE / 8) + e];
+      bf16_t* dst = &xs[buf][row * XS + xk * PE];
+      if constexpr (U8) {
+        const uint4 u = R.x[i];
+        *reinterpret_cast<uint4*>(dst) =
+            __builtin_bit_cast(uint4, u8x8_to_bf16(make_uint2(u.x, u.y), a.scale));
+        *reinterpret_cast<uint4*>(dst + 8) =
+            __builtin_bit_cast(uint4, u8x8_to_bf16(make_uint2(u.z, u.w), a.scale));
+      } else {
+        *reinterpret_cast<uint4*>(dst) = R.x[i];
+      }
     }
   };
   __syncthreads();  // sbase
@@ -222,15 +229,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-
-  if (nchunks > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nchunks) load(c + 1);
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     const bf16_t* D = dys[buf];
     const bf16_t* X = xs[buf];
 #pragma unroll
@@ -244,7 +243,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
       const bf16x8_t bfr = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
       acc = mfma32(af, bfr, acc);
     }
-    if (c + 1 < nchunks) store(buf ^ 1);
+  };
+
+  // two register sets: chunk c+2 is loading while chunk c is computed from LDS and
+  // chunk c+1 is written to the other LDS buffer (one barrier per chunk)
+  Regs RA, RB;
+  if (nchunks > 0) load(0, RA);
+  if (nchunks > 1) load(1, RB);
+  if (nchunks > 0) store(0, RA);
+  __syncthreads();
+  for (int c = 0; c < nchunks; c += 2) {
+    if (c + 2 < nchunks) load(c + 2, RA);
+    compute(0);
+    if (c + 1 < nchunks) store(1, RB);
+    __syncthreads();
+    if (c + 1 >= nchunks) break;
+    if (c + 3 < nchunks) load(c + 3, RB);
+    compute(1);
+    if (c + 2 < nchunks) store(0, RA);
     __syncthreads();
   }
   // partial tile -> part[blockIdx.x][n][k]
