@@ -2111,8 +2111,12 @@ class CoreWorker:
                 else:
                     fn = getattr(self.actor_instance, m)
                 loop = asyncio.get_running_loop()
-                args, kwargs = await loop.run_in_executor(None, self._decode_args, spec["args"],
-                                                          owner)
+                enc = spec["args"]
+                if all(inl is not None for _, _, inl in (enc[1] or ())):
+                    # every argument is inline: decoding cannot block, skip the thread hop
+                    args, kwargs = self._decode_args(enc, owner)
+                else:  # may wait for ObjectRef arguments: off the event loop
+                    args, kwargs = await loop.run_in_executor(None, self._decode_args, enc, owner)
                 if spec["nret"] == -1 and inspect.isasyncgenfunction(
                         getattr(fn, "__func__", fn)):
                     # async generators run on the actor's own event loop (they may share
@@ -2133,7 +2137,11 @@ class CoreWorker:
                     r = fn(*args, **kwargs)
                     if inspect.isawaitable(r):
                         r = await r
-                    returns = await loop.run_in_executor(None, self._package_returns, spec, r)
+                    if _small_value(r):  # serialising a scalar / short bytes is cheap
+                        returns = self._package_returns(spec, r)
+                    else:  # large values are written to the object store off the loop
+                        returns = await loop.run_in_executor(None, self._package_returns, spec,
+                                                             r)
                     extra = {}
             except _ActorExit:
                 self._send_reply(conn, owner, tid, self._package_returns(spec, None), {})
@@ -2217,3 +2225,10 @@ class _DynamicRefs(list):
 
 def _ready():
     return True
+
+
+def _small_value(v) -> bool:
+    """Return values packaged inline on an async actor's event loop."""
+    if v is None or isinstance(v, (bool, int, float)):
+        return True
+    return isinstance(v, (bytes, str)) and len(v) <= 4096
