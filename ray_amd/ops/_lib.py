@@ -107,6 +107,10 @@ _SIGS = {
     "ra_attn_bwd_kv": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
     "ra_attn_bwd_q": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
     "ra_attn_bwd_fused": [c_void_p] * 7 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "ra_gemm_nt": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
+                   c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                   c_void_p],
+    "ra_gemm_dgelu_work": [c_int, c_int],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],
     "ra_arena_open": [c_int, c_void_p, ctypes.POINTER(c_void_p)],
