@@ -157,7 +157,7 @@ __device__ __forceinline__ void epilogue_tile(f32x4_t (&acc)[4][8], int m0, int 
         s += __shfl_xor(s, 8, 64);
         csum[nb][i] = s;
       }
-    if ((lane & 15) == 0) {
+    if ((lane & 15) == 0 && m0 + wm * 128 < M) {  // colpart has ceil(M / 128) rows
       float* prow = colpart + (long)(m0 / 128 + wm) * N;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
