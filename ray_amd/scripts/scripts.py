@@ -286,6 +286,35 @@ def cmd_memory(a):
     return 0
 
 
+def cmd_debug(a):
+    """List live remote-pdb breakpoints (util.rpdb) and attach the terminal to one."""
+    import time
+
+    _connect(a.address)
+    from ray_amd.util import rpdb
+
+    deadline = time.time() + a.wait
+    bps = rpdb.list_breakpoints()
+    while not bps and time.time() < deadline:
+        time.sleep(0.5)
+        bps = rpdb.list_breakpoints()
+    if not bps:
+        print("No active breakpoints.")
+        return 0
+    for i, b in enumerate(bps):
+        print(f"{i}: pid={b['pid']} {b['host']}:{b['port']} task={b.get('task_id')} "
+              f"actor={b.get('actor_id')}")
+    idx = a.index
+    if idx is None:
+        if len(bps) == 1 or not sys.stdin.isatty():
+            idx = 0
+        else:
+            idx = int(input("Enter breakpoint index: "))
+    b = bps[idx]
+    rpdb.connect_pdb_client(b["host"], b["port"])
+    return 0
+
+
 def cmd_timeline(a):
     ray = _connect(a.address)
     out = a.output or f"/tmp/ray_amd-timeline-{time.strftime('%Y-%m-%d_%H-%M-%S')}.json"
@@ -449,6 +478,12 @@ def build_parser():
     s.add_argument("--address")
     s.add_argument("--limit", type=int, default=50)
     s.set_defaults(fn=cmd_memory)
+
+    s = sub.add_parser("debug", help="attach to a remote pdb breakpoint (util.pdb.set_trace)")
+    s.add_argument("--address")
+    s.add_argument("--index", type=int)
+    s.add_argument("--wait", type=float, default=0.0, help="seconds to wait for a breakpoint")
+    s.set_defaults(fn=cmd_debug)
 
     s = sub.add_parser("microbenchmark")
     s.add_argument("--quick", action="store_true")
