@@ -8,7 +8,10 @@ from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface
                                    from_items, from_numpy, from_numpy_refs, from_pandas,
                                    from_pandas_refs, from_torch, range, range_tensor,
                                    read_binary_files, read_csv, read_datasource, read_images,
-                                   read_json, read_numpy, read_parquet, read_text)
+                                   read_json, read_numpy, read_parquet, read_parquet_bulk,
+                                   read_text)
+from ray_amd.data.datasource import (Datasink, Datasource, RandomAccessDataset,  # noqa: F401
+                                     ReadTask, read_sql, read_webdataset)
 from ray_amd.data import preprocessors  # noqa: F401
 from ray_amd.data._executor import ExecutionOptions, ExecutionResources  # noqa: F401
 

@@ -706,6 +706,50 @@ class Dataset:
     def write_numpy(self, path, *, column, **kw):
         self._write(path, "numpy", column=column)
 
+    def write_datasink(self, datasink, *, ray_remote_args=None, **kw):
+        """Write through a custom ``Datasink`` (data/datasource.py)."""
+        from ray_amd.data.datasource import write_datasink
+
+        return write_datasink(self, datasink, ray_remote_args)
+
+    def write_sql(self, sql: str, connection_factory, **kw):
+        """INSERT every row with ``sql`` (one DB-API placeholder per column)."""
+        from ray_amd.data.datasource import SQLDatasink
+
+        return self.write_datasink(SQLDatasink(sql, connection_factory))
+
+    def write_webdataset(self, path: str, *, encoder: bool = True, **kw):
+        """One tar shard per block; row -> members ``<__key__>.<column>``."""
+        from ray_amd.data.datasource import _write_tar
+
+        ray.get([_write_tar.remote(r, path, i, encoder)
+                 for i, (r, _) in enumerate(X.execute(self._plan))])
+
+    def write_images(self, path: str, column: str, file_format: str = "png", **kw):
+        from ray_amd.data.datasource import _write_images_block
+
+        ray.get([_write_images_block.remote(r, path, column, file_format, i)
+                 for i, (r, _) in enumerate(X.execute(self._plan))])
+
+    def to_random_access_dataset(self, key: str, num_workers: int | None = None):
+        from ray_amd.data.datasource import RandomAccessDataset
+
+        return RandomAccessDataset(self, key, num_workers or 2)
+
+    def randomize_block_order(self, *, seed: int | None = None) -> "Dataset":
+        """Same blocks, shuffled order (no data movement)."""
+        parent = self
+
+        def lazy():
+            refs, metas = parent._blocks()
+            order = np.random.default_rng(seed).permutation(len(refs))
+            return [refs[i] for i in order], [metas[i] for i in order]
+
+        return Dataset(X.Plan(("lazy", lazy)))
+
+    def to_pandas_refs(self):
+        return [ray.put(B.to_batch(ray.get(r), "pandas")) for r, _ in X.execute(self._plan)]
+
     def __repr__(self):
         return f"Dataset(stages={[s.name for s in self._plan.stages]})"
 

@@ -191,13 +191,31 @@ def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
 
 
 def read_images(paths, *, size=None, mode=None, include_paths=False, **kw) -> Dataset:
-    """Reads .npy image arrays (PIL is not installed in this image): HWC uint8."""
+    """Image files (png/jpg/bmp/gif/webp/tiff via PIL, or .npy HWC arrays) -> rows with an
+    ``image`` HWC uint8 array; ``size=(h, w)`` resizes, ``mode`` converts (e.g. "RGB")."""
+    exts = [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".webp", ".tif", ".tiff", ".npy"]
 
     def rd(f):
-        img = np.load(f)
+        if f.endswith(".npy"):
+            img = np.load(f)
+        else:
+            from PIL import Image
+
+            im = Image.open(f)
+            if mode is not None:
+                im = im.convert(mode)
+            if size is not None:
+                im = im.resize((size[1], size[0]))
+            img = np.asarray(im)
         return {"image": img[None]}
 
-    return _file_ds(paths, [".npy"], rd, include_paths)
+    return _file_ds(paths, exts, rd, include_paths)
+
+
+def read_parquet_bulk(paths, *, columns=None, include_paths=False, **kw) -> Dataset:
+    """read_parquet over an explicit file list (no directory expansion / metadata pass)."""
+    return read_parquet(list(paths) if not isinstance(paths, str) else [paths],
+                        columns=columns, include_paths=include_paths)
 
 
 def read_datasource(datasource, *, parallelism=-1, **kw) -> Dataset:
