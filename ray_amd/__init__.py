@@ -65,10 +65,29 @@ __all__ = [
     "get_gpu_ids", "init", "is_initialized", "kill", "method", "nodes", "put", "remote",
     "shutdown", "timeline", "wait", "get_runtime_context", "ObjectRef", "ObjectRefGenerator",
     "ActorHandle", "LOCAL_MODE", "SCRIPT_MODE", "WORKER_MODE", "exceptions", "Language",
+    "client", "ClientBuilder", "show_in_dashboard",
 ]
 
+from ray_amd.client_builder import ClientBuilder, client  # noqa: F401,E402
+
+
+def show_in_dashboard(message: str, key: str = "", dtype: str = "text"):
+    """Attach a message to the current actor / task, shown by the dashboard and the state
+    API (``list_actors(detail=True)``) (reference: python/ray/_private/worker.py)."""
+    if dtype not in ("text", "html"):
+        raise ValueError(f"dtype accepts only text or html, got {dtype!r}")
+    from ray_amd._private import worker as _w
+
+    cw = _w._check_connected()
+    msgs = getattr(cw, "dashboard_messages", None)
+    if msgs is None:
+        msgs = cw.dashboard_messages = {}
+    msgs[key] = {"message": message, "dtype": dtype}
+
+
 _LAZY_SUBPACKAGES = ("data", "train", "tune", "serve", "rllib", "util", "workflow", "dag",
-                     "air", "cluster_utils", "job_submission", "dashboard", "experimental")
+                     "air", "cluster_utils", "job_submission", "dashboard", "experimental",
+                     "autoscaler", "runtime_env")
 
 
 def __getattr__(name):

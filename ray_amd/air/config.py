@@ -91,6 +91,26 @@ class RunConfig:
 
 
 @dataclass
+class SyncConfig:
+    """Checkpoint/artifact sync to ``RunConfig.storage_path`` (reference: train/
+    _internal/syncer.py SyncConfig). Storage here is a (shared) filesystem path written
+    directly, so these knobs only bound how often / how long driver-side syncs run."""
+
+    sync_period: int = 300
+    sync_timeout: int = 1800
+    sync_artifacts: bool = False
+    sync_artifacts_on_checkpoint: bool = True
+    upload_dir: str | None = None
+    syncer: object = None
+    sync_on_checkpoint: bool = True
+
+    def __post_init__(self):
+        if self.upload_dir is not None:
+            raise DeprecationWarning("SyncConfig(upload_dir) is deprecated: use "
+                                     "RunConfig(storage_path=...)")
+
+
+@dataclass
 class DatasetConfig:
     fit: bool | None = None
     split: bool | None = None

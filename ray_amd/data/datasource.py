@@ -363,3 +363,62 @@ class RandomAccessDataset:
         st = ray.get([a.stats.remote() for a in self._actors])
         return f"RandomAccessDataset: {len(st)} workers, rows per worker " \
                f"{[s['num_rows'] for s in st]}"
+
+
+# ------------------------------------------------------------ file-based datasinks
+class _FileDatasink(Datasink):
+    def __init__(self, path: str, *, file_format: str = "bin", filesystem=None,
+                 try_create_dir: bool = True, **kw):
+        self.path = path
+        self.file_format = file_format
+        self.try_create_dir = try_create_dir
+
+    def on_write_start(self):
+        if self.try_create_dir:
+            os.makedirs(self.path, exist_ok=True)
+
+    def _open(self, name: str):
+        return open(os.path.join(self.path, name), "wb")
+
+
+class RowBasedFileDatasink(_FileDatasink):
+    """One file per row: implement ``write_row_to_file(row: dict, file)``
+    (reference: data/datasource/file_datasink.py RowBasedFileDatasink)."""
+
+    def write_row_to_file(self, row: dict, file) -> None:
+        raise NotImplementedError
+
+    def write(self, blocks, ctx):
+        n = 0
+        for blk in blocks:
+            for i, row in enumerate(B.to_rows(blk)):
+                with self._open(f"{ctx['task_idx']:06d}_{i:06d}.{self.file_format}") as f:
+                    self.write_row_to_file(row, f)
+                n += 1
+        return n
+
+    def on_write_complete(self, write_results):
+        return sum(write_results)
+
+
+class BlockBasedFileDatasink(_FileDatasink):
+    """One file per block: implement ``write_block_to_file(block, file)`` (the block is a
+    pyarrow Table, like the reference's BlockAccessor.to_arrow())."""
+
+    def __init__(self, path: str, *, min_rows_per_file: int | None = None, **kw):
+        super().__init__(path, **kw)
+        self.min_rows_per_file = min_rows_per_file
+
+    def write_block_to_file(self, block, file) -> None:
+        raise NotImplementedError
+
+    def write(self, blocks, ctx):
+        n = 0
+        for j, blk in enumerate(blocks):
+            with self._open(f"{ctx['task_idx']:06d}_{j:03d}.{self.file_format}") as f:
+                self.write_block_to_file(B.to_batch(blk, "pyarrow"), f)
+            n += B.num_rows(blk)
+        return n
+
+    def on_write_complete(self, write_results):
+        return sum(write_results)

@@ -304,3 +304,306 @@ class GPUImageNormalize(Preprocessor):
         return ds.map_batches(_GPUNormalizeUDF, fn_constructor_args=self.args,
                               concurrency=self.concurrency, num_gpus=self.num_gpus,
                               batch_size=self.batch_size, batch_format="numpy")
+
+
+# ---------------------------------------------------------------- text / hashing / bins
+# Reference parity: python/ray/data/preprocessors/{tokenizer,vectorizer,hasher,encoder,
+# scaler,transformer,discretizer}.py — same output column naming; statistics computed by
+# one distributed pass (per-block partial counts / column gathers reduced in the driver).
+def _tokens(x):
+    return str(x).split(" ")
+
+
+def _stable_hash(s: str, n: int) -> int:
+    import hashlib
+
+    return int.from_bytes(hashlib.blake2b(str(s).encode(), digest_size=8).digest(), "little") % n
+
+
+def _column_values(ds, c):
+    parts = [np.asarray(b[c]) for b in ds.iter_batches(batch_size=None)]
+    return np.concatenate(parts) if parts else np.array([])
+
+
+class Tokenizer(Preprocessor):
+    """Replace each string with its token list (``tokenization_fn``, default split on " ")."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, tokenization_fn=None, output_columns=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.tokenization_fn = tokenization_fn or _tokens
+        self.output_columns = list(output_columns or self.columns)
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        for c, o in zip(self.columns, self.output_columns):
+            col = np.empty(len(b[c]), dtype=object)
+            col[:] = [list(self.tokenization_fn(x)) for x in b[c]]
+            b[o] = col
+        return b
+
+
+class CountVectorizer(Preprocessor):
+    """Per string column, one count column ``{col}_{token}`` for each of the (top
+    ``max_features``) tokens seen during fit, most frequent first."""
+
+    def __init__(self, columns, tokenization_fn=None, max_features=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.tokenization_fn = tokenization_fn or _tokens
+        self.max_features = max_features
+
+    def _fit(self, ds):
+        from collections import Counter
+
+        stats = {}
+        for c in self.columns:
+            cnt = Counter()
+            for b in ds.iter_batches(batch_size=None):
+                for x in b[c]:
+                    cnt.update(self.tokenization_fn(x))
+            stats[c] = [t for t, _ in cnt.most_common(self.max_features)]
+        self.stats_ = stats
+
+    def _transform_numpy(self, b):
+        from collections import Counter
+
+        out = {k: v for k, v in b.items() if k not in self.columns}
+        for c in self.columns:
+            counts = [Counter(self.tokenization_fn(x)) for x in b[c]]
+            for t in self.stats_[c]:
+                out[f"{c}_{t}"] = np.array([k[t] for k in counts], dtype=np.int64)
+        return out
+
+
+class HashingVectorizer(Preprocessor):
+    """Token counts hashed into ``num_features`` buckets: columns ``hash_{col}_{i}``."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, num_features: int, tokenization_fn=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.num_features = num_features
+        self.tokenization_fn = tokenization_fn or _tokens
+
+    def _transform_numpy(self, b):
+        out = {k: v for k, v in b.items() if k not in self.columns}
+        for c in self.columns:
+            m = np.zeros((len(b[c]), self.num_features), dtype=np.int64)
+            for r, x in enumerate(b[c]):
+                for t in self.tokenization_fn(x):
+                    m[r, _stable_hash(t, self.num_features)] += 1
+            for i in range(self.num_features):
+                out[f"hash_{c}_{i}"] = m[:, i]
+        return out
+
+
+class FeatureHasher(Preprocessor):
+    """Hash the (column name, value) of each listed column into ``num_features`` count
+    columns ``hash_{i}``: numeric values add their magnitude to the name's bucket."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, num_features: int, output_column: str | None = None):
+        super().__init__()
+        self.columns = list(columns)
+        self.num_features = num_features
+        self.output_column = output_column
+
+    def _transform_numpy(self, b):
+        n = len(next(iter(b.values()))) if b else 0
+        m = np.zeros((n, self.num_features), dtype=np.float64)
+        for c in self.columns:
+            v = np.asarray(b[c])
+            if np.issubdtype(v.dtype, np.number):
+                m[:, _stable_hash(c, self.num_features)] += v
+            else:
+                for r, x in enumerate(v):
+                    m[r, _stable_hash(f"{c}={x}", self.num_features)] += 1
+        out = {k: v for k, v in b.items() if k not in self.columns}
+        if self.output_column:
+            out[self.output_column] = m
+        else:
+            for i in range(self.num_features):
+                out[f"hash_{i}"] = m[:, i]
+        return out
+
+
+class MultiHotEncoder(Preprocessor):
+    """List-valued columns -> multi-hot count vectors over the categories seen in fit."""
+
+    def __init__(self, columns, max_categories=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.max_categories = max_categories or {}
+
+    def _fit(self, ds):
+        from collections import Counter
+
+        stats = {}
+        for c in self.columns:
+            cnt = Counter()
+            for b in ds.iter_batches(batch_size=None):
+                for x in b[c]:
+                    cnt.update(list(x))
+            cats = [k for k, _ in cnt.most_common(self.max_categories.get(c))]
+            stats[c] = {k: i for i, k in enumerate(sorted(cats, key=str))}
+        self.stats_ = stats
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        for c in self.columns:
+            idx = self.stats_[c]
+            m = np.zeros((len(b[c]), len(idx)), dtype=np.int64)
+            for r, x in enumerate(b[c]):
+                for v in x:
+                    j = idx.get(v.item() if isinstance(v, np.generic) else v)
+                    if j is not None:
+                        m[r, j] += 1
+            b[c] = m
+        return b
+
+
+class Categorizer(Preprocessor):
+    """Columns -> pandas ``CategoricalDtype`` with the categories seen in fit (or the
+    given ``dtypes``). ``transform_batch`` returns the categorical pandas frame; dataset
+    blocks here are numpy column dicts, so ``transform`` keeps the values (out-of-category
+    values become None) and the categorical dtype is re-applied on ``to_pandas``-side
+    batches by ``transform_batch``."""
+
+    def __init__(self, columns, dtypes=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.dtypes = dict(dtypes or {})
+
+    def _fit(self, ds):
+        import pandas as pd
+
+        self.stats_ = {c: self.dtypes.get(c) or pd.CategoricalDtype(ds.unique(c))
+                       for c in self.columns}
+
+    def transform(self, ds):
+        if self.stats_ is None:
+            raise RuntimeError("Categorizer must be fitted before transform")
+        return ds.map_batches(self._transform_pandas, batch_format="pandas", batch_size=4096)
+
+    def _transform_pandas(self, df):
+        df = df.copy()
+        for c in self.columns:
+            df[c] = df[c].astype(self.stats_[c])
+        return df
+
+    def transform_batch(self, batch):
+        import pandas as pd
+
+        return self._transform_pandas(pd.DataFrame(batch))
+
+
+class RobustScaler(Preprocessor):
+    """(x - median) / (q_high - q_low), quantile_range default (0.25, 0.75)."""
+
+    def __init__(self, columns, quantile_range=(0.25, 0.75)):
+        super().__init__()
+        self.columns = list(columns)
+        self.quantile_range = quantile_range
+
+    def _fit(self, ds):
+        lo, hi = self.quantile_range
+        st = {}
+        for c in self.columns:
+            v = _column_values(ds, c).astype(np.float64)
+            q = np.quantile(v, [lo, 0.5, hi]) if len(v) else [0.0, 0.0, 1.0]
+            st[c] = (float(q[1]), float(q[2] - q[0]))
+        self.stats_ = st
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        for c in self.columns:
+            med, iqr = self.stats_[c]
+            b[c] = (np.asarray(b[c], dtype=np.float64) - med) / (iqr if iqr else 1.0)
+        return b
+
+
+class PowerTransformer(Preprocessor):
+    """Yeo-Johnson (any sign) or Box-Cox (positive) power transform with fixed ``power``."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, power: float, method: str = "yeo-johnson"):
+        super().__init__()
+        if method not in ("yeo-johnson", "box-cox"):
+            raise ValueError(f"method must be yeo-johnson or box-cox, got {method!r}")
+        self.columns = list(columns)
+        self.power = power
+        self.method = method
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        lam = self.power
+        for c in self.columns:
+            x = np.asarray(b[c], dtype=np.float64)
+            if self.method == "box-cox":
+                y = np.log(x) if lam == 0 else (np.power(x, lam) - 1) / lam
+            else:
+                y = np.empty_like(x)
+                pos = x >= 0
+                y[pos] = np.log1p(x[pos]) if lam == 0 else (np.power(x[pos] + 1, lam) - 1) / lam
+                neg = ~pos
+                y[neg] = -np.log1p(-x[neg]) if lam == 2 else \
+                    -(np.power(1 - x[neg], 2 - lam) - 1) / (2 - lam)
+            b[c] = y
+        return b
+
+
+class CustomKBinsDiscretizer(Preprocessor):
+    """Bin index per value from user ``bins`` (edges, or {column: edges})."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, bins, *, right=True, include_lowest=False, duplicates="raise",
+                 dtypes=None):
+        super().__init__()
+        self.columns = list(columns)
+        self.bins = bins if isinstance(bins, dict) else {c: bins for c in self.columns}
+        self.right = right
+        self.include_lowest = include_lowest
+        self.stats_ = {}
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        for c in self.columns:
+            edges = np.asarray(self.bins[c], dtype=np.float64)
+            x = np.asarray(b[c], dtype=np.float64)
+            idx = np.searchsorted(edges, x, side="left" if self.right else "right") - 1
+            if self.include_lowest:
+                idx[x == edges[0]] = 0
+            bad = (idx < 0) | (idx >= len(edges) - 1) | np.isnan(x)
+            out = idx.astype(np.float64)
+            out[bad] = np.nan
+            b[c] = out
+        return b
+
+
+class UniformKBinsDiscretizer(CustomKBinsDiscretizer):
+    """``bins`` equal-width bins between each column's fitted min and max."""
+
+    _is_fittable = True
+
+    def __init__(self, columns, bins, *, right=True, include_lowest=False, duplicates="raise",
+                 dtypes=None):
+        super().__init__(columns, {}, right=right, include_lowest=include_lowest)
+        self.n_bins = bins
+        self.stats_ = None
+
+    def _fit(self, ds):
+        a = ds._aggregate(self.columns)
+        self.stats_ = {}
+        for c in self.columns:
+            k = self.n_bins[c] if isinstance(self.n_bins, dict) else self.n_bins
+            lo, hi = float(a[c]["min"]), float(a[c]["max"])
+            self.bins[c] = np.linspace(lo, hi, k + 1)
+            self.stats_[c] = self.bins[c]
+        self.include_lowest = True

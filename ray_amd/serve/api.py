@@ -41,11 +41,30 @@ def _get_controller(create=False):
     return _controller
 
 
-def start(http_options: dict | None = None, detached: bool = True, **kw):
+class HTTPOptions:
+    """HTTP proxy settings (reference: serve/config.py HTTPOptions)."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 8000, root_path: str = "",
+                 location: str = "HeadOnly", request_timeout_s: float | None = None,
+                 keep_alive_timeout_s: int = 5, **kw):
+        if location not in ("HeadOnly", "EveryNode", "NoServer"):
+            raise ValueError(f"invalid HTTP proxy location {location!r}")
+        self.host, self.port, self.root_path = host, port, root_path
+        self.location = location
+        self.request_timeout_s = request_timeout_s
+        self.keep_alive_timeout_s = keep_alive_timeout_s
+
+    def to_dict(self) -> dict:
+        return dict(self.__dict__)
+
+
+def start(http_options=None, detached: bool = True, **kw):
     global _proxy, _http_port
     if not ray.is_initialized():
         ray.init()
     c = _get_controller(create=True)
+    if isinstance(http_options, HTTPOptions):
+        http_options = http_options.to_dict()
     opts = http_options or {}
     port = opts.get("port", 8000)
     existing = ray.get(c.get_proxy.remote())

@@ -95,9 +95,12 @@ class DataParallelTrainer:
     def _shards(self, n):
         shards = [dict() for _ in range(n)]
         for name, ds in self.datasets.items():
-            split = name == "train" or (self.dataset_config is not None and
-                                        getattr(self.dataset_config, "datasets_to_split", None)
-                                        and name in self.dataset_config.datasets_to_split)
+            cfg = self.dataset_config
+            if cfg is None or not hasattr(cfg, "datasets_to_split"):
+                from ray_amd.train.data_config import DataConfig
+
+                cfg = DataConfig()
+            split = cfg.datasets_to_split == "all" or name in cfg.datasets_to_split
             if split and hasattr(ds, "streaming_split"):
                 parts = ds.streaming_split(n, equal=True)
                 for i in range(n):
@@ -142,6 +145,8 @@ class DataParallelTrainer:
                          checkpoint=Checkpoint(cpath))
                 self._save_state(trial_dir, cpath, metrics)
             cbs.end_step([trial])
+            for hook in getattr(self, "_report_hooks", ()):
+                hook(metrics, cpath)
 
         while True:
             try:
@@ -333,3 +338,42 @@ def _should_stop(stop, metrics):
         if k in metrics and metrics[k] >= v:
             return True
     return False
+
+
+class TrainingIterator:
+    """Iterate a trainer's reports as they arrive (reference: train/trainer.py
+    TrainingIterator): ``for metrics in TrainingIterator(trainer): ...``; the final
+    ``Result`` is ``it.result`` once exhausted (errors re-raise from the iteration)."""
+
+    def __init__(self, trainer: DataParallelTrainer):
+        self._trainer = trainer
+        self.result = None
+
+    def __iter__(self):
+        import queue
+        import threading
+
+        q: queue.Queue = queue.Queue()
+        done = object()
+        self._trainer._report_hooks = [lambda m, c: q.put(dict(m))]
+
+        def run():
+            try:
+                self.result = self._trainer.fit()
+                q.put(done)
+            except BaseException as e:  # noqa: BLE001
+                q.put(e)
+
+        th = threading.Thread(target=run, daemon=True, name="TrainingIterator")
+        th.start()
+        try:
+            while True:
+                item = q.get()
+                if item is done:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            th.join(timeout=0.1)
+            self._trainer._report_hooks = []

@@ -15,5 +15,11 @@ from ray_amd.tune.tuner import (CombinedStopper, ExperimentAnalysis,  # noqa: F4
                                 FunctionStopper, MaximumIterationStopper, ResultGrid, Stopper,
                                 TimeoutStopper, TrialPlateauStopper, TuneConfig, Tuner, run)
 from ray_amd.train.result import Result  # noqa: F401
+from ray_amd.tune.registry import (CLIReporter, Experiment,  # noqa: F401
+                                   JupyterNotebookReporter, PlacementGroupFactory,
+                                   ProgressReporter, create_scheduler, create_searcher,
+                                   register_env, register_trainable, run_experiments)
+from ray_amd.air.config import SyncConfig  # noqa: F401
+from ray_amd.tune.tuner import ResumeConfig  # noqa: F401
 
 TuneError = RuntimeError

@@ -129,8 +129,10 @@ class PopulationBasedTraining(TrialScheduler):
     def __init__(self, time_attr="training_iteration", metric=None, mode=None,
                  perturbation_interval=5, hyperparam_mutations=None, quantile_fraction=0.25,
                  resample_probability=0.25, perturbation_factors=(1.2, 0.8),
-                 custom_explore_fn=None, seed=None):
+                 custom_explore_fn=None, seed=None, log_config=True):
         super().__init__(metric, mode)
+        self.log_config = log_config
+        self.policy_log = {}  # trial_id -> [(step, new_config)] (PopulationBasedTrainingReplay)
         self.time_attr = time_attr
         self.interval = perturbation_interval
         self.mutations = hyperparam_mutations or {}
@@ -182,8 +184,73 @@ class PopulationBasedTraining(TrialScheduler):
         if trial in bottom and top and trial not in top:
             donor = self.rng.choice(top)
             if donor.last_checkpoint is not None:
-                trial.pending_exploit = (donor.last_checkpoint, self._explore(donor.config))
+                new_cfg = self._explore(donor.config)
+                trial.pending_exploit = (donor.last_checkpoint, new_cfg)
                 self.num_perturbations += 1
+                if self.log_config:
+                    self._log_policy(trial, donor, t, new_cfg)
+        return self.CONTINUE
+
+
+    def _log_policy(self, trial, donor, step, new_cfg):
+        """Append [trial, donor, step, new_config] to the trial's policy file
+        (pbt_policy_<trial_id>.txt in the trial dir) for PopulationBasedTrainingReplay."""
+        import json
+        import os
+
+        entry = [trial.trial_id, donor.trial_id, int(step), _jsonable(new_cfg)]
+        self.policy_log.setdefault(trial.trial_id, []).append(entry)
+        d = getattr(trial, "local_path", None)
+        if d:
+            try:
+                os.makedirs(d, exist_ok=True)
+                with open(os.path.join(d, f"pbt_policy_{trial.trial_id}.txt"), "a") as f:
+                    f.write(json.dumps(entry) + "\n")
+            except OSError:
+                pass
+
+
+def _jsonable(cfg):
+    out = {}
+    for k, v in cfg.items():
+        if isinstance(v, dict):
+            out[k] = _jsonable(v)
+        elif isinstance(v, (int, float, str, bool)) or v is None:
+            out[k] = v
+        elif hasattr(v, "item"):
+            out[k] = v.item()
+        else:
+            out[k] = repr(v)
+    return out
+
+
+class PopulationBasedTrainingReplay(TrialScheduler):
+    """Replays one PBT trial's hyperparameter schedule (reference: tune/schedulers/
+    pbt.py PopulationBasedTrainingReplay): the trial starts with the first logged
+    config and switches config (keeping its own checkpoint) at each logged step."""
+
+    def __init__(self, policy_file: str):
+        import json
+
+        with open(policy_file) as f:
+            entries = [json.loads(ln) for ln in f if ln.strip()]
+        if not entries:
+            raise ValueError(f"{policy_file} holds no PBT policy entries")
+        self.schedule = sorted((int(e[2]), e[3]) for e in entries)
+        self.config = self.schedule[0][1]
+        self._next = 1
+        super().__init__()
+
+    def on_trial_add(self, runner, trial):
+        trial.config = dict(self.config)
+
+    def on_trial_result(self, runner, trial, result):
+        step = result.get("training_iteration", 0)
+        if self._next < len(self.schedule) and step >= self.schedule[self._next][0]:
+            _, cfg = self.schedule[self._next]
+            self._next += 1
+            if trial.last_checkpoint is not None:
+                trial.pending_exploit = (trial.last_checkpoint, dict(cfg))
         return self.CONTINUE
 
 
@@ -259,6 +326,12 @@ class PB2(PopulationBasedTraining):
             val = lo + float(u) * (hi - lo)
             new[k] = int(round(val)) if isinstance(config.get(k), int) else val
         return new
+
+
+class HyperBandForBOHB(HyperBandScheduler):
+    """HyperBand brackets for BOHB (reference: tune/schedulers/hb_bohb.py). The BOHB
+    model-based searcher (hpbandster / ConfigSpace) is not installed; paired with any
+    searcher this runs the same early-stopping brackets as HyperBandScheduler."""
 
 
 def evenly_distribute_cpus_gpus(runner, trial, result, scheduler):

@@ -5,3 +5,72 @@ from ray_amd.tune.tuner import (BasicVariantGenerator, ConcurrencyLimiter, Repea
                                 Searcher)
 from ray_amd.tune.search.model_based import (BayesOptSearch, HyperOptSearch,  # noqa
                                              OptunaSearch, TPESearch)
+
+UNRESOLVED_SEARCH_SPACE = ("You passed a `{par}` parameter to {cls} that contained unresolved "
+                           "search space definitions. {cls} should however be instantiated "
+                           "with fully configured search spaces only.")
+UNDEFINED_SEARCH_SPACE = ("Trying to sample a configuration from {cls}, but no search space has "
+                          "been defined.")
+UNDEFINED_METRIC_MODE = ("Trying to sample a configuration from {cls}, but the `metric` "
+                         "({metric}) or `mode` ({mode}) parameters have not been set.")
+
+
+class SearchAlgorithm:
+    """Legacy interface above Searcher: produces trials (``next_trial``) and hears results."""
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        return True
+
+    def add_configurations(self, experiments):
+        raise NotImplementedError
+
+    def next_trial(self):
+        raise NotImplementedError
+
+    def on_trial_result(self, trial_id, result):
+        pass
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        pass
+
+    def is_finished(self) -> bool:
+        raise NotImplementedError
+
+    def set_finished(self):
+        self._finished = True
+
+
+class SearchGenerator(SearchAlgorithm):
+    """Adapts a ``Searcher`` to the SearchAlgorithm interface (Tuner accepts either)."""
+
+    def __init__(self, searcher: Searcher):
+        self.searcher = searcher
+        self._finished = False
+        self._count = 0
+
+    def set_search_properties(self, metric, mode, config, **spec):
+        return self.searcher.set_search_properties(metric, mode, config)
+
+    def next_trial(self):
+        cfg = self.searcher.suggest(f"trial_{self._count:05d}")
+        if cfg is None:
+            self._finished = True
+            return None
+        self._count += 1
+        return cfg
+
+    def suggest(self, trial_id):
+        return self.searcher.suggest(trial_id)
+
+    def on_trial_result(self, trial_id, result):
+        if hasattr(self.searcher, "on_trial_result"):
+            self.searcher.on_trial_result(trial_id, result)
+
+    def on_trial_complete(self, trial_id, result=None, error=False):
+        self.searcher.on_trial_complete(trial_id, result=result, error=error)
+
+    def is_finished(self) -> bool:
+        return self._finished
+
+    def __getattr__(self, name):
+        return getattr(self.searcher, name)

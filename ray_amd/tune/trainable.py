@@ -247,5 +247,11 @@ def with_parameters(trainable, **kwargs):
 
 
 def with_resources(trainable, resources):
+    """Per-trial resources: a dict, a PlacementGroupFactory (bundles summed) or a callable
+    config -> either."""
+    from ray_amd.tune.registry import PlacementGroupFactory
+
+    if isinstance(resources, PlacementGroupFactory):
+        resources = resources.required_resources()
     trainable._ray_amd_resources = resources
     return trainable

@@ -494,6 +494,10 @@ def _trainer_to_trainable(trainer):
 class Tuner:
     def __init__(self, trainable=None, *, param_space=None, tune_config=None, run_config=None,
                  _restore_path=None):
+        from ray_amd.tune.registry import resolve_trainable
+
+        self._resume_config = None
+        trainable = resolve_trainable(trainable)
         self.trainable = trainable
         self.param_space = param_space or {}
         self.tune_config = tune_config or TuneConfig()
@@ -541,17 +545,30 @@ class Tuner:
             t.results = results
             t.last_result = results[-1] if results else {}
             t.last_checkpoint = ckpt
-            if status in ("TERMINATED",):
-                t.status = status
+            rc = self._resume_config or ResumeConfig()
+            kind = rc.finished if status == "TERMINATED" else \
+                rc.errored if status == "ERROR" else rc.unfinished
+            if kind == ResumeConfig.ResumeType.SKIP:
+                t.status = status if status in ("TERMINATED", "ERROR") else "TERMINATED"
             else:
                 t.status = "PENDING"
-                t.restore_from = ckpt
+                t.restore_from = ckpt if kind == ResumeConfig.ResumeType.RESUME else None
+                if kind == ResumeConfig.ResumeType.RESTART:
+                    t.results, t.last_result, t.last_checkpoint = [], {}, None
             ctl.trials.append(t)
         ctl.exhausted = st["exhausted"]
 
     @classmethod
-    def restore(cls, path, trainable=None, **kw):
-        return cls(trainable, _restore_path=path, **kw)
+    def restore(cls, path, trainable=None, *, resume_config=None, resume_unfinished=True,
+                resume_errored=False, restart_errored=False, **kw):
+        if resume_config is None:
+            R = ResumeConfig.ResumeType
+            resume_config = ResumeConfig(
+                unfinished=R.RESUME if resume_unfinished else R.SKIP,
+                errored=R.RESTART if restart_errored else R.RESUME if resume_errored else R.SKIP)
+        t = cls(trainable, _restore_path=path, **kw)
+        t._resume_config = resume_config
+        return t
 
     @classmethod
     def can_restore(cls, path):
@@ -561,11 +578,41 @@ class Tuner:
         return self.fit()
 
 
+class ResumeConfig:
+    """What ``Tuner.restore`` does with finished / unfinished / errored trials (reference:
+    tune/execution/experiment_state.py ResumeConfig): RESUME from the latest checkpoint,
+    RESTART from scratch, or SKIP (keep the recorded outcome)."""
+
+    class ResumeType:
+        RESUME = "resume"
+        RESTART = "restart"
+        SKIP = "skip"
+
+    def __init__(self, finished: str = "skip", unfinished: str = "resume",
+                 errored: str = "skip"):
+        for v in (finished, unfinished, errored):
+            if v not in ("resume", "restart", "skip"):
+                raise ValueError(f"invalid ResumeType {v!r}")
+        self.finished, self.unfinished, self.errored = finished, unfinished, errored
+
+
 def run(run_or_experiment, *, config=None, num_samples=1, metric=None, mode=None,
         scheduler=None, search_alg=None, stop=None, resources_per_trial=None, name=None,
         storage_path=None, max_concurrent_trials=None, time_budget_s=None, **kw):
-    """Legacy tune.run API."""
-    t = run_or_experiment
+    """Legacy tune.run API (also accepts an Experiment or a registered trainable name)."""
+    from ray_amd.tune.registry import Experiment, resolve_trainable
+
+    if isinstance(run_or_experiment, Experiment):
+        e = run_or_experiment
+        return run(e.run, config=e.config, num_samples=e.num_samples, stop=e.stop,
+                   resources_per_trial=e.resources_per_trial, name=e.name,
+                   storage_path=e.storage_path, metric=metric, mode=mode, scheduler=scheduler,
+                   search_alg=search_alg, max_concurrent_trials=max_concurrent_trials,
+                   time_budget_s=time_budget_s)
+    for k in ("progress_reporter", "verbose", "callbacks", "sync_config", "raise_on_failed_trial",
+              "checkpoint_freq", "checkpoint_at_end", "keep_checkpoints_num"):
+        kw.pop(k, None)
+    t = resolve_trainable(run_or_experiment)
     if resources_per_trial:
         t = _with_res(t, resources_per_trial)
     tuner = Tuner(t, param_space=config or {},
