@@ -80,13 +80,16 @@ class NatureCNN(nn.Module):
             return linear_relu(x.permute(0, 2, 3, 1).flatten(1), fc.weight, fc.bias)
         if idx is not None:
             x = x.index_select(0, idx)
+        wdt = self.fc[0].weight.dtype
         if x.dtype == torch.uint8:
             if x.is_cuda:
                 from ray_amd.ops.functional import cast_scale_u8
 
-                x = cast_scale_u8(x).to(self.fc[0].weight.dtype)
-            else:
-                x = x.float().mul_(1.0 / 255.0)
+                x = cast_scale_u8(x).to(wdt)
+            else:  # CPU env runners: bf16 weights take bf16 frames (0..255 exact in bf16)
+                x = x.to(wdt if wdt == torch.bfloat16 else torch.float32).mul_(1.0 / 255.0)
+        elif x.dtype != wdt:
+            x = x.to(wdt)
         x = x.permute(0, 3, 1, 2)
         for conv, act in zip(convs, acts):
             x = act(conv(x))

@@ -89,14 +89,16 @@ class SingleAgentEnvRunner:
                 # bf16 channels-last weights: the conv encoder runs on the MFMA kernels and
                 # reads the uint8 frames directly (weights arrive fp32, cast on load)
                 self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
-        # CPU conv policies run under bf16 autocast (AVX-512 BF16 convolutions: measured
-        # 0.54 vs 0.70 ms per 5-frame Nature-CNN step on the MI355X host), matching the
-        # learner's bf16 compute; fp32 with env_runner_bf16=False
+        # CPU conv policies keep bf16 weights (AVX-512 BF16 convolutions and half the FC
+        # weight bytes per step), matching the learner's bf16 compute. Measured per 5-frame
+        # Nature-CNN step on the MI355X host (EPYC 9575F, scripts/cpu_infer_bf16_bench.py):
+        # fp32 0.68 ms, bf16 autocast 0.52 ms, bf16 weights 0.39 ms. fp32 with
+        # env_runner_bf16=False. Synced fp32 weights are cast on load (load_state_dict).
         self._cpu_bf16 = (self.device.type == "cpu" and self.module_kind == "pg"
                           and getattr(self.module, "is_image", False)
                           and config.get("env_runner_bf16", config.get("learner_bf16", True)))
         if self._cpu_bf16:
-            self.module.to(memory_format=torch.channels_last)
+            self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
         self.obs = []
         for i, e in enumerate(self.envs):
             o, _ = e.reset(seed=None if seed is None else seed * 1000 + worker_index * 100 + i)
@@ -127,7 +129,9 @@ class SingleAgentEnvRunner:
         self.weights_version = version
 
     def get_weights(self):
-        return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
+        # fp32 out (the runner may hold bf16 inference weights)
+        return {k: (v.detach().cpu().float() if v.is_floating_point() else v.detach().cpu())
+                for k, v in self.module.state_dict().items()}
 
     def ping(self):
         return self.worker_index
@@ -174,8 +178,7 @@ class SingleAgentEnvRunner:
                     a = at.float().cpu().numpy()
                     lp = lpt.float().cpu().numpy()
                 else:
-                    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=self._cpu_bf16):
-                        out = self.module.forward_inference(x)
+                    out = self.module.forward_inference(x)
                     di = out["action_dist_inputs"].float()
                     at, lpt = self.module.sample_actions(di, explore)
                     if dist_in is None:
