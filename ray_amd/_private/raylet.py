@@ -471,14 +471,42 @@ class Raylet:
                self.session_dir, "--raylet", self.addr, "--token", str(w.token), "--job",
                str(job), "--node-id", node]
         if node == self.node_hex:
-            w.proc = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
+            w.proc = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE)
             w.pid = w.proc.pid
+            self._tee_worker_logs(w)
         else:
             # the node agent forks it (its pid arrives with the worker's registration)
             self.send(self.node_recs[node]["conn"],
                       (P.REQ, 0, "spawn_worker", (w.token, cmd, env, cwd)))
         self.starting[w.token] = w
         return w
+
+    def _tee_worker_logs(self, w):
+        """worker-<token>-<pid>.out/.err under <session>/logs (state API list_logs /
+        get_log, CLI `logs`), each line also forwarded to this raylet's stdout / stderr
+        (the driver's terminal) as before."""
+        import sys
+        import threading
+
+        d = os.path.join(self.session_dir, "logs")
+        os.makedirs(d, exist_ok=True)
+        for pipe, ext, out in ((w.proc.stdout, "out", sys.stdout), (w.proc.stderr, "err",
+                                                                       sys.stderr)):
+            path = os.path.join(d, f"worker-{w.token}-{w.pid}.{ext}")
+
+            def pump(pipe=pipe, path=path, out=out):
+                with open(path, "ab", buffering=0) as f:
+                    for line in iter(pipe.readline, b""):
+                        f.write(line)
+                        try:
+                            out.buffer.write(line)
+                            out.flush()
+                        except (ValueError, OSError, AttributeError):
+                            pass
+                pipe.close()
+
+            threading.Thread(target=pump, daemon=True, name=f"log-{w.pid}-{ext}").start()
 
     def _take_idle(self, key):
         lst = self.idle.get(key)

@@ -315,6 +315,24 @@ def cmd_debug(a):
     return 0
 
 
+def cmd_logs(a):
+    """`logs` lists session log files; `logs <file>` / `logs --pid N` prints one."""
+    _connect(a.address)
+    from ray_amd.util import state
+
+    if a.filename is None and a.pid is None and a.actor_id is None:
+        for cat, files in state.list_logs(glob_filter=a.glob).items():
+            if files:
+                print(f"{cat}:")
+                for f in files:
+                    print(f"  {f}")
+        return 0
+    for ln in state.get_log(filename=a.filename, pid=a.pid, actor_id=a.actor_id, tail=a.tail,
+                            follow=a.follow, suffix="err" if a.err else "out"):
+        print(ln)
+    return 0
+
+
 def cmd_timeline(a):
     ray = _connect(a.address)
     out = a.output or f"/tmp/ray_amd-timeline-{time.strftime('%Y-%m-%d_%H-%M-%S')}.json"
@@ -478,6 +496,17 @@ def build_parser():
     s.add_argument("--address")
     s.add_argument("--limit", type=int, default=50)
     s.set_defaults(fn=cmd_memory)
+
+    s = sub.add_parser("logs", help="list / print worker log files")
+    s.add_argument("filename", nargs="?")
+    s.add_argument("--address")
+    s.add_argument("--pid", type=int)
+    s.add_argument("--actor-id")
+    s.add_argument("--glob")
+    s.add_argument("--tail", type=int, default=-1)
+    s.add_argument("--err", action="store_true")
+    s.add_argument("-f", "--follow", action="store_true")
+    s.set_defaults(fn=cmd_logs)
 
     s = sub.add_parser("debug", help="attach to a remote pdb breakpoint (util.pdb.set_trace)")
     s.add_argument("--address")

@@ -359,3 +359,67 @@ class StateApiClient:
     def summary(self, resource: str, **kw):
         return {"tasks": summarize_tasks, "actors": summarize_actors,
                 "objects": summarize_objects}[str(resource).lower()](self.address)
+
+
+
+# ---------------------------------------------------------------------------- logs
+def _logs_dir(address=None):
+    import os
+
+    from ray_amd._private import worker as _w
+
+    _core(address)
+    return os.path.join(_w.global_worker.session_dir, "logs")
+
+
+def list_logs(address=None, node_id=None, node_ip=None, glob_filter=None, timeout=None,
+              **kw) -> dict:
+    """{category: [file names]} of this node's session logs (reference: util/state/api.py
+    list_logs); categories: worker_out, worker_err, other."""
+    import fnmatch
+    import os
+
+    d = _logs_dir(address)
+    out = {"worker_out": [], "worker_err": [], "other": []}
+    for f in sorted(os.listdir(d)) if os.path.isdir(d) else []:
+        if glob_filter and not fnmatch.fnmatch(f, glob_filter):
+            continue
+        cat = "worker_out" if f.startswith("worker-") and f.endswith(".out") else \
+            "worker_err" if f.startswith("worker-") and f.endswith(".err") else "other"
+        out[cat].append(f)
+    return out
+
+
+def get_log(address=None, node_id=None, node_ip=None, filename=None, actor_id=None,
+            task_id=None, pid=None, follow=False, tail=-1, timeout=None, suffix="out",
+            **kw):
+    """Yield lines of one log file, chosen by ``filename``, or the worker ``pid`` (also
+    resolved from ``actor_id``); ``tail`` > 0 keeps only the last lines; ``follow`` keeps
+    yielding appended lines."""
+    import glob
+    import os
+    import time
+
+    d = _logs_dir(address)
+    if filename is None:
+        if pid is None and actor_id is not None:
+            a = get_actor(actor_id, address=address)
+            pid = getattr(a, "pid", None) if a is not None else None
+        if pid is None:
+            raise ValueError("get_log needs filename, pid or actor_id")
+        hits = glob.glob(os.path.join(d, f"worker-*-{pid}.{suffix}"))
+        if not hits:
+            raise FileNotFoundError(f"no {suffix} log for pid {pid} in {d}")
+        path = hits[0]
+    else:
+        path = os.path.join(d, filename)
+    with open(path, "r", errors="replace") as f:
+        lines = f.readlines()
+        for ln in (lines[-tail:] if tail and tail > 0 else lines):
+            yield ln.rstrip("\n")
+        while follow:
+            ln = f.readline()
+            if ln:
+                yield ln.rstrip("\n")
+            else:
+                time.sleep(0.2)
