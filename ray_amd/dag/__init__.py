@@ -195,6 +195,83 @@ class MultiOutputNode(DAGNode):
         return list(args[0])
 
 
+DAGNODE_TYPE_KEY = "__dag_node_type__"
+PARENT_CLASS_NODE_KEY = "__parent_class_node__"
+PREV_CLASS_METHOD_CALL_KEY = "__prev_class_method_call__"
+
+
+class DAGInputData:
+    """The positional + keyword input of one DAG execution (what an InputNode resolves to;
+    reference: dag/input_node.py DAGInputData)."""
+
+    def __init__(self, *args, **kwargs):
+        self._args = list(args)
+        self._kwargs = kwargs
+
+    def __getitem__(self, key):
+        return self._args[key] if isinstance(key, int) else self._kwargs[key]
+
+    def __getattr__(self, key):
+        try:
+            return self.__dict__["_kwargs"][key]
+        except KeyError:
+            raise AttributeError(key) from None
+
+
+def _label(n: DAGNode) -> str:
+    if isinstance(n, InputNode):
+        return "InputNode"
+    if isinstance(n, InputAttributeNode):
+        return f"Input[{getattr(n, '_key', '?')!r}]"
+    if isinstance(n, MultiOutputNode):
+        return "MultiOutputNode"
+    for attr in ("_body", "_func", "_method_name", "_cls"):
+        v = getattr(n, attr, None)
+        if v is not None:
+            return f"{type(n).__name__}({getattr(v, '__name__', v)})"
+    return type(n).__name__
+
+
+def to_dot(dag: DAGNode) -> str:
+    """Graphviz DOT text of a DAG (nodes by stable uuid, edges child -> parent)."""
+    seen, lines = {}, ["digraph dag {", "  rankdir=LR;"]
+    stack = [dag]
+    while stack:
+        n = stack.pop()
+        if n._stable_uuid in seen:
+            continue
+        seen[n._stable_uuid] = n
+        lines.append(f'  "{n._stable_uuid}" [label="{_label(n)}"];')
+        for c in n._children():
+            lines.append(f'  "{c._stable_uuid}" -> "{n._stable_uuid}";')
+            stack.append(c)
+    lines.append("}")
+    return "\n".join(lines)
+
+
+def plot(dag: DAGNode, to_file: str | None = None):
+    """Write the DAG as Graphviz DOT (``.dot``/``.gv``), or render it (``.png``/``.svg``/
+    ``.pdf``) through the ``dot`` binary when installed; returns the DOT text."""
+    import os
+    import shutil
+    import subprocess
+
+    text = to_dot(dag)
+    if to_file is None:
+        return text
+    ext = os.path.splitext(to_file)[1].lstrip(".").lower()
+    if ext in ("dot", "gv", ""):
+        with open(to_file, "w") as f:
+            f.write(text)
+        return text
+    exe = shutil.which("dot")
+    if exe is None:
+        raise ImportError(f"rendering .{ext} needs the graphviz 'dot' binary; write a .dot file "
+                          "instead")
+    subprocess.run([exe, f"-T{ext}", "-o", to_file], input=text.encode(), check=True)
+    return text
+
+
 def __getattr__(name):
     if name in ("CompiledDAG", "CompiledDAGRef", "CompiledDAGFuture"):
         from . import compiled_dag_node
@@ -205,4 +282,5 @@ def __getattr__(name):
 
 __all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode",
            "MultiOutputNode", "InputAttributeNode", "CompiledDAG",
-           "CompiledDAGRef", "CompiledDAGFuture"]
+           "CompiledDAGRef", "CompiledDAGFuture", "DAGInputData", "plot", "DAGNODE_TYPE_KEY",
+           "PARENT_CLASS_NODE_KEY", "PREV_CLASS_METHOD_CALL_KEY"]

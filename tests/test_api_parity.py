@@ -158,3 +158,23 @@ def test_file_datasinks(cluster, tmp_path):
     got = sorted(int(open(tmp_path / "blocks" / f).read()) for f in
                  os.listdir(tmp_path / "blocks"))
     assert got == [5, 5]
+
+
+def test_dag_plot_and_input_data(tmp_path):
+    from ray_amd.dag import DAGInputData, InputNode, plot
+
+    @ray.remote
+    def inc(x):
+        return x + 1
+
+    @ray.remote
+    def add(a, b):
+        return a + b
+
+    with InputNode() as inp:
+        dag = add.bind(inc.bind(inp), inc.bind(inp))
+    text = plot(dag, str(tmp_path / "g.dot"))
+    assert text.startswith("digraph") and text.count("->") == 4
+    assert open(tmp_path / "g.dot").read() == text
+    d = DAGInputData(1, 2, k=3)
+    assert d[0] == 1 and d["k"] == 3 and d.k == 3
