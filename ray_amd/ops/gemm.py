@@ -23,9 +23,10 @@ from ._lib import check, lib, ptr, stream_ptr
 
 _EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "dgelu": 3}
 
-# RAY_AMD_GEMM=hip|lt: the projections' forward / input-gradient GEMMs on this kernel
-# (default) or on hipBLASLt via torch (comparison)
-MODE = os.environ.get("RAY_AMD_GEMM", "hip")
+# Status: correct (tests/test_kernels_gpu.py::test_gemm_nt_matches_fp32) but measured at
+# 0.43-0.77x hipBLASLt on the GPT-2 shapes (profiles/r2/hip_gemm_v*.log), so the model's
+# linear layers stay on hipBLASLt; this module is the API for callers that want the fused
+# epilogues (scripts/hip_gemm_bench.py). RAY_AMD_GEMM_GRID caps the persistent grid.
 GRID_CAP = int(os.environ.get("RAY_AMD_GEMM_GRID", "0"))
 
 
