@@ -54,7 +54,7 @@ _loads = P.loads
 
 class _Owned:
     __slots__ = ("ready", "inline", "in_store", "callbacks", "borrowers", "contained",
-                 "release_when_ready", "task_id", "size", "node", "recon")
+                 "release_when_ready", "task_id", "size", "node", "recon", "lineage_refs")
 
     def __init__(self, task_id=None):
         self.ready = False
@@ -68,11 +68,18 @@ class _Owned:
         self.size = 0
         self.node = None
         self.recon = 0  # times this object was reconstructed from lineage
+        # lineage entries (finished task specs) that list this object as an argument: the
+        # VALUE is freed with the last in-scope ref, but this metadata is kept so the
+        # object can be re-created if a dependent's reconstruction needs it
+        self.lineage_refs = 0
 
 
-# Lineage (creating-task specs of stored task returns) kept per owner; the oldest specs
-# are dropped beyond this many (their objects then fail with LineageEvicted if lost).
+# Lineage (creating-task specs of stored task returns) kept per owner. A lineage entry
+# holds only argument ids, never argument values (reference: reference_count.cc lineage
+# ref counts). The oldest entries are dropped beyond either bound (their objects then
+# fail with LineageEvicted if lost); reference default max_lineage_bytes = 1 GiB.
 LINEAGE_MAX = 20000
+LINEAGE_MAX_BYTES = 1 << 30
 
 
 class _CopyLost(Exception):
@@ -189,7 +196,10 @@ class CoreWorker:
         # tid -> spec of FINISHED normal tasks whose stored returns are still owned: the
         # lineage re-executed when a primary copy is lost (object_recovery_manager.cc)
         self.lineage: "collections.OrderedDict[bytes, dict]" = collections.OrderedDict()
+        self.lineage_bytes = 0
         self.lineage_evicted: set = set()
+        # oid -> metadata of freed objects still named as arguments by lineage entries
+        self.lineage_objs: dict[bytes, _Owned] = {}
         self.task_lease: dict[bytes, _Lease] = {}
         self.actors: dict[bytes, _ActorConn] = {}
         self.actor_handle_counts: collections.Counter = collections.Counter()
@@ -484,16 +494,62 @@ class CoreWorker:
             del self.owned[oid]
             self._ready_owned.discard(oid)
             contained = o.contained
+            o.contained = None
             in_store = o.in_store
             node = o.node
-            spec = self.lineage.get(o.task_id) if o.task_id is not None else None
-            if spec is not None and not any(
-                    object_id_for_return(o.task_id, i + 1) in self.owned
-                    for i in range(max(spec["nret"], 0))):
-                del self.lineage[o.task_id]  # releases the args it pinned
+            tid = o.task_id
+            if o.lineage_refs > 0 and tid is not None and tid in self.lineage:
+                # a dependent's lineage names it: keep the metadata, free the value
+                o.ready = False
+                o.inline = None
+                o.in_store = False
+                o.node = None
+                self.lineage_objs[oid] = o
+            else:
+                self._drop_lineage_if_unused(tid)
         if in_store:
             self._delete_stored(oid, node)
         del contained
+
+    def _lineage_in_use(self, tid) -> bool:
+        spec = self.lineage.get(tid)
+        if spec is None:
+            return False
+        for i in range(max(spec["nret"], 0)):
+            r = object_id_for_return(tid, i + 1)
+            if r in self.owned or r in self.lineage_objs:
+                return True
+        return False
+
+    def _drop_lineage_if_unused(self, tid):
+        """(lock held) Delete the lineage entry of `tid` once none of its returns is owned
+        or named by another lineage entry; cascades through the argument chain."""
+        work = [tid]
+        while work:
+            t = work.pop()
+            if t is None or t not in self.lineage or self._lineage_in_use(t):
+                continue
+            spec = self.lineage.pop(t)
+            work.extend(self._release_lineage_args(spec))
+
+    def _release_lineage_args(self, spec):
+        """(lock held) Drop the lineage refs a spec holds on its arguments. Returns the task
+        ids whose lineage may have become unused."""
+        self.lineage_bytes -= spec.pop("_lbytes", 0)
+        out = []
+        for a in spec.pop("_largs", ()):
+            o = self.owned.get(a)
+            if o is None:
+                o = self.lineage_objs.get(a)
+                if o is None:
+                    continue
+                o.lineage_refs -= 1
+                if o.lineage_refs <= 0:
+                    del self.lineage_objs[a]
+                    out.append(o.task_id)
+            else:
+                o.lineage_refs -= 1
+        return out
 
     def _delete_stored(self, oid, node):
         """Free a primary copy: in our node's store, or via its node's agent."""
@@ -807,11 +863,15 @@ class CoreWorker:
         is (or will become) available, else the error to raise."""
         with self.lock:
             o = self.owned.get(oid)
+            revived = False
             if o is None:
-                return ObjectLostError(oid.hex())
-            if not o.ready:
+                o = self.lineage_objs.get(oid)
+                if o is None:
+                    return ObjectLostError(oid.hex())
+                revived = True  # a freed argument a dependent's re-execution needs
+            elif not o.ready:
                 return None  # a reconstruction is already running
-            if o.inline is not None or (o.node or None) != (failed_node or None):
+            elif o.inline is not None or (o.node or None) != (failed_node or None):
                 return None  # already recovered (another caller saw the loss first)
             tid = o.task_id
             if tid is None:  # ray.put objects have no lineage (reference semantics)
@@ -828,6 +888,11 @@ class CoreWorker:
             if spec["retries"] > 0:
                 spec["retries"] -= 1
             spec["attempt"] += 1
+            if revived:
+                del self.lineage_objs[oid]
+                self.owned[oid] = o
+            # the spec leaves the lineage table while it re-runs but keeps its argument
+            # lineage refs (_largs); _complete puts it back
             del self.lineage[tid]
             self.task_specs[tid] = spec
             for i in range(spec["nret"]):
@@ -841,17 +906,25 @@ class CoreWorker:
                     r.recon += 1
             args = [a for a, owner, inline in spec["args"][1]
                     if owner == self.addr and inline is None]
-        # lost arguments are re-created first; dependency resolution waits for them
+        # lost or freed arguments are re-created first (recursively through their own
+        # lineage); dependency resolution waits for them
+        from ray_amd.object_ref import ObjectRef
+
+        holders = []
         for a in args:
             with self.lock:
                 ao = self.owned.get(a)
+                freed = ao is None and a in self.lineage_objs
                 check = ao is not None and ao.ready and ao.in_store
                 anode = ao.node if ao is not None else None
-            if check and not self._copy_available(a, anode):
+            if freed or (check and not self._copy_available(a, anode)):
                 err = self._reconstruct(a, anode)
                 if err is not None:
                     self._fail_task(spec, err)
                     return None
+            if a in self.owned:  # pinned until the re-run completes
+                holders.append(ObjectRef(a, self.addr, _cw_obj=self))
+        spec["_holders"] = holders
         self.task_events.append((tid, spec.get("name"), time.time(), None, None, None,
                                  "PENDING_ARGS_AVAIL", P.NORMAL_TASK, self.job_id,
                                  spec["attempt"], None))
@@ -1441,20 +1514,50 @@ class CoreWorker:
             else:
                 stored = True
                 self._mark_ready(oid, in_store=True, contained=pins, size=payload, node=node)
-        if stored and spec["type"] == P.NORMAL_TASK and not spec.get("dynamic"):
-            # keep the spec (and the arg refs it holds) as lineage while its stored
-            # returns are referenced; inline returns can never be lost
-            with self.lock:
-                if any(object_id_for_return(tid, i + 1) in self.owned
-                       for i in range(spec["nret"])):
-                    self.lineage[tid] = spec
-                    self.lineage.move_to_end(tid)
-                    while len(self.lineage) > LINEAGE_MAX:
-                        old_tid, old = self.lineage.popitem(last=False)
-                        old.pop("_holders", None)
-                        self.lineage_evicted.add(old_tid)
-            return
-        spec.pop("_holders", None)
+        with self.lock:
+            if (stored and spec["type"] == P.NORMAL_TASK and not spec.get("dynamic")
+                    and any(object_id_for_return(tid, i + 1) in self.owned
+                            for i in range(spec["nret"]))):
+                # keep the spec as lineage while its stored returns are referenced
+                # (inline returns can never be lost). It names its stored arguments by
+                # id only: their values are freed with their last in-scope ref.
+                self._add_lineage(tid, spec)
+            elif "_largs" in spec:  # a re-run whose lineage is no longer needed
+                for t in self._release_lineage_args(spec):
+                    self._drop_lineage_if_unused(t)
+        holders = spec.pop("_holders", None)
+        del holders  # may free argument values (outside the lock's critical section)
+
+    def _add_lineage(self, tid, spec):
+        """(lock held) Record a finished task's spec as lineage; bounded by count and bytes."""
+        if "_largs" not in spec:  # first completion (a re-run keeps its refs)
+            largs = []
+            nbytes = 256
+            blob = spec["args"][0]
+            if isinstance(blob, (bytes, bytearray, memoryview)):
+                nbytes += len(blob)
+            for a, owner, inline in spec["args"][1]:
+                if inline is not None:
+                    nbytes += len(inline)
+                elif owner == self.addr:
+                    o = self.owned.get(a) or self.lineage_objs.get(a)
+                    if o is not None:
+                        o.lineage_refs += 1
+                        largs.append(a)
+            spec["_largs"] = largs
+            spec["_lbytes"] = nbytes
+            self.lineage_bytes += nbytes
+        self.lineage[tid] = spec
+        self.lineage.move_to_end(tid)
+        while len(self.lineage) > 1 and (len(self.lineage) > LINEAGE_MAX
+                                         or self.lineage_bytes > LINEAGE_MAX_BYTES):
+            old_tid, old = self.lineage.popitem(last=False)
+            self.lineage_evicted.add(old_tid)
+            for t in self._release_lineage_args(old):
+                self._drop_lineage_if_unused(t)
+            # freed returns of the evicted task can no longer be re-created
+            for i in range(max(old["nret"], 0)):
+                self.lineage_objs.pop(object_id_for_return(old_tid, i + 1), None)
 
     def _fail_task(self, spec, exc):
         sobj = ser.serialize_error(exc)
@@ -1478,6 +1581,10 @@ class CoreWorker:
         n = spec["nret"] if spec["type"] != P.ACTOR_CREATION_TASK else 0
         for i in range(n):
             self._mark_ready(object_id_for_return(tid, i + 1), inline=data)
+        if "_largs" in spec:  # a failed re-run: its lineage is gone
+            with self.lock:
+                for t in self._release_lineage_args(spec):
+                    self._drop_lineage_if_unused(t)
         spec.pop("_holders", None)
 
     def _on_worker_lost(self, addr):
@@ -1497,14 +1604,19 @@ class CoreWorker:
         def with_cause(ok, cause, lost=lost):
             # the raylet tells us whether IT killed the worker (memory monitor)
             oom = ok and isinstance(cause, str) and cause.startswith("oom:")
+            retry_ok = True
+            msg = ""
+            if oom:
+                _, flag, msg = cause.split(":", 2)
+                retry_ok = flag == "retry"  # the kill policy's verdict
             for spec in lost:
-                if spec["retries"] != 0:
+                if spec["retries"] != 0 and retry_ok:
                     if spec["retries"] > 0:
                         spec["retries"] -= 1
                     spec["attempt"] += 1
                     self._schedule(spec)
                 elif oom:
-                    self._fail_task(spec, OutOfMemoryError(cause[4:]))
+                    self._fail_task(spec, OutOfMemoryError(msg))
                 else:
                     self._fail_task(spec, WorkerCrashedError())
 

@@ -496,14 +496,30 @@ class Raylet:
             path = os.path.join(d, f"worker-{w.token}-{w.pid}.{ext}")
 
             def pump(pipe=pipe, path=path, out=out):
-                with open(path, "ab", buffering=0) as f:
-                    for line in iter(pipe.readline, b""):
-                        f.write(line)
+                # never stop draining the pipe: a worker whose pipe fills (64 KB) blocks on
+                # its next print. A failed file write (ENOSPC, ...) drops the file copy
+                # and keeps forwarding to the terminal.
+                try:
+                    f = open(path, "ab", buffering=0)
+                except OSError:
+                    f = None
+                for line in iter(pipe.readline, b""):
+                    if f is not None:
                         try:
-                            out.buffer.write(line)
-                            out.flush()
-                        except (ValueError, OSError, AttributeError):
-                            pass
+                            f.write(line)
+                        except (ValueError, OSError):
+                            try:
+                                f.close()
+                            except OSError:
+                                pass
+                            f = None
+                    try:
+                        out.buffer.write(line)
+                        out.flush()
+                    except (ValueError, OSError, AttributeError):
+                        pass
+                if f is not None:
+                    f.close()
                 pipe.close()
 
             threading.Thread(target=pump, daemon=True, name=f"log-{w.pid}-{ext}").start()
@@ -734,7 +750,8 @@ class Raylet:
             cause = getattr(w, "death_cause", None)
             a = self.actors.get(w.actor_id)
             if a is not None and cause and cause.startswith("oom:"):
-                a._oom_cause = "The actor died because its node ran out of memory. " + cause[4:]
+                a._oom_cause = ("The actor died because its node ran out of memory. "
+                                + cause.split(":", 2)[2])
             self._on_actor_worker_died(w.actor_id, prev_state)
         self.dirty = True
 
@@ -828,16 +845,20 @@ class Raylet:
                f"'{self.kill_policy}' choice. Set RAY_memory_usage_threshold / "
                f"RAY_memory_monitor_refresh_ms=0 to tune or disable.")
         print(f"[ray_amd] memory monitor: {msg}", file=sys.stderr, flush=True)
-        self.death_causes[w.addr] = "oom:" + msg
+        # the policy's retry verdict travels with the cause: a lease alone in its owner
+        # group is failed with OutOfMemoryError instead of being re-killed on every retry
+        cause = "oom:" + ("retry:" if retry else "noretry:") + msg
+        self.death_causes[w.addr] = cause
         while len(self.death_causes) > 1000:
             self.death_causes.popitem(last=False)
-        w.death_cause = "oom:" + msg
+        w.death_cause = cause
         self.oom_kills += 1
         self._oom_victim = (w, now + 5.0)
         self._kill_worker(w)
 
     def rpc_death_cause(self, conn, rid, addr):
-        """Why a worker died, if the raylet killed it (e.g. "oom:<message>")."""
+        """Why a worker died, if the raylet killed it ("oom:retry:<message>" or
+        "oom:noretry:<message>")."""
         self.reply(conn, rid, True, self.death_causes.get(addr))
 
     def tick(self):

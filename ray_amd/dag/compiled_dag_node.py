@@ -433,7 +433,13 @@ class CompiledDAG:
                 try:
                     kv = ch.read_raw(r, timeout=_SLICE)
                 except RayChannelTimeoutError:
+                    # the producer may be blocked writing ANOTHER output channel that
+                    # holds an unread value: buffer every ready output so it can go on
+                    # (refs may be resolved in any order)
+                    self._drain()
                     self._check_alive()
+                    if (i, j) in self._results:
+                        break
                     if deadline is not None and time.monotonic() > deadline:
                         raise RayChannelTimeoutError(
                             f"result of execution {i} not ready after {timeout}s") from None

@@ -83,7 +83,12 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True,
         flat = FlatParams(model, dtype=params[0].dtype, grad_dtype=gd)
         ddp = FlatDDP(flat, bucket_mb=kw.get("bucket_mb", 32.0))
         return FlatPreparedModel(model, flat, ddp)
-    return _maybe_autocast(_wrap_parallel(model, dev, world, parallel_strategy, kw), dev)
+    if _AMP["enabled"]:
+        # patch forward in place BEFORE the parallel wrapper (reference: train_loop_utils
+        # prepare_model with amp): no wrapper module, so state_dict keys are identical with
+        # and without AMP and checkpoints load into the plain model
+        model.forward = _AutocastForward(model, dev.type, _AMP["dtype"])
+    return _wrap_parallel(model, dev, world, parallel_strategy, kw)
 
 
 def _wrap_parallel(model, dev, world, parallel_strategy, kw):
@@ -100,12 +105,6 @@ def _wrap_parallel(model, dev, world, parallel_strategy, kw):
 
         return FSDP(model, device_id=dev if dev.type == "cuda" else None, **kw)
     return model
-
-
-def _maybe_autocast(model, dev):
-    if not _AMP["enabled"]:
-        return model
-    return _AutocastModule(model, dev.type, _AMP["dtype"])
 
 
 class _DeviceLoader:
@@ -175,24 +174,19 @@ def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_devi
 _AMP = {"enabled": False, "dtype": torch.bfloat16, "scaler": None}
 
 
-class _AutocastModule(torch.nn.Module):
-    """Runs the wrapped (possibly DDP) module's forward under torch.autocast."""
+class _AutocastForward:
+    """A module's forward, run under torch.autocast; installed as the instance attribute
+    ``forward`` so nn.Module.__call__ (and DDP/FSDP around it) pick it up. Holds the module
+    rather than a bound method, so the patched module still pickles."""
 
     def __init__(self, module, device_type, dtype):
-        super().__init__()
         self.module = module
-        self._dev = device_type
-        self._dtype = dtype
+        self.device_type = device_type
+        self.dtype = dtype
 
-    def forward(self, *a, **k):
-        with torch.autocast(self._dev, dtype=self._dtype):
-            return self.module(*a, **k)
-
-    def __getattr__(self, name):
-        try:
-            return super().__getattr__(name)
-        except AttributeError:
-            return getattr(super().__getattr__("module"), name)
+    def __call__(self, *a, **k):
+        with torch.autocast(self.device_type, dtype=self.dtype):
+            return type(self.module).forward(self.module, *a, **k)
 
 
 class _AmpOptimizer:

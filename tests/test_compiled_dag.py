@@ -135,6 +135,25 @@ def test_fan_out_fan_in_multi_output_and_input_attributes(cluster):
         cdag.teardown()
 
 
+def test_multi_output_resolved_out_of_order(cluster):
+    """The actor writes Y before X; getting execution 1's X first must not hang while Y's
+    channel still holds execution 0's unread value (every ready output is buffered)."""
+    a = Stage.remote(1)
+    with InputNode() as inp:
+        y = a.fwd.bind(inp)
+        x = a.fwd.bind(y)
+        dag = MultiOutputNode([x, y])
+    cdag = dag.experimental_compile(_get_timeout=30)
+    try:
+        refs = [cdag.execute(i) for i in range(2)]
+        assert ray.get(refs[1][0]) == 3  # X of execution 1 first
+        assert ray.get(refs[0][1]) == 1  # then Y of execution 0
+        assert ray.get(refs[1][1]) == 2
+        assert ray.get(refs[0][0]) == 2
+    finally:
+        cdag.teardown()
+
+
 def test_same_actor_multiple_nodes_and_capacity(cluster):
     a = Stage.remote(1)
     with InputNode() as inp:

@@ -72,8 +72,22 @@ def pressured(tmp_path, monkeypatch):
     ray.shutdown()
 
 
-def test_oom_kill_then_retry_succeeds(pressured):
-    cg = str(pressured)
+@pytest.fixture
+def pressured_fifo(tmp_path, monkeypatch):
+    monkeypatch.setenv("RAY_worker_killing_policy", "retriable_fifo")
+    _cg(tmp_path, 1 << 30, 100 << 20)
+    monkeypatch.setenv("RAY_AMD_CGROUP_ROOT", str(tmp_path))
+    monkeypatch.setenv("RAY_memory_usage_threshold", "0.5")
+    monkeypatch.setenv("RAY_memory_monitor_refresh_ms", "50")
+    ray.init(num_cpus=2)
+    yield tmp_path
+    ray.shutdown()
+
+
+def test_oom_kill_then_retry_succeeds(pressured_fifo):
+    """retriable_fifo retries a killed retriable task (reference
+    worker_killing_policy_retriable_fifo.cc: should_retry = the victim is retriable)."""
+    cg = str(pressured_fifo)
 
     @ray.remote(max_retries=2)
     def hog(cg):
@@ -89,6 +103,29 @@ def test_oom_kill_then_retry_succeeds(pressured):
         return "ok after OOM retry"
 
     assert ray.get(hog.remote(cg), timeout=60) == "ok after OOM retry"
+
+
+def test_oom_kill_lone_task_not_retried_by_group_by_owner(pressured):
+    """group_by_owner does not retry the last task of its owner group (reference
+    worker_killing_policy_group_by_owner.cc:87): the task fails with OutOfMemoryError even
+    though it has retries left, instead of being re-killed until they run out."""
+    cg = str(pressured)
+
+    @ray.remote(max_retries=3)
+    def hog(cg):
+        marker = os.path.join(cg, "attempts")
+        with open(marker, "a") as f:
+            f.write("x")
+        with open(os.path.join(cg, "memory.current"), "w") as f:
+            f.write(f"{900 << 20}\n")
+        time.sleep(60)
+
+    with pytest.raises(OutOfMemoryError, match="low on memory"):
+        ray.get(hog.remote(cg), timeout=60)
+    with open(os.path.join(cg, "attempts")) as f:
+        assert f.read() == "x"  # killed once, not retried
+    with open(os.path.join(cg, "memory.current"), "w") as f:
+        f.write(f"{100 << 20}\n")
 
 
 def test_oom_kill_non_retriable_raises_out_of_memory(pressured):

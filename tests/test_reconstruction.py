@@ -114,3 +114,56 @@ def test_node_death_loses_primary_copy_then_reconstructs():
     finally:
         ray.shutdown()
         c.shutdown()
+
+
+def test_lineage_does_not_pin_argument_values(local):
+    """A lineage entry names its arguments by id only (reference reference_count.cc:
+    lineage ref counts): after `b = f.remote(a); del a`, a's stored copy is freed while b is
+    alive, and a lost b still reconstructs by re-creating a first."""
+    import time
+
+    cw = W.global_worker.core
+    a = big.remote(700_000, 4.0)
+    b = add_one.remote(a)
+    assert float(ray.get(b)[0]) == 5.0
+    aid = a._id
+    assert cw.store.contains(aid)
+    del a
+    deadline = time.time() + 10
+    while cw.store.contains(aid) and time.time() < deadline:
+        time.sleep(0.02)
+    assert not cw.store.contains(aid)  # the value is gone...
+    assert aid in cw.lineage_objs  # ...its metadata is kept for b's lineage
+    _lose(b)
+    assert float(ray.get(b)[-1]) == 5.0  # b re-runs after a is re-created
+    deadline = time.time() + 10
+    while cw.store.contains(aid) and time.time() < deadline:
+        time.sleep(0.02)
+    assert not cw.store.contains(aid)  # re-created a is freed again after the re-run
+    bid = b._id
+    del b
+    deadline = time.time() + 10
+    while (cw.lineage_objs or cw.lineage) and time.time() < deadline:
+        time.sleep(0.02)
+    assert aid not in cw.lineage_objs and not cw.lineage  # whole chain released
+    assert not cw.store.contains(bid)
+
+
+def test_iterative_chain_frees_intermediates(local):
+    """x = f.remote(x) in a loop keeps only the live head's value in the store."""
+    import time
+
+    cw = W.global_worker.core
+    x = big.remote(300_000, 0.0)
+    ids = [x._id]
+    for _ in range(6):
+        x = add_one.remote(x)
+        ids.append(x._id)
+    assert float(ray.get(x)[0]) == 6.0
+    deadline = time.time() + 10
+    while any(cw.store.contains(i) for i in ids[:-1]) and time.time() < deadline:
+        time.sleep(0.02)
+    assert not any(cw.store.contains(i) for i in ids[:-1])
+    assert cw.store.contains(ids[-1])
+    _lose(x)
+    assert float(ray.get(x)[0]) == 6.0  # the whole chain re-runs from lineage

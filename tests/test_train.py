@@ -180,3 +180,32 @@ def test_accelerate_amp_bf16_and_fp16_cpu():
         tlu.accelerate(amp=False)
     m2 = tlu.prepare_model(torch.nn.Linear(8, 4), move_to_device=False)
     assert m2(torch.randn(2, 8)).dtype == torch.float32
+
+
+def test_accelerate_amp_keeps_state_dict_keys():
+    """An AMP-prepared model has the same state_dict keys as the plain model (forward is
+    patched in place, no wrapper prefix), its checkpoint loads into a plain model, and the
+    patched model pickles."""
+    import io
+
+    import torch
+
+    from ray_amd.train.torch import train_loop_utils as tlu
+
+    def net():
+        return torch.nn.Sequential(torch.nn.Linear(8, 4), torch.nn.ReLU(), torch.nn.Linear(4, 2))
+
+    plain = tlu.prepare_model(net(), move_to_device=False)
+    try:
+        tlu.accelerate(amp=True)
+        amp = tlu.prepare_model(net(), move_to_device=False)
+    finally:
+        tlu.accelerate(amp=False)
+    assert list(amp.state_dict()) == list(plain.state_dict()) == list(net().state_dict())
+    plain.load_state_dict(amp.state_dict())
+    assert amp(torch.randn(2, 8)).dtype == torch.bfloat16
+    buf = io.BytesIO()
+    torch.save(amp, buf)
+    buf.seek(0)
+    again = torch.load(buf, weights_only=False)  # our own file
+    assert again(torch.randn(2, 8)).dtype == torch.bfloat16
