@@ -290,12 +290,17 @@ def _splitk(M: int, N: int, K: int) -> int:
     batched kernels fill the 256 CUs only with many (N/256)*(K/256)*S tiles. Slices
     stay >= 2048 tokens so each batch GEMM keeps a long K loop."""
     S = 1
-    while S < _WGRAD_MAX_SPLITS and M % (2 * S) == 0 and M // (2 * S) >= 2048:
+    while (S < _WGRAD_MAX_SPLITS and M % (2 * S) == 0 and M // (2 * S) >= 2048
+           and 2 * S * N * K * 4 <= _WGRAD_PART_BYTES):
         S *= 2
     return S
 
 
 _WGRAD_MAX_SPLITS = int(os.environ.get("RAY_AMD_WGRAD_SPLITS", "16"))
+# cap on the fp32 split-K partials of one weight gradient: every partial byte is written by
+# the GEMM and read back by ra_splitk_accum while the main stream's memory-bound backward
+# kernels compete for HBM
+_WGRAD_PART_BYTES = int(float(os.environ.get("RAY_AMD_WGRAD_PART_MB", "4096")) * (1 << 20))
 
 
 def _wgrad_partials(dy2, x2, S, M, N, K):
@@ -506,6 +511,62 @@ class _CrossEntropy(torch.autograd.Function):
         return dl.view(ctx.shape), None, None, None
 
 
+_xent_streams: dict = {}
+
+# RAY_AMD_LMHEAD_PIPE=1: the LM head's three GEMMs per chunk stay in order on the current
+# stream while each chunk's softmax-xent pass runs on its own stream beside the next GEMMs.
+# Measured on MI355X (profiles/r3/lmhead_pipe.md): no gain over the default layout (dW GEMMs
+# on the wgrad side stream) — beside the K = 768 GEMMs, which move 1.5-3 TB/s themselves,
+# the xent pass stretches from 0.33 to ~2.0 ms and the chunk stays at ~2.0 ms either way.
+_LMHEAD_PIPE = os.environ.get("RAY_AMD_LMHEAD_PIPE", "0") == "1"
+
+
+def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
+    """Chunked LM head + CE, software-pipelined over two streams:
+
+        main:  L0 L1 | dh0 dW0 | L2 | dh1 dW1 | L3 ...      (GEMMs, issue order = data order)
+        xent:     X0 |   X1    |    X2  ...                 (X_i after L_i, before dh_i/dW_i)
+
+    X_{i+1} runs while dh_i / dW_i run. Two logits buffers suffice: L_{i+2} is issued on the
+    main stream after dh_i / dW_i, the last readers of its buffer."""
+    dev = h2.device
+    N = h2.shape[0]
+    xs = _xent_streams.get(dev)
+    if xs is None:
+        xs = _xent_streams[dev] = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    bufs = [torch.empty((ch, Vp), device=dev, dtype=h2.dtype) for _ in range(2)]
+    starts = list(range(0, N, ch))
+    done_x = [None] * len(starts)
+
+    def logits(i):
+        s0 = starts[i]
+        e = min(N, s0 + ch)
+        lg = bufs[i % 2][: e - s0]
+        torch.mm(h2[s0:e], wt, out=lg)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        xs.wait_event(ev)
+        with torch.cuda.stream(xs):
+            check(L.ra_xent_fused(ptr(lg), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
+                                  e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
+            ex = torch.cuda.Event()
+            ex.record(xs)
+        done_x[i] = ex
+
+    logits(0)
+    for i, s0 in enumerate(starts):
+        e = min(N, s0 + ch)
+        if i + 1 < len(starts):
+            logits(i + 1)
+        main.wait_event(done_x[i])
+        lg = bufs[i % 2][: e - s0]
+        if dh is not None:
+            torch.mm(lg, w, out=dh[s0:e])
+        if dw is not None:
+            _lm_head_dw(lg, h2[s0:e], dw, i == 0)
+
+
 def _lm_head_dw(lg, h2s, dw, first):
     if _WGRAD_LT:
         from . import lt
@@ -543,6 +604,12 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         ch = max(1, min(chunk, N))
         L = _lib.lib()
         wt = w.t()
+        if _LMHEAD_PIPE and h.is_cuda and N > ch:
+            _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp,
+                               ignore_index)
+            ctx.save_for_backward(dh, dw)
+            ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
+            return loss_rows.sum() * inv[0]
         # side stream: each chunk's dW GEMM (compute-bound) overlaps the next chunk's
         # memory-bound softmax-xent; two logits buffers alternate between the streams
         side = _side_stream(dev) if (_WGRAD_STREAM and dw is not None and h.is_cuda) else None

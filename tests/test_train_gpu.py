@@ -20,7 +20,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,C,V,Vp,chunk", [(4096, 128, 1000, 1024, 1000),
-                                            (2048, 768, 50257, 50304, 8192)])
+                                            (2048, 768, 50257, 50304, 8192),
+                                            (12388, 768, 50257, 50304, 4096)])
 def test_lm_head_cross_entropy(cuda_device, N, C, V, Vp, chunk):
     """Chunked fused LM head + CE vs fp32 logits/log_softmax/nll (loss and both grads)."""
     torch.manual_seed(21)
