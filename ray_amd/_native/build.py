@@ -26,6 +26,7 @@ BUILD_DIR = os.path.join(HERE, "build")
 HIP_LIB = os.path.join(HERE, "libray_amd_hip.so")
 ARCH = os.environ.get("RAY_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+AGPR_ACC_SOURCES = {"gemm4w.hip"}
 
 
 def _newer(target: str, sources: list[str]) -> bool:
@@ -57,9 +58,11 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         s, o = so
         # VGPR-form MFMA: accumulators live in arch VGPRs, so the softmax / epilogue VALU
         # work on them needs no v_accvgpr_read/write round trips (gfx950 unified RF)
+        # ...except the 4-wave GEMM, whose 256 accumulators per lane must sit in AGPRs
+        vgpr_form = [] if os.path.basename(s) in AGPR_ACC_SOURCES else \
+            ["-mllvm", "-amdgpu-mfma-vgpr-form"]
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-              "-munsafe-fp-atomics", "-Wno-unused-result", "-mllvm", "-amdgpu-mfma-vgpr-form",
-              "-c", s, "-o", o])
+              "-munsafe-fp-atomics", "-Wno-unused-result"] + vgpr_form + ["-c", s, "-o", o])
 
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

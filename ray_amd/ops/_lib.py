@@ -110,6 +110,9 @@ _SIGS = {
     "ra_gemm_nt": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
                    c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_int,
                    c_void_p],
+    "ra_gemm4w_nt": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
+                     c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int,
+                     c_int, c_void_p],
     "ra_gemm_dgelu_work": [c_int, c_int],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],

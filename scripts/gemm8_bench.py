@@ -17,6 +17,15 @@ import torch  # noqa: E402
 from ray_amd.ops import gemm  # noqa: E402
 from ray_amd.ops._lib import lib  # noqa: E402
 
+_L = None
+
+
+def set_variant(v):
+    """v < 4: gemm.hip schedule ra_knobs[5] = v; v == 4: the 4-wave gemm4w.hip kernel."""
+    gemm.set_four_wave(v == 4)
+    if v < 4:
+        _L.ra_set_knob(5, v)
+
 SHAPES = [  # name, M, N, K
     ("sq4096", 4096, 4096, 4096),
     ("sq8192", 8192, 8192, 8192),
@@ -59,12 +68,13 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    L = lib()
+    global _L
+    L = _L = lib()
     for M, N, K in RAGGED:
         a = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         b = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
         for v in variants:
-            L.ra_set_knob(5, v)
+            set_variant(v)
             e = rel_err(gemm.gemm_nt(a, b), a, b)
             print(json.dumps({"ragged": [M, N, K], "variant": v, "max_rel_err": round(e, 5)}),
                   flush=True)
@@ -77,13 +87,13 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         errs = {}
         for v in variants:
-            L.ra_set_knob(5, v)
+            set_variant(v)
             errs[v] = round(rel_err(gemm.gemm_nt(a, b), a, b), 5) if M * N <= 65536 * 3072 else None
         times = {v: [] for v in variants}
         t_lt = []
         for _ in range(args.rounds):
             for v in variants:
-                L.ra_set_knob(5, v)
+                set_variant(v)
                 times[v].append(timeit(lambda: gemm.gemm_nt(a, b, out=c), args.iters))
             t_lt.append(timeit(lambda: torch.mm(a, b.t(), out=c), args.iters))
         fl = 2.0 * M * N * K
