@@ -23,10 +23,15 @@ from ray_amd._private.worker import (LOCAL_MODE, SCRIPT_MODE, WORKER_MODE,  # no
                                      get_actor, get_gpu_ids, init, is_initialized, kill, method,
                                      nodes, put, shutdown, timeline, wait)
 from ray_amd.actor import ActorClass, ActorHandle  # noqa: F401
-from ray_amd.object_ref import ObjectRef, ObjectRefGenerator  # noqa: F401
+from ray_amd.object_ref import (DynamicObjectRefGenerator, ObjectRef,  # noqa: F401
+                                ObjectRefGenerator)
+from ray_amd._private.ids import (ActorClassID, ActorID, FunctionID, JobID,  # noqa: F401
+                                  NodeID, ObjectID, PlacementGroupID, TaskID, UniqueID,
+                                  WorkerID)
 from ray_amd.remote_function import RemoteFunction  # noqa: F401
 from ray_amd.runtime_context import get_runtime_context  # noqa: F401
 from ray_amd import exceptions  # noqa: F401
+from ray_amd import internal  # noqa: F401
 
 
 def remote(*args, **kwargs):
@@ -65,7 +70,9 @@ __all__ = [
     "get_gpu_ids", "init", "is_initialized", "kill", "method", "nodes", "put", "remote",
     "shutdown", "timeline", "wait", "get_runtime_context", "ObjectRef", "ObjectRefGenerator",
     "ActorHandle", "LOCAL_MODE", "SCRIPT_MODE", "WORKER_MODE", "exceptions", "Language",
-    "client", "ClientBuilder", "show_in_dashboard",
+    "client", "ClientBuilder", "show_in_dashboard", "DynamicObjectRefGenerator",
+    "ActorClassID", "ActorID", "NodeID", "JobID", "WorkerID", "FunctionID", "ObjectID",
+    "TaskID", "UniqueID", "PlacementGroupID", "internal",
 ]
 
 from ray_amd.client_builder import ClientBuilder, client  # noqa: F401,E402

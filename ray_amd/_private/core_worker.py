@@ -939,6 +939,57 @@ class CoreWorker:
             return self.store is not None and self.store.contains(oid)
         return True
 
+    # ------------------------------------------------------------------ manual free
+    def free_objects(self, oids, local_only=False):
+        """ray.internal.free: drop the stored value of each object now, whatever its
+        reference count. Later gets raise ObjectFreedError; freed objects are never
+        reconstructed. Objects owned elsewhere are freed by their owner (unless
+        local_only: then only this node's store copy goes)."""
+        by_owner: dict = {}
+        for oid in oids:
+            with self.lock:
+                owned = oid in self.owned
+                e = self.refs.get(oid)
+                owner = e[1] if e else None
+            if owned:
+                self._free_owned(oid)
+            elif local_only or owner is None:
+                if self.store is not None:
+                    try:
+                        self.store.delete(oid)
+                    except Exception:
+                        pass
+            else:
+                by_owner.setdefault(owner, []).append(oid)
+        for owner, lst in by_owner.items():
+            self.send(owner, (P.REQ, 0, "free_objects_owned", (lst,)))
+
+    def _free_owned(self, oid):
+        from ray_amd.exceptions import ObjectFreedError
+
+        data = ser.serialize_error(ObjectFreedError(oid.hex())).to_bytes()
+        with self.lock:
+            o = self.owned.get(oid)
+            if o is None:
+                return
+            tid = o.task_id
+            was_ready = o.ready
+            in_store, node = o.in_store, o.node
+            o.task_id = None  # freed values are not reconstructed
+            if was_ready:
+                o.inline, o.in_store, o.node = data, False, None
+        if not was_ready:
+            self._mark_ready(oid, inline=data)
+        elif in_store:
+            self._delete_stored(oid, node)
+        with self.lock:
+            self._drop_lineage_if_unused(tid)
+
+    def _rpc_free_objects_owned(self, conn, rid, oids):
+        for oid in oids:
+            self._free_owned(oid)
+        self._reply(conn, rid, True, None)
+
     def _rpc_recover_object(self, conn, rid, oid, failed_node):
         """A borrower could not fetch `oid`: reconstruct it, reply once it is ready."""
         err = self._reconstruct(oid, failed_node)

@@ -100,6 +100,19 @@ class UniqueID(BaseID):
     SIZE = 16
 
 
+class ActorClassID(BaseID):
+    SIZE = 16
+
+
+class ObjectID(BaseID):
+    """20 bytes: the creating task's id + a 4-byte return / put index."""
+
+    SIZE = OBJECT_ID_SIZE
+
+    def task_id(self) -> TaskID:
+        return TaskID(self._b[:TASK_ID_SIZE])
+
+
 def object_id_for_return(task_id: bytes, index: int) -> bytes:
     return task_id + struct.pack("<I", index)
 

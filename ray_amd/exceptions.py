@@ -132,6 +132,19 @@ class OwnerDiedError(ObjectLostError):
     pass
 
 
+class ObjectFreedError(ObjectLostError):
+    """The object was manually freed with ``ray_amd.internal.free``."""
+
+    def __str__(self):
+        return (f"Object {self.object_ref_hex} was manually freed using the internal `free` "
+                "call. Please ensure that `free` is only called once the object is no "
+                "longer needed.")
+
+
+class ReferenceCountingAssertionError(ObjectLostError, AssertionError):
+    """An object was deleted while a reference to it still existed."""
+
+
 class ObjectFetchTimedOutError(ObjectLostError):
     pass
 

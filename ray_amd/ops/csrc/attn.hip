@@ -154,6 +154,23 @@ __device__ __forceinline__ void tile_load(TileRegs& r, const bf16_t* g, long gst
   r.v1 = *reinterpret_cast<const u32x4*>(g + ((c + 256) >> 3) * gstride + (c & 7) * 8);
 }
 
+// The same [64 rows][64] tile through a buffer resource: the per-thread offsets are fixed
+// (voff0/voff1, bytes) and the tile's position is a scalar byte offset, so a tile costs no
+// 64-bit VALU address arithmetic (2 loads instead of ~8 VALU + 2 loads)
+struct TileAddr {
+  int voff0, voff1;
+  __device__ __forceinline__ TileAddr(long gstride) {
+    const int c = threadIdx.x;
+    voff0 = (int)(((c >> 3) * gstride + (c & 7) * 8) * 2);
+    voff1 = (int)((((c + 256) >> 3) * gstride + (c & 7) * 8) * 2);
+  }
+};
+__device__ __forceinline__ void tile_load_buf(TileRegs& r, __amdgpu_buffer_rsrc_t rs,
+                                              const TileAddr& a, int soff) {
+  r.v0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, a.voff0, soff, 0));
+  r.v1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, a.voff1, soff, 0));
+}
+
 __device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* img) {
   const int c = threadIdx.x;
   *reinterpret_cast<u32x4*>(img + img_off(c >> 3, c & 7)) = r.v0;
@@ -186,10 +203,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
   KV A, B;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2,
+                                        0x00020000);
+  const TileAddr ta(tok);
   auto load_kv = [&](KV& x, int t) __attribute__((always_inline)) {
-    const long off = (long)t * 64 * tok;
-    tile_load(x.k, base + C + off, tok);
-    tile_load(x.v, base + 2 * C + off, tok);
+    const int off = t * 64 * (int)tok * 2;
+    tile_load_buf(x.k, rs, ta, off + C * 2);
+    tile_load_buf(x.v, rs, ta, off + 2 * C * 2);
   };
   auto store_kv = [&](const KV& x, int t) __attribute__((always_inline)) {
     bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
@@ -223,23 +244,31 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int i = 0; i < 16; ++i) mt = fmaxf(mt, st[kt][i]);
       mt = half_max(mt) * sc_log2;
-      const float m_new = fmaxf(m_run, mt);
-      const float alpha = fast_exp2(m_run - m_new);
+      // Lazy rescaling: the running max moves (and O / l are rescaled) only when some
+      // query's tile max exceeds it by more than 8 (log2 units). Otherwise the stale max
+      // stays, p <= 2^8 — exact in fp32, and the final O / l is unchanged: the common tile
+      // skips the 32 multiplies of the O rescale and the exp of alpha. A wave-uniform
+      // branch (the first tile always takes it: m_run = -inf).
+      if (__builtin_amdgcn_ballot_w64(mt > m_run + 8.f)) {
+        const float m_new = fmaxf(m_run, mt);
+        const float alpha = fast_exp2(m_run - m_new);
+        l_run *= alpha;
+        m_run = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(fmaf(st[kt][i], sc_log2, -m_new));
+          const float p = fast_exp2(fmaf(st[kt][i], sc_log2, -m_run));
           st[kt][i] = p;
           ls += p;
         }
-      l_run = l_run * alpha + half_sum(ls);
-      m_run = m_new;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      l_run += half_sum(ls);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll

@@ -167,3 +167,50 @@ def test_iterative_chain_frees_intermediates(local):
     assert cw.store.contains(ids[-1])
     _lose(x)
     assert float(ray.get(x)[0]) == 6.0  # the whole chain re-runs from lineage
+
+
+def test_internal_free(local):
+    """ray.internal.free drops stored values now; gets raise ObjectFreedError, also for a
+    borrower, and a freed task return is not reconstructed (reference
+    _private/internal_api.py:177)."""
+    import time
+
+    from ray_amd.exceptions import ObjectFreedError
+
+    cw = W.global_worker.core
+    r = big.remote(600_000, 1.5)
+    p = ray.put(np.ones(300_000, np.float32))
+    ray.get([r, p])
+    assert cw.store.contains(r._id) and cw.store.contains(p._id)
+    ray.internal.free([r, p])
+    deadline = time.time() + 10
+    while (cw.store.contains(r._id) or cw.store.contains(p._id)) and time.time() < deadline:
+        time.sleep(0.02)
+    assert not cw.store.contains(r._id) and not cw.store.contains(p._id)
+    with pytest.raises(ObjectFreedError):
+        ray.get(r)
+    with pytest.raises(ObjectFreedError):
+        ray.get(p)
+
+    @ray.remote
+    def read(refs):
+        try:
+            ray.get(refs[0])
+        except ObjectFreedError:
+            return "freed"
+        return "value"
+
+    assert ray.get(read.remote([r])) == "freed"
+    with pytest.raises(TypeError):
+        ray.internal.free([1])
+
+
+def test_id_types_exported():
+    assert ray.JobID.from_int(7).int() == 7
+    oid = ray.ObjectID(bytes(range(20)))
+    assert oid.task_id() == ray.TaskID(bytes(range(16)))
+    for cls in (ray.ActorID, ray.NodeID, ray.WorkerID, ray.PlacementGroupID, ray.UniqueID,
+                ray.FunctionID, ray.ActorClassID):
+        x = cls.from_random()
+        assert cls.from_hex(x.hex()) == x and not x.is_nil() and cls.nil().is_nil()
+    assert ray.DynamicObjectRefGenerator is ray.ObjectRefGenerator
