@@ -448,6 +448,36 @@ def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch):
         assert _rel(qkv.grad[:, :, i], ref_in.grad[:, :, i]) < 2e-2, i
 
 
+@pytest.mark.parametrize("spike", [6.0, 20.0, 80.0])
+def test_flash_attention_lazy_rescale_forced(cuda_device, spike):
+    """The forward keeps a stale running max until a tile max exceeds it by > 8 (log2
+    units). Spiking key rows at later tiles (aligned with every query) forces the rescale
+    branch mid-sequence, at several spike sizes around the threshold; full fp32 reference
+    (guide rule 26: a rare data-dependent branch needs an input that takes it)."""
+    torch.manual_seed(19)
+    B, T, H, D = 2, 512, 2, 64
+    qkv = torch.randn(B, T, 3, H, D, device=cuda_device) * 0.5
+    q_dir = torch.randn(D, device=cuda_device)
+    q_dir /= q_dir.norm()
+    qkv[:, :, 0] += q_dir * 2.0  # every query has a component along q_dir
+    for t in (130, 300, 450):  # keys in later tiles that jump the row max
+        qkv[:, t, 1] += q_dir * spike * (t / 150)
+    qkv = qkv.bfloat16().requires_grad_()
+    y = rf.causal_attention_qkv(qkv)
+    ref_in = qkv.detach().double().requires_grad_()
+    q, k, v = ref_in.permute(2, 0, 3, 1, 4).unbind(0)
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    mask = torch.ones(T, T, device=cuda_device, dtype=torch.bool).triu(1)
+    p = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+    yr = (p @ v).transpose(1, 2)
+    assert torch.isfinite(y.float()).all()
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert _rel(qkv.grad, ref_in.grad) < 2e-2
+
+
 def test_flat_adamw_matches_torch(cuda_device):
     from ray_amd.parallel.flat import FlatAdamW, FlatParams
 
