@@ -395,12 +395,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* lse_bh = lse + (long)bh * T;
   const float* del_bh = delta + (long)bh * T;
   QD A, B;
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dobase, 0, T * C * 2, 0x00020000);
+  const TileAddr taq(tok), tad(C);
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)lse_bh, 0, T * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)del_bh, 0, T * 4, 0x00020000);
   auto load_qd = [&](QD& x, int t) __attribute__((always_inline)) {
-    tile_load(x.q, base + (long)t * 64 * tok, tok);
-    tile_load(x.d, dobase + (long)t * 64 * C, C);
-    if (threadIdx.x < 128) {
-      const int i = t * 64 + (threadIdx.x & 63);
-      x.rc = threadIdx.x < 64 ? lse_bh[i] * inv_c : -del_bh[i];
+    tile_load_buf(x.q, rq, taq, t * 64 * (int)tok * 2);
+    tile_load_buf(x.d, rd, tad, t * 64 * C * 2);
+    if (threadIdx.x < 128) {  // waves 0 / 1: -lse/c / -delta of the tile's 64 rows
+      // (the b32 builtin returns the raw 32 bits as an integer)
+      const float v = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(threadIdx.x < 64 ? rl : rdl,
+                                                      (t * 64 + (threadIdx.x & 63)) * 4, 0, 0));
+      x.rc = threadIdx.x < 64 ? v * inv_c : -v;
     }
   };
   auto store_qd = [&](const QD& x, int t) __attribute__((always_inline)) {
@@ -556,10 +568,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
   KV A, B;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2, 0x00020000);
+  const TileAddr ta(tok);
   auto load_kv = [&](KV& x, int t) __attribute__((always_inline)) {
-    const long off = (long)t * 64 * tok;
-    tile_load(x.k, base + C + off, tok);
-    tile_load(x.v, base + 2 * C + off, tok);
+    const int off = t * 64 * (int)tok * 2;
+    tile_load_buf(x.k, rs, ta, off + C * 2);
+    tile_load_buf(x.v, rs, ta, off + 2 * C * 2);
   };
   auto store_kv = [&](const KV& x, int t) __attribute__((always_inline)) {
     bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
