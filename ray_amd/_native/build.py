@@ -27,6 +27,7 @@ HIP_LIB = os.path.join(HERE, "libray_amd_hip.so")
 ARCH = os.environ.get("RAY_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 AGPR_ACC_SOURCES = {"gemm4w.hip"}
+NO_SLP_SOURCES = {"attn.hip"}
 
 
 def _newer(target: str, sources: list[str]) -> bool:
@@ -61,8 +62,14 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         # ...except the 4-wave GEMM, whose 256 accumulators per lane must sit in AGPRs
         vgpr_form = [] if os.path.basename(s) in AGPR_ACC_SOURCES else \
             ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+        # attention: no SLP vectorisation — it pairs the softmax / dS multiplies into
+        # v_pk_mul_f32 whose even-aligned operand pairs cost v_mov / v_alignbit / v_perm
+        # shuffles of the MFMA accumulators (and packed f32 VALU is slower beside MFMAs:
+        # MI355X_MICROARCH.md, 'price of one filler'): -10% / -14% VALU in dK/dV / dQ
+        extra = ["-fno-slp-vectorize"] if os.path.basename(s) in NO_SLP_SOURCES else []
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-              "-munsafe-fp-atomics", "-Wno-unused-result"] + vgpr_form + ["-c", s, "-o", o])
+              "-munsafe-fp-atomics", "-Wno-unused-result"] + vgpr_form + extra +
+             ["-c", s, "-o", o])
 
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
