@@ -30,15 +30,28 @@ struct LtPlan {
 };
 
 hipblasLtHandle_t g_handle = nullptr;
-void* g_ws = nullptr;
 const size_t kWs = 64ull << 20;
 std::map<LtKey, LtPlan*> g_plans;
 std::mutex g_mu;
+// One workspace PER STREAM: a stream-K / split-K kernel keeps partial tiles and arrival
+// flags in its workspace, so two GEMMs running concurrently on different streams must
+// never share one (a shared one can mix their flags and leave a grid waiting forever).
+std::map<hipStream_t, void*> g_ws_by_stream;
+std::mutex g_ws_mu;  // not g_mu: the GEMM entry points call this with g_mu held
+
+void* workspace(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws_by_stream.find(st);
+  if (it != g_ws_by_stream.end()) return it->second;
+  void* w = nullptr;
+  if (hipMalloc(&w, kWs) != hipSuccess) return nullptr;
+  g_ws_by_stream[st] = w;
+  return w;
+}
 
 int init_handle() {
   if (g_handle) return 0;
   if (hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return -1;
-  if (hipMalloc(&g_ws, kWs) != hipSuccess) return -2;
   return 0;
 }
 
@@ -88,7 +101,7 @@ int run(LtPlan* p, int idx, const void* A, const void* B, float* C, float alpha,
         hipStream_t st) {
   const hipblasStatus_t s =
       hipblasLtMatmul(g_handle, p->desc, &alpha, A, p->a, B, p->b, &beta, C, p->c, C, p->c,
-                      &p->cands[idx].algo, g_ws, kWs, st);
+                      &p->cands[idx].algo, workspace(st), kWs, st);
   return s == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + (int)s;
 }
 
@@ -237,7 +250,7 @@ RA_EXPORT int ra_lt_gemm_ep(int ta, int tb, long m, long n, long k, const void* 
   const float alpha = 1.f, beta = 0.f;
   const hipblasStatus_t s =
       hipblasLtMatmul(g_handle, p->desc, &alpha, A, p->a, B, p->b, &beta, D, p->c, D, p->c,
-                      &p->cands[idx].algo, g_ws, kWs, st);
+                      &p->cands[idx].algo, workspace(st), kWs, st);
   return s == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + (int)s;
 }
 

@@ -513,12 +513,15 @@ class _CrossEntropy(torch.autograd.Function):
 
 _xent_streams: dict = {}
 
-# RAY_AMD_LMHEAD_PIPE=1: the LM head's three GEMMs per chunk stay in order on the current
-# stream while each chunk's softmax-xent pass runs on its own stream beside the next GEMMs.
-# Measured on MI355X (profiles/r3/lmhead_pipe.md): no gain over the default layout (dW GEMMs
-# on the wgrad side stream) — beside the K = 768 GEMMs, which move 1.5-3 TB/s themselves,
-# the xent pass stretches from 0.33 to ~2.0 ms and the chunk stays at ~2.0 ms either way.
-_LMHEAD_PIPE = os.environ.get("RAY_AMD_LMHEAD_PIPE", "0") == "1"
+# RAY_AMD_LMHEAD_PIPE=1 (default): the LM head's three GEMMs per chunk stay in order on the
+# current stream while each chunk's softmax-xent pass runs on its own stream beside the next
+# GEMMs. Same speed as the older layout (=0: dW GEMMs on the wgrad side stream; measured,
+# profiles/r3/lmhead_pipe.md — beside the K = 768 GEMMs, which move 1.5-3 TB/s themselves,
+# the xent pass stretches from 0.33 to ~2.0 ms and the chunk stays at ~2.0 ms either way),
+# but it never runs two torch (hipBLASLt) GEMMs concurrently on two streams: the older
+# layout hung the GPU on a ragged last chunk (tests/test_train_gpu.py, N = 12388, chunk
+# 4096), consistent with two concurrent stream-K GEMMs sharing torch's hipBLASLt workspace.
+_LMHEAD_PIPE = os.environ.get("RAY_AMD_LMHEAD_PIPE", "1") == "1"
 
 
 def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
