@@ -15,9 +15,10 @@ torch.distributed loop for comparison.
     # (under the launcher, rank 0 drives Ray; ranks 1..7 wait on a gloo barrier)
 
 ``--workload ppo`` runs the RLlib PPO synthetic-Atari throughput bench (BASELINE.json
-config 3), ``impala`` the IMPALA V-trace one (config 5, 1 learner), ``data`` the Ray Data
-→ GPU ingest pipeline (config 4, 1 GPU) and ``microbench`` the task/actor call-rate
-microbenchmark (config 1). Prints ONE JSON line on rank 0.
+config 3), ``impala`` the IMPALA V-trace one (config 5; ``--gpus N`` = N RCCL-joined GPU
+learners), ``data`` the Ray Data → GPU ingest pipeline (config 4; ``--gpus N`` = N
+TorchTrainer workers consuming dataset shards) and ``microbench`` the task/actor
+call-rate microbenchmark (config 1). Prints ONE JSON line on rank 0.
 """
 
 from __future__ import annotations
@@ -189,6 +190,32 @@ def bench_gpt2_ray(args):
             dist.destroy_process_group()
 
 
+def _rank0_only(args, fn):
+    """Ray-driven workloads under torch.distributed.run: rank 0 runs ``fn`` (which starts
+    Ray with --gpus GPU workers / learners), the other launcher ranks hold no GPU and wait
+    on a CPU (gloo) barrier."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    launched = int(os.environ.get("WORLD_SIZE", "1"))
+    if launched <= 1:
+        return fn(args)
+    if launched != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} != launcher world size {launched}")
+    dist.init_process_group("gloo", timeout=timedelta(hours=2))
+    rank = int(os.environ.get("RANK", "0"))
+    try:
+        if rank == 0:
+            for k in list(os.environ):
+                if k in _LAUNCHER_VARS or k.startswith("TORCHELASTIC_"):
+                    os.environ.pop(k)
+            fn(args)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload == "gpt2":
@@ -199,15 +226,15 @@ def main():
     elif args.workload == "ppo":
         from ray_amd.rllib.bench import bench_ppo
 
-        bench_ppo(args)
+        _rank0_only(args, bench_ppo)
     elif args.workload == "impala":
         from ray_amd.rllib.bench import bench_impala
 
-        bench_impala(args)
+        _rank0_only(args, bench_impala)
     elif args.workload == "data":
         from ray_amd.data.bench import bench_data
 
-        bench_data(args)
+        _rank0_only(args, bench_data)
     else:  # BASELINE.json config 1: task/actor call rates (CPU plumbing)
         from ray_amd._private import ray_perf
 

@@ -15,12 +15,22 @@ import os
 import time
 
 
+def _learners(args):
+    """--gpus N: N GPU learners in one RCCL group (LearnerGroup over a Train WorkerGroup,
+    the gradient all-reduce on RCCL / xGMI), weak scaling: 8 env runners and one
+    train-batch worth of samples per learner. N = 1 keeps the local learner."""
+    n = max(1, int(getattr(args, "gpus", 1) or 1))
+    return n, (n if n > 1 else 0)
+
+
 def bench_ppo(args):
     import ray_amd as ray
     from ray_amd.rllib.algorithms import PPOConfig
 
-    n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", "8"))
-    ray.init(num_cpus=max(n_runners + 2, os.cpu_count() or 1), ignore_reinit_error=True)
+    n_gpus, n_learners = _learners(args)
+    n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", str(8 * n_gpus)))
+    ray.init(num_cpus=max(n_runners + n_gpus + 2, os.cpu_count() or 1), num_gpus=n_gpus,
+             ignore_reinit_error=True)
     # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
     runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
     sample_async = os.environ.get("RAY_AMD_PPO_ASYNC", "0") == "1"
@@ -30,10 +40,10 @@ def bench_ppo(args):
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
                         rollout_fragment_length="auto", num_gpus_per_env_runner=runner_gpus,
                         sample_async=sample_async)
-           .training(train_batch_size=5000, minibatch_size=500, num_epochs=10, lr=1e-4,
-                     lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
+           .training(train_batch_size=5000 * n_gpus, minibatch_size=500, num_epochs=10,
+                     lr=1e-4, lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
                      entropy_coeff=0.01, model={"vf_share_layers": True})
-           .learners(num_learners=0, num_gpus_per_learner=1)
+           .learners(num_learners=n_learners, num_gpus_per_learner=1)
            .debugging(seed=0))
     algo = cfg.build()
     for _ in range(args.warmup):
@@ -51,15 +61,17 @@ def bench_ppo(args):
     value = steps / dt
     print(json.dumps({
         "metric": "rllib_ppo_synthetic_atari_env_steps_per_sec",
-        "value": round(value, 1), "unit": "env_steps/s", "n_gpus": 1, "steps": args.steps,
+        "value": round(value, 1), "unit": "env_steps/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic",
         "config": {"model": "nature-cnn-ppo", "env": "SyntheticAtari-v0 84x84x4",
-                   "env_runners": n_runners, "envs_per_runner": 5, "train_batch_size": 5000,
+                   "env_runners": n_runners, "envs_per_runner": 5,
+                   "train_batch_size": 5000 * n_gpus,
                    "env_steps_per_iter_measured": sorted(set(per_iter)),
                    "rollout_fragment_length": algo.config.rollout_fragment_length,
-                   "minibatch_size": 500, "num_epochs": 10, "parallelism": "1 learner",
+                   "minibatch_size": 500, "num_epochs": 10,
+                   "parallelism": f"{n_gpus} learner{'s' if n_gpus > 1 else ''}",
                    "env_runner_gpus": runner_gpus, "sample_async": sample_async},
         "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
                                                      "sample_time_s", "sample_wait_s",
@@ -70,19 +82,22 @@ def bench_ppo(args):
 
 
 def bench_impala(args):
-    """RLlib IMPALA synthetic-Atari throughput (BASELINE.json config 5, 1-learner slice):
-    asynchronous env-runner sampling + V-trace HIP kernel learner on one MI355X."""
+    """RLlib IMPALA synthetic-Atari throughput (BASELINE.json config 5): asynchronous
+    env-runner sampling + V-trace HIP kernel learners; ``--gpus N`` runs N learners on N
+    MI355X joined by RCCL (the config's 8-learner form at N = 8)."""
     import ray_amd as ray
     from ray_amd.rllib.algorithms import IMPALAConfig
 
-    n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", "8"))
-    ray.init(num_cpus=max(n_runners + 2, os.cpu_count() or 1), ignore_reinit_error=True)
+    n_gpus, n_learners = _learners(args)
+    n_runners = int(os.environ.get("RAY_AMD_PPO_RUNNERS", str(8 * n_gpus)))
+    ray.init(num_cpus=max(n_runners + n_gpus + 2, os.cpu_count() or 1), num_gpus=n_gpus,
+             ignore_reinit_error=True)
     cfg = (IMPALAConfig().environment("SyntheticAtari-v0")
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
                         rollout_fragment_length=50)
-           .training(train_batch_size=500, lr=6e-4, vf_loss_coeff=0.5, entropy_coeff=0.01,
-                     grad_clip=40.0)
-           .learners(num_learners=0, num_gpus_per_learner=1)
+           .training(train_batch_size=500 * n_gpus, lr=6e-4, vf_loss_coeff=0.5,
+                     entropy_coeff=0.01, grad_clip=40.0)
+           .learners(num_learners=n_learners, num_gpus_per_learner=1)
            .debugging(seed=0))
     cfg.min_time_s_per_iteration = 2.0
     algo = cfg.build()
@@ -96,13 +111,15 @@ def bench_impala(args):
     dt = time.perf_counter() - t0
     print(json.dumps({
         "metric": "rllib_impala_synthetic_atari_env_steps_per_sec",
-        "value": round(steps / dt, 1), "unit": "env_steps/s", "n_gpus": 1, "steps": args.steps,
+        "value": round(steps / dt, 1), "unit": "env_steps/s", "n_gpus": n_gpus,
+        "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic",
         "config": {"model": "nature-cnn-impala", "env": "SyntheticAtari-v0 84x84x4",
                    "env_runners": n_runners, "envs_per_runner": 5, "rollout_fragment_length": 50,
-                   "train_batch_size": 500, "parallelism": "1 learner"},
+                   "train_batch_size": 500 * n_gpus,
+                   "parallelism": f"{n_gpus} learner{'s' if n_gpus > 1 else ''}"},
     }), flush=True)
     algo.stop()
     ray.shutdown()
