@@ -168,6 +168,10 @@ PYBIND11_MODULE(_core, m) {
              {
                py::gil_scoped_release r;
                ok = s.get(k, &o, true);
+               // large objects are about to be read (deserialised views, H2D sources):
+               // map their pages in one madvise rather than a read fault per 16 pages
+               if (ok && o.data_size + o.meta_size >= (1u << 20))
+                 s.populate(o.offset, o.data_size + o.meta_size, false);
              }
              if (!ok) return py::none();
              auto* b = new PinnedBuf();
@@ -217,6 +221,13 @@ PYBIND11_MODULE(_core, m) {
              return py::memoryview::from_memory((void*)(s.base() + off), (ssize_t)n, false);
            })
       .def("address", [](ShmStore& s) { return (uintptr_t)s.base(); })
+      .def("populate",
+           [](ShmStore& s, uint64_t off, uint64_t n, bool write) {
+             py::gil_scoped_release r;
+             return s.populate(off, n, write);
+           },
+           py::arg("off"), py::arg("n"), py::arg("write") = false)
+      .def_property_readonly("heap_offset", &ShmStore::heap_offset)
       .def("write",
            [](ShmStore& s, uint64_t off, py::buffer b) {
              py::buffer_info bi = b.request();

@@ -102,6 +102,20 @@ ShmStore::ShmStore(const std::string& path, uint64_t size, bool create, uint64_t
   __atomic_store_n(&hdr_->magic, kMagic, __ATOMIC_RELEASE);
 }
 
+bool ShmStore::populate(uint64_t off, uint64_t n, bool write) const {
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22
+#endif
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+  if (off >= size_) return true;
+  n = std::min<uint64_t>(n, size_ - off);
+  const uint64_t pg = 4096;
+  const uint64_t b = off / pg * pg, e = align_up(off + n, pg);
+  return madvise(base_ + b, e - b, write ? MADV_POPULATE_WRITE : MADV_POPULATE_READ) == 0;
+}
+
 ShmStore::~ShmStore() {
   if (base_) munmap(base_, size_);
 }

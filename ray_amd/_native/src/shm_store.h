@@ -103,6 +103,16 @@ class ShmStore {
 
   uint8_t* base() const { return base_; }
   uint64_t size() const { return size_; }
+  uint64_t heap_offset() const { return hdr_->heap_off; }
+
+  // Page-table population for [off, off+n) of this process's mapping. A first write to a
+  // page of the segment costs a fault per 4 KiB page in every process (tens of ms for a
+  // 36 MiB image block); MADV_POPULATE_READ maps the already-allocated pages in one
+  // syscall with fault-around (~10x cheaper), after which the copy runs at memcpy speed.
+  // write=true (MADV_POPULATE_WRITE) also allocates and zeroes pages not yet backed:
+  // the raylet runs that over the low end of the heap in the background so writers
+  // rarely meet an unbacked page. Never modifies data. Returns false if unsupported.
+  bool populate(uint64_t off, uint64_t n, bool write) const;
 
   // Returns data offset, or UINT64_MAX when the heap is full. Throws on duplicate id.
   uint64_t create(const std::string& id, uint64_t data_size, uint64_t meta_size, int device,

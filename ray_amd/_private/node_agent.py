@@ -27,7 +27,7 @@ import sys
 import time
 import traceback
 
-from ray_amd._private.object_store import table_capacity
+from ray_amd._private.object_store import start_prefault, table_capacity
 from ray_amd._native import _core
 
 from . import protocol as P
@@ -50,6 +50,7 @@ class NodeAgent:
         os.makedirs(self.spill_dir, exist_ok=True)
         self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
                                     table_capacity(args.object_store_memory))
+        start_prefault(self.store, args.object_store_memory)
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.total, self.num_cpus = node_resources(args, self.node_ip, head=False)

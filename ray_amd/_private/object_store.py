@@ -20,12 +20,43 @@ from ray_amd.exceptions import ObjectStoreFullError
 from . import serialization as ser
 
 NO_SPACE = (1 << 64) - 1
+# writes at least this large map their destination pages with one madvise first
+# (ShmStore.populate): per-page write faults cost more than the copy itself
+POPULATE_MIN = 1 << 20
 
 
 def table_capacity(store_bytes: int) -> int:
     """Object-table slots for a store of ``store_bytes``: one per 16 KiB (small objects
     live inline in their owner's memory store, not here), between 4096 and 2^18."""
     return max(4096, min(1 << 18, int(store_bytes) >> 14))
+
+
+def start_prefault(store, size: int):
+    """Back the low end of a freshly created store's heap with pages in a daemon thread
+    (ShmStore.populate(write=True): allocates + zeroes holes, never touches data), so
+    writers' populate-read finds pages already allocated. RAY_AMD_STORE_PREFAULT_BYTES
+    (default: the smallest of a quarter of the store, 1/64 of RAM and 4 GiB; 0 disables).
+    Measured on the MI355X box: 16 workers faulting fresh pages of the same segment at
+    once take ~80 ms per 36 MiB block (allocation contention) against ~2 ms for pages
+    already backed."""
+    try:
+        ram = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    except (ValueError, OSError):
+        ram = 64 << 30
+    n = int(os.environ.get("RAY_AMD_STORE_PREFAULT_BYTES", min(size // 4, ram // 64, 4 << 30)))
+    if n <= 0:
+        return None
+    base = store.heap_offset
+
+    def run():
+        chunk = 64 << 20
+        for off in range(base, base + n, chunk):
+            if not store.populate(off, min(chunk, base + n - off), True):
+                return
+
+    t = threading.Thread(target=run, name="store-prefault", daemon=True)
+    t.start()
+    return t
 
 
 class _MmapBuf:
@@ -80,6 +111,8 @@ class ObjectStore:
 
     def put_serialized(self, oid: bytes, sobj: "ser.SerializedObject", pinned: bool = True):
         off = self._alloc(oid, sobj.total, pinned)
+        if sobj.total >= POPULATE_MIN:
+            self.store.populate(off, sobj.total)
         try:
             mv = self.store.buffer(off, sobj.total)
             try:
@@ -94,6 +127,8 @@ class ObjectStore:
     def put_bytes(self, oid: bytes, data, pinned: bool = True):
         n = len(data)
         off = self._alloc(oid, n, pinned)
+        if n >= POPULATE_MIN:
+            self.store.populate(off, n)
         try:
             self.store.write(off, data)
         except BaseException:
