@@ -417,7 +417,7 @@ class CoreWorker:
         with self.lock:
             for o in self.owned.values():
                 if o.borrowers and addr in o.borrowers:
-                    o.borrowers.discard(addr)
+                    del o.borrowers[addr]
         dead = [oid for oid, o in list(self.owned.items())]
         for oid in dead:
             self._maybe_free(oid)
@@ -437,19 +437,37 @@ class CoreWorker:
             os._exit(0)
 
     # ------------------------------------------------------------------ references
+    # A borrowed id's entry in self.refs is [local count, owner, credits]: credits = how
+    # many borrower registrations the owner holds for this process (one per hand-over
+    # the owner pinned for us — a reply's contained refs — plus our own add_borrower).
+    # The owner counts registrations per borrower and the release message returns all
+    # credits at once, so a release racing a fresh hand-over of the same id (a prefetched
+    # reply already on its way) cannot drop the owner's count to zero early.
     def add_local_ref(self, oid: bytes, owner: str, deserialized: bool = False):
         register = False
         with self.lock:
             e = self.refs.get(oid)
             if e is None:
-                e = self.refs[oid] = [1, owner, False]
+                e = self.refs[oid] = [1, owner, 0]
                 if owner != self.addr and owner:
-                    e[2] = True
+                    e[2] = 1
                     register = True
             else:
                 e[0] += 1
         if register:
             self._register_borrow(oid, owner)
+
+    def _add_borrow_credit(self, oid: bytes, owner: str):
+        """The sender of a reply pinned `oid` at its owner for us: one credit, and no
+        add_borrower of our own for the pins about to be made."""
+        if not owner or owner == self.addr:
+            return
+        with self.lock:
+            e = self.refs.get(oid)
+            if e is None:
+                self.refs[oid] = [0, owner, 1]
+            else:
+                e[2] += 1
 
     def _register_borrow(self, oid, owner):
         ctx = ser.current_deser_context()
@@ -480,7 +498,7 @@ class CoreWorker:
         if owned:
             self._maybe_free(oid)
         elif notify and not self._stopped:
-            self.send(notify, (P.REQ, 0, "remove_borrower", (oid, self.addr)))
+            self.send(notify, (P.REQ, 0, "remove_borrower", (oid, self.addr, e[2])))
 
     def _maybe_free(self, oid: bytes):
         contained = None
@@ -659,15 +677,19 @@ class CoreWorker:
             o = self.owned.get(oid)
             if o is not None:
                 if o.borrowers is None:
-                    o.borrowers = set()
-                o.borrowers.add(addr)
+                    o.borrowers = {}
+                o.borrowers[addr] = o.borrowers.get(addr, 0) + 1
         self._reply(conn, rid, True, o is not None)
 
-    def _rpc_remove_borrower(self, conn, rid, oid, addr):
+    def _rpc_remove_borrower(self, conn, rid, oid, addr, n=1):
         with self.lock:
             o = self.owned.get(oid)
-            if o is not None and o.borrowers:
-                o.borrowers.discard(addr)
+            if o is not None and o.borrowers and addr in o.borrowers:
+                left = o.borrowers[addr] - n
+                if left > 0:
+                    o.borrowers[addr] = left
+                else:
+                    del o.borrowers[addr]
         self._maybe_free(oid)
         self._reply(conn, rid, True, None)
 
@@ -1559,6 +1581,8 @@ class CoreWorker:
         for oid, kind, payload, contained in returns:
             pins = None
             if contained:
+                for c_oid, c_owner in contained:
+                    self._add_borrow_credit(c_oid, c_owner)
                 pins = [ObjectRef(c_oid, c_owner, _cw_obj=self) for c_oid, c_owner in contained]
             if kind == P.RET_INLINE:
                 self._mark_ready(oid, inline=payload, contained=pins, size=len(payload))
@@ -1688,6 +1712,8 @@ class CoreWorker:
         with self.lock:
             self.owned[oid] = _Owned(tid)
         ref = ObjectRef(oid, self.addr, _cw_obj=self)
+        for a, b in contained or ():
+            self._add_borrow_credit(a, b)
         pins = [ObjectRef(a, b, _cw_obj=self) for a, b in contained] if contained else None
         if kind == P.RET_INLINE:
             self._mark_ready(oid, inline=payload, contained=pins)
@@ -2164,8 +2190,8 @@ class CoreWorker:
                 o = self.owned.get(ref._id)
                 if o is not None:
                     if o.borrowers is None:
-                        o.borrowers = set()
-                    o.borrowers.add(owner_addr)
+                        o.borrowers = {}
+                    o.borrowers[owner_addr] = o.borrowers.get(owner_addr, 0) + 1
         elif ref._owner != owner_addr:
             try:
                 self.call(ref._owner, "add_borrower", ref._id, owner_addr, timeout=30)

@@ -525,7 +525,8 @@ class Dataset:
     def streaming_split(self, n: int, *, equal: bool = False, locality_hints=None) -> list:
         from .iterator import SplitCoordinator, StreamSplitIterator
 
-        coord = ray.remote(SplitCoordinator).options(num_cpus=0, max_concurrency=n + 2).remote(
+        coord = ray.remote(SplitCoordinator).options(
+            num_cpus=0, max_concurrency=n * StreamSplitIterator.PREFETCH_BLOCKS + 2).remote(
             self._plan, n, equal)
         return [StreamSplitIterator(coord, i) for i in range(n)]
 

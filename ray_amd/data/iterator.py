@@ -238,6 +238,8 @@ class SplitCoordinator:
             return self._next_block(i, epoch)
 
     def _next_block(self, i, epoch):
+        if epoch < self.epoch:  # a prefetch request left over from a finished epoch
+            return None
         if epoch > self.epoch and all(self.finished):
             self._start()
         while not self.queues[i]:
@@ -289,13 +291,22 @@ class StreamSplitIterator(DataIterator):
         self._index = index
         self._epoch = 0
 
+    # next_block requests kept in flight per consumer: the coordinator round trip (and
+    # its wait for the executor) overlaps the consumer's work on the previous block
+    PREFETCH_BLOCKS = 2
+
     def _blocks(self):
         ep = self._epoch
         self._epoch += 1
-        while True:
-            r = ray.get(self._coord.next_block.remote(self._index, ep))
+        window = collections.deque(self._coord.next_block.remote(self._index, ep)
+                                   for _ in range(self.PREFETCH_BLOCKS))
+        while window:
+            r = ray.get(window.popleft())
             if r is None:
+                for x in window:  # the shard is exhausted: the rest answer None too
+                    ray.get(x)
                 return
+            window.append(self._coord.next_block.remote(self._index, ep))
             yield r[0]
 
     def iter_batches(self, *, batch_size=256, batch_format="default", drop_last=False,

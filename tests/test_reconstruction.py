@@ -214,3 +214,50 @@ def test_id_types_exported():
         x = cls.from_random()
         assert cls.from_hex(x.hex()) == x and not x.is_nil() and cls.nil().is_nil()
     assert ray.DynamicObjectRefGenerator is ray.ObjectRefGenerator
+
+
+def test_borrower_registrations_are_counted(local):
+    """The owner counts hand-overs per borrower: a borrower releasing its first copy while
+    a second hand-over of the same object (a prefetched reply) is already pinned for it
+    must not free the object (the streaming_split prefetch race)."""
+    cw = W.global_worker.core
+    ref = ray.put(np.arange(1 << 18))
+    oid = ref._id
+    peer = "unix:/nonexistent/borrower.sock"
+    cw._rpc_add_borrower(None, 0, oid, peer)  # hand-over 1
+    cw._rpc_add_borrower(None, 0, oid, peer)  # hand-over 2, reply still in flight
+    del ref  # the owner's own reference goes away
+    cw._rpc_remove_borrower(None, 0, oid, peer, 1)  # borrower releases copy 1
+    assert oid in cw.owned and cw.owned[oid].borrowers == {peer: 1}
+    cw._rpc_remove_borrower(None, 0, oid, peer, 1)  # and copy 2
+    assert oid not in cw.owned
+
+
+@ray.remote
+class _Dealer:
+    def __init__(self):
+        self.r = ray.put(np.ones(1 << 18))
+
+    def give(self):
+        return [self.r]
+
+    def drop(self):
+        self.r = None
+
+
+def test_prefetched_handover_survives_release(local):
+    """End to end: two replies carrying the same borrowed ref; the first is consumed and
+    released after the owner dropped its own reference; the second still resolves."""
+    import gc
+    import time
+
+    d = _Dealer.remote()
+    a, b = d.give.remote(), d.give.remote()
+    ra = ray.get(a)[0]
+    ray.get(b)  # second reply received (its pin is registered)
+    ray.get(d.drop.remote())
+    del ra, a
+    gc.collect()
+    time.sleep(0.3)
+    rb = ray.get(b)[0]
+    assert float(ray.get(rb).sum()) == float(1 << 18)
