@@ -14,6 +14,7 @@ import collections
 import numpy as np
 
 import ray_amd as ray
+from ray_amd._native import _core
 
 from . import block as B
 
@@ -150,13 +151,17 @@ def torch_batches(batches, dtypes, device, collate_fn, pin_memory=True):
                 if v.dtype == object:
                     out[k] = list(v)
                     continue
-                src = torch.from_numpy(v) if v.flags.writeable else torch.from_numpy(np.array(v))
-                key = (k, tuple(src.shape), src.dtype)
+                v = np.ascontiguousarray(v)
+                key = (k, v.shape, v.dtype.str)
                 buf = pinned[s].get(key)
                 if buf is None:
-                    buf = torch.empty(src.shape, dtype=src.dtype, pin_memory=pin_memory)
+                    buf = torch.empty(v.shape, dtype=torch.from_numpy(np.empty(0, v.dtype)).dtype,
+                                      pin_memory=pin_memory)
                     pinned[s][key] = buf
-                buf.copy_(src)
+                # one threaded copy, GIL released, straight from the (read-only) store
+                # view into the pinned buffer
+                _core.copy_into(buf.numpy().reshape(-1).view(np.uint8),
+                                v.reshape(-1).view(np.uint8))
                 t = buf.to(dev, non_blocking=True)
                 if dtypes is not None:
                     dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes

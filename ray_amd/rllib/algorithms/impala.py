@@ -30,13 +30,21 @@ class IMPALAConfig(AlgorithmConfig):
 
 class IMPALA(Algorithm):
     kind = "vtrace"
+    supports_multi_agent = True
 
     @classmethod
     def get_default_config(cls):
         return IMPALAConfig()
 
     def setup(self):
-        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space)
+        if self.is_multi_agent:  # one V-trace learner per trainable module
+            from ray_amd.rllib.core.learner import MultiAgentLearnerGroup
+
+            self.learner_group = MultiAgentLearnerGroup(self.cfg, self.module_specs,
+                                                        self.config.policies_to_train)
+        else:
+            self.learner_group = LearnerGroup(self.cfg, self.observation_space,
+                                              self.action_space)
         self._sync_weights(self.learner_group.get_weights())
         self._inflight = {}
         self._updates = 0

@@ -514,19 +514,28 @@ class Learner:
             vs, pg_adv = rf.vtrace(tgt_logp.detach() - beh_logp, disc, rewards, v.detach(), boot_v,
                                    c.get("vtrace_clip_rho_threshold", 1.0), 1.0,
                                    c.get("vtrace_clip_pg_rho_threshold", 1.0))
+        if "loss_mask" in batch:  # multi-agent padding rows: excluded from every term
+            m = _to_t(batch["loss_mask"], dev).float().view(T, B)
+            inv = 1.0 / m.sum().clamp_min(1.0)
+
+            def mean(x):
+                return (x * m).sum() * inv
+        else:
+            def mean(x):
+                return x.mean()
         if c.get("appo", False):
             ratio = torch.exp(tgt_logp - beh_logp)
             clip = c.get("clip_param", 0.4)
-            pg = -torch.minimum(pg_adv * ratio, pg_adv * ratio.clamp(1 - clip, 1 + clip)).mean()
+            pg = -mean(torch.minimum(pg_adv * ratio, pg_adv * ratio.clamp(1 - clip, 1 + clip)))
         else:
-            pg = -(tgt_logp * pg_adv).mean()
-        vf = 0.5 * ((vs - v) ** 2).mean()
-        ent = -(lp_all.exp() * lp_all).sum(-1).mean()
+            pg = -mean(tgt_logp * pg_adv)
+        vf = 0.5 * mean((vs - v) ** 2)
+        ent = mean(-(lp_all.exp() * lp_all).sum(-1).view(T, B))
         loss = pg + c.get("vf_loss_coeff", 0.5) * vf - c.get("entropy_coeff", 0.01) * ent
         self._step(loss)
         self.updates += 1
-        return {"total_loss": float(loss), "pi_loss": float(pg), "vf_loss": float(vf),
-                "entropy": float(ent)}
+        return {"total_loss": float(loss.detach()), "pi_loss": float(pg.detach()),
+                "vf_loss": float(vf.detach()), "entropy": float(ent.detach())}
 
 
 def _explained_var(y, pred):

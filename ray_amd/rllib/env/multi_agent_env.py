@@ -1,5 +1,6 @@
 """Multi-agent env API (reference: rllib/env/multi_agent_env.py: MultiAgentEnv,
-make_multi_agent; rllib/examples/envs/classes/multi_agent.py: MultiAgentCartPole).
+make_multi_agent; rllib/examples/envs/classes/multi_agent.py: MultiAgentCartPole;
+turn-based examples: TurnBasedGuess (delayed-credit probe) and TicTacToe).
 
 ``reset() -> (obs_dict, info_dict)``; ``step(action_dict) -> (obs, rewards, terminateds,
 truncateds, infos)`` with per-agent dicts and the ``"__all__"`` key in ``terminateds`` /
@@ -7,6 +8,9 @@ truncateds, infos)`` with per-agent dicts and the ``"__all__"`` key in ``termina
 
 from __future__ import annotations
 
+import numpy as np
+
+from ray_amd.rllib.env import spaces
 from ray_amd.rllib.env.envs import Env, make_env, register_env
 
 
@@ -82,3 +86,97 @@ MultiAgentCartPole = make_multi_agent("CartPole-v1")
 MultiAgentPendulum = make_multi_agent("Pendulum-v1")
 register_env("MultiAgentCartPole", lambda cfg: MultiAgentCartPole(cfg))
 register_env("multi_agent_cartpole", lambda cfg: MultiAgentCartPole(cfg))
+
+
+class TurnBasedGuess(MultiAgentEnv):
+    """Two players move in turns. The mover observes a one-hot cue (``num_cues`` wide) and
+    earns +1 when its action equals the cue, but the reward is paid only in the step the
+    OTHER player answers (the final mover is paid when the episode ends), so a learner
+    only improves if rewards are credited to the right, earlier action. An episode is
+    ``episode_len`` moves in total (env_config)."""
+
+    def __init__(self, config=None):
+        cfg = dict(config or {})
+        self.n = int(cfg.get("num_cues", 4))
+        self.length = int(cfg.get("episode_len", 10))
+        self.rng = np.random.default_rng(cfg.get("seed", 0))
+        self.possible_agents = ["p1", "p2"]
+        self.agents = list(self.possible_agents)
+        self.observation_space = spaces.Box(0.0, 1.0, (self.n,), np.float32)
+        self.action_space = spaces.Discrete(self.n)
+
+    def _cue(self):
+        self.target = int(self.rng.integers(self.n))
+        o = np.zeros(self.n, np.float32)
+        o[self.target] = 1.0
+        return o
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        self.mover = "p1"
+        self.owed = None  # (player, reward) not yet paid
+        return {"p1": self._cue()}, {}
+
+    def step(self, action_dict):
+        a = int(action_dict[self.mover])
+        earned = 1.0 if a == self.target else 0.0
+        rew = {}
+        if self.owed is not None:
+            rew[self.owed[0]] = self.owed[1]
+        self.owed = (self.mover, earned)
+        self.t += 1
+        done = self.t >= self.length
+        if done:
+            rew[self.mover] = rew.get(self.mover, 0.0) + earned
+            term = {"__all__": True, "p1": True, "p2": True}
+            return {}, rew, term, {"__all__": False}, {}
+        self.mover = "p2" if self.mover == "p1" else "p1"
+        return {self.mover: self._cue()}, rew, {"__all__": False}, {"__all__": False}, {}
+
+
+class TicTacToe(MultiAgentEnv):
+    """Turn-based 3x3 tic-tac-toe between ``player1`` (moves first) and ``player2``
+    (reference: rllib/examples/envs/classes/multi_agent/tic_tac_toe.py). Observation: the
+    board from the mover's view (+1 own, -1 opponent, 0 empty; 9 floats); action: a cell.
+    A win pays +1 / -1; an illegal move (occupied cell) ends the game with -1 for the mover
+    (+0 for the other); a full board is a draw (0, 0)."""
+
+    LINES = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (0, 3, 6), (1, 4, 7), (2, 5, 8), (0, 4, 8),
+             (2, 4, 6))
+
+    def __init__(self, config=None):
+        self.possible_agents = ["player1", "player2"]
+        self.agents = list(self.possible_agents)
+        self.observation_space = spaces.Box(-1.0, 1.0, (9,), np.float32)
+        self.action_space = spaces.Discrete(9)
+
+    def _obs(self, who):
+        sign = 1.0 if who == "player1" else -1.0
+        return (self.board * sign).astype(np.float32)
+
+    def reset(self, *, seed=None, options=None):
+        self.board = np.zeros(9, np.float32)  # +1 player1, -1 player2
+        self.mover = "player1"
+        return {self.mover: self._obs(self.mover)}, {}
+
+    def step(self, action_dict):
+        who = self.mover
+        other = "player2" if who == "player1" else "player1"
+        cell = int(action_dict[who])
+        done = {"__all__": True, "player1": True, "player2": True}
+        if self.board[cell] != 0:
+            return {}, {who: -1.0, other: 0.0}, done, {"__all__": False}, {}
+        self.board[cell] = 1.0 if who == "player1" else -1.0
+        v = self.board[cell]
+        if any(all(self.board[i] == v for i in ln) for ln in self.LINES):
+            return {}, {who: 1.0, other: -1.0}, done, {"__all__": False}, {}
+        if not (self.board == 0).any():
+            return {}, {who: 0.0, other: 0.0}, done, {"__all__": False}, {}
+        self.mover = other
+        return {other: self._obs(other)}, {}, {"__all__": False}, {"__all__": False}, {}
+
+
+register_env("TurnBasedGuess", lambda cfg: TurnBasedGuess(cfg))
+register_env("TicTacToe", lambda cfg: TicTacToe(cfg))

@@ -7,11 +7,21 @@ episode), and all agents that share a module are batched into one forward pass.
 
 The output keeps the time-major [T, B] layout the HIP GAE kernel consumes: every
 (env, agent, module) triple seen in the fragment is one column of its module's batch.
-Rows where that agent did not act (it finished before ``__all__``, or its env was
-between episodes under another mapping) are padding: ``terminateds = 1`` so the GAE
-recursion never crosses them, and ``loss_mask = 0`` so the learner drops them before
-the SGD epochs -- advantages of the real rows are therefore exact.  Agents must act on
-every step while alive (simultaneous-move envs); turn-based envs are rejected."""
+A column is that agent's OWN timeline -- row k is its k-th completed action -- right-
+aligned in the T rows; the leading rows are padding with ``terminateds = 1`` (the GAE /
+V-trace recursions never cross them) and ``loss_mask = 0`` (the learners drop them), so
+advantages of the real rows are exact.
+
+Credit assignment (reference: MultiAgentEpisode's per-agent reward buffers): an action is
+a *pending* row until its outcome is known -- rewards paid to the agent in later steps
+(turn-based games pay the mover after the opponent's reply) accumulate into it, and it
+is completed when the agent is asked to act again (or is in the very next observation
+dict: simultaneous-move envs complete every row in the step it was taken) or when the
+agent's episode ends. A pending row carries over to the next fragment; the column's
+bootstrap observation is the state the agent acts on next, i.e. that pending row's obs.
+Agents act only when they receive an observation, so turn-based envs (one mover per
+step) and simultaneous-move envs share this runner."""
+
 
 from __future__ import annotations
 
@@ -47,7 +57,7 @@ class MultiAgentEnvRunner:
         self.specs = config["_module_specs"]
         self.modules = {mid: RLModule(os_, as_, config.get("model")).eval()
                         for mid, (os_, as_) in self.specs.items()}
-        self.obs, self.alive, self.agent_module = [], [], []
+        self.obs, self.alive, self.agent_module, self.pending = [], [], [], []
         self.ep_ret = np.zeros(n)
         self.ep_len = np.zeros(n, dtype=np.int64)
         self.ep_agent_ret = [defaultdict(float) for _ in range(n)]
@@ -66,11 +76,16 @@ class MultiAgentEnvRunner:
             self.obs.append(None)
             self.alive.append(None)
             self.agent_module.append(None)
+            self.pending.append(None)
         self._ep_counter += 1
         self.ep_ids[i] = f"{self.worker_index}-{i}-{self._ep_counter}"
         self.obs[i] = dict(obs)
-        self.alive[i] = set(obs)
+        # turn-based envs show only the first mover at reset: every agent of the env is
+        # alive until it is done (or the episode is)
+        ids = self.envs[i].get_agent_ids() if hasattr(self.envs[i], "get_agent_ids") else ()
+        self.alive[i] = set(ids) | set(obs)
         self.agent_module[i] = {}
+        self.pending[i] = {}  # agent -> its last action awaiting its outcome
 
     def _module_of(self, i, aid):
         m = self.agent_module[i].get(aid)
@@ -101,37 +116,28 @@ class MultiAgentEnvRunner:
         return self.worker_index
 
     # ---------------------------------------------------------------- sampling
-    def _new_col(self, T, mid):
-        os_, as_ = self.specs[mid]
-        discrete = hasattr(as_, "n")
-        return {
-            "obs": np.zeros((T,) + tuple(os_.shape), dtype=os_.dtype),
-            "actions": np.zeros((T,) if discrete else (T,) + tuple(as_.shape),
-                                dtype=np.int64 if discrete else np.float32),
-            "rewards": np.zeros(T, np.float32),
-            "terminateds": np.ones(T, np.float32),   # padding rows cut the GAE recursion
-            "truncateds": np.zeros(T, np.float32),
-            "action_logp": np.zeros(T, np.float32),
-            "action_dist_inputs": None,
-            "loss_mask": np.zeros(T, np.float32),
-        }
+    def _complete(self, cols, i, aid, terminated=False, truncated=False):
+        """Move agent `aid`'s pending row (env i) into its column."""
+        row = self.pending[i].pop(aid, None)
+        if row is None:
+            return
+        row["terminateds"] = 1.0 if terminated else 0.0
+        row["truncateds"] = 1.0 if truncated else 0.0
+        cols.setdefault((i, aid, row["module"]), []).append(row)
 
-    def sample(self, num_timesteps: int | None = None, explore: bool = True):
+    def sample(self, num_timesteps: int | None = None, explore: bool = True,
+               with_metrics: bool = False):
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
-        cols: dict = {}   # (env, agent, module) -> column
+        boot_trunc = bool(self.config.get("bootstrap_truncated"))
+        cols: dict = {}   # (env, agent, module) -> completed rows, in order
         t0 = time.perf_counter()
-        for t in range(T):
+        for _t in range(T):
             groups = defaultdict(list)
             for i in range(len(self.envs)):
-                missing = self.alive[i] - set(self.obs[i])
-                if missing:
-                    raise NotImplementedError(
-                        f"agents {sorted(missing)} are alive but did not receive an observation; "
-                        "turn-based multi-agent envs are not supported by this runner")
-                for aid in sorted(self.alive[i], key=str):
-                    groups[self._module_of(i, aid)].append((i, aid))
+                for aid in sorted(self.obs[i], key=str):
+                    if aid in self.alive[i]:
+                        groups[self._module_of(i, aid)].append((i, aid))
             actions = [{} for _ in self.envs]
-            acted = {}
             for mid, items in groups.items():
                 mod = self.modules[mid]
                 x = torch.from_numpy(np.stack([self.obs[i][aid] for i, aid in items]))
@@ -141,39 +147,33 @@ class MultiAgentEnvRunner:
                 a, lp, di = a.cpu().numpy(), lp.cpu().numpy(), di.float().cpu().numpy()
                 as_ = self.specs[mid][1]
                 for j, (i, aid) in enumerate(items):
-                    col = cols.get((i, aid, mid))
-                    if col is None:
-                        col = cols[(i, aid, mid)] = self._new_col(T, mid)
-                    if col["action_dist_inputs"] is None:
-                        col["action_dist_inputs"] = np.zeros((T, di.shape[-1]), np.float32)
-                    col["obs"][t] = self.obs[i][aid]
-                    col["actions"][t] = a[j]
-                    col["action_logp"][t] = lp[j]
-                    col["action_dist_inputs"][t] = di[j]
-                    col["loss_mask"][t] = 1.0
-                    col["terminateds"][t] = 0.0
+                    self._complete(cols, i, aid)  # acting again: the previous row is final
+                    self.pending[i][aid] = {"module": mid, "obs": self.obs[i][aid],
+                                            "actions": a[j], "action_logp": lp[j],
+                                            "action_dist_inputs": di[j], "rewards": 0.0}
                     aj = a[j]
                     actions[i][aid] = int(aj) if hasattr(as_, "n") else \
                         np.clip(aj, as_.low, as_.high)
-                    acted[(i, aid)] = col
             for i, env in enumerate(self.envs):
                 o, r, te, tr, _ = env.step(actions[i])
-                all_done = bool(te.get("__all__")) or bool(tr.get("__all__"))
+                all_term, all_trunc = bool(te.get("__all__")), bool(tr.get("__all__"))
                 for aid, rv in r.items():
                     self.ep_ret[i] += rv
                     self.ep_agent_ret[i][aid] += rv
-                for aid in actions[i]:
-                    col = acted[(i, aid)]
-                    col["rewards"][t] = r.get(aid, 0.0)
-                    done = bool(te.get(aid)) or bool(tr.get(aid)) or all_done
-                    if done:
-                        col["terminateds"][t] = 1.0 if (te.get(aid) or te.get("__all__") or
-                                                        not self.config.get("bootstrap_truncated")
-                                                        ) else 0.0
-                        col["truncateds"][t] = float(bool(tr.get(aid) or tr.get("__all__")))
+                    row = self.pending[i].get(aid)
+                    if row is not None:
+                        row["rewards"] += float(rv)
+                for aid in list(self.alive[i]):
+                    a_te = bool(te.get(aid)) or all_term
+                    a_tr = bool(tr.get(aid)) or all_trunc
+                    if a_te or a_tr:
+                        self._complete(cols, i, aid, terminated=a_te or not boot_trunc,
+                                       truncated=a_tr)
                         self.alive[i].discard(aid)
                 self.ep_len[i] += 1
-                if all_done or not self.alive[i]:
+                if all_term or all_trunc or not self.alive[i]:
+                    for aid in list(self.pending[i]):
+                        self._complete(cols, i, aid, terminated=True)
                     self.done_returns.append(float(self.ep_ret[i]))
                     self.done_lengths.append(int(self.ep_len[i]))
                     for aid, rv in self.ep_agent_ret[i].items():
@@ -184,6 +184,8 @@ class MultiAgentEnvRunner:
                     self._start_episode(i, o)
                 else:
                     self.obs[i] = {aid: ob for aid, ob in o.items() if aid in self.alive[i]}
+                    for aid in self.obs[i]:  # asked to act next step: its reward is in
+                        self._complete(cols, i, aid)
         env_steps = T * len(self.envs)
         self.total_steps += env_steps
         modules = {}
@@ -191,22 +193,44 @@ class MultiAgentEnvRunner:
             keys = sorted((k for k in cols if k[2] == mid), key=lambda k: (k[0], str(k[1])))
             if not keys:
                 continue
-            b = {f: np.stack([cols[k][f] for k in keys], axis=1)
-                 for f in ("obs", "actions", "rewards", "terminateds", "truncateds",
-                           "action_logp", "action_dist_inputs", "loss_mask")}
-            os_ = self.specs[mid][0]
-            boot = np.zeros((len(keys),) + tuple(os_.shape), dtype=os_.dtype)
-            for j, (i, aid, m) in enumerate(keys):
-                if aid in self.alive[i] and self.agent_module[i].get(aid) == m:
+            B = len(keys)
+            os_, as_ = self.specs[mid]
+            discrete = hasattr(as_, "n")
+            b = {"obs": np.zeros((T, B) + tuple(os_.shape), dtype=os_.dtype),
+                 "actions": np.zeros((T, B) if discrete else (T, B) + tuple(as_.shape),
+                                     dtype=np.int64 if discrete else np.float32),
+                 "rewards": np.zeros((T, B), np.float32),
+                 "terminateds": np.ones((T, B), np.float32),  # padding cuts the recursion
+                 "truncateds": np.zeros((T, B), np.float32),
+                 "action_logp": np.zeros((T, B), np.float32),
+                 "loss_mask": np.zeros((T, B), np.float32)}
+            ndi = len(cols[keys[0]][0]["action_dist_inputs"])
+            b["action_dist_inputs"] = np.zeros((T, B, ndi), np.float32)
+            boot = np.zeros((B,) + tuple(os_.shape), dtype=os_.dtype)
+            for j, k in enumerate(keys):
+                rows = cols[k]
+                s0 = T - len(rows)  # right-aligned: the last real row meets the bootstrap
+                for f in ("obs", "actions", "rewards", "terminateds", "truncateds",
+                          "action_logp", "action_dist_inputs"):
+                    b[f][s0:, j] = np.stack([np.asarray(rw[f]) for rw in rows])
+                b["loss_mask"][s0:, j] = 1.0
+                i, aid, m = k
+                nxt = self.pending[i].get(aid)
+                if nxt is not None and nxt["module"] == m:
+                    boot[j] = nxt["obs"]
+                elif aid in self.obs[i] and self.agent_module[i].get(aid) == m:
                     boot[j] = self.obs[i][aid]
             b["bootstrap_obs"] = boot
             b["env_steps"] = env_steps
             b["agent_steps"] = int(b["loss_mask"].sum())
             modules[mid] = b
-        return {"modules": modules, "env_steps": env_steps,
-                "agent_steps": sum(b["agent_steps"] for b in modules.values()),
-                "sample_time_s": time.perf_counter() - t0,
-                "weights_version": self.weights_version}
+        out = {"modules": modules, "env_steps": env_steps,
+               "agent_steps": sum(b["agent_steps"] for b in modules.values()),
+               "sample_time_s": time.perf_counter() - t0,
+               "weights_version": self.weights_version}
+        if with_metrics:
+            out["_metrics"] = self.get_metrics()
+        return out
 
     def get_metrics(self):
         out = {"episode_returns": self.done_returns, "episode_lengths": self.done_lengths,
