@@ -87,22 +87,83 @@ class _QLearner:
         pass
 
 
+class _MultiQ:
+    """Multi-agent DQN: one Q learner (and one replay buffer, held by the algorithm) per
+    module; the non-trainable modules keep their initial weights."""
+
+    def __init__(self, cfg, specs, trainable):
+        self.learners = {mid: _QLearner(cfg, os_, as_) for mid, (os_, as_) in specs.items()}
+        self.trainable = set(trainable) if trainable else set(specs)
+
+    def sync_target(self):
+        for mid in self.trainable:
+            self.learners[mid].sync_target()
+
+    def get_weights(self):
+        return {mid: lr.get_weights() for mid, lr in self.learners.items()}
+
+    def get_state(self):
+        return {mid: lr.get_state() for mid, lr in self.learners.items()}
+
+    def set_state(self, s):
+        for mid, st in s.items():
+            self.learners[mid].set_state(st)
+
+    def shutdown(self):
+        pass
+
+
 class DQN(Algorithm):
     module_kind = "q"
+    supports_multi_agent = True
 
     @classmethod
     def get_default_config(cls):
         return DQNConfig()
 
-    def setup(self):
+    def _new_buffer(self):
         rb = self.config.replay_buffer_config
         cap = rb.get("capacity", 50000)
-        self.prioritized = "Prioritized" in rb.get("type", "")
-        self.buffer = PrioritizedReplayBuffer(cap, rb.get("alpha", 0.6), self.config.seed) \
+        return PrioritizedReplayBuffer(cap, rb.get("alpha", 0.6), self.config.seed) \
             if self.prioritized else ReplayBuffer(cap, self.config.seed)
-        self.learner_group = _QLearner(self.cfg, self.observation_space, self.action_space)
+
+    def setup(self):
+        self.prioritized = "Prioritized" in self.config.replay_buffer_config.get("type", "")
+        if self.is_multi_agent:
+            self.learner_group = _MultiQ(self.cfg, self.module_specs,
+                                         self.config.policies_to_train)
+            self.buffers = {mid: self._new_buffer() for mid in self.learner_group.trainable}
+        else:
+            self.buffer = self._new_buffer()
+            self.learner_group = _QLearner(self.cfg, self.observation_space, self.action_space)
         self._last_target = 0
         self._sync_weights(self.learner_group.get_weights())
+
+    def _add_multi_agent(self, b):
+        """Completed agent rows (loss_mask 1) of every trainable module's columns become
+        transitions of that module's buffer."""
+        for mid, mb in b["modules"].items():
+            if mid not in self.buffers:
+                continue
+            real = mb["loss_mask"] == 1
+            if real.any():
+                self.buffers[mid].add({k: mb[k][real] for k in
+                                       ("obs", "next_obs", "actions", "rewards", "terminateds")})
+        self.total_env_steps += b["env_steps"]
+
+    def _train_multi_agent(self, n_updates, stats):
+        cfg = self.config
+        for mid, buf in self.buffers.items():
+            if len(buf) < cfg.train_batch_size:
+                continue
+            for _ in range(n_updates):
+                kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} \
+                    if self.prioritized else {}
+                mb = buf.sample(cfg.train_batch_size, **kw)
+                loss, td = self.learner_group.learners[mid].update(mb)
+                if self.prioritized:
+                    buf.update_priorities(mb["batch_indexes"], td)
+                stats[f"{mid}/loss"] = loss
 
     def _epsilon(self):
         sched = self.config.epsilon
@@ -121,6 +182,9 @@ class DQN(Algorithm):
         else:
             bs = [self.local_runner.sample(cfg.rollout_fragment_length, True, eps)]
         for b in bs:
+            if self.is_multi_agent:
+                self._add_multi_agent(b)
+                continue
             T, B = b["rewards"].shape
             flat = {k: b[k].reshape((T * B,) + b[k].shape[2:])
                     for k in ("obs", "next_obs", "actions", "rewards", "terminateds")}
@@ -130,6 +194,9 @@ class DQN(Algorithm):
         if self.total_env_steps < cfg.num_steps_sampled_before_learning_starts:
             return stats
         n_updates = max(1, sum(b["env_steps"] for b in bs) // max(1, cfg.rollout_fragment_length))
+        if self.is_multi_agent:
+            self._train_multi_agent(n_updates, stats)
+            n_updates = 0
         for _ in range(n_updates):
             kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} if self.prioritized else {}
             mb = self.buffer.sample(cfg.train_batch_size, **kw)

@@ -55,7 +55,8 @@ class MultiAgentEnvRunner:
             self.envs.append(make_env(config["env"], ec))
         self.mapping_fn = config.get("policy_mapping_fn") or _default_mapping
         self.specs = config["_module_specs"]
-        self.modules = {mid: RLModule(os_, as_, config.get("model")).eval()
+        self.module_kind = config.get("module_kind", "actor_critic")
+        self.modules = {mid: self._make_module(os_, as_).eval()
                         for mid, (os_, as_) in self.specs.items()}
         self.obs, self.alive, self.agent_module, self.pending = [], [], [], []
         self.ep_ret = np.zeros(n)
@@ -87,6 +88,28 @@ class MultiAgentEnvRunner:
         self.agent_module[i] = {}
         self.pending[i] = {}  # agent -> its last action awaiting its outcome
 
+    def _make_module(self, os_, as_):
+        if self.module_kind == "q":  # multi-agent DQN: epsilon-greedy over Q-values
+            from ray_amd.rllib.core.rl_module import QModule
+
+            mc = dict(self.config.get("model") or {})
+            mc["dueling"] = self.config.get("dueling", True)
+            return QModule(os_, as_, mc)
+        return RLModule(os_, as_, self.config.get("model"))
+
+    def _act(self, mod, x, explore, epsilon, as_):
+        """(actions, logp, dist inputs) for a stacked observation batch."""
+        if self.module_kind == "q":
+            q = mod(x).float()
+            a = q.argmax(-1).numpy()
+            if explore and epsilon:
+                rnd = np.random.random(len(a)) < epsilon
+                a = np.where(rnd, np.random.randint(0, as_.n, len(a)), a)
+            return a, np.zeros(len(a), np.float32), q.numpy()
+        di = mod.forward_inference(x)["action_dist_inputs"]
+        a, lp = mod.sample_actions(di, explore)
+        return a.cpu().numpy(), lp.cpu().numpy(), di.float().cpu().numpy()
+
     def _module_of(self, i, aid):
         m = self.agent_module[i].get(aid)
         if m is None:
@@ -116,17 +139,19 @@ class MultiAgentEnvRunner:
         return self.worker_index
 
     # ---------------------------------------------------------------- sampling
-    def _complete(self, cols, i, aid, terminated=False, truncated=False):
-        """Move agent `aid`'s pending row (env i) into its column."""
+    def _complete(self, cols, i, aid, terminated=False, truncated=False, next_obs=None):
+        """Move agent `aid`'s pending row (env i) into its column; `next_obs` is the state
+        the agent acts on next (kept for the Q-learning transition)."""
         row = self.pending[i].pop(aid, None)
         if row is None:
             return
+        row["next_obs"] = row["obs"] if next_obs is None else next_obs
         row["terminateds"] = 1.0 if terminated else 0.0
         row["truncateds"] = 1.0 if truncated else 0.0
         cols.setdefault((i, aid, row["module"]), []).append(row)
 
     def sample(self, num_timesteps: int | None = None, explore: bool = True,
-               with_metrics: bool = False):
+               epsilon: float | None = None, with_metrics: bool = False):
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
         boot_trunc = bool(self.config.get("bootstrap_truncated"))
         cols: dict = {}   # (env, agent, module) -> completed rows, in order
@@ -141,13 +166,12 @@ class MultiAgentEnvRunner:
             for mid, items in groups.items():
                 mod = self.modules[mid]
                 x = torch.from_numpy(np.stack([self.obs[i][aid] for i, aid in items]))
-                with torch.no_grad():
-                    di = mod.forward_inference(x)["action_dist_inputs"]
-                    a, lp = mod.sample_actions(di, explore)
-                a, lp, di = a.cpu().numpy(), lp.cpu().numpy(), di.float().cpu().numpy()
                 as_ = self.specs[mid][1]
+                with torch.no_grad():
+                    a, lp, di = self._act(mod, x, explore, epsilon, as_)
                 for j, (i, aid) in enumerate(items):
-                    self._complete(cols, i, aid)  # acting again: the previous row is final
+                    # acting again: the previous row is final
+                    self._complete(cols, i, aid, next_obs=self.obs[i][aid])
                     self.pending[i][aid] = {"module": mid, "obs": self.obs[i][aid],
                                             "actions": a[j], "action_logp": lp[j],
                                             "action_dist_inputs": di[j], "rewards": 0.0}
@@ -168,7 +192,7 @@ class MultiAgentEnvRunner:
                     a_tr = bool(tr.get(aid)) or all_trunc
                     if a_te or a_tr:
                         self._complete(cols, i, aid, terminated=a_te or not boot_trunc,
-                                       truncated=a_tr)
+                                       truncated=a_tr, next_obs=o.get(aid))
                         self.alive[i].discard(aid)
                 self.ep_len[i] += 1
                 if all_term or all_trunc or not self.alive[i]:
@@ -185,7 +209,7 @@ class MultiAgentEnvRunner:
                 else:
                     self.obs[i] = {aid: ob for aid, ob in o.items() if aid in self.alive[i]}
                     for aid in self.obs[i]:  # asked to act next step: its reward is in
-                        self._complete(cols, i, aid)
+                        self._complete(cols, i, aid, next_obs=self.obs[i][aid])
         env_steps = T * len(self.envs)
         self.total_steps += env_steps
         modules = {}
@@ -206,12 +230,16 @@ class MultiAgentEnvRunner:
                  "loss_mask": np.zeros((T, B), np.float32)}
             ndi = len(cols[keys[0]][0]["action_dist_inputs"])
             b["action_dist_inputs"] = np.zeros((T, B, ndi), np.float32)
+            fields = ["obs", "actions", "rewards", "terminateds", "truncateds", "action_logp",
+                      "action_dist_inputs"]
+            if self.module_kind in ("q", "sac"):
+                b["next_obs"] = np.zeros_like(b["obs"])
+                fields.append("next_obs")
             boot = np.zeros((B,) + tuple(os_.shape), dtype=os_.dtype)
             for j, k in enumerate(keys):
                 rows = cols[k]
                 s0 = T - len(rows)  # right-aligned: the last real row meets the bootstrap
-                for f in ("obs", "actions", "rewards", "terminateds", "truncateds",
-                          "action_logp", "action_dist_inputs"):
+                for f in fields:
                     b[f][s0:, j] = np.stack([np.asarray(rw[f]) for rw in rows])
                 b["loss_mask"][s0:, j] = 1.0
                 i, aid, m = k

@@ -123,9 +123,9 @@ def test_policies_to_train_freezes_others(cluster):
     algo.stop()
 
 
-def test_non_ppo_multi_agent_rejected(cluster):
-    from ray_amd.rllib.algorithms.dqn import DQNConfig
-    cfg = (DQNConfig().environment("MultiAgentCartPole")
+def test_unsupported_multi_agent_rejected(cluster):
+    from ray_amd.rllib.algorithms.sac import SACConfig
+    cfg = (SACConfig().environment("MultiAgentCartPole")
            .multi_agent(policies={"p0"}, policy_mapping_fn=lambda aid, ep, **kw: "p0"))
     with pytest.raises(NotImplementedError):
         cfg.build()
@@ -236,4 +236,32 @@ def test_multi_agent_impala_learns(cluster):
             break
     assert {"p1", "p2"} <= set(res["learners"])
     algo.stop()
+    assert min(best.get("p1", 0), best.get("p2", 0)) > 3.5, best
+
+
+def test_multi_agent_dqn_learns_turn_based(cluster):
+    """Per-module replay buffers fed with completed agent rows (next_obs = the state the
+    agent acts on next, across the opponent's move)."""
+    from ray_amd.rllib.algorithms.dqn import DQNConfig
+
+    cfg = (DQNConfig().environment("TurnBasedGuess", env_config={"num_cues": 4,
+                                                                 "episode_len": 10})
+           .env_runners(num_env_runners=0, num_envs_per_env_runner=4)
+           .multi_agent(policies={"p1", "p2"}, policy_mapping_fn=lambda aid, ep, **kw: aid)
+           .training(lr=2e-3, gamma=0.5, train_batch_size=64, model={"fcnet_hiddens": [32]})
+           .debugging(seed=0))
+    cfg.num_steps_sampled_before_learning_starts = 200
+    cfg.target_network_update_freq = 100
+    cfg.epsilon = [(0, 1.0), (2000, 0.02)]
+    cfg.rollout_fragment_length = 10
+    algo = cfg.build()
+    best = {}
+    for _ in range(120):
+        res = algo.train()
+        for k, v in res.get("module_episode_returns_mean", {}).items():
+            best[k] = max(best.get(k, 0.0), v)
+        if best and algo.total_env_steps > 2000 and min(best.values()) > 4.0:
+            break
+    algo.stop()
+    assert any(k.endswith("/loss") for k in res["learners"])
     assert min(best.get("p1", 0), best.get("p2", 0)) > 3.5, best
