@@ -47,15 +47,26 @@ def start_prefault(store, size: int):
     if n <= 0:
         return None
     base = store.heap_offset
+    stop = threading.Event()
 
     def run():
-        chunk = 64 << 20
+        chunk = 32 << 20
         for off in range(base, base + n, chunk):
-            if not store.populate(off, min(chunk, base + n - off), True):
+            if stop.is_set() or not store.populate(off, min(chunk, base + n - off), True):
                 return
 
     t = threading.Thread(target=run, name="store-prefault", daemon=True)
     t.start()
+
+    def finish():
+        # a daemon thread still inside the native call (GIL released) when the
+        # interpreter finalises is unwound through noexcept C++ frames: std::terminate
+        stop.set()
+        t.join()
+
+    import atexit
+
+    atexit.register(finish)
     return t
 
 
