@@ -11,6 +11,8 @@
 // workload: release/train_tests + train/examples GPT-2 DDP).
 #include "common.h"
 
+typedef unsigned v2u32_t __attribute__((ext_vector_type(2)));
+
 // RES: the row is x = h + bias + skip (pre-LN residual add of the previous sub-block,
 // fused: x is computed once, written once (the next residual input) and normalised)
 template <int VPL, bool RES>
@@ -215,6 +217,150 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// Wave-wide sum without LDS: DPP within each 16-lane row (xor 1, xor 2, half-row mirror,
+// row mirror), then the gfx950 permlane16/32 swaps across rows (v1's __shfl_xor is six
+// ds_bpermute round trips through LDS per reduction).
+#define RA_DPP(v, ctrl) \
+  __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += RA_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += RA_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += RA_DPP(v, 0x141);  // row_half_mirror
+  v += RA_DPP(v, 0x140);  // row_mirror
+  const int lane = threadIdx.x & 63;
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto s16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v += __builtin_bit_cast(float, (lane & 16) ? s16[0] : s16[1]);
+  const unsigned u2 = __builtin_bit_cast(unsigned, v);
+  const auto s32 = __builtin_amdgcn_permlane32_swap(u2, u2, false, false);
+  v += __builtin_bit_cast(float, (lane & 32) ? s32[0] : s32[1]);
+  return v;
+}
+
+// Backward v2, for D == VPL * 256 (each lane owns VPL x 4 columns, no column guards) and
+// tensors under 2 GiB: rows are read and written through buffer resources, so a row past
+// N loads zeros and its store is dropped and the main loop has no branches. v1's guarded
+// loads/stores made the compiler wait for every outstanding access (vmcnt(0)) at each
+// branch join -- including the previous row pair's stores -- which serialised every
+// iteration on a full memory round trip (2.9 TB/s standalone at 65536 x 768).
+// Here the next row pair is always prefetched before the current one is reduced, the
+// only waits are counted ones, and row statistics also come in through buffer loads.
+template <int VPL, int NP, bool RES, int K>
+__global__ __launch_bounds__(256) void ln_bwd2_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N,
+    int D) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [NP][D]
+  for (int i = threadIdx.x; i < NP * D; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int bytes = N * D * 2;
+  const auto rX = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, bytes, 0x00020000);
+  const auto rDY = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, bytes, 0x00020000);
+  const auto rR = __builtin_amdgcn_make_buffer_rsrc((void*)dres, 0, RES ? bytes : 0, 0x00020000);
+  const auto rDX = __builtin_amdgcn_make_buffer_rsrc((void*)dx, 0, bytes, 0x00020000);
+  const auto rM = __builtin_amdgcn_make_buffer_rsrc((void*)mean, 0, N * 4, 0x00020000);
+  const auto rS = __builtin_amdgcn_make_buffer_rsrc((void*)rstd, 0, N * 4, 0x00020000);
+  float gg[VPL][4], acc[NP][VPL][4];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    unpack4(*reinterpret_cast<const uint2*>(g + (i * 64 + lane) * 4), gg[i]);
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[k][i][j] = 0.f;
+  }
+  const float invD = 1.f / (float)D;
+  const int stride = gridDim.x * 4;
+  const int r_first = blockIdx.x * 4 + w;
+  // rows r_first + k * stride, through a ring of K row register sets: while one row is
+  // reduced, the next K - 1 are in flight
+  const int iters = r_first < N ? (N - r_first + K * stride - 1) / (K * stride) : 0;
+  struct Row {
+    uint2 x[VPL], d[VPL], r[VPL];
+    float mu, rs;
+  };
+  auto load = [&](Row& b, int row) __attribute__((always_inline)) {
+    b.mu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rM, row * 4, 0, 0));
+    b.rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rS, row * 4, 0, 0));
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int off = (row * D + (i * 64 + lane) * 4) * 2;
+      b.x[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rX, off, 0, 0));
+      b.d[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rDY, off, 0, 0));
+      if (RES)
+        b.r[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rR, off, 0, 0));
+    }
+  };
+  auto compute = [&](const Row& b, int row) __attribute__((always_inline)) {
+    float xh[VPL][4], dv[VPL][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float xv[4];
+      unpack4(b.x[i], xv);
+      unpack4(b.d[i], dv[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xh[i][j] = (xv[j] - b.mu) * b.rs;
+        const float wd = dv[i][j] * gg[i][j];
+        s1 += wd;
+        s2 += wd * xh[i][j];
+        acc[0][i][j] += dv[i][j] * xh[i][j];
+        acc[1][i][j] += dv[i][j];
+      }
+    }
+    const float c1 = wave_sum_dpp(s1) * invD;
+    const float c2 = wave_sum_dpp(s2) * invD;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      float rv[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
+      if (RES) unpack4(b.r[i], rv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = (dv[i][j] * gg[i][j] - c1 - xh[i][j] * c2) * b.rs + rv[j];
+        if (NP == 3) acc[NP - 1][i][j] += o[j];
+      }
+      const int off = (row * D + (i * 64 + lane) * 4) * 2;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, pack4(o)), rDX, off, 0,
+                                            0);
+    }
+  };
+  Row ring[K];
+  int r = r_first;
+  if (iters > 0) {
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) load(ring[k], r + k * stride);
+  }
+  // sched_barrier: keep each set's loads where they are written (the machine scheduler
+  // otherwise hoists every set's loads to the loop top, behind a full vmcnt(0) wait)
+  for (int it = 0; it < iters; ++it, r += K * stride) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      load(ring[(k + K - 1) % K], r + (k + K - 1) * stride);  // past N: zeros, no stores
+      __builtin_amdgcn_sched_barrier(0);
+      compute(ring[k], r + k * stride);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int col = (i * 64 + lane) * 4;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(&lds[k * D + col + j], acc[k][i][j]);
+  }
+  __syncthreads();
+  const size_t P = gridDim.x;
+  for (int i = threadIdx.x; i < NP * D; i += blockDim.x) {
+    const int k = i / D, c = i - k * D;
+    part[((size_t)k * P + blockIdx.x) * D + c] = lds[i];
+  }
+}
+
 #define LN_DISPATCH(MACRO)                       \
   switch ((D + 255) / 256) {                     \
     case 1: MACRO(1); break;                     \
@@ -276,9 +422,25 @@ RA_EXPORT int ra_layernorm_bwd_parts(int N) {
   return p < cap ? p : cap;
 }
 
+// v2 applies to D in {256, 512, 768, 1024} with N*D*2 < 2^31 (ra_knobs[3] = 1 forces v1).
+static bool ln_bwd_v2(int N, int D) {
+  return ra_knobs[3] != 1 && D % 256 == 0 && D <= 1024 && (long)N * D * 2 < (1L << 31);
+}
+
+// v2 grid: ra_knobs[4] blocks (default 512), each wave >= 2 rows. Measured at 65536 x 768
+// (scripts/ln_bwd_bench.py, kernel only): 256 / 512 blocks 84 / 87 us (4.8 / 4.7 TB/s),
+// 768-1024 blocks 92-95 us, v1 105 us; a 3-deep row ring (ra_knobs[3] = 3) is no faster.
+static int ln_bwd_blocks(int N, int D) {
+  if (!ln_bwd_v2(N, D)) return ra_layernorm_bwd_parts(N);
+  int p = (N + 7) / 8;
+  const int cap = ra_knobs[4] > 0 ? ra_knobs[4] : 512;
+  return p < cap ? p : cap;
+}
+
 // fp32 workspace (in floats) required by ra_layernorm_bwd (3 partial slabs + scratch).
 RA_EXPORT long ra_layernorm_bwd_work(int N, int D) {
-  return 3L * ra_layernorm_bwd_parts(N) * D + 3L * kColsumSplits * D;
+  const int P = ln_bwd_blocks(N, D);
+  return 3L * P * D + 3L * kColsumSplits * D;
 }
 
 // dbias (optional): column sums of dx (bias grad of the residual add that produced x).
@@ -288,10 +450,38 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
                                void* dbias, float* work, int N, int D, int flags,
                                hipStream_t st) {
   if (D % 4 != 0) return hipErrorInvalidValue;
-  const int P = ra_layernorm_bwd_parts(N);
+  const int P = ln_bwd_blocks(N, D);
   const int NP = dbias ? 3 : 2;
   float* scr = work + (size_t)NP * P * D;
   const size_t lds = (size_t)NP * D * sizeof(float);
+  if (ln_bwd_v2(N, D)) {
+#define L2K(V, NPV, R, KK)                                                                     \
+  hipLaunchKernelGGL((ln_bwd2_kernel<V, NPV, R, KK>), dim3(P), dim3(256), lds, st,              \
+                     (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)g, mean, rstd,         \
+                     (const bf16_t*)dres, (bf16_t*)dx, work, N, D)
+#define L2(V, NPV, R)                                        \
+  if (ra_knobs[3] == 3) L2K(V, NPV, R, 3); else L2K(V, NPV, R, 2)
+#define L2V(V)                                       \
+  if (NP == 3) {                                     \
+    if (dres) L2(V, 3, true); else L2(V, 3, false);  \
+  } else {                                           \
+    if (dres) L2(V, 2, true); else L2(V, 2, false);  \
+  }
+    switch (D / 256) {
+      case 1: L2V(1); break;
+      case 2: L2V(2); break;
+      case 3: L2V(3); break;
+      default: L2V(4); break;
+    }
+#undef L2V
+#undef L2
+#undef L2K
+    void* outs[3] = {dg, db, dbias};
+    for (int k = 0; k < NP; ++k)
+      colsum_launch(work + (size_t)k * P * D, scr + (size_t)k * kColsumSplits * D, outs[k], P,
+                    D, flags, st);
+    return hipGetLastError();
+  }
 #define L(V)                                                                                  \
   if (NP == 3)                                                                                \
     hipLaunchKernelGGL((ln_bwd_kernel<V, 3>), dim3(P), dim3(256), lds, st, (const bf16_t*)dy, \

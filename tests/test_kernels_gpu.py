@@ -685,3 +685,38 @@ def test_gemm_nt_matches_fp32(cuda_device, variant, M, N, K):
                                    atol=2e-2 * gd.sum(0).abs().max().item())
     finally:
         _lib.lib().ra_set_knob(5, 0)
+
+
+@pytest.mark.parametrize("N,D,res", [(5003, 768, True), (4099, 1024, False), (37, 256, True),
+                                     (70000, 768, True)])
+def test_layernorm_bwd_v2_matches_fp32(cuda_device, N, D, res):
+    """Branch-free buffer-op LayerNorm backward (v2: D % 256 == 0): dx (+ skip gradient),
+    dgamma, dbeta and the residual-bias colsum against fp32 autograd, with a row count
+    that leaves the last row pair of some waves past N."""
+    from ray_amd.ops import _lib
+
+    torch.manual_seed(21)
+    h = torch.randn(N, D, device=cuda_device).bfloat16().requires_grad_()
+    skip = torch.randn(N, D, device=cuda_device).bfloat16().requires_grad_()
+    rb = (0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(D, device=cuda_device)).bfloat16().requires_grad_()
+    hr, sr, rbr, wr, br = (t.detach().float().requires_grad_() for t in (h, skip, rb, w, b))
+    gy = torch.randn(N, D, device=cuda_device)
+    gx = torch.randn(N, D, device=cuda_device)
+    _lib.lib().ra_set_knob(3, 0)  # v2
+    if res:
+        x, y = rf.residual_layer_norm(h, rb, skip, w, b)
+        torch.autograd.backward([x, y], [gx.bfloat16(), gy.bfloat16()])
+        xr = hr + rbr + sr
+        yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+        torch.autograd.backward([xr, yr], [gx, gy])
+        pairs = ((h, hr), (skip, sr), (rb, rbr), (w, wr), (b, br))
+    else:
+        y = rf.layer_norm(h, w, b)
+        y.backward(gy.bfloat16())
+        yr = torch.nn.functional.layer_norm(hr, (D,), wr, br, 1e-5)
+        yr.backward(gy)
+        pairs = ((h, hr), (w, wr), (b, br))
+    for a, r in pairs:
+        assert _rel(a.grad, r.grad) < 2e-2
