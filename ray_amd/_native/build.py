@@ -27,7 +27,7 @@ HIP_LIB = os.path.join(HERE, "libray_amd_hip.so")
 ARCH = os.environ.get("RAY_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 AGPR_ACC_SOURCES = {"gemm4w.hip"}
-NO_SLP_SOURCES = {"attn.hip", "layernorm.hip"}
+NO_SLP_SOURCES = {"attn.hip", "layernorm.hip", "gelu.hip"}
 
 
 def _newer(target: str, sources: list[str]) -> bool:

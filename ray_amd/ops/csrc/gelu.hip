@@ -13,6 +13,8 @@
 // chunk and finish with `colsum` over P partial rows.
 #include "common.h"
 
+typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float gelu_tanh(float u, float* dgelu) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float z = k0 * (u + k1 * u * u * u);
@@ -96,6 +98,87 @@ __global__ __launch_bounds__(64) void bwd_colpart_kernel(const bf16_t* __restric
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += d[j];
       }
+    }
+  }
+  float* pr = part + (size_t)blockIdx.y * F8 * 8 + (size_t)c8 * 8;
+  *reinterpret_cast<float4*>(pr) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(pr + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// v2 of the above, used by default (ra_knobs[3] != 1): the chunk [r0, r1) is addressed
+// through buffer resources that END at r1, so rows past the chunk load zeros and their
+// stores are dropped -- the loop has no guards and no break. v1's guarded batch made the
+// compiler sink every load to its use: one full memory round trip per row per wave.
+// Rows alternate between two register sets, so the next row's loads are in flight while
+// one is reduced (K row pairs per loop iteration).
+template <bool GELU, int K>
+__global__ __launch_bounds__(64) void bwd_colpart2_kernel(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ h,
+                                                          const bf16_t* __restrict__ bias,
+                                                          bf16_t* __restrict__ dh,
+                                                          float* __restrict__ part, int N,
+                                                          int F8, int rows_per_part) {
+  const int c8 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c8 >= F8) return;
+  const int r0 = blockIdx.y * rows_per_part;
+  const int r1 = min(N, r0 + rows_per_part);
+  const int nrows = r1 > r0 ? r1 - r0 : 0;
+  const size_t base = (size_t)r0 * F8 * 16;  // bytes
+  const int bytes = nrows * F8 * 16;
+  const auto rDY = __builtin_amdgcn_make_buffer_rsrc((char*)dy + base, 0, bytes, 0x00020000);
+  const auto rH = __builtin_amdgcn_make_buffer_rsrc((char*)h + (GELU ? base : 0), 0,
+                                                    GELU ? bytes : 0, 0x00020000);
+  const auto rDH = __builtin_amdgcn_make_buffer_rsrc((char*)dh + (GELU ? base : 0), 0,
+                                                     GELU ? bytes : 0, 0x00020000);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  float bv[8];
+  if (GELU) unpack8(reinterpret_cast<const uint4*>(bias)[c8], bv);
+  struct Row {
+    uint4 d, h;
+  };
+  auto load = [&](Row& b, int rr) __attribute__((always_inline)) {
+    const int off = (rr * F8 + c8) * 16;
+    b.d = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rDY, off, 0, 0));
+    if (GELU) b.h = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rH, off, 0, 0));
+  };
+  auto compute = [&](const Row& b, int rr) __attribute__((always_inline)) {
+    float d[8];
+    unpack8(b.d, d);
+    if (GELU) {
+      float hv[8], o[8];
+      unpack8(b.h, hv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dg;
+        gelu_tanh(hv[j] + bv[j], &dg);
+        o[j] = d[j] * dg;
+        acc[j] += o[j];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, pack8(o)), rDH,
+                                             (rr * F8 + c8) * 16, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += d[j];
+    }
+  };
+  // K row pairs per iteration through two register sets (A: even rows, B: odd rows)
+  const int iters = (nrows + 2 * K - 1) / (2 * K);
+  Row A, B;
+  if (iters > 0) load(A, 0);
+  int rr = 0;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < K; ++k, rr += 2) {
+      load(B, rr + 1);  // past the chunk: zeros, stores dropped
+      __builtin_amdgcn_sched_barrier(0);
+      compute(A, rr);
+      __builtin_amdgcn_sched_barrier(0);
+      load(A, rr + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(B, rr + 1);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   float* pr = part + (size_t)blockIdx.y * F8 * 8 + (size_t)c8 * 8;
@@ -259,9 +342,14 @@ RA_EXPORT int ra_bias_gelu_bwd(const void* dy, const void* h, const void* bias, 
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  hipLaunchKernelGGL(bwd_colpart_kernel<true>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
-                     (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh, work,
-                     N, F8, rpp);
+  if (ra_knobs[3] != 1 && (long)rpp * F8 * 16 < (1L << 31))
+    hipLaunchKernelGGL((bwd_colpart2_kernel<true, 1>), dim3((F8 + 63) / 64, P), dim3(64), 0, st,
+                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh,
+                       work, N, F8, rpp);
+  else
+    hipLaunchKernelGGL(bwd_colpart_kernel<true>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
+                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh,
+                       work, N, F8, rpp);
   colsum_launch(work, work + (size_t)P * F, dbias, P, F, sink_flags(flags), st);
   return hipGetLastError();
 }
@@ -271,8 +359,12 @@ RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
-                     (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
+  if (ra_knobs[3] != 1 && (long)rpp * F8 * 16 < (1L << 31))
+    hipLaunchKernelGGL((bwd_colpart2_kernel<false, 1>), dim3((F8 + 63) / 64, P), dim3(64), 0,
+                       st, (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
+  else
+    hipLaunchKernelGGL(bwd_colpart_kernel<false>, dim3((F8 + 63) / 64, P), dim3(64), 0, st,
+                       (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
   colsum_launch(work, work + (size_t)P * F, out, P, F, sink_flags(flags), st);
   return hipGetLastError();
 }

@@ -54,12 +54,71 @@ __global__ __launch_bounds__(256) void splitk_accum_kernel(const float* __restri
   }
 }
 
+// Fixed-S variant: all S partial loads of an element are issued before the first add
+// (the runtime-S loop above load-waits-adds one partial at a time: a memory round trip
+// per partial per wave, ~1.5 TB/s in the step), and the element's grad read joins them.
+template <bool OUT_F32, int S>
+__global__ __launch_bounds__(256) void splitk_accum_s_kernel(const float* __restrict__ part,
+                                                             long n4, void* __restrict__ grad,
+                                                             int accumulate) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 b[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) b[s] = reinterpret_cast<const float4*>(part)[(long)s * n4 + i];
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (accumulate) {
+      if (OUT_F32) {
+        const float4 o = reinterpret_cast<const float4*>(grad)[i];
+        v[0] = o.x, v[1] = o.y, v[2] = o.z, v[3] = o.w;
+      } else {
+        unpack4(reinterpret_cast<const uint2*>(grad)[i], v);
+      }
+    }
+    // partials summed first (same order as the runtime-S kernel), then the old gradient
+    float4 a = b[0];
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      a.x += b[s].x;
+      a.y += b[s].y;
+      a.z += b[s].z;
+      a.w += b[s].w;
+    }
+    v[0] += a.x, v[1] += a.y, v[2] += a.z, v[3] += a.w;
+    if (OUT_F32)
+      reinterpret_cast<float4*>(grad)[i] = make_float4(v[0], v[1], v[2], v[3]);
+    else
+      reinterpret_cast<uint2*>(grad)[i] = pack4(v);
+  }
+}
+
 // part: [S, n] fp32; grad: n bf16 or fp32 (n % 4 == 0, 16-byte aligned).
 // flags: bit0 accumulate into grad, bit1 grad is fp32.
 RA_EXPORT int ra_splitk_accum(const float* part, int S, long n, void* grad, int flags,
                               hipStream_t st) {
   if (n % 4 || S < 1) return hipErrorInvalidValue;
   const long n4 = n / 4;
+  const dim3 grid(ra_grid(n4, 256));
+#define SK(F32, SS)                                                                            \
+  hipLaunchKernelGGL((splitk_accum_s_kernel<F32, SS>), grid, dim3(256), 0, st, part, n4, grad, \
+                     flags & 1)
+#define SKS(F32)                   \
+  switch (S) {                     \
+    case 2: SK(F32, 2); break;     \
+    case 4: SK(F32, 4); break;     \
+    case 8: SK(F32, 8); break;     \
+    case 16: SK(F32, 16); break;   \
+    default: goto runtime_s;       \
+  }                                \
+  return hipGetLastError();
+  if (flags & 2) {
+    SKS(true)
+  } else {
+    SKS(false)
+  }
+#undef SKS
+#undef SK
+runtime_s:
   if (flags & 2)
     hipLaunchKernelGGL(splitk_accum_kernel<true>, dim3(ra_grid(n4, 256)), dim3(256), 0, st, part,
                        S, n4, grad, flags & 1);

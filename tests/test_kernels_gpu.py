@@ -37,7 +37,7 @@ def test_layernorm_fwd_bwd(cuda_device, N, D):
     assert _rel(b.grad, br.grad) < 2e-2
 
 
-@pytest.mark.parametrize("N,F", [(512, 3072), (37, 64)])
+@pytest.mark.parametrize("N,F", [(512, 3072), (37, 64), (4099, 3072)])
 def test_bias_gelu(cuda_device, N, F):
     torch.manual_seed(1)
     h = torch.randn(N, F, device=cuda_device).bfloat16().requires_grad_()
@@ -520,7 +520,8 @@ def test_gpt2_tiny_trains(cuda_device):
     assert loss < first * 0.7, (first, loss)
 
 
-@pytest.mark.parametrize("M,N,K,bias", [(16384, 256, 256, True), (1000, 384, 128, False)])
+@pytest.mark.parametrize("M,N,K,bias", [(16384, 256, 256, True), (1000, 384, 128, False),
+                                        (65536, 256, 256, False)])
 def test_linear_splitk(cuda_device, M, N, K, bias):
     torch.manual_seed(10)
     x = torch.randn(M, K, device=cuda_device).bfloat16().requires_grad_()
@@ -720,3 +721,23 @@ def test_layernorm_bwd_v2_matches_fp32(cuda_device, N, D, res):
         pairs = ((h, hr), (w, wr), (b, br))
     for a, r in pairs:
         assert _rel(a.grad, r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("f32,acc", [(True, True), (True, False), (False, True)])
+def test_splitk_accum_matches_fp32(cuda_device, S, f32, acc):
+    """ra_splitk_accum: grad (+)= sum_s part[s] for the fixed-S kernels (S = 2..16) and the
+    runtime-S fallback, fp32 and bf16 gradients."""
+    from ray_amd.ops import _lib
+    from ray_amd.ops._lib import ptr, stream_ptr
+
+    torch.manual_seed(S)
+    n = 4 * 12345
+    part = torch.randn(S, n, device=cuda_device)
+    g0 = torch.randn(n, device=cuda_device)
+    grad = g0.clone() if f32 else g0.bfloat16()
+    want = part.sum(0) + (grad.float() if acc else 0)
+    rc = _lib.lib().ra_splitk_accum(ptr(part), S, n, ptr(grad), (1 if acc else 0) | (2 if f32 else 0),
+                                    stream_ptr())
+    assert rc == 0
+    assert _rel(grad.float(), want) < (1e-6 if f32 else 5e-3)
