@@ -460,9 +460,11 @@ class Raylet:
             # large temporaries (decoded image blocks, rollout arrays) are recycled from
             # the worker's heap instead of a fresh mmap per allocation: a fresh 36 MiB
             # mapping costs ~9k page faults, more than the work that fills it (measured:
-            # the data bench's read task 35 -> 13 ms). Freed memory stays with the worker.
-            env.setdefault("MALLOC_MMAP_THRESHOLD_", str(1 << 30))
-            env.setdefault("MALLOC_TRIM_THRESHOLD_", str(4 << 30))
+            # the data bench's read task 35 -> 13 ms). Arrays above 64 MiB are still mapped
+            # and unmapped on free, and more than 256 MiB free at the heap top is returned,
+            # so a worker's RSS (what the memory monitor watches) stays near its live set.
+            env.setdefault("MALLOC_MMAP_THRESHOLD_", str(64 << 20))
+            env.setdefault("MALLOC_TRIM_THRESHOLD_", str(256 << 20))
         allr = {}
         for src in (j.get("runtime_env") or {}, renv or {}):
             allr.update(src)
