@@ -17,6 +17,49 @@ from ray_amd.rllib.env.env_runner import SingleAgentEnvRunner
 from ray_amd.rllib.env.envs import make_env
 
 
+class PerModuleLearners:
+    """Multi-agent off-policy learners (DQN, SAC): one learner per module built by
+    ``make(obs_space, action_space)``; only the ``trainable`` ones are updated. The
+    algorithm keeps one replay buffer per trainable module."""
+
+    def __init__(self, make, specs, trainable=None):
+        self.learners = {mid: make(os_, as_) for mid, (os_, as_) in specs.items()}
+        self.trainable = set(trainable) if trainable else set(specs)
+
+    def sync_target(self):
+        for mid in self.trainable:
+            getattr(self.learners[mid], "sync_target", lambda: None)()
+
+    def get_weights(self):
+        return {mid: lr.get_weights() for mid, lr in self.learners.items()}
+
+    def get_state(self):
+        return {mid: lr.get_state() for mid, lr in self.learners.items()}
+
+    def set_state(self, s):
+        for mid, st in s.items():
+            self.learners[mid].set_state(st)
+
+    def shutdown(self):
+        for lr in self.learners.values():
+            lr.shutdown()
+
+
+def add_agent_rows(buffers, batch):
+    """Completed agent rows (loss_mask 1) of a multi-agent sample become transitions of
+    their module's replay buffer; returns the number added."""
+    n = 0
+    for mid, mb in batch["modules"].items():
+        if mid not in buffers:
+            continue
+        real = mb["loss_mask"] == 1
+        if real.any():
+            buffers[mid].add({k: mb[k][real] for k in
+                              ("obs", "next_obs", "actions", "rewards", "terminateds")})
+            n += int(real.sum())
+    return n
+
+
 class Algorithm:
     kind = "ppo"
     supports_multi_agent = False

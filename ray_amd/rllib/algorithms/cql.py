@@ -72,6 +72,7 @@ class CQLLearner(SACLearner):
 
 
 class CQL(SAC):
+    supports_multi_agent = False  # offline: single-agent datasets only
     learner_class = CQLLearner
 
     @classmethod

@@ -6,7 +6,7 @@ import numpy as np
 import torch
 
 import ray_amd as ray
-from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.algorithms.algorithm import Algorithm, PerModuleLearners, add_agent_rows
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.rl_module import QModule
 from ray_amd.rllib.utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
@@ -87,32 +87,6 @@ class _QLearner:
         pass
 
 
-class _MultiQ:
-    """Multi-agent DQN: one Q learner (and one replay buffer, held by the algorithm) per
-    module; the non-trainable modules keep their initial weights."""
-
-    def __init__(self, cfg, specs, trainable):
-        self.learners = {mid: _QLearner(cfg, os_, as_) for mid, (os_, as_) in specs.items()}
-        self.trainable = set(trainable) if trainable else set(specs)
-
-    def sync_target(self):
-        for mid in self.trainable:
-            self.learners[mid].sync_target()
-
-    def get_weights(self):
-        return {mid: lr.get_weights() for mid, lr in self.learners.items()}
-
-    def get_state(self):
-        return {mid: lr.get_state() for mid, lr in self.learners.items()}
-
-    def set_state(self, s):
-        for mid, st in s.items():
-            self.learners[mid].set_state(st)
-
-    def shutdown(self):
-        pass
-
-
 class DQN(Algorithm):
     module_kind = "q"
     supports_multi_agent = True
@@ -130,8 +104,9 @@ class DQN(Algorithm):
     def setup(self):
         self.prioritized = "Prioritized" in self.config.replay_buffer_config.get("type", "")
         if self.is_multi_agent:
-            self.learner_group = _MultiQ(self.cfg, self.module_specs,
-                                         self.config.policies_to_train)
+            self.learner_group = PerModuleLearners(
+                lambda os_, as_: _QLearner(self.cfg, os_, as_), self.module_specs,
+                self.config.policies_to_train)
             self.buffers = {mid: self._new_buffer() for mid in self.learner_group.trainable}
         else:
             self.buffer = self._new_buffer()
@@ -140,15 +115,7 @@ class DQN(Algorithm):
         self._sync_weights(self.learner_group.get_weights())
 
     def _add_multi_agent(self, b):
-        """Completed agent rows (loss_mask 1) of every trainable module's columns become
-        transitions of that module's buffer."""
-        for mid, mb in b["modules"].items():
-            if mid not in self.buffers:
-                continue
-            real = mb["loss_mask"] == 1
-            if real.any():
-                self.buffers[mid].add({k: mb[k][real] for k in
-                                       ("obs", "next_obs", "actions", "rewards", "terminateds")})
+        add_agent_rows(self.buffers, b)
         self.total_env_steps += b["env_steps"]
 
     def _train_multi_agent(self, n_updates, stats):

@@ -86,6 +86,7 @@ MultiAgentCartPole = make_multi_agent("CartPole-v1")
 MultiAgentPendulum = make_multi_agent("Pendulum-v1")
 register_env("MultiAgentCartPole", lambda cfg: MultiAgentCartPole(cfg))
 register_env("multi_agent_cartpole", lambda cfg: MultiAgentCartPole(cfg))
+register_env("MultiAgentPendulum", lambda cfg: MultiAgentPendulum(cfg))
 
 
 class TurnBasedGuess(MultiAgentEnv):

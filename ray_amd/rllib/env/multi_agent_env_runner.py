@@ -95,6 +95,11 @@ class MultiAgentEnvRunner:
             mc = dict(self.config.get("model") or {})
             mc["dueling"] = self.config.get("dueling", True)
             return QModule(os_, as_, mc)
+        if self.module_kind == "sac":  # multi-agent SAC: the squashed-Gaussian actor
+            from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy
+
+            return SquashedGaussianPolicy(os_, as_, self.config.get("policy_model_config")
+                                          or self.config.get("model"))
         return RLModule(os_, as_, self.config.get("model"))
 
     def _act(self, mod, x, explore, epsilon, as_):
@@ -106,6 +111,10 @@ class MultiAgentEnvRunner:
                 rnd = np.random.random(len(a)) < epsilon
                 a = np.where(rnd, np.random.randint(0, as_.n, len(a)), a)
             return a, np.zeros(len(a), np.float32), q.numpy()
+        if self.module_kind == "sac":
+            a, lp = mod(x.float(), explore)
+            a, lp = a.float().numpy(), lp.float().numpy()
+            return a, lp, np.zeros((len(a), 1), np.float32)
         di = mod.forward_inference(x)["action_dist_inputs"]
         a, lp = mod.sample_actions(di, explore)
         return a.cpu().numpy(), lp.cpu().numpy(), di.float().cpu().numpy()

@@ -124,11 +124,41 @@ def test_policies_to_train_freezes_others(cluster):
 
 
 def test_unsupported_multi_agent_rejected(cluster):
-    from ray_amd.rllib.algorithms.sac import SACConfig
-    cfg = (SACConfig().environment("MultiAgentCartPole")
+    from ray_amd.rllib.algorithms.marwil import MARWILConfig
+    cfg = (MARWILConfig().environment("MultiAgentCartPole")
            .multi_agent(policies={"p0"}, policy_mapping_fn=lambda aid, ep, **kw: "p0"))
     with pytest.raises(NotImplementedError):
         cfg.build()
+
+
+def test_multi_agent_sac_trains_each_module(cluster):
+    """Continuous multi-agent SAC: per-module replay buffers and learners; the module left
+    out of policies_to_train keeps its weights."""
+    from ray_amd.rllib.algorithms.sac import SACConfig
+
+    cfg = (SACConfig().environment("MultiAgentPendulum", env_config={"num_agents": 3})
+           .env_runners(num_env_runners=0, num_envs_per_env_runner=2)
+           .multi_agent(policies={"p0", "p1", "p2"},
+                        policy_mapping_fn=lambda aid, ep, **kw: f"p{aid}",
+                        policies_to_train=["p0", "p1"])
+           .training(train_batch_size=32, model={"fcnet_hiddens": [32]})
+           .debugging(seed=0))
+    cfg.num_steps_sampled_before_learning_starts = 64
+    cfg.rollout_fragment_length = 16
+    algo = cfg.build()
+    w0 = {m: {k: np.array(v, np.float32) for k, v in w.items()}
+          for m, w in algo.get_weights().items()}
+    for _ in range(6):
+        res = algo.train()
+    w1 = algo.get_weights()
+    assert {"p0/critic_loss", "p1/critic_loss"} <= set(res["learners"])
+    assert not any(k.startswith("p2/") for k in res["learners"])
+    k = next(iter(w0["p2"]))
+    assert np.allclose(w0["p2"][k], np.asarray(w1["p2"][k], np.float32))
+    assert not all(np.allclose(w0["p0"][k2], np.asarray(w1["p0"][k2], np.float32))
+                   for k2 in w0["p0"])
+    assert res["env_runners"]["num_episodes"] >= 0
+    algo.stop()
 
 
 def test_make_multi_agent_from_creator():
