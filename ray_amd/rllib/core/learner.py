@@ -595,7 +595,9 @@ class LearnerGroup:
             pass
 
         self.wg = WorkerGroup(n, res)
-        _TorchBackend().on_start(self.wg, TorchConfig())
+        # learner_backend: process-group backend override (default: RCCL on GPU learners,
+        # gloo on CPU); "gloo" lets several GPU learners share one device in tests
+        _TorchBackend().on_start(self.wg, TorchConfig(backend=config.get("learner_backend")))
         self.actors = self.wg.workers
         ray.get([a.execute.remote(_make_learner, config, observation_space, action_space, i, n)
                  for i, a in enumerate(self.actors)])

@@ -79,7 +79,7 @@ class _TorchBackend(Backend):
             seen = {}
             for b, i in zip(binds, infos):
                 key = (i["node_id"], b["visible"], b["local_device"])
-                if key in seen:
+                if key in seen and backend == "nccl":  # RCCL: one rank per device
                     raise RuntimeError(f"two Train ranks bound to the same GPU: {b}")
                 seen[key] = True
         port = ray.get(worker_group.workers[0].free_port.remote())

@@ -108,3 +108,45 @@ def test_vtrace_learner_gpu(cuda_device):
     runner.set_weights(L.get_weights(), 1)
     stats = L.update_vtrace(runner.sample(32))
     assert np.isfinite(stats["total_loss"])
+
+
+@pytest.mark.parametrize("algo_name", ["ppo", "impala"])
+def test_two_gpu_learners_share_one_gpu(cuda_device, algo_name):
+    """The multi-learner GPU path (LearnerGroup on a Train WorkerGroup, world 2) on a
+    one-GPU box: two learners at 0.5 GPU join a gloo group (RCCL refuses two ranks per
+    device); both must take the same SGD steps on their HIP-resident shards and end
+    with identical weights."""
+    import ray_amd as ray
+    from ray_amd.rllib.algorithms.impala import IMPALAConfig
+    from ray_amd.rllib.algorithms.ppo import PPOConfig
+    from ray_amd.rllib.core.learner import _learner_call
+
+    ray.init(num_cpus=6, num_gpus=1)
+    try:
+        if algo_name == "ppo":
+            cfg = (PPOConfig().environment("CartPole-v1")
+                   .env_runners(num_env_runners=2, num_envs_per_env_runner=3,
+                                rollout_fragment_length=40)
+                   .training(train_batch_size=240, minibatch_size=64, num_epochs=2,
+                             model={"fcnet_hiddens": [32]}))
+        else:
+            cfg = (IMPALAConfig().environment("CartPole-v1")
+                   .env_runners(num_env_runners=2, num_envs_per_env_runner=2,
+                                rollout_fragment_length=20)
+                   .training(train_batch_size=80, lr=5e-4, model={"fcnet_hiddens": [32]}))
+        cfg = cfg.learners(num_learners=2, num_gpus_per_learner=0.5)
+        cfg.learner_backend = "gloo"
+        algo = cfg.build()
+        for _ in range(2):
+            r = algo.train()
+        assert np.isfinite(r["learners"]["total_loss"])
+        w = [ray.get(a.execute.remote(_learner_call, "get_weights"))
+             for a in algo.learner_group.actors]
+        assert all(torch.equal(torch.as_tensor(w[0][k]), torch.as_tensor(w[1][k]))
+                   for k in w[0])
+        dev = ray.get(algo.learner_group.actors[0].execute.remote(
+            _learner_call, "__getattribute__", "device"))
+        assert str(dev).startswith("cuda")
+        algo.stop()
+    finally:
+        ray.shutdown()

@@ -146,3 +146,33 @@ def test_torchtrainer_gpt2_one_gpu(cuda_device):
         assert m["grad_dtype"] == "fp32"
     finally:
         ray.shutdown()
+
+
+def test_torchtrainer_gpt2_two_workers_one_gpu_gloo(cuda_device):
+    """The world > 1 GPU path on a one-GPU box: two Train workers share the GPU
+    (0.5 each) and join a gloo group (RCCL refuses two ranks on one device), so the flat
+    DDP bucket hooks, the initial broadcast, the 1/world gradient scale and the
+    per-rank step timing all run with world size 2 on HIP tensors."""
+    import ray_amd as ray
+    from ray_amd.train import RunConfig, ScalingConfig
+    from ray_amd.train.examples.gpt2 import train_func
+    from ray_amd.train.torch import TorchConfig, TorchTrainer
+
+    ray.init(num_cpus=4, num_gpus=1)
+    try:
+        cfg = dict(model="tiny", micro_batch=4, seq_len=128, steps=4, warmup=2,
+                   tunableop="off", bucket_mb=0.25)
+        res = TorchTrainer(train_func, train_loop_config=cfg,
+                           torch_config=TorchConfig(backend="gloo"),
+                           scaling_config=ScalingConfig(num_workers=2, use_gpu=True,
+                                                        resources_per_worker={"GPU": 0.5}),
+                           run_config=RunConfig(name="t_gpt2_w2",
+                                                storage_path="/tmp/ra_t")).fit()
+        m = res.metrics
+        assert m["device"].startswith("cuda")
+        assert m["rccl_world_size"] == 2 and m["dist_backend"] == "gloo"
+        assert m["ranks_in_sync"] is True
+        assert len(m["per_rank_ms_per_step"]) == 2
+        assert m["loss"] == m["loss"] and m["tokens_per_sec"] > 0
+    finally:
+        ray.shutdown()
