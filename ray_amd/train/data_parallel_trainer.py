@@ -37,25 +37,25 @@ class _CheckpointManager:
         self.items: list[tuple[Checkpoint, dict]] = []
 
     def register(self, ckpt: Checkpoint, metrics: dict):
+        """Keep the best ``num_to_keep`` by score (by recency without a score attribute),
+        plus always the latest one, which a restore resumes from (reference:
+        train/_internal/checkpoint_manager.py register_checkpoint)."""
         self.items.append((ckpt, metrics))
         k = self.cfg.num_to_keep
-        if k is not None and len(self.items) > k:
-            attr = self.cfg.checkpoint_score_attribute
-            latest = self.items[-1]
-            if attr:
-                rev = self.cfg.checkpoint_score_order == "max"
-                ranked = sorted(self.items, key=lambda x: x[1].get(attr, float("-inf") if rev
-                                                                     else float("inf")),
-                                reverse=rev)
-                keep = ranked[:k]
-            else:
-                keep = self.items[-k:]
-            if latest not in keep:
-                keep = keep[:-1] + [latest] if k > 0 else keep
-            for c, m in self.items:
-                if (c, m) not in keep:
-                    shutil.rmtree(c.path, ignore_errors=True)
-            self.items = [x for x in self.items if x in keep]
+        if k is None or len(self.items) <= k:
+            return
+        latest = self.items[-1]
+        attr = self.cfg.checkpoint_score_attribute
+        if attr:
+            rev = self.cfg.checkpoint_score_order == "max"
+            missing = float("-inf") if rev else float("inf")
+            ranked = sorted(self.items, key=lambda x: x[1].get(attr, missing), reverse=rev)
+        else:
+            ranked = self.items[::-1]
+        drop = [x for x in ranked[k:] if x is not latest]
+        for c, _ in drop:
+            shutil.rmtree(c.path, ignore_errors=True)
+        self.items = [x for x in self.items if not any(x is d for d in drop)]
 
     @property
     def latest(self):

@@ -108,16 +108,26 @@ class MedianStoppingRule(TrialScheduler):
         self.hist = {}
 
     def on_trial_result(self, runner, trial, result):
+        """Stop a trial whose best score so far is below the median, over the other
+        trials (running or finished), of their running mean score up to the same time
+        (reference: tune/schedulers/median_stopping_rule.py)."""
         s = self._score(result)
         if s is None:
             return self.CONTINUE
-        self.hist.setdefault(trial.trial_id, []).append(s)
-        if result.get(self.time_attr, 0) < self.grace:
+        t = result.get(self.time_attr, 0)
+        self.hist.setdefault(trial.trial_id, []).append((t, s))
+        if t < self.grace:
             return self.CONTINUE
-        others = [np.mean(v) for k, v in self.hist.items() if k != trial.trial_id]
+        others = []
+        for k, v in self.hist.items():
+            if k == trial.trial_id:
+                continue
+            upto = [x for tt, x in v if tt <= t]
+            if upto:
+                others.append(np.mean(upto))
         if len(others) < self.min_samples:
             return self.CONTINUE
-        if max(self.hist[trial.trial_id]) < np.median(others):
+        if max(x for _, x in self.hist[trial.trial_id]) < np.median(others):
             return self.STOP
         return self.CONTINUE
 
