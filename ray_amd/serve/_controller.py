@@ -34,6 +34,7 @@ class _DeploymentState:
         self.status = "UPDATING"
         self.over_since = None
         self.under_since = None
+        self.retiring = {}  # old-version replicas serving until their successors are up
 
 
 class ServeController:
@@ -61,7 +62,11 @@ class ServeController:
                 if not spec.get("autoscaling_config"):
                     st.target = spec["num_replicas"]
                 if code_changed:
-                    await self._stop_replicas(st, list(st.replicas))
+                    # rolling update: the old replicas keep serving until the new ones
+                    # pass their health check, then drain (reference:
+                    # deployment_state.py version-mismatched replicas)
+                    st.retiring = dict(st.replicas)
+                    st.replicas = {}
                 elif cfg_changed and spec.get("user_config") is not None:
                     await asyncio.gather(*[r.reconfigure.remote(spec["user_config"])
                                            for r in st.replicas.values()])
@@ -75,7 +80,15 @@ class ServeController:
         self.apps[app_name] = {"route_prefix": route_prefix, "ingress": ingress,
                                "deployments": states, "status": "DEPLOYING"}
         await self._reconcile()
+        await self._push_routes(app_name)
         return True
+
+    async def _push_routes(self, app_name):
+        if self.proxy is not None:
+            try:
+                await self.proxy.invalidate_routes.remote(app_name)
+            except Exception:  # noqa: BLE001
+                pass
 
     async def _start_replica(self, st):
         spec = st.spec
@@ -91,6 +104,15 @@ class ServeController:
                                        spec["is_function"], spec.get("asgi_app"))
         st.replicas[rid] = h
         return rid, h
+
+    async def _drain(self, st, replicas):
+        """Stop replicas that are no longer routed to, after their in-flight requests."""
+        saved = st.replicas
+        st.replicas = dict(replicas)
+        try:
+            await self._stop_replicas(st, list(replicas))
+        finally:
+            st.replicas = saved
 
     async def _stop_replicas(self, st, rids):
         for rid in rids:
@@ -122,6 +144,9 @@ class ServeController:
                             st.replicas.pop(rid, None)
                         all_ok = False
                     st.version += 1
+                    if st.retiring and st.status == "HEALTHY":
+                        old, st.retiring = st.retiring, {}
+                        await self._drain(st, old)
                 elif diff < 0:
                     await self._stop_replicas(st, list(st.replicas)[:(-diff)])
                     st.status = "HEALTHY"
@@ -195,7 +220,9 @@ class ServeController:
         if app is None or deployment_name not in app["deployments"]:
             return None
         st = app["deployments"][deployment_name]
-        return st.version, list(st.replicas.items()), st.spec.get("max_ongoing_requests", 100)
+        # during a rolling update the old version serves until the new one is up
+        reps = st.replicas if st.replicas or not st.retiring else st.retiring
+        return st.version, list(reps.items()), st.spec.get("max_ongoing_requests", 100)
 
     def get_routes(self):
         return {a["route_prefix"]: (name, a["ingress"]) for name, a in self.apps.items()
@@ -209,7 +236,11 @@ class ServeController:
         app = self.apps.pop(app_name, None)
         if app:
             for st in list(app["deployments"].values()):
+                if st.retiring:
+                    old, st.retiring = st.retiring, {}
+                    await self._drain(st, old)
                 await self._stop_replicas(st, list(st.replicas))
+            await self._push_routes(app_name)
         return True
 
     def status(self):

@@ -82,31 +82,59 @@ class HTTPProxy:
             if prefix != "/":
                 fwd["root_path"] = ""
                 fwd["path"] = scope["path"][len(prefix):] or "/"
-            from ray_amd.serve.handle import _router
+            from ray_amd.serve.handle import _is_replica_death, _router
 
             r = _router(app_name, ingress)
-            rid, h = await r.achoose()
-            self.inflight += 1
-            try:
-                gen = h.handle_http_streaming.remote(fwd, body)
-                async for ref in gen:
-                    msg = await ref
-                    if msg[0] == "start":
-                        await send({"type": "http.response.start", "status": msg[1],
-                                    "headers": [(k.encode(), v.encode()) for k, v in msg[2]]})
-                        started = True
-                    else:
-                        await send({"type": "http.response.body", "body": msg[1],
-                                    "more_body": True})
-                if not started:
-                    raise RuntimeError("replica produced no response")
-                await send({"type": "http.response.body", "body": b"", "more_body": False})
-            finally:
-                self.inflight -= 1
-                r.done(rid)
+            for attempt in range(2):
+                try:
+                    rid, h = await r.achoose()
+                except RuntimeError:  # the app was deleted since the routes were read
+                    self.routes_ts = 0.0
+                    await self._arefresh()
+                    if self._match(scope["path"]) is None:
+                        await self._reply(send, 404, [("content-type", "text/plain")],
+                                          f"Path '{scope['path']}' not found".encode())
+                        return
+                    raise
+                self.inflight += 1
+                try:
+                    gen = h.handle_http_streaming.remote(fwd, body)
+                    async for ref in gen:
+                        msg = await ref
+                        if msg[0] == "start":
+                            await send({"type": "http.response.start", "status": msg[1],
+                                        "headers": [(k.encode(), v.encode())
+                                                    for k, v in msg[2]]})
+                            started = True
+                        else:
+                            await send({"type": "http.response.body", "body": msg[1],
+                                        "more_body": True})
+                    if not started:
+                        raise RuntimeError("replica produced no response")
+                    await send({"type": "http.response.body", "body": b"",
+                                "more_body": False})
+                    return
+                except Exception as e:  # noqa: BLE001
+                    # the replica died before answering (redeploy / scale-down raced the
+                    # cached routing table): once more on a freshly read replica set
+                    if started or attempt or not _is_replica_death(e):
+                        raise
+                    await r.arefresh(force=True)
+                finally:
+                    self.inflight -= 1
+                    r.done(rid)
         except Exception as e:  # noqa: BLE001
             if not started:
                 await self._reply(send, 500, [("content-type", "text/plain")], repr(e).encode())
+
+    def invalidate_routes(self, app_name=None):
+        """Pushed by the controller after a deploy or delete."""
+        self.routes_ts = 0.0
+        if app_name is not None:
+            from ray_amd.serve.handle import invalidate
+
+            invalidate(app_name)
+        return True
 
     @staticmethod
     async def _reply(send, status, headers, out):

@@ -168,6 +168,20 @@ def _to_http_response(result):
     return 200, [("content-type", "application/json")], json.dumps(result).encode()
 
 
+async def _resolve_args(args, kwargs):
+    """DeploymentResponses passed as arguments arrive as ObjectRefs inside the request's
+    args/kwargs: resolve them to values before the user method runs (reference: the
+    router resolves DeploymentResponse arguments before assignment)."""
+    from ray_amd.object_ref import ObjectRef
+
+    if not any(isinstance(a, ObjectRef) for a in args) and \
+            not any(isinstance(v, ObjectRef) for v in kwargs.values()):
+        return args, kwargs
+    args = [await a if isinstance(a, ObjectRef) else a for a in args]
+    kwargs = {k: (await v if isinstance(v, ObjectRef) else v) for k, v in kwargs.items()}
+    return tuple(args), kwargs
+
+
 class Replica:
     def __init__(self, deployment_name, app_name, callable_blob, init_args, init_kwargs,
                  user_config, replica_id, is_function, asgi_app_blob):
@@ -231,6 +245,7 @@ class Replica:
         self.total += 1
         token = context._set_request_context(multiplexed_model_id)
         try:
+            args, kwargs = await _resolve_args(args, kwargs)
             if self.is_function:
                 fn = self.obj
             else:
@@ -271,6 +286,7 @@ class Replica:
         self.total += 1
         token = context._set_request_context(multiplexed_model_id)
         try:
+            args, kwargs = await _resolve_args(args, kwargs)
             fn = self.obj if self.is_function else getattr(self.obj, method_name or "__call__")
             r = fn(*args, **kwargs)
             if inspect.isawaitable(r):

@@ -239,6 +239,9 @@ def run(target: Application, *, name: str = "default", route_prefix: str | None 
     handle = _build(target, name, specs)
     rp = target.deployment.route_prefix or route_prefix
     ray.get(c.deploy_application.remote(name, rp, target.deployment.name, list(specs.values())))
+    from ray_amd.serve import handle as H
+
+    H.invalidate(name)  # this process's routers re-read the new replica sets
     st = ray.get(c.status.remote()).get(name, {})
     if st.get("status") == "DEPLOY_FAILED":
         errs = {d: s["status"] for d, s in st.get("deployments", {}).items()}
@@ -251,6 +254,9 @@ def run(target: Application, *, name: str = "default", route_prefix: str | None 
 
 def delete(name: str, _blocking: bool = True):
     ray.get(_get_controller().delete_application.remote(name))
+    from ray_amd.serve import handle as H
+
+    H.invalidate(name)
 
 
 def shutdown():

@@ -25,6 +25,7 @@ class _Router:
         self.max_ongoing = 100
         self.lock = threading.Lock()
         self.last_refresh = 0.0
+        self.affinity = {}  # multiplexed model id -> replica that loaded it
 
     def _controller(self):
         from ray_amd.serve.api import _get_controller
@@ -63,7 +64,7 @@ class _Router:
                 self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
             self.max_ongoing = mo
 
-    async def achoose(self):
+    async def achoose(self, model_id=""):
         """choose() for event loops: the replica-set refresh is awaited, never blocks."""
         deadline = time.time() + 30
         await self.arefresh()
@@ -72,9 +73,9 @@ class _Router:
                 raise RuntimeError(f"no replicas available for {self.dep}")
             await asyncio.sleep(0.05)
             await self.arefresh(force=True)
-        return self._pick()
+        return self._pick(model_id)
 
-    def choose(self):
+    def choose(self, model_id=""):
         deadline = time.time() + 30
         while True:
             self.refresh()
@@ -86,17 +87,25 @@ class _Router:
                 raise RuntimeError(f"no replicas available for {self.dep}")
             time.sleep(0.05)
             self.refresh(force=True)
-        return self._pick()
+        return self._pick(model_id)
 
-    def _pick(self):
+    def _pick(self, model_id=""):
         with self.lock:
             reps = list(self.replicas)
-        if len(reps) == 1:
-            rid, h = reps[0]
-        else:
-            a, b = random.sample(reps, 2)
-            rid, h = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
-        with self.lock:
+            # multiplexed requests stick to the replica that already loaded the model
+            # while it is below max_ongoing_requests (reference: replica_scheduler
+            # multiplexed-model matching before power-of-two choices)
+            prev = self.affinity.get(model_id) if model_id else None
+            hit = next((x for x in reps if x[0] == prev), None)
+            if hit is not None and self.inflight.get(prev, 0) < self.max_ongoing:
+                rid, h = hit
+            elif len(reps) == 1:
+                rid, h = reps[0]
+            else:
+                a, b = random.sample(reps, 2)
+                rid, h = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
+            if model_id:
+                self.affinity[model_id] = rid
             self.inflight[rid] = self.inflight.get(rid, 0) + 1
         return rid, h
 
@@ -118,30 +127,67 @@ def _router(app, dep):
         return r
 
 
+def invalidate(app):
+    """Drop this process's cached replica sets of `app` (after a redeploy / delete)."""
+    with _rlock:
+        for key in [k for k in _routers if k[0] == app]:
+            del _routers[key]
+
+
+def _is_replica_death(e) -> bool:
+    from ray_amd.exceptions import RayActorError
+
+    return isinstance(e, RayActorError)
+
+
 class DeploymentResponse:
-    def __init__(self, ref, router, rid):
+    """``resend`` re-issues the request on a freshly chosen replica: used once when the
+    replica died before answering (a redeploy / scale-down raced the cached routing
+    table; reference: the router retries requests whose replica became unavailable)."""
+
+    def __init__(self, ref, router, rid, resend=None):
         self._ref = ref
         self._router = router
         self._rid = rid
         self._done = False
+        self._resend = resend
 
     def _finish(self):
         if not self._done:
             self._done = True
             self._router.done(self._rid)
 
+    def _retry(self):
+        self._finish()
+        self._router.refresh(force=True)
+        again, self._resend = self._resend(), None
+        self._ref, self._rid, self._done = again._ref, again._rid, False
+
     def result(self, timeout_s: float | None = None):
-        try:
-            return ray.get(self._ref, timeout=timeout_s)
-        finally:
-            self._finish()
+        while True:
+            try:
+                return ray.get(self._ref, timeout=timeout_s)
+            except Exception as e:  # noqa: BLE001
+                if self._resend is None or not _is_replica_death(e):
+                    raise
+                self._retry()
+            finally:
+                self._finish()
 
     def __await__(self):
         async def _w():
-            try:
-                return await self._ref
-            finally:
-                self._finish()
+            while True:
+                try:
+                    return await self._ref
+                except Exception as e:  # noqa: BLE001
+                    if self._resend is None or not _is_replica_death(e):
+                        raise
+                    self._finish()
+                    await self._router.arefresh(force=True)
+                    again, self._resend = self._resend(), None
+                    self._ref, self._rid, self._done = again._ref, again._rid, False
+                finally:
+                    self._finish()
 
         return _w().__await__()
 
@@ -234,7 +280,7 @@ class DeploymentHandle:
 
     def remote(self, *args, **kwargs):
         r = _router(self.app_name, self.deployment_name)
-        rid, h = r.choose()
+        rid, h = r.choose(self._mux)
         args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
         kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v)
                   for k, v in kwargs.items()}
@@ -242,6 +288,11 @@ class DeploymentHandle:
             gen = h.handle_request_streaming.remote(self._method or "__call__", args, kwargs,
                                                     self._mux)
             return DeploymentResponseGenerator(gen, r, rid)
+        ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
+        return DeploymentResponse(ref, r, rid, resend=lambda: self._send(r, args, kwargs))
+
+    def _send(self, r, args, kwargs):
+        rid, h = r.choose(self._mux)
         ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
         return DeploymentResponse(ref, r, rid)
 
