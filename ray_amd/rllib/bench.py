@@ -34,12 +34,14 @@ def bench_ppo(args):
     # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
     runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
     sample_async = os.environ.get("RAY_AMD_PPO_ASYNC", "0") == "1"
+    # CPU threads per env runner (torch intra-op threads for the Nature-CNN inference)
+    runner_cpus = float(os.environ.get("RAY_AMD_RUNNER_CPUS", "1"))
     # rollout_fragment_length "auto": 5000 / (runners x 5 envs) per env, so one sampling
     # round is exactly train_batch_size env steps (atari-ppo.yaml uses 10 x 5 x 100)
     cfg = (PPOConfig().environment("SyntheticAtari-v0")
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=5,
                         rollout_fragment_length="auto", num_gpus_per_env_runner=runner_gpus,
-                        sample_async=sample_async)
+                        num_cpus_per_env_runner=runner_cpus, sample_async=sample_async)
            .training(train_batch_size=5000 * n_gpus, minibatch_size=500, num_epochs=10,
                      lr=1e-4, lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
                      entropy_coeff=0.01, model={"vf_share_layers": True})
@@ -72,7 +74,8 @@ def bench_ppo(args):
                    "rollout_fragment_length": algo.config.rollout_fragment_length,
                    "minibatch_size": 500, "num_epochs": 10,
                    "parallelism": f"{n_gpus} learner{'s' if n_gpus > 1 else ''}",
-                   "env_runner_gpus": runner_gpus, "sample_async": sample_async},
+                   "env_runner_gpus": runner_gpus, "env_runner_cpus": runner_cpus,
+                   "sample_async": sample_async},
         "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
                                                      "sample_time_s", "sample_wait_s",
                                                      "learn_time_s", "sync_time_s")},
