@@ -290,13 +290,19 @@ def _splitk(M: int, N: int, K: int) -> int:
     batched kernels fill the 256 CUs only with many (N/256)*(K/256)*S tiles. Slices
     stay >= 2048 tokens so each batch GEMM keeps a long K loop."""
     S = 1
+    # RAY_AMD_WGRAD_TILES > 0: stop splitting once the batched GEMM has that many 256x256
+    # output tiles (one wave of the 256 CUs): more splits only add fp32 partial traffic,
+    # which competes with the main stream's memory-bound backward kernels
+    tiles = ((N + 255) // 256) * ((K + 255) // 256)
     while (S < _WGRAD_MAX_SPLITS and M % (2 * S) == 0 and M // (2 * S) >= 2048
-           and 2 * S * N * K * 4 <= _WGRAD_PART_BYTES):
+           and 2 * S * N * K * 4 <= _WGRAD_PART_BYTES
+           and not (_WGRAD_TILES and tiles * S >= _WGRAD_TILES)):
         S *= 2
     return S
 
 
 _WGRAD_MAX_SPLITS = int(os.environ.get("RAY_AMD_WGRAD_SPLITS", "16"))
+_WGRAD_TILES = int(os.environ.get("RAY_AMD_WGRAD_TILES", "0"))
 # cap on the fp32 split-K partials of one weight gradient: every partial byte is written by
 # the GEMM and read back by ra_splitk_accum while the main stream's memory-bound backward
 # kernels compete for HBM
