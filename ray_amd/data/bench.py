@@ -69,10 +69,25 @@ def _ingest_loop(config):
         step()
     torch.cuda.synchronize(dev)
     dist.barrier()
+    prof = None
+    if os.environ.get("RAY_AMD_DATA_PROFILE") == "1":  # cProfile of the timed loop
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     n = sum(step() for _ in range(steps))
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    if prof is not None:
+        import io
+        import pstats
+        import sys
+
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(30)
+        print(buf.getvalue(), file=sys.stderr, flush=True)
     t = torch.tensor([float(n), dt], device=dev, dtype=torch.float64)
     allt = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(allt, t)
