@@ -26,6 +26,7 @@ class _Session:
         self.cw = cw
         self.refs = {}
         self.actors = {}
+        self.gens = {}  # streaming task id -> server-side ObjectRefGenerator
 
     def dumps(self, obj):
         def on_ref(r):
@@ -47,9 +48,29 @@ class _Session:
         return common.loads(data, load)
 
     def keep(self, refs):
+        from ray_amd.object_ref import ObjectRefGenerator
+
+        if isinstance(refs, ObjectRefGenerator):  # streaming: items fetched by gen_next
+            self.gens[refs._task_id] = refs
+            return ("gen", refs._task_id)
         for r in refs:
             self.refs[r._id] = r
         return [r._id for r in refs]
+
+    def op_gen_next(self, tid, index, timeout):
+        gen = self.gens[tid]
+        ref = self.cw.next_stream_item(tid, index, timeout)
+        if ref is None:
+            return None
+        gen._index = index + 1
+        self.refs[ref._id] = ref
+        return ref._id
+
+    def op_gen_done(self, tid):
+        return self.cw.stream_completed_ref(tid)
+
+    def op_gen_drop(self, tid):
+        self.gens.pop(tid, None)
 
     # ---------------------------------------------------------------- ops
     def op_init(self, namespace, runtime_env):
@@ -142,6 +163,7 @@ def _serve_conn(conn, cw):
     finally:
         s.refs.clear()
         s.actors.clear()
+        s.gens.clear()
         conn.close()
 
 

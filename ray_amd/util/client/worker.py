@@ -125,20 +125,36 @@ class ClientCoreWorker:
     def wait_refs(self, oids, num_returns, timeout):
         return set(self._call("wait", list(oids), num_returns, timeout))
 
+    def _maybe_stream(self, out):
+        """A streaming task answers with ("gen", task id): the generator lives in the
+        server session and each item is fetched with one round trip."""
+        if isinstance(out, tuple) and out and out[0] == "gen":
+            from ray_amd.object_ref import ObjectRefGenerator
+
+            return ObjectRefGenerator(out[1], self, self.addr)
+        return self._refs(out)
+
     def submit_task(self, fn_key, args, kwargs, opts, name):
-        if opts.get("num_returns") == "streaming":
-            raise NotImplementedError("streaming generators are not supported over Ray Client")
-        return self._refs(self._call("task", fn_key, self._dumps((args, kwargs)), opts, name))
+        return self._maybe_stream(self._call("task", fn_key, self._dumps((args, kwargs)), opts,
+                                             name))
+
+    def next_stream_item(self, tid, index, timeout):
+        oid = self._call("gen_next", tid, index, timeout)
+        return None if oid is None else self._refs([oid])[0]
+
+    def stream_completed_ref(self, tid):
+        return self._call("gen_done", tid)
+
+    def drop_stream(self, tid):
+        self._release("gen_drop", tid)
 
     def create_actor(self, actor_id, cls_key, args, kwargs, opts, cls_name, meta):
         return self._call("actor", actor_id, cls_key, self._dumps((args, kwargs)), opts,
                           cls_name, meta)
 
     def submit_actor_task(self, actor_id, method, args, kwargs, opts):
-        if opts.get("num_returns") == "streaming":
-            raise NotImplementedError("streaming generators are not supported over Ray Client")
-        return self._refs(self._call("actor_task", actor_id, method,
-                                     self._dumps((args, kwargs)), opts))
+        return self._maybe_stream(self._call("actor_task", actor_id, method,
+                                             self._dumps((args, kwargs)), opts))
 
     def kill_actor(self, actor_id, no_restart=True):
         self._call("kill", actor_id, no_restart)

@@ -86,6 +86,24 @@ CLIENT = textwrap.dedent("""
     c2 = ray.get_actor("ctr")
     assert ray.get(c2.inc.remote(5)) == 18
     assert ray.cluster_resources()["CPU"] == 4
+
+    @ray.remote
+    def gen(n):
+        for i in range(n):
+            yield i * i
+
+    g = gen.options(num_returns="streaming").remote(5)
+    assert [ray.get(r) for r in g] == [0, 1, 4, 9, 16]         # streaming over the client
+
+    @ray.remote
+    class Streamer:
+        def items(self, n):
+            for i in range(n):
+                yield {"i": i}
+
+    st = Streamer.remote()
+    assert [ray.get(r)["i"] for r in st.items.options(num_returns="streaming").remote(3)] == \
+        [0, 1, 2]
     ray.kill(c)
     try:
         ray.get(c.inc.remote(), timeout=20)
