@@ -67,7 +67,7 @@ class _QLearner:
         if self.cfg.get("grad_clip"):
             torch.nn.utils.clip_grad_norm_(self.q.parameters(), self.cfg["grad_clip"])
         self.opt.step()
-        return float(loss), td.detach().abs().cpu().numpy()
+        return float(loss.detach()), td.detach().abs().cpu().numpy()
 
     def sync_target(self):
         self.target.load_state_dict(self.q.state_dict())
