@@ -172,9 +172,16 @@ class ServeController:
                     "target_num_ongoing_requests_per_replica", 2))
                 desired = math.ceil(total / max(tgt, 1e-9)) if total else \
                     asc.get("min_replicas", 1)
+                cur = len(st.replicas)
+                # gain on each decision (reference: AutoscalingConfig.upscaling_factor /
+                # downscaling_factor): move only that fraction of the way to the target
+                if desired > cur and asc.get("upscaling_factor"):
+                    desired = cur + math.ceil((desired - cur) * asc["upscaling_factor"])
+                elif desired < cur and asc.get("downscaling_factor"):
+                    desired = cur - max(1, math.floor((cur - desired) *
+                                                      asc["downscaling_factor"]))
                 desired = max(asc.get("min_replicas", 1), min(asc.get("max_replicas", 10),
                                                               desired))
-                cur = len(st.replicas)
                 if desired > cur:
                     st.under_since = None
                     st.over_since = st.over_since or now
@@ -222,7 +229,8 @@ class ServeController:
         st = app["deployments"][deployment_name]
         # during a rolling update the old version serves until the new one is up
         reps = st.replicas if st.replicas or not st.retiring else st.retiring
-        return st.version, list(reps.items()), st.spec.get("max_ongoing_requests", 100)
+        return (st.version, list(reps.items()), st.spec.get("max_ongoing_requests", 100),
+                st.spec.get("max_queued_requests", -1))
 
     def get_routes(self):
         return {a["route_prefix"]: (name, a["ingress"]) for name, a in self.apps.items()

@@ -82,12 +82,17 @@ class HTTPProxy:
             if prefix != "/":
                 fwd["root_path"] = ""
                 fwd["path"] = scope["path"][len(prefix):] or "/"
+            from ray_amd.serve.exceptions import BackPressureError
             from ray_amd.serve.handle import _is_replica_death, _router
 
             r = _router(app_name, ingress)
             for attempt in range(2):
                 try:
                     rid, h = await r.achoose()
+                except BackPressureError as e:
+                    await self._reply(send, 503, [("content-type", "text/plain")],
+                                      e.message.encode())
+                    return
                 except RuntimeError:  # the app was deleted since the routes were read
                     self.routes_ts = 0.0
                     await self._arefresh()

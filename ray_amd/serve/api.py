@@ -111,19 +111,26 @@ class Deployment:
     def __init__(self, func_or_class, name, num_replicas=1, ray_actor_options=None,
                  user_config=None, max_ongoing_requests=100, autoscaling_config=None,
                  route_prefix=None, graceful_shutdown_timeout_s=5.0, health_check_period_s=10.0,
-                 version=None, **kw):
+                 version=None, max_queued_requests=-1, **kw):
+        from ray_amd.serve.config import normalize_autoscaling_config
+
         self.func_or_class = func_or_class
         self.name = name
         if num_replicas == "auto":
-            autoscaling_config = autoscaling_config or {"min_replicas": 1, "max_replicas": 100}
+            autoscaling_config = autoscaling_config or {"min_replicas": 1, "max_replicas": 100,
+                                                        "target_ongoing_requests": 2.0}
             num_replicas = 1
+        if max_queued_requests != -1 and max_queued_requests < 1:
+            raise ValueError("max_queued_requests must be -1 (no limit) or a positive int")
         self.num_replicas = num_replicas
         self.ray_actor_options = ray_actor_options or {}
         self.user_config = user_config
         self.max_ongoing_requests = max_ongoing_requests
-        self.autoscaling_config = dict(autoscaling_config) if autoscaling_config else None
+        self.max_queued_requests = max_queued_requests
+        self.autoscaling_config = normalize_autoscaling_config(autoscaling_config)
         self.route_prefix = route_prefix
         self.graceful_shutdown_timeout_s = graceful_shutdown_timeout_s
+        self.health_check_period_s = health_check_period_s
         self.version = version
 
     def options(self, **kw):
@@ -131,6 +138,8 @@ class Deployment:
                  user_config=self.user_config, max_ongoing_requests=self.max_ongoing_requests,
                  autoscaling_config=self.autoscaling_config, route_prefix=self.route_prefix,
                  graceful_shutdown_timeout_s=self.graceful_shutdown_timeout_s,
+                 health_check_period_s=self.health_check_period_s,
+                 max_queued_requests=self.max_queued_requests,
                  version=self.version, name=self.name)
         if "max_concurrent_queries" in kw:
             kw["max_ongoing_requests"] = kw.pop("max_concurrent_queries")
@@ -155,14 +164,15 @@ class Application:
 def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_options=None,
                user_config=None, max_ongoing_requests=100, max_concurrent_queries=None,
                autoscaling_config=None, route_prefix=None, graceful_shutdown_timeout_s=5.0,
-               health_check_period_s=10.0, version=None, **kw):
+               health_check_period_s=10.0, version=None, max_queued_requests=-1, **kw):
     if max_concurrent_queries is not None:
         max_ongoing_requests = max_concurrent_queries
 
     def deco(fc):
         return Deployment(fc, name or fc.__name__, num_replicas, ray_actor_options, user_config,
                           max_ongoing_requests, autoscaling_config, route_prefix,
-                          graceful_shutdown_timeout_s, health_check_period_s, version)
+                          graceful_shutdown_timeout_s, health_check_period_s, version,
+                          max_queued_requests=max_queued_requests)
 
     if _func_or_class is not None and callable(_func_or_class):
         return deco(_func_or_class)
@@ -223,6 +233,7 @@ def _build(app: Application, app_name, specs: dict):
         "init_args": args, "init_kwargs": kwargs, "num_replicas": dep.num_replicas,
         "autoscaling_config": dep.autoscaling_config, "ray_actor_options": dep.ray_actor_options,
         "user_config": dep.user_config, "max_ongoing_requests": dep.max_ongoing_requests,
+        "max_queued_requests": dep.max_queued_requests,
         "asgi_app": cloudpickle.dumps(asgi) if asgi is not None else None,
         "graceful_shutdown_timeout_s": dep.graceful_shutdown_timeout_s,
         "code_version": dep.version or hashlib.blake2b(blob, digest_size=8).hexdigest(),

@@ -1,0 +1,39 @@
+"""Serve exceptions (reference: python/ray/serve/exceptions.py)."""
+
+from __future__ import annotations
+
+
+class RayServeException(Exception):
+    pass
+
+
+class BackPressureError(RayServeException):
+    """A handle already holds ``max_queued_requests`` requests waiting for a replica slot
+    (every replica at ``max_ongoing_requests``); the proxy answers HTTP 503."""
+
+    def __init__(self, *, num_queued_requests: int, max_queued_requests: int):
+        self._message = (f"Request dropped due to backpressure "
+                         f"(num_queued_requests={num_queued_requests}, "
+                         f"max_queued_requests={max_queued_requests}).")
+        self.num_queued_requests = num_queued_requests
+        self.max_queued_requests = max_queued_requests
+        super().__init__(self._message)
+
+    @property
+    def message(self) -> str:
+        return self._message
+
+    def __reduce__(self):
+        return (_rebuild_backpressure, (self.num_queued_requests, self.max_queued_requests))
+
+
+def _rebuild_backpressure(n, m):
+    return BackPressureError(num_queued_requests=n, max_queued_requests=m)
+
+
+class RequestCancelledError(RayServeException):
+    """The request was cancelled (``DeploymentResponse.cancel()``) before it finished."""
+
+
+class DeploymentUnavailableError(RayServeException):
+    """No replica of the deployment became available within the handle's wait."""

@@ -23,7 +23,12 @@ class _Router:
         self.replicas = []  # [(rid, handle)]
         self.inflight = {}
         self.max_ongoing = 100
+        self.max_queued = -1
+        self.queued = 0  # requests of this handle waiting for a replica slot
         self.lock = threading.Lock()
+        self.slot_freed = threading.Condition(self.lock)
+        self.pending = []  # [(future, send, model_id)] waiting for a slot, FIFO
+        self.dispatching = False
         self.last_refresh = 0.0
         self.affinity = {}  # multiplexed model id -> replica that loaded it
 
@@ -40,13 +45,18 @@ class _Router:
         self.last_refresh = now
         if info is None:
             raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
-        version, reps, mo = info
+        self._install(info)
+
+    def _install(self, info):
+        version, reps, mo, mq = info
         with self.lock:
             if version != self.version:
                 self.version = version
                 self.replicas = reps
                 self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
             self.max_ongoing = mo
+            self.max_queued = mq
+            self.slot_freed.notify_all()
 
     async def arefresh(self, force=False):
         now = time.time()
@@ -56,16 +66,103 @@ class _Router:
         self.last_refresh = now
         if info is None:
             raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
-        version, reps, mo = info
+        self._install(info)
+
+    def _admit(self):
+        """Count this request as queued, or raise BackPressureError when the handle's
+        queue is full (reference: max_queued_requests in the replica scheduler)."""
+        waiting = self.queued + len(self.pending)
+        if self.max_queued != -1 and waiting >= self.max_queued:
+            from ray_amd.serve.exceptions import BackPressureError
+
+            raise BackPressureError(num_queued_requests=waiting,
+                                    max_queued_requests=self.max_queued)
+        self.queued += 1
+
+    def assign(self, send, model_id=""):
+        """Non-blocking routing for DeploymentHandle.remote: ``(rid, send(h))`` when a
+        replica has a free slot, else a Future of it that the dispatcher thread fulfils
+        in arrival order as slots free up (or fails with BackPressureError)."""
+        import concurrent.futures
+
+        self.choose_wait_for_replicas()
         with self.lock:
-            if version != self.version:
-                self.version = version
-                self.replicas = reps
-                self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
-            self.max_ongoing = mo
+            got = None if self.pending else self._pick(model_id)
+            if got is None:
+                fut = concurrent.futures.Future()
+                try:
+                    self._admit()
+                    self.queued -= 1  # counted as pending instead
+                except Exception as e:  # noqa: BLE001  (BackPressureError)
+                    fut.set_exception(e)
+                    return fut
+                self.pending.append((fut, send, model_id))
+                if not self.dispatching:
+                    self.dispatching = True
+                    threading.Thread(target=self._dispatch, daemon=True,
+                                     name=f"serve-dispatch-{self.dep}").start()
+                return fut
+        slot = _Slot(self, got[0])
+        try:
+            ref = send(got[1])
+        except BaseException:
+            slot.release()
+            raise
+        _watch(slot, ref)
+        return slot, ref
+
+    def cancel_pending(self, fut) -> bool:
+        with self.lock:
+            for i, item in enumerate(self.pending):
+                if item[0] is fut:
+                    del self.pending[i]
+                    fut.cancel()
+                    return True
+        return False
+
+    def _dispatch(self):
+        while True:
+            ready = []
+            with self.lock:
+                if not self.pending:
+                    self.dispatching = False
+                    return
+                self.slot_freed.wait(0.05)
+                while self.pending:
+                    got = self._pick(self.pending[0][2])
+                    if got is None:
+                        break
+                    ready.append((self.pending.pop(0), got))
+            for (fut, send, _), (rid, h) in ready:
+                slot = _Slot(self, rid)
+                try:
+                    ref = send(h)
+                except BaseException as e:  # noqa: BLE001
+                    slot.release()
+                    fut.set_exception(e)
+                    continue
+                _watch(slot, ref)
+                fut.set_result((slot, ref))
+            try:
+                self.refresh()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def choose_wait_for_replicas(self):
+        deadline = time.time() + 30
+        while True:
+            self.refresh()
+            with self.lock:
+                if self.replicas:
+                    return
+            if time.time() > deadline:
+                raise RuntimeError(f"no replicas available for {self.dep}")
+            time.sleep(0.05)
+            self.refresh(force=True)
 
     async def achoose(self, model_id=""):
-        """choose() for event loops: the replica-set refresh is awaited, never blocks."""
+        """choose() for event loops: refreshes are awaited and a request waiting for a
+        replica slot yields to the loop instead of blocking it."""
         deadline = time.time() + 30
         await self.arefresh()
         while not self.replicas:
@@ -73,46 +170,70 @@ class _Router:
                 raise RuntimeError(f"no replicas available for {self.dep}")
             await asyncio.sleep(0.05)
             await self.arefresh(force=True)
-        return self._pick(model_id)
+        with self.lock:
+            got = self._pick(model_id)
+            if got is not None:
+                return got
+            self._admit()
+        try:
+            while True:
+                await asyncio.sleep(0.002)
+                await self.arefresh()
+                with self.lock:
+                    got = self._pick(model_id)
+                if got is not None:
+                    return got
+        finally:
+            with self.lock:
+                self.queued -= 1
 
     def choose(self, model_id=""):
-        deadline = time.time() + 30
-        while True:
-            self.refresh()
+        self.choose_wait_for_replicas()
+        with self.lock:
+            got = self._pick(model_id)
+            if got is not None:
+                return got
+            self._admit()
+        try:
+            while True:
+                with self.lock:
+                    self.slot_freed.wait(0.1)
+                    got = self._pick(model_id)
+                if got is not None:
+                    return got
+                self.refresh()
+        finally:
             with self.lock:
-                reps = list(self.replicas)
-            if reps:
-                break
-            if time.time() > deadline:
-                raise RuntimeError(f"no replicas available for {self.dep}")
-            time.sleep(0.05)
-            self.refresh(force=True)
-        return self._pick(model_id)
+                self.queued -= 1
 
     def _pick(self, model_id=""):
-        with self.lock:
-            reps = list(self.replicas)
-            # multiplexed requests stick to the replica that already loaded the model
-            # while it is below max_ongoing_requests (reference: replica_scheduler
-            # multiplexed-model matching before power-of-two choices)
-            prev = self.affinity.get(model_id) if model_id else None
-            hit = next((x for x in reps if x[0] == prev), None)
-            if hit is not None and self.inflight.get(prev, 0) < self.max_ongoing:
-                rid, h = hit
-            elif len(reps) == 1:
-                rid, h = reps[0]
-            else:
-                a, b = random.sample(reps, 2)
-                rid, h = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
-            if model_id:
-                self.affinity[model_id] = rid
-            self.inflight[rid] = self.inflight.get(rid, 0) + 1
+        """Caller holds self.lock. A replica below max_ongoing_requests, or None when all
+        are at capacity (the request then waits at the handle, as in the reference)."""
+        reps = [x for x in self.replicas if self.inflight.get(x[0], 0) < self.max_ongoing]
+        if not reps:
+            return None
+        # multiplexed requests stick to the replica that already loaded the model
+        # while it is below max_ongoing_requests (reference: replica_scheduler
+        # multiplexed-model matching before power-of-two choices)
+        prev = self.affinity.get(model_id) if model_id else None
+        hit = next((x for x in reps if x[0] == prev), None)
+        if hit is not None:
+            rid, h = hit
+        elif len(reps) == 1:
+            rid, h = reps[0]
+        else:
+            a, b = random.sample(reps, 2)
+            rid, h = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
+        if model_id:
+            self.affinity[model_id] = rid
+        self.inflight[rid] = self.inflight.get(rid, 0) + 1
         return rid, h
 
     def done(self, rid):
         with self.lock:
             if rid in self.inflight:
                 self.inflight[rid] = max(0, self.inflight[rid] - 1)
+            self.slot_freed.notify()
 
 
 _routers: dict = {}
@@ -140,69 +261,120 @@ def _is_replica_death(e) -> bool:
     return isinstance(e, RayActorError)
 
 
+class _Slot:
+    """One request's claim on a replica's max_ongoing_requests budget; released exactly
+    once, by whichever comes first: the reply landing or the caller finishing."""
+
+    __slots__ = ("router", "rid", "released")
+
+    def __init__(self, router, rid):
+        self.router, self.rid, self.released = router, rid, False
+
+    def release(self):
+        if not self.released:
+            self.released = True
+            self.router.done(self.rid)
+
+
+def _watch(slot: _Slot, ref) -> None:
+    """Release the slot when the reply lands, whether or not the caller ever reads it
+    (fire-and-forget requests must not hold max_ongoing_requests slots)."""
+    cw = ref._cw
+    if cw is None or cw._on_ready(ref._id, lambda _oid, ref=ref: slot.release()):
+        slot.release()
+
+
 class DeploymentResponse:
-    """``resend`` re-issues the request on a freshly chosen replica: used once when the
+    """Reply of one handle call. The request may still wait at the handle for a replica
+    slot (every replica at ``max_ongoing_requests``): ``pending`` then resolves to
+    ``(slot, ref)`` once the router's dispatcher sends it, or raises BackPressureError
+    (``max_queued_requests`` exceeded) / is cancelled.
+
+    ``resend`` re-issues the request on a freshly chosen replica: used once when the
     replica died before answering (a redeploy / scale-down raced the cached routing
     table; reference: the router retries requests whose replica became unavailable)."""
 
-    def __init__(self, ref, router, rid, resend=None):
+    def __init__(self, ref, router, slot=None, resend=None, pending=None):
         self._ref = ref
         self._router = router
-        self._rid = rid
-        self._done = False
+        self._slot = slot
         self._resend = resend
+        self._pending = pending
+
+    def _assigned(self, timeout_s=None):
+        if self._pending is not None:
+            import concurrent.futures
+
+            try:
+                self._slot, self._ref = self._pending.result(timeout_s)
+            except concurrent.futures.TimeoutError:
+                raise ray.exceptions.GetTimeoutError(
+                    "request still queued at the handle") from None
+            except concurrent.futures.CancelledError:
+                from ray_amd.serve.exceptions import RequestCancelledError
+
+                raise RequestCancelledError("request cancelled while queued") from None
+            self._pending = None
+        return self._ref
 
     def _finish(self):
-        if not self._done:
-            self._done = True
-            self._router.done(self._rid)
+        if self._slot is not None:
+            self._slot.release()
 
-    def _retry(self):
+    def _adopt(self, again):
         self._finish()
-        self._router.refresh(force=True)
-        again, self._resend = self._resend(), None
-        self._ref, self._rid, self._done = again._ref, again._rid, False
+        again._assigned()
+        self._ref, self._slot = again._ref, again._slot
 
     def result(self, timeout_s: float | None = None):
         while True:
             try:
-                return ray.get(self._ref, timeout=timeout_s)
+                return ray.get(self._assigned(timeout_s), timeout=timeout_s)
             except Exception as e:  # noqa: BLE001
                 if self._resend is None or not _is_replica_death(e):
                     raise
-                self._retry()
+                self._router.refresh(force=True)
+                again, self._resend = self._resend(), None
+                self._adopt(again)
             finally:
                 self._finish()
 
     def __await__(self):
         async def _w():
+            if self._pending is not None:
+                await asyncio.wrap_future(self._pending)
             while True:
                 try:
-                    return await self._ref
+                    return await self._assigned()
                 except Exception as e:  # noqa: BLE001
                     if self._resend is None or not _is_replica_death(e):
                         raise
-                    self._finish()
                     await self._router.arefresh(force=True)
                     again, self._resend = self._resend(), None
-                    self._ref, self._rid, self._done = again._ref, again._rid, False
+                    if again._pending is not None:
+                        await asyncio.wrap_future(again._pending)
+                    self._adopt(again)
                 finally:
                     self._finish()
 
         return _w().__await__()
 
     def _to_object_ref(self):
-        return self._ref
+        return self._assigned()
 
     async def _to_object_ref_async(self):
-        return self._ref
+        if self._pending is not None:
+            await asyncio.wrap_future(self._pending)
+        return self._assigned()
 
     def cancel(self):
-        ray.cancel(self._ref)
+        if self._pending is not None and self._router.cancel_pending(self._pending):
+            return
+        ray.cancel(self._assigned())
 
     def __reduce__(self):
         # passing a response to another deployment passes the underlying object
-        return (_resolve, (self._ref,))
+        return (_resolve, (self._assigned(),))
 
 
 def _resolve(ref):
@@ -280,21 +452,28 @@ class DeploymentHandle:
 
     def remote(self, *args, **kwargs):
         r = _router(self.app_name, self.deployment_name)
-        rid, h = r.choose(self._mux)
-        args = tuple(a._ref if isinstance(a, DeploymentResponse) else a for a in args)
-        kwargs = {k: (v._ref if isinstance(v, DeploymentResponse) else v)
+        args = tuple(a._to_object_ref() if isinstance(a, DeploymentResponse) else a
+                     for a in args)
+        kwargs = {k: (v._to_object_ref() if isinstance(v, DeploymentResponse) else v)
                   for k, v in kwargs.items()}
         if self._stream:
+            rid, h = r.choose(self._mux)
             gen = h.handle_request_streaming.remote(self._method or "__call__", args, kwargs,
                                                     self._mux)
             return DeploymentResponseGenerator(gen, r, rid)
-        ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
-        return DeploymentResponse(ref, r, rid, resend=lambda: self._send(r, args, kwargs))
+        return self._send(r, args, kwargs, resend=lambda: self._send(r, args, kwargs))
 
-    def _send(self, r, args, kwargs):
-        rid, h = r.choose(self._mux)
-        ref = h.handle_request.remote(self._method or "__call__", args, kwargs, self._mux)
-        return DeploymentResponse(ref, r, rid)
+    def _send(self, r, args, kwargs, resend=None):
+        method, mux = self._method or "__call__", self._mux
+
+        def send(h):
+            return h.handle_request.remote(method, args, kwargs, mux)
+
+        got = r.assign(send, mux)
+        if isinstance(got, tuple):
+            slot, ref = got
+            return DeploymentResponse(ref, r, slot, resend=resend)
+        return DeploymentResponse(None, r, resend=resend, pending=got)
 
     def __reduce__(self):
         return (DeploymentHandle, (self.deployment_name, self.app_name),
