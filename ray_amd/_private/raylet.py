@@ -396,11 +396,14 @@ class Raylet:
                 "resources": nrec["resources"], "head_node_id": self.node_hex}
         self.reply(conn, rid, True, info)
 
-    def rpc_set_job_info(self, conn, rid, job_id, sys_path, runtime_env):
+    def rpc_set_job_info(self, conn, rid, job_id, sys_path, runtime_env, job_config=None):
         j = self.jobs.get(job_id)
         if j is not None:
             j["sys_path"] = sys_path
             j["runtime_env"] = runtime_env
+            if job_config is not None:
+                j["metadata"] = dict(job_config.get("metadata") or {})
+                j["job_config"] = job_config
         self.reply(conn, rid, True, None)
 
     # ------------------------------------------------------------------ worker pool

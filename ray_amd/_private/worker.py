@@ -36,6 +36,7 @@ class Worker:
         self.lock = threading.RLock()
         self.namespace = None
         self.runtime_env = None
+        self.job_config = None
         self._local_mode = False
         self.dashboard_proc = None
         self.dashboard_url = None
@@ -121,6 +122,10 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
     from .core_worker import CoreWorker
     from .ids import random_bytes
 
+    if job_config is not None:
+        namespace = namespace or job_config.ray_namespace
+        if runtime_env is None and job_config.runtime_env:
+            runtime_env = dict(job_config.runtime_env)
     with _global_node_lock:
         if global_worker.connected:
             if ignore_reinit_error:
@@ -177,12 +182,22 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
         global_worker.session_dir = session
         global_worker.namespace = cw.namespace
         global_worker.runtime_env = runtime_env
+        global_worker.job_config = job_config
         sp = [os.path.abspath(p) if p else os.getcwd() for p in sys.path]
         main = sys.modules.get("__main__")
         if main is not None and getattr(main, "__file__", None):
             sp.insert(0, os.path.dirname(os.path.abspath(main.__file__)))
         sp.insert(0, os.getcwd())
-        cw.call_raylet("set_job_info", cw.job_id, sp, runtime_env)
+        if job_config is not None:
+            # code_search_path: importable in every worker of the job (first on the path)
+            sp = list(job_config.code_search_path) + sp
+            for p in reversed(job_config.code_search_path):
+                if p not in sys.path:
+                    sys.path.insert(0, p)
+            cw.call_raylet("set_job_info", cw.job_id, sp, runtime_env,
+                           job_config._to_dict())
+        else:
+            cw.call_raylet("set_job_info", cw.job_id, sp, runtime_env)
         atexit.register(shutdown)
         return RayContext(global_worker)
 

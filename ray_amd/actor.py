@@ -205,7 +205,8 @@ class ActorClass:
             "resources": _opt.resources_of(opts, actor=True),
             "strategy": _opt.strategy_of(opts),
             "name": opts.get("name"), "namespace": opts.get("namespace"),
-            "lifetime": opts.get("lifetime"), "max_restarts": opts.get("max_restarts", 0),
+            "lifetime": opts.get("lifetime") or _default_lifetime(),
+            "max_restarts": opts.get("max_restarts", 0),
             "max_task_retries": opts.get("max_task_retries", 0),
             "max_concurrency": max_conc, "concurrency_groups": groups,
             "runtime_env": opts.get("runtime_env"), "get_if_exists": opts.get("get_if_exists"),
@@ -219,6 +220,17 @@ class ActorClass:
         if o["name"] or o["lifetime"] == "detached":
             cw.actor_escaped.add(aid)
         return ActorHandle(aid, self._cls.__name__, self._meta, cw.addr)
+
+
+def _default_lifetime():
+    """JobConfig(default_actor_lifetime="detached") applies to actors created by the driver
+    (reference: job_config.py set_default_actor_lifetime)."""
+    from ray_amd._private import worker as W
+
+    jc = getattr(W.global_worker, "job_config", None)
+    if jc is not None and jc.default_actor_lifetime == "detached":
+        return "detached"
+    return None
 
 
 def exit_actor():

@@ -67,6 +67,9 @@ class ObjectRef:
         return (_rebuild_ref, (self._id, self._owner))
 
     # ---- futures / asyncio
+    def __class_getitem__(cls, item):  # ObjectRef[int] in annotations
+        return cls
+
     def future(self) -> concurrent.futures.Future:
         return self._cw.as_concurrent_future(self)
 

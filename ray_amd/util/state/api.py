@@ -171,7 +171,9 @@ def _job_rows(cw):
                      "status": j["status"], "driver_pid": j.get("driver_pid"),
                      "start_time": int(j["start_time"] * 1000),
                      "end_time": int(j["end_time"] * 1000) if j.get("end_time") else None,
-                     "namespace": j.get("namespace"), "type": "DRIVER"})
+                     "namespace": j.get("namespace"), "type": "DRIVER",
+                     "metadata": j.get("metadata") or {},
+                     "runtime_env": j.get("runtime_env") or {}})
     return rows
 
 
