@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "channel.h"
+#include "codec.h"
 #include "io_loop.h"
 #include "scheduler.h"
 #include "shm_store.h"
@@ -76,6 +77,36 @@ static void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
 
 PYBIND11_MODULE(_core, m) {
   m.doc() = "ray_amd native runtime core: shm object store, frame I/O loop, scheduler";
+
+  // ---- record codecs (Ray Data TFRecord read/write)
+  m.def("crc32c", [](py::buffer b, uint32_t init) {
+    py::buffer_info bi = b.request();
+    const auto* p = static_cast<const uint8_t*>(bi.ptr);
+    const size_t n = (size_t)bi.size * bi.itemsize;
+    py::gil_scoped_release r;
+    return crc32c(p, n, init);
+  }, py::arg("data"), py::arg("init") = 0u);
+  m.def("tfrecord_index", [](py::buffer b, bool verify) {
+    py::buffer_info bi = b.request();
+    const auto* p = static_cast<const uint8_t*>(bi.ptr);
+    const size_t n = (size_t)bi.size * bi.itemsize;
+    std::vector<std::pair<uint64_t, uint64_t>> idx;
+    {
+      py::gil_scoped_release r;
+      idx = tfrecord_index(p, n, verify);
+    }
+    return idx;
+  }, py::arg("data"), py::arg("verify") = true);
+  m.def("tfrecord_encode", [](const std::vector<py::bytes>& recs) {
+    std::string out;
+    for (const auto& r : recs) {
+      char* p;
+      Py_ssize_t n;
+      PyBytes_AsStringAndSize(r.ptr(), &p, &n);
+      tfrecord_append(&out, reinterpret_cast<const uint8_t*>(p), (size_t)n);
+    }
+    return py::bytes(out);
+  });
 
   // dst[:] = src (both contiguous buffers of equal byte size), split over threads with
   // the GIL released: staging a rollout batch into pinned host memory for the H2D copy

@@ -726,6 +726,18 @@ class Dataset:
         ray.get([_write_tar.remote(r, path, i, encoder)
                  for i, (r, _) in enumerate(X.execute(self._plan))])
 
+    def write_tfrecords(self, path: str, *, tf_schema=None, compression: str | None = None,
+                        **kw):
+        """One TFRecord file of tf.train.Example protos per block (data/tfrecords.py);
+        ``compression="gzip"`` writes ``.tfrecords.gz``."""
+        from ray_amd.data.tfrecords import _write_tfrecords_block
+
+        if tf_schema is not None:
+            raise NotImplementedError("tf_schema needs tensorflow_metadata (not installed)")
+        comp = compression or (kw.get("arrow_open_stream_args") or {}).get("compression")
+        ray.get([_write_tfrecords_block.remote(r, path, i, comp)
+                 for i, (r, _) in enumerate(X.execute(self._plan))])
+
     def write_images(self, path: str, column: str, file_format: str = "png", **kw):
         from ray_amd.data.datasource import _write_images_block
 

@@ -180,6 +180,20 @@ def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, include_paths=F
     return _file_ds(paths, None, rd, include_paths)
 
 
+def read_tfrecords(paths, *, include_paths=False, tf_schema=None, verify=True,
+                   arrow_open_stream_args=None, **kw) -> Dataset:
+    """TFRecord files of tf.train.Example protos (data/tfrecords.py); one block per file.
+    ``verify`` checks every record's CRC32C; ``arrow_open_stream_args={"compression":
+    "gzip"}`` (or a ``.gz`` suffix) reads compressed files."""
+    from ray_amd.data.tfrecords import read_file
+
+    if tf_schema is not None:
+        raise NotImplementedError("tf_schema needs tensorflow_metadata (not installed)")
+    comp = (arrow_open_stream_args or {}).get("compression")
+    return _file_ds(paths, [".tfrecords", ".tfrecord", ".gz"],
+                    lambda f: read_file(f, verify, comp), include_paths)
+
+
 def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
     def rd(f):
         with open(f, "rb") as fh:
