@@ -13,7 +13,7 @@ from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface
                                    from_pandas_refs, from_torch, range, range_tensor,
                                    read_binary_files, read_csv, read_datasource, read_images,
                                    read_json, read_numpy, read_parquet, read_parquet_bulk,
-                                   read_text, read_tfrecords)
+                                   read_text, read_tfrecords, read_avro)
 from ray_amd.data.datasource import (BlockBasedFileDatasink, Datasink,  # noqa: F401
                                      Datasource, RandomAccessDataset, ReadTask,
                                      RowBasedFileDatasink, read_sql, read_webdataset)

@@ -194,6 +194,14 @@ def read_tfrecords(paths, *, include_paths=False, tf_schema=None, verify=True,
                     lambda f: read_file(f, verify, comp), include_paths)
 
 
+def read_avro(paths, *, include_paths=False, **kw) -> Dataset:
+    """Avro object container files (data/avro.py): one block per file, a column per
+    top-level record field."""
+    from ray_amd.data.avro import read_file
+
+    return _file_ds(paths, [".avro"], read_file, include_paths)
+
+
 def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
     def rd(f):
         with open(f, "rb") as fh:
