@@ -53,8 +53,10 @@ def parse():
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="flat gradient buffer / all-reduce dtype; bf16 = explicit gradient "
                          "compression")
-    ap.add_argument("--lm-head-chunk", type=int, default=8192,
-                    help="tokens per fused LM-head + cross-entropy chunk")
+    ap.add_argument("--lm-head-chunk", type=int, default=65536,
+                    help="tokens per fused LM-head + cross-entropy chunk (65536 = the whole "
+                         "64x1024 micro-batch in one chunk: 6.6 GB of bf16 logits, the "
+                         "fastest on MI355X, profiles/r3/chunk/README.md)")
     ap.add_argument("--model", default="small")
     ap.add_argument("--data-path", default="hbm", choices=["hbm", "h2d"],
                     help="data workload: GPU-preprocessed device blocks through the HBM "

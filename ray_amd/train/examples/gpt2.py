@@ -25,7 +25,7 @@ import time
 
 DEFAULTS = dict(model="small", micro_batch=64, seq_len=1024, steps=20, warmup=5,
                 grad_accum=1, bucket_mb=32.0, grad_dtype="fp32", tunableop="auto",
-                lm_head_chunk=8192, device=None)
+                lm_head_chunk=65536, device=None)
 
 
 def tunableop_file(model: str, micro_batch: int, seq_len: int) -> str:
