@@ -226,6 +226,11 @@ class Algorithm:
             "learners": res,
         }
         out["episode_reward_mean"] = out["env_runners"]["episode_return_mean"]
+        # old-stack names used by tuned-example stop criteria (sampler_results/...,
+        # timesteps_total)
+        out["timesteps_total"] = self.total_env_steps
+        out["sampler_results"] = {"episode_reward_mean": out["episode_reward_mean"],
+                                  "episode_len_mean": out["env_runners"]["episode_len_mean"]}
         if self._custom_metrics:
             out["env_runners"]["custom_metrics"] = dict(self._custom_metrics)
             out["custom_metrics"] = dict(self._custom_metrics)

@@ -166,9 +166,21 @@ class AlgorithmConfig:
     def api_stack(self, **kw):
         return self
 
+    # old-API-stack config keys (tuned-example YAML files) -> current attribute names
+    _LEGACY_KEYS = {"lambda": "lambda_", "num_workers": "num_env_runners",
+                    "num_rollout_workers": "num_env_runners",
+                    "num_envs_per_worker": "num_envs_per_env_runner",
+                    "num_sgd_iter": "num_epochs", "sgd_minibatch_size": "minibatch_size",
+                    "framework": "framework_str", "callbacks": "callbacks_class",
+                    "num_cpus_per_worker": "num_cpus_per_env_runner",
+                    "num_gpus_per_worker": "num_gpus_per_env_runner"}
+
     def update_from_dict(self, d: dict):
         for k, v in d.items():
-            setattr(self, "lambda_" if k == "lambda" else k, v)
+            if k == "num_gpus":
+                self.resources(num_gpus=v)
+                continue
+            setattr(self, self._LEGACY_KEYS.get(k, k), v)
         return self
 
     def copy(self, copy_frozen=None):

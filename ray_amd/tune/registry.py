@@ -34,29 +34,78 @@ def register_env(name: str, env_creator: Callable):
 
 def _rllib_algorithms() -> Dict[str, Any]:
     try:
-        from ray_amd.rllib import algorithms as A
-    except Exception:
+        from ray_amd.rllib.algorithms.registry import _algos
+    except Exception:  # noqa: BLE001
         return {}
-    out = {}
-    for n in dir(A):
-        obj = getattr(A, n)
-        if isinstance(obj, type) and hasattr(obj, "get_default_config") and n.isupper():
-            out[n] = obj
-    return out
+    return {name: algo for name, (algo, _) in _algos().items()}
+
+
+_ALGO_TRAINABLES: Dict[Any, Any] = {}
+
+
+def algorithm_trainable(algo_cls):
+    """Tune class trainable running an RLlib Algorithm (reference: Algorithm IS a
+    tune.Trainable): the trial config dict (old- or new-stack keys, ``env`` included) is
+    applied onto the algorithm's default AlgorithmConfig; ``step`` is one ``train()``;
+    checkpoints are the algorithm's own."""
+    if algo_cls in _ALGO_TRAINABLES:
+        return _ALGO_TRAINABLES[algo_cls]
+    from ray_amd.tune.trainable import Trainable
+
+    class _AlgorithmTrainable(Trainable):
+        _algo_cls = algo_cls
+
+        def setup(self, config):
+            from ray_amd.rllib.algorithms.registry import get_config_class
+
+            cfg = get_config_class(self._algo_cls)()
+            cfg.update_from_dict({k: v for k, v in config.items() if k != "__trial_info__"})
+            self.algo = self._algo_cls(cfg)
+
+        def step(self):
+            r = dict(self.algo.train())
+            r.pop("training_iteration", None)  # the Trainable counts iterations
+            return r
+
+        def save_checkpoint(self, checkpoint_dir):
+            self.algo.save(checkpoint_dir)
+            return checkpoint_dir
+
+        def load_checkpoint(self, checkpoint):
+            self.algo.restore(checkpoint)
+
+        def cleanup(self):
+            self.algo.stop()
+
+    _AlgorithmTrainable.__name__ = _AlgorithmTrainable.__qualname__ = algo_cls.__name__
+    _ALGO_TRAINABLES[algo_cls] = _AlgorithmTrainable
+    return _AlgorithmTrainable
+
+
+def _is_algorithm_cls(t) -> bool:
+    try:
+        from ray_amd.rllib.algorithms.algorithm import Algorithm
+    except Exception:  # noqa: BLE001
+        return False
+    return isinstance(t, type) and issubclass(t, Algorithm)
 
 
 def get_trainable_cls(name: str):
     if name in _TRAINABLES:
-        return _TRAINABLES[name]
+        return resolve_trainable(_TRAINABLES[name])
     algos = _rllib_algorithms()
     if name in algos:
-        return algos[name]
+        return algorithm_trainable(algos[name])
     raise ValueError(f"Unknown trainable {name!r}; registered: "
                      f"{sorted(_TRAINABLES) + sorted(algos)}")
 
 
 def resolve_trainable(t):
-    return get_trainable_cls(t) if isinstance(t, str) else t
+    if isinstance(t, str):
+        return get_trainable_cls(t)
+    if _is_algorithm_cls(t):
+        return algorithm_trainable(t)
+    return t
 
 
 class PlacementGroupFactory:

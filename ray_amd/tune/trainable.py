@@ -153,8 +153,10 @@ def function_get_context():
 
 
 class _TrialActor:
-    def __init__(self, trainable, config, trial_dir, trial_id, trial_name, checkpoint_path):
+    def __init__(self, trainable, config, trial_dir, trial_id, trial_name, checkpoint_path,
+                 checkpoint_frequency=0):
         os.makedirs(trial_dir, exist_ok=True)
+        self.checkpoint_frequency = int(checkpoint_frequency or 0)
         self.trainable = trainable
         self.config = config
         self.trial_dir = trial_dir
@@ -194,7 +196,15 @@ class _TrialActor:
     def next_result(self):
         if self.is_class:
             try:
-                return ("result", self.inst.train(), None)
+                r = self.inst.train()
+                # class trainables checkpoint every checkpoint_frequency iterations or when
+                # a result asks for it (reference: CheckpointConfig / should_checkpoint)
+                path = None
+                if r.pop("should_checkpoint", False) or (
+                        self.checkpoint_frequency and
+                        self.inst.iteration % self.checkpoint_frequency == 0):
+                    path = self.inst.save()
+                return ("result", r, path)
             except BaseException as e:  # noqa: BLE001
                 return ("error", traceback.format_exc(), repr(e))
         kind, a, b = self.s.q.get()
@@ -203,7 +213,7 @@ class _TrialActor:
         return kind, a, b
 
     def save(self):
-        if self.is_class:
+        if self.is_class and self.inst is not None:
             return self.inst.save()
         return None
 
