@@ -54,9 +54,11 @@ _loads = P.loads
 
 class _Owned:
     __slots__ = ("ready", "inline", "in_store", "callbacks", "borrowers", "contained",
-                 "release_when_ready", "task_id", "size", "node", "recon", "lineage_refs")
+                 "release_when_ready", "task_id", "size", "node", "recon", "lineage_refs",
+                 "accessed")
 
     def __init__(self, task_id=None):
+        self.accessed = False  # value read (get / await / passed as an argument)
         self.ready = False
         self.inline = None
         self.in_store = False
@@ -511,6 +513,7 @@ class CoreWorker:
                 return
             del self.owned[oid]
             self._ready_owned.discard(oid)
+            unhandled = o.inline if (o.inline is not None and not o.accessed) else None
             contained = o.contained
             o.contained = None
             in_store = o.in_store
@@ -528,6 +531,28 @@ class CoreWorker:
         if in_store:
             self._delete_stored(oid, node)
         del contained
+        if unhandled is not None:
+            self._report_unhandled(unhandled)
+
+    def _report_unhandled(self, inline):
+        """An error object freed without ever being read (reference: core_worker memory
+        store unhandled-exception handler -> "Unhandled error" on stderr)."""
+        if os.environ.get("RAY_IGNORE_UNHANDLED_ERRORS") == "1" or self._stopped:
+            return
+        try:
+            if ser.header(memoryview(inline))[0] != ser.KIND_ERROR:
+                return
+            _, err = ser.deserialize(inline)
+        except Exception:  # noqa: BLE001
+            return
+        if isinstance(err, (TaskCancelledError,)):
+            return
+        try:
+            sys.stderr.write("Unhandled error (suppress with "
+                             f"'RAY_IGNORE_UNHANDLED_ERRORS=1'): {err}\n")
+            sys.stderr.flush()
+        except Exception:  # noqa: BLE001
+            pass
 
     def _lineage_in_use(self, tid) -> bool:
         spec = self.lineage.get(tid)
@@ -1032,6 +1057,7 @@ class CoreWorker:
                 inline, in_store = o.inline, o.in_store
                 owner = self.addr
                 node = o.node
+                o.accessed = True
             else:
                 r = self.remote.get(oid)
                 inline = r.inline if r else None
@@ -1339,8 +1365,8 @@ class CoreWorker:
             "nret": -1 if streaming else nret, "owner": self.addr, "name": name,
             "resources": opts["resources"], "strategy": opts.get("strategy"),
             "retries": opts.get("max_retries", 3), "retry_exc": opts.get("retry_exceptions", False),
-            "runtime_env": opts.get("runtime_env"), "attempt": 0, "job": self.job_id,
-            "dynamic": dynamic, "ns": self.namespace,
+            "runtime_env": self._export_renv(opts.get("runtime_env")), "attempt": 0,
+            "job": self.job_id, "dynamic": dynamic, "ns": self.namespace,
         }
         refs = []
         with self.lock:
@@ -1404,6 +1430,7 @@ class CoreWorker:
                     o = self.owned.get(oid)
                     if o is not None and o.ready and o.inline is not None:
                         inline = o.inline
+                        o.accessed = True
             new.append((oid, owner, inline))
         spec["args"] = (blob, new)
 
@@ -1810,7 +1837,7 @@ class CoreWorker:
             "actor_id": actor_id, "max_concurrency": opts.get("max_concurrency"),
             "concurrency_groups": opts.get("concurrency_groups"),
             "is_async": method_meta.get("__is_async__", False),
-            "runtime_env": opts.get("runtime_env"), "job": self.job_id,
+            "runtime_env": self._export_renv(opts.get("runtime_env")), "job": self.job_id,
             "method_meta": method_meta, "ns": self.namespace,
         }
         self._inline_ready_args(spec)
@@ -2096,6 +2123,10 @@ class CoreWorker:
         self.task_events.append((tid, name, t0, None, os.getpid(), spec.get("actor_id"), "RUNNING",
                                  spec["type"], spec.get("job"), spec.get("attempt", 0), None))
         try:
+            if getattr(self, "setup_error", None):
+                from ray_amd.exceptions import RuntimeEnvSetupError
+
+                raise RuntimeEnvSetupError(self.setup_error)
             if spec["type"] == P.ACTOR_CREATION_TASK:
                 returns = self._execute_actor_creation(spec)
             else:
@@ -2147,6 +2178,58 @@ class CoreWorker:
                                  else "FINISHED", spec["type"], spec.get("job"),
                                  spec.get("attempt", 0), extra.get("exc_type")))
         self._send_reply(conn, reply_to, tid, returns, extra)
+
+    # ---------------------------------------------------------------- setup hooks
+    _HOOK_NS = b"__runtime_env__"
+
+    def _export_renv(self, renv):
+        """A callable ``worker_process_setup_hook`` travels as ``kv:<key>``: pickled once
+        into the internal KV, fetched by each worker process that starts with this env
+        (reference: _private/runtime_env/setup_hook.py)."""
+        if not renv or not isinstance(renv, dict):
+            return renv
+        hook = renv.get("worker_process_setup_hook")
+        if hook is None or isinstance(hook, str):
+            return renv
+        if not callable(hook):
+            raise TypeError("worker_process_setup_hook must be a callable or an import path "
+                            f"string, got {type(hook).__name__}")
+        import hashlib
+
+        import cloudpickle
+
+        blob = cloudpickle.dumps(hook)
+        key = "setup_hook:" + hashlib.sha1(blob).hexdigest()
+        exported = self.__dict__.setdefault("_exported_hooks", set())
+        if key not in exported:
+            self.call_raylet("kv_put", self._HOOK_NS, key.encode(), blob, True)
+            exported.add(key)
+        out = dict(renv)
+        out["worker_process_setup_hook"] = "kv:" + key
+        return out
+
+    def run_setup_hook(self, hook: str):
+        """Run once at worker start; a failure fails every task this worker runs with
+        RuntimeEnvSetupError."""
+        import traceback
+
+        try:
+            if hook.startswith("kv:"):
+                import cloudpickle
+
+                blob = self.call_raylet("kv_get", self._HOOK_NS, hook[3:].encode())
+                if blob is None:
+                    raise RuntimeError(f"setup hook {hook[3:]} not found in the internal KV")
+                fn = cloudpickle.loads(blob)
+            else:
+                import importlib
+
+                mod, _, attr = hook.rpartition(".")
+                fn = getattr(importlib.import_module(mod), attr)
+            fn()
+        except BaseException:  # noqa: BLE001
+            self.setup_error = ("worker_process_setup_hook failed:\n" +
+                                traceback.format_exc())
 
     def _apply_runtime_env(self, spec):
         renv = spec.get("runtime_env")

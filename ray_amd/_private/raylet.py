@@ -473,6 +473,8 @@ class Raylet:
             allr.update(src)
         for k, v in (allr.get("env_vars") or {}).items():
             env[k] = str(v)
+        if allr.get("worker_process_setup_hook"):
+            env["RAY_AMD_SETUP_HOOK"] = str(allr["worker_process_setup_hook"])
         cwd = None
         if allr.get("working_dir"):
             cwd = allr["working_dir"]

@@ -188,6 +188,8 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
         if main is not None and getattr(main, "__file__", None):
             sp.insert(0, os.path.dirname(os.path.abspath(main.__file__)))
         sp.insert(0, os.getcwd())
+        runtime_env = cw._export_renv(runtime_env)
+        global_worker.runtime_env = runtime_env
         if job_config is not None:
             # code_search_path: importable in every worker of the job (first on the path)
             sp = list(job_config.code_search_path) + sp

@@ -13,7 +13,7 @@ from typing import Any, Dict, List, Optional, Union
 
 _KNOWN = ("env_vars", "working_dir", "py_modules", "pip", "conda", "uv", "container",
           "image_uri", "config", "excludes", "py_executable", "java_jars", "_ray_commit",
-          "nsight", "mpi")
+          "nsight", "mpi", "worker_process_setup_hook")
 
 
 class RuntimeEnvConfig(dict):
