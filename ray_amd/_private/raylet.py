@@ -497,6 +497,14 @@ class Raylet:
         self.starting[w.token] = w
         return w
 
+    def _dedup(self):
+        d = getattr(self, "_log_dedup", None)
+        if d is None:
+            from ray_amd._private.log_dedup import LogDeduplicator
+
+            d = self._log_dedup = LogDeduplicator.from_env()
+        return d
+
     def _tee_worker_logs(self, w):
         """worker-<token>-<pid>.out/.err under <session>/logs (state API list_logs /
         get_log, CLI `logs`), each line also forwarded to this raylet's stdout / stderr
@@ -506,6 +514,7 @@ class Raylet:
 
         d = os.path.join(self.session_dir, "logs")
         os.makedirs(d, exist_ok=True)
+        dedup = self._dedup()
         for pipe, ext, out in ((w.proc.stdout, "out", sys.stdout), (w.proc.stderr, "err",
                                                                        sys.stderr)):
             path = os.path.join(d, f"worker-{w.token}-{w.pid}.{ext}")
@@ -528,11 +537,12 @@ class Raylet:
                             except OSError:
                                 pass
                             f = None
-                    try:
-                        out.buffer.write(line)
-                        out.flush()
-                    except (ValueError, OSError, AttributeError):
-                        pass
+                    for text in dedup.feed(line, w.pid, out):
+                        try:
+                            out.buffer.write(text)
+                            out.flush()
+                        except (ValueError, OSError, AttributeError):
+                            pass
                 if f is not None:
                     f.close()
                 pipe.close()

@@ -40,7 +40,12 @@ def test_worker_logs_captured(cluster):
             break
         time.sleep(0.2)
     assert any("hello-from-actor" in ln for ln in lines)
-    errs = list(get_log(pid=pid, suffix="err"))
+    errs = []
+    while time.time() < deadline + 5:  # stderr is pumped by its own thread
+        errs = list(get_log(pid=pid, suffix="err"))
+        if any("ERR hello-from-actor" in ln for ln in errs):
+            break
+        time.sleep(0.1)
     assert any("ERR hello-from-actor" in ln for ln in errs)
     logs = list_logs()
     assert any(str(pid) in f for f in logs["worker_out"])
