@@ -219,6 +219,27 @@ def _groupby_reduce(key, aggs, map_fn, batch_format, *parts):
 
 @ray.remote
 def _write_block(blk, path, fmt, idx, kw):
+    return _write_local(blk, path, fmt, idx, kw)
+
+
+def _write_local(blk, path, fmt, idx, kw):
+    kw = dict(kw)
+    pcols = kw.pop("partition_cols", None)
+    if pcols:
+        # Hive layout (reference: write_parquet(partition_cols=...)): one file per
+        # distinct value combination under col=value/... directories, without those columns
+        n = B.num_rows(blk)
+        if n == 0:
+            return 0
+        keys = list(zip(*[[str(v) for v in np.asarray(blk[c]).tolist()] for c in pcols]))
+        groups: dict = {}
+        for i, k in enumerate(keys):
+            groups.setdefault(k, []).append(i)
+        rest = {c: v for c, v in blk.items() if c not in pcols}
+        for k, rows in groups.items():
+            sub = os.path.join(path, *[f"{c}={v}" for c, v in zip(pcols, k)])
+            _write_local(B.take_idx(rest, np.asarray(rows)), sub, fmt, idx, kw)
+        return n
     os.makedirs(path, exist_ok=True)
     base = os.path.join(path, f"part_{idx:06d}")
     if fmt == "parquet":

@@ -119,12 +119,38 @@ def _expand(paths, exts=None):
     return out
 
 
-def _file_ds(paths, exts, reader, include_paths=False):
+def _hive_values(f: str, paths) -> dict:
+    """``key=value`` directory segments between an input directory and the file
+    (reference: datasource/partitioning.py Partitioning("hive")); values stay strings."""
+    out = {}
+    for p in ([paths] if isinstance(paths, str) else paths):
+        p = os.path.abspath(p)
+        af = os.path.abspath(f)
+        if os.path.isdir(p) and af.startswith(p.rstrip(os.sep) + os.sep):
+            for seg in os.path.relpath(os.path.dirname(af), p).split(os.sep):
+                k, sep, v = seg.partition("=")
+                if sep and k:
+                    out[k] = v
+            break
+    return out
+
+
+def _file_ds(paths, exts, reader, include_paths=False, partitioning="hive",
+             partition_filter=None):
     files = _expand(paths, exts)
+    parts = {f: (_hive_values(f, paths) if partitioning == "hive" else {}) for f in files}
+    if partition_filter is not None:
+        files = [f for f in files if partition_filter(parts[f])]
+        if not files:
+            raise FileNotFoundError(f"partition_filter kept no files of {paths}")
 
     def mk(f):
         def r():
             blk = B.from_batch(reader(f))
+            n = B.num_rows(blk)
+            for k, v in parts[f].items():
+                if k not in blk:
+                    blk[k] = np.array([v] * n, dtype=object)
             if include_paths:
                 blk["path"] = np.array([f] * B.num_rows(blk), dtype=object)
             return blk
@@ -135,25 +161,28 @@ def _file_ds(paths, exts, reader, include_paths=False):
     return ds
 
 
-def read_parquet(paths, *, columns=None, include_paths=False, **kw) -> Dataset:
+def read_parquet(paths, *, columns=None, include_paths=False, partitioning="hive",
+                 partition_filter=None, **kw) -> Dataset:
     def rd(f):
         import pyarrow.parquet as pq
 
-        return pq.read_table(f, columns=columns)
+        return pq.read_table(f, columns=columns, partitioning=None)
 
-    return _file_ds(paths, [".parquet"], rd, include_paths)
+    return _file_ds(paths, [".parquet"], rd, include_paths, partitioning, partition_filter)
 
 
-def read_csv(paths, *, include_paths=False, **kw) -> Dataset:
+def read_csv(paths, *, include_paths=False, partitioning="hive", partition_filter=None,
+             **kw) -> Dataset:
     def rd(f):
         import pyarrow.csv as pc
 
         return pc.read_csv(f)
 
-    return _file_ds(paths, [".csv"], rd, include_paths)
+    return _file_ds(paths, [".csv"], rd, include_paths, partitioning, partition_filter)
 
 
-def read_json(paths, *, include_paths=False, lines=True, **kw) -> Dataset:
+def read_json(paths, *, include_paths=False, lines=True, partitioning="hive",
+              partition_filter=None, **kw) -> Dataset:
     def rd(f):
         import pandas as pd
 
@@ -162,7 +191,8 @@ def read_json(paths, *, include_paths=False, lines=True, **kw) -> Dataset:
         except ValueError:
             return pd.read_json(f)
 
-    return _file_ds(paths, [".json", ".jsonl"], rd, include_paths)
+    return _file_ds(paths, [".json", ".jsonl"], rd, include_paths, partitioning,
+                    partition_filter)
 
 
 def read_numpy(paths, *, include_paths=False, **kw) -> Dataset:

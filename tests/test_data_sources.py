@@ -109,3 +109,27 @@ def test_random_access_and_block_order(cluster):
     shuffled = ds.randomize_block_order(seed=1)
     assert sorted(r["k"] for r in shuffled.take_all()) == [i * 3 for i in range(200)]
     assert len(ds.to_pandas_refs()) == 5
+
+
+def test_partitioned_write_and_hive_read(tmp_path):
+    """write_parquet/csv(partition_cols=...) -> col=value/ directories; reads add the
+    partition columns back (reference: Partitioning("hive")) and partition_filter prunes."""
+    import os
+
+    rows = [{"year": 2020 + i % 2, "kind": "ab"[i % 3 == 0], "x": i} for i in range(12)]
+    for fmt in ("parquet", "csv"):
+        out = str(tmp_path / fmt)
+        ds = rd.from_items(rows)
+        getattr(ds, f"write_{fmt}")(out, partition_cols=["year", "kind"])
+        dirs = sorted(os.listdir(out))
+        assert dirs == ["year=2020", "year=2021"]
+        assert sorted(os.listdir(os.path.join(out, "year=2020"))) == ["kind=a", "kind=b"]
+        back = getattr(rd, f"read_{fmt}")(out).take_all()
+        assert sorted(int(r["x"]) for r in back) == list(range(12))
+        for r in back:
+            assert int(r["year"]) == 2020 + int(r["x"]) % 2
+            assert r["kind"] == "ab"[int(r["x"]) % 3 == 0]
+        only = getattr(rd, f"read_{fmt}")(out, partition_filter=lambda p: p["year"] == "2021")
+        assert sorted(int(r["x"]) for r in only.take_all()) == [1, 3, 5, 7, 9, 11]
+        plain = getattr(rd, f"read_{fmt}")(out, partitioning=None).take_all()
+        assert "year" not in plain[0] and "kind" not in plain[0]
