@@ -103,6 +103,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
             "grad_dtype": r["grad_dtype"],
             "gemm_selection": r["gemm_selection"],
             "wgrad_gemm": r.get("wgrad_gemm"),
+            "lm_head_chunk": args.lm_head_chunk,
             "launcher": mode,
         },
         "rccl_world_size": r["rccl_world_size"],
