@@ -647,17 +647,8 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
                     freed[k] = ev
                 else:
                     _lm_head_dw(lg, h2[s0:e], dw, s0 == 0)
-        ctx.dw_event = None
         if side is not None:
-            # the main stream does NOT wait for dW here: backward consumes it through an
-            # event (deferred to the embedding backward for a tied weight), so the rest of
-            # the step overlaps the dW GEMM. The allocator must not recycle what the side
-            # stream still reads or writes.
-            ev = torch.cuda.Event()
-            ev.record(side)
-            ctx.dw_event = ev
-            for tns in bufs + [h2, dw]:
-                tns.record_stream(side)
+            main.wait_stream(side)
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]
@@ -674,21 +665,12 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         dwv = None
         if dw is not None:
             sink = _grad_sink(ctx.w)
-            ev = getattr(ctx, "dw_event", None)
-            if sink is not None and ev is not None and not ctx.signal_w:
-                # tied weight: its other gradient (the embedding's) lands last in backward;
-                # the dW accumulate joins it there, so nothing waits on the dW GEMM now
-                ctx.w._ra_deferred_accum = (dw, gs, ev)
-            elif sink is not None:
-                if ev is not None:
-                    torch.cuda.current_stream().wait_event(ev)
+            if sink is not None:
                 check(L.ra_scaled_accum(ptr(dw), ptr(sink), dw.numel(), _sink_f32(sink), ptr(gs),
                                         stream_ptr()), "scaled_accum")
                 if ctx.signal_w:
                     _grad_done(ctx.w)
             else:
-                if ev is not None:
-                    torch.cuda.current_stream().wait_event(ev)
                 dwv = (dw * gs).to(ctx.w.dtype)
         return dhv, dwv, None, None, None, None, None
 
@@ -722,7 +704,6 @@ class _Embedding(torch.autograd.Function):
     def backward(ctx, dx):
         (idx,) = ctx.saved_tensors
         wte, wpe = ctx.wte, ctx.wpe
-        _flush_deferred_accum(wte)
         B, T, C = dx.shape
         d2 = dx.reshape(-1, C)
         outs = []
@@ -739,20 +720,6 @@ class _Embedding(torch.autograd.Function):
                 fill(acc)
                 outs.append(acc.to(p.dtype))
         return None, outs[0], outs[1]
-
-
-def _flush_deferred_accum(p):
-    """Accumulate a tied LM head's dW (left by _LMHeadCrossEntropy.backward) into p's
-    gradient sink, after the side-stream GEMM that produced it."""
-    pend = getattr(p, "_ra_deferred_accum", None)
-    if pend is None:
-        return
-    p._ra_deferred_accum = None
-    dw, gs, ev = pend
-    torch.cuda.current_stream().wait_event(ev)
-    sink = _grad_sink(p)
-    check(_lib.lib().ra_scaled_accum(ptr(dw), ptr(sink), dw.numel(), _sink_f32(sink), ptr(gs),
-                                     stream_ptr()), "scaled_accum")
 
 
 def embedding(idx, wte, wpe):
