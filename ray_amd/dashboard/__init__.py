@@ -21,7 +21,7 @@ def start_dashboard(session_dir: str, host: str = "127.0.0.1", port: int = 8265,
     except FileNotFoundError:
         pass
     env = dict(os.environ)
-    pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
                                     else "")
     env.pop("RAY_ADDRESS", None)

@@ -145,7 +145,12 @@ class _Router:
                 fut.set_result((slot, ref))
             try:
                 self.refresh()
-            except Exception:  # noqa: BLE001
+            except RuntimeError as e:  # the deployment was deleted: fail what still waits
+                with self.lock:
+                    waiting, self.pending = self.pending, []
+                for fut, _, _ in waiting:
+                    fut.set_exception(e)
+            except Exception:  # noqa: BLE001  (controller briefly unreachable: retry)
                 pass
 
     def choose_wait_for_replicas(self):
