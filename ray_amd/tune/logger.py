@@ -158,14 +158,129 @@ class CSVLoggerCallback(LoggerCallback):
             st[0].close()
 
 
+class EventFileWriter:
+    """TensorBoard event files without tensorboardX / TensorFlow: ``Event`` protos
+    (wall_time = 1, step = 2, file_version = 3, summary = 5; Summary.value = 1 with tag = 1,
+    simple_value = 2) encoded from the protobuf wire format and framed as TFRecords by the
+    native core (masked CRC32C), the layout TensorBoard reads from
+    ``events.out.tfevents.<time>.<host>``."""
+
+    def __init__(self, logdir: str, filename_suffix: str = ""):
+        import socket
+        import time
+
+        os.makedirs(logdir, exist_ok=True)
+        self.path = os.path.join(
+            logdir, f"events.out.tfevents.{int(time.time())}.{socket.gethostname()}"
+                    f"{filename_suffix}")
+        self._f = open(self.path, "ab")
+        self._write_event(self._event(step=0, file_version="brain.Event:2"))
+
+    @staticmethod
+    def _event(step: int, file_version: str | None = None, scalars=None) -> bytes:
+        import struct
+        import time
+
+        from ray_amd.data.tfrecords import _ld, _varint
+
+        body = b"\x09" + struct.pack("<d", time.time())  # field 1, fixed64
+        body += b"\x10" + _varint(int(step))            # field 2, varint
+        if file_version is not None:
+            body += _ld(3, file_version.encode())
+        if scalars:
+            vals = b"".join(_ld(1, _ld(1, tag.encode()) + b"\x15" + struct.pack("<f", val))
+                            for tag, val in scalars)
+            body += _ld(5, vals)
+        return body
+
+    def _write_event(self, ev: bytes):
+        from ray_amd._native import _core
+
+        self._f.write(_core.tfrecord_encode([ev]))
+        self._f.flush()
+
+    def add_scalars(self, step: int, scalars) -> None:
+        self._write_event(self._event(step=step, scalars=list(scalars)))
+
+    def close(self):
+        self._f.close()
+
+
+def read_event_file(path: str) -> list:
+    """[(step, {tag: value}, file_version)] of an event file (tests / tools)."""
+    import struct
+
+    from ray_amd._native import _core
+    from ray_amd.data.tfrecords import _fields
+
+    data = open(path, "rb").read()
+    out = []
+    for off, n in _core.tfrecord_index(data, True):
+        buf = data[off:off + n]
+        step, tags, ver = 0, {}, None
+        for fn, wt, v in _fields(buf):
+            if fn == 2:
+                step = v
+            elif fn == 3:
+                ver = buf[v[0]:v[1]].decode()
+            elif fn == 5:
+                for _, _, vspan in _fields(buf, *v):
+                    tag, val = None, None
+                    for kfn, _, kv in _fields(buf, *vspan):
+                        if kfn == 1:
+                            tag = buf[kv[0]:kv[1]].decode()
+                        elif kfn == 2:
+                            val = struct.unpack("<f", struct.pack("<I", kv))[0]
+                    tags[tag] = val
+        out.append((step, tags, ver))
+    return out
+
+
 class TBXLoggerCallback(LoggerCallback):
-    """TensorBoard logging needs tensorboardX, which this image does not ship."""
+    """TensorBoard scalars per trial (reference: tune/logger/tensorboardx.py): every
+    numeric result entry, flattened with '/', under ``ray/tune/<key>`` at step
+    ``training_iteration``; hyper-parameters as ``config/<key>`` scalars at step 0."""
+
+    _SKIP = {"config", "trial_id", "experiment_id", "date", "timestamp", "pid", "hostname",
+             "node_ip", "done", "should_checkpoint"}
 
     def __init__(self):
-        raise ImportError("TBXLoggerCallback requires tensorboardX (not installed)")
+        self._writers = {}
+
+    def log_trial_start(self, trial):
+        w = self._writers.get(id(trial))
+        if w is None:
+            w = self._writers[id(trial)] = EventFileWriter(_trial_dir(trial))
+            params = [(f"config/{k}", float(v)) for k, v in
+                      flatten_dict(dict(getattr(trial, "config", {}) or {})).items()
+                      if isinstance(v, (int, float)) and not isinstance(v, bool)]
+            if params:
+                w.add_scalars(0, params)
+
+    def log_trial_result(self, iteration, trial, result):
+        if id(trial) not in self._writers:
+            self.log_trial_start(trial)
+        step = result.get("training_iteration", iteration)
+        flat = flatten_dict({k: v for k, v in result.items() if k not in self._SKIP})
+        vals = []
+        for k, v in flat.items():
+            if isinstance(v, bool) or not isinstance(v, (int, float)):
+                item = getattr(v, "item", None)
+                if not callable(item) or getattr(v, "ndim", 1) != 0:
+                    continue
+                v = item()
+            if isinstance(v, (int, float)) and math.isfinite(v):
+                vals.append((f"ray/tune/{k}", float(v)))
+        if vals:
+            self._writers[id(trial)].add_scalars(int(step), vals)
+
+    def log_trial_end(self, trial, failed=False):
+        w = self._writers.pop(id(trial), None)
+        if w is not None:
+            w.close()
 
 
-DEFAULT_LOGGERS = (JsonLoggerCallback, CSVLoggerCallback)
+DEFAULT_LOGGERS = (JsonLoggerCallback, CSVLoggerCallback, TBXLoggerCallback)
 
 
 def default_callbacks(user: list | None) -> list:
