@@ -190,12 +190,17 @@ class Replica:
         self.deployment_name = deployment_name
         self.app_name = app_name
         self.replica_id = replica_id
+        from ray_amd.serve import context as _ctx
+
+        rc = _ctx.ReplicaContext(app_name, deployment_name, replica_id)
+        _ctx._set_replica_context(rc)  # visible to the user's constructor too
         target = cloudpickle.loads(callable_blob)
         self.is_function = is_function
         if is_function:
             self.obj = target
         else:
             self.obj = target(*init_args, **init_kwargs)
+        rc.servable_object = self.obj
         self.asgi = None
         if asgi_app_blob is not None:
             app = cloudpickle.loads(asgi_app_blob)

@@ -319,3 +319,38 @@ def test_serve_cli_build_deploy_status_config_shutdown(app_dir):
     finally:
         run("ray_amd.scripts", "stop")
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_replica_context_and_serve_metrics(cluster):
+    import pickle
+
+    from ray_amd.serve import metrics as smetrics
+    from ray_amd.serve.exceptions import RayServeException
+    from ray_amd.util.metrics import prometheus_text
+
+    with pytest.raises(RayServeException):
+        serve.get_replica_context()
+
+    @serve.deployment(num_replicas=2)
+    class Ctx:
+        def __init__(self):
+            self.at_init = serve.get_replica_context().deployment  # visible in __init__
+            self.hits = smetrics.Counter("serve_ctx_hits", "requests", tag_keys=("kind",))
+
+        def __call__(self):
+            rc = serve.get_replica_context()
+            self.hits.inc(tags={"kind": "call"})
+            assert rc.servable_object is self
+            return rc.app_name, rc.deployment, rc.replica_tag, self.at_init, \
+                rc.replica_id.unique_id
+
+    h = serve.run(Ctx.bind(), name="ctxapp", route_prefix=None)
+    outs = {h.remote().result() for _ in range(12)}
+    assert {o[:2] for o in outs} == {("ctxapp", "Ctx")}
+    assert all(o[3] == "Ctx" and o[2].endswith(o[4]) for o in outs)
+    m = smetrics.Gauge("serve_test_gauge", tag_keys=("k",))
+    assert pickle.loads(pickle.dumps(m))._tag_keys == m._tag_keys
+    with pytest.raises(ValueError):
+        smetrics.Counter("bad", tag_keys=("deployment",))
+    serve.delete("ctxapp")
+    prometheus_text()  # renders with the serve tag keys
