@@ -22,6 +22,31 @@ AMD_INSTINCT_MI325x = "AMD-Instinct-MI325X-OAM"
 AMD_INSTINCT_MI350x = "AMD-Instinct-MI350X"
 AMD_INSTINCT_MI355x = "AMD-Instinct-MI355X"
 
+AMD_RADEON_R9_200_HD_7900 = "AMD-Radeon-R9-200-HD-7900"
+AMD_RADEON_HD_7900 = "AMD-Radeon-HD-7900"
+# other vendors' type names (API parity: user code may name them; no such node here)
+NVIDIA_TESLA_V100 = "V100"
+NVIDIA_TESLA_P100 = "P100"
+NVIDIA_TESLA_T4 = "T4"
+NVIDIA_TESLA_P4 = "P4"
+NVIDIA_TESLA_K80 = "K80"
+NVIDIA_TESLA_A10G = "A10G"
+NVIDIA_L4 = "L4"
+NVIDIA_A100 = "A100"
+NVIDIA_A100_40G = "A100-40G"
+NVIDIA_A100_80G = "A100-80G"
+NVIDIA_H100 = "H100"
+INTEL_MAX_1550 = "Intel-GPU-Max-1550"
+INTEL_MAX_1100 = "Intel-GPU-Max-1100"
+INTEL_GAUDI = "Intel-GAUDI"
+AWS_NEURON_CORE = "aws-neuron-core"
+GOOGLE_TPU_V2 = "TPU-V2"
+GOOGLE_TPU_V3 = "TPU-V3"
+GOOGLE_TPU_V4 = "TPU-V4"
+GOOGLE_TPU_V5P = "TPU-V5P"
+GOOGLE_TPU_V5LITEPOD = "TPU-V5LITEPOD"
+GOOGLE_TPU_V6E = "TPU-V6E"
+
 # PCI device ids (amdgpu.ids) -> accelerator type
 _DEVICE_IDS = {
     0x738C: AMD_INSTINCT_MI100, 0x738E: AMD_INSTINCT_MI100,
