@@ -354,3 +354,54 @@ def test_replica_context_and_serve_metrics(cluster):
         smetrics.Counter("bad", tag_keys=("deployment",))
     serve.delete("ctxapp")
     prometheus_text()  # renders with the serve tag keys
+
+
+def test_batch_streaming_and_runtime_retuning(cluster):
+    @serve.deployment(max_ongoing_requests=32)
+    class B:
+        def __init__(self):
+            self.sizes = []
+
+        @serve.batch(max_batch_size=4, batch_wait_timeout_s=0.2)
+        async def tokens(self, ns):
+            self.sizes.append(len(ns))
+            for step in range(max(ns)):
+                yield [f"{n}:{step}" if step < n else None for n in ns]
+
+        @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.2)
+        async def double(self, xs):
+            self.sizes.append(len(xs))
+            return [2 * x for x in xs]
+
+        def retune(self, n):
+            self.double.set_max_batch_size(n)
+            self.double.set_batch_wait_timeout_s(0.3)
+            return self.double._get_max_batch_size(), self.double._get_batch_wait_timeout_s()
+
+        def sizes_seen(self):
+            out, self.sizes = self.sizes, []
+            return out
+
+    h = serve.run(B.bind(), name="batchx", route_prefix=None)
+    gens = [h.options(method_name="tokens", stream=True).remote(n) for n in (1, 2, 3)]
+    streams = [list(g) for g in gens]
+    assert streams[2][:3] == ["3:0", "3:1", "3:2"]
+    assert streams[0][0] == "1:0" and streams[1][:2] == ["2:0", "2:1"]
+    assert max(h.sizes_seen.remote().result()) > 1  # the three streams shared batches
+    resps = [h.double.remote(i) for i in range(8)]
+    assert [r.result() for r in resps] == [2 * i for i in range(8)]
+    assert max(h.sizes_seen.remote().result()) <= 2
+    assert h.retune.remote(8).result() == (8, 0.3)
+    resps = [h.double.remote(i) for i in range(8)]
+    assert [r.result() for r in resps] == [2 * i for i in range(8)]
+    assert max(h.sizes_seen.remote().result()) > 2
+    serve.delete("batchx")
+
+
+def test_batch_decorator_validation():
+    with pytest.raises(TypeError):
+        @serve.batch
+        def not_async(xs):
+            return xs
+    with pytest.raises(ValueError):
+        serve.batch(max_batch_size=0)
