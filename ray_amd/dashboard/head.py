@@ -141,7 +141,56 @@ def build_app(manager: JobManager) -> Starlette:
             return JSONResponse({"error": str(e)}, 400)
         return JSONResponse({"deleted": ok})
 
+    # ---- Serve REST API (reference: dashboard/modules/serve/serve_head.py)
+    def _serve_details():
+        from ray_amd import serve
+        from ray_amd.serve.schema import get_deployed_config
+
+        try:
+            st_ = serve.status()
+        except RuntimeError:
+            st_ = {}
+        cfg = get_deployed_config() or {}
+        apps = {}
+        for a in cfg.get("applications", []):
+            if a.get("name") in st_:
+                apps[a["name"]] = {"deployed_app_config": a}
+        for name, info in st_.items():
+            apps.setdefault(name, {})
+            apps[name].update({"name": name, "status": info.get("status"),
+                               "route_prefix": info.get("route_prefix"),
+                               "deployments": info.get("deployments", {})})
+        return {"proxy_location": cfg.get("proxy_location", "EveryNode"),
+                "http_options": cfg.get("http_options"), "applications": apps}
+
+    async def serve_get(_req):
+        return JSONResponse(await run_in_threadpool(_serve_details))
+
+    async def serve_put(req: Request):
+        from pydantic import ValidationError
+
+        from ray_amd.serve.schema import ServeDeploySchema, deploy_config
+
+        try:
+            cfg = ServeDeploySchema(**(await req.json()))
+        except (ValidationError, ValueError, TypeError) as e:
+            return PlainTextResponse(str(e), 400)
+        try:
+            await run_in_threadpool(deploy_config, cfg)
+        except Exception as e:  # noqa: BLE001
+            return PlainTextResponse(f"deploy failed: {e!r}", 500)
+        return PlainTextResponse("")
+
+    async def serve_delete(_req):
+        from ray_amd import serve
+
+        await run_in_threadpool(serve.shutdown)
+        return PlainTextResponse("")
+
     routes = [
+        Route("/api/serve/applications/", serve_get, methods=["GET"]),
+        Route("/api/serve/applications/", serve_put, methods=["PUT"]),
+        Route("/api/serve/applications/", serve_delete, methods=["DELETE"]),
         Route("/api/version", version),
         Route("/api/cluster_status", cluster_status),
         Route("/api/v0/{resource}/summarize", state_summary),

@@ -25,6 +25,21 @@ def _connect(address):
     return ray
 
 
+def _rest(address):
+    """The dashboard URL when --address is one (reference: the serve CLI talks to the
+    dashboard's /api/serve/applications/ REST API)."""
+    return address.rstrip("/") if address and address.startswith("http") else None
+
+
+def _http(method, url, body=None):
+    import requests
+
+    r = requests.request(method, url, json=body, timeout=300)
+    if r.status_code >= 400:
+        raise SystemExit(f"{method} {url} -> {r.status_code}: {r.text}")
+    return r
+
+
 def _is_config(p: str) -> bool:
     return p.endswith((".yaml", ".yml", ".json")) and os.path.exists(p)
 
@@ -72,6 +87,12 @@ def cmd_start(a):
 
 
 def cmd_deploy(a):
+    url = _rest(a.address)
+    if url:
+        cfg = _config_from(a)
+        _http("PUT", url + "/api/serve/applications/", cfg.model_dump(mode="json"))
+        print(f"Sent deploy request for applications: {[x.name for x in cfg.applications]}")
+        return 0
     _connect(a.address)
     from ray_amd.serve.schema import deploy_config
 
@@ -101,6 +122,13 @@ def cmd_run(a):
 
 
 def cmd_status(a):
+    url = _rest(a.address)
+    if url:
+        d = _http("GET", url + "/api/serve/applications/").json()
+        _dump({"applications": {n: {k: v for k, v in app.items()
+                                    if k not in ("name", "deployed_app_config")}
+                                for n, app in d["applications"].items()}})
+        return 0
     _connect(a.address)
     from ray_amd import serve
 
@@ -113,10 +141,16 @@ def cmd_status(a):
 
 
 def cmd_config(a):
-    _connect(a.address)
-    from ray_amd.serve.schema import get_deployed_config
+    url = _rest(a.address)
+    if url:
+        d = _http("GET", url + "/api/serve/applications/").json()
+        cfg = {"applications": [app["deployed_app_config"] for app in
+                                d["applications"].values() if "deployed_app_config" in app]}
+    else:
+        _connect(a.address)
+        from ray_amd.serve.schema import get_deployed_config
 
-    cfg = get_deployed_config()
+        cfg = get_deployed_config()
     if cfg is None:
         print("No configuration was deployed.")
         return 0
@@ -135,6 +169,11 @@ def cmd_shutdown(a):
         ans = input("This shuts down Serve and deletes every application. Continue? [y/N] ")
         if ans.strip().lower() not in ("y", "yes"):
             return 1
+    url = _rest(a.address)
+    if url:
+        _http("DELETE", url + "/api/serve/applications/")
+        print("Serve shut down.")
+        return 0
     _connect(a.address)
     from ray_amd import serve
 

@@ -298,8 +298,9 @@ def test_serve_cli_build_deploy_status_config_shutdown(app_dir):
     cfg["applications"][0]["deployments"][0]["num_replicas"] = 2
     (app_dir / "cfg.yaml").write_text(yaml.safe_dump(cfg))
 
+    dash = _free_port()
     r = run("ray_amd.scripts", "start", "--head", "--num-cpus", "4", "--dashboard-port",
-            str(_free_port()))
+            str(dash))
     assert r.returncode == 0, r.stderr
     try:
         r = run("ray_amd.serve", "deploy", "cfg.yaml")
@@ -312,7 +313,22 @@ def test_serve_cli_build_deploy_status_config_shutdown(app_dir):
         assert st["deployments"]["Greeter"]["replica_states"]["RUNNING"] == 2
         r = run("ray_amd.serve", "config")
         assert yaml.safe_load(r.stdout)["import_path"] == "greet_app:app"
-        r = run("ray_amd.serve", "shutdown", "-y")
+        # the same through the dashboard's Serve REST API (/api/serve/applications/)
+        url = f"http://127.0.0.1:{dash}"
+        r = run("ray_amd.serve", "status", "--address", url)
+        assert r.returncode == 0, r.stderr
+        st = yaml.safe_load(r.stdout)["applications"]["default"]
+        assert st["status"] == "RUNNING"
+        r = run("ray_amd.serve", "config", "--address", url)
+        assert yaml.safe_load(r.stdout)["import_path"] == "greet_app:app"
+        cfg["applications"][0]["deployments"][0]["num_replicas"] = 1
+        cfg["applications"][0]["deployments"][0]["user_config"] = {"suffix": "!"}
+        (app_dir / "cfg.yaml").write_text(yaml.safe_dump(cfg))
+        r = run("ray_amd.serve", "deploy", "cfg.yaml", "--address", url)
+        assert r.returncode == 0, r.stdout + r.stderr
+        _wait_for(lambda: requests.get(f"http://127.0.0.1:{port}/", params={"name": "rest"},
+                                       timeout=30).text == "hello rest!")
+        r = run("ray_amd.serve", "shutdown", "-y", "--address", url)
         assert r.returncode == 0, r.stderr
         r = run("ray_amd.serve", "status")
         assert yaml.safe_load(r.stdout)["applications"] == {}
