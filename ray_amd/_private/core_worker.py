@@ -537,7 +537,7 @@ class CoreWorker:
     def _report_unhandled(self, inline):
         """An error object freed without ever being read (reference: core_worker memory
         store unhandled-exception handler -> "Unhandled error" on stderr)."""
-        if os.environ.get("RAY_IGNORE_UNHANDLED_ERRORS") == "1" or self._stopped:
+        if "RAY_IGNORE_UNHANDLED_ERRORS" in os.environ or self._stopped:
             return
         try:
             if ser.header(memoryview(inline))[0] != ser.KIND_ERROR:
@@ -545,7 +545,12 @@ class CoreWorker:
             _, err = ser.deserialize(inline)
         except Exception:  # noqa: BLE001
             return
-        if isinstance(err, (TaskCancelledError,)):
+        # only task failures, as the reference (memory_store.cc IsUnhandledError:
+        # TASK_EXECUTION_EXCEPTION / WORKER_DIED; an actor that died or was killed is not)
+        from ray_amd.exceptions import WorkerCrashedError
+
+        if isinstance(err, RayActorError) or not isinstance(err, (RayTaskError,
+                                                                   WorkerCrashedError)):
             return
         try:
             sys.stderr.write("Unhandled error (suppress with "

@@ -114,3 +114,21 @@ def test_read_or_suppressed_errors_are_not_reported():
         gc.collect()
     """, env={"RAY_IGNORE_UNHANDLED_ERRORS": "1"})
     assert "Unhandled error" not in r.stderr
+
+
+def test_actor_death_is_not_an_unhandled_error():
+    r = _run_driver("""
+        @ray.remote
+        class A:
+            def slow(self):
+                time.sleep(30)
+
+        a = A.remote()
+        ref = a.slow.remote()
+        time.sleep(0.5)
+        ray.kill(a)
+        ray.wait([ref], timeout=10)
+        del ref
+        gc.collect()
+    """)
+    assert "Unhandled error" not in r.stderr
