@@ -236,9 +236,12 @@ class _Router:
 
     def done(self, rid):
         with self.lock:
-            if rid in self.inflight:
-                self.inflight[rid] = max(0, self.inflight[rid] - 1)
-            self.slot_freed.notify()
+            self._done_locked(rid)
+
+    def _done_locked(self, rid):
+        if rid in self.inflight:
+            self.inflight[rid] = max(0, self.inflight[rid] - 1)
+        self.slot_freed.notify()
 
 
 _routers: dict = {}
@@ -276,9 +279,13 @@ class _Slot:
         self.router, self.rid, self.released = router, rid, False
 
     def release(self):
-        if not self.released:
+        # reply-landed callbacks (I/O thread) race the caller's own finish: decide under
+        # the router lock so a slot is returned exactly once
+        with self.router.lock:
+            if self.released:
+                return
             self.released = True
-            self.router.done(self.rid)
+            self.router._done_locked(self.rid)
 
 
 def _watch(slot: _Slot, ref) -> None:
