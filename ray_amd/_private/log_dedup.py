@@ -3,8 +3,9 @@ python/ray/_private/ray_logging.py LogDeduplicator, RAY_DEDUP_LOGS).
 
 A line is keyed by its words that contain no digits (pids, ids, counters, timings differ
 between workers). The first occurrence of a key is printed at once; further occurrences
-within ``RAY_DEDUP_LOGS_AGG_WINDOW_S`` (default 5 s) are counted, and when the window
-closes the latest one is printed once with ``[repeated Nx across cluster]``. The per-worker
+from OTHER worker processes within ``RAY_DEDUP_LOGS_AGG_WINDOW_S`` (default 5 s) are
+counted (one process repeating itself is printed as is), and when the window closes the
+latest one is printed once with ``[repeated Nx across cluster]``. The per-worker
 log files under ``<session>/logs`` always keep every line; ``RAY_DEDUP_LOGS=0`` turns the
 terminal deduplication off. Lines matching ``RAY_DEDUP_LOGS_SKIP_REGEX`` or
 ``RAY_DEDUP_LOGS_ALLOW_REGEX`` are dropped / never deduplicated, as in the reference."""
@@ -62,9 +63,11 @@ class LogDeduplicator:
                 self.state[(out, key)] = [now, 0, line, {source}]
                 self._ensure_flusher()
                 return [raw]
+            st[3].add(source)
+            if len(st[3]) == 1:  # one process repeating itself is not deduplicated
+                return [raw]
             st[1] += 1
             st[2] = line
-            st[3].add(source)
             return []
 
     def _ensure_flusher(self):

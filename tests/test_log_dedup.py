@@ -26,6 +26,9 @@ def test_dedup_window_and_repeat_summary():
     assert d.feed(b"hello from pid 2\n", 2, out) == []
     assert d.feed(b"hello from pid 3\n", 3, out) == []
     assert d.feed(b"something else\n", 1, out) == [b"something else\n"]
+    # one process repeating itself is printed, not counted
+    assert d.feed(b"loop 1\n", 7, out) == [b"loop 1\n"]
+    assert d.feed(b"loop 2\n", 7, out) == [b"loop 2\n"]
     time.sleep(0.4)
     ready = d.flush()
     assert ready == [(out, "hello from pid 3 [repeated 2x across cluster]\n")]
@@ -51,11 +54,14 @@ def test_driver_sees_repeats_collapsed():
         ray.init(num_cpus=4)
 
         @ray.remote
-        def noisy(i):
-            print("dedup-me task output", flush=True)
-            return i
+        class Noisy:
+            def say(self, i):
+                print("dedup-me task output", flush=True)
+                return i
 
-        ray.get([noisy.remote(i) for i in range(8)])
+        actors = [Noisy.remote() for _ in range(4)]  # four processes
+        ray.get([a.say.remote(i) for i, a in enumerate(actors)])
+        ray.get([a.say.remote(i) for i, a in enumerate(actors)])
         time.sleep(2.5)
         ray.shutdown()
     ''' % REPO)
