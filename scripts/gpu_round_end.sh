@@ -12,5 +12,5 @@ timeout -k 10 300 python bench.py > gpurun_out/re/bench.log 2>&1 || { echo "benc
 tail -1 gpurun_out/re/bench.log | cut -c1-250
 timeout -k 10 300 python bench.py --workload impala --steps 5 --warmup 2 > gpurun_out/re/impala.log 2>&1 || { echo "impala rc=$?"; exit 1; }
 tail -1 gpurun_out/re/impala.log | cut -c1-200
-timeout -k 10 300 python bench.py --workload data --steps 5 --warmup 1 > gpurun_out/re/data.log 2>&1 || { echo "data rc=$?"; exit 1; }
+timeout -k 10 300 python bench.py --workload data --steps 60 --warmup 5 > gpurun_out/re/data.log 2>&1 || { echo "data rc=$?"; exit 1; }
 tail -1 gpurun_out/re/data.log | cut -c1-200
