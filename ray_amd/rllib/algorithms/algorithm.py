@@ -33,6 +33,11 @@ class PerModuleLearners:
     def get_weights(self):
         return {mid: lr.get_weights() for mid, lr in self.learners.items()}
 
+    def set_weights(self, w):
+        for mid, wm in w.items():
+            if mid in self.learners:
+                self.learners[mid].set_weights(wm)
+
     def get_state(self):
         return {mid: lr.get_state() for mid, lr in self.learners.items()}
 
@@ -278,40 +283,139 @@ class Algorithm:
         return {"env_runners": {"episode_return_mean": float(np.mean(rets[:n]))}}
 
     # ---------------------------------------------------------------- inference
-    def compute_single_action(self, obs, explore=False, policy_id=None):
-        import torch
+    def _new_module(self, obs_space, act_space):
+        """An inference module of this algorithm's kind (what its EnvRunners run)."""
+        kind = self.cfg.get("module_kind", "actor_critic")
+        if kind == "q":
+            from ray_amd.rllib.core.rl_module import QModule
 
+            mc = dict(self.config.model or {})
+            mc["dueling"] = self.cfg.get("dueling", True)
+            return QModule(obs_space, act_space, mc)
+        if kind == "sac":
+            from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy
+
+            return SquashedGaussianPolicy(obs_space, act_space,
+                                          self.cfg.get("policy_model_config") or
+                                          self.config.model)
         from ray_amd.rllib.core.rl_module import RLModule
 
+        return RLModule(obs_space, act_space, self.config.model)
+
+    def get_module(self, module_id=None):
+        """The RLModule with the current weights, on the CPU, for inference (reference:
+        Algorithm.get_module)."""
         if self.is_multi_agent:
             from ray_amd.rllib.env.multi_agent_env_runner import DEFAULT_MODULE_ID
 
-            mid = policy_id or DEFAULT_MODULE_ID
+            mid = module_id or DEFAULT_MODULE_ID
             os_, as_ = self.module_specs[mid]
             mods = self.__dict__.setdefault("_infer_modules", {})
             if mid not in mods:
-                mods[mid] = RLModule(os_, as_, self.config.model)
-            self._infer_module = mods[mid]
-            self._infer_module.load_state_dict(self.get_weights()[mid])
+                mods[mid] = self._new_module(os_, as_)
+            m = mods[mid]
+            m.load_state_dict(self.get_weights()[mid])
+            self._infer_filter = None
         else:
             if not hasattr(self, "_infer_module"):
-                self._infer_module = RLModule(self.observation_space, self.action_space,
-                                              self.config.model)
+                self._infer_module = self._new_module(self.observation_space,
+                                                      self.action_space)
+            m = self._infer_module
             w = dict(self.get_weights())
             cs = w.pop("__connector_state__", None)
-            self._infer_module.load_state_dict(w)
+            m.load_state_dict(w)
+            self._infer_filter = None
             if cs is not None:  # same normalization the EnvRunners apply
                 from ray_amd.ops.functional import RunningMeanStd
 
                 f = RunningMeanStd(tuple(cs["mean"].shape))
                 f.load_state_dict(cs)
-                obs = f.normalize(torch.as_tensor(np.asarray(obs, np.float32))).numpy()
+                self._infer_filter = f
+        m.eval()
+        return m
+
+    def compute_single_action(self, obs, explore=False, policy_id=None):
+        import torch
+
+        m = self.get_module(policy_id)
+        if self._infer_filter is not None:
+            obs = self._infer_filter.normalize(
+                torch.as_tensor(np.asarray(obs, np.float32))).numpy()
+        kind = self.cfg.get("module_kind", "actor_critic")
         with torch.no_grad():
             x = torch.as_tensor(np.asarray(obs)[None])
-            di = self._infer_module.forward_inference(x)["action_dist_inputs"]
-            a, _ = self._infer_module.sample_actions(di, explore)
+            if kind == "q":
+                a = m(x.float()).argmax(-1)
+                if explore and np.random.random() < getattr(self, "epsilon", 0.0):
+                    a = torch.tensor([np.random.randint(self.action_space.n)])
+            elif kind == "sac":
+                a, _ = m(x.float(), explore)
+                a = a.float()
+            else:
+                di = m.forward_inference(x)["action_dist_inputs"]
+                a, _ = m.sample_actions(di, explore)
         a = a[0].numpy()
         return int(a) if a.ndim == 0 else a
+
+    def compute_actions(self, observations, explore=False, policy_id=None):
+        """Batched inference: a dict of observations (agent / env ids) -> dict of actions,
+        or a sequence / stacked array -> array of actions."""
+        if isinstance(observations, dict):
+            return {k: self.compute_single_action(o, explore, policy_id)
+                    for k, o in observations.items()}
+        return np.stack([np.asarray(self.compute_single_action(o, explore, policy_id))
+                         for o in observations])
+
+    def get_policy(self, policy_id=None):
+        """Old-stack view: an object with compute_single_action / compute_actions /
+        get_weights / set_weights bound to this algorithm's module ``policy_id``."""
+        return _PolicyView(self, policy_id)
+
+    def set_weights(self, weights):
+        """Load learner weights (the format ``get_weights`` returns) and sync the
+        EnvRunners."""
+        self.learner_group.set_weights(weights)
+        self._sync_weights(self.get_weights())
+
+    def get_config(self):
+        return self.config
+
+    @property
+    def env_runner_group(self):
+        return _EnvRunnerGroupView(self)
+
+    workers = env_runner_group
+
+    def export_policy_model(self, export_dir: str, policy_id=None, onnx=None):
+        """Save the inference module: ``model.pt`` (a TorchScript trace when the module
+        traces, else the pickled module) plus ``state_dict.pt``."""
+        import torch
+
+        if onnx:
+            raise NotImplementedError("ONNX export needs the onnx package (not installed)")
+        os.makedirs(export_dir, exist_ok=True)
+        m = self.get_module(policy_id)
+        torch.save(m.state_dict(), os.path.join(export_dir, "state_dict.pt"))
+        try:
+            sample = torch.as_tensor(self.observation_space.sample()[None])
+            if self.cfg.get("module_kind", "actor_critic") == "actor_critic":
+                traced = torch.jit.trace(lambda x: m.forward_inference(x)[
+                    "action_dist_inputs"], sample)
+            else:
+                traced = torch.jit.trace(m, sample.float())
+            traced.save(os.path.join(export_dir, "model.pt"))
+        except Exception:  # noqa: BLE001  (untraceable module: pickle it)
+            torch.save(m, os.path.join(export_dir, "model.pt"))
+        return export_dir
+
+    export_model = export_policy_model
+
+    def save_checkpoint(self, checkpoint_dir: str):
+        self.save(checkpoint_dir)
+        return checkpoint_dir
+
+    def load_checkpoint(self, checkpoint):
+        self.restore(checkpoint)
 
     compute_action = compute_single_action
 
@@ -376,3 +480,72 @@ class Algorithm:
 
     def __del__(self):
         pass
+
+
+class _PolicyView:
+    def __init__(self, algo, policy_id):
+        self.algo, self.policy_id = algo, policy_id
+        self.observation_space = algo.observation_space
+        self.action_space = algo.action_space
+
+    @property
+    def model(self):
+        return self.algo.get_module(self.policy_id)
+
+    def compute_single_action(self, obs, state=None, explore=None, **kw):
+        a = self.algo.compute_single_action(obs, bool(explore), self.policy_id)
+        return a, [], {}
+
+    def compute_actions(self, obs_batch, state_batches=None, explore=None, **kw):
+        return self.algo.compute_actions(obs_batch, bool(explore), self.policy_id), [], {}
+
+    def get_weights(self):
+        w = self.algo.get_weights()
+        return w[self.policy_id] if self.policy_id is not None and self.policy_id in w else w
+
+    def set_weights(self, weights):
+        if self.policy_id is not None and self.algo.is_multi_agent:
+            full = dict(self.algo.get_weights())
+            full[self.policy_id] = weights
+            weights = full
+        self.algo.set_weights(weights)
+
+
+class _EnvRunnerGroupView:
+    """``algo.env_runner_group`` / ``algo.workers``: the EnvRunner actors (or the local
+    runner when there are none)."""
+
+    def __init__(self, algo):
+        self.algo = algo
+
+    def _all(self):
+        return list(self.algo.env_runners) or [self.algo.local_runner]
+
+    def foreach_env_runner(self, func, local_env_runner=True, remote_worker_ids=None):
+        import cloudpickle
+
+        out = []
+        if self.algo.env_runners:
+            blob = cloudpickle.dumps(func)
+            runners = self.algo.env_runners
+            if remote_worker_ids is not None:
+                runners = [runners[i - 1] for i in remote_worker_ids]
+            out = ray.get([r.apply.remote(blob) for r in runners])
+        elif local_env_runner:
+            out = [func(self.algo.local_runner)]
+        return out
+
+    foreach_worker = foreach_env_runner
+
+    def num_healthy_remote_workers(self) -> int:
+        return len(self.algo.env_runners)
+
+    num_healthy_remote_env_runners = num_healthy_remote_workers
+    num_remote_workers = num_healthy_remote_workers
+
+    def sync_weights(self, *a, **k):
+        self.algo._sync_weights(self.algo.get_weights())
+
+    def local_env_runner(self):
+        return self.algo.local_runner
+

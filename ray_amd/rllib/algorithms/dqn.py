@@ -75,6 +75,10 @@ class _QLearner:
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.q.state_dict().items()}
 
+    def set_weights(self, w):
+        self.q.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+        self.sync_target()
+
     def get_state(self):
         return {"q": self.get_weights(), "opt": self.opt.state_dict()}
 

@@ -95,6 +95,9 @@ class MARWILLearner:
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
 
+    def set_weights(self, w):
+        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+
     def get_state(self):
         return {"module": self.get_weights(), "opt": self.opt.state_dict(), "ma": self.ma_sqd}
 

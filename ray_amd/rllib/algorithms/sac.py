@@ -140,6 +140,9 @@ class SACLearner:
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.pi.state_dict().items()}
 
+    def set_weights(self, w):
+        self.pi.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+
     def get_state(self):
         return {"pi": self.get_weights(),
                 "q": {k: v.detach().cpu() for k, v in self.q.state_dict().items()},

@@ -627,6 +627,13 @@ class LearnerGroup:
 
         return ray.get(self.actors[0].execute.remote(_learner_call, "get_weights"))
 
+    def set_weights(self, w):
+        if not self.remote:
+            return self.local.set_weights(w)
+        import ray_amd as ray
+
+        ray.get([a.execute.remote(_learner_call, "set_weights", w) for a in self.actors])
+
     def get_state(self):
         if not self.remote:
             return self.local.get_state()
@@ -697,6 +704,11 @@ class MultiAgentLearnerGroup:
 
     def get_weights(self):
         return {mid: g.get_weights() for mid, g in self.groups.items()}
+
+    def set_weights(self, w):
+        for mid, wm in w.items():
+            if mid in self.groups:
+                self.groups[mid].set_weights(wm)
 
     def get_state(self):
         return {mid: g.get_state() for mid, g in self.groups.items()}

@@ -133,6 +133,12 @@ class SingleAgentEnvRunner:
         return {k: (v.detach().cpu().float() if v.is_floating_point() else v.detach().cpu())
                 for k, v in self.module.state_dict().items()}
 
+    def apply(self, fn_blob):
+        """Run ``fn(env_runner)`` here (Algorithm.env_runner_group.foreach_env_runner)."""
+        import cloudpickle
+
+        return cloudpickle.loads(fn_blob)(self)
+
     def ping(self):
         return self.worker_index
 

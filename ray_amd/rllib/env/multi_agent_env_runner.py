@@ -144,6 +144,12 @@ class MultiAgentEnvRunner:
         return {mid: {k: v.detach().cpu() for k, v in m.state_dict().items()}
                 for mid, m in self.modules.items()}
 
+    def apply(self, fn_blob):
+        """Run ``fn(env_runner)`` here (Algorithm.env_runner_group.foreach_env_runner)."""
+        import cloudpickle
+
+        return cloudpickle.loads(fn_blob)(self)
+
     def ping(self):
         return self.worker_index
 
