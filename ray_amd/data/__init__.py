@@ -1,5 +1,6 @@
 """ray_amd.data — streaming distributed datasets (reference: python/ray/data)."""
 
+from ray_amd.data import aggregate  # noqa: F401,E402
 from ray_amd.data.dataset import (ActorPoolStrategy, AggregateFn, Count, Dataset,  # noqa: F401
                                   GroupedData, Max, MaterializedDataset, Mean, Min, Std, Sum,
                                   TaskPoolStrategy)

@@ -1,0 +1,221 @@
+"""Aggregations for ``Dataset.aggregate`` and ``groupby(...).aggregate`` (reference:
+python/ray/data/aggregate/_aggregate.py).
+
+An :class:`AggregateFn` is ``init(key) -> acc``, ``accumulate_block(acc, block) -> acc``
+(or the slower ``accumulate_row(acc, row)``), ``merge(acc, acc) -> acc`` and
+``finalize(acc) -> value``. A whole-dataset aggregation accumulates every block in a
+task, then merges the per-block states on the driver; a grouped one runs after the hash
+shuffle, where each group lives in exactly one reduce partition. The built-ins
+accumulate numpy column slices (no per-row Python).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Any, Callable, Optional
+
+import numpy as np
+
+
+class AggregateFn:
+    def __init__(self, init: Callable[[Any], Any], merge: Callable[[Any, Any], Any],
+                 accumulate_row: Optional[Callable[[Any, dict], Any]] = None,
+                 accumulate_block: Optional[Callable[[Any, dict], Any]] = None,
+                 finalize: Optional[Callable[[Any], Any]] = None,
+                 name: Optional[str] = None):
+        if (accumulate_row is None) == (accumulate_block is None):
+            raise ValueError("Exactly one of accumulate_row or accumulate_block must be "
+                             "provided.")
+        if accumulate_block is None:
+            def accumulate_block(acc, block):  # noqa: F811
+                from ray_amd.data import block as B
+
+                for row in B.to_rows(block):
+                    acc = accumulate_row(acc, row)
+                return acc
+        self.init = init
+        self.merge = merge
+        self.accumulate_block = accumulate_block
+        self.finalize = finalize or (lambda a: a)
+        self.name = name or "AggregateFn"
+
+    # whole-dataset evaluation (Dataset.aggregate)
+    def _run(self, ds) -> dict:
+        import ray_amd as ray
+        from ray_amd.data import _executor as X
+
+        parts = ray.get([_accumulate.remote(r, self) for r, _ in X.execute(ds._plan)])
+        acc = None
+        for p in parts:
+            acc = p if acc is None else self.merge(acc, p)
+        if acc is None:
+            acc = self.init(None)
+        return {self.name: self.finalize(acc)}
+
+
+def _col(block, on):
+    v = block.get(on)
+    if v is None:
+        raise KeyError(f"column {on!r} not in block (columns: {list(block)})")
+    return np.asarray(v)
+
+
+def _valid(v, ignore_nulls: bool):
+    if v.dtype == object:
+        mask = np.array([x is not None and not (isinstance(x, float) and math.isnan(x))
+                         for x in v], dtype=bool)
+    elif v.dtype.kind == "f":
+        mask = ~np.isnan(v)
+    else:
+        return v, False
+    return v[mask], (not ignore_nulls) and not mask.all()
+
+
+class _NullSeen:
+    """Accumulator state after a null with ignore_nulls=False (the result is None)."""
+
+
+class _OnColumn(AggregateFn):
+    def __init__(self, kind, on, ignore_nulls, alias_name, init, merge, acc_fn, finalize):
+        self.on = on
+        self.ignore_nulls = ignore_nulls
+
+        def accumulate_block(acc, block):
+            if isinstance(acc, _NullSeen):
+                return acc
+            v, has_null = _valid(_col(block, on), ignore_nulls)
+            if has_null:
+                return _NullSeen()
+            return acc_fn(acc, v) if len(v) else acc
+
+        def merge_(a, b):  # (states cross processes: compare by type, not identity)
+            if isinstance(a, _NullSeen) or isinstance(b, _NullSeen):
+                return _NullSeen()
+            return merge(a, b)
+
+        def finalize_(a):
+            return None if isinstance(a, _NullSeen) else finalize(a)
+
+        super().__init__(init=init, merge=merge_, accumulate_block=accumulate_block,
+                         finalize=finalize_, name=alias_name or f"{kind}({on})")
+
+
+class Count(AggregateFn):
+    def __init__(self, on: Optional[str] = None, ignore_nulls: bool = False,
+                 alias_name: Optional[str] = None):
+        def acc(a, block):
+            from ray_amd.data import block as B
+
+            if on is None:
+                return a + B.num_rows(block)
+            v = _col(block, on)
+            return a + (len(_valid(v, True)[0]) if ignore_nulls else len(v))
+
+        super().__init__(init=lambda k: 0, merge=lambda a, b: a + b, accumulate_block=acc,
+                         name=alias_name or (f"count({on})" if on else "count()"))
+
+
+def _pair(fn):
+    return lambda a, b: b if a is None else (a if b is None else fn(a, b))
+
+
+class Sum(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("sum", on, ignore_nulls, alias_name, lambda k: 0,
+                         lambda a, b: a + b, lambda a, v: a + v.sum().item(), lambda a: a)
+
+
+class Min(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("min", on, ignore_nulls, alias_name, lambda k: None, _pair(min),
+                         lambda a, v: _pair(min)(a, v.min().item()), lambda a: a)
+
+
+class Max(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("max", on, ignore_nulls, alias_name, lambda k: None, _pair(max),
+                         lambda a, v: _pair(max)(a, v.max().item()), lambda a: a)
+
+
+class AbsMax(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("abs_max", on, ignore_nulls, alias_name, lambda k: None, _pair(max),
+                         lambda a, v: _pair(max)(a, np.abs(v).max().item()), lambda a: a)
+
+
+class Mean(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("mean", on, ignore_nulls, alias_name, lambda k: (0.0, 0),
+                         lambda a, b: (a[0] + b[0], a[1] + b[1]),
+                         lambda a, v: (a[0] + float(v.sum()), a[1] + len(v)),
+                         lambda a: a[0] / a[1] if a[1] else None)
+
+
+class Std(_OnColumn):
+    """Chan et al. parallel variance: (count, mean, M2) per block, merged pairwise."""
+
+    def __init__(self, on: str, ddof: int = 1, ignore_nulls: bool = True,
+                 alias_name: Optional[str] = None):
+        def acc(a, v):
+            v = v.astype(np.float64)
+            return merge(a, (len(v), float(v.mean()), float(((v - v.mean()) ** 2).sum())))
+
+        def merge(a, b):
+            n1, m1, s1 = a
+            n2, m2, s2 = b
+            n = n1 + n2
+            if n == 0:
+                return (0, 0.0, 0.0)
+            d = m2 - m1
+            return (n, m1 + d * n2 / n, s1 + s2 + d * d * n1 * n2 / n)
+
+        def fin(a):
+            n, _, m2 = a
+            return math.sqrt(m2 / (n - ddof)) if n - ddof > 0 else (0.0 if n else None)
+
+        super().__init__("std", on, ignore_nulls, alias_name, lambda k: (0, 0.0, 0.0), merge,
+                         acc, fin)
+
+
+class Quantile(_OnColumn):
+    """Exact quantile (the values are gathered; ``q`` in [0, 1], numpy's linear method)."""
+
+    def __init__(self, on: str, q: float = 0.5, ignore_nulls: bool = True,
+                 alias_name: Optional[str] = None):
+        if not 0.0 <= q <= 1.0:
+            raise ValueError("q must be within [0, 1]")
+        super().__init__("quantile", on, ignore_nulls, alias_name, lambda k: [],
+                         lambda a, b: a + b, lambda a, v: a + v.tolist(),
+                         lambda a: float(np.quantile(np.asarray(a, dtype=np.float64), q))
+                         if a else None)
+
+
+class Unique(_OnColumn):
+    def __init__(self, on: str, ignore_nulls: bool = True, alias_name: Optional[str] = None):
+        super().__init__("unique", on, ignore_nulls, alias_name, lambda k: set(),
+                         lambda a, b: a | b,
+                         lambda a, v: a | {x.item() if isinstance(x, np.generic) else x
+                                           for x in v}, lambda a: a)
+
+
+def _remote():
+    import ray_amd as ray
+
+    @ray.remote
+    def accumulate(blk, agg):
+        return agg.accumulate_block(agg.init(None), blk)
+
+    return accumulate
+
+
+class _Lazy:
+    def __init__(self):
+        self.fn = None
+
+    def remote(self, *a):
+        if self.fn is None:
+            self.fn = _remote()
+        return self.fn.remote(*a)
+
+
+_accumulate = _Lazy()

@@ -203,17 +203,17 @@ def _groupby_reduce(key, aggs, map_fn, batch_format, *parts):
         out = B.concat(outs)
         return out, X._meta(out)
     out = {key: uniq}
-    for name, col, op in aggs:
-        vals = []
-        for gi in range(len(uniq)):
-            m = inv == gi
-            if op == "count":
-                vals.append(int(m.sum()))
-                continue
-            v = blk[col][m].astype(np.float64)
-            vals.append({"sum": v.sum(), "mean": v.mean(), "min": v.min(), "max": v.max(),
-                         "std": v.std(ddof=1) if len(v) > 1 else 0.0}[op])
-        out[name] = np.asarray(vals)
+    groups = [B.take_idx(blk, np.nonzero(inv == gi)[0]) for gi in range(len(uniq))]
+    for agg in aggs:  # each group is whole in this partition: no merge step
+        vals = [agg.finalize(agg.accumulate_block(agg.init(k), g))
+                for k, g in zip(uniq, groups)]
+        col = np.empty(len(vals), dtype=object)
+        col[:] = vals
+        try:
+            col = np.asarray(vals) if all(np.isscalar(v) for v in vals) else col
+        except (ValueError, TypeError):
+            pass
+        out[agg.name] = col
     return out, X._meta(out)
 
 
@@ -820,64 +820,32 @@ class GroupedData:
         return Dataset(X.Plan(("lazy", lazy))).sort(key)
 
     def count(self):
-        return self._run([("count()", None, "count")])
+        return self._run([Count()])
 
-    def sum(self, on):
-        return self._run([(f"sum({on})", on, "sum")])
+    def sum(self, on, ignore_nulls=True):
+        return self._run([Sum(on, ignore_nulls)])
 
-    def mean(self, on):
-        return self._run([(f"mean({on})", on, "mean")])
+    def mean(self, on, ignore_nulls=True):
+        return self._run([Mean(on, ignore_nulls)])
 
-    def min(self, on):
-        return self._run([(f"min({on})", on, "min")])
+    def min(self, on, ignore_nulls=True):
+        return self._run([Min(on, ignore_nulls)])
 
-    def max(self, on):
-        return self._run([(f"max({on})", on, "max")])
+    def max(self, on, ignore_nulls=True):
+        return self._run([Max(on, ignore_nulls)])
 
-    def std(self, on, ddof=1):
-        return self._run([(f"std({on})", on, "std")])
+    def std(self, on, ddof=1, ignore_nulls=True):
+        return self._run([Std(on, ddof, ignore_nulls)])
 
     def aggregate(self, *aggs):
-        return self._run([(a.name, a.on, a.op) for a in aggs])
+        return self._run(list(aggs))
 
     def map_groups(self, fn, *, batch_format="default", **kw):
         return self._run(None, fn, "numpy" if batch_format == "default" else batch_format)
 
 
-class AggregateFn:
-    def __init__(self, op, on=None, alias_name=None):
-        self.op = op
-        self.on = on
-        self.name = alias_name or (f"{op}({on})" if on else f"{op}()")
-
-    def _run(self, ds):
-        if self.op == "count":
-            return {self.name: ds.count()}
-        return {self.name: ds._aggregate([self.on])[self.on][self.op]}
-
-
-def Count():  # noqa: N802
-    return AggregateFn("count")
-
-
-def Sum(on, alias_name=None):  # noqa: N802
-    return AggregateFn("sum", on, alias_name)
-
-
-def Mean(on, alias_name=None):  # noqa: N802
-    return AggregateFn("mean", on, alias_name)
-
-
-def Min(on, alias_name=None):  # noqa: N802
-    return AggregateFn("min", on, alias_name)
-
-
-def Max(on, alias_name=None):  # noqa: N802
-    return AggregateFn("max", on, alias_name)
-
-
-def Std(on, alias_name=None):  # noqa: N802
-    return AggregateFn("std", on, alias_name)
+from ray_amd.data.aggregate import (AbsMax, AggregateFn, Count, Max, Mean, Min,  # noqa: E402,F401
+                                    Quantile, Std, Sum, Unique)
 
 
 itertools  # noqa: B018
