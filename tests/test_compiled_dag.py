@@ -190,21 +190,25 @@ def test_compiled_faster_than_remote_chaining(cluster):
     a, b = Stage.remote(1), Stage.remote(1)
     for _ in range(20):
         ray.get(b.fwd.remote(a.fwd.remote(0)))
-    n = 200
-    t = time.perf_counter()
-    for i in range(n):
-        ray.get(b.fwd.remote(a.fwd.remote(i)))
-    t_remote = (time.perf_counter() - t) / n
+    n = 100
+
+    def best_of(fn, rounds=3):  # per-call time, best round (robust to a busy host)
+        out = []
+        for _ in range(rounds):
+            t = time.perf_counter()
+            for i in range(n):
+                fn(i)
+            out.append((time.perf_counter() - t) / n)
+        return min(out)
+
+    t_remote = best_of(lambda i: ray.get(b.fwd.remote(a.fwd.remote(i))))
     with InputNode() as inp:
         dag = b.fwd.bind(a.fwd.bind(inp))
     cdag = dag.experimental_compile()
     try:
         for i in range(20):
             ray.get(cdag.execute(i))
-        t = time.perf_counter()
-        for i in range(n):
-            ray.get(cdag.execute(i))
-        t_comp = (time.perf_counter() - t) / n
+        t_comp = best_of(lambda i: ray.get(cdag.execute(i)))
     finally:
         cdag.teardown()
     print(f"remote chain {t_remote * 1e6:.0f} us, compiled {t_comp * 1e6:.0f} us")
