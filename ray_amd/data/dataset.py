@@ -113,6 +113,51 @@ def _agg_block(blk, cols, ops):
     return out
 
 
+def _key_list(key):
+    return list(key) if isinstance(key, (list, tuple)) else [key]
+
+
+def _first_desc(descending):
+    return bool(descending[0]) if isinstance(descending, (list, tuple)) else bool(descending)
+
+
+def _lex_order(blk, keys, descending):
+    """Stable lexicographic order over ``keys`` (per-key ``descending`` flags allowed):
+    each key is replaced by its dense rank so any sortable dtype works."""
+    if len(keys) == 1 and not isinstance(descending, (list, tuple)):
+        order = np.argsort(blk[keys[0]], kind="stable")
+        return order[::-1] if descending else order
+    desc = list(descending) if isinstance(descending, (list, tuple)) else \
+        [bool(descending)] * len(keys)
+    ranks = []
+    for k, d in zip(keys, desc):
+        _, inv = np.unique(np.asarray(blk[k]), return_inverse=True)
+        ranks.append(-inv if d else inv)
+    return np.lexsort(ranks[::-1])
+
+
+def _stable_hash(x) -> int:
+    """Process-independent hash (Python's str hash is salted per process, so map tasks in
+    different workers would send equal keys to different partitions)."""
+    if isinstance(x, (int, np.integer)) and not isinstance(x, bool):
+        return int(x) & 0x7FFFFFFFFFFFFFFF
+    import zlib
+
+    return zlib.crc32(repr(x).encode())
+
+
+def _hash_keys(blk, keys):
+    cols = [blk[k] for k in keys]
+
+    def norm(x):
+        return x.item() if isinstance(x, np.generic) else \
+            (tuple(x) if isinstance(x, np.ndarray) else x)
+
+    if len(cols) == 1:
+        return [norm(x) for x in cols[0]]
+    return [tuple(norm(x) for x in row) for row in zip(*cols)]
+
+
 @ray.remote
 def _partition_block(blk, n, mode, key, boundaries, seed, descending):
     rows = B.num_rows(blk)
@@ -124,13 +169,12 @@ def _partition_block(blk, n, mode, key, boundaries, seed, descending):
         rng = np.random.default_rng(seed)
         assign = rng.integers(0, n, size=rows)
     elif mode == "hash":
-        col = blk[key]
-        assign = np.array([hash(x.item() if isinstance(x, np.generic) else
-                                (tuple(x) if isinstance(x, np.ndarray) else x)) % n
-                           for x in col], dtype=np.int64)
-    elif mode == "range":
-        assign = np.searchsorted(np.asarray(boundaries), blk[key], side="right")
-        if descending:
+        assign = np.array([_stable_hash(x) % n for x in _hash_keys(blk, _key_list(key))],
+                          dtype=np.int64)
+    elif mode == "range":  # by the first sort key; equal first keys share a partition
+        assign = np.searchsorted(np.asarray(boundaries), blk[_key_list(key)[0]],
+                                 side="right")
+        if _first_desc(descending):
             assign = (n - 1) - assign
     else:  # contiguous split
         assign = np.minimum((np.arange(rows) * n) // rows, n - 1)
@@ -151,10 +195,7 @@ def _reduce_parts(mode, key, descending, seed, *parts):
         idx = np.random.default_rng(seed).permutation(B.num_rows(blk))
         blk = B.take_idx(blk, idx)
     elif mode == "range" and B.num_rows(blk):
-        order = np.argsort(blk[key], kind="stable")
-        if descending:
-            order = order[::-1]
-        blk = B.take_idx(blk, order)
+        blk = B.take_idx(blk, _lex_order(blk, _key_list(key), descending))
     return blk, X._meta(blk)
 
 
@@ -193,8 +234,15 @@ def _groupby_reduce(key, aggs, map_fn, batch_format, *parts):
     blk = B.concat(list(parts))
     if B.num_rows(blk) == 0:
         return {}, X._meta({})
-    keys = blk[key]
-    uniq, inv = np.unique(keys, return_inverse=True)
+    kl = _key_list(key)
+    if len(kl) == 1:
+        uniq, inv = np.unique(blk[kl[0]], return_inverse=True)
+    else:  # composite keys: dense ids over the key tuples, in sorted tuple order
+        tuples = _hash_keys(blk, kl)
+        order = sorted(set(tuples))
+        idx = {t: i for i, t in enumerate(order)}
+        inv = np.array([idx[t] for t in tuples], dtype=np.int64)
+        uniq = order
     if map_fn is not None:
         outs = []
         for gi in range(len(uniq)):
@@ -202,7 +250,10 @@ def _groupby_reduce(key, aggs, map_fn, batch_format, *parts):
             outs.append(B.from_batch(map_fn(B.to_batch(g, batch_format))))
         out = B.concat(outs)
         return out, X._meta(out)
-    out = {key: uniq}
+    if len(kl) == 1:
+        out = {kl[0]: uniq}
+    else:
+        out = {k: np.asarray([t[j] for t in uniq]) for j, k in enumerate(kl)}
     groups = [B.take_idx(blk, np.nonzero(inv == gi)[0]) for gi in range(len(uniq))]
     for agg in aggs:  # each group is whole in this partition: no merge step
         vals = [agg.finalize(agg.accumulate_block(agg.init(k), g))
@@ -436,25 +487,28 @@ class Dataset:
 
         return Dataset(X.Plan(("lazy", lazy)))
 
-    def sort(self, key, descending: bool = False, **kw) -> "Dataset":
-        if isinstance(key, (list, tuple)):
-            key = key[0]
+    def sort(self, key, descending=False, **kw) -> "Dataset":
+        """Sort by one key or several (lexicographic; ``descending`` a bool or one flag
+        per key): range-partitioned by the first key, each partition sorted by all."""
+        keys = _key_list(key)
+        if isinstance(descending, (list, tuple)) and len(descending) != len(keys):
+            raise ValueError("descending must be a bool or one flag per sort key")
         parent = self
 
         def lazy():
             refs, metas = parent._blocks()
             n = max(1, len(refs))
-            samples = np.concatenate([s for s in ray.get([_sample_keys.remote(r, key, 64)
+            samples = np.concatenate([s for s in ray.get([_sample_keys.remote(r, keys[0], 64)
                                                           for r in refs]) if len(s)] or
                                      [np.array([])])
-            bounds = np.quantile(np.sort(samples), np.linspace(0, 1, n + 1)[1:-1]) \
+            # boundaries are sample elements at the quantile positions (no interpolation:
+            # works for strings and any other sortable key type)
+            srt = np.sort(samples)
+            bounds = srt[(np.linspace(0, 1, n + 1)[1:-1] * (len(srt) - 1)).astype(int)] \
                 if len(samples) else []
-            ds = parent._shuffle(n, "range", key=key, boundaries=list(bounds),
-                                 descending=descending)
-            r2, m2 = ds._blocks()
-            if descending:
-                pass
-            return r2, m2
+            ds = parent._shuffle(n, "range", key=keys if len(keys) > 1 else keys[0],
+                                 boundaries=list(bounds), descending=descending)
+            return ds._blocks()
 
         return Dataset(X.Plan(("lazy", lazy)))
 
@@ -798,7 +852,7 @@ class MaterializedDataset(Dataset):
 class GroupedData:
     def __init__(self, ds: Dataset, key):
         self._ds = ds
-        self._key = key if isinstance(key, str) else key[0]
+        self._key = key if isinstance(key, str) else list(key)
 
     def _run(self, aggs=None, map_fn=None, batch_format="numpy"):
         key = self._key

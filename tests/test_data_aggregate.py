@@ -89,3 +89,25 @@ def test_custom_aggregate_fn_rows_and_blocks():
                     name="spread")).take_all()
     assert [r["spread"] for r in g] == [27, 27, 27]
     assert not math.isnan(rd.range(10).aggregate(Mean("id"))["mean(id)"])
+
+
+def test_multi_key_sort_and_groupby_match_pandas():
+    rng = np.random.default_rng(3)
+    df = pd.DataFrame({"a": rng.integers(0, 3, 120), "b": rng.choice(["x", "y", "z"], 120),
+                       "v": rng.normal(size=120)})
+    ds = rd.from_pandas(df).repartition(6)
+    got = ds.sort(["a", "b"], descending=[False, True]).to_pandas()
+    exp = df.sort_values(["a", "b"], ascending=[True, False], kind="stable")
+    assert list(zip(got.a, got.b)) == list(zip(exp.a, exp.b))
+    got = ds.sort(["b", "a"]).to_pandas()
+    exp = df.sort_values(["b", "a"], kind="stable")
+    assert list(zip(got.b, got.a)) == list(zip(exp.b, exp.a))
+    rows = ds.groupby(["a", "b"]).aggregate(Count(), Sum("v")).take_all()
+    ref = df.groupby(["a", "b"])
+    assert [(r["a"], r["b"]) for r in rows] == sorted(ref.groups.keys())
+    for r in rows:
+        sub = ref.get_group((r["a"], r["b"]))
+        assert r["count()"] == len(sub) and r["sum(v)"] == pytest.approx(sub.v.sum())
+    sizes = ds.groupby(["a", "b"]).map_groups(
+        lambda g: {"a": g["a"][:1], "b": g["b"][:1], "n": np.array([len(g["v"])])}).take_all()
+    assert sum(int(r["n"]) for r in sizes) == 120 and len(sizes) == len(ref.groups)
