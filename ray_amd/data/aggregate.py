@@ -41,16 +41,7 @@ class AggregateFn:
 
     # whole-dataset evaluation (Dataset.aggregate)
     def _run(self, ds) -> dict:
-        import ray_amd as ray
-        from ray_amd.data import _executor as X
-
-        parts = ray.get([_accumulate.remote(r, self) for r, _ in X.execute(ds._plan)])
-        acc = None
-        for p in parts:
-            acc = p if acc is None else self.merge(acc, p)
-        if acc is None:
-            acc = self.init(None)
-        return {self.name: self.finalize(acc)}
+        return run_many(ds, [self])
 
 
 def _col(block, on):
@@ -198,12 +189,29 @@ class Unique(_OnColumn):
                                            for x in v}, lambda a: a)
 
 
+def run_many(ds, aggs) -> dict:
+    """Evaluate several AggregateFns over a dataset in ONE pass over its blocks."""
+    import ray_amd as ray
+    from ray_amd.data import _executor as X
+
+    parts = ray.get([_accumulate.remote(r, aggs) for r, _ in X.execute(ds._plan)])
+    out = {}
+    for i, agg in enumerate(aggs):
+        acc = None
+        for p in parts:
+            acc = p[i] if acc is None else agg.merge(acc, p[i])
+        if acc is None:
+            acc = agg.init(None)
+        out[agg.name] = agg.finalize(acc)
+    return out
+
+
 def _remote():
     import ray_amd as ray
 
     @ray.remote
-    def accumulate(blk, agg):
-        return agg.accumulate_block(agg.init(None), blk)
+    def accumulate(blk, aggs):
+        return [a.accumulate_block(a.init(None), blk) for a in aggs]
 
     return accumulate
 

@@ -728,26 +728,34 @@ class Dataset:
         vals = [a[c][what] for c in cols]
         return vals[0] if len(vals) == 1 else vals
 
-    def sum(self, on=None, **kw):
-        return self._single(on, "sum")
+    def _agg_cols(self, on, make):
+        cols = self.columns() if on is None else ([on] if isinstance(on, str) else list(on))
+        aggs = [make(c) for c in cols]
+        out = self.aggregate(*aggs)
+        vals = [out[a.name] for a in aggs]
+        return vals[0] if len(vals) == 1 else vals
 
-    def min(self, on=None, **kw):
-        return self._single(on, "min")
+    def sum(self, on=None, ignore_nulls=True, **kw):
+        return self._agg_cols(on, lambda c: Sum(c, ignore_nulls))
 
-    def max(self, on=None, **kw):
-        return self._single(on, "max")
+    def min(self, on=None, ignore_nulls=True, **kw):
+        return self._agg_cols(on, lambda c: Min(c, ignore_nulls))
 
-    def mean(self, on=None, **kw):
-        return self._single(on, "mean")
+    def max(self, on=None, ignore_nulls=True, **kw):
+        return self._agg_cols(on, lambda c: Max(c, ignore_nulls))
 
-    def std(self, on=None, ddof=1, **kw):
-        return self._single(on, "std")
+    def mean(self, on=None, ignore_nulls=True, **kw):
+        return self._agg_cols(on, lambda c: Mean(c, ignore_nulls))
+
+    def std(self, on=None, ddof=1, ignore_nulls=True, **kw):
+        return self._agg_cols(on, lambda c: Std(c, ddof, ignore_nulls))
 
     def aggregate(self, *aggs):
-        out = {}
-        for a in aggs:
-            out.update(a._run(self))
-        return out
+        """All aggregations in one pass over the blocks: each task accumulates every
+        AggregateFn on its block; the per-block states merge on the driver."""
+        from ray_amd.data.aggregate import run_many
+
+        return run_many(self, list(aggs))
 
     def to_pandas(self, limit=None):
         import pandas as pd

@@ -111,3 +111,13 @@ def test_multi_key_sort_and_groupby_match_pandas():
     sizes = ds.groupby(["a", "b"]).map_groups(
         lambda g: {"a": g["a"][:1], "b": g["b"][:1], "n": np.array([len(g["v"])])}).take_all()
     assert sum(int(r["n"]) for r in sizes) == 120 and len(sizes) == len(ref.groups)
+
+
+def test_dataset_convenience_aggregations():
+    df = _df(150, 4)
+    ds = rd.from_pandas(df).repartition(4)
+    assert ds.sum("y") == df.y.sum()
+    assert ds.std("x", ddof=0) == pytest.approx(df.x.std(ddof=0))
+    assert ds.std("x") == pytest.approx(df.x.std(ddof=1))
+    assert ds.mean(["x", "y"]) == pytest.approx([df.x.mean(), df.y.mean()])
+    assert ds.min("y") == df.y.min() and ds.max("y") == df.y.max()
