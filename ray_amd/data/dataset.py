@@ -542,10 +542,9 @@ class Dataset:
         return Dataset(X.Plan(("lazy", lazy)))
 
     def unique(self, column: str) -> list:
-        vals = set()
-        for b in self.iter_batches(batch_size=None):
-            vals.update(np.unique(b[column]).tolist())
-        return sorted(vals)
+        """Distinct values (per-block sets in tasks, unioned on the driver)."""
+        vals = self.aggregate(Unique(column, ignore_nulls=False))[f"unique({column})"]
+        return sorted(vals or set())
 
     # ------------------------------------------------------------- splitting
     def split(self, n: int, *, equal: bool = False, locality_hints=None) -> list:

@@ -263,6 +263,9 @@ def run(target: Application, *, name: str = "default", route_prefix: str | None 
     return handle
 
 
+_run = run  # reference: serve._run (internal alias used by tooling)
+
+
 def delete(name: str, _blocking: bool = True):
     ray.get(_get_controller().delete_application.remote(name))
     from ray_amd.serve import handle as H
