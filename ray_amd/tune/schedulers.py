@@ -191,6 +191,11 @@ class PopulationBasedTraining(TrialScheduler):
         k = max(1, int(math.ceil(n * self.q))) if n > 1 else 0
         bottom = [tr for _, tr in ranked[:k]]
         top = [tr for _, tr in ranked[-k:]] if k else []
+        if trial in top and hasattr(runner, "_save_trial"):
+            # a top trial checkpoints at its perturbation interval so bottom trials can
+            # clone it (class trainables save on demand; reference: PBT
+            # _checkpoint_or_exploit)
+            runner._save_trial(trial)
         if trial in bottom and top and trial not in top:
             donor = self.rng.choice(top)
             if donor.last_checkpoint is not None:

@@ -419,6 +419,19 @@ class _Controller:
             self.cb.fire("on_trial_save", trials=self.trials, trial=t)
             self.cb.fire("on_checkpoint", trials=self.trials, trial=t, checkpoint=ck)
 
+    def _save_trial(self, t):
+        """Checkpoint a running class-trainable trial now (between its train() calls)."""
+        if t.actor is None:
+            return None
+        try:
+            path = ray.get(t.actor.save.remote(), timeout=120)
+        except Exception:  # noqa: BLE001
+            return None
+        if path:
+            t.last_checkpoint = path
+            self._log_checkpoint(t, path)
+        return path
+
     def _log_checkpoint(self, t, path):
         ck = Checkpoint(path)
         self.cb.fire("on_trial_save", trials=self.trials, trial=t)

@@ -75,3 +75,43 @@ def test_tune_writes_tensorboard_scalars(tmp_path):
         assert seen == {1.0: {1: 1.0, 2: 2.0, 3: 3.0}, 2.0: {1: 2.0, 2: 4.0, 3: 6.0}}
     finally:
         ray.shutdown()
+
+
+def test_pbt_exploits_class_trainables_without_checkpoint_frequency(tmp_path):
+    """PBT makes top class-trainable trials checkpoint at their perturbation interval, so
+    bottom trials can clone them even when no checkpoint_frequency is configured."""
+    from ray_amd.tune.schedulers import PopulationBasedTraining
+
+    class Climb(tune.Trainable):
+        def setup(self, config):
+            self.value = 0.0
+            self.restored_from = None
+
+        def step(self):
+            self.value += self.config["lr"]
+            return {"score": self.value, "restored": self.restored_from is not None}
+
+        def save_checkpoint(self, d):
+            return {"value": self.value}
+
+        def load_checkpoint(self, state):
+            self.value = state["value"]
+            self.restored_from = state
+
+    ray.init(num_cpus=4)
+    try:
+        pbt = PopulationBasedTraining(time_attr="training_iteration", metric="score",
+                                      mode="max", perturbation_interval=2,
+                                      hyperparam_mutations={"lr": [0.1, 1.0, 10.0]},
+                                      quantile_fraction=0.5, seed=0)
+        grid = tune.Tuner(
+            Climb, param_space={"lr": tune.grid_search([0.1, 10.0])},
+            tune_config=tune.TuneConfig(scheduler=pbt, metric="score", mode="max"),
+            run_config=tune.RunConfig(stop={"training_iteration": 8},
+                                      storage_path=str(tmp_path), name="pbtc")).fit()
+        assert not grid.errors
+        assert pbt.num_perturbations >= 1
+        # the slow trial cloned the fast one's state: it ends far above 8 * 0.1
+        assert min(r.metrics["score"] for r in grid) > 8 * 0.1 + 1.0
+    finally:
+        ray.shutdown()
