@@ -119,10 +119,14 @@ class _Lease:
 
 class _ActorConn:
     __slots__ = ("actor_id", "state", "addr", "queue", "inflight", "seq", "subscribed",
-                 "death", "max_task_retries", "num_restarts", "lost")
+                 "death", "max_task_retries", "num_restarts", "lost", "release_when_idle")
 
     def __init__(self, actor_id):
         self.actor_id = actor_id
+        # every handle is gone but submitted calls are still queued / running: the actor
+        # is released once they have replied (reference: out-of-scope actors finish the
+        # tasks already submitted to them)
+        self.release_when_idle = False
         self.state = P.PENDING_CREATION
         self.addr = None
         self.queue = collections.deque()
@@ -2048,11 +2052,18 @@ class CoreWorker:
                 self._on_actor_conn_lost(ac)
 
     def _on_actor_task_reply(self, spec, returns, extra):
+        release = False
         with self.lock:
             ac = self.actors.get(spec["actor_id"])
             if ac is not None:
                 ac.inflight.pop(spec["tid"], None)
+                if ac.release_when_idle and not ac.inflight and not ac.queue and \
+                        self.actor_handle_counts.get(ac.actor_id, 0) <= 0:
+                    ac.release_when_idle = False
+                    release = True
         self._complete(spec, returns, extra)
+        if release and not self._stopped:
+            self.notify_raylet("actor_out_of_scope", spec["actor_id"])
 
     def kill_actor(self, actor_id, no_restart=True):
         self.call_raylet("kill_actor", actor_id, no_restart)
@@ -2068,6 +2079,10 @@ class CoreWorker:
             if self.actor_handle_counts[actor_id] <= 0:
                 del self.actor_handle_counts[actor_id]
                 kill = (owner_addr == self.addr and actor_id not in self.actor_escaped)
+                ac = self.actors.get(actor_id)
+                if kill and ac is not None and (ac.inflight or ac.queue):
+                    ac.release_when_idle = True  # after the submitted calls reply
+                    kill = False
         if kill and not self._stopped:
             self.notify_raylet("actor_out_of_scope", actor_id)
 

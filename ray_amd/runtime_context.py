@@ -40,6 +40,38 @@ class RuntimeContext:
         t = getattr(self._cw.current_task, "tid", None)
         return t.hex() if t else None
 
+    def get_task_name(self):
+        """The current task's name (``options(name=...)`` or the function / method)."""
+        spec = getattr(self._cw.current_task, "spec", None)
+        if not spec:
+            return None
+        m = spec.get("method")
+        if m and spec.get("name") in (None, m):  # actor call: "Class.method"
+            inst = self._cw.actor_instance
+            return f"{type(inst).__name__}.{m}" if inst is not None else m
+        return spec.get("name") or m
+
+    def get_task_function_name(self):
+        """Fully qualified name of the function (or ``Class.method``) being executed."""
+        spec = getattr(self._cw.current_task, "spec", None)
+        if not spec:
+            return None
+        if spec.get("method"):
+            inst = self._cw.actor_instance
+            cls = type(inst) if inst is not None else None
+            qual = f"{cls.__module__}.{cls.__qualname__}" if cls else "actor"
+            return f"{qual}.{spec['method']}"
+        fn = self._cw._load_function(spec["fn"]) if spec.get("fn") is not None else None
+        if fn is None:
+            return spec.get("name")
+        return f"{getattr(fn, '__module__', '')}.{getattr(fn, '__qualname__', fn)}"
+
+    def get(self):
+        """Deprecated dict form of the context (reference: RuntimeContext.get)."""
+        return {"job_id": self.get_job_id(), "node_id": self.get_node_id(),
+                "namespace": self.namespace, "task_id": self.get_task_id(),
+                "actor_id": self.get_actor_id()}
+
     def get_actor_id(self):
         a = self._cw.actor_id
         return a.hex() if a else None

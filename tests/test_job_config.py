@@ -69,3 +69,31 @@ def test_types_and_serialization_modules():
     assert callable(register_serializer) and callable(deregister_serializer)
     ok, _ = inspect_serializability(lambda: 1, name="fn")
     assert ok
+
+
+def test_runtime_context_task_names_and_out_of_scope_actor_finishes_calls():
+    ray.init(num_cpus=2)
+    try:
+        @ray.remote
+        def my_fn():
+            c = ray.get_runtime_context()
+            return c.get_task_name(), c.get_task_function_name()
+
+        @ray.remote
+        class A:
+            def m(self):
+                import time
+
+                time.sleep(0.3)
+                c = ray.get_runtime_context()
+                return c.get_task_name(), c.get_task_function_name()
+
+        name, fq = ray.get(my_fn.remote())
+        assert name.endswith("my_fn") and fq.endswith(".my_fn")
+        assert ray.get(my_fn.options(name="custom").remote())[0] == "custom"
+        # the handle is dropped right after submitting: the call still completes
+        name, fq = ray.get(A.remote().m.remote())
+        assert name == "A.m" and fq.endswith("A.m")
+        assert ray.get_runtime_context().get()["namespace"]
+    finally:
+        ray.shutdown()
