@@ -88,6 +88,9 @@ def test_pbt_exploits_class_trainables_without_checkpoint_frequency(tmp_path):
             self.restored_from = None
 
         def step(self):
+            import time
+
+            time.sleep(0.1)  # both trials run side by side (PBT ranks live trials)
             self.value += self.config["lr"]
             return {"score": self.value, "restored": self.restored_from is not None}
 
