@@ -195,10 +195,14 @@ def run_many(ds, aggs) -> dict:
     from ray_amd.data import _executor as X
 
     parts = ray.get([_accumulate.remote(r, aggs) for r, _ in X.execute(ds._plan)])
+    rows = sum(n for n, _ in parts)
     out = {}
     for i, agg in enumerate(aggs):
+        if rows == 0 and isinstance(agg, _OnColumn):
+            out[agg.name] = None  # an empty dataset aggregates to null (reference)
+            continue
         acc = None
-        for p in parts:
+        for _, p in parts:
             acc = p[i] if acc is None else agg.merge(acc, p[i])
         if acc is None:
             acc = agg.init(None)
@@ -211,7 +215,12 @@ def _remote():
 
     @ray.remote
     def accumulate(blk, aggs):
-        return [a.accumulate_block(a.init(None), blk) for a in aggs]
+        from ray_amd.data import block as B
+
+        n = B.num_rows(blk) if blk else 0
+        if n == 0:  # (an empty block has no columns to look up)
+            return 0, [a.init(None) for a in aggs]
+        return n, [a.accumulate_block(a.init(None), blk) for a in aggs]
 
     return accumulate
 

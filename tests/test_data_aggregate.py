@@ -121,3 +121,9 @@ def test_dataset_convenience_aggregations():
     assert ds.std("x") == pytest.approx(df.x.std(ddof=1))
     assert ds.mean(["x", "y"]) == pytest.approx([df.x.mean(), df.y.mean()])
     assert ds.min("y") == df.y.min() and ds.max("y") == df.y.max()
+
+
+def test_empty_dataset_aggregates_to_null():
+    ds = rd.range(10).filter(lambda r: r["id"] > 100)
+    out = ds.aggregate(Count(), Sum("id"), Mean("id"), Max("id"))
+    assert out == {"count()": 0, "sum(id)": None, "mean(id)": None, "max(id)": None}
