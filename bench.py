@@ -57,6 +57,10 @@ def parse():
                     help="tokens per fused LM-head + cross-entropy chunk (65536 = the whole "
                          "64x1024 micro-batch in one chunk: 6.6 GB of bf16 logits, the "
                          "fastest on MI355X, profiles/r3/chunk/README.md)")
+    ap.add_argument("--ddp-hooks", default="auto", choices=["auto", "always"],
+                    help="gpt2: 'always' runs FlatDDP's bucket hooks, per-bucket events, comm "
+                         "stream and RCCL all-reduce launches even at world size 1 (measures "
+                         "the overlap machinery's cost on one GPU)")
     ap.add_argument("--model", default="small")
     ap.add_argument("--data-path", default="hbm", choices=["hbm", "h2d"],
                     help="data workload: GPU-preprocessed device blocks through the HBM "
@@ -74,7 +78,7 @@ def _gpt2_config(args) -> dict:
     return dict(model=args.model, micro_batch=args.micro_batch, seq_len=args.seq_len,
                 steps=args.steps, warmup=args.warmup, grad_accum=args.grad_accum,
                 bucket_mb=args.bucket_mb, grad_dtype=args.grad_dtype, tunableop=args.tunableop,
-                lm_head_chunk=args.lm_head_chunk, device=args.device)
+                lm_head_chunk=args.lm_head_chunk, device=args.device, ddp_hooks=args.ddp_hooks)
 
 
 def _emit(args, r: dict, mode: str, n_gpus: int):
@@ -105,6 +109,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
             "wgrad_gemm": r.get("wgrad_gemm"),
             "lm_head_chunk": args.lm_head_chunk,
             "launcher": mode,
+            "ddp_hooks": r.get("ddp_hooks"),
         },
         "rccl_world_size": r["rccl_world_size"],
         "dist_backend": r["dist_backend"],
@@ -112,6 +117,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
         "ranks_in_sync": r["ranks_in_sync"],
         "model_tflops_per_gpu": round(r["model_tflops_per_gpu"], 1),
         "final_loss": round(r["loss"], 4),
+        "ddp_allreduce_launches": r.get("ddp_allreduce_launches"),
     }
     print(json.dumps(out), flush=True)
 
@@ -138,12 +144,17 @@ def bench_gpt2_bare(args):
     else:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        if world > 1:
+        if world == 1 and args.ddp_hooks == "always":  # a world-1 RCCL group to hook into
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if world > 1 or args.ddp_hooks == "always":
             dist.init_process_group("nccl", device_id=dev)
     r = run_steps(_gpt2_config(args), dev, rank, world)
     if rank == 0:
         _emit(args, r, "torch.distributed.run (no Ray)", world)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -863,6 +863,7 @@ class CoreWorker:
                     val = ("lost", None)
                 elif o.inline is not None:
                     val = ("inline", o.inline)
+                    o.accessed = True  # a borrower reads it (no false "Unhandled error")
                 else:
                     val = ("store", o.node or self.node_hex)
             self._reply(conn, rid, True, val)
@@ -1306,6 +1307,7 @@ class CoreWorker:
         with self.lock:
             o = self.owned.get(oid)
             if o is not None and o.ready and o.inline is not None:
+                o.accessed = True  # inlined into a task: the receiver reads it
                 return (oid, ref._owner, o.inline)
         return (oid, ref._owner, None)
 
@@ -1596,6 +1598,11 @@ class CoreWorker:
         tid = spec["tid"]
         with self.lock:
             self.task_specs.pop(tid, None)
+        # a failed call of a handle-less actor may be the one it was waiting for
+        # (connection loss, the lost-task fallback timer, a dead actor)
+        if spec["type"] == P.ACTOR_TASK and self._actor_call_finished(spec) and \
+                not self._stopped:
+            self.notify_raylet("actor_out_of_scope", spec["actor_id"])
         if spec["nret"] == -1:
             st = self.streams.get(tid)
             if st is not None:
@@ -1676,6 +1683,11 @@ class CoreWorker:
         tid = spec["tid"]
         with self.lock:
             self.task_specs.pop(tid, None)
+        # a failed call of a handle-less actor may be the one it was waiting for
+        # (connection loss, the lost-task fallback timer, a dead actor)
+        if spec["type"] == P.ACTOR_TASK and self._actor_call_finished(spec) and \
+                not self._stopped:
+            self.notify_raylet("actor_out_of_scope", spec["actor_id"])
         if spec["nret"] == -1:
             st = self.streams.get(tid)
             if st is not None:
@@ -2051,16 +2063,26 @@ class CoreWorker:
             if ac is not None:
                 self._on_actor_conn_lost(ac)
 
-    def _on_actor_task_reply(self, spec, returns, extra):
-        release = False
+    def _actor_call_finished(self, spec) -> bool:
+        """Drop a finished (replied OR failed) actor call from its connection's books;
+        True when that was the last call keeping a handle-less actor alive, i.e. the
+        caller must now send ``actor_out_of_scope``."""
         with self.lock:
             ac = self.actors.get(spec["actor_id"])
-            if ac is not None:
-                ac.inflight.pop(spec["tid"], None)
-                if ac.release_when_idle and not ac.inflight and not ac.queue and \
-                        self.actor_handle_counts.get(ac.actor_id, 0) <= 0:
-                    ac.release_when_idle = False
-                    release = True
+            if ac is None:
+                return False
+            tid = spec["tid"]
+            ac.inflight.pop(tid, None)
+            if ac.queue:
+                ac.queue = type(ac.queue)(s_ for s_ in ac.queue if s_["tid"] != tid)
+            if ac.release_when_idle and not ac.inflight and not ac.queue and \
+                    self.actor_handle_counts.get(ac.actor_id, 0) <= 0:
+                ac.release_when_idle = False
+                return True
+        return False
+
+    def _on_actor_task_reply(self, spec, returns, extra):
+        release = self._actor_call_finished(spec)
         self._complete(spec, returns, extra)
         if release and not self._stopped:
             self.notify_raylet("actor_out_of_scope", spec["actor_id"])

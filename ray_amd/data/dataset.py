@@ -136,11 +136,28 @@ def _lex_order(blk, keys, descending):
     return np.lexsort(ranks[::-1])
 
 
+def _sort_key(v):
+    """Total order over mixed values (numbers before strings before everything else)."""
+    if isinstance(v, (bool, int, float, np.integer, np.floating)):
+        return (0, float(v), "")
+    if isinstance(v, str):
+        return (1, 0.0, v)
+    return (2, 0.0, repr(v))
+
+
 def _stable_hash(x) -> int:
     """Process-independent hash (Python's str hash is salted per process, so map tasks in
-    different workers would send equal keys to different partitions)."""
-    if isinstance(x, (int, np.integer)) and not isinstance(x, bool):
+    different workers would send equal keys to different partitions). Numbers that compare
+    equal hash equal across dtypes (1 == 1.0 == True, as Python's hash): integral floats
+    and bools hash as their int value."""
+    if isinstance(x, (bool, np.bool_)):
+        x = int(x)
+    elif isinstance(x, (float, np.floating)) and float(x).is_integer():
+        x = int(x)
+    if isinstance(x, (int, np.integer)):
         return int(x) & 0x7FFFFFFFFFFFFFFF
+    if isinstance(x, (float, np.floating)):
+        x = float(x)  # np.float32(0.5) and 0.5 share one repr
     import zlib
 
     return zlib.crc32(repr(x).encode())
@@ -542,9 +559,22 @@ class Dataset:
         return Dataset(X.Plan(("lazy", lazy)))
 
     def unique(self, column: str) -> list:
-        """Distinct values (per-block sets in tasks, unioned on the driver)."""
-        vals = self.aggregate(Unique(column, ignore_nulls=False))[f"unique({column})"]
-        return sorted(vals or set())
+        """Distinct values (per-block sets in tasks, unioned on the driver). A null (None /
+        NaN) counts as one distinct value, listed last (reference: groupby(column).count()
+        keeps the null group)."""
+        from ray_amd.data.aggregate import AggregateFn, _col, _valid
+
+        def acc(a, blk):
+            v, _ = _valid(_col(blk, column), True)
+            n_null = len(np.asarray(blk[column])) - len(v)
+            return (a[0] | set(v.tolist()), a[1] or n_null > 0)
+
+        fn = AggregateFn(init=lambda k: (set(), False), accumulate_block=acc,
+                         merge=lambda a, b: (a[0] | b[0], a[1] or b[1]),
+                         name=f"unique({column})")
+        vals, has_null = self.aggregate(fn)[f"unique({column})"] or (set(), False)
+        out = sorted(vals, key=_sort_key)
+        return out + [None] if has_null else out
 
     # ------------------------------------------------------------- splitting
     def split(self, n: int, *, equal: bool = False, locality_hints=None) -> list:

@@ -87,6 +87,10 @@ _SIGS = {
     "ra_lt_num_cands_batched": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long],
     "ra_lt_set_choice_batched": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long,
                                                                   c_int],
+    "ra_lt_choice_name": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long,
+                                                           ctypes.c_char_p, c_int],
+    "ra_lt_allow_streamk": [c_int],
+    "ra_lt_choice_is_streamk": [c_int, c_int] + [c_long] * 6 + [c_int, c_long, c_long, c_long],
     "ra_image_normalize": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                            c_int, c_void_p],
     "ra_resize_bilinear": [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p],

@@ -12,9 +12,12 @@
 #include "common.h"
 
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <map>
+#include <cstring>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -26,6 +29,8 @@ struct LtPlan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
   std::vector<hipblasLtMatmulHeuristicResult_t> cands;
+  std::vector<signed char> streamk;  // per candidate: 1 = stream-K kernel
+  bool sk_only = false;  // hipBLASLt offers nothing but stream-K for this shape
   int choice = 0;
 };
 
@@ -47,6 +52,41 @@ void* workspace(hipStream_t st) {
   if (hipMalloc(&w, kWs) != hipSuccess) return nullptr;
   g_ws_by_stream[st] = w;
   return w;
+}
+
+// Stream-K policy. On gfx950 every hipBLASLt bf16 kernel is a Tensile StreamK=3 kernel
+// (`..._SK3_SKXCCM8_...` in every name, tests/test_train_gpu.py): whether a launch splits
+// K across workgroups (with a fixup in which the tile's owner spin-waits on the partial
+// tiles of later workgroups of the SAME grid) is decided per launch from the problem size.
+// ra_lt_allow_streamk(0) (RAY_AMD_LT_NO_STREAMK=1) restricts choices to kernels without a
+// stream-K tag where any exist; a plan with nothing else keeps its candidates (sk_only).
+bool g_allow_sk = true;
+
+bool is_streamk_name(const std::string& n) {
+  for (size_t i = n.find("_SK"); i != std::string::npos; i = n.find("_SK", i + 1))
+    if (i + 3 < n.size() && n[i + 3] >= '0' && n[i + 3] <= '9') return true;
+  return n.find("StreamK") != std::string::npos;
+}
+
+std::string cand_name(LtPlan* p, int i) {
+  return hipblaslt_ext::getKernelNameFromAlgo(g_handle, p->cands[i].algo);
+}
+
+bool cand_sk(LtPlan* p, int i) {
+  if (p->streamk.size() != p->cands.size()) {
+    p->streamk.assign(p->cands.size(), 0);
+    for (size_t j = 0; j < p->cands.size(); ++j)
+      p->streamk[j] = is_streamk_name(cand_name(p, (int)j)) ? 1 : 0;
+  }
+  return p->streamk[i] != 0;
+}
+
+bool usable(LtPlan* p, int i) { return g_allow_sk || p->sk_only || !cand_sk(p, i); }
+
+int first_usable(LtPlan* p) {
+  for (int i = 0; i < (int)p->cands.size(); ++i)
+    if (usable(p, i)) return i;
+  return -1;
 }
 
 int init_handle() {
@@ -93,6 +133,11 @@ LtPlan* get_plan(int ta, int tb, long m, long n, long k, long lda, long ldb, lon
   for (int i = 0; i < got; ++i)
     if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= kWs)
       p->cands.push_back(res[i]);
+  const int f = first_usable(p);
+  // only stream-K solutions (small shapes on gfx950): keep them, flagged; the caller then
+  // runs this GEMM on the main stream (ra_lt_choice_is_streamk), never beside another GEMM
+  if (f < 0 && !p->cands.empty()) p->sk_only = true;
+  else if (f >= 0) p->choice = f;
   g_plans[key] = p;
   return p;
 }
@@ -120,6 +165,7 @@ RA_EXPORT int ra_lt_set_choice(int ta, int tb, long m, long n, long k, long lda,
   std::lock_guard<std::mutex> g(g_mu);
   LtPlan* p = get_plan(ta, tb, m, n, k, lda, ldb, ldc);
   if (!p || choice < 0 || choice >= (int)p->cands.size()) return -1;
+  if (!usable(p, choice)) return -2;  // recorded choice is stream-K: keep the default
   p->choice = choice;
   return 0;
 }
@@ -163,8 +209,41 @@ RA_EXPORT int ra_lt_set_choice_batched(int ta, int tb, long m, long n, long k, l
   std::lock_guard<std::mutex> g(g_mu);
   LtPlan* p = get_plan(ta, tb, m, n, k, lda, ldb, ldc, batch, sa, sb, sc);
   if (!p || choice < 0 || choice >= (int)p->cands.size()) return -1;
+  if (!usable(p, choice)) return -2;
   p->choice = choice;
   return 0;
+}
+
+// Kernel name of a plan's current choice into out[cap] (diagnostics / tests). Returns the
+// choice index, or < 0.
+RA_EXPORT int ra_lt_choice_name(int ta, int tb, long m, long n, long k, long lda, long ldb,
+                                long ldc, int batch, long sa, long sb, long sc, char* out,
+                                int cap) {
+  std::lock_guard<std::mutex> g(g_mu);
+  LtPlan* p = get_plan(ta, tb, m, n, k, lda, ldb, ldc, batch, sa, sb, sc);
+  if (!p || p->cands.empty() || cap <= 0) return -1;
+  const std::string n_ = cand_name(p, p->choice);
+  std::strncpy(out, n_.c_str(), cap - 1);
+  out[cap - 1] = 0;
+  return p->choice;
+}
+
+// 1 if the shape's current choice is a stream-K kernel (the GEMM must not run concurrently
+// with another stream's GEMMs), 0 if not, < 0 if there is no solution.
+RA_EXPORT int ra_lt_choice_is_streamk(int ta, int tb, long m, long n, long k, long lda,
+                                      long ldb, long ldc, int batch, long sa, long sb,
+                                      long sc) {
+  std::lock_guard<std::mutex> g(g_mu);
+  LtPlan* p = get_plan(ta, tb, m, n, k, lda, ldb, ldc, batch, sa, sb, sc);
+  if (!p || p->cands.empty()) return -1;
+  return cand_sk(p, p->choice) ? 1 : 0;
+}
+
+// 1: allow stream-K candidates (only safe when no other stream runs GEMMs concurrently).
+// Applies to plans created afterwards and to later tuning / set_choice calls.
+RA_EXPORT void ra_lt_allow_streamk(int on) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_allow_sk = on != 0;
 }
 
 // ----------------------------------------------------------------- epilogue GEMMs
@@ -268,6 +347,7 @@ RA_EXPORT int ra_lt_tune(int ta, int tb, long m, long n, long k, const void* A, 
   int best = -1;
   float bt = 1e30f;
   for (int i = 0; i < (int)p->cands.size(); ++i) {
+    if (!usable(p, i)) continue;
     if (run(p, i, A, B, scratch, 1.f, 0.f, st) != 0) continue;  // warmup / validity
     hipEventRecord(e0, st);
     bool ok = true;

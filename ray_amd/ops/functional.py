@@ -361,19 +361,6 @@ def join_side_streams():
         torch.cuda.current_stream(dev).wait_stream(st)
 
 
-def sync_streams_for_collective():
-    """Before a collective on the current stream: also wait for the other stream of the
-    main/side pair (grads of one bucket can come from both)."""
-    if not _side:
-        return
-    for dev, st in _side.items():
-        cur = torch.cuda.current_stream(dev)
-        if cur == st:
-            cur.wait_stream(torch.cuda.default_stream(dev))
-        else:
-            cur.wait_stream(st)
-
-
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -519,17 +506,15 @@ class _CrossEntropy(torch.autograd.Function):
 
 _xent_streams: dict = {}
 
-# RAY_AMD_LMHEAD_PIPE=1 (default): the LM head's three GEMMs per chunk stay in order on the
-# current stream while each chunk's softmax-xent pass runs on its own stream beside the next
-# GEMMs. Same speed as the older layout (=0: dW GEMMs on the wgrad side stream; measured,
-# profiles/r3/lmhead_pipe.md — beside the K = 768 GEMMs, which move 1.5-3 TB/s themselves,
-# the xent pass stretches from 0.33 to ~2.0 ms and the chunk stays at ~2.0 ms either way),
-# but it never runs two torch (hipBLASLt) GEMMs concurrently on two streams: the older
-# layout hung the GPU on a ragged last chunk (tests/test_train_gpu.py, N = 12388, chunk
-# 4096), consistent with two concurrent stream-K GEMMs sharing torch's hipBLASLt workspace.
-_LMHEAD_PIPE = os.environ.get("RAY_AMD_LMHEAD_PIPE", "1") == "1"
-
-
+# Multi-chunk LM head: the three GEMMs per chunk stay in order on the current stream and
+# each chunk's softmax-xent pass runs on its own stream beside the next GEMMs (no speed
+# difference against putting the dW GEMMs on the wgrad side stream, profiles/r3/
+# lmhead_pipe.md). The side-stream-dW layout was REMOVED in round 4: it ran two torch
+# hipBLASLt GEMMs concurrently on two streams and hung the GPU on a ragged last chunk
+# (N = 12388, chunk 4096). Cause: both may be stream-K kernels, whose persistent grids
+# spin-wait on partial tiles of their own undispatched workgroups; two such grids can
+# hold every CU slot and deadlock each other (see ops/csrc/gemm_lt.hip, which also keeps
+# stream-K kernels out of every side-stream GEMM it runs).
 def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
     """Chunked LM head + CE, software-pipelined over two streams:
 
@@ -613,42 +598,21 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         ch = max(1, min(chunk, N))
         L = _lib.lib()
         wt = w.t()
-        if _LMHEAD_PIPE and h.is_cuda and N > ch:
+        if h.is_cuda and N > ch:
             _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp,
                                ignore_index)
-            ctx.save_for_backward(dh, dw)
-            ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
-            return loss_rows.sum() * inv[0]
-        # side stream: each chunk's dW GEMM (compute-bound) overlaps the next chunk's
-        # memory-bound softmax-xent; two logits buffers alternate between the streams
-        side = _side_stream(dev) if (_WGRAD_STREAM and dw is not None and h.is_cuda) else None
-        nbuf = 2 if side is not None and N > ch else 1
-        bufs = [torch.empty((ch, Vp), device=dev, dtype=h.dtype) for _ in range(nbuf)]
-        freed = [None] * nbuf  # side-stream event after the dW that last read each buffer
-        main = torch.cuda.current_stream(dev) if side is not None else None
-        for i, s0 in enumerate(range(0, N, ch)):
-            e = min(N, s0 + ch)
-            k = i % nbuf
-            if freed[k] is not None:
-                main.wait_event(freed[k])
-            lg = bufs[k][: e - s0]
-            torch.mm(h2[s0:e], wt, out=lg)
-            check(L.ra_xent_fused(ptr(lg), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]), e - s0,
-                                  V, Vp, ignore_index, stream_ptr()), "xent_fused")
-            if dh is not None:
-                torch.mm(lg, w, out=dh[s0:e])
-            if dw is not None:
-                if side is not None:
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        _lm_head_dw(lg, h2[s0:e], dw, s0 == 0)
-                        ev = torch.cuda.Event()
-                        ev.record(side)
-                    freed[k] = ev
-                else:
-                    _lm_head_dw(lg, h2[s0:e], dw, s0 == 0)
-        if side is not None:
-            main.wait_stream(side)
+        else:  # one chunk (the GPT-2 bench: 65536 tokens), or CPU: all on this stream
+            lg = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
+            for s0 in range(0, N, ch):
+                e = min(N, s0 + ch)
+                lgc = lg[: e - s0]
+                torch.mm(h2[s0:e], wt, out=lgc)
+                check(L.ra_xent_fused(ptr(lgc), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
+                                      e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
+                if dh is not None:
+                    torch.mm(lgc, w, out=dh[s0:e])
+                if dw is not None:
+                    _lm_head_dw(lgc, h2[s0:e], dw, s0 == 0)
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]

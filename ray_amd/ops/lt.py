@@ -12,10 +12,14 @@ hipBLASLt's heuristic candidates:
     its first use (into a scratch buffer) and records the winner; ``save()`` writes the
     file. Without a recorded choice and without tuning, the first heuristic candidate
     runs (hipBLASLt's own pick).
+  * ``RAY_AMD_LT_NO_STREAMK=1`` restricts the choice to non-stream-K solutions (on gfx950
+    every hipBLASLt bf16 kernel is built with StreamK=3, so this usually leaves none and
+    the plan keeps its stream-K candidates; gemm_lt.hip).
 """
 
 from __future__ import annotations
 
+import ctypes
 import os
 import threading
 
@@ -33,6 +37,11 @@ _choices: dict | None = None  # key str -> (choice, ms)
 _applied: set = set()
 _tuning = os.environ.get("RAY_AMD_LT_TUNE", "0") == "1"
 _file = os.environ.get("RAY_AMD_LT_FILE", DEFAULT_FILE)
+
+
+def _init_streamk_policy():
+    if os.environ.get("RAY_AMD_LT_NO_STREAMK", "0") == "1":
+        _lib.lib().ra_lt_allow_streamk(0)
 
 
 def set_tuning(on: bool, path: str | None = None):
@@ -66,6 +75,30 @@ def save(path: str | None = None):
     return p
 
 
+def choice_name(ta, tb, m, n, k, lda, ldb, ldc, batch=1, sa=0, sb=0, sc=0) -> str:
+    """Kernel name of the solution a shape currently runs (diagnostics, tests)."""
+    buf = ctypes.create_string_buffer(512)
+    idx = _lib.lib().ra_lt_choice_name(ta, tb, m, n, k, lda, ldb, ldc, batch, sa, sb, sc, buf,
+                                       512)
+    if idx < 0:
+        raise RuntimeError("hipBLASLt has no solution for this shape")
+    return buf.value.decode()
+
+
+def wgrad_choice_name(M: int, N: int, K: int, S: int = 1) -> str:
+    """Kernel of the fp32-out weight-gradient GEMM dy[M, N]^T x[M, K] (S = split-K slices)."""
+    if S == 1:
+        return choice_name(0, 1, K, N, M, K, N, K)
+    Ms = M // S
+    return choice_name(0, 1, K, N, Ms, K, N, K, S, Ms * K, Ms * N, N * K)
+
+
+def is_streamk(name: str) -> bool:
+    import re
+
+    return bool(re.search(r"_SK\d", name)) or "StreamK" in name
+
+
 def _key(ta, tb, m, n, k, lda, ldb, ldc, batch=1, sa=0, sb=0, sc=0):
     base = f"lt_{ta}{tb}_{m}_{n}_{k}_{lda}_{ldb}_{ldc}"
     return base if batch == 1 else f"{base}_b{batch}_{sa}_{sb}_{sc}"
@@ -81,15 +114,18 @@ def _select(ta, tb, m, n, k, A, lda, B, ldb, ldc, dev, batch=1, sa=0, sb=0, sc=0
         if key in _applied:
             return
         L = _lib.lib()
+        if not _applied:
+            _init_streamk_policy()
         nc = L.ra_lt_num_cands_batched(*shape, *bshape)
         if nc <= 0:
             raise RuntimeError(f"hipBLASLt has no solution for {key}")
         ch = _load()
-        if key in ch and ch[key][0] < nc:
-            L.ra_lt_set_choice_batched(*shape, *bshape, ch[key][0])
+        # a recorded choice that is a stream-K kernel is refused (rc -2, the plan keeps its
+        # first non-stream-K candidate; gemm_lt.hip explains the deadlock it avoids)
+        if key in ch and ch[key][0] < nc and \
+                L.ra_lt_set_choice_batched(*shape, *bshape, ch[key][0]) == 0:
+            pass
         elif _tuning:
-            import ctypes
-
             scratch = torch.empty(ldc * n + sc * (batch - 1), dtype=torch.float32, device=dev)
             best = ctypes.c_float(0.0)
             idx = L.ra_lt_tune(ta, tb, m, n, k, A, lda, B, ldb, ptr(scratch), ldc, 5,

@@ -136,7 +136,21 @@ def _fold_grad(p):
 
 
 class FlatDDP:
-    """Bucketed, backward-overlapped gradient all-reduce over the flat grad buffer."""
+    """Bucketed, backward-overlapped gradient all-reduce over the flat grad buffer.
+
+    Stream protocol (GPU). Gradients of one bucket come from two compute streams: the
+    main stream (LayerNorm/bias/embedding/LM-head kernels) and the weight-gradient side
+    stream (``ops.functional._side_stream``). Every readiness signal records a per-bucket
+    event on the stream that produced that gradient; when a bucket is full, a DEDICATED
+    comm stream waits on exactly those events and issues the RCCL ``all_reduce`` (RCCL's
+    internal stream then orders itself after the comm stream). Neither compute stream
+    ever waits on the other, or on the comm stream, during backward: the only joins are
+    in ``finish()``, right before the optimizer consumes the gradients.
+
+    ``always_hook=True`` keeps the whole path (hooks, events, comm stream, RCCL launches)
+    live on a world-1 group, so its cost can be measured on one GPU
+    (``bench.py --ddp-hooks always``).
+    """
 
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0,
                  always_hook: bool = False):
@@ -168,6 +182,13 @@ class FlatDDP:
         self._hooks = []
         self.enabled = self.world > 1 or (always_hook and dist.is_initialized())
         self.sync = True  # False inside gradient-accumulation micro-steps (no_sync)
+        self.launched = 0  # all_reduce launches since construction (tests / bench report)
+        cuda = flat.g.is_cuda and self.enabled
+        self._comm = torch.cuda.Stream(flat.device) if cuda else None
+        # per bucket: {stream handle: (stream, event)} — reused every step; ``_contrib[b]``
+        # lists the streams that produced a gradient of bucket b in THIS backward
+        self._events: list[dict] = [dict() for _ in self.buckets]
+        self._contrib: list[list] = [[] for _ in self.buckets]
         if self.enabled:
             for i, (_, p) in enumerate(flat.order):
                 hook = self._make_hook(i)
@@ -181,6 +202,29 @@ class FlatDDP:
             with torch.no_grad():
                 flat.p16.copy_(flat.p32)
 
+    def _mark(self, b: int):
+        """Record bucket b's event on the stream that just produced one of its gradients."""
+        st = torch.cuda.current_stream(self.flat.device)
+        key = st.cuda_stream
+        ent = self._events[b].get(key)
+        if ent is None:
+            ent = self._events[b][key] = (st, torch.cuda.Event())
+        ent[1].record(st)
+        if key not in self._contrib[b]:
+            self._contrib[b].append(key)
+
+    def _launch(self, b: int):
+        s, e = self.buckets[b]
+        if self._comm is None:
+            work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
+        else:
+            for key in self._contrib[b]:
+                self._comm.wait_event(self._events[b][key][1])
+            with torch.cuda.stream(self._comm):
+                work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
+        self._works.append(work)
+        self.launched += 1
+
     def _make_hook(self, i: int):
         b = self.param_bucket[i]
 
@@ -191,14 +235,10 @@ class FlatDDP:
                 return
             self._seen[i] = True
             self._ready[b] += 1
+            if self._comm is not None:
+                self._mark(b)
             if self._ready[b] == self.bucket_sizes[b]:
-                s, e = self.buckets[b]
-                if self.flat.g.is_cuda:
-                    from ray_amd.ops import functional as rf
-
-                    rf.sync_streams_for_collective()
-                self._works.append(dist.all_reduce(self.flat.g[s:e], group=self.group,
-                                                   async_op=True))
+                self._launch(b)
 
         return hook
 
@@ -210,16 +250,20 @@ class FlatDDP:
             from ray_amd.ops import functional as rf
 
             rf.join_side_streams()
-        for w in self._works:
-            w.wait()
-        # buckets never triggered (unused params) are reduced now
+        # buckets never triggered (unused params, or params without a readiness signal)
+        # are reduced now, after both compute streams joined
         for b, r in enumerate(self._ready):
-            if self.enabled and r != self.bucket_sizes[b]:
+            if r != self.bucket_sizes[b]:
                 s, e = self.buckets[b]
-                dist.all_reduce(self.flat.g[s:e], group=self.group)
+                self._works.append(dist.all_reduce(self.flat.g[s:e], group=self.group,
+                                                   async_op=True))
+                self.launched += 1
+        for w in self._works:
+            w.wait()  # the current stream waits on RCCL's stream (no host block)
         self._works.clear()
         self._ready = [0] * len(self.buckets)
         self._seen = [False] * len(self.flat.order)
+        self._contrib = [[] for _ in self.buckets]
 
     @property
     def grad_scale(self) -> float:

@@ -338,18 +338,28 @@ class DeploymentResponse:
         again._assigned()
         self._ref, self._slot = again._ref, again._slot
 
+    def _give_up(self, e):
+        # a timed-out wait leaves the request in flight: its slot is released by _watch
+        # when the reply lands, not here (releasing now would over-admit the replica)
+        if not isinstance(e, ray.exceptions.GetTimeoutError):
+            self._finish()
+
     def result(self, timeout_s: float | None = None):
         while True:
             try:
-                return ray.get(self._assigned(timeout_s), timeout=timeout_s)
+                out = ray.get(self._assigned(timeout_s), timeout=timeout_s)
             except Exception as e:  # noqa: BLE001
                 if self._resend is None or not _is_replica_death(e):
+                    self._give_up(e)
                     raise
                 self._router.refresh(force=True)
                 again, self._resend = self._resend(), None
+                # releases the dead replica's slot; the retried request keeps its own
+                # slot until its reply lands (_watch) or this loop returns / raises
                 self._adopt(again)
-            finally:
-                self._finish()
+                continue
+            self._finish()
+            return out
 
     def __await__(self):
         async def _w():
@@ -357,17 +367,19 @@ class DeploymentResponse:
                 await asyncio.wrap_future(self._pending)
             while True:
                 try:
-                    return await self._assigned()
+                    out = await self._assigned()
                 except Exception as e:  # noqa: BLE001
                     if self._resend is None or not _is_replica_death(e):
+                        self._give_up(e)
                         raise
                     await self._router.arefresh(force=True)
                     again, self._resend = self._resend(), None
                     if again._pending is not None:
                         await asyncio.wrap_future(again._pending)
                     self._adopt(again)
-                finally:
-                    self._finish()
+                    continue
+                self._finish()
+                return out
 
         return _w().__await__()
 

@@ -25,7 +25,7 @@ import time
 
 DEFAULTS = dict(model="small", micro_batch=64, seq_len=1024, steps=20, warmup=5,
                 grad_accum=1, bucket_mb=32.0, grad_dtype="fp32", tunableop="auto",
-                lm_head_chunk=65536, device=None)
+                lm_head_chunk=65536, device=None, ddp_hooks="auto")
 
 
 def tunableop_file(model: str, micro_batch: int, seq_len: int) -> str:
@@ -109,7 +109,8 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
     gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
     tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],
                      total_steps=c["warmup"] + c["steps"], grad_accum=c["grad_accum"],
-                     seed=1234, grad_dtype=gdt, lm_head_chunk=c["lm_head_chunk"])
+                     seed=1234, grad_dtype=gdt, lm_head_chunk=c["lm_head_chunk"],
+                     ddp_always_hook=c["ddp_hooks"] == "always")
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
     # synthetic token pool generated up front: data generation is not timed work
@@ -182,6 +183,8 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         "wgrad_gemm": _wgrad_mode(on_gpu),
         "grad_dtype": c["grad_dtype"],
         "global_batch": c["micro_batch"] * c["grad_accum"] * world,
+        "ddp_hooks": "on" if tr.ddp.enabled else "off",
+        "ddp_allreduce_launches": tr.ddp.launched,
     }
 
 

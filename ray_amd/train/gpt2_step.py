@@ -18,13 +18,15 @@ from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams, cosine_lr
 
 class GPT2Trainer:
     """grad_dtype: fp32 (default — the precision torch DDP reduces in) or bf16 (explicit
-    gradient compression: half the all-reduce bytes, bf16-rounded accumulation)."""
+    gradient compression: half the all-reduce bytes, bf16-rounded accumulation).
+    ddp_always_hook: run the bucket hooks / comm stream / RCCL launches even on a world-1
+    group (measures the DDP overlap machinery on one GPU)."""
 
     def __init__(self, cfg: GPT2Config, micro_batch: int, seq_len: int, device,
                  lr: float = 6e-4, bucket_mb: float = 32.0, total_steps: int = 1000,
                  warmup_steps: int = 10, seed: int = 1234, grad_accum: int = 1,
                  grad_dtype: torch.dtype = torch.float32, param_dtype: torch.dtype | None = None,
-                 lm_head_chunk: int = 8192):
+                 lm_head_chunk: int = 8192, ddp_always_hook: bool = False):
         torch.manual_seed(seed)
         self.cfg = cfg
         self.B, self.T = micro_batch, seq_len
@@ -36,7 +38,7 @@ class GPT2Trainer:
         model.lm_head_chunk = lm_head_chunk
         self.model = model
         self.flat = FlatParams(model, dtype=param_dtype, grad_dtype=grad_dtype)
-        self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb)
+        self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb, always_hook=ddp_always_hook)
         # AdamW clears the flat gradient in its own pass (no zero_grad memset per step)
         self.opt = FlatAdamW(self.flat, lr=lr, weight_decay=0.1, max_grad_norm=1.0,
                              grad_scale=self.ddp.grad_scale / grad_accum, zero_grad=True)

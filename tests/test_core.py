@@ -527,3 +527,33 @@ def test_wait_order_and_partition(cluster):
     assert r == many[:40] and nr == slow
     for s in slow:
         ray.cancel(s, force=True)
+
+
+def test_handleless_actor_released_when_pending_calls_fail(cluster):
+    """The last handle is dropped while a call is still running; the call then FAILS
+    (the actor process dies) instead of replying. The actor (max_restarts=1) must still be
+    released — DEAD, its custom resource returned — not restarted and kept forever."""
+    from ray_amd.util import state
+
+    @ray.remote(max_restarts=1, resources={"custom": 1})
+    class Holder:
+        def die_later(self):
+            time.sleep(0.5)
+            os._exit(1)
+
+    before = ray.available_resources().get("custom", 0)
+    h = Holder.remote()
+    ref = h.die_later.remote()
+    aid = h._actor_id.hex()
+    del h
+    with pytest.raises(RayActorError):
+        ray.get(ref, timeout=30)
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        st = [a for a in state.list_actors() if a["actor_id"] == aid]
+        if st and st[0]["state"] == "DEAD" and \
+                ray.available_resources().get("custom", 0) == before:
+            break
+        time.sleep(0.2)
+    assert st and st[0]["state"] == "DEAD", st
+    assert ray.available_resources().get("custom", 0) == before

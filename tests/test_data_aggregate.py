@@ -127,3 +127,25 @@ def test_empty_dataset_aggregates_to_null():
     ds = rd.range(10).filter(lambda r: r["id"] > 100)
     out = ds.aggregate(Count(), Sum("id"), Mean("id"), Max("id"))
     assert out == {"count()": 0, "sum(id)": None, "mean(id)": None, "max(id)": None}
+
+
+def test_unique_keeps_values_with_nulls():
+    """A None / NaN in the column adds one null entry instead of hiding every value."""
+    ds = rd.from_items([{"a": 3}, {"a": None}, {"a": 1}, {"a": 3}]).repartition(2)
+    assert ds.unique("a") == [1, 3, None]
+    ds = rd.from_items([{"a": 1.5}, {"a": float("nan")}, {"a": -2.0}])
+    assert ds.unique("a") == [-2.0, 1.5, None]
+    assert rd.from_items([{"a": "y"}, {"a": "x"}]).unique("a") == ["x", "y"]
+
+
+def test_groupby_equal_keys_across_dtypes_share_a_group():
+    """int64 1 in one block and float64 1.0 / bool True in another hash to the same
+    partition: groupby returns ONE group per equal key."""
+    from ray_amd.data.dataset import _stable_hash
+
+    assert _stable_hash(1) == _stable_hash(1.0) == _stable_hash(True) == _stable_hash(np.int8(1))
+    assert _stable_hash(0.5) == _stable_hash(np.float32(0.5))
+    a = rd.from_items([{"k": 1, "v": 1}, {"k": 2, "v": 1}])
+    b = rd.from_items([{"k": 1.0, "v": 1}, {"k": 2.0, "v": 1}])
+    out = a.union(b).groupby("k").count().take_all()
+    assert len(out) == 2 and sorted(r["count()"] for r in out) == [2, 2]

@@ -154,3 +154,41 @@ def test_model_multiplexing_routes_by_model_id(cluster):
     assert {o[0] for o in outs} == {"m1"}
     assert len({o[1] for o in outs}) == 1  # sticky to the replica that holds the model
     serve.delete("mux")
+
+
+def test_retried_request_keeps_its_slot_until_the_reply(monkeypatch):
+    """A request whose replica died is re-sent once; the retried request's
+    max_ongoing_requests slot must stay claimed while its reply is awaited (the dead
+    replica's slot is returned immediately)."""
+    import threading
+
+    from ray_amd.exceptions import RayActorError
+    from ray_amd.serve import handle as H
+
+    class _Router:
+        def __init__(self):
+            self.lock = threading.Lock()
+            self.done = []
+
+        def _done_locked(self, rid):
+            self.done.append(rid)
+
+        def refresh(self, force=False):
+            pass
+
+    router = _Router()
+    s1, s2 = H._Slot(router, "dead"), H._Slot(router, "retry")
+    seen = {}
+
+    def fake_get(ref, timeout=None):
+        if ref == "ref1":
+            raise RayActorError("x", "replica died")
+        seen["released_while_waiting"] = list(router.done)
+        return 42
+
+    monkeypatch.setattr(H.ray, "get", fake_get)
+    retry = H.DeploymentResponse("ref2", router, slot=s2)
+    resp = H.DeploymentResponse("ref1", router, slot=s1, resend=lambda: retry)
+    assert resp.result() == 42
+    assert seen["released_while_waiting"] == ["dead"]
+    assert router.done == ["dead", "retry"]

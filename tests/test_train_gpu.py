@@ -176,3 +176,54 @@ def test_torchtrainer_gpt2_two_workers_one_gpu_gloo(cuda_device):
         assert m["loss"] == m["loss"] and m["tokens_per_sec"] > 0
     finally:
         ray.shutdown()
+
+
+def test_lt_choice_name_reports_kernels(cuda_device):
+    """ops/lt.py names the hipBLASLt kernel a wgrad shape runs (the ragged LM-head dW of
+    N = 12388 / chunk 4096 included) and is_streamk() recognises Tensile's StreamK tag."""
+    from ray_amd.ops import lt
+
+    for M, N, K in ((100, 50304, 768), (4096, 768, 768)):
+        dy = torch.randn(M, N, device=cuda_device).bfloat16()
+        x = torch.randn(M, K, device=cuda_device).bfloat16()
+        out = torch.zeros(N, K, device=cuda_device)
+        lt.wgrad_accum(dy, x, out, beta=0.0)
+        assert _rel(out, dy.float().t() @ x.float()) < 1e-5
+        name = lt.wgrad_choice_name(M, N, K)
+        assert name.startswith(("Cijk", "Custom")), name
+    assert lt.is_streamk("Cijk_..._SK3_SKXCCM8_...") and not lt.is_streamk("Cijk_MT256_SN_LDSB0")
+
+
+def test_flat_ddp_world1_hooks_comm_stream(cuda_device):
+    """FlatDDP(always_hook=True) on a world-1 RCCL group: every bucket is launched exactly
+    once from the comm stream during backward, gradients are unchanged by the (identity)
+    all-reduce, and a second step reuses the per-bucket events."""
+    import copy
+    import os
+
+    import torch.distributed as dist
+
+    from ray_amd.models.gpt2 import GPT2
+    from ray_amd.parallel.flat import FlatDDP, FlatParams
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29534")
+        dist.init_process_group("nccl", rank=0, world_size=1)
+    torch.manual_seed(5)
+    a = GPT2(_tiny_cfg()).to(cuda_device).bfloat16()
+    b = copy.deepcopy(a)
+    fa, fb = FlatParams(a), FlatParams(b)
+    ddp = FlatDDP(fb, bucket_mb=0.1, always_hook=True)
+    assert ddp.enabled and ddp._comm is not None and len(ddp.buckets) > 3
+    idx = torch.randint(0, 1000, (4, 256), device=cuda_device)
+    for step in range(2):
+        fa.zero_grad()
+        fb.zero_grad()
+        a(idx, idx).backward()
+        b(idx, idx).backward()
+        # launched from the hooks while backward ran (not by finish())
+        assert ddp.launched == (step + 1) * len(ddp.buckets)
+        ddp.finish()
+        torch.cuda.synchronize()
+        assert _rel(fb.g, fa.g) < 1e-6

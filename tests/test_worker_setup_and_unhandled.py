@@ -132,3 +132,24 @@ def test_actor_death_is_not_an_unhandled_error():
         gc.collect()
     """)
     assert "Unhandled error" not in r.stderr
+
+
+def test_error_read_by_a_borrower_is_not_reported():
+    """The error ref travels inside a list (so it is NOT resolved as an argument) and the
+    borrower task ray.get()s it through the owner: the owner must count that as a read."""
+    r = _run_driver("""
+        @ray.remote
+        def reader(lst):
+            try:
+                ray.get(lst[0])
+            except Exception:
+                return "seen"
+
+        e = f.remote("borrowed")
+        ray.wait([e])
+        assert ray.get(reader.remote([e])) == "seen"
+        del e
+        gc.collect()
+    """)
+    assert r.returncode == 0, r.stderr
+    assert "Unhandled error" not in r.stderr
