@@ -42,60 +42,257 @@ class TrialScheduler:
     def on_trial_error(self, runner, trial):
         pass
 
+    def choose_trial_to_run(self, runner):
+        """A trial to start or resume next, or None for the controller's default (the
+        first PENDING trial, then a new one from the searcher)."""
+        return None
+
 
 class FIFOScheduler(TrialScheduler):
     pass
 
 
+class _AshaBracket:
+    """One ASHA bracket: rungs at grace * rf**(k + s), largest first; a trial reaching a rung
+    is cut when its score is below the (1 - 1/rf) quantile of the scores already recorded
+    there (reference: tune/schedulers/async_hyperband.py _Bracket)."""
+
+    def __init__(self, grace, max_t, rf, s):
+        n = int(math.log(max_t / grace) / math.log(rf) - s + 1) if max_t > grace else 0
+        self.rf = rf
+        self.s = s
+        self.rungs = [(grace * rf ** (k + s), {}) for k in reversed(range(max(n, 0)))]
+
+    def on_result(self, trial_id, t, score):
+        for milestone, recorded in self.rungs:
+            if t < milestone or trial_id in recorded:
+                continue
+            stop = False
+            if recorded:
+                cutoff = float(np.nanpercentile(list(recorded.values()), (1 - 1 / self.rf) * 100))
+                stop = score < cutoff
+            recorded[trial_id] = score
+            return stop
+        return False
+
+
 class AsyncHyperBandScheduler(TrialScheduler):
-    """ASHA (Li et al. 2018): successive halving at rungs r·η^k, asynchronous promotion."""
+    """ASHA (Li et al. 2018): asynchronous successive halving. ``brackets`` > 1 runs several
+    brackets with staggered first rungs (grace * rf**s); a new trial joins bracket s with
+    probability proportional to exp(#rungs(s)), as in the reference."""
 
     def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=100,
-                 grace_period=1, reduction_factor=4, brackets=1, stop_last_trials=True):
+                 grace_period=1, reduction_factor=4, brackets=1, stop_last_trials=True,
+                 seed=None):
         super().__init__(metric, mode)
+        if grace_period <= 0 or max_t <= 0 or reduction_factor <= 1 or brackets < 1:
+            raise ValueError("need grace_period > 0, max_t > 0, reduction_factor > 1, "
+                             "brackets >= 1")
         self.time_attr = time_attr
         self.max_t = max_t
         self.rf = reduction_factor
-        rungs = []
-        t = grace_period
-        while t < max_t:
-            rungs.append(t)
-            t *= reduction_factor
-        self.rungs = {r: [] for r in rungs}
+        self.stop_last_trials = stop_last_trials
+        self.brackets = [_AshaBracket(grace_period, max_t, reduction_factor, s)
+                         for s in range(brackets)]
+        self._rng = np.random.default_rng(seed)
+        self._assign = {}  # trial_id -> bracket
+
+    @property
+    def rungs(self):
+        """Milestone -> recorded scores of the first bracket (diagnostics)."""
+        return {m: list(r.values()) for m, r in self.brackets[0].rungs}
+
+    def on_trial_add(self, runner, trial):
+        sizes = np.array([len(b.rungs) for b in self.brackets], dtype=np.float64)
+        p = np.exp(sizes - sizes.max())
+        self._assign[trial.trial_id] = self.brackets[
+            int(self._rng.choice(len(self.brackets), p=p / p.sum()))]
 
     def on_trial_result(self, runner, trial, result):
         t = result.get(self.time_attr, 0)
-        if t >= self.max_t:
+        if t >= self.max_t and self.stop_last_trials:
             return self.STOP
         s = self._score(result)
         if s is None:
             return self.CONTINUE
-        for r in sorted(self.rungs, reverse=True):
-            if t >= r and r not in trial._asha_rungs:
-                trial._asha_rungs.add(r)
-                rec = self.rungs[r]
-                rec.append(s)
-                k = int(len(rec) / self.rf)
-                if k >= 1:
-                    cutoff = sorted(rec, reverse=True)[k - 1]
-                    if s < cutoff:
-                        return self.STOP
-                elif len(rec) > 1 and s < max(rec) and len(rec) >= self.rf:
-                    return self.STOP
-                break
-        return self.CONTINUE
+        b = self._assign.get(trial.trial_id)
+        if b is None:
+            self.on_trial_add(runner, trial)
+            b = self._assign[trial.trial_id]
+        return self.STOP if b.on_result(trial.trial_id, t, s) else self.CONTINUE
 
 
 ASHAScheduler = AsyncHyperBandScheduler
 
 
-class HyperBandScheduler(AsyncHyperBandScheduler):
-    """Synchronous HyperBand approximated by its asynchronous variant with several
-    brackets (grace periods η^s)."""
+class _HBBracket:
+    """One synchronous HyperBand bracket: n0 trials start with budget r0; when every live
+    trial has reached the current milestone, the top 1/eta continue to eta x the budget and
+    the rest stop (reference: tune/schedulers/hyperband.py _Bracket)."""
+
+    def __init__(self, n0, r0, max_t, eta, s, time_attr, stop_last):
+        self.n = n0
+        self.r = r0
+        self.max_t = max_t
+        self.eta = eta
+        self.halves = s
+        self.time_attr = time_attr
+        self.stop_last = stop_last
+        self.live = {}  # trial -> last result (None before the first)
+        self.to_unpause = set()
+        self.processing = False
+        self.progress = 0.0
+        self.work = 0.0
+        n, r = n0, r0
+        for _ in range(s + 1):
+            self.work += n * r
+            n, r = int(math.ceil(n / eta)), min(r * eta, max_t)
+
+    def t_of(self, result):
+        return 0 if result is None else result.get(self.time_attr, 0)
+
+    def filled(self):
+        return len(self.live) >= self.n
+
+    def iter_done(self):
+        return all(self.t_of(r) >= self.r for r in self.live.values())
+
+    def finished(self):
+        return self.stop_last and self.halves == 0 and self.iter_done()
+
+    def keep_going(self, trial):
+        if not self.stop_last and self.halves == 0:
+            return True
+        return self.t_of(self.live.get(trial)) < self.r
+
+    def halve(self, sign):
+        self.halves -= 1
+        self.n = int(math.ceil(self.n / self.eta))
+        self.r = int(min(self.r * self.eta, self.max_t))
+        ranked = sorted(self.live, key=lambda tr: sign * self.live[tr].get("_hb_metric", 0))
+        return ranked[-self.n:], ranked[:-self.n]
+
+    def completion(self):
+        return 1.0 if self.finished() else min(self.progress / max(self.work, 1e-9), 1.0)
+
+
+class HyperBandScheduler(TrialScheduler):
+    """Synchronous HyperBand (Li et al. 2017). Brackets s = s_max..0 (most aggressive first)
+    hold n(s) = ceil((s_max+1) / (s+1) * eta**s) trials that start with max_t * eta**-s of
+    the time attribute; a trial that reaches its bracket's milestone is PAUSED (checkpointed,
+    resources released) until all live trials of the bracket got there, then the top 1/eta
+    are unpaused with eta x the budget and the others stop. Reference:
+    python/ray/tune/schedulers/hyperband.py:42 (brackets), :239 (_process_bracket)."""
 
     def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=81,
                  reduction_factor=3, stop_last_trials=True):
-        super().__init__(time_attr, metric, mode, max_t, 1, reduction_factor)
+        super().__init__(metric, mode)
+        if reduction_factor <= 1 or max_t <= 0:
+            raise ValueError("need reduction_factor > 1 and max_t > 0")
+        self.time_attr = time_attr
+        self.max_t = max_t
+        self.eta = reduction_factor
+        self.stop_last = stop_last_trials
+        self.s_max = int(round(math.log(max_t) / math.log(reduction_factor)))
+        self.bands = [[]]  # iterations, each a list of brackets
+        self._next_s = self.s_max
+        self._cur = None
+        self._info = {}  # trial -> bracket
+        self.num_stopped = 0
+
+    def _new_bracket(self):
+        while True:
+            if self._next_s < 0:
+                self.bands.append([])
+                self._next_s = self.s_max
+            s = self._next_s
+            self._next_s -= 1
+            r0 = int(self.max_t * self.eta ** (-s))
+            if r0 > 0:
+                n0 = int(math.ceil((self.s_max + 1) / (s + 1) * self.eta ** s))
+                b = _HBBracket(n0, r0, self.max_t, self.eta, s, self.time_attr, self.stop_last)
+                self.bands[-1].append(b)
+                return b
+
+    def on_trial_add(self, runner, trial):
+        if not self.metric or not self.mode:
+            raise ValueError("HyperBandScheduler needs metric and mode (pass them to the "
+                             "scheduler or to TuneConfig)")
+        if self._cur is None or self._cur.filled():
+            self._cur = self._new_bracket()
+        self._cur.live[trial] = None
+        self._info[trial] = self._cur
+
+    def on_trial_result(self, runner, trial, result):
+        b = self._info.get(trial)
+        if b is None or trial not in b.live:
+            return self.CONTINUE
+        prev = b.t_of(b.live[trial])
+        r = dict(result)
+        r["_hb_metric"] = result.get(self.metric, 0)
+        b.progress += max(b.t_of(r) - prev, 0)
+        b.live[trial] = r
+        b.to_unpause.discard(trial)
+        if b.keep_going(trial):
+            return self.CONTINUE
+        return self._process(runner, b, trial)
+
+    def _process(self, runner, b, current=None):
+        action = self.PAUSE
+        if not b.live or not b.iter_done():
+            return action
+        if b.finished():
+            for tr in list(b.live):
+                if tr is not current and tr.status == "PAUSED":
+                    runner.stop_trial(tr)
+            return self.STOP
+        b.processing = True
+        sign = 1 if self.mode == "max" else -1
+        good, bad = b.halve(sign)
+        self.num_stopped += len(bad)
+        for tr in bad:
+            b.live.pop(tr, None)
+            if tr is current:
+                action = self.STOP
+            elif tr.status == "PAUSED":
+                runner.stop_trial(tr)
+        for tr in good:
+            if b.keep_going(tr):
+                if tr is current:
+                    action = self.CONTINUE
+                else:
+                    b.to_unpause.add(tr)
+            elif b.finished():
+                if tr is current:
+                    action = self.STOP
+                elif tr.status == "PAUSED":
+                    runner.stop_trial(tr)
+        b.processing = False
+        return action
+
+    def _remove(self, runner, trial):
+        b = self._info.get(trial)
+        if b is None:
+            return
+        b.live.pop(trial, None)
+        b.to_unpause.discard(trial)
+        if not b.processing and b.live and not b.finished():
+            self._process(runner, b)
+
+    def on_trial_complete(self, runner, trial, result):
+        self._remove(runner, trial)
+
+    def on_trial_error(self, runner, trial):
+        self._remove(runner, trial)
+
+    def choose_trial_to_run(self, runner):
+        """PENDING trials and unpaused trials, least-complete bracket first."""
+        for band in self.bands:
+            for b in sorted(band, key=lambda x: x.completion()):
+                for tr in b.live:
+                    if tr.status == "PENDING" or (tr.status == "PAUSED" and tr in b.to_unpause):
+                        return tr
+        return None
 
 
 class MedianStoppingRule(TrialScheduler):
@@ -387,6 +584,15 @@ class ResourceChangingScheduler(TrialScheduler):
         self.base_resources[trial.trial_id] = dict(trial.resources)
         if hasattr(self.base, "on_trial_add"):
             self.base.on_trial_add(runner, trial)
+
+    def on_trial_complete(self, runner, trial, result):
+        self.base.on_trial_complete(runner, trial, result)
+
+    def on_trial_error(self, runner, trial):
+        self.base.on_trial_error(runner, trial)
+
+    def choose_trial_to_run(self, runner):
+        return self.base.choose_trial_to_run(runner)
 
     def on_trial_result(self, runner, trial, result):
         decision = self.base.on_trial_result(runner, trial, result)

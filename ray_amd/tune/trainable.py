@@ -154,7 +154,7 @@ def function_get_context():
 
 class _TrialActor:
     def __init__(self, trainable, config, trial_dir, trial_id, trial_name, checkpoint_path,
-                 checkpoint_frequency=0):
+                 checkpoint_frequency=0, start_iteration=0):
         os.makedirs(trial_dir, exist_ok=True)
         self.checkpoint_frequency = int(checkpoint_frequency or 0)
         self.trainable = trainable
@@ -166,6 +166,12 @@ class _TrialActor:
         self.inst = None
         self.trial_id = trial_id
         self.trial_name = trial_name
+        # function trainables resumed from a checkpoint continue the iteration count of
+        # the result that carried it (class trainables restore it from the checkpoint)
+        self.start_iteration = int(start_iteration or 0)
+
+    def pid(self):
+        return os.getpid()
 
     def start(self):
         global _fn_session
@@ -175,6 +181,8 @@ class _TrialActor:
                 self.inst.restore(self.ckpt.path)
             return True
         s = _FnSession(self.trial_dir, self.ckpt, self.trial_id, self.trial_name, self.config)
+        s.iteration = self.start_iteration
+        s.ckpt_i = self.start_iteration
         _fn_session = s
         self.s = s
 
@@ -225,13 +233,37 @@ class _TrialActor:
             self.s.cont.release()
         return True
 
-    def reset(self, config, checkpoint_path):
-        if self.is_class and self.inst.reset_config(config):
+    def reset(self, config, trial_dir, trial_id, trial_name, checkpoint_path=None,
+              start_iteration=0):
+        """Reuse this actor for another trial (TuneConfig.reuse_actors; reference:
+        Trainable.reset / reset_config). Class trainables must implement reset_config()
+        returning True, else False is returned and the controller starts a fresh actor.
+        Function trainables get a new session thread."""
+        os.makedirs(trial_dir, exist_ok=True)
+        if self.is_class:
+            if self.inst is None or not self.inst.reset_config(config):
+                return False
             self.inst.config = config
+            self.inst.logdir = trial_dir
+            self.inst._iteration = 0
+            self.inst._time_total = 0.0
             if checkpoint_path:
                 self.inst.restore(checkpoint_path)
-            return True
-        return False
+        elif self.thread is not None:
+            self.s.stop = True
+            self.s.cont.release()
+            self.thread.join(timeout=10)
+            if self.thread.is_alive():
+                return False
+        self.config = config
+        self.trial_dir = trial_dir
+        self.trial_id = trial_id
+        self.trial_name = trial_name
+        self.ckpt = Checkpoint(checkpoint_path) if checkpoint_path else None
+        self.start_iteration = int(start_iteration or 0)
+        if not self.is_class:
+            self.start()
+        return True
 
 
 def with_parameters(trainable, **kwargs):

@@ -204,6 +204,9 @@ class Trial:
         self.pending_exploit = None
         self._asha_rungs = set()
         self.restore_from = None
+        self.num_failures = 0
+        self.last_checkpoint_iter = 0  # training_iteration of the result with the checkpoint
+        self.start_iteration = 0
 
     def __repr__(self):
         return f"Trial({self.trial_id}, {self.status})"
@@ -305,6 +308,19 @@ class _Controller:
         self.exhausted = False
         self.actor_cls = ray.remote(_TrialActor)
         self.start = time.time()
+        fc = rc.failure_config
+        self.max_failures = fc.max_failures if fc else 0
+        ff = fc.fail_fast if fc else False
+        self.fail_fast = ff.upper() if isinstance(ff, str) else bool(ff)
+        if isinstance(self.fail_fast, str) and self.fail_fast != "RAISE":
+            raise ValueError(f"fail_fast must be a bool or 'raise', got {ff!r}")
+        if self.fail_fast and self.max_failures != 0:
+            # reference tune_controller: a failing trial ends the experiment, so retries
+            # would never run
+            raise ValueError("max_failures must be 0 if fail_fast is set")
+        self._errored = False
+        self._actor_cache = []  # (resource key, actor) for TuneConfig.reuse_actors
+        self.num_actor_reuses = 0
         from ray_amd.tune.callback import CallbackList
         from ray_amd.tune.logger import default_callbacks
 
@@ -362,24 +378,108 @@ class _Controller:
         self.scheduler.on_trial_add(self, t)
         return t
 
+    @staticmethod
+    def _res_key(res):
+        return tuple(sorted((k, float(v)) for k, v in (res or {}).items()))
+
     def _launch(self, t: Trial, checkpoint=None):
         res = t.resources or self.resources
-        opts = {"num_cpus": res.get("CPU", 1)}
-        if res.get("GPU"):
-            opts["num_gpus"] = res["GPU"]
-        extra = {k: v for k, v in res.items() if k not in ("CPU", "GPU")}
-        if extra:
-            opts["resources"] = extra
         cc = self.rc.checkpoint_config
-        t.actor = self.actor_cls.options(**opts).remote(self.trainable, t.config, t.local_path,
-                                                        t.trial_id, f"trial_{t.trial_id}",
-                                                        checkpoint,
-                                                        cc.checkpoint_frequency if cc else 0)
-        t.actor.start.remote()  # actor calls are ordered: next_result runs after start
         t.status = "RUNNING"
+        actor = None
+        if self.tc.reuse_actors:
+            key = self._res_key(res)
+            for i, (k, a) in enumerate(self._actor_cache):
+                if k == key:
+                    self._actor_cache.pop(i)
+                    try:
+                        ok = ray.get(a.reset.remote(t.config, t.local_path, t.trial_id,
+                                                    f"trial_{t.trial_id}", checkpoint,
+                                                    t.start_iteration), timeout=60)
+                    except Exception:  # noqa: BLE001
+                        ok = False
+                    if ok:
+                        actor = a
+                        self.num_actor_reuses += 1
+                    else:
+                        ray.kill(a)
+                    break
+        if actor is None:
+            opts = {"num_cpus": res.get("CPU", 1)}
+            if res.get("GPU"):
+                opts["num_gpus"] = res["GPU"]
+            extra = {k: v for k, v in res.items() if k not in ("CPU", "GPU")}
+            if extra:
+                opts["resources"] = extra
+            actor = self.actor_cls.options(**opts).remote(
+                self.trainable, t.config, t.local_path, t.trial_id, f"trial_{t.trial_id}",
+                checkpoint, cc.checkpoint_frequency if cc else 0, t.start_iteration)
+            actor.start.remote()  # actor calls are ordered: next_result runs after start
+        t.actor = actor
         t.pending_ref = t.actor.next_result.remote()
         self.cb.fire("on_trial_restore" if checkpoint else "on_trial_start",
                      trials=self.trials, trial=t)
+
+    def _release_actor(self, t, reuse=False):
+        if t.actor is None:
+            return
+        a, t.actor = t.actor, None
+        t.pending_ref = None
+        try:
+            ray.get(a.stop.remote(), timeout=5)
+        except Exception:  # noqa: BLE001
+            reuse = False
+        more = not self.exhausted or any(x.status == "PENDING" for x in self.trials)
+        if reuse and self.tc.reuse_actors and more:
+            self._actor_cache.append((self._res_key(t.resources or self.resources), a))
+        else:
+            ray.kill(a)
+
+    def stop_trial(self, t):
+        """Scheduler hook (HyperBand): stop a trial that is not the one being processed."""
+        if t.status in ("TERMINATED", "ERROR"):
+            return
+        self._stop_trial(t)
+
+    def _pause_trial(self, t):
+        """Scheduler PAUSE: checkpoint the trial (class trainables save on demand; function
+        trainables keep the checkpoint of their last report), release its actor, and
+        resume it from that checkpoint when the scheduler picks it again. A trial with no
+        checkpoint restarts from scratch (as in the reference)."""
+        path = self._save_trial(t) if t.actor is not None else None
+        if path:
+            t.last_checkpoint_iter = t.last_result.get("training_iteration",
+                                                       t.last_checkpoint_iter)
+        self._release_actor(t, reuse=True)
+        t.status = "PAUSED"
+        t.restore_from = t.last_checkpoint
+        t.start_iteration = t.last_checkpoint_iter if t.last_checkpoint else 0
+
+    def _on_failure(self, t, exc):
+        """A trial raised or its actor died: retry from the last checkpoint while
+        num_failures <= FailureConfig.max_failures (-1: always), else ERROR; fail_fast ends
+        the experiment at the first ERROR, fail_fast='raise' re-raises (reference:
+        tune_controller._process_trial_failure, trial.should_recover)."""
+        if self.fail_fast == "RAISE":
+            for x in self.trials:
+                if x.status == "RUNNING" and x is not t:
+                    self._stop_trial(x)
+            self._release_actor(t)
+            raise exc
+        t.num_failures += 1
+        if self.max_failures < 0 or t.num_failures <= self.max_failures:
+            self._release_actor(t)
+            t.status = "PENDING"
+            t.restore_from = t.last_checkpoint
+            t.start_iteration = t.last_checkpoint_iter if t.last_checkpoint else 0
+            t.results = [r for r in t.results
+                         if r.get("training_iteration", 0) <= t.start_iteration]
+            t.last_result = t.results[-1] if t.results else {}
+            t.error = None
+            self.cb.fire("on_trial_recover", trials=self.trials, trial=t)
+            return
+        self._stop_trial(t, "ERROR", exc)
+        self._errored = True
 
     def _stop_trial(self, t, status="TERMINATED", error=None):
         t.status = status
@@ -393,14 +493,7 @@ class _Controller:
                     self._log_checkpoint(t, path)
             except Exception:  # noqa: BLE001
                 pass
-        if t.actor is not None:
-            try:
-                ray.get(t.actor.stop.remote(), timeout=5)
-            except Exception:
-                pass
-            ray.kill(t.actor)
-        t.actor = None
-        t.pending_ref = None
+        self._release_actor(t, reuse=(status == "TERMINATED"))
         if status == "ERROR":
             self.scheduler.on_trial_error(self, t)
             self.cb.fire("on_trial_error", trials=self.trials, trial=t)
@@ -443,16 +536,42 @@ class _Controller:
         with open(os.path.join(self.exp_dir, "experiment_state.pkl"), "wb") as f:
             pickle.dump(st, f)
 
+    def _next_to_run(self):
+        choose = getattr(self.scheduler, "choose_trial_to_run", None)
+        t = choose(self) if choose is not None else None
+        if t is not None:
+            return t
+        for t in self.trials:
+            if t.status == "PENDING":
+                return t
+        return self._new_trial()
+
     def run(self):
         maxc = self._max_concurrent()
         budget = self.tc.time_budget_s
+        try:
+            self._loop(maxc, budget)
+        finally:
+            for _, a in self._actor_cache:
+                ray.kill(a)
+            self._actor_cache = []
+        for t in self.trials:  # paused trials the scheduler never resumed
+            if t.status == "PAUSED":
+                t.status = "TERMINATED"
+        self._save_state()
+        self.cb.fire("on_experiment_end", trials=self.trials)
+        return self.trials
+
+    def _loop(self, maxc, budget):
         while True:
             running = [t for t in self.trials if t.status == "RUNNING"]
-            pending = [t for t in self.trials if t.status == "PENDING"]
             while len(running) < maxc:
-                t = pending.pop(0) if pending else self._new_trial()
+                t = self._next_to_run()
                 if t is None:
                     break
+                if t.status == "PENDING" and t.restore_from is None and t.last_checkpoint \
+                        and t.num_failures:
+                    t.restore_from = t.last_checkpoint
                 self._launch(t, t.restore_from)
                 running.append(t)
             if not running:
@@ -470,22 +589,25 @@ class _Controller:
                 break
             for r in ready:
                 t = refs[r]
+                if t.status != "RUNNING" or t.pending_ref is not r:
+                    continue  # stopped by a scheduler while this result was in flight
                 try:
                     kind, a, b = ray.get(r)
-                except Exception as e:  # noqa: BLE001
-                    self._stop_trial(t, "ERROR", e)
+                except Exception as e:  # noqa: BLE001  (actor died)
+                    self._on_failure(t, e)
                     continue
                 if kind == "done":
                     self._stop_trial(t)
                     continue
                 if kind == "error":
-                    self._stop_trial(t, "ERROR", RuntimeError(a))
+                    self._on_failure(t, RuntimeError(a))
                     continue
                 result = dict(a)
                 result["trial_id"] = t.trial_id
                 result["config"] = t.config
                 if b:
                     t.last_checkpoint = b
+                    t.last_checkpoint_iter = result.get("training_iteration", 0)
                 t.results.append(result)
                 t.last_result = result
                 self._log(t, result, b)
@@ -496,6 +618,9 @@ class _Controller:
                 if decision == TrialScheduler.STOP:
                     self._stop_trial(t)
                     continue
+                if decision == TrialScheduler.PAUSE:
+                    self._pause_trial(t)
+                    continue
                 if t.pending_exploit is not None:
                     ckpt, cfg = t.pending_exploit
                     t.pending_exploit = None
@@ -503,6 +628,7 @@ class _Controller:
                     t.status = "PENDING"
                     t.config = cfg
                     t.restore_from = ckpt
+                    t.start_iteration = 0
                     if getattr(t, "pending_resources", None):
                         t.resources = t.pending_resources
                         t.pending_resources = None
@@ -511,9 +637,14 @@ class _Controller:
                 t.pending_ref = t.actor.next_result.remote()
             self.cb.end_step(self.trials)
             self._save_state()
-        self._save_state()
-        self.cb.fire("on_experiment_end", trials=self.trials)
-        return self.trials
+            if self.fail_fast and self._errored:
+                for t in self.trials:
+                    if t.status in ("RUNNING", "PAUSED"):
+                        self._stop_trial(t)
+                    elif t.status == "PENDING":
+                        t.status = "TERMINATED"
+                self.exhausted = True
+                break
 
 
 def _trainer_to_trainable(trainer):
