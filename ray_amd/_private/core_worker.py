@@ -1379,6 +1379,8 @@ class CoreWorker:
             "runtime_env": self._export_renv(opts.get("runtime_env")), "attempt": 0,
             "job": self.job_id, "dynamic": dynamic, "ns": self.namespace,
         }
+        if opts.get("max_calls"):
+            spec["max_calls"] = int(opts["max_calls"])
         refs = []
         with self.lock:
             if streaming:
@@ -1565,11 +1567,20 @@ class CoreWorker:
             self._on_actor_task_reply(spec, returns, extra)
             return
         lease = None
+        retire = False
         with self.lock:
             lease = self.task_lease.pop(tid, None)
             if lease is not None:
                 lease.inflight.pop(tid, None)
                 lease.idle_since = time.monotonic()
+                if extra.get("worker_exit"):  # max_calls reached: retire that worker
+                    try:
+                        self.leases[lease.key].remove(lease)
+                        retire = True
+                    except ValueError:
+                        pass
+        if retire:
+            self.notify_raylet("return_lease", lease.lease_id, True)
         # application-level retry
         if extra.get("app_error") and self._should_retry_exc(spec, extra.get("exc_type")):
             for oid, kind, payload, contained in returns:
@@ -2193,6 +2204,8 @@ class CoreWorker:
                     if spec.get("dynamic"):
                         result = _DynamicRefs([self.put_object(v) for v in result])
                     returns = self._package_returns(spec, result)
+                if spec.get("max_calls") and spec["type"] == P.NORMAL_TASK:
+                    extra["worker_exit"] = self._count_call(spec)
         except _ActorExit:
             returns = self._package_returns(spec, None) if spec["nret"] != -1 else []
             self._send_reply(conn, reply_to, tid, returns, extra)
@@ -2220,6 +2233,16 @@ class CoreWorker:
                                  else "FINISHED", spec["type"], spec.get("job"),
                                  spec.get("attempt", 0), extra.get("exc_type")))
         self._send_reply(conn, reply_to, tid, returns, extra)
+
+    def _count_call(self, spec):
+        """max_calls: True once this worker has run the function max_calls times; the
+        owner then returns the lease with worker_dead=True, so the raylet retires this
+        process and the next call gets a fresh worker (reference: remote_function.py
+        max_calls; the worker exits after that many invocations)."""
+        calls = self.__dict__.setdefault("_fn_calls", {})
+        k = repr(spec["fn"])
+        calls[k] = calls.get(k, 0) + 1
+        return calls[k] >= spec["max_calls"]
 
     # ---------------------------------------------------------------- setup hooks
     _HOOK_NS = b"__runtime_env__"

@@ -73,6 +73,7 @@ class RemoteFunction:
             "max_retries": opts.get("max_retries", 3),
             "retry_exceptions": opts.get("retry_exceptions", False),
             "runtime_env": opts.get("runtime_env"),
+            "max_calls": opts.get("max_calls") or 0,
         }
         name = opts.get("name") or getattr(self._function, "__qualname__", "task")
         refs = cw.submit_task(self._key(cw), args, kwargs, o, name)

@@ -557,3 +557,29 @@ def test_handleless_actor_released_when_pending_calls_fail(cluster):
         time.sleep(0.2)
     assert st and st[0]["state"] == "DEAD", st
     assert ray.available_resources().get("custom", 0) == before
+
+
+def test_max_calls_retires_worker(cluster):
+    """max_calls=1: every call runs in a fresh worker process (reference:
+    remote_function.py max_calls); without it the pooled worker is reused."""
+    import os as _os
+
+    @ray.remote(max_calls=1)
+    def pid_once():
+        return _os.getpid()
+
+    @ray.remote
+    def pid_pooled():
+        return _os.getpid()
+
+    pids = [ray.get(pid_once.remote()) for _ in range(4)]
+    assert len(set(pids)) == 4
+    pooled = [ray.get(pid_pooled.remote()) for _ in range(4)]
+    assert len(set(pooled)) == 1
+
+    @ray.remote(max_calls=2)
+    def pid_twice():
+        return _os.getpid()
+
+    p2 = [ray.get(pid_twice.remote()) for _ in range(4)]
+    assert p2[0] == p2[1] and p2[2] == p2[3] and p2[1] != p2[2]
