@@ -17,9 +17,14 @@ import time
 
 
 class HTTPProxy:
-    def __init__(self, host="127.0.0.1", port=8000):
+    def __init__(self, host="127.0.0.1", port=8000, request_timeout_s=None):
         self.host = host
         self.port = port
+        # HTTPOptions.request_timeout_s: a request not answered by then gets 408 (reference
+        # proxy.py request_timeout_s -> "Request timed out", status 408)
+        self.request_timeout_s = request_timeout_s if request_timeout_s and \
+            request_timeout_s > 0 else None
+        self.num_timeouts = 0
         self.routes = {}
         self.routes_ts = 0.0
         self.inflight = 0
@@ -62,6 +67,21 @@ class HTTPProxy:
             body += m.get("body", b"")
             if not m.get("more_body"):
                 break
+        state = {"started": False}
+        if self.request_timeout_s is None:
+            await self._handle(scope, body, send, state)
+            return
+        try:
+            await asyncio.wait_for(self._handle(scope, body, send, state),
+                                   self.request_timeout_s)
+        except asyncio.TimeoutError:
+            self.num_timeouts += 1
+            if not state["started"]:
+                await self._reply(send, 408, [("content-type", "text/plain")],
+                                  f"Request timed out after {self.request_timeout_s}s."
+                                  .encode())
+
+    async def _handle(self, scope, body, send, state):
         started = False
         try:
             await self._arefresh()
@@ -110,7 +130,7 @@ class HTTPProxy:
                             await send({"type": "http.response.start", "status": msg[1],
                                         "headers": [(k.encode(), v.encode())
                                                     for k, v in msg[2]]})
-                            started = True
+                            started = state["started"] = True
                         else:
                             await send({"type": "http.response.body", "body": msg[1],
                                         "more_body": True})
@@ -138,7 +158,7 @@ class HTTPProxy:
         if app_name is not None:
             from ray_amd.serve.handle import invalidate
 
-            invalidate(app_name)
+            invalidate(app_name, drop=False)
         return True
 
     @staticmethod
@@ -149,6 +169,9 @@ class HTTPProxy:
 
     def num_inflight(self):
         return self.inflight
+
+    def stats(self):
+        return {"inflight": self.inflight, "timeouts": self.num_timeouts}
 
     def _serve(self):
         try:

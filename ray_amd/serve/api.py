@@ -37,7 +37,7 @@ def _get_controller(create=False):
             raise RuntimeError("Serve is not running; call serve.run() or serve.start() first")
         _controller = ray.remote(ServeController).options(
             name=CONTROLLER_NAME, namespace=SERVE_NAMESPACE, lifetime="detached", num_cpus=0,
-            max_concurrency=1000, get_if_exists=True).remote()
+            max_concurrency=1000, max_restarts=-1, get_if_exists=True).remote()
     return _controller
 
 
@@ -74,11 +74,11 @@ def start(http_options=None, detached: bool = True, **kw):
         _proxy = ray.remote(HTTPProxy).options(num_cpus=0, max_concurrency=1000,
                                                name="SERVE_PROXY", namespace=SERVE_NAMESPACE,
                                                lifetime="detached").remote(
-            opts.get("host", "127.0.0.1"), port)
+            opts.get("host", "127.0.0.1"), port, opts.get("request_timeout_s"))
         err = ray.get(_proxy.ping.remote())
         if err != "ok":
             raise RuntimeError(f"HTTP proxy failed to start: {err}")
-        ray.get(c.set_proxy.remote(_proxy))
+        ray.get(c.set_proxy.remote(_proxy, opts))
         _http_port = port
     g = kw.get("grpc_options")
     if g is not None:
@@ -111,7 +111,9 @@ class Deployment:
     def __init__(self, func_or_class, name, num_replicas=1, ray_actor_options=None,
                  user_config=None, max_ongoing_requests=100, autoscaling_config=None,
                  route_prefix=None, graceful_shutdown_timeout_s=5.0, health_check_period_s=10.0,
-                 version=None, max_queued_requests=-1, **kw):
+                 version=None, max_queued_requests=-1, health_check_timeout_s=30.0,
+                 placement_group_bundles=None, placement_group_strategy=None,
+                 max_replicas_per_node=None, **kw):
         from ray_amd.serve.config import normalize_autoscaling_config
 
         self.func_or_class = func_or_class
@@ -131,6 +133,17 @@ class Deployment:
         self.route_prefix = route_prefix
         self.graceful_shutdown_timeout_s = graceful_shutdown_timeout_s
         self.health_check_period_s = health_check_period_s
+        self.health_check_timeout_s = health_check_timeout_s
+        if placement_group_strategy is not None and placement_group_bundles is None:
+            raise ValueError("placement_group_strategy needs placement_group_bundles")
+        if max_replicas_per_node is not None and placement_group_bundles is not None:
+            raise ValueError("max_replicas_per_node cannot be combined with "
+                             "placement_group_bundles")
+        if max_replicas_per_node is not None and max_replicas_per_node < 1:
+            raise ValueError("max_replicas_per_node must be >= 1")
+        self.placement_group_bundles = placement_group_bundles
+        self.placement_group_strategy = placement_group_strategy
+        self.max_replicas_per_node = max_replicas_per_node
         self.version = version
 
     def options(self, **kw):
@@ -139,6 +152,10 @@ class Deployment:
                  autoscaling_config=self.autoscaling_config, route_prefix=self.route_prefix,
                  graceful_shutdown_timeout_s=self.graceful_shutdown_timeout_s,
                  health_check_period_s=self.health_check_period_s,
+                 health_check_timeout_s=self.health_check_timeout_s,
+                 placement_group_bundles=self.placement_group_bundles,
+                 placement_group_strategy=self.placement_group_strategy,
+                 max_replicas_per_node=self.max_replicas_per_node,
                  max_queued_requests=self.max_queued_requests,
                  version=self.version, name=self.name)
         if "max_concurrent_queries" in kw:
@@ -164,7 +181,9 @@ class Application:
 def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_options=None,
                user_config=None, max_ongoing_requests=100, max_concurrent_queries=None,
                autoscaling_config=None, route_prefix=None, graceful_shutdown_timeout_s=5.0,
-               health_check_period_s=10.0, version=None, max_queued_requests=-1, **kw):
+               health_check_period_s=10.0, version=None, max_queued_requests=-1,
+               health_check_timeout_s=30.0, placement_group_bundles=None,
+               placement_group_strategy=None, max_replicas_per_node=None, **kw):
     if max_concurrent_queries is not None:
         max_ongoing_requests = max_concurrent_queries
 
@@ -172,7 +191,11 @@ def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_opti
         return Deployment(fc, name or fc.__name__, num_replicas, ray_actor_options, user_config,
                           max_ongoing_requests, autoscaling_config, route_prefix,
                           graceful_shutdown_timeout_s, health_check_period_s, version,
-                          max_queued_requests=max_queued_requests)
+                          max_queued_requests=max_queued_requests,
+                          health_check_timeout_s=health_check_timeout_s,
+                          placement_group_bundles=placement_group_bundles,
+                          placement_group_strategy=placement_group_strategy,
+                          max_replicas_per_node=max_replicas_per_node)
 
     if _func_or_class is not None and callable(_func_or_class):
         return deco(_func_or_class)
@@ -236,6 +259,11 @@ def _build(app: Application, app_name, specs: dict):
         "max_queued_requests": dep.max_queued_requests,
         "asgi_app": cloudpickle.dumps(asgi) if asgi is not None else None,
         "graceful_shutdown_timeout_s": dep.graceful_shutdown_timeout_s,
+        "health_check_period_s": dep.health_check_period_s,
+        "health_check_timeout_s": dep.health_check_timeout_s,
+        "placement_group_bundles": dep.placement_group_bundles,
+        "placement_group_strategy": dep.placement_group_strategy,
+        "max_replicas_per_node": dep.max_replicas_per_node,
         "code_version": dep.version or hashlib.blake2b(blob, digest_size=8).hexdigest(),
     }
     return DeploymentHandle(dep.name, app_name)
@@ -252,7 +280,7 @@ def run(target: Application, *, name: str = "default", route_prefix: str | None 
     ray.get(c.deploy_application.remote(name, rp, target.deployment.name, list(specs.values())))
     from ray_amd.serve import handle as H
 
-    H.invalidate(name)  # this process's routers re-read the new replica sets
+    H.invalidate(name, drop=False)  # this process's routers re-read the new replica sets
     st = ray.get(c.status.remote()).get(name, {})
     if st.get("status") == "DEPLOY_FAILED":
         errs = {d: s["status"] for d, s in st.get("deployments", {}).items()}

@@ -2,8 +2,12 @@
 python/ray/serve/handle.py, _private/router.py, _private/replica_scheduler/pow_2_scheduler.py).
 
 Routing: power-of-two-choices on the number of requests this handle has in
-flight to each replica (no extra RPC on the hot path); the replica set is
-refreshed from the controller when its version changes or a replica fails."""
+flight to each replica (no extra RPC on the hot path). Replica-set changes arrive by
+long poll (one ``_LongPoller`` thread per process blocks in the controller's
+``long_poll`` and installs new versions as they are published; reference
+serve/_private/long_poll.py:173); an explicit refresh happens only before the first
+update or after a replica failure. A ``_MetricsPusher`` thread reports the requests each
+handle holds back to the controller's autoscaler."""
 
 from __future__ import annotations
 
@@ -30,6 +34,7 @@ class _Router:
         self.pending = []  # [(future, send, model_id)] waiting for a slot, FIFO
         self.dispatching = False
         self.last_refresh = 0.0
+        self.stale = False
         self.affinity = {}  # multiplexed model id -> replica that loaded it
 
     def _controller(self):
@@ -39,10 +44,12 @@ class _Router:
 
     def refresh(self, force=False):
         now = time.time()
-        if not force and self.replicas and now - self.last_refresh < 1.0:
+        if not force and not self.stale and self.replicas and (
+                now - self.last_refresh < 1.0 or _poller.alive):
             return
         info = ray.get(self._controller().get_replicas.remote(self.app, self.dep))
         self.last_refresh = now
+        self.stale = False
         if info is None:
             raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
         self._install(info)
@@ -60,10 +67,12 @@ class _Router:
 
     async def arefresh(self, force=False):
         now = time.time()
-        if not force and self.replicas and now - self.last_refresh < 1.0:
+        if not force and not self.stale and self.replicas and (
+                now - self.last_refresh < 1.0 or _poller.alive):
             return
         info = await self._controller().get_replicas.remote(self.app, self.dep)
         self.last_refresh = now
+        self.stale = False
         if info is None:
             raise RuntimeError(f"deployment {self.dep} of app {self.app} does not exist")
         self._install(info)
@@ -253,14 +262,117 @@ def _router(app, dep):
         r = _routers.get((app, dep))
         if r is None:
             r = _routers[(app, dep)] = _Router(app, dep)
-        return r
+    _poller.ensure()
+    _pusher.ensure()
+    return r
 
 
-def invalidate(app):
-    """Drop this process's cached replica sets of `app` (after a redeploy / delete)."""
+class _Daemon:
+    name = "serve-daemon"
+
+    def __init__(self):
+        self.thread = None
+        self.lock = threading.Lock()
+        self.alive = False
+
+    def ensure(self):
+        with self.lock:
+            if self.thread is None or not self.thread.is_alive():
+                self.thread = threading.Thread(target=self._run_safe, daemon=True,
+                                               name=self.name)
+                self.thread.start()
+
+    def _run_safe(self):
+        try:
+            self._run()
+        finally:
+            self.alive = False
+
+    def _controller(self):
+        from ray_amd.serve.api import _get_controller
+
+        return _get_controller()
+
+
+class _LongPoller(_Daemon):
+    """Blocks in ServeController.long_poll with the versions this process holds and
+    installs every change it returns (the push half of the routing-table protocol)."""
+
+    name = "serve-long-poll"
+
+    def _run(self):
+        while ray.is_initialized():
+            with _rlock:
+                routers = dict(_routers)
+            if not routers:
+                self.alive = False
+                time.sleep(0.1)
+                continue
+            snap = {f"{a}/{d}": r.version for (a, d), r in routers.items()}
+            try:
+                res = ray.get(self._controller().long_poll.remote(snap, 5.0), timeout=30)
+            except Exception:  # noqa: BLE001  (controller restarting / serve shut down)
+                self.alive = False
+                time.sleep(0.2)
+                continue
+            self.alive = True
+            now = time.time()
+            for key, info in res.items():
+                a, _, d = key.partition("/")
+                r = routers.get((a, d))
+                if r is None:
+                    continue
+                if info is None:  # deployment deleted
+                    with r.lock:
+                        r.version, r.replicas = -1, []
+                        r.slot_freed.notify_all()
+                else:
+                    r._install(info)
+                    r.last_refresh = now
+
+
+class _MetricsPusher(_Daemon):
+    """Every 0.25 s, reports each handle's held-back requests (queued for a replica
+    slot) to the controller, which adds them to the replicas' ongoing requests when it
+    autoscales over look_back_period_s."""
+
+    name = "serve-handle-metrics"
+    PERIOD_S = 0.25
+
+    def _run(self):
+        import os
+
+        last = {}
+        while ray.is_initialized():
+            time.sleep(self.PERIOD_S)
+            with _rlock:
+                routers = dict(_routers)
+            for (a, d), r in routers.items():
+                q = r.queued + len(r.pending)
+                if q or last.get((a, d)):
+                    try:
+                        self._controller().record_handle_metrics.remote(
+                            a, d, f"{os.getpid()}:{id(r)}", q)
+                    except Exception:  # noqa: BLE001
+                        continue
+                last[(a, d)] = q
+            self.alive = True
+
+
+_poller = _LongPoller()
+_pusher = _MetricsPusher()
+
+
+def invalidate(app, drop=True):
+    """After a delete (drop=True) forget this process's routers of `app`; after a redeploy
+    (drop=False) make their next use re-read the replica set (the long poll delivers it
+    too, but the caller of serve.run must not route by a set older than its own deploy)."""
     with _rlock:
         for key in [k for k in _routers if k[0] == app]:
-            del _routers[key]
+            if drop:
+                del _routers[key]
+            else:
+                _routers[key].stale = True
 
 
 def _is_replica_death(e) -> bool:
