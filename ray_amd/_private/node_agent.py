@@ -65,6 +65,10 @@ class NodeAgent:
             self.node_hex, self.total, self.labels, self.addr, self.store_path,
             self.spill_dir, os.getpid(), self.num_cpus))))
         self.registered = False
+        from ray_amd._private.reporter import NodeReporter
+
+        self.reporter = NodeReporter(self.node_hex, self.session_dir).start()
+        self._last_report = 0.0
 
     def reply(self, conn, rid, ok, value):
         if rid:
@@ -91,6 +95,12 @@ class NodeAgent:
                 except Exception:
                     traceback.print_exc()
             now = time.monotonic()
+            if self.registered and now - self._last_report >= self.reporter.interval_s:
+                self._last_report = now
+                sample = self.reporter.latest()
+                if sample is not None:  # rid 0: no reply wanted
+                    self.io.send(self.head_conn, _dumps((P.REQ, 0, "report_node_stats",
+                                                         (self.node_hex, sample))))
             if now - last > 0.5:
                 last = now
                 for pid, p in list(self.procs.items()):

@@ -230,6 +230,11 @@ class Raylet:
         os.makedirs(os.path.join(self.session_dir, "logs"), exist_ok=True)
         self.addr = os.path.join(self.session_dir, "sockets", "raylet.sock")
         self.node_id = _core.random_id(16)
+        from ray_amd._private.reporter import NodeReporter
+
+        # node / MI355X telemetry (reporter_agent.py parity); remote nodes push theirs
+        self.reporter = NodeReporter(self.node_id.hex(), self.session_dir).start()
+        self.node_stats = {}  # node hex -> latest sample pushed by that node's agent
         self.node_ip = os.environ.get("RAY_AMD_NODE_IP", "127.0.0.1")
         self.store_path = args.store_path
         self.spill_dir = os.path.join(self.session_dir, "spill")
@@ -1443,8 +1448,29 @@ class Raylet:
                         if "_group_" not in k}},
         ]
         out = list(sysm)
+        from ray_amd._private.reporter import metric_records
+
+        out.extend(metric_records(self._node_samples()))
         for snap in self.app_metrics.values():
             out.extend(snap)
+        self.reply(conn, rid, True, out)
+
+    def _node_samples(self):
+        own = self.reporter.latest() or self.reporter.sample()
+        alive = {nh for nh, rec in self.node_recs.items() if rec["alive"]}
+        return [own] + [s for nh, s in self.node_stats.items() if nh in alive]
+
+    def rpc_report_node_stats(self, conn, rid, node_hex, sample):
+        """A node agent's periodic telemetry sample."""
+        self.node_stats[node_hex] = sample
+        self.reply(conn, rid, True, None)
+
+    def rpc_node_stats(self, conn, rid):
+        """node hex -> latest telemetry sample (state API / dashboard / ray_amd status)."""
+        out = {}
+        for s in self._node_samples():
+            if s:
+                out[s["node_id"]] = s
         self.reply(conn, rid, True, out)
 
     def rpc_list_tasks(self, conn, rid):

@@ -201,6 +201,25 @@ def cmd_status(a):
         if k in ("memory", "object_store_memory"):
             t, u, unit = t / 2 ** 30, u / 2 ** 30, " GiB"
         print(f"  {u:g}/{t:g}{unit} {k}")
+    from ray_amd._private.worker import _check_connected
+
+    try:
+        stats = _check_connected().call_raylet("node_stats") or {}
+    except Exception:  # noqa: BLE001
+        stats = {}
+    if stats:
+        print("Node telemetry:")
+    for nid, s in stats.items():
+        print(f"  {nid[:12]}  cpu {s['cpu_percent']:.0f}% of {s['cpu_count']}  mem "
+              f"{s['mem_used'] / 2 ** 30:.1f}/{s['mem_total'] / 2 ** 30:.1f} GiB")
+        for g in s.get("gpus") or []:
+            def f(v, scale=1.0, fmt="{:.0f}"):
+                return "n/a" if v is None else fmt.format(v / scale)
+
+            print(f"    GPU{g['index']} {g['name']}: util {f(g['utilization_percent'])}%  "
+                  f"HBM {f(g['memory_used'], 2 ** 30, '{:.1f}')}/"
+                  f"{f(g['memory_total'], 2 ** 30, '{:.1f}')} GiB  power "
+                  f"{f(g['power_w'])} W  temp {f(g['temperature_c'])} C")
     return 0
 
 

@@ -133,11 +133,17 @@ def _task_rows(cw):
 
 def _node_rows(cw):
     rows = []
+    try:  # per-node telemetry (reporter.py): CPU / memory / per-GPU util, HBM, power, temp
+        stats = cw.call_raylet("node_stats") or {}
+    except Exception:  # noqa: BLE001
+        stats = {}
     for n in cw.call_raylet("nodes"):
         rows.append({"node_id": n["NodeID"], "node_ip": n["NodeManagerAddress"],
-                     "is_head_node": True, "state": "ALIVE" if n["Alive"] else "DEAD",
+                     "is_head_node": bool(n.get("is_head_node", True)),
+                     "state": "ALIVE" if n["Alive"] else "DEAD",
                      "node_name": n["NodeManagerHostname"], "resources_total": n["Resources"],
-                     "labels": n.get("Labels") or {}})
+                     "labels": n.get("Labels") or {},
+                     "node_stats": stats.get(n["NodeID"])})
     return rows
 
 
