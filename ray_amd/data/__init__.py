@@ -29,6 +29,7 @@ class DataContext:
         self.target_max_block_size = 128 << 20
         self.execution_options = ExecutionOptions()
         self.use_push_based_shuffle = False
+        self.push_based_shuffle_merge_factor = 8
 
     @classmethod
     def get_current(cls):

@@ -43,6 +43,28 @@ def _meta(b):
     return {"num_rows": B.num_rows(b), "size_bytes": B.size_bytes(b), "schema": B.schema_of(b)}
 
 
+def _nbytes(m):
+    return int(m.get("size_bytes", 0)) if isinstance(m, dict) else 0
+
+
+@ray.remote
+def _split_block(blk, k):
+    """Cut an oversized block into k row ranges (DataContext.target_max_block_size)."""
+    n = B.num_rows(blk)
+    bounds = [n * i // k for i in range(k + 1)]
+    out = []
+    for i in range(k):
+        b = B.slice_block(blk, bounds[i], bounds[i + 1])
+        out += [b]
+    return tuple(out) if k > 1 else out[0]
+
+
+def _target_block_size():
+    from . import DataContext
+
+    return int(getattr(DataContext.get_current(), "target_max_block_size", 0) or 0)
+
+
 def _apply(fns, blk):
     for f in fns:
         blk = f(blk)
@@ -102,6 +124,8 @@ class Stage:
 class Plan:
     def __init__(self, source, stages=None, source_meta=None):
         # source: ("read", [callables]) | ("refs", [block refs]) | ("lazy", fn -> refs)
+        #       | ("stream", fn -> iterator of (block ref, meta or meta ref)): pulled
+        #         incrementally by a feeder thread (union / zip / shuffle outputs)
         self.source = source
         self.stages = list(stages or [])
         self.source_meta = source_meta
@@ -239,23 +263,45 @@ class _Op:
     def on_complete(self, m):
         seq, b, extra = self.inflight.pop(m)
         meta = ray.get(m)
-        nb = int(meta.get("size_bytes", 0)) if meta else 0
+        nb = _nbytes(meta)
         self.out_count += 1
         self.out_total_bytes += nb
         self.out_bytes += nb
         self.stats["tasks"] += 1
         self.stats["rows"] += meta.get("num_rows", 0) if meta else 0
         self.stats["bytes"] += nb
-        self.reorder[seq] = (b, meta)
+        self.reorder[seq] = self._maybe_split(b, meta)
         while self.next_seq in self.reorder:
-            b2, m2 = self.reorder.pop(self.next_seq)
-            self.outq.append((b2, m2, self.next_seq))
+            for b2, m2 in self.reorder.pop(self.next_seq):
+                self.outq.append((b2, m2, self.next_seq))
             self.next_seq += 1
         return extra
 
+    def _maybe_split(self, b, meta):
+        """Dynamic block splitting (reference: map_operator.py:53 with
+        DataContext.target_max_block_size): an output block larger than the target is cut
+        into ceil(size / target) row ranges by one task; their metas follow from the row
+        counts, so the scheduling thread never waits for the split."""
+        target = _target_block_size()
+        nb = _nbytes(meta)
+        rows = meta.get("num_rows", 0) if isinstance(meta, dict) else 0
+        if not target or nb <= target or rows < 2:
+            return [(b, meta)]
+        k = int(min(rows, -(-nb // target)))
+        refs = _split_block.options(num_returns=k).remote(b, k)
+        refs = refs if isinstance(refs, list) else [refs]
+        bounds = [rows * i // k for i in range(k + 1)]
+        out = []
+        for i, r in enumerate(refs):
+            n = bounds[i + 1] - bounds[i]
+            out.append((r, {"num_rows": n, "size_bytes": int(nb * n / rows),
+                            "schema": meta.get("schema")}))
+        self.stats["splits"] = self.stats.get("splits", 0) + 1
+        return out
+
     def take_output(self):
         b, m, seq = self.outq.popleft()
-        self.out_bytes -= int(m.get("size_bytes", 0)) if m else 0
+        self.out_bytes -= _nbytes(m)
         return b, m, seq
 
     def can_launch_more(self):
@@ -285,6 +331,22 @@ class _TaskOp(_Op):
             b, m = _map_block.options(**self.opts).remote(item, self.fns)
         self.inflight[m] = (seq, b, None)
         return m
+
+
+class _PassOp(_Op):
+    """Input of a streamed source with no task stage: blocks pass straight through (no
+    task), so union / zip / shuffle outputs stream to the consumer as they arrive."""
+
+    def __init__(self, name):
+        super().__init__(name, {"num_cpus": 0}, 1 << 30)
+
+    def launch(self):
+        item, meta, seq, nb = self.pop_input()
+        self.out_count += 1
+        self.out_total_bytes += nb
+        self.out_bytes += nb
+        self.outq.append((item, meta, seq))
+        return None
 
 
 class _ActorPoolOp(_Op):
@@ -445,9 +507,13 @@ class StreamingExecutor:
         plan = self.plan
         cap_default = self.options.max_tasks_in_flight or max(4, 2 * default_parallelism())
         kind, src = plan.source
+        self._stream = None
         if kind == "lazy":
             refs, metas = src()
             kind, src, src_meta = "refs", refs, metas
+        elif kind == "stream":
+            self._stream = src
+            src, src_meta = [], None
         else:
             src_meta = plan.source_meta
         stages = list(plan.stages)
@@ -461,7 +527,11 @@ class StreamingExecutor:
         else:
             first_name = "Read" if kind == "read" else "Input"
         ops = []
-        if kind == "refs" and not first_fns:
+        if kind == "stream":
+            ops.append(_TaskOp(first_name, first_fns, first_res, first_cap) if first_fns
+                       else _PassOp("Input"))
+            self._source = []
+        elif kind == "refs" and not first_fns:
             self._source = [(r, (src_meta[i] if src_meta else None), i)
                             for i, r in enumerate(src)]
         else:
@@ -479,7 +549,7 @@ class StreamingExecutor:
         self.ops = ops
         self.rm = ResourceManager(ops, _cluster_limits(self.options),
                                   self.options.reservation_ratio)
-        if ops:
+        if ops and self._stream is None:
             for item, meta, seq in self._source:
                 ops[0].inq.append((item, meta, seq, 0))
             ops[0].upstream_done = True
@@ -493,9 +563,53 @@ class StreamingExecutor:
             self._finished = True
             return self
         self._t0 = time.perf_counter()
+        if self._stream is not None:
+            self._feed = collections.deque()
+            self._feed_done = False
+            self._feed_error = None
+            self._feeder = threading.Thread(target=self._feed_run, daemon=True,
+                                            name="data-feed")
+            self._feeder.start()
         self._thread = threading.Thread(target=self._run, daemon=True, name="data-exec")
         self._thread.start()
         return self
+
+    def _feed_run(self):
+        """Pull the streamed source; stay at most a few blocks ahead of the first op."""
+        seq = 0
+        try:
+            for item, meta in self._stream():
+                with self._cv:
+                    while not self._stop and len(self._feed) + len(self.ops[0].inq) > \
+                            max(8, 2 * min(self.ops[0].cap, 64)):
+                        self._cv.wait(0.05)
+                    if self._stop:
+                        return
+                    self._feed.append((item, meta, seq, _nbytes(meta)))
+                    seq += 1
+        except BaseException as e:  # noqa: BLE001
+            self._feed_error = e
+        finally:
+            with self._cv:
+                self._feed_done = True
+                self._cv.notify_all()
+
+    def _drain_feed(self):
+        if self._stream is None:
+            return False
+        moved = False
+        with self._cv:
+            while self._feed:
+                self.ops[0].push_input(self._feed.popleft())
+                moved = True
+            if self._feed_done and not self._feed and not self.ops[0].upstream_done:
+                if self._feed_error is not None:
+                    raise self._feed_error
+                self.ops[0].upstream_done = True
+                moved = True
+            if moved:
+                self._cv.notify_all()
+        return moved
 
     def _run(self):
         try:
@@ -514,18 +628,17 @@ class StreamingExecutor:
         ops = self.ops
         last = ops[-1]
         while not self._stop:
-            progressed = False
+            progressed = self._drain_feed()
             # 1. hand outputs downstream / to the consumer
             for k, op in enumerate(ops):
                 while op.outq:
                     b, m, seq = op.take_output()
                     if k + 1 < len(ops):
-                        ops[k + 1].push_input((b, m, seq, int(m.get("size_bytes", 0))
-                                               if m else 0))
+                        ops[k + 1].push_input((b, m, seq, _nbytes(m)))
                     else:
                         with self._cv:
                             self._out.append((b, m))
-                            self._out_bytes += int(m.get("size_bytes", 0)) if m else 0
+                            self._out_bytes += _nbytes(m)
                             self._cv.notify_all()
                     progressed = True
                 if k + 1 < len(ops) and op.done():
@@ -559,7 +672,7 @@ class StreamingExecutor:
                         waits[r] = op
             if not waits:
                 if not progressed:
-                    with self._cv:  # blocked on the consumer: wait until it reads
+                    with self._cv:  # blocked on the consumer / the feeder: wait for it
                         self._cv.wait(0.05)
                 continue
             ready, _ = ray.wait(list(waits), num_returns=1, timeout=0.05 if not progressed
@@ -601,7 +714,7 @@ class StreamingExecutor:
                     if self._out:
                         item = self._out.popleft()
                         m = item[1]
-                        self._out_bytes -= int(m.get("size_bytes", 0)) if m else 0
+                        self._out_bytes -= _nbytes(m)
                         self._cv.notify_all()
                     elif self._error is not None:
                         raise self._error
@@ -613,6 +726,8 @@ class StreamingExecutor:
 
     def shutdown(self):
         self._stop = True
+        with self._cv:
+            self._cv.notify_all()
         if self._thread is not None and self._thread is not threading.current_thread():
             self._thread.join(timeout=30)
 
@@ -640,6 +755,22 @@ def execute(plan: Plan, max_in_flight: int | None = None,
         if meta is not None and not isinstance(meta, dict):
             meta = ray.get(meta)
         yield ref, meta
+
+
+def execute_started(plan: Plan, options: ExecutionOptions | None = None):
+    """Like execute(), but the plan starts running NOW (before the first next()): a
+    consumer of several inputs (union) starts them all at once without blocking."""
+    if plan._cache is not None:
+        return iter(list(zip(*plan._cache)))
+    ex = StreamingExecutor(plan, options or _default_options()).start()
+
+    def gen():
+        for ref, meta in ex:
+            if meta is not None and not isinstance(meta, dict):
+                meta = ray.get(meta)
+            yield ref, meta
+
+    return gen()
 
 
 def materialize(plan: Plan):

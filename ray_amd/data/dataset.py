@@ -9,6 +9,7 @@ task graphs over the materialised upstream blocks.
 from __future__ import annotations
 
 import builtins
+import collections
 import itertools
 import math
 import os
@@ -237,6 +238,29 @@ def _concat_remote(*blks):
     return b, X._meta(b)
 
 
+@ray.remote
+def _merge_parts(*parts):
+    """Push-based shuffle merge: one reducer's parts of a round of map outputs."""
+    parts = [p for p in parts if B.num_rows(p)]
+    return B.concat(parts) if len(parts) > 1 else (parts[0] if parts else {})
+
+
+def _merge_round(plist, n_out):
+    return [_merge_parts.remote(*[pl[j] for pl in plist]) for j in range(n_out)]
+
+
+@ray.remote(num_returns=2)
+def _zip_aligned(a, *pieces):
+    """Left block `a` joined with the right rows given as (ref, start, end) triples."""
+    parts = [B.slice_block(pieces[i], pieces[i + 1], pieces[i + 2])
+             for i in range(0, len(pieces), 3)]
+    right = B.concat(parts) if len(parts) != 1 else parts[0]
+    out = dict(a)
+    for k, v in right.items():
+        out[k if k not in out else f"{k}_1"] = v
+    return out, X._meta(out)
+
+
 @ray.remote(num_returns=2)
 def _zip_remote(a, b):
     out = dict(a)
@@ -453,25 +477,41 @@ class Dataset:
         return X.materialize(self._plan)
 
     def _shuffle(self, n_out, mode, key=None, boundaries=None, seed=None, descending=False):
+        """All-to-all exchange. The map side is streamed: each upstream block is
+        partitioned as soon as it is produced. With ``DataContext.use_push_based_shuffle``
+        (reference: planner/exchange/push_based_shuffle_task_scheduler.py:400) map outputs
+        are pushed through merge tasks every ``merge_factor`` maps, so each reducer reads
+        ceil(M / merge_factor) merged inputs instead of M small ones; the reducers' output
+        blocks stream to the consumer."""
         parent = self
 
-        def lazy():
-            refs, metas = parent._blocks()
-            if not refs:
-                return [], []
-            plist = [_partition(r, n_out, mode, key, boundaries,
-                                None if seed is None else seed + i, descending)
-                     for i, r in enumerate(refs)]
-            outs, oms = [], []
+        def stream():
+            from . import DataContext
+
+            ctx = DataContext.get_current()
+            push = bool(getattr(ctx, "use_push_based_shuffle", False))
+            mf = max(2, int(getattr(ctx, "push_based_shuffle_merge_factor", 8)))
+            plist, merged, i = [], [], 0
+            for r, _m in X.execute(parent._plan):
+                plist.append(_partition(r, n_out, mode, key, boundaries,
+                                        None if seed is None else seed + i, descending))
+                i += 1
+                if push and len(plist) >= mf:
+                    merged.append(_merge_round(plist, n_out))
+                    plist = []
+            if i == 0:
+                return
+            if push and plist:
+                merged.append(_merge_round(plist, n_out))
+                plist = []
+            inputs = merged if push else plist
             for j in range(n_out):
                 b, m = _reduce_parts.remote(mode, key, descending,
                                             None if seed is None else seed * 7919 + j,
-                                            *[pl[j] for pl in plist])
-                outs.append(b)
-                oms.append(m)
-            return outs, ray.get(oms)
+                                            *[pl[j] for pl in inputs])
+                yield b, m
 
-        return Dataset(X.Plan(("lazy", lazy)))
+        return Dataset(X.Plan(("stream", stream)))
 
     def random_shuffle(self, *, seed=None, num_blocks=None, **kw) -> "Dataset":
         n = num_blocks or max(1, len(self._blocks()[0]))
@@ -533,30 +573,55 @@ class Dataset:
         return GroupedData(self, key)
 
     def union(self, *others) -> "Dataset":
+        """Streaming union (reference: operators/union_operator.py:12): every input runs
+        in its own streaming executor at once; blocks are emitted input by input, in
+        order, as they are produced — nothing is materialised first."""
         dss = [self] + list(others)
 
-        def lazy():
-            refs, metas = [], []
-            for d in dss:
-                r, m = d._blocks()
-                refs.extend(r)
-                metas.extend(m)
-            return refs, metas
+        def stream():
+            its = [X.execute_started(d._plan) for d in dss]  # all inputs run at once
+            for it in its:
+                yield from it
 
-        return Dataset(X.Plan(("lazy", lazy)))
+        return Dataset(X.Plan(("stream", stream)))
 
     def zip(self, other) -> "Dataset":
+        """Column-wise zip (reference: operators/zip_operator.py:19). Output blocks
+        follow the LEFT dataset's block boundaries: for each left block the matching row
+        range of the right dataset (spanning one or more right blocks) is sliced and
+        joined in one task, as both sides stream — no single-block repartition."""
         a, b = self, other
 
-        def lazy():
-            ra, ma = a.repartition(1)._blocks()
-            rb, mb = b.repartition(1)._blocks()
-            if ma[0]["num_rows"] != mb[0]["num_rows"]:
-                raise ValueError("Cannot zip datasets of different number of rows")
-            z, m = _zip_remote.remote(ra[0], rb[0])
-            return [z], [ray.get(m)]
+        def stream():
+            it_b = X.execute(b._plan)
+            right = collections.deque()  # (ref, first row, rows)
+            right_end = 0
+            pos = 0
+            for ra, ma in X.execute(a._plan):
+                n = ma["num_rows"]
+                need = pos + n
+                while right_end < need:
+                    nxt = next(it_b, None)
+                    if nxt is None:
+                        raise ValueError("Cannot zip datasets of different number of rows: "
+                                         f"the right side ended at row {right_end}")
+                    rb, mb = nxt
+                    if mb["num_rows"]:
+                        right.append((rb, right_end, mb["num_rows"]))
+                        right_end += mb["num_rows"]
+                pieces = [(r, max(pos, s0) - s0, min(need, s0 + k) - s0)
+                          for r, s0, k in right if s0 < need and s0 + k > pos]
+                while right and right[0][1] + right[0][2] <= need:
+                    right.popleft()
+                zb, zm = _zip_aligned.remote(ra, *[x for p in pieces for x in p])
+                yield zb, zm
+                pos = need
+            rest = right_end - pos + sum(m["num_rows"] for _, m in it_b)
+            if rest:
+                raise ValueError("Cannot zip datasets of different number of rows: the "
+                                 f"right side has {rest} more")
 
-        return Dataset(X.Plan(("lazy", lazy)))
+        return Dataset(X.Plan(("stream", stream)))
 
     def unique(self, column: str) -> list:
         """Distinct values (per-block sets in tasks, unioned on the driver). A null (None /
