@@ -93,6 +93,7 @@ class Algorithm:
         self.metrics = MetricsLogger()
         self._custom_metrics = {}
         self.is_multi_agent = bool(getattr(config, "is_multi_agent", False))
+        self.cfg["is_multi_agent"] = self.is_multi_agent
         if self.is_multi_agent and not self.supports_multi_agent:
             raise NotImplementedError(f"{type(self).__name__} does not support multi-agent "
                                       "configs yet (PPO does)")
@@ -283,7 +284,7 @@ class Algorithm:
         return {"env_runners": {"episode_return_mean": float(np.mean(rets[:n]))}}
 
     # ---------------------------------------------------------------- inference
-    def _new_module(self, obs_space, act_space):
+    def _new_module(self, obs_space, act_space, module_id=None):
         """An inference module of this algorithm's kind (what its EnvRunners run)."""
         kind = self.cfg.get("module_kind", "actor_critic")
         if kind == "q":
@@ -298,9 +299,9 @@ class Algorithm:
             return SquashedGaussianPolicy(obs_space, act_space,
                                           self.cfg.get("policy_model_config") or
                                           self.config.model)
-        from ray_amd.rllib.core.rl_module import RLModule
+        from ray_amd.rllib.core.rl_module.rl_module import build_module
 
-        return RLModule(obs_space, act_space, self.config.model)
+        return build_module(self.cfg, obs_space, act_space, module_id)
 
     def get_module(self, module_id=None):
         """The RLModule with the current weights, on the CPU, for inference (reference:
@@ -312,7 +313,7 @@ class Algorithm:
             os_, as_ = self.module_specs[mid]
             mods = self.__dict__.setdefault("_infer_modules", {})
             if mid not in mods:
-                mods[mid] = self._new_module(os_, as_)
+                mods[mid] = self._new_module(os_, as_, mid)
             m = mods[mid]
             m.load_state_dict(self.get_weights()[mid])
             self._infer_filter = None

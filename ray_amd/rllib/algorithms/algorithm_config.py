@@ -48,6 +48,26 @@ class AlgorithmConfig:
         # iteration of policy lag; the PPO ratio uses the recorded behaviour logp)
         self.sample_async = False
         self.callbacks_class = None
+        # RLModule / Learner extensibility (reference: AlgorithmConfig.rl_module, training
+        # learner_class)
+        self._rl_module_spec = None
+        self.learner_class = None
+        # fault tolerance (reference: AlgorithmConfig.fault_tolerance, algorithm_config.py
+        # :2673): recreate dead EnvRunners and resync their weights
+        self.restart_failed_env_runners = True
+        self.ignore_env_runner_failures = False
+        self.max_num_env_runner_restarts = 1000
+        self.delay_between_env_runner_restarts_s = 0.0
+        self.env_runner_health_probe_timeout_s = 30.0
+        self.restart_failed_sub_environments = False
+        self.evaluation_parallel_to_training = False
+        self.evaluation_duration_unit = "episodes"
+        self.checkpoint_trainable_policies_only = False
+        self.explore = True
+        self.exploration_config = {}
+        self.keep_per_episode_custom_metrics = False
+        self.extra_python_environs_for_driver = {}
+        self.extra_python_environs_for_worker = {}
 
     # ---------------------------------------------------------------- builders
     def environment(self, env=None, *, env_config=None, **kw):
@@ -108,6 +128,98 @@ class AlgorithmConfig:
         self.callbacks_class = callbacks_class
         return self
 
+    def rl_module(self, *, rl_module_spec=None, model_config=None, model_config_dict=None,
+                  **kw):
+        """A user RLModule (RLModuleSpec / MultiRLModuleSpec) and / or the model config
+        of the default modules (reference: AlgorithmConfig.rl_module)."""
+        if rl_module_spec is not None:
+            self._rl_module_spec = rl_module_spec
+        mc = model_config if model_config is not None else model_config_dict
+        if mc is not None:
+            self.model = dict(getattr(mc, "__dict__", mc)) if not isinstance(mc, dict) \
+                else dict(mc)
+        return self
+
+    @property
+    def rl_module_spec(self):
+        return self._rl_module_spec
+
+    @property
+    def model_config(self):
+        return dict(self.model or {})
+
+    def get_rl_module_spec(self, env=None, spaces=None):
+        from ray_amd.rllib.core.rl_module import RLModuleSpec
+
+        return self._rl_module_spec or RLModuleSpec(model_config=dict(self.model or {}))
+
+    def get_default_learner_class(self):
+        from ray_amd.rllib.core.learner import Learner
+
+        return Learner
+
+    def fault_tolerance(self, *, restart_failed_env_runners=None,
+                        ignore_env_runner_failures=None, max_num_env_runner_restarts=None,
+                        delay_between_env_runner_restarts_s=None,
+                        env_runner_health_probe_timeout_s=None,
+                        restart_failed_sub_environments=None, recreate_failed_env_runners=None,
+                        **kw):
+        if recreate_failed_env_runners is not None:  # old name
+            restart_failed_env_runners = recreate_failed_env_runners
+        for k, v in dict(restart_failed_env_runners=restart_failed_env_runners,
+                         ignore_env_runner_failures=ignore_env_runner_failures,
+                         max_num_env_runner_restarts=max_num_env_runner_restarts,
+                         delay_between_env_runner_restarts_s=delay_between_env_runner_restarts_s,
+                         env_runner_health_probe_timeout_s=env_runner_health_probe_timeout_s,
+                         restart_failed_sub_environments=restart_failed_sub_environments
+                         ).items():
+            if v is not None:
+                setattr(self, k, v)
+        return self
+
+    def checkpointing(self, *, export_native_model_files=None,
+                      checkpoint_trainable_policies_only=None, **kw):
+        if checkpoint_trainable_policies_only is not None:
+            self.checkpoint_trainable_policies_only = checkpoint_trainable_policies_only
+        return self
+
+    def exploration(self, *, explore=None, exploration_config=None, **kw):
+        if explore is not None:
+            self.explore = bool(explore)
+        if exploration_config is not None:
+            self.exploration_config = dict(exploration_config)
+        return self
+
+    def python_environment(self, *, extra_python_environs_for_driver=None,
+                           extra_python_environs_for_worker=None, **kw):
+        if extra_python_environs_for_driver is not None:
+            self.extra_python_environs_for_driver = dict(extra_python_environs_for_driver)
+        if extra_python_environs_for_worker is not None:
+            self.extra_python_environs_for_worker = dict(extra_python_environs_for_worker)
+        return self
+
+    def experimental(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k.lstrip("_"), v)
+        return self
+
+    def validate(self):
+        if self.num_env_runners < 0:
+            raise ValueError("num_env_runners must be >= 0")
+        if self.evaluation_num_env_runners < 0:
+            raise ValueError("evaluation_num_env_runners must be >= 0")
+        if isinstance(self.train_batch_size, int) and self.train_batch_size <= 0:
+            raise ValueError("train_batch_size must be > 0")
+        return True
+
+    def freeze(self):
+        self._is_frozen = True
+        return self
+
+    @classmethod
+    def from_dict(cls, d: dict):
+        return cls().update_from_dict(d)
+
     def framework(self, framework="torch", **kw):
         if framework not in ("torch",):
             raise ValueError("ray_amd RLlib supports framework='torch' only (MI355X/ROCm)")
@@ -120,7 +232,14 @@ class AlgorithmConfig:
         return self
 
     def evaluation(self, *, evaluation_interval=None, evaluation_duration=None,
-                   evaluation_num_env_runners=None, evaluation_config=None, **kw):
+                   evaluation_num_env_runners=None, evaluation_config=None,
+                   evaluation_parallel_to_training=None, evaluation_duration_unit=None, **kw):
+        if evaluation_parallel_to_training is not None:
+            self.evaluation_parallel_to_training = bool(evaluation_parallel_to_training)
+        if evaluation_duration_unit is not None:
+            if evaluation_duration_unit not in ("episodes", "timesteps"):
+                raise ValueError("evaluation_duration_unit must be 'episodes' or 'timesteps'")
+            self.evaluation_duration_unit = evaluation_duration_unit
         if evaluation_interval is not None:
             self.evaluation_interval = evaluation_interval
         if evaluation_duration is not None:
@@ -180,7 +299,11 @@ class AlgorithmConfig:
             if k == "num_gpus":
                 self.resources(num_gpus=v)
                 continue
-            setattr(self, self._LEGACY_KEYS.get(k, k), v)
+            name = self._LEGACY_KEYS.get(k, k)
+            prop = getattr(type(self), name, None)
+            if isinstance(prop, property) and prop.fset is None:
+                continue  # derived (is_multi_agent, model_config, ...): not settable
+            setattr(self, name, v)
         return self
 
     def copy(self, copy_frozen=None):

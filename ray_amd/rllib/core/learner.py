@@ -18,7 +18,13 @@ import numpy as np
 import torch
 
 from ray_amd.ops import functional as rf
+from ray_amd.rllib.core.columns import Columns
 from ray_amd.rllib.core.rl_module import RLModule, gaussian_entropy, gaussian_logp
+from ray_amd.rllib.core.rl_module.rl_module import build_module
+
+DEFAULT_MODULE_ID = "default_policy"
+# batch fields whose leading axis is the env / sequence axis (everything else is [T, B, ...])
+_AXIS0 = ("bootstrap_obs", "state_in_h", "state_in_c", "state_out_h", "state_out_c")
 
 
 def _to_t(x, device, dtype=None, non_blocking=True):
@@ -58,7 +64,7 @@ def concat_batches(batches, lazy=()):
     for k in batches[0]:
         v = batches[0][k]
         if isinstance(v, np.ndarray):
-            axis = 0 if k == "bootstrap_obs" else 1
+            axis = 0 if k in _AXIS0 else 1
             if k in lazy and axis == 1 and len(batches) > 1:
                 out[k] = Fragments([b[k] for b in batches])
             else:
@@ -69,8 +75,24 @@ def concat_batches(batches, lazy=()):
 
 
 class Learner:
+    """One learner (one GPU). Extension points (reference: rllib/core/learner/learner.py
+    :435 configure_optimizers_for_module, :948 compute_loss_for_module):
+
+    * ``configure_optimizers_for_module(module_id, config)`` — the default keeps the fused
+      flat-buffer AdamW (HIP kernel, fp32 master + bf16 compute weights); an override
+      calls ``register_optimizer(...)`` with any torch optimizer over ``self.module``'s
+      parameters (then weights stay fp32).
+    * ``compute_loss_for_module(module_id, config, batch, fwd_out)`` — the default is the
+      fused HIP PPO loss (PPO) / the V-trace loss (IMPALA/APPO); an override gets the
+      minibatch as a dict of tensors (``Columns.*`` plus ``advantages`` /
+      ``value_targets``, or ``vtrace_vs`` / ``pg_advantages``) and the module's
+      ``forward_train`` output, and returns the scalar loss.
+
+    User modules, stateful modules and overridden losses run the generic (eager) SGD loop;
+    the built-in module with the built-in loss keeps the captured HIP-graph step."""
+
     def __init__(self, config: dict, observation_space, action_space, device=None, rank=0,
-                 world=1):
+                 world=1, module_id=DEFAULT_MODULE_ID):
         self.config = config
         if device is None:
             device = torch.device("cuda", int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))) \
@@ -78,28 +100,44 @@ class Learner:
                 torch.device("cpu")
         self.device = device
         self.rank, self.world = rank, world
+        self.module_id = module_id
         torch.manual_seed(config.get("seed") or 0)
-        self.module = RLModule(observation_space, action_space, config.get("model")).to(device)
-        if device.type == "cuda":
+        self.module = build_module(config, observation_space, action_space,
+                                   module_id if config.get("is_multi_agent") else None
+                                   ).to(device)
+        self._builtin_module = isinstance(self.module, RLModule)
+        self.stateful = bool(getattr(self.module, "is_stateful", lambda: False)()) and \
+            hasattr(self.module, "forward_sequence")
+        if device.type == "cuda" and self._builtin_module:
             # NHWC conv weights (FlatParams keeps the layout): no per-call weight relayout
             self.module.to(memory_format=torch.channels_last)
         self._pinned = {}
+        self._optimizers = {}  # (module_id, name) -> (torch optimizer, params)
+        self.configure_optimizers_for_module(module_id, config)
         from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams
 
         # bf16 compute weights + fp32 master in the flat optimizer on GPU: no per-forward
-        # autocast weight casts (they were ~30 copy kernels per SGD step)
-        bf16 = device.type == "cuda" and config.get("learner_bf16", True)
+        # autocast weight casts (they were ~30 copy kernels per SGD step). A registered
+        # torch optimizer updates the parameters themselves: keep them fp32.
+        bf16 = device.type == "cuda" and config.get("learner_bf16", True) and \
+            not self._optimizers
         pdt = torch.bfloat16 if bf16 else torch.float32
         # grads alias .grad (same dtype as the compute weights): the whole SGD step,
         # including MIOpen's conv weight grads, stays capturable in one HIP graph
         self.flat = FlatParams(self.module, dtype=pdt, grad_dtype=pdt)
         self.ddp = FlatDDP(self.flat, bucket_mb=32.0)
-        self.opt = FlatAdamW(self.flat, lr=config.get("lr", 5e-5), betas=(0.9, 0.999), eps=1e-7,
-                             weight_decay=0.0, max_grad_norm=config.get("grad_clip"),
-                             grad_scale=self.ddp.grad_scale)
+        self.opt = None if self._optimizers else FlatAdamW(
+            self.flat, lr=config.get("lr", 5e-5), betas=(0.9, 0.999), eps=1e-7,
+            weight_decay=0.0, max_grad_norm=config.get("grad_clip"),
+            grad_scale=self.ddp.grad_scale)
         self.kl_coeff = config.get("kl_coeff", 0.2)
         self.amp = device.type == "cuda" and config.get("learner_bf16", True)
         self.updates = 0
+        self._custom_loss = type(self).compute_loss_for_module is not \
+            Learner.compute_loss_for_module
+        self._generic = self._custom_loss or not self._builtin_module or self.stateful or \
+            bool(self._optimizers)
+        self.metrics = {}
         # MeanStdFilter statistics live HERE: updated over every training batch by the HIP
         # Welford kernel (obsnorm_update) and broadcast to the EnvRunners with the weights
         self.obs_filter = None
@@ -107,6 +145,37 @@ class Learner:
             from ray_amd.ops.functional import RunningMeanStd
 
             self.obs_filter = RunningMeanStd(observation_space.shape, device)
+
+    # ---------------------------------------------------------------- extension API
+    def configure_optimizers_for_module(self, module_id, config):
+        """Default: the fused flat AdamW built in __init__ (nothing to register)."""
+
+    def register_optimizer(self, *, module_id=DEFAULT_MODULE_ID, optimizer_name="default",
+                           optimizer, params=None, lr_or_lr_schedule=None):
+        params = list(params) if params is not None else \
+            [p for g in optimizer.param_groups for p in g["params"]]
+        self._optimizers[(module_id, optimizer_name)] = (optimizer, params)
+
+    def get_optimizer(self, module_id=DEFAULT_MODULE_ID, optimizer_name="default"):
+        ent = self._optimizers.get((module_id, optimizer_name))
+        return ent[0] if ent else self.opt
+
+    def get_parameters(self, module=None):
+        return list((module or self.module).parameters())
+
+    def compute_loss_for_module(self, module_id, config, batch, fwd_out):
+        """Default losses: PPO (fused HIP kernel for discrete actions) or V-trace."""
+        if "vtrace_vs" in batch:
+            return self._vtrace_loss(batch, fwd_out)[0]
+        loss, st = self._ppo_loss(fwd_out, batch[Columns.ACTION_DIST_INPUTS],
+                                  batch[Columns.ACTIONS], batch[Columns.ACTION_LOGP],
+                                  batch[Columns.ADVANTAGES], batch[Columns.VALUE_TARGETS])
+        self._last_stats = st
+        return loss
+
+    def compute_losses(self, fwd_out, batch):
+        return {self.module_id: self.compute_loss_for_module(self.module_id, self.config,
+                                                             batch, fwd_out)}
 
     def _filter_obs(self, obs_flat, boot_obs):
         """Normalize raw observations (updating the running stats with this batch)."""
@@ -155,7 +224,10 @@ class Learner:
                 "master": {"p32": self.flat.p32.detach().cpu(), "names": list(self.flat.names),
                            "offsets": list(self.flat.offsets)},
                 "opt": {k: v.cpu() if torch.is_tensor(v) else v
-                        for k, v in self.opt.state_dict().items()},
+                        for k, v in self.opt.state_dict().items()} if self.opt is not None
+                else None,
+                "torch_opts": {f"{m}/{n}": o.state_dict()
+                               for (m, n), (o, _) in self._optimizers.items()},
                 "kl_coeff": self.kl_coeff,
                 "obs_filter": self.obs_filter.state_dict() if self.obs_filter is not None
                 else None}
@@ -172,8 +244,13 @@ class Learner:
                     self.flat.p16.copy_(self.flat.p32)
         else:  # older checkpoint / different layout: rebuild the master from the weights
             self.set_weights(s["weights"])
-        self.opt.load_state_dict({k: v.to(self.device) if torch.is_tensor(v) else v
-                                  for k, v in s["opt"].items()})
+        if self.opt is not None and s.get("opt") is not None:
+            self.opt.load_state_dict({k: v.to(self.device) if torch.is_tensor(v) else v
+                                      for k, v in s["opt"].items()})
+        for (m, n), (o, _) in self._optimizers.items():
+            st = (s.get("torch_opts") or {}).get(f"{m}/{n}")
+            if st is not None:
+                o.load_state_dict(st)
         self.kl_coeff = s.get("kl_coeff", self.kl_coeff)
 
     # ---------------------------------------------------------------- multi-learner agreement
@@ -236,6 +313,18 @@ class Learner:
         return torch.cat(out)
 
     def _step(self, loss):
+        if self._optimizers:
+            for opt, _ in self._optimizers.values():
+                opt.zero_grad(set_to_none=False)
+            self.flat.zero_grad()
+            loss.backward()
+            self.ddp.finish()
+            gc = self.config.get("grad_clip")
+            for opt, params in self._optimizers.values():
+                if gc:
+                    torch.nn.utils.clip_grad_norm_(params, gc)
+                opt.step()
+            return
         self.flat.zero_grad()
         loss.backward()
         self.ddp.finish()
@@ -243,6 +332,8 @@ class Learner:
 
     # ---------------------------------------------------------------- PPO
     def update_ppo(self, batch: dict) -> dict:
+        if self.stateful:
+            return self._update_ppo_stateful(batch)
         c = self.config
         dev = self.device
         obs = self._h2d(batch["obs"], "obs")
@@ -294,8 +385,8 @@ class Learner:
         stats_acc = torch.zeros(6, device=dev)
         n_mb = 0
         # masked (multi-agent) batches change N every update: no graph re-capture per call
-        g = None if masked else self._ppo_graph(obs_flat, old_di, acts, old_logp, adv, vtarg,
-                                                mb)
+        g = None if masked or self._generic else self._ppo_graph(obs_flat, old_di, acts,
+                                                                  old_logp, adv, vtarg, mb)
         if g is not None:
             # replay one captured SGD step (gather, fwd, fused loss, bwd) per minibatch;
             # the optimizer's two kernels stay eager (Adam's step count is a kernel arg)
@@ -315,8 +406,19 @@ class Learner:
             for s in range(0, n_common - mb + 1, mb):
                 idx = perm[s:s + mb]
                 out = self._fwd(obs_flat[idx])
-                loss, st = self._ppo_loss(out, old_di[idx], acts[idx], old_logp[idx], adv[idx],
-                                          vtarg[idx])
+                if self._generic:
+                    mbatch = {Columns.OBS: obs_flat[idx], Columns.ACTIONS: acts[idx],
+                              Columns.ACTION_LOGP: old_logp[idx],
+                              Columns.ACTION_DIST_INPUTS: old_di[idx],
+                              Columns.ADVANTAGES: adv[idx], Columns.VALUE_TARGETS: vtarg[idx],
+                              Columns.VF_PREDS: vals[idx]}
+                    self._last_stats = None
+                    loss = self.compute_loss_for_module(self.module_id, c, mbatch, out)
+                    st = self._last_stats if self._last_stats is not None else \
+                        torch.stack([loss.detach().float()] + [torch.zeros((), device=dev)] * 5)
+                else:
+                    loss, st = self._ppo_loss(out, old_di[idx], acts[idx], old_logp[idx],
+                                              adv[idx], vtarg[idx])
                 self._step(loss)
                 stats_acc += st.detach()
                 n_mb += 1
@@ -332,6 +434,79 @@ class Learner:
                 "entropy": stats[3], "mean_kl_loss": kl, "clip_frac": stats[5],
                 "curr_kl_coeff": self.kl_coeff, "num_minibatches": n_mb,
                 "vf_explained_var": _explained_var(vtarg, vals)}
+
+    def _update_ppo_stateful(self, batch: dict) -> dict:
+        """PPO for a stateful (recurrent) module over time-major [T, B] fragments: values
+        and the loss are computed by unrolling the module through each fragment from its
+        recorded ``state_in`` (state zeroed where an episode starts: ``resets``);
+        minibatches are whole sequences (columns), ``minibatch_size // T`` at a time."""
+        c = self.config
+        dev = self.device
+        m = self.module
+        obs = _to_t(batch["obs"], dev)
+        T, B = obs.shape[:2]
+        rewards = _to_t(batch["rewards"], dev)
+        dones = _to_t(batch["terminateds"], dev)
+        acts = _to_t(batch["actions"], dev)
+        old_logp = _to_t(batch["action_logp"], dev)
+        old_di = _to_t(batch["action_dist_inputs"], dev)
+        boot_obs = _to_t(batch["bootstrap_obs"], dev)
+        h0 = _to_t(batch["state_in_h"], dev).float()
+        c0 = _to_t(batch["state_in_c"], dev).float()
+        resets = _to_t(batch["resets"], dev).float()
+        with torch.no_grad():
+            _, vals, (hT, cT) = m.forward_sequence(obs, h0, c0, resets)
+            keep = (1.0 - dones[-1].float())[:, None]
+            _, boot_v, _ = m.step(boot_obs, {"h": hT * keep, "c": cT * keep})
+        adv, vtarg = rf.gae(rewards.float(), vals.float(), dones.float(), boot_v.float(),
+                            c.get("gamma", 0.99), c.get("lambda_", 0.95))
+        N = adv.numel()
+        mom = self._allreduce(torch.stack([adv.sum(), (adv * adv).sum(),
+                                           torch.tensor(float(N), device=dev)]).double())
+        cnt = max(float(mom[2]), 1.0)
+        mean = mom[0] / cnt
+        std = torch.sqrt(torch.clamp(mom[1] / cnt - mean * mean, min=0.0))
+        adv = (adv - mean.float()) / (std.float() + 1e-8)
+        n_common = int(self._allreduce(torch.tensor([B], device=dev), op="min")[0]) \
+            if self.world > 1 else B
+        seq_mb = max(1, min(n_common, int(c.get("minibatch_size", 128)) // T))
+        stats_acc = torch.zeros(6, device=dev)
+        n_mb = 0
+        for _ in range(int(c.get("num_epochs", 1))):
+            perm = torch.randperm(B, device=dev)[:n_common]
+            for s in range(0, n_common - seq_mb + 1, seq_mb):
+                cols = perm[s:s + seq_mb]
+                logits, v, _ = m.forward_sequence(obs[:, cols], h0[cols], c0[cols],
+                                                  resets[:, cols])
+                n = T * cols.numel()
+                out = {Columns.ACTION_DIST_INPUTS: logits.reshape(n, -1),
+                       Columns.VF_PREDS: v.reshape(n)}
+                mbatch = {Columns.OBS: obs[:, cols].reshape((n,) + tuple(obs.shape[2:])),
+                          Columns.ACTIONS: acts[:, cols].reshape((n,) + tuple(acts.shape[2:])),
+                          Columns.ACTION_LOGP: old_logp[:, cols].reshape(n),
+                          Columns.ACTION_DIST_INPUTS: old_di[:, cols].reshape(n, -1),
+                          Columns.ADVANTAGES: adv[:, cols].reshape(n),
+                          Columns.VALUE_TARGETS: vtarg[:, cols].reshape(n),
+                          Columns.VF_PREDS: vals[:, cols].reshape(n)}
+                self._last_stats = None
+                loss = self.compute_loss_for_module(self.module_id, c, mbatch, out)
+                st = self._last_stats if self._last_stats is not None else \
+                    torch.stack([loss.detach().float()] + [torch.zeros((), device=dev)] * 5)
+                self._step(loss)
+                stats_acc += st.detach()
+                n_mb += 1
+        stats = (stats_acc / max(1, n_mb)).tolist()
+        kl = stats[4]
+        if c.get("use_kl_loss", True) and c.get("kl_target"):
+            if kl > 2.0 * c["kl_target"]:
+                self.kl_coeff *= 1.5
+            elif kl < 0.5 * c["kl_target"]:
+                self.kl_coeff *= 0.5
+        self.updates += 1
+        return {"total_loss": stats[0], "policy_loss": stats[1], "vf_loss": stats[2],
+                "entropy": stats[3], "mean_kl_loss": kl, "curr_kl_coeff": self.kl_coeff,
+                "num_minibatches": n_mb, "vf_explained_var": _explained_var(
+                    vtarg.reshape(-1), vals.reshape(-1))}
 
     def _ppo_graph(self, obs, old_di, acts, old_logp, adv, vtarg, mb):
         """HIP graph of one PPO SGD step over static full-batch buffers (the minibatch
@@ -514,8 +689,36 @@ class Learner:
             vs, pg_adv = rf.vtrace(tgt_logp.detach() - beh_logp, disc, rewards, v.detach(), boot_v,
                                    c.get("vtrace_clip_rho_threshold", 1.0), 1.0,
                                    c.get("vtrace_clip_pg_rho_threshold", 1.0))
+        vb = {Columns.OBS: obs_flat, Columns.ACTIONS: acts.reshape(-1) if acts.dim() == 2
+              else acts.reshape((T * B,) + tuple(acts.shape[2:])),
+              Columns.ACTION_LOGP: beh_logp.reshape(-1), "vtrace_vs": vs.reshape(-1),
+              "pg_advantages": pg_adv.reshape(-1), "_T": T, "_B": B}
         if "loss_mask" in batch:  # multi-agent padding rows: excluded from every term
-            m = _to_t(batch["loss_mask"], dev).float().view(T, B)
+            vb[Columns.LOSS_MASK] = _to_t(batch["loss_mask"], dev).float().reshape(-1)
+        out = dict(out)
+        if self._custom_loss:
+            self._vt_stats = None
+            loss = self.compute_loss_for_module(self.module_id, c, vb, out)
+            pg = vf = ent = loss.detach()
+        else:
+            loss, (pg, vf, ent) = self._vtrace_loss(vb, out)
+        self._step(loss)
+        self.updates += 1
+        return {"total_loss": float(loss.detach()), "pi_loss": float(pg),
+                "vf_loss": float(vf), "entropy": float(ent)}
+
+    def _vtrace_loss(self, vb, out):
+        """IMPALA / APPO loss over flat [T*B] rows given V-trace targets (vtrace_vs) and
+        policy-gradient advantages (pg_advantages)."""
+        c = self.config
+        logits = out[Columns.ACTION_DIST_INPUTS].float()
+        v = out[Columns.VF_PREDS].float().reshape(-1)
+        lp_all = torch.log_softmax(logits, -1)
+        tgt_logp = lp_all.gather(-1, vb[Columns.ACTIONS].reshape(-1, 1).long())[:, 0]
+        beh_logp = vb[Columns.ACTION_LOGP]
+        pg_adv, vs = vb["pg_advantages"], vb["vtrace_vs"]
+        m = vb.get(Columns.LOSS_MASK)
+        if m is not None:
             inv = 1.0 / m.sum().clamp_min(1.0)
 
             def mean(x):
@@ -530,12 +733,23 @@ class Learner:
         else:
             pg = -mean(tgt_logp * pg_adv)
         vf = 0.5 * mean((vs - v) ** 2)
-        ent = mean(-(lp_all.exp() * lp_all).sum(-1).view(T, B))
+        ent = mean(-(lp_all.exp() * lp_all).sum(-1))
         loss = pg + c.get("vf_loss_coeff", 0.5) * vf - c.get("entropy_coeff", 0.01) * ent
-        self._step(loss)
-        self.updates += 1
-        return {"total_loss": float(loss.detach()), "pi_loss": float(pg.detach()),
-                "vf_loss": float(vf.detach()), "entropy": float(ent.detach())}
+        return loss, (pg.detach(), vf.detach(), ent.detach())
+
+
+def _learner_cls(config):
+    """``config.training(learner_class=...)``: a Learner subclass (custom losses /
+    optimizers); default Learner."""
+    return config.get("learner_class") or Learner
+
+
+# reference class names (rllib/core/learner/torch/torch_learner.py,
+# algorithms/{ppo,impala,appo}/torch/*_torch_learner.py): one MI355X learner serves all
+TorchLearner = Learner
+PPOTorchLearner = Learner
+IMPALATorchLearner = Learner
+APPOTorchLearner = Learner
 
 
 def _explained_var(y, pred):
@@ -553,7 +767,8 @@ class LearnerActor:
 
     def setup(self):
         obs_space, act_space, rank, world = self.args
-        self.learner = Learner(self.config, obs_space, act_space, rank=rank, world=world)
+        self.learner = _learner_cls(self.config)(self.config, obs_space, act_space, rank=rank,
+                                                 world=world)
         return True
 
     def update(self, kind, batches):
@@ -574,12 +789,14 @@ class LearnerActor:
 
 
 class LearnerGroup:
-    def __init__(self, config: dict, observation_space, action_space):
+    def __init__(self, config: dict, observation_space, action_space,
+                 module_id=DEFAULT_MODULE_ID):
         self.config = config
         n = int(config.get("num_learners", 0))
         self.remote = n > 0
         if not self.remote:
-            self.local = Learner(config, observation_space, action_space)
+            self.local = _learner_cls(config)(config, observation_space, action_space,
+                                              module_id=module_id)
             self.actors = []
             return
         import ray_amd as ray
@@ -599,8 +816,8 @@ class LearnerGroup:
         # gloo on CPU); "gloo" lets several GPU learners share one device in tests
         _TorchBackend().on_start(self.wg, TorchConfig(backend=config.get("learner_backend")))
         self.actors = self.wg.workers
-        ray.get([a.execute.remote(_make_learner, config, observation_space, action_space, i, n)
-                 for i, a in enumerate(self.actors)])
+        ray.get([a.execute.remote(_make_learner, config, observation_space, action_space, i, n,
+                                  module_id) for i, a in enumerate(self.actors)])
         self.local = None
 
     def update(self, kind, batches):
@@ -656,9 +873,10 @@ class LearnerGroup:
 _LEARNER = None
 
 
-def _make_learner(config, obs_space, act_space, rank, world):
+def _make_learner(config, obs_space, act_space, rank, world, module_id=DEFAULT_MODULE_ID):
     global _LEARNER
-    _LEARNER = Learner(config, obs_space, act_space, rank=rank, world=world)
+    _LEARNER = _learner_cls(config)(config, obs_space, act_space, rank=rank, world=world,
+                                    module_id=module_id)
     return True
 
 
@@ -675,7 +893,7 @@ def _split_b(batch, n, i):
     out = {}
     for k, v in batch.items():
         if isinstance(v, np.ndarray):
-            axis = 0 if k == "bootstrap_obs" else 1
+            axis = 0 if k in _AXIS0 else 1
             out[k] = np.array_split(v, n, axis=axis)[i]
         else:
             out[k] = v
@@ -690,7 +908,8 @@ class MultiAgentLearnerGroup:
     def __init__(self, config: dict, specs: dict, policies_to_train=None):
         self.specs = specs
         self.trainable = set(policies_to_train) if policies_to_train else set(specs)
-        self.groups = {mid: LearnerGroup(config, os_, as_) for mid, (os_, as_) in specs.items()}
+        self.groups = {mid: LearnerGroup(config, os_, as_, module_id=mid)
+                       for mid, (os_, as_) in specs.items()}
 
     def update(self, kind, batches):
         stats = {}

@@ -190,6 +190,12 @@ class RLModule(nn.Module):
     def set_state(self, state):
         self.load_state_dict(state)
 
+    def get_initial_state(self):
+        return {}
+
+    def is_stateful(self):
+        return False
+
 
 def gaussian_logp(a, mean, log_std):
     log_std = log_std.clamp(-20, 2)

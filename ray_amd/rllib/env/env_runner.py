@@ -79,8 +79,19 @@ class SingleAgentEnvRunner:
                                                  config.get("policy_model_config") or
                                                  config.get("model"))
         else:
-            self.module = RLModule(self.module_obs_space, self.action_space, config.get("model"))
+            from ray_amd.rllib.core.rl_module.rl_module import build_module
+
+            self.module = build_module(config, self.module_obs_space, self.action_space)
         self.module.eval()
+        # stateful (recurrent) modules: one state per env, carried across fragments, zeroed
+        # at episode starts; each fragment records the state it started from
+        self._stateful = bool(getattr(self.module, "is_stateful", lambda: False)()) and \
+            self.module_kind not in ("q", "sac")
+        if self._stateful:
+            init = self.module.get_initial_state()
+            self._state = {k: np.repeat(np.asarray(v, np.float32)[None], n, 0)
+                           for k, v in init.items()}
+            self._state0 = {k: np.asarray(v, np.float32) for k, v in init.items()}
         self.device = torch.device("cpu")
         if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
             self.device = torch.device("cuda", 0)
@@ -113,6 +124,9 @@ class SingleAgentEnvRunner:
         self.weights_version = -1
         self.total_steps = 0
         self.epsilon = 1.0
+        # SingleAgentEpisode recording (episode replay buffers / sample_episodes)
+        self._record = bool(config.get("_record_episodes"))
+        self._eps = None
 
     # ---------------------------------------------------------------- weights
     def set_weights(self, weights, version: int = 0):
@@ -143,10 +157,28 @@ class SingleAgentEnvRunner:
         return self.worker_index
 
     # ---------------------------------------------------------------- sampling
+    def sample_episodes(self, num_timesteps: int | None = None, explore: bool = True,
+                        epsilon: float | None = None):
+        """Sample and return the SingleAgentEpisode chunks of the rollout (finished
+        episodes, then the ongoing chunks, which continue in the next call; reference:
+        SingleAgentEnvRunner.sample returning episodes)."""
+        rec = self._record
+        self._record = True
+        try:
+            return self.sample(num_timesteps, explore, epsilon)["episodes"]
+        finally:
+            self._record = rec
+
     def sample(self, num_timesteps: int | None = None, explore: bool = True,
                epsilon: float | None = None, with_metrics: bool = False):
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
         B = len(self.envs)
+        if self._record and self._eps is None:
+            from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+
+            self._eps = [SingleAgentEpisode(observation_space=self.module_obs_space,
+                                            action_space=self.action_space) for _ in range(B)]
+        done_eps = []
         osh = self.observation_space.shape
         obs_buf = np.empty((T, B) + tuple(osh), dtype=self.observation_space.dtype) \
             if not self._pre else None  # connector output shape known after step 0
@@ -161,6 +193,10 @@ class SingleAgentEnvRunner:
         next_obs_buf = None
         if self.module_kind in ("q", "sac"):
             next_obs_buf = np.empty_like(obs_buf)
+        resets = None
+        if self._stateful:
+            state_in = {k: v.copy() for k, v in self._state.items()}
+            resets = np.zeros((T, B), np.float32)
         t0 = time.perf_counter()
         for t in range(T):
             rec, ob = self._module_obs(np.stack(self.obs), explore)
@@ -169,6 +205,10 @@ class SingleAgentEnvRunner:
                 if next_obs_buf is not None:
                     next_obs_buf = np.empty_like(obs_buf)
             obs_buf[t] = rec
+            if self._record:
+                for i in range(B):
+                    if not self._eps[i].observations:
+                        self._eps[i].add_env_reset(rec[i])
             with torch.no_grad():
                 x = torch.from_numpy(np.ascontiguousarray(ob)).to(self.device)
                 if self.module_kind == "q":
@@ -184,7 +224,14 @@ class SingleAgentEnvRunner:
                     a = at.float().cpu().numpy()
                     lp = lpt.float().cpu().numpy()
                 else:
-                    out = self.module.forward_inference(x)
+                    if self._stateful:
+                        st = {k: torch.from_numpy(v).to(self.device)
+                              for k, v in self._state.items()}
+                        out = self.module.forward_inference(x, state=st)
+                        self._state = {k: v.float().cpu().numpy()
+                                       for k, v in out["state_out"].items()}
+                    else:
+                        out = self.module.forward_inference(x)
                     di = out["action_dist_inputs"].float()
                     at, lpt = self.module.sample_actions(di, explore)
                     if dist_in is None:
@@ -224,6 +271,19 @@ class SingleAgentEnvRunner:
                 if next_obs_buf is not None:
                     next_obs_buf[t, i] = self._module_obs(o[None], explore, update=False)[0][0] \
                         if self._pre else o
+                if self._record:
+                    nxt = next_obs_buf[t, i] if next_obs_buf is not None else (
+                        self._module_obs(o[None], explore, update=False)[0][0] if self._pre
+                        else o)
+                    self._eps[i].add_env_step(np.array(nxt), a[i], r, terminated=bool(te),
+                                              truncated=bool(tr) and not te)
+                    if te or tr:
+                        from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+
+                        done_eps.append(self._eps[i])
+                        self._eps[i] = SingleAgentEpisode(
+                            observation_space=self.module_obs_space,
+                            action_space=self.action_space)
                 if te or tr:
                     term[t, i] = 1.0 if (te or not self.config.get("bootstrap_truncated")) \
                         else 0.0
@@ -237,6 +297,11 @@ class SingleAgentEnvRunner:
                     for k, v in ep.custom_metrics.items():
                         self.metrics.log_value(k, v)
                     o, _ = env.reset()
+                    if self._stateful:  # the next episode starts from the initial state
+                        for k, v in self._state0.items():
+                            self._state[k][i] = v
+                        if t + 1 < T:
+                            resets[t + 1, i] = 1.0
                     ep.reset(self._act_dummy, self._next_eid)
                     self._next_eid += 1
                     self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i,
@@ -253,6 +318,17 @@ class SingleAgentEnvRunner:
                  "weights_version": self.weights_version}
         if dist_in is not None:
             batch["action_dist_inputs"] = dist_in
+        if resets is not None:
+            for k, v in state_in.items():
+                batch[f"state_in_{k}"] = v
+            batch["resets"] = resets
+        if self._record:
+            ongoing = []
+            for i, e in enumerate(self._eps):
+                if len(e):
+                    ongoing.append(e)
+                    self._eps[i] = e.cut()
+            batch["episodes"] = done_eps + ongoing
         if next_obs_buf is not None:
             batch["next_obs"] = next_obs_buf
         if self.config.get("output"):

@@ -204,7 +204,45 @@ class RandomEnv(Env):
             bool(self.rng.random() < self.p_done), False, {}
 
 
+class RepeatAfterMeEnv(Env):
+    """Memory task (reference: rllib/examples/envs/classes/repeat_after_me_env.py): each
+    step shows one of ``n`` symbols (one-hot); the reward is +1 for repeating the symbol
+    shown ``delay`` steps earlier, -1 otherwise. A memoryless policy averages 0 per step;
+    a recurrent one can reach +1."""
+
+    def __init__(self, config=None):
+        cfg = config or {}
+        self.n = int(cfg.get("num_symbols", 2))
+        self.delay = int(cfg.get("repeat_delay", 1))
+        self.episode_len = int(cfg.get("episode_len", 20))
+        self.observation_space = spaces.Box(0.0, 1.0, (self.n,))
+        self.action_space = spaces.Discrete(self.n)
+        self.rng = np.random.default_rng(cfg.get("seed"))
+
+    def _obs(self):
+        o = np.zeros(self.n, np.float32)
+        o[self.hist[-1]] = 1.0
+        return o
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        self.hist = [int(self.rng.integers(self.n))]
+        return self._obs(), {}
+
+    def step(self, action):
+        self.t += 1
+        r = 0.0
+        if len(self.hist) > self.delay:  # the symbol shown `delay` steps before this one
+            r = 1.0 if int(action) == self.hist[-1 - self.delay] else -1.0
+        self.hist.append(int(self.rng.integers(self.n)))
+        self.hist = self.hist[-(self.delay + 1):]
+        return self._obs(), r, False, self.t >= self.episode_len, {}
+
+
 register_env("CartPole-v1", CartPoleEnv)
+register_env("RepeatAfterMeEnv", RepeatAfterMeEnv)
 register_env("CartPole-v0", lambda c: CartPoleEnv({"max_episode_steps": 200, **(c or {})}))
 register_env("Pendulum-v1", PendulumEnv)
 register_env("SyntheticAtari-v0", SyntheticAtariEnv)

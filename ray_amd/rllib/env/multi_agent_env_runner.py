@@ -56,7 +56,7 @@ class MultiAgentEnvRunner:
         self.mapping_fn = config.get("policy_mapping_fn") or _default_mapping
         self.specs = config["_module_specs"]
         self.module_kind = config.get("module_kind", "actor_critic")
-        self.modules = {mid: self._make_module(os_, as_).eval()
+        self.modules = {mid: self._make_module(os_, as_, mid).eval()
                         for mid, (os_, as_) in self.specs.items()}
         self.obs, self.alive, self.agent_module, self.pending = [], [], [], []
         self.ep_ret = np.zeros(n)
@@ -88,7 +88,7 @@ class MultiAgentEnvRunner:
         self.agent_module[i] = {}
         self.pending[i] = {}  # agent -> its last action awaiting its outcome
 
-    def _make_module(self, os_, as_):
+    def _make_module(self, os_, as_, mid=None):
         if self.module_kind == "q":  # multi-agent DQN: epsilon-greedy over Q-values
             from ray_amd.rllib.core.rl_module import QModule
 
@@ -100,7 +100,9 @@ class MultiAgentEnvRunner:
 
             return SquashedGaussianPolicy(os_, as_, self.config.get("policy_model_config")
                                           or self.config.get("model"))
-        return RLModule(os_, as_, self.config.get("model"))
+        from ray_amd.rllib.core.rl_module.rl_module import build_module
+
+        return build_module(self.config, os_, as_, mid)
 
     def _act(self, mod, x, explore, epsilon, as_):
         """(actions, logp, dist inputs) for a stacked observation batch."""
