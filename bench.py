@@ -61,6 +61,9 @@ def parse():
                     help="gpt2: 'always' runs FlatDDP's bucket hooks, per-bucket events, comm "
                          "stream and RCCL all-reduce launches even at world size 1 (measures "
                          "the overlap machinery's cost on one GPU)")
+    ap.add_argument("--step-graph", default="on", choices=["on", "off"],
+                    help="gpt2: capture the whole training step as a HIP graph after warmup "
+                         "(world-1 groups; multi-rank steps stay eager with overlapped RCCL)")
     ap.add_argument("--model", default="small")
     ap.add_argument("--data-path", default="hbm", choices=["hbm", "h2d"],
                     help="data workload: GPU-preprocessed device blocks through the HBM "
@@ -78,7 +81,8 @@ def _gpt2_config(args) -> dict:
     return dict(model=args.model, micro_batch=args.micro_batch, seq_len=args.seq_len,
                 steps=args.steps, warmup=args.warmup, grad_accum=args.grad_accum,
                 bucket_mb=args.bucket_mb, grad_dtype=args.grad_dtype, tunableop=args.tunableop,
-                lm_head_chunk=args.lm_head_chunk, device=args.device, ddp_hooks=args.ddp_hooks)
+                lm_head_chunk=args.lm_head_chunk, device=args.device, ddp_hooks=args.ddp_hooks,
+                step_graph=args.step_graph == "on")
 
 
 def _emit(args, r: dict, mode: str, n_gpus: int):
@@ -110,6 +114,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
             "lm_head_chunk": args.lm_head_chunk,
             "launcher": mode,
             "ddp_hooks": r.get("ddp_hooks"),
+            "step_graph": r.get("step_graph"),
         },
         "rccl_world_size": r["rccl_world_size"],
         "dist_backend": r["dist_backend"],

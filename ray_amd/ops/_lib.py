@@ -47,6 +47,8 @@ _SIGS = {
                      c_void_p],
     "ra_adamw_flat": [c_void_p] * 5 + [c_long, c_long] + [c_float] * 5 + [c_int, c_void_p,
                                                                             c_int, c_void_p],
+    "ra_adamw_flat_dev": [c_void_p] * 5 + [c_long, c_long] + [c_float] * 5 +
+    [c_int, c_void_p, c_int, c_void_p, c_void_p],
     "ra_set_knob": [c_int, c_int],
     "ra_scaled_accum": [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p],
     "ra_scale_bf16": [c_void_p, c_long, c_void_p, c_void_p],

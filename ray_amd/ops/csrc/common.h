@@ -152,8 +152,9 @@ __global__ __launch_bounds__(256) void colsum_atomic(const float* __restrict__ p
 
 // Runtime tuning knobs (A/B without rebuilding; set through ra_set_knob, defined in
 // layernorm.hip): 0 = LayerNorm-bwd partial rows cap, 1 = column-partial waves target,
-// 2 = fp32 colsum via atomics (1) or two-stage (0).
-extern int ra_knobs[8];
+// 2 = fp32 colsum via atomics (1) or two-stage (0), 9 = attention forward variant
+// (0 = attn_fwd_kernel, 1 = attn_fwd_kernel2).
+extern int ra_knobs[16];
 
 namespace {
 

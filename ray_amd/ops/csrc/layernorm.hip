@@ -405,10 +405,10 @@ RA_EXPORT int ra_residual_layernorm_fwd(const void* h, const void* rbias, const 
   return hipGetLastError();
 }
 
-int ra_knobs[8] = {512, 8192, 1, 0, 0, 0, 0, 0};
+int ra_knobs[16] = {512, 8192, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 RA_EXPORT int ra_set_knob(int k, int v) {
-  if (k < 0 || k >= 8) return hipErrorInvalidValue;
+  if (k < 0 || k >= 16) return hipErrorInvalidValue;
   ra_knobs[k] = v;
   return hipSuccess;
 }

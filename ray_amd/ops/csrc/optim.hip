@@ -52,8 +52,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p32,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     long n4, long nd4, float lr, float b1,
                                                     float b2, float eps, float wd, float rbc1,
-                                                    float rbc2, const float* __restrict__ gscale) {
+                                                    float rbc2, const float* __restrict__ gscale,
+                                                    const float* __restrict__ hyper) {
   const float sc = gscale ? *gscale : 1.f;
+  if (hyper) {  // graph-replayed step: {lr, 1/(1-b1^t), 1/(1-b2^t)} from device memory
+    lr = hyper[0];
+    rbc1 = hyper[1];
+    rbc2 = hyper[2];
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float gv[4];
@@ -171,16 +177,32 @@ RA_EXPORT int ra_grad_clip(const void* g, long n, int is_bf16, float max_norm, f
 }
 
 // flags: bit0 g is fp32 (else bf16), bit1 zero g after use. p16 may be null.
+// hyper (nullable): device {lr, 1/(1-b1^t), 1/(1-b2^t)} read by the kernel instead of the
+// lr / step arguments — a captured (HIP-graph) optimizer step whose schedule advances
+// between replays without re-capture
+RA_EXPORT int ra_adamw_flat_dev(float* p32, void* p16, void* g, float* m, float* v, long n,
+                                long n_decay, float lr, float b1, float b2, float eps, float wd,
+                                int step, const float* gscale, int flags, const float* hyper,
+                                hipStream_t st);
+
 RA_EXPORT int ra_adamw_flat(float* p32, void* p16, void* g, float* m, float* v, long n,
                             long n_decay, float lr, float b1, float b2, float eps, float wd,
                             int step, const float* gscale, int flags, hipStream_t st) {
+  return ra_adamw_flat_dev(p32, p16, g, m, v, n, n_decay, lr, b1, b2, eps, wd, step, gscale,
+                           flags, nullptr, st);
+}
+
+RA_EXPORT int ra_adamw_flat_dev(float* p32, void* p16, void* g, float* m, float* v, long n,
+                                long n_decay, float lr, float b1, float b2, float eps, float wd,
+                                int step, const float* gscale, int flags, const float* hyper,
+                                hipStream_t st) {
   if (n % 4 || n_decay % 4) return hipErrorInvalidValue;
   const float rbc1 = 1.f / (1.f - powf(b1, (float)step));
   const float rbc2 = 1.f / (1.f - powf(b2, (float)step));
   const dim3 grid(ra_grid(n / 4, 256)), blk(256);
 #define A(G, Z)                                                                              \
   hipLaunchKernelGGL((adamw_kernel<G, Z>), grid, blk, 0, st, p32, (bf16_t*)p16, (G*)g, m, v, \
-                     n / 4, n_decay / 4, lr, b1, b2, eps, wd, rbc1, rbc2, gscale)
+                     n / 4, n_decay / 4, lr, b1, b2, eps, wd, rbc1, rbc2, gscale, hyper)
   switch (flags & 3) {
     case 0: A(bf16_t, false); break;
     case 1: A(float, false); break;

@@ -293,6 +293,30 @@ class FlatAdamW:
         self.use_hip = flat.p32.is_cuda
         # clear the gradient inside the AdamW pass (the caller then skips zero_grad)
         self.zero_grad = zero_grad
+        # graph-captured steps: {lr, 1/(1-b1^t), 1/(1-b2^t)} live in device memory and are
+        # refreshed before every replay (set_device_hyper)
+        self.hyper = None
+        self._hyper_ring = None
+
+    def use_device_hyper(self):
+        """Switch to device-resident lr / bias corrections (HIP-graph capture of step())."""
+        dev = self.flat.device
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=dev)
+        # pinned staging slots, each reusable once its async copy has run
+        self._hyper_ring = [(torch.zeros(4, dtype=torch.float32, pin_memory=True),
+                             torch.cuda.Event()) for _ in range(8)]
+        self._ring_i = 0
+
+    def set_device_hyper(self, lr: float, step: int):
+        """Enqueue (on the current stream) the hyper-parameters of optimizer step ``step``."""
+        host, ev = self._hyper_ring[self._ring_i % len(self._hyper_ring)]
+        self._ring_i += 1
+        ev.synchronize()  # the copy that last read this slot has executed
+        host[0] = lr
+        host[1] = 1.0 / (1.0 - self.b1 ** step)
+        host[2] = 1.0 / (1.0 - self.b2 ** step)
+        self.hyper.copy_(host, non_blocking=True)
+        ev.record()
 
     def step(self, lr: float | None = None):
         if self.use_hip:
@@ -316,10 +340,12 @@ class FlatAdamW:
             else:
                 gptr = None
             g32 = f.g.dtype == torch.float32
-            check(L.ra_adamw_flat(ptr(f.p32), ptr(f.p16) if f.p16 is not f.p32 else None,
-                                  ptr(f.g), ptr(self.m), ptr(self.v), f.numel, f.n_decay, lr,
-                                  self.b1, self.b2, self.eps, self.wd, self.step_count, gptr,
-                                  (1 if g32 else 0) | (2 if self.zero_grad else 0), s), "adamw")
+            check(L.ra_adamw_flat_dev(ptr(f.p32), ptr(f.p16) if f.p16 is not f.p32 else None,
+                                      ptr(f.g), ptr(self.m), ptr(self.v), f.numel, f.n_decay,
+                                      lr, self.b1, self.b2, self.eps, self.wd, self.step_count,
+                                      gptr, (1 if g32 else 0) | (2 if self.zero_grad else 0),
+                                      ptr(self.hyper) if self.hyper is not None else None, s),
+                  "adamw")
             return
         # CPU reference path (same math)
         g = f.g.float() * self.grad_scale

@@ -140,6 +140,11 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
             if rank == 0:
                 print(f"[gpt2] hipBLASLt fp32-out choices -> {lt.save()}", file=sys.stderr)
             lt.set_tuning(False)
+    graphed = False
+    if on_gpu and c.get("step_graph", True) and \
+            os.environ.get("RAY_AMD_STEP_GRAPH", "1") != "0":
+        graphed = tr.enable_graph(batches(c["warmup"]))
+        sync()
     if world > 1:
         dist.barrier()
     sync()
@@ -185,6 +190,7 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         "global_batch": c["micro_batch"] * c["grad_accum"] * world,
         "ddp_hooks": "on" if tr.ddp.enabled else "off",
         "ddp_allreduce_launches": tr.ddp.launched,
+        "step_graph": graphed,
     }
 
 

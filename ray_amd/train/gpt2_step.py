@@ -53,8 +53,71 @@ class GPT2Trainer:
                           generator=gen)
         return x[:, :-1].contiguous(), x[:, 1:].contiguous()
 
+    # ------------------------------------------------------------------ HIP graph
+    def enable_graph(self, batches, warm: int = 2):
+        """Capture one whole training step — forward, backward (both compute streams),
+        DDP finish, clip and AdamW — as a HIP graph and replay it from then on: the step
+        costs one host launch instead of ~1.3k, so the GPU never waits for the Python
+        launch path (the eager step had ~2.2 ms of idle launch gaps; profiles/r4).
+        lr / Adam bias corrections move to device memory (FlatAdamW.use_device_hyper).
+        ``warm`` eager steps run first on the capture stream (per-stream GEMM workspaces,
+        kernel choices); they are real training steps. World-1 groups only: a multi-rank
+        step keeps the eager path with its overlapped RCCL buckets."""
+        if self.device.type != "cuda" or self.ddp.enabled:
+            return False
+        self._static = [(x.clone(), y.clone()) for x, y in batches]
+        self.opt.use_device_hyper()
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            for _ in range(warm):
+                self._eager_step(self._static)
+        cur.wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._graph_loss = self._body(self._static)
+        self.opt.step_count -= 1  # capture ran opt.step() on the host, no step happened
+        self._graph = g
+        return True
+
+    def _body(self, batches):
+        """The captured work: identical to an eager step minus the host bookkeeping."""
+        loss_sum = None
+        for i, (x, y) in enumerate(batches):
+            self.ddp.sync = i == len(batches) - 1
+            loss = self.model(x, y)
+            loss.backward()
+            loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        self.ddp.finish()
+        self.opt.step()
+        return loss_sum / len(batches)
+
+    def _eager_step(self, batches):
+        lr = cosine_lr(self.step_idx, self.base_lr, self.warmup, self.total_steps)
+        if self.opt.hyper is not None:
+            self.opt.set_device_hyper(lr, self.opt.step_count + 1)
+        self.opt.lr = lr
+        self.last_loss = self._body(batches)
+        self.step_idx += 1
+        return self.last_loss
+
     def step(self, batches):
         """batches: list of (idx, targets), len == grad_accum."""
+        g = getattr(self, "_graph", None)
+        if g is not None:
+            for (sx, sy), (x, y) in zip(self._static, batches):
+                if sx.data_ptr() != x.data_ptr():
+                    sx.copy_(x, non_blocking=True)
+                    sy.copy_(y, non_blocking=True)
+            lr = cosine_lr(self.step_idx, self.base_lr, self.warmup, self.total_steps)
+            self.opt.step_count += 1
+            self.opt.set_device_hyper(lr, self.opt.step_count)
+            g.replay()
+            self.step_idx += 1
+            self.last_loss = self._graph_loss
+            return self.last_loss
         # the flat gradient was zeroed by the previous AdamW pass (or at creation)
         loss_sum = None
         for i, (x, y) in enumerate(batches):

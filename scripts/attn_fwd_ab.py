@@ -1,0 +1,91 @@
+"""A/B of the attention forward variants (ra_knobs[9]: 0 = attn_fwd_kernel, 1 =
+attn_fwd_kernel2) at the GPT-2 training shape, interleaved in one process, plus a
+correctness check of each variant against an fp32 PyTorch reference (random data and a
+spiked-key input that forces the lazy-rescale branch). Prints one JSON line.
+
+    python scripts/attn_fwd_ab.py [--B 64] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from ray_amd.ops import _lib  # noqa: E402
+from ray_amd.ops._lib import ptr, stream_ptr  # noqa: E402
+
+
+def ref_attn(qkv, scale):
+    q, k, v = qkv.float().unbind(2)  # [B, T, H, D]
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = q @ k.transpose(-1, -2) * scale
+    T = s.shape[-1]
+    s = s.masked_fill(torch.triu(torch.ones(T, T, dtype=torch.bool, device=s.device), 1),
+                      float("-inf"))
+    lse2 = torch.logsumexp(s, -1) / 0.6931471805599453  # log2 units
+    return (torch.softmax(s, -1) @ v).transpose(1, 2), lse2
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    L = _lib.lib()
+    D = 64
+    sc = D ** -0.5
+    res = {"variants": {}}
+    # correctness (small batch, fp32 reference)
+    for name, spike in (("random", False), ("spiked", True)):
+        torch.manual_seed(1)
+        qkv = torch.randn(2, a.T, 3, a.H, D, device="cuda").bfloat16()
+        if spike:  # one key row far above the rest: the running max jumps mid-sequence
+            qkv[:, 700, 1] *= 40.0
+            qkv[:, 5, 1] *= -40.0
+        ro, rl = ref_attn(qkv, sc)
+        for var in (0, 1):
+            L.ra_set_knob(9, var)
+            out = torch.empty(2, a.T, a.H, D, device="cuda", dtype=torch.bfloat16)
+            lse = torch.empty(2, a.H, a.T, device="cuda")
+            L.ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), 2, a.T, a.H, D, sc, stream_ptr())
+            torch.cuda.synchronize()
+            err = (out.float() - ro).abs().max().item()
+            lerr = (lse - rl).abs().max().item()
+            res["variants"].setdefault(str(var), {})[f"max_err_{name}"] = round(err, 5)
+            res["variants"][str(var)][f"lse_err_{name}"] = round(lerr, 5)
+    # timing, interleaved
+    torch.manual_seed(0)
+    B = a.B
+    qkv = torch.randn(B, a.T, 3, a.H, D, device="cuda").bfloat16()
+    out = torch.empty(B, a.T, a.H, D, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B, a.H, a.T, device="cuda")
+    fl = 2 * 2 * B * a.H * a.T * a.T * D / 2
+    times = {0: [], 1: []}
+    for _ in range(a.rounds):
+        for var in (0, 1):
+            L.ra_set_knob(9, var)
+            L.ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), B, a.T, a.H, D, sc, stream_ptr())
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                L.ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), B, a.T, a.H, D, sc, stream_ptr())
+            e.record()
+            torch.cuda.synchronize()
+            times[var].append(s.elapsed_time(e) / a.iters)
+    for var in (0, 1):
+        t = sorted(times[var])
+        res["variants"][str(var)].update({"ms_median": round(t[len(t) // 2], 4),
+                                          "ms_min": round(t[0], 4),
+                                          "tflops_median": round(fl / t[len(t) // 2] / 1e9, 1)})
+    L.ra_set_knob(9, 0)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
