@@ -119,14 +119,35 @@ class Algorithm:
         opts = {"num_cpus": config.num_cpus_per_env_runner}
         if config.num_gpus_per_env_runner:
             opts["num_gpus"] = config.num_gpus_per_env_runner
+        self._runner_remote_cls, self._runner_opts = runner_cls, opts
+        from ray_amd.rllib.utils.actor_manager import FaultTolerantActorManager
+
+        # EnvRunners behind a FaultTolerantActorManager (reference: actor_manager.py:193,
+        # AlgorithmConfig.fault_tolerance): a dead runner is recreated with the same
+        # worker index and the current weights, or dropped (ignore_env_runner_failures)
+        self._runners = FaultTolerantActorManager(restore_fn=self._restore_runner)
+        self._last_weights_ref = None
         if nr > 0:
-            self.env_runners = [runner_cls.options(**opts).remote(self.cfg, i + 1)
-                                for i in range(nr)]
-            ray.get([r.ping.remote() for r in self.env_runners])
+            rs = [runner_cls.options(**opts).remote(self.cfg, i + 1) for i in range(nr)]
+            ray.get([r.ping.remote() for r in rs])
+            self._runners.add_actors(rs)
             self.local_runner = None
         else:
-            self.env_runners = []
             self.local_runner = local_cls(self.cfg, 0)
+        # evaluation EnvRunners (evaluation_num_env_runners): exploration off, the
+        # evaluation_config overrides, run beside training (evaluation_parallel_to_training)
+        self._eval_runners = []
+        self._eval_local = None
+        self._eval_pending = None
+        ne = int(getattr(config, "evaluation_num_env_runners", 0) or 0)
+        if ne > 0:
+            ecfg = dict(self.cfg)
+            ecfg.update(dict(getattr(config, "evaluation_config", None) or {}))
+            ecfg["_record_episodes"] = False
+            self._eval_cfg = ecfg
+            self._eval_runners = [runner_cls.options(**opts).remote(ecfg, 1000 + i)
+                                  for i in range(ne)]
+            ray.get([r.ping.remote() for r in self._eval_runners])
         self.setup()
         self.callbacks.on_algorithm_init(algorithm=self, metrics_logger=self.metrics)
 
@@ -162,12 +183,79 @@ class Algorithm:
     def setup(self):
         pass
 
+    # ---------------------------------------------------------------- env runner group
+    @property
+    def env_runners(self):
+        """The healthy EnvRunner actors."""
+        return self._runners.actors()
+
+    @env_runners.setter
+    def env_runners(self, runners):
+        from ray_amd.rllib.utils.actor_manager import FaultTolerantActorManager
+
+        self._runners = FaultTolerantActorManager(restore_fn=self._restore_runner)
+        self._runners.add_actors(list(runners or []))
+
+    def _restore_runner(self, actor_id):
+        cfg = self.config
+        if self._runners.num_restarts >= cfg.max_num_env_runner_restarts:
+            return None
+        if cfg.delay_between_env_runner_restarts_s:
+            time.sleep(cfg.delay_between_env_runner_restarts_s)
+        r = self._runner_remote_cls.options(**self._runner_opts).remote(self.cfg, actor_id)
+        ray.get(r.ping.remote())
+        w = self._last_weights_ref
+        if w is None:
+            w = ray.put(self._weights_for_runners())
+        ray.get(r.set_weights.remote(w, self.weights_version))
+        return r
+
+    def _weights_for_runners(self):
+        return self.learner_group.get_weights()
+
+    def _foreach_runner(self, fn):
+        """fn(runner) -> ObjectRef on every healthy EnvRunner; results of the ones that
+        answered. Dead runners are handled per AlgorithmConfig.fault_tolerance."""
+        res = self._runners.foreach_actor(fn)
+        bad = [r for r in res if not r.ok]
+        if bad:
+            self._on_runner_failures(bad)
+        return [r.value for r in res if r.ok]
+
+    def _on_runner_failures(self, bad):
+        from ray_amd.rllib.utils.actor_manager import _is_actor_failure
+
+        app = [r for r in bad if not _is_actor_failure(r.value)]
+        if app:  # an exception inside the runner (env / user code): not a lost actor
+            raise app[0].value
+        cfg = self.config
+        if cfg.restart_failed_env_runners:
+            self.restore_env_runners()
+        elif not cfg.ignore_env_runner_failures:
+            raise bad[0].value
+        if self._runners.num_healthy_actors() == 0:
+            raise RuntimeError("no healthy EnvRunner left (all failed; restart disabled or "
+                               "max_num_env_runner_restarts reached)")
+
+    def restore_env_runners(self):
+        """Probe unhealthy EnvRunners; recreate dead ones (reference:
+        Algorithm.restore_env_runners / EnvRunnerGroup.probe_unhealthy_env_runners)."""
+        restored = self._runners.probe_unhealthy_actors(
+            self.config.env_runner_health_probe_timeout_s,
+            restore=self.config.restart_failed_env_runners)
+        return restored
+
+    @property
+    def num_env_runner_restarts(self):
+        return self._runners.num_restarts
+
     # ---------------------------------------------------------------- weights
     def _sync_weights(self, weights):
         self.weights_version += 1
-        if self.env_runners:
+        if self._runners.num_actors():
             ref = ray.put(weights)
-            ray.get([r.set_weights.remote(ref, self.weights_version) for r in self.env_runners])
+            self._last_weights_ref = ref
+            self._foreach_runner(lambda r: r.set_weights.remote(ref, self.weights_version))
         else:
             self.local_runner.set_weights(weights, self.weights_version)
 
@@ -180,8 +268,8 @@ class Algorithm:
     def _collect_metrics(self):
         if getattr(self, "_metrics_from_samples", False) and self.env_runners:
             ms, self._async_ms = self.__dict__.get("_async_ms", []), []
-        elif self.env_runners:
-            ms = ray.get([r.get_metrics.remote() for r in self.env_runners])
+        elif self._runners.num_actors():
+            ms = self._foreach_runner(lambda r: r.get_metrics.remote())
         else:
             ms = [self.local_runner.get_metrics()]
         cm = {}
@@ -202,6 +290,16 @@ class Algorithm:
     def train(self) -> dict:
         t0 = time.time()
         steps0 = self.total_env_steps
+        if self.config.restart_failed_env_runners and self._runners.num_actors() and \
+                self._runners.num_healthy_actors() < self._runners.num_actors():
+            self.restore_env_runners()
+        do_eval = bool(self.config.evaluation_interval) and \
+            (self.iteration + 1) % self.config.evaluation_interval == 0
+        parallel_eval = do_eval and self._eval_runners and \
+            getattr(self.config, "evaluation_parallel_to_training", False)
+        if parallel_eval:
+            self.callbacks.on_evaluate_start(algorithm=self, metrics_logger=self.metrics)
+            self._eval_pending = self._start_eval()
         res = self.training_step()
         mt = self.config.min_time_s_per_iteration
         while mt and time.time() - t0 < mt:
@@ -240,12 +338,17 @@ class Algorithm:
         if self._custom_metrics:
             out["env_runners"]["custom_metrics"] = dict(self._custom_metrics)
             out["custom_metrics"] = dict(self._custom_metrics)
-        if self.config.evaluation_interval and self.iteration % self.config.evaluation_interval \
-                == 0:
-            self.callbacks.on_evaluate_start(algorithm=self, metrics_logger=self.metrics)
-            out["evaluation"] = self.evaluate()
+        if do_eval:
+            if parallel_eval:
+                out["evaluation"] = self._finish_eval(self._eval_pending)
+                self._eval_pending = None
+            else:
+                self.callbacks.on_evaluate_start(algorithm=self, metrics_logger=self.metrics)
+                out["evaluation"] = self.evaluate()
             self.callbacks.on_evaluate_end(algorithm=self, evaluation_metrics=out["evaluation"],
                                            metrics_logger=self.metrics)
+        out["num_healthy_env_runners"] = self._runners.num_healthy_actors()
+        out["num_env_runner_restarts"] = self._runners.num_restarts
         self.callbacks.on_train_result(algorithm=self, result=out, metrics_logger=self.metrics)
         extra = self.metrics.reduce_all()
         if extra:
@@ -263,8 +366,8 @@ class Algorithm:
         batches = []
         got = 0
         while got < total:
-            if self.env_runners:
-                bs = ray.get([r.sample.remote(per) for r in self.env_runners])
+            if self._runners.num_actors():
+                bs = self._foreach_runner(lambda r: r.sample.remote(per))
             else:
                 bs = [self.local_runner.sample(per)]
             for b in bs:
@@ -274,14 +377,72 @@ class Algorithm:
         return batches
 
     def evaluate(self) -> dict:
-        runner = self._runner_cls(self.cfg, 999)
-        runner.set_weights(self.get_weights(), None)
-        n = self.config.evaluation_duration
-        rets = []
-        while len(rets) < n:
-            runner.sample(self.config.rollout_fragment_length, explore=False)
-            rets.extend(runner.get_metrics()["episode_returns"])
-        return {"env_runners": {"episode_return_mean": float(np.mean(rets[:n]))}}
+        """Evaluation rollouts (exploration off) over ``evaluation_duration`` episodes or
+        timesteps: on the evaluation EnvRunners in parallel when
+        ``evaluation_num_env_runners`` > 0, else on one local evaluation runner that is
+        built once and reused (reference: algorithm.py:642,908)."""
+        return self._finish_eval(self._start_eval())
+
+    def _start_eval(self):
+        w = self._weights_for_runners()
+        if self._eval_runners:
+            ref = ray.put(w)
+            for r in self._eval_runners:
+                r.set_weights.remote(ref, None)
+            return {"inflight": {r.sample.remote(self.config.rollout_fragment_length,
+                                                 explore=False, with_metrics=True): r
+                                 for r in self._eval_runners}}
+        if self._eval_local is None:
+            ecfg = dict(self.cfg)
+            ecfg.update(dict(getattr(self.config, "evaluation_config", None) or {}))
+            ecfg["_record_episodes"] = False
+            self._eval_local = self._runner_cls(ecfg, 999)
+        self._eval_local.set_weights(w, None)
+        return {"local": True}
+
+    def _finish_eval(self, st) -> dict:
+        n = int(self.config.evaluation_duration)
+        by_steps = getattr(self.config, "evaluation_duration_unit", "episodes") == "timesteps"
+        rets, lens, steps = [], [], 0
+
+        def done():
+            return steps >= n if by_steps else len(rets) >= n
+
+        frag = self.config.rollout_fragment_length
+        if st.get("local"):
+            while not done():
+                b = self._eval_local.sample(frag, explore=False)
+                steps += b["env_steps"]
+                m = self._eval_local.get_metrics()
+                rets.extend(m["episode_returns"])
+                lens.extend(m["episode_lengths"])
+        else:
+            inflight = st["inflight"]
+            while inflight:
+                ready, _ = ray.wait(list(inflight), num_returns=1)
+                r = inflight.pop(ready[0])
+                try:
+                    b = ray.get(ready[0])
+                except Exception:  # noqa: BLE001  (a dead evaluation runner: skip it)
+                    continue
+                steps += b["env_steps"]
+                m = b.get("_metrics") or {}
+                rets.extend(m.get("episode_returns", []))
+                lens.extend(m.get("episode_lengths", []))
+                if not done():
+                    inflight[r.sample.remote(frag, explore=False, with_metrics=True)] = r
+            if not done():  # every runner died: finish locally
+                return self._finish_eval(self._start_eval_local_fallback())
+        sel = rets if by_steps else rets[:n]
+        return {"env_runners": {
+            "episode_return_mean": float(np.mean(sel)) if sel else float("nan"),
+            "episode_len_mean": float(np.mean(lens[:len(sel)])) if sel else float("nan"),
+            "num_episodes": len(sel), "num_env_steps_sampled": steps},
+            "num_evaluation_env_runners": len(self._eval_runners)}
+
+    def _start_eval_local_fallback(self):
+        self._eval_runners = []
+        return self._start_eval()
 
     # ---------------------------------------------------------------- inference
     def _new_module(self, obs_space, act_space, module_id=None):
@@ -471,12 +632,13 @@ class Algorithm:
         return algo
 
     def stop(self):
-        for r in self.env_runners:
+        self._runners.clear()
+        for r in self._eval_runners:
             try:
                 ray.kill(r)
-            except Exception:
+            except Exception:  # noqa: BLE001
                 pass
-        self.env_runners = []
+        self._eval_runners = []
         self.learner_group.shutdown()
 
     def __del__(self):
@@ -539,7 +701,12 @@ class _EnvRunnerGroupView:
     foreach_worker = foreach_env_runner
 
     def num_healthy_remote_workers(self) -> int:
-        return len(self.algo.env_runners)
+        return self.algo._runners.num_healthy_actors()
+
+    def probe_unhealthy_env_runners(self):
+        return self.algo.restore_env_runners()
+
+    probe_unhealthy_workers = probe_unhealthy_env_runners
 
     num_healthy_remote_env_runners = num_healthy_remote_workers
     num_remote_workers = num_healthy_remote_workers

@@ -169,9 +169,9 @@ class DQN(Algorithm):
     def training_step(self):
         cfg = self.config
         eps = self._epsilon()
-        if self.env_runners:
-            bs = ray.get([r.sample.remote(cfg.rollout_fragment_length, True, eps)
-                          for r in self.env_runners])
+        if self._runners.num_actors():
+            bs = self._foreach_runner(lambda r: r.sample.remote(cfg.rollout_fragment_length,
+                                                                True, eps))
         else:
             bs = [self.local_runner.sample(cfg.rollout_fragment_length, True, eps)]
         for b in bs:

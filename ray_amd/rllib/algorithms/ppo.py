@@ -73,6 +73,31 @@ class PPO(Algorithm):
         per = self.config.rollout_fragment_length
         return [r.sample.remote(per, with_metrics=True) for r in self.env_runners]
 
+    def _get_round(self, pending):
+        """Results of one sampling round; a runner that died mid-round is handled per
+        fault_tolerance (its fragment is dropped)."""
+        out, dead = [], False
+        for ref in pending:
+            try:
+                out.append(ray.get(ref))
+            except Exception as e:  # noqa: BLE001
+                from ray_amd.rllib.utils.actor_manager import _is_actor_failure
+
+                if not _is_actor_failure(e):
+                    raise
+                dead = True
+        if dead:
+            for aid in self._runners.healthy_actor_ids():
+                try:
+                    ray.get(self._runners.get(aid).ping.remote(), timeout=5)
+                except Exception:  # noqa: BLE001
+                    self._runners.set_actor_state(aid, False)
+            from ray_amd.rllib.utils.actor_manager import CallResult
+            from ray_amd.exceptions import ActorDiedError
+
+            self._on_runner_failures([CallResult(0, False, ActorDiedError("EnvRunner died"))])
+        return out
+
     def _training_step_async(self) -> dict:
         """Overlapped sampling (``sample_async``): the runners already sample batch k+1
         while the learner updates on batch k; fresh weights are queued behind that
@@ -83,7 +108,7 @@ class PPO(Algorithm):
         pending = self.__dict__.pop("_pending_round", None) or self._launch_round()
         batches, got = [], 0
         while True:
-            for b in ray.get(pending):
+            for b in self._get_round(pending):
                 self._take_metrics(b)
                 got += b["env_steps"]
                 batches.append(b)
@@ -97,6 +122,7 @@ class PPO(Algorithm):
         t2 = time.perf_counter()
         self.weights_version += 1
         ref = ray.put(self.learner_group.get_weights())
+        self._last_weights_ref = ref
         for r in self.env_runners:  # applied right after the in-flight sample
             r.set_weights.remote(ref, self.weights_version)
         return dict(stats, sample_wait_s=t1 - t0, learn_time_s=t2 - t1,

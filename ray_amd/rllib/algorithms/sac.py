@@ -209,8 +209,8 @@ class SAC(Algorithm):
     def training_step(self):
         cfg = self.config
         frag = max(1, cfg.rollout_fragment_length)
-        if self.env_runners:
-            bs = ray.get([r.sample.remote(frag) for r in self.env_runners])
+        if self._runners.num_actors():
+            bs = self._foreach_runner(lambda r: r.sample.remote(frag))
         else:
             bs = [self.local_runner.sample(frag)]
         new = 0

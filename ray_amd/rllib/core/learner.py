@@ -837,6 +837,38 @@ class LearnerGroup:
                        for a, s in zip(self.actors, shards)])
         return res[0]
 
+    def update_from_refs(self, kind, refs, async_update=False):
+        """Remote learners pull their share of the sample batches straight from the object
+        store (ObjectRefs assigned round-robin, at least one per learner): the driver never
+        fetches frames (reference: impala.py:130,194 — batches go to the learners, not
+        through the algorithm). async_update: return the per-learner result refs instead
+        of waiting (collect with ``collect_async``)."""
+        import ray_amd as ray
+
+        n = len(self.actors)
+        if not self.remote or len(refs) < n:
+            batches = ray.get(list(refs))
+            return self.update(kind, batches)
+        shares = [refs[i::n] for i in range(n)]
+        out = [a.execute.remote(_learner_update_refs, kind, sh)
+               for a, sh in zip(self.actors, shares)]
+        if async_update:
+            return out
+        return ray.get(out)[0]
+
+    @staticmethod
+    def collect_async(pending, block=False):
+        """Stats of an async update when it finished (None while running)."""
+        import ray_amd as ray
+
+        if not pending:
+            return None
+        ready, _ = ray.wait(list(pending), num_returns=len(pending),
+                            timeout=None if block else 0)
+        if len(ready) < len(pending):
+            return None
+        return ray.get(list(pending))[0]
+
     def get_weights(self):
         if not self.remote:
             return self.local.get_weights()
@@ -882,6 +914,14 @@ def _make_learner(config, obs_space, act_space, rank, world, module_id=DEFAULT_M
 
 def _learner_update(kind, batches):
     b = concat_batches(batches) if isinstance(batches, list) else batches
+    return _LEARNER.update_ppo(b) if kind == "ppo" else _LEARNER.update_vtrace(b)
+
+
+def _learner_update_refs(kind, refs):
+    import ray_amd as ray
+
+    batches = ray.get(list(refs))  # this learner's fragments, zero-copy from the store
+    b = concat_batches(batches) if len(batches) > 1 else batches[0]
     return _LEARNER.update_ppo(b) if kind == "ppo" else _LEARNER.update_vtrace(b)
 
 

@@ -345,6 +345,15 @@ class SingleAgentEnvRunner:
             batch["_metrics"] = self.get_metrics()
         return batch
 
+    def sample_with_meta(self, num_timesteps: int | None = None, explore: bool = True):
+        """(batch, meta) as TWO objects (call with ``.options(num_returns=2)``): a driver
+        that only routes the batch to learner actors fetches the small meta (env steps,
+        episode metrics) and hands the batch's ObjectRef on untouched (IMPALA / APPO)."""
+        b = self.sample(num_timesteps, explore, with_metrics=True)
+        meta = {"env_steps": b["env_steps"], "_metrics": b.pop("_metrics"),
+                "weights_version": b.get("weights_version")}
+        return b, meta
+
     def _module_obs(self, ob, explore, update=True):
         """(observation to record, module input) for a batched env step: the env-to-module
         connectors run in order; learner-side ones (MeanStdFilter) only shape the module

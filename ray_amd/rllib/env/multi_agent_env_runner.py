@@ -167,6 +167,13 @@ class MultiAgentEnvRunner:
         row["truncateds"] = 1.0 if truncated else 0.0
         cols.setdefault((i, aid, row["module"]), []).append(row)
 
+    def sample_with_meta(self, num_timesteps: int | None = None, explore: bool = True):
+        """(batch, meta) as two objects (see SingleAgentEnvRunner.sample_with_meta)."""
+        b = self.sample(num_timesteps, explore, with_metrics=True)
+        meta = {"env_steps": b["env_steps"], "_metrics": b.pop("_metrics"),
+                "weights_version": b.get("weights_version")}
+        return b, meta
+
     def sample(self, num_timesteps: int | None = None, explore: bool = True,
                epsilon: float | None = None, with_metrics: bool = False):
         T = int(num_timesteps or self.config.get("rollout_fragment_length", 50))
