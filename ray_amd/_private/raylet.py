@@ -292,6 +292,17 @@ class Raylet:
         self.next_internal = -1
         self.start_time = time.time()
         self.gpu_arenas = {}
+        # GCS durability (reference: gcs_server + gcs_table_storage on an external store):
+        # with RAY_AMD_GCS_STORAGE_PATH set, the head persists KV, jobs, detached actors and
+        # detached placement groups to <path>/gcs_snapshot.pkl and a restarted head reloads
+        # them (detached actors are re-created, counting one restart)
+        self._gcs_path = os.environ.get("RAY_AMD_GCS_STORAGE_PATH") if args.head else None
+        self._gcs_dirty = False
+        self._gcs_saved = 0.0
+        self.gcs_restored = None
+        if self._gcs_path:
+            os.makedirs(self._gcs_path, exist_ok=True)
+            self._gcs_restore()
         # memory monitor + worker killing policy (reference: memory_monitor.cc,
         # worker_killing_policy.cc; config names follow RAY_memory_usage_threshold etc.)
         env = os.environ
@@ -382,6 +393,7 @@ class Raylet:
             w.state = "driver"
             w.job = job_id
             w.namespace = namespace or f"anon-{job_id}"
+            self._gcs_dirty = True
             self.jobs[job_id] = {"job_id": job_id, "driver_pid": pid, "driver_addr": addr,
                                  "start_time": time.time(), "end_time": None,
                                  "status": "RUNNING", "namespace": w.namespace,
@@ -828,6 +840,7 @@ class Raylet:
         if j:
             j["status"] = "SUCCEEDED"
             j["end_time"] = time.time()
+            self._gcs_dirty = True
         # leases held by the driver: kill those workers (they may run its tasks)
         for lid, lease in list(self.leases.items()):
             if lease.owner == w.addr:
@@ -891,8 +904,81 @@ class Raylet:
         "oom:noretry:<message>")."""
         self.reply(conn, rid, True, self.death_causes.get(addr))
 
+    # ------------------------------------------------------------------ GCS durability
+    def _gcs_file(self):
+        return os.path.join(self._gcs_path, "gcs_snapshot.pkl")
+
+    def _gcs_snapshot(self):
+        actors = [{"info": a.info, "spec": a.spec, "restarts": a.restarts}
+                  for a in self.actors.values()
+                  if a.info.get("lifetime") == "detached" and a.state != P.DEAD]
+        pgs = [{"pg_id": pg.pg_id, "bundles": pg.bundles, "strategy": pg.strategy,
+                "name": pg.name, "lifetime": pg.lifetime, "namespace": pg.namespace}
+               for pg in self.pgs.values()
+               if pg.lifetime == "detached" and pg.state != "REMOVED"]
+        return {"version": 1, "kv": dict(self.kv), "jobs": dict(self.jobs),
+                "job_counter": self.job_counter, "actors": actors, "pgs": pgs,
+                "saved_at": time.time()}
+
+    def _gcs_save(self):
+        import pickle
+
+        tmp = self._gcs_file() + f".tmp{os.getpid()}"
+        try:
+            with open(tmp, "wb") as f:
+                pickle.dump(self._gcs_snapshot(), f, protocol=5)
+            os.replace(tmp, self._gcs_file())
+        except Exception:  # noqa: BLE001
+            traceback.print_exc()
+        self._gcs_dirty = False
+        self._gcs_saved = time.monotonic()
+
+    def _gcs_restore(self):
+        import pickle
+
+        path = self._gcs_file()
+        if not os.path.exists(path):
+            return
+        with open(path, "rb") as f:  # written by _gcs_save of an earlier head (our own file)
+            st = pickle.load(f)
+        self.kv.update(st.get("kv") or {})
+        now = time.time()
+        for jid, j in (st.get("jobs") or {}).items():
+            j = dict(j)
+            if j.get("status") == "RUNNING":  # its driver died with the previous head
+                j["status"] = "FAILED"
+                j["end_time"] = j.get("end_time") or now
+                j["message"] = "the head node restarted"
+            self.jobs[jid] = j
+        self.job_counter = max([self.job_counter, int(st.get("job_counter") or 0)] +
+                               [int(k) for k in self.jobs])
+        for d in st.get("pgs") or []:
+            pg = PGRec(d["pg_id"], d["bundles"], d["strategy"], d["name"], d["lifetime"], None,
+                       d["namespace"])
+            self.pgs[pg.pg_id] = pg
+            if pg.name:
+                self.pg_names[(pg.namespace, pg.name)] = pg.pg_id
+        for d in st.get("actors") or []:
+            a = ActorRec(d["info"], d["spec"])
+            a.restarts = int(d.get("restarts") or 0) + 1
+            a.state = P.RESTARTING
+            self.actors[a.aid] = a
+            if a.info.get("name"):
+                self.named[(a.info.get("namespace"), a.info["name"])] = a.aid
+            self._schedule_actor(a)
+        self.gcs_restored = {"kv": len(st.get("kv") or {}), "jobs": len(st.get("jobs") or {}),
+                             "actors": len(st.get("actors") or []),
+                             "pgs": len(st.get("pgs") or [])}
+        self._gcs_dirty = True
+
+    def rpc_gcs_status(self, conn, rid):
+        self.reply(conn, rid, True, {"storage_path": self._gcs_path,
+                                     "restored": self.gcs_restored})
+
     def tick(self):
         now = time.monotonic()
+        if self._gcs_path and self._gcs_dirty and now - self._gcs_saved > 0.2:
+            self._gcs_save()
         self._memory_check(now)
         for pg in self.pgs.values():
             if pg.state == "PENDING":
@@ -918,6 +1004,7 @@ class Raylet:
 
     # ------------------------------------------------------------------ kv
     def rpc_kv_put(self, conn, rid, ns, key, value, overwrite=True):
+        self._gcs_dirty = True
         k = (ns, key)
         existed = k in self.kv
         if overwrite or not existed:
@@ -928,6 +1015,7 @@ class Raylet:
         self.reply(conn, rid, True, self.kv.get((ns, key)))
 
     def rpc_kv_del(self, conn, rid, ns, key, prefix=False):
+        self._gcs_dirty = True
         if prefix:
             ks = [k for k in self.kv if k[0] == ns and _startswith(k[1], key)]
             for k in ks:
@@ -966,6 +1054,7 @@ class Raylet:
         if name:
             self.named[(ns, name)] = a.aid
         self._schedule_actor(a)
+        self._gcs_dirty = True
         self.reply(conn, rid, True, None)
 
     def _schedule_actor(self, a):
@@ -1062,6 +1151,7 @@ class Raylet:
                              if not a.no_restart else "The actor was killed (ray.kill).")
 
     def _actor_dead(self, a, death):
+        self._gcs_dirty = True
         a.state = P.DEAD
         a.death = death
         a.end_time = time.time()
@@ -1146,6 +1236,7 @@ class Raylet:
             return
         pg = PGRec(pg_id, bundles, strategy, name, lifetime, owner, namespace)
         self.pgs[pg_id] = pg
+        self._gcs_dirty = True
         if name:
             self.pg_names[(namespace, name)] = pg_id
         self._try_place(pg)
@@ -1192,6 +1283,7 @@ class Raylet:
     def _remove_pg(self, pg):
         if pg.state == "REMOVED":
             return
+        self._gcs_dirty = True
         # kill workers leased inside the pg
         for lid, lease in list(self.leases.items()):
             if lease.pg == pg.pg_id:
@@ -1535,6 +1627,8 @@ class Raylet:
         self.stop = True
 
     def shutdown(self):
+        if self._gcs_path:
+            self._gcs_save()
         for w in list(self.workers.values()) + list(self.starting.values()):
             if w.mode != "driver":
                 self._kill_worker(w)
