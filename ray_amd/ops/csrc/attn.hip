@@ -834,11 +834,13 @@ RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, 
                           float scale, hipStream_t st) {
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
+  // v2 by default (profiles/r4/README.md: 0.198 vs 0.228 ms at B64 T1024 H12, and exact
+  // on the spiked-key input where v1's LSE is off); ra_knobs[9] = 1 selects v1
   if (ra_knobs[9] == 1)
-    hipLaunchKernelGGL(attn_fwd_kernel2, dim3(B * H * (T / 128)), dim3(256), 0, st,
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
                        (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
+    hipLaunchKernelGGL(attn_fwd_kernel2, dim3(B * H * (T / 128)), dim3(256), 0, st,
                        (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   return hipGetLastError();
 }

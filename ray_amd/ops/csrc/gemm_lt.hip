@@ -14,8 +14,9 @@
 #include <hipblaslt/hipblaslt.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 
-#include <map>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -46,6 +47,13 @@ std::mutex g_ws_mu;  // not g_mu: the GEMM entry points call this with g_mu held
 
 void* workspace(hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
+  // RAY_AMD_LT_SHARED_WS=1: one workspace for every stream. Diagnostic only — it recreates
+  // the failure described above for scripts/lmhead_hang_repro.py (mode lt2shared).
+  static const bool shared = [] {
+    const char* e = getenv("RAY_AMD_LT_SHARED_WS");
+    return e && e[0] == '1';
+  }();
+  if (shared) st = nullptr;
   auto it = g_ws_by_stream.find(st);
   if (it != g_ws_by_stream.end()) return it->second;
   void* w = nullptr;

@@ -511,10 +511,12 @@ _xent_streams: dict = {}
 # difference against putting the dW GEMMs on the wgrad side stream, profiles/r3/
 # lmhead_pipe.md). The side-stream-dW layout was REMOVED in round 4: it ran two torch
 # hipBLASLt GEMMs concurrently on two streams and hung the GPU on a ragged last chunk
-# (N = 12388, chunk 4096). Cause: both may be stream-K kernels, whose persistent grids
-# spin-wait on partial tiles of their own undispatched workgroups; two such grids can
-# hold every CU slot and deadlock each other (see ops/csrc/gemm_lt.hip, which also keeps
-# stream-K kernels out of every side-stream GEMM it runs).
+# (N = 12388, chunk 4096). Root cause (profiles/r4/README.md §2, three-arm repro in
+# scripts/lmhead_hang_repro.py): not stream-K concurrency as such — the same dW on the side
+# stream through ops/lt (stream-K kernel, one hipBLASLt workspace PER STREAM) drains beside
+# the same main-stream GEMMs — but torch's hipBLASLt call on the second stream, whose
+# stream-K fixup flags live in workspace state shared with the main stream's GEMMs. Side-
+# stream GEMMs therefore only ever go through ops/lt's per-stream workspaces.
 def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
     """Chunked LM head + CE, software-pipelined over two streams:
 

@@ -141,8 +141,9 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
                 print(f"[gpt2] hipBLASLt fp32-out choices -> {lt.save()}", file=sys.stderr)
             lt.set_tuning(False)
     graphed = False
-    if on_gpu and c.get("step_graph", True) and \
-            os.environ.get("RAY_AMD_STEP_GRAPH", "1") != "0":
+    # whole-step HIP graph: opt-in (step_graph=True or RAY_AMD_STEP_GRAPH=1); eager is
+    # faster on MI355X at this config (profiles/r4/README.md)
+    if on_gpu and (c.get("step_graph") or os.environ.get("RAY_AMD_STEP_GRAPH") == "1"):
         graphed = tr.enable_graph(batches(c["warmup"]))
         sync()
     if world > 1:

@@ -1,5 +1,5 @@
-"""A/B of the attention forward variants (ra_knobs[9]: 0 = attn_fwd_kernel, 1 =
-attn_fwd_kernel2) at the GPT-2 training shape, interleaved in one process, plus a
+"""A/B of the attention forward variants (ra_knobs[9]: 1 = attn_fwd_kernel (v1), 0 =
+attn_fwd_kernel2 (v2, the default)) at the GPT-2 training shape, interleaved in one process, plus a
 correctness check of each variant against an fp32 PyTorch reference (random data and a
 spiked-key input that forces the lazy-rescale branch). Prints one JSON line.
 
@@ -59,6 +59,11 @@ def main():
             lerr = (lse - rl).abs().max().item()
             res["variants"].setdefault(str(var), {})[f"max_err_{name}"] = round(err, 5)
             res["variants"][str(var)][f"lse_err_{name}"] = round(lerr, 5)
+            if spike:  # where the error sits: rows (token index) with the largest LSE error
+                e = (lse - rl).abs()
+                top = torch.topk(e.flatten(), 8).indices
+                res["variants"][str(var)]["worst_rows_bht"] = [
+                    [int(i // (a.H * a.T)), int(i // a.T % a.H), int(i % a.T)] for i in top]
     # timing, interleaved
     torch.manual_seed(0)
     B = a.B
@@ -83,7 +88,7 @@ def main():
         res["variants"][str(var)].update({"ms_median": round(t[len(t) // 2], 4),
                                           "ms_min": round(t[0], 4),
                                           "tflops_median": round(fl / t[len(t) // 2] / 1e9, 1)})
-    L.ra_set_knob(9, 0)
+    L.ra_set_knob(9, 0)  # back to the default (v2)
     print(json.dumps(res), flush=True)
 
 
