@@ -327,6 +327,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
 //    of very negative scores does not underflow);
 //  * the wave index is made wave-uniform (readfirstlane) so the causal-mask branches are
 //    scalar branches, not exec-masked regions.
+//  PF = register prefetch depth (2: tile t+2's loads in flight during tiles t and t+1; 1: one
+//  register set, tile t+1 loaded at the top of tile t and written to LDS after its compute);
+//  UW = wave index via readfirstlane (scalar branches; +~60 VGPRs measured).
+template <int PF, bool UW>
 __global__ __launch_bounds__(256) void attn_fwd_kernel2(const bf16_t* __restrict__ qkv,
                                                         bf16_t* __restrict__ out,
                                                         float* __restrict__ lse, int T, int H,
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel2(const bf16_t* __restrict
   const int C = H * HD;
   const long tok = 3L * C;
   const bf16_t* base = qkv + (long)b * T * tok + h * HD;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = UW ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const LaneOffs lo(lane);
   const int q0 = qb * 128;
@@ -360,7 +364,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel2(const bf16_t* __restrict
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmin = q0 + 32 * w;
   const int wave_qmax = wave_qmin + 31;
-  KV A, B;
+  KV A;
+  [[maybe_unused]] KV B;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2,
                                         0x00020000);
@@ -447,19 +452,31 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel2(const bf16_t* __restrict
       else body(t, std::false_type{});
     }
   };
-  auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
-    if (t + 2 < ntiles) load_kv(next, t + 2);
-    compute(t);
-    if (t + 1 < ntiles) store_kv(held, t + 1);
+  if constexpr (PF == 2) {
+    auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) load_kv(next, t + 2);
+      compute(t);
+      if (t + 1 < ntiles) store_kv(held, t + 1);
+      __syncthreads();
+    };
+    load_kv(A, 0);
+    store_kv(A, 0);
+    load_kv(A, 1);  // ntiles >= 2
     __syncthreads();
-  };
-  load_kv(A, 0);
-  store_kv(A, 0);
-  load_kv(A, 1);  // ntiles >= 2
-  __syncthreads();
-  for (int t = 0; t < ntiles; t += 2) {
-    step(t, A, B);
-    if (t + 1 < ntiles) step(t + 1, B, A);
+    for (int t = 0; t < ntiles; t += 2) {
+      step(t, A, B);
+      if (t + 1 < ntiles) step(t + 1, B, A);
+    }
+  } else {
+    load_kv(A, 0);
+    store_kv(A, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) load_kv(A, t + 1);  // lands during compute(t)
+      compute(t);
+      if (t + 1 < ntiles) store_kv(A, t + 1);  // the other buffer: read by tile t - 1
+      __syncthreads();
+    }
   }
   const float inv = 1.f / l_run;
   bf16_t* orow = out + ((long)b * T + qrow) * C + h * HD;
@@ -840,8 +857,16 @@ RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, 
     hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
                        (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel2, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                       (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
+  {
+    // ra_knobs[10]: v2 sub-variant (0: prefetch 2 + uniform wave index, 1: prefetch 1,
+    // 2: prefetch 1 + non-uniform wave index, 3: prefetch 2 + non-uniform)
+    auto k = attn_fwd_kernel2<2, true>;
+    if (ra_knobs[10] == 1) k = attn_fwd_kernel2<1, true>;
+    else if (ra_knobs[10] == 2) k = attn_fwd_kernel2<1, false>;
+    else if (ra_knobs[10] == 3) k = attn_fwd_kernel2<2, false>;
+    hipLaunchKernelGGL(k, dim3(B * H * (T / 128)), dim3(256), 0, st, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, T, H, sc_log2);
+  }
   return hipGetLastError();
 }
 

@@ -213,8 +213,231 @@ class AlgorithmConfig:
         return True
 
     def freeze(self):
-        self._is_frozen = True
+        """After this, setting any attribute raises (reference: AlgorithmConfig.freeze —
+        the Algorithm freezes its copy so a running algorithm's config cannot drift)."""
+        object.__setattr__(self, "_is_frozen", True)
         return self
+
+    def __setattr__(self, k, v):
+        if self.__dict__.get("_is_frozen", False):
+            raise AttributeError(f"Cannot set attribute ({k}) of an already frozen "
+                                 "AlgorithmConfig; use config.copy(copy_frozen=False)")
+        object.__setattr__(self, k, v)
+
+    # ---------------------------------------------------------------- dict-like access
+    def keys(self):
+        return self.to_dict().keys()
+
+    def values(self):
+        return self.to_dict().values()
+
+    def items(self):
+        return self.to_dict().items()
+
+    def pop(self, k, default=None):
+        if self.__dict__.get("_is_frozen", False):
+            raise AttributeError("Cannot pop from a frozen AlgorithmConfig")
+        return self.__dict__.pop(k, default)
+
+    # ---------------------------------------------------------------- derived settings
+    @property
+    def num_workers(self):  # old name of num_env_runners
+        return self.num_env_runners
+
+    @property
+    def uses_new_env_runners(self):
+        return True
+
+    @property
+    def is_atari(self) -> bool:
+        e = self.env if isinstance(self.env, str) else ""
+        return e.startswith("ALE/") or "NoFrameskip" in e
+
+    @property
+    def total_train_batch_size(self) -> int:
+        """train_batch_size_per_learner x max(1, num_learners) when set per learner, else
+        train_batch_size (reference: AlgorithmConfig.total_train_batch_size)."""
+        per = getattr(self, "train_batch_size_per_learner", None)
+        if per:
+            return int(per) * max(1, int(self.num_learners or 0))
+        return int(self.train_batch_size)
+
+    def get_rollout_fragment_length(self, worker_index: int = 0) -> int:
+        """'auto' = the train batch split evenly over all env-runner envs (worker_index
+        1..N gets one extra step while the split has a remainder)."""
+        if self.rollout_fragment_length != "auto":
+            return int(self.rollout_fragment_length)
+        nr = max(1, self.num_env_runners)
+        per_env = self.total_train_batch_size // (nr * self.num_envs_per_env_runner)
+        rem = self.total_train_batch_size - per_env * nr * self.num_envs_per_env_runner
+        extra = 1 if worker_index and rem and worker_index * self.num_envs_per_env_runner <= rem \
+            else 0
+        return max(1, per_env + extra)
+
+    def validate_train_batch_size_vs_rollout_fragment_length(self):
+        """The sampled fragments must be able to fill one train batch within 10 % (the
+        reference's tolerance); otherwise raise with the rollout_fragment_length to use."""
+        if self.rollout_fragment_length == "auto":
+            return
+        per_round = max(1, self.num_env_runners) * self.num_envs_per_env_runner * \
+            int(self.rollout_fragment_length)
+        tb = self.total_train_batch_size
+        if per_round > tb and per_round - tb > 0.1 * tb:
+            suggested = max(1, tb // (max(1, self.num_env_runners) *
+                                      self.num_envs_per_env_runner))
+            raise ValueError(
+                f"one sampling round ({per_round} env steps = num_env_runners x "
+                f"num_envs_per_env_runner x rollout_fragment_length) exceeds the train batch "
+                f"({tb}) by more than 10%; set rollout_fragment_length={suggested} or 'auto'")
+
+    @property
+    def multiagent(self) -> dict:
+        return {"policies": self.policies, "policy_mapping_fn": self.policy_mapping_fn,
+                "policies_to_train": self.policies_to_train}
+
+    def get_multi_agent_setup(self, *, env=None, spaces=None, default_policy_class=None):
+        """(policies dict id -> (obs_space, act_space), policy_mapping_fn). Module ids
+        given without spaces take the env's single-agent spaces."""
+        if self.policies is None:
+            from ray_amd.rllib.core.learner import DEFAULT_MODULE_ID
+
+            pol = {DEFAULT_MODULE_ID: None}
+        elif isinstance(self.policies, dict):
+            pol = dict(self.policies)
+        else:
+            pol = {pid: None for pid in self.policies}
+        if any(v is None for v in pol.values()):
+            obs, act = (spaces or (None, None))
+            if obs is None and (env is not None or self.env is not None):
+                from ray_amd.rllib.env.envs import make_env
+
+                e = env if env is not None else make_env(self.env, self.env_config)
+                obs, act = e.observation_space, e.action_space
+            pol = {k: (v if v is not None else (obs, act)) for k, v in pol.items()}
+        fn = self.policy_mapping_fn or (lambda agent_id, *a, **k: next(iter(pol)))
+        return pol, fn
+
+    def get_config_for_module(self, module_id):
+        """This config with the per-module overrides applied (reference:
+        AlgorithmConfig.get_config_for_module; overrides come from
+        ``algorithm_config_overrides_per_module={module_id: {key: value}}`` passed to
+        multi_agent())."""
+        ov = (getattr(self, "algorithm_config_overrides_per_module", None) or {}).get(module_id)
+        if not ov:
+            return self
+        c = self.copy(copy_frozen=False)
+        c.update_from_dict(dict(ov))
+        return c
+
+    def get_evaluation_config_object(self):
+        """A copy of this config with ``evaluation_config`` applied on top, evaluation of
+        the evaluation config disabled (what the evaluation EnvRunners are built from)."""
+        c = self.copy(copy_frozen=False)
+        c.update_from_dict(dict(self.evaluation_config or {}))
+        c.evaluation_interval = None
+        c.num_env_runners = self.evaluation_num_env_runners
+        if "explore" not in (self.evaluation_config or {}):
+            c.explore = False
+        return c
+
+    def get_default_rl_module_spec(self):
+        from ray_amd.rllib.core.rl_module import RLModuleSpec
+
+        return RLModuleSpec(model_config=dict(self.model or {}))
+
+    def get_marl_module_spec(self, *, env=None, spaces=None):
+        """MultiRLModuleSpec over get_multi_agent_setup's modules."""
+        from ray_amd.rllib.core.rl_module import MultiRLModuleSpec, RLModuleSpec
+
+        if isinstance(self._rl_module_spec, MultiRLModuleSpec):
+            return self._rl_module_spec
+        pol, _ = self.get_multi_agent_setup(env=env, spaces=spaces)
+        base = self._rl_module_spec
+        specs = {}
+        for mid, sp in pol.items():
+            obs, act = sp if isinstance(sp, tuple) else (None, None)
+            specs[mid] = RLModuleSpec(
+                module_class=getattr(base, "module_class", None), observation_space=obs,
+                action_space=act, model_config=dict(getattr(base, "model_config", None)
+                                                    or self.model or {}))
+        return MultiRLModuleSpec(rl_module_specs=specs)
+
+    def get_torch_compile_worker_config(self) -> dict:
+        """No torch.compile on this stack: the MI355X learner's hot path is hand-written HIP
+        kernels replayed as HIP graphs, so there is nothing to configure."""
+        return {"torch_compile": False}
+
+    # ---------------------------------------------------------------- builders of parts
+    def build_env_to_module_connector(self, env=None, spaces=None):
+        from ray_amd.rllib.connectors.connector_v2 import build_pipeline
+
+        obs, act = self._spaces(env, spaces)
+        return build_pipeline(self.env_to_module_connector, obs, act)
+
+    def build_module_to_env_connector(self, env=None, spaces=None):
+        from ray_amd.rllib.connectors.connector_v2 import build_pipeline
+
+        obs, act = self._spaces(env, spaces)
+        return build_pipeline(self.module_to_env_connector, obs, act)
+
+    def build_learner_connector(self, input_observation_space=None,
+                                input_action_space=None, device=None):
+        from ray_amd.rllib.connectors.connector_v2 import build_pipeline
+
+        return build_pipeline(self.learner_connector, input_observation_space,
+                              input_action_space)
+
+    def _spaces(self, env, spaces):
+        if spaces is not None:
+            return spaces
+        from ray_amd.rllib.env.envs import make_env
+
+        e = env if env is not None else make_env(self.env, self.env_config)
+        return e.observation_space, e.action_space
+
+    def build_learner_group(self, *, env=None, spaces=None):
+        """The LearnerGroup an Algorithm of this config trains with (num_learners remote
+        learner actors over RCCL/gloo, or one local learner)."""
+        from ray_amd.rllib.core.learner import LearnerGroup
+
+        obs, act = self._spaces(env, spaces)
+        cfg = self.to_dict()
+        cfg.setdefault("module_kind", "actor_critic")
+        return LearnerGroup(cfg, obs, act)
+
+    def build_learner(self, *, env=None, spaces=None, device=None):
+        """One local Learner (the configured learner_class, default per algorithm)."""
+        from ray_amd.rllib.core.learner import _learner_cls
+
+        obs, act = self._spaces(env, spaces)
+        cfg = self.to_dict()
+        cfg.setdefault("module_kind", "actor_critic")
+        return _learner_cls(cfg)(cfg, obs, act, device=device)
+
+    def serialize(self) -> dict:
+        """JSON-able dict: classes and callables as their qualified names."""
+        def conv(v):
+            if isinstance(v, (str, int, float, bool)) or v is None:
+                return v
+            if isinstance(v, dict):
+                return {str(k): conv(x) for k, x in v.items()}
+            if isinstance(v, (list, tuple, set)):
+                return [conv(x) for x in v]
+            if isinstance(v, type) or callable(v):
+                return f"{getattr(v, '__module__', '?')}.{getattr(v, '__qualname__', repr(v))}"
+            return repr(v)
+
+        return {k: conv(v) for k, v in self.to_dict().items() if k != "_is_frozen"}
+
+    @classmethod
+    def overrides(cls, **kwargs) -> dict:
+        """Validated per-module / evaluation override dict (reference:
+        AlgorithmConfig.overrides): unknown keys raise."""
+        proto = cls()
+        for k in kwargs:
+            if not hasattr(proto, cls._LEGACY_KEYS.get(k, k)):
+                raise KeyError(f"unknown AlgorithmConfig key in overrides: {k}")
+        return dict(kwargs)
 
     @classmethod
     def from_dict(cls, d: dict):
@@ -267,7 +490,7 @@ class AlgorithmConfig:
         return self
 
     def multi_agent(self, *, policies=None, policy_mapping_fn=None, policies_to_train=None,
-                    **kw):
+                    algorithm_config_overrides_per_module=None, **kw):
         """reference: AlgorithmConfig.multi_agent -- ``policies`` is a set/list of module ids
         or a dict id -> (observation_space, action_space) / PolicySpec / None."""
         if policies is not None:
@@ -276,6 +499,9 @@ class AlgorithmConfig:
             self.policy_mapping_fn = policy_mapping_fn
         if policies_to_train is not None:
             self.policies_to_train = list(policies_to_train)
+        if algorithm_config_overrides_per_module is not None:
+            self.algorithm_config_overrides_per_module = dict(
+                algorithm_config_overrides_per_module)
         return self
 
     @property
@@ -307,10 +533,13 @@ class AlgorithmConfig:
         return self
 
     def copy(self, copy_frozen=None):
-        return copy.deepcopy(self)
+        c = copy.deepcopy(self)
+        if not copy_frozen:  # None / False: the copy is writable (reference default)
+            c.__dict__.pop("_is_frozen", None)
+        return c
 
     def to_dict(self) -> dict:
-        return {k: v for k, v in self.__dict__.items() if k != "algo_class"}
+        return {k: v for k, v in self.__dict__.items() if k not in ("algo_class", "_is_frozen")}
 
     def get(self, k, default=None):
         return getattr(self, k, default)

@@ -1,5 +1,5 @@
-"""A/B of the attention forward variants (ra_knobs[9]: 1 = attn_fwd_kernel (v1), 0 =
-attn_fwd_kernel2 (v2, the default)) at the GPT-2 training shape, interleaved in one process, plus a
+"""A/B of the attention forward variants (VARIANTS below: ra_knobs[9] = 1 selects
+attn_fwd_kernel (v1), 0 the attn_fwd_kernel2 family with ra_knobs[10] picking its template) at the GPT-2 training shape, interleaved in one process, plus a
 correctness check of each variant against an fp32 PyTorch reference (random data and a
 spiked-key input that forces the lazy-rescale branch). Prints one JSON line.
 
@@ -16,6 +16,20 @@ import torch  # noqa: E402
 
 from ray_amd.ops import _lib  # noqa: E402
 from ray_amd.ops._lib import ptr, stream_ptr  # noqa: E402
+
+
+# name -> (ra_knobs[9], ra_knobs[10]); VGPRs from hipcc (-amdgpu-mfma-vgpr-form)
+VARIANTS = {"v1": (1, 0),        # 162 VGPR, 3 waves/SIMD
+            "v2": (0, 0),        # prefetch 2, uniform wave index: 246 VGPR, 2 waves
+            "v2_pf1": (0, 1),    # 234
+            "v2_pf1_nu": (0, 2),  # 168: 3 waves
+            "v2_nu": (0, 3)}     # 184
+
+
+def _set(L, var):
+    k9, k10 = VARIANTS[var]
+    L.ra_set_knob(9, k9)
+    L.ra_set_knob(10, k10)
 
 
 def ref_attn(qkv, scale):
@@ -49,8 +63,8 @@ def main():
             qkv[:, 700, 1] *= 40.0
             qkv[:, 5, 1] *= -40.0
         ro, rl = ref_attn(qkv, sc)
-        for var in (0, 1):
-            L.ra_set_knob(9, var)
+        for var in VARIANTS:
+            _set(L, var)
             out = torch.empty(2, a.T, a.H, D, device="cuda", dtype=torch.bfloat16)
             lse = torch.empty(2, a.H, a.T, device="cuda")
             L.ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), 2, a.T, a.H, D, sc, stream_ptr())
@@ -71,10 +85,10 @@ def main():
     out = torch.empty(B, a.T, a.H, D, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(B, a.H, a.T, device="cuda")
     fl = 2 * 2 * B * a.H * a.T * a.T * D / 2
-    times = {0: [], 1: []}
+    times = {v: [] for v in VARIANTS}
     for _ in range(a.rounds):
-        for var in (0, 1):
-            L.ra_set_knob(9, var)
+        for var in VARIANTS:
+            _set(L, var)
             L.ra_attn_fwd(ptr(qkv), ptr(out), ptr(lse), B, a.T, a.H, D, sc, stream_ptr())
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -83,12 +97,12 @@ def main():
             e.record()
             torch.cuda.synchronize()
             times[var].append(s.elapsed_time(e) / a.iters)
-    for var in (0, 1):
+    for var in VARIANTS:
         t = sorted(times[var])
         res["variants"][str(var)].update({"ms_median": round(t[len(t) // 2], 4),
                                           "ms_min": round(t[0], 4),
                                           "tflops_median": round(fl / t[len(t) // 2] / 1e9, 1)})
-    L.ra_set_knob(9, 0)  # back to the default (v2)
+    _set(L, "v2")  # back to the default
     print(json.dumps(res), flush=True)
 
 

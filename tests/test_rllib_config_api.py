@@ -1,0 +1,86 @@
+"""AlgorithmConfig API surface beyond the builders (reference:
+rllib/algorithms/algorithm_config.py — freeze, dict access, derived sizes, per-module and
+evaluation configs, MultiRLModuleSpec, part builders, serialize/overrides)."""
+import json
+
+import pytest
+
+from ray_amd.rllib.algorithms.ppo import PPOConfig
+from ray_amd.rllib.core.rl_module import MultiRLModuleSpec
+
+
+def test_freeze_blocks_writes_and_copy_unfreezes():
+    c = PPOConfig().environment("CartPole-v1").training(lr=1e-3)
+    c.freeze()
+    with pytest.raises(AttributeError):
+        c.lr = 0.1
+    with pytest.raises(AttributeError):
+        c.training(lr=0.2)
+    c2 = c.copy()
+    c2.lr = 0.3
+    assert c.lr == 1e-3 and c2.lr == 0.3
+    assert "_is_frozen" not in c.to_dict()
+
+
+def test_dict_access_and_derived_sizes():
+    c = (PPOConfig().environment("CartPole-v1")
+         .env_runners(num_env_runners=3, num_envs_per_env_runner=2,
+                      rollout_fragment_length="auto")
+         .training(train_batch_size=1000))
+    assert "lr" in c.keys() and dict(c.items())["train_batch_size"] == 1000
+    assert c.num_workers == 3 and c.uses_new_env_runners and not c.is_atari
+    assert c.total_train_batch_size == 1000
+    # 1000 steps over 6 envs: 166 per env with 4 left over -> runners 1, 2 take 167
+    assert c.get_rollout_fragment_length(0) == 166
+    assert c.get_rollout_fragment_length(1) == 167
+    assert c.get_rollout_fragment_length(3) == 166
+    c.training(train_batch_size_per_learner=256).learners(num_learners=2)
+    assert c.total_train_batch_size == 512
+    assert PPOConfig().environment("ALE/Pong-v5").is_atari
+
+
+def test_rollout_fragment_validation():
+    c = (PPOConfig().env_runners(num_env_runners=4, num_envs_per_env_runner=4,
+                                 rollout_fragment_length=200)
+         .training(train_batch_size=1000))
+    with pytest.raises(ValueError, match="rollout_fragment_length=62"):
+        c.validate_train_batch_size_vs_rollout_fragment_length()
+    c.env_runners(rollout_fragment_length=62)
+    c.validate_train_batch_size_vs_rollout_fragment_length()
+
+
+def test_multi_agent_setup_module_config_and_marl_spec():
+    c = (PPOConfig().environment("CartPole-v1")
+         .multi_agent(policies={"a", "b"}, policy_mapping_fn=lambda aid, *a, **k: "a",
+                      algorithm_config_overrides_per_module={"b": {"lr": 7e-4}}))
+    pol, fn = c.get_multi_agent_setup()
+    assert set(pol) == {"a", "b"} and pol["a"][0].shape == (4,) and fn(0) == "a"
+    assert c.get_config_for_module("b").lr == 7e-4
+    assert c.get_config_for_module("a") is c
+    spec = c.get_marl_module_spec()
+    assert isinstance(spec, MultiRLModuleSpec) and set(spec.rl_module_specs) == {"a", "b"}
+    assert c.multiagent["policies"] == {"a", "b"}
+
+
+def test_evaluation_config_object():
+    c = (PPOConfig().environment("CartPole-v1")
+         .evaluation(evaluation_interval=2, evaluation_num_env_runners=3,
+                     evaluation_config={"gamma": 0.5}))
+    e = c.get_evaluation_config_object()
+    assert e.gamma == 0.5 and e.num_env_runners == 3 and e.evaluation_interval is None
+    assert e.explore is False and c.gamma == 0.99
+
+
+def test_part_builders_serialize_overrides():
+    c = PPOConfig().environment("CartPole-v1").rl_module(model_config={"fcnet_hiddens": [16]})
+    pipe = c.build_env_to_module_connector()
+    assert pipe.observation_space.shape == (4,)
+    learner = c.build_learner()
+    assert sum(p.numel() for p in learner.module.parameters()) > 0
+    assert c.get_default_rl_module_spec().model_config == {"fcnet_hiddens": [16]}
+    js = json.dumps(c.serialize())
+    assert "CartPole-v1" in js
+    assert PPOConfig.overrides(lr=1e-4, explore=False) == {"lr": 1e-4, "explore": False}
+    with pytest.raises(KeyError):
+        PPOConfig.overrides(no_such_key=1)
+    assert c.get_torch_compile_worker_config() == {"torch_compile": False}
