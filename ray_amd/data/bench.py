@@ -75,10 +75,12 @@ def _ingest_loop(config):
 
         prof = cProfile.Profile()
         prof.enable()
+    w0 = time.time()
     t0 = time.perf_counter()
     n = sum(step() for _ in range(steps))
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    w1 = time.time()
     if prof is not None:
         import io
         import pstats
@@ -93,6 +95,7 @@ def _ingest_loop(config):
     dist.all_gather(allt, t)
     train.report({"images": sum(float(x[0]) for x in allt),
                   "seconds": max(float(x[1]) for x in allt),
+                  "window": [w0, w1],  # wall-clock bounds of rank 0's timed loop
                   "rccl_world_size": dist.get_world_size()})
 
 
@@ -125,6 +128,12 @@ def bench_data_trainer(args, n_gpus: int):
             datasets={"train": ds},
             run_config=RunConfig(name="bench_data", storage_path="/tmp/ray_amd_bench"))
         m = trainer.fit().metrics
+        tl = os.environ.get("RAY_AMD_DATA_TIMELINE")
+        if tl:  # task timeline of the whole run + the timed window (scripts/data_timeline.py)
+            trace = ray.timeline()
+            with open(tl, "w") as f:
+                json.dump({"window": m.get("window"), "cpus": max(16, 4 * n_gpus),
+                           "trace": trace}, f)
     finally:
         ray.shutdown()
     dt = m["seconds"]

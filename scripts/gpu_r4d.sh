@@ -18,6 +18,11 @@ for i in 1 2; do
   timeout -k 10 300 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_$i.log 2>&1 || { echo "bench rc=$?"; tail -30 $O/bench_noray_$i.log; exit 1; }
   echo "no-ray: $(tail -1 $O/bench_noray_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
+timeout -k 10 300 env RAY_AMD_DATA_TRAINER=1 RAY_AMD_DATA_TIMELINE=$O/data_timeline.json python bench.py --workload data --steps 60 --warmup 5 > $O/data_trainer.log 2>&1 || { echo "data rc=$?"; tail -20 $O/data_trainer.log; exit 1; }
+tail -1 $O/data_trainer.log | cut -c1-200
+python scripts/data_timeline.py $O/data_timeline.json > $O/data_timeline.txt 2>&1; head -20 $O/data_timeline.txt
+timeout -k 10 300 python bench.py --workload data --steps 60 --warmup 5 > $O/data_direct.log 2>&1 || { echo "data direct rc=$?"; tail -20 $O/data_direct.log; exit 1; }
+tail -1 $O/data_direct.log | cut -c1-200
 timeout -k 10 120 python scripts/lmhead_hang_repro.py 10 40 lt2 > $O/lmhead_lt2.log 2>&1; rc=$?
 echo "lt2 rc=$rc: $(tail -1 $O/lmhead_lt2.log)"
 [ $rc -eq 0 ] || exit 1
