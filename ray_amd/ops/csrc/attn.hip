@@ -523,7 +523,10 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 // over all 128 keys (8 MFMAs) and adds it to an fp32 dQ workspace with no-return float
 // atomics (two 128-B row segments per instruction: the full-rate shape). This replaces the
 // separate dq kernel, which recomputed S and dP (2 of its 3 MFMA products) from scratch.
-template <bool FUSED>
+// PF: Q/dO register prefetch depth (2: two register sets, tile t+2 in flight; 1: one set,
+// tile t+1 loaded at the top of tile t and written to LDS after its compute — 17 fewer
+// VGPRs for the compiler's LDS-fragment prefetch). ra_knobs[11] = 1 selects PF 1.
+template <bool FUSED, int PF = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -571,7 +574,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float inv_c = -1.f / sc_log2;
   const float* lse_bh = lse + (long)bh * T;
   const float* del_bh = delta + (long)bh * T;
-  QD A, B;
+  QD A;
+  [[maybe_unused]] QD B;
   const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
       (void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
@@ -685,23 +689,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int i = 0; i < 16; ++i) unsafeAtomicAdd(g + crow(i, hh) * HD, acc[i]);
   };
-  auto step = [&](int t, QD& held, QD& next) __attribute__((always_inline)) {
-    if (t + 2 < ntiles) load_qd(next, t + 2);
-    compute(t);
-    if (FUSED) {
-      __syncthreads();  // dS^T image complete
-      if (!(dbg & 2)) dq_tile(t);
-    }
-    if (t + 1 < ntiles) store_qd(held, t + 1);
+  if constexpr (PF == 2) {
+    auto step = [&](int t, QD& held, QD& next) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) load_qd(next, t + 2);
+      compute(t);
+      if (FUSED) {
+        __syncthreads();  // dS^T image complete
+        if (!(dbg & 2)) dq_tile(t);
+      }
+      if (t + 1 < ntiles) store_qd(held, t + 1);
+      __syncthreads();
+    };
+    load_qd(A, t0);
+    store_qd(A, t0);
+    load_qd(A, t0 + 1);  // t0 + 2 <= ntiles
     __syncthreads();
-  };
-  load_qd(A, t0);
-  store_qd(A, t0);
-  load_qd(A, t0 + 1);  // t0 + 2 <= ntiles
-  __syncthreads();
-  for (int t = t0; t < ntiles; t += 2) {
-    step(t, A, B);
-    if (t + 1 < ntiles) step(t + 1, B, A);
+    for (int t = t0; t < ntiles; t += 2) {
+      step(t, A, B);
+      if (t + 1 < ntiles) step(t + 1, B, A);
+    }
+  } else {
+    load_qd(A, t0);
+    store_qd(A, t0);
+    __syncthreads();
+    for (int t = t0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) load_qd(A, t + 1);  // lands during compute(t)
+      compute(t);
+      if (FUSED) {
+        __syncthreads();
+        if (!(dbg & 2)) dq_tile(t);
+      }
+      if (t + 1 < ntiles) store_qd(A, t + 1);  // the other buffer: last read by tile t - 1
+      __syncthreads();
+    }
   }
   // dV / dK tiles: rows = keys (registers), cols = d (lane)
 #pragma unroll
@@ -716,6 +736,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // dQ: workgroup = 128 queries; forward orientation (S^T, lanes = queries).
+// PF as in attn_bwd_dkdv_kernel (K/V tiles); ra_knobs[12] = 1 selects PF 1.
+template <int PF = 2>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -744,7 +766,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   f32x16 dq[2] = {};
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
-  KV A, B;
+  KV A;
+  [[maybe_unused]] KV B;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2, 0x00020000);
   const TileAddr ta(tok);
@@ -800,19 +823,31 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
       else body(t, std::false_type{});
     }
   };
-  auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
-    if (t + 2 < ntiles) load_kv(next, t + 2);
-    compute(t);
-    if (t + 1 < ntiles) store_kv(held, t + 1);
+  if constexpr (PF == 2) {
+    auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
+      if (t + 2 < ntiles) load_kv(next, t + 2);
+      compute(t);
+      if (t + 1 < ntiles) store_kv(held, t + 1);
+      __syncthreads();
+    };
+    load_kv(A, 0);
+    store_kv(A, 0);
+    load_kv(A, 1);  // ntiles >= 2
     __syncthreads();
-  };
-  load_kv(A, 0);
-  store_kv(A, 0);
-  load_kv(A, 1);  // ntiles >= 2
-  __syncthreads();
-  for (int t = 0; t < ntiles; t += 2) {
-    step(t, A, B);
-    if (t + 1 < ntiles) step(t + 1, B, A);
+    for (int t = 0; t < ntiles; t += 2) {
+      step(t, A, B);
+      if (t + 1 < ntiles) step(t + 1, B, A);
+    }
+  } else {
+    load_kv(A, 0);
+    store_kv(A, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) load_kv(A, t + 1);
+      compute(t);
+      if (t + 1 < ntiles) store_kv(A, t + 1);
+      __syncthreads();
+    }
   }
   bf16_t* g = dqkv + ((long)b * T + qrow) * tok + h * HD;
 #pragma unroll
@@ -879,10 +914,14 @@ RA_EXPORT int ra_attn_bwd(const void* qkv, const void* out, const void* dout, co
   const long rows = (long)B * T * H;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+  auto kkv = attn_bwd_dkdv_kernel<false, 2>;
+  if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
+  hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
+  auto kq = attn_bwd_dq_kernel<2>;
+  if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
+  hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
                      sc_log2, scale);
   return hipGetLastError();
@@ -925,7 +964,9 @@ RA_EXPORT int ra_attn_bwd_kv(const void* qkv, const void* dout, const float* lse
                              float scale, hipStream_t st) {
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+  auto kkv = attn_bwd_dkdv_kernel<false, 2>;
+  if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
+  hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);
   return hipGetLastError();
@@ -936,7 +977,9 @@ RA_EXPORT int ra_attn_bwd_q(const void* qkv, const void* dout, const float* lse,
                             float scale, hipStream_t st) {
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
+  auto kq = attn_bwd_dq_kernel<2>;
+  if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
+  hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
                      sc_log2, scale);
   return hipGetLastError();

@@ -11,6 +11,8 @@ O=gpurun_out/r4d
 mkdir -p $O
 timeout -k 10 200 python scripts/attn_fwd_ab.py > $O/attn_ab.log 2>&1 || { echo "attn ab rc=$?"; tail -20 $O/attn_ab.log; exit 1; }
 tail -1 $O/attn_ab.log
+timeout -k 10 200 python scripts/attn_bwd_ab.py > $O/attn_bwd_ab.log 2>&1 || { echo "attn bwd ab rc=$?"; tail -20 $O/attn_bwd_ab.log; exit 1; }
+tail -1 $O/attn_bwd_ab.log
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 echo "gpu tests rc=$rc"; tail -4 $O/gpu_tests.log
 case $rc in 0|1) ;; *) exit 1;; esac
