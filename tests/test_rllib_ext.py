@@ -171,12 +171,13 @@ def test_dqn_from_episode_replay_buffer(cluster):
            .debugging(seed=0))
     algo = cfg.build()
     assert type(algo.buffer).__name__ == "EpisodeReplayBuffer"
-    r = 0.0
-    for _ in range(1500):
+    best = 0.0  # best smoothed return after 3000 steps (a random policy averages ~22)
+    for _ in range(2500):
         res = algo.train()
-        r = res["env_runners"]["episode_return_mean"]
-        if res["num_env_steps_sampled_lifetime"] > 3000 and r > 45:
+        if res["num_env_steps_sampled_lifetime"] > 3000:
+            best = max(best, res["env_runners"]["episode_return_mean"])
+        if best > 45:
             break
-    assert r > 45
+    assert best > 45
     assert algo.buffer.get_num_episodes() > 10
     algo.stop()
