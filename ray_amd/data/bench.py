@@ -28,6 +28,14 @@ MEAN, STD = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
 _POOL = None
 
 
+def _gpu_actors() -> int:
+    """Preprocessing actors per GPU (RAY_AMD_DATA_GPU_ACTORS, default 1). One actor per
+    block runs ray.get of the 38.5 MB uint8 block, the H2D copy, the normalise kernel and
+    the HBM-store put serially; in the TorchTrainer timeline (profiles/r4) that one actor's
+    `process` was busy 95 % of the timed window."""
+    return max(1, int(os.environ.get("RAY_AMD_DATA_GPU_ACTORS", "1")))
+
+
 def _make_images(batch):
     """Synthetic uint8 images: a per-process pool of random images (generated once), each
     block a rotation of it by its first id — a memcpy-speed stand-in for decode, so the
@@ -118,8 +126,9 @@ def bench_data_trainer(args, n_gpus: int):
         ds = rd.range(total, override_num_blocks=max(8, total // bs)).map_batches(
             _make_images, batch_size=bs)
         if path == "hbm":
-            ds = GPUImageNormalize(out_dtype="bf16", batch_size=bs, num_gpus=0.5,
-                                   concurrency=n_gpus, keep_on_device=True).transform(ds)
+            na = _gpu_actors() * n_gpus
+            ds = GPUImageNormalize(out_dtype="bf16", batch_size=bs, num_gpus=0.5 / _gpu_actors(),
+                                   concurrency=na, keep_on_device=True).transform(ds)
         trainer = TorchTrainer(
             _ingest_loop, train_loop_config={"bs": bs, "warmup": args.warmup,
                                              "steps": args.steps, "path": path},
@@ -172,8 +181,8 @@ def bench_data(args):
     ds = rd.range(total, override_num_blocks=max(8, total // bs)).map_batches(
         _make_images, batch_size=bs)
     if path == "hbm":
-        ds = GPUImageNormalize(out_dtype="bf16", batch_size=bs, num_gpus=0.5,
-                               keep_on_device=True).transform(ds)
+        ds = GPUImageNormalize(out_dtype="bf16", batch_size=bs, num_gpus=0.5 / _gpu_actors(),
+                               concurrency=_gpu_actors(), keep_on_device=True).transform(ds)
     dev = torch.device("cuda", 0)
     it = iter(ds.iter_torch_batches(batch_size=bs, device=dev, drop_last=True))
 

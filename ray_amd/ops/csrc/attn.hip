@@ -314,183 +314,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   if (hh == 0) lse[(long)bh * T + qrow] = m_run + log2f(l_run);
 }
 
-// ============================================================================ forward v2
-// Same tiling as attn_fwd_kernel, with the per-score VALU cut (PMC, profiles/r4: v1 is
-// VALU-issue bound at ~12 VALU per MFMA, MFMA pipe 20% busy):
-//  * Q is prescaled by scale*log2(e) when it is loaded, so S^T comes out in log2 units;
-//  * the S^T accumulators START at -m_run (the running max, a lane-constant: each lane
-//    owns one query) instead of 0 — the MFMA chain then yields s - m directly and
-//    p = exp2(s) needs no subtract/scale (the "row constant as initial accumulator" form
-//    the backward already uses);
-//  * m_run starts at 0 and moves only when a tile's max exceeds it by > 8 (lazy rescale;
-//    p <= 2^8), or, before anything was accumulated, when every score is < -96 (so a row
-//    of very negative scores does not underflow);
-//  * the wave index is made wave-uniform (readfirstlane) so the causal-mask branches are
-//    scalar branches, not exec-masked regions.
-//  PF = register prefetch depth (2: tile t+2's loads in flight during tiles t and t+1; 1: one
-//  register set, tile t+1 loaded at the top of tile t and written to LDS after its compute);
-//  UW = wave index via readfirstlane (scalar branches; +~60 VGPRs measured).
-template <int PF, bool UW>
-__global__ __launch_bounds__(256) void attn_fwd_kernel2(const bf16_t* __restrict__ qkv,
-                                                        bf16_t* __restrict__ out,
-                                                        float* __restrict__ lse, int T, int H,
-                                                        float sc_log2) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS];  // [buf][K,V]
-  const int nqb = T / 128;
-  const int L = xcd_block(blockIdx.x, gridDim.x);
-  const int qb = nqb - 1 - L % nqb;
-  const int bh = L / nqb;
-  const int b = bh / H, h = bh % H;
-  const int C = H * HD;
-  const long tok = 3L * C;
-  const bf16_t* base = qkv + (long)b * T * tok + h * HD;
-  const int w = UW ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const LaneOffs lo(lane);
-  const int q0 = qb * 128;
-  const int qrow = q0 + 32 * w + r;
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const bf16x8_t raw = ld8(base + (long)qrow * tok + 16 * kk + 8 * hh);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)((float)raw[j] * sc_log2);
-  }
-  f32x16 o[2] = {};
-  float m_run = 0.f, l_run = 0.f;
-  f32x16 nm;  // -m_run in every register: the S^T chains' initial accumulator
-#pragma unroll
-  for (int i = 0; i < 16; ++i) nm[i] = 0.f;
-  const int ntiles = (q0 + 128) / 64;
-  const int wave_qmin = q0 + 32 * w;
-  const int wave_qmax = wave_qmin + 31;
-  KV A;
-  [[maybe_unused]] KV B;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2,
-                                        0x00020000);
-  const TileAddr ta(tok);
-  auto load_kv = [&](KV& x, int t) __attribute__((always_inline)) {
-    const int off = t * 64 * (int)tok * 2;
-    tile_load_buf(x.k, rs, ta, off + C * 2);
-    tile_load_buf(x.v, rs, ta, off + 2 * C * 2);
-  };
-  auto store_kv = [&](const KV& x, int t) __attribute__((always_inline)) {
-    bf16_t* d = lds + (t & 1) * 2 * TILE_ELEMS;
-    tile_store(x.k, d);
-    tile_store(x.v, d + TILE_ELEMS);
-  };
-  auto body = [&](int t, auto diag_c) __attribute__((always_inline)) {
-    constexpr bool diag = decltype(diag_c)::value;
-    const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
-    const bf16_t* Vs = Ks + TILE_ELEMS;
-    const int kv0 = t * 64;
-    f32x16 st[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[0]), qf[0], nm);
-#pragma unroll
-      for (int kk = 1; kk < 4; ++kk)
-        st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st[kt]);
-    }
-    if (diag) {  // diagonal tile: mask keys > query
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (kv0 + 32 * kt + crow(i, hh) > qrow) st[kt][i] = -INFINITY;
-    }
-    float mt = st[0][0];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, st[kt][i]);
-    mt = half_max(mt);  // this tile's max of (s - m_run), per query
-    if (__builtin_amdgcn_ballot_w64(mt > 8.f || (l_run == 0.f && mt < -96.f))) {
-      // rare: move the running max by d = mt where it grew past the threshold (or where
-      // nothing was accumulated yet), rescale O and l, and re-base this tile's scores
-      const bool mv = mt > 8.f || (l_run == 0.f && mt < -96.f && mt > -INFINITY);
-      const float d = mv ? mt : 0.f;
-      const float alpha = l_run == 0.f ? 0.f : fast_exp2(-d);
-      m_run += d;
-      l_run *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        nm[i] = -m_run;
-        st[0][i] -= d;
-        st[1][i] -= d;
-      }
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-    }
-    float ls = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fast_exp2(st[kt][i]);
-        st[kt][i] = p;
-        ls += p;
-      }
-    l_run += half_sum(ls);
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8_t pf = acc_frag(st[kt], s2);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = mfma32(tr_frag(Vs, lo, 32 * kt + 16 * s2, dt), pf, o[dt]);
-      }
-  };
-  auto compute = [&](int t) __attribute__((always_inline)) {
-    const int kv0 = t * 64;
-    if (kv0 <= wave_qmax) {
-      if (kv0 + 63 > wave_qmin) body(t, std::true_type{});
-      else body(t, std::false_type{});
-    }
-  };
-  if constexpr (PF == 2) {
-    auto step = [&](int t, KV& held, KV& next) __attribute__((always_inline)) {
-      if (t + 2 < ntiles) load_kv(next, t + 2);
-      compute(t);
-      if (t + 1 < ntiles) store_kv(held, t + 1);
-      __syncthreads();
-    };
-    load_kv(A, 0);
-    store_kv(A, 0);
-    load_kv(A, 1);  // ntiles >= 2
-    __syncthreads();
-    for (int t = 0; t < ntiles; t += 2) {
-      step(t, A, B);
-      if (t + 1 < ntiles) step(t + 1, B, A);
-    }
-  } else {
-    load_kv(A, 0);
-    store_kv(A, 0);
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-      if (t + 1 < ntiles) load_kv(A, t + 1);  // lands during compute(t)
-      compute(t);
-      if (t + 1 < ntiles) store_kv(A, t + 1);  // the other buffer: read by tile t - 1
-      __syncthreads();
-    }
-  }
-  const float inv = 1.f / l_run;
-  bf16_t* orow = out + ((long)b * T + qrow) * C + h * HD;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float v[4] = {o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                    o[dt][4 * g + 3] * inv};
-      *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g + 4 * hh) = pack4(v);
-    }
-  if (hh == 0) lse[(long)bh * T + qrow] = m_run + log2f(l_run);
-}
-
 // ============================================================================ backward
 // delta[bh][t] = sum_d dO[b,t,h,d] * O[b,t,h,d]   (one thread per (token, head) row)
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ o,
@@ -526,7 +349,10 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 // PF: Q/dO register prefetch depth (2: two register sets, tile t+2 in flight; 1: one set,
 // tile t+1 loaded at the top of tile t and written to LDS after its compute — 17 fewer
 // VGPRs for the compiler's LDS-fragment prefetch). ra_knobs[11] = 1 selects PF 1.
-template <bool FUSED, int PF = 2>
+// ILP (non-FUSED, with PF 1): both 32-query halves of a tile are in flight at once — the
+// S / dP chains of both halves issue first, then each half's softmax VALU runs while the
+// other half's MFMAs execute (the 17 VGPRs PF 1 frees hold the second half's S / dP).
+template <bool FUSED, int PF = 2, bool ILP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -610,7 +436,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr bool diag = decltype(diag_c)::value;
     const int cur = (t - t0) & 1;
     const int q0 = t * 64;
-    {
+    if constexpr (ILP && !FUSED) {
+      const bf16_t* Qs = lds + cur * 2 * TILE_ELEMS;
+      const bf16_t* Ds = Qs + TILE_ELEMS;
+      const float* nl = rowc + cur * 128;
+      const float* nd = nl + 64;
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 a = *reinterpret_cast<const float4*>(nl + 32 * qt + 8 * g + 4 * hh);
+          const float4 d = *reinterpret_cast<const float4*>(nd + 32 * qt + 8 * g + 4 * hh);
+          s[qt][4 * g] = a.x; s[qt][4 * g + 1] = a.y; s[qt][4 * g + 2] = a.z;
+          s[qt][4 * g + 3] = a.w;
+          dp[qt][4 * g] = d.x; dp[qt][4 * g + 1] = d.y; dp[qt][4 * g + 2] = d.z;
+          dp[qt][4 * g + 3] = d.w;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          s[qt] = mfma32(ld8(Qs + 2048 * qt + lo.row[kk]), kf[kk], s[qt]);
+          dp[qt] = mfma32(ld8(Ds + 2048 * qt + lo.row[kk]), vf[kk], dp[qt]);
+        }
+      }
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(s[qt][i] * sc_log2);
+          if (diag && key > q0 + 32 * qt + crow(i, hh)) p = 0.f;
+          s[qt][i] = p;
+          dp[qt][i] = p * dp[qt][i];
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8_t pa = acc_frag(s[qt], ks);
+          const bf16x8_t da = acc_frag(dp[qt], ks);
+          const int kbq = 32 * qt + 16 * ks;
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            dv[dt] = mfma32(pa, tr_frag(Ds, lo, kbq, dt), dv[dt]);
+            dk[dt] = mfma32(da, tr_frag(Qs, lo, kbq, dt), dk[dt]);
+          }
+        }
+      }
+    } else {
       const bf16_t* Qs = lds + cur * 2 * TILE_ELEMS;
       const bf16_t* Ds = Qs + TILE_ELEMS;
       const float* nl = rowc + cur * 128;
@@ -737,7 +607,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 // dQ: workgroup = 128 queries; forward orientation (S^T, lanes = queries).
 // PF as in attn_bwd_dkdv_kernel (K/V tiles); ra_knobs[12] = 1 selects PF 1.
-template <int PF = 2>
+// ILP: both 32-key halves of a tile in flight (as attn_bwd_dkdv_kernel's ILP).
+template <int PF = 2, bool ILP = false>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -784,7 +655,40 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   auto body = [&](int t, auto diag_c) __attribute__((always_inline)) {
     constexpr bool diag = decltype(diag_c)::value;
     const int kv0 = t * 64;
-    {
+    if constexpr (ILP) {
+      const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
+      const bf16_t* Vs = Ks + TILE_ELEMS;
+      f32x16 st[2], dpt[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          st[kt][i] = nlq;
+          dpt[kt][i] = ndel;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st[kt]);
+          dpt[kt] = mfma32(ld8(Vs + 2048 * kt + lo.row[kk]), df[kk], dpt[kt]);
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(st[kt][i] * sc_log2);
+          if (diag && kv0 + 32 * kt + crow(i, hh) > qrow) p = 0.f;
+          dpt[kt][i] = p * dpt[kt][i];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8_t bfrag = acc_frag(dpt[kt], s2);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dq[dt] = mfma32(tr_frag(Ks, lo, 32 * kt + 16 * s2, dt), bfrag, dq[dt]);
+        }
+      }
+    } else {
       const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
       const bf16_t* Vs = Ks + TILE_ELEMS;
 #pragma unroll
@@ -886,22 +790,8 @@ RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, 
                           float scale, hipStream_t st) {
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
-  // v2 by default (profiles/r4/README.md: 0.198 vs 0.228 ms at B64 T1024 H12, and exact
-  // on the spiked-key input where v1's LSE is off); ra_knobs[9] = 1 selects v1
-  if (ra_knobs[9] == 1)
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                       (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
-  else
-  {
-    // ra_knobs[10]: v2 sub-variant (0: prefetch 2 + uniform wave index, 1: prefetch 1,
-    // 2: prefetch 1 + non-uniform wave index, 3: prefetch 2 + non-uniform)
-    auto k = attn_fwd_kernel2<2, true>;
-    if (ra_knobs[10] == 1) k = attn_fwd_kernel2<1, true>;
-    else if (ra_knobs[10] == 2) k = attn_fwd_kernel2<1, false>;
-    else if (ra_knobs[10] == 3) k = attn_fwd_kernel2<2, false>;
-    hipLaunchKernelGGL(k, dim3(B * H * (T / 128)), dim3(256), 0, st, (const bf16_t*)qkv,
-                       (bf16_t*)out, lse, T, H, sc_log2);
-  }
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   return hipGetLastError();
 }
 
@@ -916,11 +806,14 @@ RA_EXPORT int ra_attn_bwd(const void* qkv, const void* out, const void* dout, co
                      (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
   auto kkv = attn_bwd_dkdv_kernel<false, 2>;
   if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
+  else if (ra_knobs[11] == 2) kkv = attn_bwd_dkdv_kernel<false, 1, true>;
   hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);
   auto kq = attn_bwd_dq_kernel<2>;
   if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
+  else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true>;
+  else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true>;
   hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
                      sc_log2, scale);
@@ -966,6 +859,7 @@ RA_EXPORT int ra_attn_bwd_kv(const void* qkv, const void* dout, const float* lse
   const float sc_log2 = scale * 1.4426950408889634f;
   auto kkv = attn_bwd_dkdv_kernel<false, 2>;
   if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
+  else if (ra_knobs[11] == 2) kkv = attn_bwd_dkdv_kernel<false, 1, true>;
   hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);
@@ -979,6 +873,8 @@ RA_EXPORT int ra_attn_bwd_q(const void* qkv, const void* dout, const float* lse,
   const float sc_log2 = scale * 1.4426950408889634f;
   auto kq = attn_bwd_dq_kernel<2>;
   if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
+  else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true>;
+  else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true>;
   hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
                      sc_log2, scale);

@@ -39,20 +39,40 @@ hipblasLtHandle_t g_handle = nullptr;
 const size_t kWs = 64ull << 20;
 std::map<LtKey, LtPlan*> g_plans;
 std::mutex g_mu;
-// One workspace PER STREAM: a stream-K / split-K kernel keeps partial tiles and arrival
-// flags in its workspace, so two GEMMs running concurrently on different streams must
-// never share one (a shared one can mix their flags and leave a grid waiting forever).
+// One workspace AND one hipBLASLt handle PER STREAM. Stream-K kernels keep partial tiles
+// and arrival flags in the workspace, and hipBLASLt keeps further stream-K synchronisation
+// state per handle: two stream-K GEMMs running concurrently on two streams through ONE
+// handle hang even with separate workspaces (profiles/r4/README.md §2: the two-stream
+// ops/lt repro hung with per-stream workspaces and a shared handle; torch's own GEMMs on
+// two streams share torch's handle the same way). Heuristic queries and plans use g_handle;
+// every launch uses its stream's handle.
 std::map<hipStream_t, void*> g_ws_by_stream;
+std::map<hipStream_t, hipblasLtHandle_t> g_handle_by_stream;
 std::mutex g_ws_mu;  // not g_mu: the GEMM entry points call this with g_mu held
+
+bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
+// RAY_AMD_LT_SHARED_HANDLE=1: launch everything through g_handle (diagnostic only: the
+// failure above, scripts/lmhead_hang_repro.py mode lt2h)
+hipblasLtHandle_t handle_for(hipStream_t st) {
+  static const bool shared = env_on("RAY_AMD_LT_SHARED_HANDLE");
+  if (shared) return g_handle;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_handle_by_stream.find(st);
+  if (it != g_handle_by_stream.end()) return it->second;
+  hipblasLtHandle_t h = nullptr;
+  if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) return g_handle;
+  g_handle_by_stream[st] = h;
+  return h;
+}
 
 void* workspace(hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
-  // RAY_AMD_LT_SHARED_WS=1: one workspace for every stream. Diagnostic only — it recreates
-  // the failure described above for scripts/lmhead_hang_repro.py (mode lt2shared).
-  static const bool shared = [] {
-    const char* e = getenv("RAY_AMD_LT_SHARED_WS");
-    return e && e[0] == '1';
-  }();
+  // RAY_AMD_LT_SHARED_WS=1: one workspace for every stream (diagnostic only, mode lt2shared)
+  static const bool shared = env_on("RAY_AMD_LT_SHARED_WS");
   if (shared) st = nullptr;
   auto it = g_ws_by_stream.find(st);
   if (it != g_ws_by_stream.end()) return it->second;
@@ -153,8 +173,8 @@ LtPlan* get_plan(int ta, int tb, long m, long n, long k, long lda, long ldb, lon
 int run(LtPlan* p, int idx, const void* A, const void* B, float* C, float alpha, float beta,
         hipStream_t st) {
   const hipblasStatus_t s =
-      hipblasLtMatmul(g_handle, p->desc, &alpha, A, p->a, B, p->b, &beta, C, p->c, C, p->c,
-                      &p->cands[idx].algo, workspace(st), kWs, st);
+      hipblasLtMatmul(handle_for(st), p->desc, &alpha, A, p->a, B, p->b, &beta, C, p->c, C,
+                      p->c, &p->cands[idx].algo, workspace(st), kWs, st);
   return s == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + (int)s;
 }
 
@@ -336,8 +356,8 @@ RA_EXPORT int ra_lt_gemm_ep(int ta, int tb, long m, long n, long k, const void* 
   const int idx = choice >= 0 && choice < (int)p->cands.size() ? choice : p->choice;
   const float alpha = 1.f, beta = 0.f;
   const hipblasStatus_t s =
-      hipblasLtMatmul(g_handle, p->desc, &alpha, A, p->a, B, p->b, &beta, D, p->c, D, p->c,
-                      &p->cands[idx].algo, workspace(st), kWs, st);
+      hipblasLtMatmul(handle_for(st), p->desc, &alpha, A, p->a, B, p->b, &beta, D, p->c, D,
+                      p->c, &p->cands[idx].algo, workspace(st), kWs, st);
   return s == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + (int)s;
 }
 

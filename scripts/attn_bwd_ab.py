@@ -1,5 +1,6 @@
 """A/B of the attention backward prefetch variants at the GPT-2 training shape, interleaved
-in one process: dK/dV (ra_knobs[11]: 0 = two Q/dO register sets, 1 = one) and dQ
+in one process: dK/dV (ra_knobs[11]: 0 = two Q/dO register sets, 1 = one, 2 = one + both query halves in
+flight) and dQ
 (ra_knobs[12], same for K/V), plus a check of every variant's dQKV against an fp32
 PyTorch reference on a small batch. Prints one JSON line.
 
@@ -64,7 +65,7 @@ def main():
     torch.manual_seed(3)
     qkv, out, dout, lse, delta, dqkv = alloc(2)
     ref = ref_grads(qkv, dout, sc)
-    for kv in (0, 1):
+    for kv in (0, 1, 2):
         for q in (0, 1):
             L.ra_set_knob(11, kv)
             L.ra_set_knob(12, q)
@@ -76,10 +77,12 @@ def main():
     B = a.B
     qkv, out, dout, lse, delta, dqkv = alloc(B)
     L.ra_attn_bwd_pre(ptr(out), ptr(dout), ptr(delta), B, a.T, a.H, stream_ptr())
-    times = {f"{k}{v}": [] for k in ("kv", "q") for v in (0, 1)}
+    times = {f"{k}{v}": [] for k in ("kv", "q") for v in ((0, 1, 2) if k == "kv" else (0, 1))}
     for _ in range(a.rounds):
-        for v in (0, 1):
+        for v in (0, 1, 2):
             for kind in ("kv", "q"):
+                if kind == "q" and v == 2:
+                    continue
                 L.ra_set_knob(11 if kind == "kv" else 12, v)
                 f = L.ra_attn_bwd_kv if kind == "kv" else L.ra_attn_bwd_q
                 args = (ptr(qkv), ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), B, a.T, a.H, D,
