@@ -511,12 +511,12 @@ _xent_streams: dict = {}
 # difference against putting the dW GEMMs on the wgrad side stream, profiles/r3/
 # lmhead_pipe.md). The side-stream-dW layout was REMOVED in round 4: it ran two torch
 # hipBLASLt GEMMs concurrently on two streams and hung the GPU on a ragged last chunk
-# (N = 12388, chunk 4096). Root cause (profiles/r4/README.md §2, three-arm repro in
-# scripts/lmhead_hang_repro.py): not stream-K concurrency as such — the same dW on the side
-# stream through ops/lt (stream-K kernel, one hipBLASLt workspace PER STREAM) drains beside
-# the same main-stream GEMMs — but torch's hipBLASLt call on the second stream, whose
-# stream-K fixup flags live in workspace state shared with the main stream's GEMMs. Side-
-# stream GEMMs therefore only ever go through ops/lt's per-stream workspaces.
+# (N = 12388, chunk 4096). Root cause (profiles/r4/README.md §2, repro arms in
+# scripts/lmhead_hang_repro.py): two streams issuing stream-K hipBLASLt GEMMs concurrently
+# through ONE hipBLASLt handle — torch uses one handle for all its GEMMs, and ops/lt with a
+# single handle hung the same way even with per-stream workspaces, while a stream-K dW on a
+# side stream through a different handle drained. Side-stream GEMMs therefore only go
+# through ops/lt, which keeps a hipBLASLt handle and a workspace per stream.
 def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
     """Chunked LM head + CE, software-pipelined over two streams:
 
