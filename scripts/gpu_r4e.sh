@@ -21,6 +21,8 @@ for i in 1 2; do
   timeout -k 10 300 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_$i.log 2>&1 || { echo "bench rc=$?"; tail -30 $O/bench_noray_$i.log; exit 1; }
   echo "no-ray: $(tail -1 $O/bench_noray_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
+timeout -k 10 300 python scripts/dgrad_layout_ab.py > $O/dgrad_layout.log 2>&1 || { echo "dgrad ab rc=$?"; tail -20 $O/dgrad_layout.log; exit 1; }
+tail -1 $O/dgrad_layout.log
 for a in 1 2; do
   timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=$a RAY_AMD_DATA_TRAINER=1 RAY_AMD_DATA_TIMELINE=$O/data_timeline_a$a.json python bench.py --workload data --steps 300 --warmup 20 > $O/data_trainer_a$a.log 2>&1 || { echo "data rc=$?"; tail -20 $O/data_trainer_a$a.log; exit 1; }
   echo "trainer actors=$a: $(tail -1 $O/data_trainer_a$a.log | cut -c1-120)"
