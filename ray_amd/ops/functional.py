@@ -361,11 +361,46 @@ def join_side_streams():
         torch.cuda.current_stream(dev).wait_stream(st)
 
 
+# RAY_AMD_DGRAD_WT=1: the input-gradient GEMM dX = dY @ W reads a transposed bf16 copy of
+# W ([in, out], refreshed once per optimizer step on the side stream during the forward),
+# so it runs in the forward GEMMs' operand layout (TunableOp "tn" instead of "nn";
+# scripts/dgrad_layout_ab.py measures both). Costs one extra bf16 copy of every weight.
+_DGRAD_WT = os.environ.get("RAY_AMD_DGRAD_WT", "0") == "1"
+_weights_epoch = [0]
+
+
+def bump_weights_epoch():
+    """Called after every in-place weight update that bypasses autograd's version counter
+    (the flat AdamW kernel): transposed weight copies are refreshed on next use."""
+    _weights_epoch[0] += 1
+
+
+def _transposed_weight(w):
+    """(Wt, event): W^T contiguous, refreshed on the side stream when the weights changed
+    since the last refresh (always under graph capture, where host state is frozen)."""
+    cache = getattr(w, "_ra_wt", None)
+    key = (_weights_epoch[0], w._version, w.data_ptr())  # kernel updates, copy_(), rebinding
+    stale = cache is None or cache[1] != key or torch.cuda.is_current_stream_capturing()
+    if not stale:
+        return cache[0], cache[2]
+    wt = cache[0] if cache is not None else torch.empty(w.shape[1], w.shape[0], dtype=w.dtype,
+                                                        device=w.device)
+    side = _side_stream(w.device)
+    side.wait_stream(torch.cuda.current_stream(w.device))
+    with torch.cuda.stream(side):
+        wt.copy_(w.detach().t())
+        ev = torch.cuda.Event()
+        ev.record(side)
+    w._ra_wt = (wt, key, ev)
+    return wt, ev
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.b = b
+        ctx.wt = _transposed_weight(w) if _DGRAD_WT and w.is_cuda and x.dim() >= 2 else None
         return torch.nn.functional.linear(x, w, b)
 
     @staticmethod
@@ -375,7 +410,14 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         dy2 = dy.reshape(-1, N)
         M = x2.shape[0]
-        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.wt is not None:
+                wt, ev = ctx.wt
+                torch.cuda.current_stream(dy2.device).wait_event(ev)
+                dx = (dy2 @ wt.t()).view(x.shape)
+            else:
+                dx = (dy2 @ w).view(x.shape)
         dw = db = None
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)

@@ -319,10 +319,11 @@ class FlatAdamW:
         ev.record()
 
     def step(self, lr: float | None = None):
-        if self.use_hip:
-            from ray_amd.ops import functional as rf
+        from ray_amd.ops import functional as rf
 
+        if self.use_hip:
             rf.join_side_streams()  # weight gradients queued on the side stream
+        rf.bump_weights_epoch()  # the kernel updates p16 in place: cached copies go stale
         self.step_count += 1
         lr = self.lr if lr is None else lr
         f = self.flat

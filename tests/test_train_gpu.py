@@ -227,3 +227,33 @@ def test_flat_ddp_world1_hooks_comm_stream(cuda_device):
         ddp.finish()
         torch.cuda.synchronize()
         assert _rel(fb.g, fa.g) < 1e-6
+
+
+def test_dgrad_transposed_weight_copy(cuda_device, monkeypatch):
+    """RAY_AMD_DGRAD_WT: dX from the transposed bf16 weight copy equals dY @ W, and the copy
+    follows in-place weight updates (autograd's version counter) and optimizer steps (the
+    weights epoch) instead of serving a stale transpose."""
+    torch.manual_seed(5)
+    x = torch.randn(512, 256, device=cuda_device).bfloat16().requires_grad_()
+    w = (torch.randn(384, 256, device=cuda_device) * 0.05).bfloat16().requires_grad_()
+    b = torch.zeros(384, device=cuda_device).bfloat16().requires_grad_()
+    g = torch.randn(512, 384, device=cuda_device).bfloat16()
+
+    def dx():
+        x.grad = None
+        rf.linear(x, w, b).backward(g)
+        torch.cuda.synchronize()
+        return x.grad.float()
+
+    monkeypatch.setattr(rf, "_DGRAD_WT", False)
+    ref = dx()
+    monkeypatch.setattr(rf, "_DGRAD_WT", True)
+    assert (dx() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    with torch.no_grad():
+        w.mul_(0.5)  # in-place update: version counter moves
+    assert (dx() - 0.5 * ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    wt_before = w._ra_wt[0].clone()
+    rf.bump_weights_epoch()  # what FlatAdamW.step does after its in-place kernel
+    dx()
+    assert torch.equal(w._ra_wt[0], wt_before)  # refreshed from unchanged weights
+    assert torch.equal(w._ra_wt[0], w.detach().t().contiguous())
