@@ -63,6 +63,10 @@ def main():
     res["per_layer_ms"] = {"nn": round(tot_nn, 4), "tn": round(tot_tn, 4),
                            "transpose": round(tot_tr, 4)}
     res["per_step_saving_ms_12_layers"] = round(12 * (tot_nn - tot_tn - tot_tr), 3)
+    torch.cuda.tunable.write_file(dst)
+    old = set(open(SRC).read().splitlines())
+    res["new_tunableop_entries"] = [ln for ln in open(dst).read().splitlines()
+                                    if ln not in old and not ln.startswith("Validator")]
     print(json.dumps(res), flush=True)
 
 
