@@ -36,6 +36,9 @@ class _Router:
         self.last_refresh = 0.0
         self.stale = False
         self.affinity = {}  # multiplexed model id -> replica that loaded it
+        # replicas a request of this handle saw die: skipped until the controller's replica
+        # set no longer lists them (its health check has not noticed the death yet)
+        self.dead = set()
 
     def _controller(self):
         from ray_amd.serve.api import _get_controller
@@ -57,7 +60,10 @@ class _Router:
     def _install(self, info):
         version, reps, mo, mq = info
         with self.lock:
-            if version != self.version:
+            listed = {rid for rid, _ in reps}
+            self.dead &= listed  # the controller dropped them: forget
+            reps = [x for x in reps if x[0] not in self.dead]
+            if version != self.version or len(reps) != len(self.replicas):
                 self.version = version
                 self.replicas = reps
                 self.inflight = {rid: self.inflight.get(rid, 0) for rid, _ in reps}
@@ -243,6 +249,15 @@ class _Router:
         self.inflight[rid] = self.inflight.get(rid, 0) + 1
         return rid, h
 
+    def mark_dead(self, rid):
+        """A request on replica ``rid`` failed with an actor death: stop routing to it
+        before the controller's health check removes it from the replica set."""
+        with self.lock:
+            self.dead.add(rid)
+            self.replicas = [x for x in self.replicas if x[0] != rid]
+            self.inflight.pop(rid, None)
+            self.slot_freed.notify_all()
+
     def done(self, rid):
         with self.lock:
             self._done_locked(rid)
@@ -414,9 +429,13 @@ class DeploymentResponse:
     ``(slot, ref)`` once the router's dispatcher sends it, or raises BackPressureError
     (``max_queued_requests`` exceeded) / is cancelled.
 
-    ``resend`` re-issues the request on a freshly chosen replica: used once when the
-    replica died before answering (a redeploy / scale-down raced the cached routing
-    table; reference: the router retries requests whose replica became unavailable)."""
+    ``resend`` re-issues the request on a freshly chosen replica when the replica died
+    before answering (killed, crashed, or a redeploy / scale-down raced the cached routing
+    table; reference: the router retries requests whose replica became unavailable). The
+    dead replica is excluded from this handle's routing at once, and up to MAX_RETRIES
+    resends are made."""
+
+    MAX_RETRIES = 3
 
     def __init__(self, ref, router, slot=None, resend=None, pending=None):
         self._ref = ref
@@ -424,6 +443,17 @@ class DeploymentResponse:
         self._slot = slot
         self._resend = resend
         self._pending = pending
+        self._retries = 0
+
+    def _retry(self):
+        """The assigned replica died: stop routing to it, resend; None when out of
+        retries (the caller re-raises)."""
+        if self._resend is None or self._retries >= self.MAX_RETRIES:
+            return None
+        self._retries += 1
+        if self._slot is not None:
+            self._router.mark_dead(self._slot.rid)
+        return self._resend
 
     def _assigned(self, timeout_s=None):
         if self._pending is not None:
@@ -461,11 +491,12 @@ class DeploymentResponse:
             try:
                 out = ray.get(self._assigned(timeout_s), timeout=timeout_s)
             except Exception as e:  # noqa: BLE001
-                if self._resend is None or not _is_replica_death(e):
+                resend = self._retry() if _is_replica_death(e) else None
+                if resend is None:
                     self._give_up(e)
                     raise
                 self._router.refresh(force=True)
-                again, self._resend = self._resend(), None
+                again = resend()
                 # releases the dead replica's slot; the retried request keeps its own
                 # slot until its reply lands (_watch) or this loop returns / raises
                 self._adopt(again)
@@ -481,11 +512,12 @@ class DeploymentResponse:
                 try:
                     out = await self._assigned()
                 except Exception as e:  # noqa: BLE001
-                    if self._resend is None or not _is_replica_death(e):
+                    resend = self._retry() if _is_replica_death(e) else None
+                    if resend is None:
                         self._give_up(e)
                         raise
                     await self._router.arefresh(force=True)
-                    again, self._resend = self._resend(), None
+                    again = resend()
                     if again._pending is not None:
                         await asyncio.wrap_future(again._pending)
                     self._adopt(again)

@@ -157,7 +157,7 @@ def test_model_multiplexing_routes_by_model_id(cluster):
 
 
 def test_retried_request_keeps_its_slot_until_the_reply(monkeypatch):
-    """A request whose replica died is re-sent once; the retried request's
+    """A request whose replica died is re-sent; the retried request's
     max_ongoing_requests slot must stay claimed while its reply is awaited (the dead
     replica's slot is returned immediately)."""
     import threading
@@ -176,6 +176,9 @@ def test_retried_request_keeps_its_slot_until_the_reply(monkeypatch):
         def refresh(self, force=False):
             pass
 
+        def mark_dead(self, rid):  # the failed replica leaves this handle's routing
+            self.dead = rid
+
     router = _Router()
     s1, s2 = H._Slot(router, "dead"), H._Slot(router, "retry")
     seen = {}
@@ -191,4 +194,4 @@ def test_retried_request_keeps_its_slot_until_the_reply(monkeypatch):
     resp = H.DeploymentResponse("ref1", router, slot=s1, resend=lambda: retry)
     assert resp.result() == 42
     assert seen["released_while_waiting"] == ["dead"]
-    assert router.done == ["dead", "retry"]
+    assert router.done == ["dead", "retry"] and router.dead == "dead"
