@@ -6,6 +6,8 @@ kernel (ops/csrc/preprocess.hip) inside an actor pool that holds a GPU."""
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -264,14 +266,20 @@ class _GPUNormalizeUDF:
         self.dtype = torch.bfloat16 if out_dtype == "bf16" else torch.float32
         self.resize = resize
         self.dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        self.pin_store = os.environ.get("RAY_AMD_DATA_PIN_STORE", "0") == "1"
 
     def __call__(self, batch):
         import torch
 
         from ray_amd.ops import functional as rf
 
-        x = torch.from_numpy(np.ascontiguousarray(batch[self.column])).to(self.dev,
-                                                                          non_blocking=True)
+        src = np.ascontiguousarray(batch[self.column])
+        if self.pin_store and self.dev.type == "cuda":
+            from ray_amd._private.h2d import to_device_pinned
+
+            x = to_device_pinned(src, self.dev)  # DMA from registered store pages
+        else:
+            x = torch.from_numpy(src).to(self.dev, non_blocking=True)
         y = rf.image_normalize(x, self.mean, self.std, self.dtype)
         if self.resize is not None:
             y = rf.resize_bilinear(y, self.resize)

@@ -27,12 +27,13 @@ for i in 1 2; do
 done
 timeout -k 10 300 python scripts/dgrad_layout_ab.py > $O/dgrad_layout.log 2>&1 || { echo "dgrad ab rc=$?"; tail -20 $O/dgrad_layout.log; exit 1; }
 tail -1 $O/dgrad_layout.log
-for a in 1 2; do
-  timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=$a RAY_AMD_DATA_TRAINER=1 RAY_AMD_DATA_TIMELINE=$O/data_timeline_a$a.json python bench.py --workload data --steps 300 --warmup 20 > $O/data_trainer_a$a.log 2>&1 || { echo "data rc=$?"; tail -20 $O/data_trainer_a$a.log; exit 1; }
-  echo "trainer actors=$a: $(tail -1 $O/data_trainer_a$a.log | cut -c1-120)"
-  python scripts/data_timeline.py $O/data_timeline_a$a.json > $O/data_timeline_a$a.txt 2>&1; head -8 $O/data_timeline_a$a.txt
-  timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=$a python bench.py --workload data --steps 300 --warmup 20 > $O/data_direct_a$a.log 2>&1 || { echo "data direct rc=$?"; tail -20 $O/data_direct_a$a.log; exit 1; }
-  echo "direct actors=$a: $(tail -1 $O/data_direct_a$a.log | cut -c1-120)"
+for cfg in a1 a2 a1pin; do
+  a=${cfg:1:1}; pin=0; [ "$cfg" = a1pin ] && pin=1
+  timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=$a RAY_AMD_DATA_PIN_STORE=$pin RAY_AMD_DATA_TRAINER=1 RAY_AMD_DATA_TIMELINE=$O/data_timeline_$cfg.json python bench.py --workload data --steps 300 --warmup 20 > $O/data_trainer_$cfg.log 2>&1 || { echo "data rc=$?"; tail -20 $O/data_trainer_$cfg.log; exit 1; }
+  echo "trainer $cfg: $(tail -1 $O/data_trainer_$cfg.log | cut -c1-120)"
+  python scripts/data_timeline.py $O/data_timeline_$cfg.json > $O/data_timeline_$cfg.txt 2>&1; head -8 $O/data_timeline_$cfg.txt
+  timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=$a RAY_AMD_DATA_PIN_STORE=$pin python bench.py --workload data --steps 300 --warmup 20 > $O/data_direct_$cfg.log 2>&1 || { echo "data direct rc=$?"; tail -20 $O/data_direct_$cfg.log; exit 1; }
+  echo "direct $cfg: $(tail -1 $O/data_direct_$cfg.log | cut -c1-120)"
 done
 for e in 5 20; do
   timeout -k 10 400 env RAY_AMD_RUNNER_ENVS=$e RAY_AMD_PPO_ASYNC=1 python bench.py --workload ppo --steps 8 --warmup 2 > $O/ppo_envs$e.log 2>&1 || { echo "ppo rc=$?"; tail -20 $O/ppo_envs$e.log; exit 1; }
