@@ -12,6 +12,7 @@ from ray_amd.tune.search.sample import (choice, grid_search, lograndint, logunif
                                         randint, randn, sample_from, uniform)
 from ray_amd.tune.trainable import Trainable, with_parameters, with_resources  # noqa: F401
 from ray_amd.tune.tuner import (CombinedStopper, ExperimentAnalysis,  # noqa: F401
+                                ExperimentPlateauStopper, NoopStopper,
                                 FunctionStopper, MaximumIterationStopper, ResultGrid, Stopper,
                                 TimeoutStopper, TrialPlateauStopper, TuneConfig, Tuner, run)
 from ray_amd.train.result import Result  # noqa: F401

@@ -136,20 +136,73 @@ class FunctionStopper(Stopper):
         return self.fn(trial_id, result)
 
 
+class NoopStopper(Stopper):
+    """Never stops anything (reference: tune/stopper/noop.py)."""
+
+
 class TrialPlateauStopper(Stopper):
+    """Stop a trial once the standard deviation of its last ``num_results`` values of
+    ``metric`` is at most ``std``, after ``grace_period`` results; with
+    ``metric_threshold`` the plateau must also be at or beyond it (below for
+    mode="min", above for mode="max") (reference: tune/stopper/trial_plateau.py)."""
+
     def __init__(self, metric, std=0.01, num_results=4, grace_period=4, metric_threshold=None,
                  mode=None):
+        if metric_threshold is not None and mode not in ("min", "max"):
+            raise ValueError("TrialPlateauStopper: metric_threshold needs mode 'min' or 'max'")
         self.metric, self.std, self.n, self.grace = metric, std, num_results, grace_period
+        self.threshold, self.mode = metric_threshold, mode
         self.hist = {}
 
     def __call__(self, trial_id, result):
         import numpy as np
 
+        if self.metric not in result:
+            return False
         h = self.hist.setdefault(trial_id, [])
-        h.append(result.get(self.metric, 0))
+        h.append(float(result[self.metric]))
         if len(h) < max(self.grace, self.n):
             return False
+        last = h[-1]
+        if self.threshold is not None and (
+                (self.mode == "min" and last > self.threshold) or
+                (self.mode == "max" and last < self.threshold)):
+            return False
         return float(np.std(h[-self.n:])) <= self.std
+
+
+class ExperimentPlateauStopper(Stopper):
+    """Stop the whole experiment when the best ``top`` values of ``metric`` seen so far
+    (over all trials) have a standard deviation of at most ``std`` for more than
+    ``patience`` consecutive results (reference: tune/stopper/experiment_plateau.py)."""
+
+    def __init__(self, metric, std=0.001, top=10, mode="min", patience=0):
+        if mode not in ("min", "max"):
+            raise ValueError("ExperimentPlateauStopper: mode must be 'min' or 'max'")
+        if patience < 0 or top < 1:
+            raise ValueError("ExperimentPlateauStopper: patience >= 0 and top >= 1")
+        self.metric, self.std, self.top, self.mode, self.patience = metric, std, top, mode, \
+            patience
+        self.best = []
+        self.iterations = 0
+
+    def __call__(self, trial_id, result):
+        import numpy as np
+
+        if self.metric not in result:
+            return False
+        v = float(result[self.metric])
+        self.best.append(v)
+        self.best.sort(reverse=self.mode == "max")
+        del self.best[self.top:]
+        if len(self.best) == self.top and float(np.std(self.best)) <= self.std:
+            self.iterations += 1
+        else:
+            self.iterations = 0
+        return False
+
+    def stop_all(self):
+        return self.iterations > self.patience
 
 
 class TimeoutStopper(Stopper):

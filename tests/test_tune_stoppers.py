@@ -1,0 +1,54 @@
+"""Tune stoppers (reference: python/ray/tune/tests/test_stopper.py): trial plateau with a
+metric threshold, experiment plateau over the top-k results, noop, and an experiment the
+plateau stopper ends early."""
+import pytest
+
+import ray_amd as ray
+from ray_amd import tune
+from ray_amd.tune.stopper import ExperimentPlateauStopper, NoopStopper, TrialPlateauStopper
+
+
+def test_trial_plateau_threshold_and_mode():
+    s = TrialPlateauStopper("loss", std=0.01, num_results=3, grace_period=3,
+                            metric_threshold=0.5, mode="min")
+    for v in (1.0, 1.0, 1.0):  # flat but above the threshold (mode min): keep going
+        assert not s("t", {"loss": v})
+    for v in (0.4, 0.4):
+        assert not s("t", {"loss": v})
+    assert s("t", {"loss": 0.4})  # last three flat and below the threshold
+    assert not s("u", {"other": 1.0})  # results without the metric never stop a trial
+    with pytest.raises(ValueError):
+        TrialPlateauStopper("loss", metric_threshold=0.1)
+
+
+def test_experiment_plateau_top_k_and_patience():
+    s = ExperimentPlateauStopper("acc", std=0.001, top=3, mode="max", patience=1)
+    for v in (0.1, 0.5, 0.9):
+        s("a", {"acc": v})
+    assert not s.stop_all()
+    s("b", {"acc": 0.9}), s("c", {"acc": 0.9})  # top-3 = 0.9, 0.9, 0.9: plateau starts
+    assert not s.stop_all()  # within patience
+    s("d", {"acc": 0.2})
+    assert s.stop_all()
+    assert not NoopStopper()("x", {"acc": 1}) and not NoopStopper().stop_all()
+
+
+def test_experiment_plateau_ends_tuner_early(tmp_path):
+    ray.init(num_cpus=4)
+    try:
+        def trainable(config):
+            for i in range(100):
+                tune.report({"score": 1.0, "it": i})  # a flat metric from the start
+
+        res = tune.Tuner(
+            trainable, param_space={"x": tune.grid_search([1, 2])},
+            run_config=tune.RunConfig(
+                storage_path=str(tmp_path),
+                stop=ExperimentPlateauStopper("score", top=4, mode="max", patience=2)),
+        ).fit()
+        # the experiment stops once the plateau outlasts the patience: the running trial
+        # ends early and a trial still pending never starts
+        iters = [r.metrics.get("it", -1) for r in res]
+        assert 0 <= max(iters) < 50, iters
+    finally:
+        ray.shutdown()
