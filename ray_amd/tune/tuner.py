@@ -253,6 +253,7 @@ class Trial:
         self.actor = None
         self.pending_ref = None
         self.resources = resources
+        self.trial_name = f"trial_{trial_id}"
         self.local_path = os.path.join(exp_dir, f"trial_{trial_id}")
         self.pending_exploit = None
         self._asha_rungs = set()
@@ -263,6 +264,20 @@ class Trial:
 
     def __repr__(self):
         return f"Trial({self.trial_id}, {self.status})"
+
+    def __str__(self):
+        return self.trial_name
+
+    def name_with(self, tc, exp_dir):
+        """TuneConfig.trial_name_creator / trial_dirname_creator (callables of the Trial)."""
+        if tc is not None and tc.trial_name_creator is not None:
+            self.trial_name = str(tc.trial_name_creator(self))
+        if tc is not None and tc.trial_dirname_creator is not None:
+            d = str(tc.trial_dirname_creator(self))
+            if os.sep in d or d in ("", ".", ".."):
+                raise ValueError(f"trial_dirname_creator returned an invalid name: {d!r}")
+            self.local_path = os.path.join(exp_dir, d)
+        return self
 
 
 class ResultGrid:
@@ -426,7 +441,7 @@ class _Controller:
             self.exhausted = True
             return None
         self._n_suggested += 1
-        t = Trial(cfg, tid, self.exp_dir, self.resources)
+        t = Trial(cfg, tid, self.exp_dir, self.resources).name_with(self.tc, self.exp_dir)
         self.trials.append(t)
         self.scheduler.on_trial_add(self, t)
         return t
@@ -447,7 +462,7 @@ class _Controller:
                     self._actor_cache.pop(i)
                     try:
                         ok = ray.get(a.reset.remote(t.config, t.local_path, t.trial_id,
-                                                    f"trial_{t.trial_id}", checkpoint,
+                                                    t.trial_name, checkpoint,
                                                     t.start_iteration), timeout=60)
                     except Exception:  # noqa: BLE001
                         ok = False
@@ -465,7 +480,7 @@ class _Controller:
             if extra:
                 opts["resources"] = extra
             actor = self.actor_cls.options(**opts).remote(
-                self.trainable, t.config, t.local_path, t.trial_id, f"trial_{t.trial_id}",
+                self.trainable, t.config, t.local_path, t.trial_id, t.trial_name,
                 checkpoint, cc.checkpoint_frequency if cc else 0, t.start_iteration)
             actor.start.remote()  # actor calls are ordered: next_result runs after start
         t.actor = actor
@@ -773,7 +788,7 @@ class Tuner:
         with open(p, "rb") as f:
             st = pickle.load(f)
         for tid, cfg, status, ckpt, results in st["trials"]:
-            t = Trial(cfg, tid, ctl.exp_dir, ctl.resources)
+            t = Trial(cfg, tid, ctl.exp_dir, ctl.resources).name_with(ctl.tc, ctl.exp_dir)
             t.results = results
             t.last_result = results[-1] if results else {}
             t.last_checkpoint = ckpt

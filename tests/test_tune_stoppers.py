@@ -52,3 +52,27 @@ def test_experiment_plateau_ends_tuner_early(tmp_path):
         assert 0 <= max(iters) < 50, iters
     finally:
         ray.shutdown()
+
+
+def test_trial_name_and_dirname_creators(tmp_path):
+    import os
+
+    from ray_amd import train
+
+    ray.init(num_cpus=4)
+    try:
+        def trainable(config):
+            ctx = train.get_context()
+            tune.report({"name": ctx.get_trial_name(), "dir": os.path.basename(ctx.get_trial_dir())})
+
+        res = tune.Tuner(
+            trainable, param_space={"x": tune.grid_search([1, 2])},
+            tune_config=tune.TuneConfig(
+                trial_name_creator=lambda t: f"run_x{t.config['x']}",
+                trial_dirname_creator=lambda t: f"dir_{t.config['x']}"),
+            run_config=tune.RunConfig(storage_path=str(tmp_path)),
+        ).fit()
+        got = sorted((r.metrics["name"], r.metrics["dir"], os.path.basename(r.path)) for r in res)
+        assert got == [("run_x1", "dir_1", "dir_1"), ("run_x2", "dir_2", "dir_2")]
+    finally:
+        ray.shutdown()
