@@ -173,6 +173,21 @@ class _TrialActor:
     def pid(self):
         return os.getpid()
 
+    def set_log_files(self, stdout_path, stderr_path):
+        """RunConfig.log_to_file: this trial's prints go to files in its directory (the
+        actor process is the trial's; a reused actor is re-pointed at the next trial)."""
+        import sys
+
+        for attr in ("_log_out", "_log_err"):
+            f = getattr(self, attr, None)
+            if f is not None and not f.closed:
+                f.flush()
+        out = open(stdout_path, "a", buffering=1)
+        err = out if stderr_path == stdout_path else open(stderr_path, "a", buffering=1)
+        self._log_out, self._log_err = out, err
+        sys.stdout, sys.stderr = out, err
+        return True
+
     def start(self):
         global _fn_session
         if self.is_class:

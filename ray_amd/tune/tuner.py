@@ -450,6 +450,23 @@ class _Controller:
     def _res_key(res):
         return tuple(sorted((k, float(v)) for k, v in (res or {}).items()))
 
+    def _log_files(self, actor, t):
+        """RunConfig.log_to_file: True -> trial_dir/stdout + stderr; a str -> both streams
+        into that file; a (stdout, stderr) pair. Relative names are in the trial dir."""
+        spec = getattr(self.rc, "log_to_file", False)
+        if not spec:
+            return
+        if spec is True:
+            names = ("stdout", "stderr")
+        elif isinstance(spec, str):
+            names = (spec, spec)
+        elif isinstance(spec, (tuple, list)) and len(spec) == 2:
+            names = tuple(spec)
+        else:
+            raise ValueError("RunConfig.log_to_file must be a bool, a str or a (str, str) pair")
+        paths = [n if os.path.isabs(n) else os.path.join(t.local_path, n) for n in names]
+        actor.set_log_files.remote(*paths)
+
     def _launch(self, t: Trial, checkpoint=None):
         res = t.resources or self.resources
         cc = self.rc.checkpoint_config
@@ -469,6 +486,7 @@ class _Controller:
                     if ok:
                         actor = a
                         self.num_actor_reuses += 1
+                        self._log_files(actor, t)
                     else:
                         ray.kill(a)
                     break
@@ -482,6 +500,7 @@ class _Controller:
             actor = self.actor_cls.options(**opts).remote(
                 self.trainable, t.config, t.local_path, t.trial_id, t.trial_name,
                 checkpoint, cc.checkpoint_frequency if cc else 0, t.start_iteration)
+            self._log_files(actor, t)
             actor.start.remote()  # actor calls are ordered: next_result runs after start
         t.actor = actor
         t.pending_ref = t.actor.next_result.remote()

@@ -76,3 +76,30 @@ def test_trial_name_and_dirname_creators(tmp_path):
         assert got == [("run_x1", "dir_1", "dir_1"), ("run_x2", "dir_2", "dir_2")]
     finally:
         ray.shutdown()
+
+
+@pytest.mark.parametrize("spec", [True, "out.log"])
+def test_log_to_file(tmp_path, spec):
+    import os
+
+    ray.init(num_cpus=2)
+    try:
+        def trainable(config):
+            import sys
+
+            print("hello from", config["x"])
+            print("warn", config["x"], file=sys.stderr)
+            tune.report({"ok": 1})
+
+        res = tune.Tuner(trainable, param_space={"x": 7},
+                         run_config=tune.RunConfig(storage_path=str(tmp_path),
+                                                   log_to_file=spec)).fit()
+        d = res[0].path
+        if spec is True:
+            assert "hello from 7" in open(os.path.join(d, "stdout")).read()
+            assert "warn 7" in open(os.path.join(d, "stderr")).read()
+        else:
+            txt = open(os.path.join(d, "out.log")).read()
+            assert "hello from 7" in txt and "warn 7" in txt
+    finally:
+        ray.shutdown()
