@@ -885,8 +885,11 @@ def run(run_or_experiment, *, config=None, num_samples=1, metric=None, mode=None
                                 checkpoint_at_end=kw.pop("checkpoint_at_end", None),
                                 checkpoint_score_attribute=attr, checkpoint_score_order=order)
     callbacks = kw.pop("callbacks", None)
-    for k in ("progress_reporter", "verbose", "sync_config", "raise_on_failed_trial"):
-        kw.pop(k, None)
+    raise_on_failed = kw.pop("raise_on_failed_trial", True)
+    # reporting only: progress_reporter / verbose go to RunConfig; sync_config has nothing
+    # to sync to (storage_path is a local or shared filesystem path here)
+    extra_rc = {k: kw.pop(k) for k in ("progress_reporter", "verbose", "sync_config",
+                                       "log_to_file") if k in kw}
     t = resolve_trainable(run_or_experiment)
     if resources_per_trial:
         t = _with_res(t, resources_per_trial)
@@ -896,8 +899,17 @@ def run(run_or_experiment, *, config=None, num_samples=1, metric=None, mode=None
                                          max_concurrent_trials=max_concurrent_trials,
                                          time_budget_s=time_budget_s),
                   run_config=RunConfig(name=name, storage_path=storage_path, stop=stop,
-                                       checkpoint_config=ckpt_cfg, callbacks=callbacks))
-    return ExperimentAnalysis(tuner.fit(), metric, mode)
+                                       checkpoint_config=ckpt_cfg, callbacks=callbacks,
+                                       **extra_rc))
+    grid = tuner.fit()
+    if raise_on_failed and grid.num_errors:
+        # reference tune.run: TuneError("Trials did not complete", incomplete_trials)
+        from ray_amd.tune import TuneError
+
+        failed = [r for r in grid if r.error is not None]
+        raise TuneError(f"Trials did not complete: {len(failed)} of {len(grid)} errored "
+                        f"(first: {failed[0].error!r})")
+    return ExperimentAnalysis(grid, metric, mode)
 
 
 def _with_res(t, res):

@@ -103,3 +103,20 @@ def test_log_to_file(tmp_path, spec):
             assert "hello from 7" in txt and "warn 7" in txt
     finally:
         ray.shutdown()
+
+
+def test_tune_run_raise_on_failed_trial(tmp_path):
+    ray.init(num_cpus=2)
+    try:
+        def bad(config):
+            if config["x"] == 2:
+                raise ValueError("boom")
+            tune.report({"ok": 1})
+
+        with pytest.raises(tune.TuneError, match="1 of 2 errored"):
+            tune.run(bad, config={"x": tune.grid_search([1, 2])}, storage_path=str(tmp_path))
+        ana = tune.run(bad, config={"x": tune.grid_search([1, 2])}, storage_path=str(tmp_path),
+                       raise_on_failed_trial=False, verbose=0)
+        assert len(ana.trials) == 2
+    finally:
+        ray.shutdown()
