@@ -90,21 +90,28 @@ LabelMap Scheduler::labels(const std::string& node) {
   return it == nodes_.end() ? LabelMap() : it->second.labels;
 }
 
+// A wanted value is a comma-separated "in" list; a leading '!' negates it ("not in": a
+// node without the label matches a negated constraint, as in the reference's
+// label_selector "!value" / "!in(a,b)").
 bool Scheduler::labels_match(const NodeRes& n, const LabelMap& want) const {
   for (auto& kv : want) {
+    const std::string& raw = kv.second;
+    const bool neg = !raw.empty() && raw[0] == '!';
     auto it = n.labels.find(kv.first);
-    if (it == n.labels.end()) return false;
-    // value may be a comma-separated "in" list
-    const std::string& v = kv.second;
-    size_t s = 0;
-    bool ok = false;
-    while (s <= v.size()) {
-      size_t e = v.find(',', s);
-      if (e == std::string::npos) e = v.size();
-      if (v.compare(s, e - s, it->second) == 0) { ok = true; break; }
+    if (it == n.labels.end()) {
+      if (neg) continue;
+      return false;
+    }
+    const size_t s0 = neg ? 1 : 0;
+    size_t s = s0;
+    bool in = false;
+    while (s <= raw.size()) {
+      size_t e = raw.find(',', s);
+      if (e == std::string::npos) e = raw.size();
+      if (raw.compare(s, e - s, it->second) == 0) { in = true; break; }
       s = e + 1;
     }
-    if (!ok) return false;
+    if (neg ? in : !in) return false;
   }
   return true;
 }

@@ -142,13 +142,16 @@ class _ActorConn:
 
 
 class _Stream:
-    __slots__ = ("items", "done", "error_ref", "cv_waiters", "total")
+    __slots__ = ("items", "done", "error_ref", "cv_waiters", "total", "conn", "consumed", "bp")
 
-    def __init__(self):
+    def __init__(self, bp=0):
         self.items = {}
         self.done = False
         self.error_ref = None
         self.total = None
+        self.conn = None  # the executing worker's connection (backpressure acks)
+        self.consumed = 0
+        self.bp = bp  # _generator_backpressure_num_objects (0: unbounded)
 
 
 class _Waiter:
@@ -343,6 +346,7 @@ class CoreWorker:
             P.TASK: self._on_task,
             P.TASK_REPLY: self._on_task_reply,
             P.STREAM_ITEM: self._on_stream_item,
+            P.STREAM_ACK: self._on_stream_ack,
         }
         while not self._stopped:
             try:
@@ -1381,10 +1385,15 @@ class CoreWorker:
         }
         if opts.get("max_calls"):
             spec["max_calls"] = int(opts["max_calls"])
+        if opts.get("enable_task_events", True) is False:
+            spec["no_events"] = True  # kept out of the task-event stream / timeline
+        bp = int(opts.get("_generator_backpressure_num_objects") or 0)
+        if streaming and bp > 0:
+            spec["gen_bp"] = bp
         refs = []
         with self.lock:
             if streaming:
-                self.streams[tid] = _Stream()
+                self.streams[tid] = _Stream(spec.get("gen_bp", 0))
             else:
                 for i in range(nret):
                     oid = object_id_for_return(tid, i + 1)
@@ -1394,8 +1403,10 @@ class CoreWorker:
             refs = [ObjectRef(object_id_for_return(tid, i + 1), self.addr, _cw_obj=self)
                     for i in range(nret)]
         spec["_holders"] = holders
-        self.task_events.append((tid, name, time.time(), None, None, None, "PENDING_NODE_ASSIGNMENT",
-                                 P.NORMAL_TASK, self.job_id, 0, None))
+        if not spec.get("no_events"):
+            self.task_events.append((tid, name, time.time(), None, None, None,
+                                     "PENDING_NODE_ASSIGNMENT", P.NORMAL_TASK, self.job_id, 0,
+                                     None))
         if self.local_mode:
             self._run_local(spec)
         else:
@@ -1780,6 +1791,7 @@ class CoreWorker:
             self._mark_ready(oid, in_store=True, contained=pins, size=payload, node=node)
         with self.lock:
             st.items[index] = ref
+            st.conn = conn
         self._wake_stream(tid)
 
     def _wake_stream(self, tid):
@@ -1800,6 +1812,9 @@ class CoreWorker:
                 return None
             while True:
                 if index in st.items:
+                    st.consumed = max(st.consumed, index + 1)
+                    if st.bp and st.conn is not None:  # let a throttled generator go on
+                        self.io.send(st.conn, _dumps((P.STREAM_ACK, tid, st.consumed)))
                     return st.items.pop(index)
                 if st.done:
                     if st.total is not None and index < st.total:
@@ -2011,6 +2026,13 @@ class CoreWorker:
             ac = self.actors.get(actor_id)
             if ac is None:
                 ac = self.actors[actor_id] = _ActorConn(actor_id)
+            limit = opts.get("max_pending_calls") or -1
+            if limit > 0 and len(ac.inflight) + len(ac.queue) >= limit:
+                from ray_amd.exceptions import PendingCallsLimitExceeded
+
+                raise PendingCallsLimitExceeded(
+                    f"The actor {actor_id.hex()} has {limit} pending calls from this caller "
+                    f"(max_pending_calls={limit}); wait for some of them before submitting more")
             ac.seq += 1
             seq = ac.seq
         spec = {
@@ -2020,6 +2042,8 @@ class CoreWorker:
             "retries": opts.get("max_task_retries", ac.max_task_retries),
             "concurrency_group": opts.get("concurrency_group"), "_holders": holders,
         }
+        if opts.get("enable_task_events", True) is False:
+            spec["no_events"] = True
         with self.lock:
             if streaming:
                 self.streams[tid] = _Stream()
@@ -2029,8 +2053,9 @@ class CoreWorker:
             self.task_specs[tid] = spec
         refs = [] if streaming else [ObjectRef(object_id_for_return(tid, i + 1), self.addr,
                                                _cw_obj=self) for i in range(nret)]
-        self.task_events.append((tid, spec["name"], time.time(), None, None, actor_id,
-                                 "SUBMITTED_TO_WORKER", P.ACTOR_TASK, self.job_id, 0, None))
+        if not spec.get("no_events"):
+            self.task_events.append((tid, spec["name"], time.time(), None, None, actor_id,
+                                     "SUBMITTED_TO_WORKER", P.ACTOR_TASK, self.job_id, 0, None))
         self._subscribe_actor(actor_id)
         # wait for owned pending args (ordering preserved: we block the caller)
         pend = [oid for oid, owner, inline in encoded[1] if owner == self.addr and inline is None]
@@ -2173,8 +2198,10 @@ class CoreWorker:
         t0 = time.time()
         extra = {}
         name = spec.get("name") or "task"
-        self.task_events.append((tid, name, t0, None, os.getpid(), spec.get("actor_id"), "RUNNING",
-                                 spec["type"], spec.get("job"), spec.get("attempt", 0), None))
+        if not spec.get("no_events"):
+            self.task_events.append((tid, name, t0, None, os.getpid(), spec.get("actor_id"),
+                                     "RUNNING", spec["type"], spec.get("job"),
+                                     spec.get("attempt", 0), None))
         try:
             if getattr(self, "setup_error", None):
                 from ray_amd.exceptions import RuntimeEnvSetupError
@@ -2228,10 +2255,11 @@ class CoreWorker:
                 self.running.pop(tid, None)
             self.current_task.tid = None
             self.current_task.spec = None
-        self.task_events.append((tid, name, t0, time.time(), os.getpid(),
-                                 spec.get("actor_id"), "FAILED" if extra.get("app_error")
-                                 else "FINISHED", spec["type"], spec.get("job"),
-                                 spec.get("attempt", 0), extra.get("exc_type")))
+        if not spec.get("no_events"):
+            self.task_events.append((tid, name, t0, time.time(), os.getpid(),
+                                     spec.get("actor_id"), "FAILED" if extra.get("app_error")
+                                     else "FINISHED", spec["type"], spec.get("job"),
+                                     spec.get("attempt", 0), extra.get("exc_type")))
         self._send_reply(conn, reply_to, tid, returns, extra)
 
     def _count_call(self, spec):
@@ -2359,6 +2387,33 @@ class CoreWorker:
         return [self._package_one(object_id_for_return(tid, i + 1), v, owner)
                 for i, v in enumerate(result)]
 
+    def _on_stream_ack(self, conn, msg):
+        tid, consumed = msg[1], msg[2]
+        cv = self._gen_ack_cv()
+        with cv:
+            if consumed > self._gen_acks.get(tid, 0):
+                self._gen_acks[tid] = consumed
+                cv.notify_all()
+
+    def _gen_ack_cv(self):
+        cv = getattr(self, "_gacv", None)
+        if cv is None:
+            self._gen_acks = {}
+            self._gacv = cv = threading.Condition()
+        return cv
+
+    def _gen_throttle(self, spec, produced):
+        """_generator_backpressure_num_objects: block the generator while ``produced`` -
+        consumed >= the threshold (the owner acks every item its caller takes)."""
+        bp = spec.get("gen_bp", 0)
+        if not bp:
+            return
+        tid = spec["tid"]
+        cv = self._gen_ack_cv()
+        with cv:
+            while produced - self._gen_acks.get(tid, 0) >= bp and not self._stopped:
+                cv.wait(0.5)
+
     def _run_generator(self, spec, fn, args, kwargs, conn, reply_to):
         tid = spec["tid"]
         owner = spec["owner"]
@@ -2377,6 +2432,7 @@ class CoreWorker:
                     ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
                     self.send(owner, (P.STREAM_ITEM, tid, i, ret, self.node_hex))
                     i += 1
+                    self._gen_throttle(spec, i)
             finally:
                 loop.close()
         else:
@@ -2384,7 +2440,11 @@ class CoreWorker:
                 ret = self._package_one(object_id_for_return(tid, i + 1), v, owner)
                 self.send(owner, (P.STREAM_ITEM, tid, i, ret, self.node_hex))
                 i += 1
+                self._gen_throttle(spec, i)
         self._last_gen_count = i
+        if spec.get("gen_bp"):
+            with self._gen_ack_cv():
+                self._gen_acks.pop(tid, None)
         return []
 
     # ---- actor side

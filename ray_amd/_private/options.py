@@ -64,6 +64,27 @@ def resources_of(opts: dict, actor: bool) -> dict:
     return res
 
 
+def parse_label_selector(sel: dict) -> dict:
+    """label_selector values (reference: ray.util.scheduling_strategies / label_selector):
+    "v" equals, "!v" not equal, "in(a,b)" one of, "!in(a,b)" none of -> the scheduler's
+    label constraint strings ("a,b" = one of, leading "!" = negated)."""
+    out = {}
+    for k, v in sel.items():
+        if not isinstance(k, str) or not isinstance(v, str):
+            raise ValueError(f"label_selector entries must be str -> str, got {k!r}: {v!r}")
+        neg = v.startswith("!")
+        body = v[1:] if neg else v
+        if body.startswith("in(") and body.endswith(")"):
+            vals = [x.strip() for x in body[3:-1].split(",") if x.strip()]
+            if not vals:
+                raise ValueError(f"empty in() in label_selector[{k!r}]")
+            body = ",".join(vals)
+        elif not body or "," in body or "(" in body:
+            raise ValueError(f"invalid label_selector value {v!r} for {k!r}")
+        out[k] = ("!" if neg else "") + body
+    return out
+
+
 def strategy_of(opts: dict):
     from ray_amd.util.placement_group import PlacementGroup
     from ray_amd.util.scheduling_strategies import (NodeAffinitySchedulingStrategy,
@@ -71,6 +92,11 @@ def strategy_of(opts: dict):
                                                     PlacementGroupSchedulingStrategy)
 
     st = opts.get("scheduling_strategy")
+    sel = opts.get("label_selector")
+    if sel:
+        if st not in (None, "DEFAULT"):
+            raise ValueError("label_selector cannot be combined with a scheduling_strategy")
+        return {"type": "node_label", "hard": parse_label_selector(sel), "soft": {}}
     pg = opts.get("placement_group")
     if pg is not None and pg != "default" and st is None:
         st = PlacementGroupSchedulingStrategy(pg, opts.get("placement_group_bundle_index", -1),

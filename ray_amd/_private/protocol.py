@@ -17,6 +17,8 @@ HELLO = 10
 TASK = 11
 TASK_REPLY = 12
 STREAM_ITEM = 13
+# owner -> executing worker: (STREAM_ACK, tid, items consumed) for generator backpressure
+STREAM_ACK = 14
 
 # task types
 NORMAL_TASK = 0

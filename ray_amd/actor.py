@@ -65,6 +65,11 @@ class ActorMethod:
                         f"'object.{self._name}()', try 'object.{self._name}.remote()'.")
 
 
+# key in an ActorHandle's method-metadata dict holding actor-level options that apply to
+# every call made through the handle (max_pending_calls, enable_task_events)
+_HANDLE_OPTS = "__ray_amd_handle_opts__"
+
+
 class ActorHandle:
     def __init__(self, actor_id: bytes, class_name: str, meta: dict, owner: str, *,
                  _register=True):
@@ -106,6 +111,12 @@ class ActorHandle:
              "concurrency_group": opts.get("concurrency_group")}
         if "max_task_retries" in opts:
             o["max_task_retries"] = opts["max_task_retries"]
+        # actor-level options the handle carries (serialised with it in _meta)
+        hopts = self._meta.get(_HANDLE_OPTS)
+        if hopts:
+            o.update(hopts)
+        if "enable_task_events" in opts:
+            o["enable_task_events"] = opts["enable_task_events"]
         refs = cw.submit_actor_task(self._actor_id, name, args, kwargs, o)
         if nret == "streaming":
             return refs
@@ -219,7 +230,12 @@ class ActorClass:
             return h
         if o["name"] or o["lifetime"] == "detached":
             cw.actor_escaped.add(aid)
-        return ActorHandle(aid, self._cls.__name__, self._meta, cw.addr)
+        meta = self._meta
+        hopts = {k: opts[k] for k in ("max_pending_calls", "enable_task_events")
+                 if opts.get(k) is not None and (k != "max_pending_calls" or opts[k] != -1)}
+        if hopts:
+            meta = dict(meta, **{_HANDLE_OPTS: hopts})
+        return ActorHandle(aid, self._cls.__name__, meta, cw.addr)
 
 
 def _default_lifetime():

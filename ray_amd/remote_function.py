@@ -74,6 +74,9 @@ class RemoteFunction:
             "retry_exceptions": opts.get("retry_exceptions", False),
             "runtime_env": opts.get("runtime_env"),
             "max_calls": opts.get("max_calls") or 0,
+            "enable_task_events": opts.get("enable_task_events", True),
+            "_generator_backpressure_num_objects":
+                opts.get("_generator_backpressure_num_objects") or 0,
         }
         name = opts.get("name") or getattr(self._function, "__qualname__", "task")
         refs = cw.submit_task(self._key(cw), args, kwargs, o, name)

@@ -137,3 +137,21 @@ def test_large_object_pulled_in_chunks(cluster3):
         assert arr.shape == (6 << 20,) and float(arr.sum()) == float(6 << 20)
     finally:
         cw.PULL_CHUNK = old
+
+
+def test_label_selector(cluster3):
+    """label_selector (reference: ray.remote(label_selector=...)): equality, negation,
+    in() / !in() lists; a node without the label matches a negated selector."""
+    c, n1, n2 = cluster3
+    head = c.head_node.node_id
+    assert ray.get(where.options(label_selector={"zone": "z2"}).remote()) == n2.node_id
+    assert ray.get(where.options(label_selector={"zone": "in(z1,z9)"}).remote()) == n1.node_id
+    got = {ray.get(where.options(label_selector={"zone": "!z1"}).remote()) for _ in range(8)}
+    assert n1.node_id not in got and got <= {n2.node_id, head}
+    got = {ray.get(where.options(label_selector={"zone": "!in(z1,z2)"}).remote())
+           for _ in range(4)}
+    assert got == {head}
+    with pytest.raises(ValueError):
+        where.options(label_selector={"zone": "in()"}).remote()
+    with pytest.raises(ValueError):
+        where.options(label_selector={"zone": "z1"}, scheduling_strategy="SPREAD").remote()
