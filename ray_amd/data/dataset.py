@@ -715,7 +715,8 @@ class Dataset:
 
         refs = (r for r, _ in X.execute(self._plan))
         yield from batch_blocks(refs, batch_size, batch_format, drop_last,
-                                local_shuffle_buffer_size, local_shuffle_seed)
+                                local_shuffle_buffer_size, local_shuffle_seed,
+                                prefetch=prefetch_batches)
 
     def iter_rows(self, **kw):
         for r, _ in X.execute(self._plan):
@@ -732,7 +733,8 @@ class Dataset:
         yield from torch_batches(self.iter_batches(
             batch_size=batch_size, drop_last=drop_last,
             local_shuffle_buffer_size=local_shuffle_buffer_size,
-            local_shuffle_seed=local_shuffle_seed), dtypes, device, collate_fn, pin_memory)
+            local_shuffle_seed=local_shuffle_seed, prefetch_batches=prefetch_batches),
+            dtypes, device, collate_fn, pin_memory)
 
     def to_torch(self, **kw):
         return self.iter_torch_batches(**kw)

@@ -19,7 +19,60 @@ from ray_amd._native import _core
 from . import block as B
 
 
-def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer, seed):
+def _fetch(ref):
+    if isinstance(ref, tuple):  # (block ref, start row, end row): an equal split's share
+        r0, a, b = ref
+        return B.slice_block(ray.get(r0), a, b)
+    return ray.get(ref)
+
+
+def _prefetched_blocks(block_refs, depth):
+    """Blocks of ``block_refs`` fetched (ray.get + deserialise) ``depth`` ahead on a
+    background thread, so the fetch of the next block overlaps the consumer's work on this
+    one (reference: iter_batches(prefetch_batches=...)). depth 0: fetched inline."""
+    if depth <= 0:
+        for ref in block_refs:
+            yield _fetch(ref)
+        return
+    import queue
+    import threading
+
+    q = queue.Queue(maxsize=depth)
+    stop = threading.Event()
+    _END = object()
+
+    def run():
+        try:
+            for ref in block_refs:
+                blk = _fetch(ref)
+                while not stop.is_set():
+                    try:
+                        q.put((True, blk), timeout=0.2)
+                        break
+                    except queue.Full:
+                        continue
+                if stop.is_set():
+                    return
+            q.put((True, _END))
+        except BaseException as e:  # noqa: BLE001  (re-raised in the consumer)
+            q.put((False, e))
+
+    t = threading.Thread(target=run, daemon=True, name="ray_amd-data-prefetch")
+    t.start()
+    try:
+        while True:
+            ok, item = q.get()
+            if not ok:
+                raise item
+            if item is _END:
+                return
+            yield item
+    finally:
+        stop.set()
+
+
+def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer, seed,
+                 prefetch=0):
     rng = np.random.default_rng(seed)
     buf = []
     buffered = 0
@@ -29,13 +82,7 @@ def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer
     def emit(blk):
         return B.to_batch(blk, fmt)
 
-    pending = collections.deque()
-    for ref in block_refs:
-        if isinstance(ref, tuple):  # (block ref, start row, end row): an equal split's share
-            r0, a, b = ref
-            blk = B.slice_block(ray.get(r0), a, b)
-        else:
-            blk = ray.get(ref)
+    for blk in _prefetched_blocks(block_refs, prefetch):
         if B.num_rows(blk) == 0:
             continue
         if bs is None:
@@ -53,7 +100,6 @@ def batch_blocks(block_refs, batch_size, batch_format, drop_last, shuffle_buffer
             buf = [rest] if B.num_rows(rest) else []
             buffered = B.num_rows(rest)
             yield emit(out)
-    pending  # noqa: B018
     if buf and bs is not None:
         cat = B.concat(buf)
         if shuffle_buffer:
@@ -315,9 +361,11 @@ class StreamSplitIterator(DataIterator):
             yield r[0]
 
     def iter_batches(self, *, batch_size=256, batch_format="default", drop_last=False,
-                     local_shuffle_buffer_size=None, local_shuffle_seed=None, **kw):
+                     local_shuffle_buffer_size=None, local_shuffle_seed=None, prefetch_batches=1,
+                     **kw):
         return batch_blocks(self._blocks(), batch_size, batch_format, drop_last,
-                            local_shuffle_buffer_size, local_shuffle_seed)
+                            local_shuffle_buffer_size, local_shuffle_seed,
+                            prefetch=prefetch_batches)
 
     def iter_rows(self, **kw):
         for ref in self._blocks():
@@ -328,10 +376,11 @@ class StreamSplitIterator(DataIterator):
 
     def iter_torch_batches(self, *, batch_size=256, dtypes=None, device="auto", collate_fn=None,
                            drop_last=False, local_shuffle_buffer_size=None,
-                           local_shuffle_seed=None, **kw):
+                           local_shuffle_seed=None, prefetch_batches=1, **kw):
         return torch_batches(self.iter_batches(batch_size=batch_size, drop_last=drop_last,
                                                local_shuffle_buffer_size=local_shuffle_buffer_size,
-                                               local_shuffle_seed=local_shuffle_seed),
+                                               local_shuffle_seed=local_shuffle_seed,
+                                               prefetch_batches=prefetch_batches),
                              dtypes, device, collate_fn)
 
     def __reduce__(self):
