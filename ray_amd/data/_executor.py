@@ -170,7 +170,13 @@ class ExecutionOptions:
         self.verbose_progress = verbose_progress
 
 
-def _task_opts(res):
+# ray_remote_args of map-like operators passed through to the tasks / actors they launch
+PASS_THROUGH_REMOTE_ARGS = ("memory", "max_retries", "retry_exceptions", "scheduling_strategy",
+                            "runtime_env", "accelerator_type", "label_selector",
+                            "max_restarts", "max_task_retries")
+
+
+def _task_opts(res, actor=False):
     o = {}
     if "num_cpus" in res:
         o["num_cpus"] = res["num_cpus"]
@@ -178,6 +184,14 @@ def _task_opts(res):
         o["num_gpus"] = res["num_gpus"]
     if res.get("resources"):
         o["resources"] = res["resources"]
+    for k in PASS_THROUGH_REMOTE_ARGS:
+        if res.get(k) is None:
+            continue
+        if actor and k in ("max_retries", "retry_exceptions"):
+            continue
+        if not actor and k in ("max_restarts", "max_task_retries"):
+            continue
+        o[k] = res[k]
     return o
 
 
@@ -361,7 +375,7 @@ class _ActorPoolOp(_Op):
         self.fns = st.fns
         self.make_fn = st.make_fn
         self.cls = ray.remote(_MapWorker)
-        self.opts = _task_opts(self.res)
+        self.opts = _task_opts(self.res, actor=True)
         self.actors = {}  # idx -> handle (ready)
         self.starting = {}  # ready ref -> (idx, handle)
         self.load = {}

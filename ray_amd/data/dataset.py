@@ -62,32 +62,129 @@ def _batcher(fn, batch_size, batch_format, fn_args, fn_kwargs, zero_copy=False):
     return run
 
 
-def _row_map(fn):
+def _row_map(fn, a=(), k=None):
+    k = k or {}
+
     def run(blk):
-        return B.from_rows([fn(r) for r in B.to_rows(blk)])
+        return B.from_rows([fn(r, *a, **k) for r in B.to_rows(blk)])
 
     return run
 
 
-def _row_flat_map(fn):
+def _row_flat_map(fn, a=(), k=None):
+    k = k or {}
+
     def run(blk):
         rows = []
         for r in B.to_rows(blk):
-            rows.extend(fn(r))
+            rows.extend(fn(r, *a, **k))
         return B.from_rows(rows)
 
     return run
 
 
-def _row_filter(fn):
+def _row_filter(fn, a=(), k=None):
+    k = k or {}
+
     def run(blk):
         n = B.num_rows(blk)
         if n == 0:
             return blk
-        keep = np.fromiter((bool(fn(r)) for r in B.to_rows(blk)), dtype=bool, count=n)
+        keep = np.fromiter((bool(fn(r, *a, **k)) for r in B.to_rows(blk)), dtype=bool,
+                           count=n)
         return B.take_idx(blk, np.nonzero(keep)[0])
 
     return run
+
+
+def _compile_expr(expr: str):
+    """A filter expression (reference: Dataset.filter(expr="...")) over column names,
+    constants, comparisons, and/or/not, arithmetic and `in` lists, compiled to a vectorised
+    numpy predicate over a batch. Anything else (calls, attributes, subscripts) is refused."""
+    import ast
+    import operator as op
+
+    tree = ast.parse(expr, mode="eval")
+    bins = {ast.Add: op.add, ast.Sub: op.sub, ast.Mult: op.mul, ast.Div: op.truediv,
+            ast.Mod: op.mod, ast.FloorDiv: op.floordiv, ast.Pow: op.pow}
+    cmps = {ast.Eq: op.eq, ast.NotEq: op.ne, ast.Lt: op.lt, ast.LtE: op.le, ast.Gt: op.gt,
+            ast.GtE: op.ge}
+
+    def ev(n, b):
+        if isinstance(n, ast.Expression):
+            return ev(n.body, b)
+        if isinstance(n, ast.Name):
+            if n.id not in b:
+                raise KeyError(f"filter expression: unknown column {n.id!r}")
+            return np.asarray(b[n.id])
+        if isinstance(n, ast.Constant):
+            return n.value
+        if isinstance(n, (ast.List, ast.Tuple)):
+            return [ev(e, b) for e in n.elts]
+        if isinstance(n, ast.BoolOp):
+            vals = [np.asarray(ev(v, b), dtype=bool) for v in n.values]
+            out = vals[0]
+            for v in vals[1:]:
+                out = (out & v) if isinstance(n.op, ast.And) else (out | v)
+            return out
+        if isinstance(n, ast.UnaryOp):
+            v = ev(n.operand, b)
+            if isinstance(n.op, ast.Not):
+                return ~np.asarray(v, dtype=bool)
+            if isinstance(n.op, ast.USub):
+                return -v
+            if isinstance(n.op, ast.UAdd):
+                return v
+        if isinstance(n, ast.BinOp) and type(n.op) in bins:
+            return bins[type(n.op)](ev(n.left, b), ev(n.right, b))
+        if isinstance(n, ast.Compare):
+            left = ev(n.left, b)
+            out = None
+            for o, rn in zip(n.ops, n.comparators):
+                right = ev(rn, b)
+                if isinstance(o, (ast.In, ast.NotIn)):
+                    r = np.isin(left, np.asarray(right, dtype=object)
+                                if any(isinstance(x, str) for x in right) else right)
+                    r = ~r if isinstance(o, ast.NotIn) else r
+                elif type(o) in cmps:
+                    r = cmps[type(o)](left, right)
+                else:
+                    raise ValueError(f"filter expression: unsupported comparison {ast.dump(o)}")
+                out = r if out is None else (out & r)
+                left = right
+            return out
+        raise ValueError(f"filter expression: unsupported syntax {type(n).__name__} in {expr!r}")
+
+    def run(blk):
+        n = B.num_rows(blk)
+        if n == 0:
+            return blk
+        keep = np.broadcast_to(np.asarray(ev(tree, B.to_batch(blk, "numpy")), dtype=bool),
+                               (n,))
+        return B.take_idx(blk, np.nonzero(keep)[0])
+
+    return run
+
+
+def _remote_res(num_cpus, num_gpus, ray_remote_args):
+    """Stage resources + the remote args the executor passes through to its tasks/actors
+    (memory, max_retries, scheduling_strategy, runtime_env, ...). Unknown keys raise."""
+    from ._executor import PASS_THROUGH_REMOTE_ARGS
+
+    res = {"num_cpus": num_cpus if num_cpus is not None else 1}
+    if num_gpus:
+        res["num_gpus"] = num_gpus
+    for k, v in (ray_remote_args or {}).items():
+        if k == "resources":
+            if v:
+                res["resources"] = v
+        elif k in PASS_THROUGH_REMOTE_ARGS:
+            res[k] = v
+        elif k in ("num_cpus", "num_gpus"):
+            res[k] = v
+        else:
+            raise ValueError(f"unsupported ray_remote_args key {k!r} for a Data operator")
+    return res
 
 
 def _make_callable_class(cls, batch_size, batch_format, ctor_args, ctor_kwargs, fn_args,
@@ -363,11 +460,7 @@ class Dataset:
                     num_gpus=None, concurrency=None, **ray_remote_args) -> "Dataset":
         if batch_size == "default":
             batch_size = 1024
-        res = {"num_cpus": num_cpus if num_cpus is not None else 1}
-        if num_gpus:
-            res["num_gpus"] = num_gpus
-        if ray_remote_args.get("resources"):
-            res["resources"] = ray_remote_args["resources"]
+        res = _remote_res(num_cpus, num_gpus, ray_remote_args)
         is_class = isinstance(fn, type)
         if is_class or isinstance(compute, ActorPoolStrategy) or (concurrency is not None and
                                                                   is_class):
@@ -393,34 +486,49 @@ class Dataset:
                                   else None))
 
     def map(self, fn, *, compute=None, num_cpus=None, num_gpus=None, concurrency=None,
-            **kw) -> "Dataset":
+            fn_args=None, fn_kwargs=None, fn_constructor_args=None, fn_constructor_kwargs=None,
+            **ray_remote_args) -> "Dataset":
         if isinstance(fn, type):
             cls = fn
+
+            fa, fk = tuple(fn_args or ()), dict(fn_kwargs or {})
 
             class _RowCls:
                 def __init__(self, *a, **k):
                     self.inner = cls(*a, **k)
 
                 def __call__(self, batch):
-                    return B.from_rows([self.inner(r) for r in B.to_rows(batch)])
+                    return B.from_rows([self.inner(r, *fa, **fk) for r in B.to_rows(batch)])
 
             return self.map_batches(_RowCls, batch_size=None, compute=compute, num_cpus=num_cpus,
                                     num_gpus=num_gpus, concurrency=concurrency,
                                     zero_copy_batch=True,
-                                    fn_constructor_args=kw.get("fn_constructor_args"),
-                                    fn_constructor_kwargs=kw.get("fn_constructor_kwargs"))
-        res = {"num_cpus": num_cpus if num_cpus is not None else 1}
-        if num_gpus:
-            res["num_gpus"] = num_gpus
-        return self._with(X.Stage("task", [_row_map(fn)], resources=res, name="Map"))
+                                    fn_constructor_args=fn_constructor_args,
+                                    fn_constructor_kwargs=fn_constructor_kwargs,
+                                    **ray_remote_args)
+        return self._row_stage(_row_map(fn, fn_args or (), fn_kwargs), "Map", num_cpus,
+                               num_gpus, concurrency, ray_remote_args)
 
-    def flat_map(self, fn, **kw) -> "Dataset":
-        return self._with(X.Stage("task", [_row_flat_map(fn)], resources={"num_cpus": 1},
-                                  name="FlatMap"))
+    def _row_stage(self, f, name, num_cpus, num_gpus, concurrency, ray_remote_args):
+        res = _remote_res(num_cpus, num_gpus, ray_remote_args)
+        return self._with(X.Stage("task", [f], resources=res, name=name,
+                                  concurrency=concurrency if isinstance(concurrency, int)
+                                  else None))
 
-    def filter(self, fn=None, *, expr=None, **kw) -> "Dataset":
-        return self._with(X.Stage("task", [_row_filter(fn)], resources={"num_cpus": 1},
-                                  name="Filter"))
+    def flat_map(self, fn, *, num_cpus=None, num_gpus=None, concurrency=None, fn_args=None,
+                 fn_kwargs=None, **ray_remote_args) -> "Dataset":
+        return self._row_stage(_row_flat_map(fn, fn_args or (), fn_kwargs), "FlatMap",
+                               num_cpus, num_gpus, concurrency, ray_remote_args)
+
+    def filter(self, fn=None, *, expr=None, num_cpus=None, num_gpus=None, concurrency=None,
+               fn_args=None, fn_kwargs=None, **ray_remote_args) -> "Dataset":
+        """Keep rows where ``fn(row)`` is true, or where the column expression ``expr``
+        (e.g. ``"id > 5 and label in ['a', 'b']"``) holds, evaluated per batch with numpy."""
+        if (fn is None) == (expr is None):
+            raise ValueError("filter takes exactly one of fn or expr")
+        f = _compile_expr(expr) if expr is not None else \
+            _row_filter(fn, fn_args or (), fn_kwargs)
+        return self._row_stage(f, "Filter", num_cpus, num_gpus, concurrency, ray_remote_args)
 
     def add_column(self, col, fn, **kw) -> "Dataset":
         def f(batch):
