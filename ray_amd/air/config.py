@@ -23,7 +23,16 @@ class ScalingConfig:
             r["CPU"] = 1
         if self.use_gpu and "GPU" not in r:
             r["GPU"] = 1
+        if self.accelerator_type:  # workers only on nodes with that accelerator
+            r[f"accelerator_type:{self.accelerator_type}"] = 0.001
         return {k: v for k, v in r.items() if v}
+
+    @property
+    def _trainer_bundle(self) -> dict | None:
+        """trainer_resources: reserved for the run's coordinator (the driver-side trainer)
+        as the placement group's first bundle; None when not requested."""
+        tr = {k: v for k, v in (self.trainer_resources or {}).items() if v}
+        return tr or None
 
     @property
     def num_gpus_per_worker(self):
@@ -34,7 +43,9 @@ class ScalingConfig:
         return self._resources_per_worker_not_none.get("CPU", 0)
 
     def as_placement_group_factory(self):
-        return [self._resources_per_worker_not_none for _ in range(self.num_workers)]
+        workers = [self._resources_per_worker_not_none for _ in range(self.num_workers)]
+        tb = self._trainer_bundle
+        return ([tb] if tb else []) + workers
 
     @property
     def total_resources(self):

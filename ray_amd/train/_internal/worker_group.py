@@ -90,9 +90,14 @@ class RayTrainWorker:
 
 class WorkerGroup:
     def __init__(self, num_workers: int, resources_per_worker: dict,
-                 placement_strategy: str = "PACK", actor_cls=RayTrainWorker):
+                 placement_strategy: str = "PACK", actor_cls=RayTrainWorker,
+                 trainer_resources: dict | None = None):
         self.num_workers = num_workers
         bundles = [dict(resources_per_worker) for _ in range(num_workers)]
+        # ScalingConfig.trainer_resources: a first bundle held for the coordinator
+        self._first = 1 if trainer_resources else 0
+        if trainer_resources:
+            bundles = [dict(trainer_resources)] + bundles
         self.pg = placement_group(bundles, strategy=placement_strategy)
         if not self.pg.wait(timeout_seconds=600):
             remove_placement_group(self.pg)
@@ -103,7 +108,7 @@ class WorkerGroup:
         other = {k: v for k, v in resources_per_worker.items() if k not in ("CPU", "GPU")}
         self.workers = []
         for i in range(num_workers):
-            st = PlacementGroupSchedulingStrategy(self.pg, i)
+            st = PlacementGroupSchedulingStrategy(self.pg, i + self._first)
             # GPU ranks on one node see each other's devices (set at process spawn)
             st._share_gpus = bool(num_gpus)
             self.workers.append(remote_cls.options(

@@ -248,7 +248,7 @@ class DataParallelTrainer:
     def _run_once(self, trial_dir, name, ckpt, ckpt_index, mgr, history, on_report=None):
         sc = self.scaling_config
         wg = WorkerGroup(sc.num_workers, sc._resources_per_worker_not_none,
-                         sc.placement_strategy)
+                         sc.placement_strategy, trainer_resources=sc._trainer_bundle)
         backend = self.backend_config.backend_cls()
         try:
             try:
