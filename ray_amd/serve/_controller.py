@@ -343,6 +343,8 @@ class ServeController:
         h = cls.options(**opts).remote(st.name, st.app, spec["callable"], spec["init_args"],
                                        spec["init_kwargs"], spec.get("user_config"), rid,
                                        spec["is_function"], spec.get("asgi_app"))
+        if spec.get("logging_config"):  # ordered before the controller's health checks
+            h.set_logging.remote(spec["logging_config"])
         st.starting[rid] = h
         self._spawn(self._await_started(st, rid, h))
         return rid
@@ -379,8 +381,9 @@ class ServeController:
 
     async def _drain_and_kill(self, st, rid, h):
         try:
-            await asyncio.wait_for(h.prepare_for_shutdown.remote(),
-                                   st.spec.get("graceful_shutdown_timeout_s", 5))
+            await asyncio.wait_for(
+                h.prepare_for_shutdown.remote(st.spec.get("graceful_shutdown_wait_loop_s", 2.0)),
+                st.spec.get("graceful_shutdown_timeout_s", 5))
         except BaseException:  # noqa: BLE001
             pass
         await self._kill_replica(st, rid, h)

@@ -249,6 +249,8 @@ class Replica:
         self.ongoing += 1
         self.total += 1
         token = context._set_request_context(multiplexed_model_id)
+        t0 = time.perf_counter() if getattr(self, "access_log", False) else None
+        status = "OK"
         try:
             args, kwargs = await _resolve_args(args, kwargs)
             if self.is_function:
@@ -263,9 +265,18 @@ class Replica:
             elif inspect.isasyncgen(r):
                 r = [x async for x in r]
             return r
+        except BaseException:
+            status = "ERROR"
+            raise
         finally:
             context._reset_request_context(token)
             self.ongoing -= 1
+            if t0 is not None:  # logging_config enable_access_log: one line per request
+                import logging
+
+                logging.getLogger("ray.serve").info(
+                    "%s %s %s %.1fms", self.deployment_name, method_name or "__call__",
+                    status, (time.perf_counter() - t0) * 1e3)
 
     async def handle_http(self, scope, body):
         self.ongoing += 1
@@ -337,8 +348,21 @@ class Replica:
         finally:
             self.ongoing -= 1
 
-    async def prepare_for_shutdown(self):
+    def set_logging(self, cfg: dict):
+        """Deployment logging_config: the replica's Python log level (root and the user
+        code's loggers) and whether it logs one access line per request."""
+        import logging
+
+        logging.getLogger().setLevel(cfg.get("log_level", "INFO"))
+        self.access_log = bool(cfg.get("enable_access_log", True))
+        return True
+
+    async def prepare_for_shutdown(self, wait_loop_s: float = 2.0):
+        """Wait until no request is in flight, checking every ``wait_loop_s`` seconds
+        (graceful_shutdown_wait_loop_s); the controller bounds the whole wait by
+        graceful_shutdown_timeout_s."""
+        self.draining = True
         while self.ongoing > 0:
-            await asyncio.sleep(0.01)
+            await asyncio.sleep(wait_loop_s)
         f = getattr(self.obj, "__del__", None)
         return True

@@ -107,14 +107,39 @@ class gRPCOptions:
         self.host = host
 
 
+def _logging_config(cfg):
+    """serve LoggingConfig / dict -> {"log_level": LEVEL}; the replica applies it to its
+    Python loggers (reference: serve/schema.py LoggingConfig)."""
+    if cfg is None:
+        return None
+    d = dict(getattr(cfg, "__dict__", cfg)) if not isinstance(cfg, dict) else dict(cfg)
+    level = str(d.get("log_level", "INFO")).upper()
+    import logging
+
+    if not isinstance(logging.getLevelName(level), int):
+        raise ValueError(f"invalid log_level {level!r}")
+    unknown = set(d) - {"log_level", "encoding", "logs_dir", "enable_access_log"}
+    if unknown:
+        raise ValueError(f"unsupported logging_config keys: {sorted(unknown)}")
+    return {"log_level": level, "enable_access_log": bool(d.get("enable_access_log", True))}
+
+
 class Deployment:
     def __init__(self, func_or_class, name, num_replicas=1, ray_actor_options=None,
                  user_config=None, max_ongoing_requests=100, autoscaling_config=None,
                  route_prefix=None, graceful_shutdown_timeout_s=5.0, health_check_period_s=10.0,
                  version=None, max_queued_requests=-1, health_check_timeout_s=30.0,
                  placement_group_bundles=None, placement_group_strategy=None,
-                 max_replicas_per_node=None, **kw):
+                 max_replicas_per_node=None, graceful_shutdown_wait_loop_s=2.0,
+                 logging_config=None, **kw):
         from ray_amd.serve.config import normalize_autoscaling_config
+
+        if kw:
+            raise TypeError(f"unsupported deployment option(s): {sorted(kw)}")
+        if graceful_shutdown_wait_loop_s <= 0:
+            raise ValueError("graceful_shutdown_wait_loop_s must be > 0")
+        self.graceful_shutdown_wait_loop_s = graceful_shutdown_wait_loop_s
+        self.logging_config = _logging_config(logging_config)
 
         self.func_or_class = func_or_class
         self.name = name
@@ -157,6 +182,8 @@ class Deployment:
                  placement_group_strategy=self.placement_group_strategy,
                  max_replicas_per_node=self.max_replicas_per_node,
                  max_queued_requests=self.max_queued_requests,
+                 graceful_shutdown_wait_loop_s=self.graceful_shutdown_wait_loop_s,
+                 logging_config=self.logging_config,
                  version=self.version, name=self.name)
         if "max_concurrent_queries" in kw:
             kw["max_ongoing_requests"] = kw.pop("max_concurrent_queries")
@@ -183,9 +210,12 @@ def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_opti
                autoscaling_config=None, route_prefix=None, graceful_shutdown_timeout_s=5.0,
                health_check_period_s=10.0, version=None, max_queued_requests=-1,
                health_check_timeout_s=30.0, placement_group_bundles=None,
-               placement_group_strategy=None, max_replicas_per_node=None, **kw):
+               placement_group_strategy=None, max_replicas_per_node=None,
+               graceful_shutdown_wait_loop_s=2.0, logging_config=None, **kw):
     if max_concurrent_queries is not None:
         max_ongoing_requests = max_concurrent_queries
+    if kw:
+        raise TypeError(f"unsupported deployment option(s): {sorted(kw)}")
 
     def deco(fc):
         return Deployment(fc, name or fc.__name__, num_replicas, ray_actor_options, user_config,
@@ -195,7 +225,9 @@ def deployment(_func_or_class=None, *, name=None, num_replicas=1, ray_actor_opti
                           health_check_timeout_s=health_check_timeout_s,
                           placement_group_bundles=placement_group_bundles,
                           placement_group_strategy=placement_group_strategy,
-                          max_replicas_per_node=max_replicas_per_node)
+                          max_replicas_per_node=max_replicas_per_node,
+                          graceful_shutdown_wait_loop_s=graceful_shutdown_wait_loop_s,
+                          logging_config=logging_config)
 
     if _func_or_class is not None and callable(_func_or_class):
         return deco(_func_or_class)
@@ -259,6 +291,8 @@ def _build(app: Application, app_name, specs: dict):
         "max_queued_requests": dep.max_queued_requests,
         "asgi_app": cloudpickle.dumps(asgi) if asgi is not None else None,
         "graceful_shutdown_timeout_s": dep.graceful_shutdown_timeout_s,
+        "graceful_shutdown_wait_loop_s": dep.graceful_shutdown_wait_loop_s,
+        "logging_config": dep.logging_config,
         "health_check_period_s": dep.health_check_period_s,
         "health_check_timeout_s": dep.health_check_timeout_s,
         "placement_group_bundles": dep.placement_group_bundles,

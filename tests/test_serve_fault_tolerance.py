@@ -63,3 +63,30 @@ def test_replica_killed_mid_request_is_retried_and_replaced(cluster):
     after = [rid for rid, _ in ray.get(ctrl.get_replicas.remote("ft", "Slow"))[1]]
     assert victim_id not in after and len(after) == 2
     serve.delete("ft")
+
+
+def test_deployment_options_validated_and_graceful_wait_loop(cluster):
+    with pytest.raises(TypeError, match="unsupported deployment option"):
+        serve.deployment(lambda: 1, no_such_option=3)
+    with pytest.raises(ValueError):
+        serve.deployment(lambda: 1, logging_config={"log_level": "LOUD"})
+
+    @serve.deployment(graceful_shutdown_wait_loop_s=0.05, graceful_shutdown_timeout_s=10,
+                      logging_config={"log_level": "DEBUG", "enable_access_log": True})
+    class Busy:
+        def __call__(self, t):
+            import logging
+
+            time.sleep(t)
+            return logging.getLogger().getEffectiveLevel()
+
+    h = serve.run(Busy.bind(), name="gw", route_prefix="/gw")
+    import logging
+
+    assert h.remote(0).result() == logging.DEBUG  # the replica applied logging_config
+    slow = h.remote(1.0)
+    time.sleep(0.2)
+    t0 = time.time()
+    serve.delete("gw")  # drains: the in-flight request still completes
+    assert slow.result(timeout_s=15) == logging.DEBUG
+    assert time.time() - t0 < 10
