@@ -99,9 +99,23 @@ class AlgorithmConfig:
         return self.env_runners(num_env_runners=num_rollout_workers,
                                 num_envs_per_env_runner=num_envs_per_worker, **kw)
 
+    # training() keys the learners read without a config default (RLlib options of this
+    # framework: the learner group's collective backend, HIP-graph capture of the learner
+    # update, bf16 CPU inference in env runners, per-learner batch)
+    _TRAINING_EXTRA = frozenset({"learner_backend", "learner_cuda_graph", "env_runner_bf16",
+                                 "train_batch_size_per_learner", "learner_class", "model",
+                                 "optimizer", "grad_clip_by"})
+
     def training(self, **kw):
+        """Set training hyperparameters. Keys must be known to this algorithm's config
+        (its defaults, the reference's old names, or _TRAINING_EXTRA): a typo raises instead
+        of being silently ignored."""
         aliases = {"sgd_minibatch_size": "minibatch_size", "num_sgd_iter": "num_epochs",
                    "lambda": "lambda_"}
+        known = set(vars(self)) | self._TRAINING_EXTRA
+        unknown = sorted(k for k in kw if aliases.get(k, k) not in known)
+        if unknown:
+            raise ValueError(f"{type(self).__name__}.training() got unknown key(s) {unknown}")
         for k, v in kw.items():
             if v is None:
                 continue

@@ -84,3 +84,10 @@ def test_part_builders_serialize_overrides():
     with pytest.raises(KeyError):
         PPOConfig.overrides(no_such_key=1)
     assert c.get_torch_compile_worker_config() == {"torch_compile": False}
+
+
+def test_training_rejects_unknown_keys():
+    c = PPOConfig().training(lr=1e-3, lambda_=0.9, clip_param=0.3, num_sgd_iter=4)
+    assert c.num_epochs == 4 and c.clip_param == 0.3
+    with pytest.raises(ValueError, match="lamda"):
+        c.training(lamda=0.5)
