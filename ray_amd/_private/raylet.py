@@ -532,11 +532,12 @@ class Raylet:
         d = os.path.join(self.session_dir, "logs")
         os.makedirs(d, exist_ok=True)
         dedup = self._dedup()
+        to_driver = os.environ.get("RAY_AMD_LOG_TO_DRIVER", "1") != "0"
         for pipe, ext, out in ((w.proc.stdout, "out", sys.stdout), (w.proc.stderr, "err",
                                                                        sys.stderr)):
             path = os.path.join(d, f"worker-{w.token}-{w.pid}.{ext}")
 
-            def pump(pipe=pipe, path=path, out=out):
+            def pump(pipe=pipe, path=path, out=out if to_driver else None):
                 # never stop draining the pipe: a worker whose pipe fills (64 KB) blocks on
                 # its next print. A failed file write (ENOSPC, ...) drops the file copy
                 # and keeps forwarding to the terminal.
@@ -554,6 +555,8 @@ class Raylet:
                             except OSError:
                                 pass
                             f = None
+                    if out is None:  # init(log_to_driver=False): files only
+                        continue
                     for text in dedup.feed(line, w.pid, out):
                         try:
                             out.buffer.write(text)

@@ -69,8 +69,43 @@ def _default_object_store_memory():
     return int(max(256 << 20, min(0.3 * total, 0.8 * shm_free, 200 << 30)))
 
 
+# _system_config keys this runtime honours, as the RAY_<key> variables the raylet reads
+# (reference names: memory monitor and worker-killing policy)
+SYSTEM_CONFIG_KEYS = ("memory_usage_threshold", "memory_monitor_refresh_ms",
+                      "min_memory_free_bytes", "worker_killing_policy")
+
+
+def _node_env(system_config, log_to_driver, logging_level) -> dict:
+    env = {}
+    for k, v in (system_config or {}).items():
+        if k not in SYSTEM_CONFIG_KEYS:
+            raise ValueError(f"unsupported _system_config key {k!r}; supported: "
+                             f"{list(SYSTEM_CONFIG_KEYS)}")
+        env[f"RAY_{k}"] = str(v)
+    if not log_to_driver:
+        env["RAY_AMD_LOG_TO_DRIVER"] = "0"  # worker output only in <session>/logs
+    if logging_level is not None:
+        env["RAY_AMD_LOGGING_LEVEL"] = str(logging_level)
+    return env
+
+
+def _configure_logging(level, fmt):
+    """init(logging_level=..., logging_format=...): the ray_amd logger's level and format in
+    this driver (workers get the level through RAY_AMD_LOGGING_LEVEL)."""
+    import logging
+
+    lg = logging.getLogger("ray_amd")
+    if level is not None:
+        lg.setLevel(level if isinstance(level, int) else str(level).upper())
+    if fmt is not None:
+        h = logging.StreamHandler()
+        h.setFormatter(logging.Formatter(fmt))
+        lg.handlers = [h]
+        lg.propagate = False
+
+
 def _start_raylet(session_dir, num_cpus, num_gpus, resources, object_store_memory, labels,
-                  head=True, detach_output=False):
+                  head=True, detach_output=False, extra_env=None):
     os.makedirs(session_dir, exist_ok=True)
     store_path = "/dev/shm/ray_amd_" + os.path.basename(session_dir)
     cmd = [sys.executable, "-m", "ray_amd._private.raylet", "--session-dir", session_dir,
@@ -83,6 +118,7 @@ def _start_raylet(session_dir, num_cpus, num_gpus, resources, object_store_memor
     if head:
         cmd.append("--head")
     env = dict(os.environ)
+    env.update(extra_env or {})
     pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
                                     else "")
@@ -122,6 +158,20 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
     from .core_worker import CoreWorker
     from .ids import random_bytes
 
+    unknown = sorted(k for k in kwargs if not k.startswith("_"))
+    if unknown:
+        raise TypeError(f"init() got unexpected keyword argument(s) {unknown}")
+    for k in kwargs:  # private reference knobs with no meaning here (_redis_password, ...)
+        import warnings
+
+        warnings.warn(f"ray_amd.init: internal option {k} has no effect", stacklevel=2)
+    if configure_logging:
+        _configure_logging(logging_level, logging_format)
+    node_env = _node_env(_system_config, log_to_driver, logging_level)
+    if storage is not None:
+        # default storage of Train / Tune / Workflow results (RunConfig.storage_path)
+        os.environ["RAY_AMD_STORAGE"] = str(storage)
+
     if job_config is not None:
         namespace = namespace or job_config.ray_namespace
         if runtime_env is None and job_config.runtime_env:
@@ -154,7 +204,7 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
                 _temp_dir, os.path.basename(new_session_dir()))
             osm = int(object_store_memory or _default_object_store_memory())
             proc, raylet_addr = _start_raylet(session, num_cpus, num_gpus, resources, osm,
-                                              labels)
+                                              labels, extra_env=node_env)
             global_worker.raylet_proc = proc
             global_worker.node_started_here = True
             if include_dashboard:
@@ -163,6 +213,9 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
                 global_worker.dashboard_proc, global_worker.dashboard_url = start_dashboard(
                     session, dashboard_host or "127.0.0.1", int(dashboard_port or 8265))
         else:
+            if _system_config:
+                raise ValueError("_system_config applies when init() starts a new node, not "
+                                 "when connecting to an existing cluster")
             if address == "auto":
                 if not os.path.exists(CURRENT_CLUSTER_FILE):
                     raise ConnectionError("Could not find any running ray_amd instance. "

@@ -16,6 +16,11 @@ def main():
     ap.add_argument("--job", default=None)
     ap.add_argument("--node-id", default=None)
     args = ap.parse_args()
+    lvl = os.environ.get("RAY_AMD_LOGGING_LEVEL")
+    if lvl:  # init(logging_level=...): the workers' ray_amd logger follows the driver's
+        import logging
+
+        logging.getLogger("ray_amd").setLevel(int(lvl) if lvl.isdigit() else lvl.upper())
     try:  # die with the raylet / node agent that forked us (PR_SET_PDEATHSIG)
         import ctypes
         import signal
