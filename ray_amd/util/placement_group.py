@@ -95,6 +95,10 @@ def placement_group(bundles, strategy: str = "PACK", name: str = "", lifetime=No
     if strategy not in VALID_STRATEGIES:
         raise ValueError(f"Invalid placement group strategy {strategy}. Supported strategies "
                          f"are: {VALID_STRATEGIES}.")
+    if _max_cpu_fraction_per_node is not None or _soft_target_node_id is not None:
+        # experimental reference knobs (deprecated there): refused rather than ignored
+        raise NotImplementedError("_max_cpu_fraction_per_node / _soft_target_node_id are not "
+                                  "supported by this scheduler")
     if lifetime not in (None, "detached"):
         raise ValueError("placement group `lifetime` argument must be either `None` or "
                          "'detached'")
