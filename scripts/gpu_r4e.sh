@@ -26,7 +26,7 @@ for i in 1 2; do
   echo "no-ray dgrad-wt: $(tail -1 $O/bench_noray_wt_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
 for sp in 4 8; do
-  timeout -k 10 300 env RAY_AMD_WGRAD_SPLITS=$sp python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_splits$sp.log 2>&1 || { echo "bench splits rc=$?"; tail -30 $O/bench_noray_splits$sp.log; exit 1; }
+  timeout -k 10 300 env RAY_AMD_WGRAD_SPLITS=$sp RAY_AMD_LT_TUNE=1 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_splits$sp.log 2>&1 || { echo "bench splits rc=$?"; tail -30 $O/bench_noray_splits$sp.log; exit 1; }
   echo "no-ray wgrad splits=$sp: $(tail -1 $O/bench_noray_splits$sp.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
 timeout -k 10 300 python scripts/dgrad_layout_ab.py > $O/dgrad_layout.log 2>&1 || { echo "dgrad ab rc=$?"; tail -20 $O/dgrad_layout.log; exit 1; }
