@@ -26,3 +26,4 @@ from ray_amd.workflow.api import (  # noqa: F401
     sleep,
     wait_for_event,
 )
+from ray_amd.workflow.context import get_current_task_id, get_current_workflow_id  # noqa: F401

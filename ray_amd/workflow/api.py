@@ -219,16 +219,34 @@ class TimerListener(EventListener):
         await asyncio.sleep(max(0.0, timestamp - time.time()))
 
 
+class _EventResult:
+    """An event step's value: _step checkpoints ``event`` first and only then tells the
+    listener (``event_checkpointed``), so a provider never acknowledges an event the
+    workflow could still lose (reference: workflow.wait_for_event semantics)."""
+
+    def __init__(self, listener, event):
+        self.listener, self.event = listener, event
+
+
 @ray.remote(num_cpus=0)
 def _event_step(listener_cls, args, kwargs):
     listener = listener_cls()
+    return _EventResult(listener, asyncio.run(listener.poll_for_event(*args, **kwargs)))
 
-    async def go():
-        ev = await listener.poll_for_event(*args, **kwargs)
-        await listener.event_checkpointed(ev)
-        return ev
 
-    return asyncio.run(go())
+# ------------------------------------------------------------------------ step context
+def get_current_workflow_id() -> Optional[str]:
+    """Inside a workflow step: the workflow's id (reference: workflow_context)."""
+    from ray_amd.workflow import context
+
+    return context.get_current_workflow_id()
+
+
+def get_current_task_id() -> Optional[str]:
+    """Inside a workflow step: the step's task id."""
+    from ray_amd.workflow import context
+
+    return context.get_current_task_id()
 
 
 def wait_for_event(event_listener_type, *args, **kwargs) -> DAGNode:
@@ -248,8 +266,15 @@ def _step(fn, root, wid, task_id, wopts, cancel_file, *args, **kwargs):
         return value
     t0 = time.time()
     catch = wopts.get("catch_exceptions", False)
+    from ray_amd.workflow import context
+
+    context._set(wid, task_id)
+    evr = None
     try:
         out = fn(*args, **kwargs)
+        evr = out if isinstance(out, _EventResult) else None
+        if evr is not None:
+            out = evr.event
         if isinstance(out, _Continuation):
             out = _execute(out.dag, root, wid, prefix=task_id + ".", inputs=((), {}),
                            cancel_file=cancel_file)
@@ -266,6 +291,8 @@ def _step(fn, root, wid, task_id, wopts, cancel_file, *args, **kwargs):
                      {"task_id": task_id, "task_options": wopts,
                       "user_metadata": wopts.get("metadata") or {},
                       "stats": {"start_time": t0, "end_time": time.time()}})
+    if evr is not None:  # the event is durable now: let the listener acknowledge it
+        asyncio.run(evr.listener.event_checkpointed(evr.event))
     return result
 
 
