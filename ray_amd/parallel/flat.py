@@ -203,15 +203,21 @@ class FlatDDP:
                 flat.p16.copy_(flat.p32)
 
     def _mark(self, b: int):
-        """Record bucket b's event on the stream that just produced one of its gradients."""
+        """Note the stream that just produced one of bucket b's gradients. No event is
+        recorded here: ``_launch`` records one per contributing stream when the bucket is
+        full. An event recorded then follows every gradient that stream produced for the
+        bucket (their kernels were enqueued before their hooks ran), so the comm stream
+        never starts early; it may wait for a little more of that stream's work than the
+        gradients themselves, which the overlapped backward hides. One record per
+        (bucket, stream) instead of one per parameter keeps the host cost of the hooks low
+        (they run between the kernel launches of backward)."""
         st = torch.cuda.current_stream(self.flat.device)
         key = st.cuda_stream
-        ent = self._events[b].get(key)
-        if ent is None:
-            ent = self._events[b][key] = (st, torch.cuda.Event())
-        ent[1].record(st)
-        if key not in self._contrib[b]:
-            self._contrib[b].append(key)
+        c = self._contrib[b]
+        if key not in c:
+            c.append(key)
+            if key not in self._events[b]:
+                self._events[b][key] = (st, torch.cuda.Event())
 
     def _launch(self, b: int):
         s, e = self.buckets[b]
@@ -219,7 +225,9 @@ class FlatDDP:
             work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
         else:
             for key in self._contrib[b]:
-                self._comm.wait_event(self._events[b][key][1])
+                st, ev = self._events[b][key]
+                ev.record(st)
+                self._comm.wait_event(ev)
             with torch.cuda.stream(self._comm):
                 work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
         self._works.append(work)

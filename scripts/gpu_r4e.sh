@@ -20,6 +20,8 @@ for i in 1 2; do
   timeout -k 10 300 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_$i.log 2>&1 || { echo "bench rc=$?"; tail -30 $O/bench_noray_$i.log; exit 1; }
   echo "no-ray: $(tail -1 $O/bench_noray_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
+timeout -k 10 300 python bench.py --no-ray --ddp-hooks always --steps 20 --warmup 5 > $O/bench_noray_hooks.log 2>&1 || { echo "bench hooks rc=$?"; tail -30 $O/bench_noray_hooks.log; exit 1; }
+echo "no-ray ddp-hooks always: $(tail -1 $O/bench_noray_hooks.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_tt.log 2>&1 || { echo "bench tt rc=$?"; tail -30 $O/bench_tt.log; exit 1; }
 echo "torchtrainer: $(tail -1 $O/bench_tt.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 for i in 1 2; do
