@@ -62,6 +62,26 @@ class Checkpoint:
         m.update(metadata)
         self.set_metadata(m)
 
+    # framework checkpoints (TorchCheckpoint, SklearnCheckpoint) keep the fitted
+    # preprocessor beside the model so a Predictor built from the checkpoint applies it
+    # (reference: train/_internal/framework_checkpoint.py)
+    PREPROCESSOR_FILENAME = "preprocessor.pkl"
+
+    def set_preprocessor(self, preprocessor) -> None:
+        import cloudpickle
+
+        with open(os.path.join(self.path, self.PREPROCESSOR_FILENAME), "wb") as f:
+            cloudpickle.dump(preprocessor, f)
+
+    def get_preprocessor(self):
+        import pickle
+
+        p = os.path.join(self.path, self.PREPROCESSOR_FILENAME)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as f:
+            return pickle.load(f)
+
     def __repr__(self):
         return f"Checkpoint(filesystem=local, path={self.path})"
 

@@ -37,13 +37,19 @@ class TorchCheckpoint(Checkpoint):
     def from_state_dict(cls, state_dict, *, preprocessor=None):
         d = tempfile.mkdtemp(prefix="ra_torch_ckpt_")
         torch.save(state_dict, os.path.join(d, cls.MODEL_FILENAME))
-        return cls(d)
+        c = cls(d)
+        if preprocessor is not None:
+            c.set_preprocessor(preprocessor)
+        return c
 
     @classmethod
     def from_model(cls, model, *, preprocessor=None):
         d = tempfile.mkdtemp(prefix="ra_torch_ckpt_")
         torch.save(model, os.path.join(d, cls.MODEL_FILENAME))
-        return cls(d)
+        c = cls(d)
+        if preprocessor is not None:
+            c.set_preprocessor(preprocessor)
+        return c
 
     def get_model(self, model=None):
         obj = torch.load(os.path.join(self.path, self.MODEL_FILENAME), weights_only=False)
@@ -53,6 +59,10 @@ class TorchCheckpoint(Checkpoint):
         return obj
 
 
-__all__ = ["TorchTrainer", "TorchConfig", "TorchCheckpoint", "prepare_model",
+from ray_amd.train.torch.torch_predictor import (TorchDetectionPredictor,  # noqa: E402
+                                                  TorchPredictor)
+
+__all__ = ["TorchTrainer", "TorchConfig", "TorchCheckpoint", "TorchPredictor",
+           "TorchDetectionPredictor", "prepare_model",
            "prepare_data_loader", "prepare_optimizer", "get_device", "get_devices", "backward",
            "enable_reproducibility", "accelerate"]
