@@ -32,6 +32,10 @@ class TrainContext:
     trial_dir: str = ""
     storage_path: str = ""
     metadata: dict = field(default_factory=dict)
+    # non-local run storage (train/_internal/storage.py): checkpoints are uploaded to
+    # ``remote_trial_dir`` on ``storage_filesystem``
+    storage_filesystem: object = None
+    remote_trial_dir: str = ""
 
     def get_world_rank(self):
         return self.world_rank
@@ -97,6 +101,15 @@ class _Session:
     def _persist(self, ckpt: Checkpoint) -> str:
         """Copy the worker-local checkpoint dir into the run's storage (all ranks write
         into the same indexed directory, like the reference)."""
+        fs = self.ctx.storage_filesystem
+        if fs is not None:
+            from ray_amd.train._internal import storage
+
+            dst = storage.join(self.ctx.remote_trial_dir,
+                               f"checkpoint_{self.checkpoint_index:06d}")
+            storage.upload_dir(ckpt.path, fs, dst)
+            self.checkpoint_index += 1
+            return dst
         dst = os.path.join(self.ctx.trial_dir, f"checkpoint_{self.checkpoint_index:06d}")
         os.makedirs(dst, exist_ok=True)
         if os.path.abspath(ckpt.path) != os.path.abspath(dst):

@@ -54,7 +54,12 @@ class _CheckpointManager:
             ranked = self.items[::-1]
         drop = [x for x in ranked[k:] if x is not latest]
         for c, _ in drop:
-            shutil.rmtree(c.path, ignore_errors=True)
+            if c.filesystem is not None:
+                from ray_amd.train._internal.storage import delete_dir
+
+                delete_dir(c.filesystem, c.path)
+            else:
+                shutil.rmtree(c.path, ignore_errors=True)
         self.items = [x for x in self.items if not any(x is d for d in drop)]
 
     @property
@@ -118,7 +123,16 @@ class DataParallelTrainer:
             ray.init()
         rc = self.run_config
         name = rc.name or f"{type(self).__name__}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
-        trial_dir = os.path.join(rc.storage_path, name)
+        from ray_amd.train._internal import storage
+
+        fs, root = storage.resolve(rc.storage_path, rc.storage_filesystem)
+        if fs is None:
+            trial_dir, remote_dir = os.path.join(root, name), None
+        else:  # local staging for the driver's files; checkpoints go straight to fs
+            staging = os.environ.get("RAY_AMD_STORAGE", os.path.expanduser("~/ray_amd_results"))
+            trial_dir, remote_dir = os.path.join(staging, name), storage.join(root, name)
+            fs.create_dir(remote_dir, recursive=True)
+        self._storage = (fs, remote_dir)
         os.makedirs(trial_dir, exist_ok=True)
         self._save_trainer(trial_dir)
         mgr = _CheckpointManager(rc.checkpoint_config)
@@ -142,7 +156,7 @@ class DataParallelTrainer:
             if cpath:
                 cbs.fire("on_trial_save", trials=[trial], trial=trial)
                 cbs.fire("on_checkpoint", trials=[trial], trial=trial,
-                         checkpoint=Checkpoint(cpath))
+                         checkpoint=Checkpoint(cpath, filesystem=self._storage[0]))
                 self._save_state(trial_dir, cpath, metrics)
             cbs.end_step([trial])
             for hook in getattr(self, "_report_hooks", ()):
@@ -166,13 +180,24 @@ class DataParallelTrainer:
             trial.status = "ERROR"
             cbs.fire("on_trial_error", trials=[trial], trial=trial)
             cbs.fire("on_experiment_end", trials=[trial])
+            self._sync_up(trial_dir)
             raise error
         trial.status = "TERMINATED"
         cbs.fire("on_trial_complete", trials=[trial], trial=trial)
         cbs.fire("on_experiment_end", trials=[trial])
+        self._sync_up(trial_dir)
         return Result(metrics=history[-1] if history else {}, checkpoint=mgr.latest, error=None,
-                      path=trial_dir, metrics_history=history,
-                      best_checkpoints=[(c, m) for c, m in mgr.items])
+                      path=remote_dir or trial_dir, metrics_history=history,
+                      best_checkpoints=[(c, m) for c, m in mgr.items], filesystem=fs)
+
+    def _sync_up(self, trial_dir):
+        """Upload the staged driver files (result.json, progress.csv, trainer state) to a
+        non-local run storage."""
+        fs, remote_dir = getattr(self, "_storage", (None, None))
+        if fs is not None:
+            from ray_amd.train._internal import storage
+
+            storage.upload_dir(trial_dir, fs, remote_dir)
 
     # ------------------------------------------------------------------ restore
     _TRAINER_FILE = "trainer.pkl"
@@ -216,6 +241,10 @@ class DataParallelTrainer:
         persisted checkpoint. Datasets must be passed again (they are not pickled)."""
         import cloudpickle
 
+        if "://" in str(path):
+            raise NotImplementedError(
+                "restore() reads a local run directory: download the run from its storage "
+                "filesystem first (pyarrow.fs.copy_files)")
         path = os.path.abspath(os.path.expanduser(path))
         with open(os.path.join(path, cls._TRAINER_FILE), "rb") as f:
             tcls, d = cloudpickle.loads(f.read())
@@ -269,7 +298,9 @@ class DataParallelTrainer:
                                    node_rank=node_ranks[nid], experiment_name=name,
                                    trial_name=name, trial_id=trial_id, trial_dir=trial_dir,
                                    storage_path=self.run_config.storage_path,
-                                   metadata=self.metadata)
+                                   metadata=self.metadata,
+                                   storage_filesystem=self._storage[0],
+                                   remote_trial_dir=self._storage[1] or "")
                 futs.append((w, ctx))
             for w, ctx in futs:
                 ctx.local_world_size = local_counts[wg.infos[ctx.world_rank]["node_id"]]
@@ -298,7 +329,7 @@ class DataParallelTrainer:
                     metrics, cpath = rank0
                     history.append(metrics)
                     if cpath:
-                        c = Checkpoint(cpath)
+                        c = Checkpoint(cpath, filesystem=self._storage[0])
                         mgr.register(c, metrics)
                         ckpt_index = int(os.path.basename(cpath).split("_")[-1]) + 1
                     if on_report is not None:

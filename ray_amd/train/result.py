@@ -14,6 +14,7 @@ class Result:
     metrics_history: list = field(default_factory=list)
     best_checkpoints: list = field(default_factory=list)
     _config: dict | None = None
+    filesystem: object = None  # pyarrow filesystem of ``path`` (None: local)
 
     @property
     def metrics_dataframe(self):

@@ -41,7 +41,7 @@ class SklearnCheckpoint(Checkpoint):
     def get_estimator(self):
         import pickle
 
-        with open(os.path.join(self.path, self.MODEL_FILENAME), "rb") as f:
+        with open(os.path.join(self._local_path(), self.MODEL_FILENAME), "rb") as f:
             return pickle.load(f)
 
 

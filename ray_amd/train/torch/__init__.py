@@ -52,7 +52,8 @@ class TorchCheckpoint(Checkpoint):
         return c
 
     def get_model(self, model=None):
-        obj = torch.load(os.path.join(self.path, self.MODEL_FILENAME), weights_only=False)
+        obj = torch.load(os.path.join(self._local_path(), self.MODEL_FILENAME),
+                         weights_only=False)
         if isinstance(obj, dict) and model is not None:
             model.load_state_dict(obj)
             return model
