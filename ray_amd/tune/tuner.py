@@ -651,6 +651,27 @@ class _Controller:
                 return t
         return self._new_trial()
 
+    def _reporter(self):
+        """RunConfig.progress_reporter, else a CLIReporter unless verbose=0 (reference:
+        tune/progress_reporter.py, tune.py _detect_reporter)."""
+        if getattr(self, "_rep", False) is not False:
+            return self._rep
+        rep = self.rc.progress_reporter
+        if rep is None and (self.rc.verbose or 0) >= 1:
+            from ray_amd.tune.registry import CLIReporter
+
+            rep = CLIReporter(metric=self.tc.metric, mode=self.tc.mode)
+        if rep is not None and hasattr(rep, "setup"):
+            rep.setup(start_time=time.time(), total_samples=self.tc.num_samples,
+                      metric=self.tc.metric, mode=self.tc.mode)
+        self._rep = rep
+        return rep
+
+    def _report_progress(self, done=False):
+        rep = self._reporter()
+        if rep is not None and self.trials and rep.should_report(self.trials, done=done):
+            rep.report(self.trials, done)
+
     def run(self):
         maxc = self._max_concurrent()
         budget = self.tc.time_budget_s
@@ -664,6 +685,7 @@ class _Controller:
             if t.status == "PAUSED":
                 t.status = "TERMINATED"
         self._save_state()
+        self._report_progress(done=True)
         self.cb.fire("on_experiment_end", trials=self.trials)
         self._maybe_sync(force=True)
         return self.trials
@@ -743,6 +765,7 @@ class _Controller:
                 t.pending_ref = t.actor.next_result.remote()
             self.cb.end_step(self.trials)
             self._save_state()
+            self._report_progress()
             if self.fail_fast and self._errored:
                 for t in self.trials:
                     if t.status in ("RUNNING", "PAUSED"):
