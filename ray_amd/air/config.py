@@ -104,8 +104,11 @@ class RunConfig:
 @dataclass
 class SyncConfig:
     """Checkpoint/artifact sync to ``RunConfig.storage_path`` (reference: train/
-    _internal/syncer.py SyncConfig). Storage here is a (shared) filesystem path written
-    directly, so these knobs only bound how often / how long driver-side syncs run."""
+    _internal/syncer.py SyncConfig). A local or shared path is written in place (nothing
+    to sync). With a non-local ``storage_filesystem`` Train workers upload checkpoints as
+    they are reported, and Tune uploads its staged experiment directory (trial
+    artifacts included) every ``sync_period`` seconds and at the end; uploads are
+    synchronous, so ``sync_timeout`` and the artifact switches have nothing to bound."""
 
     sync_period: int = 300
     sync_timeout: int = 1800
