@@ -645,11 +645,16 @@ class Algorithm:
         pass
 
 
-class _PolicyView:
+from ray_amd.rllib.policy import Policy as _Policy  # noqa: E402
+
+
+class _PolicyView(_Policy):
     def __init__(self, algo, policy_id):
         self.algo, self.policy_id = algo, policy_id
         self.observation_space = algo.observation_space
         self.action_space = algo.action_space
+        self.config = {}
+        self.global_timestep = 0
 
     @property
     def model(self):

@@ -25,11 +25,22 @@ class SingleAgentEnvRunner:
         self.worker_index = worker_index
         n = int(config.get("num_envs_per_env_runner", 1))
         seed = config.get("seed")
+        from ray_amd.rllib.env.vector_env import VectorEnv
+
         self.envs = []
         for i in range(n):
             ec = dict(config.get("env_config") or {})
             ec.setdefault("seed", (seed or 0) * 1000 + worker_index * 100 + i)
-            self.envs.append(make_env(config["env"], ec))
+            e = make_env(config["env"], ec)
+            if isinstance(e, VectorEnv):  # its sub-environments join the lock-step batch
+                subs = e.get_sub_environments()
+                if not subs:
+                    raise ValueError(f"{type(e).__name__} exposes no sub-environments; "
+                                     "EnvRunners step concrete envs")
+                self.envs.extend(subs)
+            else:
+                self.envs.append(e)
+        n = len(self.envs)
         self.observation_space = self.envs[0].observation_space
         self.action_space = self.envs[0].action_space
         # ConnectorV2 pipelines: env -> module (per batched step) and module -> env

@@ -46,19 +46,26 @@ def register_env(name: str, creator):
     _REGISTRY[name] = creator
 
 
+def _wrap(e):
+    """ExternalEnvs are stepped through their gym-style adapter."""
+    from ray_amd.rllib.env.external_env import ExternalEnv, ExternalEnvAdapter
+
+    return ExternalEnvAdapter(e) if isinstance(e, ExternalEnv) else e
+
+
 def make_env(env, env_config=None):
     cfg = dict(env_config or {})
     if isinstance(env, str):
         if env in _REGISTRY:
-            return _REGISTRY[env](cfg)
+            return _wrap(_REGISTRY[env](cfg))
         raise ValueError(f"unknown env {env!r}; registered: {sorted(_REGISTRY)}")
     if isinstance(env, type):
         try:
-            return env(cfg)
+            return _wrap(env(cfg))
         except TypeError:
-            return env()
+            return _wrap(env())
     if callable(env):
-        return env(cfg)
+        return _wrap(env(cfg))
     raise ValueError(f"cannot build env from {env!r}")
 
 
