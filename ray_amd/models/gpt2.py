@@ -128,7 +128,6 @@ class GPT2(nn.Module):
         self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_eps)
         self.lm_head_chunk = 8192  # tokens per fused LM-head/CE chunk
-        self._weights_ready = None  # per-group optimizer events (overlapped AdamW)
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -150,23 +149,14 @@ class GPT2(nn.Module):
             n -= self.wpe.numel()
         return n
 
-    def _ready(self, k):
-        """Wait (on the current stream) for optimizer group k of an overlapped AdamW
-        (GPT2Trainer, RAY_AMD_OPT_OVERLAP=1) before reading its weights."""
-        evs = self._weights_ready
-        if evs is not None:
-            torch.cuda.current_stream().wait_event(evs[k])
-
     def forward(self, idx, targets=None):
         B, T = idx.shape
-        self._ready(0)
         x = rf.embedding(idx, self.wte, self.wpe)
         # Pre-LN seams fused: every "x += sub_block(h) + bias; h = LN(x)" is ONE kernel
         # forward and ONE kernel backward (residual grads, LN grads and the projection-bias
         # grad together) — see ops.functional.residual_layer_norm.
         x, h = self.h[0].ln_1.fork(x)
         for i, blk in enumerate(self.h):
-            self._ready(i + 1)
             x, h = rf.residual_layer_norm(blk.attn(h), blk.c_proj_b, x, blk.ln_2.weight,
                                           blk.ln_2.bias, blk.ln_2.eps)
             nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f

@@ -375,50 +375,6 @@ class FlatAdamW:
         if self.zero_grad:
             f.g.zero_()
 
-    def step_overlapped(self, lr: float, groups: list, stream) -> list:
-        """AdamW split into parameter groups that run on ``stream`` in the order the next
-        forward uses them, beside that forward: the global-norm clip runs first on the
-        current stream (every group needs its scale), then group k's AdamW ranges, then
-        event k. The caller makes the next forward wait on event k before it reads group
-        k's weights (GPT2Trainer with RAY_AMD_OPT_OVERLAP=1). ``groups``: lists of flat
-        (offset, numel) ranges. Elementwise, so the result equals step() bit for bit."""
-        from ray_amd.ops import functional as rf
-
-        assert self.use_hip and self.hyper is None
-        rf.join_side_streams()
-        rf.bump_weights_epoch()
-        self.step_count += 1
-        f = self.flat
-        L = _lib.lib()
-        gptr = None
-        if self.max_grad_norm or self.grad_scale != 1.0:
-            if self._work is None:
-                self._work = torch.empty(L.ra_norm_parts(), dtype=torch.float32,
-                                         device=f.device)
-            check(L.ra_grad_clip(ptr(f.g), f.numel, 1 if f.g.dtype == torch.bfloat16 else 0,
-                                 float(self.max_grad_norm or 0.0), float(self.grad_scale),
-                                 ptr(self._work), ptr(self._scale), ptr(self.last_norm),
-                                 stream_ptr()), "grad_clip")
-            gptr = ptr(self._scale)
-        stream.wait_stream(torch.cuda.current_stream(f.device))
-        g32 = f.g.dtype == torch.float32
-        flags = (1 if g32 else 0) | (2 if self.zero_grad else 0)
-        evs = []
-        with torch.cuda.stream(stream):
-            sp = stream_ptr()
-            for ranges in groups:
-                for off, n in ranges:
-                    nd = min(max(f.n_decay - off, 0), n)
-                    check(L.ra_adamw_flat_dev(
-                        ptr(f.p32[off:]), ptr(f.p16[off:]) if f.p16 is not f.p32 else None,
-                        ptr(f.g[off:]), ptr(self.m[off:]), ptr(self.v[off:]), n, nd, lr,
-                        self.b1, self.b2, self.eps, self.wd, self.step_count, gptr, flags,
-                        None, sp), "adamw")
-                ev = torch.cuda.Event()
-                ev.record(stream)
-                evs.append(ev)
-        return evs
-
     def state_dict(self):
         return {"m": self.m, "v": self.v, "step": self.step_count}
 

@@ -13,11 +13,7 @@ import torch
 import torch.distributed as dist
 
 from ray_amd.models.gpt2 import GPT2, GPT2Config
-from ray_amd.parallel.flat import ALIGN, FlatAdamW, FlatDDP, FlatParams, cosine_lr
-
-
-def _round_up(n: int) -> int:
-    return (n + ALIGN - 1) // ALIGN * ALIGN
+from ray_amd.parallel.flat import FlatAdamW, FlatDDP, FlatParams, cosine_lr
 
 
 class GPT2Trainer:
@@ -46,52 +42,11 @@ class GPT2Trainer:
         # AdamW clears the flat gradient in its own pass (no zero_grad memset per step)
         self.opt = FlatAdamW(self.flat, lr=lr, weight_decay=0.1, max_grad_norm=1.0,
                              grad_scale=self.ddp.grad_scale / grad_accum, zero_grad=True)
-        # RAY_AMD_OPT_OVERLAP=1: AdamW runs per layer group on its own stream beside the
-        # next forward (which waits per group) instead of before it
-        import os
-
-        self._opt_overlap = (os.environ.get("RAY_AMD_OPT_OVERLAP", "0") == "1"
-                             and self.device.type == "cuda")
-        self._opt_groups = self._layer_groups() if self._opt_overlap else None
-        self._opt_stream = torch.cuda.Stream(self.device) if self._opt_overlap else None
         self.base_lr = lr
         self.total_steps = total_steps
         self.warmup = warmup_steps
         self.step_idx = 0
         self.last_loss = None
-
-    def _layer_groups(self):
-        """Flat (offset, numel) ranges of the parameters the forward reads, grouped in
-        forward order: [embeddings + first LN], then per block its weights, biases, LN-2
-        and the NEXT block's LN-1 (ln_f after the last block) — GPT2.forward waits for
-        group 0 before the embedding and group i + 1 before block i."""
-        m = self.model
-        off = {id(p): (o, p.numel()) for (_, p), o in zip(self.flat.order, self.flat.offsets)}
-        groups = [[m.wte, m.wpe, m.h[0].ln_1.weight, m.h[0].ln_1.bias]]
-        for i, blk in enumerate(m.h):
-            nxt = m.h[i + 1].ln_1 if i + 1 < len(m.h) else m.ln_f
-            own = [p for n, p in blk.named_parameters() if not n.startswith("ln_1.")]
-            groups.append(own + [nxt.weight, nxt.bias])
-        seen = set()
-        out = []
-        for g in groups:
-            ranges = []
-            for p in g:
-                if id(p) in seen or id(p) not in off:
-                    continue
-                seen.add(id(p))
-                o, n = off[id(p)]
-                ranges.append((o, n))
-            ranges.sort()
-            merged = []
-            for o, n in ranges:  # adjacent params (rounded sizes) -> one launch
-                if merged and merged[-1][0] + _round_up(merged[-1][1]) == o:
-                    merged[-1] = (merged[-1][0], o + n - merged[-1][0])
-                else:
-                    merged.append((o, n))
-            out.append(merged)
-        assert len(seen) == len(self.flat.order), "every parameter in exactly one group"
-        return out
 
     def synthetic_batch(self, gen: torch.Generator | None = None):
         x = torch.randint(0, self.cfg.vocab_size, (self.B, self.T + 1), device=self.device,
@@ -108,7 +63,7 @@ class GPT2Trainer:
         ``warm`` eager steps run first on the capture stream (per-stream GEMM workspaces,
         kernel choices); they are real training steps. World-1 groups only: a multi-rank
         step keeps the eager path with its overlapped RCCL buckets."""
-        if self.device.type != "cuda" or self.ddp.enabled or self._opt_overlap:
+        if self.device.type != "cuda" or self.ddp.enabled:
             return False
         self._static = [(x.clone(), y.clone()) for x, y in batches]
         self.opt.use_device_hyper()
@@ -172,11 +127,7 @@ class GPT2Trainer:
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         self.ddp.finish()
         lr = cosine_lr(self.step_idx, self.base_lr, self.warmup, self.total_steps)
-        if self._opt_overlap:
-            self.model._weights_ready = self.opt.step_overlapped(lr, self._opt_groups,
-                                                                 self._opt_stream)
-        else:
-            self.opt.step(lr)
+        self.opt.step(lr)
         self.step_idx += 1
         self.last_loss = loss_sum / len(batches)
         return self.last_loss

@@ -28,10 +28,6 @@ for i in 1 2; do
   timeout -k 10 300 env RAY_AMD_DGRAD_WT=1 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_wt_$i.log 2>&1 || { echo "bench wt rc=$?"; tail -30 $O/bench_noray_wt_$i.log; exit 1; }
   echo "no-ray dgrad-wt: $(tail -1 $O/bench_noray_wt_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
 done
-for i in 1 2; do
-  timeout -k 10 300 env RAY_AMD_OPT_OVERLAP=1 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_optov_$i.log 2>&1 || { echo "bench optov rc=$?"; tail -30 $O/bench_noray_optov_$i.log; exit 1; }
-  echo "no-ray opt-overlap: $(tail -1 $O/bench_noray_optov_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"
-done
 for sp in 4 8; do
   timeout -k 10 300 env RAY_AMD_WGRAD_SPLITS=$sp RAY_AMD_LT_TUNE=1 python bench.py --no-ray --steps 20 --warmup 5 > $O/bench_noray_splits$sp.log 2>&1 || { echo "bench splits rc=$?"; tail -30 $O/bench_noray_splits$sp.log; exit 1; }
   echo "no-ray wgrad splits=$sp: $(tail -1 $O/bench_noray_splits$sp.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"

@@ -257,27 +257,3 @@ def test_dgrad_transposed_weight_copy(cuda_device, monkeypatch):
     dx()
     assert torch.equal(w._ra_wt[0], wt_before)  # refreshed from unchanged weights
     assert torch.equal(w._ra_wt[0], w.detach().t().contiguous())
-
-
-def test_overlapped_adamw_matches_serial(cuda_device, monkeypatch):
-    """RAY_AMD_OPT_OVERLAP: AdamW split into forward-order layer groups on its own stream,
-    the next forward waiting per group, gives bit-identical weights to the one-pass step."""
-    import os
-
-    from ray_amd.models.gpt2 import GPT2Config
-    from ray_amd.train.gpt2_step import GPT2Trainer
-
-    def run(overlap):
-        monkeypatch.setenv("RAY_AMD_OPT_OVERLAP", "1" if overlap else "0")
-        tr = GPT2Trainer(_tiny_cfg(), 4, 128, cuda_device, lr=3e-3, warmup_steps=1,
-                         total_steps=10, seed=7)
-        g = torch.Generator(device=cuda_device).manual_seed(3)
-        for _ in range(4):
-            tr.step([tr.synthetic_batch(g)])
-        torch.cuda.synchronize()
-        return tr
-
-    a, b = run(False), run(True)
-    assert b._opt_groups is not None and len(b._opt_groups) == _tiny_cfg().n_layer + 1
-    assert torch.equal(a.flat.p32, b.flat.p32) and torch.equal(a.opt.m, b.opt.m)
-    assert float(a.last_loss) == float(b.last_loss)
