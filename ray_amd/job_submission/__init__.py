@@ -10,9 +10,24 @@ import time
 import urllib.error
 import urllib.request
 from dataclasses import dataclass, field
+from enum import Enum
 from typing import Any, AsyncIterator, Dict, List, Optional
 
 from ray_amd.dashboard.job_manager import JobStatus  # noqa: F401
+
+
+class JobType(str, Enum):
+    """How a job started (reference: dashboard/modules/job/pydantic_models.py:26)."""
+    SUBMISSION = "SUBMISSION"  # through the Jobs API
+    DRIVER = "DRIVER"  # a driver script that called ray_amd.init
+
+
+@dataclass
+class DriverInfo:
+    """The driver process of a job (pydantic_models.py:13)."""
+    id: str
+    node_ip_address: str
+    pid: str
 
 
 @dataclass
@@ -20,7 +35,7 @@ class JobDetails:
     submission_id: str
     entrypoint: str
     status: JobStatus
-    type: str = "SUBMISSION"
+    type: JobType = JobType.SUBMISSION
     job_id: Optional[str] = None
     message: Optional[str] = None
     error_type: Optional[str] = None
@@ -35,11 +50,21 @@ class JobDetails:
     entrypoint_resources: Optional[Dict[str, float]] = None
     driver_node_id: Optional[str] = None
     driver_pid: Optional[int] = None
+    driver_info: Optional[DriverInfo] = None
 
     @classmethod
     def from_dict(cls, d: dict) -> "JobDetails":
         known = {k: v for k, v in d.items() if k in cls.__dataclass_fields__}
         known["status"] = JobStatus(known["status"])
+        known["type"] = JobType(known.get("type") or "SUBMISSION")
+        di = known.get("driver_info")
+        if isinstance(di, dict):
+            known["driver_info"] = DriverInfo(**{k: str(v) for k, v in di.items()
+                                                 if k in ("id", "node_ip_address", "pid")})
+        elif known.get("driver_pid") is not None and di is None:
+            known["driver_info"] = DriverInfo(id=str(known.get("job_id") or ""),
+                                              node_ip_address="127.0.0.1",
+                                              pid=str(known["driver_pid"]))
         return cls(**known)
 
 
@@ -148,4 +173,4 @@ class JobSubmissionClient:
             time.sleep(0.1)
 
 
-__all__ = ["JobSubmissionClient", "JobStatus", "JobDetails", "JobInfo"]
+__all__ = ["JobSubmissionClient", "JobStatus", "JobDetails", "JobInfo", "JobType", "DriverInfo"]

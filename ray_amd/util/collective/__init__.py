@@ -7,4 +7,9 @@ from ray_amd.util.collective.collective import (allgather, allreduce,  # noqa: F
                                                 get_collective_group_size, get_rank,
                                                 init_collective_group, is_group_initialized,
                                                 recv, reduce, reducescatter, send, synchronize)
+from ray_amd.util.collective.collective import (allgather_multigpu,  # noqa: F401
+                                                allreduce_multigpu, broadcast_multigpu,
+                                                gloo_available, nccl_available,
+                                                recv_multigpu, reduce_multigpu,
+                                                reducescatter_multigpu, send_multigpu)
 from ray_amd.util.collective.types import Backend, ReduceOp  # noqa: F401

@@ -275,3 +275,116 @@ def recv(tensor, src_rank: int, group_name: str = "default"):
 def synchronize(gpu_id: int = 0):
     if torch.cuda.is_available():
         torch.cuda.synchronize(gpu_id)
+
+
+# ------------------------------------------------------------------ availability / multigpu
+def gloo_available() -> bool:
+    return dist.is_available() and dist.is_gloo_available()
+
+
+def nccl_available() -> bool:
+    """RCCL (torch's "nccl" backend on ROCm)."""
+    return dist.is_available() and dist.is_nccl_available()
+
+
+# The *_multigpu calls (reference: util/collective/collective.py) take one tensor per GPU
+# of the calling process. This framework runs one process per GPU, so the list usually
+# has one tensor; longer lists (several devices driven from one process) are reduced
+# locally onto the first tensor's device, go through the one inter-process collective,
+# and are copied back: the result is the same as the reference's flat (process x gpu)
+# rank space for every reduce op.
+def _local_reduce(tensors, op, into: int = 0):
+    acc = tensors[into]
+    for i, t in enumerate(tensors):
+        if i == into:
+            continue
+        x = t.to(acc.device, non_blocking=True)
+        if op == ReduceOp.SUM:
+            acc.add_(x)
+        elif op == ReduceOp.PRODUCT:
+            acc.mul_(x)
+        elif op == ReduceOp.MIN:
+            torch.minimum(acc, x, out=acc)
+        elif op == ReduceOp.MAX:
+            torch.maximum(acc, x, out=acc)
+        else:
+            raise ValueError(f"unsupported reduce op {op}")
+    return acc
+
+
+def allreduce_multigpu(tensor_list, group_name: str = "default", op=ReduceOp.SUM):
+    acc = _local_reduce(tensor_list, op)
+    allreduce(acc, group_name, op)
+    for t in tensor_list[1:]:
+        t.copy_(acc)
+    return tensor_list
+
+
+def reduce_multigpu(tensor_list, dst_rank: int = 0, dst_tensor: int = 0,
+                    group_name: str = "default", op=ReduceOp.SUM):
+    acc = _local_reduce(tensor_list, op, into=dst_tensor)
+    reduce(acc, dst_rank, group_name, op)
+    return tensor_list
+
+
+def broadcast_multigpu(tensor_list, src_rank: int = 0, src_tensor: int = 0,
+                       group_name: str = "default"):
+    g = _g(group_name)
+    buf = tensor_list[src_tensor] if g.rank == src_rank else tensor_list[0]
+    broadcast(buf, src_rank, group_name)
+    for t in tensor_list:
+        if t is not buf:
+            t.copy_(buf)
+    return tensor_list
+
+
+def allgather_multigpu(output_tensor_lists, input_tensor_list, group_name: str = "default"):
+    """output_tensor_lists[i] (one list per local tensor) receives all world * N inputs in
+    global (process, local index) order."""
+    g = _g(group_name)
+    n = len(input_tensor_list)
+    dev = input_tensor_list[0].device
+    stacked = torch.stack([t.to(dev) for t in input_tensor_list])
+    parts = [torch.empty_like(stacked) for _ in range(g.world_size)]
+    dist.all_gather(parts, stacked, group=g.pg)
+    for outs in output_tensor_lists:
+        if len(outs) != g.world_size * n:
+            raise RuntimeError("each output list needs world_size * len(input_tensor_list) "
+                               "tensors")
+        for p in range(g.world_size):
+            for k in range(n):
+                outs[p * n + k].copy_(parts[p][k])
+    return output_tensor_lists
+
+
+def reducescatter_multigpu(output_tensor_list, input_tensor_lists, group_name: str = "default",
+                           op=ReduceOp.SUM):
+    """Local tensor i receives the reduction of chunk (rank * N + i) of every input list."""
+    g = _g(group_name)
+    n = len(output_tensor_list)
+    chunks = len(input_tensor_lists[0])
+    if chunks != g.world_size * n:
+        raise RuntimeError("each input list needs world_size * len(output_tensor_list) tensors")
+    dev = output_tensor_list[0].device
+    per = [torch.stack([t.to(dev) for t in lst]) for lst in input_tensor_lists]
+    flat = _local_reduce(per, op)
+    dist.all_reduce(flat, op=_TORCH_OPS[op], group=g.pg)
+    for i, out in enumerate(output_tensor_list):
+        out.copy_(flat[g.rank * n + i])
+    return output_tensor_list
+
+
+def send_multigpu(tensor, dst_rank: int, dst_gpu_index: int = 0,
+                  group_name: str = "default", n_elements: int = 0):
+    t = tensor.reshape(-1)[:n_elements] if n_elements else tensor
+    send(t.contiguous(), dst_rank, group_name)
+
+
+def recv_multigpu(tensor, src_rank: int, src_gpu_index: int = 0,
+                  group_name: str = "default", n_elements: int = 0):
+    if n_elements:
+        buf = torch.empty(n_elements, dtype=tensor.dtype, device=tensor.device)
+        recv(buf, src_rank, group_name)
+        tensor.reshape(-1)[:n_elements].copy_(buf)
+        return tensor
+    return recv(tensor, src_rank, group_name)

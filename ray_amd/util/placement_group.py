@@ -132,12 +132,11 @@ def get_current_placement_group() -> PlacementGroup | None:
     cw = W.global_worker.core
     if cw is None:
         return None
-    spec = getattr(cw.current_task, "spec", None) or cw.actor_spec
-    if spec is None:
-        return None
-    st = spec.get("strategy")
-    if isinstance(st, dict) and st.get("type") == "pg":
-        return PlacementGroup(PlacementGroupID.from_hex(st["pg_id"]))
+    # a task's own strategy, else (actor method calls carry none) the actor's creation one
+    for spec in (getattr(cw.current_task, "spec", None), cw.actor_spec):
+        st = spec.get("strategy") if spec else None
+        if isinstance(st, dict) and st.get("type") == "pg":
+            return PlacementGroup(PlacementGroupID.from_hex(st["pg_id"]))
     return None
 
 

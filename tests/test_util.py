@@ -174,6 +174,51 @@ def test_collective_gloo(cluster):
     assert (r0[6], r1[6], r0[7]) == (0, 1, 2)
 
 
+@ray.remote
+class MultiWorker:
+    def setup(self, world, rank):
+        from ray_amd.util import collective as col
+
+        col.init_collective_group(world, rank, backend="gloo", group_name="m")
+        return col.gloo_available()
+
+    def run(self, rank):
+        from ray_amd.util import collective as col
+
+        # two "local devices" per process: global tensor index = rank * 2 + i
+        ar = [torch.full((2,), float(rank * 2 + i)) for i in range(2)]
+        col.allreduce_multigpu(ar, group_name="m", op=col.ReduceOp.MAX)
+        bc = [torch.full((2,), float(10 * rank + i)) for i in range(2)]
+        col.broadcast_multigpu(bc, src_rank=1, src_tensor=1, group_name="m")
+        outs = [[torch.zeros(1) for _ in range(4)] for _ in range(2)]
+        col.allgather_multigpu(outs, [torch.tensor([rank * 2.0 + i]) for i in range(2)],
+                               group_name="m")
+        rs_out = [torch.zeros(1) for _ in range(2)]
+        col.reducescatter_multigpu(rs_out, [[torch.tensor([float(c)]) for c in range(4)]
+                                            for _ in range(2)], group_name="m")
+        if rank == 0:
+            col.send_multigpu(torch.arange(5.0), 1, 0, group_name="m", n_elements=3)
+            got = None
+        else:
+            got = torch.zeros(5)
+            col.recv_multigpu(got, 0, 0, group_name="m", n_elements=3)
+            got = got.tolist()
+        return ([t.tolist() for t in ar], [t.tolist() for t in bc],
+                [[o.item() for o in lst] for lst in outs], [o.item() for o in rs_out], got)
+
+
+def test_collective_multigpu_gloo(cluster):
+    ws = [MultiWorker.remote() for _ in range(2)]
+    assert all(ray.get([w.setup.remote(2, i) for i, w in enumerate(ws)]))
+    r0, r1 = ray.get([w.run.remote(i) for i, w in enumerate(ws)])
+    assert r0[0] == [[3.0, 3.0]] * 2 and r1[0] == [[3.0, 3.0]] * 2
+    assert r0[1] == [[11.0, 11.0]] * 2 and r1[1] == [[11.0, 11.0]] * 2
+    assert r0[2] == [[0.0, 1.0, 2.0, 3.0]] * 2
+    # chunk c summed over 2 local lists x 2 processes = 4c; rank r, local i gets chunk 2r+i
+    assert r0[3] == [0.0, 4.0] and r1[3] == [8.0, 12.0]
+    assert r1[4] == [0.0, 1.0, 2.0, 0.0, 0.0]
+
+
 def test_create_collective_group_from_driver(cluster):
     from ray_amd.util import collective as col
 
