@@ -63,11 +63,13 @@ def main():
     res["per_layer_ms"] = {"nn": round(tot_nn, 4), "tn": round(tot_tn, 4),
                            "transpose": round(tot_tr, 4)}
     res["per_step_saving_ms_12_layers"] = round(12 * (tot_nn - tot_tn - tot_tr), 3)
-    torch.cuda.tunable.write_file(dst)
-    old = set(open(SRC).read().splitlines())
-    res["new_tunableop_entries"] = [ln for ln in open(dst).read().splitlines()
-                                    if ln not in old and not ln.startswith("Validator")]
     print(json.dumps(res), flush=True)
+    # the tuned entries of this process (torch 2.10 has no tunable.write_file: the
+    # results table is read back instead)
+    old = set(open(SRC).read().splitlines())
+    rows = [",".join(str(x) for x in r) for r in torch.cuda.tunable.get_results()]
+    print(json.dumps({"new_tunableop_entries": [r for r in rows if r not in old]}),
+          flush=True)
 
 
 if __name__ == "__main__":
