@@ -348,9 +348,13 @@ class CoreWorker:
             P.STREAM_ITEM: self._on_stream_item,
             P.STREAM_ACK: self._on_stream_ack,
         }
+        # poll timeout: messages wake the loop at once; the timeout only paces the periodic
+        # work below (lease reaping, task-event flushes). Every wake takes the GIL from the
+        # process's compute thread (a Train worker's launch loop), so it is configurable.
+        poll_ms = int(os.environ.get("RAY_AMD_POLL_MS", "10"))
         while not self._stopped:
             try:
-                events = io.poll(10, 4096)
+                events = io.poll(poll_ms, 4096)
             except Exception:
                 break
             for typ, conn, payload in events:
