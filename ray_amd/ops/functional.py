@@ -361,11 +361,12 @@ def join_side_streams():
         torch.cuda.current_stream(dev).wait_stream(st)
 
 
-# RAY_AMD_DGRAD_WT=1: the input-gradient GEMM dX = dY @ W reads a transposed bf16 copy of
+# RAY_AMD_DGRAD_WT (default on; 0 disables): the input-gradient GEMM dX = dY @ W reads a transposed bf16 copy of
 # W ([in, out], refreshed once per optimizer step on the side stream during the forward),
 # so it runs in the forward GEMMs' operand layout (TunableOp "tn" instead of "nn";
 # scripts/dgrad_layout_ab.py measures both). Costs one extra bf16 copy of every weight.
-_DGRAD_WT = os.environ.get("RAY_AMD_DGRAD_WT", "0") == "1"
+# Measured on MI355X (profiles/r4/r4g): 67.09 vs 67.59 ms/step, three interleaved pairs.
+_DGRAD_WT = os.environ.get("RAY_AMD_DGRAD_WT", "1") == "1"
 _weights_epoch = [0]
 
 

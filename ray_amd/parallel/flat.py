@@ -140,10 +140,10 @@ class FlatDDP:
 
     Stream protocol (GPU). Gradients of one bucket come from two compute streams: the
     main stream (LayerNorm/bias/embedding/LM-head kernels) and the weight-gradient side
-    stream (``ops.functional._side_stream``). Every readiness signal records a per-bucket
-    event on the stream that produced that gradient; when a bucket is full, a DEDICATED
-    comm stream waits on exactly those events and issues the RCCL ``all_reduce`` (RCCL's
-    internal stream then orders itself after the comm stream). Neither compute stream
+    stream (``ops.functional._side_stream``). A readiness signal only counts; when a bucket
+    is full, an event is recorded on each compute stream and a DEDICATED comm stream waits
+    on those events and issues the RCCL ``all_reduce`` (RCCL's internal stream then orders
+    itself after the comm stream). Neither compute stream
     ever waits on the other, or on the comm stream, during backward: the only joins are
     in ``finish()``, right before the optimizer consumes the gradients.
 
@@ -185,10 +185,11 @@ class FlatDDP:
         self.launched = 0  # all_reduce launches since construction (tests / bench report)
         cuda = flat.g.is_cuda and self.enabled
         self._comm = torch.cuda.Stream(flat.device) if cuda else None
-        # per bucket: {stream handle: (stream, event)} — reused every step; ``_contrib[b]``
-        # lists the streams that produced a gradient of bucket b in THIS backward
+        # the training loop's stream (backward's main stream); hooks may fire while a side
+        # stream is current, so it is named explicitly
+        self._main = torch.cuda.current_stream(flat.device) if cuda else None
+        # per bucket: {compute-stream index: event}, reused every step
         self._events: list[dict] = [dict() for _ in self.buckets]
-        self._contrib: list[list] = [[] for _ in self.buckets]
         if self.enabled:
             for i, (_, p) in enumerate(flat.order):
                 hook = self._make_hook(i)
@@ -202,30 +203,35 @@ class FlatDDP:
             with torch.no_grad():
                 flat.p16.copy_(flat.p32)
 
-    def _mark(self, b: int):
-        """Note the stream that just produced one of bucket b's gradients. No event is
-        recorded here: ``_launch`` records one per contributing stream when the bucket is
-        full. An event recorded then follows every gradient that stream produced for the
-        bucket (their kernels were enqueued before their hooks ran), so the comm stream
-        never starts early; it may wait for a little more of that stream's work than the
-        gradients themselves, which the overlapped backward hides. One record per
-        (bucket, stream) instead of one per parameter keeps the host cost of the hooks low
-        (they run between the kernel launches of backward)."""
-        st = torch.cuda.current_stream(self.flat.device)
-        key = st.cuda_stream
-        c = self._contrib[b]
-        if key not in c:
-            c.append(key)
-            if key not in self._events[b]:
-                self._events[b][key] = (st, torch.cuda.Event())
+    def _compute_streams(self):
+        from ray_amd.ops import functional as rf
+
+        dev = self.flat.device
+        out, seen = [], set()
+        for st in (self._main, torch.cuda.current_stream(dev), rf._side.get(dev),
+                   rf._side2.get(dev)):
+            if st is not None and st.cuda_stream not in seen:
+                seen.add(st.cuda_stream)
+                out.append(st)
+        return out
 
     def _launch(self, b: int):
         s, e = self.buckets[b]
         if self._comm is None:
             work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
         else:
-            for key in self._contrib[b]:
-                st, ev = self._events[b][key]
+            # one event per compute stream (main + weight-gradient side streams), recorded
+            # now: it follows every gradient of the bucket those streams produced (their
+            # kernels were enqueued before their hooks ran), so the comm stream never
+            # starts early; it may wait for a little more of a stream's work than the
+            # bucket's gradients, which the overlapped backward hides. Nothing is recorded
+            # per parameter: the hooks stay a counter bump (host cost between backward's
+            # kernel launches)
+            for i, st in enumerate(self._compute_streams()):
+                evs = self._events[b]
+                ev = evs.get(i)
+                if ev is None:
+                    ev = evs[i] = torch.cuda.Event()
                 ev.record(st)
                 self._comm.wait_event(ev)
             with torch.cuda.stream(self._comm):
@@ -243,8 +249,6 @@ class FlatDDP:
                 return
             self._seen[i] = True
             self._ready[b] += 1
-            if self._comm is not None:
-                self._mark(b)
             if self._ready[b] == self.bucket_sizes[b]:
                 self._launch(b)
 
@@ -271,7 +275,6 @@ class FlatDDP:
         self._works.clear()
         self._ready = [0] * len(self.buckets)
         self._seen = [False] * len(self.flat.order)
-        self._contrib = [[] for _ in self.buckets]
 
     @property
     def grad_scale(self) -> float:

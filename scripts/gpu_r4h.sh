@@ -18,6 +18,13 @@ for i in 1 2; do
     echo "tt poll $p $i: $(ms $O/bench_tt_poll${p}_$i.log)"
   done
 done
+for i in 1 2; do
+  for arm in auto:32 always:32 always:64; do
+    h=${arm%%:*}; mb=${arm##*:}
+    timeout -k 10 300 python bench.py --no-ray --ddp-hooks $h --bucket-mb $mb --steps 30 --warmup 5 > $O/bench_hooks_${h}_${mb}_$i.log 2>&1 || { echo "bench hooks rc=$?"; tail -30 $O/bench_hooks_${h}_${mb}_$i.log; exit 1; }
+    echo "hooks $h bucket $mb $i: $(ms $O/bench_hooks_${h}_${mb}_$i.log)"
+  done
+done
 timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 || { echo "bench default rc=$?"; tail -30 $O/bench_default.log; exit 1; }
 echo "default: $(ms $O/bench_default.log)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python bench.py --no-ray --steps 10 --warmup 3 > $O/prof.log 2>&1 || { echo "prof rc=$?"; tail -20 $O/prof.log; exit 1; }
