@@ -27,6 +27,10 @@ for i in 1 2; do
 done
 timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 || { echo "bench default rc=$?"; tail -30 $O/bench_default.log; exit 1; }
 echo "default: $(ms $O/bench_default.log)"
+for pin in 0 1; do
+  timeout -k 10 400 env RAY_AMD_DATA_GPU_ACTORS=2 RAY_AMD_DATA_PIN_STORE=$pin RAY_AMD_DATA_TRAINER=1 python bench.py --workload data --steps 300 --warmup 20 > $O/data_trainer_a2_pin$pin.log 2>&1 || { echo "data rc=$?"; tail -20 $O/data_trainer_a2_pin$pin.log; exit 1; }
+  echo "data trainer a2 pin=$pin: $(ms $O/data_trainer_a2_pin$pin.log)"
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python bench.py --no-ray --steps 10 --warmup 3 > $O/prof.log 2>&1 || { echo "prof rc=$?"; tail -20 $O/prof.log; exit 1; }
 find $O/prof -name "*kernel_stats.csv" | head -3
 exit 0
