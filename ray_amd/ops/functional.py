@@ -389,7 +389,11 @@ def _transposed_weight(w):
     side = _side_stream(w.device)
     side.wait_stream(torch.cuda.current_stream(w.device))
     with torch.cuda.stream(side):
-        wt.copy_(w.detach().t())
+        if w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous():
+            check(_lib.lib().ra_transpose_bf16(ptr(w), ptr(wt), w.shape[0], w.shape[1],
+                                               side.cuda_stream), "transpose_bf16")
+        else:
+            wt.copy_(w.detach().t())
         ev = torch.cuda.Event()
         ev.record(side)
     w._ra_wt = (wt, key, ev)

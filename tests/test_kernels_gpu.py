@@ -741,3 +741,14 @@ def test_splitk_accum_matches_fp32(cuda_device, S, f32, acc):
                                     stream_ptr())
     assert rc == 0
     assert _rel(grad.float(), want) < (1e-6 if f32 else 5e-3)
+
+
+@pytest.mark.parametrize("rows,cols", [(768, 2304), (3072, 768), (70, 130)])
+def test_transpose_bf16_kernel(cuda_device, rows, cols):
+    """LDS-tiled bf16 transpose (the transposed-weight copy) vs torch, ragged edges incl."""
+    w = torch.randn(rows, cols, device=cuda_device).bfloat16()
+    wt = torch.full((cols, rows), 7.0, device=cuda_device, dtype=torch.bfloat16)
+    st = torch.cuda.current_stream(cuda_device).cuda_stream
+    assert _lib.lib().ra_transpose_bf16(w.data_ptr(), wt.data_ptr(), rows, cols, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(wt, w.t())
