@@ -27,6 +27,10 @@ import argparse
 import json
 import os
 import sys
+
+# 8 hardware queues per process before HIP initialises (ray_amd/_private/worker_main.py has
+# the measurement); Ray workers inherit it through the raylet's environment
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

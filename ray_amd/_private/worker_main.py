@@ -7,6 +7,14 @@ import json
 import os
 import sys
 
+# Hardware queues per process (HIP's default is 4). A training process drives more streams
+# than that — the compute stream, the weight-gradient side streams, the DDP comm stream and
+# RCCL's internal streams — and streams beyond the queue count share a hardware queue,
+# where one stream's event wait stalls the other's kernels. With 8 queues the GPT-2
+# TorchTrainer step went from 68.6-68.7 to 65.8-66.1 ms and the DDP-hooks-on step from
+# 69.6 to 66.4-66.5 ms on MI355X (profiles/r4/README.md §8). Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 
 def main():
     ap = argparse.ArgumentParser()
