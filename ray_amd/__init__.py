@@ -13,13 +13,13 @@ RCCL over xGMI (ray_amd.util.collective, ray_amd.parallel). Runtime core:
 native C++ (ray_amd._native: shared-memory object store, frame I/O loop,
 resource scheduler).
 """
+
+from __future__ import annotations
+
 import os as _os
 
 # 8 hardware queues per process unless the user chose (see _private/worker_main.py)
 _os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
-
-from __future__ import annotations
 
 __version__ = "0.1.0"
 
