@@ -30,7 +30,8 @@ import sys
 
 # 8 hardware queues per process before HIP initialises (ray_amd/_private/worker_main.py has
 # the measurement); Ray workers inherit it through the raylet's environment
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if os.environ.get("RAY_AMD_HW_QUEUES", "8") != "0":  # 0: leave HIP's setting alone
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RAY_AMD_HW_QUEUES", "8")
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

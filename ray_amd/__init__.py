@@ -18,8 +18,9 @@ from __future__ import annotations
 
 import os as _os
 
-# 8 hardware queues per process unless the user chose (see _private/worker_main.py)
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# 8 hardware queues per process (RAY_AMD_HW_QUEUES; see _private/worker_main.py)
+if _os.environ.get("RAY_AMD_HW_QUEUES", "8") != "0":  # 0: leave HIP's setting alone
+    _os.environ["GPU_MAX_HW_QUEUES"] = _os.environ.get("RAY_AMD_HW_QUEUES", "8")
 
 __version__ = "0.1.0"
 

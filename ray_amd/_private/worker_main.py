@@ -12,8 +12,11 @@ import sys
 # RCCL's internal streams — and streams beyond the queue count share a hardware queue,
 # where one stream's event wait stalls the other's kernels. With 8 queues the GPT-2
 # TorchTrainer step went from 68.6-68.7 to 65.8-66.1 ms and the DDP-hooks-on step from
-# 69.6 to 66.4-66.5 ms on MI355X (profiles/r4/README.md §8). Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# 69.6 to 66.4-66.5 ms on MI355X (profiles/r4/README.md §8). Set before HIP initialises,
+# overriding an inherited GPU_MAX_HW_QUEUES (RAY_AMD_HW_QUEUES=<n> picks the count, 0 keeps
+# the inherited setting).
+if os.environ.get("RAY_AMD_HW_QUEUES", "8") != "0":  # 0: leave HIP's setting alone
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RAY_AMD_HW_QUEUES", "8")
 
 
 def main():
