@@ -163,6 +163,10 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = c_long if name.endswith("_work") else c_int
+        # RAY_AMD_KNOBS="11=0,12=1": kernel variant knobs (A/B runs without code edits)
+        for kv in filter(None, os.environ.get("RAY_AMD_KNOBS", "").split(",")):
+            k, v = kv.split("=")
+            L.ra_set_knob(int(k), int(v))
         _lib = L
     return _lib
 

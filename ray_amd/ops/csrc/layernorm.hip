@@ -405,7 +405,8 @@ RA_EXPORT int ra_residual_layernorm_fwd(const void* h, const void* rbias, const 
   return hipGetLastError();
 }
 
-int ra_knobs[16] = {512, 8192, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+// [11] = 2: attention dK/dV with both query halves in flight (r4e: 0.312 vs 0.322 ms)
+int ra_knobs[16] = {512, 8192, 1, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0, 0};
 
 RA_EXPORT int ra_set_knob(int k, int v) {
   if (k < 0 || k >= 16) return hipErrorInvalidValue;
