@@ -40,6 +40,9 @@ _SIGS = {
     "ra_colsum_bf16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
     "ra_splitk_accum": [c_void_p, c_int, c_long, c_void_p, c_int, c_void_p],
     "ra_transpose_bf16": [c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "ra_wgrad": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p,
+                 c_void_p, c_int, c_void_p],
+    "ra_wgrad_splits": [c_int, c_int, c_int],
     "ra_bias_residual": [c_void_p] * 4 + [c_long, c_int, c_void_p],
     "ra_xent_fwd": [c_void_p] * 4 + [c_int, c_int, c_int, c_long, c_void_p],
     "ra_xent_bwd": [c_void_p] * 4 + [c_float, c_void_p, c_int, c_int, c_int, c_long, c_void_p],

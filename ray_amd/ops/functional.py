@@ -318,8 +318,69 @@ def _wgrad_partials(dy2, x2, S, M, N, K):
                      out_dtype=torch.float32)
 
 
-def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K):
-    """sink += dy2^T x2 (fp32 or bf16 flat-gradient view), then signal DDP readiness."""
+def _wgrad_hip_ok(dy2, x2, sink, bias_sink=None) -> bool:
+    M, N = dy2.shape
+    K = x2.shape[1]
+    return (dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and M >= 64 and N % 8 == 0 and K % 8 == 0
+            and dy2.stride(1) == 1 and x2.stride(1) == 1
+            and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
+            and sink.is_contiguous() and sink.numel() == N * K
+            and sink.dtype in (torch.float32, torch.bfloat16) and sink.data_ptr() % 16 == 0
+            and (bias_sink is None or (bias_sink.dtype == sink.dtype
+                                       and bias_sink.is_contiguous()
+                                       and bias_sink.numel() == N)))
+
+
+def wgrad_accumulate(dy2, x2, sink, bias_sink=None, accumulate=True):
+    """sink[N, K] (+)= dy2[M, N]^T @ x2[M, K] and, with ``bias_sink``, bias_sink[N] (+)=
+    colsum(dy2) — the hand-written CDNA4 weight-gradient kernel (ops/csrc/wgrad.hip: both
+    operands read token-major through LDS transpose reads, split-K over tokens sized to one
+    wave of workgroups, fp32 slabs summed into the sink by one pass). ``sink``/``bias_sink``
+    are fp32 or bf16 (same dtype); fp32 math throughout. A token tail (M % 64) is added by
+    an fp32 torch GEMM. Use ``_wgrad_hip_ok`` to check the layout first."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    L = _lib.lib()
+    Mk = M - M % 64
+    flags = (1 if sink.dtype == torch.bfloat16 else 0) | (2 if accumulate else 0) | \
+        (4 if bias_sink is not None else 0)
+    S = L.ra_wgrad_splits(Mk, N, K)
+    if S == 1:
+        check(L.ra_wgrad(ptr(dy2), dy2.stride(0), ptr(x2), x2.stride(0), Mk, N, K, 1, ptr(sink),
+                         ptr(bias_sink), flags, stream_ptr()), "wgrad")
+    else:
+        ws = torch.empty(S * N * K + (S * N if bias_sink is not None else 0),
+                         device=dy2.device, dtype=torch.float32)
+        bws = ws[S * N * K:] if bias_sink is not None else None
+        check(L.ra_wgrad(ptr(dy2), dy2.stride(0), ptr(x2), x2.stride(0), Mk, N, K, S, ptr(ws),
+                         ptr(bws), flags, stream_ptr()), "wgrad")
+        acc = (1 if accumulate else 0) | 2 * _sink_f32(sink)
+        check(L.ra_splitk_accum(ptr(ws), S, N * K, ptr(sink), acc, stream_ptr()), "splitk_accum")
+        if bias_sink is not None:
+            check(L.ra_splitk_accum(ptr(bws), S, N, ptr(bias_sink), acc, stream_ptr()),
+                  "splitk_accum")
+    if Mk < M:  # token tail: an fp32 GEMM on at most 63 rows
+        dt, xt = dy2[Mk:].float(), x2[Mk:].float()
+        sv = sink.view(N, K)
+        sv.copy_(sv.float().addmm_(dt.t(), xt))
+        if bias_sink is not None:
+            bias_sink.copy_(bias_sink.float() + dt.sum(0))
+
+
+def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, bias=None, bias_sink=None):
+    """sink += dy2^T x2 (fp32 or bf16 flat-gradient view), then signal DDP readiness. With
+    ``bias_sink`` (hip path only) the bias gradient is fused into the same kernel."""
+    if _WGRAD == "hip" and _wgrad_hip_ok(dy2, x2, sink, bias_sink):
+        wgrad_accumulate(dy2, x2, sink, bias_sink)
+        _grad_done(w)
+        if bias_sink is not None:
+            _grad_done(bias)
+        return
+    if bias_sink is not None:  # layout not supported by the fused kernel: separate colsum
+        _colsum_bf16(dy2, out=bias_sink)
+        _grad_done(bias)
     if _sink_f32(sink) and _WGRAD_LT:
         # hipBLASLt accumulates straight into the fp32 flat gradient (beta = 1)
         from . import lt
@@ -424,6 +485,15 @@ class _Linear(torch.autograd.Function):
             else:
                 dx = (dy2 @ w).view(x.shape)
         dw = db = None
+        # hip wgrad: the bias gradient (colsum of dY) is fused into the weight-gradient kernel
+        # when both parameters write flat-gradient sinks of one dtype
+        bsink = None
+        if _WGRAD == "hip" and ctx.b is not None and ctx.needs_input_grad[2] and \
+                ctx.needs_input_grad[1]:
+            bsink = _grad_sink(ctx.b)
+            ws_ = _grad_sink(w)
+            if bsink is not None and (ws_ is None or ws_.dtype != bsink.dtype):
+                bsink = None
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             S = _splitk(M, N, K)
@@ -433,11 +503,11 @@ class _Linear(torch.autograd.Function):
                 side = _side_stream(dy2.device)
                 side.wait_stream(torch.cuda.current_stream(dy2.device))
                 with torch.cuda.stream(side):
-                    _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K)
+                    _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
                     dy2.record_stream(side)
                     x2.record_stream(side)
             elif sink is not None:
-                _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K)
+                _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
             elif S > 1:
                 part = _wgrad_partials(dy2, x2, S, M, N, K)
                 dw = torch.empty_like(w)
@@ -445,7 +515,7 @@ class _Linear(torch.autograd.Function):
                                                  stream_ptr()), "splitk_accum")
             else:
                 dw = dy2.t() @ x2
-        if ctx.b is not None and ctx.needs_input_grad[2]:
+        if ctx.b is not None and ctx.needs_input_grad[2] and bsink is None:
             db = _bias_grad(dy2, ctx.b)
         return dx, dw, db
 

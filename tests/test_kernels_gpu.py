@@ -752,3 +752,70 @@ def test_transpose_bf16_kernel(cuda_device, rows, cols):
     assert _lib.lib().ra_transpose_bf16(w.data_ptr(), wt.data_ptr(), rows, cols, st) == 0
     torch.cuda.synchronize()
     assert torch.equal(wt, w.t())
+
+
+# ----------------------------------------------------------------- hand-written wgrad kernel
+@pytest.mark.parametrize("M,N,K,bias,sdtype", [
+    (65536 // 16, 2304, 768, True, torch.float32),   # GPT-2 qkv shape, fewer tokens
+    (4096, 768, 3072, False, torch.float32),          # mlp_proj
+    (1000, 264, 136, True, torch.float32),            # ragged N, K (not multiples of 256), token tail
+    (640, 72, 40, True, torch.bfloat16),              # bf16 sink, tiny ragged tiles
+    (64 * 300, 3072, 3072, False, torch.float32),     # S == 1 path (144 tiles... or split)
+])
+def test_wgrad_kernel_matches_fp32(cuda_device, M, N, K, bias, sdtype):
+    """ops/csrc/wgrad.hip vs an fp32 torch reference: dW += dY^T X, db += colsum(dY),
+    accumulated onto a non-zero sink (the flat-gradient contract)."""
+    torch.manual_seed(11)
+    dy = torch.randn(M, N, device=cuda_device).bfloat16()
+    x = torch.randn(M, K, device=cuda_device).bfloat16()
+    sink0 = torch.randn(N, K, device=cuda_device)
+    bsink0 = torch.randn(N, device=cuda_device)
+    sink = sink0.to(sdtype).clone()
+    bsink = bsink0.to(sdtype).clone() if bias else None
+    assert rf._wgrad_hip_ok(dy, x, sink, bsink)
+    rf.wgrad_accumulate(dy, x, sink, bsink)
+    ref_w = sink0.to(sdtype).float() + dy.float().t() @ x.float()
+    assert _rel(sink, ref_w) < (2e-3 if sdtype == torch.float32 else 1e-2)
+    if bias:
+        ref_b = bsink0.to(sdtype).float() + dy.float().sum(0)
+        assert _rel(bsink, ref_b) < (2e-3 if sdtype == torch.float32 else 1e-2)
+    # overwrite mode (accumulate=False)
+    out = torch.full((N, K), 7.0, device=cuda_device)
+    rf.wgrad_accumulate(dy, x, out, accumulate=False)
+    assert _rel(out, dy.float().t() @ x.float()) < 2e-3
+
+
+def test_wgrad_kernel_strided_rows(cuda_device):
+    """Operands that are column slices of wider rows (ld > N / K), as packed activations."""
+    torch.manual_seed(12)
+    big = torch.randn(2048, 1024, device=cuda_device).bfloat16()
+    dy, x = big[:, :512], big[:, 512:768]
+    sink = torch.zeros(512, 256, device=cuda_device)
+    assert rf._wgrad_hip_ok(dy, x, sink)
+    rf.wgrad_accumulate(dy, x, sink)
+    assert _rel(sink, dy.float().t() @ x.float()) < 2e-3
+
+
+def test_linear_hip_wgrad_fused_bias_into_flat_sinks(cuda_device, monkeypatch):
+    """_Linear backward with RAY_AMD_WGRAD=hip: weight and bias gradients land in the flat
+    fp32 sinks from one kernel, matching autograd in fp32."""
+    monkeypatch.setattr(rf, "_WGRAD", "hip")
+    torch.manual_seed(13)
+    M, K, N = 1024, 256, 768
+    x = torch.randn(M, K, device=cuda_device).bfloat16().requires_grad_()
+    w = (0.05 * torch.randn(N, K, device=cuda_device)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(N, device=cuda_device)).bfloat16().requires_grad_()
+    flat = torch.zeros(N * K + N, device=cuda_device)
+    w._ra_grad, w._ra_direct_grad = flat[:N * K].view(N, K), True
+    b._ra_grad, b._ra_direct_grad = flat[N * K:], True
+    y = rf.linear(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    torch.cuda.synchronize()
+    rf.join_side_streams()
+    torch.cuda.synchronize()
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    torch.nn.functional.linear(xr, wr, br).backward(g.float())
+    assert _rel(w._ra_grad, wr.grad) < 5e-3
+    assert _rel(b._ra_grad, br.grad) < 5e-3
+    assert _rel(x.grad, xr.grad) < 2e-2
