@@ -222,6 +222,13 @@ class CoreWorker:
         self.current_task = threading.local()
         self.running: dict[bytes, int] = {}  # tid -> thread ident
         self.cancelled: set = set()
+        # cancellation: tasks submitted while executing task P (recursive cancel), the
+        # asyncio tasks of an async actor, and whether the main thread is inside user code
+        # (SIGINT is honoured only there: never while arguments are being deserialised)
+        self._children: dict[bytes, list] = {}
+        self._async_tasks: dict = {}
+        self._main_interruptible = False
+        self._sigint_installed = False
         self.actor_instance = None
         self.actor_id = None
         self.actor_spec = None
@@ -1403,6 +1410,7 @@ class CoreWorker:
                     oid = object_id_for_return(tid, i + 1)
                     self.owned[oid] = _Owned(tid)
             self.task_specs[tid] = spec
+        self._note_child(tid)
         if not streaming:
             refs = [ObjectRef(object_id_for_return(tid, i + 1), self.addr, _cw_obj=self)
                     for i in range(nret)]
@@ -1841,7 +1849,31 @@ class CoreWorker:
 
     # ------------------------------------------------------------------ cancellation
     def cancel(self, ref, force=False, recursive=True):
+        """ray.cancel (reference: python/ray/_raylet.pyx:2357 kill_main_task,
+        src/ray/core_worker/core_worker.cc:3821 HandleCancelTask). A queued task fails
+        with TaskCancelledError at once; a running one is interrupted where it runs: the
+        worker's main thread gets a real SIGINT (time.sleep, socket reads, ray.get and
+        other blocking calls return at once with KeyboardInterrupt -> TaskCancelledError),
+        an async actor's coroutine is cancelled on its loop, and force=True kills the
+        worker process. recursive=True also cancels the tasks the cancelled task submitted.
+        A non-owner forwards the request to the owner."""
         tid = ref._id[:16]
+        with self.lock:
+            known = tid in self.task_specs
+        if not known:
+            owner = getattr(ref, "_owner", None)
+            if owner and owner != self.addr:
+                self.send(owner, (P.REQ, 0, "cancel_request", (tid, force, recursive)))
+            return
+        self._cancel_tid(tid, force, recursive)
+
+    def _rpc_cancel_request(self, conn, rid, tid, force, recursive=True):
+        """A borrower asked the owner to cancel one of its tasks."""
+        self._cancel_tid(tid, force, recursive)
+        if rid:
+            self._reply(conn, rid, True, None)
+
+    def _cancel_tid(self, tid, force=False, recursive=True):
         with self.lock:
             spec = self.task_specs.get(tid)
             if spec is None:
@@ -1859,23 +1891,71 @@ class CoreWorker:
         if queued:
             self._fail_task(spec, TaskCancelledError(tid.hex()))
             return
+        msg = (P.REQ, 0, "cancel_task", (tid, force, recursive))
         if spec["type"] == P.ACTOR_TASK:
             ac = self.actors.get(spec["actor_id"])
             if ac is not None and ac.addr:
-                self.send(ac.addr, (P.REQ, 0, "cancel_task", (tid, force)))
+                self.send(ac.addr, msg)
             return
         if lease is not None:
-            self.send(lease.addr, (P.REQ, 0, "cancel_task", (tid, force)))
+            self.send(lease.addr, msg)
 
-    def _rpc_cancel_task(self, conn, rid, tid, force):
+    def _rpc_cancel_task(self, conn, rid, tid, force, recursive=True):
         with self.lock:
             self.cancelled.add(tid)
             th = self.running.get(tid)
-        if th is not None:
+            kids = list(self._children.get(tid, ())) if recursive else []
+            atask = self._async_tasks.get(tid)
+        for k in kids:  # tasks this task submitted (this worker owns them)
+            try:
+                self._cancel_tid(k, force, recursive)
+            except Exception:
+                pass
+        if atask is not None:
             if force:
                 os._exit(1)
+            loop, task = atask
+            loop.call_soon_threadsafe(task.cancel)
+        elif th is not None:
+            if force:
+                os._exit(1)
+            self._interrupt_thread(th)
+        if rid:
+            self._reply(conn, rid, True, None)
+
+    def _interrupt_thread(self, th: int):
+        """Deliver the cancellation to the thread running the task: a real SIGINT for the
+        main thread (interrupts blocking C calls), an asynchronous exception otherwise
+        (threaded actors: raised at the thread's next bytecode)."""
+        import signal
+
+        if self._sigint_installed and th == threading.main_thread().ident:
+            signal.pthread_kill(th, signal.SIGINT)
+        else:
             _raise_in_thread(th, KeyboardInterrupt)
-        self._reply(conn, rid, True, None)
+
+    def install_cancel_handler(self):
+        """Worker processes: SIGINT raises KeyboardInterrupt in the main thread only while
+        a cancelled task's user code runs there; stray or early signals (argument
+        deserialisation, between tasks) are ignored — the pre-call check catches those."""
+        import signal
+
+        def _on_sigint(signum, frame):
+            tid = getattr(self.current_task, "tid", None)
+            if self._main_interruptible and tid is not None and tid in self.cancelled:
+                raise KeyboardInterrupt
+
+        try:
+            signal.signal(signal.SIGINT, _on_sigint)
+            self._sigint_installed = True
+        except ValueError:  # not the main thread
+            self._sigint_installed = False
+
+    def _note_child(self, tid):
+        parent = getattr(self.current_task, "tid", None)
+        if parent is not None:
+            with self.lock:
+                self._children.setdefault(parent, []).append(tid)
 
     # ------------------------------------------------------------------ actors (caller)
     def create_actor(self, actor_id: bytes, cls_key, args, kwargs, opts: dict, cls_name: str,
@@ -2055,6 +2135,7 @@ class CoreWorker:
                 for i in range(nret):
                     self.owned[object_id_for_return(tid, i + 1)] = _Owned(tid)
             self.task_specs[tid] = spec
+        self._note_child(tid)
         refs = [] if streaming else [ObjectRef(object_id_for_return(tid, i + 1), self.addr,
                                                _cw_obj=self) for i in range(nret)]
         if not spec.get("no_events"):
@@ -2227,11 +2308,18 @@ class CoreWorker:
                     fn = getattr(self.actor_instance, spec["method"])
                 args, kwargs = self._decode_args(spec["args"], spec["owner"])
                 self._apply_runtime_env(spec)
+                on_main = threading.current_thread() is threading.main_thread()
+                if tid in self.cancelled:  # cancelled while its arguments were decoded
+                    raise KeyboardInterrupt
+                if on_main:
+                    self._main_interruptible = True
                 if spec["nret"] == -1:
                     returns = self._run_generator(spec, fn, args, kwargs, conn, reply_to)
                     extra["num_items"] = self._last_gen_count
                 else:
                     result = fn(*args, **kwargs)
+                    if on_main:
+                        self._main_interruptible = False
                     if spec.get("dynamic"):
                         result = _DynamicRefs([self.put_object(v) for v in result])
                     returns = self._package_returns(spec, result)
@@ -2255,8 +2343,11 @@ class CoreWorker:
                 extra["app_error"] = True
                 extra["exc_type"] = type(e).__name__
         finally:
+            if threading.current_thread() is threading.main_thread():
+                self._main_interruptible = False
             with self.lock:
                 self.running.pop(tid, None)
+                self._children.pop(tid, None)
             self.current_task.tid = None
             self.current_task.spec = None
         if not spec.get("no_events"):
@@ -2498,6 +2589,24 @@ class CoreWorker:
         tid = spec["tid"]
         conn = spec.pop("_conn", None)
         owner = spec["owner"]
+        me = asyncio.current_task()
+        with self.lock:
+            self._async_tasks[tid] = (asyncio.get_running_loop(), me)
+        try:
+            await self._run_async_actor_task_body(spec, tid, conn, owner)
+        except asyncio.CancelledError:
+            self._send_reply(conn, owner, tid,
+                             self._error_returns(spec, TaskCancelledError(tid.hex())), {})
+        finally:
+            with self.lock:
+                self._async_tasks.pop(tid, None)
+
+    async def _run_async_actor_task_body(self, spec, tid, conn, owner):
+        import asyncio
+        import inspect
+
+        if tid in self.cancelled:
+            raise asyncio.CancelledError()
         async with self._async_sem:
             self.current_task.tid = tid
             try:
@@ -2548,6 +2657,8 @@ class CoreWorker:
                 self._send_reply(conn, owner, tid, self._package_returns(spec, None), {})
                 self._exit_actor()
                 return
+            except asyncio.CancelledError:
+                raise
             except BaseException as e:  # noqa: BLE001
                 err = RayTaskError.from_exception(e, spec.get("name", "task"), pid=os.getpid())
                 returns = self._error_returns(spec, err)

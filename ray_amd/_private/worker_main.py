@@ -54,6 +54,7 @@ def main():
                     worker_id=random_bytes(16), job_id=job, gpu_ids=gpu_ids,
                     startup_token=args.token)
     W.global_worker.connect_worker(cw)
+    cw.install_cancel_handler()  # ray.cancel interrupts the main thread with a real SIGINT
     hook = os.environ.get("RAY_AMD_SETUP_HOOK")
     if hook:
         cw.run_setup_hook(hook)

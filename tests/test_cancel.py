@@ -1,0 +1,163 @@
+"""ray.cancel semantics (modelled on python/ray/tests/test_cancel.py:73-100, 525-560):
+a running task blocked in a C call (time.sleep, ray.get) is interrupted at once by a real
+SIGINT on the worker's main thread, cancellation during argument deserialisation is
+deferred, recursive cancel reaches child tasks and actor tasks, async actor coroutines are
+cancelled on their loop, and a non-owner's cancel is forwarded to the owner."""
+
+import time
+
+import pytest
+
+import ray_amd as ray
+from ray_amd.exceptions import RayTaskError, TaskCancelledError, WorkerCrashedError
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4)
+    yield
+    ray.shutdown()
+
+
+def _cancelled(ref, timeout=10):
+    t0 = time.time()
+    with pytest.raises((TaskCancelledError, RayTaskError)) as ei:
+        ray.get(ref, timeout=timeout)
+    if isinstance(ei.value, RayTaskError):
+        assert "TaskCancelled" in str(ei.value)
+    return time.time() - t0
+
+
+def test_cancel_task_in_long_sleep_is_immediate(cluster):
+    @ray.remote
+    def sleeper():
+        time.sleep(600)
+        return "finished"
+
+    r = sleeper.remote()
+    time.sleep(1.0)  # running
+    t0 = time.time()
+    ray.cancel(r)
+    _cancelled(r)
+    assert time.time() - t0 < 1.0, "cancel must interrupt the blocking sleep"
+
+    # the worker survived and serves the next task
+    @ray.remote
+    def ok():
+        return 7
+
+    assert ray.get(ok.remote(), timeout=30) == 7
+
+
+def test_cancel_task_blocked_in_ray_get(cluster):
+    @ray.remote
+    def inner():
+        time.sleep(600)
+
+    @ray.remote
+    def outer():
+        return ray.get(inner.remote())
+
+    r = outer.remote()
+    time.sleep(1.5)
+    t0 = time.time()
+    ray.cancel(r)  # recursive by default: inner is cancelled too
+    _cancelled(r)
+    assert time.time() - t0 < 2.0
+
+
+def test_cancel_during_arg_deserialization(cluster):
+    class SlowToDeserialize:
+        def __reduce__(self):
+            def reconstruct():
+                import time as _t
+
+                _t.sleep(3)
+                return SlowToDeserialize()
+
+            return reconstruct, ()
+
+    @ray.remote
+    def dummy(a):
+        raise AssertionError("must never run")
+
+    obj = dummy.remote(SlowToDeserialize())
+    assert len(ray.wait([obj], timeout=0.1)[0]) == 0
+    ray.cancel(obj)
+    _cancelled(obj, timeout=20)
+
+
+def test_force_cancel_kills_worker(cluster):
+    @ray.remote(max_retries=0)
+    def spin():
+        while True:
+            pass
+
+    r = spin.remote()
+    time.sleep(1.0)
+    ray.cancel(r, force=True)
+    with pytest.raises((TaskCancelledError, WorkerCrashedError, RayTaskError)):
+        ray.get(r, timeout=30)
+
+
+def test_recursive_cancel_actor_task(cluster):
+    @ray.remote(num_cpus=0)
+    class Semaphore:
+        def wait(self):
+            time.sleep(600)
+
+    @ray.remote(num_cpus=0)
+    class Canceller:
+        def __init__(self, obj):
+            (self.obj,) = obj
+
+        def cancel(self):
+            ray.cancel(self.obj)  # not the owner: forwarded to the driver
+
+    @ray.remote
+    def task(sema):
+        return ray.get(sema.wait.remote())
+
+    sema = Semaphore.remote()
+    t = task.remote(sema)
+    time.sleep(1.5)
+    c = Canceller.remote((t,))
+    c.cancel.remote()
+    _cancelled(t, timeout=15)
+
+
+def test_cancel_async_actor_coroutine(cluster):
+    import asyncio
+
+    @ray.remote
+    class A:
+        async def slow(self):
+            await asyncio.sleep(600)
+
+        async def fast(self):
+            return 1
+
+    a = A.remote()
+    r = a.slow.remote()
+    time.sleep(1.0)
+    ray.cancel(r)
+    _cancelled(r)
+    assert ray.get(a.fast.remote(), timeout=10) == 1  # the actor keeps serving
+
+
+def test_cancel_does_not_hit_the_next_task(cluster):
+    """A cancel that lands after its task finished must not interrupt the next task on
+    the same worker (the handler checks the running task id)."""
+    @ray.remote
+    def quick(i):
+        return i
+
+    @ray.remote
+    def slowish():
+        time.sleep(1.0)
+        return "done"
+
+    r = quick.remote(1)
+    assert ray.get(r) == 1
+    ray.cancel(r)  # already finished: no effect
+    assert ray.get(slowish.remote(), timeout=30) == "done"
