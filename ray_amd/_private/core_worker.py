@@ -678,7 +678,7 @@ class CoreWorker:
             if buf is not None:
                 return buf
         try:
-            off0 = self.store._alloc(oid, total, False)
+            off0 = self.store._alloc(oid, total, False, wait=False)
         except Exception:
             off0 = None
         if off0 is None:  # store full: assemble on the heap and serve this read from it

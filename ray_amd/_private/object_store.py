@@ -91,21 +91,20 @@ class ObjectStore:
         self._lock = threading.Lock()
         self.spilled_bytes = 0
         self.restored_bytes = 0
+        self.fallback_bytes = 0
+        self.fallback_objects = 0
+        self.waited_allocs = 0
 
     # ------------------------------------------------------------------ write
-    def _alloc(self, oid: bytes, size: int, pinned: bool, device: int = -1) -> int:
+    def _try_make_room(self, oid: bytes, size: int, pinned: bool, device: int) -> int:
         off = self.store.create(oid, size, 0, device, pinned)
         if off != NO_SPACE:
             return off
         # 1) evict unpinned LRU copies
         self.store.evict(size * 2, device)
         off = self.store.create(oid, size, 0, device, pinned)
-        if off != NO_SPACE:
+        if off != NO_SPACE or device >= 0:
             return off
-        if device >= 0:
-            raise ObjectStoreFullError(f"HBM object store on GPU {device} is full "
-                                       f"({self.store.used(device)} / "
-                                       f"{self.store.capacity(device)} bytes)")
         # 2) spill pinned primary copies
         for _ in range(8):
             cands = self.store.spill_candidates(max(size * 2, 64 << 20), device)
@@ -116,12 +115,100 @@ class ObjectStore:
             off = self.store.create(oid, size, 0, device, pinned)
             if off != NO_SPACE:
                 return off
-        raise ObjectStoreFullError(
-            f"object of {size} bytes does not fit in the object store "
-            f"({self.store.used(-1)} / {self.store.capacity(-1)} bytes in use, nothing spillable)")
+        return NO_SPACE
+
+    def _spill_pending(self) -> bool:
+        """Another process on the node is writing a spill file right now (its space frees
+        when the write completes: ``spill`` writes ``<oid>.tmp<pid>`` then renames)."""
+        try:
+            with os.scandir(self.spill_dir) as it:
+                return any(".tmp" in e.name for e in it)
+        except FileNotFoundError:
+            return False
+
+    def _alloc(self, oid: bytes, size: int, pinned: bool, device: int = -1, wait: bool = True):
+        """Offset of a new ``size``-byte entry, or None: the caller then writes the object
+        to the disk-backed fallback (``_fallback_write``).
+
+        The create-request queue of plasma (reference: src/ray/object_manager/plasma/
+        create_request_queue.cc:89-125, plasma_allocator.cc:62-70), per request: evict,
+        spill, and if the object still does not fit, WAIT — with exponential backoff, a
+        local gc pass that drops unreachable zero-copy readers, and the wait extended
+        for as long as spills are in flight — up to ``oom_grace_period_s``
+        (RAY_AMD_OOM_GRACE_PERIOD_S, default 2 s as the reference) of no progress; then
+        allocate from the fallback (a file under the session's spill directory, read
+        back zero-copy through mmap and deleted with the object)."""
+        off = self._try_make_room(oid, size, pinned, device)
+        if off != NO_SPACE:
+            return off
+        if device >= 0:
+            raise ObjectStoreFullError(f"HBM object store on GPU {device} is full "
+                                       f"({self.store.used(device)} / "
+                                       f"{self.store.capacity(device)} bytes)")
+        if not wait:
+            return None
+        if size > self.store.capacity(-1) or os.environ.get("RAY_AMD_OBJECT_STORE_FALLBACK",
+                                                             "1") == "0":
+            if os.environ.get("RAY_AMD_OBJECT_STORE_FALLBACK", "1") == "0":
+                raise ObjectStoreFullError(
+                    f"object of {size} bytes does not fit in the object store "
+                    f"({self.store.used(-1)} / {self.store.capacity(-1)} bytes in use, "
+                    "nothing spillable)")
+            return None  # larger than the whole store: straight to the fallback
+        import gc
+        import time
+
+        grace = float(os.environ.get("RAY_AMD_OOM_GRACE_PERIOD_S", "2.0"))
+        delay = float(os.environ.get("RAY_AMD_OBJECT_STORE_FULL_DELAY_MS", "10")) / 1000.0
+        start = time.monotonic()
+        gc_done = False
+        while True:
+            if not gc_done:
+                gc.collect()  # reference: trigger_global_gc_ (this process's share)
+                gc_done = True
+            time.sleep(delay)
+            delay = min(delay * 2, 0.1)
+            off = self._try_make_room(oid, size, pinned, device)
+            if off != NO_SPACE:
+                self.waited_allocs += 1
+                return off
+            if self._spill_pending():
+                start = time.monotonic()  # progress is being made: reset the grace period
+                continue
+            if time.monotonic() - start >= grace:
+                return None
+
+    def _fallback_write(self, oid: bytes, size: int, fill):
+        """Disk-backed fallback allocation: the object's bytes in ``<spill_dir>/<oid>``,
+        written through a shared writable mapping (no staging copy) and published by
+        rename, where every reader (get_buffer, contains, the cross-node pull) already
+        looks for file-backed objects."""
+        p = self._spill_path(oid)
+        tmp = p + f".fb{os.getpid()}"
+        with open(tmp, "wb+") as f:
+            f.truncate(max(size, 1))
+            if size:
+                mm = mmap.mmap(f.fileno(), size)
+                try:
+                    mv = memoryview(mm)
+                    try:
+                        fill(mv)
+                    finally:
+                        mv.release()
+                finally:
+                    mm.close()
+        os.replace(tmp, p)
+        self.fallback_bytes += size
+        self.fallback_objects += 1
 
     def put_serialized(self, oid: bytes, sobj: "ser.SerializedObject", pinned: bool = True):
         off = self._alloc(oid, sobj.total, pinned)
+        if off is None:
+            def fill(mv):
+                sobj.write_to(mv)
+
+            self._fallback_write(oid, sobj.total, fill)
+            return
         if sobj.total >= POPULATE_MIN:
             self.store.populate(off, sobj.total)
         try:
@@ -138,6 +225,12 @@ class ObjectStore:
     def put_bytes(self, oid: bytes, data, pinned: bool = True):
         n = len(data)
         off = self._alloc(oid, n, pinned)
+        if off is None:
+            def fill(mv):
+                mv[:n] = memoryview(data).cast("B")
+
+            self._fallback_write(oid, n, fill)
+            return
         if n >= POPULATE_MIN:
             self.store.populate(off, n)
         try:
@@ -205,6 +298,9 @@ class ObjectStore:
             "evictions": self.store.evictions(),
             "spilled_bytes": self.spilled_bytes,
             "restored_bytes": self.restored_bytes,
+            "fallback_bytes": self.fallback_bytes,
+            "fallback_objects": self.fallback_objects,
+            "waited_allocs": self.waited_allocs,
         }
 
 

@@ -133,3 +133,82 @@ def test_spilled_objects_roundtrip_through_runtime(tmp_path):
         assert ray.get([total.remote(r) for r in refs[:4]]) == [16 * i for i in range(4)]
     finally:
         ray.shutdown()
+
+
+def test_put_falls_back_to_disk_when_readers_pin_the_store(tmp_path, monkeypatch):
+    """The round-4 probe: a 300 MiB store, zero-copy readers holding two 100 MiB objects,
+    a third 100 MiB put. Nothing is spillable (both are pinned by readers), so after the
+    grace period the put is served by the disk-backed fallback allocation (reference:
+    create_request_queue.cc:89-125, plasma_allocator.cc:62-70) — readable zero-copy,
+    deleted with the object."""
+    monkeypatch.setenv("RAY_AMD_OOM_GRACE_PERIOD_S", "0.5")
+    ray.init(num_cpus=1, object_store_memory=300 << 20)
+    try:
+        a = ray.put(np.full(100 << 20, 1, dtype=np.uint8))
+        b = ray.put(np.full(100 << 20, 2, dtype=np.uint8))
+        ra, rb = ray.get(a), ray.get(b)  # zero-copy readers pin both
+        t0 = time.time()
+        c = ray.put(np.full(100 << 20, 3, dtype=np.uint8))
+        assert time.time() - t0 >= 0.4  # waited the grace period first
+        rc = ray.get(c)
+        assert int(rc[0]) == 3 and int(rc[-1]) == 3 and rc.shape == (100 << 20,)
+        assert not rc.flags.writeable  # still a zero-copy (mmap) view
+        assert int(ra[-1]) == 1 and int(rb[0]) == 2
+
+        @ray.remote
+        def tail(x):
+            return int(x[-1])
+
+        assert ray.get(tail.remote(c)) == 3  # a worker reads the fallback object too
+        from ray_amd._private import worker as W
+
+        st = W.global_worker.core.store.stats()
+        assert st["fallback_objects"] >= 1
+        spill_dir = W.global_worker.core.store.spill_dir
+        path = os.path.join(spill_dir, c.binary().hex())
+        assert os.path.exists(path)
+        del rc, c
+        import gc
+
+        gc.collect()
+        deadline = time.time() + 10
+        while os.path.exists(path) and time.time() < deadline:
+            time.sleep(0.1)
+        assert not os.path.exists(path)  # freed with the object
+    finally:
+        ray.shutdown()
+
+
+def test_put_waits_for_space_instead_of_failing(tmp_path, monkeypatch):
+    """A put that does not fit while a reader pins the only spill candidate waits (grace
+    period) and lands IN the store once the reader lets go; and while another process's
+    spill is in flight the grace period keeps restarting, so the put keeps waiting instead
+    of falling back."""
+    import threading
+
+    monkeypatch.setenv("RAY_AMD_OOM_GRACE_PERIOD_S", "1.0")
+    spill = str(tmp_path / "spill")
+    st = ObjectStore(str(tmp_path / "segw"), spill, create=True, size=48 << 20,
+                     table_cap=1024)
+    blob = bytes(30 << 20)
+    st.put_bytes(_oid(1), blob, pinned=True)
+    reader = st.get_buffer(_oid(1))  # pins the only candidate: not spillable now
+    # an in-flight spill of another process: its temp file exists for 2.5 s
+    marker = os.path.join(spill, "ff" * 20 + ".tmp999")
+    open(marker, "wb").close()
+
+    def release():
+        time.sleep(2.5)
+        os.unlink(marker)
+        reader.release()  # the pin goes: the object becomes spillable
+
+    th = threading.Thread(target=release)
+    th.start()
+    t0 = time.time()
+    st.put_bytes(_oid(2), blob, pinned=True)
+    waited = time.time() - t0
+    th.join()
+    assert waited >= 2.0  # kept waiting while the spill was in flight (grace was 1 s)
+    assert st.store.contains(_oid(2))  # allocated in the store, not the fallback
+    assert st.stats()["fallback_objects"] == 0 and st.stats()["waited_allocs"] == 1
+    assert os.path.exists(os.path.join(spill, _oid(1).hex()))  # the old one was spilled
