@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gpt2",
-                    choices=["gpt2", "ppo", "impala", "data", "microbench"])
+                    choices=["gpt2", "ppo", "impala", "data", "microbench", "allreduce"])
+    ap.add_argument("--max-mb", type=int, default=256,
+                    help="allreduce workload: largest all-reduce size (MiB), swept from 1 MiB "
+                         "in powers of two")
     ap.add_argument("--no-ray", action="store_true",
                     help="gpt2: run the identical step in a bare torch.distributed loop "
                          "(one process per GPU under torch.distributed.run) instead of "
@@ -131,6 +134,11 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
         "final_loss": round(r["loss"], 4),
         "ddp_allreduce_launches": r.get("ddp_allreduce_launches"),
     }
+    # self-diagnosing multi-GPU runs: exposed comm, all-reduce launches / bytes and
+    # per-bucket bus bandwidth per rank (FlatDDP.read_stats; zeros at world 1)
+    out.update(r.get("ddp_stats") or {"ddp_exposed_comm_ms_per_step": 0.0,
+                                       "ddp_allreduce_launches_per_step": 0.0,
+                                       "ddp_allreduce_mb_per_step": 0.0})
     print(json.dumps(out), flush=True)
 
 
@@ -242,6 +250,64 @@ def _rank0_only(args, fn):
         dist.destroy_process_group()
 
 
+def bench_allreduce(args):
+    """RCCL (gloo with --device cpu) all-reduce size sweep, 1 MiB .. --max-mb MiB fp32, one
+    process per GPU under torch.distributed.run: per size the median time of --steps
+    launches after --warmup, algorithm and bus bandwidth (busbw = bytes / t x 2 (n-1) / n,
+    what each xGMI link of the ring carries). Explains a GPT-2 scaling curve: FlatDDP's
+    32 MiB buckets sit on this curve."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29571")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    if args.device == "cpu":
+        dev = torch.device("cpu")
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
+    rows = []
+    mib = 1
+    while mib <= args.max_mb:
+        x = torch.ones(mib * (1 << 20) // 4, dtype=torch.float32, device=dev)
+        for _ in range(args.warmup):
+            dist.all_reduce(x)
+        times = []
+        for _ in range(args.steps):
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            dist.all_reduce(x)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t0)
+        t = sorted(times)[len(times) // 2]
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt)
+        nbytes = mib * (1 << 20)
+        algbw = nbytes / t / 1e9
+        factor = 2.0 * (world - 1) / world if world > 1 else 1.0
+        rows.append({"mib": mib, "ms": round(t * 1e3, 4), "algbw_gbps": round(algbw, 2),
+                     "busbw_gbps": round(algbw * factor, 2)})
+        mib *= 2
+    if rank == 0:
+        print(json.dumps({"metric": "allreduce_busbw_gbps", "value": rows[-1]["busbw_gbps"],
+                          "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "higher_is_better": True,
+                          "backend": dist.get_backend(), "dtype": "fp32",
+                          "data": "synthetic", "sweep": rows}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload == "gpt2":
@@ -257,6 +323,8 @@ def main():
         from ray_amd.rllib.bench import bench_impala
 
         _rank0_only(args, bench_impala)
+    elif args.workload == "allreduce":
+        bench_allreduce(args)
     elif args.workload == "data":
         from ray_amd.data.bench import bench_data
 

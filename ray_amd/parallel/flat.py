@@ -49,7 +49,13 @@ def _round(n: int, a: int = ALIGN) -> int:
 
 class FlatParams:
     def __init__(self, module: torch.nn.Module, dtype=torch.bfloat16,
-                 no_decay: callable | None = None, grad_dtype=torch.float32):
+                 no_decay: callable | None = None, grad_dtype=torch.float32,
+                 transpose: callable | None = None):
+        """``transpose(name, p) -> bool``: 2-D (decayed) weights that keep a transposed bf16
+        copy W^T (``p._ra_wt_view``) refreshed by the fused AdamW kernel itself
+        (``ra_adamw_flat_wt``) — the nn.Linear input-gradient GEMM reads it
+        (ops.functional._transposed_weight). Those weights go first in the buffer,
+        [0, n_wt)."""
         self.module = module
         seen = {}
         for name, p in module.named_parameters():
@@ -60,6 +66,12 @@ class FlatParams:
             no_decay = lambda name, p: p.dim() < 2  # noqa: E731
         dec = [(n, p) for n, p in params if not no_decay(n, p)][::-1]
         nod = [(n, p) for n, p in params if no_decay(n, p)][::-1]
+        wt = []
+        if transpose is not None and dtype == torch.bfloat16 and dev_is_cuda(params):
+            wt = [(n, p) for n, p in dec if p.dim() == 2 and p.shape[1] % 4 == 0
+                  and p.is_contiguous() and transpose(n, p)]
+            ids = {id(p) for _, p in wt}
+            dec = wt + [(n, p) for n, p in dec if id(p) not in ids]
         self.order = dec + nod
         dev = params[0][1].device
         offs = []
@@ -80,6 +92,10 @@ class FlatParams:
         self.g = torch.zeros(o, dtype=grad_dtype, device=dev)
         self.offsets = offs
         self.names = [n for n, _ in self.order]
+        self.n_wt = sum(_round(p.numel()) for _, p in wt)
+        self.pt16 = None
+        self.wt_table = None
+        self.wt_tiles = 0
         # .grad can alias the flat buffer only when dtypes match; otherwise autograd
         # gradients are folded in by a post-accumulate hook (registered before any DDP
         # readiness hook, so the bucket never launches before the add)
@@ -104,6 +120,48 @@ class FlatParams:
                     self._fold_hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
                 # ray_amd.ops backward kernels accumulate straight into p._ra_grad
                 p._ra_direct_grad = True
+        if wt:
+            self._build_wt(wt)
+
+    def _build_wt(self, wt):
+        """pt16 (mirrors [0, n_wt): W^T [C, R] at W's own offset) + the device segment table
+        of ra_adamw_flat_wt; the copies start fresh (the optimizer keeps them so)."""
+        import numpy as np
+
+        L = _lib.lib()
+        if len(wt) > L.ra_wt_max_segments():
+            return
+        self.pt16 = torch.empty(self.n_wt, dtype=torch.bfloat16, device=self.device)
+        segs = np.zeros(len(wt), dtype=[("off", "<i8"), ("R", "<i4"), ("C", "<i4"),
+                                        ("tile0", "<i4"), ("tc", "<i4")])
+        tile = 0
+        with torch.no_grad():
+            for i, ((n, p), off) in enumerate(zip(wt, self.offsets)):
+                R, C = p.shape
+                tr, tc = (R + 63) // 64, (C + 63) // 64
+                segs[i] = (off, R, C, tile, tc)
+                tile += tr * tc
+                view = self.pt16[off:off + R * C].view(C, R)
+                view.copy_(p.detach().t())
+                p._ra_wt_view = view
+        self.wt_tiles = tile
+        blob = np.zeros(L.ra_wt_table_bytes(), dtype=np.uint8)
+        blob[:4] = np.frombuffer(np.int32(len(wt)).tobytes(), dtype=np.uint8)
+        raw = segs.tobytes()
+        blob[8:8 + len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+        self.wt_table = torch.from_numpy(blob).to(self.device)
+        self.wt_params = [p for _, p in wt]
+        self.mark_wt_fresh()
+
+    def mark_wt_fresh(self):
+        """Record that every W^T copy matches its weight as of now (the validity key that
+        ops.functional._transposed_weight checks before trusting the copy)."""
+        from ray_amd.ops import functional as rf
+
+        ep = rf.weights_epoch()
+        for p in getattr(self, "wt_params", ()):
+            p._ra_wt_key = (ep, p._version)
+            p._ra_wt_ev = None
 
     @staticmethod
     def _view(buf, off, shape, channels_last):
@@ -125,6 +183,10 @@ class FlatParams:
     def sync_master_from_params(self):
         with torch.no_grad():
             self.p32.copy_(self.p16.float())
+
+
+def dev_is_cuda(params) -> bool:
+    return bool(params) and params[0][1].is_cuda
 
 
 def _fold_grad(p):
@@ -183,6 +245,11 @@ class FlatDDP:
         self.enabled = self.world > 1 or (always_hook and dist.is_initialized())
         self.sync = True  # False inside gradient-accumulation micro-steps (no_sync)
         self.launched = 0  # all_reduce launches since construction (tests / bench report)
+        self.launched_bytes = 0
+        # per-step diagnostics (bench.py): per-bucket all-reduce time on the comm stream and
+        # the main stream's exposed wait in finish(), as CUDA events read after a sync
+        self.stats = False
+        self._step_events: list = []  # [(kind, bytes, ev_start, ev_end)]
         cuda = flat.g.is_cuda and self.enabled
         self._comm = torch.cuda.Stream(flat.device) if cuda else None
         # the training loop's stream (backward's main stream); hooks may fire while a side
@@ -235,9 +302,22 @@ class FlatDDP:
                 ev.record(st)
                 self._comm.wait_event(ev)
             with torch.cuda.stream(self._comm):
+                if self.stats:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(self._comm)
                 work = dist.all_reduce(self.flat.g[s:e], group=self.group, async_op=True)
+                if self.stats:
+                    # the comm stream waits for the collective: the next bucket's start
+                    # event then marks an idle RCCL stream, so (ev0, ev1) is this bucket's
+                    # all-reduce time, not queueing behind the previous one
+                    work.wait()
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(self._comm)
+                    self._step_events.append(("bucket", (e - s) * self.flat.g.element_size(),
+                                              ev0, ev1))
         self._works.append(work)
         self.launched += 1
+        self.launched_bytes += (e - s) * self.flat.g.element_size()
 
     def _make_hook(self, i: int):
         b = self.param_bucket[i]
@@ -270,11 +350,50 @@ class FlatDDP:
                 self._works.append(dist.all_reduce(self.flat.g[s:e], group=self.group,
                                                    async_op=True))
                 self.launched += 1
+                self.launched_bytes += (e - s) * self.flat.g.element_size()
+        t_ev = None
+        if self.stats and self.flat.g.is_cuda:
+            # recorded after the side-stream join: only the wait for RCCL lies between
+            t_ev = torch.cuda.Event(enable_timing=True)
+            t_ev.record()
         for w in self._works:
             w.wait()  # the current stream waits on RCCL's stream (no host block)
+        if t_ev is not None:
+            t_end = torch.cuda.Event(enable_timing=True)
+            t_end.record()
+            self._step_events.append(("exposed", 0, t_ev, t_end))
         self._works.clear()
         self._ready = [0] * len(self.buckets)
         self._seen = [False] * len(self.flat.order)
+
+    def reset_stats(self):
+        self._step_events = []
+        self._stats_launched = self.launched
+        self._stats_bytes = self.launched_bytes
+
+    def read_stats(self, steps: int) -> dict:
+        """Per-step DDP diagnostics since ``reset_stats`` (call after a device sync):
+        exposed communication (the main stream's wait for RCCL in finish()), all-reduce
+        launches / bytes per step, and per-bucket all-reduce time and bus bandwidth
+        (busbw = bytes / t x 2 (n - 1) / n, the ring all-reduce's per-link traffic)."""
+        steps = max(1, steps)
+        exposed = [a.elapsed_time(b) for k, _, a, b in self._step_events if k == "exposed"]
+        buckets = [(n, a.elapsed_time(b)) for k, n, a, b in self._step_events if k == "bucket"]
+        n = self.world
+        factor = 2.0 * (n - 1) / n if n > 1 else 1.0
+        bus = [nb / (ms * 1e-3) / 1e9 * factor for nb, ms in buckets if ms > 0]
+        launched = self.launched - getattr(self, "_stats_launched", 0)
+        nbytes = self.launched_bytes - getattr(self, "_stats_bytes", 0)
+        return {
+            "ddp_exposed_comm_ms_per_step": round(sum(exposed) / steps, 4) if exposed else 0.0,
+            "ddp_allreduce_launches_per_step": round(launched / steps, 2),
+            "ddp_allreduce_mb_per_step": round(nbytes / steps / 2 ** 20, 2),
+            "ddp_allreduce_ms_per_step": round(sum(ms for _, ms in buckets) / steps, 4)
+            if buckets else 0.0,
+            "ddp_bucket_busbw_gbps_mean": round(sum(bus) / len(bus), 2) if bus else None,
+            "ddp_bucket_busbw_gbps_min": round(min(bus), 2) if bus else None,
+            "ddp_buckets": len(self.buckets),
+        }
 
     @property
     def grad_scale(self) -> float:
@@ -352,6 +471,17 @@ class FlatAdamW:
             else:
                 gptr = None
             g32 = f.g.dtype == torch.float32
+            if f.pt16 is not None:
+                # AdamW + the W^T copies of the linear weights in one pass
+                check(L.ra_adamw_flat_wt(ptr(f.p32), ptr(f.p16), ptr(f.pt16), ptr(f.g),
+                                         ptr(self.m), ptr(self.v), f.numel, f.n_decay, f.n_wt,
+                                         ptr(f.wt_table), f.wt_tiles, lr, self.b1, self.b2,
+                                         self.eps, self.wd, self.step_count, gptr,
+                                         (1 if g32 else 0) | (2 if self.zero_grad else 0),
+                                         ptr(self.hyper) if self.hyper is not None else None, s),
+                      "adamw_wt")
+                f.mark_wt_fresh()
+                return
             check(L.ra_adamw_flat_dev(ptr(f.p32), ptr(f.p16) if f.p16 is not f.p32 else None,
                                       ptr(f.g), ptr(self.m), ptr(self.v), f.numel, f.n_decay,
                                       lr, self.b1, self.b2, self.eps, self.wd, self.step_count,

@@ -146,6 +146,9 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
     if on_gpu and (c.get("step_graph") or os.environ.get("RAY_AMD_STEP_GRAPH") == "1"):
         graphed = tr.enable_graph(batches(c["warmup"]))
         sync()
+    diag = on_gpu and tr.ddp.enabled and os.environ.get("RAY_AMD_DDP_STATS", "1") == "1"
+    tr.ddp.stats = diag
+    tr.ddp.reset_stats()
     if world > 1:
         dist.barrier()
     sync()
@@ -157,6 +160,15 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         dist.barrier()
     sync()
     dt = time.perf_counter() - t0
+    ddp_stats = tr.ddp.read_stats(c["steps"])
+    if world > 1:  # per-rank diagnostics gathered to every rank (rank 0 reports them)
+        vals = torch.tensor([ddp_stats["ddp_exposed_comm_ms_per_step"],
+                             ddp_stats["ddp_allreduce_ms_per_step"]], device=device,
+                            dtype=torch.float64)
+        allv = [torch.zeros_like(vals) for _ in range(world)]
+        dist.all_gather(allv, vals)
+        ddp_stats["per_rank_exposed_comm_ms"] = [round(float(v[0]), 4) for v in allv]
+        ddp_stats["per_rank_allreduce_ms"] = [round(float(v[1]), 4) for v in allv]
     loss = float(tr.last_loss)
     per_rank = [dt]
     if world > 1:
@@ -192,6 +204,7 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         "ddp_hooks": "on" if tr.ddp.enabled else "off",
         "ddp_allreduce_launches": tr.ddp.launched,
         "step_graph": graphed,
+        "ddp_stats": ddp_stats,
     }
 
 
@@ -200,8 +213,8 @@ def _wgrad_mode(on_gpu: bool) -> str:
         return "torch"
     from ray_amd.ops import functional as rf
 
-    return {"lt": "hipblaslt-lt-beta1", "lt-splitk": "splitk-partials-hipblaslt-tuned"}.get(
-        rf._WGRAD, "splitk-partials-torch-bmm")
+    return {"lt": "hipblaslt-lt-beta1", "lt-splitk": "splitk-partials-hipblaslt-tuned",
+            "hip": "hip-wgrad-kernel"}.get(rf._WGRAD, "splitk-partials-torch-bmm")
 
 
 def train_func(config: dict):

@@ -158,6 +158,34 @@ def test_bench_launcher_gloo_two_ranks(no_ray):
     assert j["config"]["launcher"] == ("torch.distributed.run (no Ray)" if no_ray
                                        else "ray_amd TorchTrainer")
     assert abs(j["final_loss"] - 6.24) < 0.05  # same seed, same synthetic data either way
+    # self-diagnosing N>1 runs: per-rank exposed comm / all-reduce time, launches and
+    # bytes per step (every bucket of the flat fp32 gradient once per step)
+    assert j["ddp_allreduce_launches_per_step"] >= 1
+    assert j["ddp_allreduce_mb_per_step"] > 0
+    assert len(j["per_rank_exposed_comm_ms"]) == 2 and len(j["per_rank_allreduce_ms"]) == 2
+    assert "ddp_exposed_comm_ms_per_step" in j and "ddp_bucket_busbw_gbps_mean" in j
+
+
+def test_bench_allreduce_workload_gloo_two_ranks():
+    """bench.py --workload allreduce: the collective size sweep (1 MiB .. 256 MiB on RCCL;
+    small sizes on gloo here) with per-size time and bus bandwidth."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29621", "bench.py", "--gpus", "2",
+           "--device", "cpu", "--workload", "allreduce", "--steps", "3", "--warmup", "1",
+           "--max-mb", "4"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _bench_json(r.stdout)
+    assert j["metric"] == "allreduce_busbw_gbps" and j["n_gpus"] == 2
+    sizes = [row["mib"] for row in j["sweep"]]
+    assert sizes == [1, 2, 4]
+    assert all(row["busbw_gbps"] > 0 and row["ms"] > 0 for row in j["sweep"])
+    assert j["value"] == j["sweep"][-1]["busbw_gbps"]
 
 
 def test_accelerate_amp_bf16_and_fp16_cpu():
