@@ -51,6 +51,10 @@ _SIGS = {
                      c_void_p],
     "ra_adamw_flat": [c_void_p] * 5 + [c_long, c_long] + [c_float] * 5 + [c_int, c_void_p,
                                                                             c_int, c_void_p],
+    "ra_adamw_flat_wt": [c_void_p] * 6 + [c_long, c_long, c_long, c_void_p, c_int]
+                        + [c_float] * 5 + [c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "ra_wt_table_bytes": [],
+    "ra_wt_max_segments": [],
     "ra_adamw_flat_dev": [c_void_p] * 5 + [c_long, c_long] + [c_float] * 5 +
     [c_int, c_void_p, c_int, c_void_p, c_void_p],
     "ra_set_knob": [c_int, c_int],

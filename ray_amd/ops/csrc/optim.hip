@@ -230,3 +230,156 @@ RA_EXPORT int ra_sgd_flat(float* p32, void* p16, const void* g, float* buf, long
                      (const bf16_t*)g, buf, n / 4, lr, mom, wd, gscale);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// AdamW that also refreshes the transposed bf16 copy W^T of every nn.Linear weight
+// (the dX = dY . W input-gradient GEMM reads W^T so that it runs in the forward GEMMs'
+// operand layout: ops/functional.py _transposed_weight). The flat layout puts those
+// weights first, [0, n_wt) (FlatParams(transpose=...)); each is processed as 64 x 64
+// tiles: the tile's p/m/v/g are read and written row-major (coalesced, as the 1-D pass),
+// its bf16 values go through an LDS tile and are stored transposed — also coalesced — into
+// pt16, which mirrors [0, n_wt) with W^T [C][R] at the weight's own offset. The rest of
+// the buffer, [n_wt, n), is the ordinary 1-D grid-stride pass. One launch, one HBM pass:
+// the per-weight transpose kernels that used to run beside the forward GEMMs are gone.
+struct WtSeg {
+  long off;   // flat offset (elements) of W [R][C] (= offset of W^T in pt16)
+  int R, C;   // C % 4 == 0
+  int tile0;  // first tile index of this segment
+  int tc;     // tiles along C
+};
+constexpr int kWtMaxSeg = 256;
+struct WtTable {
+  int nseg;
+  WtSeg seg[kWtMaxSeg];
+};
+
+__device__ __forceinline__ void adam_elem4(float (&pa)[4], float (&ma)[4], float (&va)[4],
+                                           const float (&gv)[4], float sc, float b1, float b2,
+                                           float eps, float lr, float rbc1, float rbc2,
+                                           float decay) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gr = gv[j] * sc;
+    ma[j] = b1 * ma[j] + (1.f - b1) * gr;
+    va[j] = b2 * va[j] + (1.f - b2) * gr * gr;
+    const float upd = (ma[j] * rbc1) / (sqrtf(va[j] * rbc2) + eps);
+    pa[j] = pa[j] * decay - lr * upd;
+  }
+}
+
+template <typename G, bool ZERO>
+__global__ __launch_bounds__(256) void adamw_wt_kernel(
+    float* __restrict__ p32, bf16_t* __restrict__ p16, bf16_t* __restrict__ pt16,
+    G* __restrict__ g, float* __restrict__ m, float* __restrict__ v, long n4, long nd,
+    long nwt4, int ntiles, float lr, float b1, float b2, float eps, float wd, float rbc1,
+    float rbc2, const float* __restrict__ gscale, const float* __restrict__ hyper,
+    const WtTable* __restrict__ tab) {
+  const float sc = gscale ? *gscale : 1.f;
+  if (hyper) {
+    lr = hyper[0];
+    rbc1 = hyper[1];
+    rbc2 = hyper[2];
+  }
+  auto load_g = [&](long i, float (&gv)[4]) __attribute__((always_inline)) {
+    if constexpr (sizeof(G) == 2) {
+      unpack4(reinterpret_cast<const uint2*>(g)[i], gv);
+      if (ZERO) reinterpret_cast<uint2*>(g)[i] = make_uint2(0u, 0u);
+    } else {
+      const float4 g4 = reinterpret_cast<const float4*>(g)[i];
+      gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
+      if (ZERO) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto update4 = [&](long i, float (&pa)[4]) __attribute__((always_inline)) {
+    float gv[4];
+    load_g(i, gv);
+    const float4 p = reinterpret_cast<float4*>(p32)[i];
+    const float4 mm = reinterpret_cast<float4*>(m)[i];
+    const float4 vv = reinterpret_cast<float4*>(v)[i];
+    pa[0] = p.x, pa[1] = p.y, pa[2] = p.z, pa[3] = p.w;
+    float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+    adam_elem4(pa, ma, va, gv, sc, b1, b2, eps, lr, rbc1, rbc2,
+               (4 * i < nd) ? (1.f - lr * wd) : 1.f);
+    reinterpret_cast<float4*>(p32)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+    reinterpret_cast<uint2*>(p16)[i] = pack4(pa);
+  };
+
+  if ((int)blockIdx.x < ntiles) {
+    // ---- one 64 x 64 tile of a transposed weight
+    __shared__ __attribute__((aligned(16))) bf16_t tl[64 * 72];  // [col][row], 144-B rows
+    const int b = blockIdx.x;
+    int s = 0;
+    while (s + 1 < tab->nseg && tab->seg[s + 1].tile0 <= b) ++s;
+    const WtSeg sg = tab->seg[s];
+    const int t = b - sg.tile0;
+    const int r0 = (t / sg.tc) * 64, c0 = (t % sg.tc) * 64;
+    const int lr_ = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + lr_ + 16 * i, c = c0 + lc;
+      float pa[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < sg.R && c < sg.C) update4((sg.off + (long)r * sg.C + c) >> 2, pa);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tl[(lc + j) * 72 + lr_ + 16 * i] = f2bf(pa[j]);
+    }
+    __syncthreads();
+    // W^T rows c0 + cc, 16 rows of W (32 B) per thread
+    const int cc = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;
+    const int c = c0 + cc;
+    if (c < sg.C) {
+      const uint4 a0 = *reinterpret_cast<const uint4*>(tl + cc * 72 + rr);
+      const uint4 a1 = *reinterpret_cast<const uint4*>(tl + cc * 72 + rr + 8);
+      bf16_t* dst = pt16 + sg.off + (long)c * sg.R + r0 + rr;
+      if (r0 + rr + 16 <= sg.R && (sg.R % 8) == 0) {
+        reinterpret_cast<uint4*>(dst)[0] = a0;
+        reinterpret_cast<uint4*>(dst)[1] = a1;
+      } else {
+        const bf16_t* src = tl + cc * 72 + rr;
+        for (int k = 0; k < 16 && r0 + rr + k < sg.R; ++k) dst[k] = src[k];
+      }
+    }
+    return;
+  }
+  // ---- 1-D grid-stride over [n_wt, n)
+  const long stride = (long)(gridDim.x - ntiles) * blockDim.x;
+  for (long i = nwt4 + (long)(blockIdx.x - ntiles) * blockDim.x + threadIdx.x; i < n4;
+       i += stride) {
+    float pa[4];
+    update4(i, pa);
+  }
+}
+
+// AdamW over the flat buffer + W^T refresh of the table's weights (device table built by
+// FlatParams: WtTable bytes). n_wt: elements at the start of the buffer covered by the
+// table (every segment lies inside [0, n_wt), which must lie inside the decay group or
+// straddle nothing: decay is decided per element against n_decay). flags as
+// ra_adamw_flat_dev.
+RA_EXPORT int ra_adamw_flat_wt(float* p32, void* p16, void* pt16, void* g, float* m, float* v,
+                               long n, long n_decay, long n_wt, const void* table, int ntiles,
+                               float lr, float b1, float b2, float eps, float wd, int step,
+                               const float* gscale, int flags, const float* hyper,
+                               hipStream_t st) {
+  if (n % 4 || n_decay % 4 || n_wt % 4 || !p16 || !pt16 || !table || ntiles < 0)
+    return hipErrorInvalidValue;
+  const float rbc1 = 1.f / (1.f - powf(b1, (float)step));
+  const float rbc2 = 1.f / (1.f - powf(b2, (float)step));
+  const int g1 = ra_grid((n - n_wt) / 4, 256);
+  const dim3 grid(ntiles + g1), blk(256);
+#define A(G, Z)                                                                             \
+  hipLaunchKernelGGL((adamw_wt_kernel<G, Z>), grid, blk, 0, st, p32, (bf16_t*)p16,          \
+                     (bf16_t*)pt16, (G*)g, m, v, n / 4, n_decay, n_wt / 4, ntiles, lr, b1,  \
+                     b2, eps, wd, rbc1, rbc2, gscale, hyper, (const WtTable*)table)
+  switch (flags & 3) {
+    case 0: A(bf16_t, false); break;
+    case 1: A(float, false); break;
+    case 2: A(bf16_t, true); break;
+    default: A(float, true);
+  }
+#undef A
+  return hipGetLastError();
+}
+
+RA_EXPORT int ra_wt_table_bytes() { return (int)sizeof(WtTable); }
+RA_EXPORT int ra_wt_max_segments() { return kWtMaxSeg; }

@@ -263,11 +263,13 @@ def bias_residual(h, bias, res):
 
 
 # --------------------------------------------------------------------- linear (split-K wgrad)
-# Weight-gradient GEMMs (fp32 out): "lt-splitk" (default) = split-K fp32 partials from a
+# Weight-gradient GEMMs (fp32 out): "hip" (default) = the hand-written CDNA4 kernel
+# (ops/csrc/wgrad.hip, bias gradient fused; measured -2.3 ms/step vs "lt-splitk" on MI355X,
+# profiles/r5/r5c); "lt-splitk" = split-K fp32 partials from a
 # tuned strided-batched hipBLASLt GEMM (ops/lt.py) summed by ra_splitk_accum; "splitk" =
 # the same with torch.bmm's heuristic kernel; "lt" = one tuned GEMM accumulating straight
 # into the fp32 sink (beta = 1; measured slower at GPT-2 shapes: K = 65536 wants split-K)
-_WGRAD = os.environ.get("RAY_AMD_WGRAD", "lt-splitk")
+_WGRAD = os.environ.get("RAY_AMD_WGRAD", "hip")
 # attention backward: "split" (dkdv + dq kernels, no atomics, bitwise reproducible dQ) or
 # "fused" (dK, dV, dQ in one pass with fp32 dQ atomics). Measured at GPT-2 small, B 64
 # (profiles/r2/attn_bwd_fused_vs_split.md): split 384 + 337 us, fused 730 us — the fused
@@ -437,9 +439,36 @@ def bump_weights_epoch():
     _weights_epoch[0] += 1
 
 
+def weights_epoch() -> int:
+    return _weights_epoch[0]
+
+
 def _transposed_weight(w):
     """(Wt, event): W^T contiguous, refreshed on the side stream when the weights changed
-    since the last refresh (always under graph capture, where host state is frozen)."""
+    since the last refresh (always under graph capture, where host state is frozen).
+
+    Weights of a FlatParams built with ``transpose=`` own a W^T view (``_ra_wt_view``) that
+    the fused AdamW kernel rewrites every step: it is used as is (no kernel, no event) while
+    its validity key matches, and under graph capture (the captured optimizer step keeps it
+    fresh on every replay). Any other in-place change of W (copy_, load) bumps its version,
+    and the copy is refreshed into the same view by the side-stream transpose."""
+    view = getattr(w, "_ra_wt_view", None)
+    if view is not None:
+        if torch.cuda.is_current_stream_capturing() or \
+                getattr(w, "_ra_wt_key", None) == (_weights_epoch[0], w._version):
+            return view, getattr(w, "_ra_wt_ev", None)
+        side = _side_stream(w.device)
+        side.wait_stream(torch.cuda.current_stream(w.device))
+        with torch.cuda.stream(side):
+            check(_lib.lib().ra_transpose_bf16(ptr(w), ptr(view), w.shape[0], w.shape[1],
+                                               side.cuda_stream), "transpose_bf16")
+            ev = torch.cuda.Event()
+            ev.record(side)
+        w._ra_wt_key = (_weights_epoch[0], w._version)
+        # later users on the main stream must see the refresh: keep the event until the
+        # next optimizer step marks the view fresh again
+        w._ra_wt_ev = ev
+        return view, ev
     cache = getattr(w, "_ra_wt", None)
     key = (_weights_epoch[0], w._version, w.data_ptr())  # kernel updates, copy_(), rebinding
     stale = cache is None or cache[1] != key or torch.cuda.is_current_stream_capturing()
@@ -480,7 +509,8 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.wt is not None:
                 wt, ev = ctx.wt
-                torch.cuda.current_stream(dy2.device).wait_event(ev)
+                if ev is not None:
+                    torch.cuda.current_stream(dy2.device).wait_event(ev)
                 dx = (dy2 @ wt.t()).view(x.shape)
             else:
                 dx = (dy2 @ w).view(x.shape)

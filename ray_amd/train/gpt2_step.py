@@ -37,7 +37,16 @@ class GPT2Trainer:
         model = GPT2(cfg).to(device=self.device, dtype=param_dtype)
         model.lm_head_chunk = lm_head_chunk
         self.model = model
-        self.flat = FlatParams(model, dtype=param_dtype, grad_dtype=grad_dtype)
+        from ray_amd.ops import functional as rf
+
+        # the block linear weights keep a W^T copy refreshed by the fused AdamW pass (the
+        # input-gradient GEMMs read it; no per-weight transpose kernels beside the forward)
+        import os
+
+        flat_wt = rf._DGRAD_WT and os.environ.get("RAY_AMD_FLAT_WT", "1") == "1"
+        transpose = (lambda n, p: n.endswith("_w")) if flat_wt else None
+        self.flat = FlatParams(model, dtype=param_dtype, grad_dtype=grad_dtype,
+                               transpose=transpose)
         self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb, always_hook=ddp_always_hook)
         # AdamW clears the flat gradient in its own pass (no zero_grad memset per step)
         self.opt = FlatAdamW(self.flat, lr=lr, weight_decay=0.1, max_grad_norm=1.0,
@@ -115,6 +124,13 @@ class GPT2Trainer:
             self.opt.step_count += 1
             self.opt.set_device_hyper(lr, self.opt.step_count)
             g.replay()
+            # the replayed AdamW changed the weights through raw pointers: host-side caches
+            # keyed on the weights epoch (transposed copies outside the flat W^T views) go
+            # stale; the flat W^T views were rewritten by the replay itself
+            from ray_amd.ops import functional as rf
+
+            rf.bump_weights_epoch()
+            self.flat.mark_wt_fresh()
             self.step_idx += 1
             self.last_loss = self._graph_loss
             return self.last_loss

@@ -257,3 +257,77 @@ def test_dgrad_transposed_weight_copy(cuda_device, monkeypatch):
     dx()
     assert torch.equal(w._ra_wt[0], wt_before)  # refreshed from unchanged weights
     assert torch.equal(w._ra_wt[0], w.detach().t().contiguous())
+
+
+def test_adamw_wt_matches_plain_adamw_and_refreshes_transposes(cuda_device):
+    """ra_adamw_flat_wt (AdamW + the W^T copies of the linear weights in one pass) updates
+    p32/m/v/p16 exactly like the plain flat AdamW kernel and leaves every W^T view equal to
+    the transpose of its updated bf16 weight; ragged weight shapes included."""
+    from ray_amd.parallel.flat import FlatAdamW, FlatParams
+
+    def make():
+        torch.manual_seed(21)
+        m = torch.nn.Module()
+        m.a_w = torch.nn.Parameter(torch.randn(2304, 768, device=cuda_device))
+        m.b_w = torch.nn.Parameter(torch.randn(200, 132, device=cuda_device))  # ragged tiles
+        m.c_w = torch.nn.Parameter(torch.randn(768, 3072, device=cuda_device))
+        m.d = torch.nn.Parameter(torch.randn(1000, device=cuda_device))  # 1-D tail
+        return m.bfloat16()
+
+    mods = [make(), make()]
+    fps = [FlatParams(mods[0], transpose=lambda n, p: n.endswith("_w")), FlatParams(mods[1])]
+    assert fps[0].pt16 is not None and fps[1].pt16 is None
+    assert fps[0].names == fps[1].names  # same layout: the _w weights were first anyway
+    opts = [FlatAdamW(fp, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0, zero_grad=True)
+            for fp in fps]
+    for step in range(3):
+        torch.manual_seed(100 + step)
+        grad = torch.randn(fps[0].numel, device=cuda_device)
+        for fp, opt in zip(fps, opts):
+            fp.g.copy_(grad)
+            opt.step()
+        torch.cuda.synchronize()
+        # compare the parameters' own elements (the alignment padding between the tiled
+        # weights is not part of any tile)
+        for (name, prm), off in zip(fps[0].order, fps[0].offsets):
+            k = prm.numel()
+            # p16: the two kernels may contract the update differently (FMA), so a p32 value
+            # a few ulps apart can round to the neighbouring bf16 (1 bf16 ulp ~ 2^-8 relative)
+            for a, b, tol in ((fps[0].p32, fps[1].p32, 1e-6), (fps[0].p16, fps[1].p16, 4e-3),
+                              (opts[0].m, opts[1].m, 1e-6), (opts[0].v, opts[1].v, 1e-6)):
+                x, y = a[off:off + k].float(), b[off:off + k].float()
+                assert (x - y).abs().max().item() <= tol * y.abs().max().item() + 1e-12, name
+            assert float(fps[0].g[off:off + k].abs().max()) == 0.0  # zeroed in the same pass
+        for name in ("a_w", "b_w", "c_w"):
+            p = getattr(mods[0], name)
+            assert torch.equal(p._ra_wt_view, p.detach().t()), name
+            assert rf._transposed_weight(p)[0].data_ptr() == p._ra_wt_view.data_ptr()
+
+
+def test_gpt2_graph_replay_matches_eager_then_eager_after_replay(cuda_device):
+    """graphed steps reproduce the eager loss trajectory, and an eager step
+    after replays (transposed weights, epoch-keyed caches) continues it."""
+    from ray_amd.models.gpt2 import GPT2Config
+    from ray_amd.train.gpt2_step import GPT2Trainer
+
+    cfg = GPT2Config.tiny()
+    gen = torch.Generator(device=cuda_device).manual_seed(3)
+    ids = torch.randint(0, cfg.vocab_size, (6, 4, 129), device=cuda_device, generator=gen)
+    batches = [[(b[:, :-1].contiguous(), b[:, 1:].contiguous())] for b in ids]
+
+    def trainer():
+        return GPT2Trainer(cfg, 4, 128, cuda_device, lr=3e-3, warmup_steps=1, seed=7)
+
+    # eager: b0, b0 (the graph run's two warm-up steps), then b1 .. b5
+    ta = trainer()
+    eager = [float(ta.step(b)) for b in [batches[0], batches[0]] + batches[1:]]
+    # graphed: enable_graph runs the two eager warm-up steps on b0, replays b1 .. b4, then
+    # one eager step on b5 after the replays
+    tb = trainer()
+    assert tb.enable_graph(batches[0], warm=2)
+    graphed = [float(tb.step(b)) for b in batches[1:5]]
+    tb._graph = None
+    graphed.append(float(tb.step(batches[5])))
+    torch.cuda.synchronize()
+    for a, b in zip(eager[2:], graphed):
+        assert abs(a - b) <= 2e-3 * abs(a), (eager, graphed)
