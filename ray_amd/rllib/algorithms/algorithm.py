@@ -23,8 +23,30 @@ class PerModuleLearners:
     algorithm keeps one replay buffer per trainable module."""
 
     def __init__(self, make, specs, trainable=None):
-        self.learners = {mid: make(os_, as_) for mid, (os_, as_) in specs.items()}
+        self.make = make
+        self.learners = {mid: self._make(mid, os_, as_) for mid, (os_, as_) in specs.items()}
         self.trainable = set(trainable) if trainable else set(specs)
+
+    def _make(self, mid, os_, as_):
+        import inspect
+
+        try:
+            n = len(inspect.signature(self.make).parameters)
+        except (TypeError, ValueError):
+            n = 2
+        return self.make(os_, as_, mid) if n >= 3 else self.make(os_, as_)
+
+    def add(self, mid, spec, trainable=True):
+        """A new module's learner(s) mid-training (Algorithm.add_module)."""
+        self.learners[mid] = self._make(mid, spec[0], spec[1])
+        if trainable:
+            self.trainable.add(mid)
+
+    def remove(self, mid):
+        lr = self.learners.pop(mid, None)
+        self.trainable.discard(mid)
+        if lr is not None:
+            lr.shutdown()
 
     def sync_target(self):
         for mid in self.trainable:
@@ -541,6 +563,139 @@ class Algorithm:
 
     def get_config(self):
         return self.config
+
+    # ---------------------------------------------------------------- module set (multi-agent)
+    def add_module(self, module_id, module_spec=None, *, config_overrides=None,
+                   new_agent_to_module_mapping_fn=None, new_should_module_be_updated=None,
+                   add_to_learners=True, add_to_env_runners=True,
+                   add_to_eval_env_runners=True, weights=None):
+        """Add an RLModule to a running multi-agent algorithm (reference:
+        rllib/algorithms/algorithm.py:2054 add_module): a learner group for it (when it is
+        trained), a replay buffer for off-policy algorithms, the module on every EnvRunner
+        (inference), the new agent -> module mapping and the trainable set. ``module_spec``:
+        an RLModuleSpec (its observation/action spaces; missing ones default to an
+        existing module's), or an (observation_space, action_space) tuple. ``weights``:
+        initial weights (e.g. a frozen copy of the main policy for league / self-play);
+        otherwise the new module keeps its fresh initialisation. Returns the module ids."""
+        if not self.is_multi_agent:
+            raise ValueError("add_module needs a multi-agent config (config.multi_agent)")
+        if module_id in self.module_specs:
+            raise ValueError(f"module {module_id!r} already exists")
+        ref = next(iter(self.module_specs.values()))
+        if isinstance(module_spec, (tuple, list)):
+            os_, as_ = module_spec
+        else:
+            os_ = getattr(module_spec, "observation_space", None) or ref[0]
+            as_ = getattr(module_spec, "action_space", None) or ref[1]
+        spec = (os_, as_)
+        trainable = self._trainable_after(module_id, new_should_module_be_updated)
+        self.module_specs = dict(self.module_specs)
+        self.module_specs[module_id] = spec
+        self.cfg["_module_specs"] = self.module_specs
+        if add_to_learners:
+            lg = self.learner_group
+            if hasattr(lg, "add"):
+                lg.add(module_id, spec, trainable=module_id in trainable)
+            if hasattr(self, "buffers") and module_id in trainable:
+                self.buffers[module_id] = self._new_buffer()
+            self._set_trainable(trainable)
+            if weights is not None:
+                lg.groups[module_id].set_weights(weights) if hasattr(lg, "groups") else \
+                    lg.learners[module_id].set_weights(weights)
+        w = weights if weights is not None else self.get_weights().get(module_id)
+        if new_agent_to_module_mapping_fn is not None:
+            self.config.policy_mapping_fn = new_agent_to_module_mapping_fn
+            self.cfg["policy_mapping_fn"] = new_agent_to_module_mapping_fn
+        if add_to_env_runners:
+            self._on_runners(lambda r: r.add_module(module_id, spec, w))
+            if new_agent_to_module_mapping_fn is not None:
+                fn = new_agent_to_module_mapping_fn
+                self._on_runners(lambda r: r.set_mapping_fn(fn))
+        if add_to_eval_env_runners and self._eval_runners:
+            import cloudpickle
+
+            blob = cloudpickle.dumps(lambda r: r.add_module(module_id, spec, w))
+            ray.get([r.apply.remote(blob) for r in self._eval_runners])
+        self.weights_version += 1  # runners re-sync every module's weights
+        self._sync_weights(self.get_weights())
+        return list(self.module_specs)
+
+    def remove_module(self, module_id, *, new_agent_to_module_mapping_fn=None,
+                      new_should_module_be_updated=None, remove_from_learners=True,
+                      remove_from_env_runners=True, remove_from_eval_env_runners=True):
+        """Remove a module (reference: algorithm.py remove_module); the mapping must no
+        longer route agents to it."""
+        if not self.is_multi_agent or module_id not in self.module_specs:
+            raise ValueError(f"unknown module {module_id!r}")
+        trainable = self._trainable_after(None, new_should_module_be_updated) - {module_id}
+        self.module_specs = {k: v for k, v in self.module_specs.items() if k != module_id}
+        self.cfg["_module_specs"] = self.module_specs
+        if new_agent_to_module_mapping_fn is not None:
+            self.config.policy_mapping_fn = new_agent_to_module_mapping_fn
+            self.cfg["policy_mapping_fn"] = new_agent_to_module_mapping_fn
+            fn = new_agent_to_module_mapping_fn
+            self._on_runners(lambda r: r.set_mapping_fn(fn))
+        if remove_from_env_runners:
+            self._on_runners(lambda r: r.remove_module(module_id))
+        if remove_from_eval_env_runners and self._eval_runners:
+            import cloudpickle
+
+            blob = cloudpickle.dumps(lambda r: r.remove_module(module_id))
+            ray.get([r.apply.remote(blob) for r in self._eval_runners])
+        if remove_from_learners:
+            lg = self.learner_group
+            if hasattr(lg, "remove"):
+                lg.remove(module_id)
+            if hasattr(self, "buffers"):
+                self.buffers.pop(module_id, None)
+        self._set_trainable(trainable)
+        return list(self.module_specs)
+
+    def add_policy(self, policy_id, policy_cls=None, policy=None, *, observation_space=None,
+                   action_space=None, config=None, policy_state=None,
+                   policy_mapping_fn=None, policies_to_train=None, **kwargs):
+        """Old-stack spelling of ``add_module`` (reference: algorithm.py:1929)."""
+        ref = next(iter(self.module_specs.values())) if self.is_multi_agent else None
+        spaces = (observation_space or (ref[0] if ref else self.observation_space),
+                  action_space or (ref[1] if ref else self.action_space))
+        weights = policy_state.get("weights", policy_state) if isinstance(policy_state, dict) \
+            else None
+        self.add_module(policy_id, spaces, new_agent_to_module_mapping_fn=policy_mapping_fn,
+                        new_should_module_be_updated=policies_to_train, weights=weights)
+        return self.get_policy(policy_id)
+
+    def remove_policy(self, policy_id, *, policy_mapping_fn=None, policies_to_train=None,
+                      **kwargs):
+        self.remove_module(policy_id, new_agent_to_module_mapping_fn=policy_mapping_fn,
+                           new_should_module_be_updated=policies_to_train)
+
+    def _trainable_after(self, new_id, spec):
+        """The trainable module set after add/remove: ``spec`` is a list / set of ids or a
+        callable(module_id) -> bool; None keeps the current set (+ the new module)."""
+        lg = getattr(self, "learner_group", None)
+        cur = set(getattr(lg, "trainable", ()) or self.module_specs)
+        ids = set(self.module_specs) | ({new_id} if new_id is not None else set())
+        if spec is None:
+            return cur | ({new_id} if new_id is not None else set())
+        if callable(spec):
+            return {m for m in ids if spec(m)}
+        return set(spec)
+
+    def _set_trainable(self, trainable):
+        lg = getattr(self, "learner_group", None)
+        if lg is not None and hasattr(lg, "trainable"):
+            lg.trainable = set(trainable)
+        self.config.policies_to_train = sorted(trainable, key=str)
+
+    def _on_runners(self, fn):
+        """fn(runner) on the local runner and every remote EnvRunner (through apply)."""
+        import cloudpickle
+
+        if self._runners.num_actors():
+            blob = cloudpickle.dumps(fn)
+            self._foreach_runner(lambda r: r.apply.remote(blob))
+        if self.local_runner is not None:
+            fn(self.local_runner)
 
     @property
     def env_runner_group(self):

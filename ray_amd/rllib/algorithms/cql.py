@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from ray_amd.rllib.algorithms.sac import SAC, SACConfig, SACLearner
+from ray_amd.rllib.core.learner import LearnerGroup
 from ray_amd.rllib.offline import OfflineData
 
 
@@ -30,11 +31,20 @@ class CQLConfig(SACConfig):
 
 
 class CQLLearner(SACLearner):
-    def __init__(self, cfg, obs_space, act_space):
-        super().__init__(cfg, obs_space, act_space)
+    """CQL on the SAC learner pipeline (reference: cql/torch/cql_torch_learner.py)."""
+
+    def build_module(self):
         self.n_updates = 0
-        self.low = torch.as_tensor(np.asarray(act_space.low, np.float32)).to(self.device)
-        self.high = torch.as_tensor(np.asarray(act_space.high, np.float32)).to(self.device)
+        a = self.action_space
+        self.low = torch.as_tensor(np.asarray(a.low, np.float32)).to(self.device)
+        self.high = torch.as_tensor(np.asarray(a.high, np.float32)).to(self.device)
+        return super().build_module()
+
+    def _extra_state(self):
+        return {"n_updates": self.n_updates}
+
+    def _load_extra_state(self, s):
+        self.n_updates = s.get("n_updates", self.n_updates)
 
     def _q_rep(self, obs, act, N):
         o = obs.repeat_interleave(N, 0)
@@ -83,7 +93,8 @@ class CQL(SAC):
         if not self.config.input_:
             raise ValueError("CQL is offline: set config.offline_data(input_=<dir>)")
         self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
-        self.learner_group = CQLLearner(self.cfg, self.observation_space, self.action_space)
+        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space,
+                                          learner_class=self.learner_class)
         self.prioritized = False
         self._sync_weights(self.learner_group.get_weights())
 
@@ -93,7 +104,8 @@ class CQL(SAC):
         for _ in range(int(cfg.updates_per_iteration)):
             b = self.offline.sample(cfg.train_batch_size)
             b["terminateds"] = b["terminateds"].astype(np.float32)
-            stats, _ = self.learner_group.update(b)
+            stats = self.learner_group.update_from_batch(b)
+            stats = {k: v for k, v in stats.items() if not isinstance(v, np.ndarray)}
         self._sync_weights(self.learner_group.get_weights())
         if cfg.eval_steps_per_iteration:
             self.local_runner.sample(cfg.eval_steps_per_iteration, explore=False) \

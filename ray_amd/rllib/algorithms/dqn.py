@@ -8,6 +8,7 @@ import torch
 import ray_amd as ray
 from ray_amd.rllib.algorithms.algorithm import Algorithm, PerModuleLearners, add_agent_rows
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import QModule
 from ray_amd.rllib.utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
 
@@ -32,66 +33,69 @@ class DQNConfig(AlgorithmConfig):
         self.n_step = 1
 
 
-class _QLearner:
-    def __init__(self, cfg, obs_space, act_space):
-        self.cfg = cfg
-        dev = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
-            "num_gpus_per_learner", 1) else torch.device("cpu")
-        self.device = dev
-        mc = dict(cfg.get("model") or {})
-        mc["dueling"] = cfg.get("dueling", True)
-        self.q = QModule(obs_space, act_space, mc).to(dev)
-        self.target = QModule(obs_space, act_space, mc).to(dev)
-        self.target.load_state_dict(self.q.state_dict())
-        self.opt = torch.optim.Adam(self.q.parameters(), lr=cfg.get("lr", 5e-4))
+class DQNLearner(TorchLearner):
+    """DQN on the learner pipeline (reference: rllib/algorithms/dqn/torch/
+    dqn_torch_learner.py): forward_train evaluates Q(s, a) and the (double-)Q target from
+    the target network, the loss is the importance-weighted Huber TD error, the target
+    network is synced by ``sync_target``; per-row |TD| comes back as ``td_error`` for the
+    prioritized replay buffer. ``num_learners=N``: N learners on 1/N of each batch."""
 
-    def update(self, b):
-        dev = self.device
-        obs = torch.as_tensor(b["obs"]).to(dev)
-        nobs = torch.as_tensor(b["next_obs"]).to(dev)
-        a = torch.as_tensor(b["actions"]).long().to(dev)
-        r = torch.as_tensor(b["rewards"]).float().to(dev)
-        d = torch.as_tensor(b["terminateds"]).float().to(dev)
-        w = torch.as_tensor(b.get("weights", np.ones(len(r), np.float32))).to(dev)
-        q = self.q(obs).gather(-1, a[:, None])[:, 0]
+    def build_module(self):
+        mc = dict(self.config.get("model") or {})
+        mc["dueling"] = self.config.get("dueling", True)
+        m = torch.nn.ModuleDict({"q": QModule(self.observation_space, self.action_space, mc),
+                                 "target": QModule(self.observation_space, self.action_space,
+                                                   mc)})
+        m["target"].load_state_dict(m["q"].state_dict())
+        m["target"].requires_grad_(False)
+        return m
+
+    def configure_optimizers_for_module(self, module_id, config):
+        params = list(self.module["q"].parameters())
+        self.register_optimizer(module_id=module_id, optimizer=torch.optim.Adam(
+            params, lr=config.get("lr", 5e-4)), params=params)
+
+    def forward_train(self, b):
+        q = self.module["q"]
+        qa = q(b["obs"]).gather(-1, b["actions"].long()[:, None])[:, 0]
         with torch.no_grad():
-            if self.cfg.get("double_q", True):
-                na = self.q(nobs).argmax(-1)
-                nq = self.target(nobs).gather(-1, na[:, None])[:, 0]
+            nobs = b["next_obs"]
+            if self.config.get("double_q", True):
+                na = q(nobs).argmax(-1)
+                nq = self.module["target"](nobs).gather(-1, na[:, None])[:, 0]
             else:
-                nq = self.target(nobs).max(-1).values
-            disc = torch.as_tensor(b["discounts"]).float().to(dev) if "discounts" in b else \
-                self.cfg.get("gamma", 0.99)  # n-step rows carry gamma ** k
-            tgt = r + disc * (1 - d) * nq
-        td = q - tgt
-        loss = (w * torch.nn.functional.huber_loss(q, tgt, reduction="none")).mean()
-        self.opt.zero_grad()
-        loss.backward()
-        if self.cfg.get("grad_clip"):
-            torch.nn.utils.clip_grad_norm_(self.q.parameters(), self.cfg["grad_clip"])
-        self.opt.step()
-        return float(loss.detach()), td.detach().abs().cpu().numpy()
+                nq = self.module["target"](nobs).max(-1).values
+            disc = b["discounts"].float() if "discounts" in b else \
+                self.config.get("gamma", 0.99)  # n-step rows carry gamma ** k
+            tgt = b["rewards"].float() + disc * (1 - b["terminateds"].float()) * nq
+        return {"q": qa, "target": tgt}
+
+    def compute_loss_for_module(self, *, module_id, config, batch, fwd_out):
+        q, tgt = fwd_out["q"], fwd_out["target"]
+        w = batch.get("weights")
+        self._td = (q - tgt).detach()
+        hub = torch.nn.functional.huber_loss(q, tgt, reduction="none")
+        return (hub * w.float()).mean() if w is not None else hub.mean()
+
+    def _update(self, batch, timesteps=None):
+        out = super()._update(batch, timesteps=timesteps)
+        out["loss"] = out["total_loss"]
+        out["td_error"] = self._td.abs().float().cpu().numpy()
+        return out
 
     def sync_target(self):
-        self.target.load_state_dict(self.q.state_dict())
+        self.module["target"].load_state_dict(self.module["q"].state_dict())
 
+    # the EnvRunners run the online Q network: its state dict is "the weights"
     def get_weights(self):
-        return {k: v.detach().cpu() for k, v in self.q.state_dict().items()}
+        return {k: v.detach().cpu() for k, v in self.module["q"].state_dict().items()}
 
     def set_weights(self, w):
-        self.q.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+        self.module["q"].load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
         self.sync_target()
 
-    def get_state(self):
-        return {"q": self.get_weights(), "opt": self.opt.state_dict()}
 
-    def set_state(self, s):
-        self.q.load_state_dict(s["q"])
-        self.target.load_state_dict(s["q"])
-        self.opt.load_state_dict(s["opt"])
-
-    def shutdown(self):
-        pass
+_QLearner = DQNLearner  # earlier name
 
 
 class DQN(Algorithm):
@@ -131,12 +135,14 @@ class DQN(Algorithm):
             not self.episodic
         if self.is_multi_agent:
             self.learner_group = PerModuleLearners(
-                lambda os_, as_: _QLearner(self.cfg, os_, as_), self.module_specs,
-                self.config.policies_to_train)
+                lambda os_, as_, mid: LearnerGroup(self.cfg, os_, as_, module_id=mid,
+                                                   learner_class=DQNLearner),
+                self.module_specs, self.config.policies_to_train)
             self.buffers = {mid: self._new_buffer() for mid in self.learner_group.trainable}
         else:
             self.buffer = self._new_buffer()
-            self.learner_group = _QLearner(self.cfg, self.observation_space, self.action_space)
+            self.learner_group = LearnerGroup(self.cfg, self.observation_space,
+                                              self.action_space, learner_class=DQNLearner)
         self._last_target = 0
         self._sync_weights(self.learner_group.get_weights())
 
@@ -153,10 +159,11 @@ class DQN(Algorithm):
                 kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} \
                     if self.prioritized else {}
                 mb = buf.sample(cfg.train_batch_size, **kw)
-                loss, td = self.learner_group.learners[mid].update(mb)
+                res = self.learner_group.learners[mid].update_from_batch(
+                    mb, timesteps=self.total_env_steps)
                 if self.prioritized:
-                    buf.update_priorities(mb["batch_indexes"], td)
-                stats[f"{mid}/loss"] = loss
+                    buf.update_priorities(mb["batch_indexes"], res["td_error"])
+                stats[f"{mid}/loss"] = res["loss"]
 
     def _epsilon(self):
         sched = self.config.epsilon
@@ -204,10 +211,10 @@ class DQN(Algorithm):
             if self.episodic:
                 kw = {"n_step": int(getattr(cfg, "n_step", 1) or 1), "gamma": cfg.gamma}
             mb = self.buffer.sample(cfg.train_batch_size, **kw)
-            loss, td = self.learner_group.update(mb)
+            res = self.learner_group.update_from_batch(mb, timesteps=self.total_env_steps)
             if self.prioritized:
-                self.buffer.update_priorities(mb["batch_indexes"], td)
-            stats["loss"] = loss
+                self.buffer.update_priorities(mb["batch_indexes"], res["td_error"])
+            stats["loss"] = res["loss"]
         if self.total_env_steps - self._last_target >= cfg.target_network_update_freq:
             self.learner_group.sync_target()
             self._last_target = self.total_env_steps

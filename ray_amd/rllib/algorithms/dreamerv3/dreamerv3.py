@@ -27,10 +27,13 @@ from __future__ import annotations
 
 import math
 import time
+from types import SimpleNamespace
 
 import numpy as np
+import torch
 
 from ray_amd.rllib.algorithms.algorithm import Algorithm
+from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.env.envs import make_env
 
@@ -251,6 +254,10 @@ class DreamerV3EnvRunner:
         seed = cfg.get("seed")
         self.obs = [e.reset(seed=None if seed is None else seed + i)[0]
                     for i, e in enumerate(self.envs)]
+        if seed is not None and hasattr(self.act_space, "seed"):
+            # the random warm-up actions come from the action space: seeded, so a seeded
+            # run replays bit for bit
+            self.act_space.seed(seed + 1000 * worker_index)
         self.first = [True] * n
         self.ep_ret = [0.0] * n
         self.ep_len = [0] * n
@@ -388,58 +395,120 @@ class _StreamReplay:
         return b
 
 
-# ============================================================================ algorithm
-class DreamerV3(Algorithm):
-    kind = "dreamerv3"
-    env_runner_cls = DreamerV3EnvRunner
+# ============================================================================ learner
+class _Cfg(SimpleNamespace):
+    """Attribute view of the algorithm's config dict (the learner runs in learner actors,
+    where only the dict travels)."""
 
-    @classmethod
-    def get_default_config(cls):
-        return DreamerV3Config()
 
-    def setup(self):
-        import torch
+class DreamerV3Learner(TorchLearner):
+    """DreamerV3 on the learner pipeline (reference: rllib/algorithms/dreamerv3/
+    dreamerv3_learner.py, torch/dreamerv3_torch_learner.py): world model (RSSM encoder /
+    GRU / posterior / prior / decoder / reward / continue heads), actor and critic with
+    their own optimizers. One update: the world-model loss through compute_gradients ->
+    postprocess_gradients (clip by ``world_model_grad_clip_by_global_norm``) ->
+    apply_gradients; then dreamed trajectories from the posterior states give the critic
+    and actor losses, each back-propagated into its own network (per-optimizer losses)
+    and clipped by its own norm; the slow critic follows by EMA. With ``num_learners=N``
+    every learner trains on B/N of each [B, T] batch, gradients averaged, and the return
+    scale statistic is averaged over the group."""
 
-        cfg = self.config
-        use_gpu = cfg.num_gpus_per_learner and torch.cuda.is_available()
-        self.device = torch.device("cuda" if use_gpu else "cpu")
-        if cfg.seed is not None:
-            torch.manual_seed(cfg.seed)
+    def build_module(self):
+        c = self.c = _Cfg(**self.config)
+        if c.seed is not None:
+            torch.manual_seed(c.seed)
         obs_shape = tuple(self.observation_space.shape)
         self.discrete = hasattr(self.action_space, "n")
         self.act_dim = int(self.action_space.n) if self.discrete else \
             int(np.prod(self.action_space.shape))
-        self.world, self.actor, self.critic, dims = _build_nets(
-            obs_shape, self.act_dim, self.discrete, cfg.model_size, self.device)
+        world, actor, critic, dims = _build_nets(obs_shape, self.act_dim, self.discrete,
+                                                 c.model_size, self.device)
         self.gru_units, self.zdim, self.cats, self.classes = dims
         import copy
 
-        self.slow_critic = copy.deepcopy(self.critic).requires_grad_(False)
-        self.opt_wm = torch.optim.Adam(self.world.parameters(), lr=cfg.world_model_lr, eps=1e-8)
-        self.opt_actor = torch.optim.Adam(self.actor.parameters(), lr=cfg.actor_lr, eps=1e-5)
-        self.opt_critic = torch.optim.Adam(self.critic.parameters(), lr=cfg.critic_lr, eps=1e-5)
+        m = torch.nn.Module()
+        m.world, m.actor, m.critic = world, actor, critic
+        m.slow_critic = copy.deepcopy(critic).requires_grad_(False)
         self.twohot = _TwoHot(self.device)
         self.image = len(obs_shape) == 3
-        self.symlog_obs = (not self.image) if cfg.symlog_obs == "auto" else bool(cfg.symlog_obs)
+        self.symlog_obs = (not self.image) if c.symlog_obs == "auto" else bool(c.symlog_obs)
         self.ret_scale = None  # EMA of the 5-95 percentile range of lambda-returns
-        self.replay = _StreamReplay(int(cfg.replay_buffer_config.get("capacity", 1e6)),
-                                    cfg.seed)
-        self.local_runner.bind(self)
-        self.replayed_steps = 0
-        self.env_steps = 0
-        self.learner_group = _NoLearnerGroup()
+        return m
 
-    # --- helpers --------------------------------------------------------------------
+    def configure_optimizers_for_module(self, module_id, config):
+        c = self.c
+        m = self.module
+        for name, net, lr, eps in (("world_model", m.world, c.world_model_lr, 1e-8),
+                                   ("actor", m.actor, c.actor_lr, 1e-5),
+                                   ("critic", m.critic, c.critic_lr, 1e-5)):
+            self.register_optimizer(module_id=module_id, optimizer_name=name,
+                                    optimizer=torch.optim.Adam(net.parameters(), lr=lr, eps=eps),
+                                    params=list(net.parameters()))
+
+    @property
+    def actor(self):
+        return self.module.actor
+
+    @property
+    def critic(self):
+        return self.module.critic
+
+    @property
+    def slow_critic(self):
+        return self.module.slow_critic
+
+    def postprocess_gradients(self, gradients_dict):
+        """Clip each network's gradients by its own global norm."""
+        c = self.c
+        clip = {"world_model": c.world_model_grad_clip_by_global_norm,
+                "actor": c.actor_grad_clip_by_global_norm,
+                "critic": c.critic_grad_clip_by_global_norm}
+        names = self._named_params()
+        inv = {id(p): n for n, p in names.items()}
+        for (_, oname), (_, ps) in self._optimizers.items():
+            gs = [gradients_dict[inv[id(p)]] for p in ps if inv.get(id(p)) in gradients_dict]
+            if gs and clip.get(oname):
+                torch.nn.utils.clip_grad_norm_(gs, clip[oname])
+        return gradients_dict
+
+    def _update(self, b, timesteps=None):
+        loss, post, stats = self._observe(b)
+        self.apply_gradients(self.postprocess_gradients(
+            self.compute_gradients({"world_model": loss})))
+        stats["WORLD_MODEL_L_total"] = loss.item()
+        losses, st2 = self._actor_critic_losses(post)
+        if losses:
+            self.apply_gradients(self.postprocess_gradients(self.compute_gradients(losses)))
+        for k in ("critic", "actor"):
+            if k in losses:
+                stats[{"critic": "CRITIC_L_total", "actor": "ACTOR_L_total"}[k]] = \
+                    losses[k].item()
+        stats.update(st2)
+        self.updates += 1
+        self.after_gradient_based_update(timesteps=timesteps)
+        return stats
+
+    def after_gradient_based_update(self, *, timesteps=None):
+        if self.c.train_critic:
+            with torch.no_grad():  # slow critic EMA
+                for ps, p in zip(self.slow_critic.parameters(), self.critic.parameters()):
+                    ps.mul_(0.98).add_(p.detach(), alpha=0.02)
+
+    def _convert_batch(self, batch):
+        return batch  # _observe moves the [B, T] fields itself
+
+    def _extra_state(self):
+        return {"ret_scale": self.ret_scale}
+
+    def _load_extra_state(self, s):
+        self.ret_scale = s.get("ret_scale", self.ret_scale)
+
+    # --- world model ----------------------------------------------------------------
     def _prep_obs(self, x):
         if self.image:
             return x
         x = x.float().flatten(1)
         return symlog(x) if self.symlog_obs else x
-
-    def _action_vec(self, acts):
-        if self.discrete:
-            return np.eye(self.act_dim, dtype=np.float32)[acts.astype(np.int64)]
-        return np.asarray(acts, np.float32).reshape(len(acts), -1)
 
     def _policy(self, s, explore):
         torch = _torch()
@@ -473,21 +542,21 @@ class DreamerV3(Algorithm):
         obs = torch.as_tensor(b["obs"], device=dev)
         B, T = obs.shape[:2]
         x = self._prep_obs(obs.reshape(B * T, *obs.shape[2:]))
-        emb = self.world.encoder(x).view(B, T, -1)
+        emb = self.module.world.encoder(x).view(B, T, -1)
         pa = torch.as_tensor(b["prev_action"], device=dev)
         first = torch.as_tensor(b["is_first"], device=dev).unsqueeze(-1)
-        h, z = self.world.initial(B)
+        h, z = self.module.world.initial(B)
         hs, zs, post_p, prior_p = [], [], [], []
-        h0, z0 = self.world.initial(B)
+        h0, z0 = self.module.world.initial(B)
         for t in range(T):
             f = first[:, t]
             h = f * h0 + (1 - f) * h
             z = f * z0 + (1 - f) * z
             a = (1 - f) * pa[:, t]
-            h = self.world.gru(self.world.pre_gru(torch.cat([z, a], -1)), h)
-            prior_logits = self.world.prior(h)
-            post_logits = self.world.post(torch.cat([h, emb[:, t]], -1))
-            z, pp = self.world.dist_sample(post_logits)
+            h = self.module.world.gru(self.module.world.pre_gru(torch.cat([z, a], -1)), h)
+            prior_logits = self.module.world.prior(h)
+            post_logits = self.module.world.post(torch.cat([h, emb[:, t]], -1))
+            z, pp = self.module.world.dist_sample(post_logits)
             lp = prior_logits.view(B, self.cats, self.classes)
             prior_p.append(0.99 * lp.softmax(-1) + 0.01 / self.classes)
             post_p.append(pp)
@@ -498,16 +567,16 @@ class DreamerV3(Algorithm):
         post_p = torch.stack(post_p, 1)
         prior_p = torch.stack(prior_p, 1)
         s = torch.cat([H_, Z_], -1)
-        recon = self.world.decoder(s.reshape(B * T, -1))
+        recon = self.module.world.decoder(s.reshape(B * T, -1))
         target = x.float().flatten(1)
         if self.image:
             target = target / 255.0 - 0.5
         l_dec = ((recon - target) ** 2).sum(-1).view(B, T)
         rew = torch.as_tensor(b["reward"], device=dev)
-        l_rew = self.twohot.loss(self.world.reward(s), rew)
+        l_rew = self.twohot.loss(self.module.world.reward(s), rew)
         cont = 1.0 - torch.as_tensor(b["is_terminal"], device=dev)
         l_cont = torch.nn.functional.binary_cross_entropy_with_logits(
-            self.world.cont(s).squeeze(-1), cont, reduction="none")
+            self.module.world.cont(s).squeeze(-1), cont, reduction="none")
         kl_dyn = _kl(post_p.detach(), prior_p).clamp_min(1.0)
         kl_rep = _kl(post_p, prior_p.detach()).clamp_min(1.0)
         loss = (l_dec + l_rew + l_cont + 0.5 * kl_dyn + 0.1 * kl_rep).mean()
@@ -521,7 +590,7 @@ class DreamerV3(Algorithm):
     # --- imagination ----------------------------------------------------------------
     def _imagine(self, start):
         torch = _torch()
-        H = self.config.horizon_H
+        H = self.c.horizon_H
         h, z = start[:, :self.gru_units], start[:, self.gru_units:]
         states, acts = [start], []
         for _ in range(H):
@@ -531,17 +600,18 @@ class DreamerV3(Algorithm):
             if not self.discrete:
                 a = torch.tanh(a)
             acts.append(a)
-            h, z, _ = self.world.img_step(h, z, a)
+            h, z, _ = self.module.world.img_step(h, z, a)
             states.append(torch.cat([h, z], -1))
         return torch.stack(states, 0), torch.stack(acts, 0)  # [H+1, N, S], [H, N, A]
 
-    def _train_actor_critic(self, post_states):
+    def _actor_critic_losses(self, post_states):
+        """Dreamed trajectories from the posterior states -> critic / actor losses."""
         torch = _torch()
-        cfg = self.config
+        cfg = self.c
         with torch.no_grad():
             states, acts = self._imagine(post_states.reshape(-1, post_states.shape[-1]))
-            rew = self.twohot.mean(self.world.reward(states))  # [H+1, N]
-            cont = torch.sigmoid(self.world.cont(states).squeeze(-1))
+            rew = self.twohot.mean(self.module.world.reward(states))  # [H+1, N]
+            cont = torch.sigmoid(self.module.world.cont(states).squeeze(-1))
             disc = cfg.gamma * cont
             v_slow = self.twohot.mean(self.slow_critic(states))
         # lambda-returns from the critic (bootstrap at the horizon)
@@ -556,25 +626,16 @@ class DreamerV3(Algorithm):
             w = torch.cumprod(torch.cat([torch.ones_like(disc[:1]), disc[1:-1]], 0), 0)
             lo, hi = torch.quantile(ret.flatten().float(), torch.tensor([0.05, 0.95],
                                                                         device=ret.device))
-            rng = (hi - lo).item()
+            rng = self._allreduce_mean((hi - lo).item())  # the same scale on every learner
             d = cfg.return_normalization_decay
             self.ret_scale = rng if self.ret_scale is None else d * self.ret_scale + \
                 (1 - d) * rng
             scale = max(1.0, self.ret_scale)
-        stats = {}
+        stats, losses = {}, {}
         if cfg.train_critic:
             logits = self.critic(states[:-1].detach())
             l_c = self.twohot.loss(logits, ret) + self.twohot.loss(logits, v_slow[:-1])
-            l_c = (l_c * w).mean()
-            self.opt_critic.zero_grad(set_to_none=True)
-            l_c.backward()
-            torch.nn.utils.clip_grad_norm_(self.critic.parameters(),
-                                           cfg.critic_grad_clip_by_global_norm)
-            self.opt_critic.step()
-            with torch.no_grad():  # slow critic EMA
-                for ps, p in zip(self.slow_critic.parameters(), self.critic.parameters()):
-                    ps.mul_(0.98).add_(p.detach(), alpha=0.02)
-            stats["CRITIC_L_total"] = l_c.item()
+            losses["critic"] = (l_c * w).mean()
         if cfg.train_actor:
             dist = self._actor_dist(states[:-1].detach())
             a = acts if self.discrete else torch.atanh(acts.clamp(-0.999, 0.999))
@@ -582,29 +643,93 @@ class DreamerV3(Algorithm):
             adv = ((ret - vv[:-1]) / scale).detach()
             ent = dist.entropy()
             l_a = (-(logp * adv) - cfg.entropy_scale * ent) * w
-            l_a = l_a.mean()
-            self.opt_actor.zero_grad(set_to_none=True)
-            l_a.backward()
-            torch.nn.utils.clip_grad_norm_(self.actor.parameters(),
-                                           cfg.actor_grad_clip_by_global_norm)
-            self.opt_actor.step()
-            stats.update({"ACTOR_L_total": l_a.item(), "ACTOR_entropy": ent.mean().item()})
+            losses["actor"] = l_a.mean()
+            stats["ACTOR_entropy"] = ent.mean().item()
         stats["DREAM_return_scale"] = scale
         stats["DREAM_rewards_mean"] = rew.mean().item()
-        return stats
+        return losses, stats
 
-    def _update(self, b):
-        torch = _torch()
+
+
+# ============================================================================ algorithm
+class DreamerV3(Algorithm):
+    kind = "dreamerv3"
+    env_runner_cls = DreamerV3EnvRunner
+
+    @classmethod
+    def get_default_config(cls):
+        return DreamerV3Config()
+
+    def setup(self):
         cfg = self.config
-        loss, post, stats = self._observe(b)
-        self.opt_wm.zero_grad(set_to_none=True)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.world.parameters(),
-                                       cfg.world_model_grad_clip_by_global_norm)
-        self.opt_wm.step()
-        stats["WORLD_MODEL_L_total"] = loss.item()
-        stats.update(self._train_actor_critic(post))
-        return stats
+        if cfg.seed is not None:
+            torch.manual_seed(cfg.seed)
+        self.cfg["num_gpus_per_learner"] = 1 if (cfg.num_gpus_per_learner and
+                                                 torch.cuda.is_available()) else 0
+        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space,
+                                          learner_class=DreamerV3Learner)
+        # the networks the EnvRunner acts with: the learner's own when it is local, else an
+        # inference copy refreshed from the learners after every training step
+        self._infer = self.learner_group.local if self.learner_group.is_local else \
+            DreamerV3Learner(self.cfg, self.observation_space, self.action_space)
+        self.device = self._infer.device
+        self.discrete, self.act_dim = self._infer.discrete, self._infer.act_dim
+        self.gru_units, self.zdim = self._infer.gru_units, self._infer.zdim
+        self.cats, self.classes = self._infer.cats, self._infer.classes
+        self.image = self._infer.image
+        self.replay = _StreamReplay(int(cfg.replay_buffer_config.get("capacity", 1e6)),
+                                    cfg.seed)
+        self.local_runner.bind(self)
+        self.replayed_steps = 0
+        self.env_steps = 0
+        self._sync_infer()
+
+    # networks / helpers of the acting copy
+    @property
+    def world(self):
+        return self._infer.module.world
+
+    @property
+    def actor(self):
+        return self._infer.actor
+
+    @property
+    def critic(self):
+        return self._infer.critic
+
+    @property
+    def slow_critic(self):
+        return self._infer.slow_critic
+
+    @property
+    def ret_scale(self):
+        return self.learner_group.foreach_learner(lambda lr: lr.ret_scale)[0]
+
+    def _prep_obs(self, x):
+        return self._infer._prep_obs(x)
+
+    def _action_vec(self, acts):
+        if self.discrete:
+            return np.eye(self.act_dim, dtype=np.float32)[acts.astype(np.int64)]
+        return np.asarray(acts, np.float32).reshape(len(acts), -1)
+
+    def _policy(self, s, explore):
+        return self._infer._policy(s, explore)
+
+    def _sync_infer(self):
+        if not self.learner_group.is_local:
+            self._infer.module.load_state_dict(
+                {k: torch.as_tensor(v) for k, v in self.learner_group.foreach_learner(
+                    lambda lr: {k: v.detach().cpu() for k, v in
+                                lr.module.state_dict().items()})[0].items()})
+
+    def _update(self, b, sync=True):
+        """One learner-group update on a [B, T] replay batch (then the acting copy follows
+        unless ``sync=False``: the training loop syncs once per iteration)."""
+        res = self.learner_group.update_from_batch(b)
+        if sync:
+            self._sync_infer()
+        return res
 
     # --- training loop --------------------------------------------------------------
     def training_step(self) -> dict:
@@ -629,9 +754,10 @@ class DreamerV3(Algorithm):
         t1 = time.perf_counter()
         stats, n_up = {}, 0
         while self.replayed_steps < cfg.training_ratio * self.env_steps:
-            stats = self._update(self.replay.sample(B, T))
+            stats = self._update(self.replay.sample(B, T), sync=False)
             self.replayed_steps += B * T
             n_up += 1
+        self._sync_infer()
         stats.update({"sample_time_s": t1 - t0, "learn_time_s": time.perf_counter() - t1,
                       "num_updates": n_up, "replay_timesteps": self.replay.num_timesteps(),
                       "replayed_steps": self.replayed_steps})
@@ -661,23 +787,14 @@ class DreamerV3(Algorithm):
                 "critic": self.critic.state_dict()}
 
     def get_state(self):
-        return {"world": self.world.state_dict(), "actor": self.actor.state_dict(),
-                "critic": self.critic.state_dict(), "slow_critic": self.slow_critic.state_dict(),
-                "opt_wm": self.opt_wm.state_dict(), "opt_actor": self.opt_actor.state_dict(),
-                "opt_critic": self.opt_critic.state_dict(), "ret_scale": self.ret_scale,
+        return {"learner": self.learner_group.get_state(),
                 "iteration": self.iteration, "total_env_steps": self.total_env_steps,
                 "env_steps": self.env_steps, "replayed_steps": self.replayed_steps,
                 "config": self.cfg}
 
     def set_state(self, s):
-        self.world.load_state_dict(s["world"])
-        self.actor.load_state_dict(s["actor"])
-        self.critic.load_state_dict(s["critic"])
-        self.slow_critic.load_state_dict(s["slow_critic"])
-        self.opt_wm.load_state_dict(s["opt_wm"])
-        self.opt_actor.load_state_dict(s["opt_actor"])
-        self.opt_critic.load_state_dict(s["opt_critic"])
-        self.ret_scale = s["ret_scale"]
+        self.learner_group.set_state(s["learner"])
+        self._sync_infer()
         self.iteration = s["iteration"]
         self.total_env_steps = s["total_env_steps"]
         self.env_steps = s["env_steps"]
@@ -685,11 +802,7 @@ class DreamerV3(Algorithm):
 
     def stop(self):
         self.local_runner.stop()
-
-
-class _NoLearnerGroup:
-    def shutdown(self):
-        pass
+        self.learner_group.shutdown()
 
 
 DreamerV3Config.algo_class = DreamerV3

@@ -16,6 +16,7 @@ import torch
 
 from ray_amd.rllib.algorithms.algorithm import Algorithm
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import RLModule
 from ray_amd.rllib.offline import OfflineData
 
@@ -43,14 +44,20 @@ class BCConfig(MARWILConfig):
         self.vf_coeff = 0.0
 
 
-class MARWILLearner:
-    def __init__(self, cfg, obs_space, act_space):
-        self.cfg = cfg
-        self.device = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
-            "num_gpus_per_learner", 1) else torch.device("cpu")
-        self.module = RLModule(obs_space, act_space, cfg.get("model")).to(self.device)
-        self.opt = torch.optim.Adam(self.module.parameters(), lr=cfg.get("lr", 1e-4))
-        self.ma_sqd = float(cfg.get("moving_average_sqd_adv_norm_start", 100.0))
+class MARWILLearner(TorchLearner):
+    """MARWIL / BC on the learner pipeline (reference: marwil/torch/
+    marwil_torch_learner.py). The running mean of squared advantages is a learner-side
+    statistic: with several learners it is updated from the group-wide batch mean, so
+    every rank keeps the same value (and the same weights)."""
+
+    def build_module(self):
+        self.ma_sqd = float(self.config.get("moving_average_sqd_adv_norm_start", 100.0))
+        return RLModule(self.observation_space, self.action_space, self.config.get("model"))
+
+    def configure_optimizers_for_module(self, module_id, config):
+        params = list(self.module.parameters())
+        self.register_optimizer(module_id=module_id, optimizer=torch.optim.Adam(
+            params, lr=config.get("lr", 1e-4)), params=params)
 
     def _logp(self, di, actions):
         m = self.module
@@ -61,53 +68,32 @@ class MARWILLearner:
         mean, log_std = di.float().chunk(2, -1)
         return gaussian_logp(actions.float(), mean, log_std)
 
-    def update(self, b):
-        dev = self.device
-        obs = torch.as_tensor(b["obs"]).to(dev)
-        act = torch.as_tensor(b["actions"]).to(dev)
-        ret = torch.as_tensor(b["returns"]).float().to(dev)
-        out = self.module.forward_train(obs)
-        logp = self._logp(out["action_dist_inputs"], act)
-        beta = float(self.cfg.get("beta", 1.0))
-        stats = {}
-        if beta != 0.0:
-            v = out["vf_preds"].float()
-            adv = ret - v
-            with torch.no_grad():
-                rate = float(self.cfg.get("moving_average_sqd_adv_norm_update_rate", 1e-8))
-                self.ma_sqd += rate * (float((adv.detach() ** 2).mean()) - self.ma_sqd)
-                w = torch.exp(beta * adv.detach() / (1e-8 + self.ma_sqd ** 0.5)).clamp(max=20.0)
-            pi_loss = -(w * logp).mean()
-            vf_loss = 0.5 * (adv ** 2).mean()
-            loss = pi_loss + float(self.cfg.get("vf_coeff", 1.0)) * vf_loss
-            stats["vf_loss"] = float(vf_loss.detach())
-        else:
-            pi_loss = -logp.mean()
-            loss = pi_loss
-        self.opt.zero_grad(set_to_none=True)
-        loss.backward()
-        if self.cfg.get("grad_clip"):
-            torch.nn.utils.clip_grad_norm_(self.module.parameters(), self.cfg["grad_clip"])
-        self.opt.step()
-        stats.update(policy_loss=float(pi_loss.detach()), total_loss=float(loss.detach()))
-        return stats
+    def compute_loss_for_module(self, *, module_id, config, batch, fwd_out):
+        logp = self._logp(fwd_out["action_dist_inputs"], batch["actions"])
+        beta = float(config.get("beta", 1.0))
+        self.metrics = {}
+        if beta == 0.0:  # BC: plain negative log-likelihood
+            loss = -logp.mean()
+            self.metrics["policy_loss"] = float(loss.detach())
+            return loss
+        v = fwd_out["vf_preds"].float()
+        adv = batch["returns"].float() - v
+        with torch.no_grad():
+            rate = float(config.get("moving_average_sqd_adv_norm_update_rate", 1e-8))
+            sq = self._allreduce_mean(float((adv.detach() ** 2).mean()))
+            self.ma_sqd += rate * (sq - self.ma_sqd)
+            w = torch.exp(beta * adv.detach() / (1e-8 + self.ma_sqd ** 0.5)).clamp(max=20.0)
+        pi_loss = -(w * logp).mean()
+        vf_loss = 0.5 * (adv ** 2).mean()
+        self.metrics.update(policy_loss=float(pi_loss.detach()),
+                            vf_loss=float(vf_loss.detach()))
+        return pi_loss + float(config.get("vf_coeff", 1.0)) * vf_loss
 
-    def get_weights(self):
-        return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
+    def _extra_state(self):
+        return {"ma": self.ma_sqd}
 
-    def set_weights(self, w):
-        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
-
-    def get_state(self):
-        return {"module": self.get_weights(), "opt": self.opt.state_dict(), "ma": self.ma_sqd}
-
-    def set_state(self, s):
-        self.module.load_state_dict(s["module"])
-        self.opt.load_state_dict(s["opt"])
-        self.ma_sqd = s["ma"]
-
-    def shutdown(self):
-        pass
+    def _load_extra_state(self, s):
+        self.ma_sqd = s.get("ma", self.ma_sqd)
 
 
 class MARWIL(Algorithm):
@@ -120,14 +106,16 @@ class MARWIL(Algorithm):
             raise ValueError(f"{type(self).__name__} is offline: set "
                              "config.offline_data(input_=<recorded experience dir>)")
         self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
-        self.learner_group = MARWILLearner(self.cfg, self.observation_space, self.action_space)
+        self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space,
+                                          learner_class=MARWILLearner)
         self._sync_weights(self.learner_group.get_weights())
 
     def training_step(self):
         cfg = self.config
         stats = {}
         for _ in range(int(cfg.updates_per_iteration)):
-            stats = self.learner_group.update(self.offline.sample(cfg.train_batch_size))
+            stats = self.learner_group.update_from_batch(
+                self.offline.sample(cfg.train_batch_size))
         self._sync_weights(self.learner_group.get_weights())
         if cfg.eval_steps_per_iteration:  # online metrics with the current policy
             runner = self.env_runners[0] if self.env_runners else self.local_runner

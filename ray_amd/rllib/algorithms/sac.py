@@ -16,6 +16,7 @@ import torch
 import ray_amd as ray
 from ray_amd.rllib.algorithms.algorithm import Algorithm, PerModuleLearners, add_agent_rows
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy, TwinQ
 from ray_amd.rllib.utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
 
@@ -46,37 +47,78 @@ class SACConfig(AlgorithmConfig):
         self.q_model_config = None
 
 
-def _to(b, dev):
-    return {k: torch.as_tensor(np.asarray(v)).to(dev) for k, v in b.items()
-            if k in ("obs", "next_obs", "actions", "rewards", "terminateds", "weights")}
+class _SACModule(torch.nn.Module):
+    """The SAC networks of one learner: squashed-Gaussian actor, twin Q critics, their
+    Polyak-averaged targets and the entropy temperature log(alpha)."""
 
-
-class SACLearner:
     def __init__(self, cfg, obs_space, act_space):
-        self.cfg = cfg
-        self.device = torch.device("cuda") if torch.cuda.is_available() and cfg.get(
-            "num_gpus_per_learner", 1) else torch.device("cpu")
-        dev = self.device
+        super().__init__()
         pm = cfg.get("policy_model_config") or cfg.get("model")
         qm = cfg.get("q_model_config") or cfg.get("model")
-        self.pi = SquashedGaussianPolicy(obs_space, act_space, pm).to(dev)
-        self.q = TwinQ(obs_space, act_space, qm).to(dev)
+        self.pi = SquashedGaussianPolicy(obs_space, act_space, pm)
+        self.q = TwinQ(obs_space, act_space, qm)
         self.q_t = copy.deepcopy(self.q)
-        for p in self.q_t.parameters():
-            p.requires_grad_(False)
-        act_dim = int(np.prod(act_space.shape))
-        te = cfg.get("target_entropy", "auto")
+        self.q_t.requires_grad_(False)
+        self.log_alpha = torch.nn.Parameter(
+            torch.tensor(float(np.log(cfg.get("initial_alpha", 1.0)))))
+
+
+class SACLearner(TorchLearner):
+    """SAC on the learner pipeline (reference: rllib/algorithms/sac/sac_learner.py,
+    torch/sac_torch_learner.py): ``compute_losses`` returns the critic, actor and
+    temperature losses keyed by their optimizers' names, so ``compute_gradients``
+    back-propagates each into its own parameters only (the actor's loss does not touch
+    the critics' gradients); gradients of every learner of the group are averaged before
+    the three optimizers step; the target critics follow by Polyak averaging in
+    ``after_gradient_based_update``. CQL overrides ``extra_critic_loss`` / ``actor_loss``."""
+
+    def build_module(self):
+        return _SACModule(self.config, self.observation_space, self.action_space)
+
+    def configure_optimizers_for_module(self, module_id, config):
+        m = self.module
+        fused = self.device.type == "cuda"
+        act_dim = int(np.prod(self.action_space.shape))
+        te = config.get("target_entropy", "auto")
         self.target_entropy = -float(act_dim) if te in (None, "auto") else float(te)
-        self.log_alpha = torch.tensor(float(np.log(cfg.get("initial_alpha", 1.0))),
-                                      device=dev, requires_grad=True)
-        fused = dev.type == "cuda"
-        self.opt_pi = torch.optim.Adam(self.pi.parameters(), lr=cfg.get("actor_lr", 3e-4),
-                                       fused=fused)
-        self.opt_q = torch.optim.Adam(self.q.parameters(), lr=cfg.get("critic_lr", 3e-4),
-                                      fused=fused)
-        self.opt_a = torch.optim.Adam([self.log_alpha], lr=cfg.get("alpha_lr", 3e-4))
-        self.gamma = cfg.get("gamma", 0.99)
-        self.tau = cfg.get("tau", 5e-3)
+        self.gamma = config.get("gamma", 0.99)
+        self.tau = config.get("tau", 5e-3)
+        self.register_optimizer(module_id=module_id, optimizer_name="critic",
+                                optimizer=torch.optim.Adam(m.q.parameters(),
+                                                           lr=config.get("critic_lr", 3e-4),
+                                                           fused=fused),
+                                params=list(m.q.parameters()))
+        self.register_optimizer(module_id=module_id, optimizer_name="actor",
+                                optimizer=torch.optim.Adam(m.pi.parameters(),
+                                                           lr=config.get("actor_lr", 3e-4),
+                                                           fused=fused),
+                                params=list(m.pi.parameters()))
+        self.register_optimizer(module_id=module_id, optimizer_name="alpha",
+                                optimizer=torch.optim.Adam([m.log_alpha],
+                                                           lr=config.get("alpha_lr", 3e-4)),
+                                params=[m.log_alpha])
+
+    # convenience views (CQL, tests)
+    @property
+    def pi(self):
+        return self.module.pi
+
+    @property
+    def q(self):
+        return self.module.q
+
+    @property
+    def q_t(self):
+        return self.module.q_t
+
+    @property
+    def log_alpha(self):
+        return self.module.log_alpha
+
+    def _convert_batch(self, batch):
+        keep = ("obs", "next_obs", "actions", "rewards", "terminateds", "weights")
+        return super()._convert_batch({k: np.asarray(v) if not torch.is_tensor(v) else v
+                                       for k, v in batch.items() if k in keep})
 
     # ---------------------------------------------------------------- losses
     def critic_target(self, b):
@@ -90,77 +132,52 @@ class SACLearner:
     def extra_critic_loss(self, b, q1, q2):
         return None  # CQL adds its conservative regulariser here
 
-    def update(self, batch):
-        b = _to(batch, self.device)
-        w = b.get("weights")
-        tgt = self.critic_target(b)
-        q1, q2 = self.q(b["obs"], b["actions"])
-        td = (q1 - tgt).detach()
-        l1 = (q1 - tgt) ** 2
-        l2 = (q2 - tgt) ** 2
-        if w is not None:
-            l1, l2 = l1 * w, l2 * w
-        critic_loss = 0.5 * (l1.mean() + l2.mean())
-        extra = self.extra_critic_loss(b, q1, q2)
-        if extra is not None:
-            critic_loss = critic_loss + extra
-        self.opt_q.zero_grad(set_to_none=True)
-        critic_loss.backward()
-        if self.cfg.get("grad_clip"):
-            torch.nn.utils.clip_grad_norm_(self.q.parameters(), self.cfg["grad_clip"])
-        self.opt_q.step()
-        # actor: maximise min-Q - alpha * logp (critics frozen for this step)
-        for p in self.q.parameters():
-            p.requires_grad_(False)
-        a, logp = self.pi(b["obs"])
-        qa1, qa2 = self.q(b["obs"], a)
-        alpha = self.log_alpha.exp().detach()
-        actor_loss = self.actor_loss(b, a, logp, torch.min(qa1, qa2), alpha)
-        self.opt_pi.zero_grad(set_to_none=True)
-        actor_loss.backward()
-        self.opt_pi.step()
-        for p in self.q.parameters():
-            p.requires_grad_(True)
-        alpha_loss = -(self.log_alpha * (logp.detach() + self.target_entropy)).mean()
-        self.opt_a.zero_grad(set_to_none=True)
-        alpha_loss.backward()
-        self.opt_a.step()
-        with torch.no_grad():  # Polyak target update
-            for pt, p in zip(self.q_t.parameters(), self.q.parameters()):
-                pt.lerp_(p, self.tau)
-        stats = {"critic_loss": float(critic_loss.detach()),
-                 "actor_loss": float(actor_loss.detach()), "alpha_loss": float(alpha_loss.detach()), "alpha_value": float(alpha),
-                 "mean_q": float(q1.detach().mean()), "entropy": float(-logp.detach().mean())}
-        return stats, td.abs().cpu().numpy()
-
     def actor_loss(self, b, a, logp, qmin, alpha):
         return (alpha * logp - qmin).mean()
 
-    # ---------------------------------------------------------------- state
+    def forward_train(self, b):
+        tgt = self.critic_target(b)
+        q1, q2 = self.q(b["obs"], b["actions"])
+        a, logp = self.pi(b["obs"])
+        qa1, qa2 = self.q(b["obs"], a)
+        return {"target": tgt, "q1": q1, "q2": q2, "a": a, "logp": logp,
+                "qmin_pi": torch.min(qa1, qa2)}
+
+    def compute_losses(self, *, fwd_out, batch):
+        f, b = fwd_out, batch
+        w = b.get("weights")
+        tgt, q1, q2 = f["target"], f["q1"], f["q2"]
+        self._td = (q1 - tgt).detach()
+        l1, l2 = (q1 - tgt) ** 2, (q2 - tgt) ** 2
+        if w is not None:
+            l1, l2 = l1 * w, l2 * w
+        critic = 0.5 * (l1.mean() + l2.mean())
+        extra = self.extra_critic_loss(b, q1, q2)
+        if extra is not None:
+            critic = critic + extra
+        alpha = self.log_alpha.exp().detach()
+        actor = self.actor_loss(b, f["a"], f["logp"], f["qmin_pi"], alpha)
+        alpha_loss = -(self.log_alpha * (f["logp"].detach() + self.target_entropy)).mean()
+        self.metrics = {"alpha_value": float(alpha), "mean_q": float(q1.detach().mean()),
+                        "entropy": float(-f["logp"].detach().mean())}
+        return {"critic": critic, "actor": actor, "alpha": alpha_loss}
+
+    def after_gradient_based_update(self, *, timesteps=None):
+        with torch.no_grad():  # Polyak target update
+            for pt, p in zip(self.q_t.parameters(), self.q.parameters()):
+                pt.lerp_(p, self.tau)
+
+    def _update(self, batch, timesteps=None):
+        out = super()._update(batch, timesteps=timesteps)
+        out["td_error"] = self._td.abs().float().cpu().numpy()
+        return out
+
+    # the EnvRunners run the actor: its state dict is "the weights"
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.pi.state_dict().items()}
 
     def set_weights(self, w):
         self.pi.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
-
-    def get_state(self):
-        return {"pi": self.get_weights(),
-                "q": {k: v.detach().cpu() for k, v in self.q.state_dict().items()},
-                "q_t": {k: v.detach().cpu() for k, v in self.q_t.state_dict().items()},
-                "log_alpha": float(self.log_alpha.detach()),
-                "opt": [o.state_dict() for o in (self.opt_pi, self.opt_q, self.opt_a)]}
-
-    def set_state(self, s):
-        self.pi.load_state_dict(s["pi"])
-        self.q.load_state_dict(s["q"])
-        self.q_t.load_state_dict(s["q_t"])
-        with torch.no_grad():
-            self.log_alpha.fill_(s["log_alpha"])
-        for o, st in zip((self.opt_pi, self.opt_q, self.opt_a), s["opt"]):
-            o.load_state_dict(st)
-
-    def shutdown(self):
-        pass
 
 
 class SAC(Algorithm):
@@ -180,15 +197,16 @@ class SAC(Algorithm):
 
     def setup(self):
         self.prioritized = "Prioritized" in self.config.replay_buffer_config.get("type", "")
-        if self.is_multi_agent:  # one SAC learner + replay buffer per trainable module
+        if self.is_multi_agent:  # one SAC learner group + replay buffer per module
             self.learner_group = PerModuleLearners(
-                lambda os_, as_: self.learner_class(self.cfg, os_, as_), self.module_specs,
-                self.config.policies_to_train)
+                lambda os_, as_, mid: LearnerGroup(self.cfg, os_, as_, module_id=mid,
+                                                   learner_class=self.learner_class),
+                self.module_specs, self.config.policies_to_train)
             self.buffers = {mid: self._new_buffer() for mid in self.learner_group.trainable}
         else:
             self.buffer = self._new_buffer()
-            self.learner_group = self.learner_class(self.cfg, self.observation_space,
-                                                    self.action_space)
+            self.learner_group = LearnerGroup(self.cfg, self.observation_space,
+                                              self.action_space, learner_class=self.learner_class)
         self._sync_weights(self.learner_group.get_weights())
 
     def _updates(self, buf, learner, new, stats, prefix=""):
@@ -201,10 +219,10 @@ class SAC(Algorithm):
         for _ in range(n_updates):
             kw = {"beta": cfg.replay_buffer_config.get("beta", 0.4)} if self.prioritized else {}
             mb = buf.sample(cfg.train_batch_size, **kw)
-            st, td = learner.update(mb)
+            st = learner.update_from_batch(mb, timesteps=self.total_env_steps)
             if self.prioritized:
-                buf.update_priorities(mb["batch_indexes"], td)
-        stats.update({prefix + k: v for k, v in st.items()})
+                buf.update_priorities(mb["batch_indexes"], st["td_error"])
+        stats.update({prefix + k: v for k, v in st.items() if not isinstance(v, np.ndarray)})
 
     def training_step(self):
         cfg = self.config
@@ -235,11 +253,9 @@ class SAC(Algorithm):
         self._sync_weights(self.learner_group.get_weights())
         return stats
 
-    def compute_single_action(self, obs, explore=False):
-        lg = self.learner_group
-        with torch.no_grad():
-            x = torch.as_tensor(np.asarray(obs, np.float32)[None]).to(lg.device)
-            a, _ = lg.pi(x, explore, with_logp=False)
-        return a[0].cpu().numpy()
+    def compute_single_action(self, obs, explore=False, policy_id=None):
+        a = super().compute_single_action(obs, explore, policy_id)
+        return np.asarray(a, np.float32).reshape(self.action_space.shape) \
+            if not self.is_multi_agent else a
 
     compute_action = compute_single_action

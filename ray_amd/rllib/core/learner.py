@@ -74,7 +74,349 @@ def concat_batches(batches, lazy=()):
     return out
 
 
-class Learner:
+
+def _default_device(config) -> torch.device:
+    if torch.cuda.is_available() and config.get("num_gpus_per_learner", 1):
+        return torch.device("cuda", int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0")))
+    return torch.device("cpu")
+
+
+class TorchLearner:
+    """The learner pipeline every RLlib algorithm trains through (reference:
+    rllib/core/learner/learner.py — :455 compute_gradients, :475 postprocess_gradients,
+    :585 apply_gradients, :1149 update_from_batch, :1192 update_from_episodes, :1237
+    _update, :1498/:1531 save_state/load_state; torch_learner.py).
+
+    One update::
+
+        batch -> _convert_batch -> forward_train -> compute_losses (compute_loss_for_module
+        per module) -> compute_gradients (backward; with several learners the gradients
+        are averaged over the learner group in ONE flat all-reduce on RCCL / gloo)
+        -> postprocess_gradients (default: clipping by ``grad_clip`` / ``grad_clip_by``)
+        -> apply_gradients (every registered optimizer steps)
+        -> after_gradient_based_update (target networks, schedules)
+
+    ``compute_losses`` may return one loss per REGISTERED OPTIMIZER (e.g. SAC's critic /
+    actor / alpha): then each loss is back-propagated into that optimizer's parameters
+    only (``backward(inputs=...)``). Subclasses build their networks in ``build_module``
+    and their optimizers in ``configure_optimizers_for_module``. Learners of one group
+    start from rank 0's parameters (broadcast) and apply identical averaged gradients,
+    so their weights stay identical."""
+
+    def __init__(self, config: dict, observation_space, action_space, device=None, rank=0,
+                 world=1, module_id=DEFAULT_MODULE_ID):
+        self.config = config
+        self.observation_space = observation_space
+        self.action_space = action_space
+        self.device = device if device is not None else _default_device(config)
+        self.rank, self.world = rank, world
+        self.module_id = module_id
+        torch.manual_seed(config.get("seed") or 0)
+        self._optimizers = {}  # (module_id, name) -> (torch optimizer, params)
+        self.metrics = {}
+        self.updates = 0
+        self.build()
+        if self.world > 1:
+            self._broadcast_params()
+
+    @property
+    def cfg(self) -> dict:
+        return self.config
+
+    # ---------------------------------------------------------------- build
+    def build(self):
+        self.module = self.build_module().to(self.device)
+        self.configure_optimizers()
+
+    def build_module(self) -> torch.nn.Module:
+        from ray_amd.rllib.core.rl_module.rl_module import build_module
+
+        return build_module(self.config, self.observation_space, self.action_space,
+                            self.module_id if self.config.get("is_multi_agent") else None)
+
+    def configure_optimizers(self):
+        self.configure_optimizers_for_module(self.module_id, self.config)
+
+    def configure_optimizers_for_module(self, module_id, config):
+        """Default: one Adam over the module's trainable parameters at ``lr``."""
+        params = [p for p in self.module.parameters() if p.requires_grad]
+        self.register_optimizer(module_id=module_id, optimizer=torch.optim.Adam(
+            params, lr=config.get("lr") or 1e-3), params=params)
+
+    def register_optimizer(self, *, module_id=DEFAULT_MODULE_ID, optimizer_name="default",
+                           optimizer, params=None, lr_or_lr_schedule=None):
+        params = list(params) if params is not None else \
+            [p for g in optimizer.param_groups for p in g["params"]]
+        self._optimizers[(module_id, optimizer_name)] = (optimizer, params)
+
+    def get_optimizer(self, module_id=DEFAULT_MODULE_ID, optimizer_name="default"):
+        ent = self._optimizers.get((module_id, optimizer_name))
+        return ent[0] if ent else None
+
+    def get_optimizers_for_module(self, module_id=DEFAULT_MODULE_ID):
+        return [(n, o) for (m, n), (o, _) in self._optimizers.items() if m == module_id]
+
+    def get_parameters(self, module=None):
+        return list((module or self.module).parameters())
+
+    def _named_params(self):
+        """name -> parameter over every registered optimizer's parameters (stable order)."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        out = {}
+        for (m, oname), (_, ps) in self._optimizers.items():
+            for i, p in enumerate(ps):
+                out.setdefault(names.get(id(p), f"{m}/{oname}/{i}"), p)
+        return out
+
+    # ---------------------------------------------------------------- multi-learner
+    def _broadcast_params(self):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            return
+        with torch.no_grad():
+            for t in list(self.module.parameters()) + list(self.module.buffers()):
+                dist.broadcast(t.data, src=0)
+
+    def _allreduce_grads(self, params):
+        """Average the gradients of ``params`` over the learner group: one flat fp32
+        all-reduce (missing gradients count as zeros, so every rank packs the same)."""
+        if self.world <= 1:
+            return
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            return
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                          .float() for p in params])
+        dist.all_reduce(flat)
+        flat.div_(self.world)
+        o = 0
+        for p in params:
+            n = p.numel()
+            g = flat[o:o + n].view_as(p).to(p.dtype)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            o += n
+
+    def _allreduce_mean(self, x: float) -> float:
+        """Mean of a host scalar over the learner group (learner-side statistics that must
+        stay identical on every rank)."""
+        if self.world <= 1:
+            return float(x)
+        import torch.distributed as dist
+
+        t = torch.tensor([float(x)], dtype=torch.float64,
+                         device=self.device if self.device.type == "cuda" else "cpu")
+        dist.all_reduce(t)
+        return float(t) / self.world
+
+    # ---------------------------------------------------------------- the pipeline
+    def update_from_batch(self, batch, *, timesteps=None, num_epochs=1, minibatch_size=None,
+                          shuffle_batch_per_epoch=False, **kwargs) -> dict:
+        """Gradient updates on ``batch`` (a dict of arrays / tensors with a common leading
+        row axis): ``num_epochs`` passes in minibatches of ``minibatch_size`` rows (the
+        whole batch by default). Returns the last update's metrics (scalars; per-row
+        arrays such as ``td_error`` cover the whole batch)."""
+        n = _rows(batch)
+        if not minibatch_size or minibatch_size >= n:
+            res = {}
+            for _ in range(max(1, num_epochs)):
+                res = self._update(batch, timesteps=timesteps)
+            return res
+        res, per_row = {}, {}
+        rng = np.random.default_rng(self.config.get("seed"))
+        for _ in range(max(1, num_epochs)):
+            order = rng.permutation(n) if shuffle_batch_per_epoch else np.arange(n)
+            for s in range(0, n - minibatch_size + 1, minibatch_size):
+                idx = order[s:s + minibatch_size]
+                res = self._update(_take_rows(batch, idx), timesteps=timesteps)
+                for k, v in list(res.items()):
+                    if isinstance(v, np.ndarray) and v.shape[:1] == (len(idx),):
+                        per_row.setdefault(k, np.zeros((n,) + v.shape[1:], v.dtype))[idx] = v
+        res.update(per_row)
+        return res
+
+    def update_from_episodes(self, episodes, *, timesteps=None, **kwargs) -> dict:
+        """Train on a list of SingleAgentEpisodes (the learner connector step of the
+        reference: ``episodes_to_batch`` flattens them into transition rows)."""
+        return self.update_from_batch(self.episodes_to_batch(episodes), timesteps=timesteps,
+                                      **kwargs)
+
+    def episodes_to_batch(self, episodes) -> dict:
+        obs, nobs, act, rew, term = [], [], [], [], []
+        for ep in episodes:
+            o = np.asarray(ep.get_observations())
+            T = len(ep.get_actions())
+            obs.append(o[:T])
+            nobs.append(o[1:T + 1])
+            act.append(np.asarray(ep.get_actions()))
+            rew.append(np.asarray(ep.get_rewards(), np.float32))
+            t = np.zeros(T, np.float32)
+            if ep.is_terminated and T:
+                t[-1] = 1.0
+            term.append(t)
+        return {"obs": np.concatenate(obs), "next_obs": np.concatenate(nobs),
+                "actions": np.concatenate(act), "rewards": np.concatenate(rew),
+                "terminateds": np.concatenate(term)}
+
+    def _update(self, batch, timesteps=None) -> dict:
+        batch = self._convert_batch(batch)
+        fwd_out = self.forward_train(batch)
+        losses = self.compute_losses(fwd_out=fwd_out, batch=batch)
+        grads = self.compute_gradients(losses)
+        grads = self.postprocess_gradients(grads)
+        self.apply_gradients(grads)
+        self.updates += 1
+        self.after_gradient_based_update(timesteps=timesteps)
+        out = {f"{k}_loss" if not str(k).endswith("loss") else str(k): float(v.detach())
+               for k, v in losses.items()}
+        out["total_loss"] = float(sum(float(v.detach()) for v in losses.values()))
+        out.update(self.metrics)
+        return out
+
+    def _convert_batch(self, batch) -> dict:
+        out = {}
+        for k, v in batch.items():
+            if isinstance(v, np.ndarray):
+                out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(self.device)
+            elif torch.is_tensor(v):
+                out[k] = v.to(self.device)
+            else:
+                out[k] = v
+        return out
+
+    def forward_train(self, batch) -> dict:
+        return self.module.forward_train(batch[Columns.OBS])
+
+    def compute_losses(self, *, fwd_out, batch) -> dict:
+        return {self.module_id: self.compute_loss_for_module(module_id=self.module_id,
+                                                             config=self.config, batch=batch,
+                                                             fwd_out=fwd_out)}
+
+    def compute_loss_for_module(self, *, module_id, config, batch, fwd_out):
+        raise NotImplementedError
+
+    def compute_gradients(self, loss_per_module, **kwargs) -> dict:
+        """Back-propagate and average over the learner group; returns {param name: grad}.
+        Losses keyed by optimizer names go into those optimizers' parameters only."""
+        named = self._named_params()
+        params = list(named.values())
+        for p in params:
+            p.grad = None
+        by_opt = {n: ps for (m, n), (_, ps) in self._optimizers.items()}
+        if len(self._optimizers) > 1 and set(loss_per_module) <= set(by_opt):
+            keys = list(loss_per_module)
+            for i, k in enumerate(keys):
+                loss_per_module[k].backward(retain_graph=i + 1 < len(keys),
+                                            inputs=list(by_opt[k]))
+        else:
+            sum(loss_per_module.values()).backward()
+        self._allreduce_grads(params)
+        return {n: p.grad for n, p in named.items() if p.grad is not None}
+
+    def postprocess_gradients(self, gradients_dict) -> dict:
+        return self.postprocess_gradients_for_module(module_id=self.module_id,
+                                                     config=self.config,
+                                                     module_gradients_dict=gradients_dict)
+
+    def postprocess_gradients_for_module(self, *, module_id, config, module_gradients_dict):
+        """Default: ``grad_clip`` by ``grad_clip_by`` ("global_norm" (default), "norm" per
+        tensor, or "value")."""
+        clip = (config or {}).get("grad_clip")
+        if not clip:
+            return module_gradients_dict
+        by = (config or {}).get("grad_clip_by", "global_norm")
+        grads = [g for g in module_gradients_dict.values() if g is not None]
+        if by == "value":
+            for g in grads:
+                g.clamp_(-clip, clip)
+        elif by == "norm":
+            for g in grads:
+                n = g.norm()
+                if n > clip:
+                    g.mul_(clip / (n + 1e-6))
+        else:
+            torch.nn.utils.clip_grad_norm_(grads, clip)  # clips the tensors in place
+        return module_gradients_dict
+
+    def apply_gradients(self, gradients_dict):
+        named = self._named_params()
+        for n, g in gradients_dict.items():
+            p = named.get(n)
+            if p is not None and g is not p.grad:
+                p.grad = g
+        for opt, _ in self._optimizers.values():
+            opt.step()
+
+    def after_gradient_based_update(self, *, timesteps=None):
+        """Hook after every update (target networks, schedules)."""
+
+    # ---------------------------------------------------------------- state
+    def get_weights(self):
+        return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
+
+    def set_weights(self, w):
+        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in w.items()})
+
+    def get_state(self):
+        return {"module": {k: v.detach().cpu() for k, v in self.module.state_dict().items()},
+                "optimizers": {f"{m}/{n}": o.state_dict()
+                               for (m, n), (o, _) in self._optimizers.items()},
+                "updates": self.updates, "extra": self._extra_state()}
+
+    def set_state(self, s):
+        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in s["module"].items()})
+        for (m, n), (o, _) in self._optimizers.items():
+            st = (s.get("optimizers") or {}).get(f"{m}/{n}")
+            if st is not None:
+                o.load_state_dict(st)
+        self.updates = s.get("updates", self.updates)
+        self._load_extra_state(s.get("extra") or {})
+
+    def _extra_state(self) -> dict:
+        return {}
+
+    def _load_extra_state(self, s: dict):
+        pass
+
+    def save_state(self, path: str):
+        """Checkpoint this learner (module weights, optimizer states, counters) into the
+        directory ``path``."""
+        os.makedirs(path, exist_ok=True)
+        torch.save(self.get_state(), os.path.join(path, "learner_state.pt"))
+        return path
+
+    def load_state(self, path: str):
+        f = os.path.join(path, "learner_state.pt") if os.path.isdir(path) else path
+        self.set_state(torch.load(f, map_location="cpu", weights_only=False))
+
+    def shutdown(self):
+        pass
+
+
+def _rows(batch) -> int:
+    for v in batch.values():
+        if isinstance(v, (np.ndarray, torch.Tensor)) and getattr(v, "ndim", 0) >= 1:
+            return int(v.shape[0])
+    return 0
+
+
+def _take_rows(batch, idx):
+    out = {}
+    n = _rows(batch)
+    for k, v in batch.items():
+        if isinstance(v, (np.ndarray, torch.Tensor)) and getattr(v, "ndim", 0) >= 1 and \
+                v.shape[0] == n:
+            out[k] = v[idx] if isinstance(v, np.ndarray) else v[torch.as_tensor(idx)]
+        else:
+            out[k] = v
+    return out
+
+
+class Learner(TorchLearner):
     """One learner (one GPU). Extension points (reference: rllib/core/learner/learner.py
     :435 configure_optimizers_for_module, :948 compute_loss_for_module):
 
@@ -135,8 +477,13 @@ class Learner:
         self.updates = 0
         self._custom_loss = type(self).compute_loss_for_module is not \
             Learner.compute_loss_for_module
+        # an overridden gradient hook also needs the eager loop (the captured HIP-graph
+        # step fuses backward, clip and AdamW)
+        hooks = any(getattr(type(self), h) is not getattr(Learner, h) for h in
+                    ("compute_gradients", "postprocess_gradients",
+                     "postprocess_gradients_for_module", "apply_gradients"))
         self._generic = self._custom_loss or not self._builtin_module or self.stateful or \
-            bool(self._optimizers)
+            bool(self._optimizers) or hooks
         self.metrics = {}
         # MeanStdFilter statistics live HERE: updated over every training batch by the HIP
         # Welford kernel (obsnorm_update) and broadcast to the EnvRunners with the weights
@@ -313,22 +660,49 @@ class Learner:
         return torch.cat(out)
 
     def _step(self, loss):
+        """One optimizer step of the generic (eager) path, through the pipeline hooks."""
+        grads = self.compute_gradients({self.module_id: loss})
+        grads = self.postprocess_gradients(grads)
+        self.apply_gradients(grads)
+
+    # ---- pipeline hooks on the flat-buffer layout: gradients are views of ONE buffer
+    # that FlatDDP all-reduces bucket by bucket during backward; the fused AdamW kernel
+    # clips by global norm on device, so the default postprocessing is a no-op there
+    def compute_gradients(self, loss_per_module, **kwargs) -> dict:
+        for opt, _ in self._optimizers.values():
+            opt.zero_grad(set_to_none=False)
+        self.flat.zero_grad()
+        sum(loss_per_module.values()).backward()
+        self.ddp.finish()
+        return {n: (p._ra_grad if getattr(p, "_ra_grad", None) is not None else p.grad)
+                for n, p in zip(self.flat.names, self.flat.params())}
+
+    def postprocess_gradients_for_module(self, *, module_id, config, module_gradients_dict):
+        if self._optimizers:  # torch optimizers: clip here (the flat AdamW clips itself)
+            return super().postprocess_gradients_for_module(
+                module_id=module_id, config=config, module_gradients_dict=module_gradients_dict)
+        return module_gradients_dict
+
+    def apply_gradients(self, gradients_dict):
+        for n, p in zip(self.flat.names, self.flat.params()):
+            g = gradients_dict.get(n)
+            dst = getattr(p, "_ra_grad", None)
+            if dst is None:
+                dst = p.grad
+            if g is not None and dst is not None and g is not dst:
+                dst.copy_(g)
         if self._optimizers:
             for opt, _ in self._optimizers.values():
-                opt.zero_grad(set_to_none=False)
-            self.flat.zero_grad()
-            loss.backward()
-            self.ddp.finish()
-            gc = self.config.get("grad_clip")
-            for opt, params in self._optimizers.values():
-                if gc:
-                    torch.nn.utils.clip_grad_norm_(params, gc)
                 opt.step()
-            return
-        self.flat.zero_grad()
-        loss.backward()
-        self.ddp.finish()
-        self.opt.step()
+        else:
+            self.opt.step()
+
+    def update_from_batch(self, batch, *, timesteps=None, **kwargs) -> dict:
+        """PPO (GAE + epochs of minibatch SGD) or V-trace on a [T, B] rollout batch: the
+        fused HIP path (loss+grad kernel, HIP-graph step) unless a pipeline hook is
+        overridden, then the eager loop through the hooks."""
+        kind = kwargs.get("kind") or self.config.get("_learner_kind", "ppo")
+        return self.update_ppo(batch) if kind == "ppo" else self.update_vtrace(batch)
 
     # ---------------------------------------------------------------- PPO
     def update_ppo(self, batch: dict) -> dict:
@@ -744,9 +1118,8 @@ def _learner_cls(config):
     return config.get("learner_class") or Learner
 
 
-# reference class names (rllib/core/learner/torch/torch_learner.py,
-# algorithms/{ppo,impala,appo}/torch/*_torch_learner.py): one MI355X learner serves all
-TorchLearner = Learner
+# reference class names (algorithms/{ppo,impala,appo}/torch/*_torch_learner.py): one
+# MI355X learner serves all three; TorchLearner is the generic pipeline base above
 PPOTorchLearner = Learner
 IMPALATorchLearner = Learner
 APPOTorchLearner = Learner
@@ -789,14 +1162,23 @@ class LearnerActor:
 
 
 class LearnerGroup:
+    """The learners of one module (reference: rllib/core/learner/learner_group.py):
+    ``num_learners=0`` -> one local learner in the algorithm process; ``N > 0`` -> N learner
+    actors (one GPU each) joined in one torch process group (RCCL on GPUs, gloo on CPUs),
+    each training on its 1/N share of every batch with gradients averaged in
+    ``compute_gradients``. ``learner_class`` (or ``config["learner_class"]``) picks the
+    algorithm's Learner (PPO/IMPALA: the fused HIP ``Learner``; DQN, SAC, CQL, MARWIL/BC:
+    their ``TorchLearner`` subclasses)."""
+
     def __init__(self, config: dict, observation_space, action_space,
-                 module_id=DEFAULT_MODULE_ID):
+                 module_id=DEFAULT_MODULE_ID, learner_class=None):
         self.config = config
+        self.learner_class = config.get("learner_class") or learner_class or Learner
         n = int(config.get("num_learners", 0))
         self.remote = n > 0
         if not self.remote:
-            self.local = _learner_cls(config)(config, observation_space, action_space,
-                                              module_id=module_id)
+            self.local = self.learner_class(config, observation_space, action_space,
+                                            module_id=module_id)
             self.actors = []
             return
         import ray_amd as ray
@@ -817,8 +1199,72 @@ class LearnerGroup:
         _TorchBackend().on_start(self.wg, TorchConfig(backend=config.get("learner_backend")))
         self.actors = self.wg.workers
         ray.get([a.execute.remote(_make_learner, config, observation_space, action_space, i, n,
-                                  module_id) for i, a in enumerate(self.actors)])
+                                  module_id, self.learner_class)
+                 for i, a in enumerate(self.actors)])
         self.local = None
+
+    @property
+    def is_local(self) -> bool:
+        return not self.remote
+
+    def update_from_batch(self, batch, *, async_update=False, timesteps=None, **kwargs):
+        """One update step on ``batch`` (rows split evenly over the learners; per-row
+        outputs such as ``td_error`` come back in row order, scalars averaged).
+        ``async_update=True`` returns pending results (``collect_async``) instead."""
+        if not self.remote:
+            return self.local.update_from_batch(batch, timesteps=timesteps, **kwargs)
+        import ray_amd as ray
+
+        n = len(self.actors)
+        shards = _split_rows(batch, n)
+        refs = [a.execute.remote(_learner_call_kw, "update_from_batch", (sh,),
+                                 dict(kwargs, timesteps=timesteps))
+                for a, sh in zip(self.actors, shards)]
+        if async_update:
+            return refs
+        return _reduce_results(ray.get(refs))
+
+    def update_from_episodes(self, episodes, *, async_update=False, timesteps=None, **kwargs):
+        """One update step on a list of episodes, dealt round-robin to the learners."""
+        if not self.remote:
+            return self.local.update_from_episodes(episodes, timesteps=timesteps, **kwargs)
+        import ray_amd as ray
+
+        n = len(self.actors)
+        refs = [a.execute.remote(_learner_call_kw, "update_from_episodes", (episodes[i::n],),
+                                 dict(kwargs, timesteps=timesteps))
+                for i, a in enumerate(self.actors)]
+        if async_update:
+            return refs
+        return _reduce_results(ray.get(refs))
+
+    def foreach_learner(self, func, **kwargs) -> list:
+        """``func(learner, **kwargs)`` on every learner (local or remote), results in rank
+        order (reference: learner_group.py:613)."""
+        if not self.remote:
+            return [func(self.local, **kwargs)]
+        import ray_amd as ray
+
+        return ray.get([a.execute.remote(_learner_apply, func, kwargs) for a in self.actors])
+
+    def save_state(self, path: str):
+        """Rank 0's learner state into directory ``path`` (all ranks hold the same)."""
+        if not self.remote:
+            return self.local.save_state(path)
+        import ray_amd as ray
+
+        st = ray.get(self.actors[0].execute.remote(_learner_call, "get_state"))
+        os.makedirs(path, exist_ok=True)
+        torch.save(st, os.path.join(path, "learner_state.pt"))
+        return path
+
+    def load_state(self, path: str):
+        f = os.path.join(path, "learner_state.pt") if os.path.isdir(path) else path
+        self.set_state(torch.load(f, map_location="cpu", weights_only=False))
+
+    def sync_target(self):
+        """Off-policy learners: copy the online networks into their targets."""
+        self.foreach_learner(lambda lr: getattr(lr, "sync_target", lambda: None)())
 
     def update(self, kind, batches):
         if not self.remote:
@@ -905,11 +1351,56 @@ class LearnerGroup:
 _LEARNER = None
 
 
-def _make_learner(config, obs_space, act_space, rank, world, module_id=DEFAULT_MODULE_ID):
+def _make_learner(config, obs_space, act_space, rank, world, module_id=DEFAULT_MODULE_ID,
+                  learner_class=None):
     global _LEARNER
-    _LEARNER = _learner_cls(config)(config, obs_space, act_space, rank=rank, world=world,
-                                    module_id=module_id)
+    cls = learner_class or _learner_cls(config)
+    _LEARNER = cls(config, obs_space, act_space, rank=rank, world=world, module_id=module_id)
     return True
+
+
+def _learner_call_kw(name, args, kwargs):
+    return getattr(_LEARNER, name)(*args, **kwargs)
+
+
+def _learner_apply(func, kwargs):
+    return func(_LEARNER, **kwargs)
+
+
+def _split_rows(batch, n):
+    """Row shards of a dict batch (arrays with the common leading row axis are split,
+    everything else is replicated)."""
+    rows = _rows(batch)
+    idx = np.array_split(np.arange(rows), n)
+    out = []
+    for ix in idx:
+        sh = {}
+        for k, v in batch.items():
+            if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == rows:
+                sh[k] = v[ix[0]:ix[-1] + 1] if len(ix) else v[:0]
+            else:
+                sh[k] = v
+        out.append(sh)
+    return out
+
+
+def _reduce_results(results):
+    """Per-learner metrics -> one dict: per-row arrays concatenated in rank order,
+    numbers averaged, anything else from rank 0."""
+    if not results:
+        return {}
+    if not isinstance(results[0], dict):
+        return results[0]
+    out = {}
+    for k, v in results[0].items():
+        vals = [r.get(k) for r in results]
+        if all(isinstance(x, np.ndarray) for x in vals):
+            out[k] = np.concatenate(vals)
+        elif all(isinstance(x, (int, float, np.floating, np.integer)) for x in vals):
+            out[k] = float(np.mean(vals))
+        else:
+            out[k] = v
+    return out
 
 
 def _learner_update(kind, batches):
@@ -946,10 +1437,29 @@ class MultiAgentLearnerGroup:
     so each gets its own flat-param learner; runner outputs are split by module id."""
 
     def __init__(self, config: dict, specs: dict, policies_to_train=None):
+        self.config = config
         self.specs = specs
         self.trainable = set(policies_to_train) if policies_to_train else set(specs)
         self.groups = {mid: LearnerGroup(config, os_, as_, module_id=mid)
                        for mid, (os_, as_) in specs.items()}
+
+    def add(self, mid, spec, trainable=True):
+        """A new module's learner group mid-training (Algorithm.add_module)."""
+        self.specs = dict(self.specs)
+        self.specs[mid] = spec
+        self.groups[mid] = LearnerGroup(self.config, spec[0], spec[1], module_id=mid)
+        if trainable:
+            self.trainable.add(mid)
+
+    def remove(self, mid):
+        g = self.groups.pop(mid, None)
+        self.specs = {k: v for k, v in self.specs.items() if k != mid}
+        self.trainable.discard(mid)
+        if g is not None:
+            g.shutdown()
+
+    def foreach_learner(self, func, **kwargs):
+        return {mid: g.foreach_learner(func, **kwargs) for mid, g in self.groups.items()}
 
     def update(self, kind, batches):
         stats = {}

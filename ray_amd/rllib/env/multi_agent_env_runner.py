@@ -146,6 +146,39 @@ class MultiAgentEnvRunner:
         return {mid: {k: v.detach().cpu() for k, v in m.state_dict().items()}
                 for mid, m in self.modules.items()}
 
+    # ---------------------------------------------------------------- module set
+    def add_module(self, module_id, spaces, weights=None):
+        """A module added mid-training (Algorithm.add_module): built here for inference,
+        with ``weights`` when given."""
+        os_, as_ = spaces
+        self.specs = dict(self.specs)
+        self.specs[module_id] = (os_, as_)
+        m = self._make_module(os_, as_, module_id).eval()
+        if weights is not None:
+            m.load_state_dict({k: torch.as_tensor(v) for k, v in weights.items()})
+        self.modules[module_id] = m
+        return True
+
+    def remove_module(self, module_id):
+        """Drop a module; agents of episodes in progress that acted with it are re-mapped
+        on their next step (their unfinished rows of the removed module are dropped)."""
+        self.modules.pop(module_id, None)
+        self.specs = {k: v for k, v in self.specs.items() if k != module_id}
+        for i in range(len(self.envs)):
+            for aid, m in list(self.agent_module[i].items()):
+                if m == module_id:
+                    del self.agent_module[i][aid]
+            for aid, row in list(self.pending[i].items()):
+                if row["module"] == module_id:
+                    del self.pending[i][aid]
+        return True
+
+    def set_mapping_fn(self, fn):
+        """New agent -> module mapping; episodes in progress keep their agents' modules
+        (the mapping is evaluated once per agent per episode)."""
+        self.mapping_fn = fn
+        return True
+
     def apply(self, fn_blob):
         """Run ``fn(env_runner)`` here (Algorithm.env_runner_group.foreach_env_runner)."""
         import cloudpickle

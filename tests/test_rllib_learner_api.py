@@ -1,0 +1,238 @@
+"""The RLlib learner pipeline and LearnerGroup (modelled on rllib/core/learner/tests/
+test_learner.py, test_learner_group.py and rllib/algorithms/tests/test_algorithm.py's
+add/remove module cases): compute_losses -> compute_gradients -> postprocess_gradients
+-> apply_gradients behind update_from_batch / update_from_episodes, save_state /
+load_state, foreach_learner, off-policy algorithms on 2 gloo learners with identical
+weights, a postprocess_gradients override, and a self-play module added mid-training."""
+
+import numpy as np
+import pytest
+import torch
+
+import ray_amd as ray
+from ray_amd.rllib.algorithms.dqn import DQNConfig, DQNLearner
+from ray_amd.rllib.algorithms.ppo import PPOConfig
+from ray_amd.rllib.algorithms.sac import SACConfig, SACLearner
+from ray_amd.rllib.core.learner import Learner, LearnerGroup
+from ray_amd.rllib.env import make_env
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=6)
+    yield
+    ray.shutdown()
+
+
+def _cartpole_batch(n=64, seed=0):
+    rng = np.random.default_rng(seed)
+    return {"obs": rng.standard_normal((n, 4)).astype(np.float32),
+            "next_obs": rng.standard_normal((n, 4)).astype(np.float32),
+            "actions": rng.integers(0, 2, n), "rewards": np.ones(n, np.float32),
+            "terminateds": (rng.random(n) < 0.05).astype(np.float32)}
+
+
+def _dqn_cfg(**kw):
+    c = {"model": {"fcnet_hiddens": [32]}, "lr": 1e-3, "gamma": 0.99, "double_q": True,
+         "dueling": True, "grad_clip": 10.0, "num_gpus_per_learner": 0, "seed": 0}
+    c.update(kw)
+    return c
+
+
+def test_learner_pipeline_hooks_called_in_order_and_state_roundtrip(tmp_path):
+    env = make_env("CartPole-v1", {})
+    calls = []
+
+    class Traced(DQNLearner):
+        def compute_losses(self, *, fwd_out, batch):
+            calls.append("losses")
+            return super().compute_losses(fwd_out=fwd_out, batch=batch)
+
+        def compute_gradients(self, loss_per_module, **kw):
+            calls.append("gradients")
+            return super().compute_gradients(loss_per_module, **kw)
+
+        def postprocess_gradients(self, g):
+            calls.append("postprocess")
+            return super().postprocess_gradients(g)
+
+        def apply_gradients(self, g):
+            calls.append("apply")
+            return super().apply_gradients(g)
+
+    lr = Traced(_dqn_cfg(), env.observation_space, env.action_space)
+    res = lr.update_from_batch(_cartpole_batch())
+    assert calls == ["losses", "gradients", "postprocess", "apply"]
+    assert res["td_error"].shape == (64,) and np.isfinite(res["loss"])
+    # minibatches over epochs: per-row outputs still cover the whole batch
+    res = lr.update_from_batch(_cartpole_batch(64, 1), num_epochs=2, minibatch_size=16,
+                               shuffle_batch_per_epoch=True)
+    assert res["td_error"].shape == (64,)
+    path = lr.save_state(str(tmp_path / "ckpt"))
+    w0 = {k: v.clone() for k, v in lr.get_weights().items()}
+    lr.update_from_batch(_cartpole_batch(64, 2))
+    assert any(not torch.equal(w0[k], v) for k, v in lr.get_weights().items())
+    lr2 = DQNLearner(_dqn_cfg(seed=5), env.observation_space, env.action_space)
+    lr2.load_state(path)
+    assert all(torch.equal(w0[k], v) for k, v in lr2.get_weights().items())
+    assert lr2.get_optimizer().state_dict()["state"]  # Adam moments restored too
+
+
+def test_update_from_episodes(tmp_path):
+    from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+
+    env = make_env("CartPole-v1", {})
+    eps = []
+    for s in range(3):
+        ep = SingleAgentEpisode()
+        o, _ = env.reset(seed=s)
+        ep.add_env_reset(o)
+        for t in range(10):
+            a = t % 2
+            o, r, te, tr, _ = env.step(a)
+            ep.add_env_step(o, a, r, terminated=te, truncated=tr)
+            if te or tr:
+                break
+        eps.append(ep)
+    lr = DQNLearner(_dqn_cfg(), env.observation_space, env.action_space)
+    res = lr.update_from_episodes(eps)
+    assert res["td_error"].shape[0] == sum(len(e.get_actions()) for e in eps)
+
+
+def test_postprocess_gradients_override_freezes_training():
+    env = make_env("CartPole-v1", {})
+
+    class NoGrad(DQNLearner):
+        def postprocess_gradients(self, gradients_dict):
+            return {k: torch.zeros_like(g) for k, g in gradients_dict.items()}
+
+    lr = NoGrad(_dqn_cfg(), env.observation_space, env.action_space)
+    w0 = {k: v.clone() for k, v in lr.get_weights().items()}
+    for i in range(3):
+        lr.update_from_batch(_cartpole_batch(32, i))
+    # Adam with all-zero gradients leaves the weights unchanged
+    assert all(torch.equal(w0[k], v) for k, v in lr.get_weights().items())
+
+
+def test_ppo_learner_postprocess_override_takes_the_eager_path():
+    """An overridden gradient hook on the fused PPO Learner switches it to the eager
+    pipeline (the captured fused step would bypass the hook)."""
+    env = make_env("CartPole-v1", {})
+    seen = []
+
+    class Scaled(Learner):
+        def postprocess_gradients(self, g):
+            seen.append(len(g))
+            return {k: v * 0.0 for k, v in g.items()}
+
+    cfg = {"model": {"fcnet_hiddens": [16]}, "num_gpus_per_learner": 0, "seed": 0, "lr": 1e-2,
+           "num_epochs": 1, "minibatch_size": 32, "train_batch_size": 64}
+    lr = Scaled(cfg, env.observation_space, env.action_space)
+    assert lr._generic
+    T, B = 16, 4
+    rng = np.random.default_rng(0)
+    batch = {"obs": rng.standard_normal((T, B, 4)).astype(np.float32),
+             "actions": rng.integers(0, 2, (T, B)), "rewards": np.ones((T, B), np.float32),
+             "terminateds": np.zeros((T, B), np.float32),
+             "truncateds": np.zeros((T, B), np.float32),
+             "action_logp": np.full((T, B), np.log(0.5), np.float32),
+             "action_dist_inputs": np.zeros((T, B, 2), np.float32),
+             "bootstrap_obs": rng.standard_normal((B, 4)).astype(np.float32)}
+    w0 = {k: v.clone() for k, v in lr.get_weights().items()}
+    lr.update_from_batch(batch)
+    assert seen  # the hook ran
+    assert all(torch.equal(w0[k], v) for k, v in lr.get_weights().items())
+
+
+def _weights_equal_across(group):
+    ws = group.foreach_learner(lambda lr: {k: v.detach().cpu().numpy().copy()
+                                           for k, v in lr.module.state_dict().items()})
+    assert len(ws) == 2
+    for k in ws[0]:
+        np.testing.assert_array_equal(ws[0][k], ws[1][k], err_msg=k)
+    return ws
+
+
+def test_dqn_two_gloo_learners_identical_weights(cluster):
+    cfg = (DQNConfig().environment("CartPole-v1")
+           .env_runners(num_env_runners=0)
+           .learners(num_learners=2, num_gpus_per_learner=0)
+           .training(train_batch_size=32, num_steps_sampled_before_learning_starts=64,
+                     model={"fcnet_hiddens": [32]}, learner_backend="gloo")
+           .debugging(seed=0))
+    cfg.rollout_fragment_length = 64
+    algo = cfg.build()
+    try:
+        assert isinstance(algo.learner_group, LearnerGroup) and algo.learner_group.remote
+        w_init = algo.get_weights()
+        for _ in range(3):
+            res = algo.train()
+        assert np.isfinite(res["learners"]["loss"])
+        ws = _weights_equal_across(algo.learner_group)
+        # the learners trained (not a no-op)
+        assert any(not np.array_equal(np.asarray(w_init[k]), ws[0]["q." + k])
+                   for k in w_init)
+    finally:
+        algo.stop()
+
+
+def test_sac_two_gloo_learners_identical_weights(cluster):
+    cfg = (SACConfig().environment("Pendulum-v1")
+           .env_runners(num_env_runners=0)
+           .learners(num_learners=2, num_gpus_per_learner=0)
+           .training(train_batch_size=32, num_steps_sampled_before_learning_starts=64,
+                     model={"fcnet_hiddens": [32, 32]}, learner_backend="gloo")
+           .debugging(seed=0))
+    cfg.rollout_fragment_length = 64
+    algo = cfg.build()
+    try:
+        for _ in range(3):
+            res = algo.train()
+        assert np.isfinite(res["learners"]["critic_loss"])
+        ws = _weights_equal_across(algo.learner_group)
+        assert "log_alpha" in ws[0]
+        a = algo.compute_single_action(np.zeros(3, np.float32))
+        assert a.shape == (1,)
+    finally:
+        algo.stop()
+
+
+def test_self_play_add_module_mid_training(cluster):
+    """League / self-play: train "main", then add a frozen snapshot "main_v1" as the
+    opponent of agent 1 mid-training; only "main" keeps learning."""
+    cfg = (PPOConfig().environment("MultiAgentCartPole", env_config={"num_agents": 2})
+           .env_runners(num_env_runners=1, num_envs_per_env_runner=2)
+           .multi_agent(policies={"main"}, policy_mapping_fn=lambda aid, ep, **kw: "main")
+           .training(train_batch_size=400, minibatch_size=100, num_epochs=2, lr=1e-3,
+                     model={"fcnet_hiddens": [32]})
+           .debugging(seed=0))
+    algo = cfg.build()
+    try:
+        algo.train()
+        snap = {k: np.asarray(v).copy() for k, v in algo.get_weights()["main"].items()}
+        ids = algo.add_module(
+            "main_v1", weights=snap,
+            new_agent_to_module_mapping_fn=lambda aid, ep, **kw: "main" if aid == 0
+            else "main_v1",
+            new_should_module_be_updated=["main"])
+        assert set(ids) == {"main", "main_v1"}
+        assert algo.config.policies_to_train == ["main"]
+        for _ in range(2):
+            res = algo.train()
+        w = algo.get_weights()
+        for k, v in w["main_v1"].items():  # frozen opponent: unchanged
+            np.testing.assert_array_equal(np.asarray(v), snap[k])
+        assert any(not np.array_equal(np.asarray(w["main"][k]), snap[k]) for k in snap)
+        assert set(res["module_episode_returns_mean"]) == {"main", "main_v1"}
+        # the runner plays the snapshot with the snapshot's weights
+        got = algo.env_runner_group.foreach_env_runner(
+            lambda r: {k: v.numpy().copy() for k, v in r.modules["main_v1"].state_dict()
+                       .items()})[0]
+        for k, v in got.items():
+            np.testing.assert_array_equal(v, snap[k])
+        algo.remove_module("main_v1",
+                           new_agent_to_module_mapping_fn=lambda aid, ep, **kw: "main")
+        res = algo.train()
+        assert set(algo.get_weights()) == {"main"}
+    finally:
+        algo.stop()
