@@ -135,6 +135,9 @@ class _DeploymentScheduler:
         return best
 
 
+PROXY_TICK_S = 1.0  # per-node proxy reconciliation period (EveryNode)
+
+
 class ServeController:
     def __init__(self, http_options=None):
         self.apps = {}  # app name -> {"route_prefix", "ingress", "deployments", "status"}
@@ -549,6 +552,67 @@ class ServeController:
                 else:
                     st.over_since = st.under_since = None
 
+    # ------------------------------------------------------------------ per-node proxies
+    def _proxy_tick(self, now):
+        """ProxyLocation.EveryNode (reference: serve/_private/proxy_state.py:533,608
+        ProxyStateManager.update): one HTTP proxy per alive node, pinned to it by a hard
+        node-affinity strategy, started when a node joins and dropped when it dies. The
+        head node's proxy is the one serve.start() created ("SERVE_PROXY"). Proxies of
+        nodes that share the head's address (a one-machine cluster) listen on port + i so
+        they do not collide; ``get_proxies`` reports every node's (host, port)."""
+        opts = self.http_options or {}
+        if opts.get("location") != "EveryNode" or self.proxy is None:
+            return
+        if now - getattr(self, "_proxy_checked", 0.0) < PROXY_TICK_S:
+            return
+        self._proxy_checked = now
+        nodes = {n["NodeID"]: n for n in ray.nodes() if n.get("Alive")}
+        head = next((nid for nid, n in nodes.items() if n.get("is_head_node")), None)
+        head_addr = nodes[head]["NodeManagerAddress"] if head in nodes else "127.0.0.1"
+        table = self.__dict__.setdefault("node_proxies", {})
+        if head is not None and head not in table:
+            table[head] = (self.proxy, opts.get("host", "127.0.0.1"), opts.get("port", 8000))
+        for nid in [nid for nid in table if nid not in nodes]:  # node died / left
+            actor = table.pop(nid)[0]
+            if actor is not self.proxy:
+                try:
+                    ray.kill(actor)
+                except Exception:  # noqa: BLE001
+                    pass
+        from ray_amd.serve._proxy import HTTPProxy
+        from ray_amd.util.scheduling_strategies import NodeAffinitySchedulingStrategy
+
+        for nid, n in nodes.items():
+            if nid in table:
+                continue
+            shared = n.get("NodeManagerAddress") == head_addr
+            used = {port for _, _, port in table.values()}
+            port = int(opts.get("port", 8000))
+            while shared and port in used:
+                port += 1
+            host = opts.get("host", "127.0.0.1")
+            actor = ray.remote(HTTPProxy).options(
+                num_cpus=0, max_concurrency=1000, name=f"SERVE_PROXY:{nid}",
+                namespace=SERVE_NAMESPACE, lifetime="detached",
+                scheduling_strategy=NodeAffinitySchedulingStrategy(nid, soft=False)).remote(
+                host, port, opts.get("request_timeout_s"))
+            table[nid] = (actor, host, port)
+
+    async def get_proxies(self):
+        """{node_id: {"host", "port", "ready"}} of the running HTTP proxies."""
+        out = {}
+        for nid, (actor, host, port) in list(self.__dict__.get("node_proxies", {}).items()):
+            try:
+                ok = await asyncio.wait_for(actor.ping.remote(), 5.0) == "ok"
+            except Exception:  # noqa: BLE001
+                ok = False
+            out[nid] = {"host": host, "port": port, "ready": ok}
+        if not out and self.proxy is not None:
+            o = self.http_options or {}
+            out["head"] = {"host": o.get("host", "127.0.0.1"), "port": o.get("port", 8000),
+                           "ready": True}
+        return out
+
     async def _control_loop(self):
         while True:
             try:
@@ -557,6 +621,7 @@ class ServeController:
                 self._autoscale(now)
                 self._reconcile()
                 self._health_tick(now)
+                self._proxy_tick(now)
             except Exception:  # noqa: BLE001
                 import traceback
 
@@ -635,6 +700,12 @@ class ServeController:
     async def shutdown(self):
         for name in list(self.apps):
             await self.delete_application(name)
+        for actor, _, _ in list(self.__dict__.get("node_proxies", {}).values()):
+            if actor is not self.proxy:
+                try:
+                    ray.kill(actor)
+                except Exception:  # noqa: BLE001
+                    pass
         for p in (self.proxy, self.grpc_proxy):
             if p is not None:
                 try:

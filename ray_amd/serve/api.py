@@ -68,6 +68,9 @@ def start(http_options=None, detached: bool = True, **kw):
     opts = http_options or {}
     port = opts.get("port", 8000)
     existing = ray.get(c.get_proxy.remote())
+    if existing is not None and opts and opts != ray.get(c.get_http_options.remote()) and \
+            opts.get("location") == "EveryNode":
+        ray.get(c.set_proxy.remote(existing, opts))  # switch an existing head proxy's mode
     if existing is None and opts.get("location", "HeadOnly") != "NoServer":
         from ray_amd.serve._proxy import HTTPProxy
 

@@ -98,8 +98,9 @@ class DeploymentMode(str, Enum):
 
 
 class ProxyLocation(str, Enum):
-    """Where HTTP/gRPC proxies run. This runtime starts one proxy on the head node, so
-    ``EveryNode`` and ``HeadOnly`` both mean that proxy; ``Disabled`` starts none."""
+    """Where HTTP proxies run: ``HeadOnly`` one on the head node, ``EveryNode`` one per
+    alive node (started / stopped by the controller as nodes join and leave),
+    ``Disabled`` none."""
     Disabled = "Disabled"
     HeadOnly = "HeadOnly"
     EveryNode = "EveryNode"

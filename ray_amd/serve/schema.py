@@ -224,8 +224,9 @@ def deploy_config(config) -> Dict[str, Any]:
         config = ServeDeploySchema(**config)
     ho = config.http_options
     http = HTTPOptions(host=ho.host, port=ho.port, root_path=ho.root_path,
-                       location="NoServer" if config.proxy_location == ProxyLocation.Disabled
-                       else "HeadOnly")
+                       location={ProxyLocation.Disabled: "NoServer",
+                                 ProxyLocation.EveryNode: "EveryNode"}.get(
+                           ProxyLocation(config.proxy_location), "HeadOnly"))
     grpc = None
     if config.grpc_options.grpc_servicer_functions:
         grpc = {"port": config.grpc_options.port,

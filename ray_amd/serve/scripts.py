@@ -80,8 +80,9 @@ def cmd_start(a):
     from ray_amd.serve.api import HTTPOptions
 
     serve.start(http_options=HTTPOptions(host=a.http_host, port=a.http_port,
-                                         location="NoServer" if a.proxy_location ==
-                                         "Disabled" else "HeadOnly"))
+                                         location={"Disabled": "NoServer",
+                                                   "EveryNode": "EveryNode"}.get(
+                                             a.proxy_location, "HeadOnly")))
     print(f"Serve started (HTTP {a.http_host}:{a.http_port}).")
     return 0
 
