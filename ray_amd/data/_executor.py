@@ -132,6 +132,16 @@ class Plan:
         self._cache = None  # materialized (refs, metas)
         self.last_stats = None
 
+    def num_blocks_hint(self):
+        """Upstream block count known without executing anything (read tasks, given refs,
+        a materialized cache), or None. Stages may split blocks, so it is a hint."""
+        if self._cache is not None:
+            return len(self._cache[0])
+        kind, val = self.source[0], self.source[1]
+        if kind in ("read", "refs") and isinstance(val, (list, tuple)):
+            return len(val)
+        return None
+
     def with_stage(self, st: Stage) -> "Plan":
         stages = list(self.stages)
         if stages and stages[-1].fusable_with(st):

@@ -600,7 +600,18 @@ class Dataset:
             push = bool(getattr(ctx, "use_push_based_shuffle", False))
             mf = max(2, int(getattr(ctx, "push_based_shuffle_merge_factor", 8)))
             plist, merged, i = [], [], 0
-            for r, _m in X.execute(parent._plan):
+            nonlocal n_out
+            upstream = X.execute(parent._plan)
+            if n_out is None:
+                # output blocks = upstream blocks, decided now (at execution), not when the
+                # shuffle was declared: from the plan when it knows, else after the
+                # upstream block refs are in (the data stays in the object store)
+                hint = parent._plan.num_blocks_hint()
+                if hint is None:
+                    upstream = list(upstream)
+                    hint = len(upstream)
+                n_out = max(1, hint)
+            for r, _m in upstream:
                 plist.append(_partition(r, n_out, mode, key, boundaries,
                                         None if seed is None else seed + i, descending))
                 i += 1
@@ -622,8 +633,9 @@ class Dataset:
         return Dataset(X.Plan(("stream", stream)))
 
     def random_shuffle(self, *, seed=None, num_blocks=None, **kw) -> "Dataset":
-        n = num_blocks or max(1, len(self._blocks()[0]))
-        return self._shuffle(n, "random", seed=seed if seed is not None else
+        """Lazy: nothing upstream runs until the shuffled dataset is consumed; without
+        ``num_blocks`` the output has as many blocks as the upstream (decided then)."""
+        return self._shuffle(num_blocks or None, "random", seed=seed if seed is not None else
                              int(time.time_ns() % (1 << 31)))
 
     def repartition(self, num_blocks: int, *, shuffle: bool = False, **kw) -> "Dataset":

@@ -90,3 +90,28 @@ def test_shuffle_and_sort_push_based(cluster, push):
         assert [r["id"] for r in srt.take_all()] == list(range(1999, -1, -1))
     finally:
         ctx.use_push_based_shuffle, ctx.push_based_shuffle_merge_factor = old
+
+
+def test_random_shuffle_is_lazy(cluster, tmp_path):
+    """random_shuffle() without num_blocks runs nothing upstream until consumption (the
+    block count is decided at execution), for a plan that knows its block count (read
+    tasks) and for one that does not (a streamed union)."""
+    marker = tmp_path / "ran"
+
+    def touch(batch):
+        marker.write_text("x")
+        return batch
+
+    ds = ray.data.range(1000, override_num_blocks=8).map_batches(touch)
+    sh = ds.random_shuffle(seed=3)
+    import time
+
+    time.sleep(0.5)
+    assert not marker.exists()  # declared, not executed
+    rows = [r["id"] for r in sh.iter_rows()]
+    assert marker.exists() and sorted(rows) == list(range(1000))
+    assert rows != list(range(1000))
+    assert sh.materialize().num_blocks() == 8
+    u = ray.data.range(10, override_num_blocks=2).union(ray.data.range(10, override_num_blocks=3))
+    su = u.random_shuffle(seed=1)
+    assert sorted(r["id"] for r in su.iter_rows()) == sorted(list(range(10)) * 2)
