@@ -43,6 +43,10 @@ _SIGS = {
     "ra_wgrad": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p,
                  c_void_p, c_int, c_void_p],
     "ra_wgrad_splits": [c_int, c_int, c_int],
+    "ra_wgrad_group": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "ra_wgrad_group_ws_bytes": [c_int, c_int],
+    "ra_wgrad_group_splits": [c_int, c_int],
     "ra_bias_residual": [c_void_p] * 4 + [c_long, c_int, c_void_p],
     "ra_xent_fwd": [c_void_p] * 4 + [c_int, c_int, c_int, c_long, c_void_p],
     "ra_xent_bwd": [c_void_p] * 4 + [c_float, c_void_p, c_int, c_int, c_int, c_long, c_void_p],
@@ -141,6 +145,9 @@ _SIGS = {
 }
 
 
+_LONG_RET = {"ra_wgrad_group_ws_bytes"}
+
+
 class HipKernelError(RuntimeError):
     pass
 
@@ -169,7 +176,7 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = c_long if name.endswith("_work") else c_int
+            f.restype = c_long if name.endswith("_work") or name in _LONG_RET else c_int
         # RAY_AMD_KNOBS="11=0,12=1": kernel variant knobs (A/B runs without code edits)
         for kv in filter(None, os.environ.get("RAY_AMD_KNOBS", "").split(",")):
             k, v = kv.split("=")

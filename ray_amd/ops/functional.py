@@ -371,6 +371,91 @@ def wgrad_accumulate(dy2, x2, sink, bias_sink=None, accumulate=True):
             bias_sink.copy_(bias_sink.float() + dt.sum(0))
 
 
+# Grouped weight gradients (RAY_AMD_WGRAD_GROUP=1, default): the hip wgrads of a layer's
+# linears are queued and launched together once their 256x256 tiles reach
+# RAY_AMD_WGRAD_GROUP_TILES (GPT-2 small: mlp_proj 36 + fc 36 + proj 9 + qkv 27 = 108 ->
+# one launch per layer after qkv's backward) as ONE kernel with the split-K reduction
+# inside (ra_wgrad_group: S = 2 at 108 tiles, 27 MB of fp32 slabs per layer instead of the
+# per-linear S = 7..28 slabs and the separate ra_splitk_accum pass). DDP readiness of the
+# queued weights (and fused biases) is signalled at the launch.
+_WGRAD_GROUP = os.environ.get("RAY_AMD_WGRAD_GROUP", "1") == "1"
+_WGRAD_GROUP_TILES = int(os.environ.get("RAY_AMD_WGRAD_GROUP_TILES", "96"))
+_pending_wg: dict = {}  # device -> {"items": [...], "tiles": int, "M": int}
+
+
+def _wg_tiles(N, K):
+    return ((N + 255) // 256) * ((K + 255) // 256)
+
+
+def _queue_wgrad(dy2, x2, w, sink, bias=None, bias_sink=None):
+    dev = dy2.device
+    M, N = dy2.shape
+    K = x2.shape[1]
+    q = _pending_wg.get(dev)
+    if q is not None and (q["M"] != M or len(q["items"]) >= 8):
+        flush_wgrads(dev)
+        q = None
+    if q is None:
+        q = _pending_wg[dev] = {"items": [], "tiles": 0, "M": M}
+    # autograd's AccumulateGrad post-hook fires for these parameters (with a None grad) as
+    # soon as this backward returns: the pending mark keeps a DDP bucket hook from counting
+    # them ready before the grouped kernel that writes their gradients is enqueued
+    w._ra_grad_pending = True
+    if bias_sink is not None:
+        bias._ra_grad_pending = True
+    q["items"].append((dy2, x2, w, sink, bias, bias_sink))
+    q["tiles"] += _wg_tiles(N, K)
+    if q["tiles"] >= _WGRAD_GROUP_TILES or len(q["items"]) >= 8:
+        flush_wgrads(dev)
+
+
+def flush_wgrads(device=None):
+    """Launch every queued weight gradient (on the side stream, after the current stream's
+    work that produced their inputs) and signal their DDP readiness."""
+    import ctypes
+
+    devs = [device] if device is not None else list(_pending_wg)
+    for dev in devs:
+        q = _pending_wg.pop(dev, None)
+        if not q or not q["items"]:
+            continue
+        items = q["items"]
+        n = len(items)
+        M = q["M"]
+        L = _lib.lib()
+        side = _side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            P = ctypes.c_void_p * n
+            I = ctypes.c_int * n
+            Lg = ctypes.c_long * n
+            dys = P(*[it[0].data_ptr() for it in items])
+            xs = P(*[it[1].data_ptr() for it in items])
+            ldy = Lg(*[it[0].stride(0) for it in items])
+            ldx = Lg(*[it[1].stride(0) for it in items])
+            sinks = P(*[it[3].data_ptr() for it in items])
+            bsinks = P(*[it[5].data_ptr() if it[5] is not None else None for it in items])
+            Ns = I(*[it[0].shape[1] for it in items])
+            Ks = I(*[it[1].shape[1] for it in items])
+            fl = I(*[(1 if it[3].dtype == torch.bfloat16 else 0) | 2 |
+                     (4 if it[5] is not None else 0) for it in items])
+            tiles = q["tiles"]
+            S = L.ra_wgrad_group_splits(M, tiles)
+            ws = torch.empty((L.ra_wgrad_group_ws_bytes(tiles, S) + 3) // 4, device=dev,
+                             dtype=torch.float32)
+            check(L.ra_wgrad_group(n, dys, ldy, xs, ldx, sinks, bsinks, Ns, Ks, fl, M, S,
+                                   ptr(ws), stream_ptr()), "wgrad_group")
+            for it in items:
+                it[0].record_stream(side)
+                it[1].record_stream(side)
+        for it in items:
+            it[2]._ra_grad_pending = False
+            _grad_done(it[2])
+            if it[5] is not None:
+                it[4]._ra_grad_pending = False
+                _grad_done(it[4])
+
+
 def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, bias=None, bias_sink=None):
     """sink += dy2^T x2 (fp32 or bf16 flat-gradient view), then signal DDP readiness. With
     ``bias_sink`` (hip path only) the bias gradient is fused into the same kernel."""
@@ -419,7 +504,10 @@ def _side_stream2(device):
 
 def join_side_streams():
     """Make the current stream wait for weight-gradient work queued on side streams (call
-    before consuming the flat gradients: optimizer step, collective)."""
+    before consuming the flat gradients: optimizer step, collective); grouped weight
+    gradients still queued are launched first."""
+    if _pending_wg:
+        flush_wgrads()
     for dev, st in _side.items():
         torch.cuda.current_stream(dev).wait_stream(st)
 
@@ -527,7 +615,11 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             S = _splitk(M, N, K)
-            if sink is not None and _WGRAD_STREAM and dy2.is_cuda:
+            if sink is not None and _WGRAD_STREAM and dy2.is_cuda and _WGRAD == "hip" and \
+                    _WGRAD_GROUP and M % 64 == 0 and _wgrad_hip_ok(dy2, x2, sink, bsink):
+                # queued: launched with the layer's other linears as one grouped kernel
+                _queue_wgrad(dy2, x2, w, sink, ctx.b, bsink)
+            elif sink is not None and _WGRAD_STREAM and dy2.is_cuda:
                 # weight gradient on the side stream: it overlaps the memory-bound kernels
                 # of the dX chain that continues on the main stream
                 side = _side_stream(dy2.device)

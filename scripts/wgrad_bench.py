@@ -76,6 +76,51 @@ def main():
             res[arm + "_tflops"] = round(flop / best / 1e9, 1)
         out[name] = res
         print(name, json.dumps(res), flush=True)
+    # one GPT-2 layer as ONE grouped launch (in-kernel split-K reduction) vs the four
+    # per-linear hip launches (+ their slab reductions)
+    import ctypes
+
+    torch.manual_seed(0)
+    prob = []
+    for name, (M, N, K) in SHAPES.items():
+        prob.append(((torch.rand(M, N, device=dev) * 2 - 1).bfloat16(),
+                     (torch.rand(M, K, device=dev) * 2 - 1).bfloat16(),
+                     torch.zeros(N, K, device=dev)))
+    n = len(prob)
+    M = 65536
+    tiles = sum(((d.shape[1] + 255) // 256) * ((x.shape[1] + 255) // 256) for d, x, _ in prob)
+    S = L.ra_wgrad_group_splits(M, tiles)
+    ws = torch.empty((L.ra_wgrad_group_ws_bytes(tiles, S) + 3) // 4, device=dev)
+    P, I, Lg = ctypes.c_void_p * n, ctypes.c_int * n, ctypes.c_long * n
+    gargs = (n, P(*[ptr(d) for d, _, _ in prob]), Lg(*[d.stride(0) for d, _, _ in prob]),
+            P(*[ptr(x) for _, x, _ in prob]), Lg(*[x.stride(0) for _, x, _ in prob]),
+            P(*[ptr(s) for _, _, s in prob]), P(*[None] * n),
+            I(*[d.shape[1] for d, _, _ in prob]), I(*[x.shape[1] for _, x, _ in prob]),
+            I(*[2] * n), M, S, ptr(ws))
+
+    def grouped():
+        L.ra_wgrad_group(*gargs, stream_ptr())
+
+    def per_linear():
+        for d, x, s_ in prob:
+            rf.wgrad_accumulate(d, x, s_)
+
+    for _, _, s_ in prob:
+        s_.zero_()
+    grouped()
+    torch.cuda.synchronize()
+    errs = [((s_ - d.float().t() @ x.float()).norm() / (d.float().t() @ x.float()).norm()).item()
+            for d, x, s_ in prob]
+    g_ms, p_ms = [], []
+    for r in range(args.rounds):
+        g_ms.append(round(timeit(grouped), 4))
+        p_ms.append(round(timeit(per_linear), 4))
+    flop = sum(2.0 * M * d.shape[1] * x.shape[1] for d, x, _ in prob)
+    print("layer_group", json.dumps({"S": S, "tiles": tiles, "rel_err_max": max(errs),
+                                      "grouped_ms": g_ms, "per_linear_ms": p_ms,
+                                      "grouped_tflops": round(flop / min(g_ms) / 1e9, 1),
+                                      "per_linear_tflops": round(flop / min(p_ms) / 1e9, 1)}),
+          flush=True)
     tot_h = sum(min(v["hip"]) for v in out.values())
     tot_b = sum(min(v["hipblaslt"]) for v in out.values())
     print(json.dumps({"per_layer_ms_hip": round(tot_h, 4), "per_layer_ms_hipblaslt": round(tot_b, 4),

@@ -819,3 +819,87 @@ def test_linear_hip_wgrad_fused_bias_into_flat_sinks(cuda_device, monkeypatch):
     assert _rel(w._ra_grad, wr.grad) < 5e-3
     assert _rel(b._ra_grad, br.grad) < 5e-3
     assert _rel(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 4])
+def test_wgrad_group_kernel_matches_fp32(cuda_device, S):
+    """ra_wgrad_group: a layer's linears (ragged shapes, fp32 + bf16 sinks, fused bias)
+    in one launch with the split-K reduction inside the kernel (arrival tickets, slabs,
+    release / acquire); repeated launches reuse the workspace (stale-cache check)."""
+    import ctypes
+
+    from ray_amd.ops._lib import ptr, stream_ptr
+
+    torch.manual_seed(31)
+    M = 64 * 37
+    shapes = [(2304, 768, True, torch.float32), (264, 136, True, torch.float32),
+              (768, 3072, False, torch.float32), (72, 40, True, torch.bfloat16)]
+    dys = [torch.randn(M, n, device=cuda_device).bfloat16() for n, _, _, _ in shapes]
+    xs = [torch.randn(M, k, device=cuda_device).bfloat16() for _, k, _, _ in shapes]
+    L = _lib.lib()
+    n = len(shapes)
+    tiles = sum(((a + 255) // 256) * ((b + 255) // 256) for a, b, _, _ in shapes)
+    ws = torch.empty((L.ra_wgrad_group_ws_bytes(tiles, S) + 3) // 4, device=cuda_device)
+    for rep in range(3):
+        sinks = [torch.randn(a, b, device=cuda_device).to(dt) for a, b, _, dt in shapes]
+        bsinks = [torch.randn(a, device=cuda_device).to(dt) if bias else None
+                  for a, _, bias, dt in shapes]
+        refs = [s.float() + d.float().t() @ x.float() for s, d, x in zip(sinks, dys, xs)]
+        brefs = [b.float() + d.float().sum(0) if b is not None else None
+                 for b, d in zip(bsinks, dys)]
+        P, I, Lg = ctypes.c_void_p * n, ctypes.c_int * n, ctypes.c_long * n
+        rc = L.ra_wgrad_group(
+            n, P(*[ptr(d) for d in dys]), Lg(*[d.stride(0) for d in dys]),
+            P(*[ptr(x) for x in xs]), Lg(*[x.stride(0) for x in xs]),
+            P(*[ptr(s) for s in sinks]), P(*[ptr(b) for b in bsinks]),
+            I(*[a for a, _, _, _ in shapes]), I(*[b for _, b, _, _ in shapes]),
+            I(*[(1 if dt == torch.bfloat16 else 0) | 2 | (4 if bias else 0)
+                for _, _, bias, dt in shapes]), M, S, ptr(ws), stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+        for s_, r, (_, _, _, dt) in zip(sinks, refs, shapes):
+            assert _rel(s_, r) < (2e-3 if dt == torch.float32 else 1e-2), rep
+        for b, r, (_, _, _, dt) in zip(bsinks, brefs, shapes):
+            if b is not None:
+                assert _rel(b, r) < (2e-3 if dt == torch.float32 else 1e-2), rep
+
+
+def test_linear_grouped_wgrad_matches_ungrouped(cuda_device, monkeypatch):
+    """Four linears' weight (and bias) gradients queued and launched as one grouped kernel
+    equal the per-linear hip path; readiness is signalled only at the flush."""
+    monkeypatch.setattr(rf, "_WGRAD", "hip")
+    torch.manual_seed(32)
+    M = 1024
+    dims = [(768, 2304, True), (768, 768, False), (768, 3072, False), (3072, 768, False)]
+
+    def run(group: bool):
+        monkeypatch.setattr(rf, "_WGRAD_GROUP", group)
+        torch.manual_seed(33)
+        ws, flats, done = [], [], []
+        x = torch.randn(M, 768, device=cuda_device).bfloat16()
+        outs = []
+        for kin, kout, bias in dims:
+            w = (0.02 * torch.randn(kout, kin, device=cuda_device)).bfloat16().requires_grad_()
+            b = torch.zeros(kout, device=cuda_device).bfloat16().requires_grad_() if bias \
+                else None
+            flat = torch.zeros(kout * kin + kout, device=cuda_device)
+            w._ra_grad, w._ra_direct_grad = flat[:kout * kin].view(kout, kin), True
+            w._ra_grad_ready = lambda w=w: done.append(id(w))
+            if b is not None:
+                b._ra_grad, b._ra_direct_grad = flat[kout * kin:], True
+                b._ra_grad_ready = lambda b=b: done.append(id(b))
+            xin = torch.randn(M, kin, device=cuda_device).bfloat16().requires_grad_()
+            outs.append(rf.linear(xin, w, b))
+            flats.append(flat)
+        loss = sum((o.float() ** 2).mean() for o in outs)
+        loss.backward()
+        n_before = len(done)
+        rf.join_side_streams()  # flushes anything still queued
+        torch.cuda.synchronize()
+        return [f.clone() for f in flats], n_before, len(done)
+
+    g_flats, g_before, g_after = run(True)
+    u_flats, _, u_after = run(False)
+    for a, b in zip(g_flats, u_flats):
+        assert _rel(a, b) < 1e-5
+    assert g_after == u_after == 5  # 4 weights + 1 fused bias signalled
