@@ -8,6 +8,12 @@ whole: ``StorePinCache`` registers the fixed 64 MiB chunks that a copy touches, 
 registered (blocks are recycled through the same heap regions by the streaming executor)
 and unregisters the least recently used chunks beyond a byte cap.
 
+The copy is asynchronous, so two things must outlive it: the chunk registration (an
+unregister under an in-flight DMA would fault or fall back mid-copy) and the store object
+the numpy view points into (a released block is recycled by the next ``put``). Every copy
+records a HIP event; the chunks it touched remember that event and an eviction waits on it
+first, and the source array is held in a pending list until its event has completed.
+
 Enabled in the Ray Data GPU preprocessing actors with ``RAY_AMD_DATA_PIN_STORE=1``
 (reference config 4, "pinned async H2D"; ``ray_amd/data/preprocessors.py``).
 """
@@ -29,6 +35,8 @@ class StorePinCache:
         self._lock = threading.Lock()
         self.registered_bytes = 0
         self.failures = 0
+        self._last_use = {}  # chunk index -> event of the latest copy that read it
+        self._pending = collections.deque()  # (event, source array) of in-flight copies
 
     def _L(self):
         if self._lib is None:
@@ -67,9 +75,32 @@ class StorePinCache:
                     self._chunks[c] = length
                     self._chunks.move_to_end(c, last=False)
                     break
+                ev = self._last_use.pop(c, None)
+                if ev is not None:
+                    ev.synchronize()  # a copy still reading this chunk finishes first
                 self._L().ra_host_unregister(self.base + c * CHUNK)
                 self.registered_bytes -= length
             return ok
+
+    def track(self, ptr: int, n: int, event, src) -> None:
+        """Record that an async copy of [ptr, ptr + n) completes at ``event``: the chunks it
+        read stay registered and ``src`` stays referenced until then."""
+        with self._lock:
+            if n > 0 and self.covers(ptr, n):
+                for c in range((ptr - self.base) // CHUNK,
+                               (ptr + n - 1 - self.base) // CHUNK + 1):
+                    if c in self._chunks:
+                        self._last_use[c] = event
+            self._pending.append((event, src))
+            while self._pending and self._pending[0][0].query():
+                self._pending.popleft()
+
+    def drain(self) -> None:
+        """Wait for every tracked copy (tests, shutdown)."""
+        with self._lock:
+            while self._pending:
+                self._pending.popleft()[0].synchronize()
+            self._last_use.clear()
 
 
 _cache = None
@@ -101,6 +132,11 @@ def to_device_pinned(arr, device):
 
     t = torch.from_numpy(arr)
     c = store_pin_cache()
-    if c is not None:
-        c.ensure(arr.__array_interface__["data"][0], arr.nbytes)
-    return t.to(device, non_blocking=True)
+    ptr = arr.__array_interface__["data"][0]
+    if c is None or not c.ensure(ptr, arr.nbytes):
+        return t.to(device)  # pageable: the runtime stages it and the call returns done
+    out = t.to(device, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(out.device))
+    c.track(ptr, arr.nbytes, ev, arr)
+    return out

@@ -19,6 +19,7 @@ import os
 import signal
 import subprocess
 import sys
+import threading
 import time
 import traceback
 
@@ -299,6 +300,7 @@ class Raylet:
         self._gcs_path = os.environ.get("RAY_AMD_GCS_STORAGE_PATH") if args.head else None
         self._gcs_dirty = False
         self._gcs_saved = 0.0
+        self._gcs_writer = None
         self.gcs_restored = None
         if self._gcs_path:
             os.makedirs(self._gcs_path, exist_ok=True)
@@ -912,6 +914,8 @@ class Raylet:
         return os.path.join(self._gcs_path, "gcs_snapshot.pkl")
 
     def _gcs_snapshot(self):
+        """A copy of the durable tables, taken on the loop thread (values the loop mutates
+        later — job records — are copied; KV values are immutable bytes)."""
         actors = [{"info": a.info, "spec": a.spec, "restarts": a.restarts}
                   for a in self.actors.values()
                   if a.info.get("lifetime") == "detached" and a.state != P.DEAD]
@@ -919,22 +923,42 @@ class Raylet:
                 "name": pg.name, "lifetime": pg.lifetime, "namespace": pg.namespace}
                for pg in self.pgs.values()
                if pg.lifetime == "detached" and pg.state != "REMOVED"]
-        return {"version": 1, "kv": dict(self.kv), "jobs": dict(self.jobs),
+        return {"version": 1, "kv": dict(self.kv),
+                "jobs": {k: dict(v) for k, v in self.jobs.items()},
                 "job_counter": self.job_counter, "actors": actors, "pgs": pgs,
                 "saved_at": time.time()}
 
-    def _gcs_save(self):
+    def _gcs_write(self, snap):
         import pickle
 
         tmp = self._gcs_file() + f".tmp{os.getpid()}"
         try:
             with open(tmp, "wb") as f:
-                pickle.dump(self._gcs_snapshot(), f, protocol=5)
+                pickle.dump(snap, f, protocol=5)
             os.replace(tmp, self._gcs_file())
         except Exception:  # noqa: BLE001
             traceback.print_exc()
+
+    def _gcs_save(self, sync=False):
+        """Persist the snapshot. The loop thread only copies the tables; pickling and the
+        file write run on a background writer (one at a time: while one is in flight the
+        tables stay dirty and the next tick saves again), so a large KV — Serve checkpoints,
+        runtime_env packages — does not stall the head's control loop. ``sync`` (shutdown)
+        waits for an in-flight writer and writes inline."""
+        w = self._gcs_writer
+        if w is not None and w.is_alive():
+            if not sync:
+                return
+            w.join()
+        snap = self._gcs_snapshot()
         self._gcs_dirty = False
         self._gcs_saved = time.monotonic()
+        if sync:
+            self._gcs_write(snap)
+            return
+        self._gcs_writer = threading.Thread(target=self._gcs_write, args=(snap,),
+                                            name="gcs-snapshot", daemon=True)
+        self._gcs_writer.start()
 
     def _gcs_restore(self):
         import pickle
@@ -963,9 +987,18 @@ class Raylet:
                 self.pg_names[(pg.namespace, pg.name)] = pg.pg_id
         for d in st.get("actors") or []:
             a = ActorRec(d["info"], d["spec"])
-            a.restarts = int(d.get("restarts") or 0) + 1
-            a.state = P.RESTARTING
+            a.restarts = int(d.get("restarts") or 0)
             self.actors[a.aid] = a
+            # the head restart killed the actor's process: that is a restart like any
+            # other, so an actor that has used its max_restarts stays dead
+            if a.max_restarts != -1 and a.restarts >= a.max_restarts:
+                a.state = P.DEAD
+                a.death = ("The actor died with the head node and has no restarts left "
+                           f"(max_restarts={a.max_restarts}).")
+                a.end_time = now
+                continue
+            a.restarts += 1
+            a.state = P.RESTARTING
             if a.info.get("name"):
                 self.named[(a.info.get("namespace"), a.info["name"])] = a.aid
             self._schedule_actor(a)
@@ -1631,7 +1664,7 @@ class Raylet:
 
     def shutdown(self):
         if self._gcs_path:
-            self._gcs_save()
+            self._gcs_save(sync=True)
         for w in list(self.workers.values()) + list(self.starting.values()):
             if w.mode != "driver":
                 self._kill_worker(w)

@@ -274,6 +274,38 @@ RA_EXPORT void ra_lt_allow_streamk(int on) {
   g_allow_sk = on != 0;
 }
 
+// Drop the handle and workspace cached for a stream that is about to be destroyed (the
+// capture stream of a graph, a per-chunk stream, a data actor's stream): without it each
+// short-lived stream that ran an lt GEMM keeps a handle and kWs bytes of HBM, and a later
+// stream allocated at the same address would silently reuse the stale entry. Work queued on
+// the stream is drained first (the workspace may still be read). Returns the entries freed.
+RA_EXPORT int ra_lt_release_stream(void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  int freed = 0;
+  auto w = g_ws_by_stream.find(st);
+  auto h = g_handle_by_stream.find(st);
+  if (w == g_ws_by_stream.end() && h == g_handle_by_stream.end()) return 0;
+  hipStreamSynchronize(st);
+  if (w != g_ws_by_stream.end()) {
+    hipFree(w->second);
+    g_ws_by_stream.erase(w);
+    ++freed;
+  }
+  if (h != g_handle_by_stream.end()) {
+    if (h->second != g_handle) hipblasLtDestroy(h->second);
+    g_handle_by_stream.erase(h);
+    ++freed;
+  }
+  return freed;
+}
+
+RA_EXPORT int ra_lt_num_streams() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  return (int)(g_ws_by_stream.size() > g_handle_by_stream.size() ? g_ws_by_stream.size()
+                                                                   : g_handle_by_stream.size());
+}
+
 // ----------------------------------------------------------------- epilogue GEMMs
 // D (bf16) = epilogue(op(A) * op(B)) for the fused MLP: GELU_AUX_BIAS (forward: D = gelu(AB +
 // bias), aux = AB + bias) and DGELU_BGRAD (backward: D = AB * gelu'(aux), bias = colsum(D)).

@@ -43,6 +43,8 @@
 // (release/air_tests/air_benchmarks/workloads/torch_benchmark.py:81).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16x8w_t __attribute__((ext_vector_type(8)));
@@ -609,8 +611,15 @@ RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
         g_cus_w <= 0)
       g_cus_w = 256;
   }
+  // RAY_AMD_WGRAD_WAVES=w: w waves of workgroups (shorter-lived workgroups, so a main-stream
+  // kernel launched meanwhile gets CUs sooner; more fp32 slab traffic)
+  static const int waves = [] {
+    const char* e = getenv("RAY_AMD_WGRAD_WAVES");
+    const int w = e ? atoi(e) : 1;
+    return w < 1 ? 1 : (w > 8 ? 8 : w);
+  }();
   const int tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-  int S = g_cus_w / tiles;
+  int S = waves * g_cus_w / tiles;
   const int nks = M / kT;
   if (S > nks) S = nks;
   if (S < 1) S = 1;

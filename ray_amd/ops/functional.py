@@ -311,11 +311,20 @@ _WGRAD_TILES = int(os.environ.get("RAY_AMD_WGRAD_TILES", "0"))
 _WGRAD_PART_BYTES = int(float(os.environ.get("RAY_AMD_WGRAD_PART_MB", "4096")) * (1 << 20))
 
 
+def _on_side_stream(t) -> bool:
+    st = _side.get(t.device)
+    return st is not None and torch.cuda.current_stream(t.device) == st
+
+
 def _wgrad_partials(dy2, x2, S, M, N, K):
-    if _WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous():
+    """fp32 split-K partials [S, N, K]. On the wgrad side stream they always come from
+    ops/lt (a per-stream hipBLASLt handle): torch.bmm would share torch's one handle with
+    the main stream's dX GEMM, the concurrent stream-K setup that hung in round 4."""
+    side = dy2.is_cuda and _on_side_stream(dy2)
+    if (_WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous()) or side:
         from . import lt
 
-        return lt.wgrad_partials(dy2, x2, S)
+        return lt.wgrad_partials(dy2.contiguous(), x2.contiguous(), S)
     return torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K),
                      out_dtype=torch.float32)
 
@@ -377,8 +386,11 @@ def wgrad_accumulate(dy2, x2, sink, bias_sink=None, accumulate=True):
 # one launch per layer after qkv's backward) as ONE kernel with the split-K reduction
 # inside (ra_wgrad_group: S = 2 at 108 tiles, 27 MB of fp32 slabs per layer instead of the
 # per-linear S = 7..28 slabs and the separate ra_splitk_accum pass). DDP readiness of the
-# queued weights (and fused biases) is signalled at the launch.
-_WGRAD_GROUP = os.environ.get("RAY_AMD_WGRAD_GROUP", "1") == "1"
+# queued weights (and fused biases) is signalled at the launch. Opt-in (=1): measured on
+# MI355X (profiles/r5/r5e) the layer's one 1.1 ms launch lands on the next layer's fc2
+# dgrad GEMM, a persistent 256-workgroup hipBLASLt kernel that then takes 1.17 ms instead
+# of 0.23 ms; the step is 65.1 ms grouped vs 64.8 ms per-linear.
+_WGRAD_GROUP = os.environ.get("RAY_AMD_WGRAD_GROUP", "0") == "1"
 _WGRAD_GROUP_TILES = int(os.environ.get("RAY_AMD_WGRAD_GROUP_TILES", "96"))
 _pending_wg: dict = {}  # device -> {"items": [...], "tiles": int, "M": int}
 

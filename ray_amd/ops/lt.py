@@ -174,3 +174,15 @@ def wgrad_accum(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor, beta: fl
     assert x2.shape[0] == M and out.shape == (N, K) and out.dtype == torch.float32
     assert dy2.stride(1) == 1 and x2.stride(1) == 1 and out.is_contiguous()
     gemm_f32(0, 1, K, N, M, x2, x2.stride(0), dy2, dy2.stride(0), out, K, alpha, beta)
+
+
+def release_stream(stream) -> int:
+    """Free the hipBLASLt handle and workspace cached for ``stream`` (ra_lt_release_stream).
+    Owners of short-lived streams call it once no more lt GEMMs run there and no captured
+    graph refers to the stream's workspace. torch hands out streams from a fixed per-device
+    pool, so the cached set is bounded even without it; a release returns the 64 MiB
+    workspaces early. Returns the number of entries freed (0 when the stream never ran an
+    lt GEMM)."""
+    from ._lib import lib
+
+    return int(lib().ra_lt_release_stream(stream.cuda_stream))

@@ -1002,6 +1002,12 @@ class Learner(TorchLearner):
             for _ in range(3):  # warm kernels and solver choices; no optimizer step
                 body()
         torch.cuda.current_stream(dev).wait_stream(side)
+        try:  # the warm stream's GEMM workspace is not baked into the graph
+            from ray_amd.ops import lt
+
+            lt.release_stream(side)
+        except (OSError, RuntimeError, AttributeError):
+            pass
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             body()

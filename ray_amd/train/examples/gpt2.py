@@ -105,6 +105,11 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
             from ray_amd.ops import lt
 
             lt.set_tuning(True)  # fp32-output wgrad GEMMs: ops/lt.py selector
+    if on_gpu and os.environ.get("RAY_AMD_MAIN_PRIO") == "1":
+        # the step on a high-priority stream: its workgroups are dispatched ahead of the
+        # side stream's weight-gradient workgroups when both have work queued
+        torch.cuda.set_stream(torch.cuda.Stream(device, priority=min(
+            torch.cuda.Stream.priority_range())))
     mcfg = getattr(GPT2Config, c["model"])()
     gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
     tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],

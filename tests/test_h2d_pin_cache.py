@@ -48,3 +48,36 @@ def test_outside_store_and_failures():
     assert not c.ensure(base + 4 * CHUNK, 1)
     assert not c.ensure(base + CHUNK, 10)  # registration failed: copy runs pageable
     assert c.failures == 1 and c.ensure(base, 10)
+
+
+class _FakeEvent:
+    def __init__(self):
+        self.done = False
+        self.waited = 0
+
+    def query(self):
+        return self.done
+
+    def synchronize(self):
+        self.waited += 1
+        self.done = True
+
+
+def test_inflight_copy_keeps_chunk_and_source_alive():
+    """An async copy's chunks are unregistered only after its event; its source array is
+    held until the event completes (the store block may not be recycled under the DMA)."""
+    base = 1 << 40
+    lib = _FakeLib()
+    c = StorePinCache(base, 8 * CHUNK, cap_bytes=2 * CHUNK, lib=lib)
+    src = object()
+    assert c.ensure(base, 10)
+    ev = _FakeEvent()
+    c.track(base, 10, ev, src)
+    assert c._pending and c._pending[0][1] is src
+    assert c.ensure(base + CHUNK, 10) and c.ensure(base + 2 * CHUNK, 10)  # evicts chunk 0
+    assert lib.unreg == [base] and ev.waited == 1  # waited for the copy before unregister
+    ev2 = _FakeEvent()
+    c.track(base + 2 * CHUNK, 10, ev2, object())
+    assert len(c._pending) == 1  # the completed copy was released, the new one is held
+    c.drain()
+    assert ev2.done and not c._pending
