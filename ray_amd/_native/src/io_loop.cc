@@ -6,6 +6,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
@@ -42,7 +43,9 @@ IOLoop::IOLoop() {
   ev.events = EPOLLIN;
   ev.data.u64 = 0;  // id 0 = wake fd
   epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
-  th_ = std::thread([this] { run(); });
+  const char* e = getenv("RAY_AMD_IO_THREAD");
+  direct_ = !(e && e[0] == '1');
+  if (!direct_) th_ = std::thread([this] { run(); });
 }
 
 IOLoop::~IOLoop() {
@@ -320,38 +323,69 @@ void IOLoop::close_conn(int conn) {
   if (c) do_close(c, false);
 }
 
+void IOLoop::process(const epoll_event* evs, int n) {
+  for (int i = 0; i < n; ++i) {
+    int id = (int)evs[i].data.u64;
+    if (id == 0) {
+      uint64_t v;
+      ssize_t r = ::read(evfd_, &v, sizeof(v));
+      (void)r;
+      continue;
+    }
+    auto c = get(id);
+    if (!c) continue;
+    if (c->listener) {
+      while (true) {
+        int fd = accept4(c->fd, nullptr, nullptr, SOCK_CLOEXEC);
+        if (fd < 0) break;
+        tune_socket(fd, false);
+        int nid = add_fd(fd, false);
+        push(Event{kAccepted, nid, c->id, std::string()});
+      }
+      continue;
+    }
+    if (evs[i].events & EPOLLOUT) handle_write(c);
+    if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) handle_read(c);
+  }
+}
+
 void IOLoop::run() {
   epoll_event evs[256];
   while (!stop_.load()) {
     int n = epoll_wait(epfd_, evs, 256, 200);
-    for (int i = 0; i < n; ++i) {
-      int id = (int)evs[i].data.u64;
-      if (id == 0) {
-        uint64_t v;
-        ssize_t r = ::read(evfd_, &v, sizeof(v));
-        (void)r;
-        continue;
-      }
-      auto c = get(id);
-      if (!c) continue;
-      if (c->listener) {
-        while (true) {
-          int fd = accept4(c->fd, nullptr, nullptr, SOCK_CLOEXEC);
-          if (fd < 0) break;
-          tune_socket(fd, false);
-          int nid = add_fd(fd, false);
-          push(Event{kAccepted, nid, c->id, std::string()});
-        }
-        continue;
-      }
-      if (evs[i].events & EPOLLOUT) handle_write(c);
-      if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) handle_read(c);
-    }
+    if (n > 0) process(evs, n);
   }
 }
 
 std::vector<Event> IOLoop::poll(int timeout_ms, size_t max_events) {
   std::vector<Event> out;
+  if (direct_) {
+    {
+      std::lock_guard<std::mutex> g(qmu_);
+      if (wake_pending_ > 0) {
+        wake_pending_--;
+        while (!q_.empty() && out.size() < max_events) {
+          out.push_back(std::move(q_.front()));
+          q_.pop_front();
+        }
+        return out;
+      }
+      if (!q_.empty()) timeout_ms = 0;  // frames left from the last read: do not block
+    }
+    if (!stop_.load()) {
+      std::lock_guard<std::mutex> ep(ep_mu_);
+      epoll_event evs[256];
+      int n = epoll_wait(epfd_, evs, 256, timeout_ms);
+      if (n > 0) process(evs, n);
+    }
+    std::lock_guard<std::mutex> g(qmu_);
+    if (wake_pending_ > 0) wake_pending_--;
+    while (!q_.empty() && out.size() < max_events) {
+      out.push_back(std::move(q_.front()));
+      q_.pop_front();
+    }
+    return out;
+  }
   std::unique_lock<std::mutex> lk(qmu_);
   auto ready = [this] { return !q_.empty() || wake_pending_ > 0 || stop_.load(); };
   if (timeout_ms < 0) qcv_.wait(lk, ready);
@@ -370,6 +404,11 @@ void IOLoop::wakeup() {
     wake_pending_++;
   }
   qcv_.notify_all();
+  if (direct_) {  // a poller blocked in epoll_wait returns on the event fd
+    uint64_t one = 1;
+    ssize_t r = write(evfd_, &one, sizeof(one));
+    (void)r;
+  }
 }
 
 size_t IOLoop::pending() {

@@ -7,6 +7,14 @@
 // condition-variable queue; Python never holds the GIL while waiting and
 // `send` writes directly from the calling thread when the socket is idle
 // (falling back to the epoll thread's EPOLLOUT flush under back-pressure).
+//
+// Direct mode (the default; RAY_AMD_IO_THREAD=1 restores the epoll thread): there is no
+// epoll thread, the thread calling poll() runs epoll_wait and reads the frames itself.
+// Every received message then costs one thread wake-up instead of two (epoll thread ->
+// condition variable -> poller); on a VM, where waking an idle vCPU costs 50-150 us, that
+// is most of a small task's round trip. Every user of the loop polls it continuously from
+// one thread (the core worker's dispatcher, the raylet / node agent main loops), which is
+// what direct mode requires: a send that hits a full socket is flushed on the next poll.
 #pragma once
 #include <stdint.h>
 
@@ -19,6 +27,8 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+struct epoll_event;  // <sys/epoll.h>
 
 namespace ray_amd {
 
@@ -63,6 +73,7 @@ class IOLoop {
 
  private:
   void run();
+  void process(const ::epoll_event* evs, int n);
   int add_fd(int fd, bool listener);
   void handle_read(std::shared_ptr<Conn> c);
   void handle_write(std::shared_ptr<Conn> c);
@@ -83,6 +94,8 @@ class IOLoop {
   std::condition_variable qcv_;
   std::deque<Event> q_;
   int wake_pending_ = 0;
+  bool direct_ = true;  // poll() drives epoll itself (no epoll thread)
+  std::mutex ep_mu_;    // one epoll driver at a time in direct mode
 };
 
 }  // namespace ray_amd

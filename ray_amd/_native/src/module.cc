@@ -75,6 +75,8 @@ static void parallel_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
   for (auto& t : ts) t.join();
 }
 
+constexpr ssize_t kGilSendBytes = 256 << 10;
+
 PYBIND11_MODULE(_core, m) {
   m.doc() = "ray_amd native runtime core: shm object store, frame I/O loop, scheduler";
 
@@ -301,11 +303,17 @@ PYBIND11_MODULE(_core, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("connect_tcp", &IOLoop::connect_tcp, py::arg("host"), py::arg("port"),
            py::arg("timeout_ms") = 10000, py::call_guard<py::gil_scoped_release>())
+      // Small frames are written with the GIL held: the socket is non-blocking (a full
+      // socket buffers the rest for the epoll thread), so the write is a few-microsecond
+      // syscall, while dropping the GIL around it hands the interpreter to another thread
+      // and the sender then waits up to the switch interval to get it back (measured 75-90
+      // us per send on the task-reply path of an 8-CPU node). Large frames release it.
       .def("send",
            [](IOLoop& io, int conn, py::bytes data) {
              char* p;
              ssize_t n;
              PyBytes_AsStringAndSize(data.ptr(), &p, &n);
+             if (n < kGilSendBytes) return io.send(conn, p, (size_t)n);
              py::gil_scoped_release r;
              return io.send(conn, p, (size_t)n);
            })
@@ -315,8 +323,11 @@ PYBIND11_MODULE(_core, m) {
              ssize_t n;
              PyBytes_AsStringAndSize(a.ptr(), &p, &n);
              py::buffer_info bi = b.request();
+             const size_t nb = (size_t)(bi.size * bi.itemsize);
+             if ((size_t)n + nb < (size_t)kGilSendBytes)
+               return io.send2(conn, p, (size_t)n, (const char*)bi.ptr, nb);
              py::gil_scoped_release r;
-             return io.send2(conn, p, (size_t)n, (const char*)bi.ptr, (size_t)(bi.size * bi.itemsize));
+             return io.send2(conn, p, (size_t)n, (const char*)bi.ptr, nb);
            })
       .def("close", &IOLoop::close_conn)
       .def("poll",

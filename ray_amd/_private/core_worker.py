@@ -47,6 +47,28 @@ INLINE_MAX = 100 * 1024  # reference: max_direct_call_object_size
 ARGS_INLINE_MAX = 100 * 1024
 LEASE_IDLE_S = 0.02
 MAX_PENDING_LEASES_PER_KEY = 64
+# Tasks in flight per leased worker while the node is saturated for the task's scheduling
+# class (lease requests unanswered for PIPELINE_AFTER_S): the next task waits in the
+# worker's queue instead of a full owner -> worker round trip after each reply. A worker
+# whose running task blocks in get/wait hands its queued tasks back, and an owner whose
+# lease goes idle steals a queued task back from a busy one (work stealing), so a pipelined
+# task never waits behind a task that depends on it. RAY_AMD_PIPELINE_DEPTH=1 disables it.
+
+
+def _drain(q: collections.deque) -> list:
+    """Pop everything from a deque that other threads also pop from (a threaded actor's
+    pool threads send replies concurrently): popleft until empty, never a length taken
+    before the pops."""
+    out = []
+    try:
+        while True:
+            out.append(q.popleft())
+    except IndexError:
+        pass
+    return out
+
+PIPELINE_DEPTH = max(1, int(os.environ.get("RAY_AMD_PIPELINE_DEPTH", "2")))
+PIPELINE_AFTER_S = float(os.environ.get("RAY_AMD_PIPELINE_AFTER_MS", "5")) / 1000.0
 
 _dumps = P.dumps
 _loads = P.loads
@@ -184,6 +206,7 @@ class CoreWorker:
         self.io.listen_unix(self.addr)
         self.lock = threading.RLock()
         self._ready_cv = threading.Condition(self.lock)
+        self._wake_targets: list = []  # ready-seq values at which a waiter wants a wake-up
         self._ready_log = collections.deque(maxlen=1 << 16)
         self._ready_owned: set = set()  # owned oids that are ready (set algebra in wait)
         self._ready_seq = 0
@@ -201,6 +224,9 @@ class CoreWorker:
         self.sched_queues: dict = collections.defaultdict(collections.deque)
         self.leases: dict = collections.defaultdict(list)
         self.pending_leases: dict = collections.defaultdict(int)
+        self._lease_wait_t: dict = {}  # key -> when its lease requests last went unanswered
+        self._stealing: set = set()  # tids with a STEAL in flight
+        self.pipeline_stats = collections.Counter()  # pipelined / requeued / steals
         self.task_specs: dict[bytes, dict] = {}  # tid -> spec (pending/running)
         # tid -> spec of FINISHED normal tasks whose stored returns are still owned: the
         # lineage re-executed when a primary copy is lost (object_recovery_manager.cc)
@@ -354,12 +380,26 @@ class CoreWorker:
             P.TASK_REPLY: self._on_task_reply,
             P.STREAM_ITEM: self._on_stream_item,
             P.STREAM_ACK: self._on_stream_ack,
+            P.STEAL: self._on_steal,
         }
         # poll timeout: messages wake the loop at once; the timeout only paces the periodic
         # work below (lease reaping, task-event flushes). Every wake takes the GIL from the
         # process's compute thread (a Train worker's launch loop), so it is configurable.
         poll_ms = int(os.environ.get("RAY_AMD_POLL_MS", "10"))
+        prof_dir = os.environ.get("RAY_AMD_WORKER_CPROFILE")  # diagnostics (worker_main.py)
+        prof, prof_t = None, 0.0
+        if prof_dir:
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         while not self._stopped:
+            if prof is not None and time.monotonic() - prof_t > 2.0:
+                prof_t = time.monotonic()
+                prof.disable()
+                prof.dump_stats(os.path.join(prof_dir,
+                                             f"{self.mode}-{os.getpid()}-dispatch.prof"))
+                prof.enable()
             try:
                 events = io.poll(poll_ms, 4096)
             except Exception:
@@ -378,8 +418,11 @@ class CoreWorker:
                         traceback.print_exc()
             try:
                 self._reap_idle_leases()
-                if self.task_events and (self.mode == "worker" or len(self.task_events) > 4096
-                                         or time.monotonic() - self._events_flushed > 0.5):
+                # workers flush every 0.1 s (their task events mostly travel on the task
+                # replies), drivers every 0.5 s; state queries flush the caller first
+                if self.task_events and (
+                        len(self.task_events) > 4096 or time.monotonic() - self._events_flushed
+                        > (0.1 if self.mode == "worker" else 0.5)):
                     self._flush_task_events()
             except Exception:
                 if not self._stopped:
@@ -766,7 +809,12 @@ class CoreWorker:
             self._ready_owned.add(oid)
             self._ready_log.append(oid)
             self._ready_seq += 1
-            self._ready_cv.notify_all()
+            # wake waiters only once enough objects became ready to possibly satisfy one:
+            # a get() of 1000 refs is woken once, not 1000 times (each wake-up takes the GIL
+            # from the dispatcher thread that is delivering the replies)
+            wt = self._wake_targets
+            if wt and self._ready_seq >= min(wt):
+                self._ready_cv.notify_all()
             cbs = o.callbacks
             o.callbacks = None
             free = o.release_when_ready
@@ -1156,7 +1204,15 @@ class CoreWorker:
                     rem = None if deadline is None else deadline - time.monotonic()
                     if rem is not None and rem <= 0:
                         break
-                    cv.wait(rem if rem is not None else 1.0)
+                    # every ready object bumps _ready_seq, so num_returns - len(done) more
+                    # is the earliest point at which this wait can be satisfied (borrowed
+                    # refs notify directly through remote_hit)
+                    target = self._ready_seq + (num_returns - len(done))
+                    self._wake_targets.append(target)
+                    try:
+                        cv.wait(rem if rem is not None else 1.0)
+                    finally:
+                        self._wake_targets.remove(target)
                     new = self._ready_seq - seen
                     seen = self._ready_seq
                     if new > len(log):  # log wrapped: rescan what is left
@@ -1239,6 +1295,10 @@ class CoreWorker:
             first = self.blocked_depth == 1
         if first:
             self.notify_raylet("notify_blocked", self.worker_id)
+            if PIPELINE_DEPTH > 1:
+                # tasks pipelined behind this one go back to their owners: the blocked task
+                # may be waiting for one of them
+                self._requeue_to_owner(self._take_queued())
         return True
 
     def _notify_unblocked(self):
@@ -1490,6 +1550,17 @@ class CoreWorker:
             return
         self._pump(key)
 
+    @staticmethod
+    def _pipelinable(spec) -> bool:
+        # never queued behind another task: tasks that retire their worker (max_calls),
+        # streaming generators and tasks without retries (a worker death would fail a task
+        # that never ran)
+        return not spec.get("max_calls") and spec["nret"] != -1 and spec["retries"] != 0
+
+    def _saturated(self, key, now) -> bool:
+        t = self._lease_wait_t.get(key)
+        return t is not None and self.pending_leases[key] > 0 and now - t > PIPELINE_AFTER_S
+
     def _pump(self, key):
         to_send = []
         request = 0
@@ -1497,21 +1568,55 @@ class CoreWorker:
             q = self.sched_queues.get(key)
             if not q:
                 return
-            for lease in self.leases.get(key, ()):
+            leases = self.leases.get(key, ())
+            for lease in leases:
                 while q and not lease.inflight:
                     spec = q.popleft()
                     lease.inflight[spec["tid"]] = spec
                     self.task_lease[spec["tid"]] = lease
                     to_send.append((lease, spec))
+            if q and PIPELINE_DEPTH > 1 and leases and \
+                    self._saturated(key, time.monotonic()):
+                for lease in leases:
+                    while q and len(lease.inflight) < PIPELINE_DEPTH and \
+                            self._pipelinable(q[0]) and \
+                            all(self._pipelinable(sp) for sp in lease.inflight.values()):
+                        spec = q.popleft()
+                        lease.inflight[spec["tid"]] = spec
+                        self.task_lease[spec["tid"]] = lease
+                        to_send.append((lease, spec))
+                        self.pipeline_stats["pipelined"] += 1
             if q:
                 want = min(len(q), MAX_PENDING_LEASES_PER_KEY) - self.pending_leases[key]
                 if want > 0:
                     request = want
+                    if self.pending_leases[key] == 0:
+                        self._lease_wait_t[key] = time.monotonic()
                     self.pending_leases[key] += want
         for lease, spec in to_send:
             self._push_task(lease.addr, spec, lease.lease_id)
         for _ in range(request):
             self._request_lease(key)
+
+    def _steal_for(self, key):
+        """A lease of ``key`` went idle with nothing queued: take back one pipelined task
+        that is still waiting in a busy worker's queue (the worker answers with a requeue
+        reply if it has not started it)."""
+        with self.lock:
+            if self.sched_queues.get(key):
+                return
+            for lease in self.leases.get(key, ()):
+                if len(lease.inflight) > 1:
+                    tid = next(reversed(lease.inflight))
+                    if tid in self._stealing:
+                        continue
+                    self._stealing.add(tid)
+                    self.pipeline_stats["steals"] += 1
+                    addr = lease.addr
+                    break
+            else:
+                return
+        self.send(addr, (P.STEAL, tid))
 
     def _push_task(self, addr, spec, lease_id):
         wire = {k: v for k, v in spec.items() if not k.startswith("_")}
@@ -1537,6 +1642,8 @@ class CoreWorker:
         def on_lease(ok, value, key=key):
             with self.lock:
                 self.pending_leases[key] -= 1
+                # a grant: the node had room; the wait clock restarts for what is still out
+                self._lease_wait_t[key] = time.monotonic()
             if not ok:
                 err = value if isinstance(value, BaseException) else RuntimeError(str(value))
                 with self.lock:
@@ -1578,6 +1685,14 @@ class CoreWorker:
 
     def _on_task_reply(self, conn, msg):
         _, tid, returns, extra = msg
+        evs = extra.get("events")
+        if evs:
+            self.task_events.extend(evs)
+        if extra.get("requeue"):  # a pipelined task handed back unstarted
+            self._on_requeue(tid)
+            return
+        if self._stealing:
+            self._stealing.discard(tid)  # finished before the steal reached it
         with self.lock:
             spec = self.task_specs.get(tid)
         if spec is None:
@@ -1614,6 +1729,26 @@ class CoreWorker:
             self._schedule(spec)
         else:
             self._complete(spec, returns, extra)
+        if lease is not None:
+            self._pump(lease.key)
+            if not lease.inflight and PIPELINE_DEPTH > 1:
+                self._steal_for(lease.key)
+
+    def _on_requeue(self, tid):
+        with self.lock:
+            self.pipeline_stats["requeued"] += 1
+            self._stealing.discard(tid)
+            lease = self.task_lease.pop(tid, None)
+            spec = self.task_specs.get(tid)
+            if lease is not None:
+                lease.inflight.pop(tid, None)
+                if not lease.inflight:
+                    lease.idle_since = time.monotonic()
+            if spec is None:
+                return
+            key = self._sched_key(spec)
+            self.sched_queues[key].appendleft(spec)
+        self._pump(key)
         if lease is not None:
             self._pump(lease.key)
 
@@ -1746,15 +1881,21 @@ class CoreWorker:
 
     def _on_worker_lost(self, addr):
         lost = []
+        queued = []  # pipelined behind the running task: never started on that worker
         with self.lock:
             for key, ls in list(self.leases.items()):
                 for lease in list(ls):
                     if lease.addr == addr:
                         ls.remove(lease)
-                        lost.extend(lease.inflight.values())
+                        specs = list(lease.inflight.values())
+                        lost.extend(specs[:1])
+                        queued.extend(specs[1:])
                         for t in lease.inflight:
                             self.task_lease.pop(t, None)
+                            self._stealing.discard(t)
                         lease.inflight.clear()
+        for spec in queued:  # rescheduled as they are: no retry consumed
+            self._schedule(spec)
         if not lost:
             return
 
@@ -2238,6 +2379,30 @@ class CoreWorker:
         else:
             self.exec_queue.put(spec)
 
+    def _take_queued(self, tid=None):
+        """Remove unstarted normal tasks from the executor queue (one ``tid``, or all)."""
+        q = self.exec_queue
+        out = []
+        with q.mutex:
+            keep = collections.deque()
+            for spec in q.queue:
+                if spec is not None and spec["type"] == P.NORMAL_TASK and \
+                        (tid is None or spec["tid"] == tid):
+                    out.append(spec)
+                else:
+                    keep.append(spec)
+            q.queue.clear()
+            q.queue.extend(keep)
+        return out
+
+    def _requeue_to_owner(self, specs):
+        for spec in specs:
+            conn = spec.pop("_conn", None)
+            self._send_reply(conn, spec["owner"], spec["tid"], [], {"requeue": True})
+
+    def _on_steal(self, conn, msg):
+        self._requeue_to_owner(self._take_queued(msg[1]))
+
     def _dispatch_actor_task(self, spec):
         if self.async_loop is not None:
             import asyncio
@@ -2252,17 +2417,32 @@ class CoreWorker:
 
     def run_task_loop(self):
         """Main-thread executor loop for worker processes."""
+        prof_dir = os.environ.get("RAY_AMD_WORKER_CPROFILE")  # diagnostics (worker_main.py)
+        prof, prof_t = None, time.monotonic()
+        if prof_dir:
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         while not self.exiting:
+            if prof is not None and time.monotonic() - prof_t > 2.0:
+                prof_t = time.monotonic()
+                prof.disable()
+                prof.dump_stats(os.path.join(prof_dir, f"{self.mode}-{os.getpid()}-main.prof"))
+                prof.enable()
             try:
                 spec = self.exec_queue.get(timeout=1.0)
             except queue.Empty:
                 continue
             if spec is None:
                 break
-            if spec["type"] == P.ACTOR_TASK and self.actor_pools:
-                self._dispatch_actor_task(spec)
-                continue
-            self._execute(spec)
+            try:
+                if spec["type"] == P.ACTOR_TASK and self.actor_pools:
+                    self._dispatch_actor_task(spec)
+                    continue
+                self._execute(spec)
+            except Exception:  # never let one task's bookkeeping end the worker loop
+                traceback.print_exc()
 
     def _execute(self, spec):
         tid = spec["tid"]
@@ -2427,9 +2607,20 @@ class CoreWorker:
     def _send_reply(self, conn, reply_to, tid, returns, extra):
         if any(r[1] == P.RET_STORE for r in returns):
             extra["node"] = self.node_hex
+        evs = None
+        if reply_to is not None and self.task_events:
+            # this worker's task events ride on the reply; the owner forwards them with its
+            # own batch (one raylet message per owner flush instead of one per task)
+            q = self.task_events
+            evs = _drain(q)
+            if evs:
+                extra["events"] = evs
         msg = (P.TASK_REPLY, tid, returns, extra)
         if reply_to is not None and self.send(reply_to, msg):
             return
+        if evs:
+            self.task_events.extend(evs)
+            extra.pop("events", None)
         if conn is not None:
             self.io.send(conn, _dumps(msg))
 
@@ -2677,7 +2868,7 @@ class CoreWorker:
     def _flush_task_events(self):
         self._events_flushed = time.monotonic()
         q = self.task_events
-        ev = [q.popleft() for _ in range(len(q))]
+        ev = _drain(q)
         if ev:
             self.notify_raylet("task_events", ev)
 

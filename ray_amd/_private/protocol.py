@@ -19,6 +19,7 @@ TASK_REPLY = 12
 STREAM_ITEM = 13
 # owner -> executing worker: (STREAM_ACK, tid, items consumed) for generator backpressure
 STREAM_ACK = 14
+STEAL = 15  # owner -> worker: give back a pipelined task that has not started yet
 
 # task types
 NORMAL_TASK = 0

@@ -100,7 +100,7 @@ def select_worker_to_kill(leases, policy: str = "group_by_owner"):
 
 class LeaseReq:
     __slots__ = ("rid", "conn", "req", "alloc", "node", "waiting_token", "cb", "t0", "warned",
-                 "resources")
+                 "resources", "shape")
 
     def __init__(self, rid, conn, req, cb=None):
         self.rid = rid
@@ -113,6 +113,7 @@ class LeaseReq:
         self.t0 = time.monotonic()
         self.warned = False
         self.resources = None
+        self.shape = None  # (resources, strategy, target, hard labels, soft labels), resolved once
 
 
 class ActorRec:
@@ -332,7 +333,19 @@ class Raylet:
         handlers = {P.REQ: self.on_req, P.HELLO: self.on_hello, P.TASK_REPLY: self.on_task_reply,
                     P.RESP: self.on_resp}
         last_tick = 0.0
+        prof_dir = os.environ.get("RAY_AMD_WORKER_CPROFILE")  # diagnostics (worker_main.py)
+        prof, prof_t = None, 0.0
+        if prof_dir:
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         while not self.stop:
+            if prof is not None and time.monotonic() - prof_t > 2.0:
+                prof_t = time.monotonic()
+                prof.disable()
+                prof.dump_stats(os.path.join(prof_dir, f"raylet-{os.getpid()}.prof"))
+                prof.enable()
             ev = self.io.poll(20, 4096)
             for typ, conn, payload in ev:
                 try:
@@ -605,11 +618,38 @@ class Raylet:
             return out
         return res
 
+    @staticmethod
+    def _lease_shape(req):
+        """(strategy code, target node, hard labels, soft labels, class key) of a lease
+        request: everything pick_node needs besides the resources."""
+        st = req.get("strategy")
+        strategy, target = 0, ""
+        hard_l, soft_l = {}, {}
+        if st == "SPREAD":
+            strategy = 1
+        elif isinstance(st, dict):
+            if st.get("type") == "node_affinity":
+                strategy = 3 if st.get("soft") else 2
+                target = st["node_id"]
+            elif st.get("type") == "node_label":
+                hard_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
+                          for k, v in (st.get("hard") or {}).items()}
+                soft_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
+                          for k, v in (st.get("soft") or {}).items()}
+        res = req.get("resources") or {}
+        skey = (tuple(sorted((k, float(v)) for k, v in res.items() if v)), repr(st))
+        return strategy, target, hard_l, soft_l, skey
+
     def try_schedule(self):
         if not self.pending:
             return
         keep = collections.deque()
         starting_budget = self.max_starting - len(self.starting)
+        # scheduling classes that found no room in this pass: later requests of the same
+        # class wait without another pick (the owners keep up to 64 lease requests per
+        # class pending, so a full node would otherwise be re-searched for each of them;
+        # reference: cluster_task_manager.cc skips a scheduling class once it is blocked)
+        blocked = set()
         while self.pending:
             lr = self.pending.popleft()
             if lr.conn is not None and lr.conn not in self.conn_worker and lr.cb is None:
@@ -618,24 +658,18 @@ class Raylet:
                     self.sched.release(lr.alloc, lr.resources)
                 continue
             if lr.alloc is None:
-                res = self._resolve_resources(lr.req)
-                lr.resources = res
+                if lr.shape is None:
+                    lr.resources = self._resolve_resources(lr.req)
+                    lr.shape = self._lease_shape(lr.req)
+                res = lr.resources
                 st = lr.req.get("strategy")
-                strategy, target, soft = 0, "", False
-                hard_l, soft_l = {}, {}
-                if st == "SPREAD":
-                    strategy = 1
-                elif isinstance(st, dict):
-                    if st.get("type") == "node_affinity":
-                        strategy = 3 if st.get("soft") else 2
-                        target = st["node_id"]
-                    elif st.get("type") == "node_label":
-                        hard_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
-                                  for k, v in (st.get("hard") or {}).items()}
-                        soft_l = {k: ",".join(v) if isinstance(v, (list, tuple)) else str(v)
-                                  for k, v in (st.get("soft") or {}).items()}
+                strategy, target, hard_l, soft_l, skey = lr.shape
                 rw = self.conn_worker.get(lr.conn)
                 local = rw.node if rw is not None and rw.node else self.node_hex
+                bkey = (skey, local)
+                if bkey in blocked:
+                    keep.append(lr)
+                    continue
                 node = self.sched.pick_node(res, strategy, target, local, hard_l, soft_l)
                 if node == "!":
                     if isinstance(st, dict) and st.get("type") == "pg" and \
@@ -650,10 +684,12 @@ class Raylet:
                     keep.append(lr)
                     continue
                 if node == "":
+                    blocked.add(bkey)
                     keep.append(lr)
                     continue
                 alloc = self.sched.allocate(node, res)
                 if alloc is None:
+                    blocked.add(bkey)
                     keep.append(lr)
                     continue
                 lr.alloc = alloc

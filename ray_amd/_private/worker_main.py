@@ -59,6 +59,8 @@ def main():
     if hook:
         cw.run_setup_hook(hook)
     try:
+        # RAY_AMD_WORKER_CPROFILE=<dir>: the task loop and the dispatcher thread dump
+        # cProfile stats there every 2 s (core-worker throughput diagnostics)
         cw.run_task_loop()
     finally:
         os._exit(0)

@@ -59,6 +59,31 @@ __device__ __forceinline__ float gelu_grad(float u) {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
+// 16-byte global -> LDS DMA as inline asm (LDS address = M0 + lane * 16), M0 saved and
+// restored. Through __builtin_amdgcn_global_load_lds hipcc cannot tell the DMA's LDS write
+// from the fragment reads of the other stage buffer and puts s_waitcnt vmcnt(0) in front of
+// them, draining the prefetch every K-step (the same fix as ops/csrc/wgrad.hip glds16_w).
+// RAY_AMD_GEMM_GLDS_BUILTIN (compile-time define) keeps the builtin for A/B runs.
+__device__ __forceinline__ void glds16(const bf16_t* gsrc, bf16_t* ldst) {
+#ifdef RAY_AMD_GEMM_GLDS_BUILTIN
+  __builtin_amdgcn_global_load_lds((glb_void_t*)gsrc, (lds_void_t*)ldst, 16, 0, 0);
+#else
+  const unsigned la = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)ldst);
+  unsigned saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(gsrc), "s"(la)
+      : "memory");
+#endif
+}
+
+
 // LDS bank swizzle of a [rows][BK] bf16 image: 16-B chunk p of row r holds global chunk
 // p ^ swz(r). BK = 64 (128-B rows, two rows per 256-B bank row): (r>>1)&7; BK = 32 (64-B
 // rows, four per bank row): (r>>2)&3. Either way the 16 lanes of a ds_read_b128 group
@@ -85,8 +110,7 @@ __device__ __forceinline__ void stage_operand(bf16_t* img, const bf16_t* __restr
     gr = gr < rows ? gr : rows - 1;  // clamp ragged edges (results masked at the store)
     const int ch = p ^ swz<BK>(r);
     const bf16_t* src = g + (long)gr * ld + k0 + 8 * ch;
-    __builtin_amdgcn_global_load_lds((glb_void_t*)src,
-                                     (lds_void_t*)(img + (32 * w + RPI * j) * BK), 16, 0, 0);
+    glds16(src, img + (32 * w + RPI * j) * BK);
   }
 }
 
@@ -499,7 +523,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_8ph_kernel(
       gr = gr < rows ? gr : rows - 1;  // clamp ragged edges (results masked at the store)
       const int ch = p ^ swz<BK>(r);
       const bf16_t* s = src + (long)gr * ld + kt * BK + 8 * ch;
-      __builtin_amdgcn_global_load_lds((glb_void_t*)s, (lds_void_t*)(img + prow0 * BK), 16, 0, 0);
+      glds16(s, img + prow0 * BK);
     }
   };
   auto barrier = []() __attribute__((always_inline)) {

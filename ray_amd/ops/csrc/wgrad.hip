@@ -602,7 +602,8 @@ RA_EXPORT int ra_wgrad(const void* dy, long ldy, const void* x, long ldx, int M,
   return hipGetLastError();
 }
 
-// Splits that fill the chip with one wave of workgroups: tiles * S <= #CUs.
+// Splits that fill the chip with one wave of workgroups: tiles * S <= #CUs (fewer tiles
+// than CUs), or the fewest partly-filled waves (more tiles than CUs).
 RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
   if (g_cus_w == 0) {
     int dev = 0;
@@ -621,6 +622,17 @@ RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
   const int tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
   int S = waves * g_cus_w / tiles;
   const int nks = M / kT;
+  if (S < 1) {
+    // more tiles than CUs (the LM head's dW: 197 x 3 = 591 tiles): the split count that
+    // minimises the partly-filled last wave, ceil(tiles * S / CUs) / S in full-K tile
+    // times (591 tiles: S = 3, 7 waves of 1/3-K workgroups = 2.33 vs 3 at S = 1)
+    S = 1;
+    double best = (double)((tiles + g_cus_w - 1) / g_cus_w);
+    for (int s = 2; s <= 4 && s <= nks; ++s) {
+      const double t = (double)((tiles * s + g_cus_w - 1) / g_cus_w) / s;
+      if (t < best - 1e-9) best = t, S = s;
+    }
+  }
   if (S > nks) S = nks;
   if (S < 1) S = 1;
   return S;

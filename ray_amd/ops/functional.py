@@ -380,7 +380,7 @@ def wgrad_accumulate(dy2, x2, sink, bias_sink=None, accumulate=True):
             bias_sink.copy_(bias_sink.float() + dt.sum(0))
 
 
-# Grouped weight gradients (RAY_AMD_WGRAD_GROUP=1, default): the hip wgrads of a layer's
+# Grouped weight gradients (RAY_AMD_WGRAD_GROUP=1, opt-in): the hip wgrads of a layer's
 # linears are queued and launched together once their 256x256 tiles reach
 # RAY_AMD_WGRAD_GROUP_TILES (GPT-2 small: mlp_proj 36 + fc 36 + proj 9 + qkv 27 = 108 ->
 # one launch per layer after qkv's backward) as ONE kernel with the split-K reduction
@@ -814,8 +814,24 @@ def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignor
             _lm_head_dw(lg, h2[s0:e], dw, i == 0)
 
 
-def _lm_head_dw(lg, h2s, dw, first):
-    if _WGRAD_LT:
+# LM-head weight gradient: "hip" = the wgrad kernel (split count from ra_wgrad_splits: 3
+# at 591 tiles), "lt" = ops/lt's fp32-out hipBLASLt GEMM (per-stream handle), "torch" =
+# torch.addmm (torch's handle: main stream only). RAY_AMD_LMHEAD_DW_SIDE=1 (default): with a
+# flat-gradient sink and one chunk, dW runs on the wgrad side stream, overlapping the
+# transformer backward; its scaled accumulation into the sink stays there and the
+# embedding's backward (the other user of the tied weight's sink) waits on its event.
+_LMHEAD_DW = os.environ.get("RAY_AMD_LMHEAD_DW", "hip")
+_LMHEAD_DW_SIDE = os.environ.get("RAY_AMD_LMHEAD_DW_SIDE", "1") == "1"
+
+
+def _lm_head_dw(lg, h2s, dw, first, side=False):
+    mode = _LMHEAD_DW
+    if mode == "torch" and side:
+        mode = "lt"  # torch's one hipBLASLt handle is never used off the main stream
+    if mode == "hip" and _wgrad_hip_ok(lg, h2s, dw):
+        wgrad_accumulate(lg, h2s, dw, accumulate=not first)
+        return
+    if _WGRAD_LT or mode == "lt" or side:
         from . import lt
 
         lt.wgrad_accum(lg, h2s, dw, beta=0.0 if first else 1.0)
@@ -851,10 +867,13 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         ch = max(1, min(chunk, N))
         L = _lib.lib()
         wt = w.t()
+        ctx.side_dw = False
         if h.is_cuda and N > ch:
             _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp,
                                ignore_index)
         else:  # one chunk (the GPT-2 bench: 65536 tokens), or CPU: all on this stream
+            side_dw = (dw is not None and h.is_cuda and N <= ch and _WGRAD_STREAM
+                       and _LMHEAD_DW_SIDE and _grad_sink(w) is not None)
             lg = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
             for s0 in range(0, N, ch):
                 e = min(N, s0 + ch)
@@ -864,8 +883,16 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
                                       e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
                 if dh is not None:
                     torch.mm(lgc, w, out=dh[s0:e])
-                if dw is not None:
+                if dw is not None and side_dw:
+                    side = _side_stream(dev)
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(side):
+                        _lm_head_dw(lgc, h2[s0:e], dw, True, side=True)
+                    for t_ in (lg, h2, dw):
+                        t_.record_stream(side)
+                elif dw is not None:
                     _lm_head_dw(lgc, h2[s0:e], dw, s0 == 0)
+            ctx.side_dw = side_dw
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]
@@ -882,7 +909,21 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         dwv = None
         if dw is not None:
             sink = _grad_sink(ctx.w)
-            if sink is not None:
+            if sink is not None and ctx.side_dw:
+                # dW was computed on the side stream: scale + accumulate there too, and
+                # leave an event for the other writer of this sink (the embedding)
+                side = _side_stream(dw.device)
+                side.wait_stream(torch.cuda.current_stream(dw.device))
+                with torch.cuda.stream(side):
+                    check(L.ra_scaled_accum(ptr(dw), ptr(sink), dw.numel(), _sink_f32(sink),
+                                            ptr(gs), stream_ptr()), "scaled_accum")
+                    gs.record_stream(side)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    ctx.w._ra_sink_event = ev
+                    if ctx.signal_w:
+                        _grad_done(ctx.w)
+            elif sink is not None:
                 check(L.ra_scaled_accum(ptr(dw), ptr(sink), dw.numel(), _sink_f32(sink), ptr(gs),
                                         stream_ptr()), "scaled_accum")
                 if ctx.signal_w:
@@ -929,6 +970,10 @@ class _Embedding(torch.autograd.Function):
                         (wpe, lambda acc: acc[:T].add_(dx.float().sum(0).to(acc.dtype)))):
             sink = _grad_sink(p)
             if sink is not None:
+                ev = getattr(p, "_ra_sink_event", None)
+                if ev is not None:  # the LM head's side-stream dW accumulation comes first
+                    torch.cuda.current_stream(dx.device).wait_event(ev)
+                    p._ra_sink_event = None
                 fill(sink)
                 _grad_done(p)
                 outs.append(None)

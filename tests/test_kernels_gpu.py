@@ -785,6 +785,26 @@ def test_wgrad_kernel_matches_fp32(cuda_device, M, N, K, bias, sdtype):
     assert _rel(out, dy.float().t() @ x.float()) < 2e-3
 
 
+def test_wgrad_kernel_many_tiles_split(cuda_device):
+    """More 256 x 256 tiles than CUs (the LM head's dW, vocab x C): ra_wgrad_splits picks
+    the split count with the fewest partly-filled waves (3 at 591 tiles on 256 CUs) and the
+    slab-summed result matches fp32, with the padded vocabulary rows exactly zero."""
+    L = _lib.lib()
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    if cus == 256:
+        assert L.ra_wgrad_splits(65536, 50304, 768) == 3
+    torch.manual_seed(14)
+    M, V, Vp, C = 2048, 50257, 50304, 768
+    lg = torch.randn(M, Vp, device=cuda_device).bfloat16()
+    lg[:, V:] = 0
+    h = torch.randn(M, C, device=cuda_device).bfloat16()
+    dw = torch.full((Vp, C), 3.0, device=cuda_device)
+    assert rf._wgrad_hip_ok(lg, h, dw)
+    rf.wgrad_accumulate(lg, h, dw, accumulate=False)
+    assert _rel(dw, lg.float().t() @ h.float()) < 2e-3
+    assert float(dw[V:].abs().max()) == 0.0
+
+
 def test_wgrad_kernel_strided_rows(cuda_device):
     """Operands that are column slices of wider rows (ld > N / K), as packed activations."""
     torch.manual_seed(12)

@@ -72,6 +72,34 @@ def test_flat_fp32_grads_match_autograd(cuda_device):
         assert _rel(p._ra_grad, pr.grad) < 3e-2, n
 
 
+@pytest.mark.parametrize("mode", ["hip", "lt"])
+def test_lm_head_side_stream_dw_matches_main_stream(cuda_device, monkeypatch, mode):
+    """The tied LM head's dW on the wgrad side stream (and its scaled accumulation into the
+    flat sink, ordered before the embedding's scatter by an event) gives the gradients of
+    the all-main-stream path, for 2 micro-batches accumulated into one flat buffer."""
+    import copy
+
+    from ray_amd.models.gpt2 import GPT2
+    from ray_amd.parallel.flat import FlatParams
+
+    monkeypatch.setattr(rf, "_LMHEAD_DW", mode)
+    torch.manual_seed(23)
+    base = GPT2(_tiny_cfg()).to(cuda_device).bfloat16()
+    idx = torch.randint(0, 1000, (2, 4, 256), device=cuda_device)
+    tgt = torch.randint(0, 1000, (2, 4, 256), device=cuda_device)
+    grads = []
+    for side in (False, True):
+        monkeypatch.setattr(rf, "_LMHEAD_DW_SIDE", side)
+        m = copy.deepcopy(base)
+        flat = FlatParams(m)
+        for i in range(2):
+            (m(idx[i], tgt[i]) * (0.5 + i)).backward()
+        rf.join_side_streams()
+        torch.cuda.synchronize()
+        grads.append(flat.g.clone())
+    assert _rel(grads[1], grads[0]) < 1e-5
+
+
 def test_flat_fp32_grad_accum_exact(cuda_device):
     """grad_accum=4 into the fp32 flat buffer equals the fp64 sum of the four
     micro-batch gradients to ~1e-6 (bf16 accumulation is orders of magnitude worse)."""
