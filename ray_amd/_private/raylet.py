@@ -540,49 +540,22 @@ class Raylet:
     def _tee_worker_logs(self, w):
         """worker-<token>-<pid>.out/.err under <session>/logs (state API list_logs /
         get_log, CLI `logs`), each line also forwarded to this raylet's stdout / stderr
-        (the driver's terminal) as before."""
+        (the driver's terminal). All pipes are drained by ONE pump thread
+        (``_private/log_pump.py``), not two threads per worker."""
         import sys
-        import threading
 
+        pump = getattr(self, "_log_pump", None)
+        if pump is None:
+            from ray_amd._private.log_pump import LogPump
+
+            pump = self._log_pump = LogPump(self._dedup())
         d = os.path.join(self.session_dir, "logs")
         os.makedirs(d, exist_ok=True)
-        dedup = self._dedup()
         to_driver = os.environ.get("RAY_AMD_LOG_TO_DRIVER", "1") != "0"
         for pipe, ext, out in ((w.proc.stdout, "out", sys.stdout), (w.proc.stderr, "err",
                                                                        sys.stderr)):
             path = os.path.join(d, f"worker-{w.token}-{w.pid}.{ext}")
-
-            def pump(pipe=pipe, path=path, out=out if to_driver else None):
-                # never stop draining the pipe: a worker whose pipe fills (64 KB) blocks on
-                # its next print. A failed file write (ENOSPC, ...) drops the file copy
-                # and keeps forwarding to the terminal.
-                try:
-                    f = open(path, "ab", buffering=0)
-                except OSError:
-                    f = None
-                for line in iter(pipe.readline, b""):
-                    if f is not None:
-                        try:
-                            f.write(line)
-                        except (ValueError, OSError):
-                            try:
-                                f.close()
-                            except OSError:
-                                pass
-                            f = None
-                    if out is None:  # init(log_to_driver=False): files only
-                        continue
-                    for text in dedup.feed(line, w.pid, out):
-                        try:
-                            out.buffer.write(text)
-                            out.flush()
-                        except (ValueError, OSError, AttributeError):
-                            pass
-                if f is not None:
-                    f.close()
-                pipe.close()
-
-            threading.Thread(target=pump, daemon=True, name=f"log-{w.pid}-{ext}").start()
+            pump.add(pipe, path, out if to_driver else None, w.pid)
 
     def _take_idle(self, key):
         lst = self.idle.get(key)

@@ -619,8 +619,15 @@ RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
     const int w = e ? atoi(e) : 1;
     return w < 1 ? 1 : (w > 8 ? 8 : w);
   }();
+  // RAY_AMD_WGRAD_FILL=f (0 < f <= 1): fill only a fraction f of the CUs (fewer, longer
+  // workgroups: less fp32 slab traffic and fewer CUs taken from the main stream)
+  static const double fill = [] {
+    const char* e = getenv("RAY_AMD_WGRAD_FILL");
+    const double f = e ? atof(e) : 1.0;
+    return f <= 0.0 || f > 1.0 ? 1.0 : f;
+  }();
   const int tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-  int S = waves * g_cus_w / tiles;
+  int S = (int)(waves * fill * g_cus_w) / tiles;
   const int nks = M / kT;
   if (S < 1) {
     // more tiles than CUs (the LM head's dW: 197 x 3 = 591 tiles): the split count that
