@@ -46,7 +46,12 @@ from .ids import object_id_for_put, object_id_for_return
 INLINE_MAX = 100 * 1024  # reference: max_direct_call_object_size
 ARGS_INLINE_MAX = 100 * 1024
 LEASE_IDLE_S = 0.02
-MAX_PENDING_LEASES_PER_KEY = 64
+# Lease requests in flight per scheduling class. The reference caps this at the number of
+# nodes (ray_config_def.h max_pending_lease_requests_per_scheduling_category = -1 ->
+# #nodes) and requests more as grants return; 64 here flooded the raylet with requests it
+# rescanned on every scheduling pass: with 4, multi-client async tasks went from 5.6-8.8k
+# to 13-21.5k tasks/s on the 8-CPU node (profiles/microbenchmark_r5.md).
+MAX_PENDING_LEASES_PER_KEY = int(os.environ.get("RAY_AMD_MAX_PENDING_LEASES", "4"))
 # Tasks in flight per leased worker while the node is saturated for the task's scheduling
 # class (lease requests unanswered for PIPELINE_AFTER_S): the next task waits in the
 # worker's queue instead of a full owner -> worker round trip after each reply. A worker
