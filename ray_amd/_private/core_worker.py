@@ -1766,16 +1766,17 @@ class CoreWorker:
         names = {getattr(c, "__name__", str(c)) for c in re}
         return exc_type_name in names
 
-    def _complete(self, spec, returns, extra):
+    def _complete(self, spec, returns, extra, call_finished=False):
         from ray_amd.object_ref import ObjectRef
 
         tid = spec["tid"]
         with self.lock:
             self.task_specs.pop(tid, None)
         # a failed call of a handle-less actor may be the one it was waiting for
-        # (connection loss, the lost-task fallback timer, a dead actor)
-        if spec["type"] == P.ACTOR_TASK and self._actor_call_finished(spec) and \
-                not self._stopped:
+        # (connection loss, the lost-task fallback timer, a dead actor); a reply already
+        # went through _actor_call_finished (call_finished)
+        if spec["type"] == P.ACTOR_TASK and not call_finished and \
+                self._actor_call_finished(spec) and not self._stopped:
             self.notify_raylet("actor_out_of_scope", spec["actor_id"])
         if spec["nret"] == -1:
             st = self.streams.get(tid)
@@ -2350,7 +2351,7 @@ class CoreWorker:
 
     def _on_actor_task_reply(self, spec, returns, extra):
         release = self._actor_call_finished(spec)
-        self._complete(spec, returns, extra)
+        self._complete(spec, returns, extra, call_finished=True)
         if release and not self._stopped:
             self.notify_raylet("actor_out_of_scope", spec["actor_id"])
 

@@ -113,13 +113,31 @@ class NodeAgent:
         env = dict(env)
         env["RAY_AMD_NODE_ID"] = self.node_hex
         try:
-            p = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True)
+            p = subprocess.Popen(cmd, env=env, cwd=cwd, close_fds=True,
+                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE)
             self.procs[p.pid] = p
+            self._tee_logs(token, p)
             self.reply(conn, rid, True, p.pid)
         except Exception as e:  # noqa: BLE001
             print(f"[ray_amd] node {self.node_hex[:12]}: worker spawn failed: {e}",
                   file=sys.stderr, flush=True)
             self.reply(conn, rid, False, str(e))
+
+    def _tee_logs(self, token, p):
+        """worker-<token>-<pid>.out/.err under <session>/logs, forwarded to this agent's
+        stdout / stderr, through one selector thread for the node (as the head raylet)."""
+        pump = getattr(self, "_log_pump", None)
+        if pump is None:
+            from ray_amd._private.log_dedup import LogDeduplicator
+            from ray_amd._private.log_pump import LogPump
+
+            pump = self._log_pump = LogPump(LogDeduplicator.from_env())
+        d = os.path.join(self.session_dir, "logs")
+        os.makedirs(d, exist_ok=True)
+        to_driver = os.environ.get("RAY_AMD_LOG_TO_DRIVER", "1") != "0"
+        for pipe, ext, out in ((p.stdout, "out", sys.stdout), (p.stderr, "err", sys.stderr)):
+            pump.add(pipe, os.path.join(d, f"worker-{token}-{p.pid}.{ext}"),
+                     out if to_driver else None, p.pid)
 
     def rpc_kill_worker(self, conn, rid, pid, graceful):
         p = self.procs.get(pid)

@@ -155,3 +155,30 @@ def test_label_selector(cluster3):
         where.options(label_selector={"zone": "in()"}).remote()
     with pytest.raises(ValueError):
         where.options(label_selector={"zone": "z1"}, scheduling_strategy="SPREAD").remote()
+
+
+def test_worker_logs_on_other_nodes(cluster3):
+    """A worker forked by a node agent gets worker-<token>-<pid>.out under the session's
+    logs directory, drained by the agent's LogPump (reference: log_monitor.py runs per
+    node)."""
+    import glob
+    import os
+    import time
+
+    c, n1, n2 = cluster3
+
+    @ray.remote(resources={"b": 1})
+    def shout():
+        print("hello-from-node-b", flush=True)
+        return ray.get_runtime_context().get_node_id()
+
+    assert ray.get(shout.remote()) != ray.get(where.options(resources={"a": 1}).remote())
+    deadline = time.time() + 10
+    hit = []
+    while time.time() < deadline and not hit:
+        for f in glob.glob(os.path.join(c.session_dir, "logs", "worker-*.out")):
+            with open(f, "rb") as fh:
+                if b"hello-from-node-b" in fh.read():
+                    hit.append(f)
+        time.sleep(0.1)
+    assert hit
