@@ -133,6 +133,7 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
         "model_tflops_per_gpu": round(r["model_tflops_per_gpu"], 1),
         "final_loss": round(r["loss"], 4),
         "ddp_allreduce_launches": r.get("ddp_allreduce_launches"),
+        "wgrad_stream_autotune": r.get("wgrad_stream_autotune"),
     }
     # self-diagnosing multi-GPU runs: exposed comm, all-reduce launches / bytes and
     # per-bucket bus bandwidth per rank (FlatDDP.read_stats; zeros at world 1)

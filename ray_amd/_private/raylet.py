@@ -1769,6 +1769,8 @@ def main():
     ap.add_argument("--head-address", default=None,
                     help="join an existing cluster as a worker node (head raylet socket)")
     ap.add_argument("--ready-file", default="raylet.ready")
+    ap.add_argument("--fate-share-pid", type=int, default=0,
+                    help="exit (graceful shutdown) once this process is gone")
     args = ap.parse_args()
     if args.head_address:
         from .node_agent import NodeAgent
@@ -1777,6 +1779,21 @@ def main():
     else:
         r = Raylet(args)
     signal.signal(signal.SIGTERM, lambda *_: setattr(r, "stop", True))
+    if args.fate_share_pid:
+        import threading
+
+        def _watch(pid=args.fate_share_pid):
+            while not r.stop:
+                time.sleep(1.0)
+                try:
+                    os.kill(pid, 0)
+                except ProcessLookupError:
+                    r.stop = True  # the run loop shuts the node down (workers, store file)
+                    return
+                except PermissionError:
+                    pass
+
+        threading.Thread(target=_watch, name="fate-share", daemon=True).start()
     ready = os.path.join(args.session_dir, args.ready_file)
     with open(ready + ".tmp", "w") as f:
         json.dump({"addr": r.addr, "node_id": r.node_id.hex(), "pid": os.getpid()}, f)

@@ -117,6 +117,11 @@ def _start_raylet(session_dir, num_cpus, num_gpus, resources, object_store_memor
         cmd += ["--num-gpus", str(int(num_gpus))]
     if head:
         cmd.append("--head")
+    if not detach_output:
+        # fate sharing (reference: services.py start_ray_process(fate_share=True)): a node
+        # started by ray.init() / cluster_utils exits when this process is gone, even if it
+        # was killed without running ray.shutdown(); `start` (detached) nodes outlive it
+        cmd += ["--fate-share-pid", str(os.getpid())]
     env = dict(os.environ)
     env.update(extra_env or {})
     pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
