@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5, call R: the side-stream autotune back to back (the second and third processes
+# round 5, call R (+ S): the side-stream autotune back to back (the second and third processes
 # start inside the post-process slow window), plus the default Ray TorchTrainer bench
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -15,4 +15,5 @@ for i in 1 2 3; do
 done
 timeout -k 10 400 python bench.py > $O/bench_default.log 2>&1 || { echo "rc=$?"; tail -5 $O/bench_default.log; exit 1; }
 echo "default (TorchTrainer): $(show $O/bench_default.log)"
-exit 0
+sleep 35
+bash scripts/gpu_r5s.sh

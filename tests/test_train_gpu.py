@@ -359,3 +359,20 @@ def test_gpt2_graph_replay_matches_eager_then_eager_after_replay(cuda_device):
     torch.cuda.synchronize()
     for a, b in zip(eager[2:], graphed):
         assert abs(a - b) <= 2e-3 * abs(a), (eager, graphed)
+
+
+def test_bench_stream_autotune_reports_and_restores(cuda_device, monkeypatch):
+    """run_steps times 2 side-stream and 2 single-stream warmup steps and runs the timed
+    steps in the faster mode; the choice is reported, and training stays correct."""
+    from ray_amd.ops import functional as rf
+    from ray_amd.train.examples.gpt2 import run_steps
+
+    monkeypatch.setenv("RAY_AMD_STREAM_AUTOTUNE", "1")
+    monkeypatch.setattr(rf, "_WGRAD_STREAM", True)
+    r = run_steps({"model": "tiny", "micro_batch": 4, "seq_len": 128, "steps": 3,
+                   "warmup": 5, "tunableop": "off"}, cuda_device, 0, 1)
+    ab = r["wgrad_stream_autotune"]
+    assert ab is not None and ab["chosen"] in ("side", "serial")
+    assert ab["side_stream_ms"] > 0 and ab["serial_ms"] > 0
+    assert rf._WGRAD_STREAM == (ab["chosen"] == "side")
+    assert r["ms_per_step"] > 0 and r["loss"] == r["loss"]  # finite
