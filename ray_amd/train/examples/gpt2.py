@@ -130,37 +130,40 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
             torch.cuda.synchronize(device)
 
     # Side-stream autotune inside the warmup (RAY_AMD_STREAM_AUTOTUNE=1, default): the last
-    # 4 of >= 5 warmup steps time 2 steps with the weight gradients on the side stream and
-    # 2 with them on the main stream, and the timed steps use the faster mode. Measured on
-    # MI355X boxes right after another multi-stream process exited, the two-stream step ran
-    # ~180 ms against ~64 ms single-stream for ~30 s (profiles/r5/r5p); on a settled box
-    # the side stream wins by ~2 ms. The decision is all-reduced so every rank runs one
-    # mode. Still exactly `warmup` untimed steps.
+    # 4 of >= 5 warmup steps alternate single-stream / side-stream weight gradients (each
+    # step timed on its own), and the timed steps use the side stream unless the single
+    # stream was clearly (>3 %) faster. On a settled box the side stream wins by ~1 ms
+    # (profiles/r5/r5s: 62.7 vs 63.8 ms); on MI355X boxes right after another multi-stream
+    # process exited, two-stream steps ran ~180 ms against ~64 ms single-stream for ~30 s
+    # (profiles/r5/r5p). The decision is all-reduced so every rank runs one mode. Still
+    # exactly `warmup` untimed steps.
     from ray_amd.ops import functional as rf
 
     auto = on_gpu and os.environ.get("RAY_AMD_STREAM_AUTOTUNE", "1") == "1" and \
         c["warmup"] >= 5 and rf._WGRAD_STREAM
-    n_ab = 2
-    t_mark = 0.0
+    first_ab = c["warmup"] - 4
+    times = {True: [], False: []}
     ab = None
     for i in range(c["warmup"]):
-        if auto and i == c["warmup"] - 2 * n_ab:
+        mode = None
+        if auto and i >= first_ab:
+            mode = (i - first_ab) % 2 == 1  # serial, side, serial, side
             sync()
-            t_mark = time.perf_counter()
-        elif auto and i == c["warmup"] - n_ab:
-            sync()
-            side_ms = (time.perf_counter() - t_mark) / n_ab * 1e3
-            rf._WGRAD_STREAM = False  # next steps: everything on the main stream
+            rf._WGRAD_STREAM = mode
             t_mark = time.perf_counter()
         tr.step(batches(i))
+        if mode is not None:
+            sync()
+            times[mode].append(time.perf_counter() - t_mark)
     sync()
     if auto:
-        serial_ms = (time.perf_counter() - t_mark) / n_ab * 1e3
+        side_ms = sum(times[True]) / len(times[True]) * 1e3
+        serial_ms = sum(times[False]) / len(times[False]) * 1e3
         v = torch.tensor([side_ms, serial_ms], device=device, dtype=torch.float64)
         if world > 1:
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         side_ms, serial_ms = float(v[0]), float(v[1])
-        rf._WGRAD_STREAM = not (serial_ms < side_ms)
+        rf._WGRAD_STREAM = not (serial_ms < 0.97 * side_ms)
         ab = {"side_stream_ms": round(side_ms, 3), "serial_ms": round(serial_ms, 3),
               "chosen": "side" if rf._WGRAD_STREAM else "serial"}
     if gemm == "tunableop-tuning":
