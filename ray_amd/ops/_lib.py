@@ -87,6 +87,8 @@ _SIGS = {
     "ra_obsnorm_apply": [c_void_p] * 4 + [c_long, c_int, c_double, c_float, c_float, c_void_p],
     "ra_lt_num_cands": [c_int, c_int] + [c_long] * 6,
     "ra_lt_release_stream": [c_void_p],
+    "ra_embed_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                     c_void_p],
     "ra_lt_num_streams": [],
     "ra_lt_set_choice": [c_int, c_int] + [c_long] * 6 + [c_int],
     "ra_lt_gemm": [c_int, c_int, c_long, c_long, c_long, c_void_p, c_long, c_void_p, c_long,

@@ -964,6 +964,24 @@ class _Embedding(torch.autograd.Function):
         wte, wpe = ctx.wte, ctx.wpe
         B, T, C = dx.shape
         d2 = dx.reshape(-1, C)
+        sw, sp = _grad_sink(wte), _grad_sink(wpe)
+        if (sw is not None and sp is not None and dx.is_cuda and dx.dtype == torch.bfloat16
+                and sw.dtype == torch.float32 and sp.dtype == torch.float32 and C % 8 == 0
+                and sw.is_contiguous() and sp.is_contiguous() and sp.shape[0] >= T):
+            # one HIP pass: scatter-add into the token table, batch-sum into positions
+            ev = getattr(wte, "_ra_sink_event", None)
+            if ev is not None:  # the LM head's side-stream dW accumulation comes first
+                torch.cuda.current_stream(dx.device).wait_event(ev)
+                wte._ra_sink_event = None
+            ids = idx.reshape(-1)
+            ids = ids if ids.dtype == torch.int64 and ids.is_contiguous() else \
+                ids.long().contiguous()
+            d2c = d2.contiguous()
+            check(_lib.lib().ra_embed_bwd(ptr(d2c), ptr(ids), ptr(sw), ptr(sp), B, T, C,
+                                          sw.shape[0], stream_ptr()), "embed_bwd")
+            _grad_done(wte)
+            _grad_done(wpe)
+            return None, None, None
         outs = []
         for p, fill in ((wte, lambda acc: acc.index_add_(0, idx.reshape(-1),
                                                          d2.to(acc.dtype))),

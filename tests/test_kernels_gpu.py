@@ -923,3 +923,30 @@ def test_linear_grouped_wgrad_matches_ungrouped(cuda_device, monkeypatch):
     for a, b in zip(g_flats, u_flats):
         assert _rel(a, b) < 1e-5
     assert g_after == u_after == 5  # 4 weights + 1 fused bias signalled
+
+
+def test_embedding_backward_into_flat_sinks(cuda_device):
+    """ra_embed_bwd (ops/csrc/embed.hip): token-table scatter-add (duplicate ids included)
+    and position batch-sum into pre-filled fp32 sinks vs the fp32 torch reference."""
+    torch.manual_seed(15)
+    B, T, C, V, P = 8, 96, 768, 1000, 128
+    idx = torch.randint(0, 40, (B, T), device=cuda_device)  # many duplicates
+    wte = torch.zeros(V, C, device=cuda_device).bfloat16()
+    wpe = torch.zeros(P, C, device=cuda_device).bfloat16()
+    flat = torch.randn(V * C + P * C, device=cuda_device)
+    ref_flat = flat.clone()
+    wte._ra_grad, wte._ra_direct_grad = flat[:V * C].view(V, C), True
+    wpe._ra_grad, wpe._ra_direct_grad = flat[V * C:].view(P, C), True
+    wte.requires_grad_()
+    wpe.requires_grad_()
+    x = rf.embedding(idx, wte, wpe)
+    dx = torch.randn_like(x)
+    x.backward(dx)
+    torch.cuda.synchronize()
+    d2 = dx.float().reshape(-1, C)
+    ref_wte = ref_flat[:V * C].view(V, C).index_add(0, idx.reshape(-1), d2)
+    ref_wpe = ref_flat[V * C:].view(P, C).clone()
+    ref_wpe[:T] += dx.float().sum(0)
+    assert _rel(wte._ra_grad, ref_wte) < 1e-5
+    assert _rel(wpe._ra_grad, ref_wpe) < 1e-5
+    assert wte.grad is None and wpe.grad is None
