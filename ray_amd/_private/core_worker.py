@@ -1661,6 +1661,10 @@ class CoreWorker:
             with self.lock:
                 self.leases[key].append(lease)
             self._pump(key)
+            if not lease.inflight and PIPELINE_DEPTH > 1:
+                # a fresh worker with nothing queued: take back a task pipelined behind a
+                # running one elsewhere (it would otherwise wait for that task to finish)
+                self._steal_for(key)
             # nothing left to run on it: give it back
             self._maybe_return_lease(lease, force=False)
 

@@ -6,8 +6,8 @@
 // Replaces torch's `index_add_(0, idx, dx.to(fp32))` (a bf16 -> fp32 copy of dx, then an
 // atomic index kernel) and `add_(dx.float().sum(0))` (another fp32 copy and a reduce):
 // dx is read twice as bf16 and nothing else is materialised. Both passes run in one launch
-// on disjoint workgroup ranges: the first N*C/8/256 workgroups scatter 8 columns per lane
-// (16-byte bf16 loads, eight no-return global fp32 atomic adds), the rest reduce one
+// on disjoint workgroup ranges: the first N/4 workgroups scatter one row per wave (lane-
+// linear fp32 atomic adds, 256 contiguous bytes per instruction), the rest reduce one
 // (position, 8-column) cell per lane over the batch. Reference: the embedding gradient of
 // torch.nn.functional.embedding that the reference's GPT-2 benchmark runs through DDP
 // (release/air_tests/air_benchmarks/workloads/torch_benchmark.py).
@@ -22,17 +22,18 @@ __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(
     float* __restrict__ wpe_g, int B, int T, int C, int V, int scatter_blocks) {
   const int C8 = C >> 3;
   if ((int)blockIdx.x < scatter_blocks) {
-    const long item = (long)blockIdx.x * kThreads + threadIdx.x;
-    const long n = item / C8;
+    // one row per wave; lane l adds columns l, l + 64, ...: every atomic instruction of
+    // the wave covers 256 contiguous bytes of the sink row (4-byte words, lane-linear),
+    // the coalesced shape for L2 atomics (per-lane 8-column runs would scatter each
+    // instruction over 2 KB)
+    const long n = (long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     if (n >= (long)B * T) return;
-    const int c8 = (int)(item - n * C8);
     const long tok = idx[n];
     if (tok < 0 || tok >= V) return;
-    float v[8];
-    unpack8(reinterpret_cast<const uint4*>(dx + n * C)[c8], v);
-    float* g = wte_g + tok * C + c8 * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) unsafeAtomicAdd(g + j, v[j]);
+    const int lane = threadIdx.x & 63;
+    const bf16_t* src = dx + n * C;
+    float* g = wte_g + tok * C;
+    for (int c = lane; c < C; c += 64) unsafeAtomicAdd(g + c, bf2f(src[c]));
     return;
   }
   const long item = (long)(blockIdx.x - scatter_blocks) * kThreads + threadIdx.x;
@@ -61,9 +62,9 @@ __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(
 RA_EXPORT int ra_embed_bwd(const void* dx, const long* idx, float* wte_g, float* wpe_g, int B,
                            int T, int C, int V, hipStream_t st) {
   if (B <= 0 || T <= 0 || C <= 0 || C % 8 || V <= 0) return hipErrorInvalidValue;
-  const long scatter_items = (long)B * T * (C / 8);
+  const long rows = (long)B * T;
   const long reduce_items = (long)T * (C / 8);
-  const int sb = (int)((scatter_items + kThreads - 1) / kThreads);
+  const int sb = (int)((rows + kThreads / 64 - 1) / (kThreads / 64));
   const int rb = (int)((reduce_items + kThreads - 1) / kThreads);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(sb + rb), dim3(kThreads), 0, st,
                      (const bf16_t*)dx, idx, wte_g, wpe_g, B, T, C, V, sb);

@@ -151,15 +151,22 @@ def test_force_cancel_kills_a_busy_worker(cluster):
 
 
 def test_fractional_cpus_pack_two_per_cpu(cluster):
+    """8 tasks of 0.5 CPU on 4 CPUs all run at once (max overlap of their run intervals is
+    8; at 1 CPU each it would be 4)."""
+
     @ray.remote(num_cpus=0.5)
     def hold(t):
+        t0 = time.time()
         time.sleep(t)
-        return os.getpid()
+        return t0, time.time()
 
-    t0 = time.time()
-    pids = ray.get([hold.remote(1.0) for _ in range(8)])  # 8 x 0.5 CPU on 4 CPUs: one wave
-    assert time.time() - t0 < 1.9
-    assert len(set(pids)) == 8
+    spans = ray.get([hold.remote(3.0) for _ in range(8)], timeout=120)
+    events = sorted([(a, 1) for a, _ in spans] + [(b, -1) for _, b in spans])
+    cur = peak = 0
+    for _, d in events:
+        cur += d
+        peak = max(peak, cur)
+    assert peak == 8
 
 
 def test_actor_init_error_surfaces_on_method_calls(cluster):

@@ -131,3 +131,20 @@ def test_pipelining_disabled_by_env_matches(monkeypatch):
     assert not cwm.CoreWorker._pipelinable({"nret": 1, "retries": 0})
     assert not cwm.CoreWorker._pipelinable({"nret": -1, "retries": 3})
     assert not cwm.CoreWorker._pipelinable({"nret": 1, "retries": 3, "max_calls": 1})
+
+
+def test_fresh_lease_steals_pipelined_task(two_cpus):
+    """Long tasks saturate the node, so later ones get pipelined behind them. Once a worker
+    frees up (a short task ends), its idle lease takes back a queued long task instead of
+    leaving it behind a running one: all long tasks finish in about two task-lengths, not
+    three."""
+
+    @ray.remote
+    def long(t):
+        time.sleep(t)
+        return 1
+
+    t0 = time.time()
+    refs = [long.remote(1.5) for _ in range(4)]
+    assert sum(ray.get(refs, timeout=60)) == 4
+    assert time.time() - t0 < 4.4  # 2 CPUs: two rounds of 1.5 s (+ startup), never three
