@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--tunableop", default="auto", choices=["off", "tune", "auto"],
                     help="PyTorch TunableOp GEMM selection: 'tune' benchmarks every hipBLASLt/"
                          "rocBLAS solution per GEMM shape during warmup and writes "
-                         "profiles/tunableop/<config>.csv; 'auto' uses that file if present")
+                         "ray_amd/tuned/<config>.csv; 'auto' uses that file if present")
     ap.add_argument("--device", default=None, help="gpt2: 'cpu' runs the launcher on gloo "
                     "(tests)")
     return ap.parse_args()

@@ -6,7 +6,7 @@ into an fp32 gradient buffer: the buffer is the GEMM's C/D operand with beta = 1
 split-K partials are written and re-read. Every problem shape uses the fastest of
 hipBLASLt's heuristic candidates:
 
-  * choices are read from ``profiles/tunableop/lt_f32out.csv`` (committed next to the
+  * choices are read from ``ray_amd/tuned/lt_f32out.csv`` (committed next to the
     TunableOp file for the bf16-output GEMMs);
   * ``RAY_AMD_LT_TUNE=1`` (or ``set_tuning(True)``) times every candidate of a shape on
     its first use (into a scratch buffer) and records the winner; ``save()`` writes the
@@ -29,8 +29,7 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-DEFAULT_FILE = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "profiles", "tunableop",
-                            "lt_f32out.csv")
+DEFAULT_FILE = os.path.join(os.path.dirname(_HERE), "tuned", "lt_f32out.csv")
 
 _lock = threading.Lock()
 _choices: dict | None = None  # key str -> (choice, ms)

@@ -29,10 +29,9 @@ DEFAULTS = dict(model="small", micro_batch=64, seq_len=1024, steps=20, warmup=5,
 
 
 def tunableop_file(model: str, micro_batch: int, seq_len: int) -> str:
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(
-        os.path.abspath(__file__)))))
-    return os.path.join(root, "profiles", "tunableop",
-                        f"gpt2_{model}_mb{micro_batch}_t{seq_len}.csv")
+    # ray_amd/tuned/: shipped with the package (profiles/ is not uploaded to GPU boxes)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return os.path.join(root, "tuned", f"gpt2_{model}_mb{micro_batch}_t{seq_len}.csv")
 
 
 def setup_tunableop(mode: str, src: str, rank: int):
