@@ -40,7 +40,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 20; the data workload defaults to 300: its "
+                         "pipeline prefetches, so a 20-step window times blocks produced "
+                         "during warmup)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gpt2",
                     choices=["gpt2", "ppo", "impala", "data", "microbench", "allreduce"])
@@ -84,7 +87,10 @@ def parse():
                          "ray_amd/tuned/<config>.csv; 'auto' uses that file if present")
     ap.add_argument("--device", default=None, help="gpt2: 'cpu' runs the launcher on gloo "
                     "(tests)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 300 if args.workload == "data" else 20
+    return args
 
 
 def _gpt2_config(args) -> dict:
