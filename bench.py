@@ -140,6 +140,8 @@ def _emit(args, r: dict, mode: str, n_gpus: int):
         "final_loss": round(r["loss"], 4),
         "ddp_allreduce_launches": r.get("ddp_allreduce_launches"),
         "wgrad_stream_autotune": r.get("wgrad_stream_autotune"),
+        "hbm": r.get("hbm"),
+        "gpu_settle_wait_s": _SETTLE_WAIT,
     }
     # self-diagnosing multi-GPU runs: exposed comm, all-reduce launches / bytes and
     # per-bucket bus bandwidth per rank (FlatDDP.read_stats; zeros at world 1)
@@ -181,6 +183,9 @@ def bench_gpt2_bare(args):
     r = run_steps(_gpt2_config(args), dev, rank, world)
     if rank == 0:
         _emit(args, r, "torch.distributed.run (no Ray)", world)
+    from ray_amd.train.examples.gpt2 import release_device_memory
+
+    release_device_memory(dev)
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -315,8 +320,63 @@ def bench_allreduce(args):
     dist.destroy_process_group()
 
 
+def _other_gpu_processes_vram() -> int:
+    """Bytes of HBM that OTHER processes hold on the visible GPU(s), from `rocm-smi
+    --showpids` (KFD process table; processes of this job — our torchrun siblings — are
+    excluded). -1 when rocm-smi is unavailable."""
+    import shutil
+    import subprocess
+
+    exe = shutil.which("rocm-smi") or "/opt/rocm/bin/rocm-smi"
+    if not os.path.exists(exe):
+        return -1
+    try:
+        out = subprocess.run([exe, "--showpids"], capture_output=True, text=True,
+                             timeout=20).stdout
+    except (OSError, subprocess.SubprocessError):
+        return -1
+    me, parent = os.getpid(), os.getppid()
+    total = 0
+    for line in out.splitlines():
+        f = line.split()
+        if len(f) < 4 or not f[0].isdigit() or not f[3].isdigit():
+            continue
+        pid = int(f[0])
+        if pid == me:
+            continue
+        try:
+            with open(f"/proc/{pid}/stat") as fh:
+                if int(fh.read().rsplit(")", 1)[1].split()[1]) == parent:
+                    continue  # a sibling rank of this job
+        except (OSError, ValueError, IndexError):
+            pass  # gone from /proc but still in the KFD table: its teardown is running
+        total += int(f[3])
+    return total
+
+
+def _settle_gpu(max_wait_s: float) -> float:
+    """Wait (before any GPU work) until no other process holds HBM on this GPU. A process
+    that exits with tens of GB allocated stays in the KFD table with that memory for
+    ~30 s while the driver tears it down; a two-stream step started in that window ran
+    140-316 ms instead of 62-64 (profiles/r5/r5p, r5y, r5aa). Returns seconds waited."""
+    t0 = time.time()
+    while time.time() - t0 < max_wait_s:
+        held = _other_gpu_processes_vram()
+        if held < (1 << 30):  # -1 (no rocm-smi) or under 1 GiB
+            break
+        time.sleep(2.0)
+    return round(time.time() - t0, 1)
+
+
+_SETTLE_WAIT = None
+
+
 def main():
+    global _SETTLE_WAIT
     args = parse()
+    if args.workload in ("gpt2", "allreduce") and args.device != "cpu" and \
+            os.environ.get("RAY_AMD_BENCH_SETTLE", "1") == "1":
+        _SETTLE_WAIT = _settle_gpu(float(os.environ.get("RAY_AMD_BENCH_SETTLE_MAX_S", "120")))
     if args.workload == "gpt2":
         if args.no_ray:
             bench_gpt2_bare(args)
