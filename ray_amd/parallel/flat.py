@@ -455,6 +455,7 @@ class FlatAdamW:
 
         if self.use_hip:
             rf.join_side_streams()  # weight gradients queued on the side stream
+            rf.bound_run_ahead()
         rf.bump_weights_epoch()  # the kernel updates p16 in place: cached copies go stale
         self.step_count += 1
         lr = self.lr if lr is None else lr

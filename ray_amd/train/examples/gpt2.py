@@ -226,8 +226,13 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
     flops = tr.model.flops_per_token(c["seq_len"]) * tokens
     mem = None
     if on_gpu:
+        st = torch.cuda.memory_stats(device)
         mem = {"max_allocated_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
-               "reserved_gb": round(torch.cuda.memory_reserved(device) / 2**30, 2)}
+               "reserved_gb": round(torch.cuda.memory_reserved(device) / 2**30, 2),
+               "alloc_retries": int(st.get("num_alloc_retries", 0)),
+               "device_mallocs": int(st.get("num_device_alloc", 0)),
+               "device_frees": int(st.get("num_device_free", 0)),
+               "segments": int(st.get("segment.all.current", 0))}
     return {
         "tokens_per_sec": tokens / dt,
         "ms_per_step": dt / c["steps"] * 1000,
