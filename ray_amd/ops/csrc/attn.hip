@@ -608,11 +608,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // dQ: workgroup = 128 queries; forward orientation (S^T, lanes = queries).
 // PF as in attn_bwd_dkdv_kernel (K/V tiles); ra_knobs[12] = 1 selects PF 1.
 // ILP: both 32-key halves of a tile in flight (as attn_bwd_dkdv_kernel's ILP).
-template <int PF = 2, bool ILP = false>
+// DELTA: the kernel computes delta = rowsum(dO * O) of its own queries (each lane already
+// holds half of its query's dO row; O is read the same way and the halves meet by one
+// permlane32 swap) and writes it for the dK/dV kernel that runs after it: this replaces the
+// attn_bwd_pre_kernel pass (a separate read of O and dO, 50 us per layer at B64 T1024 H12).
+template <int PF = 2, bool ILP = false, bool DELTA = false>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
-    const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-    int T, int H, float sc_log2, float scale) {
+    const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+    int T, int H, float sc_log2, float scale, const bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS];  // [buf][K, V]
   const int nqb = T / 128;
   const int L = xcd_block(blockIdx.x, gridDim.x);
@@ -633,7 +637,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     df[kk] = ld8(dout + ((long)b * T + qrow) * C + h * HD + 16 * kk + 8 * hh);
   }
   const float nlq = -lse[(long)bh * T + qrow] / sc_log2;
-  const float ndel = -delta[(long)bh * T + qrow];
+  float ndel;
+  if constexpr (DELTA) {
+    float part = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bf16x8_t of = ld8(out + ((long)b * T + qrow) * C + h * HD + 16 * kk + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)df[kk][j];
+    }
+    const float dl = half_sum(part);
+    if (hh == 0) delta[(long)bh * T + qrow] = dl;
+    ndel = -dl;
+  } else {
+    ndel = -delta[(long)bh * T + qrow];
+  }
   f32x16 dq[2] = {};
   const int ntiles = (q0 + 128) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
@@ -802,21 +820,36 @@ RA_EXPORT int ra_attn_bwd(const void* qkv, const void* out, const void* dout, co
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
   const long rows = (long)B * T * H;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                     (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
   auto kkv = attn_bwd_dkdv_kernel<false, 2>;
   if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
   else if (ra_knobs[11] == 2) kkv = attn_bwd_dkdv_kernel<false, 1, true>;
+  // ra_knobs[13] = 1: the separate delta pre-pass and the dQ kernel after dK/dV (round 4's
+  // order); default: dQ first, computing delta on the way (attn_bwd_dq_kernel DELTA)
+  if (ra_knobs[13] == 1) {
+    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                       (const bf16_t*)out, (const bf16_t*)dout, delta, B * T, T, H);
+    hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
+                       (float*)nullptr, T, H, sc_log2, scale, 0);
+    auto kq = attn_bwd_dq_kernel<2>;
+    if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
+    else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true>;
+    else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true>;
+    hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
+                       sc_log2, scale, (const bf16_t*)nullptr);
+    return hipGetLastError();
+  }
+  auto kq = attn_bwd_dq_kernel<2, false, true>;
+  if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1, false, true>;
+  else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true, true>;
+  else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true, true>;
+  hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
+                     sc_log2, scale, (const bf16_t*)out);
   hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);
-  auto kq = attn_bwd_dq_kernel<2>;
-  if (ra_knobs[12] == 1) kq = attn_bwd_dq_kernel<1>;
-  else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true>;
-  else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true>;
-  hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
-                     sc_log2, scale);
   return hipGetLastError();
 }
 
@@ -876,7 +909,7 @@ RA_EXPORT int ra_attn_bwd_q(const void* qkv, const void* dout, const float* lse,
   else if (ra_knobs[12] == 2) kq = attn_bwd_dq_kernel<1, true>;
   else if (ra_knobs[12] == 3) kq = attn_bwd_dq_kernel<2, true>;
   hipLaunchKernelGGL(kq, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, T, H,
-                     sc_log2, scale);
+                     (const bf16_t*)qkv, (const bf16_t*)dout, lse, (float*)delta,
+                     (bf16_t*)dqkv, T, H, sc_log2, scale, (const bf16_t*)nullptr);
   return hipGetLastError();
 }
