@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ g,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N,
-    int D) {
+    int D, float* __restrict__ o0, float* __restrict__ o1, float* __restrict__ o2) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [NP][D]
   for (int i = threadIdx.x; i < NP * D; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
@@ -354,6 +354,16 @@ __global__ __launch_bounds__(256) void ln_bwd2_kernel(
       for (int j = 0; j < 4; ++j) atomicAdd(&lds[k * D + col + j], acc[k][i][j]);
   }
   __syncthreads();
+  if (o0) {
+    // fp32 sinks accumulated in place (the flat gradient): the block's column sums go
+    // straight in with lane-linear float atomics (P adds per address, 256 contiguous bytes
+    // per wave instruction), instead of a partial slab and one colsum launch per sink
+    for (int i = threadIdx.x; i < NP * D; i += blockDim.x) {
+      const int k = i / D, c = i - k * D;
+      unsafeAtomicAdd((k == 0 ? o0 : k == 1 ? o1 : o2) + c, lds[i]);
+    }
+    return;
+  }
   const size_t P = gridDim.x;
   for (int i = threadIdx.x; i < NP * D; i += blockDim.x) {
     const int k = i / D, c = i - k * D;
@@ -456,10 +466,17 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
   float* scr = work + (size_t)NP * P * D;
   const size_t lds = (size_t)NP * D * sizeof(float);
   if (ln_bwd_v2(N, D)) {
+    // fp32 sinks accumulated in place: column sums by atomics inside the kernel
+    // (ra_knobs[14] = 1: partial slabs + colsum launches as before)
+    const bool direct = !(flags & kColsumBF16) && (flags & kColsumAcc) && ra_knobs[2] &&
+                        ra_knobs[14] != 1;
+    float* o0 = direct ? (float*)dg : nullptr;
+    float* o1 = direct ? (float*)db : nullptr;
+    float* o2 = direct ? (float*)dbias : nullptr;
 #define L2K(V, NPV, R, KK)                                                                     \
   hipLaunchKernelGGL((ln_bwd2_kernel<V, NPV, R, KK>), dim3(P), dim3(256), lds, st,              \
                      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)g, mean, rstd,         \
-                     (const bf16_t*)dres, (bf16_t*)dx, work, N, D)
+                     (const bf16_t*)dres, (bf16_t*)dx, work, N, D, o0, o1, o2)
 #define L2(V, NPV, R)                                        \
   if (ra_knobs[3] == 3) L2K(V, NPV, R, 3); else L2K(V, NPV, R, 2)
 #define L2V(V)                                       \
@@ -477,6 +494,7 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
 #undef L2V
 #undef L2
 #undef L2K
+    if (direct) return hipGetLastError();
     void* outs[3] = {dg, db, dbias};
     for (int k = 0; k < NP; ++k)
       colsum_launch(work + (size_t)k * P * D, scr + (size_t)k * kColsumSplits * D, outs[k], P,

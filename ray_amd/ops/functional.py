@@ -500,7 +500,14 @@ _side: dict = {}
 def _side_stream(device):
     st = _side.get(device)
     if st is None:
-        st = _side[device] = torch.cuda.Stream(device)
+        cus = os.environ.get("RAY_AMD_SIDE_CUS")
+        if cus:  # experiment: the side stream on a CU subset (ops/cu_mask.py)
+            from . import cu_mask
+
+            st = cu_mask.masked_stream(device, cu_mask.cu_range(device, cus))
+        else:
+            st = torch.cuda.Stream(device)
+        _side[device] = st
     return st
 
 

@@ -109,6 +109,12 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         # side stream's weight-gradient workgroups when both have work queued
         torch.cuda.set_stream(torch.cuda.Stream(device, priority=min(
             torch.cuda.Stream.priority_range())))
+    if on_gpu and os.environ.get("RAY_AMD_MAIN_CUS"):
+        # experiment: the step's main stream on a CU subset disjoint from the side stream's
+        from ray_amd.ops import cu_mask
+
+        torch.cuda.set_stream(cu_mask.masked_stream(
+            device, cu_mask.cu_range(device, os.environ["RAY_AMD_MAIN_CUS"])))
     mcfg = getattr(GPT2Config, c["model"])()
     gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
     tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],

@@ -425,9 +425,17 @@ def test_image_normalize_vector_path(cuda_device, C):
     assert torch.allclose(yb.float().cpu(), yr, atol=2e-2, rtol=8e-3)
 
 
-@pytest.mark.parametrize("mode", ["fused", "split", "split2"])
+@pytest.mark.parametrize("mode", ["fused", "split", "split2", "split_pre"])
 @pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2), (2, 128, 1)])
-def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch):
+def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch, request):
+    """split: dQ (computing delta) then dK/dV; split_pre: round 4's separate delta pre-pass
+    (ra_knobs[13] = 1)."""
+    from ray_amd.ops import _lib
+
+    if mode == "split_pre":
+        _lib.lib().ra_set_knob(13, 1)
+        request.addfinalizer(lambda: _lib.lib().ra_set_knob(13, 0))
+        mode = "split"
     monkeypatch.setattr(rf, "_ATTN_BWD", mode)
     torch.manual_seed(9)
     D = 64
@@ -721,6 +729,52 @@ def test_layernorm_bwd_v2_matches_fp32(cuda_device, N, D, res):
         pairs = ((h, hr), (w, wr), (b, br))
     for a, r in pairs:
         assert _rel(a.grad, r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("slabs", [False, True])
+@pytest.mark.parametrize("N,D,res", [(5003, 768, True), (65536, 768, False)])
+def test_layernorm_bwd_fp32_sinks_accumulate(cuda_device, N, D, res, slabs):
+    """Flat-gradient contract of ra_layernorm_bwd (fp32 sinks, accumulate): dgamma, dbeta
+    and the residual-bias colsum are ADDED onto non-zero sinks, by in-kernel atomics
+    (default) or partial slabs + colsum launches (ra_knobs[14] = 1)."""
+    from ray_amd.ops import _lib
+    from ray_amd.ops._lib import check, ptr, stream_ptr
+
+    L = _lib.lib()
+    torch.manual_seed(5)
+    x = torch.randn(N, D, device=cuda_device).bfloat16()
+    w = (1 + 0.1 * torch.randn(D, device=cuda_device)).bfloat16()
+    dy = torch.randn(N, D, device=cuda_device).bfloat16()
+    dres = torch.randn(N, D, device=cuda_device).bfloat16() if res else None
+    xf = x.float()
+    mean = xf.mean(1)
+    rstd = torch.rsqrt(xf.var(1, unbiased=False) + 1e-5)
+    xh = (xf - mean[:, None]) * rstd[:, None]
+    g = dy.float() * w.float()
+    dxr = (g - g.mean(1, keepdim=True) - xh * (g * xh).mean(1, keepdim=True)) * rstd[:, None]
+    if res:
+        dxr = dxr + dres.float()
+    init = [torch.randn(D, device=cuda_device) for _ in range(3)]
+    sinks = [t.clone() for t in init]
+    dx = torch.empty_like(x)
+    work = torch.empty(L.ra_layernorm_bwd_work(N, D), device=cuda_device, dtype=torch.float32)
+    L.ra_set_knob(3, 0)
+    L.ra_set_knob(14, 1 if slabs else 0)
+    try:
+        check(L.ra_layernorm_bwd(ptr(dy), ptr(x), ptr(w), ptr(mean), ptr(rstd), ptr(dres),
+                                 ptr(dx), ptr(sinks[0]), ptr(sinks[1]),
+                                 ptr(sinks[2]) if res else None, ptr(work), N, D, 2,
+                                 stream_ptr()), "layernorm_bwd")
+        torch.cuda.synchronize()
+    finally:
+        L.ra_set_knob(14, 0)
+    assert _rel(dx, dxr) < 2e-2
+    assert _rel(sinks[0] - init[0], (dy.float() * xh).sum(0)) < 1e-3
+    assert _rel(sinks[1] - init[1], dy.float().sum(0)) < 1e-3
+    if res:
+        assert _rel(sinks[2] - init[2], dx.float().sum(0)) < 1e-2
+    else:
+        assert torch.equal(sinks[2], init[2])
 
 
 @pytest.mark.parametrize("S", [1, 2, 3, 4, 8, 16])
