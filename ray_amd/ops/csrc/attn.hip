@@ -352,15 +352,22 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 // ILP (non-FUSED, with PF 1): both 32-query halves of a tile are in flight at once — the
 // S / dP chains of both halves issue first, then each half's softmax VALU runs while the
 // other half's MFMAs execute (the 17 VGPRs PF 1 frees hold the second half's S / dP).
-template <bool FUSED, int PF = 2, bool ILP = false>
+// RCG (PF 1, not FUSED, ra_knobs[11] = 3; with ILP it spills): the row constants come straight from global
+// memory into registers (16 broadcast buffer loads per tile, issued at the top of the tile and
+// consumed after the S / dP chains, which start from zero accumulators: p = exp2(c S - lse),
+// dS = p (dP - delta)) instead of through LDS. The kernel then needs exactly 32 KB of LDS,
+// which fits beside a 128 KB weight-gradient workgroup of the side stream on one CU (160 KB);
+// with the 1 KB LDS row-constant buffer it did not (profiles/r5/README.md).
+template <bool FUSED, int PF = 2, bool ILP = false, bool RCG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     float* __restrict__ dq_ws, int T, int H, float sc_log2, float scale, int dbg) {
+  static_assert(!RCG || (PF == 1 && !FUSED), "RCG: PF 1 split form only");
   // [buf][Q, dO] images, then per buf 64 x (-lse/c) and 64 x (-delta); FUSED: + K image
   // [128][64] and dS^T image [128][64]
   __shared__ __attribute__((aligned(16)))
-  bf16_t lds[2 * 2 * TILE_ELEMS + 2 * 2 * 64 * 2 + (FUSED ? 4 * TILE_ELEMS : 0)];
+  bf16_t lds[2 * 2 * TILE_ELEMS + (RCG ? 0 : 2 * 2 * 64 * 2) + (FUSED ? 4 * TILE_ELEMS : 0)];
   float* rowc = reinterpret_cast<float*>(lds + 4 * TILE_ELEMS);  // [buf][2][64]
   bf16_t* Kimg = lds + 4 * TILE_ELEMS + 512;
   bf16_t* dsT = Kimg + 2 * TILE_ELEMS;
@@ -414,7 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto load_qd = [&](QD& x, int t) __attribute__((always_inline)) {
     tile_load_buf(x.q, rq, taq, t * 64 * (int)tok * 2);
     tile_load_buf(x.d, rd, tad, t * 64 * C * 2);
-    if (threadIdx.x < 128) {  // waves 0 / 1: -lse/c / -delta of the tile's 64 rows
+    if (!RCG && threadIdx.x < 128) {  // waves 0 / 1: -lse/c / -delta of the tile's 64 rows
       // (the b32 builtin returns the raw 32 bits as an integer)
       const float v = __builtin_bit_cast(
           float, __builtin_amdgcn_raw_buffer_load_b32(threadIdx.x < 64 ? rl : rdl,
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     bf16_t* d = lds + buf * 2 * TILE_ELEMS;
     tile_store(x.q, d);
     tile_store(x.d, d + TILE_ELEMS);
-    if (threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = x.rc;
+    if (!RCG && threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = x.rc;
   };
   // DIAG is a template-like constant: the causal mask costs 3 VALU per score element
   // (compare, select, index add), so only the diagonal tiles instantiate it — the
@@ -442,8 +449,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const float* nl = rowc + cur * 128;
       const float* nd = nl + 64;
       f32x16 s[2], dp[2];
+      [[maybe_unused]] f32x16 rl_[2], rd_[2];  // RCG: lse / delta of the accumulator rows
+      if constexpr (RCG) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int off = (q0 + 32 * qt + 8 * g + 4 * hh) * 4;
+            const u32x4 a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, off, 0, 0));
+            const u32x4 d = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rdl, off, 0, 0));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              rl_[qt][4 * g + j] = __uint_as_float(a[j]);
+              rd_[qt][4 * g + j] = __uint_as_float(d[j]);
+            }
+          }
+      }
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
+        if constexpr (RCG) {
+          s[qt] = f32x16{};
+          dp[qt] = f32x16{};
+        } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 a = *reinterpret_cast<const float4*>(nl + 32 * qt + 8 * g + 4 * hh);
@@ -452,6 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           s[qt][4 * g + 3] = a.w;
           dp[qt][4 * g] = d.x; dp[qt][4 * g + 1] = d.y; dp[qt][4 * g + 2] = d.z;
           dp[qt][4 * g + 3] = d.w;
+        }
         }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
@@ -463,10 +491,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int qt = 0; qt < 2; ++qt) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = fast_exp2(s[qt][i] * sc_log2);
+          float p = RCG ? fast_exp2(fmaf(s[qt][i], sc_log2, -rl_[qt][i]))
+                        : fast_exp2(s[qt][i] * sc_log2);
           if (diag && key > q0 + 32 * qt + crow(i, hh)) p = 0.f;
           s[qt][i] = p;
-          dp[qt][i] = p * dp[qt][i];
+          dp[qt][i] = RCG ? p * (dp[qt][i] - rd_[qt][i]) : p * dp[qt][i];
         }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -489,12 +518,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int qt = 0; qt < 2; ++qt) {
         // S' = Q K^T - LSE/c ; dP' = dO V^T - delta   (rows q, cols = this wave's keys)
         f32x16 s, dp;
+        [[maybe_unused]] f32x16 rl_, rd_;
+        if constexpr (RCG) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int off = (q0 + 32 * qt + 8 * g + 4 * hh) * 4;
+            const u32x4 a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, off, 0, 0));
+            const u32x4 d = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rdl, off, 0, 0));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              rl_[4 * g + j] = __uint_as_float(a[j]);
+              rd_[4 * g + j] = __uint_as_float(d[j]);
+            }
+          }
+          s = f32x16{};
+          dp = f32x16{};
+        } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 a = *reinterpret_cast<const float4*>(nl + 32 * qt + 8 * g + 4 * hh);
           const float4 d = *reinterpret_cast<const float4*>(nd + 32 * qt + 8 * g + 4 * hh);
           s[4 * g] = a.x; s[4 * g + 1] = a.y; s[4 * g + 2] = a.z; s[4 * g + 3] = a.w;
           dp[4 * g] = d.x; dp[4 * g + 1] = d.y; dp[4 * g + 2] = d.z; dp[4 * g + 3] = d.w;
+        }
         }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
@@ -504,10 +550,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = fast_exp2(s[i] * sc_log2);
+          float p = RCG ? fast_exp2(fmaf(s[i], sc_log2, -rl_[i])) : fast_exp2(s[i] * sc_log2);
           if (diag && key > q0 + 32 * qt + crow(i, hh)) p = 0.f;
-          s[i] = p;              // P
-          dp[i] = p * dp[i];     // dS (wrt scaled scores)
+          s[i] = p;                                   // P
+          dp[i] = RCG ? p * (dp[i] - rd_[i]) : p * dp[i];  // dS (wrt scaled scores)
         }
         if (FUSED) {  // dS^T rows = this lane's key, 4 consecutive q per 8-byte write
 #pragma unroll
@@ -823,6 +869,7 @@ RA_EXPORT int ra_attn_bwd(const void* qkv, const void* out, const void* dout, co
   auto kkv = attn_bwd_dkdv_kernel<false, 2>;
   if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
   else if (ra_knobs[11] == 2) kkv = attn_bwd_dkdv_kernel<false, 1, true>;
+  else if (ra_knobs[11] == 3) kkv = attn_bwd_dkdv_kernel<false, 1, false, true>;
   // ra_knobs[13] = 1: the separate delta pre-pass and the dQ kernel after dK/dV (round 4's
   // order); default: dQ first, computing delta on the way (attn_bwd_dq_kernel DELTA)
   if (ra_knobs[13] == 1) {
@@ -893,6 +940,7 @@ RA_EXPORT int ra_attn_bwd_kv(const void* qkv, const void* dout, const float* lse
   auto kkv = attn_bwd_dkdv_kernel<false, 2>;
   if (ra_knobs[11] == 1) kkv = attn_bwd_dkdv_kernel<false, 1>;
   else if (ra_knobs[11] == 2) kkv = attn_bwd_dkdv_kernel<false, 1, true>;
+  else if (ra_knobs[11] == 3) kkv = attn_bwd_dkdv_kernel<false, 1, false, true>;
   hipLaunchKernelGGL(kkv, dim3(B * H * (T / 128)), dim3(256), 0, st,
                      (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv,
                      (float*)nullptr, T, H, sc_log2, scale, 0);

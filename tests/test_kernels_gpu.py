@@ -425,16 +425,21 @@ def test_image_normalize_vector_path(cuda_device, C):
     assert torch.allclose(yb.float().cpu(), yr, atol=2e-2, rtol=8e-3)
 
 
-@pytest.mark.parametrize("mode", ["fused", "split", "split2", "split_pre"])
+@pytest.mark.parametrize("mode", ["fused", "split", "split2", "split_pre", "split_rcg"])
 @pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2), (2, 128, 1)])
 def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch, request):
     """split: dQ (computing delta) then dK/dV; split_pre: round 4's separate delta pre-pass
-    (ra_knobs[13] = 1)."""
+    (ra_knobs[13] = 1); split_rcg: dK/dV reading its row constants into registers
+    (ra_knobs[11] = 3)."""
     from ray_amd.ops import _lib
 
     if mode == "split_pre":
         _lib.lib().ra_set_knob(13, 1)
         request.addfinalizer(lambda: _lib.lib().ra_set_knob(13, 0))
+        mode = "split"
+    elif mode == "split_rcg":  # dK/dV with the row constants in registers (32 KB LDS)
+        _lib.lib().ra_set_knob(11, 3)
+        request.addfinalizer(lambda: _lib.lib().ra_set_knob(11, 2))
         mode = "split"
     monkeypatch.setattr(rf, "_ATTN_BWD", mode)
     torch.manual_seed(9)
