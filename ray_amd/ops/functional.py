@@ -804,14 +804,18 @@ _xent_streams: dict = {}
 # single handle hung the same way even with per-stream workspaces, while a stream-K dW on a
 # side stream through a different handle drained. Side-stream GEMMs therefore only go
 # through ops/lt, which keeps a hipBLASLt handle and a workspace per stream.
-def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index):
+def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index,
+                       side_dw=False):
     """Chunked LM head + CE, software-pipelined over two streams:
 
         main:  L0 L1 | dh0 dW0 | L2 | dh1 dW1 | L3 ...      (GEMMs, issue order = data order)
         xent:     X0 |   X1    |    X2  ...                 (X_i after L_i, before dh_i/dW_i)
 
     X_{i+1} runs while dh_i / dW_i run. Two logits buffers suffice: L_{i+2} is issued on the
-    main stream after dh_i / dW_i, the last readers of its buffer."""
+    main stream after dh_i / dW_i, the last readers of its buffer. With ``side_dw`` every dW_i
+    runs on the weight-gradient side stream instead (after X_i), and L_{i+2} also waits for
+    it; the memory-bound cross-entropy pass (no LDS) shares CUs with the GEMMs, which the
+    one-chunk form cannot overlap with anything."""
     dev = h2.device
     N = h2.shape[0]
     xs = _xent_streams.get(dev)
@@ -821,11 +825,15 @@ def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignor
     bufs = [torch.empty((ch, Vp), device=dev, dtype=h2.dtype) for _ in range(2)]
     starts = list(range(0, N, ch))
     done_x = [None] * len(starts)
+    done_w = [None] * len(starts)
+    side = _side_stream(dev) if side_dw and dw is not None else None
 
     def logits(i):
         s0 = starts[i]
         e = min(N, s0 + ch)
         lg = bufs[i % 2][: e - s0]
+        if i >= 2 and done_w[i - 2] is not None:
+            main.wait_event(done_w[i - 2])  # dW_{i-2} on the side stream read this buffer
         torch.mm(h2[s0:e], wt, out=lg)
         ev = torch.cuda.Event()
         ev.record(main)
@@ -844,10 +852,20 @@ def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignor
             logits(i + 1)
         main.wait_event(done_x[i])
         lg = bufs[i % 2][: e - s0]
+        if side is not None:  # dW_i beside dh_i: it needs only X_i
+            side.wait_event(done_x[i])
+            with torch.cuda.stream(side):
+                _lm_head_dw(lg, h2[s0:e], dw, i == 0, side=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            done_w[i] = ev
         if dh is not None:
             torch.mm(lg, w, out=dh[s0:e])
-        if dw is not None:
+        if dw is not None and side is None:
             _lm_head_dw(lg, h2[s0:e], dw, i == 0)
+    if side is not None:
+        for t_ in bufs + [h2, dw]:
+            t_.record_stream(side)
 
 
 # LM-head weight gradient: "hip" = the wgrad kernel (split count from ra_wgrad_splits: 3
@@ -905,8 +923,11 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         wt = w.t()
         ctx.side_dw = False
         if h.is_cuda and N > ch:
+            side_dw = (dw is not None and _WGRAD_STREAM and _LMHEAD_DW_SIDE
+                       and _grad_sink(w) is not None)
             _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp,
-                               ignore_index)
+                               ignore_index, side_dw)
+            ctx.side_dw = side_dw
         else:  # one chunk (the GPT-2 bench: 65536 tokens), or CPU: all on this stream
             side_dw = (dw is not None and h.is_cuda and N <= ch and _WGRAD_STREAM
                        and _LMHEAD_DW_SIDE and _grad_sink(w) is not None)

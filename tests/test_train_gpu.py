@@ -72,11 +72,14 @@ def test_flat_fp32_grads_match_autograd(cuda_device):
         assert _rel(p._ra_grad, pr.grad) < 3e-2, n
 
 
+@pytest.mark.parametrize("chunk", [None, 256])
 @pytest.mark.parametrize("mode", ["hip", "lt"])
-def test_lm_head_side_stream_dw_matches_main_stream(cuda_device, monkeypatch, mode):
+def test_lm_head_side_stream_dw_matches_main_stream(cuda_device, monkeypatch, mode, chunk):
     """The tied LM head's dW on the wgrad side stream (and its scaled accumulation into the
     flat sink, ordered before the embedding's scatter by an event) gives the gradients of
-    the all-main-stream path, for 2 micro-batches accumulated into one flat buffer."""
+    the all-main-stream path, for 2 micro-batches accumulated into one flat buffer.
+    chunk=256: the pipelined form (4 chunks of the 1024 tokens, cross-entropy on its own
+    stream, dW_i on the side stream, logits buffers reused after dW_{i-2})."""
     import copy
 
     from ray_amd.models.gpt2 import GPT2
@@ -91,6 +94,8 @@ def test_lm_head_side_stream_dw_matches_main_stream(cuda_device, monkeypatch, mo
     for side in (False, True):
         monkeypatch.setattr(rf, "_LMHEAD_DW_SIDE", side)
         m = copy.deepcopy(base)
+        if chunk:
+            m.lm_head_chunk = chunk
         flat = FlatParams(m)
         for i in range(2):
             (m(idx[i], tgt[i]) * (0.5 + i)).backward()
