@@ -374,7 +374,10 @@ _SETTLE_WAIT = None
 def main():
     global _SETTLE_WAIT
     args = parse()
-    if args.workload in ("gpt2", "allreduce") and args.device != "cpu" and \
+    # not under a profiler: its preloaded library has initialised the GPU before main(),
+    # and the settle check starts rocm-smi (a Python script) as a child process
+    profiled = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+    if args.workload in ("gpt2", "allreduce") and args.device != "cpu" and not profiled and \
             os.environ.get("RAY_AMD_BENCH_SETTLE", "1") == "1":
         _SETTLE_WAIT = _settle_gpu(float(os.environ.get("RAY_AMD_BENCH_SETTLE_MAX_S", "120")))
     if args.workload == "gpt2":
