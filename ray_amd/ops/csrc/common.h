@@ -151,9 +151,13 @@ __global__ __launch_bounds__(256) void colsum_atomic(const float* __restrict__ p
 }  // namespace
 
 // Runtime tuning knobs (A/B without rebuilding; set through ra_set_knob, defined in
-// layernorm.hip): 0 = LayerNorm-bwd partial rows cap, 1 = column-partial waves target,
-// 2 = fp32 colsum via atomics (1) or two-stage (0), 9 = attention forward variant
-// (0 = attn_fwd_kernel, 1 = attn_fwd_kernel2).
+// layernorm.hip, or RAY_AMD_KNOBS="k=v,..."): 0 = LayerNorm-bwd partial rows cap, 1 =
+// column-partial waves target, 2 = fp32 colsum via atomics (1) or two-stage (0), 3 = v1
+// LayerNorm / column-partial kernels (1), 4 = LayerNorm-bwd v2 blocks, 5 = gemm.hip
+// schedule, 6 = fused attention-bwd diagnostics, 7 = conv partial target, 11 = attention
+// dK/dV variant (2 = ILP default, 1 = PF 1, 0 = PF 2, 3 = row constants in registers), 12 =
+// attention dQ variant, 13 = attention delta pre-pass (1) instead of inside dQ, 14 =
+// LayerNorm-bwd partial slabs (1) instead of in-kernel atomics into fp32 sinks.
 extern int ra_knobs[16];
 
 namespace {
