@@ -178,12 +178,18 @@ __device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* img) {
 }
 
 // ============================================================================ forward
+// QB = 32-query blocks per wave (1: a workgroup covers 128 queries; 2: 256 queries, every K
+// row fragment and V transposed fragment read from LDS feeds two MFMAs, and each wave has
+// two independent S / softmax / PV chains in flight; ra_knobs[9] = 1 selects QB 2).
+template <int QB>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                        bf16_t* __restrict__ out,
                                                        float* __restrict__ lse, int T, int H,
                                                        float sc_log2) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * 2 * TILE_ELEMS];  // [buf][K,V]
-  const int nqb = T / 128;
+  constexpr int QW = 32 * QB;    // queries per wave
+  constexpr int QBLK = 4 * QW;   // queries per workgroup
+  const int nqb = T / QBLK;
   const int L = xcd_block(blockIdx.x, gridDim.x);
   const int qb = nqb - 1 - L % nqb;  // heaviest causal blocks first
   const int bh = L / nqb;
@@ -193,15 +199,24 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   const bf16_t* base = qkv + (long)b * T * tok + h * HD;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const LaneOffs lo(lane);
-  const int q0 = qb * 128;
-  const int qrow = q0 + 32 * w + r;
-  bf16x8_t qf[4];
+  const int q0 = qb * QBLK;
+  const int wave_qmin = q0 + QW * w;
+  const int wave_qmax = wave_qmin + QW - 1;
+  int qrow[QB];
+  bf16x8_t qf[QB][4];
+  f32x16 o[QB][2];
+  float m_run[QB], l_run[QB];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) qf[kk] = ld8(base + (long)qrow * tok + 16 * kk + 8 * hh);
-  f32x16 o[2] = {};
-  float m_run = -INFINITY, l_run = 0.f;
-  const int ntiles = (q0 + 128) / 64;
-  const int wave_qmax = q0 + 32 * w + 31;
+  for (int j = 0; j < QB; ++j) {
+    qrow[j] = wave_qmin + 32 * j + r;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) qf[j][kk] = ld8(base + (long)qrow[j] * tok + 16 * kk + 8 * hh);
+    o[j][0] = f32x16{};
+    o[j][1] = f32x16{};
+    m_run[j] = -INFINITY;
+    l_run[j] = 0.f;
+  }
+  const int ntiles = (q0 + QBLK) / 64;
   KV A, B;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (T - 1) * (int)tok * 2 + 3 * C * 2,
@@ -222,67 +237,76 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     const bf16_t* Ks = lds + (t & 1) * 2 * TILE_ELEMS;
     const bf16_t* Vs = Ks + TILE_ELEMS;
     const int kv0 = t * 64;
-    {
-      f32x16 st[2];
+    f32x16 st[QB][2];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        st[kt] = f32x16{};
+    for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          st[kt] = mfma32(ld8(Ks + 2048 * kt + lo.row[kk]), qf[kk], st[kt]);
+      for (int j = 0; j < QB; ++j) st[j][kt] = f32x16{};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8_t kfrag = ld8(Ks + 2048 * kt + lo.row[kk]);
+#pragma unroll
+        for (int j = 0; j < QB; ++j) st[j][kt] = mfma32(kfrag, qf[j][kk], st[j][kt]);
       }
+    }
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
       if (diag) {  // diagonal tile: mask keys > query
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if (kv0 + 32 * kt + crow(i, hh) > qrow) st[kt][i] = -INFINITY;
+            if (kv0 + 32 * kt + crow(i, hh) > qrow[j]) st[j][kt][i] = -INFINITY;
       }
-      float mt = st[0][0];
+      float mt = st[j][0][0];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, st[kt][i]);
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, st[j][kt][i]);
       mt = half_max(mt) * sc_log2;
       // Lazy rescaling: the running max moves (and O / l are rescaled) only when some
       // query's tile max exceeds it by more than 8 (log2 units). Otherwise the stale max
       // stays, p <= 2^8 — exact in fp32, and the final O / l is unchanged: the common tile
       // skips the 32 multiplies of the O rescale and the exp of alpha. A wave-uniform
-      // branch (the first tile always takes it: m_run = -inf).
-      if (__builtin_amdgcn_ballot_w64(mt > m_run + 8.f)) {
-        const float m_new = fmaxf(m_run, mt);
-        const float alpha = fast_exp2(m_run - m_new);
-        l_run *= alpha;
-        m_run = m_new;
+      // branch (the first tile always takes it: m_run = -inf). A tile entirely above the
+      // diagonal for this block (QB 2, first block) has mt = -inf and changes nothing.
+      if (__builtin_amdgcn_ballot_w64(mt > m_run[j] + 8.f)) {
+        const float m_new = fmaxf(m_run[j], mt);
+        const float alpha = fast_exp2(m_run[j] - m_new);
+        l_run[j] *= alpha;
+        m_run[j] = m_new;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+          for (int i = 0; i < 16; ++i) o[j][dt][i] *= alpha;
       }
       float ls = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(fmaf(st[kt][i], sc_log2, -m_run));
-          st[kt][i] = p;
+          const float p = fast_exp2(fmaf(st[j][kt][i], sc_log2, -m_run[j]));
+          st[j][kt][i] = p;
           ls += p;
         }
-      l_run += half_sum(ls);
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8_t pf = acc_frag(st[kt], s);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(tr_frag(Vs, lo, 32 * kt + 16 * s, dt), pf, o[dt]);
-        }
+      l_run[j] += half_sum(ls);
     }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8_t vfrag = tr_frag(Vs, lo, 32 * kt + 16 * s, dt);
+#pragma unroll
+          for (int j = 0; j < QB; ++j) o[j][dt] = mfma32(vfrag, acc_frag(st[j][kt], s), o[j][dt]);
+        }
+      }
   };
   auto compute = [&](int t) __attribute__((always_inline)) {
     const int kv0 = t * 64;
     if (kv0 <= wave_qmax) {
-      if (kv0 + 63 > q0 + 32 * w) body(t, std::true_type{});
+      if (kv0 + 63 > wave_qmin) body(t, std::true_type{});
       else body(t, std::false_type{});
     }
   };
@@ -301,17 +325,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     step(t, A, B);
     if (t + 1 < ntiles) step(t + 1, B, A);
   }
-  const float inv = 1.f / l_run;
-  bf16_t* orow = out + ((long)b * T + qrow) * C + h * HD;
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int j = 0; j < QB; ++j) {
+    const float inv = 1.f / l_run[j];
+    bf16_t* orow = out + ((long)b * T + qrow[j]) * C + h * HD;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float v[4] = {o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                    o[dt][4 * g + 3] * inv};
-      *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g + 4 * hh) = pack4(v);
-    }
-  if (hh == 0) lse[(long)bh * T + qrow] = m_run + log2f(l_run);
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4] = {o[j][dt][4 * g] * inv, o[j][dt][4 * g + 1] * inv,
+                      o[j][dt][4 * g + 2] * inv, o[j][dt][4 * g + 3] * inv};
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g + 4 * hh) = pack4(v);
+      }
+    if (hh == 0) lse[(long)bh * T + qrow[j]] = m_run[j] + log2f(l_run[j]);
+  }
 }
 
 // ============================================================================ backward
@@ -854,8 +881,12 @@ RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, 
                           float scale, hipStream_t st) {
   if (!attn_shape_ok(T, D)) return hipErrorInvalidValue;
   const float sc_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / 128)), dim3(256), 0, st,
-                     (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
+  if (ra_knobs[9] == 1 && T % 256 == 0)
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(B * H * (T / 256)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(B * H * (T / 128)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   return hipGetLastError();
 }
 
