@@ -212,7 +212,10 @@ def test_compiled_faster_than_remote_chaining(cluster):
     finally:
         cdag.teardown()
     print(f"remote chain {t_remote * 1e6:.0f} us, compiled {t_comp * 1e6:.0f} us")
-    assert t_comp * 5 < t_remote
+    # 2.5x: round 5's task path cut the .remote() chain from ~845 to ~470-640 us on this VM
+    # while the compiled call stays at 40-170 us depending on host load (a 5x bound failed
+    # once with a compiler build running beside the suite)
+    assert t_comp * 2.5 < t_remote
 
 
 def test_function_nodes_rejected(cluster):
