@@ -264,7 +264,155 @@ __device__ __forceinline__ void wgrad_mainloop(bf16_t* lds, const TileJob& j,
   }
 }
 
-template <int MODE>  // 0: fp32 slab store, 1: fp32 sink RMW, 2: bf16 sink RMW
+// Deep-prefetch variant (ra_knobs[15] = 1): the same 128 KB of LDS as a ring of FOUR
+// 32-token stages instead of two 64-token ones, so three stages (96 tokens) are in flight
+// behind the one being read instead of one (64 tokens): the PMC pass (profiles/r5/r5al) has
+// the two-stage loop waiting in 35 % of its wave cycles. Per 32-token step s, both groups run
+//   [DMA of stage s+3 into the buffer step s-1 read] R(s) | Ba | M(s) | Bb
+// with waves 4-7 one barrier behind (the staggered schedule above); a group waits for its
+// own DMA of stage s+1 with a COUNTED vmcnt (stages s+2, s+3 stay in flight) before the
+// barrier that precedes the other group's read of s+1: group 0 before Bb, group 1 before Ba.
+// The buffer refilled at the top of step s was last read by R(s-1), which every wave
+// finished (lgkmcnt(0)) before a barrier that both groups have passed by then.
+constexpr int kT4 = 32;
+constexpr int kImg4 = kT4 * kTile;
+constexpr int kStage4 = 2 * kImg4;
+
+__device__ __forceinline__ void stage_t4(bf16_t* img, const bf16_t* __restrict__ g, long ld,
+                                         int col0, int cols, long t0, int w, int lane) {
+  const int rsub = lane >> 5, cp = lane & 31;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // wave w stages rows 4w .. 4w+3
+    const int r = 4 * w + 2 * j + rsub;
+    const int c = cp ^ (2 * fsw(r));
+    int col = col0 + 8 * c;
+    col = col < cols ? col : cols - 8;
+    const bf16_t* src = g + (t0 + r) * ld + col;
+    glds16_w(src, img + (4 * w + 2 * j) * kTile);
+  }
+}
+
+__device__ __forceinline__ void wait_stages_w(int n) {  // n stages (4 DMAs each) may remain
+  if (n >= 2) wait_vm_w<8>();
+  else if (n == 1) wait_vm_w<4>();
+  else wait_vm_w<0>();
+}
+
+__device__ __forceinline__ void wgrad_mainloop_deep(bf16_t* lds, const TileJob& j,
+                                                    f32x4w_t (&acc)[4][8], float (&bsum)[2],
+                                                    int w, int lane) {
+  const int wm = w >> 2, wn = w & 3;
+  const bool g1 = wm == 1;
+  const bool do_bias = j.do_bias;
+  const int total = 2 * j.total;  // 32-token steps
+  const int s0 = 2 * j.s_beg;
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int fl = q | ((gq & 1) << 2);
+  const int row_off = (8 * gq + q) * kTile + 4 * (p & 1);
+  int xoff[4], yoff[8];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) xoff[kb] = row_off + 8 * ((2 * (wn * 4 + kb) + (p >> 1)) ^ (2 * fl));
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) yoff[nb] = row_off + 8 * ((2 * (wm * 8 + nb) + (p >> 1)) ^ (2 * fl));
+  auto stage = [&](int ks) __attribute__((always_inline)) {
+    bf16_t* img = lds + (ks & 3) * kStage4;
+    const long t0 = (long)(s0 + ks) * kT4;
+    stage_t4(img, j.x, j.ldx, j.k0, j.K, t0, w, lane);
+    stage_t4(img + kImg4, j.dy, j.ldy, j.n0, j.N, t0, w, lane);
+  };
+  auto barrier = []() __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc[i][jj] = f32x4w_t{0.f, 0.f, 0.f, 0.f};
+  bsum[0] = bsum[1] = 0.f;
+  bf16x8w_t xf[4], yf[8];
+  auto read_frags = [&](int ks) __attribute__((always_inline)) {
+    const bf16_t* sx = lds + (ks & 3) * kStage4;
+    const bf16_t* sy = sx + kImg4;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const bf16x4w_t lo = tr4(sy + yoff[nb]);
+      const bf16x4w_t hi = tr4(sy + yoff[nb] + 4 * kTile);
+      yf[nb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x4w_t lo = tr4(sx + xoff[kb]);
+      const bf16x4w_t hi = tr4(sx + xoff[kb] + 4 * kTile);
+      xf[kb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto mfma_cluster = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+        acc[kb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[kb], yf[nb], acc[kb][nb], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (do_bias) {
+      auto dot8 = [&](const bf16x8w_t& v, float& acc_) __attribute__((always_inline)) {
+        const bf16x2w_t one = {(__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16x2w_t pr = {v[2 * e], v[2 * e + 1]};
+          acc_ = __builtin_amdgcn_fdot2_f32_bf16(pr, one, acc_, false);
+        }
+      };
+      if (wn == 0) {
+        dot8(yf[0], bsum[0]);
+        dot8(yf[1], bsum[1]);
+      } else if (wn == 1) {
+        dot8(yf[2], bsum[0]);
+        dot8(yf[3], bsum[1]);
+      } else if (wn == 2) {
+        dot8(yf[4], bsum[0]);
+        dot8(yf[5], bsum[1]);
+      } else {
+        dot8(yf[6], bsum[0]);
+        dot8(yf[7], bsum[1]);
+      }
+    }
+  };
+  // stages still allowed in flight once stage s+1 must have landed (issued: up to s+3)
+  auto pending_after = [&](int s) __attribute__((always_inline)) {
+    const int last = (s + 3 < total ? s + 3 : total - 1);
+    const int n = last - (s + 1);
+    return n < 0 ? 0 : n;
+  };
+  if (total > 0) {
+    const int pre = total < 3 ? total : 3;
+    for (int k = 0; k < pre; ++k) stage(k);
+    wait_stages_w(pre - 1);  // stage 0 landed
+  }
+  barrier();
+  if (g1) barrier();
+  for (int st = 0; st < total; ++st) {
+    if (st + 3 < total) stage(st + 3);  // buffer of step st-1: every wave's reads retired
+    read_frags(st);
+    if (g1) wait_stages_w(pending_after(st));
+    barrier();
+    mfma_cluster();
+    if (!g1) wait_stages_w(pending_after(st));
+    barrier();
+  }
+  if (!g1) barrier();
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bsum[i] += __shfl_xor(bsum[i], 16, 64);
+      bsum[i] += __shfl_xor(bsum[i], 32, 64);
+    }
+  }
+}
+
+template <int MODE, bool DEEP = false>  // 0: fp32 slab store, 1: fp32 sink RMW, 2: bf16 sink RMW
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
   const int G = gridDim.x;
@@ -282,7 +430,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a) {
   f32x4w_t acc[4][8];
   float bsum[2];
   const TileJob job{a.dy, a.x, a.ldy, a.ldx, a.N, a.K, n0, k0, s_beg, s_end - s_beg, do_bias};
-  wgrad_mainloop(lds, job, acc, bsum, w, lane);
+  if constexpr (DEEP) wgrad_mainloop_deep(lds, job, acc, bsum, w, lane);
+  else wgrad_mainloop(lds, job, acc, bsum, w, lane);
 
   // ---- epilogue: lane holds D[k = kc + 4(lane>>4) + r][n = nc + (lane & 15)]
   const int nrow = n0 + wm * 128 + (lane & 15);
@@ -591,14 +740,14 @@ RA_EXPORT int ra_wgrad(const void* dy, long ldy, const void* x, long ldx, int M,
   a.S = S;
   a.flags = flags;
   const int G = a.ntiles * S;
-  if (S == 1) {
-    if (flags & 1)
-      hipLaunchKernelGGL(wgrad_kernel<2>, dim3(G), dim3(kThreads), 0, st, a);
-    else
-      hipLaunchKernelGGL(wgrad_kernel<1>, dim3(G), dim3(kThreads), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(wgrad_kernel<0>, dim3(G), dim3(kThreads), 0, st, a);
-  }
+  const bool deep = ra_knobs[15] == 1;
+  void (*k)(WgradArgs);
+  if (S == 1)
+    k = (flags & 1) ? (deep ? wgrad_kernel<2, true> : wgrad_kernel<2, false>)
+                    : (deep ? wgrad_kernel<1, true> : wgrad_kernel<1, false>);
+  else
+    k = deep ? wgrad_kernel<0, true> : wgrad_kernel<0, false>;
+  hipLaunchKernelGGL(k, dim3(G), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -826,9 +826,14 @@ def test_transpose_bf16_kernel(cuda_device, rows, cols):
     (640, 72, 40, True, torch.bfloat16),              # bf16 sink, tiny ragged tiles
     (64 * 300, 3072, 3072, False, torch.float32),     # S == 1 path (144 tiles... or split)
 ])
-def test_wgrad_kernel_matches_fp32(cuda_device, M, N, K, bias, sdtype):
+@pytest.mark.parametrize("deep", [False, True])
+def test_wgrad_kernel_matches_fp32(cuda_device, M, N, K, bias, sdtype, deep, request):
     """ops/csrc/wgrad.hip vs an fp32 torch reference: dW += dY^T X, db += colsum(dY),
-    accumulated onto a non-zero sink (the flat-gradient contract)."""
+    accumulated onto a non-zero sink (the flat-gradient contract). deep: the four-stage
+    32-token ring main loop (ra_knobs[15] = 1)."""
+    if deep:
+        _lib.lib().ra_set_knob(15, 1)
+        request.addfinalizer(lambda: _lib.lib().ra_set_knob(15, 0))
     torch.manual_seed(11)
     dy = torch.randn(M, N, device=cuda_device).bfloat16()
     x = torch.randn(M, K, device=cuda_device).bfloat16()
@@ -869,8 +874,12 @@ def test_wgrad_kernel_many_tiles_split(cuda_device):
     assert float(dw[V:].abs().max()) == 0.0
 
 
-def test_wgrad_kernel_strided_rows(cuda_device):
+@pytest.mark.parametrize("deep", [False, True])
+def test_wgrad_kernel_strided_rows(cuda_device, deep, request):
     """Operands that are column slices of wider rows (ld > N / K), as packed activations."""
+    if deep:
+        _lib.lib().ra_set_knob(15, 1)
+        request.addfinalizer(lambda: _lib.lib().ra_set_knob(15, 0))
     torch.manual_seed(12)
     big = torch.randn(2048, 1024, device=cuda_device).bfloat16()
     dy, x = big[:, :512], big[:, 512:768]
