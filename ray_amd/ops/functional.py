@@ -496,6 +496,29 @@ def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, bias=None, bias_sink=None):
 
 _side: dict = {}
 
+# RAY_AMD_WGRAD_DEFER=1 (experiment): weight gradients of linears called with wg_hint="defer"
+# (GPT-2: c_fc, c_attn) are not issued after their dgrad GEMM but at the next flush point
+# (the backward of a linear with wg_hint="flush": c_proj), so they run beside the attention
+# backward (the dQ kernel shares CUs with a wgrad workgroup) instead of beside the next
+# dgrad GEMM, which cannot share a CU with one (131 / 133 KB of LDS; profiles/r5/README.md).
+_WGRAD_DEFER = os.environ.get("RAY_AMD_WGRAD_DEFER", "0") == "1"
+_deferred_wg: list = []
+
+
+def _issue_side_wgrad(job):
+    dy2, x2, w, sink, S, M, N, K, b, bsink = job
+    side = _side_stream(dy2.device)
+    side.wait_stream(torch.cuda.current_stream(dy2.device))
+    with torch.cuda.stream(side):
+        _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, b, bsink)
+        dy2.record_stream(side)
+        x2.record_stream(side)
+
+
+def flush_deferred_wgrads():
+    while _deferred_wg:
+        _issue_side_wgrad(_deferred_wg.pop(0))
+
 
 def _side_stream(device):
     st = _side.get(device)
@@ -527,6 +550,8 @@ def join_side_streams():
     gradients still queued are launched first."""
     if _pending_wg:
         flush_wgrads()
+    if _deferred_wg:
+        flush_deferred_wgrads()
     for dev, st in _side.items():
         torch.cuda.current_stream(dev).wait_stream(st)
 
@@ -628,9 +653,10 @@ def _transposed_weight(w):
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, wg_hint=None):
         ctx.save_for_backward(x, w)
         ctx.b = b
+        ctx.wg_hint = wg_hint
         ctx.wt = _transposed_weight(w) if _DGRAD_WT and w.is_cuda and x.dim() >= 2 else None
         return torch.nn.functional.linear(x, w, b)
 
@@ -670,12 +696,13 @@ class _Linear(torch.autograd.Function):
             elif sink is not None and _WGRAD_STREAM and dy2.is_cuda:
                 # weight gradient on the side stream: it overlaps the memory-bound kernels
                 # of the dX chain that continues on the main stream
-                side = _side_stream(dy2.device)
-                side.wait_stream(torch.cuda.current_stream(dy2.device))
-                with torch.cuda.stream(side):
-                    _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
-                    dy2.record_stream(side)
-                    x2.record_stream(side)
+                job = (dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
+                if _WGRAD_DEFER and ctx.wg_hint == "defer":
+                    _deferred_wg.append(job)  # issued at the next flush point
+                else:
+                    _issue_side_wgrad(job)
+                    if _WGRAD_DEFER and ctx.wg_hint == "flush":
+                        flush_deferred_wgrads()
             elif sink is not None:
                 _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
             elif S > 1:
@@ -687,15 +714,16 @@ class _Linear(torch.autograd.Function):
                 dw = dy2.t() @ x2
         if ctx.b is not None and ctx.needs_input_grad[2] and bsink is None:
             db = _bias_grad(dy2, ctx.b)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x, w, b=None):
+def linear(x, w, b=None, wg_hint=None):
     """y = x @ w^T + b with the MI355X backward (split-K fp32 wgrad, in-place flat-grad
-    accumulation). Same numerics contract as F.linear."""
+    accumulation). Same numerics contract as F.linear. ``wg_hint`` ("defer" / "flush")
+    places the weight gradient under RAY_AMD_WGRAD_DEFER (see _WGRAD_DEFER)."""
     if _hip(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and \
             (w.shape[0] * w.shape[1]) % 4 == 0:
-        return _Linear.apply(x, w, b)
+        return _Linear.apply(x, w, b, wg_hint)
     return torch.nn.functional.linear(x, w, b)
 
 

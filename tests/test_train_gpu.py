@@ -105,6 +105,33 @@ def test_lm_head_side_stream_dw_matches_main_stream(cuda_device, monkeypatch, mo
     assert _rel(grads[1], grads[0]) < 1e-5
 
 
+def test_deferred_wgrads_match_immediate(cuda_device, monkeypatch):
+    """RAY_AMD_WGRAD_DEFER: c_fc / c_attn weight gradients issued at the next c_proj backward
+    (or at the side-stream join) land the same flat gradients as issued right away."""
+    import copy
+
+    from ray_amd.models.gpt2 import GPT2
+    from ray_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(29)
+    base = GPT2(_tiny_cfg()).to(cuda_device).bfloat16()
+    idx = torch.randint(0, 1000, (4, 256), device=cuda_device)
+    tgt = torch.randint(0, 1000, (4, 256), device=cuda_device)
+    grads = []
+    for defer in (False, True):
+        monkeypatch.setattr(rf, "_WGRAD_DEFER", defer)
+        m = copy.deepcopy(base)
+        flat = FlatParams(m)
+        m(idx, tgt).backward()
+        if defer:
+            assert rf._deferred_wg  # the first layer's c_attn wgrad waits for the join
+        rf.join_side_streams()
+        assert not rf._deferred_wg
+        torch.cuda.synchronize()
+        grads.append(flat.g.clone())
+    assert _rel(grads[1], grads[0]) < 1e-6
+
+
 def test_flat_fp32_grad_accum_exact(cuda_device):
     """grad_accum=4 into the fp32 flat buffer equals the fp64 sum of the four
     micro-batch gradients to ~1e-6 (bf16 accumulation is orders of magnitude worse)."""
