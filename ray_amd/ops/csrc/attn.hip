@@ -181,8 +181,10 @@ __device__ __forceinline__ void tile_store(const TileRegs& r, bf16_t* img) {
 // QB = 32-query blocks per wave (1: a workgroup covers 128 queries; 2: 256 queries, every K
 // row fragment and V transposed fragment read from LDS feeds two MFMAs, and each wave has
 // two independent S / softmax / PV chains in flight; ra_knobs[9] = 1 selects QB 2).
-template <int QB>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv,
+// WPE > 0: the register budget of WPE waves per SIMD (QB 1 at WPE 3: 162 registers, no spill,
+// vs 208 = 2 waves unconstrained; ra_knobs[9] = 2 selects it).
+template <int QB, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, WPE > 0 ? WPE : 8))) void attn_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                        bf16_t* __restrict__ out,
                                                        float* __restrict__ lse, int T, int H,
                                                        float sc_log2) {
@@ -883,6 +885,9 @@ RA_EXPORT int ra_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, 
   const float sc_log2 = scale * 1.4426950408889634f;
   if (ra_knobs[9] == 1 && T % 256 == 0)
     hipLaunchKernelGGL(attn_fwd_kernel<2>, dim3(B * H * (T / 256)), dim3(256), 0, st,
+                       (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
+  else if (ra_knobs[9] == 2)
+    hipLaunchKernelGGL((attn_fwd_kernel<1, 3>), dim3(B * H * (T / 128)), dim3(256), 0, st,
                        (const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sc_log2);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<1>, dim3(B * H * (T / 128)), dim3(256), 0, st,

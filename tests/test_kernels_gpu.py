@@ -426,7 +426,7 @@ def test_image_normalize_vector_path(cuda_device, C):
 
 
 @pytest.mark.parametrize("mode", ["fused", "split", "split2", "split_pre", "split_rcg",
-                                  "fwd_qb2"])
+                                  "fwd_qb2", "fwd_wpe3"])
 @pytest.mark.parametrize("B,T,H", [(2, 256, 3), (1, 1024, 2), (2, 128, 1)])
 def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch, request):
     """split: dQ (computing delta) then dK/dV; split_pre: round 4's separate delta pre-pass
@@ -438,8 +438,9 @@ def test_flash_attention_fwd_bwd(cuda_device, B, T, H, mode, monkeypatch, reques
         _lib.lib().ra_set_knob(13, 1)
         request.addfinalizer(lambda: _lib.lib().ra_set_knob(13, 0))
         mode = "split"
-    elif mode == "fwd_qb2":  # forward with two 32-query blocks per wave (T % 256 == 0)
-        _lib.lib().ra_set_knob(9, 1)
+    elif mode in ("fwd_qb2", "fwd_wpe3"):  # two 32-query blocks per wave (T % 256 == 0) /
+        # the one-block forward on a 3-waves-per-SIMD register budget
+        _lib.lib().ra_set_knob(9, 1 if mode == "fwd_qb2" else 2)
         request.addfinalizer(lambda: _lib.lib().ra_set_knob(9, 0))
         mode = "split"
     elif mode == "split_rcg":  # dK/dV with the row constants in registers (32 KB LDS)
