@@ -31,6 +31,7 @@ from ray_amd._private.object_store import start_prefault, table_capacity
 from ray_amd._native import _core
 
 from . import protocol as P
+from . import shm_segment
 from .raylet import free_object, node_resources, read_object_bytes, read_object_chunk
 
 _dumps = P.dumps
@@ -45,7 +46,7 @@ class NodeAgent:
         self.node_hex = self.node_id.hex()
         self.node_ip = "127.0.0.1"
         self.addr = os.path.join(sock_dir, f"raylet_{self.node_hex[:16]}.sock")
-        self.store_path = args.store_path
+        self.store_path, self._store_fd = shm_segment.create(args.store_path)
         self.spill_dir = os.path.join(self.session_dir, f"spill_{self.node_hex[:16]}")
         os.makedirs(self.spill_dir, exist_ok=True)
         self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
@@ -190,8 +191,5 @@ class NodeAgent:
                 p.wait(timeout=2)
             except Exception:
                 pass
-        try:
-            os.unlink(self.store_path)
-        except OSError:
-            pass
+        shm_segment.release(self.store_path, self._store_fd)
         self.io.stop()

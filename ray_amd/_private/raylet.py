@@ -27,6 +27,7 @@ from ray_amd._native import _core
 
 from . import protocol as P
 from . import serialization as ser
+from . import shm_segment
 from .object_store import start_prefault, table_capacity
 
 _dumps = P.dumps
@@ -238,7 +239,9 @@ class Raylet:
         self.reporter = NodeReporter(self.node_id.hex(), self.session_dir).start()
         self.node_stats = {}  # node hex -> latest sample pushed by that node's agent
         self.node_ip = os.environ.get("RAY_AMD_NODE_IP", "127.0.0.1")
-        self.store_path = args.store_path
+        # anonymous memfd segment: freed by the kernel with the last process holding it,
+        # however this raylet exits (shm_segment.py; plasma's unlink-after-map model)
+        self.store_path, self._store_fd = shm_segment.create(args.store_path)
         self.spill_dir = os.path.join(self.session_dir, "spill")
         os.makedirs(self.spill_dir, exist_ok=True)
         self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
@@ -1685,10 +1688,7 @@ class Raylet:
                 p.kill()
             except Exception:
                 pass
-        try:
-            os.unlink(self.store_path)
-        except OSError:
-            pass
+        shm_segment.release(self.store_path, self._store_fd)
         self.io.stop()
 
 

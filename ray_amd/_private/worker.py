@@ -205,6 +205,9 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
             atexit.register(shutdown)
             return RayContext(global_worker)
         if address in (None, "local", ""):
+            from . import shm_segment
+
+            shm_segment.sweep_dead()  # named segments of dead sessions (RAY_AMD_SHM_MEMFD=0)
             session = new_session_dir() if _temp_dir is None else os.path.join(
                 _temp_dir, os.path.basename(new_session_dir()))
             osm = int(object_store_memory or _default_object_store_memory())

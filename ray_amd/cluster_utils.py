@@ -187,8 +187,18 @@ class Cluster:
         if self.connected and ray_amd.is_initialized():
             ray_amd.shutdown()
         self.connected = False
-        for n in list(self.worker_nodes):
-            n.kill(False)
+        # graceful first (SIGTERM: the agent kills its workers and releases its store),
+        # all nodes at once, then SIGKILL whatever did not exit. Even a SIGKILLed agent
+        # leaves no store behind: it is a memfd (_private/shm_segment.py)
+        nodes = [n for n in self.worker_nodes if n.alive()]
+        for n in nodes:
+            n.proc.terminate()
+        deadline = time.time() + 10
+        for n in nodes:
+            try:
+                n.proc.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                n.kill(False)
         self.worker_nodes.clear()
         if self.head_node is not None:
             self.head_node.kill(True)

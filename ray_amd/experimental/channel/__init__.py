@@ -12,8 +12,12 @@ node's HBM object store (one D2D copy into the arena on the writer's stream, zer
 DLPack view on the reader, no host bounce) when ``gpu=True``; the writer frees a value's
 HBM sub-objects once all readers consumed it (readers still holding the tensors keep
 them alive through their pins). Payloads larger than the buffer transparently grow the
-channel: the writer publishes a resize marker naming a larger file and all readers
+channel: the writer publishes a resize marker naming a larger segment and all readers
 follow it.
+
+Segments are anonymous memfds (``_private/shm_segment.py``): readers open them through
+``/proc/<creator pid>/fd/<fd>``, and the kernel frees them with the last process holding
+one, so a killed driver or actor leaves nothing in ``/dev/shm``.
 """
 
 from __future__ import annotations
@@ -22,6 +26,7 @@ import os
 import uuid
 
 from ray_amd._native import _core
+from ray_amd._private import shm_segment
 from ray_amd.exceptions import RayChannelError, RayChannelTimeoutError
 
 ChannelClosedError = _core.ChannelClosedError
@@ -46,13 +51,21 @@ class Channel:
         self.num_readers = int(num_readers)
         self.gpu = gpu
         self._owner = _path is None
-        self.path = _path or os.path.join(
-            _shm_dir(), f"ramd_ch_{os.getpid()}_{uuid.uuid4().hex[:16]}")
+        self._created = []  # (path, memfd or None) of every segment this endpoint created
+        if self._owner:
+            self.path = self._new_segment(
+                os.path.join(_shm_dir(), f"ramd_ch_{os.getpid()}_{uuid.uuid4().hex[:16]}"))
+        else:
+            self.path = _path
         self._c = _core.ShmChannel(self.path, int(buffer_size_bytes), self.num_readers,
                                    True) if self._owner else None
         self._prev_gpu_oid = None
         self._resizes = 0
-        self._created = [self.path] if self._owner else []
+
+    def _new_segment(self, name):
+        path, fd = shm_segment.create(name)
+        self._created.append((path, fd))
+        return path
 
     def __reduce__(self):
         return (_attach, (self.path, self.num_readers, self.gpu))
@@ -93,19 +106,21 @@ class Channel:
 
     def _grow(self, need: int, timeout):
         self._resizes += 1
-        new_path = f"{self.path.split('.r')[0]}.r{self._resizes}"
+        new_path = self._new_segment(
+            os.path.join(_shm_dir(), f"ramd_ch_{os.getpid()}_{uuid.uuid4().hex[:16]}"
+                                     f".r{self._resizes}"))
         cap = max(need * 2, self._chan().capacity * 2)
         new = _core.ShmChannel(new_path, cap, self._chan().num_readers, True)
         if not self._chan().write(_RESIZE + new_path.encode(), _to(timeout)):
             raise RayChannelTimeoutError(f"resize of channel {self.path} timed out")
-        if self._owner:
+        if self._owner and not shm_segment.is_anonymous(self.path):
             try:
                 os.unlink(self.path)  # readers keep their mapping until they switch
             except OSError:
                 pass
+            self._created = [c for c in self._created if c[0] != self.path]
         self.path = new_path
         self._c = new
-        self._created.append(new_path)
         return new
 
     @staticmethod
@@ -166,11 +181,8 @@ class Channel:
         self.close()
         self._free_gpu(self._prev_gpu_oid)
         self._prev_gpu_oid = None
-        for p in self._created:
-            try:
-                os.unlink(p)
-            except OSError:
-                pass
+        for p, fd in self._created:
+            shm_segment.release(p, fd)
         self._created = []
 
 

@@ -73,7 +73,12 @@ def main(M=65536, C=768, F=3072):
     shape = (0, 0, F, M, C, F, C, F)
     n = L.ra_lt_ep_num_cands(*shape, DGELU_BGRAD, F)
     out["bwd_cands"] = n
-    if n > 0 and "fwd_best" in out:
+    for nm, ep in (("gelu", 32), ("gelu_bias", 36), ("gelu_aux", 160), ("dgelu", 192)):
+        out[nm + "_cands_fwdshape"] = L.ra_lt_ep_num_cands(1, 0, F, M, C, C, C, F, ep, F)
+        out[nm + "_cands_bwdshape"] = L.ra_lt_ep_num_cands(*shape, ep, F)
+    if "fwd_best" not in out:  # aux from torch for the backward-only probe
+        aux.copy_((x.float() @ wfc.float().t() + bfc.float()).to(bf))
+    if n > 0:
         L.ra_lt_gemm_ep(0, 0, F, M, C, ptr(wpr), F, ptr(dout), C, ptr(dh), F, DGELU_BGRAD,
                         ptr(db), ptr(aux), F, -1, stream_ptr())
         torch.cuda.synchronize()
