@@ -2010,7 +2010,12 @@ class CoreWorker:
         A non-owner forwards the request to the owner."""
         tid = ref._id[:16]
         with self.lock:
-            known = tid in self.task_specs
+            spec = self.task_specs.get(tid)
+            known = spec is not None
+        if known and force and spec["type"] == P.ACTOR_TASK:
+            # reference: core_worker.cc HandleCancelTask / CancelTask rejects it — killing
+            # the actor process would take its state and every other in-flight call along
+            raise ValueError("force=True is not supported for actor tasks.")
         if not known:
             owner = getattr(ref, "_owner", None)
             if owner and owner != self.addr:
@@ -2042,6 +2047,8 @@ class CoreWorker:
         if queued:
             self._fail_task(spec, TaskCancelledError(tid.hex()))
             return
+        if spec["type"] == P.ACTOR_TASK:
+            force = False  # a forwarded force=True never kills an actor process
         msg = (P.REQ, 0, "cancel_task", (tid, force, recursive))
         if spec["type"] == P.ACTOR_TASK:
             ac = self.actors.get(spec["actor_id"])
@@ -2062,9 +2069,7 @@ class CoreWorker:
                 self._cancel_tid(k, force, recursive)
             except Exception:
                 pass
-        if atask is not None:
-            if force:
-                os._exit(1)
+        if atask is not None:  # async actor method: never force-killed (see cancel)
             loop, task = atask
             loop.call_soon_threadsafe(task.cancel)
         elif th is not None:

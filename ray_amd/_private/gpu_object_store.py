@@ -227,7 +227,12 @@ def _spill_one(cw, sid: bytes, phys: int) -> bool:
         base = _arena(phys)[0]
         hid = spill_id(sid)
         if not cw.store.store.contains(hid):
-            hoff = cw.store._alloc(hid, size, True)
+            # no wait: a full host store fails this spill now (the caller tries the next
+            # victim or reports the HBM store full) instead of blocking for the grace period
+            hoff = cw.store._alloc(hid, size, True, wait=False)
+            if hoff is None:
+                st.release(sid)
+                return False
             _copy_bytes(st.address() + hoff, base + off, size)  # D2H into the shm segment
             cw.store.store.seal(hid)
     except Exception:  # noqa: BLE001

@@ -48,6 +48,42 @@ class PerModuleLearners:
         if lr is not None:
             lr.shutdown()
 
+    # reference-named module-set API (learner_group.py:494 add_module, :520 remove_module,
+    # get/set_module_state, get/set_optimizer_state): here each module has its own learner
+    # (group), built by ``make`` — the off-policy algorithms keep one replay buffer and one
+    # target network per module
+    def add_module(self, *, module_id, module_spec, config_overrides=None,
+                   new_should_module_be_updated=None):
+        spec = tuple(module_spec) if isinstance(module_spec, (tuple, list)) else \
+            (module_spec.observation_space, module_spec.action_space)
+        self.add(module_id, spec)
+        if new_should_module_be_updated is not None:
+            ids = list(self.learners)
+            f = new_should_module_be_updated
+            self.trainable = {m for m in ids if f(m)} if callable(f) else set(f) & set(ids)
+        return list(self.learners)
+
+    def remove_module(self, module_id, *, new_should_module_be_updated=None):
+        self.remove(module_id)
+        return list(self.learners)
+
+    def get_module_state(self, module_ids=None) -> dict:
+        ids = list(self.learners) if module_ids is None else \
+            [m for m in module_ids if m in self.learners]
+        return {m: self.learners[m].get_weights() for m in ids}
+
+    def set_module_state(self, state: dict):
+        for m, w in state.items():
+            self.learners[m].set_weights(w)
+
+    def get_optimizer_state(self) -> dict:
+        """{module_id: that module's optimizer states} (each learner group holds one)."""
+        return {m: lr.get_optimizer_state()[m] for m, lr in self.learners.items()}
+
+    def set_optimizer_state(self, state: dict):
+        for m, st in state.items():
+            self.learners[m].set_optimizer_state({m: st})
+
     def sync_target(self):
         for mid in self.trainable:
             getattr(self.learners[mid], "sync_target", lambda: None)()
@@ -594,14 +630,16 @@ class Algorithm:
         self.cfg["_module_specs"] = self.module_specs
         if add_to_learners:
             lg = self.learner_group
-            if hasattr(lg, "add"):
-                lg.add(module_id, spec, trainable=module_id in trainable)
+            # the learners build the module (its network, optimizers and loss) through
+            # Learner.add_module on every learner of the group (learner_group.py:494)
+            lg.add_module(module_id=module_id, module_spec=spec,
+                          config_overrides=config_overrides,
+                          new_should_module_be_updated=sorted(trainable, key=str))
             if hasattr(self, "buffers") and module_id in trainable:
                 self.buffers[module_id] = self._new_buffer()
             self._set_trainable(trainable)
             if weights is not None:
-                lg.groups[module_id].set_weights(weights) if hasattr(lg, "groups") else \
-                    lg.learners[module_id].set_weights(weights)
+                lg.set_module_state({module_id: weights})
         w = weights if weights is not None else self.get_weights().get(module_id)
         if new_agent_to_module_mapping_fn is not None:
             self.config.policy_mapping_fn = new_agent_to_module_mapping_fn
@@ -644,8 +682,7 @@ class Algorithm:
             ray.get([r.apply.remote(blob) for r in self._eval_runners])
         if remove_from_learners:
             lg = self.learner_group
-            if hasattr(lg, "remove"):
-                lg.remove(module_id)
+            lg.remove_module(module_id)
             if hasattr(self, "buffers"):
                 self.buffers.pop(module_id, None)
         self._set_trainable(trainable)

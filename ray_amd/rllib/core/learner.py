@@ -149,12 +149,18 @@ class TorchLearner:
             [p for g in optimizer.param_groups for p in g["params"]]
         self._optimizers[(module_id, optimizer_name)] = (optimizer, params)
 
-    def get_optimizer(self, module_id=DEFAULT_MODULE_ID, optimizer_name="default"):
-        ent = self._optimizers.get((module_id, optimizer_name))
+    def get_optimizer(self, module_id=None, optimizer_name="default"):
+        """The named optimizer of ``module_id`` (default: this learner's own module; an
+        added module's is looked up on its learner)."""
+        module_id = self.module_id if module_id is None else module_id
+        lr = self._module_learners().get(module_id, self)
+        ent = lr._optimizers.get((module_id, optimizer_name))
         return ent[0] if ent else None
 
-    def get_optimizers_for_module(self, module_id=DEFAULT_MODULE_ID):
-        return [(n, o) for (m, n), (o, _) in self._optimizers.items() if m == module_id]
+    def get_optimizers_for_module(self, module_id=None):
+        module_id = self.module_id if module_id is None else module_id
+        lr = self._module_learners().get(module_id, self)
+        return [(n, o) for (m, n), (o, _) in lr._optimizers.items() if m == module_id]
 
     def get_parameters(self, module=None):
         return list((module or self.module).parameters())
@@ -213,24 +219,61 @@ class TorchLearner:
         dist.all_reduce(t)
         return float(t) / self.world
 
+    def _allreduce_min(self, x: int) -> int:
+        if self.world <= 1:
+            return int(x)
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            return int(x)
+        t = torch.tensor([int(x)], dtype=torch.int64,
+                         device=self.device if self.device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t)
+
+    def _minibatch_rng(self):
+        """The minibatch shuffler: created once, so a seeded learner draws a new permutation
+        every epoch and iteration (the reference's MiniBatchCyclicIterator keeps its state);
+        rank-offset so the learners of a group shuffle their shards independently."""
+        rng = getattr(self, "_mb_rng", None)
+        if rng is None:
+            seed = self.config.get("seed")
+            rng = self._mb_rng = np.random.default_rng(
+                None if seed is None else int(seed) + 1000003 * self.rank)
+        return rng
+
     # ---------------------------------------------------------------- the pipeline
     def update_from_batch(self, batch, *, timesteps=None, num_epochs=1, minibatch_size=None,
                           shuffle_batch_per_epoch=False, **kwargs) -> dict:
         """Gradient updates on ``batch`` (a dict of arrays / tensors with a common leading
         row axis): ``num_epochs`` passes in minibatches of ``minibatch_size`` rows (the
         whole batch by default). Returns the last update's metrics (scalars; per-row
-        arrays such as ``td_error`` cover the whole batch)."""
+        arrays such as ``td_error`` cover the whole batch). A module-keyed batch
+        (``{module_id: batch}``) trains each of this learner's modules in it."""
+        if self._is_module_batch(batch):
+            return self._update_modules(batch, timesteps=timesteps, num_epochs=num_epochs,
+                                        minibatch_size=minibatch_size,
+                                        shuffle_batch_per_epoch=shuffle_batch_per_epoch,
+                                        **kwargs)
         n = _rows(batch)
-        if not minibatch_size or minibatch_size >= n:
+        # every update all-reduces gradients across the group, so all learners must run the
+        # same number of them: agree on the smallest shard (an empty shard raises on every
+        # rank together instead of leaving the others blocked in the collective)
+        n_min = self._allreduce_min(n)
+        if n_min == 0:
+            raise ValueError(f"learner {self.rank}/{self.world}: a learner received an empty "
+                             "batch shard")
+        if not minibatch_size or minibatch_size >= n_min:
             res = {}
             for _ in range(max(1, num_epochs)):
                 res = self._update(batch, timesteps=timesteps)
             return res
         res, per_row = {}, {}
-        rng = np.random.default_rng(self.config.get("seed"))
+        n_mb = n_min // minibatch_size  # minibatches per epoch, identical on every rank
+        rng = self._minibatch_rng()
         for _ in range(max(1, num_epochs)):
             order = rng.permutation(n) if shuffle_batch_per_epoch else np.arange(n)
-            for s in range(0, n - minibatch_size + 1, minibatch_size):
+            for s in range(0, n_mb * minibatch_size, minibatch_size):
                 idx = order[s:s + minibatch_size]
                 res = self._update(_take_rows(batch, idx), timesteps=timesteps)
                 for k, v in list(res.items()):
@@ -354,6 +397,154 @@ class TorchLearner:
     def after_gradient_based_update(self, *, timesteps=None):
         """Hook after every update (target networks, schedules)."""
 
+    # ---------------------------------------------------------------- the module set
+    # Reference: rllib/core/learner/learner.py :821 add_module, :845 remove_module, :696 /
+    # :714 get_module_state / set_module_state, :1308 / :1316 set_optimizer_state /
+    # get_optimizer_state, :607 register_metrics. A learner owns its own module (built in
+    # __init__) and any number of added ones. Each added module gets a learner of this
+    # same class (same rank / world / device): its network, its optimizers (from
+    # configure_optimizers_for_module) and its loss, so every algorithm's learner can grow
+    # a module. A module-keyed batch ({module_id: batch}) trains every module in it, in
+    # sorted module-id order, each with its own gradient all-reduce — the same order on
+    # every learner of the group, so the collectives match.
+    def _module_learners(self) -> dict:
+        return {self.module_id: self, **(getattr(self, "_sub_learners", None) or {})}
+
+    @property
+    def module_ids(self) -> list:
+        return list(self._module_learners())
+
+    def get_module(self, module_id=None):
+        lr = self._module_learners().get(module_id if module_id is not None else self.module_id)
+        if lr is None:
+            raise KeyError(f"no module {module_id!r} in this learner")
+        return lr.module
+
+    def add_module(self, *, module_id, module_spec=None, config_overrides=None,
+                   new_should_module_be_updated=None):
+        """Build and add a module. ``module_spec``: an RLModuleSpec (a user module and/or
+        its spaces) or an ``(observation_space, action_space)`` tuple; missing spaces
+        default to this learner's. ``config_overrides``: per-module config keys (e.g. its
+        ``lr``). ``new_should_module_be_updated``: ids (or a predicate) of the modules
+        that train from now on. Collective with several learners: every learner of the
+        group must add it (``LearnerGroup.add_module``), which starts every copy from rank
+        0's initial weights."""
+        if module_id in self._module_learners():
+            raise ValueError(f"module {module_id!r} already exists")
+        from ray_amd.rllib.core.rl_module.rl_module import RLModuleSpec
+
+        os_, as_ = self.observation_space, self.action_space
+        cfg = dict(self.config)
+        cfg.update(config_overrides or {})
+        if isinstance(module_spec, (tuple, list)):
+            os_, as_ = module_spec
+        elif isinstance(module_spec, RLModuleSpec):
+            os_ = module_spec.observation_space or os_
+            as_ = module_spec.action_space or as_
+            if module_spec.module_class is not None:
+                cfg["_rl_module_spec"] = module_spec
+        elif module_spec is not None:
+            raise TypeError(f"module_spec must be an RLModuleSpec or (obs_space, act_space), "
+                            f"got {type(module_spec).__name__}")
+        cfg["is_multi_agent"] = bool(cfg.get("is_multi_agent"))
+        sub = type(self)(cfg, os_, as_, device=self.device, rank=self.rank, world=self.world,
+                         module_id=module_id)
+        if not hasattr(self, "_sub_learners"):
+            self._sub_learners = {}
+        self._sub_learners[module_id] = sub
+        if new_should_module_be_updated is not None:
+            self._set_trainable_modules(new_should_module_be_updated)
+        return self.module_ids
+
+    def remove_module(self, module_id, *, new_should_module_be_updated=None):
+        if module_id == self.module_id:
+            raise ValueError("a learner cannot remove its own (first) module")
+        sub = (getattr(self, "_sub_learners", None) or {}).pop(module_id, None)
+        if sub is None:
+            raise KeyError(f"no module {module_id!r} in this learner")
+        sub.shutdown()
+        if new_should_module_be_updated is not None:
+            self._set_trainable_modules(new_should_module_be_updated)
+        return self.module_ids
+
+    def _set_trainable_modules(self, spec):
+        ids = self.module_ids
+        self._trainable = {m for m in ids if spec(m)} if callable(spec) else \
+            set(spec) & set(ids)
+
+    def should_module_be_updated(self, module_id) -> bool:
+        tr = getattr(self, "_trainable", None)
+        return tr is None or module_id in tr
+
+    def get_module_state(self, module_ids=None) -> dict:
+        """{module_id: the module's full state dict (cpu tensors: target networks and
+        buffers included)}; ``module_ids`` selects."""
+        lrs = self._module_learners()
+        ids = lrs if module_ids is None else [m for m in lrs if m in set(module_ids)]
+        return {m: {k: v.detach().cpu().clone() for k, v in lrs[m].module.state_dict().items()}
+                for m in ids}
+
+    def set_module_state(self, state: dict):
+        """Load ``get_module_state`` output — or a module's EnvRunner weights
+        (``get_weights`` format, e.g. an online network without its target)."""
+        lrs = self._module_learners()
+        for m, w in state.items():
+            if m not in lrs:
+                raise KeyError(f"no module {m!r} in this learner")
+            lr = lrs[m]
+            if set(w) == set(lr.module.state_dict()):
+                lr._load_module_state_dict(w)
+            else:
+                lr.set_weights(w)
+
+    def _load_module_state_dict(self, sd):
+        self.module.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()})
+
+    def _own_optimizer_state(self) -> dict:
+        return {f"{m}/{n}": o.state_dict() for (m, n), (o, _) in self._optimizers.items()}
+
+    def _load_own_optimizer_state(self, st: dict):
+        for (m, n), (o, _) in self._optimizers.items():
+            if f"{m}/{n}" in st:
+                o.load_state_dict(st[f"{m}/{n}"])
+
+    def get_optimizer_state(self) -> dict:
+        """{module_id: {"<module>/<optimizer name>": optimizer state_dict}} over every
+        module of this learner (moments, step counts: enough to resume bit-exactly)."""
+        return {m: lr._own_optimizer_state() for m, lr in self._module_learners().items()}
+
+    def set_optimizer_state(self, state: dict):
+        lrs = self._module_learners()
+        for m, st in state.items():
+            if m not in lrs:
+                raise KeyError(f"no module {m!r} in this learner")
+            lrs[m]._load_own_optimizer_state(st)
+
+    def register_metrics(self, module_id, metrics_dict: dict):
+        """Metrics a loss wants reported with the update results (per module; the
+        learner's own module's appear unprefixed, an added module's as ``<id>/<key>``)."""
+        lr = self._module_learners().get(module_id)
+        if lr is None:
+            raise KeyError(f"no module {module_id!r} in this learner")
+        lr.metrics.update({k: float(v.detach()) if torch.is_tensor(v) else v
+                           for k, v in metrics_dict.items()})
+
+    def _is_module_batch(self, batch) -> bool:
+        lrs = self._module_learners()
+        return isinstance(batch, dict) and bool(batch) and len(lrs) > 1 and \
+            all(k in lrs and isinstance(v, dict) for k, v in batch.items())
+
+    def _update_modules(self, batch, **kwargs) -> dict:
+        lrs = self._module_learners()
+        out = {}
+        for m in sorted(batch, key=str):
+            if not self.should_module_be_updated(m):
+                continue
+            # the owner's own update entry point (not this method again)
+            res = lrs[m].update_from_batch(batch[m], **kwargs)
+            out.update(res if m == self.module_id else {f"{m}/{k}": v for k, v in res.items()})
+        return out
+
     # ---------------------------------------------------------------- state
     def get_weights(self):
         return {k: v.detach().cpu() for k, v in self.module.state_dict().items()}
@@ -383,18 +574,50 @@ class TorchLearner:
         pass
 
     def save_state(self, path: str):
-        """Checkpoint this learner (module weights, optimizer states, counters) into the
-        directory ``path``."""
+        """Checkpoint this learner (module weights, optimizer states, counters, added
+        modules) into the directory ``path``: tensors and plain containers only, loaded
+        back with ``torch.load(weights_only=True)`` (no code runs from the file)."""
         os.makedirs(path, exist_ok=True)
-        torch.save(self.get_state(), os.path.join(path, "learner_state.pt"))
+        torch.save(_plain(self.get_full_state()), os.path.join(path, "learner_state.pt"))
         return path
 
     def load_state(self, path: str):
         f = os.path.join(path, "learner_state.pt") if os.path.isdir(path) else path
-        self.set_state(torch.load(f, map_location="cpu", weights_only=False))
+        self.set_full_state(torch.load(f, map_location="cpu", weights_only=True))
+
+    def get_full_state(self) -> dict:
+        """This learner's state plus every added module's (``get_state`` per module)."""
+        st = self.get_state()
+        subs = getattr(self, "_sub_learners", None)
+        if subs:
+            st = dict(st, __modules__={m: lr.get_state() for m, lr in subs.items()})
+        return st
+
+    def set_full_state(self, s: dict):
+        s = dict(s)
+        mods = s.pop("__modules__", None) or {}
+        self.set_state(s)
+        for m, st in mods.items():
+            sub = (getattr(self, "_sub_learners", None) or {}).get(m)
+            if sub is not None:
+                sub.set_state(st)
 
     def shutdown(self):
         pass
+
+
+def _plain(x):
+    """numpy values -> tensors / Python scalars, recursively, so a state file needs no
+    unpickling of arbitrary classes (torch.load(weights_only=True))."""
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_plain(v) for v in x)
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(np.ascontiguousarray(x))
+    if isinstance(x, np.generic):
+        return x.item()
+    return x
 
 
 def _rows(batch) -> int:
@@ -436,6 +659,7 @@ class Learner(TorchLearner):
     def __init__(self, config: dict, observation_space, action_space, device=None, rank=0,
                  world=1, module_id=DEFAULT_MODULE_ID):
         self.config = config
+        self.observation_space, self.action_space = observation_space, action_space
         if device is None:
             device = torch.device("cuda", int(os.environ.get("RAY_AMD_LOCAL_DEVICE", "0"))) \
                 if torch.cuda.is_available() and config.get("num_gpus_per_learner", 1) else \
@@ -503,9 +727,11 @@ class Learner(TorchLearner):
             [p for g in optimizer.param_groups for p in g["params"]]
         self._optimizers[(module_id, optimizer_name)] = (optimizer, params)
 
-    def get_optimizer(self, module_id=DEFAULT_MODULE_ID, optimizer_name="default"):
-        ent = self._optimizers.get((module_id, optimizer_name))
-        return ent[0] if ent else self.opt
+    def get_optimizer(self, module_id=None, optimizer_name="default"):
+        module_id = self.module_id if module_id is None else module_id
+        lr = self._module_learners().get(module_id, self)
+        ent = lr._optimizers.get((module_id, optimizer_name))
+        return ent[0] if ent else lr.opt
 
     def get_parameters(self, module=None):
         return list((module or self.module).parameters())
@@ -599,6 +825,24 @@ class Learner(TorchLearner):
             if st is not None:
                 o.load_state_dict(st)
         self.kl_coeff = s.get("kl_coeff", self.kl_coeff)
+
+    def _load_module_state_dict(self, sd):
+        super()._load_module_state_dict(sd)
+        self.flat.sync_master_from_params()
+
+    def _own_optimizer_state(self) -> dict:
+        st = super()._own_optimizer_state()
+        if self.opt is not None:  # the fused flat AdamW (moments of the fp32 master)
+            st[f"{self.module_id}/default"] = {
+                k: v.detach().cpu().clone() if torch.is_tensor(v) else v
+                for k, v in self.opt.state_dict().items()}
+        return st
+
+    def _load_own_optimizer_state(self, st: dict):
+        super()._load_own_optimizer_state(st)
+        if self.opt is not None and f"{self.module_id}/default" in st:
+            self.opt.load_state_dict({k: v.to(self.device) if torch.is_tensor(v) else v
+                                      for k, v in st[f"{self.module_id}/default"].items()})
 
     # ---------------------------------------------------------------- multi-learner agreement
     def _allreduce(self, t, op="sum"):
@@ -700,7 +944,10 @@ class Learner(TorchLearner):
     def update_from_batch(self, batch, *, timesteps=None, **kwargs) -> dict:
         """PPO (GAE + epochs of minibatch SGD) or V-trace on a [T, B] rollout batch: the
         fused HIP path (loss+grad kernel, HIP-graph step) unless a pipeline hook is
-        overridden, then the eager loop through the hooks."""
+        overridden, then the eager loop through the hooks. A module-keyed batch trains
+        each of this learner's modules in it (``add_module``)."""
+        if self._is_module_batch(batch):
+            return self._update_modules(batch, timesteps=timesteps, **kwargs)
         kind = kwargs.get("kind") or self.config.get("_learner_kind", "ppo")
         return self.update_ppo(batch) if kind == "ppo" else self.update_vtrace(batch)
 
@@ -1222,7 +1469,16 @@ class LearnerGroup:
         import ray_amd as ray
 
         n = len(self.actors)
-        shards = _split_rows(batch, n)
+        if batch and all(isinstance(v, dict) for v in batch.values()):  # module-keyed
+            per = {m: _split_rows(b, n) for m, b in batch.items()}
+            shards = [{m: per[m][i] for m in batch} for i in range(n)]
+            rows = [min(_rows(b) for b in sh.values()) for sh in shards]
+        else:
+            shards = _split_rows(batch, n)
+            rows = [_rows(sh) for sh in shards]
+        if min(rows) == 0:
+            raise ValueError(f"a batch of {_rows(batch) if shards else 0} rows cannot feed "
+                             f"{n} learners: every learner needs at least one row")
         refs = [a.execute.remote(_learner_call_kw, "update_from_batch", (sh,),
                                  dict(kwargs, timesteps=timesteps))
                 for a, sh in zip(self.actors, shards)]
@@ -1231,13 +1487,23 @@ class LearnerGroup:
         return _reduce_results(ray.get(refs))
 
     def update_from_episodes(self, episodes, *, async_update=False, timesteps=None, **kwargs):
-        """One update step on a list of episodes, dealt round-robin to the learners."""
+        """One update step on a list of episodes, split across the learners by rows: the
+        longest episodes first, each to the learner with the fewest rows so far (the
+        learners then agree on a common minibatch count, see ``update_from_batch``)."""
         if not self.remote:
             return self.local.update_from_episodes(episodes, timesteps=timesteps, **kwargs)
         import ray_amd as ray
 
         n = len(self.actors)
-        refs = [a.execute.remote(_learner_call_kw, "update_from_episodes", (episodes[i::n],),
+        if len(episodes) < n:
+            raise ValueError(f"{len(episodes)} episodes cannot feed {n} learners: every "
+                             "learner needs at least one")
+        shards, rows = [[] for _ in range(n)], [0] * n
+        for ep in sorted(episodes, key=len, reverse=True):
+            i = rows.index(min(rows))
+            shards[i].append(ep)
+            rows[i] += len(ep)
+        refs = [a.execute.remote(_learner_call_kw, "update_from_episodes", (shards[i],),
                                  dict(kwargs, timesteps=timesteps))
                 for i, a in enumerate(self.actors)]
         if async_update:
@@ -1259,14 +1525,60 @@ class LearnerGroup:
             return self.local.save_state(path)
         import ray_amd as ray
 
-        st = ray.get(self.actors[0].execute.remote(_learner_call, "get_state"))
+        st = ray.get(self.actors[0].execute.remote(_learner_call, "get_full_state"))
         os.makedirs(path, exist_ok=True)
-        torch.save(st, os.path.join(path, "learner_state.pt"))
+        torch.save(_plain(st), os.path.join(path, "learner_state.pt"))
         return path
 
     def load_state(self, path: str):
         f = os.path.join(path, "learner_state.pt") if os.path.isdir(path) else path
-        self.set_state(torch.load(f, map_location="cpu", weights_only=False))
+        st = torch.load(f, map_location="cpu", weights_only=True)
+        if not self.remote:
+            return self.local.set_full_state(st)
+        import ray_amd as ray
+
+        ray.get([a.execute.remote(_learner_call, "set_full_state", st) for a in self.actors])
+
+    # ---------------------------------------------------------------- the module set
+    # reference: rllib/core/learner/learner_group.py:494 add_module, :520 remove_module,
+    # get/set_module_state, get/set_optimizer_state. Every learner of the group runs the
+    # call (adding a module is collective: its initial weights come from rank 0).
+    def _all(self, name, *args, **kwargs):
+        if not self.remote:
+            return [getattr(self.local, name)(*args, **kwargs)]
+        import ray_amd as ray
+
+        return ray.get([a.execute.remote(_learner_call_kw, name, args, kwargs)
+                        for a in self.actors])
+
+    def add_module(self, *, module_id, module_spec=None, config_overrides=None,
+                   new_should_module_be_updated=None):
+        return self._all("add_module", module_id=module_id, module_spec=module_spec,
+                         config_overrides=config_overrides,
+                         new_should_module_be_updated=new_should_module_be_updated)[0]
+
+    def remove_module(self, module_id, *, new_should_module_be_updated=None):
+        return self._all("remove_module", module_id,
+                         new_should_module_be_updated=new_should_module_be_updated)[0]
+
+    def get_module_state(self, module_ids=None) -> dict:
+        return self._all("get_module_state", module_ids)[0] if not self.remote else \
+            self._rank0("get_module_state", module_ids)
+
+    def set_module_state(self, state: dict):
+        self._all("set_module_state", state)
+
+    def get_optimizer_state(self) -> dict:
+        return self._all("get_optimizer_state")[0] if not self.remote else \
+            self._rank0("get_optimizer_state")
+
+    def set_optimizer_state(self, state: dict):
+        self._all("set_optimizer_state", state)
+
+    def _rank0(self, name, *args):
+        import ray_amd as ray
+
+        return ray.get(self.actors[0].execute.remote(_learner_call_kw, name, args, {}))
 
     def sync_target(self):
         """Off-policy learners: copy the online networks into their targets."""
@@ -1336,18 +1648,42 @@ class LearnerGroup:
         ray.get([a.execute.remote(_learner_call, "set_weights", w) for a in self.actors])
 
     def get_state(self):
+        """Rank 0's learner state, added modules included (all ranks hold the same)."""
         if not self.remote:
-            return self.local.get_state()
+            return self.local.get_full_state()
         import ray_amd as ray
 
-        return ray.get(self.actors[0].execute.remote(_learner_call, "get_state"))
+        return ray.get(self.actors[0].execute.remote(_learner_call, "get_full_state"))
 
     def set_state(self, s):
         if not self.remote:
-            return self.local.set_state(s)
+            return self.local.set_full_state(s)
         import ray_amd as ray
 
-        ray.get([a.execute.remote(_learner_call, "set_state", s) for a in self.actors])
+        ray.get([a.execute.remote(_learner_call, "set_full_state", s) for a in self.actors])
+
+    def update_modules(self, kind, per_module: dict) -> dict:
+        """One PPO / V-trace update of several modules of this group's learners:
+        ``per_module`` = {module_id: list of rollout batches}; returns {module_id: stats}
+        (rank 0's). Modules train in sorted id order on every learner."""
+        if not self.remote:
+            lrs = self.local._module_learners()
+            lazy = ("obs",) if self.local.device.type == "cuda" else ()
+            out = {}
+            for m in sorted(per_module, key=str):
+                bs = per_module[m]
+                b = concat_batches(bs, lazy) if isinstance(bs, list) else bs
+                out[m] = lrs[m].update_ppo(b) if kind == "ppo" else lrs[m].update_vtrace(b)
+            return out
+        import ray_amd as ray
+
+        n = len(self.actors)
+        whole = {m: concat_batches(bs) if isinstance(bs, list) else bs
+                 for m, bs in per_module.items()}
+        shards = [{m: _split_b(b, n, i) for m, b in whole.items()} for i in range(n)]
+        res = ray.get([a.execute.remote(_learner_update_modules, kind, sh)
+                       for a, sh in zip(self.actors, shards)])
+        return res[0]
 
     def shutdown(self):
         if self.remote:
@@ -1414,6 +1750,12 @@ def _learner_update(kind, batches):
     return _LEARNER.update_ppo(b) if kind == "ppo" else _LEARNER.update_vtrace(b)
 
 
+def _learner_update_modules(kind, per_module):
+    lrs = _LEARNER._module_learners()
+    return {m: (lrs[m].update_ppo(b) if kind == "ppo" else lrs[m].update_vtrace(b))
+            for m, b in sorted(per_module.items(), key=lambda kv: str(kv[0]))}
+
+
 def _learner_update_refs(kind, refs):
     import ray_amd as ray
 
@@ -1438,60 +1780,117 @@ def _split_b(batch, n, i):
 
 
 class MultiAgentLearnerGroup:
-    """One LearnerGroup per trainable module (reference: rllib/core/learner/learner_group.py
-    over a MultiRLModule).  Modules are independent networks with independent optimizers,
-    so each gets its own flat-param learner; runner outputs are split by module id."""
+    """The learners of a multi-agent algorithm (reference: rllib/core/learner/
+    learner_group.py over a MultiRLModule): ONE LearnerGroup whose every learner holds every
+    module — the first module is each learner's own, the others join through
+    ``Learner.add_module`` (their own networks, optimizers and losses; gradients averaged
+    over the group per module). Runner outputs are split by module id; only the
+    ``trainable`` modules are updated."""
 
     def __init__(self, config: dict, specs: dict, policies_to_train=None):
         self.config = config
-        self.specs = specs
+        self.specs = dict(specs)
         self.trainable = set(policies_to_train) if policies_to_train else set(specs)
-        self.groups = {mid: LearnerGroup(config, os_, as_, module_id=mid)
-                       for mid, (os_, as_) in specs.items()}
+        ids = list(specs)
+        self.primary = ids[0]
+        self.group = LearnerGroup(config, *specs[self.primary], module_id=self.primary)
+        self._hidden = set()  # a removed primary: kept inside the learners, never reported
+        for mid in ids[1:]:
+            self.group.add_module(module_id=mid, module_spec=tuple(specs[mid]))
+
+    @property
+    def module_ids(self) -> list:
+        return [m for m in self.specs if m not in self._hidden]
+
+    def _set_trainable(self, spec):
+        ids = self.module_ids
+        self.trainable = ({m for m in ids if spec(m)} if callable(spec)
+                          else set(spec) & set(ids))
+
+    # reference-named module-set API (learner_group.py:494 add_module, :520 remove_module)
+    def add_module(self, *, module_id, module_spec, config_overrides=None,
+                   new_should_module_be_updated=None):
+        spec = tuple(module_spec) if isinstance(module_spec, (tuple, list)) else module_spec
+        self.group.add_module(module_id=module_id, module_spec=spec,
+                              config_overrides=config_overrides)
+        self.specs = dict(self.specs)
+        self.specs[module_id] = spec if isinstance(spec, tuple) else \
+            (spec.observation_space, spec.action_space)
+        if new_should_module_be_updated is None:
+            self.trainable.add(module_id)
+        else:
+            self._set_trainable(new_should_module_be_updated)
+        return self.module_ids
+
+    def remove_module(self, module_id, *, new_should_module_be_updated=None):
+        if module_id == self.primary:
+            self._hidden.add(module_id)  # the learners' own module stays built, unused
+        else:
+            self.group.remove_module(module_id)
+        self.specs = {k: v for k, v in self.specs.items() if k != module_id}
+        self.trainable.discard(module_id)
+        if new_should_module_be_updated is not None:
+            self._set_trainable(new_should_module_be_updated)
+        return self.module_ids
 
     def add(self, mid, spec, trainable=True):
-        """A new module's learner group mid-training (Algorithm.add_module)."""
-        self.specs = dict(self.specs)
-        self.specs[mid] = spec
-        self.groups[mid] = LearnerGroup(self.config, spec[0], spec[1], module_id=mid)
-        if trainable:
-            self.trainable.add(mid)
+        """Algorithm.add_module's spelling (a trainable flag instead of the update set)."""
+        self.add_module(module_id=mid, module_spec=spec)
+        if not trainable:
+            self.trainable.discard(mid)
 
     def remove(self, mid):
-        g = self.groups.pop(mid, None)
-        self.specs = {k: v for k, v in self.specs.items() if k != mid}
-        self.trainable.discard(mid)
-        if g is not None:
-            g.shutdown()
+        self.remove_module(mid)
+
+    def get_module_state(self, module_ids=None) -> dict:
+        ids = self.module_ids if module_ids is None else \
+            [m for m in module_ids if m in self.module_ids]
+        return self.group.get_module_state(ids)
+
+    def set_module_state(self, state: dict):
+        self.group.set_module_state(state)
+
+    def get_optimizer_state(self) -> dict:
+        return {m: st for m, st in self.group.get_optimizer_state().items()
+                if m not in self._hidden}
+
+    def set_optimizer_state(self, state: dict):
+        self.group.set_optimizer_state(state)
 
     def foreach_learner(self, func, **kwargs):
-        return {mid: g.foreach_learner(func, **kwargs) for mid, g in self.groups.items()}
+        """{module_id: [func(that module's learner) on every rank]}."""
+        out = {}
+        for mid in self.module_ids:
+            out[mid] = self.group.foreach_learner(_on_module, _mid=mid, _func=func, **kwargs)
+        return out
 
     def update(self, kind, batches):
-        stats = {}
-        for mid, g in self.groups.items():
+        per = {}
+        for mid in self.module_ids:
             if mid not in self.trainable:
                 continue
             mb = [b["modules"][mid] for b in batches if mid in b["modules"]]
             if mb:
-                stats[mid] = g.update(kind, mb)
-        return stats
+                per[mid] = mb
+        return self.group.update_modules(kind, per) if per else {}
 
     def get_weights(self):
-        return {mid: g.get_weights() for mid, g in self.groups.items()}
+        return self.get_module_state()
 
     def set_weights(self, w):
-        for mid, wm in w.items():
-            if mid in self.groups:
-                self.groups[mid].set_weights(wm)
+        self.set_module_state({m: wm for m, wm in w.items() if m in self.specs})
 
     def get_state(self):
-        return {mid: g.get_state() for mid, g in self.groups.items()}
+        return {"modules": self.module_ids, "trainable": sorted(self.trainable, key=str),
+                "learner": self.group.get_state()}
 
     def set_state(self, s):
-        for mid, st in s.items():
-            self.groups[mid].set_state(st)
+        self.group.set_state(s["learner"])
+        self.trainable = set(s.get("trainable") or self.trainable)
 
     def shutdown(self):
-        for g in self.groups.values():
-            g.shutdown()
+        self.group.shutdown()
+
+
+def _on_module(lr, _mid, _func, **kwargs):
+    return _func(lr._module_learners()[_mid], **kwargs)

@@ -161,3 +161,29 @@ def test_cancel_does_not_hit_the_next_task(cluster):
     assert ray.get(r) == 1
     ray.cancel(r)  # already finished: no effect
     assert ray.get(slowish.remote(), timeout=30) == "done"
+
+
+def test_force_cancel_of_actor_task_is_rejected(cluster):
+    """Reference: test_actor_cancel.py — force=True is not supported for actor tasks
+    (core_worker.cc CancelTask returns InvalidArgument); the actor and its state survive."""
+
+    @ray.remote(num_cpus=0)
+    class Counter:
+        def __init__(self):
+            self.n = 0
+
+        def inc(self):
+            self.n += 1
+            return self.n
+
+        def slow(self):
+            time.sleep(2)
+            return "done"
+
+    a = Counter.remote()
+    assert ray.get(a.inc.remote()) == 1
+    r = a.slow.remote()
+    with pytest.raises(ValueError, match="force=True is not supported for actor tasks"):
+        ray.cancel(r, force=True)
+    assert ray.get(r, timeout=30) == "done"
+    assert ray.get(a.inc.remote()) == 2

@@ -236,3 +236,88 @@ def test_self_play_add_module_mid_training(cluster):
         assert set(algo.get_weights()) == {"main"}
     finally:
         algo.stop()
+
+
+def test_two_gloo_learners_add_module_and_restore_optimizer_state(cluster):
+    """Learner / LearnerGroup module-set API (reference: learner.py:607,696,714,821,845,
+    1308,1316; learner_group.py:494,520): a module added mid-training trains with
+    identical weights on both ranks, and a second group restored from the first's module
+    + optimizer state takes the next update bit-exactly like the first."""
+    env = make_env("CartPole-v1", {})
+    cfg = _dqn_cfg(num_learners=2, learner_backend="gloo")
+
+    def group():
+        return LearnerGroup(cfg, env.observation_space, env.action_space,
+                            learner_class=DQNLearner)
+
+    g = group()
+    try:
+        g.update_from_batch(_cartpole_batch(64, 0), minibatch_size=16)
+        ids = g.add_module(module_id="opp", module_spec=(env.observation_space,
+                                                         env.action_space),
+                           config_overrides={"lr": 5e-3})
+        assert ids == ["default_policy", "opp"]
+        w_opp0 = g.get_module_state(["opp"])["opp"]
+        for i in range(3):
+            res = g.update_from_batch({"default_policy": _cartpole_batch(64, 10 + i),
+                                       "opp": _cartpole_batch(48, 20 + i)},
+                                      minibatch_size=16, shuffle_batch_per_epoch=True)
+        assert "opp/loss" in res and np.isfinite(res["opp/loss"])
+        both = g.foreach_learner(lambda lr: {m: {k: v.numpy().copy() for k, v in w.items()}
+                                             for m, w in lr.get_module_state().items()})
+        for m in ("default_policy", "opp"):
+            for k in both[0][m]:
+                np.testing.assert_array_equal(both[0][m][k], both[1][m][k], err_msg=f"{m}/{k}")
+        assert any(not np.array_equal(np.asarray(w_opp0[k]), both[0]["opp"][k])
+                   for k in w_opp0)
+        lr_opp = g.foreach_learner(lambda lr: lr._module_learners()["opp"].get_optimizer()
+                                   .param_groups[0]["lr"])
+        assert lr_opp == [5e-3, 5e-3]  # config_overrides reached the module's optimizer
+
+        # restore into a fresh group: module weights + optimizer moments
+        ms, os_ = g.get_module_state(), g.get_optimizer_state()
+        assert set(os_) == {"default_policy", "opp"} and os_["opp"]["opp/default"]["state"]
+        h = group()
+        try:
+            h.add_module(module_id="opp", module_spec=(env.observation_space,
+                                                       env.action_space),
+                         config_overrides={"lr": 5e-3})
+            h.set_module_state(ms)
+            h.set_optimizer_state(os_)
+            nb = {"default_policy": _cartpole_batch(64, 99), "opp": _cartpole_batch(48, 98)}
+            g.update_from_batch(nb)
+            h.update_from_batch(nb)
+            a, b = g.get_module_state(), h.get_module_state()
+            for m in a:
+                for k in a[m]:
+                    assert torch.equal(a[m][k], b[m][k]), f"{m}/{k}"
+            # remove_module drops it from every learner
+            assert h.remove_module("opp") == ["default_policy"]
+            assert h.foreach_learner(lambda lr: lr.module_ids) == [["default_policy"]] * 2
+        finally:
+            h.shutdown()
+    finally:
+        g.shutdown()
+
+
+def test_register_metrics_and_weights_only_state(tmp_path):
+    env = make_env("CartPole-v1", {})
+    lr = DQNLearner(_dqn_cfg(), env.observation_space, env.action_space)
+    lr.add_module(module_id="b", module_spec=(env.observation_space, env.action_space))
+    lr.register_metrics("b", {"my_metric": torch.tensor(2.5)})
+    assert lr._module_learners()["b"].metrics["my_metric"] == 2.5
+    res = lr.update_from_batch({"default_policy": _cartpole_batch(32, 0),
+                                "b": _cartpole_batch(32, 1)})
+    assert res["b/my_metric"] == 2.5
+    path = lr.save_state(str(tmp_path / "s"))
+    # loadable without unpickling code
+    st = torch.load(str(tmp_path / "s" / "learner_state.pt"), weights_only=True)
+    assert "b" in st["__modules__"]
+    lr2 = DQNLearner(_dqn_cfg(seed=3), env.observation_space, env.action_space)
+    lr2.add_module(module_id="b", module_spec=(env.observation_space, env.action_space))
+    lr2.load_state(path)
+    for m, w in lr.get_module_state().items():
+        for k, v in w.items():
+            assert torch.equal(v, lr2.get_module_state()[m][k])
+    with pytest.raises(ValueError):
+        lr.add_module(module_id="b")
