@@ -108,6 +108,17 @@ class PerModuleLearners:
             lr.shutdown()
 
 
+def flat_transitions(b: dict, keys=("obs", "next_obs", "actions", "rewards", "terminateds")):
+    """[T, B] runner fragment -> transition rows for a replay buffer; padding rows
+    (loss_mask 0, batch_mode="complete_episodes") are dropped."""
+    T, B = b["rewards"].shape
+    flat = {k: b[k].reshape((T * B,) + b[k].shape[2:]) for k in keys}
+    if "loss_mask" in b:
+        keep = b["loss_mask"].reshape(-1) > 0
+        flat = {k: v[keep] for k, v in flat.items()}
+    return flat
+
+
 def add_agent_rows(buffers, batch):
     """Completed agent rows (loss_mask 1) of a multi-agent sample become transitions of
     their module's replay buffer; returns the number added."""

@@ -68,32 +68,98 @@ class AlgorithmConfig:
         self.keep_per_episode_custom_metrics = False
         self.extra_python_environs_for_driver = {}
         self.extra_python_environs_for_worker = {}
+        # environment() (reference: algorithm_config.py:1385-1398): rewards clipped in the
+        # train batch (True: sign, float c: [-c, c]); Box actions unsquashed from [-1, 1]
+        # to the bounds (normalize_actions) or clipped to them (clip_actions)
+        self.clip_rewards = None
+        self.normalize_actions = True
+        self.clip_actions = False
+        self.observation_space = None
+        self.action_space = None
+        self.render_env = False
+        self.disable_env_checking = False
+        self.action_mask_key = "action_mask"
+        self.env_task_fn = None
+        # env_runners() (reference: :1515 batch_mode and the runner options around it)
+        self.batch_mode = "truncate_episodes"
+        self.sample_timeout_s = 60.0
+        self.create_env_on_local_worker = False
+        self.custom_resources_per_env_runner = {}
+        self.validate_env_runners_after_construction = True
+        self.max_requests_in_flight_per_env_runner = 2
+        self.episode_lookback_horizon = 1
+        self.compress_observations = False
+        self.remote_worker_envs = False
+        self.remote_env_batch_wait_ms = 0
+        self.add_default_connectors_to_env_to_module_pipeline = True
+        self.add_default_connectors_to_module_to_env_pipeline = True
+        self.update_worker_filter_stats = True
+        self.use_worker_filter_stats = True
+        # learners()
+        self.num_cpus_per_learner = 1
+        self.local_gpu_idx = 0
+        # checkpointing() / debugging() / reporting()
+        self.export_native_model_files = False
+        self.log_level = "WARN"
+        self.log_sys_usage = True
+        self.logger_config = None
+        self.fake_sampler = False
+        self.keep_per_episode_custom_metrics = False
+        self.min_sample_timesteps_per_iteration = 0
+        self.min_train_timesteps_per_iteration = 0
 
     # ---------------------------------------------------------------- builders
-    def environment(self, env=None, *, env_config=None, **kw):
+    def _set_keys(self, method: str, kw: dict, known, renames=None) -> "AlgorithmConfig":
+        """Set builder keywords: every key must be one this builder knows (a typo raises
+        instead of being silently dropped); None leaves the current value."""
+        renames = renames or {}
+        unknown = sorted(k for k in kw if k not in known and k not in renames)
+        if unknown:
+            raise ValueError(f"{type(self).__name__}.{method}() got unknown key(s) {unknown}")
+        for k, v in kw.items():
+            if v is not None:
+                setattr(self, renames.get(k, k), v)
+        return self
+
+    _ENV_KEYS = ("observation_space", "action_space", "render_env", "clip_rewards",
+                 "normalize_actions", "clip_actions", "disable_env_checking",
+                 "action_mask_key", "env_task_fn")
+
+    def environment(self, env=None, *, env_config=None, is_atari=None, **kw):
+        """reference: AlgorithmConfig.environment (algorithm_config.py:1360)."""
         if env is not None:
             self.env = env
         if env_config is not None:
             self.env_config = dict(env_config)
-        return self
+        if is_atari is not None:
+            self._is_atari = bool(is_atari)
+        if kw.get("clip_rewards") not in (None, True, False) and \
+                not isinstance(kw["clip_rewards"], (int, float)):
+            raise ValueError("clip_rewards must be None, a bool or a float bound")
+        return self._set_keys("environment", kw, self._ENV_KEYS)
 
-    def env_runners(self, *, num_env_runners=None, num_envs_per_env_runner=None,
-                    rollout_fragment_length=None, num_cpus_per_env_runner=None,
-                    num_gpus_per_env_runner=None, env_to_module_connector=None,
-                    module_to_env_connector=None, observation_filter=None,
-                    sample_async=None, **kw):
-        for k, v in dict(num_env_runners=num_env_runners,
-                         num_envs_per_env_runner=num_envs_per_env_runner,
-                         rollout_fragment_length=rollout_fragment_length,
-                         num_cpus_per_env_runner=num_cpus_per_env_runner,
-                         num_gpus_per_env_runner=num_gpus_per_env_runner,
-                         env_to_module_connector=env_to_module_connector,
-                         module_to_env_connector=module_to_env_connector,
-                         observation_filter=observation_filter,
-                         sample_async=sample_async).items():
-            if v is not None:
-                setattr(self, k, v)
-        return self
+    _RUNNER_KEYS = ("num_env_runners", "num_envs_per_env_runner", "rollout_fragment_length",
+                    "num_cpus_per_env_runner", "num_gpus_per_env_runner",
+                    "env_to_module_connector", "module_to_env_connector",
+                    "observation_filter", "sample_async", "batch_mode", "explore",
+                    "exploration_config", "sample_timeout_s", "create_env_on_local_worker",
+                    "custom_resources_per_env_runner", "validate_env_runners_after_construction",
+                    "max_requests_in_flight_per_env_runner", "episode_lookback_horizon",
+                    "compress_observations", "remote_worker_envs", "remote_env_batch_wait_ms",
+                    "add_default_connectors_to_env_to_module_pipeline",
+                    "add_default_connectors_to_module_to_env_pipeline",
+                    "update_worker_filter_stats", "use_worker_filter_stats")
+
+    def env_runners(self, **kw):
+        """reference: AlgorithmConfig.env_runners (algorithm_config.py:1480)."""
+        bm = kw.get("batch_mode")
+        if bm is not None and bm not in ("truncate_episodes", "complete_episodes"):
+            raise ValueError(f"batch_mode must be 'truncate_episodes' or 'complete_episodes', "
+                             f"got {bm!r}")
+        return self._set_keys("env_runners", kw, self._RUNNER_KEYS,
+                              {"create_local_env_runner": "create_env_on_local_worker",
+                               "num_rollout_workers": "num_env_runners",
+                               "num_envs_per_worker": "num_envs_per_env_runner"})
 
     def rollouts(self, *, num_rollout_workers=None, num_envs_per_worker=None, **kw):
         return self.env_runners(num_env_runners=num_rollout_workers,
@@ -122,30 +188,56 @@ class AlgorithmConfig:
             setattr(self, aliases.get(k, k), v)
         return self
 
-    def resources(self, *, num_gpus=None, **kw):
+    def resources(self, *, num_gpus=None, num_cpus_for_main_process=None,
+                  num_cpus_per_worker=None, num_gpus_per_worker=None, **kw):
+        self._set_keys("resources", kw, ("placement_strategy", "custom_resources_per_worker",
+                                         "num_cpus_per_learner_worker",
+                                         "num_gpus_per_learner_worker", "num_learner_workers"),
+                       )
         if num_gpus is not None:
             self.num_gpus_per_learner = num_gpus if num_gpus <= 1 else 1
             if num_gpus > 1:
                 self.num_learners = int(num_gpus)
+        if num_cpus_for_main_process is not None:
+            self.num_cpus_for_main_process = num_cpus_for_main_process
+        if num_cpus_per_worker is not None:
+            self.num_cpus_per_env_runner = num_cpus_per_worker
+        if num_gpus_per_worker is not None:
+            self.num_gpus_per_env_runner = num_gpus_per_worker
         return self
 
-    def learners(self, *, num_learners=None, num_gpus_per_learner=None, **kw):
-        if num_learners is not None:
-            self.num_learners = num_learners
-        if num_gpus_per_learner is not None:
-            self.num_gpus_per_learner = num_gpus_per_learner
-        return self
+    def learners(self, **kw):
+        """reference: AlgorithmConfig.learners (algorithm_config.py:2200)."""
+        return self._set_keys("learners", kw, ("num_learners", "num_gpus_per_learner",
+                                               "num_cpus_per_learner", "local_gpu_idx",
+                                               "max_requests_in_flight_per_learner"))
 
     def callbacks(self, callbacks_class=None, **kw):
         """RLlibCallback subclass / instance / list of them (reference:
-        AlgorithmConfig.callbacks)."""
+        AlgorithmConfig.callbacks); per-event callables (``on_episode_end=fn``, ...) are
+        kept in ``callbacks_on_events``."""
+        if kw:
+            events = ("on_algorithm_init", "on_train_result", "on_evaluate_start",
+                      "on_evaluate_end", "on_env_runners_recreated", "on_checkpoint_loaded",
+                      "on_environment_created", "on_episode_created", "on_episode_start",
+                      "on_episode_step", "on_episode_end", "on_sample_end")
+            bad = sorted(k for k in kw if k not in events)
+            if bad:
+                raise ValueError(f"{type(self).__name__}.callbacks() got unknown key(s) {bad}")
+            self.callbacks_on_events = {k: v for k, v in kw.items() if v is not None}
         self.callbacks_class = callbacks_class
         return self
 
     def rl_module(self, *, rl_module_spec=None, model_config=None, model_config_dict=None,
-                  **kw):
+                  algorithm_config_overrides_per_module=None, **kw):
         """A user RLModule (RLModuleSpec / MultiRLModuleSpec) and / or the model config
         of the default modules (reference: AlgorithmConfig.rl_module)."""
+        if kw:
+            raise ValueError(f"{type(self).__name__}.rl_module() got unknown key(s) "
+                             f"{sorted(kw)}")
+        if algorithm_config_overrides_per_module is not None:
+            self.algorithm_config_overrides_per_module = dict(
+                algorithm_config_overrides_per_module)
         if rl_module_spec is not None:
             self._rl_module_spec = rl_module_spec
         mc = model_config if model_config is not None else model_config_dict
@@ -178,6 +270,8 @@ class AlgorithmConfig:
                         env_runner_health_probe_timeout_s=None,
                         restart_failed_sub_environments=None, recreate_failed_env_runners=None,
                         **kw):
+        self._set_keys("fault_tolerance", kw, ("num_consecutive_env_runner_failures_tolerance",
+                                               "env_runner_restore_timeout_s"))
         if recreate_failed_env_runners is not None:  # old name
             restart_failed_env_runners = recreate_failed_env_runners
         for k, v in dict(restart_failed_env_runners=restart_failed_env_runners,
@@ -191,13 +285,14 @@ class AlgorithmConfig:
                 setattr(self, k, v)
         return self
 
-    def checkpointing(self, *, export_native_model_files=None,
-                      checkpoint_trainable_policies_only=None, **kw):
-        if checkpoint_trainable_policies_only is not None:
-            self.checkpoint_trainable_policies_only = checkpoint_trainable_policies_only
-        return self
+    def checkpointing(self, **kw):
+        return self._set_keys("checkpointing", kw, ("export_native_model_files",
+                                                    "checkpoint_trainable_policies_only"))
 
     def exploration(self, *, explore=None, exploration_config=None, **kw):
+        if kw:
+            raise ValueError(f"{type(self).__name__}.exploration() got unknown key(s) "
+                             f"{sorted(kw)}")
         if explore is not None:
             self.explore = bool(explore)
         if exploration_config is not None:
@@ -206,6 +301,9 @@ class AlgorithmConfig:
 
     def python_environment(self, *, extra_python_environs_for_driver=None,
                            extra_python_environs_for_worker=None, **kw):
+        if kw:
+            raise ValueError(f"{type(self).__name__}.python_environment() got unknown "
+                             f"key(s) {sorted(kw)}")
         if extra_python_environs_for_driver is not None:
             self.extra_python_environs_for_driver = dict(extra_python_environs_for_driver)
         if extra_python_environs_for_worker is not None:
@@ -213,6 +311,14 @@ class AlgorithmConfig:
         return self
 
     def experimental(self, **kw):
+        known = ("_validate_config", "_use_msgpack_checkpoints", "_torch_grad_scaler_class",
+                 "_torch_lr_scheduler_classes", "_tf_policy_handles_more_than_one_loss",
+                 "_disable_preprocessor_api", "_disable_action_flattening",
+                 "_disable_initialize_loss_from_dummy_batch", "_disable_execution_plan_api",
+                 "_enable_new_api_stack")
+        bad = sorted(k for k in kw if k not in known and "_" + k not in known)
+        if bad:
+            raise ValueError(f"{type(self).__name__}.experimental() got unknown key(s) {bad}")
         for k, v in kw.items():
             setattr(self, k.lstrip("_"), v)
         return self
@@ -264,6 +370,8 @@ class AlgorithmConfig:
 
     @property
     def is_atari(self) -> bool:
+        if self.__dict__.get("_is_atari") is not None:
+            return self.__dict__["_is_atari"]
         e = self.env if isinstance(self.env, str) else ""
         return e.startswith("ALE/") or "NoFrameskip" in e
 
@@ -458,19 +566,38 @@ class AlgorithmConfig:
         return cls().update_from_dict(d)
 
     def framework(self, framework="torch", **kw):
+        # tf / torch.compile options of the reference: accepted and recorded; this stack
+        # has no tracing compiler (HIP graphs + hand-written kernels)
+        self._set_keys("framework", kw, (
+            "eager_tracing", "eager_max_retraces", "tf_session_args", "local_tf_session_args",
+            "torch_compile_learner", "torch_compile_learner_what_to_compile",
+            "torch_compile_learner_dynamo_mode", "torch_compile_learner_dynamo_backend",
+            "torch_compile_worker", "torch_compile_worker_dynamo_backend",
+            "torch_compile_worker_dynamo_mode", "torch_ddp_kwargs",
+            "torch_skip_nan_gradients"))
         if framework not in ("torch",):
             raise ValueError("ray_amd RLlib supports framework='torch' only (MI355X/ROCm)")
         self.framework_str = framework
         return self
 
-    def debugging(self, *, seed=None, **kw):
-        if seed is not None:
-            self.seed = seed
-        return self
+    def debugging(self, **kw):
+        return self._set_keys("debugging", kw, ("seed", "log_level", "log_sys_usage",
+                                                "logger_config", "fake_sampler",
+                                                "logger_creator"))
+
+    _EVAL_KEYS = ("evaluation_sample_timeout_s", "evaluation_force_reset_envs_before_iteration",
+                  "evaluation_auto_duration_min_env_steps_per_sample",
+                  "evaluation_auto_duration_max_env_steps_per_sample", "custom_evaluation_function",
+                  "off_policy_estimation_methods", "ope_split_batch_by_episode",
+                  "always_attach_evaluation_results")
 
     def evaluation(self, *, evaluation_interval=None, evaluation_duration=None,
                    evaluation_num_env_runners=None, evaluation_config=None,
-                   evaluation_parallel_to_training=None, evaluation_duration_unit=None, **kw):
+                   evaluation_parallel_to_training=None, evaluation_duration_unit=None,
+                   evaluation_num_workers=None, **kw):
+        if evaluation_num_workers is not None:  # old name
+            evaluation_num_env_runners = evaluation_num_workers
+        self._set_keys("evaluation", kw, self._EVAL_KEYS)
         if evaluation_parallel_to_training is not None:
             self.evaluation_parallel_to_training = bool(evaluation_parallel_to_training)
         if evaluation_duration_unit is not None:
@@ -489,14 +616,31 @@ class AlgorithmConfig:
 
     def reporting(self, *, min_time_s_per_iteration=None, metrics_num_episodes_for_smoothing=None,
                   **kw):
+        self._set_keys("reporting", kw, ("keep_per_episode_custom_metrics",
+                                         "min_sample_timesteps_per_iteration",
+                                         "min_train_timesteps_per_iteration",
+                                         "metrics_episode_collection_timeout_s", "log_gradients"))
         if min_time_s_per_iteration is not None:
             self.min_time_s_per_iteration = min_time_s_per_iteration
         if metrics_num_episodes_for_smoothing is not None:
             self.metrics_num_episodes_for_smoothing = metrics_num_episodes_for_smoothing
         return self
 
+    _OFFLINE_KEYS = ("input_config", "input_read_method", "input_read_method_kwargs",
+                     "input_read_schema", "input_read_episodes", "input_read_sample_batches",
+                     "input_read_batch_size", "input_filesystem", "input_compress_columns",
+                     "map_batches_kwargs", "iter_batches_kwargs", "prelearner_class",
+                     "dataset_num_iters_per_learner", "actions_in_input_normalized",
+                     "postprocess_inputs", "shuffle_buffer_size", "output_config",
+                     "output_compress_columns", "output_max_file_size",
+                     "output_max_rows_per_file", "output_write_method",
+                     "output_write_episodes", "offline_sampling")
+
     def offline_data(self, *, input_=None, output=None, **kw):
-        """Offline experience source / sink (reference: AlgorithmConfig.offline_data)."""
+        """Offline experience source / sink (reference: AlgorithmConfig.offline_data,
+        algorithm_config.py:2379): ``input_`` is a path / list of paths (JSON lines or
+        parquet, read through ray_amd.data) or "sampler"."""
+        self._set_keys("offline_data", kw, self._OFFLINE_KEYS)
         if input_ is not None:
             self.input_ = input_
         if output is not None:
@@ -507,6 +651,8 @@ class AlgorithmConfig:
                     algorithm_config_overrides_per_module=None, **kw):
         """reference: AlgorithmConfig.multi_agent -- ``policies`` is a set/list of module ids
         or a dict id -> (observation_space, action_space) / PolicySpec / None."""
+        self._set_keys("multi_agent", kw, ("policy_map_capacity", "policy_states_are_swappable",
+                                           "observation_fn", "count_steps_by"))
         if policies is not None:
             self.policies = policies
         if policy_mapping_fn is not None:
@@ -523,7 +669,8 @@ class AlgorithmConfig:
         return self.policies is not None
 
     def api_stack(self, **kw):
-        return self
+        return self._set_keys("api_stack", kw, ("enable_rl_module_and_learner",
+                                                "enable_env_runner_and_connector_v2"))
 
     # old-API-stack config keys (tuned-example YAML files) -> current attribute names
     _LEGACY_KEYS = {"lambda": "lambda_", "num_workers": "num_env_runners",

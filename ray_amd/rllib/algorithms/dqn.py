@@ -6,7 +6,8 @@ import numpy as np
 import torch
 
 import ray_amd as ray
-from ray_amd.rllib.algorithms.algorithm import Algorithm, PerModuleLearners, add_agent_rows
+from ray_amd.rllib.algorithms.algorithm import (Algorithm, PerModuleLearners, add_agent_rows,
+                                                 flat_transitions)
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import QModule
@@ -189,11 +190,9 @@ class DQN(Algorithm):
                 self.buffer.add(b["episodes"])
                 self.total_env_steps += b["env_steps"]
                 continue
-            T, B = b["rewards"].shape
-            flat = {k: b[k].reshape((T * B,) + b[k].shape[2:])
-                    for k in ("obs", "next_obs", "actions", "rewards", "terminateds")}
+            flat = flat_transitions(b)
             self.buffer.add(flat)
-            self.total_env_steps += T * B
+            self.total_env_steps += len(flat["rewards"])
         stats = {"epsilon": eps}
         if self.total_env_steps < cfg.num_steps_sampled_before_learning_starts:
             return stats

@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 import ray_amd as ray
-from ray_amd.rllib.algorithms.algorithm import Algorithm, PerModuleLearners, add_agent_rows
+from ray_amd.rllib.algorithms.algorithm import (Algorithm, PerModuleLearners, add_agent_rows,
+                                                 flat_transitions)
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import SquashedGaussianPolicy, TwinQ
@@ -237,10 +238,9 @@ class SAC(Algorithm):
                 add_agent_rows(self.buffers, b)
                 new += b["env_steps"]
                 continue
-            T, B = b["rewards"].shape
-            self.buffer.add({k: b[k].reshape((T * B,) + b[k].shape[2:])
-                             for k in ("obs", "next_obs", "actions", "rewards", "terminateds")})
-            new += T * B
+            flat = flat_transitions(b)
+            self.buffer.add(flat)
+            new += len(flat["rewards"])
         self.total_env_steps += new
         stats = {}
         if self.total_env_steps < cfg.num_steps_sampled_before_learning_starts:

@@ -57,9 +57,38 @@ class Fragments:
         return a if dtype is None else a.astype(dtype)
 
 
+def pad_fragment(b: dict, T: int) -> dict:
+    """A [t, B] runner fragment padded to T rows: padding rows are terminated with
+    loss_mask 0 (batch_mode="complete_episodes" fragments have per-runner lengths; the
+    learners drop masked rows and GAE / V-trace never cross a terminated row)."""
+    t0 = b["rewards"].shape[0]
+    if t0 == T and "loss_mask" in b:
+        return b
+    out = {}
+    for k, v in b.items():
+        if isinstance(v, np.ndarray) and k not in _AXIS0 and v.ndim >= 2 and v.shape[0] == t0:
+            pad = np.repeat(v[-1:], T - t0, 0) if k in ("obs", "next_obs") else \
+                np.zeros((T - t0,) + v.shape[1:], v.dtype)
+            if k == "terminateds":
+                pad[:] = 1
+            out[k] = np.concatenate([v, pad], 0) if T > t0 else v
+        else:
+            out[k] = v
+    if "loss_mask" not in b:
+        m = np.zeros((T,) + b["rewards"].shape[1:], np.float32)
+        m[:t0] = 1.0
+        out["loss_mask"] = m
+    return out
+
+
 def concat_batches(batches, lazy=()):
     """Concatenate runner fragments along the env (B) axis (keys in ``lazy`` become
-    ``Fragments``)."""
+    ``Fragments``); fragments of different lengths are padded (``pad_fragment``)."""
+    lens = {b["rewards"].shape[0] for b in batches if isinstance(b.get("rewards"), np.ndarray)}
+    if len(lens) > 1 or (len(batches) > 1 and any("loss_mask" in b for b in batches)
+                         and not all("loss_mask" in b for b in batches)):
+        T = max(lens)
+        batches = [pad_fragment(b, T) for b in batches]
     out = {}
     for k in batches[0]:
         v = batches[0][k]

@@ -18,6 +18,13 @@ import torch
 from ray_amd.rllib.env.envs import make_env
 
 
+def _grow(x, n):
+    """Append n uninitialised-but-zeroed rows along the time axis."""
+    if x is None:
+        return None
+    return np.concatenate([x, np.zeros((n,) + x.shape[1:], x.dtype)], 0)
+
+
 class SingleAgentEnvRunner:
     def __init__(self, config: dict, worker_index: int = 0):
         torch.set_num_threads(int(config.get("num_cpus_per_env_runner", 1) or 1))
@@ -62,6 +69,31 @@ class SingleAgentEnvRunner:
                       if getattr(c, "learner_side", False)]
         self.module_to_env = build_pipeline(config.get("module_to_env_connector"),
                                             self.observation_space, self.action_space)
+        # AlgorithmConfig env / rollout semantics (reference: algorithm_config.py:1385-1398
+        # clip_rewards, normalize_actions, clip_actions; :1515 batch_mode)
+        self.clip_rewards = config.get("clip_rewards")
+        self.batch_mode = config.get("batch_mode") or "truncate_episodes"
+        if self.batch_mode not in ("truncate_episodes", "complete_episodes"):
+            raise ValueError(f"batch_mode must be 'truncate_episodes' or 'complete_episodes', "
+                             f"got {self.batch_mode!r}")
+        kind = config.get("module_kind", "actor_critic")
+        self._final_clip = False
+        if hasattr(self.action_space, "low"):
+            from ray_amd.rllib.connectors.module_to_env import (ClipActions,
+                                                                NormalizeAndClipActions)
+
+            have = {type(c) for c in self.module_to_env.connectors}
+            if kind == "sac":
+                # the SAC actor already rescales its tanh output to the Box bounds
+                self._final_clip = True
+            elif config.get("normalize_actions", True):
+                # the policy acts in [-1, 1]; unsquash to the bounds (and clip) for env.step
+                if NormalizeAndClipActions not in have:
+                    self.module_to_env.append(NormalizeAndClipActions(self.observation_space,
+                                                                      self.action_space))
+            elif config.get("clip_actions", False) and ClipActions not in have:
+                self.module_to_env.append(ClipActions(self.observation_space,
+                                                      self.action_space))
         self.module_obs_space = self.env_to_module.observation_space
         self.callbacks = make_callbacks(config.get("callbacks_class"))
         self.metrics = MetricsLogger()
@@ -209,13 +241,37 @@ class SingleAgentEnvRunner:
             state_in = {k: v.copy() for k, v in self._state.items()}
             resets = np.zeros((T, B), np.float32)
         t0 = time.perf_counter()
-        for t in range(T):
+        # batch_mode "complete_episodes": every env runs its episode to the end once it has
+        # stepped T times, then idles (padding rows: loss_mask 0, terminated); the fragment
+        # is [T' >= T, B] and every env starts the next call at a fresh episode
+        complete = self.batch_mode == "complete_episodes"
+        active = np.ones(B, bool)
+        env_steps = np.zeros(B, np.int64)
+        mask = np.ones((T, B), np.float32) if complete else None
+        reset_next = np.zeros(B, bool)
+        cap = T
+        t = 0
+        while (t < T) if not complete else active.any():
             rec, ob = self._module_obs(np.stack(self.obs), explore)
             if obs_buf is None:
-                obs_buf = np.empty((T,) + rec.shape, dtype=rec.dtype)
+                obs_buf = np.empty((cap,) + rec.shape, dtype=rec.dtype)
                 if next_obs_buf is not None:
                     next_obs_buf = np.empty_like(obs_buf)
+            if t >= cap:  # complete_episodes ran past T: grow every time-major buffer
+                grow = cap
+                obs_buf, act_buf, rew, term, trunc, logp, mask = (
+                    _grow(x, grow) for x in (obs_buf, act_buf, rew, term, trunc, logp, mask))
+                if next_obs_buf is not None:
+                    next_obs_buf = _grow(next_obs_buf, grow)
+                if dist_in is not None:
+                    dist_in = _grow(dist_in, grow)
+                if resets is not None:
+                    resets = _grow(resets, grow)
+                cap += grow
             obs_buf[t] = rec
+            if resets is not None and reset_next.any():  # episode starts in this row
+                resets[t, reset_next] = 1.0
+                reset_next[:] = False
             if self._record:
                 for i in range(B):
                     if not self._eps[i].observations:
@@ -246,7 +302,7 @@ class SingleAgentEnvRunner:
                     di = out["action_dist_inputs"].float()
                     at, lpt = self.module.sample_actions(di, explore)
                     if dist_in is None:
-                        dist_in = np.zeros((T, B, di.shape[-1]), np.float32)
+                        dist_in = np.zeros((cap, B, di.shape[-1]), np.float32)
                     if discrete and di.is_cuda:  # one device->host copy per step
                         h = torch.cat([at.float()[:, None], lpt[:, None], di], 1).cpu().numpy()
                         a = h[:, 0].astype(np.int64)
@@ -265,11 +321,26 @@ class SingleAgentEnvRunner:
                                            episodes=self.episodes,
                                            explore=explore)["actions_for_env"]
             for i, env in enumerate(self.envs):
+                if complete and not active[i]:  # padding row of an env that is done
+                    rew[t, i] = 0.0
+                    term[t, i] = 1.0
+                    trunc[t, i] = 0.0
+                    mask[t, i] = 0.0
+                    if next_obs_buf is not None:
+                        next_obs_buf[t, i] = obs_buf[t, i]
+                    if self._stateful:  # it starts the next call from the initial state
+                        for k, v in self._state0.items():
+                            self._state[k][i] = v
+                    continue
                 ai = a_env[i]
-                if not discrete:
+                if not discrete and self._final_clip:
                     ai = np.clip(ai, self.action_space.low, self.action_space.high)
                 o, r, te, tr, _ = env.step(ai if not discrete else int(ai))
-                rew[t, i] = r
+                env_steps[i] += 1
+                if complete:
+                    mask[t, i] = 1.0
+                rt = self._clip_reward(r)  # the train batch's reward; metrics keep r
+                rew[t, i] = rt
                 self.ep_ret[i] += r
                 self.ep_len[i] += 1
                 ep = self.episodes[i]
@@ -286,7 +357,7 @@ class SingleAgentEnvRunner:
                     nxt = next_obs_buf[t, i] if next_obs_buf is not None else (
                         self._module_obs(o[None], explore, update=False)[0][0] if self._pre
                         else o)
-                    self._eps[i].add_env_step(np.array(nxt), a[i], r, terminated=bool(te),
+                    self._eps[i].add_env_step(np.array(nxt), a[i], rt, terminated=bool(te),
                                               truncated=bool(tr) and not te)
                     if te or tr:
                         from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode
@@ -311,24 +382,38 @@ class SingleAgentEnvRunner:
                     if self._stateful:  # the next episode starts from the initial state
                         for k, v in self._state0.items():
                             self._state[k][i] = v
-                        if t + 1 < T:
-                            resets[t + 1, i] = 1.0
+                        reset_next[i] = True
                     ep.reset(self._act_dummy, self._next_eid)
                     self._next_eid += 1
                     self.callbacks.on_episode_start(episode=ep, env_runner=self, env_index=i,
                                                     metrics_logger=self.metrics)
+                    if complete and env_steps[i] >= T:
+                        active[i] = False
                 self.obs[i] = o
-        self.total_steps += T * B
+            t += 1
+        if complete:  # trim to the steps taken
+            obs_buf, act_buf, rew, term, trunc, logp, mask = (
+                x[:t] for x in (obs_buf, act_buf, rew, term, trunc, logp, mask))
+            if next_obs_buf is not None:
+                next_obs_buf = next_obs_buf[:t]
+            if dist_in is not None:
+                dist_in = dist_in[:t]
+            if resets is not None:
+                resets = resets[:t]
+        n_real = int(env_steps.sum())
+        self.total_steps += n_real
         boot = np.stack(self.obs)
         if self._pre:
             boot = self._module_obs(boot, explore, update=False)[0]
         batch = {"obs": obs_buf, "actions": act_buf, "rewards": rew, "terminateds": term,
                  "truncateds": trunc, "action_logp": logp,
-                 "bootstrap_obs": boot, "env_steps": T * B,
+                 "bootstrap_obs": boot, "env_steps": n_real,
                  "sample_time_s": time.perf_counter() - t0,
                  "weights_version": self.weights_version}
         if dist_in is not None:
             batch["action_dist_inputs"] = dist_in
+        if mask is not None:
+            batch["loss_mask"] = mask
         if resets is not None:
             for k, v in state_in.items():
                 batch[f"state_in_{k}"] = v
@@ -348,7 +433,7 @@ class SingleAgentEnvRunner:
 
                 self._writer = JsonWriter(self.config["output"], self.worker_index)
             if next_obs_buf is None:  # next_obs from the rolled-forward observations
-                nxt = np.concatenate([obs_buf[1:], np.stack(self.obs)[None]], 0)
+                nxt = np.concatenate([obs_buf[1:], np.stack(self.obs)[None]], 0)[:len(obs_buf)]
                 batch = dict(batch, next_obs=nxt)
             self._writer.write(batch)
         self.callbacks.on_sample_end(env_runner=self, samples=batch, metrics_logger=self.metrics)
@@ -380,6 +465,14 @@ class SingleAgentEnvRunner:
             for c in self._post:
                 b = c(rl_module=self.module, batch=b, episodes=self.episodes, explore=explore)
         return rec, b["obs"]
+
+    def _clip_reward(self, r):
+        c = self.clip_rewards
+        if c is None or c is False:
+            return r
+        if c is True:  # the reference: np.sign (Atari-style)
+            return float(np.sign(r))
+        return float(np.clip(r, -float(c), float(c)))
 
     def get_metrics(self):
         r, ln = self.done_returns, self.done_lengths

@@ -176,6 +176,9 @@ class SyntheticAtariEnv(Env):
         self.bank = bank_rng.integers(0, 256, size=(64, self.H, self.W, self.stack),
                                       dtype=np.uint8)
         self.rng = np.random.default_rng(seed)
+        # per-game reward magnitudes of the stand-ins (Breakout bricks score 1 / 4 / 7,
+        # Qbert 25, ...): clip_rewards=True is what maps them to {-1, 0, 1}
+        self.reward_values = [float(v) for v in cfg.get("reward_values", (1.0,))]
         self.t = 0
         self.i = 0
 
@@ -190,7 +193,10 @@ class SyntheticAtariEnv(Env):
         self.t += 1
         self.i = (self.i + 1 + int(action)) & 63
         r = self.rng.random()
-        reward = 1.0 if r < 0.01 else (-1.0 if r < 0.02 else 0.0)
+        reward = 0.0
+        if r < 0.02:
+            v = self.reward_values[int(self.rng.integers(len(self.reward_values)))]
+            reward = v if r < 0.01 else -v
         term = self.rng.random() < 1.0 / self.episode_len
         return self.bank[self.i], reward, bool(term), self.t >= 10 * self.episode_len, {}
 
@@ -253,5 +259,10 @@ register_env("RepeatAfterMeEnv", RepeatAfterMeEnv)
 register_env("CartPole-v0", lambda c: CartPoleEnv({"max_episode_steps": 200, **(c or {})}))
 register_env("Pendulum-v1", PendulumEnv)
 register_env("SyntheticAtari-v0", SyntheticAtariEnv)
-register_env("ALE/Pong-v5", SyntheticAtariEnv)  # shape-compatible stand-in (no ALE in image)
+# shape-compatible stand-ins for the ALE games of the tuned examples (no ALE in the image)
+register_env("ALE/Pong-v5", SyntheticAtariEnv)
+for _game, _rv in (("Breakout", (1.0, 4.0, 7.0)), ("BeamRider", (44.0,)), ("Qbert", (25.0,)),
+                   ("SpaceInvaders", (5.0, 10.0, 15.0, 30.0))):
+    register_env(f"ALE/{_game}-v5",
+                 lambda c, _rv=_rv: SyntheticAtariEnv({"reward_values": _rv, **(c or {})}))
 register_env("RandomEnv", RandomEnv)
