@@ -153,11 +153,47 @@ def from_batch(batch) -> Block:
 
 
 def _arrow_col_to_numpy(col):
+    """Arrow column -> numpy; a (fixed-size) list column of equal-length rows becomes an
+    N-d tensor column again (the form write_parquet stores tensor columns in)."""
+    import pyarrow as pa
+
+    t = col.type
+    if (pa.types.is_list(t) or pa.types.is_large_list(t) or pa.types.is_fixed_size_list(t)) \
+            and col.null_count == 0:
+        try:
+            c = col.combine_chunks() if hasattr(col, "combine_chunks") else col
+            flat = c.flatten()
+            n = len(c)
+            if n and len(flat) % n == 0:
+                offs = np.asarray(c.offsets) if hasattr(c, "offsets") else None
+                if offs is None or np.all(np.diff(offs) == len(flat) // n):
+                    inner = _arrow_col_to_numpy(flat)
+                    if inner.dtype != object:
+                        return inner.reshape((n, len(flat) // n) + inner.shape[1:])
+        except Exception:  # noqa: BLE001 - fall back to per-row conversion
+            pass
     try:
-        return col.to_numpy()
+        return _col(col.to_numpy(zero_copy_only=False)) if hasattr(col, "to_numpy") \
+            else _col(col.to_pylist())
     except Exception:
         v = col.to_pylist()
         return _col(v)
+
+
+def _np_to_arrow(v):
+    """numpy column -> arrow: an N-d numeric tensor column becomes nested fixed-size lists
+    (read back as the same tensor by _arrow_col_to_numpy)."""
+    import pyarrow as pa
+
+    if _is_tensor(v):
+        v = v.detach().cpu().numpy()
+    v = np.asarray(v)
+    if v.ndim <= 1 or v.dtype == object:
+        return pa.array(list(v)) if v.ndim > 1 else pa.array(v)
+    arr = pa.array(np.ascontiguousarray(v).reshape(-1))
+    for d in reversed(v.shape[1:]):
+        arr = pa.FixedSizeListArray.from_arrays(arr, int(d))
+    return arr
 
 
 def to_batch(b: Block, batch_format: str = "numpy"):
@@ -172,7 +208,7 @@ def to_batch(b: Block, batch_format: str = "numpy"):
 
         cols = {}
         for k, v in b.items():
-            cols[k] = pa.array(list(v)) if v.ndim > 1 or v.dtype == object else pa.array(v)
+            cols[k] = _np_to_arrow(v)
         return pa.table(cols)
     raise ValueError(f"unknown batch_format {batch_format}")
 

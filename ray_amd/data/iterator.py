@@ -279,20 +279,43 @@ class SplitCoordinator:
         self.carry_rows = 0
         self.done = False
         self.finished = [False] * self.n
+        self.served = [0] * self.n  # requests answered per consumer this epoch
 
-    def next_block(self, i, epoch):
+    def next_block(self, i, epoch, seq=None):
+        """Consumer ``i``'s ``seq``-th block of ``epoch`` (None: its share is exhausted).
+
+        The actor serves requests on several threads, so a consumer's prefetched requests
+        can arrive out of order: each is answered in ``seq`` order per consumer (request
+        k waits for k-1), or a later request could take the block an earlier one should
+        have returned while the earlier one reports the end of the epoch. A consumer that
+        starts epoch e+1 while others still read epoch e waits for them (the reference
+        coordinator's epoch barrier) instead of getting an empty epoch; waits are bounded
+        so a consumer that never comes back cannot wedge the others forever."""
         import threading
+        import time
 
-        if not hasattr(self, "_lock"):
-            self._lock = threading.Lock()
-        with self._lock:
-            return self._next_block(i, epoch)
+        if not hasattr(self, "_cond"):
+            self._cond = threading.Condition()
+        with self._cond:
+            deadline = time.monotonic() + 600.0
+            while True:
+                if epoch < self.epoch:  # a prefetch request left over from a finished epoch
+                    return None
+                if epoch > self.epoch and all(self.finished):
+                    self._start()
+                    continue
+                if epoch == self.epoch and (seq is None or seq == self.served[i]):
+                    break
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"streaming_split consumer {i} waited 600 s for "
+                                       f"epoch {epoch} (the coordinator is at {self.epoch})")
+                self._cond.wait(timeout=1.0)
+            r = self._next_block(i, epoch)
+            self.served[i] += 1
+            self._cond.notify_all()
+            return r
 
     def _next_block(self, i, epoch):
-        if epoch < self.epoch:  # a prefetch request left over from a finished epoch
-            return None
-        if epoch > self.epoch and all(self.finished):
-            self._start()
         while not self.queues[i]:
             if self.done:
                 self.finished[i] = True
@@ -349,15 +372,19 @@ class StreamSplitIterator(DataIterator):
     def _blocks(self):
         ep = self._epoch
         self._epoch += 1
-        window = collections.deque(self._coord.next_block.remote(self._index, ep)
-                                   for _ in range(self.PREFETCH_BLOCKS))
+        seq = 0
+        window = collections.deque()
+        for _ in range(self.PREFETCH_BLOCKS):
+            window.append(self._coord.next_block.remote(self._index, ep, seq))
+            seq += 1
         while window:
             r = ray.get(window.popleft())
             if r is None:
                 for x in window:  # the shard is exhausted: the rest answer None too
                     ray.get(x)
                 return
-            window.append(self._coord.next_block.remote(self._index, ep))
+            window.append(self._coord.next_block.remote(self._index, ep, seq))
+            seq += 1
             yield r[0]
 
     def iter_batches(self, *, batch_size=256, batch_format="default", drop_last=False,

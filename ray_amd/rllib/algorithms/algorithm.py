@@ -450,7 +450,64 @@ class Algorithm:
         timesteps: on the evaluation EnvRunners in parallel when
         ``evaluation_num_env_runners`` > 0, else on one local evaluation runner that is
         built once and reused (reference: algorithm.py:642,908)."""
-        return self._finish_eval(self._start_eval())
+        ope = getattr(self.config, "off_policy_estimation_methods", None)
+        ev = dict(getattr(self.config, "evaluation_config", None) or {})
+        if ope and (ev.get("input_") or ev.get("input")):
+            # offline evaluation (reference: evaluation_config={"input": ...}): the
+            # estimators run on the logged evaluation data, no env rollouts
+            return {"off_policy_estimator": self.off_policy_estimates()}
+        out = self._finish_eval(self._start_eval())
+        if ope:
+            out["off_policy_estimator"] = self.off_policy_estimates()
+        return out
+
+    def off_policy_estimates(self) -> dict:
+        """Off-policy estimates of the current policy (reference: algorithm_config.py:2040
+        off_policy_estimation_methods, rllib/offline/offline_evaluator.py): every
+        configured estimator ({name: {"type": ImportanceSampling | "wis" | ..., kwargs}})
+        on the logged data of ``evaluation_config["input_"]`` (else ``input_``), read
+        through ray_amd.data. DM / DR first fit their Q-model on the same rows."""
+        from ray_amd.rllib.offline import estimators as E
+        from ray_amd.rllib.offline.io import read_offline_dataset
+
+        methods = getattr(self.config, "off_policy_estimation_methods", None) or {}
+        ev = dict(getattr(self.config, "evaluation_config", None) or {})
+        inp = ev.get("input_") or ev.get("input") or self.config.input_
+        if not inp:
+            raise ValueError("off_policy_estimation_methods need logged data: "
+                             "evaluation_config={'input_': path} or offline_data(input_=...)")
+        if getattr(self, "_ope_batch", None) is None:
+            ds = read_offline_dataset(inp, read_method=getattr(self.config,
+                                                               "input_read_method", None))
+            cols = {}
+            for b in ds.iter_batches(batch_size=65536):
+                for k, v in b.items():
+                    cols.setdefault(k, []).append(np.asarray(v))
+            self._ope_batch = {k: np.concatenate(v) for k, v in cols.items()}
+        batch = self._ope_batch
+        names = {"is": E.ImportanceSampling, "importancesampling": E.ImportanceSampling,
+                 "wis": E.WeightedImportanceSampling,
+                 "weightedimportancesampling": E.WeightedImportanceSampling,
+                 "dm": E.DirectMethod, "directmethod": E.DirectMethod,
+                 "dr": E.DoublyRobust, "doublyrobust": E.DoublyRobust}
+        split = getattr(self.config, "ope_split_batch_by_episode", True)
+        policy = self.get_policy()
+        out = {}
+        for name, spec in methods.items():
+            spec = dict(spec or {})
+            cls = spec.pop("type", name)
+            if isinstance(cls, str):
+                key = cls.rsplit(".", 1)[-1].lower()
+                if key not in names:
+                    raise ValueError(f"unknown off-policy estimator {cls!r}")
+                cls = names[key]
+            est = cls(policy, gamma=self.config.gamma, **spec)
+            train_metrics = est.train(batch)
+            res = est.estimate(batch, split_batch_by_episode=split)
+            if train_metrics:
+                res.update({f"train_{k}": v for k, v in train_metrics.items()})
+            out[name] = res
+        return out
 
     def _start_eval(self):
         w = self._weights_for_runners()
@@ -512,6 +569,44 @@ class Algorithm:
     def _start_eval_local_fallback(self):
         self._eval_runners = []
         return self._start_eval()
+
+    # ---------------------------------------------------------------- offline data
+    def _setup_offline(self):
+        """Offline algorithms (BC, MARWIL, CQL): the recorded experience as a ray_amd.data
+        dataset (rllib/offline/offline_data.py)."""
+        from ray_amd.rllib.offline import OfflineData
+
+        cfg = self.config
+        if not cfg.input_:
+            raise ValueError(f"{type(self).__name__} is offline: set "
+                             "config.offline_data(input_=<recorded experience>)")
+        self.offline = OfflineData(cfg.input_, cfg.gamma, cfg.seed,
+                                   read_method=getattr(cfg, "input_read_method", None),
+                                   read_kwargs=getattr(cfg, "input_read_method_kwargs", None),
+                                   shuffle_buffer_size=getattr(cfg, "shuffle_buffer_size",
+                                                               None))
+        self._offline_fed = False
+
+    def _offline_updates(self, n_updates: int, batch_size: int, transform=None) -> dict:
+        """``n_updates`` learner updates on offline batches of ``batch_size`` rows in
+        total: one local learner samples the dataset's shuffled epoch stream; N learner
+        actors each pull batch_size / N rows per update from their streaming_split shard
+        (reference: offline_data.py sample(num_shards=N) -> update_from_iterator)."""
+        lg = self.learner_group
+        if getattr(lg, "remote", False):
+            n = len(lg.actors)
+            its = None
+            if not self._offline_fed:
+                its = self.offline.shards(n)
+                self._offline_fed = True
+            return lg.update_from_iterator(its, num_iters=n_updates,
+                                           minibatch_size=max(1, batch_size // n),
+                                           transform=transform, seed=self.config.seed)
+        stats = {}
+        for _ in range(int(n_updates)):
+            b = self.offline.sample(batch_size)
+            stats = lg.update_from_batch(transform(b) if transform else b)
+        return stats
 
     # ---------------------------------------------------------------- inference
     def _new_module(self, obs_space, act_space, module_id=None):
@@ -869,6 +964,35 @@ class _PolicyView(_Policy):
 
     def compute_actions(self, obs_batch, state_batches=None, explore=None, **kw):
         return self.algo.compute_actions(obs_batch, bool(explore), self.policy_id), [], {}
+
+    def compute_log_likelihoods(self, actions, obs_batch, **kw):
+        """log pi(a | s) of the module's current weights (reference: Policy.
+        compute_log_likelihoods): categorical for discrete actions, the diagonal Gaussian
+        (or SAC's squashed Gaussian) for Box actions, greedy one-hot for Q modules."""
+        import torch
+
+        m = self.algo.get_module(self.policy_id)
+        obs = np.asarray(obs_batch, np.float32)
+        f = getattr(self.algo, "_infer_filter", None)
+        x = torch.as_tensor(obs)
+        if f is not None:
+            x = f.normalize(x)
+        a = torch.as_tensor(np.asarray(actions))
+        kind = self.algo.cfg.get("module_kind", "actor_critic")
+        with torch.no_grad():
+            if kind == "q":
+                greedy = m(x.float()).argmax(-1)
+                return np.where(greedy.numpy() == a.numpy(), 0.0, -np.inf)
+            if kind == "sac":
+                return m.logp_of(x.float(), a.float()).double().numpy()
+            di = m.forward_inference(x)["action_dist_inputs"].float()
+            if hasattr(self.action_space, "n"):
+                return torch.log_softmax(di, -1).gather(-1, a.long()[:, None])[:, 0] \
+                    .double().numpy()
+            from ray_amd.rllib.core.rl_module.default import gaussian_logp
+
+            mean, log_std = di.chunk(2, -1)
+            return gaussian_logp(a.float(), mean, log_std).double().numpy()
 
     def get_weights(self):
         w = self.algo.get_weights()

@@ -95,6 +95,15 @@ class AlgorithmConfig:
         self.add_default_connectors_to_module_to_env_pipeline = True
         self.update_worker_filter_stats = True
         self.use_worker_filter_stats = True
+        # evaluation(): off-policy estimation on logged data (reference: :2040)
+        self.off_policy_estimation_methods = {}
+        self.ope_split_batch_by_episode = True
+        # offline_data() readers / writers (reference: :2379)
+        self.input_read_method = None
+        self.input_read_method_kwargs = None
+        self.output_write_method = "write_json"
+        self.output_max_rows_per_file = 100_000
+        self.shuffle_buffer_size = None
         # learners()
         self.num_cpus_per_learner = 1
         self.local_gpu_idx = 0

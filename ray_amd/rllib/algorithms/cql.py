@@ -16,7 +16,6 @@ import torch
 
 from ray_amd.rllib.algorithms.sac import SAC, SACConfig, SACLearner
 from ray_amd.rllib.core.learner import LearnerGroup
-from ray_amd.rllib.offline import OfflineData
 
 
 class CQLConfig(SACConfig):
@@ -81,6 +80,11 @@ class CQLLearner(SACLearner):
         return (alpha * logp - qmin).mean()
 
 
+def _float_terminateds(b):
+    b["terminateds"] = np.asarray(b["terminateds"]).astype(np.float32)
+    return b
+
+
 class CQL(SAC):
     supports_multi_agent = False  # offline: single-agent datasets only
     learner_class = CQLLearner
@@ -90,9 +94,7 @@ class CQL(SAC):
         return CQLConfig()
 
     def setup(self):
-        if not self.config.input_:
-            raise ValueError("CQL is offline: set config.offline_data(input_=<dir>)")
-        self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
+        self._setup_offline()
         self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space,
                                           learner_class=self.learner_class)
         self.prioritized = False
@@ -100,12 +102,9 @@ class CQL(SAC):
 
     def training_step(self):
         cfg = self.config
-        stats = {}
-        for _ in range(int(cfg.updates_per_iteration)):
-            b = self.offline.sample(cfg.train_batch_size)
-            b["terminateds"] = b["terminateds"].astype(np.float32)
-            stats = self.learner_group.update_from_batch(b)
-            stats = {k: v for k, v in stats.items() if not isinstance(v, np.ndarray)}
+        stats = self._offline_updates(int(cfg.updates_per_iteration),
+                                      int(cfg.train_batch_size), _float_terminateds)
+        stats = {k: v for k, v in stats.items() if not isinstance(v, np.ndarray)}
         self._sync_weights(self.learner_group.get_weights())
         if cfg.eval_steps_per_iteration:
             self.local_runner.sample(cfg.eval_steps_per_iteration, explore=False) \

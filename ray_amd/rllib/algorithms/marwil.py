@@ -1,8 +1,9 @@
 """MARWIL and BC (reference: rllib/algorithms/marwil/marwil.py,
 torch/marwil_torch_learner.py, rllib/algorithms/bc/bc.py; Wang et al. 2018).
 
-Offline: minibatches come from ``OfflineData`` (recorded EnvRunner fragments with
-discounted returns). Loss = -E[exp(beta * A / c) * log pi(a|s)] + vf_coeff * 0.5 *
+Offline: minibatches come from ``OfflineData`` (recorded experience read through
+ray_amd.data — fragment JSON or transition Parquet — with per-episode discounted
+returns; ``streaming_split`` shards when there are learner actors). Loss = -E[exp(beta * A / c) * log pi(a|s)] + vf_coeff * 0.5 *
 (V(s) - R)^2 with A = R - V(s) and c the running RMS of A (moving-average update
 rate ``moving_average_sqd_adv_norm_update_rate``). BC is MARWIL with beta = 0: the
 value head is not trained and the loss is plain negative log-likelihood.
@@ -18,7 +19,6 @@ from ray_amd.rllib.algorithms.algorithm import Algorithm
 from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
 from ray_amd.rllib.core.learner import LearnerGroup, TorchLearner
 from ray_amd.rllib.core.rl_module import RLModule
-from ray_amd.rllib.offline import OfflineData
 
 
 class MARWILConfig(AlgorithmConfig):
@@ -102,20 +102,15 @@ class MARWIL(Algorithm):
         return MARWILConfig()
 
     def setup(self):
-        if not self.config.input_:
-            raise ValueError(f"{type(self).__name__} is offline: set "
-                             "config.offline_data(input_=<recorded experience dir>)")
-        self.offline = OfflineData(self.config.input_, self.config.gamma, self.config.seed)
+        self._setup_offline()
         self.learner_group = LearnerGroup(self.cfg, self.observation_space, self.action_space,
                                           learner_class=MARWILLearner)
         self._sync_weights(self.learner_group.get_weights())
 
     def training_step(self):
         cfg = self.config
-        stats = {}
-        for _ in range(int(cfg.updates_per_iteration)):
-            stats = self.learner_group.update_from_batch(
-                self.offline.sample(cfg.train_batch_size))
+        stats = self._offline_updates(int(cfg.updates_per_iteration), int(cfg.train_batch_size))
+        stats = {k: v for k, v in stats.items() if not isinstance(v, np.ndarray)}
         self._sync_weights(self.learner_group.get_weights())
         if cfg.eval_steps_per_iteration:  # online metrics with the current policy
             runner = self.env_runners[0] if self.env_runners else self.local_runner

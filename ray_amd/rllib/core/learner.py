@@ -311,6 +311,27 @@ class TorchLearner:
         res.update(per_row)
         return res
 
+    def update_from_iterator(self, iterator=None, *, timesteps=None, minibatch_size=None,
+                             num_iters=None, transform=None, seed=None, **kwargs) -> dict:
+        """``num_iters`` updates on batches of ``minibatch_size`` rows pulled from a
+        ray_amd.data iterator (reference: learner.py update_from_iterator): this learner's
+        ``streaming_split`` shard of the offline dataset. The iterator is kept across calls
+        (epochs continue); ``transform`` maps each batch before the update."""
+        from ray_amd.rllib.offline.offline_data import iterate_forever
+
+        if iterator is not None and iterator is not getattr(self, "_data_it", None):
+            self._data_it = iterator
+            self._data_gen = iterate_forever(iterator, int(minibatch_size), seed)
+        if getattr(self, "_data_gen", None) is None:
+            raise ValueError("update_from_iterator needs an iterator on the first call")
+        res = {}
+        for _ in range(int(num_iters or 1)):
+            b = next(self._data_gen)
+            if transform is not None:
+                b = transform(b)
+            res = self.update_from_batch(b, timesteps=timesteps, **kwargs)
+        return res
+
     def update_from_episodes(self, episodes, *, timesteps=None, **kwargs) -> dict:
         """Train on a list of SingleAgentEpisodes (the learner connector step of the
         reference: ``episodes_to_batch`` flattens them into transition rows)."""
@@ -1539,6 +1560,30 @@ class LearnerGroup:
             return refs
         return _reduce_results(ray.get(refs))
 
+    def update_from_iterator(self, iterators=None, *, num_iters=1, minibatch_size=None,
+                             transform=None, seed=None, timesteps=None, **kwargs):
+        """Each learner actor trains ``num_iters`` updates on batches of ``minibatch_size``
+        rows pulled from its own data shard (``iterators``: one per learner, e.g.
+        ``Dataset.streaming_split(n, equal=True)``; passed once, kept by the learners).
+        Equal shards + a fixed update count keep the learners' gradient all-reduces in
+        step. Returns the rank-averaged metrics."""
+        if not self.remote:
+            it = iterators[0] if isinstance(iterators, (list, tuple)) else iterators
+            return self.local.update_from_iterator(
+                it, num_iters=num_iters, minibatch_size=minibatch_size, transform=transform,
+                seed=seed, timesteps=timesteps, **kwargs)
+        import ray_amd as ray
+
+        its = list(iterators) if iterators is not None else [None] * len(self.actors)
+        if len(its) != len(self.actors):
+            raise ValueError(f"{len(its)} iterators for {len(self.actors)} learners")
+        refs = [a.execute.remote(_learner_call_kw, "update_from_iterator", (it,), dict(
+                    kwargs, num_iters=num_iters, minibatch_size=minibatch_size,
+                    transform=transform, seed=None if seed is None else seed + i,
+                    timesteps=timesteps))
+                for i, (a, it) in enumerate(zip(self.actors, its))]
+        return _reduce_results(_get_fail_fast(refs))
+
     def foreach_learner(self, func, **kwargs) -> list:
         """``func(learner, **kwargs)`` on every learner (local or remote), results in rank
         order (reference: learner_group.py:613)."""
@@ -1728,6 +1773,18 @@ def _make_learner(config, obs_space, act_space, rank, world, module_id=DEFAULT_M
     cls = learner_class or _learner_cls(config)
     _LEARNER = cls(config, obs_space, act_space, rank=rank, world=world, module_id=module_id)
     return True
+
+
+def _get_fail_fast(refs):
+    """ray.get of every learner's result, raising the first learner error at once: the
+    other learners may be blocked in a collective that the failed one never joins."""
+    import ray_amd as ray
+
+    pending = list(refs)
+    while pending:
+        ready, pending = ray.wait(pending, num_returns=1)
+        ray.get(ready)  # raises the learner's error
+    return ray.get(list(refs))
 
 
 def _learner_call_kw(name, args, kwargs):

@@ -429,9 +429,14 @@ class SingleAgentEnvRunner:
             batch["next_obs"] = next_obs_buf
         if self.config.get("output"):
             if getattr(self, "_writer", None) is None:
-                from ray_amd.rllib.offline import JsonWriter
+                from ray_amd.rllib.offline import JsonWriter, ParquetWriter
 
-                self._writer = JsonWriter(self.config["output"], self.worker_index)
+                if self.config.get("output_write_method") == "write_parquet":
+                    self._writer = ParquetWriter(
+                        self.config["output"], self.worker_index,
+                        self.config.get("output_max_rows_per_file") or 100_000)
+                else:
+                    self._writer = JsonWriter(self.config["output"], self.worker_index)
             if next_obs_buf is None:  # next_obs from the rolled-forward observations
                 nxt = np.concatenate([obs_buf[1:], np.stack(self.obs)[None]], 0)[:len(obs_buf)]
                 batch = dict(batch, next_obs=nxt)
@@ -483,6 +488,12 @@ class SingleAgentEnvRunner:
     def set_epsilon(self, eps):
         self.epsilon = eps
 
+    def flush_output(self):
+        w = getattr(self, "_writer", None)
+        if w is not None and hasattr(w, "flush"):
+            w.flush()
+
     def stop(self):
+        self.flush_output()
         for e in self.envs:
             e.close()

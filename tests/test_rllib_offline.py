@@ -48,7 +48,7 @@ def _cartpole_expert(o, rng):
     return int(o[2] + 0.5 * o[3] > 0)
 
 
-def test_json_roundtrip(tmp_path):
+def test_json_roundtrip(cluster, tmp_path):
     _record("CartPole-v1", _cartpole_expert, tmp_path, n_frag=2, T=50)
     bs = list(JsonReader(str(tmp_path)))
     assert len(bs) == 2 and bs[0]["obs"].shape == (50, 2, 4) and bs[0]["actions"].dtype == np.int64
