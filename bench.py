@@ -307,9 +307,11 @@ def bench_allreduce(args):
         t = float(tt)
         nbytes = mib * (1 << 20)
         algbw = nbytes / t / 1e9
-        factor = 2.0 * (world - 1) / world if world > 1 else 1.0
+        # busbw = algbw x 2 (n-1) / n is a LINK figure: one rank has no link, so at N = 1 it
+        # is null (the all-reduce is a local no-op copy, not a bus transfer)
+        busbw = round(algbw * 2.0 * (world - 1) / world, 2) if world > 1 else None
         rows.append({"mib": mib, "ms": round(t * 1e3, 4), "algbw_gbps": round(algbw, 2),
-                     "busbw_gbps": round(algbw * factor, 2)})
+                     "busbw_gbps": busbw})
         mib *= 2
     if rank == 0:
         print(json.dumps({"metric": "allreduce_busbw_gbps", "value": rows[-1]["busbw_gbps"],

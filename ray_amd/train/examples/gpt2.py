@@ -84,6 +84,24 @@ def save_tunableop(dst: str):
     torch.cuda.tunable.tuning_enable(False)
 
 
+def _master_checksum(p32):
+    """Device-side checksum of the WHOLE fp32 master buffer: its sum and a position-weighted
+    sum (weights 1..9973 by index), in fp64, in 16M-element chunks, so ranks whose masters
+    differ anywhere (or are permuted) disagree."""
+    import torch
+
+    flat = p32.reshape(-1)
+    acc = torch.zeros(2, dtype=torch.float64, device=flat.device)
+    step = 1 << 24
+    for s in range(0, flat.numel(), step):
+        x = flat[s:s + step].double()
+        w = torch.arange(s, s + x.numel(), device=x.device, dtype=torch.float64) \
+            .remainder_(9973).add_(1.0)
+        acc[0] += x.sum()
+        acc[1] += (x * w).sum()
+    return acc
+
+
 def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
     """Build the model on ``device`` and run warmup + timed steps (shared by the Ray Train
     worker and the bare torchrun baseline). torch.distributed must already be set up
@@ -222,10 +240,10 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
         per_rank = [float(x) for x in allt]
         dt = max(per_rank)
         # ranks must hold identical weights after the run (same all-reduced grads)
-        chk = tr.flat.p32[: min(4096, tr.flat.numel)].double().sum().reshape(1)
+        chk = _master_checksum(tr.flat.p32)
         allc = [torch.zeros_like(chk) for _ in range(world)]
         dist.all_gather(allc, chk)
-        in_sync = all(float(x) == float(allc[0]) for x in allc)
+        in_sync = all(torch.equal(x, allc[0]) for x in allc)
     else:
         in_sync = True
     tokens = tr.tokens_per_step() * c["steps"]

@@ -65,6 +65,18 @@ def _init_pg(backend, master_addr, master_port, rank, world, local_rank, timeout
     return True
 
 
+def _destroy_pg():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            import torch
+
+            torch.cuda.synchronize()
+        dist.destroy_process_group()
+    return True
+
+
 class _TorchBackend(Backend):
     share_cuda_visible_devices = True
 
@@ -94,4 +106,13 @@ class _TorchBackend(Backend):
         ray.get(futs)
 
     def on_shutdown(self, worker_group, backend_config):
-        pass
+        """Destroy every rank's process group (reference: train/torch/config.py:201-204
+        _shutdown_torch / on_shutdown): RCCL communicators and their HIP resources are
+        released before the workers are reused or stopped."""
+        import ray_amd as ray
+
+        try:
+            ray.get([w.execute.remote(_destroy_pg) for w in worker_group.workers],
+                    timeout=backend_config.timeout_s)
+        except Exception:  # noqa: BLE001 - a dead worker has nothing left to destroy
+            pass
