@@ -1062,8 +1062,11 @@ class _Embedding(torch.autograd.Function):
             ids = ids if ids.dtype == torch.int64 and ids.is_contiguous() else \
                 ids.long().contiguous()
             d2c = d2.contiguous()
+            # V = the table's row count (the sink may be a flat 1-D view of V*C floats).
+            # Out-of-range ids never get here: F.embedding in the forward device-asserts on
+            # them, as torch's index_add_ would; the kernel's bound check is a guard only.
             check(_lib.lib().ra_embed_bwd(ptr(d2c), ptr(ids), ptr(sw), ptr(sp), B, T, C,
-                                          sw.shape[0], stream_ptr()), "embed_bwd")
+                                          wte.shape[0], stream_ptr()), "embed_bwd")
             _grad_done(wte)
             _grad_done(wpe)
             return None, None, None
