@@ -275,6 +275,14 @@ PYBIND11_MODULE(_core, m) {
       .def("capacity", &ShmStore::capacity, py::arg("device") = -1)
       .def("num_objects", &ShmStore::num_objects)
       .def("evictions", &ShmStore::evictions)
+      .def("spill_request", &ShmStore::spill_request)
+      .def("spill_take", &ShmStore::spill_take)
+      .def("spill_inflight_add", &ShmStore::spill_inflight_add)
+      .def("spill_inflight", &ShmStore::spill_inflight)
+      .def("set_spiller", &ShmStore::set_spiller)
+      .def("spiller_beat", &ShmStore::spiller_beat)
+      .def("live_spiller", &ShmStore::live_spiller, py::arg("max_age_ms") = 2000)
+      .def("spilled_total_add", &ShmStore::spilled_total_add)
       .def("release_all_pins_of", &ShmStore::release_all_pins_of)
       .def("abort", [](ShmStore& s, py::bytes id) { return s.abort(as_str(id)); })
       .def_property_readonly("size", &ShmStore::size);

@@ -7,6 +7,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <time.h>
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -558,6 +560,44 @@ bool ShmStore::abort(const std::string& id) {
   if (!e || e->state != kCreated) return false;
   free_entry(e);
   return true;
+}
+
+static int64_t mono_ms() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (int64_t)t.tv_sec * 1000 + t.tv_nsec / 1000000;
+}
+
+int64_t ShmStore::spill_request(int64_t bytes) {
+  return __atomic_add_fetch(&hdr_->spill_want, bytes, __ATOMIC_ACQ_REL);
+}
+
+int64_t ShmStore::spill_take() { return __atomic_exchange_n(&hdr_->spill_want, 0, __ATOMIC_ACQ_REL); }
+
+int64_t ShmStore::spill_inflight_add(int64_t d) {
+  return __atomic_add_fetch(&hdr_->spills_inflight, d, __ATOMIC_ACQ_REL);
+}
+
+int64_t ShmStore::spill_inflight() const {
+  return __atomic_load_n(&hdr_->spills_inflight, __ATOMIC_ACQUIRE);
+}
+
+void ShmStore::set_spiller(int64_t pid) {
+  __atomic_store_n(&hdr_->spiller_beat_ms, mono_ms(), __ATOMIC_RELEASE);
+  __atomic_store_n(&hdr_->spiller_pid, pid, __ATOMIC_RELEASE);
+}
+
+void ShmStore::spiller_beat() { __atomic_store_n(&hdr_->spiller_beat_ms, mono_ms(), __ATOMIC_RELEASE); }
+
+int64_t ShmStore::live_spiller(int64_t max_age_ms) const {
+  const int64_t pid = __atomic_load_n(&hdr_->spiller_pid, __ATOMIC_ACQUIRE);
+  if (pid <= 0) return 0;
+  const int64_t beat = __atomic_load_n(&hdr_->spiller_beat_ms, __ATOMIC_ACQUIRE);
+  return mono_ms() - beat <= max_age_ms ? pid : 0;
+}
+
+uint64_t ShmStore::spilled_total_add(uint64_t n) {
+  return __atomic_add_fetch(&hdr_->spilled_total, n, __ATOMIC_ACQ_REL);
 }
 
 }  // namespace ray_amd

@@ -83,6 +83,14 @@ struct SegHeader {
   uint64_t stats_evictions, stats_creates;
   pthread_mutex_t mu;
   HeapHdr heaps[1 + kMaxDevices];  // [0] host, [1+d] device d
+  // Spill coordination (lock-free, every process of the node): puts that found the heap
+  // full post the bytes they need; the node's spill thread (pid + heartbeat) takes them,
+  // and counts the fused spill files it is writing, which puts wait on.
+  int64_t spill_want;      // bytes requested by blocked puts, not yet taken
+  int64_t spills_inflight; // fused spill writes in progress
+  int64_t spiller_pid;     // the spill thread's process (0: none)
+  int64_t spiller_beat_ms; // its last heartbeat (CLOCK_MONOTONIC ms)
+  uint64_t spilled_total;  // bytes spilled since creation
 };
 
 struct ObjInfo {
@@ -133,6 +141,16 @@ class ShmStore {
   uint64_t capacity(int device);
   uint64_t num_objects();
   uint64_t evictions();
+  // spill coordination (see SegHeader)
+  int64_t spill_request(int64_t bytes);
+  int64_t spill_take();
+  int64_t spill_inflight_add(int64_t d);
+  int64_t spill_inflight() const;
+  void set_spiller(int64_t pid);
+  void spiller_beat();
+  // the spill thread's pid if it beat within max_age_ms, else 0
+  int64_t live_spiller(int64_t max_age_ms) const;
+  uint64_t spilled_total_add(uint64_t n);
   // Drops every pin `pid` holds and aborts the objects it created but never sealed;
   // returns how many entries changed. Called by the raylet when a worker dies.
   uint64_t release_all_pins_of(int pid);

@@ -52,6 +52,9 @@ class NodeAgent:
         self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
                                     table_capacity(args.object_store_memory))
         start_prefault(self.store, args.object_store_memory)
+        from ray_amd._private.object_store import SpillManager
+
+        self.spiller = SpillManager(self.store, self.spill_dir).start()
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.total, self.num_cpus = node_resources(args, self.node_ip, head=False)
@@ -191,5 +194,6 @@ class NodeAgent:
                 p.wait(timeout=2)
             except Exception:
                 pass
+        self.spiller.stop()
         shm_segment.release(self.store_path, self._store_fd)
         self.io.stop()

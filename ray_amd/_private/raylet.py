@@ -247,6 +247,9 @@ class Raylet:
         self.store = _core.ShmStore(self.store_path, args.object_store_memory, True,
                                     table_capacity(args.object_store_memory))
         start_prefault(self.store, args.object_store_memory)
+        from .object_store import SpillManager
+
+        self.spiller = SpillManager(self.store, self.spill_dir).start()
         self.io = _core.IOLoop()
         self.io.listen_unix(self.addr)
         self.sched = _core.Scheduler()
@@ -1688,6 +1691,7 @@ class Raylet:
                 p.kill()
             except Exception:
                 pass
+        self.spiller.stop()
         shm_segment.release(self.store_path, self._store_fd)
         self.io.stop()
 
@@ -1702,12 +1706,24 @@ def read_object_bytes(store, spill_dir, oid):
         finally:
             mv.release()
             b.release()
-    p = os.path.join(spill_dir, oid.hex())
+    p, off, size = _spill_range(store, spill_dir, oid)
     try:
         with open(p, "rb") as f:
-            return f.read()
+            f.seek(off)
+            return f.read(size) if size is not None else f.read()
     except OSError:
         return None
+
+
+def _spill_range(store, spill_dir, oid):
+    """(file, offset, size) of a spilled object: its fused-file range (stub), else the
+    per-object fallback file (size None = whole file)."""
+    from .object_store import spilled_location
+
+    loc = spilled_location(store, spill_dir, oid)
+    if loc is not None:
+        return loc
+    return os.path.join(spill_dir, oid.hex()), 0, None
 
 
 def read_object_chunk(store, spill_dir, oid, off, n):
@@ -1721,18 +1737,21 @@ def read_object_chunk(store, spill_dir, oid, off, n):
         finally:
             mv.release()
             b.release()
-    p = os.path.join(spill_dir, oid.hex())
+    p, base, size = _spill_range(store, spill_dir, oid)
     try:
         with open(p, "rb") as f:
-            total = os.fstat(f.fileno()).st_size
-            f.seek(off)
+            total = os.fstat(f.fileno()).st_size if size is None else size
+            f.seek(base + off)
             return total, f.read(max(0, min(n, total - off)))
     except OSError:
         return None
 
 
 def free_object(store, spill_dir, oid):
+    from .object_store import stub_id
+
     store.remove(oid)
+    store.remove(stub_id(oid))  # a spilled object's stub (its fused file is GC'd)
     try:
         os.unlink(os.path.join(spill_dir, oid.hex()))
     except OSError:

@@ -107,12 +107,21 @@ def test_store_evicts_lru_unpinned_and_spills_primary(tmp_path):
         os_.put_bytes(_oid(i), blob, pinned=True)
     assert os_.stats()["spilled_bytes"] > 0
     spilled = [i for i in range(10, 28) if not os_.store.contains(_oid(i)) and
-               os.path.exists(os.path.join(spill, _oid(i).hex()))]
+               os_.contains(_oid(i))]
     assert spilled
+    # fused spill files (several objects per file), no per-object files
+    fused = [n for n in os.listdir(spill) if n.endswith(".bin")]
+    assert fused and len(fused) < len(spilled)
+    assert not any(os.path.exists(os.path.join(spill, _oid(i).hex())) for i in spilled)
     mv = os_.get_buffer(_oid(spilled[0]))
     assert bytes(mv[:64]) == blob[:64] and len(mv) == len(blob)
-    os_.delete(_oid(spilled[0]))
-    assert not os.path.exists(os.path.join(spill, _oid(spilled[0]).hex()))
+    del mv
+    for i in spilled:
+        os_.delete(_oid(i))
+    from ray_amd._private.object_store import gc_fused_files
+
+    assert gc_fused_files(os_.store, spill) == len(fused)
+    assert not [n for n in os.listdir(spill) if n.startswith("fused-")]
 
 
 def test_spilled_objects_roundtrip_through_runtime(tmp_path):
@@ -193,13 +202,12 @@ def test_put_waits_for_space_instead_of_failing(tmp_path, monkeypatch):
     blob = bytes(30 << 20)
     st.put_bytes(_oid(1), blob, pinned=True)
     reader = st.get_buffer(_oid(1))  # pins the only candidate: not spillable now
-    # an in-flight spill of another process: its temp file exists for 2.5 s
-    marker = os.path.join(spill, "ff" * 20 + ".tmp999")
-    open(marker, "wb").close()
+    # an in-flight fused spill of another process (the segment's shared counter) for 2.5 s
+    st.store.spill_inflight_add(1)
 
     def release():
         time.sleep(2.5)
-        os.unlink(marker)
+        st.store.spill_inflight_add(-1)
         reader.release()  # the pin goes: the object becomes spillable
 
     th = threading.Thread(target=release)
@@ -211,4 +219,57 @@ def test_put_waits_for_space_instead_of_failing(tmp_path, monkeypatch):
     assert waited >= 2.0  # kept waiting while the spill was in flight (grace was 1 s)
     assert st.store.contains(_oid(2))  # allocated in the store, not the fallback
     assert st.stats()["fallback_objects"] == 0 and st.stats()["waited_allocs"] == 1
-    assert os.path.exists(os.path.join(spill, _oid(1).hex()))  # the old one was spilled
+    assert not st.store.contains(_oid(1)) and st.contains(_oid(1))  # the old one spilled
+
+
+def test_put_completes_while_the_node_spill_thread_writes_fused_files(monkeypatch):
+    """Spilling runs on the raylet's spill thread (reference: local_object_manager.cc
+    SpillObjectUptoMaxThroughput, external_storage.py fused files), not in the put path:
+    a put that fits completes while another process's ~500 MiB spill is in flight, and the
+    spill directory holds fused multi-object files."""
+    import threading
+
+    from ray_amd._private import worker as W
+
+    monkeypatch.setenv("RAY_AMD_SPILL_HIGH_WATER", "0.25")  # raylet spills down to 25 %
+    ray.init(num_cpus=1, object_store_memory=1 << 30)
+    try:
+        cw = W.global_worker.core
+        st = cw.store
+        refs = [ray.put(np.full(100 << 20, i, np.uint8)) for i in range(6)]  # 600 MiB
+        seen = {"inflight_puts": 0, "max_inflight": 0}
+        stop = threading.Event()
+
+        def watch():
+            while not stop.is_set():
+                seen["max_inflight"] = max(seen["max_inflight"], st.store.spill_inflight())
+                time.sleep(0.0005)
+
+        th = threading.Thread(target=watch)
+        th.start()
+        small = []
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            before = st.store.spill_inflight()
+            t0 = time.perf_counter()
+            small.append(ray.put(np.ones(1 << 20, np.uint8)))
+            dt = time.perf_counter() - t0
+            if before > 0 and st.store.spill_inflight() > 0 and dt < 0.5:
+                seen["inflight_puts"] += 1
+            if seen["inflight_puts"] >= 3 or (st.stats()["spilled_bytes"] >= 300 << 20
+                                               and st.store.spill_inflight() == 0):
+                break
+        stop.set()
+        th.join()
+        assert seen["max_inflight"] >= 1
+        assert seen["inflight_puts"] >= 1  # puts went through while the spill was running
+        assert st.stats()["spilled_bytes"] >= 200 << 20
+        fused = [n for n in os.listdir(st.spill_dir) if n.endswith(".bin")]
+        assert fused
+        idx = [open(os.path.join(st.spill_dir, n + ".idx")).read().split() for n in fused]
+        assert max(len(x) for x in idx) >= 2  # several objects per file
+        for i, r in enumerate(refs):  # spilled or not, every object reads back
+            v = ray.get(r)
+            assert v[0] == i and v[-1] == i and v.shape == (100 << 20,)
+    finally:
+        ray.shutdown()
