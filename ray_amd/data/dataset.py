@@ -8,6 +8,8 @@ task graphs over the materialised upstream blocks.
 
 from __future__ import annotations
 
+import copy
+
 import builtins
 import collections
 import itertools
@@ -449,6 +451,70 @@ class Dataset:
     def __init__(self, plan: X.Plan):
         self._plan = plan
         self._name = None
+        from . import DataContext
+
+        self._context = copy.deepcopy(DataContext.get_current())
+
+    # ------------------------------------------------------------- identity / lineage
+    # reference: python/ray/data/dataset.py:231 copy, :4634 has_serializable_lineage,
+    # :4654 serialize_lineage, :4745 deserialize_lineage, :4786 context
+    @property
+    def context(self):
+        """The DataContext this Dataset was created under (a snapshot)."""
+        return self._context
+
+    @staticmethod
+    def copy(ds: "Dataset", _deep_copy: bool = False, _as=None) -> "Dataset":
+        """A new Dataset over the same plan (deep: the stage list and source copied too,
+        the materialised cache dropped)."""
+        cls = _as or type(ds)
+        if _deep_copy:
+            p = X.Plan(copy.copy(ds._plan.source), [copy.copy(st) for st in ds._plan.stages],
+                       ds._plan.source_meta)
+        else:
+            p = X.Plan(ds._plan.source, list(ds._plan.stages), ds._plan.source_meta)
+            p._cache = ds._plan._cache
+        out = cls.__new__(cls)
+        out.__dict__.update(ds.__dict__)
+        out._plan = p
+        return out
+
+    def has_serializable_lineage(self) -> bool:
+        """True when the dataset can be rebuilt from its lineage alone: it starts from read
+        tasks (files / datasources that exist outside this cluster), not from object refs
+        or in-process streams (from_items / from_numpy / union / zip / shuffle outputs)."""
+        return self._plan.source[0] == "read"
+
+    def serialize_lineage(self) -> bytes:
+        """The read tasks and transformations (not the data, not any computed block) as
+        bytes; ``Dataset.deserialize_lineage`` rebuilds the dataset, possibly on another
+        cluster, and everything is recomputed from the source."""
+        if not self.has_serializable_lineage():
+            raise ValueError("Lineage-based serialization is only supported for datasets "
+                             "created by read_*() APIs (no from_* inputs, unions, zips or "
+                             "all-to-all outputs)")
+        import cloudpickle
+
+        p = self._plan
+        return cloudpickle.dumps({"source": p.source, "stages": p.stages,
+                                  "source_meta": p.source_meta, "name": self._name,
+                                  "context": self._context,
+                                  "input_files": getattr(self, "_input_files", None)})
+
+    @staticmethod
+    def deserialize_lineage(serialized_ds: bytes) -> "Dataset":
+        """Rebuild a dataset from ``serialize_lineage`` bytes (trusted input: they hold
+        the pickled read and transformation functions)."""
+        import cloudpickle
+
+        d = cloudpickle.loads(serialized_ds)
+        ds = Dataset(X.Plan(d["source"], d["stages"], d["source_meta"]))
+        ds._name = d.get("name")
+        if d.get("context") is not None:
+            ds._context = d["context"]
+        if d.get("input_files"):
+            ds._input_files = d["input_files"]
+        return ds
 
     # ------------------------------------------------------------- transformations
     def _with(self, stage: X.Stage) -> "Dataset":

@@ -144,6 +144,8 @@ class Algorithm:
         self.config = config
         self.cfg = config.to_dict()
         self.cfg["module_kind"] = getattr(self, "module_kind", "actor_critic")
+        if type(self).validate_env is not Algorithm.validate_env:  # overridden: runners call it
+            self.cfg["_validate_env"] = type(self).validate_env
         probe = make_env(config.env, config.env_config)
         self.observation_space = probe.observation_space
         self.action_space = probe.action_space
@@ -885,7 +887,40 @@ class Algorithm:
 
     def get_state(self):
         return {"learner": self.learner_group.get_state(), "iteration": self.iteration,
-                "total_env_steps": self.total_env_steps, "config": self.cfg}
+                "total_env_steps": self.total_env_steps, "config": self.cfg,
+                "algorithm_class": type(self)}
+
+    @classmethod
+    def from_state(cls, state: dict) -> "Algorithm":
+        """A new Algorithm from a ``get_state()`` dict (reference: algorithm.py:353): the
+        class recorded in the state (or ``cls``), its config rebuilt from the state's
+        config, then the learner / counters state loaded."""
+        algo_cls = state.get("algorithm_class") or cls
+        if not isinstance(algo_cls, type) or not issubclass(algo_cls, Algorithm):
+            raise ValueError(f"state names no Algorithm class ({algo_cls!r})")
+        from ray_amd.rllib.algorithms.registry import get_config_class
+
+        cfg_state = {k: v for k, v in dict(state["config"]).items()
+                     if not k.startswith("_") and k not in ("module_kind",)}
+        config = get_config_class(algo_cls)().update_from_dict(cfg_state)
+        algo = algo_cls(config)
+        algo.set_state(state)
+        return algo
+
+    def restore_workers(self, workers=None):
+        """Old-stack name (reference: algorithm.py:1429): probe the given (default: all)
+        EnvRunners, recreate the dead ones and push the current weights to them."""
+        restored = self.restore_env_runners()
+        if restored:
+            self._sync_weights(self.get_weights())
+        return restored
+
+    @staticmethod
+    def validate_env(env, env_context) -> None:
+        """Hook to validate a freshly created env (reference: algorithm.py:2680; the
+        default accepts every env). Subclasses override it to reject envs they cannot
+        train on; it runs on every env an EnvRunner of this algorithm creates."""
+        return None
 
     def set_state(self, s):
         self.learner_group.set_state(s["learner"])

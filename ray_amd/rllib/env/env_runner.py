@@ -39,6 +39,8 @@ class SingleAgentEnvRunner:
             ec = dict(config.get("env_config") or {})
             ec.setdefault("seed", (seed or 0) * 1000 + worker_index * 100 + i)
             e = make_env(config["env"], ec)
+            if config.get("_validate_env") is not None:  # Algorithm.validate_env
+                config["_validate_env"](e, ec)
             if isinstance(e, VectorEnv):  # its sub-environments join the lock-step batch
                 subs = e.get_sub_environments()
                 if not subs:

@@ -74,3 +74,43 @@ def test_sac_get_module_and_action_bounds():
     assert np.asarray(a).shape == (1,) and -2.0 <= float(np.asarray(a)[0]) <= 2.0
     assert algo.get_module() is not None
     algo.stop()
+
+
+def test_from_state_restore_workers_and_validate_env():
+    """reference: algorithm.py:353 from_state, :1429 restore_workers, :2680 validate_env."""
+    import ray_amd as ray
+    from ray_amd.rllib.algorithms.ppo import PPO, PPOConfig
+
+    ray.init(num_cpus=3, ignore_reinit_error=True)
+    try:
+        cfg = (PPOConfig().environment("CartPole-v1").env_runners(num_env_runners=1)
+               .learners(num_gpus_per_learner=0)
+               .training(train_batch_size=200, minibatch_size=64, num_epochs=1,
+                         model={"fcnet_hiddens": [16]}))
+        algo = cfg.build()
+        try:
+            algo.train()
+            st = algo.get_state()
+            w = algo.get_weights()
+            assert not algo.restore_workers()  # all healthy: nothing to restore
+        finally:
+            algo.stop()
+        algo2 = PPO.from_state(st)
+        try:
+            assert type(algo2) is PPO and algo2.iteration == 1
+            w2 = algo2.get_weights()
+            for k in w:
+                np.testing.assert_array_equal(np.asarray(w[k]), np.asarray(w2[k]))
+        finally:
+            algo2.stop()
+
+        class Picky(PPO):
+            @staticmethod
+            def validate_env(env, env_context):
+                if env.observation_space.shape != (3,):
+                    raise ValueError("Picky trains on 3-d observations only")
+
+        with pytest.raises(Exception, match="3-d observations"):
+            Picky(cfg.copy().env_runners(num_env_runners=0))
+    finally:
+        ray.shutdown()
