@@ -26,7 +26,6 @@ BUILD_DIR = os.path.join(HERE, "build")
 HIP_LIB = os.path.join(HERE, "libray_amd_hip.so")
 ARCH = os.environ.get("RAY_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-AGPR_ACC_SOURCES = {"gemm4w.hip"}
 NO_SLP_SOURCES = {"attn.hip", "layernorm.hip", "gelu.hip"}
 
 
@@ -59,9 +58,7 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         s, o = so
         # VGPR-form MFMA: accumulators live in arch VGPRs, so the softmax / epilogue VALU
         # work on them needs no v_accvgpr_read/write round trips (gfx950 unified RF)
-        # ...except the 4-wave GEMM, whose 256 accumulators per lane must sit in AGPRs
-        vgpr_form = [] if os.path.basename(s) in AGPR_ACC_SOURCES else \
-            ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+        vgpr_form = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
         # attention: no SLP vectorisation — it pairs the softmax / dS multiplies into
         # v_pk_mul_f32 whose even-aligned operand pairs cost v_mov / v_alignbit / v_perm
         # shuffles of the MFMA accumulators (and packed f32 VALU is slower beside MFMAs:

@@ -103,15 +103,13 @@ class Block(nn.Module):
         """Attention sub-block on the normalised input; returns the projection output
         WITHOUT its bias (added by the fused residual+LayerNorm seam)."""
         B, T, C = h.shape
-        # wg_hint: weight-gradient placement under RAY_AMD_WGRAD_DEFER=1 (ops/functional.py):
-        # c_fc's and c_attn's wgrads wait for the next c_proj backward (attention backward)
-        qkv = rf.linear(h, self.c_attn_w, self.c_attn_b, wg_hint="defer")  # + bias epilogue
+        qkv = rf.linear(h, self.c_attn_w, self.c_attn_b)  # + bias epilogue
         # HIP MFMA flash attention straight off the packed QKV layout (no permutes/copies)
         y = rf.causal_attention_qkv(qkv.view(B, T, 3, self.n_head, C // self.n_head))
-        return rf.linear(y.reshape(B, T, C), self.c_proj_w, wg_hint="flush")
+        return rf.linear(y.reshape(B, T, C), self.c_proj_w)
 
     def mlp(self, h):
-        a = rf.bias_gelu(rf.linear(h, self.c_fc_w, wg_hint="defer"), self.c_fc_b)
+        a = rf.bias_gelu(rf.linear(h, self.c_fc_w), self.c_fc_b)
         return rf.linear(a, self.mlp_proj_w)
 
     def forward(self, x):

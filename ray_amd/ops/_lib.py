@@ -43,10 +43,6 @@ _SIGS = {
     "ra_wgrad": [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p,
                  c_void_p, c_int, c_void_p],
     "ra_wgrad_splits": [c_int, c_int, c_int],
-    "ra_wgrad_group": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                       c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
-    "ra_wgrad_group_ws_bytes": [c_int, c_int],
-    "ra_wgrad_group_splits": [c_int, c_int],
     "ra_bias_residual": [c_void_p] * 4 + [c_long, c_int, c_void_p],
     "ra_xent_fwd": [c_void_p] * 4 + [c_int, c_int, c_int, c_long, c_void_p],
     "ra_xent_bwd": [c_void_p] * 4 + [c_float, c_void_p, c_int, c_int, c_int, c_long, c_void_p],
@@ -61,7 +57,6 @@ _SIGS = {
     "ra_wt_max_segments": [],
     "ra_adamw_flat_dev": [c_void_p] * 5 + [c_long, c_long] + [c_float] * 5 +
     [c_int, c_void_p, c_int, c_void_p, c_void_p],
-    "ra_set_knob": [c_int, c_int],
     "ra_scaled_accum": [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p],
     "ra_scale_bf16": [c_void_p, c_long, c_void_p, c_void_p],
     "ra_xent_fused": [c_void_p] * 4 + [c_int, c_int, c_int, c_long, c_void_p],
@@ -125,16 +120,9 @@ _SIGS = {
     "ra_attn_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                     c_void_p],
     "ra_attn_bwd": [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
-    "ra_attn_bwd_pre": [c_void_p] * 3 + [c_int] * 3 + [c_void_p],
-    "ra_attn_bwd_kv": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
-    "ra_attn_bwd_q": [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p],
-    "ra_attn_bwd_fused": [c_void_p] * 7 + [c_int, c_int, c_int, c_int, c_float, c_void_p],
     "ra_gemm_nt": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
                    c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int, c_int,
                    c_void_p],
-    "ra_gemm4w_nt": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
-                     c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int,
-                     c_int, c_void_p],
     "ra_gemm_dgelu_work": [c_int, c_int],
     "ra_arena_alloc": [c_int, c_size_t, ctypes.POINTER(c_void_p), c_void_p],
     "ra_ipc_handle_size": [],
@@ -149,7 +137,6 @@ _SIGS = {
 }
 
 
-_LONG_RET = {"ra_wgrad_group_ws_bytes"}
 
 
 class HipKernelError(RuntimeError):
@@ -180,11 +167,7 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = c_long if name.endswith("_work") or name in _LONG_RET else c_int
-        # RAY_AMD_KNOBS="11=0,12=1": kernel variant knobs (A/B runs without code edits)
-        for kv in filter(None, os.environ.get("RAY_AMD_KNOBS", "").split(",")):
-            k, v = kv.split("=")
-            L.ra_set_knob(int(k), int(v))
+            f.restype = c_long if name.endswith("_work") else c_int
         _lib = L
     return _lib
 

@@ -150,16 +150,6 @@ __global__ __launch_bounds__(256) void colsum_atomic(const float* __restrict__ p
 
 }  // namespace
 
-// Runtime tuning knobs (A/B without rebuilding; set through ra_set_knob, defined in
-// layernorm.hip, or RAY_AMD_KNOBS="k=v,..."): 0 = LayerNorm-bwd partial rows cap, 1 =
-// column-partial waves target, 2 = fp32 colsum via atomics (1) or two-stage (0), 3 = v1
-// LayerNorm / column-partial kernels (1), 4 = LayerNorm-bwd v2 blocks, 5 = gemm.hip
-// schedule, 6 = fused attention-bwd diagnostics, 7 = conv partial target, 11 = attention
-// dK/dV variant (2 = ILP default, 1 = PF 1, 0 = PF 2, 3 = row constants in registers), 12 =
-// attention dQ variant, 13 = attention delta pre-pass (1) instead of inside dQ, 14 =
-// LayerNorm-bwd partial slabs (1) instead of in-kernel atomics into fp32 sinks.
-extern int ra_knobs[16];
-
 namespace {
 
 // flags: bit0 = bf16 output, bit1 = accumulate into out. scratch: kColsumSplits * D floats.
@@ -169,7 +159,7 @@ static inline void colsum_launch(const float* part, float* scratch, void* out, i
   int S = (P + 15) / 16;
   if (S > kColsumSplits) S = kColsumSplits;
   if (S < 1) S = 1;
-  if (!(flags & kColsumBF16) && ra_knobs[2]) {
+  if (!(flags & kColsumBF16)) {  // fp32 out: atomics, one pass
     if (!(flags & kColsumAcc)) (void)hipMemsetAsync(out, 0, (size_t)D * sizeof(float), st);
     hipLaunchKernelGGL(colsum_atomic, dim3((D + 63) / 64, S), dim3(256), 0, st, part,
                        (float*)out, P, D);
@@ -177,12 +167,10 @@ static inline void colsum_launch(const float* part, float* scratch, void* out, i
   }
   hipLaunchKernelGGL(colsum_stage1, dim3((D + 63) / 64, S), dim3(256), 0, st, part, scratch, P, D);
   const dim3 g((D + 255) / 256), b(256);
-  switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((colsum_stage2<false, false>), g, b, 0, st, scratch, out, S, D); break;
-    case 1: hipLaunchKernelGGL((colsum_stage2<true, false>), g, b, 0, st, scratch, out, S, D); break;
-    case 2: hipLaunchKernelGGL((colsum_stage2<false, true>), g, b, 0, st, scratch, out, S, D); break;
-    default: hipLaunchKernelGGL((colsum_stage2<true, true>), g, b, 0, st, scratch, out, S, D);
-  }
+  if (flags & kColsumAcc)
+    hipLaunchKernelGGL((colsum_stage2<true, true>), g, b, 0, st, scratch, out, S, D);
+  else
+    hipLaunchKernelGGL((colsum_stage2<true, false>), g, b, 0, st, scratch, out, S, D);
 }
 
 }  // namespace

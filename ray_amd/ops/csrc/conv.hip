@@ -414,7 +414,7 @@ static int launch_wgrad(const ConvArgs& a, int P, hipStream_t st) {
 static int wgrad_rows(int M, int K, int NOUT) {
   (void)K;
   (void)NOUT;
-  int want = ra_knobs[7] > 0 ? ra_knobs[7] : 512;
+  int want = 512;
   if (want > kMaxWgRows) want = kMaxWgRows;
   int r = (want + 63) / 64 * 64;
   return M < r ? (M + 63) / 64 * 64 : r;

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64) void bwd_colpart_kernel(const bf16_t* __restric
   *reinterpret_cast<float4*>(pr + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
-// v2 of the above, used by default (ra_knobs[3] != 1): the chunk [r0, r1) is addressed
+// v2 of the above, used whenever the chunk fits 32-bit offsets: the chunk [r0, r1) is addressed
 // through buffer resources that END at r1, so rows past the chunk load zeros and their
 // stores are dropped -- the loop has no guards and no break. v1's guarded batch made the
 // compiler sink every load to its use: one full memory round trip per row per wave.
@@ -299,13 +299,12 @@ __global__ __launch_bounds__(256) void bias_residual_kernel(const bf16_t* __rest
   }
 }
 
-// Row partitions of a column reduction: enough (64-thread) blocks to put ~ra_knobs[1]
+// Row partitions of a column reduction: enough (64-thread) blocks to put ~8192
 // waves on the chip (8192 = 32 per CU) whatever F is (F = 768 gives only 2 column
 // blocks), >= 32 rows per partial.
 static inline int parts_for(int N, int F) {
   const int bx = (F / 8 + 63) / 64;
-  const int waves = ra_knobs[1] > 0 ? ra_knobs[1] : 8192;
-  int p = (waves + bx - 1) / bx;
+  int p = (8192 + bx - 1) / bx;
   if (p < 256) p = 256;
   const int pmax = (N + 31) / 32;
   return p < pmax ? p : (pmax > 0 ? pmax : 1);
@@ -342,7 +341,7 @@ RA_EXPORT int ra_bias_gelu_bwd(const void* dy, const void* h, const void* bias, 
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  if (ra_knobs[3] != 1 && (long)rpp * F8 * 16 < (1L << 31))
+  if ((long)rpp * F8 * 16 < (1L << 31))
     hipLaunchKernelGGL((bwd_colpart2_kernel<true, 1>), dim3((F8 + 63) / 64, P), dim3(64), 0, st,
                        (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dh,
                        work, N, F8, rpp);
@@ -359,7 +358,7 @@ RA_EXPORT int ra_colsum_bf16(const void* x, void* out, float* work, int N, int F
   if (F % 8) return hipErrorInvalidValue;
   const int P = parts_for(N, F), F8 = F / 8;
   const int rpp = (N + P - 1) / P;
-  if (ra_knobs[3] != 1 && (long)rpp * F8 * 16 < (1L << 31))
+  if ((long)rpp * F8 * 16 < (1L << 31))
     hipLaunchKernelGGL((bwd_colpart2_kernel<false, 1>), dim3((F8 + 63) / 64, P), dim3(64), 0,
                        st, (const bf16_t*)x, nullptr, nullptr, nullptr, work, N, F8, rpp);
   else

@@ -63,11 +63,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // restored. Through __builtin_amdgcn_global_load_lds hipcc cannot tell the DMA's LDS write
 // from the fragment reads of the other stage buffer and puts s_waitcnt vmcnt(0) in front of
 // them, draining the prefetch every K-step (the same fix as ops/csrc/wgrad.hip glds16_w).
-// RAY_AMD_GEMM_GLDS_BUILTIN (compile-time define) keeps the builtin for A/B runs.
 __device__ __forceinline__ void glds16(const bf16_t* gsrc, bf16_t* ldst) {
-#ifdef RAY_AMD_GEMM_GLDS_BUILTIN
-  __builtin_amdgcn_global_load_lds((glb_void_t*)gsrc, (lds_void_t*)ldst, 16, 0, 0);
-#else
   const unsigned la = __builtin_amdgcn_readfirstlane(
       (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)ldst);
   unsigned saved;
@@ -80,7 +76,6 @@ __device__ __forceinline__ void glds16(const bf16_t* gsrc, bf16_t* ldst) {
       : "=&s"(saved)
       : "v"(gsrc), "s"(la)
       : "memory");
-#endif
 }
 
 
@@ -198,129 +193,8 @@ __device__ __forceinline__ void epilogue_tile(f32x4_t (&acc)[4][8], int m0, int 
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 }
 
-// NSTAGE LDS buffers, NSTAGE-1 K-steps staged ahead. Per K-step: stage step s+NSTAGE-1,
-// MFMA step s, counted vmcnt for step s+1 (the younger steps stay in flight across the
-// barrier: raw s_barrier, no __syncthreads vmcnt(0) drain), barrier. At a tile's last
-// K-step the epilogue's stores join the counter, so that wait drains to 0.
-template <int EPI, int BK, int NSTAGE>
-__global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
-    const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb,
-    bf16_t* __restrict__ C, long ldc, int M, int N, int K, const bf16_t* __restrict__ bias,
-    bf16_t* __restrict__ aux, long ldaux, float* __restrict__ colpart) {
-  constexpr int kStage = (kBM + kBN) * BK;  // bf16 elements per stage buffer
-  constexpr int GPW = 2 * (32 / (64 / (BK / 8)));  // DMA instructions per wave per K-step
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NSTAGE * kStage];
-  const int G = gridDim.x;
-  const int L = xcd_remap(blockIdx.x, G);
-  const int tm_cnt = (M + kBM - 1) / kBM, tn_cnt = (N + kBN - 1) / kBN;
-  const int ntiles = tm_cnt * tn_cnt;
-  const bool n_major = tm_cnt <= tn_cnt;  // inner loop over the dimension with fewer tiles
-  const int nk = K / BK;
-  if (L >= ntiles) return;
-
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int wm = w >> 2, wn = w & 3;
-  constexpr int NKS = BK / 32;  // 32-deep MFMA k-steps per K-tile
-  int roff[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
-    roff[ks] = (lane & 15) * BK + 8 * ((4 * ks + (lane >> 4)) ^ swz<BK>(lane & 15));
-
-  auto tile_mn = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
-    if (n_major) {
-      n0 = (t / tm_cnt) * kBN;
-      m0 = (t % tm_cnt) * kBM;
-    } else {
-      m0 = (t / tn_cnt) * kBM;
-      n0 = (t % tn_cnt) * kBN;
-    }
-  };
-  auto stage = [&](int buf, int t, int kt) __attribute__((always_inline)) {
-    int m0, n0;
-    tile_mn(t, m0, n0);
-    bf16_t* img = lds + buf * kStage;
-    stage_operand<BK>(img, A, lda, m0, M, kt * BK, w, lane);
-    stage_operand<BK>(img + kBM * BK, B, ldb, n0, N, kt * BK, w, lane);
-  };
-
-  f32x4_t acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) __attribute__((always_inline)) {
-    const bf16_t* sA = lds + buf * kStage + (wm * 128) * BK;
-    const bf16_t* sB = lds + buf * kStage + kBM * BK + (wn * 64) * BK;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      bf16x8_t bf[4], af[8];
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * BK + roff[ks]);
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb)
-        af[mb] = *reinterpret_cast<const bf16x8_t*>(sA + mb * 16 * BK + roff[ks]);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int mb = 0; mb < 8; ++mb)
-          acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[nb], af[mb], acc[nb][mb], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  };
-
-  auto epilogue = [&](int t) __attribute__((always_inline)) {
-    int m0, n0;
-    tile_mn(t, m0, n0);
-    epilogue_tile<EPI>(acc, m0, n0, wm, wn, lane, M, N, C, ldc, bias, aux, ldaux, colpart);
-  };
-
-  // load cursor (lt, lkt): next K-step to stage; compute cursor (t, kt)
-  int lt = L, lkt = 0, staged = 0;
-  auto stage_next = [&]() __attribute__((always_inline)) {
-    stage(staged % NSTAGE, lt, lkt);
-    ++staged;
-    if (++lkt == nk) {
-      lkt = 0;
-      lt += G;
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < NSTAGE - 1; ++i)
-    if (lt < ntiles) stage_next();
-  // step 0 complete: the younger staged steps may stay in flight
-  if (staged >= 3 && NSTAGE >= 4) wait_vm<2 * GPW>();
-  else if (staged >= 2 && NSTAGE >= 3) wait_vm<GPW>();
-  else wait_vm<0>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  int t = L, kt = 0, done = 0;
-  for (;;) {
-    if (lt < ntiles) stage_next();
-    compute(done % NSTAGE);
-    ++done;
-    const bool tile_end = kt == nk - 1;
-    if (tile_end) epilogue(t);
-    // wait for step `done` (staged - done - 1 younger steps may stay in flight)
-    const int ahead = staged - done - 1;
-    if (tile_end || ahead <= 0) wait_vm<0>();
-    else if (NSTAGE >= 4 && ahead >= 2) wait_vm<2 * GPW>();
-    else wait_vm<GPW>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (done == staged) break;
-    if (++kt == nk) {
-      kt = 0;
-      t += G;
-    }
-  }
-}
-
-// Staggered two-group schedule (variant 0, the default): BK = 64, two stage buffers.
+// Staggered two-group schedule: BK = 64, two stage buffers (measured faster than the
+// single-group, BK 32 x 4-stage and quadrant 8-phase forms it replaced: profiles/r5).
 // Waves w and w+4 share a SIMD; waves 0-3 (group 0) and 4-7 (group 1) run the same
 // slot sequence per K-step — R0 (stage next step, read ks0 fragments) | M0 (16x16x32
 // MFMA cluster on ks0) | R1 | M1 — with barriers between slots, and group 1 starts one
@@ -438,218 +312,12 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_stagger_kernel(
   if (!g1) barrier();  // group 1 ran one extra barrier at the start
 }
 
-// ---------------------------------------------------------------------------------------
-// Quadrant-phased schedule (variant 3): 256x256 tile, BK = 64, two K-tile LDS buffers
-// (128 KB) restaged HALF-TILE by half-tile, so ~1.5 K-tiles of loads stay in flight
-// across the barriers (cdna_hip_programming.md §5 "The 256² 8-phase template": counted
-// vmcnt(6) once per K-tile, raw s_barrier, waves 4-7 staggered one barrier late).
-//
-// Each wave's 128 x 64 output is four 64 x 32 quadrants; one PHASE = one quadrant over the
-// whole K-tile = 16 v_mfma_f32_16x16x32_bf16. Quadrant order per K-tile and the register
-// subtiles read in that phase (A set: 64 rows, B sets: 32 columns, each over K = 64):
-//   a: (m0, n0)  read A rows m0 and B cols n0 (-> B set 0)      12 x ds_read_b128
-//   b: (m0, n1)  read B cols n1 (-> B set 1)                      4
-//   c: (m1, n1)  read A rows m1                                   8
-//   d: (m1, n0)  nothing (B set 0 still held)                     0
-// The LDS halves are cut along the same lines so that each is fully consumed in ONE phase:
-//   A-h0 = rows {64·0.., 128+64·0..} (the m0 rows of both wave groups), A-h1 = the m1 rows,
-//   B-h0 = cols {64·wc + 0..31}, B-h1 = cols {64·wc + 32..63}.
-// Reads are retired (lgkmcnt(0)) BEFORE the barrier that ends their segment, so a half may
-// be restaged in the very next phase (WAR). Restage schedule in phase j of K-tile k:
-//   j=0: A-h1 of k+1   j=1: A-h0 of k+2   j=2: B-h0 of k+2   j=3: B-h1 of k+2
-// and at j=3 each wave waits vmcnt(6): everything but its 3 youngest half-tiles (those of
-// K-tile k+2) has landed, i.e. all of K-tile k+1 (RAW: read after the next barrier).
-// Stagger: waves 4-7 run one barrier behind waves 0-3, so in every barrier interval one
-// wave of each SIMD issues its MFMA phase while its partner reads LDS / issues DMAs.
 template <int EPI>
-__global__ __launch_bounds__(kThreads) void gemm_nt_8ph_kernel(
-    const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B, long ldb,
-    bf16_t* __restrict__ C, long ldc, int M, int N, int K, const bf16_t* __restrict__ bias,
-    bf16_t* __restrict__ aux, long ldaux, float* __restrict__ colpart) {
-  constexpr int BK = 64;
-  constexpr int kStage = (kBM + kBN) * BK;  // one K-tile: A [256][64] then B [256][64]
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
-  const int G = gridDim.x;
-  const int L = xcd_remap(blockIdx.x, G);
-  const int tm_cnt = (M + kBM - 1) / kBM, tn_cnt = (N + kBN - 1) / kBN;
-  const int ntiles = tm_cnt * tn_cnt;
-  const bool n_major = tm_cnt <= tn_cnt;
-  const int nk = K / BK;
-  if (L >= ntiles) return;
-  const int total = ((ntiles - 1 - L) / G + 1) * nk;  // K-tiles this workgroup runs
-
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int wm = w >> 2, wn = w & 3;
-  const bool g1 = wm == 1;  // wave-uniform: the late group
-  int roff[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-    roff[ks] = (lane & 15) * BK + 8 * ((4 * ks + (lane >> 4)) ^ swz<BK>(lane & 15));
-
-  auto tile_mn = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
-    if (n_major) {
-      n0 = (t / tm_cnt) * kBN;
-      m0 = (t % tm_cnt) * kBM;
-    } else {
-      m0 = (t / tn_cnt) * kBM;
-      n0 = (t % tn_cnt) * kBN;
-    }
-  };
-  // stage one half-tile (128 rows of one operand = 2 DMA instructions per thread) of
-  // global K-tile g. half: 0 = A-h0, 1 = A-h1, 2 = B-h0, 3 = B-h1. Wave w moves half-rows
-  // q = 16w .. 16w+15 (8 rows = 1 KB per instruction, never crossing a 32-row block).
-  auto stage_half = [&](int g, int half) __attribute__((always_inline)) {
-    const int t = L + (g / nk) * G, kt = g % nk;
-    int m0, n0;
-    tile_mn(t, m0, n0);
-    const bool isA = half < 2;
-    const int h = half & 1;
-    const bf16_t* src = isA ? A : B;
-    const long ld = isA ? lda : ldb;
-    const int row0 = isA ? m0 : n0;
-    const int rows = isA ? M : N;
-    bf16_t* img = lds + (g & 1) * kStage + (isA ? 0 : kBM * BK);
-    const int rsub = lane >> 3, p = lane & 7;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int q0 = 16 * w + 8 * j;  // first half-row of this instruction
-      // physical tile row of half-row q: A halves are two 64-row blocks, B halves four
-      // 32-row blocks
-      const int prow0 = isA ? ((q0 >> 6) << 7) + 64 * h + (q0 & 63)
-                            : ((q0 >> 5) << 6) + 32 * h + (q0 & 31);
-      const int r = prow0 + rsub;
-      int gr = row0 + r;
-      gr = gr < rows ? gr : rows - 1;  // clamp ragged edges (results masked at the store)
-      const int ch = p ^ swz<BK>(r);
-      const bf16_t* s = src + (long)gr * ld + kt * BK + 8 * ch;
-      glds16(s, img + prow0 * BK);
-    }
-  };
-  auto barrier = []() __attribute__((always_inline)) {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  f32x4_t acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  bf16x8_t af[4][2], b0f[2][2], b1f[2][2];  // [block][ks]
-  // A rows of m-half hm of this wave: tile rows 128 wm + 64 hm + 16 mb + (lane & 15)
-  auto read_a = [&](const bf16_t* buf, int hm) __attribute__((always_inline)) {
-    const bf16_t* s = buf + (wm * 128 + hm * 64) * BK;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        af[mb][ks] = *reinterpret_cast<const bf16x8_t*>(s + mb * 16 * BK + roff[ks]);
-  };
-  auto read_b = [&](const bf16_t* buf, int hn, bf16x8_t (&bf)[2][2]) __attribute__((always_inline)) {
-    const bf16_t* s = buf + kBM * BK + (wn * 64 + hn * 32) * BK;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        bf[nb][ks] = *reinterpret_cast<const bf16x8_t*>(s + nb * 16 * BK + roff[ks]);
-  };
-  auto mfma_quadrant = [&](int hm, int hn, const bf16x8_t (&bf)[2][2]) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-          acc[2 * hn + nb][4 * hm + mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              bf[nb][ks], af[mb][ks], acc[2 * hn + nb][4 * hm + mb], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // prologue: K-tile 0 (all halves) + K-tile 1's A-h0, B-h0, B-h1; wait for K-tile 0
-  stage_half(0, 0);
-  stage_half(0, 2);
-  stage_half(0, 3);
-  stage_half(0, 1);
-  if (total > 1) {
-    stage_half(1, 0);
-    stage_half(1, 2);
-    stage_half(1, 3);
-    wait_vm<6>();
-  } else {
-    wait_vm<0>();
-  }
-  barrier();
-  if (g1) barrier();
-
-  for (int k = 0; k < total; ++k) {
-    const bf16_t* buf = lds + (k & 1) * kStage;
-    const bool more1 = k + 1 < total, more2 = k + 2 < total;
-    // ---- phase a: quadrant (m0, n0)
-    read_b(buf, 0, b0f);
-    read_a(buf, 0);
-    if (more1) stage_half(k + 1, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-    mfma_quadrant(0, 0, b0f);
-    barrier();
-    // ---- phase b: quadrant (m0, n1)
-    read_b(buf, 1, b1f);
-    if (more2) stage_half(k + 2, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-    mfma_quadrant(0, 1, b1f);
-    barrier();
-    // ---- phase c: quadrant (m1, n1)
-    read_a(buf, 1);
-    if (more2) stage_half(k + 2, 2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-    mfma_quadrant(1, 1, b1f);
-    barrier();
-    // ---- phase d: quadrant (m1, n0); K-tile k+1 must have landed before the next phase
-    if (more2) {
-      stage_half(k + 2, 3);
-      wait_vm<6>();
-    } else {
-      wait_vm<0>();
-    }
-    barrier();
-    mfma_quadrant(1, 0, b0f);
-    if (k % nk == nk - 1) {
-      int m0, n0;
-      tile_mn(L + (k / nk) * G, m0, n0);
-      epilogue_tile<EPI>(acc, m0, n0, wm, wn, lane, M, N, C, ldc, bias, aux, ldaux, colpart);
-    }
-    barrier();
-  }
-  if (!g1) barrier();  // group 1 ran one extra barrier at the start
-}
-
-template <int EPI, int BK, int NS>
-static void launch_gemm(int G, hipStream_t st, const bf16_t* a, long lda, const bf16_t* b,
-                        long ldb, bf16_t* c, long ldc, int M, int N, int K, const bf16_t* bi,
-                        bf16_t* ax, long ldaux, float* colpart) {
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, BK, NS>), dim3(G), dim3(kThreads), 0, st, a, lda, b,
+static void launch_epi(int G, hipStream_t st, const bf16_t* a, long lda, const bf16_t* b,
+                       long ldb, bf16_t* c, long ldc, int M, int N, int K, const bf16_t* bi,
+                       bf16_t* ax, long ldaux, float* colpart) {
+  hipLaunchKernelGGL((gemm_nt_stagger_kernel<EPI>), dim3(G), dim3(kThreads), 0, st, a, lda, b,
                      ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
-}
-
-template <int EPI>
-static void launch_epi(int variant, int G, hipStream_t st, const bf16_t* a, long lda,
-                       const bf16_t* b, long ldb, bf16_t* c, long ldc, int M, int N, int K,
-                       const bf16_t* bi, bf16_t* ax, long ldaux, float* colpart) {
-  if (variant == 3)
-    hipLaunchKernelGGL((gemm_nt_8ph_kernel<EPI>), dim3(G), dim3(kThreads), 0, st, a, lda, b, ldb,
-                       c, ldc, M, N, K, bi, ax, ldaux, colpart);
-  else if (variant == 1)
-    launch_gemm<EPI, 64, 2>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
-  else if (variant == 2)
-    launch_gemm<EPI, 32, 4>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
-  else
-    hipLaunchKernelGGL((gemm_nt_stagger_kernel<EPI>), dim3(G), dim3(kThreads), 0, st, a, lda, b,
-                       ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
 }
 
 int g_num_cus = 0;
@@ -685,20 +353,19 @@ RA_EXPORT int ra_gemm_nt(const void* A, long lda, const void* B, long ldb, void*
   const auto c = (bf16_t*)C;
   const auto bi = (const bf16_t*)bias;
   const auto ax = (bf16_t*)aux;
-  const int variant = ra_knobs[5];  // 0 = staggered (default), 1 = BK 64 x 2, 2 = BK 32 x 4
   switch (epi) {
     case EPI_NONE:
-      launch_epi<EPI_NONE>(variant, G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
+      launch_epi<EPI_NONE>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
       break;
     case EPI_BIAS:
-      launch_epi<EPI_BIAS>(variant, G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
+      launch_epi<EPI_BIAS>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux, colpart);
       break;
     case EPI_BIAS_GELU:
-      launch_epi<EPI_BIAS_GELU>(variant, G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux,
+      launch_epi<EPI_BIAS_GELU>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux,
                                 colpart);
       break;
     case EPI_DGELU:
-      launch_epi<EPI_DGELU>(variant, G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux,
+      launch_epi<EPI_DGELU>(G, st, a, lda, b, ldb, c, ldc, M, N, K, bi, ax, ldaux,
                             colpart);
       if (db != nullptr) {
         if (scratch == nullptr) return hipErrorInvalidValue;

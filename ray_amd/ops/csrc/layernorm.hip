@@ -415,37 +415,26 @@ RA_EXPORT int ra_residual_layernorm_fwd(const void* h, const void* rbias, const 
   return hipGetLastError();
 }
 
-// [11] = 2: attention dK/dV with both query halves in flight (r4e: 0.312 vs 0.322 ms)
-int ra_knobs[16] = {512, 8192, 1, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0, 0};
-
-RA_EXPORT int ra_set_knob(int k, int v) {
-  if (k < 0 || k >= 16) return hipErrorInvalidValue;
-  ra_knobs[k] = v;
-  return hipSuccess;
-}
-
-// Partial-row count for the backward: up to ra_knobs[0] blocks, each wave >= 2 rows.
+// Partial-row count for the v1 backward: up to 512 blocks, each wave >= 2 rows.
 // Measured at 65536 x 768 (profiles/r2_perf_bench.log, "norm"): 512 blocks beat 1024 /
 // 2048 / 4096 — more blocks only add partial-slab traffic and LDS-atomic tails.
 RA_EXPORT int ra_layernorm_bwd_parts(int N) {
   int p = (N + 7) / 8;
-  const int cap = ra_knobs[0] > 0 ? ra_knobs[0] : 2048;
-  return p < cap ? p : cap;
+  return p < 512 ? p : 512;
 }
 
-// v2 applies to D in {256, 512, 768, 1024} with N*D*2 < 2^31 (ra_knobs[3] = 1 forces v1).
+// v2 applies to D in {256, 512, 768, 1024} with N*D*2 < 2^31.
 static bool ln_bwd_v2(int N, int D) {
-  return ra_knobs[3] != 1 && D % 256 == 0 && D <= 1024 && (long)N * D * 2 < (1L << 31);
+  return D % 256 == 0 && D <= 1024 && (long)N * D * 2 < (1L << 31);
 }
 
-// v2 grid: ra_knobs[4] blocks (default 512), each wave >= 2 rows. Measured at 65536 x 768
+// v2 grid: 512 blocks, each wave >= 2 rows. Measured at 65536 x 768
 // (scripts/ln_bwd_bench.py, kernel only): 256 / 512 blocks 84 / 87 us (4.8 / 4.7 TB/s),
-// 768-1024 blocks 92-95 us, v1 105 us; a 3-deep row ring (ra_knobs[3] = 3) is no faster.
+// 768-1024 blocks 92-95 us, v1 105 us; a 3-deep row ring is no faster.
 static int ln_bwd_blocks(int N, int D) {
   if (!ln_bwd_v2(N, D)) return ra_layernorm_bwd_parts(N);
   int p = (N + 7) / 8;
-  const int cap = ra_knobs[4] > 0 ? ra_knobs[4] : 512;
-  return p < cap ? p : cap;
+  return p < 512 ? p : 512;
 }
 
 // fp32 workspace (in floats) required by ra_layernorm_bwd (3 partial slabs + scratch).
@@ -467,9 +456,7 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
   const size_t lds = (size_t)NP * D * sizeof(float);
   if (ln_bwd_v2(N, D)) {
     // fp32 sinks accumulated in place: column sums by atomics inside the kernel
-    // (ra_knobs[14] = 1: partial slabs + colsum launches as before)
-    const bool direct = !(flags & kColsumBF16) && (flags & kColsumAcc) && ra_knobs[2] &&
-                        ra_knobs[14] != 1;
+    const bool direct = !(flags & kColsumBF16) && (flags & kColsumAcc);
     float* o0 = direct ? (float*)dg : nullptr;
     float* o1 = direct ? (float*)db : nullptr;
     float* o2 = direct ? (float*)dbias : nullptr;
@@ -477,8 +464,7 @@ RA_EXPORT int ra_layernorm_bwd(const void* dy, const void* x, const void* g, con
   hipLaunchKernelGGL((ln_bwd2_kernel<V, NPV, R, KK>), dim3(P), dim3(256), lds, st,              \
                      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)g, mean, rstd,         \
                      (const bf16_t*)dres, (bf16_t*)dx, work, N, D, o0, o1, o2)
-#define L2(V, NPV, R)                                        \
-  if (ra_knobs[3] == 3) L2K(V, NPV, R, 3); else L2K(V, NPV, R, 2)
+#define L2(V, NPV, R) L2K(V, NPV, R, 2)
 #define L2V(V)                                       \
   if (NP == 3) {                                     \
     if (dres) L2(V, 3, true); else L2(V, 3, false);  \

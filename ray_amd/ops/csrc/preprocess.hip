@@ -170,7 +170,7 @@ RA_EXPORT int ra_image_normalize(const void* x, void* y, int N, int H, int W, in
   if (vec) {
     const long groups = (long)N * HW / 16;
     const dim3 g((unsigned)((groups + 255) / 256));
-    // ra_knobs[5] == 2: nontemporal loads/stores (measured slower on MI355X: 4.4 vs 5.5 TB/s)
+    // plain loads/stores: nontemporal ones measured slower on MI355X (4.4 vs 5.5 TB/s)
 #define RA_IMN2(CC, NTV)                                                                        \
   if (bf16_out)                                                                                 \
     hipLaunchKernelGGL((image_normalize_vec_kernel<CC, true, NTV>), g, dim3(256), 0, st,        \
@@ -180,7 +180,7 @@ RA_EXPORT int ra_image_normalize(const void* x, void* y, int N, int H, int W, in
                        (const uint8_t*)x, y, groups, HW / 16, p);
 #define RA_IMN(CC)                                                                              \
   if (C == CC) {                                                                                \
-    if (ra_knobs[5] == 2) { RA_IMN2(CC, true) } else { RA_IMN2(CC, false) }                     \
+    RA_IMN2(CC, false)                                                                          \
   }
     RA_IMN(1) RA_IMN(2) RA_IMN(3) RA_IMN(4)
 #undef RA_IMN

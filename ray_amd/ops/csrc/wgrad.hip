@@ -43,8 +43,6 @@
 // (release/air_tests/air_benchmarks/workloads/torch_benchmark.py:81).
 #include "common.h"
 
-#include <cstdlib>
-
 namespace {
 
 typedef __bf16 bf16x8w_t __attribute__((ext_vector_type(8)));
@@ -264,155 +262,7 @@ __device__ __forceinline__ void wgrad_mainloop(bf16_t* lds, const TileJob& j,
   }
 }
 
-// Deep-prefetch variant (ra_knobs[15] = 1): the same 128 KB of LDS as a ring of FOUR
-// 32-token stages instead of two 64-token ones, so three stages (96 tokens) are in flight
-// behind the one being read instead of one (64 tokens): the PMC pass (profiles/r5/r5al) has
-// the two-stage loop waiting in 35 % of its wave cycles. Per 32-token step s, both groups run
-//   [DMA of stage s+3 into the buffer step s-1 read] R(s) | Ba | M(s) | Bb
-// with waves 4-7 one barrier behind (the staggered schedule above); a group waits for its
-// own DMA of stage s+1 with a COUNTED vmcnt (stages s+2, s+3 stay in flight) before the
-// barrier that precedes the other group's read of s+1: group 0 before Bb, group 1 before Ba.
-// The buffer refilled at the top of step s was last read by R(s-1), which every wave
-// finished (lgkmcnt(0)) before a barrier that both groups have passed by then.
-constexpr int kT4 = 32;
-constexpr int kImg4 = kT4 * kTile;
-constexpr int kStage4 = 2 * kImg4;
-
-__device__ __forceinline__ void stage_t4(bf16_t* img, const bf16_t* __restrict__ g, long ld,
-                                         int col0, int cols, long t0, int w, int lane) {
-  const int rsub = lane >> 5, cp = lane & 31;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {  // wave w stages rows 4w .. 4w+3
-    const int r = 4 * w + 2 * j + rsub;
-    const int c = cp ^ (2 * fsw(r));
-    int col = col0 + 8 * c;
-    col = col < cols ? col : cols - 8;
-    const bf16_t* src = g + (t0 + r) * ld + col;
-    glds16_w(src, img + (4 * w + 2 * j) * kTile);
-  }
-}
-
-__device__ __forceinline__ void wait_stages_w(int n) {  // n stages (4 DMAs each) may remain
-  if (n >= 2) wait_vm_w<8>();
-  else if (n == 1) wait_vm_w<4>();
-  else wait_vm_w<0>();
-}
-
-__device__ __forceinline__ void wgrad_mainloop_deep(bf16_t* lds, const TileJob& j,
-                                                    f32x4w_t (&acc)[4][8], float (&bsum)[2],
-                                                    int w, int lane) {
-  const int wm = w >> 2, wn = w & 3;
-  const bool g1 = wm == 1;
-  const bool do_bias = j.do_bias;
-  const int total = 2 * j.total;  // 32-token steps
-  const int s0 = 2 * j.s_beg;
-  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int fl = q | ((gq & 1) << 2);
-  const int row_off = (8 * gq + q) * kTile + 4 * (p & 1);
-  int xoff[4], yoff[8];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb) xoff[kb] = row_off + 8 * ((2 * (wn * 4 + kb) + (p >> 1)) ^ (2 * fl));
-#pragma unroll
-  for (int nb = 0; nb < 8; ++nb) yoff[nb] = row_off + 8 * ((2 * (wm * 8 + nb) + (p >> 1)) ^ (2 * fl));
-  auto stage = [&](int ks) __attribute__((always_inline)) {
-    bf16_t* img = lds + (ks & 3) * kStage4;
-    const long t0 = (long)(s0 + ks) * kT4;
-    stage_t4(img, j.x, j.ldx, j.k0, j.K, t0, w, lane);
-    stage_t4(img + kImg4, j.dy, j.ldy, j.n0, j.N, t0, w, lane);
-  };
-  auto barrier = []() __attribute__((always_inline)) {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) acc[i][jj] = f32x4w_t{0.f, 0.f, 0.f, 0.f};
-  bsum[0] = bsum[1] = 0.f;
-  bf16x8w_t xf[4], yf[8];
-  auto read_frags = [&](int ks) __attribute__((always_inline)) {
-    const bf16_t* sx = lds + (ks & 3) * kStage4;
-    const bf16_t* sy = sx + kImg4;
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      const bf16x4w_t lo = tr4(sy + yoff[nb]);
-      const bf16x4w_t hi = tr4(sy + yoff[nb] + 4 * kTile);
-      yf[nb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const bf16x4w_t lo = tr4(sx + xoff[kb]);
-      const bf16x4w_t hi = tr4(sx + xoff[kb] + 4 * kTile);
-      xf[kb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  auto mfma_cluster = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb)
-        acc[kb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[kb], yf[nb], acc[kb][nb], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (do_bias) {
-      auto dot8 = [&](const bf16x8w_t& v, float& acc_) __attribute__((always_inline)) {
-        const bf16x2w_t one = {(__bf16)1.f, (__bf16)1.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bf16x2w_t pr = {v[2 * e], v[2 * e + 1]};
-          acc_ = __builtin_amdgcn_fdot2_f32_bf16(pr, one, acc_, false);
-        }
-      };
-      if (wn == 0) {
-        dot8(yf[0], bsum[0]);
-        dot8(yf[1], bsum[1]);
-      } else if (wn == 1) {
-        dot8(yf[2], bsum[0]);
-        dot8(yf[3], bsum[1]);
-      } else if (wn == 2) {
-        dot8(yf[4], bsum[0]);
-        dot8(yf[5], bsum[1]);
-      } else {
-        dot8(yf[6], bsum[0]);
-        dot8(yf[7], bsum[1]);
-      }
-    }
-  };
-  // stages still allowed in flight once stage s+1 must have landed (issued: up to s+3)
-  auto pending_after = [&](int s) __attribute__((always_inline)) {
-    const int last = (s + 3 < total ? s + 3 : total - 1);
-    const int n = last - (s + 1);
-    return n < 0 ? 0 : n;
-  };
-  if (total > 0) {
-    const int pre = total < 3 ? total : 3;
-    for (int k = 0; k < pre; ++k) stage(k);
-    wait_stages_w(pre - 1);  // stage 0 landed
-  }
-  barrier();
-  if (g1) barrier();
-  for (int st = 0; st < total; ++st) {
-    if (st + 3 < total) stage(st + 3);  // buffer of step st-1: every wave's reads retired
-    read_frags(st);
-    if (g1) wait_stages_w(pending_after(st));
-    barrier();
-    mfma_cluster();
-    if (!g1) wait_stages_w(pending_after(st));
-    barrier();
-  }
-  if (!g1) barrier();
-  if (do_bias) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      bsum[i] += __shfl_xor(bsum[i], 16, 64);
-      bsum[i] += __shfl_xor(bsum[i], 32, 64);
-    }
-  }
-}
-
-template <int MODE, bool DEEP = false>  // 0: fp32 slab store, 1: fp32 sink RMW, 2: bf16 sink RMW
+template <int MODE>  // 0: fp32 slab store, 1: fp32 sink RMW, 2: bf16 sink RMW
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
   const int G = gridDim.x;
@@ -430,8 +280,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a) {
   f32x4w_t acc[4][8];
   float bsum[2];
   const TileJob job{a.dy, a.x, a.ldy, a.ldx, a.N, a.K, n0, k0, s_beg, s_end - s_beg, do_bias};
-  if constexpr (DEEP) wgrad_mainloop_deep(lds, job, acc, bsum, w, lane);
-  else wgrad_mainloop(lds, job, acc, bsum, w, lane);
+  wgrad_mainloop(lds, job, acc, bsum, w, lane);
 
   // ---- epilogue: lane holds D[k = kc + 4(lane>>4) + r][n = nc + (lane & 15)]
   const int nrow = n0 + wm * 128 + (lane & 15);
@@ -512,204 +361,6 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Grouped weight gradients: the (up to kMaxProb) linears of one transformer layer in ONE
-// launch, with the split-K reduction inside the kernel. All problems share the token
-// count M; the grid is (sum of their 256 x 256 tiles) x S workgroups, S <= 4 chosen so the
-// launch is one wave of workgroups (GPT-2 small: 108 tiles x 2). Each tile's S partial
-// sums meet through an arrival ticket per tile: the first S-1 arrivers publish fp32 slabs
-// (plain stores, every wave drains, workgroup barrier, one agent-scope release fence, then
-// a "done" counter add); the last arriver polls "done" (one lane, relaxed atomic loads +
-// s_sleep), takes one agent-scope acquire fence, and adds the slabs to its registers
-// before its read-modify-write of the sink (MI355X_MICROARCH.md § Workgroup dispatch,
-// cdna_hip_programming.md §5 'In-launch split-K reduction'). A ticket is taken only after
-// the main loop, so the last arriver only ever waits for workgroups that are already in
-// their epilogue: no deadlock for any placement or dispatch order. The slab traffic is
-// (S-1) x tiles x 256 KB per layer (27 MB at S = 2) instead of S x the weights' bytes
-// written AND re-read by a separate pass.
-constexpr int kMaxProb = 8;
-struct WgProb {
-  const bf16_t* dy;
-  const bf16_t* x;
-  long ldy, ldx;
-  void* sink;       // [N][K] fp32 or bf16 (flags bit0)
-  void* bias_sink;  // [N] same dtype, or null
-  int N, K, tk_cnt, tile0, flags;  // flags: bit0 bf16 sinks, bit1 accumulate, bit2 bias
-};
-struct WgGroupArgs {
-  WgProb p[kMaxProb];
-  int np, ntiles, S, nks;
-  float* ws;   // (S-1) slabs per tile: [ntiles][S-1][256*256] then bias [ntiles][S-1][256]
-  int* cnt;    // [ntiles][2]: arrival tickets, published-slab count (zero at launch)
-};
-
-__global__ __launch_bounds__(kThreads) void wgrad_group_kernel(WgGroupArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
-  const int G = gridDim.x;
-  const int L = xcd_remap_w(blockIdx.x, G);
-  const int split = L / g.ntiles, tile = L - split * g.ntiles;
-  // this workgroup's problem: field-wise selects over constant-index kernarg reads (any
-  // runtime index into the by-value table makes hipcc copy all of it to scratch)
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxProb; ++i)
-    if (i < g.np && g.p[i].tile0 <= tile) pi = i;
-  pi = __builtin_amdgcn_readfirstlane(pi);  // provably wave-uniform: SGPR selects
-#define RA_SEL(f)                                                                          \
-  (pi == 0 ? g.p[0].f : pi == 1 ? g.p[1].f : pi == 2 ? g.p[2].f : pi == 3 ? g.p[3].f      \
-   : pi == 4 ? g.p[4].f : pi == 5 ? g.p[5].f : pi == 6 ? g.p[6].f : g.p[7].f)
-  struct {
-    const bf16_t* dy;
-    const bf16_t* x;
-    long ldy, ldx;
-    void* sink;
-    void* bias_sink;
-    int N, K, tk_cnt, tile0, flags;
-  } P = {RA_SEL(dy), RA_SEL(x), RA_SEL(ldy), RA_SEL(ldx), RA_SEL(sink), RA_SEL(bias_sink),
-         RA_SEL(N), RA_SEL(K), RA_SEL(tk_cnt), RA_SEL(tile0), RA_SEL(flags)};
-#undef RA_SEL
-  const int tl = tile - P.tile0;
-  const int tn = tl / P.tk_cnt, tk = tl - tn * P.tk_cnt;
-  const int n0 = tn * kTile, k0 = tk * kTile;
-  const int s_beg = (int)((long)split * g.nks / g.S);
-  const int s_end = (int)((long)(split + 1) * g.nks / g.S);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int wm = w >> 2, wn = w & 3;
-  const bool do_bias = (P.flags & 4) && tk == 0;
-  f32x4w_t acc[4][8];
-  float bsum[2];
-  const TileJob job{P.dy, P.x, P.ldy, P.ldx, P.N, P.K, n0, k0, s_beg, s_end - s_beg, do_bias};
-  wgrad_mainloop(lds, job, acc, bsum, w, lane);
-
-  // tile-local coordinates of this lane's accumulators (same for slabs and the sink)
-  const int nl = wm * 128 + (lane & 15);
-  const int kl = wn * 64 + 4 * (lane >> 4);
-  if (g.S > 1) {
-    __syncthreads();
-    int* tick = reinterpret_cast<int*>(lds);  // the staging array is free now
-    if (threadIdx.x == 0)
-      tick[0] = __hip_atomic_fetch_add(g.cnt + 2 * tile, 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int slot = tick[0];
-    float* slab0 = g.ws + (long)tile * (g.S - 1) * (kTile * kTile);
-    float* bslab0 = g.ws + (long)g.ntiles * (g.S - 1) * (kTile * kTile) +
-                    (long)tile * (g.S - 1) * kTile;
-    if (slot < g.S - 1) {  // publish this partial and leave
-      float* slab = slab0 + (long)slot * (kTile * kTile);
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-          const f32x4w_t v = acc[kb][nb];
-          *reinterpret_cast<float4*>(slab + (nl + nb * 16) * kTile + kl + kb * 16) =
-              make_float4(v[0], v[1], v[2], v[3]);
-        }
-      if (do_bias && lane < 16) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          bslab0[(long)slot * kTile + wm * 128 + (2 * wn + i) * 16 + lane] = bsum[i];
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(g.cnt + 2 * tile + 1, 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    // last arriver: wait until the S-1 earlier arrivers have published (they are all in
-    // their epilogue already); bounded, so a broken protocol cannot hang the GPU
-    if (threadIdx.x == 0) {
-      for (long it = 0; it < (1L << 26); ++it) {
-        if (__hip_atomic_load(g.cnt + 2 * tile + 1, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT) >= g.S - 1)
-          break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // the earlier arrivers' slabs are folded into the RMW pass below (4 loads per slab
-    // per batch: the accumulators keep their registers)
-  }
-  // the tile's full sum: read-modify-write of the sink (single writer per tile now)
-  const bool bf = P.flags & 1, accum = P.flags & 2;
-  const int nslab = g.S > 1 ? g.S - 1 : 0;
-  const float* slab0 = g.ws + (long)tile * (g.S > 1 ? g.S - 1 : 1) * (kTile * kTile);
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
-    const int k = k0 + kl + kb * 16;
-    const int kc = k < P.K ? k : P.K - 4;
-    for (int sl = 0; sl < nslab; ++sl) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float4 o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          o[j] = *reinterpret_cast<const float4*>(slab0 + (long)sl * (kTile * kTile) +
-                                                  (nl + (4 * h + j) * 16) * kTile + kl +
-                                                  kb * 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[kb][4 * h + j] += f32x4w_t{o[j].x, o[j].y, o[j].z, o[j].w};
-      }
-    }
-    float old[8][4];
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      const int n = n0 + nl + nb * 16;
-      const long o = (long)(n < P.N ? n : P.N - 1) * P.K + kc;
-      if (!accum) {
-        old[nb][0] = old[nb][1] = old[nb][2] = old[nb][3] = 0.f;
-      } else if (!bf) {
-        const float4 t = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.sink) + o);
-        old[nb][0] = t.x, old[nb][1] = t.y, old[nb][2] = t.z, old[nb][3] = t.w;
-      } else {
-        unpack4(*reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(P.sink) + o),
-                old[nb]);
-      }
-    }
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      const int n = n0 + nl + nb * 16;
-      if (n >= P.N || k >= P.K) continue;
-      const f32x4w_t v = acc[kb][nb];
-      float f[4] = {v[0] + old[nb][0], v[1] + old[nb][1], v[2] + old[nb][2], v[3] + old[nb][3]};
-      const long o = (long)n * P.K + k;
-      if (!bf)
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(P.sink) + o) =
-            make_float4(f[0], f[1], f[2], f[3]);
-      else
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(P.sink) + o) = pack4(f);
-    }
-  }
-  if (do_bias && lane < 16) {
-    const float* bslab0 = g.ws + (long)g.ntiles * (g.S > 1 ? g.S - 1 : 1) * (kTile * kTile) +
-                          (long)tile * (g.S > 1 ? g.S - 1 : 1) * kTile;
-    for (int sl = 0; sl < nslab; ++sl)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        bsum[i] += bslab0[(long)sl * kTile + wm * 128 + (2 * wn + i) * 16 + lane];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = n0 + wm * 128 + (2 * wn + i) * 16 + lane;
-      if (n >= P.N) continue;
-      if (!bf) {
-        float* d = reinterpret_cast<float*>(P.bias_sink) + n;
-        *d = accum ? *d + bsum[i] : bsum[i];
-      } else {
-        bf16_t* d = reinterpret_cast<bf16_t*>(P.bias_sink) + n;
-        *d = f2bf(accum ? bf2f(*d) + bsum[i] : bsum[i]);
-      }
-    }
-  }
-}
-
 int g_cus_w = 0;
 
 }  // namespace
@@ -718,7 +369,7 @@ int g_cus_w = 0;
 //   S = 1: RMW into `sink` (flags bit0: bf16 sink, bit1: accumulate) and `bias_sink`.
 //   S > 1: fp32 slabs ws[S][N][K] (+ bias slabs bws[S][N]); the caller sums them.
 // Requirements (checked): N % 8 == 0, K % 8 == 0, ldy / ldx % 8 == 0, 16-byte aligned
-// pointers. Returns the number of splits used through *s_used (S = 0: auto).
+// pointers. S (>= 1, clamped to the 64-token slices) is chosen by ra_wgrad_splits.
 RA_EXPORT int ra_wgrad(const void* dy, long ldy, const void* x, long ldx, int M, int N, int K,
                        int S, void* out, void* bias_out, int flags, hipStream_t st) {
   if (M < 64 || N <= 0 || K <= 0 || N % 8 || K % 8 || ldy % 8 || ldx % 8 || S < 1)
@@ -740,13 +391,11 @@ RA_EXPORT int ra_wgrad(const void* dy, long ldy, const void* x, long ldx, int M,
   a.S = S;
   a.flags = flags;
   const int G = a.ntiles * S;
-  const bool deep = ra_knobs[15] == 1;
   void (*k)(WgradArgs);
   if (S == 1)
-    k = (flags & 1) ? (deep ? wgrad_kernel<2, true> : wgrad_kernel<2, false>)
-                    : (deep ? wgrad_kernel<1, true> : wgrad_kernel<1, false>);
+    k = (flags & 1) ? wgrad_kernel<2> : wgrad_kernel<1>;
   else
-    k = deep ? wgrad_kernel<0, true> : wgrad_kernel<0, false>;
+    k = wgrad_kernel<0>;
   hipLaunchKernelGGL(k, dim3(G), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
@@ -761,22 +410,11 @@ RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
         g_cus_w <= 0)
       g_cus_w = 256;
   }
-  // RAY_AMD_WGRAD_WAVES=w: w waves of workgroups (shorter-lived workgroups, so a main-stream
-  // kernel launched meanwhile gets CUs sooner; more fp32 slab traffic)
-  static const int waves = [] {
-    const char* e = getenv("RAY_AMD_WGRAD_WAVES");
-    const int w = e ? atoi(e) : 1;
-    return w < 1 ? 1 : (w > 8 ? 8 : w);
-  }();
-  // RAY_AMD_WGRAD_FILL=f (0 < f <= 1): fill only a fraction f of the CUs (fewer, longer
-  // workgroups: less fp32 slab traffic and fewer CUs taken from the main stream)
-  static const double fill = [] {
-    const char* e = getenv("RAY_AMD_WGRAD_FILL");
-    const double f = e ? atof(e) : 1.0;
-    return f <= 0.0 || f > 1.0 ? 1.0 : f;
-  }();
+  // (measured: two waves of shorter workgroups or a partial fill of the CUs were no
+  // faster in the step, profiles/r5/r5ah; fixed split counts on several side streams
+  // slower, profiles/r6/r6b)
   const int tiles = ((N + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-  int S = (int)(waves * fill * g_cus_w) / tiles;
+  int S = g_cus_w / tiles;
   const int nks = M / kT;
   if (S < 1) {
     // more tiles than CUs (the LM head's dW: 197 x 3 = 591 tiles): the split count that
@@ -792,68 +430,4 @@ RA_EXPORT int ra_wgrad_splits(int M, int N, int K) {
   if (S > nks) S = nks;
   if (S < 1) S = 1;
   return S;
-}
-
-// Grouped weight gradients of up to 8 linears with one token count M (a multiple of 64):
-// problem i = (dy_i [M][ldy_i], x_i [M][ldx_i], sink_i [N_i][K_i], bias_sink_i, flags_i),
-// passed as parallel arrays. S: splits of the token range (1..4; 0 = auto: one wave of
-// workgroups). ws: workspace of ra_wgrad_group_ws_bytes(...) bytes (counters zeroed here).
-RA_EXPORT long ra_wgrad_group_ws_bytes(int ntiles, int S) {
-  if (S < 2) S = 2;
-  return (long)ntiles * (S - 1) * (kTile * kTile + kTile) * 4 + (long)ntiles * 2 * 4 + 256;
-}
-
-RA_EXPORT int ra_wgrad_group_splits(int M, int ntiles) {
-  if (g_cus_w == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_cus_w, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        g_cus_w <= 0)
-      g_cus_w = 256;
-  }
-  int S = ntiles > 0 ? g_cus_w / ntiles : 1;
-  if (S > 4) S = 4;
-  if (S > M / kT) S = M / kT;
-  return S < 1 ? 1 : S;
-}
-
-RA_EXPORT int ra_wgrad_group(int np, const void* const* dy, const long* ldy,
-                             const void* const* x, const long* ldx, void* const* sink,
-                             void* const* bias_sink, const int* N, const int* K,
-                             const int* flags, int M, int S, void* ws, hipStream_t st) {
-  if (np < 1 || np > kMaxProb || M < 64 || M % 64 || S < 1 || S > 4 || !ws)
-    return hipErrorInvalidValue;
-  WgGroupArgs g;
-  int tiles = 0;
-  for (int i = 0; i < np; ++i) {
-    if (N[i] <= 0 || K[i] <= 0 || N[i] % 8 || K[i] % 8 || ldy[i] % 8 || ldx[i] % 8 || !sink[i])
-      return hipErrorInvalidValue;
-    if ((flags[i] & 4) && !bias_sink[i]) return hipErrorInvalidValue;
-    WgProb& P = g.p[i];
-    P.dy = (const bf16_t*)dy[i];
-    P.x = (const bf16_t*)x[i];
-    P.ldy = ldy[i];
-    P.ldx = ldx[i];
-    P.sink = sink[i];
-    P.bias_sink = bias_sink[i];
-    P.N = N[i];
-    P.K = K[i];
-    P.tk_cnt = (K[i] + kTile - 1) / kTile;
-    P.tile0 = tiles;
-    P.flags = flags[i];
-    tiles += ((N[i] + kTile - 1) / kTile) * P.tk_cnt;
-  }
-  for (int i = np; i < kMaxProb; ++i) g.p[i] = g.p[0];
-  g.np = np;
-  g.ntiles = tiles;
-  g.S = S;
-  g.nks = M / kT;
-  g.ws = (float*)ws;
-  g.cnt = (int*)((char*)ws + (long)tiles * (S > 1 ? S - 1 : 1) * (kTile * kTile + kTile) * 4);
-  if (S > 1) {
-    const hipError_t e = hipMemsetAsync(g.cnt, 0, (size_t)tiles * 2 * sizeof(int), st);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(wgrad_group_kernel, dim3(tiles * S), dim3(kThreads), 0, st, g);
-  return hipGetLastError();
 }

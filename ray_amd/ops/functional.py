@@ -263,52 +263,31 @@ def bias_residual(h, bias, res):
 
 
 # --------------------------------------------------------------------- linear (split-K wgrad)
-# Weight-gradient GEMMs (fp32 out): "hip" (default) = the hand-written CDNA4 kernel
-# (ops/csrc/wgrad.hip, bias gradient fused; measured -2.3 ms/step vs "lt-splitk" on MI355X,
-# profiles/r5/r5c); "lt-splitk" = split-K fp32 partials from a
-# tuned strided-batched hipBLASLt GEMM (ops/lt.py) summed by ra_splitk_accum; "splitk" =
-# the same with torch.bmm's heuristic kernel; "lt" = one tuned GEMM accumulating straight
-# into the fp32 sink (beta = 1; measured slower at GPT-2 shapes: K = 65536 wants split-K)
-_WGRAD = os.environ.get("RAY_AMD_WGRAD", "hip")
-# attention backward: "split" (dkdv + dq kernels, no atomics, bitwise reproducible dQ) or
-# "fused" (dK, dV, dQ in one pass with fp32 dQ atomics). Measured at GPT-2 small, B 64
-# (profiles/r2/attn_bwd_fused_vs_split.md): split 384 + 337 us, fused 730 us — the fused
-# pass moves 0.9 GB of fp32 dQ partial sums (16 KB per workgroup x q-tile) against the
-# split dq kernel's 100 MB, which outweighs the S / dP recompute it saves at head_dim 64
-_ATTN_BWD = os.environ.get("RAY_AMD_ATTN_BWD", "split")
-_WGRAD_LT = _WGRAD == "lt"
-# RAY_AMD_WGRAD_STREAM=1: weight-gradient GEMMs (into flat grads) run on a side stream
+# Weight gradients (fp32 out) run the hand-written CDNA4 kernel (ops/csrc/wgrad.hip, bias
+# gradient fused; measured -2.3 ms/step vs hipBLASLt split-K partials on MI355X,
+# profiles/r5/r5c). Layouts that kernel does not take fall back to fp32 split-K partials
+# from S token-slice GEMMs (torch.bmm on the main stream, ops/lt's per-stream hipBLASLt
+# handle on the side stream) summed into the sink by one HIP pass.
+# RAY_AMD_WGRAD_STREAM=1 (default): weight gradients run on a side stream
 _WGRAD_STREAM = os.environ.get("RAY_AMD_WGRAD_STREAM", "1") == "1"
 # RAY_AMD_CONV_DGRAD=0: conv input gradients on MIOpen instead of conv.hip
 _CONV_DGRAD = os.environ.get("RAY_AMD_CONV_DGRAD", "1") == "1"
 # RAY_AMD_CONV_WGRAD_STREAM=1: the same for the conv weight-gradient kernels
 _CONV_WGRAD_STREAM = os.environ.get("RAY_AMD_CONV_WGRAD_STREAM", "0") == "1"
 
+# fallback split-K: at most 16 token slices of >= 2048 tokens, <= 4 GiB of fp32 partials
+# (profiles/r2_perf_bench.log: S = 16 fastest for every GPT-2 projection on hipBLASLt)
+_WGRAD_MAX_SPLITS = 16
+_WGRAD_PART_BYTES = 4 << 30
+
 
 def _splitk(M: int, N: int, K: int) -> int:
-    """Token slices for the wgrad GEMM. Measured on MI355X at M = 65536 (GPT-2 small,
-    profiles/r2_perf_bench.log): S = 16 is the fastest for every projection (qkv 0.28 ms
-    vs 0.39 at S = 4, proj 0.09 vs 0.14 at S = 8, fc/mlp_proj within 3 %) — hipBLASLt's
-    batched kernels fill the 256 CUs only with many (N/256)*(K/256)*S tiles. Slices
-    stay >= 2048 tokens so each batch GEMM keeps a long K loop."""
+    """Token slices for the fallback split-K weight gradient."""
     S = 1
-    # RAY_AMD_WGRAD_TILES > 0: stop splitting once the batched GEMM has that many 256x256
-    # output tiles (one wave of the 256 CUs): more splits only add fp32 partial traffic,
-    # which competes with the main stream's memory-bound backward kernels
-    tiles = ((N + 255) // 256) * ((K + 255) // 256)
     while (S < _WGRAD_MAX_SPLITS and M % (2 * S) == 0 and M // (2 * S) >= 2048
-           and 2 * S * N * K * 4 <= _WGRAD_PART_BYTES
-           and not (_WGRAD_TILES and tiles * S >= _WGRAD_TILES)):
+           and 2 * S * N * K * 4 <= _WGRAD_PART_BYTES):
         S *= 2
     return S
-
-
-_WGRAD_MAX_SPLITS = int(os.environ.get("RAY_AMD_WGRAD_SPLITS", "16"))
-_WGRAD_TILES = int(os.environ.get("RAY_AMD_WGRAD_TILES", "0"))
-# cap on the fp32 split-K partials of one weight gradient: every partial byte is written by
-# the GEMM and read back by ra_splitk_accum while the main stream's memory-bound backward
-# kernels compete for HBM
-_WGRAD_PART_BYTES = int(float(os.environ.get("RAY_AMD_WGRAD_PART_MB", "4096")) * (1 << 20))
 
 
 def _on_side_stream(t) -> bool:
@@ -321,7 +300,7 @@ def _wgrad_partials(dy2, x2, S, M, N, K):
     ops/lt (a per-stream hipBLASLt handle): torch.bmm would share torch's one handle with
     the main stream's dX GEMM, the concurrent stream-K setup that hung in round 4."""
     side = dy2.is_cuda and _on_side_stream(dy2)
-    if (_WGRAD == "lt-splitk" and dy2.is_contiguous() and x2.is_contiguous()) or side:
+    if side:
         from . import lt
 
         return lt.wgrad_partials(dy2.contiguous(), x2.contiguous(), S)
@@ -380,98 +359,10 @@ def wgrad_accumulate(dy2, x2, sink, bias_sink=None, accumulate=True):
             bias_sink.copy_(bias_sink.float() + dt.sum(0))
 
 
-# Grouped weight gradients (RAY_AMD_WGRAD_GROUP=1, opt-in): the hip wgrads of a layer's
-# linears are queued and launched together once their 256x256 tiles reach
-# RAY_AMD_WGRAD_GROUP_TILES (GPT-2 small: mlp_proj 36 + fc 36 + proj 9 + qkv 27 = 108 ->
-# one launch per layer after qkv's backward) as ONE kernel with the split-K reduction
-# inside (ra_wgrad_group: S = 2 at 108 tiles, 27 MB of fp32 slabs per layer instead of the
-# per-linear S = 7..28 slabs and the separate ra_splitk_accum pass). DDP readiness of the
-# queued weights (and fused biases) is signalled at the launch. Opt-in (=1): measured on
-# MI355X (profiles/r5/r5e) the layer's one 1.1 ms launch lands on the next layer's fc2
-# dgrad GEMM, a persistent 256-workgroup hipBLASLt kernel that then takes 1.17 ms instead
-# of 0.23 ms; the step is 65.1 ms grouped vs 64.8 ms per-linear.
-_WGRAD_GROUP = os.environ.get("RAY_AMD_WGRAD_GROUP", "0") == "1"
-_WGRAD_GROUP_TILES = int(os.environ.get("RAY_AMD_WGRAD_GROUP_TILES", "96"))
-_pending_wg: dict = {}  # device -> {"items": [...], "tiles": int, "M": int}
-
-
-def _wg_tiles(N, K):
-    return ((N + 255) // 256) * ((K + 255) // 256)
-
-
-def _queue_wgrad(dy2, x2, w, sink, bias=None, bias_sink=None):
-    dev = dy2.device
-    M, N = dy2.shape
-    K = x2.shape[1]
-    q = _pending_wg.get(dev)
-    if q is not None and (q["M"] != M or len(q["items"]) >= 8):
-        flush_wgrads(dev)
-        q = None
-    if q is None:
-        q = _pending_wg[dev] = {"items": [], "tiles": 0, "M": M}
-    # autograd's AccumulateGrad post-hook fires for these parameters (with a None grad) as
-    # soon as this backward returns: the pending mark keeps a DDP bucket hook from counting
-    # them ready before the grouped kernel that writes their gradients is enqueued
-    w._ra_grad_pending = True
-    if bias_sink is not None:
-        bias._ra_grad_pending = True
-    q["items"].append((dy2, x2, w, sink, bias, bias_sink))
-    q["tiles"] += _wg_tiles(N, K)
-    if q["tiles"] >= _WGRAD_GROUP_TILES or len(q["items"]) >= 8:
-        flush_wgrads(dev)
-
-
-def flush_wgrads(device=None):
-    """Launch every queued weight gradient (on the side stream, after the current stream's
-    work that produced their inputs) and signal their DDP readiness."""
-    import ctypes
-
-    devs = [device] if device is not None else list(_pending_wg)
-    for dev in devs:
-        q = _pending_wg.pop(dev, None)
-        if not q or not q["items"]:
-            continue
-        items = q["items"]
-        n = len(items)
-        M = q["M"]
-        L = _lib.lib()
-        side = _side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            P = ctypes.c_void_p * n
-            I = ctypes.c_int * n
-            Lg = ctypes.c_long * n
-            dys = P(*[it[0].data_ptr() for it in items])
-            xs = P(*[it[1].data_ptr() for it in items])
-            ldy = Lg(*[it[0].stride(0) for it in items])
-            ldx = Lg(*[it[1].stride(0) for it in items])
-            sinks = P(*[it[3].data_ptr() for it in items])
-            bsinks = P(*[it[5].data_ptr() if it[5] is not None else None for it in items])
-            Ns = I(*[it[0].shape[1] for it in items])
-            Ks = I(*[it[1].shape[1] for it in items])
-            fl = I(*[(1 if it[3].dtype == torch.bfloat16 else 0) | 2 |
-                     (4 if it[5] is not None else 0) for it in items])
-            tiles = q["tiles"]
-            S = L.ra_wgrad_group_splits(M, tiles)
-            ws = torch.empty((L.ra_wgrad_group_ws_bytes(tiles, S) + 3) // 4, device=dev,
-                             dtype=torch.float32)
-            check(L.ra_wgrad_group(n, dys, ldy, xs, ldx, sinks, bsinks, Ns, Ks, fl, M, S,
-                                   ptr(ws), stream_ptr()), "wgrad_group")
-            for it in items:
-                it[0].record_stream(side)
-                it[1].record_stream(side)
-        for it in items:
-            it[2]._ra_grad_pending = False
-            _grad_done(it[2])
-            if it[5] is not None:
-                it[4]._ra_grad_pending = False
-                _grad_done(it[4])
-
-
 def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, bias=None, bias_sink=None):
     """sink += dy2^T x2 (fp32 or bf16 flat-gradient view), then signal DDP readiness. With
     ``bias_sink`` (hip path only) the bias gradient is fused into the same kernel."""
-    if _WGRAD == "hip" and _wgrad_hip_ok(dy2, x2, sink, bias_sink):
+    if _wgrad_hip_ok(dy2, x2, sink, bias_sink):
         wgrad_accumulate(dy2, x2, sink, bias_sink)
         _grad_done(w)
         if bias_sink is not None:
@@ -480,30 +371,15 @@ def _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, bias=None, bias_sink=None):
     if bias_sink is not None:  # layout not supported by the fused kernel: separate colsum
         _colsum_bf16(dy2, out=bias_sink)
         _grad_done(bias)
-    if _sink_f32(sink) and _WGRAD_LT:
-        # hipBLASLt accumulates straight into the fp32 flat gradient (beta = 1)
-        from . import lt
-
-        lt.wgrad_accum(dy2, x2, sink.view(N, K))
-    else:
-        # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into the
-        # flat gradient) by one HIP pass
-        part = _wgrad_partials(dy2, x2, S, M, N, K)
-        check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(sink),
-                                         1 | 2 * _sink_f32(sink), stream_ptr()), "splitk_accum")
+    # fp32 partials [S, N, K] from S token-slice GEMMs, summed (+ accumulated into the flat
+    # gradient) by one HIP pass
+    part = _wgrad_partials(dy2, x2, S, M, N, K)
+    check(_lib.lib().ra_splitk_accum(ptr(part), S, N * K, ptr(sink),
+                                     1 | 2 * _sink_f32(sink), stream_ptr()), "splitk_accum")
     _grad_done(w)
 
 
 _side: dict = {}
-
-# RAY_AMD_WGRAD_DEFER=1 (experiment): weight gradients of linears called with wg_hint="defer"
-# (GPT-2: c_fc, c_attn) are not issued after their dgrad GEMM but at the next flush point
-# (the backward of a linear with wg_hint="flush": c_proj), so they run beside the attention
-# backward (the dQ kernel shares CUs with a wgrad workgroup) instead of beside the next
-# dgrad GEMM, which cannot share a CU with one (131 / 133 KB of LDS; profiles/r5/README.md).
-_WGRAD_DEFER = os.environ.get("RAY_AMD_WGRAD_DEFER", "0") == "1"
-_deferred_wg: list = []
-
 
 def _issue_side_wgrad(job):
     dy2, x2, w, sink, S, M, N, K, b, bsink = job
@@ -515,43 +391,16 @@ def _issue_side_wgrad(job):
         x2.record_stream(side)
 
 
-def flush_deferred_wgrads():
-    while _deferred_wg:
-        _issue_side_wgrad(_deferred_wg.pop(0))
-
-
 def _side_stream(device):
     st = _side.get(device)
     if st is None:
-        cus = os.environ.get("RAY_AMD_SIDE_CUS")
-        if cus:  # experiment: the side stream on a CU subset (ops/cu_mask.py)
-            from . import cu_mask
-
-            st = cu_mask.masked_stream(device, cu_mask.cu_range(device, cus))
-        else:
-            st = torch.cuda.Stream(device)
-        _side[device] = st
-    return st
-
-
-_side2: dict = {}
-
-
-def _side_stream2(device):
-    st = _side2.get(device)
-    if st is None:
-        st = _side2[device] = torch.cuda.Stream(device)
+        st = _side[device] = torch.cuda.Stream(device)
     return st
 
 
 def join_side_streams():
     """Make the current stream wait for weight-gradient work queued on side streams (call
-    before consuming the flat gradients: optimizer step, collective); grouped weight
-    gradients still queued are launched first."""
-    if _pending_wg:
-        flush_wgrads()
-    if _deferred_wg:
-        flush_deferred_wgrads()
+    before consuming the flat gradients: optimizer step, collective)."""
     for dev, st in _side.items():
         torch.cuda.current_stream(dev).wait_stream(st)
 
@@ -653,10 +502,9 @@ def _transposed_weight(w):
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, wg_hint=None):
+    def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.b = b
-        ctx.wg_hint = wg_hint
         ctx.wt = _transposed_weight(w) if _DGRAD_WT and w.is_cuda and x.dim() >= 2 else None
         return torch.nn.functional.linear(x, w, b)
 
@@ -680,8 +528,7 @@ class _Linear(torch.autograd.Function):
         # hip wgrad: the bias gradient (colsum of dY) is fused into the weight-gradient kernel
         # when both parameters write flat-gradient sinks of one dtype
         bsink = None
-        if _WGRAD == "hip" and ctx.b is not None and ctx.needs_input_grad[2] and \
-                ctx.needs_input_grad[1]:
+        if ctx.b is not None and ctx.needs_input_grad[2] and ctx.needs_input_grad[1]:
             bsink = _grad_sink(ctx.b)
             ws_ = _grad_sink(w)
             if bsink is not None and (ws_ is None or ws_.dtype != bsink.dtype):
@@ -689,20 +536,10 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             S = _splitk(M, N, K)
-            if sink is not None and _WGRAD_STREAM and dy2.is_cuda and _WGRAD == "hip" and \
-                    _WGRAD_GROUP and M % 64 == 0 and _wgrad_hip_ok(dy2, x2, sink, bsink):
-                # queued: launched with the layer's other linears as one grouped kernel
-                _queue_wgrad(dy2, x2, w, sink, ctx.b, bsink)
-            elif sink is not None and _WGRAD_STREAM and dy2.is_cuda:
+            if sink is not None and _WGRAD_STREAM and dy2.is_cuda:
                 # weight gradient on the side stream: it overlaps the memory-bound kernels
                 # of the dX chain that continues on the main stream
-                job = (dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
-                if _WGRAD_DEFER and ctx.wg_hint == "defer":
-                    _deferred_wg.append(job)  # issued at the next flush point
-                else:
-                    _issue_side_wgrad(job)
-                    if _WGRAD_DEFER and ctx.wg_hint == "flush":
-                        flush_deferred_wgrads()
+                _issue_side_wgrad((dy2, x2, w, sink, S, M, N, K, ctx.b, bsink))
             elif sink is not None:
                 _wgrad_to_sink(dy2, x2, w, sink, S, M, N, K, ctx.b, bsink)
             elif S > 1:
@@ -714,16 +551,15 @@ class _Linear(torch.autograd.Function):
                 dw = dy2.t() @ x2
         if ctx.b is not None and ctx.needs_input_grad[2] and bsink is None:
             db = _bias_grad(dy2, ctx.b)
-        return dx, dw, db, None
+        return dx, dw, db
 
 
-def linear(x, w, b=None, wg_hint=None):
+def linear(x, w, b=None):
     """y = x @ w^T + b with the MI355X backward (split-K fp32 wgrad, in-place flat-grad
-    accumulation). Same numerics contract as F.linear. ``wg_hint`` ("defer" / "flush")
-    places the weight gradient under RAY_AMD_WGRAD_DEFER (see _WGRAD_DEFER)."""
+    accumulation). Same numerics contract as F.linear."""
     if _hip(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and \
             (w.shape[0] * w.shape[1]) % 4 == 0:
-        return _Linear.apply(x, w, b, wg_hint)
+        return _Linear.apply(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 
 
@@ -748,31 +584,12 @@ class _FlashAttnQKV(torch.autograd.Function):
         dout = dout.contiguous()
         dqkv = torch.empty_like(qkv)
         delta = torch.empty((B, H, T), device=qkv.device, dtype=torch.float32)
-        if _ATTN_BWD == "fused":  # one pass: dK, dV + dQ through fp32 atomics
-            dq_ws = torch.empty((B * H * T * D,), device=qkv.device, dtype=torch.float32)
-            check(_lib.lib().ra_attn_bwd_fused(ptr(qkv), ptr(out), ptr(dout), ptr(lse),
-                                               ptr(delta), ptr(dq_ws), ptr(dqkv), B, T, H, D,
-                                               ctx.scale, stream_ptr()), "attn_bwd_fused")
-        elif _ATTN_BWD == "split2":  # dK/dV and dQ kernels concurrently on two streams
-            L = _lib.lib()
-            dev = qkv.device
-            main = torch.cuda.current_stream(dev)
-            side = _side_stream2(dev)
-            check(L.ra_attn_bwd_pre(ptr(out), ptr(dout), ptr(delta), B, T, H, stream_ptr()),
-                  "attn_bwd_pre")
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                check(L.ra_attn_bwd_q(ptr(qkv), ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), B,
-                                      T, H, D, ctx.scale, stream_ptr()), "attn_bwd_q")
-                for t_ in (qkv, dout, lse, delta, dqkv):
-                    t_.record_stream(side)
-            check(L.ra_attn_bwd_kv(ptr(qkv), ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), B, T,
-                                   H, D, ctx.scale, stream_ptr()), "attn_bwd_kv")
-            main.wait_stream(side)
-        else:
-            check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
-                                         ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()),
-                  "attn_bwd")
+        # dQ (with delta = rowsum(dO*O) inside) then dK/dV: no float atomics, bitwise
+        # reproducible (measured against a fused one-pass form with fp32 dQ atomics and a
+        # two-stream split: profiles/r2/attn_bwd_fused_vs_split.md, profiles/r5/r5au)
+        check(_lib.lib().ra_attn_bwd(ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
+                                     ptr(dqkv), B, T, H, D, ctx.scale, stream_ptr()),
+              "attn_bwd")
         return dqkv, None
 
 
@@ -819,106 +636,25 @@ class _CrossEntropy(torch.autograd.Function):
         return dl.view(ctx.shape), None, None, None
 
 
-_xent_streams: dict = {}
-
-# Multi-chunk LM head: the three GEMMs per chunk stay in order on the current stream and
-# each chunk's softmax-xent pass runs on its own stream beside the next GEMMs (no speed
-# difference against putting the dW GEMMs on the wgrad side stream, profiles/r3/
-# lmhead_pipe.md). The side-stream-dW layout was REMOVED in round 4: it ran two torch
-# hipBLASLt GEMMs concurrently on two streams and hung the GPU on a ragged last chunk
-# (N = 12388, chunk 4096). Root cause (profiles/r4/README.md §2, repro arms in
-# scripts/lmhead_hang_repro.py): two streams issuing stream-K hipBLASLt GEMMs concurrently
-# through ONE hipBLASLt handle — torch uses one handle for all its GEMMs, and ops/lt with a
-# single handle hung the same way even with per-stream workspaces, while a stream-K dW on a
-# side stream through a different handle drained. Side-stream GEMMs therefore only go
-# through ops/lt, which keeps a hipBLASLt handle and a workspace per stream.
-def _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp, ignore_index,
-                       side_dw=False):
-    """Chunked LM head + CE, software-pipelined over two streams:
-
-        main:  L0 L1 | dh0 dW0 | L2 | dh1 dW1 | L3 ...      (GEMMs, issue order = data order)
-        xent:     X0 |   X1    |    X2  ...                 (X_i after L_i, before dh_i/dW_i)
-
-    X_{i+1} runs while dh_i / dW_i run. Two logits buffers suffice: L_{i+2} is issued on the
-    main stream after dh_i / dW_i, the last readers of its buffer. With ``side_dw`` every dW_i
-    runs on the weight-gradient side stream instead (after X_i), and L_{i+2} also waits for
-    it; the memory-bound cross-entropy pass (no LDS) shares CUs with the GEMMs, which the
-    one-chunk form cannot overlap with anything."""
-    dev = h2.device
-    N = h2.shape[0]
-    xs = _xent_streams.get(dev)
-    if xs is None:
-        xs = _xent_streams[dev] = torch.cuda.Stream(dev)
-    main = torch.cuda.current_stream(dev)
-    bufs = [torch.empty((ch, Vp), device=dev, dtype=h2.dtype) for _ in range(2)]
-    starts = list(range(0, N, ch))
-    done_x = [None] * len(starts)
-    done_w = [None] * len(starts)
-    side = _side_stream(dev) if side_dw and dw is not None else None
-
-    def logits(i):
-        s0 = starts[i]
-        e = min(N, s0 + ch)
-        lg = bufs[i % 2][: e - s0]
-        if i >= 2 and done_w[i - 2] is not None:
-            main.wait_event(done_w[i - 2])  # dW_{i-2} on the side stream read this buffer
-        torch.mm(h2[s0:e], wt, out=lg)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        xs.wait_event(ev)
-        with torch.cuda.stream(xs):
-            check(L.ra_xent_fused(ptr(lg), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
-                                  e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
-            ex = torch.cuda.Event()
-            ex.record(xs)
-        done_x[i] = ex
-
-    logits(0)
-    for i, s0 in enumerate(starts):
-        e = min(N, s0 + ch)
-        if i + 1 < len(starts):
-            logits(i + 1)
-        main.wait_event(done_x[i])
-        lg = bufs[i % 2][: e - s0]
-        if side is not None:  # dW_i beside dh_i: it needs only X_i
-            side.wait_event(done_x[i])
-            with torch.cuda.stream(side):
-                _lm_head_dw(lg, h2[s0:e], dw, i == 0, side=True)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            done_w[i] = ev
-        if dh is not None:
-            torch.mm(lg, w, out=dh[s0:e])
-        if dw is not None and side is None:
-            _lm_head_dw(lg, h2[s0:e], dw, i == 0)
-    if side is not None:
-        for t_ in bufs + [h2, dw]:
-            t_.record_stream(side)
-
-
-# LM-head weight gradient: "hip" = the wgrad kernel (split count from ra_wgrad_splits: 3
-# at 591 tiles), "lt" = ops/lt's fp32-out hipBLASLt GEMM (per-stream handle), "torch" =
-# torch.addmm (torch's handle: main stream only). RAY_AMD_LMHEAD_DW_SIDE=1 (default): with a
-# flat-gradient sink and one chunk, dW runs on the wgrad side stream, overlapping the
-# transformer backward; its scaled accumulation into the sink stays there and the
-# embedding's backward (the other user of the tied weight's sink) waits on its event.
-_LMHEAD_DW = os.environ.get("RAY_AMD_LMHEAD_DW", "hip")
-_LMHEAD_DW_SIDE = os.environ.get("RAY_AMD_LMHEAD_DW_SIDE", "1") == "1"
-
-
+# LM-head weight gradient: the wgrad kernel (split count from ra_wgrad_splits: 3 at 591
+# tiles); layouts it does not take use an fp32-out hipBLASLt GEMM — ops/lt (a per-stream
+# handle) on the side stream, torch.addmm on the main stream. Two streams issuing stream-K
+# hipBLASLt GEMMs through ONE handle hung the GPU in round 4 (profiles/r4/README.md §2).
+# With a flat-gradient sink and one chunk, dW runs on the wgrad side stream, overlapping
+# the transformer backward (measured equal to or faster than the main stream, r5g / r5am);
+# its scaled accumulation into the sink stays there and the embedding's backward (the
+# other user of the tied weight's sink) waits on its event.
 def _lm_head_dw(lg, h2s, dw, first, side=False):
-    mode = _LMHEAD_DW
-    if mode == "torch" and side:
-        mode = "lt"  # torch's one hipBLASLt handle is never used off the main stream
-    if mode == "hip" and _wgrad_hip_ok(lg, h2s, dw):
+    if _wgrad_hip_ok(lg, h2s, dw):
         wgrad_accumulate(lg, h2s, dw, accumulate=not first)
         return
-    if _WGRAD_LT or mode == "lt" or side:
+    if side:
         from . import lt
 
         lt.wgrad_accum(lg, h2s, dw, beta=0.0 if first else 1.0)
     else:
-        torch.addmm(dw, lg.t(), h2s, out_dtype=torch.float32, out=dw)
+        torch.addmm(dw, lg.t(), h2s, out_dtype=torch.float32, beta=0.0 if first else 1.0,
+                    out=dw)
 
 
 class _LMHeadCrossEntropy(torch.autograd.Function):
@@ -944,40 +680,34 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         loss_rows = torch.empty(N, device=dev, dtype=torch.float32)
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         dh = torch.empty_like(h2) if need_grad else None
-        dw = (torch.empty if _WGRAD_LT else torch.zeros)(
-            w.shape, device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        dw = torch.zeros(w.shape, device=dev, dtype=torch.float32) \
+            if ctx.needs_input_grad[1] else None
         ch = max(1, min(chunk, N))
         L = _lib.lib()
         wt = w.t()
-        ctx.side_dw = False
-        if h.is_cuda and N > ch:
-            side_dw = (dw is not None and _WGRAD_STREAM and _LMHEAD_DW_SIDE
-                       and _grad_sink(w) is not None)
-            _lm_head_pipelined(L, h2, w, wt, t, inv, loss_rows, dh, dw, ch, V, Vp,
-                               ignore_index, side_dw)
-            ctx.side_dw = side_dw
-        else:  # one chunk (the GPT-2 bench: 65536 tokens), or CPU: all on this stream
-            side_dw = (dw is not None and h.is_cuda and N <= ch and _WGRAD_STREAM
-                       and _LMHEAD_DW_SIDE and _grad_sink(w) is not None)
-            lg = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
-            for s0 in range(0, N, ch):
-                e = min(N, s0 + ch)
-                lgc = lg[: e - s0]
-                torch.mm(h2[s0:e], wt, out=lgc)
-                check(L.ra_xent_fused(ptr(lgc), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
-                                      e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
-                if dh is not None:
-                    torch.mm(lgc, w, out=dh[s0:e])
-                if dw is not None and side_dw:
-                    side = _side_stream(dev)
-                    side.wait_stream(torch.cuda.current_stream(dev))
-                    with torch.cuda.stream(side):
-                        _lm_head_dw(lgc, h2[s0:e], dw, True, side=True)
-                    for t_ in (lg, h2, dw):
-                        t_.record_stream(side)
-                elif dw is not None:
-                    _lm_head_dw(lgc, h2[s0:e], dw, s0 == 0)
-            ctx.side_dw = side_dw
+        # chunks in order on this stream (the GPT-2 bench: one 65536-token chunk); with one
+        # chunk, dW goes to the wgrad side stream
+        side_dw = (dw is not None and h.is_cuda and N <= ch and _WGRAD_STREAM
+                   and _grad_sink(w) is not None)
+        lg = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
+        for s0 in range(0, N, ch):
+            e = min(N, s0 + ch)
+            lgc = lg[: e - s0]
+            torch.mm(h2[s0:e], wt, out=lgc)
+            check(L.ra_xent_fused(ptr(lgc), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
+                                  e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
+            if dh is not None:
+                torch.mm(lgc, w, out=dh[s0:e])
+            if dw is not None and side_dw:
+                side = _side_stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    _lm_head_dw(lgc, h2[s0:e], dw, True, side=True)
+                for t_ in (lg, h2, dw):
+                    t_.record_stream(side)
+            elif dw is not None:
+                _lm_head_dw(lgc, h2[s0:e], dw, s0 == 0)
+        ctx.side_dw = side_dw
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w
         return loss_rows.sum() * inv[0]

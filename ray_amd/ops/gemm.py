@@ -26,15 +26,8 @@ _EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "dgelu": 3}
 # Status: correct (tests/test_kernels_gpu.py::test_gemm_nt_matches_fp32) but measured at
 # 0.43-0.77x hipBLASLt on the GPT-2 shapes (profiles/r2/hip_gemm_v*.log), so the model's
 # linear layers stay on hipBLASLt; this module is the API for callers that want the fused
-# epilogues (scripts/hip_gemm_bench.py). RAY_AMD_GEMM_GRID caps the persistent grid.
-GRID_CAP = int(os.environ.get("RAY_AMD_GEMM_GRID", "0"))
-# kernel family: 0 = 8-wave gemm.hip (variants by ra_knobs[5]), 1 = 4-wave gemm4w.hip
-_FOUR_WAVE = os.environ.get("RAY_AMD_GEMM_4W", "0") == "1"
-
-
-def set_four_wave(on: bool):
-    global _FOUR_WAVE
-    _FOUR_WAVE = bool(on)
+# epilogues (scripts/hip_gemm_bench.py). The persistent grid is sized by the kernel.
+GRID_CAP = 0
 
 
 def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -64,9 +57,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none", bias=None, a
         scratch = work[P * N:]
         if db is not None:
             flags = (1 if db.dtype == torch.bfloat16 else 0) | (2 if db_acc else 0)
-    fn = lib().ra_gemm4w_nt if (_FOUR_WAVE and K % 64 == 0 and K >= 128 and N % 8 == 0) \
-        else lib().ra_gemm_nt
-    check(fn(ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0), M, N, K, e,
+    check(lib().ra_gemm_nt(ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0), M, N, K, e,
              ptr(bias), ptr(aux), aux.stride(0) if aux is not None else 0, ptr(colpart), ptr(db),
              ptr(scratch), flags, GRID_CAP, stream_ptr()), "gemm_nt")
     if epi == "bias_gelu":

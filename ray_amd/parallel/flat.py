@@ -324,10 +324,8 @@ class FlatDDP:
 
         def hook(_p):
             # a param can be signalled twice per backward (a direct-accumulating op, then the
-            # AccumulateGrad post-hook which PyTorch also runs for a None grad): count once;
-            # a gradient still queued for a grouped kernel (ops.functional.flush_wgrads)
-            # is counted when that kernel is enqueued, not by the early post-hook
-            if not self.sync or self._seen[i] or getattr(_p, "_ra_grad_pending", False):
+            # AccumulateGrad post-hook which PyTorch also runs for a None grad): count once
+            if not self.sync or self._seen[i]:
                 return
             self._seen[i] = True
             self._ready[b] += 1

@@ -122,17 +122,6 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
             from ray_amd.ops import lt
 
             lt.set_tuning(True)  # fp32-output wgrad GEMMs: ops/lt.py selector
-    if on_gpu and os.environ.get("RAY_AMD_MAIN_PRIO") == "1":
-        # the step on a high-priority stream: its workgroups are dispatched ahead of the
-        # side stream's weight-gradient workgroups when both have work queued
-        torch.cuda.set_stream(torch.cuda.Stream(device, priority=min(
-            torch.cuda.Stream.priority_range())))
-    if on_gpu and os.environ.get("RAY_AMD_MAIN_CUS"):
-        # experiment: the step's main stream on a CU subset disjoint from the side stream's
-        from ray_amd.ops import cu_mask
-
-        torch.cuda.set_stream(cu_mask.masked_stream(
-            device, cu_mask.cu_range(device, os.environ["RAY_AMD_MAIN_CUS"])))
     mcfg = getattr(GPT2Config, c["model"])()
     gdt = torch.float32 if c["grad_dtype"] == "fp32" else torch.bfloat16
     tr = GPT2Trainer(mcfg, c["micro_batch"], c["seq_len"], device, bucket_mb=c["bucket_mb"],
@@ -282,12 +271,7 @@ def run_steps(cfg: dict, device, rank: int, world: int) -> dict:
 
 
 def _wgrad_mode(on_gpu: bool) -> str:
-    if not on_gpu:
-        return "torch"
-    from ray_amd.ops import functional as rf
-
-    return {"lt": "hipblaslt-lt-beta1", "lt-splitk": "splitk-partials-hipblaslt-tuned",
-            "hip": "hip-wgrad-kernel"}.get(rf._WGRAD, "splitk-partials-torch-bmm")
+    return "hip-wgrad-kernel" if on_gpu else "torch"
 
 
 def train_func(config: dict):

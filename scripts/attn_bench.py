@@ -30,12 +30,7 @@ def main():
     ap.add_argument("--B", type=int, default=16)
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--H", type=int, default=12)
-    ap.add_argument("--knob6", type=int, default=0, help="fused-bwd diagnostics")
     a = ap.parse_args()
-    if a.knob6:
-        from ray_amd.ops import _lib
-
-        _lib.lib().ra_set_knob(6, a.knob6)
     B, T, H, D = a.B, a.T, a.H, 64
     dev = "cuda"
     qkv = torch.randn(B, T, 3, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Nature-CNN conv layers at the PPO learner minibatch (B=500): MFMA kernels (ops/csrc/conv.hip)
-vs MIOpen NHWC, forward and weight gradient, with optional knob sweeps.
+vs MIOpen NHWC, forward and weight gradient.
 
-    python scripts/conv_bench.py [--fwd-caps 256,512,1024] [--wg-rows 256,512]
+    python scripts/conv_bench.py
 """
 import argparse
 import json
@@ -37,8 +37,6 @@ def timeit(fn, iters=50):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=500)
-    ap.add_argument("--fwd-caps", default="512")
-    ap.add_argument("--wg-rows", default="512")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda")
@@ -63,20 +61,13 @@ def main():
         dw = torch.empty(O, K, K, C, device=dev, dtype=torch.bfloat16)
         xh = xin if u8 else xin.permute(0, 2, 3, 1)
         rec = {"layer": name, "B": B}
-        for cap in [int(v) for v in a.fwd_caps.split(",")]:
-            L.ra_set_knob(4, cap)
-            rec[f"fwd_us_cap{cap}"] = round(timeit(lambda: check(L.ra_conv_fwd(
-                ptr(xh), ptr(idx), int(u8), ptr(w), ptr(b), ptr(y), B, HW, HW, C, K, K, S, O,
-                1 / 255.0, 1, stream_ptr()), "fwd")), 2)
-        L.ra_set_knob(4, 0)
-        for rows in [int(v) for v in a.wg_rows.split(",")]:
-            L.ra_set_knob(7, rows)
-            # partial-slab size depends on the rows knob: size it AFTER setting the knob
-            work = torch.empty(L.ra_conv_wgrad_work(B, HW, HW, C, K, K, S, O), device=dev)
-            rec[f"wgrad_us_rows{rows}"] = round(timeit(lambda: check(L.ra_conv_wgrad(
-                ptr(xh), ptr(idx), int(u8), ptr(dy), ptr(work), work.numel(), ptr(dw), 0, B, HW, HW, C, K, K,
-                S, O, 1 / 255.0, stream_ptr()), "wgrad")), 2)
-        L.ra_set_knob(7, 0)
+        rec["fwd_us"] = round(timeit(lambda: check(L.ra_conv_fwd(
+            ptr(xh), ptr(idx), int(u8), ptr(w), ptr(b), ptr(y), B, HW, HW, C, K, K, S, O,
+            1 / 255.0, 1, stream_ptr()), "fwd")), 2)
+        work = torch.empty(L.ra_conv_wgrad_work(B, HW, HW, C, K, K, S, O), device=dev)
+        rec["wgrad_us"] = round(timeit(lambda: check(L.ra_conv_wgrad(
+            ptr(xh), ptr(idx), int(u8), ptr(dy), ptr(work), work.numel(), ptr(dw), 0, B, HW, HW,
+            C, K, K, S, O, 1 / 255.0, stream_ptr()), "wgrad")), 2)
         dyc = dy.permute(0, 3, 1, 2)
         rec["miopen_fwd_us"] = round(timeit(lambda: torch.nn.functional.conv2d(xb, w, b, S)), 2)
         rec["miopen_wgrad_us"] = round(timeit(lambda: torch.ops.aten.convolution_backward(

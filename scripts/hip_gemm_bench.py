@@ -48,7 +48,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--no-epi", action="store_true")
-    ap.add_argument("--variant", type=int, default=-1, help="time only this kernel variant")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -63,26 +62,14 @@ def main():
         err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
         del ref
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        t_hip, t_v1, t_lt = [], [], []
-        lib().ra_set_knob(5, 1)
-        o1 = gemm.gemm_nt(a, b)
-        lib().ra_set_knob(5, 0)
-        torch.cuda.synchronize()
-        assert torch.equal(o1, out), "variants disagree"
-        if args.variant >= 0:
-            lib().ra_set_knob(5, args.variant)
-            print(name, timeit(lambda: gemm.gemm_nt(a, b, out=c), args.iters), flush=True)
-            continue
+        t_hip, t_lt = [], []
         for _ in range(args.rounds):
             t_hip.append(timeit(lambda: gemm.gemm_nt(a, b, out=c), args.iters))
-            lib().ra_set_knob(5, 1)
-            t_v1.append(timeit(lambda: gemm.gemm_nt(a, b, out=c), args.iters))
-            lib().ra_set_knob(5, 0)
             t_lt.append(timeit(lambda: torch.mm(a, b.t(), out=c), args.iters))
         fl = 2.0 * M * N * K
         th, tl = min(t_hip), min(t_lt)
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "max_rel_err": round(err, 5),
-                          "hip_ms": round(th, 4), "hip_bk64x2_ms": round(min(t_v1), 4), "torch_ms": round(tl, 4),
+                          "hip_ms": round(th, 4), "torch_ms": round(tl, 4),
                           "hip_tflops": round(fl / th / 1e9, 1),
                           "torch_tflops": round(fl / tl / 1e9, 1),
                           "speedup": round(tl / th, 3)}), flush=True)
