@@ -270,10 +270,6 @@ def bias_residual(h, bias, res):
 # handle on the side stream) summed into the sink by one HIP pass.
 # RAY_AMD_WGRAD_STREAM=1 (default): weight gradients run on a side stream
 _WGRAD_STREAM = os.environ.get("RAY_AMD_WGRAD_STREAM", "1") == "1"
-# RAY_AMD_CONV_DGRAD=0: conv input gradients on MIOpen instead of conv.hip
-_CONV_DGRAD = os.environ.get("RAY_AMD_CONV_DGRAD", "1") == "1"
-# RAY_AMD_CONV_WGRAD_STREAM=1: the same for the conv weight-gradient kernels
-_CONV_WGRAD_STREAM = os.environ.get("RAY_AMD_CONV_WGRAD_STREAM", "0") == "1"
 
 # fallback split-K: at most 16 token slices of >= 2048 tokens, <= 4 GiB of fp32 partials
 # (profiles/r2_perf_bench.log: S = 16 fastest for every GPT-2 projection on hipBLASLt)
@@ -1199,25 +1195,15 @@ class _ConvBiasReLU(torch.autograd.Function):
                                   work.numel(), ptr(dw), flags, B, H, W, C, KH, KW, S, O, scale,
                                   stream_ptr()), "conv_wgrad")
 
-        if sink is not None and _CONV_WGRAD_STREAM:
-            # opt-in: the weight gradient (into the flat buffer) overlaps the input-gradient
-            # chain on the main stream; consumers join through join_side_streams(). Measured
-            # slower inside the PPO learner's HIP graph (46.3 vs 41.3 ms/update), so off
-            side = _side_stream(dy.device)
-            side.wait_stream(torch.cuda.current_stream(dy.device))
-            with torch.cuda.stream(side):
-                wgrad()
-            for t in (dh, work, x, idx):
-                if t is not None:
-                    t.record_stream(side)
-        else:
-            wgrad()
+        # on the main stream: a side-stream conv wgrad measured slower inside the PPO
+        # learner's HIP graph (46.3 vs 41.3 ms/update)
+        wgrad()
         if sink is not None:
             _grad_done(ctx.weight)
             dw = None
         dx = None
         if not u8 and ctx.needs_input_grad[0]:
-            if _CONV_DGRAD and L.ra_conv_dgrad_supported(KH, KW, C, S, O):
+            if L.ra_conv_dgrad_supported(KH, KW, C, S, O):
                 dxh = torch.empty((B, H, W, C), device=dy.device, dtype=torch.bfloat16)
                 check(L.ra_conv_dgrad(ptr(_nhwc_rows(dh)), ptr(w), ptr(dxh), B, H, W, C, KH, KW,
                                       S, O, stream_ptr()), "conv_dgrad")

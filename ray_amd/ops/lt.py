@@ -12,9 +12,6 @@ hipBLASLt's heuristic candidates:
     its first use (into a scratch buffer) and records the winner; ``save()`` writes the
     file. Without a recorded choice and without tuning, the first heuristic candidate
     runs (hipBLASLt's own pick).
-  * ``RAY_AMD_LT_NO_STREAMK=1`` restricts the choice to non-stream-K solutions (on gfx950
-    every hipBLASLt bf16 kernel is built with StreamK=3, so this usually leaves none and
-    the plan keeps its stream-K candidates; gemm_lt.hip).
 """
 
 from __future__ import annotations
@@ -36,11 +33,6 @@ _choices: dict | None = None  # key str -> (choice, ms)
 _applied: set = set()
 _tuning = os.environ.get("RAY_AMD_LT_TUNE", "0") == "1"
 _file = os.environ.get("RAY_AMD_LT_FILE", DEFAULT_FILE)
-
-
-def _init_streamk_policy():
-    if os.environ.get("RAY_AMD_LT_NO_STREAMK", "0") == "1":
-        _lib.lib().ra_lt_allow_streamk(0)
 
 
 def set_tuning(on: bool, path: str | None = None):
@@ -113,8 +105,6 @@ def _select(ta, tb, m, n, k, A, lda, B, ldb, ldc, dev, batch=1, sa=0, sb=0, sc=0
         if key in _applied:
             return
         L = _lib.lib()
-        if not _applied:
-            _init_streamk_policy()
         nc = L.ra_lt_num_cands_batched(*shape, *bshape)
         if nc <= 0:
             raise RuntimeError(f"hipBLASLt has no solution for {key}")

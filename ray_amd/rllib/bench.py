@@ -31,6 +31,15 @@ def _envs_per_runner() -> int:
     return int(os.environ.get("RAY_AMD_RUNNER_ENVS", "5"))
 
 
+def _inference_where(runner_gpus: float) -> str:
+    """Where the env runners' policy forward runs (reported in the JSON line)."""
+    if runner_gpus <= 0:
+        return "cpu (bf16 Nature-CNN, torch)"
+    if os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1":
+        return "gpu (one HIP graph per step: conv.hip MFMA convs, Gumbel-max draw)"
+    return "gpu (eager)"
+
+
 def bench_ppo(args):
     import ray_amd as ray
     from ray_amd.rllib.algorithms import PPOConfig
@@ -83,6 +92,7 @@ def bench_ppo(args):
                    "minibatch_size": 500, "num_epochs": 10,
                    "parallelism": f"{n_gpus} learner{'s' if n_gpus > 1 else ''}",
                    "env_runner_gpus": runner_gpus, "env_runner_cpus": runner_cpus,
+                   "env_runner_inference": _inference_where(runner_gpus),
                    "sample_async": sample_async},
         "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
                                                      "sample_time_s", "sample_wait_s",

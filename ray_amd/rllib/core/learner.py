@@ -1243,7 +1243,6 @@ class Learner(TorchLearner):
             m = self.module
             # the fused heads kernel needs a shared encoder and bf16 heads on the GPU
             fused_heads = (m.vf_encoder is None and self.amp
-                           and os.environ.get("RAY_AMD_PPO_FUSED_HEADS", "1") == "1"
                            and m.pi.weight.dtype == torch.bfloat16
                            and m.encoder.out_dim % 8 == 0 and m.encoder.out_dim <= 1024
                            and m.pi.weight.shape[0] <= 18)
@@ -1278,8 +1277,6 @@ class Learner(TorchLearner):
                 src_ = [x for x in gs if x is not None]
                 if dst:
                     torch._foreach_copy_(dst, src_)
-                if rf._CONV_WGRAD_STREAM:
-                    rf.join_side_streams()  # conv weight gradients ran on the side stream
         else:
             obs, old_di, acts, old_logp, adv, vtarg = bufs
 

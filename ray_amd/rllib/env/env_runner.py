@@ -10,6 +10,7 @@ cut)."""
 
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -138,6 +139,12 @@ class SingleAgentEnvRunner:
                            for k, v in init.items()}
             self._state0 = {k: np.asarray(v, np.float32) for k, v in init.items()}
         self.device = torch.device("cpu")
+        if config.get("num_gpus_per_env_runner") and worker_index > 0 and \
+                not torch.cuda.is_initialized():
+            # a runner process drives one stream: cap its HIP hardware queues before the
+            # runtime starts (8 runners x 8 queues beside the learner oversubscribe the
+            # queue slots, and oversubscribed queues are time-sliced)
+            os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RAY_AMD_RUNNER_HW_QUEUES", "1")
         if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
             self.device = torch.device("cuda", 0)
             self.module.to(self.device)
@@ -155,6 +162,13 @@ class SingleAgentEnvRunner:
                           and config.get("env_runner_bf16", config.get("learner_bf16", True)))
         if self._cpu_bf16:
             self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
+        # GPU discrete policies: the whole inference step as one HIP graph (gpu_policy.py)
+        self._graphed = (self.device.type == "cuda" and self.module_kind == "pg"
+                         and not self._stateful and hasattr(self.action_space, "n")
+                         and os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1")
+        self._gpol = None
+        self._act_rng = np.random.default_rng(
+            None if seed is None else seed * 7919 + worker_index)
         self.obs = []
         for i, e in enumerate(self.envs):
             o, _ = e.reset(seed=None if seed is None else seed * 1000 + worker_index * 100 + i)
@@ -279,7 +293,8 @@ class SingleAgentEnvRunner:
                     if not self._eps[i].observations:
                         self._eps[i].add_env_reset(rec[i])
             with torch.no_grad():
-                x = torch.from_numpy(np.ascontiguousarray(ob)).to(self.device)
+                x = None if (self._graphed and not self._stateful) else \
+                    torch.from_numpy(np.ascontiguousarray(ob)).to(self.device)
                 if self.module_kind == "q":
                     q = self.module(x)
                     a = q.argmax(-1).cpu().numpy()
@@ -299,21 +314,37 @@ class SingleAgentEnvRunner:
                         out = self.module.forward_inference(x, state=st)
                         self._state = {k: v.float().cpu().numpy()
                                        for k, v in out["state_out"].items()}
+                    elif self._graphed:
+                        out = None
                     else:
                         out = self.module.forward_inference(x)
-                    di = out["action_dist_inputs"].float()
-                    at, lpt = self.module.sample_actions(di, explore)
-                    if dist_in is None:
-                        dist_in = np.zeros((cap, B, di.shape[-1]), np.float32)
-                    if discrete and di.is_cuda:  # one device->host copy per step
-                        h = torch.cat([at.float()[:, None], lpt[:, None], di], 1).cpu().numpy()
-                        a = h[:, 0].astype(np.int64)
-                        lp = h[:, 1]
-                        dist_in[t] = h[:, 2:]
+                    if out is None:
+                        if self._gpol is None or self._gpol.obs_shape != ob.shape:
+                            from ray_amd.rllib.env.gpu_policy import GraphedDiscretePolicy
+
+                            self._gpol = GraphedDiscretePolicy(self.module, ob,
+                                                               self.action_space.n,
+                                                               self.device)
+                        a, lp, d = self._gpol.step(ob, explore, self._act_rng)
+                        if dist_in is None:
+                            dist_in = np.zeros((cap, B, d.shape[-1]), np.float32)
+                        dist_in[t] = d
+                        lp = lp.copy()
                     else:
-                        a = at.cpu().numpy()
-                        lp = lpt.cpu().numpy()
-                        dist_in[t] = di.cpu().numpy()
+                        di = out["action_dist_inputs"].float()
+                        at, lpt = self.module.sample_actions(di, explore)
+                        if dist_in is None:
+                            dist_in = np.zeros((cap, B, di.shape[-1]), np.float32)
+                        if discrete and di.is_cuda:  # one device->host copy per step
+                            h = torch.cat([at.float()[:, None], lpt[:, None], di],
+                                          1).cpu().numpy()
+                            a = h[:, 0].astype(np.int64)
+                            lp = h[:, 1]
+                            dist_in[t] = h[:, 2:]
+                        else:
+                            a = at.cpu().numpy()
+                            lp = lpt.cpu().numpy()
+                            dist_in[t] = di.cpu().numpy()
             act_buf[t] = a
             logp[t] = lp
             a_env = a
