@@ -475,6 +475,13 @@ class CoreWorker:
                 del self.conns[addr]
         if addr == self.raylet_addr:
             if not self._stopped and self.mode == "worker":
+                if getattr(self, "_reattaching", False):
+                    return  # the re-attach loop sees its call fail and reconnects
+                if self._can_reattach():
+                    self._reattaching = True
+                    threading.Thread(target=self._reattach_loop, name="ray_amd-reattach",
+                                     daemon=True).start()
+                    return
                 os._exit(1)
             return
         # fail outstanding RPCs to that peer
@@ -496,6 +503,42 @@ class CoreWorker:
         for ac in list(self.actors.values()):
             if ac.addr == addr and ac.state == P.ALIVE:
                 self._on_actor_conn_lost(ac)
+
+    def _can_reattach(self) -> bool:
+        """An actor worker on a node other than the head's outlives a head restart when the
+        head persists its tables (the restarted head awaits re-attachment)."""
+        return (self.actor_id is not None and bool(os.environ.get("RAY_AMD_GCS_STORAGE_PATH"))
+                and self.node_hex != (self.cluster_info or {}).get("head_node_id"))
+
+    def _reattach_loop(self):
+        """Reconnect to the restarted head on its socket, register again and re-attach this
+        actor (reference: core_worker.cc re-subscribing after a GCS restart). Gives up —
+        the process exits as before — after RAY_AMD_HEAD_RECONNECT_S or when the head has
+        re-created or dropped the actor."""
+        deadline = time.monotonic() + float(os.environ.get("RAY_AMD_HEAD_RECONNECT_S", "30"))
+        while time.monotonic() < deadline and not self._stopped:
+            c = self.io.connect_unix(self.raylet_addr, 200)
+            if c < 0:
+                continue
+            with self.lock:
+                self.conns[self.raylet_addr] = c
+                self.conn_addr[c] = self.raylet_addr
+            self.io.send(c, _dumps((P.HELLO, self.addr, self.worker_id)))
+            while time.monotonic() < deadline:
+                try:
+                    self.call_raylet("register", "worker", self.worker_id, os.getpid(),
+                                     self.addr, self.job_id, self._ns, None, self.node_hex,
+                                     timeout=5)
+                    ok = self.call_raylet("reattach_actor", self.actor_id, timeout=5)
+                except Exception:  # noqa: BLE001 - the head went away again: reconnect
+                    break
+                if ok is True:
+                    self._reattaching = False
+                    return
+                if ok != "retry":
+                    os._exit(1)
+                time.sleep(0.2)
+        os._exit(1)
 
     def _on_push(self, conn, msg):
         _, topic, data = msg

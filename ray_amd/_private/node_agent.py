@@ -14,7 +14,11 @@ which
     secondary, evictable copy into its own node's store) and frees primaries on the
     owner's request (``free_objects``);
   * dies with its head connection and takes its workers with it, which is how the
-    head observes a node failure.
+    head observes a node failure — unless the head persists its tables
+    (RAY_AMD_GCS_STORAGE_PATH): then a lost head is taken to be restarting, and the agent
+    keeps its store and workers and re-registers with the new head on the same socket
+    (reference: raylet NodeManager::HandleNotifyGCSRestart), giving up after
+    RAY_AMD_HEAD_RECONNECT_S (default 30 s). Its actor workers re-attach themselves.
 """
 
 from __future__ import annotations
@@ -61,18 +65,42 @@ class NodeAgent:
         self.labels = json.loads(args.labels or "{}")
         self.procs: dict[int, subprocess.Popen] = {}
         self.stop = False
+        self.head_address = args.head_address
         self.head_conn = self.io.connect_unix(args.head_address, 30000)
         if self.head_conn < 0:
             raise ConnectionError(f"cannot reach head raylet at {args.head_address}")
-        self.io.send(self.head_conn, _dumps((P.HELLO, self.addr, self.node_id)))
-        self.io.send(self.head_conn, _dumps((P.REQ, 1, "register_node", (
-            self.node_hex, self.total, self.labels, self.addr, self.store_path,
-            self.spill_dir, os.getpid(), self.num_cpus))))
         self.registered = False
+        self._register()
+        self.reconnect_s = float(os.environ.get("RAY_AMD_HEAD_RECONNECT_S", "30")) \
+            if os.environ.get("RAY_AMD_GCS_STORAGE_PATH") else 0.0
+        self._head_lost_at = None
         from ray_amd._private.reporter import NodeReporter
 
         self.reporter = NodeReporter(self.node_hex, self.session_dir).start()
         self._last_report = 0.0
+
+    def _register(self):
+        self.io.send(self.head_conn, _dumps((P.HELLO, self.addr, self.node_id)))
+        self.io.send(self.head_conn, _dumps((P.REQ, 1, "register_node", (
+            self.node_hex, self.total, self.labels, self.addr, self.store_path,
+            self.spill_dir, os.getpid(), self.num_cpus))))
+
+    def _try_reconnect(self, now):
+        """Head lost with GCS persistence on: retry its socket until the deadline."""
+        if now - self._head_lost_at > self.reconnect_s:
+            print(f"[ray_amd] node {self.node_hex[:12]}: head did not come back in "
+                  f"{self.reconnect_s:.0f}s; exiting", file=sys.stderr, flush=True)
+            self.stop = True
+            return
+        c = self.io.connect_unix(self.head_address, 200)
+        if c < 0:
+            return
+        self.head_conn = c
+        self.registered = False
+        self._head_lost_at = None
+        self._register()
+        print(f"[ray_amd] node {self.node_hex[:12]}: re-registered with the restarted head",
+              file=sys.stderr, flush=True)
 
     def reply(self, conn, rid, ok, value):
         if rid:
@@ -95,10 +123,18 @@ class NodeAgent:
                         elif msg[0] == P.RESP and msg[1] == 1:
                             self.registered = bool(msg[2])
                     elif typ == 2 and conn == self.head_conn:
-                        self.stop = True
+                        if self.reconnect_s > 0:
+                            self.head_conn = None
+                            self.registered = False
+                            self._head_lost_at = time.monotonic()
+                        else:
+                            self.stop = True
                 except Exception:
                     traceback.print_exc()
             now = time.monotonic()
+            if self.head_conn is None and not self.stop:
+                self._try_reconnect(now)
+                continue
             if self.registered and now - self._last_report >= self.reporter.interval_s:
                 self._last_report = now
                 sample = self.reporter.latest()

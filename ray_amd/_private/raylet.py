@@ -309,6 +309,11 @@ class Raylet:
         self._gcs_saved = 0.0
         self._gcs_writer = None
         self.gcs_restored = None
+        # detached actors of the previous head that lived on OTHER nodes: their workers may
+        # survive the head restart and re-attach (rpc_reattach_actor) within the grace
+        # period; the ones that do not are re-created from their specs afterwards
+        self._readopt: dict = {}
+        self._readopt_grace = float(os.environ.get("RAY_AMD_GCS_READOPT_S", "5"))
         if self._gcs_path:
             os.makedirs(self._gcs_path, exist_ok=True)
             self._gcs_restore()
@@ -931,7 +936,9 @@ class Raylet:
     def _gcs_snapshot(self):
         """A copy of the durable tables, taken on the loop thread (values the loop mutates
         later — job records — are copied; KV values are immutable bytes)."""
-        actors = [{"info": a.info, "spec": a.spec, "restarts": a.restarts}
+        actors = [{"info": a.info, "spec": a.spec, "restarts": a.restarts,
+                   "node": a.worker.node if a.worker is not None else
+                   getattr(a, "readopt_node", None)}
                   for a in self.actors.values()
                   if a.info.get("lifetime") == "detached" and a.state != P.DEAD]
         pgs = [{"pg_id": pg.pg_id, "bundles": pg.bundles, "strategy": pg.strategy,
@@ -941,7 +948,7 @@ class Raylet:
         return {"version": 1, "kv": dict(self.kv),
                 "jobs": {k: dict(v) for k, v in self.jobs.items()},
                 "job_counter": self.job_counter, "actors": actors, "pgs": pgs,
-                "saved_at": time.time()}
+                "head": self.node_hex, "saved_at": time.time()}
 
     def _gcs_write(self, snap):
         import pickle
@@ -1004,23 +1011,90 @@ class Raylet:
             a = ActorRec(d["info"], d["spec"])
             a.restarts = int(d.get("restarts") or 0)
             self.actors[a.aid] = a
-            # the head restart killed the actor's process: that is a restart like any
-            # other, so an actor that has used its max_restarts stays dead
-            if a.max_restarts != -1 and a.restarts >= a.max_restarts:
-                a.state = P.DEAD
-                a.death = ("The actor died with the head node and has no restarts left "
-                           f"(max_restarts={a.max_restarts}).")
-                a.end_time = now
+            node = d.get("node")
+            if node and node != st.get("head") and self._readopt_grace > 0:
+                # it ran on a worker node, whose agent and workers may outlive the head:
+                # wait for its worker to re-attach before re-creating it
+                a.state = P.RESTARTING
+                a.readopt_node = node
+                self._readopt[a.aid] = (a, time.monotonic() + self._readopt_grace)
+                if a.info.get("name"):
+                    self.named[(a.info.get("namespace"), a.info["name"])] = a.aid
                 continue
-            a.restarts += 1
-            a.state = P.RESTARTING
-            if a.info.get("name"):
-                self.named[(a.info.get("namespace"), a.info["name"])] = a.aid
-            self._schedule_actor(a)
+            self._restart_restored(a, now)
         self.gcs_restored = {"kv": len(st.get("kv") or {}), "jobs": len(st.get("jobs") or {}),
                              "actors": len(st.get("actors") or []),
-                             "pgs": len(st.get("pgs") or [])}
+                             "pgs": len(st.get("pgs") or []),
+                             "awaiting_reattach": len(self._readopt)}
         self._gcs_dirty = True
+
+    def _restart_restored(self, a, now):
+        """A restored detached actor whose process died with the previous head (or did not
+        re-attach in time): re-create it if it has restarts left (the head restart killed
+        the actor's process: that is a restart like any other, so an actor that has used
+        its max_restarts stays dead)."""
+        if a.max_restarts != -1 and a.restarts >= a.max_restarts:
+            a.state = P.DEAD
+            a.death = ("The actor died with the head node and has no restarts left "
+                       f"(max_restarts={a.max_restarts}).")
+            a.end_time = now
+            return
+        a.restarts += 1
+        a.state = P.RESTARTING
+        if a.info.get("name"):
+            self.named[(a.info.get("namespace"), a.info["name"])] = a.aid
+        self._schedule_actor(a)
+        self._gcs_dirty = True
+
+    def rpc_reattach_actor(self, conn, rid, aid):
+        """A surviving worker re-attaches its actor to this (restarted) head (reference:
+        raylet NodeManager::HandleNotifyGCSRestart → workers re-subscribe; the GCS actor
+        table keeps the actor ALIVE at its address). The worker registered on this
+        connection first; its node agent must have re-registered too. Replies True
+        (adopted), "retry" (its node is not back yet) or False (exit: the actor was
+        re-created, removed or was never durable)."""
+        w = self.conn_worker.get(conn)
+        ent = self._readopt.get(aid)
+        a = ent[0] if ent else None
+        if w is None or a is None or a.worker is not None or a.state == P.DEAD:
+            self.reply(conn, rid, True, False)
+            return
+        rec = self.node_recs.get(w.node)
+        if rec is None or not rec["alive"] or w.node == self.node_hex:
+            self.reply(conn, rid, True, "retry")
+            return
+        res = {k: float(v) for k, v in (a.spec.get("resources") or {}).items()}
+        alloc = self.sched.allocate(w.node, res)
+        if alloc is None:
+            self.reply(conn, rid, True, False)
+            return
+        lid = self.next_lease
+        self.next_lease += 1
+        lease = Lease(lid, w, alloc, res, self.addr, a.spec.get("strategy"),
+                      a.max_restarts != 0)
+        lease.actor_id = aid
+        self.leases[lid] = lease
+        w.state = "actor"
+        w.lease = lease
+        w.actor_id = aid
+        w.job = a.spec.get("job")
+        a.worker, a.lease, a.pid = w, lease, w.pid
+        a.state = P.ALIVE
+        self._readopt.pop(aid, None)
+        self._publish(a)
+        self._gcs_dirty = True
+        self.dirty = True
+        print(f"[ray_amd] actor {a.info.get('class_name')} re-attached from node "
+              f"{w.node[:12]} (pid {w.pid})", file=sys.stderr, flush=True)
+        self.reply(conn, rid, True, True)
+
+    def _readopt_expired(self, now_m):
+        for aid, (a, deadline) in list(self._readopt.items()):
+            if a.worker is not None or a.state == P.DEAD:
+                self._readopt.pop(aid, None)
+            elif now_m > deadline:
+                self._readopt.pop(aid, None)
+                self._restart_restored(a, time.time())
 
     def rpc_gcs_status(self, conn, rid):
         self.reply(conn, rid, True, {"storage_path": self._gcs_path,
@@ -1028,6 +1102,8 @@ class Raylet:
 
     def tick(self):
         now = time.monotonic()
+        if self._readopt:
+            self._readopt_expired(now)
         if self._gcs_path and self._gcs_dirty and now - self._gcs_saved > 0.2:
             self._gcs_save()
         self._memory_check(now)
@@ -1150,6 +1226,8 @@ class Raylet:
             self._kill_worker(w)
             return
         a.state = P.ALIVE
+        if a.info.get("lifetime") == "detached":
+            self._gcs_dirty = True  # its node goes into the snapshot (re-attach on restart)
         self._publish(a)
 
     def _publish(self, a):

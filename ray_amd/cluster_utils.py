@@ -94,8 +94,9 @@ class Cluster:
                     labels=labels or {}, object_store_memory=object_store_memory)
         if self.head_node is None:
             self.session_dir = _W.new_session_dir()
-            proc, addr = _W._start_raylet(self.session_dir, num_cpus, num_gpus, resources,
-                                          int(object_store_memory), labels)
+            self._head_start = (num_cpus, num_gpus, resources, int(object_store_memory),
+                                labels)
+            proc, addr = _W._start_raylet(self.session_dir, *self._head_start)
             with open(os.path.join(self.session_dir, "raylet.ready")) as f:
                 nid = json.load(f)["node_id"]
             self.head_node = Node(proc, nid, addr, True, args)
@@ -173,6 +174,28 @@ class Cluster:
             if ids is None or node.node_id not in ids:
                 return
             time.sleep(0.05)
+
+    def restart_head(self, timeout: float = 60):
+        """Kill the head raylet (SIGKILL: a crash, no goodbye to the node agents) and start
+        a new one on the same session and socket. With RAY_AMD_GCS_STORAGE_PATH the new
+        head reloads the persisted tables, the worker-node agents re-register and their
+        detached actors re-attach with their state (reference: GCS fault tolerance tests'
+        kill_gcs_server / restart_gcs_server). The driver is disconnected first; connect
+        again with ``ray_amd.init(address=cluster.address)``."""
+        if self.connected and ray_amd.is_initialized():
+            ray_amd.shutdown()
+        self.connected = False
+        old = self.head_node
+        old.kill(graceful=False)
+        try:
+            os.unlink(os.path.join(self.session_dir, "raylet.ready"))
+        except FileNotFoundError:
+            pass
+        proc, addr = _W._start_raylet(self.session_dir, *self._head_start)
+        with open(os.path.join(self.session_dir, "raylet.ready")) as f:
+            nid = json.load(f)["node_id"]
+        self.head_node = Node(proc, nid, addr, True, old.node_args)
+        return self.head_node
 
     def list_all_nodes(self):
         nodes = list(self.worker_nodes)

@@ -138,6 +138,7 @@ class SingleAgentEnvRunner:
             self._state = {k: np.repeat(np.asarray(v, np.float32)[None], n, 0)
                            for k, v in init.items()}
             self._state0 = {k: np.asarray(v, np.float32) for k, v in init.items()}
+        ac_module = self.module_kind in ("actor_critic", "pg")  # PPO / IMPALA / APPO / A2C
         self.device = torch.device("cpu")
         if config.get("num_gpus_per_env_runner") and worker_index > 0 and \
                 not torch.cuda.is_initialized():
@@ -148,7 +149,7 @@ class SingleAgentEnvRunner:
         if config.get("num_gpus_per_env_runner") and torch.cuda.is_available():
             self.device = torch.device("cuda", 0)
             self.module.to(self.device)
-            if self.module_kind == "pg" and getattr(self.module, "is_image", False):
+            if ac_module and getattr(self.module, "is_image", False):
                 # bf16 channels-last weights: the conv encoder runs on the MFMA kernels and
                 # reads the uint8 frames directly (weights arrive fp32, cast on load)
                 self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
@@ -157,13 +158,13 @@ class SingleAgentEnvRunner:
         # Nature-CNN step on the MI355X host (EPYC 9575F, scripts/cpu_infer_bf16_bench.py):
         # fp32 0.68 ms, bf16 autocast 0.52 ms, bf16 weights 0.39 ms. fp32 with
         # env_runner_bf16=False. Synced fp32 weights are cast on load (load_state_dict).
-        self._cpu_bf16 = (self.device.type == "cpu" and self.module_kind == "pg"
+        self._cpu_bf16 = (self.device.type == "cpu" and ac_module
                           and getattr(self.module, "is_image", False)
                           and config.get("env_runner_bf16", config.get("learner_bf16", True)))
         if self._cpu_bf16:
             self.module.to(torch.bfloat16).to(memory_format=torch.channels_last)
         # GPU discrete policies: the whole inference step as one HIP graph (gpu_policy.py)
-        self._graphed = (self.device.type == "cuda" and self.module_kind == "pg"
+        self._graphed = (self.device.type == "cuda" and ac_module
                          and not self._stateful and hasattr(self.action_space, "n")
                          and os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1")
         self._gpol = None

@@ -23,4 +23,7 @@ run ppo_gpu_async RAY_AMD_RUNNER_GPUS=0.125 RAY_AMD_PPO_ASYNC=1
 run ppo_gpu_sync RAY_AMD_RUNNER_GPUS=0.125
 run ppo_cpu_async RAY_AMD_PPO_ASYNC=1
 run ppo_cpu_sync RAY_AMD_X=0
+
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python bench.py --no-ray --steps 8 --warmup 3 > $O/prof.log 2>&1 || { echo "prof failed"; tail -5 $O/prof.log; exit 1; }
+echo "prof ok"
 exit 0
