@@ -636,7 +636,7 @@ class _CrossEntropy(torch.autograd.Function):
 # tiles); layouts it does not take use an fp32-out hipBLASLt GEMM — ops/lt (a per-stream
 # handle) on the side stream, torch.addmm on the main stream. Two streams issuing stream-K
 # hipBLASLt GEMMs through ONE handle hung the GPU in round 4 (profiles/r4/README.md §2).
-# With a flat-gradient sink and one chunk, dW runs on the wgrad side stream, overlapping
+# With a flat-gradient sink, dW runs once over all tokens on the wgrad side stream, overlapping
 # the transformer backward (measured equal to or faster than the main stream, r5g / r5am);
 # its scaled accumulation into the sink stays there and the embedding's backward (the
 # other user of the tied weight's sink) waits on its event.
@@ -681,28 +681,32 @@ class _LMHeadCrossEntropy(torch.autograd.Function):
         ch = max(1, min(chunk, N))
         L = _lib.lib()
         wt = w.t()
-        # chunks in order on this stream (the GPT-2 bench: one 65536-token chunk); with one
-        # chunk, dW goes to the wgrad side stream
-        side_dw = (dw is not None and h.is_cuda and N <= ch and _WGRAD_STREAM
+        # Token chunks in order on this stream: logits GEMM -> in-place cross-entropy ->
+        # dh GEMM, each chunk's logits small enough to stay in the Infinity Cache between
+        # the three passes when chunk is small. With a flat-gradient sink the dlogits of
+        # all chunks are kept ([N, Vp]) and dW runs ONCE over all tokens on the wgrad side
+        # stream (no per-chunk read-modify-write of the fp32 dW); otherwise dW accumulates
+        # per chunk on this stream into a chunk-sized logits buffer.
+        side_dw = (dw is not None and h.is_cuda and _WGRAD_STREAM
                    and _grad_sink(w) is not None)
-        lg = torch.empty((ch, Vp), device=dev, dtype=h.dtype)
+        lg = torch.empty((N if side_dw else ch, Vp), device=dev, dtype=h.dtype)
         for s0 in range(0, N, ch):
             e = min(N, s0 + ch)
-            lgc = lg[: e - s0]
+            lgc = lg[s0:e] if side_dw else lg[: e - s0]
             torch.mm(h2[s0:e], wt, out=lgc)
             check(L.ra_xent_fused(ptr(lgc), ptr(t[s0:e]), ptr(inv), ptr(loss_rows[s0:e]),
                                   e - s0, V, Vp, ignore_index, stream_ptr()), "xent_fused")
             if dh is not None:
                 torch.mm(lgc, w, out=dh[s0:e])
-            if dw is not None and side_dw:
-                side = _side_stream(dev)
-                side.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(side):
-                    _lm_head_dw(lgc, h2[s0:e], dw, True, side=True)
-                for t_ in (lg, h2, dw):
-                    t_.record_stream(side)
-            elif dw is not None:
+            if dw is not None and not side_dw:
                 _lm_head_dw(lgc, h2[s0:e], dw, s0 == 0)
+        if side_dw:
+            side = _side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                _lm_head_dw(lg, h2, dw, True, side=True)
+            for t_ in (lg, h2, dw):
+                t_.record_stream(side)
         ctx.side_dw = side_dw
         ctx.save_for_backward(dh, dw)
         ctx.w, ctx.shape, ctx.signal_w = w, h.shape, signal_w

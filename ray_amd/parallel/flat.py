@@ -275,8 +275,7 @@ class FlatDDP:
 
         dev = self.flat.device
         out, seen = [], set()
-        for st in (self._main, torch.cuda.current_stream(dev), rf._side.get(dev),
-                   rf._side2.get(dev)):
+        for st in (self._main, torch.cuda.current_stream(dev), rf._side.get(dev)):
             if st is not None and st.cuda_stream not in seen:
                 seen.add(st.cuda_stream)
                 out.append(st)
