@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--gap-us", type=float, default=5.0)
     a = ap.parse_args()
     ks = load(a.path)
-    ends = [i for i, k in enumerate(ks) if "adamw_kernel" in k[2]]
+    ends = [i for i, k in enumerate(ks) if "adamw" in k[2]]
     out = []
     for a_i, b_i in zip(ends[:-1], ends[1:]):
         step = ks[a_i + 1:b_i + 1]
