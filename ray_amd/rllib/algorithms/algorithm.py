@@ -198,6 +198,9 @@ class Algorithm:
         # worker index and the current weights, or dropped (ignore_env_runner_failures)
         self._runners = FaultTolerantActorManager(restore_fn=self._restore_runner)
         self._last_weights_ref = None
+        self._policy_server = None
+        if nr > 0 and float(getattr(config, "num_gpus_per_policy_server", 0) or 0) > 0:
+            self._start_policy_server(config, nr, probe)
         if nr > 0:
             rs = [runner_cls.options(**opts).remote(self.cfg, i + 1) for i in range(nr)]
             ray.get([r.ping.remote() for r in rs])
@@ -213,6 +216,7 @@ class Algorithm:
         ne = int(getattr(config, "evaluation_num_env_runners", 0) or 0)
         if ne > 0:
             ecfg = dict(self.cfg)
+            ecfg.pop("_policy_server", None)  # evaluation runners infer locally
             ecfg.update(dict(getattr(config, "evaluation_config", None) or {}))
             ecfg["_record_episodes"] = False
             self._eval_cfg = ecfg
@@ -320,9 +324,34 @@ class Algorithm:
     def num_env_runner_restarts(self):
         return self._runners.num_restarts
 
+    def _start_policy_server(self, config, nr, probe):
+        """One batched GPU inference process for all runners (rllib/env/policy_server.py):
+        discrete actor-critic modules whose observations reach the module unchanged."""
+        import functools
+
+        from ray_amd.rllib.core.rl_module.rl_module import build_module
+        from ray_amd.rllib.env.policy_server import PolicyServer
+
+        if self.cfg.get("module_kind", "actor_critic") != "actor_critic" or \
+                not hasattr(probe.action_space, "n") or self.is_multi_agent or \
+                self.cfg.get("env_to_module_connector") or \
+                self.cfg.get("observation_filter", "NoFilter") not in (None, "NoFilter"):
+            raise ValueError("num_gpus_per_policy_server needs a single-agent discrete "
+                             "actor-critic module fed the raw observations")
+        fn = functools.partial(build_module, dict(self.cfg), probe.observation_space,
+                               probe.action_space)
+        B = int(config.num_envs_per_env_runner)
+        srv = ray.remote(PolicyServer).options(
+            num_gpus=float(config.num_gpus_per_policy_server), num_cpus=1).remote(
+            fn, nr, B, tuple(probe.observation_space.shape), int(probe.action_space.n))
+        self._policy_server = srv
+        self.cfg["_policy_server"] = ray.get(srv.mailbox.remote())
+
     # ---------------------------------------------------------------- weights
     def _sync_weights(self, weights):
         self.weights_version += 1
+        if self._policy_server is not None:
+            self._policy_server.set_weights.remote(weights, self.weights_version)
         if self._runners.num_actors():
             ref = ray.put(weights)
             self._last_weights_ref = ref
@@ -522,6 +551,7 @@ class Algorithm:
                                  for r in self._eval_runners}}
         if self._eval_local is None:
             ecfg = dict(self.cfg)
+            ecfg.pop("_policy_server", None)  # evaluation runners infer locally
             ecfg.update(dict(getattr(self.config, "evaluation_config", None) or {}))
             ecfg["_record_episodes"] = False
             self._eval_local = self._runner_cls(ecfg, 999)
@@ -966,6 +996,12 @@ class Algorithm:
 
     def stop(self):
         self._runners.clear()
+        if self._policy_server is not None:
+            try:
+                ray.kill(self._policy_server)
+            except Exception:  # noqa: BLE001
+                pass
+            self._policy_server = None
         for r in self._eval_runners:
             try:
                 ray.kill(r)

@@ -17,6 +17,9 @@ class AlgorithmConfig:
         self.rollout_fragment_length = 200
         self.num_cpus_per_env_runner = 1
         self.num_gpus_per_env_runner = 0
+        # > 0: the runners' policy forward runs batched in ONE GPU process holding this GPU
+        # share (rllib/env/policy_server.py); the runners keep stepping envs on CPU
+        self.num_gpus_per_policy_server = 0
         self.gamma = 0.99
         self.lr = 5e-5
         self.train_batch_size = 4000
@@ -149,7 +152,7 @@ class AlgorithmConfig:
 
     _RUNNER_KEYS = ("num_env_runners", "num_envs_per_env_runner", "rollout_fragment_length",
                     "num_cpus_per_env_runner", "num_gpus_per_env_runner",
-                    "env_to_module_connector", "module_to_env_connector",
+                    "num_gpus_per_policy_server", "env_to_module_connector", "module_to_env_connector",
                     "observation_filter", "sample_async", "batch_mode", "explore",
                     "exploration_config", "sample_timeout_s", "create_env_on_local_worker",
                     "custom_resources_per_env_runner", "validate_env_runners_after_construction",

@@ -31,8 +31,11 @@ def _envs_per_runner() -> int:
     return int(os.environ.get("RAY_AMD_RUNNER_ENVS", "5"))
 
 
-def _inference_where(runner_gpus: float) -> str:
+def _inference_where(runner_gpus: float, server_gpus: float = 0.0) -> str:
     """Where the env runners' policy forward runs (reported in the JSON line)."""
+    if server_gpus > 0:
+        return ("gpu policy server (one process: all runners' envs batched into one HIP "
+                "graph per step, shared-memory mailbox)")
     if runner_gpus <= 0:
         return "cpu (bf16 Nature-CNN, torch)"
     if os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1":
@@ -50,6 +53,8 @@ def bench_ppo(args):
              ignore_reinit_error=True)
     # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
     runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
+    # > 0: one batched GPU inference process for all runners (rllib/env/policy_server.py)
+    server_gpus = float(os.environ.get("RAY_AMD_POLICY_SERVER_GPUS", "0"))
     sample_async = os.environ.get("RAY_AMD_PPO_ASYNC", "0") == "1"
     # CPU threads per env runner (torch intra-op threads for the Nature-CNN inference)
     runner_cpus = float(os.environ.get("RAY_AMD_RUNNER_CPUS", "1"))
@@ -58,7 +63,8 @@ def bench_ppo(args):
     cfg = (PPOConfig().environment("SyntheticAtari-v0")
            .env_runners(num_env_runners=n_runners, num_envs_per_env_runner=_envs_per_runner(),
                         rollout_fragment_length="auto", num_gpus_per_env_runner=runner_gpus,
-                        num_cpus_per_env_runner=runner_cpus, sample_async=sample_async)
+                        num_cpus_per_env_runner=runner_cpus, sample_async=sample_async,
+                        num_gpus_per_policy_server=server_gpus)
            .training(train_batch_size=5000 * n_gpus, minibatch_size=500, num_epochs=10,
                      lr=1e-4, lambda_=0.95, kl_coeff=0.5, clip_param=0.1, vf_clip_param=10.0,
                      entropy_coeff=0.01, model={"vf_share_layers": True})
@@ -92,7 +98,7 @@ def bench_ppo(args):
                    "minibatch_size": 500, "num_epochs": 10,
                    "parallelism": f"{n_gpus} learner{'s' if n_gpus > 1 else ''}",
                    "env_runner_gpus": runner_gpus, "env_runner_cpus": runner_cpus,
-                   "env_runner_inference": _inference_where(runner_gpus),
+                   "env_runner_inference": _inference_where(runner_gpus, server_gpus),
                    "sample_async": sample_async},
         "learner": {k: learn_stats.get(k) for k in ("total_loss", "entropy", "mean_kl_loss",
                                                      "sample_time_s", "sample_wait_s",

@@ -168,6 +168,15 @@ class SingleAgentEnvRunner:
                          and not self._stateful and hasattr(self.action_space, "n")
                          and os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1")
         self._gpol = None
+        # the runners' shared GPU inference process (num_gpus_per_policy_server)
+        self._pclient = None
+        srv = config.get("_policy_server")
+        if srv is not None and worker_index > 0 and ac_module and not self._stateful:
+            from ray_amd.rllib.env.policy_server import PolicyClient
+
+            path, n_slots, pB, oshape, na = srv
+            self._pclient = PolicyClient(path, worker_index - 1, n_slots, pB, oshape, na)
+            self._graphed = True
         self._act_rng = np.random.default_rng(
             None if seed is None else seed * 7919 + worker_index)
         self.obs = []
@@ -320,13 +329,16 @@ class SingleAgentEnvRunner:
                     else:
                         out = self.module.forward_inference(x)
                     if out is None:
-                        if self._gpol is None or self._gpol.obs_shape != ob.shape:
-                            from ray_amd.rllib.env.gpu_policy import GraphedDiscretePolicy
+                        if self._pclient is not None:
+                            pol = self._pclient
+                        else:
+                            if self._gpol is None or self._gpol.obs_shape != ob.shape:
+                                from ray_amd.rllib.env.gpu_policy import GraphedDiscretePolicy
 
-                            self._gpol = GraphedDiscretePolicy(self.module, ob,
-                                                               self.action_space.n,
-                                                               self.device)
-                        a, lp, d = self._gpol.step(ob, explore, self._act_rng)
+                                self._gpol = GraphedDiscretePolicy(
+                                    self.module, ob, self.action_space.n, self.device)
+                            pol = self._gpol
+                        a, lp, d = pol.step(ob, explore, self._act_rng)
                         if dist_in is None:
                             dist_in = np.zeros((cap, B, d.shape[-1]), np.float32)
                         dist_in[t] = d
