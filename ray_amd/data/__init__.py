@@ -15,6 +15,9 @@ from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface
                                    read_binary_files, read_csv, read_datasource, read_images,
                                    read_json, read_numpy, read_parquet, read_parquet_bulk,
                                    read_text, read_tfrecords, read_avro)
+from ray_amd.data.integrations import (from_dask, from_mars, from_modin,  # noqa: F401
+                                       from_spark, from_tf, read_bigquery,
+                                       read_databricks_tables, read_mongo)
 from ray_amd.data.datasource import (BlockBasedFileDatasink, Datasink,  # noqa: F401
                                      Datasource, RandomAccessDataset, ReadTask,
                                      RowBasedFileDatasink, read_sql, read_webdataset)

@@ -1078,6 +1078,58 @@ class Dataset:
 
         return write_datasink(self, datasink, ray_remote_args)
 
+    def write_datasource(self, datasource, *, ray_remote_args=None, **write_args):
+        """Legacy form of ``write_datasink`` (reference: deprecated ``Datasource.write``
+        path): a Datasink is written directly; a Datasource with a ``write(blocks)``
+        method receives every block."""
+        from ray_amd.data.datasource import Datasink
+
+        if isinstance(datasource, Datasink):
+            return self.write_datasink(datasource, ray_remote_args=ray_remote_args)
+        blocks = [b for b in self.iter_batches(batch_size=None, batch_format="pyarrow")]
+        return datasource.write(blocks, **write_args)
+
+    # external frameworks (data/integrations.py): ImportError naming the missing package
+    def to_dask(self, *a, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.to_dask(self, *a, **kw)
+
+    def to_modin(self):
+        from ray_amd.data import integrations
+
+        return integrations.to_modin(self)
+
+    def to_mars(self):
+        from ray_amd.data import integrations
+
+        return integrations.to_mars(self)
+
+    def to_spark(self, spark):
+        from ray_amd.data import integrations
+
+        return integrations.to_spark(self, spark)
+
+    def to_tf(self, feature_columns, label_columns, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.to_tf(self, feature_columns, label_columns, **kw)
+
+    def iter_tf_batches(self, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.iter_tf_batches(self, **kw)
+
+    def write_bigquery(self, project_id, dataset, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.write_bigquery(self, project_id, dataset, **kw)
+
+    def write_mongo(self, uri, database, collection, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.write_mongo(self, uri, database, collection, **kw)
+
     def write_sql(self, sql: str, connection_factory, **kw):
         """INSERT every row with ``sql`` (one DB-API placeholder per column)."""
         from ray_amd.data.datasource import SQLDatasink
