@@ -256,6 +256,42 @@ class DataIterator:
     def stats(self):
         return self._ds.stats()
 
+    def schema(self):
+        """Schema of the rows this iterator yields (the dataset's)."""
+        return self._ds.schema()
+
+    def to_torch(self, *, label_column=None, feature_columns=None, batch_size=1,
+                 label_column_dtype=None, feature_column_dtypes=None, **kw):
+        """A torch ``IterableDataset`` of (features, label) batches (reference: the
+        deprecated ``DataIterator.to_torch``)."""
+        import torch
+
+        it = self
+
+        class _Iterable(torch.utils.data.IterableDataset):
+            def __iter__(self):
+                for b in it.iter_torch_batches(batch_size=batch_size, **kw):
+                    y = b.pop(label_column) if label_column else None
+                    cols = feature_columns or sorted(b)
+                    x = torch.stack([b[c].float() if feature_column_dtypes is None
+                                     else b[c].to(feature_column_dtypes) for c in cols], 1) \
+                        if isinstance(cols, list) else b[cols]
+                    if y is not None and label_column_dtype is not None:
+                        y = y.to(label_column_dtype)
+                    yield (x, y) if y is not None else x
+
+        return _Iterable()
+
+    def to_tf(self, feature_columns, label_columns, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.to_tf(self, feature_columns, label_columns, **kw)
+
+    def iter_tf_batches(self, **kw):
+        from ray_amd.data import integrations
+
+        return integrations.iter_tf_batches(self, **kw)
+
 
 class SplitCoordinator:
     """Actor that runs ONE streaming execution and deals its blocks to n consumers

@@ -458,6 +458,148 @@ class Algorithm:
     def training_step(self) -> dict:
         raise NotImplementedError
 
+    # ---------------------------------------------------------------- Trainable surface
+    # (reference: rllib/algorithms/algorithm.py — Algorithm is a tune.Trainable)
+    def step(self) -> dict:
+        """One training iteration (Trainable.step); ``train`` is the same call."""
+        return self.train()
+
+    def cleanup(self):
+        """Trainable.cleanup: release runners, learners and the policy server."""
+        self.stop()
+
+    def log_result(self, result: dict) -> None:
+        """Trainable.log_result: keep the latest result (``callbacks`` already saw it)."""
+        self._last_result = result
+
+    def get_auto_filled_metrics(self, now=None, time_this_iter=None, timestamp=None,
+                                debug_metrics_only=False) -> dict:
+        import datetime
+        import os as _os
+        import socket
+
+        now = now or datetime.datetime.now()
+        m = {"trial_id": getattr(self, "trial_id", "default"),
+             "time_this_iter_s": time_this_iter,
+             "time_total_s": time.time() - self._t_start,
+             "training_iteration": self.iteration}
+        if not debug_metrics_only:
+            m.update({"date": now.strftime("%Y-%m-%d_%H-%M-%S"),
+                      "timestamp": int(timestamp or time.time()),
+                      "pid": _os.getpid(), "hostname": socket.gethostname(),
+                      "node_ip": "127.0.0.1"})
+        return m
+
+    @classmethod
+    def get_default_config(cls):
+        """The AlgorithmConfig subclass whose ``algo_class`` is this algorithm."""
+        from ray_amd.rllib.algorithms.algorithm_config import AlgorithmConfig
+
+        def subs(c):
+            for s_ in c.__subclasses__():
+                yield s_
+                yield from subs(s_)
+
+        for sub in subs(AlgorithmConfig):
+            try:
+                inst = sub()
+            except Exception:  # noqa: BLE001 - configs that need arguments
+                continue
+            if inst.algo_class is cls:
+                return inst
+        return AlgorithmConfig(algo_class=cls)
+
+    @classmethod
+    def get_default_policy_class(cls, config=None):
+        return _PolicyView
+
+    @classmethod
+    def validate_config(cls, config) -> None:
+        v = getattr(config, "validate", None)
+        if callable(v):
+            v()
+
+    @staticmethod
+    def merge_algorithm_configs(config1: dict, config2: dict,
+                                _allow_unknown_configs: bool | None = None) -> dict:
+        """Deep-merge ``config2`` into a copy of ``config1`` (reference:
+        Algorithm.merge_algorithm_configs); unknown top-level keys raise unless allowed."""
+        import copy
+
+        out = copy.deepcopy(dict(config1))
+        for k, v in dict(config2 or {}).items():
+            if k not in out and _allow_unknown_configs is False:
+                raise ValueError(f"Unknown config parameter `{k}`")
+            if isinstance(v, dict) and isinstance(out.get(k), dict):
+                out[k] = Algorithm.merge_algorithm_configs(out[k], v, True)
+            else:
+                out[k] = v
+        return out
+
+    @classmethod
+    def default_resource_request(cls, config):
+        """Resources one trial of this algorithm holds (Tune): the driver bundle (CPU +
+        local learner GPUs), one bundle per env runner, one per remote learner."""
+        from ray_amd.tune.registry import PlacementGroupFactory
+
+        c = config if not isinstance(config, dict) else cls.get_default_config().update_from_dict(
+            config)
+        nl = int(getattr(c, "num_learners", 0) or 0)
+        g = float(getattr(c, "num_gpus_per_learner", 0) or 0)
+        head = {"CPU": 1.0}
+        if nl == 0 and g:
+            head["GPU"] = g
+        bundles = [head]
+        for _ in range(int(getattr(c, "num_env_runners", 0) or 0)):
+            b = {"CPU": float(getattr(c, "num_cpus_per_env_runner", 1) or 1)}
+            if getattr(c, "num_gpus_per_env_runner", 0):
+                b["GPU"] = float(c.num_gpus_per_env_runner)
+            bundles.append(b)
+        for _ in range(nl):
+            bundles.append({"CPU": 1.0, **({"GPU": g} if g else {})})
+        if float(getattr(c, "num_gpus_per_policy_server", 0) or 0) > 0:
+            bundles.append({"CPU": 1.0, "GPU": float(c.num_gpus_per_policy_server)})
+        return PlacementGroupFactory(bundles, strategy="PACK")
+
+    @classmethod
+    def resource_help(cls, config) -> str:
+        pgf = cls.default_resource_request(config)
+        return (f"{cls.__name__} asks for {len(pgf.bundles)} bundles {pgf.bundles}: the "
+                "driver / local learner, one per env runner (num_cpus_per_env_runner, "
+                "num_gpus_per_env_runner), one per remote learner (num_gpus_per_learner).")
+
+    def export_policy_checkpoint(self, export_dir: str, policy_id=None) -> None:
+        """Policy state (weights + spaces) as a weights-only checkpoint directory."""
+        import os as _os
+
+        import torch
+
+        _os.makedirs(export_dir, exist_ok=True)
+        pol = self.get_policy(policy_id)
+        torch.save({"weights": {k: torch.as_tensor(v) for k, v in pol.get_weights().items()},
+                    "policy_id": policy_id or "default_policy"},
+                   _os.path.join(export_dir, "policy_state.pt"))
+
+    def import_model(self, import_file: str):
+        """Load module weights exported by ``export_policy_model`` (weights-only .pt);
+        Keras h5 files (``import_policy_model_from_h5``) need tensorflow."""
+        import torch
+
+        if str(import_file).endswith(".h5"):
+            return self.import_policy_model_from_h5(import_file)
+        sd = torch.load(import_file, weights_only=True, map_location="cpu")
+        if isinstance(sd, dict) and "weights" in sd:
+            sd = sd["weights"]
+        self.set_weights(sd)
+
+    def import_policy_model_from_h5(self, import_file: str, policy_id=None):
+        try:
+            import tensorflow  # noqa: F401
+        except ImportError:
+            raise ImportError("import_policy_model_from_h5 requires tensorflow (Keras h5 "
+                              "weights), which is not installed") from None
+        raise NotImplementedError("Keras h5 weights cannot be mapped onto torch RLModules")
+
     def _sample(self, total: int):
         """Synchronous parallel sampling of >= total env steps (reference:
         rllib/execution/rollout_ops.py:synchronous_parallel_sample)."""

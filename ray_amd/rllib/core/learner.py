@@ -579,6 +579,67 @@ class TorchLearner:
         lr.metrics.update({k: float(v.detach()) if torch.is_tensor(v) else v
                            for k, v in metrics_dict.items()})
 
+    def register_metric(self, module_id, key: str, value) -> None:
+        """One metric (reference: Learner.register_metric)."""
+        self.register_metrics(module_id, {key: value})
+
+    @property
+    def distributed(self) -> bool:
+        """True when this learner all-reduces with peers (a multi-learner group)."""
+        return self.world > 1
+
+    def apply(self, func, *args, **kwargs):
+        """``func(self, *args, **kwargs)`` (LearnerGroup.foreach_learner's per-learner call)."""
+        return func(self, *args, **kwargs)
+
+    def compute_loss(self, *, fwd_out, batch):
+        """The total loss: the sum of ``compute_losses`` over modules (old-stack name)."""
+        losses = self.compute_losses(fwd_out=fwd_out, batch=batch)
+        return sum(losses.values()) if isinstance(losses, dict) else losses
+
+    def compile_results(self, *, batch, fwd_out, loss_per_module, metrics_per_module=None):
+        """Per-module result dicts: the loss plus the metrics registered for the module."""
+        out = {}
+        for mid, loss in (loss_per_module or {}).items():
+            r = {"total_loss": float(loss.detach()) if torch.is_tensor(loss) else loss}
+            lr = self._module_learners().get(mid)
+            if lr is not None:
+                r.update(getattr(lr, "metrics", {}) or {})
+            r.update((metrics_per_module or {}).get(mid, {}))
+            out[mid] = r
+        return out
+
+    def filter_param_dict_for_optimizer(self, param_dict: dict, optimizer) -> dict:
+        """The entries of ``param_dict`` whose tensors ``optimizer`` updates."""
+        groups = getattr(optimizer, "param_groups", None)
+        if groups is not None:
+            ids = {id(p) for g in groups for p in g["params"]}
+        else:  # a flat-buffer optimizer (FlatAdamW) updates every parameter of its buffer
+            flat = getattr(optimizer, "flat", None)
+            ps = flat.params() if flat is not None and callable(getattr(flat, "params", None)) \
+                else self.module.parameters()
+            ids = {id(p) for p in ps}
+        return {k: v for k, v in param_dict.items() if id(v) in ids}
+
+    def get_param_ref(self, param):
+        """A stable reference to a parameter: its qualified name in the module."""
+        for n, p in self.module.named_parameters():
+            if p is param:
+                return n
+        return id(param)
+
+    def additional_update(self, *, module_ids_to_update=None, timestep=None, **kwargs) -> dict:
+        """Old-stack hook run after the gradient updates (reference:
+        Learner.additional_update): ``additional_update_for_module`` per module."""
+        mids = module_ids_to_update or self.module_ids
+        return {mid: self.additional_update_for_module(module_id=mid, config=self.config,
+                                                       timestep=timestep, **kwargs)
+                for mid in mids}
+
+    def additional_update_for_module(self, *, module_id, config=None, timestep=None,
+                                     **kwargs) -> dict:
+        return {}
+
     def _is_module_batch(self, batch) -> bool:
         lrs = self._module_learners()
         return isinstance(batch, dict) and bool(batch) and len(lrs) > 1 and \
@@ -1506,6 +1567,44 @@ class LearnerGroup:
     @property
     def is_local(self) -> bool:
         return not self.remote
+
+    @property
+    def is_remote(self) -> bool:
+        return bool(self.remote)
+
+    def async_update(self, batch, **kwargs):
+        """Old-stack name of ``update_from_batch(async_update=True)``."""
+        return self.update_from_batch(batch, async_update=True, **kwargs)
+
+    def additional_update(self, **kwargs):
+        """Run every learner's ``additional_update``; the first learner's results."""
+        return self._all("additional_update", **kwargs)[0]
+
+    def get_stats(self) -> dict:
+        return {"num_learners": len(self.actors) if self.remote else 1,
+                "is_local": self.is_local, "module_ids": sorted(self.get_module_state().keys())}
+
+    def load_module_state(self, *, rl_module_ckpt_dirs=None, modules_to_load=None,
+                          marl_module_ckpt_dir=None):
+        """Module weights from weights-only files: ``rl_module_ckpt_dirs`` maps module ids
+        to a directory holding ``module_state.pt`` (or the file itself);
+        ``marl_module_ckpt_dir`` holds ``<module_id>/module_state.pt`` for every module
+        (filtered by ``modules_to_load``)."""
+        import os as _os
+
+        def load(path):
+            f = path if _os.path.isfile(path) else _os.path.join(path, "module_state.pt")
+            return torch.load(f, weights_only=True, map_location="cpu")
+
+        state = {}
+        if marl_module_ckpt_dir:
+            for mid in sorted(_os.listdir(marl_module_ckpt_dir)):
+                if modules_to_load is None or mid in modules_to_load:
+                    state[mid] = load(_os.path.join(marl_module_ckpt_dir, mid))
+        for mid, path in (rl_module_ckpt_dirs or {}).items():
+            state[mid] = load(path)
+        if state:
+            self.set_module_state(state)
 
     def update_from_batch(self, batch, *, async_update=False, timesteps=None, **kwargs):
         """One update step on ``batch`` (rows split evenly over the learners; per-row

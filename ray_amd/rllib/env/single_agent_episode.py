@@ -61,9 +61,31 @@ class SingleAgentEpisode:
     def __len__(self) -> int:
         return len(self.actions)
 
-    @property
-    def env_steps(self):
+    def env_steps(self) -> int:
+        """Env steps in this chunk (reference: SingleAgentEpisode.env_steps)."""
         return len(self)
+
+    def agent_steps(self) -> int:
+        """Same as ``env_steps`` for a single agent."""
+        return len(self)
+
+    @property
+    def is_finalized(self) -> bool:
+        return self._finalized
+
+    def validate(self) -> None:
+        """The chunk invariants: one more observation / info than actions, rewards and
+        each extra-model-output column."""
+        n = len(self.actions)
+        if len(self.observations) != n + 1 and not (n == 0 and len(self.observations) <= 1):
+            raise AssertionError(f"{len(self.observations)} observations for {n} actions")
+        if len(self.rewards) != n:
+            raise AssertionError(f"{len(self.rewards)} rewards for {n} actions")
+        if len(self.infos) != len(self.observations):
+            raise AssertionError(f"{len(self.infos)} infos for {len(self.observations)} obs")
+        for k, v in self.extra_model_outputs.items():
+            if len(v) != n:
+                raise AssertionError(f"extra_model_outputs[{k!r}] has {len(v)} rows for {n}")
 
     def get_return(self) -> float:
         return float(np.sum(self.rewards)) if self.rewards else 0.0
@@ -96,6 +118,61 @@ class SingleAgentEpisode:
 
     def get_extra_model_outputs(self, key, indices=None):
         return self._pick(self.extra_model_outputs[key], indices)
+
+    # ---------------------------------------------------------------- overwrite
+    def _set(self, lst, new_data, at_indices):
+        """Overwrite ``lst[at_indices]`` (an int, a slice, a list, or None = every row)."""
+        if self._finalized:
+            raise ValueError("set_*() on a finalized episode (numpy arrays): set before "
+                             "finalize()")
+        if isinstance(at_indices, int):
+            lst[at_indices] = new_data
+            return
+        idx = list(range(len(lst))[at_indices]) if isinstance(at_indices, slice) else \
+            list(range(len(lst))) if at_indices is None else list(at_indices)
+        vals = list(new_data)
+        if len(vals) != len(idx):
+            raise IndexError(f"{len(vals)} values for {len(idx)} indices")
+        for i, v in zip(idx, vals):
+            lst[i] = v
+
+    def set_observations(self, *, new_data, at_indices=None):
+        self._set(self.observations, new_data, at_indices)
+
+    def set_actions(self, *, new_data, at_indices=None):
+        self._set(self.actions, new_data, at_indices)
+
+    def set_rewards(self, *, new_data, at_indices=None):
+        self._set(self.rewards, float(new_data) if isinstance(at_indices, int) else
+                  [float(r) for r in np.atleast_1d(new_data)], at_indices)
+
+    def set_extra_model_outputs(self, *, key, new_data, at_indices=None):
+        col = self.extra_model_outputs.setdefault(key, [None] * len(self.actions))
+        self._set(col, new_data, at_indices)
+
+    # ---------------------------------------------------------------- batches
+    def get_data_dict(self) -> dict:
+        """Column dict of this chunk, one row per action: obs / next_obs, actions, rewards,
+        terminateds / truncateds (last row only), t, eps_id and the extra model outputs."""
+        n = len(self.actions)
+        obs = np.asarray(self.observations)
+        d = {"obs": obs[:n], "new_obs": obs[1:n + 1], "actions": np.asarray(self.actions),
+             "rewards": np.asarray(self.rewards, np.float32),
+             "terminateds": np.zeros(n, bool), "truncateds": np.zeros(n, bool),
+             "t": np.arange(self.t_started, self.t_started + n),
+             "eps_id": np.array([self.id_] * n)}
+        if n:
+            d["terminateds"][-1] = self.is_terminated
+            d["truncateds"][-1] = self.is_truncated
+        for k, v in self.extra_model_outputs.items():
+            d[k] = np.asarray(v)
+        return d
+
+    def get_sample_batch(self):
+        """The chunk as an old-stack ``SampleBatch``."""
+        from ray_amd.rllib.policy_sample_batch import SampleBatch
+
+        return SampleBatch(self.get_data_dict())
 
     # ---------------------------------------------------------------- chunks
     def cut(self, len_lookback_buffer=0) -> "SingleAgentEpisode":

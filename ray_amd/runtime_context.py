@@ -114,6 +114,17 @@ class RuntimeContext:
         spec = getattr(self._cw.current_task, "spec", None) or self._cw.actor_spec
         return dict((spec or {}).get("resources") or {})
 
+    @property
+    def task_id(self):
+        """Deprecated property form of ``get_task_id``."""
+        return self.get_task_id()
+
+    def get_resource_ids(self):
+        """Deprecated: ``{"GPU": [(id, fraction), ...]}`` of this worker."""
+        res = self.get_assigned_resources()
+        frac = float(res.get("GPU", 1.0) or 1.0)
+        return {"GPU": [(int(i), frac) for i in self._cw.gpu_ids]}
+
     def get_accelerator_ids(self):
         return {"GPU": [str(i) for i in self._cw.gpu_ids]}
 

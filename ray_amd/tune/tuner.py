@@ -287,6 +287,17 @@ class ResultGrid:
         self._metric = metric
         self._mode = mode
 
+    @property
+    def filesystem(self):
+        """The pyarrow filesystem the experiment directory lives on (a URI's scheme, or
+        the local filesystem)."""
+        import pyarrow.fs as pafs
+
+        p = str(self.experiment_path or "")
+        if "://" in p:
+            return pafs.FileSystem.from_uri(p)[0]
+        return pafs.LocalFileSystem()
+
     def __len__(self):
         return len(self._results)
 

@@ -58,3 +58,23 @@ def test_write_datasource_legacy(cluster):
     ds.write_datasource(_Collect())
     src = _LegacySource()
     assert ds.write_datasource(src) == 25 and src.rows == 25
+
+
+def test_data_iterator_schema_and_to_torch(cluster):
+    ds = rd.from_items([{"a": float(i), "b": float(2 * i), "y": i % 2} for i in range(8)])
+    it = ds.iterator()
+    assert set(it.schema().names) == {"a", "b", "y"}
+    batches = list(it.to_torch(label_column="y", feature_columns=["a", "b"], batch_size=4))
+    assert len(batches) == 2
+    x, y = batches[0]
+    assert tuple(x.shape) == (4, 2) and tuple(y.shape) == (4,)
+
+
+def test_runtime_context_legacy_ids(cluster):
+    @ray.remote
+    def f():
+        ctx = ray.get_runtime_context()
+        return ctx.task_id, ctx.get_resource_ids()
+
+    tid, rids = ray.get(f.remote())
+    assert isinstance(tid, str) and rids == {"GPU": []}

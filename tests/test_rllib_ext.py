@@ -181,3 +181,35 @@ def test_dqn_from_episode_replay_buffer(cluster):
     assert best > 45
     assert algo.buffer.get_num_episodes() > 10
     algo.stop()
+
+
+def test_single_agent_episode_setters_and_batches():
+    """SingleAgentEpisode: env_steps()/agent_steps(), validate, set_* overwrites, and the
+    chunk as a column dict / SampleBatch (reference: single_agent_episode.py)."""
+    import numpy as np
+
+    from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode
+
+    e = SingleAgentEpisode()
+    e.add_env_reset(np.zeros(2))
+    for i in range(4):
+        e.add_env_step(np.full(2, i + 1.0), i, 1.0, extra_model_outputs={"logp": -0.5},
+                       terminated=i == 3)
+    e.validate()
+    assert e.env_steps() == e.agent_steps() == 4
+    e.set_rewards(new_data=[5.0, 6.0], at_indices=slice(1, 3))
+    e.set_actions(new_data=7, at_indices=0)
+    e.set_extra_model_outputs(key="vf", new_data=[0.1, 0.2, 0.3, 0.4])
+    assert e.get_rewards() == [1.0, 5.0, 6.0, 1.0] and e.get_actions()[0] == 7
+    d = e.get_data_dict()
+    assert d["obs"].shape == (4, 2) and np.array_equal(d["new_obs"][:, 0], [1, 2, 3, 4])
+    assert d["terminateds"].tolist() == [False, False, False, True]
+    assert d["vf"].tolist() == [0.1, 0.2, 0.3, 0.4]
+    sb = e.get_sample_batch()
+    assert len(sb["rewards"]) == 4
+    e.finalize()
+    assert e.is_finalized
+    import pytest as _pt
+
+    with _pt.raises(ValueError):
+        e.set_rewards(new_data=0.0, at_indices=0)

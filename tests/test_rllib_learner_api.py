@@ -321,3 +321,72 @@ def test_register_metrics_and_weights_only_state(tmp_path):
             assert torch.equal(v, lr2.get_module_state()[m][k])
     with pytest.raises(ValueError):
         lr.add_module(module_id="b")
+
+
+def test_trainable_and_learner_surface():
+    """Trainable-style Algorithm API and the remaining Learner / LearnerGroup methods
+    (reference: algorithm.py step/cleanup/get_default_config/default_resource_request/
+    merge_algorithm_configs; learner.py register_metric/compute_loss/apply/...;
+    learner_group.py is_remote/get_stats/load_module_state)."""
+    import os
+    import tempfile
+
+    import torch
+
+    import ray_amd as ray
+    from ray_amd.rllib.algorithms import PPO, PPOConfig
+    from ray_amd.rllib.algorithms.algorithm import Algorithm
+
+    cfg = PPO.get_default_config()
+    assert isinstance(cfg, PPOConfig)
+    merged = Algorithm.merge_algorithm_configs({"a": {"x": 1, "y": 2}, "b": 1},
+                                               {"a": {"y": 3}, "c": 4})
+    assert merged == {"a": {"x": 1, "y": 3}, "b": 1, "c": 4}
+    with pytest.raises(ValueError):
+        Algorithm.merge_algorithm_configs({"a": 1}, {"zz": 1}, _allow_unknown_configs=False)
+    c = (PPOConfig().environment("CartPole-v1")
+         .env_runners(num_env_runners=2, num_cpus_per_env_runner=1)
+         .learners(num_learners=0, num_gpus_per_learner=0))
+    pgf = PPO.default_resource_request(c)
+    assert len(pgf.bundles) == 3 and pgf.bundles[1] == {"CPU": 1.0}
+    assert "bundles" in PPO.resource_help(c)
+    started = not ray.is_initialized()
+    if started:
+        ray.init(num_cpus=2)
+    try:
+        algo = (PPOConfig().environment("CartPole-v1")
+                .env_runners(num_env_runners=0, num_envs_per_env_runner=2,
+                             rollout_fragment_length=32)
+                .training(train_batch_size=64, minibatch_size=32, num_epochs=1)
+                .debugging(seed=0)).build()
+        r = algo.step()
+        assert r["training_iteration"] == 1
+        algo.log_result(r)
+        m = algo.get_auto_filled_metrics(time_this_iter=1.0)
+        assert m["training_iteration"] == 1 and "pid" in m
+        lg = algo.learner_group
+        assert lg.is_remote is False and lg.get_stats()["num_learners"] == 1
+        lr = lg.local
+        assert lr.distributed is False
+        assert lr.apply(lambda le, k: k + 1, 1) == 2
+        mid = lr.module_ids[0]
+        lr.register_metric(mid, "my_metric", 3.0)
+        p0 = next(lr.module.parameters())
+        assert isinstance(lr.get_param_ref(p0), str)
+        opt = lr.get_optimizer()
+        pd = dict(lr.module.named_parameters())
+        assert lr.filter_param_dict_for_optimizer(pd, opt).keys() == pd.keys()
+        assert lr.additional_update(timestep=0) == {m_: {} for m_ in lr.module_ids}
+        with tempfile.TemporaryDirectory() as d:
+            sd = lg.get_module_state()[mid]
+            sd = {k: (v * 0 if torch.is_tensor(v) and v.is_floating_point() else v)
+                  for k, v in sd.items()}
+            os.makedirs(os.path.join(d, mid))
+            torch.save(sd, os.path.join(d, mid, "module_state.pt"))
+            lg.load_module_state(marl_module_ckpt_dir=d)
+            assert all(float(v.abs().sum()) == 0 for v in lg.get_module_state()[mid].values()
+                       if torch.is_tensor(v) and v.is_floating_point())
+        algo.cleanup()
+    finally:
+        if started:
+            ray.shutdown()
