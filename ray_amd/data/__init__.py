@@ -9,6 +9,7 @@ from ray_amd.data.block import Schema  # noqa: F401
 from ray_amd.data.preprocessors import Preprocessor  # noqa: F401
 
 DatasetIterator = DataIterator
+NodeIdStr = str  # reference: data/_internal/execution/interfaces/common.py
 from ray_amd.data.read_api import (from_arrow, from_arrow_refs, from_huggingface,  # noqa: F401
                                    from_items, from_numpy, from_numpy_refs, from_pandas,
                                    from_pandas_refs, from_torch, range, range_tensor,

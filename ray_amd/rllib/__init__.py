@@ -8,7 +8,7 @@ from ray_amd.rllib.env.env_runner import SingleAgentEnvRunner  # noqa: F401,E402
 
 from ray_amd.rllib.env.external_env import ExternalEnv  # noqa: F401,E402
 from ray_amd.rllib.env.vector_env import VectorEnv  # noqa: F401,E402
-from ray_amd.rllib.policy import Policy, TorchPolicy  # noqa: F401,E402
+from ray_amd.rllib.policy import Policy, TFPolicy, TorchPolicy  # noqa: F401,E402
 
 # classic-stack names: the env runner is this stack's rollout worker
 RolloutWorker = SingleAgentEnvRunner

@@ -166,3 +166,17 @@ class TorchPolicy(Policy):
 
 
 __all__ = ["Policy", "TorchPolicy"]
+
+
+class TFPolicy(Policy):
+    """TensorFlow policies (reference: rllib/policy/tf_policy.py) need tensorflow, which
+    this framework does not ship: constructing one fails like the reference does without
+    it. Torch policies (``TorchPolicy``) are the supported kind."""
+
+    def __init__(self, *args, **kwargs):
+        try:
+            import tensorflow  # noqa: F401
+        except ImportError:
+            raise ImportError("TFPolicy requires tensorflow, which is not installed; use "
+                              "TorchPolicy") from None
+        raise NotImplementedError("TFPolicy: RLlib modules here are torch modules")

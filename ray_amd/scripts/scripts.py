@@ -368,6 +368,50 @@ def cmd_metrics(a):
     return 0
 
 
+def cmd_up(a):
+    from ray_amd.autoscaler import sdk
+
+    st = sdk.create_or_update_cluster(a.cluster_config, no_restart=a.no_restart,
+                                      restart_only=a.restart_only)
+    print(f"Cluster {st['cluster_name']} is up: address {st['address']}, "
+          f"{len(st['workers'])} worker node(s). Connect with "
+          f"ray_amd.init(address='{st['address']}').")
+    return 0
+
+
+def cmd_down(a):
+    from ray_amd.autoscaler import sdk
+
+    sdk.teardown_cluster(a.cluster_config, workers_only=a.workers_only,
+                         keep_min_workers=a.keep_min_workers)
+    print("Cluster torn down." if not a.workers_only else "Worker nodes torn down.")
+    return 0
+
+
+def cmd_exec(a):
+    from ray_amd.autoscaler import sdk
+
+    sdk.run_on_cluster(a.cluster_config, cmd=a.cmd)
+    return 0
+
+
+def cmd_rsync(a):
+    from ray_amd.autoscaler import sdk
+
+    sdk.rsync(a.cluster_config, source=a.source, target=a.target, down=a.down)
+    return 0
+
+
+def cmd_ips(a):
+    from ray_amd.autoscaler import sdk
+
+    if a.which == "get-head-ip":
+        print(sdk.get_head_node_ip(a.cluster_config))
+    else:
+        print("\n".join(sdk.get_worker_node_ips(a.cluster_config)))
+    return 0
+
+
 def cmd_microbenchmark(a):
     from ray_amd._private import ray_perf
 
@@ -532,6 +576,34 @@ def build_parser():
     s.add_argument("--index", type=int)
     s.add_argument("--wait", type=float, default=0.0, help="seconds to wait for a breakpoint")
     s.set_defaults(fn=cmd_debug)
+
+    # cluster launcher (reference: `ray up/down/exec/rsync-up/rsync-down/get-head-ip`)
+    s = sub.add_parser("up", help="start or update a cluster from a cluster YAML")
+    s.add_argument("cluster_config")
+    s.add_argument("--no-restart", action="store_true")
+    s.add_argument("--restart-only", action="store_true")
+    s.add_argument("-y", "--yes", action="store_true")
+    s.set_defaults(fn=cmd_up)
+    s = sub.add_parser("down", help="tear a cluster down")
+    s.add_argument("cluster_config")
+    s.add_argument("--workers-only", action="store_true")
+    s.add_argument("--keep-min-workers", action="store_true")
+    s.add_argument("-y", "--yes", action="store_true")
+    s.set_defaults(fn=cmd_down)
+    s = sub.add_parser("exec", help="run a command on the cluster's head node")
+    s.add_argument("cluster_config")
+    s.add_argument("cmd")
+    s.set_defaults(fn=cmd_exec)
+    for name, down in (("rsync-up", False), ("rsync-down", True)):
+        s = sub.add_parser(name)
+        s.add_argument("cluster_config")
+        s.add_argument("source")
+        s.add_argument("target")
+        s.set_defaults(fn=cmd_rsync, down=down)
+    for name in ("get-head-ip", "get-worker-ips"):
+        s = sub.add_parser(name)
+        s.add_argument("cluster_config")
+        s.set_defaults(fn=cmd_ips, which=name)
 
     s = sub.add_parser("microbenchmark")
     s.add_argument("--quick", action="store_true")

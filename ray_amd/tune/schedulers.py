@@ -606,3 +606,22 @@ class ResourceChangingScheduler(TrialScheduler):
             trial.pending_resources = dict(new)
             self.num_reallocations += 1
         return decision
+
+
+_SCHEDULERS = {"fifo": "FIFOScheduler", "async_hyperband": "AsyncHyperBandScheduler",
+               "asynchyperband": "AsyncHyperBandScheduler", "asha": "ASHAScheduler",
+               "median_stopping_rule": "MedianStoppingRule", "medianstopping": "MedianStoppingRule",
+               "hyperband": "HyperBandScheduler", "hb_bohb": "HyperBandForBOHB",
+               "pbt": "PopulationBasedTraining", "pbt_replay": "PopulationBasedTrainingReplay",
+               "pb2": "PB2", "resource_changing": "ResourceChangingScheduler"}
+
+
+def create_scheduler(scheduler, **kwargs):
+    """A trial scheduler by name (reference: tune/schedulers/__init__.py
+    create_scheduler); an instance passes through."""
+    if not isinstance(scheduler, str):
+        return scheduler
+    key = scheduler.lower()
+    if key not in _SCHEDULERS:
+        raise ValueError(f"Scheduler must be one of {sorted(_SCHEDULERS)}. Got: {scheduler}")
+    return globals()[_SCHEDULERS[key]](**kwargs)

@@ -74,3 +74,28 @@ class SearchGenerator(SearchAlgorithm):
 
     def __getattr__(self, name):
         return getattr(self.searcher, name)
+
+
+# name -> searcher (reference: tune/search/__init__.py SEARCH_ALG_IMPORT / create_searcher)
+def _searcher_registry():
+    from ray_amd.tune.search import model_based as mb
+
+    reg = {"variant_generator": BasicVariantGenerator, "random": BasicVariantGenerator}
+    for name, attr in (("bayesopt", "BayesOptSearch"), ("hyperopt", "HyperOptSearch"),
+                       ("optuna", "OptunaSearch"), ("tpe", "TPESearch")):
+        cls = globals().get(attr) or getattr(mb, attr, None)
+        if cls is not None:
+            reg[name] = cls
+    return reg
+
+
+def create_searcher(search_alg, **kwargs):
+    """A searcher by name ("variant_generator", "random", "bayesopt", "hyperopt",
+    "optuna", "tpe"), constructed with ``kwargs``; a Searcher instance passes through."""
+    if not isinstance(search_alg, str):
+        return search_alg
+    reg = _searcher_registry()
+    key = search_alg.lower()
+    if key not in reg:
+        raise ValueError(f"Search algorithm must be one of {sorted(reg)}. Got: {search_alg}")
+    return reg[key](**kwargs)

@@ -3,6 +3,7 @@
 from ray_amd._private.serialization import (deregister_serializer,  # noqa: F401
                                             register_serializer)
 from ray_amd.util import iter  # noqa: F401,A004
+from ray_amd.util import ray_debugpy  # noqa: F401
 from ray_amd.util.actor_group import ActorGroup  # noqa: F401
 from ray_amd.util.actor_pool import ActorPool  # noqa: F401
 from ray_amd.util.debug import (disable_log_once_globally,  # noqa: F401

@@ -1,0 +1,62 @@
+"""Round-6 API parity additions: experimental.load_package / set_resource /
+get_object_locations, tune create_searcher / create_scheduler, data.NodeIdStr,
+rllib.TFPolicy and util.ray_debugpy refusals (reference: python/ray/experimental/
+__init__.py, tune/search/__init__.py, tune/schedulers/__init__.py)."""
+import pytest
+
+import ray_amd as ray
+
+
+def test_load_package(tmp_path):
+    (tmp_path / "interface.py").write_text(
+        "import ray_amd as ray\n\n"
+        "@ray.remote\n"
+        "def add(a, b):\n    import os\n    return a + b, os.environ.get('PKG_FLAG')\n\n"
+        "@ray.remote\n"
+        "class Counter:\n    def __init__(self):\n        self.n = 0\n"
+        "    def inc(self):\n        self.n += 1\n        return self.n\n")
+    (tmp_path / "pkg.yaml").write_text(
+        "name: demo\ndescription: a demo package\ninterface_file: interface.py\n"
+        "runtime_env:\n  env_vars:\n    PKG_FLAG: 'on'\n")
+    from ray_amd.experimental import load_package
+
+    ray.init(num_cpus=2)
+    try:
+        pkg = load_package(str(tmp_path / "pkg.yaml"))
+        assert pkg._runtime_env["working_dir"] == str(tmp_path)
+        assert ray.get(pkg.add.remote(2, 3)) == (5, "on")
+        c = pkg.Counter.remote()
+        assert ray.get(c.inc.remote()) == 1
+        from ray_amd.experimental import get_object_locations
+
+        ref = ray.put(b"x" * (1 << 20))
+        locs = get_object_locations([ref])
+        assert locs[ref]["object_size"] >= 1 << 20
+    finally:
+        ray.shutdown()
+    with pytest.raises(DeprecationWarning):
+        from ray_amd.experimental import set_resource
+
+        set_resource("foo", 1)
+
+
+def test_tune_factories_and_refusals():
+    from ray_amd.tune.schedulers import ASHAScheduler, FIFOScheduler, create_scheduler
+    from ray_amd.tune.search import BasicVariantGenerator, create_searcher
+
+    assert isinstance(create_scheduler("fifo"), FIFOScheduler)
+    assert isinstance(create_scheduler("asha", metric="m", mode="max"), ASHAScheduler)
+    assert isinstance(create_searcher("random"), BasicVariantGenerator)
+    with pytest.raises(ValueError):
+        create_scheduler("nope")
+    import ray_amd.data as rd
+
+    assert rd.NodeIdStr is str
+    from ray_amd.rllib import TFPolicy
+
+    with pytest.raises(ImportError, match="tensorflow"):
+        TFPolicy(None, None, {})
+    from ray_amd.util import ray_debugpy
+
+    with pytest.raises(ImportError, match="debugpy"):
+        ray_debugpy.set_trace()
