@@ -158,6 +158,14 @@ def _arrow_col_to_numpy(col):
     import pyarrow as pa
 
     t = col.type
+    if isinstance(t, pa.ExtensionType) and t.extension_name in (
+            "ray.data.arrow_tensor", "ray.data.arrow_variable_shaped_tensor"):
+        # tensor extension columns (written by Ray or data/extensions): N-d numpy back
+        from ray_amd.data.extensions import tensor_extension  # noqa: F401 - registers types
+
+        chunks = col.chunks if isinstance(col, pa.ChunkedArray) else [col]
+        parts = [c.to_numpy() for c in chunks]
+        return np.concatenate(parts) if parts else np.empty(0)
     if (pa.types.is_list(t) or pa.types.is_large_list(t) or pa.types.is_fixed_size_list(t)) \
             and col.null_count == 0:
         try:

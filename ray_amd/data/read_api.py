@@ -166,6 +166,10 @@ def read_parquet(paths, *, columns=None, include_paths=False, partitioning="hive
     def rd(f):
         import pyarrow.parquet as pq
 
+        # tensor extension columns (ray.data.arrow_tensor) must be registered in the
+        # reading process, or they load as plain lists
+        from ray_amd.data.extensions import tensor_extension  # noqa: F401
+
         return pq.read_table(f, columns=columns, partitioning=None)
 
     return _file_ds(paths, [".parquet"], rd, include_paths, partitioning, partition_filter)

@@ -60,3 +60,23 @@ def test_tune_factories_and_refusals():
 
     with pytest.raises(ImportError, match="debugpy"):
         ray_debugpy.set_trace()
+
+
+def test_dummy_trainer_and_aliases():
+    import ray_amd.data as rd
+    from ray_amd.cloudpickle import dumps, loads
+    from ray_amd.train import ScalingConfig
+    from ray_amd.train.util import DummyTrainer
+    from ray_amd.tune.analysis import ExperimentAnalysis  # noqa: F401
+    from ray_amd.tune.experiment import Experiment, _convert_to_experiment_list
+
+    assert loads(dumps(lambda x: x * 3))(2) == 6
+    exps = _convert_to_experiment_list({"e1": {"run": lambda c: None}})
+    assert len(exps) == 1 and isinstance(exps[0], Experiment)
+    ray.init(num_cpus=4)
+    try:
+        r = DummyTrainer(scaling_config=ScalingConfig(num_workers=2),
+                         datasets={"train": rd.range(4000)}, batch_size=500).fit()
+        assert r.metrics["rows_read"] == 2000 and r.metrics["batches_read"] == 4
+    finally:
+        ray.shutdown()
