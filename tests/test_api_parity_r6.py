@@ -80,3 +80,53 @@ def test_dummy_trainer_and_aliases():
         assert r.metrics["rows_read"] == 2000 and r.metrics["batches_read"] == 4
     finally:
         ray.shutdown()
+
+
+def test_tune_utils():
+    from ray_amd.tune.utils import (UtilMonitor, deep_update, diagnose_serialization,
+                                    flatten_dict, merge_dicts, unflattened_lookup,
+                                    warn_if_slow)
+
+    assert flatten_dict({"a": {"b": 1, "c": {"d": 2}}, "e": 3}) == {"a/b": 1, "a/c/d": 2,
+                                                                     "e": 3}
+    assert merge_dicts({"a": {"b": 1}}, {"a": {"c": 2}}) == {"a": {"b": 1, "c": 2}}
+    with pytest.raises(Exception):
+        deep_update({"a": 1}, {"zz": 2})
+    assert unflattened_lookup("a/1/b", {"a": [0, {"b": 7}]}) == 7
+    assert unflattened_lookup("x/y", {}, default=None) is None
+    import threading
+
+    lock = threading.Lock()
+    assert diagnose_serialization(lambda: 1) is True
+    bad = diagnose_serialization(lambda: lock.acquire())
+    assert "lock" in bad
+    m = UtilMonitor(delay=0.05)
+    import time
+
+    time.sleep(0.2)
+    m.stop()
+    assert "cpu_util_percent" in m.get_data().get("perf", {})
+    with warn_if_slow("noop"):
+        pass
+
+
+def test_workflow_filesystem_storage(tmp_path):
+    import asyncio
+
+    from ray_amd.workflow.storage import FilesystemStorage, KeyNotFoundError, Storage
+
+    st = FilesystemStorage(str(tmp_path / "wf"))
+    assert isinstance(st, Storage)
+
+    async def run():
+        k = st.make_key("wf1", "steps", "a")
+        await st.put(k, {"x": 1}, is_json=True)
+        await st.put(st.make_key("wf1", "steps", "b"), [1, 2, 3])
+        assert await st.get(k, is_json=True) == {"x": 1}
+        assert await st.scan_prefix("wf1/steps") == ["a", "b"]
+        await st.delete_prefix("wf1")
+        with pytest.raises(KeyNotFoundError):
+            await st.get(k)
+
+    asyncio.run(run())
+    assert st.storage_url.startswith("file://")
