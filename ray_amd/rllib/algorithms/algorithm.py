@@ -144,6 +144,15 @@ class Algorithm:
         self.config = config
         self.cfg = config.to_dict()
         self.cfg["module_kind"] = getattr(self, "module_kind", "actor_critic")
+        mcfg = self.cfg.get("model") or {}
+        if isinstance(mcfg.get("custom_model"), str):
+            # the driver's ModelCatalog registration travels with the config to the
+            # runner and learner processes (reference: the registry in the GCS KV)
+            from ray_amd.rllib.models import ModelCatalog
+
+            cls = ModelCatalog._custom_models.get(mcfg["custom_model"])
+            if cls is not None:
+                self.cfg["model"] = dict(mcfg, custom_model=cls)
         if type(self).validate_env is not Algorithm.validate_env:  # overridden: runners call it
             self.cfg["_validate_env"] = type(self).validate_env
         probe = make_env(config.env, config.env_config)

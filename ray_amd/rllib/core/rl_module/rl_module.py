@@ -294,6 +294,10 @@ def build_module(cfg: dict, observation_space, action_space, module_id=None):
         if isinstance(m, TorchRLModule):
             return _UserModuleAdapter(m)
         return m
+    if mc.get("custom_model"):  # an old-stack ModelV2 (rllib/models ModelCatalog)
+        from ray_amd.rllib.models import _custom_model_module
+
+        return _UserModuleAdapter(_custom_model_module(cfg, observation_space, action_space))
     if mc.get("use_lstm"):
         return LSTMActorCritic(observation_space, action_space, mc)
     return D.RLModule(observation_space, action_space, mc)
