@@ -208,6 +208,7 @@ class Algorithm:
         self._runners = FaultTolerantActorManager(restore_fn=self._restore_runner)
         self._last_weights_ref = None
         self._policy_server = None
+        self._policy_server_local = None
         if nr > 0 and float(getattr(config, "num_gpus_per_policy_server", 0) or 0) > 0:
             self._start_policy_server(config, nr, probe)
         if nr > 0:
@@ -350,9 +351,18 @@ class Algorithm:
         fn = functools.partial(build_module, dict(self.cfg), probe.observation_space,
                                probe.action_space)
         B = int(config.num_envs_per_env_runner)
+        args = (fn, nr, B, tuple(probe.observation_space.shape), int(probe.action_space.n))
+        import torch
+
+        if int(getattr(config, "num_learners", 0) or 0) == 0 and torch.cuda.is_available():
+            # local learner: the server thread lives in this process and shares the
+            # learner's GPU context (its own stream; graph captures take turns through
+            # ops.graph_lock) — no second process time-slicing the GPU with the learner
+            self._policy_server_local = PolicyServer(*args)
+            self.cfg["_policy_server"] = self._policy_server_local.mailbox()
+            return
         srv = ray.remote(PolicyServer).options(
-            num_gpus=float(config.num_gpus_per_policy_server), num_cpus=1).remote(
-            fn, nr, B, tuple(probe.observation_space.shape), int(probe.action_space.n))
+            num_gpus=float(config.num_gpus_per_policy_server), num_cpus=1).remote(*args)
         self._policy_server = srv
         self.cfg["_policy_server"] = ray.get(srv.mailbox.remote())
 
@@ -361,6 +371,8 @@ class Algorithm:
         self.weights_version += 1
         if self._policy_server is not None:
             self._policy_server.set_weights.remote(weights, self.weights_version)
+        if getattr(self, "_policy_server_local", None) is not None:
+            self._policy_server_local.set_weights(weights, self.weights_version)
         if self._runners.num_actors():
             ref = ray.put(weights)
             self._last_weights_ref = ref
@@ -1153,6 +1165,9 @@ class Algorithm:
             except Exception:  # noqa: BLE001
                 pass
             self._policy_server = None
+        if getattr(self, "_policy_server_local", None) is not None:
+            self._policy_server_local.shutdown()
+            self._policy_server_local = None
         for r in self._eval_runners:
             try:
                 ray.kill(r)

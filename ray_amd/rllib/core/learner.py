@@ -1363,8 +1363,10 @@ class Learner(TorchLearner):
             lt.release_stream(side)
         except (OSError, RuntimeError, AttributeError):
             pass
+        from ray_amd.ops.graph_lock import CAPTURE_LOCK
+
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with CAPTURE_LOCK, torch.cuda.graph(graph):  # an in-process policy server waits
             body()
         self.flat.zero_grad()
         return graph

@@ -74,8 +74,10 @@ class GraphedDiscretePolicy:
                 self._body()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        from ray_amd.ops.graph_lock import CAPTURE_LOCK
+
         g = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(g):
+        with CAPTURE_LOCK, torch.no_grad(), torch.cuda.graph(g):
             self._body()
         self.graph = g
 
@@ -87,8 +89,11 @@ class GraphedDiscretePolicy:
         else:
             self.u_np[:, self.n] = 0.0
             self.u_np[:, :self.n] = 0.5
-        self.graph.replay()
-        torch.cuda.current_stream(self.device).synchronize()
+        from ray_amd.ops.graph_lock import CAPTURE_LOCK
+
+        with CAPTURE_LOCK:
+            self.graph.replay()
+            torch.cuda.current_stream(self.device).synchronize()
         h = self.out_np
         return h[:, 0].astype(np.int64), h[:, 1], h[:, 2:]
 

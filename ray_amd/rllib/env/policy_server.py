@@ -18,6 +18,11 @@ owns the GPU work:
   step costs one memcpy each way plus the batched forward, with no RPC and no GPU context
   in the runner.
 
+With a local learner (``num_learners=0``) the server is a thread of the learner's own
+process: one GPU context, the forward passes on their own stream beside the learner's
+kernels, HIP-graph captures serialized through ``ops.graph_lock``. With remote learners it
+is an actor holding ``num_gpus_per_policy_server`` of a GPU.
+
 Weights reach the server through ``set_weights`` beside the runners' weight sync. The
 uniforms are drawn by each runner from its own generator, so the actions are the same as
 the runner's local GPU graph path would draw for the same weights.
@@ -67,8 +72,8 @@ class _Layout:
 
 
 class PolicyServer:
-    """Actor body (``ray.remote(num_gpus=...)(PolicyServer)``): ``module_fn`` builds the
-    RLModule; the mailbox has ``n_slots`` slots of ``B`` envs."""
+    """In-process server or actor body (``ray.remote(num_gpus=...)(PolicyServer)``):
+    ``module_fn`` builds the RLModule; the mailbox has ``n_slots`` slots of ``B`` envs."""
 
     def __init__(self, module_fn, n_slots, B, obs_shape, n_actions):
         import torch
@@ -113,15 +118,22 @@ class PolicyServer:
               for k, v in w.items()}
         with self._lock:  # copies into the captured parameter storage
             self.module.load_state_dict(sd)
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
         self.version = version if version is not None else self.version
 
     def stats(self):
         return {"batches": self.batches, "rows": self.rows}
 
     def _loop(self):
+        import torch
+
+        from ray_amd.ops.graph_lock import CAPTURE_LOCK
+
         B, n = self.lay.B, self.lay.n
         pol = self.pol
+        # its own stream: in the learner's process the forward passes overlap the
+        # learner's kernels instead of queueing behind them
+        torch.cuda.set_stream(torch.cuda.Stream(self.device))
         idle_spins = 0
         while not self._stop:
             ready = np.flatnonzero(self.state == REQUEST)
@@ -137,10 +149,9 @@ class PolicyServer:
                 for j, s in enumerate(ready):
                     pol.obs_np[j * B:(j + 1) * B] = self.obs[s]
                     pol.u_np[j * B:(j + 1) * B] = self.u[s]
-                pol.graph.replay()
-                import torch
-
-                torch.cuda.current_stream(self.device).synchronize()
+                with CAPTURE_LOCK:
+                    pol.graph.replay()
+                    torch.cuda.current_stream(self.device).synchronize()
                 for j, s in enumerate(ready):
                     self.out[s][...] = pol.out_np[j * B:(j + 1) * B]
             self.state[ready] = RESPONSE

@@ -96,7 +96,8 @@ def test_gpu_env_runner_fragment(cuda_device):
     assert (d[..., 5] - d[..., 0]).mean() > 4.0
 
 
-def test_policy_server_serves_all_runners(cuda_device):
+@pytest.mark.parametrize("remote_learner", [False, True])
+def test_policy_server_serves_all_runners(cuda_device, remote_learner):
     """num_gpus_per_policy_server: two CPU env runners hand their policy forward to one GPU
     process through the shared-memory mailbox; a training iteration runs through it, the
     fragments' log-probs match their recorded logits, and weight syncs reach the server."""
@@ -110,12 +111,18 @@ def test_policy_server_serves_all_runners(cuda_device):
                              rollout_fragment_length=20, num_gpus_per_policy_server=0.5)
                 .training(train_batch_size=120, minibatch_size=60, num_epochs=1,
                           model={"vf_share_layers": True})
+                .learners(num_learners=1 if remote_learner else 0,
+                          num_gpus_per_learner=0.25 if remote_learner else 1)
                 .debugging(seed=1)).build()
-        srv = algo._policy_server
-        assert srv is not None
+        if remote_learner:  # the server is an actor holding its GPU share
+            srv = algo._policy_server
+            assert srv is not None and algo._policy_server_local is None
+        else:  # local learner: the server runs in the learner's process
+            srv = algo._policy_server_local
+            assert srv is not None and algo._policy_server is None
         r = algo.train()
         assert r["num_env_steps_sampled_this_iter"] >= 120
-        st = ray.get(srv.stats.remote())
+        st = ray.get(srv.stats.remote()) if remote_learner else srv.stats()
         assert st["batches"] > 0 and st["rows"] >= 120
         runner = algo._runners.actors()[0] if hasattr(algo._runners, "actors") else None
         if runner is not None:
