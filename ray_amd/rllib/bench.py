@@ -34,8 +34,8 @@ def _envs_per_runner() -> int:
 def _inference_where(runner_gpus: float, server_gpus: float = 0.0) -> str:
     """Where the env runners' policy forward runs (reported in the JSON line)."""
     if server_gpus > 0:
-        return ("gpu policy server (one process: all runners' envs batched into one HIP "
-                "graph per step, shared-memory mailbox)")
+        return ("gpu policy server (all runners' envs batched into one HIP graph per step, "
+                "shared-memory mailbox; in the learner's process with a local learner)")
     if runner_gpus <= 0:
         return "cpu (bf16 Nature-CNN, torch)"
     if os.environ.get("RAY_AMD_RUNNER_GRAPH", "1") == "1":
@@ -53,8 +53,14 @@ def bench_ppo(args):
              ignore_reinit_error=True)
     # env-runner policy inference device: fractional MI355X shares (8 x 0.125) or CPU (0)
     runner_gpus = float(os.environ.get("RAY_AMD_RUNNER_GPUS", "0"))
-    # > 0: one batched GPU inference process for all runners (rllib/env/policy_server.py)
-    server_gpus = float(os.environ.get("RAY_AMD_POLICY_SERVER_GPUS", "0"))
+    # > 0: one batched GPU policy server for all runners (rllib/env/policy_server.py). The
+    # default with a local learner: the server is a thread of the learner's process
+    # (profiles/r6/README.md r6i: 56k sync / 84-89k async against 44-47k / 54-71k with CPU
+    # inference on the same boxes)
+    import torch
+
+    default_srv = "0.5" if n_learners == 0 and torch.cuda.is_available() else "0"
+    server_gpus = float(os.environ.get("RAY_AMD_POLICY_SERVER_GPUS", default_srv))
     sample_async = os.environ.get("RAY_AMD_PPO_ASYNC", "0") == "1"
     # CPU threads per env runner (torch intra-op threads for the Nature-CNN inference)
     runner_cpus = float(os.environ.get("RAY_AMD_RUNNER_CPUS", "1"))
