@@ -656,9 +656,10 @@ class Raylet:
                     continue
                 node = self.sched.pick_node(res, strategy, target, local, hard_l, soft_l)
                 if node == "!":
-                    if isinstance(st, dict) and st.get("type") == "pg" and \
-                            st["pg_id"] not in self.pgs:
-                        self._fail_lease(lr, "placement group was removed")
+                    if isinstance(st, dict) and st.get("type") == "pg" and (
+                            st["pg_id"] not in self.pgs or
+                            self.pgs[st["pg_id"]].state == "REMOVED"):
+                        self._fail_lease(lr, "placement group was removed", pg_removed=True)
                         continue
                     if not lr.warned:
                         lr.warned = True
@@ -726,10 +727,15 @@ class Raylet:
         else:
             self.reply(lr.conn, lr.rid, True, grant)
 
-    def _fail_lease(self, lr, msg):
-        from ray_amd.exceptions import TaskUnschedulableError
+    def _fail_lease(self, lr, msg, pg_removed=False):
+        from ray_amd.exceptions import (ActorPlacementGroupRemoved, TaskPlacementGroupRemoved,
+                                        TaskUnschedulableError)
 
-        err = TaskUnschedulableError(msg)
+        if pg_removed:  # lr.cb is set for actor-creation leases, None for task leases
+            err = (ActorPlacementGroupRemoved if lr.cb is not None else
+                   TaskPlacementGroupRemoved)(msg)
+        else:
+            err = TaskUnschedulableError(msg)
         if lr.cb is not None:
             lr.cb(None, err)
         else:

@@ -26,23 +26,7 @@ from ray_amd.data import preprocessors  # noqa: F401
 from ray_amd.data._executor import ExecutionOptions, ExecutionResources  # noqa: F401
 
 
-class DataContext:
-    _current = None
-
-    def __init__(self):
-        self.target_max_block_size = 128 << 20
-        self.execution_options = ExecutionOptions()
-        self.use_push_based_shuffle = False
-        self.push_based_shuffle_merge_factor = 8
-
-    @classmethod
-    def get_current(cls):
-        if cls._current is None:
-            cls._current = DataContext()
-        return cls._current
-
-
-DatasetContext = DataContext
+from ray_amd.data.context import DataContext, DatasetContext  # noqa: E402,F401
 
 
 def set_progress_bars(enabled: bool) -> bool:

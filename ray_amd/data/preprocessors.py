@@ -7,15 +7,32 @@ kernel (ops/csrc/preprocess.hip) inside an actor pool that holds a GPU."""
 from __future__ import annotations
 
 import os
+from enum import Enum
 
 import numpy as np
 
 
+class PreprocessorNotFittedException(RuntimeError):
+    """``transform`` called on a fittable preprocessor that was never fitted."""
+
+
 class Preprocessor:
+    class FitStatus(str, Enum):
+        NOT_FITTABLE = "NOT_FITTABLE"
+        NOT_FITTED = "NOT_FITTED"
+        PARTIALLY_FITTED = "PARTIALLY_FITTED"  # a Chain with some stages fitted
+        FITTED = "FITTED"
+
     _is_fittable = True
 
     def __init__(self):
         self.stats_ = None
+
+    def fit_status(self) -> "Preprocessor.FitStatus":
+        if not self._is_fittable:
+            return Preprocessor.FitStatus.NOT_FITTABLE
+        return Preprocessor.FitStatus.FITTED if self.stats_ is not None else \
+            Preprocessor.FitStatus.NOT_FITTED
 
     def fit(self, ds):
         if self._is_fittable:
@@ -25,19 +42,53 @@ class Preprocessor:
     def fit_transform(self, ds):
         return self.fit(ds).transform(ds)
 
+    def _check_fitted(self):
+        if self.fit_status() in (Preprocessor.FitStatus.NOT_FITTED,
+                                 Preprocessor.FitStatus.PARTIALLY_FITTED):
+            raise PreprocessorNotFittedException(
+                f"{type(self).__name__} must be fitted before transform")
+
     def transform(self, ds):
-        if self._is_fittable and self.stats_ is None:
-            raise RuntimeError(f"{type(self).__name__} must be fitted before transform")
+        self._check_fitted()
         return ds.map_batches(self._transform_numpy, batch_format="numpy", batch_size=4096)
 
     def transform_batch(self, batch):
+        """One in-memory batch: a dict of arrays, or a pandas DataFrame (returned as one)."""
+        self._check_fitted()
+        try:
+            import pandas as pd
+        except ImportError:  # pragma: no cover
+            pd = None
+        if pd is not None and isinstance(batch, pd.DataFrame):
+            out = self._transform_numpy({c: batch[c].to_numpy() for c in batch.columns})
+            return pd.DataFrame({k: (list(v) if getattr(v, "ndim", 1) > 1 else v)
+                                 for k, v in out.items()})
         return self._transform_numpy(dict(batch))
+
+    def serialize(self) -> str:
+        """This (fitted) preprocessor as a string (cloudpickle, base64)."""
+        import base64
+
+        import cloudpickle
+
+        return base64.b64encode(cloudpickle.dumps(self)).decode()
+
+    @staticmethod
+    def deserialize(serialized: str) -> "Preprocessor":
+        import base64
+
+        import cloudpickle
+
+        return cloudpickle.loads(base64.b64decode(serialized))
 
     def _fit(self, ds):
         pass
 
     def _transform_numpy(self, batch):
         raise NotImplementedError
+
+    def __repr__(self):
+        return f"{type(self).__name__}()"
 
 
 class StandardScaler(Preprocessor):
@@ -239,6 +290,17 @@ class Chain(Preprocessor):
     def __init__(self, *preprocessors):
         super().__init__()
         self.preprocessors = preprocessors
+
+    def fit_status(self):
+        st = [p.fit_status() for p in self.preprocessors]
+        F = Preprocessor.FitStatus
+        fittable = [x for x in st if x != F.NOT_FITTABLE]
+        if not fittable:
+            return F.NOT_FITTABLE
+        if all(x == F.FITTED for x in fittable):
+            return F.FITTED
+        return F.NOT_FITTED if all(x == F.NOT_FITTED for x in fittable) else \
+            F.PARTIALLY_FITTED
 
     def fit(self, ds):
         for p in self.preprocessors:

@@ -101,6 +101,33 @@ class TaskUnschedulableError(RayError):
     pass
 
 
+class TaskPlacementGroupRemoved(TaskUnschedulableError):
+    """The placement group a task was scheduled into was removed before it ran."""
+
+
+class ActorPlacementGroupRemoved(ActorUnschedulableError):
+    """The placement group an actor was scheduled into was removed before it started."""
+
+
+class UserCodeException(RayError):
+    """An exception raised by user code run by a library (Ray Data UDFs and the like)."""
+
+
+class RpcError(RayError):
+    """A control-plane RPC failed (``rpc_code`` carries the transport's status, if any)."""
+
+    def __init__(self, message, rpc_code=None):
+        self.rpc_code = rpc_code
+        super().__init__(message)
+
+    def __reduce__(self):
+        return (RpcError, (str(self), self.rpc_code))
+
+
+class ObjectRefStreamEndOfStreamError(RayError, StopIteration):
+    """Reading past the last item of a streaming generator's ObjectRef stream."""
+
+
 class WorkerCrashedError(RayError):
     def __init__(self, msg="The worker died unexpectedly while executing this task."):
         super().__init__(msg)

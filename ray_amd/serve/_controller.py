@@ -19,12 +19,12 @@ actors mapping. Its control loop never blocks on a replica:
 from __future__ import annotations
 
 import asyncio
-import math
 import time
 import uuid
 from collections import deque
 
 import ray_amd as ray
+from ray_amd.serve.autoscaling_policy import resolve_policy
 
 CONTROLLER_NAME = "SERVE_CONTROLLER_ACTOR"
 SERVE_NAMESPACE = "serve"
@@ -54,8 +54,7 @@ class _DeploymentState:
         self.status = "UPDATING"
         self.error = None
         self.start_failures = 0
-        self.over_since = None
-        self.under_since = None
+        self.policy_state = {}  # the autoscaling policy's memory between ticks
         self.retiring = {}  # old-version replicas serving until their successors are up
         self.hc = {}  # rid -> (last check start time, task or None, consecutive failures)
         self.load = {}  # rid -> (ongoing, time)
@@ -522,35 +521,27 @@ class ServeController:
                 while st.samples and now - st.samples[0][0] > look:
                     st.samples.popleft()
                 avg = sum(v for _, v in st.samples) / len(st.samples)
-                tgt = asc.get("target_ongoing_requests", asc.get(
-                    "target_num_ongoing_requests_per_replica", 2))
                 cur = len(st.replicas) + len(st.starting)
-                desired = math.ceil(avg / max(tgt, 1e-9)) if avg > 1e-9 else \
-                    asc.get("min_replicas", 1)
-                # gain on each decision (reference: AutoscalingConfig.upscaling_factor /
-                # downscaling_factor): move only that fraction of the way to the target
-                if desired > cur and asc.get("upscaling_factor"):
-                    desired = cur + math.ceil((desired - cur) * asc["upscaling_factor"])
-                elif desired < cur and asc.get("downscaling_factor"):
-                    desired = cur - max(1, math.floor((cur - desired) *
-                                                      asc["downscaling_factor"]))
+                # the decision itself is the deployment's policy (serve/autoscaling_policy.py;
+                # reference: AutoscalingConfig._policy), called with the reference's kwargs
+                st.policy_state["now"] = now
+                try:
+                    policy = resolve_policy(asc.get("policy"))
+                    desired = int(policy(
+                        curr_target_num_replicas=cur, total_num_requests=avg,
+                        num_running_replicas=len(st.replicas), config=asc,
+                        capacity_adjusted_min_replicas=asc.get("min_replicas", 1),
+                        capacity_adjusted_max_replicas=asc.get("max_replicas", 10),
+                        policy_state=st.policy_state))
+                except Exception as e:  # noqa: BLE001 - a broken user policy: keep serving
+                    st.error = f"autoscaling policy failed: {e!r}"
+                    continue
                 desired = max(asc.get("min_replicas", 1), min(asc.get("max_replicas", 10),
                                                               desired))
-                if desired > cur:
-                    st.under_since = None
-                    st.over_since = st.over_since or now
-                    if now - st.over_since >= asc.get("upscale_delay_s", 30.0):
-                        st.target = desired
-                        st.over_since = None
-                elif desired < cur:
-                    st.over_since = None
-                    st.under_since = st.under_since or now
-                    if now - st.under_since >= asc.get("downscale_delay_s", 600.0):
-                        st.target = desired
-                        st.under_since = None
-                        st.samples.clear()
-                else:
-                    st.over_since = st.under_since = None
+                if desired != cur:
+                    st.target = desired
+                if st.policy_state.pop("reset_samples", False):
+                    st.samples.clear()
 
     # ------------------------------------------------------------------ per-node proxies
     def _proxy_tick(self, now):

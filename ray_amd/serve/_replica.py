@@ -207,6 +207,9 @@ class Replica:
             self.asgi = app
             if hasattr(self.obj, "__serve_bind_asgi__"):
                 self.obj.__serve_bind_asgi__(app)
+        elif getattr(self.obj, "_serve_asgi_instance_app", None) is not None:
+            # an ASGI app the constructor builds (gradio_integrations.GradioIngress)
+            self.asgi = self.obj._serve_asgi_instance_app
         self.ongoing = 0
         self.total = 0
         self.started = time.time()

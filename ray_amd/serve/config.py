@@ -8,7 +8,7 @@ apply to the rest."""
 from __future__ import annotations
 
 from enum import Enum
-from typing import Optional
+from typing import Any, Optional
 
 from pydantic import BaseModel, Field, model_validator
 
@@ -31,6 +31,9 @@ class AutoscalingConfig(BaseModel):
     downscaling_factor: Optional[float] = Field(default=None, gt=0)
     downscale_delay_s: float = Field(default=600.0, ge=0)
     upscale_delay_s: float = Field(default=30.0, ge=0)
+    # the decision function (serve/autoscaling_policy.py): a callable or an import path;
+    # None = replica_queue_length_autoscaling_policy
+    policy: Optional[Any] = None
 
     @model_validator(mode="after")
     def _replica_bounds(self):
@@ -83,6 +86,9 @@ def normalize_autoscaling_config(cfg) -> Optional[dict]:
     if isinstance(cfg, AutoscalingConfig):
         return cfg.to_controller_dict()
     if isinstance(cfg, dict):
+        if "_policy" in cfg:  # the reference's private spelling
+            cfg = dict(cfg)
+            cfg["policy"] = cfg.pop("_policy")
         known = set(AutoscalingConfig.model_fields)
         unknown = set(cfg) - known
         if unknown:

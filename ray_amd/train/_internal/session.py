@@ -123,8 +123,10 @@ _session: _Session | None = None
 
 def _get_session(required=True) -> _Session | None:
     if _session is None and required:
-        raise RuntimeError("`train.report` / `train.get_context` must be called from inside a "
-                           "training function run by a ray_amd Trainer.")
+        from ray_amd.train.error import SessionMisuseError
+
+        raise SessionMisuseError("`train.report` / `train.get_context` must be called from "
+                                 "inside a training function run by a ray_amd Trainer.")
     return _session
 
 

@@ -24,6 +24,7 @@ from ray_amd.train._checkpoint import Checkpoint
 from ray_amd.train._internal.session import TrainContext
 from ray_amd.train._internal.worker_group import WorkerGroup
 from ray_amd.train.backend import BackendConfig
+from ray_amd.train.base_trainer import BaseTrainer
 from ray_amd.train.result import Result
 
 
@@ -77,7 +78,7 @@ class _CheckpointManager:
         return sorted(self.items, key=lambda x: x[1].get(attr, 0), reverse=rev)[0][0]
 
 
-class DataParallelTrainer:
+class DataParallelTrainer(BaseTrainer):
     _default_backend_config = BackendConfig
 
     def __init__(self, train_loop_per_worker, *, train_loop_config: dict | None = None,

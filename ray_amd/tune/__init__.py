@@ -23,9 +23,6 @@ from ray_amd.tune.registry import (CLIReporter, Experiment,  # noqa: F401
 from ray_amd.air.config import SyncConfig  # noqa: F401
 from ray_amd.tune.tuner import ResumeConfig  # noqa: F401
 
+from ray_amd.tune.error import TuneError  # noqa: E402,F401
 
-
-class TuneError(RuntimeError):
-    """A Tune experiment failed (reference: python/ray/tune/error.py); tune.run raises it
-    when trials errored and raise_on_failed_trial is left True."""
 

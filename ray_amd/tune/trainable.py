@@ -118,7 +118,9 @@ _fn_session: _FnSession | None = None
 def function_report(metrics, checkpoint=None):
     s = _fn_session
     if s is None:
-        raise RuntimeError("report() called outside of a Tune / Train session")
+        from ray_amd.train.error import SessionMisuseError
+
+        raise SessionMisuseError("report() called outside of a Tune / Train session")
     if s.stop:
         raise SystemExit(0)
     s.iteration += 1

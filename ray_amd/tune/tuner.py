@@ -795,9 +795,10 @@ def _trainer_to_trainable(trainer):
         from ray_amd.tune.trainable import function_report
 
         tr = copy.copy(trainer)
-        tlc = dict(tr.train_loop_config or {})
-        tlc.update(config.get("train_loop_config", {}))
-        tr.train_loop_config = tlc
+        if hasattr(tr, "train_loop_config"):
+            tlc = dict(tr.train_loop_config or {})
+            tlc.update(config.get("train_loop_config", {}))
+            tr.train_loop_config = tlc
         if "scaling_config" in config:
             tr.scaling_config = config["scaling_config"]
         res = tr.fit()
@@ -843,9 +844,9 @@ class Tuner:
         os.makedirs(exp_dir, exist_ok=True)
         trainable = self.trainable
         resources = {"CPU": 1}
-        from ray_amd.train.data_parallel_trainer import DataParallelTrainer
+        from ray_amd.train.base_trainer import BaseTrainer
 
-        if isinstance(trainable, DataParallelTrainer):
+        if isinstance(trainable, BaseTrainer):
             resources = {"CPU": 0}
             trainable = _trainer_to_trainable(trainable)
         elif getattr(trainable, "_ray_amd_resources", None):

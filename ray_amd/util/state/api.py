@@ -357,17 +357,33 @@ class StateApiClient:
     def __init__(self, address: Optional[str] = None):
         self.address = address
 
-    def list(self, resource: str, filters=None, limit=DEFAULT_LIMIT, **kw):
+    @staticmethod
+    def _name(resource) -> str:
+        return str(getattr(resource, "value", resource)).lower()
+
+    def list(self, resource, options=None, raise_on_missing_output=True,
+             _explain=False, filters=None, limit=DEFAULT_LIMIT, **kw):
+        """``resource``: a name or ``common.StateResource``; ``options``: a
+        ``common.ListApiOptions`` (its filters / limit win over the keywords)."""
+        if options is not None:
+            filters, limit = options.filters, options.limit
         fn = {"actors": list_actors, "tasks": list_tasks, "objects": list_objects,
               "nodes": list_nodes, "workers": list_workers, "jobs": list_jobs,
               "placement_groups": list_placement_groups,
-              "runtime_envs": list_runtime_envs}[str(resource).lower()]
+              "runtime_envs": list_runtime_envs,
+              "cluster_events": list_cluster_events}[self._name(resource)]
         return fn(self.address, filters=filters, limit=limit)
 
-    def summary(self, resource: str, **kw):
-        return {"tasks": summarize_tasks, "actors": summarize_actors,
-                "objects": summarize_objects}[str(resource).lower()](self.address)
+    def get(self, resource, id: str, options=None, _explain=False):
+        fn = {"actors": get_actor, "tasks": get_task, "objects": get_objects,
+              "nodes": get_node, "workers": get_worker, "jobs": get_job,
+              "placement_groups": get_placement_group}[self._name(resource)]
+        return fn(id, self.address)
 
+    def summary(self, resource, options=None, raise_on_missing_output=True, _explain=False,
+                **kw):
+        return {"tasks": summarize_tasks, "actors": summarize_actors,
+                "objects": summarize_objects}[self._name(resource)](self.address)
 
 
 # ---------------------------------------------------------------------------- logs

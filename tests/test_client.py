@@ -123,3 +123,31 @@ def test_client_end_to_end(client_server):
     assert "CLIENT_OK" in r.stdout, r.stdout + r.stderr
     # the client's session released its server-side refs/actors on disconnect
     time.sleep(0.5)
+
+
+CONNECT = textwrap.dedent("""
+    from ray_amd.util.client_connect import connect, disconnect
+    import ray_amd as ray
+
+    info = connect("127.0.0.1:%d")
+    assert "ray_version" in info
+
+    @ray.remote
+    def sq(x):
+        return x * x
+
+    assert ray.get(sq.remote(7)) == 49
+    disconnect()
+    assert not ray.is_initialized()
+    print("CONNECT_OK")
+""")
+
+
+def test_client_connect_module(client_server):
+    """util.client_connect.connect / disconnect (reference: python/ray/util/
+    client_connect.py) over the same client server."""
+    env = dict(os.environ, PYTHONPATH=REPO)
+    env.pop("RAY_ADDRESS", None)
+    r = subprocess.run([sys.executable, "-c", CONNECT % client_server], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert "CONNECT_OK" in r.stdout, r.stdout + r.stderr

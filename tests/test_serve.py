@@ -124,6 +124,38 @@ def test_autoscaling(cluster):
     assert n > 1
 
 
+def test_custom_autoscaling_policy(cluster):
+    """autoscaling_config["policy"] replaces the decision function (reference:
+    AutoscalingConfig._policy): called with the reference's keyword arguments; its answer
+    is clamped to [min_replicas, max_replicas]."""
+    seen = []
+
+    def always_three(curr_target_num_replicas, total_num_requests, num_running_replicas,
+                     config, capacity_adjusted_min_replicas, capacity_adjusted_max_replicas,
+                     policy_state):
+        policy_state["calls"] = policy_state.get("calls", 0) + 1
+        return 3
+
+    @serve.deployment(autoscaling_config={"min_replicas": 1, "max_replicas": 2,
+                                          "_policy": always_three})
+    class Idle:
+        def __call__(self):
+            return 1
+
+    h = serve.run(Idle.bind(), name="custom_asc", route_prefix=None)
+    assert h.remote().result() == 1
+    deadline = time.time() + 15
+    n = 1
+    while time.time() < deadline:
+        n = serve.status()["custom_asc"]["deployments"]["Idle"]["replica_states"]["RUNNING"]
+        if n == 2:
+            break
+        time.sleep(0.2)
+    assert n == 2  # the policy's 3 clamped to max_replicas, with no load at all
+    serve.delete("custom_asc")
+    del seen
+
+
 def test_fastapi_ingress(cluster):
     from fastapi import FastAPI
 
