@@ -20,8 +20,9 @@ from ray_amd.data.integrations import (from_dask, from_mars, from_modin,  # noqa
                                        from_spark, from_tf, read_bigquery,
                                        read_databricks_tables, read_mongo)
 from ray_amd.data.datasource import (BlockBasedFileDatasink, Datasink,  # noqa: F401
-                                     Datasource, RandomAccessDataset, ReadTask,
-                                     RowBasedFileDatasink, read_sql, read_webdataset)
+                                     Datasource, ReadTask, RowBasedFileDatasink,
+                                     FileBasedDatasource, read_sql, read_webdataset)
+from ray_amd.data.random_access_dataset import RandomAccessDataset  # noqa: F401
 from ray_amd.data import preprocessors  # noqa: F401
 from ray_amd.data._executor import ExecutionOptions, ExecutionResources  # noqa: F401
 

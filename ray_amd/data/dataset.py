@@ -432,7 +432,15 @@ def _write_local(blk, path, fmt, idx, kw):
             _write_local(B.take_idx(rest, np.asarray(rows)), sub, fmt, idx, kw)
         return n
     os.makedirs(path, exist_ok=True)
-    base = os.path.join(path, f"part_{idx:06d}")
+    fp = kw.pop("filename_provider", None)
+    for k in ("try_create_dir", "arrow_open_stream_args", "ray_remote_args", "concurrency",
+              "num_rows_per_file", "min_rows_per_file"):
+        kw.pop(k, None)
+    if fp is not None:  # a datasource.FilenameProvider names the block's file
+        name = fp.get_filename_for_block(blk, idx, 0)
+        base = os.path.join(path, os.path.splitext(name)[0])
+    else:
+        base = os.path.join(path, f"part_{idx:06d}")
     if fmt == "parquet":
         import pyarrow.parquet as pq
 
@@ -1162,7 +1170,7 @@ class Dataset:
                  for i, (r, _) in enumerate(X.execute(self._plan))])
 
     def to_random_access_dataset(self, key: str, num_workers: int | None = None):
-        from ray_amd.data.datasource import RandomAccessDataset
+        from ray_amd.data.random_access_dataset import RandomAccessDataset
 
         return RandomAccessDataset(self, key, num_workers or 2)
 

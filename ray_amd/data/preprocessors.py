@@ -319,6 +319,58 @@ class Chain(Preprocessor):
         return b
 
 
+class TorchVisionPreprocessor(Preprocessor):
+    """Apply a torchvision-style transform (tensor or ndarray in, tensor or ndarray out) to
+    image columns, per image or (``batched=True``) to the whole (B, H, W, C) batch
+    (reference: data/preprocessors/torch.py). Any callable works; torchvision itself is not
+    needed (not installed here)."""
+
+    _is_fittable = False
+
+    def __init__(self, columns, transform, output_columns=None, batched: bool = False):
+        super().__init__()
+        output_columns = output_columns or columns
+        if len(columns) != len(output_columns):
+            raise ValueError(f"The length of columns should match the length of "
+                             f"output_columns: {columns} vs {output_columns}.")
+        self._columns, self._output_columns = list(columns), list(output_columns)
+        self._fn, self._batched = transform, batched
+
+    def _apply(self, arr):
+        import torch
+
+        try:
+            out = self._fn(torch.as_tensor(np.ascontiguousarray(arr)))
+        except TypeError:
+            out = self._fn(arr)
+        if isinstance(out, torch.Tensor):
+            out = out.detach().cpu().numpy()
+        if not isinstance(out, np.ndarray):
+            raise ValueError("TorchVisionPreprocessor expected the transform to return a "
+                             f"torch.Tensor or np.ndarray, got {type(out).__name__}")
+        return out
+
+    def _transform_numpy(self, b):
+        b = dict(b)
+        for c, oc in zip(self._columns, self._output_columns):
+            col = b[c]
+            if self._batched:
+                b[oc] = self._apply(np.asarray(col))
+            else:
+                outs = [self._apply(x) for x in col]
+                if outs and all(o.shape == outs[0].shape for o in outs):
+                    b[oc] = np.stack(outs)
+                else:
+                    arr = np.empty(len(outs), dtype=object)
+                    arr[:] = outs
+                    b[oc] = arr
+        return b
+
+    def __repr__(self):
+        return (f"TorchVisionPreprocessor(columns={self._columns}, "
+                f"output_columns={self._output_columns}, transform={self._fn!r})")
+
+
 class _GPUNormalizeUDF:
     def __init__(self, column, mean, std, out_dtype, resize, keep_on_device=False):
         import torch

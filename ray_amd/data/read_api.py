@@ -2,7 +2,6 @@
 
 from __future__ import annotations
 
-import glob
 import os
 
 import numpy as np
@@ -100,183 +99,105 @@ def from_huggingface(dataset) -> Dataset:
     return from_items([dict(r) for r in dataset])
 
 
-def _expand(paths, exts=None):
-    if isinstance(paths, str):
-        paths = [paths]
-    out = []
-    for p in paths:
-        if os.path.isdir(p):
-            for root, _, files in os.walk(p):
-                for f in sorted(files):
-                    if exts is None or any(f.endswith(e) for e in exts):
-                        out.append(os.path.join(root, f))
-        elif any(c in p for c in "*?["):
-            out.extend(sorted(glob.glob(p)))
-        else:
-            out.append(p)
-    if not out:
-        raise FileNotFoundError(f"no files found for {paths}")
+_FILE_KW = ("filesystem", "schema", "open_stream_args", "arrow_open_stream_args",
+            "meta_provider", "partition_filter", "partitioning", "ignore_missing_paths",
+            "shuffle", "include_paths", "file_extensions")
+
+
+def _file_kw(kw: dict, partitioning_default="hive") -> dict:
+    """The FileBasedDatasource keywords of a read_* call (the rest are format options)."""
+    out = {k: kw.pop(k) for k in list(kw) if k in _FILE_KW}
+    if "arrow_open_stream_args" in out:
+        out["open_stream_args"] = out.pop("arrow_open_stream_args")
+    out.setdefault("partitioning", partitioning_default)
+    for k in ("parallelism", "override_num_blocks", "ray_remote_args", "concurrency",
+              "tensor_column_schema", "dataset_kwargs"):
+        kw.pop(k, None)
     return out
 
 
-def _hive_values(f: str, paths) -> dict:
-    """``key=value`` directory segments between an input directory and the file
-    (reference: datasource/partitioning.py Partitioning("hive")); values stay strings."""
-    out = {}
-    for p in ([paths] if isinstance(paths, str) else paths):
-        p = os.path.abspath(p)
-        af = os.path.abspath(f)
-        if os.path.isdir(p) and af.startswith(p.rstrip(os.sep) + os.sep):
-            for seg in os.path.relpath(os.path.dirname(af), p).split(os.sep):
-                k, sep, v = seg.partition("=")
-                if sep and k:
-                    out[k] = v
-            break
-    return out
+def read_parquet(paths, *, columns=None, **kw) -> Dataset:
+    from ray_amd.data.datasource.formats import ParquetDatasource
+
+    return read_datasource(ParquetDatasource(paths, columns=columns, **_file_kw(kw)))
 
 
-def _file_ds(paths, exts, reader, include_paths=False, partitioning="hive",
-             partition_filter=None):
-    files = _expand(paths, exts)
-    parts = {f: (_hive_values(f, paths) if partitioning == "hive" else {}) for f in files}
-    if partition_filter is not None:
-        files = [f for f in files if partition_filter(parts[f])]
-        if not files:
-            raise FileNotFoundError(f"partition_filter kept no files of {paths}")
+def read_csv(paths, **kw) -> Dataset:
+    from ray_amd.data.datasource.formats import CSVDatasource
 
-    def mk(f):
-        def r():
-            blk = B.from_batch(reader(f))
-            n = B.num_rows(blk)
-            for k, v in parts[f].items():
-                if k not in blk:
-                    blk[k] = np.array([v] * n, dtype=object)
-            if include_paths:
-                blk["path"] = np.array([f] * B.num_rows(blk), dtype=object)
-            return blk
-        return r
-
-    ds = Dataset(X.Plan(("read", [mk(f) for f in files])))
-    ds._input_files = files
-    return ds
+    fkw = _file_kw(kw)
+    return read_datasource(CSVDatasource(paths, arrow_csv_args=kw, **fkw))
 
 
-def read_parquet(paths, *, columns=None, include_paths=False, partitioning="hive",
-                 partition_filter=None, **kw) -> Dataset:
-    def rd(f):
-        import pyarrow.parquet as pq
+def read_json(paths, *, lines=None, **kw) -> Dataset:
+    from ray_amd.data.datasource.formats import JSONDatasource
 
-        # tensor extension columns (ray.data.arrow_tensor) must be registered in the
-        # reading process, or they load as plain lists
-        from ray_amd.data.extensions import tensor_extension  # noqa: F401
-
-        return pq.read_table(f, columns=columns, partitioning=None)
-
-    return _file_ds(paths, [".parquet"], rd, include_paths, partitioning, partition_filter)
+    return read_datasource(JSONDatasource(paths, lines=lines, **_file_kw(kw)))
 
 
-def read_csv(paths, *, include_paths=False, partitioning="hive", partition_filter=None,
-             **kw) -> Dataset:
-    def rd(f):
-        import pyarrow.csv as pc
+def read_numpy(paths, **kw) -> Dataset:
+    from ray_amd.data.datasource.formats import NumpyDatasource
 
-        return pc.read_csv(f)
-
-    return _file_ds(paths, [".csv"], rd, include_paths, partitioning, partition_filter)
+    return read_datasource(NumpyDatasource(paths, **_file_kw(kw, None)))
 
 
-def read_json(paths, *, include_paths=False, lines=True, partitioning="hive",
-              partition_filter=None, **kw) -> Dataset:
-    def rd(f):
-        import pandas as pd
+def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, **kw):
+    from ray_amd.data.datasource.formats import TextDatasource
 
-        try:
-            return pd.read_json(f, lines=True)
-        except ValueError:
-            return pd.read_json(f)
-
-    return _file_ds(paths, [".json", ".jsonl"], rd, include_paths, partitioning,
-                    partition_filter)
+    return read_datasource(TextDatasource(paths, drop_empty_lines=drop_empty_lines,
+                                          encoding=encoding, **_file_kw(kw, None)))
 
 
-def read_numpy(paths, *, include_paths=False, **kw) -> Dataset:
-    return _file_ds(paths, [".npy"], lambda f: {"data": np.load(f)}, include_paths)
-
-
-def read_text(paths, *, encoding="utf-8", drop_empty_lines=True, include_paths=False, **kw):
-    def rd(f):
-        with open(f, encoding=encoding) as fh:
-            lines = [ln.rstrip("\n") for ln in fh]
-        if drop_empty_lines:
-            lines = [ln for ln in lines if ln.strip()]
-        return {"text": np.array(lines, dtype=object)}
-
-    return _file_ds(paths, None, rd, include_paths)
-
-
-def read_tfrecords(paths, *, include_paths=False, tf_schema=None, verify=True,
-                   arrow_open_stream_args=None, **kw) -> Dataset:
+def read_tfrecords(paths, *, tf_schema=None, verify=True, **kw) -> Dataset:
     """TFRecord files of tf.train.Example protos (data/tfrecords.py); one block per file.
     ``verify`` checks every record's CRC32C; ``arrow_open_stream_args={"compression":
     "gzip"}`` (or a ``.gz`` suffix) reads compressed files."""
-    from ray_amd.data.tfrecords import read_file
+    from ray_amd.data.datasource.formats import TFRecordDatasource
 
-    if tf_schema is not None:
-        raise NotImplementedError("tf_schema needs tensorflow_metadata (not installed)")
-    comp = (arrow_open_stream_args or {}).get("compression")
-    return _file_ds(paths, [".tfrecords", ".tfrecord", ".gz"],
-                    lambda f: read_file(f, verify, comp), include_paths)
+    return read_datasource(TFRecordDatasource(paths, tf_schema=tf_schema, verify=verify,
+                                              **_file_kw(kw, None)))
 
 
-def read_avro(paths, *, include_paths=False, **kw) -> Dataset:
+def read_avro(paths, **kw) -> Dataset:
     """Avro object container files (data/avro.py): one block per file, a column per
     top-level record field."""
-    from ray_amd.data.avro import read_file
+    from ray_amd.data.datasource.formats import AvroDatasource
 
-    return _file_ds(paths, [".avro"], read_file, include_paths)
-
-
-def read_binary_files(paths, *, include_paths=False, **kw) -> Dataset:
-    def rd(f):
-        with open(f, "rb") as fh:
-            b = np.empty(1, dtype=object)
-            b[0] = fh.read()
-        return {"bytes": b}
-
-    return _file_ds(paths, None, rd, include_paths)
+    return read_datasource(AvroDatasource(paths, **_file_kw(kw, None)))
 
 
-def read_images(paths, *, size=None, mode=None, include_paths=False, **kw) -> Dataset:
+def read_binary_files(paths, **kw) -> Dataset:
+    from ray_amd.data.datasource.formats import BinaryDatasource
+
+    return read_datasource(BinaryDatasource(paths, **_file_kw(kw, None)))
+
+
+def read_images(paths, *, size=None, mode=None, **kw) -> Dataset:
     """Image files (png/jpg/bmp/gif/webp/tiff via PIL, or .npy HWC arrays) -> rows with an
     ``image`` HWC uint8 array; ``size=(h, w)`` resizes, ``mode`` converts (e.g. "RGB")."""
-    exts = [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".webp", ".tif", ".tiff", ".npy"]
+    from ray_amd.data.datasource.formats import ImageDatasource
 
-    def rd(f):
-        if f.endswith(".npy"):
-            img = np.load(f)
-        else:
-            from PIL import Image
-
-            im = Image.open(f)
-            if mode is not None:
-                im = im.convert(mode)
-            if size is not None:
-                im = im.resize((size[1], size[0]))
-            img = np.asarray(im)
-        return {"image": img[None]}
-
-    return _file_ds(paths, exts, rd, include_paths)
+    return read_datasource(ImageDatasource(paths, size=size, mode=mode,
+                                           **_file_kw(kw, None)))
 
 
-def read_parquet_bulk(paths, *, columns=None, include_paths=False, **kw) -> Dataset:
-    """read_parquet over an explicit file list (no directory expansion / metadata pass)."""
+def read_parquet_bulk(paths, *, columns=None, **kw) -> Dataset:
+    """read_parquet over an explicit file list (no metadata pass; sizes not fetched)."""
+    from ray_amd.data.datasource.file_meta_provider import FastFileMetadataProvider
+
+    kw.setdefault("meta_provider", FastFileMetadataProvider())
     return read_parquet(list(paths) if not isinstance(paths, str) else [paths],
-                        columns=columns, include_paths=include_paths)
+                        columns=columns, **kw)
 
 
-def read_datasource(datasource, *, parallelism=-1, **kw) -> Dataset:
-    tasks = datasource.get_read_tasks(_parallelism(parallelism))
-    return Dataset(X.Plan(("read", list(tasks))))
+def read_datasource(datasource, *, parallelism=-1, override_num_blocks=None,
+                    **kw) -> Dataset:
+    p = override_num_blocks if override_num_blocks is not None else parallelism
+    tasks = datasource.get_read_tasks(_parallelism(p))
+    ds = Dataset(X.Plan(("read", list(tasks))))
+    if hasattr(datasource, "input_files"):
+        ds._input_files = datasource.input_files()
+    return ds
 
 
 import builtins  # noqa: E402

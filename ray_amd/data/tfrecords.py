@@ -218,6 +218,15 @@ def read_file(path: str, verify: bool = True, compression: str | None = None):
     return _rows_to_block(rows)
 
 
+def encode_block(blk) -> bytes:
+    """One block as the bytes of a TFRecord file (framing + CRC32C natively)."""
+    from ray_amd._native import _core
+    from ray_amd.data import block as B
+
+    kinds = _block_kinds(blk)
+    return _core.tfrecord_encode([encode_example(row, kinds) for row in B.to_rows(blk)])
+
+
 @ray.remote
 def _write_tfrecords_block(blk, path, idx, compression):
     from ray_amd._native import _core

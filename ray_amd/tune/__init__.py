@@ -5,8 +5,10 @@ from ray_amd.train._checkpoint import Checkpoint  # noqa: F401
 from ray_amd.train._internal.session import get_checkpoint, get_context, report  # noqa: F401
 from ray_amd.tune import schedulers, search  # noqa: F401
 from ray_amd.tune.callback import Callback  # noqa: F401
-from ray_amd.tune.logger import (CSVLoggerCallback, JsonLoggerCallback,  # noqa: F401
-                                 LoggerCallback, TBXLoggerCallback)
+from ray_amd.tune.logger import (CSVLogger, CSVLoggerCallback, JsonLogger,  # noqa: F401
+                                 JsonLoggerCallback, LegacyLoggerCallback, Logger,
+                                 LoggerCallback, NoopLogger, TBXLogger, TBXLoggerCallback,
+                                 UnifiedLogger, pretty_print)
 from ray_amd.tune.search.sample import (choice, grid_search, lograndint, loguniform,  # noqa
                                         qlograndint, qloguniform, qrandint, qrandn, quniform,
                                         randint, randn, sample_from, uniform)

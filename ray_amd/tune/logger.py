@@ -293,3 +293,128 @@ def default_callbacks(user: list | None) -> list:
         if not any(isinstance(c, cls) for c in cbs):
             cbs.append(cls())
     return cbs
+
+
+# ----------------------------------------------------------------- legacy Logger API
+class _LoggerTrial:
+    """The minimal trial the callback loggers need (config + directory)."""
+
+    def __init__(self, config, logdir, trial=None):
+        self.config = config or {}
+        self.local_path = self.path = logdir
+        self.trial_id = getattr(trial, "trial_id", os.path.basename(logdir or ""))
+
+
+class Logger:
+    """The reference's per-trial logger (python/ray/tune/logger/logger.py ``Logger``):
+    ``on_result(result)`` per reported result, ``update_config``, ``flush``, ``close``.
+    New code uses the ``LoggerCallback`` classes; these wrap them."""
+
+    _callback_cls = None
+
+    def __init__(self, config: dict, logdir: str, trial=None):
+        self.config = config
+        self.logdir = logdir
+        self.trial = trial
+        os.makedirs(logdir, exist_ok=True)
+        self._t = _LoggerTrial(config, logdir, trial)
+        self._cb = self._callback_cls() if self._callback_cls else None
+        self._init()
+
+    def _init(self):
+        if self._cb is not None:
+            self._cb.log_trial_start(self._t)
+
+    def on_result(self, result: dict):
+        if self._cb is not None:
+            self._cb.log_trial_result(result.get("training_iteration", 0), self._t, result)
+
+    def update_config(self, config: dict):
+        self.config = self._t.config = config
+        if self._cb is not None:
+            self._cb.log_trial_start(self._t)
+
+    def close(self):
+        if self._cb is not None:
+            self._cb.log_trial_end(self._t)
+
+    def flush(self):
+        pass
+
+
+class NoopLogger(Logger):
+    pass
+
+
+class JsonLogger(Logger):
+    _callback_cls = JsonLoggerCallback
+
+
+class CSVLogger(Logger):
+    _callback_cls = CSVLoggerCallback
+
+
+class TBXLogger(Logger):
+    _callback_cls = TBXLoggerCallback
+
+
+class UnifiedLogger(Logger):
+    """JSON + CSV + TensorBoard (or the ``loggers`` given)."""
+
+    def __init__(self, config, logdir, trial=None, loggers=None):
+        self._loggers = [cls(config, logdir, trial) for cls in
+                         (loggers or (JsonLogger, CSVLogger, TBXLogger))]
+        self.config, self.logdir, self.trial = config, logdir, trial
+
+    def on_result(self, result):
+        for lg in self._loggers:
+            lg.on_result(result)
+
+    def update_config(self, config):
+        for lg in self._loggers:
+            lg.update_config(config)
+
+    def close(self):
+        for lg in self._loggers:
+            lg.close()
+
+    def flush(self):
+        for lg in self._loggers:
+            lg.flush()
+
+
+class LegacyLoggerCallback(LoggerCallback):
+    """Runs ``Logger`` classes as a callback: one logger of each class per trial."""
+
+    def __init__(self, logger_classes):
+        self.logger_classes = list(logger_classes)
+        self._loggers = {}
+
+    def log_trial_start(self, trial):
+        if id(trial) not in self._loggers:
+            d = _trial_dir(trial)
+            self._loggers[id(trial)] = [c(getattr(trial, "config", {}) or {}, d, trial)
+                                        for c in self.logger_classes]
+        else:
+            for lg in self._loggers[id(trial)]:
+                lg.update_config(getattr(trial, "config", {}) or {})
+
+    def log_trial_result(self, iteration, trial, result):
+        if id(trial) not in self._loggers:
+            self.log_trial_start(trial)
+        for lg in self._loggers[id(trial)]:
+            lg.on_result(result)
+
+    def log_trial_end(self, trial, failed=False):
+        for lg in self._loggers.pop(id(trial), []):
+            lg.close()
+
+
+def pretty_print(result: dict, exclude=None) -> str:
+    """A result dict as indented YAML, without ``config`` / hidden keys (reference:
+    tune/logger/logger.py pretty_print)."""
+    import yaml
+
+    out = {k: _jsonable(v) for k, v in result.items()
+           if k != "config" and not k.startswith("_") and k not in set(exclude or ())}
+    return yaml.safe_dump(out, default_flow_style=False, sort_keys=True)

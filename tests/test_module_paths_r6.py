@@ -319,3 +319,49 @@ def test_iter_metrics_and_spark_stub():
     except ImportError:
         with pytest.raises(ImportError, match="pyspark"):
             setup_ray_cluster(max_worker_nodes=1)
+
+
+def test_legacy_tune_loggers(tmp_path):
+    import json
+
+    from ray_amd.tune.logger import (CSVLogger, JsonLogger, LegacyLoggerCallback,
+                                     UnifiedLogger, pretty_print)
+
+    lg = UnifiedLogger({"lr": 0.1}, str(tmp_path / "u"), loggers=[JsonLogger, CSVLogger])
+    for i in range(3):
+        lg.on_result({"training_iteration": i + 1, "loss": 1.0 / (i + 1)})
+    lg.close()
+    lines = (tmp_path / "u" / "result.json").read_text().splitlines()
+    assert [json.loads(x)["training_iteration"] for x in lines] == [1, 2, 3]
+    assert (tmp_path / "u" / "progress.csv").read_text().count("\n") == 4
+    assert json.loads((tmp_path / "u" / "params.json").read_text()) == {"lr": 0.1}
+    cb = LegacyLoggerCallback([JsonLogger])
+
+    class T:
+        config = {"a": 1}
+        local_path = str(tmp_path / "t")
+
+    t = T()
+    cb.on_trial_start(0, [t], t)
+    cb.on_trial_result(1, [t], t, {"training_iteration": 1, "x": 2})
+    cb.on_trial_complete(1, [t], t)
+    assert json.loads((tmp_path / "t" / "result.json").read_text())["x"] == 2
+    s = pretty_print({"a": 1, "config": {"z": 1}, "b": {"c": 2.5}})
+    assert "a: 1" in s and "config" not in s and "c: 2.5" in s
+
+
+def test_torchvision_preprocessor_with_plain_callables():
+    import torch
+
+    from ray_amd.data.preprocessors import TorchVisionPreprocessor
+
+    imgs = np.arange(2 * 4 * 4 * 3, dtype=np.float32).reshape(2, 4, 4, 3)
+    per = TorchVisionPreprocessor(["image"], lambda t: t.permute(2, 0, 1) / 255.0,
+                                  output_columns=["chw"])
+    out = per.transform_batch({"image": imgs})
+    assert out["chw"].shape == (2, 3, 4, 4)
+    assert np.allclose(out["chw"][1], np.transpose(imgs[1], (2, 0, 1)) / 255.0)
+    bat = TorchVisionPreprocessor(["image"], lambda t: torch.flip(t, dims=[1]), batched=True)
+    assert np.array_equal(bat.transform_batch({"image": imgs})["image"], imgs[:, ::-1])
+    with pytest.raises(ValueError):
+        TorchVisionPreprocessor(["a", "b"], lambda t: t, output_columns=["c"])
