@@ -285,6 +285,12 @@ class RayContext(dict):
 
 def shutdown(_exiting_interpreter=False):
     w = global_worker
+    dx = sys.modules.get("ray_amd.data._executor")
+    if dx is not None and w.core is not None:  # abandoned Data iterators stop first
+        try:
+            dx.stop_all()
+        except Exception:  # noqa: BLE001
+            pass
     with _global_node_lock:
         cw = w.core
         if cw is None:

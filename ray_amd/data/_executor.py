@@ -32,6 +32,7 @@ from __future__ import annotations
 import collections
 import os
 import threading
+import weakref
 import time
 
 import ray_amd as ray
@@ -510,10 +511,29 @@ class ResourceManager:
 
 
 # ============================================================================ execution
+_ACTIVE: "weakref.WeakSet[StreamingExecutor]" = weakref.WeakSet()
+
+
+def stop_all(timeout: float = 5.0) -> None:
+    """Stop every running executor of this process and wait for their scheduling threads
+    (``ray_amd.shutdown`` calls this first: an abandoned iterator's executor must not keep
+    calling into a cluster that is going away, or auto-initialise a new one)."""
+    execs = list(_ACTIVE)
+    for ex in execs:
+        ex._stop = True
+        with ex._cv:
+            ex._cv.notify_all()
+    for ex in execs:
+        t = ex._thread
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=timeout)
+
+
 class StreamingExecutor:
     """Runs one plan on a scheduling thread; iterate to receive (block_ref, meta)."""
 
     def __init__(self, plan: Plan, options: ExecutionOptions | None = None):
+        _ACTIVE.add(self)
         self.plan = plan
         self.options = options or _default_options()
         self._cv = threading.Condition()

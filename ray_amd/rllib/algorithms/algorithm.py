@@ -155,7 +155,17 @@ class Algorithm:
                 self.cfg["model"] = dict(mcfg, custom_model=cls)
         if type(self).validate_env is not Algorithm.validate_env:  # overridden: runners call it
             self.cfg["_validate_env"] = type(self).validate_env
-        probe = make_env(config.env, config.env_config)
+        if config.env is None and config.observation_space is not None and \
+                config.action_space is not None:
+            # no local env (external simulators via PolicyServerInput, or offline data):
+            # the spaces come from the config
+            import types
+
+            probe = types.SimpleNamespace(observation_space=config.observation_space,
+                                          action_space=config.action_space,
+                                          close=lambda: None)
+        else:
+            probe = make_env(config.env, config.env_config)
         self.observation_space = probe.observation_space
         self.action_space = probe.action_space
         # the modules see the env-to-module connector pipeline's output space; a

@@ -1,5 +1,5 @@
-"""reference import path ``ray.rllib.algorithms.bc``."""
+"""``ray.rllib.algorithms.bc`` (reference: python/ray/rllib/algorithms/bc/)."""
 
-from ray_amd.rllib.algorithms.marwil import BC, BCConfig  # noqa: F401
+from ray_amd.rllib.algorithms.bc.bc import BC, BCConfig  # noqa: F401
 
 __all__ = ["BC", "BCConfig"]

@@ -36,10 +36,23 @@ class SingleAgentEnvRunner:
         from ray_amd.rllib.env.vector_env import VectorEnv
 
         self.envs = []
+        from ray_amd.rllib.env.env_context import EnvContext
+
+        env_spec = config["env"]
+        if env_spec is None and callable(config.get("input_")):
+            # no local env: the input factory provides an ExternalEnv (PolicyServerInput:
+            # remote simulators drive the episodes; reference: offline_data(input_=...))
+            from ray_amd.rllib.offline.io_context import IOContext
+
+            inp = config["input_"]
+            env_spec = (lambda ec, inp=inp: inp(IOContext(config=config,
+                                                          worker_index=ec.worker_index)))
         for i in range(n):
-            ec = dict(config.get("env_config") or {})
+            ec = EnvContext(config.get("env_config") or {}, worker_index=worker_index,
+                            vector_index=i, remote=worker_index > 0,
+                            num_workers=config.get("num_env_runners"))
             ec.setdefault("seed", (seed or 0) * 1000 + worker_index * 100 + i)
-            e = make_env(config["env"], ec)
+            e = make_env(env_spec, ec)
             if config.get("_validate_env") is not None:  # Algorithm.validate_env
                 config["_validate_env"](e, ec)
             if isinstance(e, VectorEnv):  # its sub-environments join the lock-step batch

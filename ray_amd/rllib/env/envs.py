@@ -54,7 +54,10 @@ def _wrap(e):
 
 
 def make_env(env, env_config=None):
-    cfg = dict(env_config or {})
+    from ray_amd.rllib.env.env_context import EnvContext
+
+    # creators get an EnvContext (a dict with worker_index / vector_index / num_workers)
+    cfg = env_config if isinstance(env_config, EnvContext) else EnvContext(env_config or {})
     if isinstance(env, str):
         if env in _REGISTRY:
             return _wrap(_REGISTRY[env](cfg))

@@ -11,10 +11,15 @@
 from .io import (JsonReader, JsonWriter, ParquetWriter, discounted_returns,
                  fragment_to_transitions, read_offline_dataset)
 from .offline_data import OfflineData, add_returns, iterate_forever
+from .io_context import (DatasetReader, DatasetWriter, InputReader, IOContext,  # noqa: F401
+                         MixedInput, NoopOutput, OutputWriter, ShuffledInput,
+                         get_dataset_and_shards, get_offline_io_resource_bundles)
 from .estimators import (DirectMethod, DoublyRobust, FQETorchModel, ImportanceSampling,
                          OfflineEvaluator, OffPolicyEstimator, WeightedImportanceSampling)
 
-__all__ = ["DirectMethod", "DoublyRobust", "FQETorchModel", "ImportanceSampling",
+__all__ = ["DatasetReader", "DatasetWriter", "InputReader", "IOContext", "MixedInput",
+           "NoopOutput", "OutputWriter", "ShuffledInput", "get_dataset_and_shards",
+           "get_offline_io_resource_bundles", "DirectMethod", "DoublyRobust", "FQETorchModel", "ImportanceSampling",
            "JsonReader", "JsonWriter", "OfflineData", "OfflineEvaluator",
            "OffPolicyEstimator", "ParquetWriter", "WeightedImportanceSampling",
            "add_returns", "discounted_returns", "fragment_to_transitions", "iterate_forever",

@@ -178,3 +178,13 @@ class ReservoirReplayBuffer(ReplayBuffer):
                     continue
             for k, v in batch.items():
                 self._cols[k][i] = v[j]
+
+
+from ray_amd.rllib.utils.replay_buffers.episode_replay_buffer import (  # noqa: E402,F401
+    EpisodeReplayBuffer)
+from ray_amd.rllib.utils.replay_buffers.multi_agent import (  # noqa: E402,F401
+    FifoReplayBuffer, MultiAgentMixInReplayBuffer, MultiAgentPrioritizedReplayBuffer,
+    MultiAgentReplayBuffer, ReplayMode, StorageUnit)
+from ray_amd.rllib.utils.replay_buffers.prioritized_episode_buffer import (  # noqa: E402,F401
+    PrioritizedEpisodeReplayBuffer)
+from ray_amd.rllib.utils.replay_buffers import utils  # noqa: E402,F401
