@@ -91,3 +91,12 @@ class PrevActionsPrevRewards(ConnectorV2):
         na = act_space.n if hasattr(act_space, "n") else int(np.prod(act_space.shape))
         n = int(np.prod(obs_space.shape)) + na + 1
         return Box(-np.inf, np.inf, (n,), np.float32)
+
+
+def __getattr__(name):  # the pipeline pieces live in env_to_module_extra.py (imported lazily: no cycle)
+    from ray_amd.rllib.connectors import env_to_module_extra as _x
+
+    try:
+        return getattr(_x, name)
+    except AttributeError:
+        raise AttributeError(name) from None

@@ -28,3 +28,12 @@ class NormalizeAndClipActions(ConnectorV2):
             a = np.clip(batch.get("actions_for_env", batch["actions"]), -1.0, 1.0)
             batch["actions_for_env"] = sp.low + (a + 1.0) * 0.5 * (sp.high - sp.low)
         return batch
+
+
+def __getattr__(name):  # the pipeline pieces live in module_to_env_extra.py (imported lazily: no cycle)
+    from ray_amd.rllib.connectors import module_to_env_extra as _x
+
+    try:
+        return getattr(_x, name)
+    except AttributeError:
+        raise AttributeError(name) from None

@@ -1,0 +1,80 @@
+"""Connector pieces of the reference's pipelines (rllib/connectors/{common,env_to_module,
+module_to_env,learner}/) on ray_amd's lock-step batches, and in a training run."""
+import numpy as np
+import pytest
+import torch
+
+import ray_amd as ray
+from ray_amd.rllib.connectors.env_to_module import (AddObservationsFromEpisodesToBatch,
+                                                    BatchIndividualItems, EnvToModulePipeline,
+                                                    NumpyToTensor)
+from ray_amd.rllib.connectors.learner import GeneralAdvantageEstimation
+from ray_amd.rllib.connectors.module_to_env import (GetActions, ModuleToEnvPipeline,
+                                                    RemoveSingleTsTimeRankFromBatch,
+                                                    TensorToNumpy, UnBatchToIndividualItems)
+
+
+def test_pieces_on_batches():
+    b = BatchIndividualItems()(batch={"obs": [np.zeros(3), np.ones(3)]})
+    assert b["obs"].shape == (2, 3)
+    t = NumpyToTensor()(batch={"obs": np.ones((2, 3), np.float32), "name": ["a", "b"]})
+    assert isinstance(t["obs"], torch.Tensor) and t["name"] == ["a", "b"]
+    back = TensorToNumpy()(batch=t)
+    assert isinstance(back["obs"], np.ndarray)
+    m2e = ModuleToEnvPipeline(connectors=[GetActions(), TensorToNumpy(),
+                                          UnBatchToIndividualItems()])
+    out = m2e(batch={"action_dist_inputs": np.array([[0.0, 9.0], [9.0, 0.0]], np.float32)},
+              explore=False)
+    assert [int(a) for a in out["actions_for_env"]] == [1, 0]
+    assert out["action_logp"].shape == (2,)
+    r = RemoveSingleTsTimeRankFromBatch()(batch={"vf_preds": np.zeros((4, 1)),
+                                                 "obs": np.zeros((4, 1))})
+    assert r["vf_preds"].shape == (4,) and r["obs"].shape == (4, 1)
+
+    class Ep:
+        def __init__(self, v):
+            self.observations = [np.full(2, v)]
+
+    e2m = EnvToModulePipeline(connectors=[AddObservationsFromEpisodesToBatch()])
+    assert e2m(batch={}, episodes=[Ep(1.0), Ep(2.0)])["obs"][:, 0].tolist() == [1.0, 2.0]
+
+
+def test_gae_piece_matches_recursion():
+    rng = np.random.default_rng(0)
+    T, B = 6, 3
+    r, v = rng.normal(size=(T, B)), rng.normal(size=(T, B))
+    d = (rng.random((T, B)) < 0.2).astype(np.float64)
+    out = GeneralAdvantageEstimation(gamma=0.97, lambda_=0.9)(
+        batch={"rewards": r, "vf_preds": v, "terminateds": d})
+    adv = np.zeros((T, B))
+    for b_ in range(B):
+        acc = 0.0
+        for t in reversed(range(T)):
+            nv = 0.0 if t == T - 1 else v[t + 1, b_]
+            delta = r[t, b_] + 0.97 * nv * (1 - d[t, b_]) - v[t, b_]
+            acc = delta + 0.97 * 0.9 * (1 - d[t, b_]) * acc
+            adv[t, b_] = acc
+    assert np.allclose(out["advantages"], adv, atol=1e-5)
+    assert np.allclose(out["value_targets"], adv + v, atol=1e-5)
+
+
+def test_pipeline_pieces_in_training():
+    from ray_amd.rllib.algorithms import PPOConfig
+
+    started = not ray.is_initialized()
+    if started:
+        ray.init(num_cpus=2)
+    try:
+        cfg = (PPOConfig().environment("CartPole-v1")
+               .env_runners(num_env_runners=0, rollout_fragment_length=64,
+                            env_to_module_connector=lambda *a: [
+                                AddObservationsFromEpisodesToBatch(), BatchIndividualItems()],
+                            module_to_env_connector=lambda *a: [UnBatchToIndividualItems()])
+               .training(train_batch_size=128, minibatch_size=64, num_epochs=1))
+        algo = cfg.build()
+        res = algo.train()
+        assert res["num_env_steps_sampled_lifetime"] >= 128
+        algo.stop()
+    finally:
+        if started:
+            ray.shutdown()
