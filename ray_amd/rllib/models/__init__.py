@@ -69,7 +69,15 @@ class ModelCatalog:
 
     @staticmethod
     def get_preprocessor_for_space(observation_space, options=None):
-        return None  # observations reach the module unflattened (its encoder flattens)
+        """The old-stack preprocessor of ``observation_space`` (models/preprocessors.py).
+        ray_amd's own modules take observations unflattened; this is for old-stack code."""
+        from ray_amd.rllib.models.preprocessors import get_preprocessor
+
+        return get_preprocessor(observation_space)(observation_space, options)
+
+    @staticmethod
+    def get_preprocessor(env, options=None):
+        return ModelCatalog.get_preprocessor_for_space(env.observation_space, options)
 
 
 def _custom_model_module(cfg: dict, observation_space, action_space):
@@ -100,4 +108,8 @@ def _custom_model_module(cfg: dict, observation_space, action_space):
     return _ModelV2Module(observation_space, action_space, model_config=mc)
 
 
-__all__ = ["ModelCatalog", "MODEL_DEFAULTS"]
+from ray_amd.rllib.models.action_dist import ActionDistribution  # noqa: E402,F401
+from ray_amd.rllib.models.modelv2 import ModelV2  # noqa: E402,F401
+from ray_amd.rllib.models.preprocessors import Preprocessor  # noqa: E402,F401
+
+__all__ = ["ActionDistribution", "ModelCatalog", "ModelV2", "MODEL_DEFAULTS", "Preprocessor"]

@@ -78,3 +78,36 @@ def test_pipeline_pieces_in_training():
     finally:
         if started:
             ray.shutdown()
+
+
+def test_old_stack_models_and_evaluation_pieces():
+    from ray_amd.rllib.env import spaces
+    from ray_amd.rllib.evaluation import (MultiAgentSampleBatchBuilder, RolloutWorker,
+                                          SampleBatchBuilder, collect_metrics)
+    from ray_amd.rllib.models import ModelCatalog
+    from ray_amd.rllib.models.torch.torch_action_dist import (TorchCategorical,
+                                                              TorchDiagGaussian)
+
+    sp = spaces.Tuple((spaces.Discrete(2), spaces.Box(-1, 1, (3,))))
+    p = ModelCatalog.get_preprocessor_for_space(sp)
+    assert p.shape == (5,) and p.transform((1, np.ones(3))).tolist() == [0, 1, 1, 1, 1]
+    oh = ModelCatalog.get_preprocessor_for_space(spaces.MultiDiscrete([2, 3]))
+    assert oh.transform(np.array([1, 2])).tolist() == [0, 1, 0, 0, 1]
+    d = TorchCategorical(torch.tensor([[0.0, 50.0]]))
+    assert int(d.deterministic_sample()) == 1 and float(d.entropy()) < 1e-6
+    g1, g2 = TorchDiagGaussian(torch.zeros(1, 2)), TorchDiagGaussian(torch.tensor([[1.0, 0.0]]))
+    assert float(g1.kl(g2)) == pytest.approx(0.5)
+    assert TorchDiagGaussian.required_model_output_shape(spaces.Box(-1, 1, (3,))) == 6
+    mb = MultiAgentSampleBatchBuilder()
+    mb.add_values("a0", "p0", obs=1, rewards=3.0)
+    mb.add_values("a1", "p1", obs=2, rewards=-2.0)
+    ma = mb.build_and_reset()
+    assert set(ma.policy_batches) == {"p0", "p1"}
+    sb = SampleBatchBuilder()
+    sb.add_batch({"x": np.arange(3)})
+    assert sb.build_and_reset()["x"].tolist() == [0, 1, 2]
+    w = RolloutWorker({"env": "CartPole-v1", "num_envs_per_env_runner": 2,
+                       "module_kind": "actor_critic", "rollout_fragment_length": 300})
+    w.sample()
+    m = collect_metrics([w])
+    assert m["episodes_this_iter"] >= 1 and m["episode_reward_mean"] > 0
