@@ -111,3 +111,48 @@ def test_old_stack_models_and_evaluation_pieces():
     w.sample()
     m = collect_metrics([w])
     assert m["episodes_this_iter"] >= 1 and m["episode_reward_mean"] > 0
+
+
+def test_old_stack_exploration():
+    from ray_amd.rllib.env import spaces
+    from ray_amd.rllib.models.action_dist import TorchCategorical, TorchDeterministic
+    from ray_amd.rllib.utils.exploration import (EpsilonGreedy, GaussianNoise,
+                                                 OrnsteinUhlenbeckNoise, ParameterNoise,
+                                                 PerWorkerEpsilonGreedy, SoftQ,
+                                                 StochasticSampling)
+
+    q = torch.tensor([[0.0, 5.0, 1.0]] * 400)
+    eg = EpsilonGreedy(spaces.Discrete(3), initial_epsilon=1.0, final_epsilon=0.0,
+                       epsilon_timesteps=100, seed=0)
+    a0, _ = eg.get_exploration_action(action_distribution=TorchCategorical(q), timestep=0)
+    assert (a0 != 1).float().mean() > 0.5  # epsilon 1: mostly random
+    a1, _ = eg.get_exploration_action(action_distribution=TorchCategorical(q), timestep=200)
+    assert bool((a1 == 1).all())  # annealed to 0: greedy
+    assert eg.get_state()["cur_epsilon"] == 0.0
+    pw = [PerWorkerEpsilonGreedy(spaces.Discrete(3), num_workers=4, worker_index=i)
+          for i in range(5)]
+    eps = [p.epsilon(0) for p in pw]
+    assert eps[0] == 0.0 and eps[1] == pytest.approx(0.4) and eps[1] > eps[2] > eps[4]
+    ss = StochasticSampling(spaces.Discrete(3))
+    a, lp = ss.get_exploration_action(action_distribution=TorchCategorical(q[:4]),
+                                      timestep=1, explore=False)
+    assert a.tolist() == [1, 1, 1, 1]
+    sq, _ = SoftQ(spaces.Discrete(3), temperature=100.0).get_exploration_action(
+        action_distribution=TorchCategorical(q), timestep=1)
+    assert len(set(sq.tolist())) == 3  # high temperature: near uniform
+    box = spaces.Box(-1.0, 1.0, (2,))
+    gn = GaussianNoise(box, random_timesteps=0, stddev=0.5, initial_scale=1.0, seed=0)
+    det = TorchDeterministic(torch.zeros(500, 2))
+    ga, _ = gn.get_exploration_action(action_distribution=det, timestep=5)
+    assert float(ga.std()) > 0.2 and float(ga.abs().max()) <= 1.0
+    ou = OrnsteinUhlenbeckNoise(box, random_timesteps=0, seed=0)
+    o1, _ = ou.get_exploration_action(action_distribution=TorchDeterministic(torch.zeros(1, 2)),
+                                      timestep=5)
+    assert ou.get_state()["ou_state"] is not None
+    model = torch.nn.Linear(2, 2)
+    w0 = model.weight.detach().clone()
+    pn = ParameterNoise(box, model=model, initial_stddev=0.5)
+    pn.on_episode_start()
+    assert not torch.equal(model.weight, w0)
+    pn.on_episode_end()
+    assert torch.allclose(model.weight, w0)
