@@ -6,6 +6,17 @@ import copy
 
 
 class AlgorithmConfig:
+
+    @staticmethod
+    def DEFAULT_POLICY_MAPPING_FN(agent_id, episode=None, worker=None, **kwargs):
+        """Every agent to the default module (reference: the same static method)."""
+        return "default_policy"
+
+    @staticmethod
+    def DEFAULT_AGENT_TO_MODULE_MAPPING_FN(agent_id, episode=None):
+        return "default_policy"
+
+
     algo_class = None
 
     def __init__(self, algo_class=None):

@@ -19,15 +19,117 @@ import traceback
 from ray_amd.train._checkpoint import Checkpoint
 
 
+_pending_trial_info = threading.local()  # set by _TrialActor around construction
+
+
 class Trainable:
     """Class API: override setup/step/save_checkpoint/load_checkpoint."""
 
-    def __init__(self, config=None, trial_dir=None):
+    def __init__(self, config=None, trial_dir=None, logger_creator=None, storage=None,
+                 trial_info=None):
         self.config = config or {}
         self._iteration = 0
         self._time_total = 0.0
+        self._timesteps_total = None
+        self._episodes_total = None
+        self._last_result = {}
+        self._start_time = time.time()
+        info = trial_info or getattr(_pending_trial_info, "value", None) or {}
+        self._trial_info = dict(info)
         self.logdir = trial_dir or tempfile.mkdtemp(prefix="trainable_")
         self.setup(dict(self.config))
+
+    # ------------------------------------------------------------------ trial identity
+    @property
+    def trial_id(self) -> str:
+        return self._trial_info.get("trial_id", "default")
+
+    @property
+    def trial_name(self) -> str:
+        return self._trial_info.get("trial_name", "default")
+
+    @property
+    def trial_resources(self):
+        return self._trial_info.get("resources")
+
+    def get_config(self) -> dict:
+        return self.config
+
+    @staticmethod
+    def is_actor() -> bool:
+        """True inside a trial actor (a ray_amd worker process)."""
+        from ray_amd._private import worker as _w
+
+        return _w.global_worker.mode == _w.WORKER_MODE
+
+    def get_current_ip_pid(self):
+        from ray_amd.util import get_node_ip_address
+
+        return get_node_ip_address(), os.getpid()
+
+    @classmethod
+    def default_resource_request(cls, config):
+        """Resources a trial of this class needs (None: the Tuner's default)."""
+        return None
+
+    @classmethod
+    def resource_help(cls, config) -> str:
+        return ""
+
+    def get_auto_filled_metrics(self, now=None, time_this_iter=None, timestamp=None,
+                                debug_metrics_only: bool = False) -> dict:
+        import datetime
+        import socket
+
+        now = now or datetime.datetime.now()
+        out = {"time_this_iter_s": time_this_iter, "time_total_s": self._time_total,
+               "timestamp": int(timestamp or time.time()),
+               "time_since_restore": time.time() - self._start_time}
+        if not debug_metrics_only:
+            out.update({"trial_id": self.trial_id, "date": now.strftime("%Y-%m-%d_%H-%M-%S"),
+                        "pid": os.getpid(), "hostname": socket.gethostname(),
+                        "node_ip": self.get_current_ip_pid()[0]})
+        return out
+
+    def log_result(self, result: dict) -> None:
+        """Called with every result (subclasses may log them elsewhere)."""
+        self._last_result = result
+
+    def get_state(self) -> dict:
+        return {"iteration": self._iteration, "timesteps_total": self._timesteps_total,
+                "time_total": self._time_total, "episodes_total": self._episodes_total,
+                "last_result": self._last_result}
+
+    def train_buffered(self, buffer_time_s: float, max_buffer_length: int = 1000) -> list:
+        """Run ``train()`` repeatedly for up to ``buffer_time_s`` (at least once), stopping
+        early at a result with ``done`` or ``should_checkpoint``."""
+        results, t0 = [], time.time()
+        while True:
+            r = self.train()
+            results.append(r)
+            if r.get("done") or r.get("should_checkpoint") or                     len(results) >= max_buffer_length or time.time() - t0 >= buffer_time_s:
+                return results
+
+    def export_model(self, export_formats, export_dir=None) -> dict:
+        """Export the model in ``export_formats`` (subclasses implement ``_export_model``)."""
+        if isinstance(export_formats, str):
+            export_formats = [export_formats]
+        export_dir = export_dir or os.path.join(self.logdir, "export")
+        os.makedirs(export_dir, exist_ok=True)
+        return self._export_model(list(export_formats), export_dir)
+
+    def _export_model(self, export_formats, export_dir) -> dict:
+        return {}
+
+    def reset(self, new_config, logger_creator=None, storage=None) -> bool:
+        """Reuse this instance for a new trial config (``reset_config`` must agree)."""
+        if not self.reset_config(new_config):
+            return False
+        self.config = new_config
+        self._iteration, self._time_total = 0, 0.0
+        self._last_result = {}
+        self._start_time = time.time()
+        return True
 
     @property
     def iteration(self):
@@ -59,10 +161,21 @@ class Trainable:
         t0 = time.time()
         r = self.step() or {}
         self._iteration += 1
-        self._time_total += time.time() - t0
+        dt = time.time() - t0
+        self._time_total += dt
         r = dict(r)
         r.setdefault("training_iteration", self._iteration)
         r.setdefault("time_total_s", self._time_total)
+        for k, v in self.get_auto_filled_metrics(time_this_iter=dt).items():
+            r.setdefault(k, v)
+        r.setdefault("done", False)
+        if "timesteps_this_iter" in r:
+            self._timesteps_total = (self._timesteps_total or 0) + r["timesteps_this_iter"]
+            r.setdefault("timesteps_total", self._timesteps_total)
+        if "episodes_this_iter" in r:
+            self._episodes_total = (self._episodes_total or 0) + r["episodes_this_iter"]
+            r.setdefault("episodes_total", self._episodes_total)
+        self.log_result(r)
         return r
 
     def save(self, checkpoint_dir=None):
@@ -193,7 +306,12 @@ class _TrialActor:
     def start(self):
         global _fn_session
         if self.is_class:
-            self.inst = self.trainable(self.config, self.trial_dir)
+            _pending_trial_info.value = {"trial_id": self.trial_id,
+                                         "trial_name": self.trial_name}
+            try:
+                self.inst = self.trainable(self.config, self.trial_dir)
+            finally:
+                _pending_trial_info.value = None
             if self.ckpt is not None:
                 self.inst.restore(self.ckpt.path)
             return True

@@ -365,3 +365,36 @@ def test_torchvision_preprocessor_with_plain_callables():
     assert np.array_equal(bat.transform_batch({"image": imgs})["image"], imgs[:, ::-1])
     with pytest.raises(ValueError):
         TorchVisionPreprocessor(["a", "b"], lambda t: t, output_columns=["c"])
+
+
+def test_trainable_class_api(tmp_path):
+    from ray_amd.tune import Trainable
+
+    class T(Trainable):
+        def setup(self, config):
+            self.x = config.get("x", 0)
+
+        def step(self):
+            self.x += 1
+            return {"x": self.x, "timesteps_this_iter": 10, "done": self.x >= 3}
+
+        def reset_config(self, new_config):
+            self.x = new_config["x"]
+            return True
+
+        def _export_model(self, export_formats, export_dir):
+            return {f: f"{export_dir}/{f}" for f in export_formats}
+
+    t = T({"x": 0}, str(tmp_path))
+    r = t.train()
+    assert r["training_iteration"] == 1 and r["timesteps_total"] == 10
+    assert {"time_this_iter_s", "pid", "hostname", "date", "trial_id"} <= set(r)
+    rs = t.train_buffered(buffer_time_s=10.0)
+    assert rs[-1]["done"] and rs[-1]["x"] == 3
+    st = t.get_state()
+    assert st["iteration"] == 3 and st["timesteps_total"] == 30
+    assert t.export_model("torch") == {"torch": f"{tmp_path}/export/torch"}
+    assert t.reset({"x": 10}) and t.get_config() == {"x": 10} and t.iteration == 0
+    assert T.default_resource_request({}) is None and not Trainable.is_actor()
+    ip, pid = t.get_current_ip_pid()
+    assert pid > 0 and ip
