@@ -33,6 +33,33 @@ class MultiAgentEnv(Env):
             return self.action_spaces[agent_id]
         return self.action_space
 
+    def observation_space_contains(self, x: dict) -> bool:
+        return all(self.get_observation_space(a).contains(v) for a, v in x.items())
+
+    def action_space_contains(self, x: dict) -> bool:
+        return all(self.get_action_space(a).contains(v) for a, v in x.items())
+
+    def action_space_sample(self, agent_ids=None) -> dict:
+        ids = agent_ids if agent_ids is not None else sorted(self.get_agent_ids(), key=str)
+        return {a: self.get_action_space(a).sample() for a in ids}
+
+    def observation_space_sample(self, agent_ids=None) -> dict:
+        ids = agent_ids if agent_ids is not None else sorted(self.get_agent_ids(), key=str)
+        return {a: self.get_observation_space(a).sample() for a in ids}
+
+    def with_agent_groups(self, groups: dict, obs_space=None, act_space=None):
+        """This env with agent groups presented as single agents (GroupAgentsWrapper)."""
+        from ray_amd.rllib.env.wrappers.group_agents_wrapper import GroupAgentsWrapper
+
+        return GroupAgentsWrapper(self, groups, obs_space, act_space)
+
+    def to_base_env(self, make_env=None, num_envs: int = 1, remote_envs: bool = False,
+                    **kw):
+        from ray_amd.rllib.env.base_env import convert_to_base_env
+
+        return convert_to_base_env(self, make_env=make_env, num_envs=num_envs,
+                                   remote_envs=remote_envs)
+
 
 def make_multi_agent(env_name_or_creator):
     """Wrap a single-agent env into a MultiAgentEnv of ``num_agents`` independent copies

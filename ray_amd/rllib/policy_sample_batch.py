@@ -74,7 +74,9 @@ class SampleBatch(dict):
     def __getitem__(self, key):
         if isinstance(key, slice):
             return self.slice(key.start or 0, self.count if key.stop is None else key.stop)
-        return super().__getitem__(key)
+        v = super().__getitem__(key)
+        f = self.__dict__.get("_get_interceptor")
+        return f(v) if f is not None else v
 
     def copy(self, shallow: bool = False) -> "SampleBatch":
         return SampleBatch({k: (v if shallow else np.array(v, copy=True))
@@ -138,8 +140,114 @@ class SampleBatch(dict):
     def as_multi_agent(self, module_id: str = "default_policy") -> "MultiAgentBatch":
         return MultiAgentBatch({module_id: self}, self.count)
 
+    # ------------------------------------------------------- reference helpers
+    _training = False
+    _slice_by_batch_id = False
+
+    def is_training(self) -> bool:
+        return bool(getattr(self, "_training", False))
+
+    def set_training(self, training: bool = True) -> None:
+        self._training = bool(training)
+
+    def enable_slicing_by_batch_id(self) -> None:
+        self._slice_by_batch_id = True
+
+    def disable_slicing_by_batch_id(self) -> None:
+        self._slice_by_batch_id = False
+
+    def is_terminated_or_truncated(self) -> bool:
+        """True when the last row ends an episode."""
+        n = self.count
+        if n == 0:
+            return False
+        t = self.get(self.TERMINATEDS)
+        u = self.get(self.TRUNCATEDS)
+        return bool((t is not None and t[-1]) or (u is not None and u[-1]))
+
+    def is_single_trajectory(self) -> bool:
+        """One episode, with no episode end before the last row."""
+        eps = self.get(self.EPS_ID)
+        if eps is not None and len(np.unique(eps)) > 1:
+            return False
+        for col in (self.TERMINATEDS, self.TRUNCATEDS):
+            v = self.get(col)
+            if v is not None and len(v) > 1 and np.any(np.asarray(v)[:-1]):
+                return False
+        return True
+
+    def concat_samples(self, samples) -> "SampleBatch":
+        return concat_samples(samples)
+
+    def zero_pad(self, max_seq_len: int, exclude_states: bool = True) -> "SampleBatch":
+        """In place: each sequence of ``seq_lens`` padded to ``max_seq_len`` rows."""
+        lens = self.get(self.SEQ_LENS)
+        if lens is None:
+            return self.right_zero_pad(max_seq_len)
+        lens = np.asarray(lens)
+        for k, v in list(self.items()):
+            if k == self.SEQ_LENS or (exclude_states and k.startswith("state_in")):
+                continue
+            v = np.asarray(v)
+            out = np.zeros((len(lens) * max_seq_len,) + v.shape[1:], v.dtype)
+            off = 0
+            for i, ln in enumerate(lens):
+                out[i * max_seq_len: i * max_seq_len + ln] = v[off:off + ln]
+                off += ln
+            dict.__setitem__(self, k, out)
+        self.count = len(lens) * max_seq_len
+        return self
+
+    def compress(self, bulk: bool = False, columns=("obs", "new_obs")) -> "SampleBatch":
+        """Observation columns as LZ4/zlib-compressed bytes (in place)."""
+        import zlib
+
+        for c in columns:
+            if c in self and isinstance(self[c], np.ndarray):
+                a = np.ascontiguousarray(self[c])
+                blob = (a.dtype.str, a.shape, zlib.compress(a.tobytes(), 1))
+                dict.__setitem__(self, c, _Compressed(blob))
+        return self
+
+    def decompress_if_needed(self, columns=("obs", "new_obs")) -> "SampleBatch":
+        import zlib
+
+        for c in columns:
+            v = dict.get(self, c)
+            if isinstance(v, _Compressed):
+                dt, shape, data = v.blob
+                dict.__setitem__(self, c, np.frombuffer(zlib.decompress(data),
+                                                        dtype=np.dtype(dt)).reshape(shape))
+        return self
+
+    def set_get_interceptor(self, fn) -> None:
+        """``fn(value)`` applied to every column read (e.g. a device transfer)."""
+        self._get_interceptor = fn
+
+    def get_single_step_input_dict(self, view_requirements=None, index="last") -> dict:
+        """One row (the last, or ``index``) as a batch of size 1, ``new_obs`` as ``obs``."""
+        i = self.count - 1 if index == "last" else int(index)
+        out = {}
+        for k, v in self.items():
+            if k == self.SEQ_LENS:
+                continue
+            out[k] = np.asarray(v)[i:i + 1]
+        if self.NEXT_OBS in out:
+            out[self.OBS] = out[self.NEXT_OBS]
+        return SampleBatch(out)
+
     def __repr__(self):
         return f"SampleBatch({self.count}: {list(self.keys())})"
+
+
+class _Compressed:
+    """A compressed column (dtype, shape, zlib bytes); ``len`` is its row count."""
+
+    def __init__(self, blob):
+        self.blob = blob
+
+    def __len__(self):
+        return int(self.blob[1][0]) if self.blob[1] else 0
 
 
 def concat_samples(samples: List) -> "SampleBatch | MultiAgentBatch":
@@ -181,6 +289,32 @@ class MultiAgentBatch:
 
     def size_bytes(self) -> int:
         return sum(b.size_bytes() for b in self.policy_batches.values())
+
+    def timeslices(self, k: int) -> List["MultiAgentBatch"]:
+        """Cut into batches of ``k`` env steps (each policy batch sliced alike)."""
+        out = []
+        for s in range(0, self.count, k):
+            out.append(MultiAgentBatch({pid: b.slice(s, min(s + k, len(b)))
+                                        for pid, b in self.policy_batches.items()
+                                        if s < len(b)}, min(k, self.count - s)))
+        return out
+
+    @staticmethod
+    def concat_samples(samples) -> "MultiAgentBatch":
+        return concat_samples_into_ma_batch(samples)
+
+    def compress(self, bulk: bool = False, columns=("obs", "new_obs")) -> "MultiAgentBatch":
+        for b in self.policy_batches.values():
+            b.compress(bulk, columns)
+        return self
+
+    def decompress_if_needed(self, columns=("obs", "new_obs")) -> "MultiAgentBatch":
+        for b in self.policy_batches.values():
+            b.decompress_if_needed(columns)
+        return self
+
+    def as_multi_agent(self) -> "MultiAgentBatch":
+        return self
 
     def __repr__(self):
         return f"MultiAgentBatch({self.count} env steps: {list(self.policy_batches)})"

@@ -197,6 +197,28 @@ class Deployment:
     def bind(self, *args, **kwargs):
         return Application(self, args, kwargs)
 
+    @property
+    def max_concurrent_queries(self) -> int:  # the reference's deprecated name
+        return self.max_ongoing_requests
+
+    @property
+    def init_args(self) -> tuple:
+        return ()
+
+    @property
+    def init_kwargs(self) -> dict:
+        return {}
+
+    @property
+    def url(self):
+        """HTTP URL of a deployment with a route prefix (None otherwise)."""
+        if self.route_prefix is None:
+            return None
+        return f"http://127.0.0.1:{_http_port}{self.route_prefix}"
+
+    def set_logging_config(self, logging_config) -> None:
+        self.logging_config = _logging_config(logging_config)
+
     def __call__(self, *a, **k):
         raise RuntimeError("Deployments cannot be constructed directly; use .bind().")
 

@@ -47,6 +47,30 @@ class TrialScheduler:
         first PENDING trial, then a new one from the searcher)."""
         return None
 
+    _supports_buffered_results = True
+
+    @property
+    def supports_buffered_results(self) -> bool:
+        return self._supports_buffered_results
+
+    def on_trial_remove(self, runner, trial):
+        """A trial was removed (stopped) outside the scheduler's decisions."""
+
+    def debug_string(self) -> str:
+        return f"Using {type(self).__name__}"
+
+    def save(self, checkpoint_path: str) -> None:
+        import cloudpickle
+
+        with open(checkpoint_path, "wb") as f:
+            f.write(cloudpickle.dumps(self.__dict__))
+
+    def restore(self, checkpoint_path: str) -> None:
+        import cloudpickle
+
+        with open(checkpoint_path, "rb") as f:
+            self.__dict__.update(cloudpickle.loads(f.read()))
+
 
 class FIFOScheduler(TrialScheduler):
     pass

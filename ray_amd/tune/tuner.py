@@ -40,6 +40,58 @@ class Searcher:
     def on_trial_complete(self, trial_id, result=None, error=False):
         pass
 
+    FINISHED = "FINISHED"
+    CKPT_FILE_TMPL = "searcher-state-{}.pkl"
+
+    def add_evaluated_point(self, parameters: dict, value: float, error: bool = False,
+                            pruned: bool = False, intermediate_values=None) -> None:
+        """Tell the searcher about a configuration evaluated outside it (subclasses that
+        model the objective override this; the default ignores it)."""
+
+    def add_evaluated_trials(self, trials_or_analysis, metric: str) -> None:
+        trials = getattr(trials_or_analysis, "trials", trials_or_analysis)
+        for t in trials or []:
+            res = getattr(t, "last_result", None) or {}
+            if metric in res:
+                self.add_evaluated_point(getattr(t, "config", {}), res[metric],
+                                         error=getattr(t, "status", "") == "ERROR")
+
+    def set_max_concurrency(self, max_concurrent: int) -> bool:
+        return False
+
+    def get_state(self) -> dict:
+        return {k: v for k, v in self.__dict__.items() if not k.startswith("__")}
+
+    def set_state(self, state: dict) -> None:
+        self.__dict__.update(state)
+
+    def save(self, checkpoint_path: str) -> None:
+        import cloudpickle
+
+        with open(checkpoint_path, "wb") as f:
+            f.write(cloudpickle.dumps(self.get_state()))
+
+    def restore(self, checkpoint_path: str) -> None:
+        """State written by ``save`` of this process's own searcher (a local file this
+        framework created, read back as such)."""
+        import cloudpickle
+
+        with open(checkpoint_path, "rb") as f:
+            self.set_state(cloudpickle.loads(f.read()))
+
+    def save_to_dir(self, checkpoint_dir: str, session_str: str = "default") -> None:
+        os.makedirs(checkpoint_dir, exist_ok=True)
+        self.save(os.path.join(checkpoint_dir, self.CKPT_FILE_TMPL.format(session_str)))
+
+    def restore_from_dir(self, checkpoint_dir: str) -> None:
+        import glob as _glob
+
+        files = sorted(_glob.glob(os.path.join(checkpoint_dir,
+                                               self.CKPT_FILE_TMPL.format("*"))))
+        if not files:
+            raise RuntimeError(f"no searcher checkpoint in {checkpoint_dir}")
+        self.restore(files[-1])
+
 
 class BasicVariantGenerator(Searcher):
     def __init__(self, points_to_evaluate=None, max_concurrent=0, random_state=None):

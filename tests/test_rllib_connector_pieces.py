@@ -156,3 +156,74 @@ def test_old_stack_exploration():
     assert not torch.equal(model.weight, w0)
     pn.on_episode_end()
     assert torch.allclose(model.weight, w0)
+
+
+def test_sample_batch_and_multi_agent_env_helpers():
+    from ray_amd.rllib.env import spaces
+    from ray_amd.rllib.env.multi_agent_env import make_multi_agent
+    from ray_amd.rllib.env.envs import CartPoleEnv
+    from ray_amd.rllib.policy_sample_batch import MultiAgentBatch, SampleBatch
+
+    b = SampleBatch({"obs": np.arange(12.0).reshape(6, 2), "terminateds": [0, 0, 1, 0, 0, 1],
+                     "eps_id": [0, 0, 0, 1, 1, 1]})
+    assert b.is_terminated_or_truncated() and not b.is_single_trajectory()
+    assert b.slice(0, 3).is_single_trajectory()
+    one = b.get_single_step_input_dict()
+    assert len(one) == 1 and one["obs"][0].tolist() == [10.0, 11.0]
+    b.compress(columns=("obs",))
+    b.decompress_if_needed(columns=("obs",))
+    assert b["obs"].shape == (6, 2) and b["obs"][5, 1] == 11.0
+    b.set_training(True)
+    assert b.is_training()
+    b.set_get_interceptor(lambda v: np.asarray(v) * 0)
+    assert float(b["obs"].sum()) == 0.0
+    s = SampleBatch({"x": np.arange(5), "seq_lens": np.array([2, 3])})
+    s.zero_pad(4)
+    assert s["x"].tolist() == [0, 1, 0, 0, 2, 3, 4, 0] and len(s) == 8
+    ma = MultiAgentBatch({"p": SampleBatch({"x": np.arange(10)})}, 10)
+    parts = ma.timeslices(4)
+    assert [len(p) for p in parts] == [4, 4, 2]
+    assert len(MultiAgentBatch.concat_samples(parts)) == 10
+    MA = make_multi_agent(lambda cfg: CartPoleEnv(cfg))
+    env = MA({"num_agents": 2})
+    acts = env.action_space_sample()
+    assert set(acts) == {0, 1} and env.action_space_contains(acts)
+    obs, _ = env.reset(seed=0)
+    assert env.observation_space_contains(obs)
+    assert set(env.with_agent_groups({"g": [0, 1]}).reset(seed=0)[0]) == {"g"}
+    base = env.to_base_env()
+    o, *_ = base.poll()
+    assert set(o[0]) == {0, 1}
+
+
+def test_custom_searcher_and_scheduler_hooks(tmp_path):
+    from ray_amd.tune.schedulers import FIFOScheduler
+    from ray_amd.tune.search import Searcher
+
+    class Grid(Searcher):
+        def __init__(self):
+            super().__init__(metric="m", mode="max")
+            self.seen = []
+            self.i = 0
+
+        def suggest(self, trial_id):
+            self.i += 1
+            return {"x": self.i}
+
+        def add_evaluated_point(self, parameters, value, **kw):
+            self.seen.append((parameters["x"], value))
+
+    g = Grid()
+    g.add_evaluated_point({"x": 7}, 1.5)
+    g.suggest("t1")
+    g.save_to_dir(str(tmp_path))
+    h = Grid()
+    h.restore_from_dir(str(tmp_path))
+    assert h.seen == [(7, 1.5)] and h.i == 1 and h.metric == "m"
+    sch = FIFOScheduler()
+    assert sch.supports_buffered_results and "FIFOScheduler" in sch.debug_string()
+    sch.metric = "loss"
+    sch.save(str(tmp_path / "s.pkl"))
+    s2 = FIFOScheduler()
+    s2.restore(str(tmp_path / "s.pkl"))
+    assert s2.metric == "loss"
