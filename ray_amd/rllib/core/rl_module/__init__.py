@@ -13,6 +13,9 @@ from ray_amd.rllib.core.rl_module.rl_module import (MultiRLModuleSpec,  # noqa: 
                                                     RLModuleSpec, TorchRLModule,
                                                     ValueFunctionAPI, build_module)
 
+from ray_amd.rllib.core.rl_module.checkpoint import MultiRLModule  # noqa: F401,E402
+
 DefaultActorCriticModule = RLModule
+MultiAgentRLModule = MultiRLModule
 SingleAgentRLModuleSpec = RLModuleSpec
 MultiAgentRLModuleSpec = MultiRLModuleSpec

@@ -15,6 +15,8 @@ import math
 import numpy as np
 import torch
 import torch.nn as nn
+
+from ray_amd.rllib.core.rl_module.checkpoint import CheckpointableModuleMixin
 import torch.nn.functional as F
 
 from ray_amd.rllib.env import spaces
@@ -96,7 +98,7 @@ class NatureCNN(nn.Module):
         return self.fc(x.permute(0, 2, 3, 1).flatten(1))
 
 
-class RLModule(nn.Module):
+class RLModule(CheckpointableModuleMixin, nn.Module):
     """Actor-critic module used by PPO / IMPALA / APPO."""
 
     framework = "torch"
@@ -133,6 +135,8 @@ class RLModule(nn.Module):
         nn.init.zeros_(self.vf.bias)
 
     def _flat(self, obs):
+        if isinstance(obs, dict):  # the reference's batch-dict calling convention
+            obs = obs["obs"]
         if self.is_image:
             return obs
         return obs.reshape(obs.shape[0], -1).float()

@@ -29,6 +29,9 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ray_amd.rllib.core.rl_module.checkpoint import (CheckpointableModuleMixin,  # noqa: F401
+                                                  MultiRLModule)
+
 from ray_amd.rllib.core.columns import Columns
 from ray_amd.rllib.core.rl_module import default as D
 from ray_amd.rllib.env import spaces
@@ -41,7 +44,7 @@ class ValueFunctionAPI:
         raise NotImplementedError
 
 
-class TorchRLModule(nn.Module):
+class TorchRLModule(CheckpointableModuleMixin, nn.Module):
     """Base class of user RLModules (reference: TorchRLModule / RLModule new API)."""
 
     framework = "torch"
@@ -94,6 +97,11 @@ class TorchRLModule(nn.Module):
 
     def set_state(self, state):
         self.load_state_dict(state)
+
+    def _ctor_args(self):
+        return ((self.observation_space, self.action_space),
+                {"inference_only": self.inference_only, "model_config": self.model_config,
+                 "catalog_class": self.catalog_class})
 
 
 @dataclasses.dataclass

@@ -227,3 +227,41 @@ def test_custom_searcher_and_scheduler_hooks(tmp_path):
     s2 = FIFOScheduler()
     s2.restore(str(tmp_path / "s.pkl"))
     assert s2.metric == "loss"
+
+
+def test_rl_module_checkpoints_and_multi_module(tmp_path):
+    from ray_amd.rllib.core.rl_module import MultiRLModule, RLModule, TorchRLModule
+    from ray_amd.rllib.env import spaces
+    from ray_amd.rllib.models.action_dist import TorchCategorical
+
+    obs_sp, act_sp = spaces.Box(-1, 1, (4,)), spaces.Discrete(2)
+    m = RLModule(obs_sp, act_sp, {"fcnet_hiddens": [16]})
+    path = m.save_to_checkpoint(str(tmp_path / "m"))
+    m2 = RLModule.from_checkpoint(path)
+    x = torch.randn(3, 4)
+    with torch.no_grad():
+        a = m.forward_inference({"obs": x})["action_dist_inputs"]
+        b = m2.forward_inference({"obs": x})["action_dist_inputs"]
+    assert torch.allclose(a, b)
+    assert m.get_inference_action_dist_cls() is TorchCategorical and m.unwrapped() is m
+
+    class Tiny(TorchRLModule):
+        def setup(self):
+            self.lin = torch.nn.Linear(4, 2)
+
+        def _forward(self, batch, **kw):
+            return {"action_dist_inputs": self.lin(batch["obs"])}
+
+    t = Tiny(obs_sp, act_sp, model_config={"k": 1})
+    mm = t.as_multi_agent()
+    mm.add_module("other", RLModule(obs_sp, act_sp, {"fcnet_hiddens": [8]}))
+    assert set(mm.keys()) == {"default_policy", "other"}
+    out = mm.forward_inference({"default_policy": {"obs": x}})
+    assert out["default_policy"]["action_dist_inputs"].shape == (3, 2)
+    mp = mm.save_to_checkpoint(str(tmp_path / "mm"))
+    back = MultiRLModule.from_checkpoint(mp)
+    assert set(back.keys()) == {"default_policy", "other"}
+    with torch.no_grad():
+        assert torch.allclose(back["default_policy"].lin.weight, t.lin.weight)
+    mm.remove_module("other")
+    assert list(mm.keys()) == ["default_policy"]
