@@ -57,7 +57,71 @@ class DAGNode:
         return cache[key]
 
     def execute(self, *args, **kwargs):
-        return self._exec({}, (args, kwargs))
+        cache = {}
+        out = self._exec(cache, (args, kwargs))
+        self._last_cache = cache
+        return out
+
+    # ------------------------------------------------ reference DAGNode helpers
+    def get_stable_uuid(self) -> str:
+        return self._stable_uuid
+
+    def get_other_args_to_resolve(self) -> dict:
+        return dict(getattr(self, "_bound_other_args_to_resolve", {}) or {})
+
+    def get_object_refs_from_last_execute(self) -> dict:
+        """{node uuid: the value (ObjectRef for remote nodes) the last ``execute`` got}."""
+        return dict(getattr(self, "_last_cache", {}) or {})
+
+    def clear_cache(self) -> None:
+        self._last_cache = {}
+
+    def apply_recursive(self, fn):
+        """Post-order: ``fn`` on every upstream node then on this one; returns ``fn(self)``
+        of a copy whose children were replaced by their ``fn`` results."""
+        memo = {}
+
+        def visit(node):
+            key = node._stable_uuid
+            if key in memo:
+                return memo[key]
+
+            def sub(v):
+                if isinstance(v, DAGNode):
+                    return visit(v)
+                if isinstance(v, list):
+                    return [sub(x) for x in v]
+                if isinstance(v, tuple):
+                    return tuple(sub(x) for x in v)
+                if isinstance(v, dict):
+                    return {k: sub(x) for k, x in v.items()}
+                return v
+
+            import copy
+
+            clone = copy.copy(node)
+            clone._bound_args = tuple(sub(a) for a in node._bound_args)
+            clone._bound_kwargs = {k: sub(v) for k, v in node._bound_kwargs.items()}
+            memo[key] = fn(clone)
+            return memo[key]
+
+        return visit(self)
+
+    def apply_functional(self, source_input_list, predictate_fn, apply_fn):
+        """``apply_fn(x)`` for every ``x`` in ``source_input_list`` (recursing into lists
+        / tuples / dicts) for which ``predictate_fn(x)``; returns the transformed copy."""
+        def go(v):
+            if predictate_fn(v):
+                return apply_fn(v)
+            if isinstance(v, list):
+                return [go(x) for x in v]
+            if isinstance(v, tuple):
+                return tuple(go(x) for x in v)
+            if isinstance(v, dict):
+                return {k: go(x) for k, x in v.items()}
+            return v
+
+        return go(source_input_list)
 
     def _execute_impl(self, args, kwargs, cache, inputs):
         raise NotImplementedError

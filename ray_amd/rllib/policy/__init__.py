@@ -81,6 +81,125 @@ class Policy:
 
             cloudpickle.dump(self.get_state(), f)
 
+    # --------------------------------------------------- reference helper surface
+    def compute_actions_from_input_dict(self, input_dict, explore=None, timestep=None,
+                                        episodes=None, **kwargs):
+        d = dict(input_dict)
+        states = [v for k, v in sorted(d.items()) if k.startswith("state_in")]
+        return self.compute_actions(d["obs"], states or None,
+                                    prev_action_batch=d.get("prev_actions"),
+                                    prev_reward_batch=d.get("prev_rewards"),
+                                    explore=explore, timestep=timestep, **kwargs)
+
+    def compute_log_likelihoods(self, actions, obs_batch, state_batches=None,
+                                prev_action_batch=None, prev_reward_batch=None,
+                                actions_normalized: bool = True, in_training: bool = True):
+        raise NotImplementedError
+
+    def postprocess_trajectory(self, sample_batch, other_agent_batches=None, episode=None):
+        """Per-trajectory postprocessing (GAE and the like); identity by default."""
+        return sample_batch
+
+    def loss(self, model, dist_class, train_batch):
+        raise NotImplementedError
+
+    def compute_gradients(self, postprocessed_batch):
+        raise NotImplementedError
+
+    def apply_gradients(self, gradients) -> None:
+        raise NotImplementedError
+
+    # multi-GPU "tower" API: load once, learn on slices
+    def load_batch_into_buffer(self, batch, buffer_index: int = 0) -> int:
+        self._loaded = getattr(self, "_loaded", {})
+        self._loaded[buffer_index] = batch
+        return len(batch)
+
+    def get_num_samples_loaded_into_buffer(self, buffer_index: int = 0) -> int:
+        b = getattr(self, "_loaded", {}).get(buffer_index)
+        return len(b) if b is not None else 0
+
+    def learn_on_loaded_batch(self, offset: int = 0, buffer_index: int = 0):
+        b = self._loaded[buffer_index]
+        mb = self.config.get("minibatch_size") or self.config.get("sgd_minibatch_size") \
+            or len(b)
+        sl = b.slice(offset, min(offset + mb, len(b))) if hasattr(b, "slice") else b
+        return self.learn_on_batch(sl)
+
+    def learn_on_batch_from_replay_buffer(self, replay_actor, policy_id: str):
+        """Sample a train batch from a (local or actor) replay buffer and learn on it."""
+        import ray_amd as ray
+
+        n = self.config.get("train_batch_size", 32)
+        samp = replay_actor.sample.remote(n) if hasattr(replay_actor.sample, "remote") \
+            else replay_actor.sample(n)
+        batch = ray.get(samp) if isinstance(samp, ray.ObjectRef) else samp
+        if isinstance(batch, dict) and policy_id in batch:
+            batch = batch[policy_id]
+        if not batch:
+            return {}
+        from ray_amd.rllib.policy_sample_batch import SampleBatch
+
+        return self.learn_on_batch(SampleBatch({k: v for k, v in dict(batch).items()
+                                                if k != "batch_indexes"}))
+
+    def get_exploration_state(self) -> dict:
+        e = getattr(self, "exploration", None)
+        return e.get_state() if e is not None else {}
+
+    def export_model(self, export_dir: str, onnx=None) -> None:
+        os.makedirs(export_dir, exist_ok=True)
+        m = getattr(self, "model", None)
+        if m is None:
+            raise NotImplementedError("this policy has no torch model to export")
+        torch.save(m.state_dict(), os.path.join(export_dir, "model.pt"))
+
+    def import_model_from_h5(self, import_file: str) -> None:
+        raise NotImplementedError("h5 (Keras) weights need tensorflow")
+
+    def apply(self, func, *args, **kwargs):
+        return func(self, *args, **kwargs)
+
+    def get_host(self) -> str:
+        import socket
+
+        return socket.gethostname()
+
+    def get_session(self):
+        return None
+
+    def init_view_requirements(self) -> None:
+        self.view_requirements = {}
+
+    def make_rl_module(self):
+        return getattr(self, "model", None)
+
+    def maybe_add_time_dimension(self, input_dict, seq_lens=None, framework="torch"):
+        return input_dict
+
+    def maybe_remove_time_dimension(self, input_dict):
+        return input_dict
+
+    def get_connector_metrics(self) -> dict:
+        return {}
+
+    def reset_connectors(self, env_id) -> None:
+        pass
+
+    def restore_connectors(self, state) -> None:
+        pass
+
+    @staticmethod
+    def from_state(state: dict) -> "Policy":
+        cls, obs, act, cfg = state["policy_spec"]
+        p = cls.__new__(cls)
+        if hasattr(p, "_from_state"):
+            p._from_state(obs, act, cfg, state)
+        else:
+            Policy.__init__(p, obs, act, cfg)
+            p.set_state(state)
+        return p
+
     @staticmethod
     def from_checkpoint(checkpoint: str) -> "Policy":
         with open(os.path.join(checkpoint, "policy_state.pkl"), "rb") as f:
@@ -139,6 +258,43 @@ class TorchPolicy(Policy):
         out = self.model(obs)
         lp = self._dist(out).log_prob(actions)
         return lp.sum(-1) if lp.dim() > 1 else lp
+
+    def compute_log_likelihoods(self, actions, obs_batch, state_batches=None,
+                                prev_action_batch=None, prev_reward_batch=None,
+                                actions_normalized: bool = True, in_training: bool = True):
+        obs = torch.as_tensor(np.asarray(obs_batch), dtype=torch.float32, device=self.device)
+        a = torch.as_tensor(np.asarray(actions), device=self.device)
+        with torch.no_grad():
+            return self.action_log_prob(obs, a).cpu().numpy()
+
+    def loss(self, model, dist_class, train_batch):
+        if self.loss_fn is None:
+            raise NotImplementedError("TorchPolicy(loss_fn=...) defines the loss")
+        return self.loss_fn(self, model, train_batch)
+
+    def _tensor_batch(self, samples):
+        return {k: torch.as_tensor(np.asarray(v), device=self.device)
+                for k, v in dict(samples).items()
+                if isinstance(v, (np.ndarray, list)) and np.asarray(v).dtype != object}
+
+    def compute_gradients(self, postprocessed_batch):
+        """(gradients as numpy arrays in parameter order, info)."""
+        self.model.train()
+        loss = self.loss(self.model, None, self._tensor_batch(postprocessed_batch))
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        grads = [None if p.grad is None else p.grad.detach().cpu().numpy()
+                 for p in self.model.parameters()]
+        self.model.eval()
+        return grads, {"learner_stats": {"total_loss": float(loss.detach())}}
+
+    def apply_gradients(self, gradients) -> None:
+        for p, g in zip(self.model.parameters(), gradients):
+            p.grad = None if g is None else torch.as_tensor(g, device=p.device)
+        gc = self.config.get("grad_clip")
+        if gc:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), gc)
+        self.optimizer.step()
 
     def learn_on_batch(self, samples) -> dict:
         if self.loss_fn is None:

@@ -265,3 +265,70 @@ def test_rl_module_checkpoints_and_multi_module(tmp_path):
         assert torch.allclose(back["default_policy"].lin.weight, t.lin.weight)
     mm.remove_module("other")
     assert list(mm.keys()) == ["default_policy"]
+
+
+def test_old_stack_policy_surface(tmp_path):
+    from ray_amd.rllib.env import spaces
+    from ray_amd.rllib.policy import Policy, TorchPolicy
+    from ray_amd.rllib.policy_sample_batch import SampleBatch
+    from ray_amd.rllib.utils.replay_buffers import ReplayBuffer
+
+    model = torch.nn.Linear(3, 2)
+
+    def loss_fn(policy, m, batch):
+        lp = policy.action_log_prob(batch["obs"].float(), batch["actions"])
+        return -(lp * batch["rewards"].float()).mean()
+
+    pol = TorchPolicy(spaces.Box(-1, 1, (3,)), spaces.Discrete(2), {"lr": 0.1,
+                                                                    "train_batch_size": 8},
+                      model=model, loss_fn=loss_fn)
+    obs = np.random.default_rng(0).normal(size=(8, 3)).astype(np.float32)
+    acts, _, extra = pol.compute_actions_from_input_dict({"obs": obs}, explore=False)
+    assert acts.shape == (8,)
+    ll = pol.compute_log_likelihoods(acts, obs)
+    assert np.all(ll <= 0) and np.allclose(ll, extra["action_logp"] * 0 + ll)
+    batch = SampleBatch({"obs": obs, "actions": acts, "rewards": np.ones(8, np.float32)})
+    w0 = model.weight.detach().clone()
+    grads, info = pol.compute_gradients(batch)
+    pol.apply_gradients(grads)
+    assert not torch.allclose(model.weight, w0) and "total_loss" in info["learner_stats"]
+    assert pol.load_batch_into_buffer(batch) == 8
+    assert pol.get_num_samples_loaded_into_buffer() == 8
+    assert "learner_stats" in pol.learn_on_loaded_batch(0)
+    rb = ReplayBuffer(100)
+    rb.add({"obs": obs, "actions": acts, "rewards": np.ones(8, np.float32)})
+    assert "learner_stats" in pol.learn_on_batch_from_replay_buffer(rb, "default_policy")
+    pol.export_model(str(tmp_path / "exp"))
+    assert (tmp_path / "exp" / "model.pt").exists()
+    assert pol.apply(lambda p, k: k + 1, 1) == 2 and pol.postprocess_trajectory(batch) is batch
+
+
+def test_dag_node_helpers():
+    import ray_amd as ray
+    from ray_amd.dag import DAGNode, InputNode
+
+    started = not ray.is_initialized()
+    if started:
+        ray.init(num_cpus=2)
+    try:
+        @ray.remote
+        def inc(x):
+            return x + 1
+
+        with InputNode() as inp:
+            dag = inc.bind(inc.bind(inp))
+        assert ray.get(dag.execute(1)) == 3
+        refs = dag.get_object_refs_from_last_execute()
+        assert len(refs) >= 2 and dag.get_stable_uuid() in refs
+        dag.clear_cache()
+        assert dag.get_object_refs_from_last_execute() == {}
+        seen = []
+        dag.apply_recursive(lambda n: seen.append(type(n).__name__) or n)
+        assert seen[-1] == type(dag).__name__ and len(seen) == 3
+        out = dag.apply_functional([1, (2, {"a": 3})], lambda v: isinstance(v, int),
+                                   lambda v: v * 10)
+        assert out == [10, (20, {"a": 30})]
+        assert isinstance(dag, DAGNode)
+    finally:
+        if started:
+            ray.shutdown()
