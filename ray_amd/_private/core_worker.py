@@ -31,6 +31,7 @@ import traceback
 import cloudpickle
 
 from ray_amd._native import _core
+from ray_amd.util.tracing import tracing_helper as _tracing
 from ray_amd.exceptions import (ObjectReconstructionFailedError,
                                 ObjectReconstructionFailedLineageEvictedError,
                                 ObjectReconstructionFailedMaxAttemptsExceededError)
@@ -1523,6 +1524,8 @@ class CoreWorker:
             refs = [ObjectRef(object_id_for_return(tid, i + 1), self.addr, _cw_obj=self)
                     for i in range(nret)]
         spec["_holders"] = holders
+        if _tracing.ENABLED:
+            _tracing.inject(spec, "function")
         if not spec.get("no_events"):
             self.task_events.append((tid, name, time.time(), None, None, None,
                                      "PENDING_NODE_ASSIGNMENT", P.NORMAL_TASK, self.job_id, 0,
@@ -2170,6 +2173,8 @@ class CoreWorker:
             "runtime_env": self._export_renv(opts.get("runtime_env")), "job": self.job_id,
             "method_meta": method_meta, "ns": self.namespace,
         }
+        if _tracing.ENABLED:
+            _tracing.inject(spec, "actor")
         self._inline_ready_args(spec)
         info = {
             "actor_id": actor_id, "name": opts.get("name"),
@@ -2327,6 +2332,8 @@ class CoreWorker:
         }
         if opts.get("enable_task_events", True) is False:
             spec["no_events"] = True
+        if _tracing.ENABLED:
+            _tracing.inject(spec, "actor")
         with self.lock:
             if streaming:
                 self.streams[tid] = _Stream()
@@ -2521,6 +2528,8 @@ class CoreWorker:
         t0 = time.time()
         extra = {}
         name = spec.get("name") or "task"
+        tspan = _tracing.on_execute_start(spec, spec.get("actor_id")) \
+            if spec.get("trace") else None
         if not spec.get("no_events"):
             self.task_events.append((tid, name, t0, None, os.getpid(), spec.get("actor_id"),
                                      "RUNNING", spec["type"], spec.get("job"),
@@ -2588,6 +2597,8 @@ class CoreWorker:
                 self._children.pop(tid, None)
             self.current_task.tid = None
             self.current_task.spec = None
+            if tspan is not None:
+                _tracing.on_execute_end(tspan, bool(extra.get("app_error")))
         if not spec.get("no_events"):
             self.task_events.append((tid, name, t0, time.time(), os.getpid(),
                                      spec.get("actor_id"), "FAILED" if extra.get("app_error")

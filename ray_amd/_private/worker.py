@@ -166,6 +166,12 @@ def init(address: str | None = None, *, num_cpus=None, num_gpus=None, resources=
     unknown = sorted(k for k in kwargs if not k.startswith("_"))
     if unknown:
         raise TypeError(f"init() got unexpected keyword argument(s) {unknown}")
+    hook = kwargs.pop("_tracing_startup_hook", None)
+    if hook:  # "module:fn" (or "module.fn"): enables span export in this process
+        import importlib
+
+        mod, _, fn = hook.partition(":") if ":" in hook else hook.rpartition(".")
+        getattr(importlib.import_module(mod), fn)()
     for k in kwargs:  # private reference knobs with no meaning here (_redis_password, ...)
         import warnings
 
