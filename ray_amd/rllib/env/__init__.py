@@ -11,3 +11,5 @@ from ray_amd.rllib.env.policy_server_input import PolicyServerInput  # noqa: F40
 from ray_amd.rllib.env.wrappers import (DMEnv, DMCEnv, GroupAgentsWrapper,  # noqa: F401
                                         ParallelPettingZooEnv, PettingZooEnv, Unity3DEnv)
 from ray_amd.rllib.env.base_env import BaseEnv, ExternalMultiAgentEnv, RemoteBaseEnv  # noqa
+from ray_amd.rllib.env.multi_agent_episode import MultiAgentEpisode  # noqa: F401,E402
+from ray_amd.rllib.env.single_agent_episode import SingleAgentEpisode  # noqa: F401,E402

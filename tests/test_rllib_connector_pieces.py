@@ -332,3 +332,26 @@ def test_dag_node_helpers():
     finally:
         if started:
             ray.shutdown()
+
+
+def test_multi_agent_episode_turn_based_credit():
+    from ray_amd.rllib.env.multi_agent_episode import MultiAgentEpisode
+
+    ep = MultiAgentEpisode(agent_to_module_mapping_fn=lambda aid, e: f"m_{aid}")
+    ep.add_env_reset(observations={"a": 0})
+    # turn-based: a acts, b observes next; a's reward arrives later
+    ep.add_env_step({"b": 10}, {"a": 1}, {"a": 0.5})
+    assert ep.get_agents_to_act() == {"b"} and len(ep.agent_episodes["a"]) == 0
+    ep.add_env_step({"a": 1}, {"b": 2}, {"a": 1.0, "b": 0.0})
+    assert len(ep.agent_episodes["a"]) == 1
+    assert ep.agent_episodes["a"].rewards == [1.5]  # hanging reward credited on observation
+    nxt = ep.cut()
+    ep.add_env_step({"b": 11}, {"a": 0}, {"b": 2.0},
+                    terminateds={"__all__": True})
+    assert ep.is_done and ep.agent_episodes["b"].rewards == [2.0]
+    assert ep.get_return() == pytest.approx(3.5)
+    ma = ep.get_sample_batch()
+    assert set(ma.policy_batches) == {"m_a", "m_b"}
+    assert ep.module_for("a") == "m_a" and nxt.id_ == ep.id_
+    back = MultiAgentEpisode.from_state(ep.get_state())
+    assert back.get_return() == pytest.approx(3.5) and back.is_done
