@@ -314,6 +314,91 @@ class Trial:
         self.last_checkpoint_iter = 0  # training_iteration of the result with the checkpoint
         self.start_iteration = 0
 
+    # ------------------------------------------------ reference Trial surface
+    PENDING, RUNNING, PAUSED, TERMINATED, ERROR = ("PENDING", "RUNNING", "PAUSED",
+                                                   "TERMINATED", "ERROR")
+
+    @property
+    def path(self):
+        return self.local_path
+
+    @property
+    def logdir(self):
+        return self.local_path
+
+    @property
+    def evaluated_params(self) -> dict:
+        from ray_amd.tune.utils import flatten_dict
+
+        return flatten_dict(dict(self.config or {}))
+
+    @property
+    def experiment_tag(self) -> str:
+        return ",".join(f"{k}={v}" for k, v in sorted(self.evaluated_params.items())
+                        if isinstance(v, (int, float, str, bool)))
+
+    @property
+    def checkpoint(self):
+        """The latest persisted checkpoint (``train.Checkpoint``) or None."""
+        if not self.last_checkpoint:
+            return None
+        from ray_amd.train._checkpoint import Checkpoint
+
+        return self.last_checkpoint if isinstance(self.last_checkpoint, Checkpoint) else \
+            Checkpoint(self.last_checkpoint)
+
+    def has_checkpoint(self) -> bool:
+        return bool(self.last_checkpoint)
+
+    def has_reported_at_least_once(self) -> bool:
+        return bool(self.results)
+
+    def is_finished(self) -> bool:
+        return self.status in ("TERMINATED", "ERROR")
+
+    @property
+    def node_ip(self):
+        return self.last_result.get("node_ip")
+
+    @property
+    def error_file(self):
+        p = os.path.join(self.local_path, "error.txt")
+        return p if os.path.exists(p) else None
+
+    def get_error(self):
+        """The trial's failure as an exception (or None)."""
+        if self.error is None:
+            return None
+        from ray_amd.tune.error import TuneError
+
+        return self.error if isinstance(self.error, BaseException) else \
+            TuneError(str(self.error))
+
+    def should_stop(self, result: dict) -> bool:
+        return bool(result.get("done"))
+
+    def metric_analysis(self) -> dict:
+        """Per-metric last / min / max / avg over this trial's results."""
+        out = {}
+        for r in self.results:
+            for k, v in r.items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    m = out.setdefault(k, {"max": v, "min": v, "sum": 0.0, "n": 0})
+                    m["max"], m["min"] = max(m["max"], v), min(m["min"], v)
+                    m["sum"] += v
+                    m["n"] += 1
+                    m["last"] = v
+        return {k: {"max": m["max"], "min": m["min"], "avg": m["sum"] / m["n"],
+                    "last": m["last"]} for k, m in out.items()}
+
+    def get_json_state(self) -> str:
+        import json as _json
+
+        return _json.dumps({"trial_id": self.trial_id, "status": self.status,
+                            "config": self.evaluated_params, "local_path": self.local_path,
+                            "num_failures": self.num_failures},
+                           default=str)
+
     def __repr__(self):
         return f"Trial({self.trial_id}, {self.status})"
 

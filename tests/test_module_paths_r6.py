@@ -398,3 +398,22 @@ def test_trainable_class_api(tmp_path):
     assert T.default_resource_request({}) is None and not Trainable.is_actor()
     ip, pid = t.get_current_ip_pid()
     assert pid > 0 and ip
+
+
+def test_trial_surface(tmp_path):
+    from ray_amd.tune.experiment import Trial
+
+    t = Trial({"lr": 0.1, "nest": {"a": 1}}, "abc", str(tmp_path), {"CPU": 1})
+    assert t.evaluated_params == {"lr": 0.1, "nest/a": 1} and "lr=0.1" in t.experiment_tag
+    assert not t.has_reported_at_least_once() and not t.has_checkpoint()
+    t.results = [{"loss": 3.0}, {"loss": 1.0}]
+    t.last_result = t.results[-1]
+    ma = t.metric_analysis()["loss"]
+    assert (ma["min"], ma["max"], ma["last"]) == (1.0, 3.0, 1.0)
+    t.status = "TERMINATED"
+    assert t.is_finished() and t.path == t.logdir == t.local_path
+    t.error = "boom"
+    assert "boom" in str(t.get_error())
+    import json
+
+    assert json.loads(t.get_json_state())["trial_id"] == "abc"
