@@ -88,7 +88,11 @@ def test_median_stopping_rule_cuts_losers(cluster, tmp_path):
                                min_samples_required=2)
     # the weak trial comes last, so the others' histories exist when it is judged
     g = tune.Tuner(fn, param_space={"q": tune.grid_search([1.0, 1.1, 1.2, 0.1])},
-                   tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=sched),
+                   tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=sched,
+                                               # two at a time: the weak trial starts
+                                               # after two others finished, however
+                                               # loaded the machine is
+                                               max_concurrent_trials=2),
                    run_config=RunConfig(storage_path=str(tmp_path), name="m")).fit()
     iters = {r.config["q"]: r.metrics["training_iteration"] for r in g}
     assert iters[0.1] < 30 and iters[1.2] == 30
