@@ -18,7 +18,8 @@ MODULES = {
     "util": ["client_connect", "debugpy", "iter_metrics", "serialization_addons",
              "accelerators.accelerators", "collective.const", "collective.collective_group",
              "dask", "dask.callbacks", "dask.scheduler", "dask.common", "spark",
-             "state.common", "state.exception", "state.custom_types", "state.util"],
+             "state.common", "state.exception", "state.custom_types", "state.util",
+             "state.state_cli", "tracing", "tracing.setup_local_tmp_tracing"],
 }
 
 
