@@ -20,6 +20,20 @@ MODULES = {
              "dask", "dask.callbacks", "dask.scheduler", "dask.common", "spark",
              "state.common", "state.exception", "state.custom_types", "state.util",
              "state.state_cli", "tracing", "tracing.setup_local_tmp_tracing"],
+    "rllib": ["core.rl_module.marl_module", "core.rl_module.multi_rl_module",
+              "core.rl_module.rl_module_with_target_networks_interface",
+              "core.rl_module.torch.torch_rl_module", "core.learner.learner",
+              "core.learner.learner_group", "core.learner.torch.torch_learner",
+              "env.multi_agent_episode", "env.policy_client", "env.policy_server_input",
+              "env.env_context", "env.base_env", "algorithms.ppo.ppo",
+              "algorithms.ppo.ppo_learner", "algorithms.dqn.dqn", "algorithms.sac.sac",
+              "algorithms.impala.impala", "algorithms.appo.appo", "algorithms.bc.bc",
+              "algorithms.marwil.marwil", "algorithms.cql.cql", "utils.exploration",
+              "utils.filter", "utils.filter_manager", "utils.replay_buffers.utils",
+              "connectors.common", "connectors.learner", "evaluation.metrics",
+              "evaluation.sample_batch_builder", "models.modelv2", "models.action_dist",
+              "models.preprocessors", "models.torch.torch_action_dist",
+              "offline.io_context"],
 }
 
 
