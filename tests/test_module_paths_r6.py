@@ -33,7 +33,8 @@ MODULES = {
               "connectors.common", "connectors.learner", "evaluation.metrics",
               "evaluation.sample_batch_builder", "models.modelv2", "models.action_dist",
               "models.preprocessors", "models.torch.torch_action_dist",
-              "offline.io_context"],
+              "offline.io_context", "utils.annotations", "utils.typing", "utils.framework",
+              "utils.numpy", "utils.torch_utils", "utils.deprecation", "utils.from_config"],
 }
 
 
@@ -432,3 +433,33 @@ def test_trial_surface(tmp_path):
     import json
 
     assert json.loads(t.get_json_state())["trial_id"] == "abc"
+
+
+def test_rllib_utils_submodules():
+    import torch
+
+    from ray_amd.rllib.utils.deprecation import Deprecated
+    from ray_amd.rllib.utils.from_config import from_config
+    from ray_amd.rllib.utils.numpy import convert_to_numpy, flatten_inputs_to_1d_tensor
+    from ray_amd.rllib.utils.torch_utils import (apply_grad_clipping, convert_to_torch_tensor,
+                                                 explained_variance, sequence_mask)
+
+    assert convert_to_numpy({"a": torch.ones(2, dtype=torch.float64)})["a"].dtype == np.float32
+    assert flatten_inputs_to_1d_tensor({"a": np.ones((2, 3)), "b": np.zeros((2, 2, 2))}
+                                       ).shape == (2, 7)
+    t = convert_to_torch_tensor({"x": np.ones(3)})
+    assert t["x"].dtype == torch.float32
+    assert sequence_mask([1, 2]).tolist() == [[True, False], [True, True]]
+    assert float(explained_variance(torch.arange(4.0), torch.arange(4.0))) == 1.0
+    lin = torch.nn.Linear(3, 1)
+    opt = torch.optim.SGD(lin.parameters(), lr=0.1)
+    (lin(torch.ones(4, 3)) * 1e6).sum().backward()
+    assert apply_grad_clipping(opt, grad_clip=1.0)["grad_gnorm"] > 1.0
+
+    @Deprecated(new="g")
+    def f():
+        return 3
+
+    with pytest.warns(DeprecationWarning):
+        assert f() == 3
+    assert from_config(dict, {"a": 1}, b=2) == {"a": 1, "b": 2}
